@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Headline benchmark: RANSAC hypotheses/sec at 100k correspondences (BASELINE.json `metric`,
+config[2]: findHomography RANSAC, 100k correspondences x 1M hypotheses, 1 MI355X).
+
+A step = one findHomography RANSAC call on HBM-resident correspondences (packed float4, seeded
+synthetic data of the cfg3 shape): generate + minimal-solve + inlier-count 1M hypotheses
+(per GPU), reduce to the best packed key (RCCL all-reduce MAX across ranks when N > 1), then
+finalize: mask of the winner, refit on its inliers and 10 LM iterations.
+
+Scaling: weak — each GPU evaluates its own 1M-hypothesis batch of the same problem (the union is
+one RANSAC call over N x 1M hypotheses), one 16-byte all-reduce per step.
+
+Printed JSON carries the live roofline of the dominant kernel (mcv_h_verify, HIP events on its
+launch stream; algorithmic bytes = 16 B x N correspondences per hypothesis) and the oracle's CPU
+throughput on a bounded sample of the same workload (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+N_CORR = 100_000
+HYPS_PER_GPU = 1 << 20
+THR = 5e-3
+SEED = 3
+HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--hyps", type=int, default=HYPS_PER_GPU, help="hypotheses per GPU per step")
+    ap.add_argument("--n", type=int, default=N_CORR)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(src, dst, target_s: float):
+    """Oracle (plain-C restatement, OpenMP over hypotheses) on a bounded sample of the same workload."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import numpy as np
+    import _oracle as O
+    pts4 = O.pack4(src, dst)
+    thr2 = float(np.float32(THR * THR))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    t = time.perf_counter()
+    O.h_counts(pts4, SEED, 0, 4 * threads, thr2, threads)
+    cal = (time.perf_counter() - t) / (4 * threads)
+    sample = max(4 * threads, int(target_s / max(cal, 1e-6)))
+    t = time.perf_counter()
+    O.h_counts(pts4, SEED, 0, sample, thr2, threads)
+    el = time.perf_counter() - t
+    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port",
+            "sample": f"{sample} hypotheses x {src.shape[0]} correspondences (sample+solve+fp32 count), "
+                      f"oracle/oracle.c, OpenMP {threads} threads, {el:.1f} s"}
+
+
+def load_traffic(n: int, hyps: int):
+    """HBM bytes per mcv_h_verify launch from the committed rocprofv3 PMC summary, if present."""
+    p = ROOT / "profiles" / "pmc_h_verify.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        if d.get("n") == n and d.get("hyps") == hyps:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from minicv_amd import native as NL, opencv, synthetic as S
+    from minicv_amd import device as D
+    from minicv_amd import dist as MD
+
+    n, hyps = args.n, args.hyps
+    src, dst, _ = S.homography_problem(n, SEED)
+    pts = D.pack_points_tensor(src, dst, dev)
+    plan = D.RansacPlan(NL.MODEL_HOMOGRAPHY, n, hyps)
+    total = hyps * world
+    cfg = opencv.RansacParams(threshold=THR, confidence=0.995, max_iters=total, seed=SEED, fixed_iters=True).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    mask = torch.zeros(n, dtype=torch.uint8, device=dev)
+    red = torch.zeros(2, dtype=torch.int64, device=dev)
+
+    def evaluate(begin, count):
+        plan.evaluate(pts, n, cfg, begin, count, key)
+        k = key.cpu()   # synchronises the stream
+        return int(k[0]), int(k[1])
+
+    def allreduce_max(vals):
+        if world == 1:
+            return vals
+        red.copy_(torch.tensor(vals, dtype=torch.int64))
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+        return [int(v) for v in red.cpu()]
+
+    result = {}
+
+    def step():
+        cnt, idx, _ = MD.global_best(evaluate, total, rank, world, allreduce_max)
+        if idx < 0:
+            raise RuntimeError("no model found")
+        fc, H = plan.finalize(pts, n, cfg, idx, mask)
+        result.update(count=cnt, idx=idx, final_count=fc, H=H)
+
+    for _ in range(args.warmup):
+        step()
+    NL.lib().mcvProfileReset()
+    NL.lib().mcvProfileEnable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    NL.lib().mcvProfileEnable(0)
+    import ctypes as C
+    kms = C.c_double(0)
+    launches = NL.lib().mcvProfileRead(b"h_verify", C.addressof(kms))
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    if rank == 0:
+        value = total * args.steps / el
+        avg_ms = kms.value / max(launches, 1)
+        alg_bytes = 16.0 * n * hyps            # per launch: every hypothesis reads all N float4 pairs
+        achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+        traffic = load_traffic(n, hyps)
+        line = {
+            "metric": "RANSAC hypotheses/sec @100k corrs; achieved HBM GB/s vs roofline, 1/2/4/8 GPU",
+            "value": value,
+            "unit": "hypotheses/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded cfg3 homography problem: cvTest H, 50% outliers, sigma 1e-3)",
+            "config": {"workload": f"findHomography RANSAC, {n} correspondences x {hyps} hypotheses per GPU "
+                                   f"(fixed iterations) + refit/LM, best model via RCCL all-reduce",
+                       "correspondences": n, "hypotheses_per_gpu": hyps, "threshold": THR,
+                       "parallelism": f"hypothesis-sharded dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "kernel": "mcv_h_verify", "avg_launch_ms": avg_ms, "launches": launches,
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "result": {"best_count": result["count"], "best_hyp": result["idx"],
+                       "refined_count": result["final_count"]},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(src, dst, args.cpu_seconds)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    plan.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,242 @@
+/*
+ * minicv_native.h — C-ABI of the MI355X-native MiniCVNative drop-in.
+ *
+ * The managed host (F# `module OpenCV.Native`, /root/reference/src/MiniCV/OpenCV.fs:339-382)
+ * binds `[<DllImport("MiniCVNative")>]` entry points. This header declares
+ *   (1) the 13 existing exports of the reference library, byte-compatible signatures
+ *       (definitions: /root/reference/src/MiniCVNative/MiniCVNative.cpp:48-548, ap3p.cpp:282);
+ *   (2) the new hot-path exports (findHomography / findFundamentalMat RANSAC, brute-force
+ *       Hamming / L2 matching), written in the conventions of the existing ones
+ *       (AoS fp64 point arrays + separate N, caller-allocated byte mask, M33d& out, int return);
+ *   (3) a device-level API (plain device pointers + hipStream_t passed as void*) used by
+ *       bench.py / multi-GPU ranks that keep inputs resident in HBM.
+ *
+ * Conventions:
+ *   V2d  = 2 x double (x, y)            <-> Aardvark V2d / cv::Point2d
+ *   V3d  = 3 x double                   <-> Aardvark V3d / cv::Vec3d
+ *   M33d = 9 x double, row-major        <-> Aardvark M33d / cv::Matx33d
+ *   masks are caller-allocated uint8[N], values 0/1
+ *   no exception crosses the boundary: failure = false / 0 / NULL; mcvGetLastError() says why.
+ */
+#ifndef MINICV_NATIVE_H
+#define MINICV_NATIVE_H
+
+#include <stdint.h>
+#include <stdbool.h>
+
+#if defined(_WIN32)
+#define MCV_API __declspec(dllexport)
+#else
+#define MCV_API __attribute__((visibility("default")))
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { double X, Y; } mcvV2d;
+typedef struct { double X, Y, Z; } mcvV3d;
+typedef struct { double M[9]; } mcvM33d;       /* row-major */
+typedef struct { float X, Y; } mcvV2f;
+
+/* ------------------------------------------------------------------------------------------
+ * (1) Existing exports of the reference (same names, same argument meaning).
+ * ---------------------------------------------------------------------------------------- */
+
+/* RecoverPoseConfig — MiniCVNative.cpp:39-46, OpenCV.fs:16-36 (40 bytes). */
+typedef struct {
+    double FocalLength;
+    mcvV2d PrincipalPoint;
+    double Probability;
+    double InlierThreshold;
+} RecoverPoseConfig;
+
+/* KeyPoint2d / DetectorResult — MiniCVNative.h:14-29, OpenCV.fs:300-337. */
+typedef struct {
+    mcvV2f pt;
+    float size;
+    float angle;
+    float response;
+    int octave;
+    int class_id;
+} KeyPoint2d;
+
+typedef struct {
+    int PointCount;
+    int DescriptorEntries;
+    int DescriptorElementType;   /* OpenCV depth code (0 = u8, 5 = f32) */
+    KeyPoint2d* Points;
+    uint8_t* Descriptors;        /* row-major [PointCount][dim] */
+} DetectorResult;
+
+typedef struct {
+    int Id;
+    mcvV2f P0, P1, P2, P3;
+} ArucoMarkerInfo;
+
+/* Essential-matrix RANSAC — MiniCVNative.cpp:197-215 (next row f1; currently fails loudly). */
+MCV_API int  cvRecoverPose(const RecoverPoseConfig* config, const int N, const mcvV2d* pa, const mcvV2d* pb,
+                           mcvM33d* rMat, mcvV3d* tVec, uint8_t* ms);
+/* MiniCVNative.cpp:165-194 */
+MCV_API bool cvRecoverPoses(const RecoverPoseConfig* config, const int N, const mcvV2d* pa, const mcvV2d* pb,
+                            mcvM33d* rMat1, mcvM33d* rMat2, mcvV3d* tVec, uint8_t* ms);
+/* Feature detection — MiniCVNative.cpp:221-365 (out of scope: returns NULL). */
+MCV_API DetectorResult* cvDetectFeatures(char* data, int width, int height, int channels, int mode, void* config);
+MCV_API void cvFreeFeatures(DetectorResult* res);
+/* Debug export — MiniCVNative.cpp:504 (no-op). */
+MCV_API void cvTest(void);
+/* Five-point minimal solver — MiniCVNative.cpp:368-382 (next row f1). */
+MCV_API int  cvFivePoint(const mcvV2d* pa, const mcvV2d* pb, mcvM33d* Es);
+/* PnP — MiniCVNative.cpp:48-163 (next row f2). K passed by value as in the reference. */
+MCV_API bool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+                        const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec);
+MCV_API bool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+                              const double* distortionCoeffs, const int solverKind, const int iterationsCount,
+                              const float reprojectionError, const double confidence, mcvV3d* tVec, mcvV3d* rVec,
+                              int* inlierCount, int* outInliers);
+MCV_API void cvRefinePnPLM(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+                           const double* distortionCoeffs, mcvV3d* tVec, mcvV3d* rVec);
+MCV_API void cvRefinePnPVVS(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+                            const double* distortionCoeffs, mcvV3d* tVec, mcvV3d* rVec);
+/* AP3P — ap3p.cpp:282-317 (next row f2). */
+MCV_API int  solveAp3p(mcvM33d* Rs, mcvV3d* ts, float mu0, float mv0, float X0, float Y0, float Z0,
+                       float mu1, float mv1, float X1, float Y1, float Z1,
+                       float mu2, float mv2, float X2, float Y2, float Z2,
+                       float inv_fx, float inv_fy, float cx_fx, float cy_fy);
+/* Fiducials — MiniCVNative.cpp:384-502 (out of scope: return false). */
+MCV_API bool cvDetectQRCode(char* data, int width, int height, int channels, int* positions, int* count);
+MCV_API bool cvDetectArucoMarkers(char* data, int width, int height, int channels, int* infoCount,
+                                  ArucoMarkerInfo* infos);
+
+/* ------------------------------------------------------------------------------------------
+ * (2) New hot-path exports (replace the OpenCV calls a maintainer would otherwise add:
+ *     cv::findHomography, cv::findFundamentalMat, cv::BFMatcher(NORM_HAMMING / NORM_L2)).
+ * ---------------------------------------------------------------------------------------- */
+
+/* method codes (OpenCV numbering) */
+#define MCV_METHOD_LSQ     0   /* all points, no RANSAC (OpenCV method 0) */
+#define MCV_METHOD_RANSAC  8   /* cv::RANSAC */
+
+/* flags */
+#define MCV_FLAG_FIXED_ITERS  1   /* evaluate exactly maxIters hypotheses (no adaptive stop) */
+#define MCV_FLAG_NO_REFINE    2   /* return the best hypothesis' model (skip inlier refit + LM) */
+
+/* F error metric (cfg->errorKind, fundamental only) */
+#define MCV_FERR_SAMPSON   0   /* first-order geometric (Sampson) distance^2 (north_star) */
+#define MCV_FERR_EPIPOLAR  1   /* OpenCV FM_RANSAC: max of the two squared point-to-epipolar-line distances */
+
+typedef struct {
+    double threshold;     /* max reprojection / epipolar distance of an inlier (point units) */
+    double confidence;    /* RANSAC confidence in (0,1) */
+    int    maxIters;      /* hypothesis budget */
+    int    method;        /* MCV_METHOD_* */
+    uint64_t seed;        /* counter-based sampler key: hypothesis i depends only on (seed, i) */
+    int    deviceCount;   /* 0/1: one GPU; >1 shard hypotheses over that many local GPUs */
+    int    flags;         /* MCV_FLAG_* */
+    int    errorKind;     /* MCV_FERR_* (fundamental only) */
+    int    reserved;
+} RansacConfig;           /* 48 bytes */
+
+/* findHomography. src/dst: N AoS fp64 points (converted to fp32 like OpenCV's convertTo(CV_32F)).
+ * H: out, row-major, H[8] == 1. mask: caller-allocated uint8[N] (RANSAC inliers of the best
+ * hypothesis; all 1 for METHOD_LSQ / N == 4). Returns the inlier count (>= 4), 0 on failure. */
+MCV_API int cvFindHomography(const mcvV2d* src, const mcvV2d* dst, const int N, const RansacConfig* cfg,
+                             mcvM33d* H, uint8_t* mask);
+
+/* findFundamentalMat, 8-point minimal sets. a/b: N AoS fp64 points. F: out (||F||_F = 1 scale, F[8] >= 0).
+ * mask: caller-allocated uint8[N]. Returns inlier count (>= 8), 0 on failure. */
+MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, const int N, const RansacConfig* cfg,
+                                 mcvM33d* F, uint8_t* mask);
+
+/* Brute-force Hamming matcher (BFMatcher NORM_HAMMING, knn k = 2). q: [nq][bytesPerDesc],
+ * t: [nt][bytesPerDesc] row-major bytes; bytesPerDesc in [1, 64]; nt < 2^22.
+ * Outputs per query: best train index / distance and second best (idx2/dist2 may be NULL;
+ * -1 / INT_MAX when nt < 2). Ties -> lowest train index. Returns nq, or -1 on failure. */
+MCV_API int cvMatchHamming(const uint8_t* q, const int nq, const uint8_t* t, const int nt, const int bytesPerDesc,
+                           int* idx, int* dist, int* idx2, int* dist2);
+
+/* Brute-force L2 matcher (BFMatcher NORM_L2, knn k = 2) on fp32 descriptors [n][dim].
+ * dist = sqrt of the squared distance (fp32). Returns nq, or -1 on failure. */
+MCV_API int cvMatchL2(const float* q, const int nq, const float* t, const int nt, const int dim,
+                      int* idx, float* dist, int* idx2, float* dist2);
+
+/* Last error message of the calling thread ("" if none). */
+MCV_API const char* mcvGetLastError(void);
+/* Library / device info: number of visible HIP devices (0 when none), -1 on runtime error. */
+MCV_API int mcvDeviceCount(void);
+MCV_API const char* mcvVersion(void);
+
+/* ------------------------------------------------------------------------------------------
+ * (3) Device-level API: device pointers, caller's stream (hipStream_t as void*), current device.
+ *     Points on device are packed fp32 correspondences float4 {x, y, x', y'} (16 B each).
+ * ---------------------------------------------------------------------------------------- */
+
+typedef struct mcvRansacPlan_ mcvRansacPlan;
+
+#define MCV_MODEL_HOMOGRAPHY   0
+#define MCV_MODEL_FUNDAMENTAL  1
+
+/* Workspace for problems up to maxN correspondences and maxHyps hypotheses per evaluate call. */
+MCV_API mcvRansacPlan* mcvRansacPlanCreate(int model, int maxN, int64_t maxHyps);
+MCV_API void mcvRansacPlanDestroy(mcvRansacPlan* plan);
+
+/* Pack host AoS fp64 pairs into the device float4 layout (synchronous H2D on `stream`). */
+MCV_API int mcvPackCorrespondences(const mcvV2d* a, const mcvV2d* b, int N, float* d_pts4, void* stream);
+
+/* Evaluate hypotheses [hypBegin, hypBegin + hypCount) against all N correspondences:
+ * sample + minimal solve + inlier count, then reduce to the best packed key
+ *   key = (count << 32) | (0xFFFFFFFF - hypIndex)     (0 when no hypothesis has >= m inliers)
+ * written to d_key[0]; d_key[1] = first hypothesis index whose sampler failed (or INT64 max).
+ * d_counts (optional, may be NULL): per-hypothesis status/count (int32, -1 no model, -2 no sample).
+ * Asynchronous on `stream`. Returns 1 on successful launch, 0 on error. */
+MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const float* d_pts4, int N, const RansacConfig* cfg,
+                              int64_t hypBegin, int64_t hypCount, uint64_t* d_key, int* d_counts, void* stream);
+
+/* Recompute the best hypothesis' model (hypIndex), write the inlier mask (d_mask, uint8[N]),
+ * optionally refit on the inliers + LM refine (per cfg->flags), model out to host `model9`.
+ * Synchronises `stream`. Returns the inlier count, 0 on failure. */
+MCV_API int mcvRansacFinalize(mcvRansacPlan* plan, const float* d_pts4, int N, const RansacConfig* cfg,
+                              int64_t hypIndex, double* model9, uint8_t* d_mask, void* stream);
+
+/* Sequential-RANSAC replay over per-hypothesis counts (host arrays), OpenCV semantics:
+ * improvement iff count > max(best, m-1); niters <- RANSACUpdateNumIters(conf, 1-count/N, m, niters);
+ * loop stops at iter >= niters or at the first sampler failure. State carried across chunks.
+ * Returns 1 when the replay stopped inside this chunk (no more hypotheses needed), else 0. */
+typedef struct {
+    int64_t niters;      /* current iteration budget */
+    int64_t bestIndex;   /* -1 if none */
+    int32_t bestCount;
+    int32_t stopped;
+} mcvReplayState;
+MCV_API void mcvReplayInit(mcvReplayState* st, int maxIters);
+MCV_API int  mcvReplayChunk(mcvReplayState* st, const int* counts, int64_t hypBegin, int64_t hypCount,
+                            int N, int modelPoints, double confidence, int fixedIters);
+
+/* Device-level matchers: d_q/d_t device arrays, outputs device arrays. Asynchronous on stream. */
+MCV_API int mcvMatchHammingDevice(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc,
+                                  int* d_idx, int* d_dist, int* d_idx2, int* d_dist2, void* stream);
+MCV_API int mcvMatchL2Device(const float* d_q, int nq, const float* d_t, int nt, int dim,
+                             int* d_idx, float* d_dist, int* d_idx2, float* d_dist2, void* stream);
+
+/* Opt-in kernel timing: HIP events recorded around the inlier-sweep launches on their stream.
+ * mcvProfileRead returns the number of launches of `kernel` ("h_verify", "f_verify") and their
+ * summed duration in ms (synchronises the recorded events). */
+MCV_API void mcvProfileEnable(int on);
+MCV_API void mcvProfileReset(void);
+MCV_API int  mcvProfileRead(const char* kernel, double* total_ms);
+
+/* ------------------------------------------------------------------------------------------
+ * Test hooks: the host-compiled copy of the per-hypothesis code that the kernels run
+ * (sampler + subset check + minimal solver + error), so CPU tests can check it against the
+ * oracle bit for bit without a GPU. Never on a product path.
+ * ---------------------------------------------------------------------------------------- */
+MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, uint64_t seed, int64_t hyp,
+                              double* model9, float* modelf9, int* sampleIdx);
+MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                           uint32_t* out4);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MINICV_NATIVE_H */

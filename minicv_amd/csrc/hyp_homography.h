@@ -1,0 +1,231 @@
+// hyp_homography.h — one RANSAC homography hypothesis: sample 4 correspondences, check the
+// subset, solve the minimal DLT, emit the fp32 model the inlier sweep uses. Compiled for gfx950
+// (kernel `mcv_h_generate`) and for the host (mcvHostHypothesis test hook). Built with
+// -ffp-contract=off: every expression rounds as written, so host and device agree bit for bit.
+//
+// Semantics restated from OpenCV 4.x calib3d (not present in this container, version unpinned,
+// SURVEY.md §8c) — the reference's own call sites are MiniCVNative.cpp:177,204 (findEssentialMat,
+// the same RANSACPointSetRegistrator loop):
+//   * subset check   = HomographyEstimatorCallback::checkSubset: haveCollinearPoints on both point
+//                      sets (last point vs lines through earlier pairs, FLT_EPSILON test), then the
+//                      4-triangle orientation-consistency test (Marquez-Neila et al. 2013);
+//   * minimal solver = normalised DLT of runKernel (centroid + mean-|dev| scaling). For exactly 4
+//                      points the 8x9 system has a 1-D null space, solved here with h22 = 1 by 8x8
+//                      Gaussian elimination with partial pivoting instead of the 9x9 Jacobi
+//                      eigen-solve (identical model up to rounding; documented in DESIGN.md §3);
+//   * error          = HomographyEstimatorCallback::computeError: fp32, model cast to float,
+//                      ww = 1/(h6 x + h7 y + 1), err = dx^2 + dy^2; inlier iff err <= (float)thr^2.
+#pragma once
+
+#include "mcv_common.h"
+
+namespace mcv {
+
+struct HModelF { float h[8]; };   // rows 0..1 and h20, h21 of H / H22 (h22 == 1 implied)
+
+// OpenCV Matx_DetOp<double,3> expansion order.
+MCV_HD double det3(double a00, double a01, double a02, double a10, double a11, double a12,
+                   double a20, double a21, double a22) {
+    return a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
+}
+
+// haveCollinearPoints(ms, 4): point 3 against lines through pairs of points 0..2.
+// Differences are float - float (rounded to float), then promoted, as in OpenCV.
+MCV_HD bool have_collinear4(const float* px, const float* py) {
+    const int i = 3;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int j = 0; j < i; ++j) {
+        const double dx1 = (double)(px[j] - px[i]);
+        const double dy1 = (double)(py[j] - py[i]);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int k = 0; k < j; ++k) {
+            const double dx2 = (double)(px[k] - px[i]);
+            const double dy2 = (double)(py[k] - py[i]);
+            if (fabs(dx2 * dy1 - dy2 * dx1) <= (double)kFltEpsilon * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
+                return true;
+        }
+    }
+    return false;
+}
+
+MCV_HD bool h_check_subset(const float* sx, const float* sy, const float* dx, const float* dy) {
+    if (have_collinear4(sx, sy) || have_collinear4(dx, dy)) return false;
+    const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
+    int negative = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 4; ++i) {
+        const int a = tt[i][0], b = tt[i][1], c = tt[i][2];
+        const double dA = det3(sx[a], sy[a], 1.0, sx[b], sy[b], 1.0, sx[c], sy[c], 1.0);
+        const double dB = det3(dx[a], dy[a], 1.0, dx[b], dy[b], 1.0, dx[c], dy[c], 1.0);
+        negative += (dA * dB < 0) ? 1 : 0;
+    }
+    return negative == 0 || negative == 4;
+}
+
+// C = A * B for 3x3 row-major, sum order ((a0 b0 + a1 b1) + a2 b2).
+MCV_HD void mat3_mul(const double* A, const double* B, double* C) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 3; ++i)
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int j = 0; j < 3; ++j)
+            C[3 * i + j] = A[3 * i + 0] * B[0 * 3 + j] + A[3 * i + 1] * B[1 * 3 + j] + A[3 * i + 2] * B[2 * 3 + j];
+}
+
+// Minimal 4-point homography src -> dst. Returns false when degenerate (zero scale, zero pivot,
+// non-finite result). H: row-major, scaled by 1/H22 (OpenCV convertTo(..., 1./H(2,2))).
+MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const float* dy, double* H) {
+    // Normalisation (runKernel): centroids and mean absolute deviations, in double.
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 4; ++i) {
+        cmx += (double)dx[i]; cmy += (double)dy[i];
+        cMx += (double)sx[i]; cMy += (double)sy[i];
+    }
+    cmx /= 4; cmy /= 4; cMx /= 4; cMy /= 4;
+    double smx = 0, smy = 0, sMx = 0, sMy = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 4; ++i) {
+        smx += fabs((double)dx[i] - cmx); smy += fabs((double)dy[i] - cmy);
+        sMx += fabs((double)sx[i] - cMx); sMy += fabs((double)sy[i] - cMy);
+    }
+    if (fabs(smx) < kDblEpsilon || fabs(smy) < kDblEpsilon || fabs(sMx) < kDblEpsilon || fabs(sMy) < kDblEpsilon)
+        return false;
+    smx = 4 / smx; smy = 4 / smy; sMx = 4 / sMx; sMy = 4 / sMy;
+
+    // Augmented 8x9 system for Hn (h22 = 1) in normalised coordinates.
+    double a[8][9];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 4; ++i) {
+        const double x = ((double)dx[i] - cmx) * smx, y = ((double)dy[i] - cmy) * smy;
+        const double X = ((double)sx[i] - cMx) * sMx, Y = ((double)sy[i] - cMy) * sMy;
+        double* r0 = a[2 * i];
+        double* r1 = a[2 * i + 1];
+        r0[0] = X; r0[1] = Y; r0[2] = 1; r0[3] = 0; r0[4] = 0; r0[5] = 0; r0[6] = -(x * X); r0[7] = -(x * Y); r0[8] = x;
+        r1[0] = 0; r1[1] = 0; r1[2] = 0; r1[3] = X; r1[4] = Y; r1[5] = 1; r1[6] = -(y * X); r1[7] = -(y * Y); r1[8] = y;
+    }
+    // Forward elimination with partial pivoting (first maximum wins). Row swaps are done with
+    // selects over all rows so the matrix stays in registers on the device.
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int c = 0; c < 8; ++c) {
+        int p = c;
+        double best = fabs(a[c][c]);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int r = c + 1; r < 8; ++r) {
+            const double v = fabs(a[r][c]);
+            if (v > best) { best = v; p = r; }
+        }
+        if (!(best > 0)) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int r = c + 1; r < 8; ++r) {
+            const bool sw = (r == p);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+            for (int k = c; k < 9; ++k) {
+                const double t = a[c][k];
+                a[c][k] = sw ? a[r][k] : t;
+                a[r][k] = sw ? t : a[r][k];
+            }
+        }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int r = c + 1; r < 8; ++r) {
+            const double f = a[r][c] / a[c][c];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+            for (int k = c + 1; k < 9; ++k) a[r][k] = a[r][k] - f * a[c][k];
+        }
+    }
+    double h[8];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 7; i >= 0; --i) {
+        double s = a[i][8];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int k = i + 1; k < 8; ++k) s = s - a[i][k] * h[k];
+        h[i] = s / a[i][i];
+    }
+    const double Hn[9] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], 1.0};
+    const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double T[9];
+    mat3_mul(invHnorm, Hn, T);
+    mat3_mul(T, Hnorm2, H);
+    const double s = 1. / H[8];
+    bool ok = true;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 9; ++i) {
+        H[i] = H[i] * s;
+        ok = ok && isfinite(H[i]);
+    }
+    return ok;
+}
+
+// One hypothesis: returns 1 (model written), kStatusNoModel, or kStatusNoSample.
+// pts4: N packed {x, y, x', y'}. idx_out (optional) receives the accepted sample.
+MCV_HD int h_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, double* H, HModelF* mf,
+                        int* idx_out) {
+    HypStream rs;
+    rs.init(seed, hyp);
+    float sx[4], sy[4], dx[4], dy[4];
+    int idx[4];
+    for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
+        if (!draw_distinct<4>(rs, N, idx)) continue;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = 0; i < 4; ++i) {
+            const float* p = pts4 + 4 * (int64_t)idx[i];
+            sx[i] = p[0]; sy[i] = p[1]; dx[i] = p[2]; dy[i] = p[3];
+        }
+        if (!h_check_subset(sx, sy, dx, dy)) continue;
+        if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
+        if (!h_solve4(sx, sy, dx, dy, H)) return kStatusNoModel;
+        bool ok = true;
+        for (int i = 0; i < 8; ++i) {
+            mf->h[i] = (float)H[i];
+            ok = ok && isfinite(mf->h[i]);
+        }
+        return ok ? 1 : kStatusNoModel;
+    }
+    return kStatusNoSample;
+}
+
+// HomographyEstimatorCallback::computeError for one correspondence (fp32, as written).
+MCV_HD float h_error(const float* h, float x, float y, float mx, float my) {
+    const float ww = 1.f / (h[6] * x + h[7] * y + 1.f);
+    const float ex = (h[0] * x + h[1] * y + h[2]) * ww - mx;
+    const float ey = (h[3] * x + h[4] * y + h[5]) * ww - my;
+    return ex * ex + ey * ey;
+}
+
+}  // namespace mcv

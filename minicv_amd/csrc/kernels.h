@@ -1,0 +1,47 @@
+// kernels.h — host-side launchers of the gfx950 kernels (definitions in *.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mcv {
+
+// Hypotheses per wave in the inlier sweep (models live in SGPRs: 8 per hypothesis).
+static const int kVerifyHypPerWave = 8;
+// Upper bound of reduction partial blocks (reduce.h).
+static const int kReduceMaxBlocksHost = 1024;
+
+// ---- homography (ransac_h.hip)
+struct HOneOut {
+    double H[9];
+    float hf[8];
+    int status;
+    int idx[4];
+};
+void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOut* d_out, hipStream_t s);
+void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+                       int* d_counts, hipStream_t s);
+void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
+                     hipStream_t s);
+void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, uint8_t* d_mask, int* d_count,
+                   hipStream_t s);
+void h_reduce_sums(const float* d_pts4, int N, const uint8_t* d_mask, double* d_part, double* d_out, hipStream_t s);
+void h_reduce_absdev(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, double* d_part,
+                     double* d_out, hipStream_t s);
+void h_reduce_ltl(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,
+                  double* d_part, double* d_out, hipStream_t s);
+void h_reduce_lm(const float* d_pts4, int N, const uint8_t* d_mask, const double* h8, bool wantJ, double* d_part,
+                 double* d_out, hipStream_t s);
+
+// ---- shared (ransac_h.hip)
+void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uint64_t* d_pkey, int64_t* d_pfail,
+                 uint64_t* d_out, hipStream_t s);
+void launch_fill_u8(uint8_t* d, int n, uint8_t v, hipStream_t s);
+
+// ---- matchers (match_hamming.hip, match_l2.hip)
+int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc, int* d_idx,
+                         int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s);
+int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim, int* d_idx, float* d_dist,
+                    int* d_idx2, float* d_dist2, hipStream_t s);
+
+}  // namespace mcv

@@ -1,0 +1,122 @@
+// mcv_common.h — shared definitions for the MI355X MiniCVNative kernels and their host twins.
+//
+// Everything here is compiled twice: for gfx950 (kernels) and for x86-64 (shim host code and
+// the mcvHost* test hooks). Files that include it are built with -ffp-contract=off so that every
+// floating-point expression rounds exactly as written on both sides (bit-exact inlier masks).
+#pragma once
+
+#include <stdint.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define MCV_HD __host__ __device__ __forceinline__
+#else
+#define MCV_HD inline
+#endif
+
+namespace mcv {
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11). Counter-based: hypothesis i's random stream is a pure
+// function of (seed, i), so hypotheses can be generated in any order, on any GPU, and replayed
+// on the host. Replaces OpenCV's sequential cv::RNG(-1) in RANSACPointSetRegistrator::getSubset
+// (documented divergence).
+// ---------------------------------------------------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+
+MCV_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+MCV_HD U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
+        const uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+        U4 n;
+        n.x = hi1 ^ c.y ^ k0;
+        n.y = lo1;
+        n.z = hi0 ^ c.w ^ k1;
+        n.w = lo0;
+        c = n;
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+
+// Stream of 32-bit words for one hypothesis. Word s lives in block s/4 (one Philox call per
+// block), lane s%4. Counter = {block, hyp_lo, hyp_hi, tag}, key = {seed_lo, seed_hi}.
+static const uint32_t kStreamTag = 0x4D435631u;  // "MCV1"
+
+struct HypStream {
+    uint32_t k0, k1, hlo, hhi;
+    uint32_t block;   // next block to generate
+    U4 buf;
+    int avail;        // words left in buf (taken from x..w in order)
+
+    MCV_HD void init(uint64_t seed, uint64_t hyp) {
+        k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32);
+        hlo = (uint32_t)hyp; hhi = (uint32_t)(hyp >> 32);
+        block = 0; avail = 0;
+        buf.x = buf.y = buf.z = buf.w = 0;
+    }
+    MCV_HD uint32_t next() {
+        if (avail == 0) {
+            U4 c; c.x = block; c.y = hlo; c.z = hhi; c.w = kStreamTag;
+            buf = philox4x32_10(c, k0, k1);
+            ++block;
+            avail = 4;
+        }
+        uint32_t v;
+        switch (4 - avail) {
+            case 0: v = buf.x; break;
+            case 1: v = buf.y; break;
+            case 2: v = buf.z; break;
+            default: v = buf.w; break;
+        }
+        --avail;
+        return v;
+    }
+    // Uniform index in [0, n): Lemire multiply-shift (deterministic, integer only).
+    MCV_HD int uniform(int n) { return (int)mulhi32(next(), (uint32_t)n); }
+};
+
+// Sampler bounds. kMaxAttempts follows RANSACPointSetRegistrator::run's getSubset(..., 10000)
+// [ext: OpenCV 4.x ptsetreg.cpp]; kMaxRedraw bounds the duplicate-rejection loop (OpenCV's is
+// unbounded; with N >= m it terminates after a few draws in practice).
+static const int kMaxAttempts = 10000;
+static const int kMaxRedraw = 1000;
+
+// Per-hypothesis status codes stored in the counts array.
+static const int kStatusNoModel = -1;   // minimal solver degenerate -> OpenCV `continue`
+static const int kStatusNoSample = -2;  // sampler exhausted attempts -> OpenCV `break`
+
+static const double kDblEpsilon = 2.2204460492503131e-16;
+static const float kFltEpsilon = 1.19209290e-07f;
+
+// Draw m distinct indices from [0, N) with duplicate rejection (getSubset's inner loop).
+// Returns false if the redraw bound is hit.
+template <int M>
+MCV_HD bool draw_distinct(HypStream& rs, int N, int (&idx)[M]) {
+    for (int i = 0; i < M; ++i) {
+        int tries = 0;
+        int v = rs.uniform(N);
+        for (;;) {
+            bool dup = false;
+            for (int j = 0; j < i; ++j) dup |= (idx[j] == v);
+            if (!dup) break;
+            if (++tries >= kMaxRedraw) return false;
+            v = rs.uniform(N);
+        }
+        idx[i] = v;
+    }
+    return true;
+}
+
+}  // namespace mcv

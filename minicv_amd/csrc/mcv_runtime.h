@@ -1,0 +1,87 @@
+// mcv_runtime.h — host runtime helpers for the C-ABI shim: per-thread last error, HIP error
+// checking, device-buffer RAII. No exception crosses an extern "C" boundary: every export wraps
+// its body in MCV_GUARD, which records the message and returns the export's failure value.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdexcept>
+#include <string>
+#include <cstdio>
+#include <cstdarg>
+
+namespace mcv {
+
+struct Error : std::runtime_error {
+    explicit Error(const std::string& m) : std::runtime_error(m) {}
+};
+
+void set_last_error(const char* msg);
+void clear_last_error();
+
+[[noreturn]] inline void fail(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    throw Error(buf);
+}
+
+#define MCV_HIP(call)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (call);                                                                         \
+        if (e_ != hipSuccess) ::mcv::fail("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                                          __LINE__);                                                    \
+    } while (0)
+
+// Throws unless a HIP device is usable: the product path has no CPU fallback.
+void require_device();
+
+#define MCV_GUARD(failval, ...)                                                     \
+    try {                                                                           \
+        ::mcv::clear_last_error();                                                  \
+        __VA_ARGS__                                                                 \
+    } catch (const std::exception& ex) {                                            \
+        ::mcv::set_last_error(ex.what());                                           \
+        return failval;                                                             \
+    } catch (...) {                                                                 \
+        ::mcv::set_last_error("unknown exception");                                 \
+        return failval;                                                             \
+    }
+
+// Device allocation that grows on demand (never shrinks) and is freed on destruction.
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void ensure(size_t count) {
+        if (count <= n) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        MCV_HIP(hipMalloc((void**)&p, (count ? count : 1) * sizeof(T)));
+        n = count;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+template <class T>
+struct PinnedBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void ensure(size_t count) {
+        if (count <= n) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        MCV_HIP(hipHostMalloc((void**)&p, (count ? count : 1) * sizeof(T), hipHostMallocDefault));
+        n = count;
+    }
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+}  // namespace mcv

@@ -1,0 +1,81 @@
+// plan.h — device workspace of one RANSAC problem family (homography or fundamental) on one GPU.
+#pragma once
+
+#include "minicv_native.h"
+#include "mcv_runtime.h"
+#include <stdint.h>
+
+namespace mcv {
+
+// Host-API chunking of the hypothesis stream for the adaptive (sequential-replay) search.
+static const int64_t kChunkFirst = 4096;
+static const int64_t kChunkMax = 1 << 20;
+
+size_t model_bytes(int model);
+int model_points(int model);
+
+struct Plan {
+    int model = MCV_MODEL_HOMOGRAPHY;
+    int device = 0;
+    int maxN = 0;
+    int64_t maxHyps = 0;
+    hipStream_t stream = nullptr;   // only for the host-pointer exports
+
+    DevBuf<float> pts;        // packed float4 correspondences (host-API path)
+    DevBuf<uint8_t> models;   // per-hypothesis fp32 models
+    DevBuf<int> counts;       // per-hypothesis status / inlier count
+    DevBuf<uint64_t> pkey;    // best-key partials
+    DevBuf<int64_t> pfail;
+    DevBuf<uint64_t> key;
+    DevBuf<double> part;      // reduction partials
+    DevBuf<double> red;       // reduction result
+    DevBuf<uint8_t> mask;
+    DevBuf<int> count;
+    DevBuf<uint8_t> one;      // single-hypothesis output record
+    PinnedBuf<int> h_counts;
+    PinnedBuf<double> h_red;
+    PinnedBuf<float> h_pack;
+    PinnedBuf<uint8_t> h_one;
+    PinnedBuf<int> h_i;
+
+    void reserve(int n, int64_t hyps);
+    hipStream_t own_stream();
+    ~Plan();
+};
+
+Plan& thread_plan(int model);
+
+// Opt-in kernel timing with HIP events recorded on the launch stream (bench.py's live roofline).
+bool prof_enabled();
+void prof_record(const char* name, hipEvent_t a, hipEvent_t b);
+struct ProfScope {
+    const char* name;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(const char* n, hipStream_t st) : name(n), s(st) {
+        if (prof_enabled() && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+            (void)hipEventRecord(a, s);
+    }
+    ~ProfScope() {
+        if (a && b) {
+            (void)hipEventRecord(b, s);
+            prof_record(name, a, b);
+        }
+    }
+};
+void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst, hipStream_t s);
+double effective_threshold(const RansacConfig& cfg);
+RansacConfig config_or_default(const RansacConfig* cfg);
+int64_t ransac_search(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, hipStream_t s);
+int finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
+             uint8_t* d_mask, hipStream_t s);
+
+// fundamental-matrix family (ransac_f.hip / ransac_f_host.cpp)
+void f_evaluate_chunk(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
+                      int* d_counts, hipStream_t s);
+int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* F, uint8_t* d_mask,
+               hipStream_t s);
+int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F);
+int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F9, float* Ff9, int* sampleIdx);
+
+}  // namespace mcv

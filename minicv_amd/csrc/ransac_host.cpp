@@ -1,0 +1,509 @@
+// ransac_host.cpp — host orchestration of the RANSAC hot path behind the C-ABI.
+//
+// cvFindHomography (new export, conventions of cvRecoverPose, MiniCVNative.cpp:197-215):
+//   pack V2d -> float4 on device  ->  [chunks of hypotheses: generate + verify on the GPU,
+//   counts back, OpenCV-order sequential replay on the host (adaptive niters)]  ->  finalize:
+//   mask of the winner, refit on its inliers (runKernel: GPU reductions + 9x9 Jacobi here),
+//   10 Levenberg-Marquardt iterations (GPU reductions + 8x8 solve here)  ->  H, mask.
+// Mirrors cv::findHomography(..., RANSAC, thr, mask, maxIters, conf) of OpenCV 4.x
+// [ext: calib3d/src/fundam.cpp, ptsetreg.cpp, levmarq.cpp — absent here, SURVEY.md §8c].
+#include "minicv_native.h"
+#include "mcv_runtime.h"
+#include "kernels.h"
+#include "linalg.h"
+#include "mcv_common.h"
+#include "hyp_homography.h"
+#include "plan.h"
+
+#include <cmath>
+#include <cfloat>
+#include <cstring>
+#include <vector>
+#include <algorithm>
+#include <memory>
+
+namespace mcv {
+
+// ------------------------------------------------------------------------------------------
+// Sequential replay (RANSACPointSetRegistrator::run loop order + RANSACUpdateNumIters).
+// ------------------------------------------------------------------------------------------
+int ransac_update_num_iters(double p, double ep, int modelPoints, int64_t maxIters) {
+    p = std::max(p, 0.);
+    p = std::min(p, 1.);
+    ep = std::max(ep, 0.);
+    ep = std::min(ep, 1.);
+    double num = std::max(1. - p, DBL_MIN);
+    double denom = 1. - std::pow(1. - ep, modelPoints);
+    if (denom < DBL_MIN) return 0;
+    num = std::log(num);
+    denom = std::log(denom);
+    return (denom >= 0 || -num >= (double)maxIters * (-denom)) ? (int)maxIters : (int)std::lrint(num / denom);
+}
+
+}  // namespace mcv
+
+using namespace mcv;
+
+extern "C" MCV_API void mcvReplayInit(mcvReplayState* st, int maxIters) {
+    st->niters = std::max(maxIters, 1);
+    st->bestIndex = -1;
+    st->bestCount = 0;
+    st->stopped = 0;
+}
+
+extern "C" MCV_API int mcvReplayChunk(mcvReplayState* st, const int* counts, int64_t hypBegin, int64_t hypCount,
+                                      int N, int modelPoints, double confidence, int fixedIters) {
+    if (st->stopped) return 1;
+    for (int64_t i = 0; i < hypCount; ++i) {
+        const int64_t it = hypBegin + i;
+        if (it >= st->niters) { st->stopped = 1; return 1; }
+        const int c = counts[i];
+        if (c == kStatusNoSample) { st->stopped = 1; return 1; }
+        if (c < 0) continue;
+        if (c > std::max(st->bestCount, modelPoints - 1)) {
+            st->bestCount = c;
+            st->bestIndex = it;
+            if (!fixedIters)
+                st->niters = ransac_update_num_iters(confidence, (double)(N - c) / N, modelPoints, st->niters);
+        }
+    }
+    if (hypBegin + hypCount >= st->niters) { st->stopped = 1; return 1; }
+    return 0;
+}
+
+namespace mcv {
+
+// ------------------------------------------------------------------------------------------
+// Plan
+// ------------------------------------------------------------------------------------------
+void Plan::reserve(int n, int64_t hyps) {
+    if (n > maxN) maxN = n;
+    if (hyps > maxHyps) maxHyps = hyps;
+    pts.ensure((size_t)maxN * 4);
+    models.ensure((size_t)maxHyps * model_bytes(model));
+    counts.ensure((size_t)maxHyps);
+    pkey.ensure(512);
+    pfail.ensure(512);
+    key.ensure(2);
+    part.ensure((size_t)kReduceMaxBlocksHost * 64);
+    red.ensure(64);
+    mask.ensure((size_t)maxN);
+    count.ensure(1);
+    one.ensure(512);
+    h_counts.ensure((size_t)maxHyps);
+    h_red.ensure(64);
+    h_pack.ensure((size_t)maxN * 4);
+    h_one.ensure(512);
+    h_i.ensure(4);
+}
+
+size_t model_bytes(int model) { return model == MCV_MODEL_FUNDAMENTAL ? 80 : 32; }
+
+hipStream_t Plan::own_stream() {
+    if (!stream) MCV_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    return stream;
+}
+
+Plan::~Plan() {
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+// Per-thread cached plans for the host-pointer exports (one per device and model).
+Plan& thread_plan(int model) {
+    int dev = 0;
+    MCV_HIP(hipGetDevice(&dev));
+    thread_local std::vector<std::unique_ptr<Plan>> plans;
+    for (auto& p : plans)
+        if (p->device == dev && p->model == model) return *p;
+    plans.emplace_back(new Plan());
+    plans.back()->device = dev;
+    plans.back()->model = model;
+    return *plans.back();
+}
+
+void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst, hipStream_t s) {
+    P.h_pack.ensure((size_t)N * 4);
+    float* h = P.h_pack.p;
+    for (int i = 0; i < N; ++i) {   // OpenCV: points.convertTo(CV_32F)
+        h[4 * i + 0] = (float)a[i].X;
+        h[4 * i + 1] = (float)a[i].Y;
+        h[4 * i + 2] = (float)b[i].X;
+        h[4 * i + 3] = (float)b[i].Y;
+    }
+    MCV_HIP(hipMemcpyAsync(d_dst, h, (size_t)N * 16, hipMemcpyHostToDevice, s));
+    MCV_HIP(hipStreamSynchronize(s));
+}
+
+double effective_threshold(const RansacConfig& cfg) { return cfg.threshold > 0 ? cfg.threshold : 3.0; }
+
+// Sum V doubles over (masked) correspondences: GPU two-stage reduction, result to host.
+template <class F>
+static void reduce_to_host(Plan& P, hipStream_t s, int V, double* out, F launch) {
+    launch(P.part.p, P.red.p);
+    MCV_HIP(hipGetLastError());
+    MCV_HIP(hipMemcpyAsync(P.h_red.p, P.red.p, V * sizeof(double), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    std::memcpy(out, P.h_red.p, V * sizeof(double));
+}
+
+// HomographyEstimatorCallback::runKernel over the masked correspondences (mask == NULL: all).
+bool h_refit(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipStream_t s, double* H) {
+    double sums[5];
+    reduce_to_host(P, s, 5, sums, [&](double* part, double* red) { h_reduce_sums(d_pts, N, d_mask, part, red, s); });
+    const double count = sums[4];
+    if (count <= 0) return false;
+    double c4[4] = {sums[0] / count, sums[1] / count, sums[2] / count, sums[3] / count};   // cm.x, cm.y, cM.x, cM.y
+    double dev[4];
+    reduce_to_host(P, s, 4, dev, [&](double* part, double* red) { h_reduce_absdev(d_pts, N, d_mask, c4, part, red, s); });
+    for (int k = 0; k < 4; ++k)
+        if (std::fabs(dev[k]) < DBL_EPSILON) return false;
+    double s4[4] = {count / dev[0], count / dev[1], count / dev[2], count / dev[3]};   // sm.x, sm.y, sM.x, sM.y
+    double ltl[45];
+    reduce_to_host(P, s, 45, ltl, [&](double* part, double* red) { h_reduce_ltl(d_pts, N, d_mask, c4, s4, part, red, s); });
+    double A[81], w[9], V[81];
+    int o = 0;
+    for (int j = 0; j < 9; ++j)
+        for (int k = j; k < 9; ++k) { A[j * 9 + k] = ltl[o]; A[k * 9 + j] = ltl[o]; ++o; }
+    jacobi_eigen(A, 9, w, V);
+    const double* H0 = V + 8 * 9;   // eigenvector of the smallest eigenvalue
+    const double invHnorm[9] = {1. / s4[0], 0, c4[0], 0, 1. / s4[1], c4[1], 0, 0, 1};
+    const double Hnorm2[9] = {s4[2], 0, -c4[2] * s4[2], 0, s4[3], -c4[3] * s4[3], 0, 0, 1};
+    double T[9], R[9];
+    mat3_mul(invHnorm, H0, T);
+    mat3_mul(T, Hnorm2, R);
+    const double sc = 1. / R[8];
+    for (int k = 0; k < 9; ++k) {
+        H[k] = R[k] * sc;
+        if (!std::isfinite(H[k])) return false;
+    }
+    return true;
+}
+
+// LMSolver::create(HomographyRefineCallback(src, dst), 10)->run(H8) — the classic LMSolverImpl
+// (Marquardt-Nielsen lambda control, eigen-based solve). The O(N) JtJ / Jtr / |r|^2 sums run on
+// the GPU; the 8x8 algebra runs here.
+void h_lm_refine(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipStream_t s, double* H, int maxIters) {
+    const int lx = 8;
+    const double epsx = FLT_EPSILON, epsf = FLT_EPSILON;
+    double x[8], xd[8], d[8], v[8], A[64], Ap[64], D[8], temp_d[8];
+    for (int i = 0; i < 8; ++i) x[i] = H[i];
+    auto compute = [&](const double* h, bool wantJ, double* Aout, double* vout) -> double {
+        double buf[45];
+        if (wantJ) {
+            reduce_to_host(P, s, 45, buf, [&](double* part, double* red) { h_reduce_lm(d_pts, N, d_mask, h, true, part, red, s); });
+            int o = 0;
+            for (int j = 0; j < 8; ++j)
+                for (int k = j; k < 8; ++k) { Aout[j * 8 + k] = buf[o]; Aout[k * 8 + j] = buf[o]; ++o; }
+            for (int j = 0; j < 8; ++j) vout[j] = buf[36 + j];
+            return buf[44];
+        }
+        reduce_to_host(P, s, 1, buf, [&](double* part, double* red) { h_reduce_lm(d_pts, N, d_mask, h, false, part, red, s); });
+        return buf[0];
+    };
+    double S = compute(x, true, A, v);
+    for (int i = 0; i < lx; ++i) D[i] = A[i * lx + i];
+    const double Rlo = 0.25, Rhi = 0.75;
+    double lambda = 1, lc = 0.75;
+    int iter = 0;
+    for (;;) {
+        for (int i = 0; i < lx * lx; ++i) Ap[i] = A[i];
+        for (int i = 0; i < lx; ++i) Ap[i * lx + i] += lambda * D[i];
+        eig_solve(Ap, lx, v, d);
+        for (int i = 0; i < lx; ++i) xd[i] = x[i] - d[i];
+        const double Sd = compute(xd, false, nullptr, nullptr);
+        for (int i = 0; i < lx; ++i) {   // temp_d = -A d + 2 v
+            double acc = 0;
+            for (int k = 0; k < lx; ++k) acc += A[i * lx + k] * d[k];
+            temp_d[i] = -acc + 2 * v[i];
+        }
+        double dS = 0;
+        for (int i = 0; i < lx; ++i) dS += d[i] * temp_d[i];
+        const double R = (S - Sd) / (std::fabs(dS) > DBL_EPSILON ? dS : 1);
+        if (R > Rhi) {
+            lambda *= 0.5;
+            if (lambda < lc) lambda = 0;
+        } else if (R < Rlo) {
+            double t = 0;
+            for (int i = 0; i < lx; ++i) t += d[i] * v[i];
+            double nu = (Sd - S) / (std::fabs(t) > DBL_EPSILON ? t : 1) + 2;
+            nu = std::min(std::max(nu, 2.), 10.);
+            if (lambda == 0) {
+                eig_invert(A, lx, Ap);
+                double maxval = DBL_EPSILON;
+                for (int i = 0; i < lx; ++i) maxval = std::max(maxval, std::fabs(Ap[i * lx + i]));
+                lambda = lc = 1. / maxval;
+                nu *= 0.5;
+            }
+            lambda *= nu;
+        }
+        if (Sd < S) {
+            S = Sd;
+            for (int i = 0; i < lx; ++i) x[i] = xd[i];
+            S = compute(x, true, A, v);
+        }
+        ++iter;
+        double dn = 0;
+        for (int i = 0; i < lx; ++i) dn = std::max(dn, std::fabs(d[i]));
+        const bool proceed = iter < maxIters && dn >= epsx && S >= epsf * epsf;
+        if (!proceed) break;
+    }
+    for (int i = 0; i < 8; ++i) H[i] = x[i];
+}
+
+// Evaluate one chunk of hypotheses on the device (generate + verify [+ best key]).
+void evaluate_chunk(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
+                    int* d_counts, uint64_t* d_key, hipStream_t s) {
+    const double t = effective_threshold(cfg);
+    const float thr2 = (float)(t * t);
+    if (P.model == MCV_MODEL_HOMOGRAPHY) {
+        launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+        ProfScope ps("h_verify", s);
+        launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, s);
+    } else {
+        f_evaluate_chunk(P, d_pts, N, cfg, hypBegin, hypCount, d_counts, s);
+    }
+    if (d_key) launch_best(d_counts, hypCount, hypBegin, model_points(P.model), P.pkey.p, P.pfail.p, d_key, s);
+    MCV_HIP(hipGetLastError());
+}
+
+int model_points(int model) { return model == MCV_MODEL_FUNDAMENTAL ? 8 : 4; }
+
+// Winner -> mask (+ refit + LM). Returns inlier count, 0 on failure. Synchronises s.
+int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* H, uint8_t* d_mask,
+               hipStream_t s) {
+    const double t = effective_threshold(cfg);
+    const float thr2 = (float)(t * t);
+    HOneOut* d_one = (HOneOut*)P.one.p;
+    launch_h_one(d_pts, N, cfg.seed, hyp, d_one, s);
+    MCV_HIP(hipGetLastError());
+    HOneOut one;
+    MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(HOneOut), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    std::memcpy(&one, P.h_one.p, sizeof(HOneOut));
+    if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
+    MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
+    launch_h_mask(d_pts, N, one.hf, thr2, d_mask, P.count.p, s);
+    MCV_HIP(hipGetLastError());
+    MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    const int count = P.h_i.p[0];
+    for (int k = 0; k < 9; ++k) H[k] = one.H[k];
+    if (cfg.flags & MCV_FLAG_NO_REFINE) return count;
+    if (N > 4 && count > 0) {
+        double Hr[9];
+        if (h_refit(P, d_pts, N, d_mask, s, Hr))
+            for (int k = 0; k < 9; ++k) H[k] = Hr[k];
+        h_lm_refine(P, d_pts, N, d_mask, s, H, 10);
+    }
+    return count;
+}
+
+int finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
+             uint8_t* d_mask, hipStream_t s) {
+    if (P.model == MCV_MODEL_HOMOGRAPHY) return h_finalize(P, d_pts, N, cfg, hyp, model9, d_mask, s);
+    return f_finalize(P, d_pts, N, cfg, hyp, model9, d_mask, s);
+}
+
+// Full RANSAC on device-resident points with the OpenCV sequential-replay semantics.
+// Returns the best hypothesis index or -1.
+int64_t ransac_search(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, hipStream_t s) {
+    const int m = model_points(P.model);
+    mcvReplayState st;
+    mcvReplayInit(&st, cfg.maxIters);
+    const bool fixed = (cfg.flags & MCV_FLAG_FIXED_ITERS) != 0;
+    int64_t begin = 0;
+    int64_t chunk = std::min<int64_t>(std::max<int64_t>(st.niters, 1), kChunkFirst);
+    while (!st.stopped) {
+        const int64_t remaining = st.niters - begin;
+        if (remaining <= 0) break;
+        const int cnt = (int)std::min<int64_t>(remaining, chunk);
+        P.reserve(N, cnt);
+        evaluate_chunk(P, d_pts, N, cfg, begin, cnt, P.counts.p, nullptr, s);
+        MCV_HIP(hipMemcpyAsync(P.h_counts.p, P.counts.p, (size_t)cnt * sizeof(int), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        mcvReplayChunk(&st, P.h_counts.p, begin, cnt, N, m, cfg.confidence, fixed ? 1 : 0);
+        begin += cnt;
+        chunk = std::min<int64_t>(chunk * 2, kChunkMax);
+    }
+    return st.bestIndex;
+}
+
+void require_device() {
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        fail("no HIP device available (hipGetDeviceCount: %s, n=%d); the MI355X path has no CPU fallback",
+             hipGetErrorString(e), n);
+}
+
+RansacConfig config_or_default(const RansacConfig* cfg) {
+    if (cfg) return *cfg;
+    RansacConfig c;
+    std::memset(&c, 0, sizeof(c));
+    c.threshold = 3.0;
+    c.confidence = 0.995;
+    c.maxIters = 2000;
+    c.method = MCV_METHOD_RANSAC;
+    return c;
+}
+
+}  // namespace mcv
+
+// ------------------------------------------------------------------------------------------
+// Exports
+// ------------------------------------------------------------------------------------------
+extern "C" MCV_API int cvFindHomography(const mcvV2d* src, const mcvV2d* dst, const int N, const RansacConfig* cfgp,
+                                        mcvM33d* H, uint8_t* mask) {
+    MCV_GUARD(0, {
+        if (!src || !dst || !H || N < 0) fail("cvFindHomography: null argument or negative N");
+        if (mask) std::memset(mask, 0, (size_t)N);
+        if (N < 4) fail("cvFindHomography: need at least 4 correspondences (N=%d)", N);
+        const RansacConfig cfg = config_or_default(cfgp);
+        if (cfg.method != MCV_METHOD_RANSAC && cfg.method != MCV_METHOD_LSQ)
+            fail("cvFindHomography: unsupported method %d", cfg.method);
+        if (cfg.method == MCV_METHOD_RANSAC && !(cfg.confidence > 0 && cfg.confidence < 1))
+            fail("cvFindHomography: confidence must be in (0,1)");
+        require_device();
+        Plan& P = thread_plan(MCV_MODEL_HOMOGRAPHY);
+        hipStream_t s = P.own_stream();
+        P.reserve(N, 1);
+        pack_points(P, src, dst, N, P.pts.p, s);
+        double Hm[9];
+        int count = 0;
+        if (cfg.method == MCV_METHOD_LSQ || N == 4) {
+            if (!h_refit(P, P.pts.p, N, nullptr, s, Hm)) fail("cvFindHomography: degenerate point set");
+            if (N > 4) h_lm_refine(P, P.pts.p, N, nullptr, s, Hm, 10);
+            if (mask) std::memset(mask, 1, (size_t)N);
+            count = N;
+        } else {
+            const int64_t best = ransac_search(P, P.pts.p, N, cfg, s);
+            if (best < 0) fail("cvFindHomography: RANSAC found no model with >= 4 inliers");
+            count = h_finalize(P, P.pts.p, N, cfg, best, Hm, P.mask.p, s);
+            if (mask) {
+                MCV_HIP(hipMemcpyAsync(mask, P.mask.p, (size_t)N, hipMemcpyDeviceToHost, s));
+                MCV_HIP(hipStreamSynchronize(s));
+            }
+        }
+        for (int k = 0; k < 9; ++k) H->M[k] = Hm[k];
+        return count;
+    })
+}
+
+extern "C" MCV_API mcvRansacPlan* mcvRansacPlanCreate(int model, int maxN, int64_t maxHyps) {
+    MCV_GUARD(nullptr, {
+        if (model != MCV_MODEL_HOMOGRAPHY && model != MCV_MODEL_FUNDAMENTAL) fail("unknown model %d", model);
+        require_device();
+        std::unique_ptr<Plan> p(new Plan());
+        MCV_HIP(hipGetDevice(&p->device));
+        p->model = model;
+        p->reserve(std::max(maxN, 1), std::max<int64_t>(maxHyps, 1));
+        return reinterpret_cast<mcvRansacPlan*>(p.release());
+    })
+}
+
+extern "C" MCV_API void mcvRansacPlanDestroy(mcvRansacPlan* plan) {
+    try {
+        delete reinterpret_cast<Plan*>(plan);
+    } catch (...) {
+    }
+}
+
+extern "C" MCV_API int mcvPackCorrespondences(const mcvV2d* a, const mcvV2d* b, int N, float* d_pts4, void* stream) {
+    MCV_GUARD(0, {
+        if (!a || !b || !d_pts4 || N < 0) fail("mcvPackCorrespondences: bad argument");
+        require_device();
+        Plan& P = thread_plan(MCV_MODEL_HOMOGRAPHY);
+        pack_points(P, a, b, N, d_pts4, (hipStream_t)stream);
+        return 1;
+    })
+}
+
+extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const float* d_pts4, int N, const RansacConfig* cfg,
+                                         int64_t hypBegin, int64_t hypCount, uint64_t* d_key, int* d_counts,
+                                         void* stream) {
+    MCV_GUARD(0, {
+        Plan* P = reinterpret_cast<Plan*>(plan);
+        if (!P || !d_pts4 || !cfg || !d_key) fail("mcvRansacEvaluate: null argument");
+        if (N < model_points(P->model)) fail("mcvRansacEvaluate: N=%d below the minimal sample", N);
+        if (hypCount <= 0 || hypCount > P->maxHyps) fail("mcvRansacEvaluate: hypCount %lld outside plan capacity %lld",
+                                                         (long long)hypCount, (long long)P->maxHyps);
+        if (hypBegin < 0 || hypBegin + hypCount > 0xFFFFFFFFll) fail("mcvRansacEvaluate: hypothesis index beyond 2^32");
+        evaluate_chunk(*P, d_pts4, N, *cfg, hypBegin, (int)hypCount, d_counts ? d_counts : P->counts.p, d_key,
+                       (hipStream_t)stream);
+        return 1;
+    })
+}
+
+extern "C" MCV_API int mcvRansacFinalize(mcvRansacPlan* plan, const float* d_pts4, int N, const RansacConfig* cfg,
+                                         int64_t hypIndex, double* model9, uint8_t* d_mask, void* stream) {
+    MCV_GUARD(0, {
+        Plan* P = reinterpret_cast<Plan*>(plan);
+        if (!P || !d_pts4 || !cfg || !model9 || !d_mask) fail("mcvRansacFinalize: null argument");
+        if (hypIndex < 0) fail("mcvRansacFinalize: no winning hypothesis");
+        P->reserve(N, 1);
+        return finalize(*P, d_pts4, N, *cfg, hypIndex, model9, d_mask, (hipStream_t)stream);
+    })
+}
+
+extern "C" MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, uint64_t seed, int64_t hyp,
+                                         double* model9, float* modelf9, int* sampleIdx) {
+    MCV_GUARD(kStatusNoSample - 1, {
+        if (!pts4 || !model9 || !modelf9) fail("mcvHostHypothesis: null argument");
+        if (model == MCV_MODEL_HOMOGRAPHY) {
+            if (N < 4) fail("N < 4");
+            HModelF mf;
+            for (int k = 0; k < 9; ++k) model9[k] = 0;
+            for (int k = 0; k < 8; ++k) mf.h[k] = 0;
+            const int st = h_hypothesis(pts4, N, seed, (uint64_t)hyp, model9, &mf, sampleIdx);
+            for (int k = 0; k < 8; ++k) modelf9[k] = mf.h[k];
+            modelf9[8] = 1.f;
+            return st;
+        }
+        return f_host_hypothesis(pts4, N, seed, hyp, model9, modelf9, sampleIdx);
+    })
+}
+
+extern "C" MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                                      uint32_t* out4) {
+    U4 c;
+    c.x = c0; c.y = c1; c.z = c2; c.w = c3;
+    const U4 r = philox4x32_10(c, k0, k1);
+    out4[0] = r.x; out4[1] = r.y; out4[2] = r.z; out4[3] = r.w;
+}
+
+extern "C" MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, const int N, const RansacConfig* cfgp,
+                                            mcvM33d* F, uint8_t* mask) {
+    MCV_GUARD(0, {
+        if (!a || !b || !F || N < 0) fail("cvFindFundamentalMat: null argument or negative N");
+        if (mask) std::memset(mask, 0, (size_t)N);
+        if (N < 8) fail("cvFindFundamentalMat: need at least 8 correspondences (N=%d)", N);
+        RansacConfig cfg = config_or_default(cfgp);
+        if (!cfgp) cfg.confidence = 0.99;
+        if (cfg.method != MCV_METHOD_RANSAC && cfg.method != MCV_METHOD_LSQ)
+            fail("cvFindFundamentalMat: unsupported method %d", cfg.method);
+        if (cfg.method == MCV_METHOD_RANSAC && !(cfg.confidence > 0 && cfg.confidence < 1))
+            fail("cvFindFundamentalMat: confidence must be in (0,1)");
+        require_device();
+        Plan& P = thread_plan(MCV_MODEL_FUNDAMENTAL);
+        hipStream_t s = P.own_stream();
+        P.reserve(N, 1);
+        pack_points(P, a, b, N, P.pts.p, s);
+        double Fm[9];
+        int count = 0;
+        if (cfg.method == MCV_METHOD_LSQ || N == 8) {
+            count = f_fit_all(P, P.pts.p, N, s, Fm);
+            if (count <= 0) fail("cvFindFundamentalMat: degenerate point set");
+            if (mask) std::memset(mask, 1, (size_t)N);
+        } else {
+            const int64_t best = ransac_search(P, P.pts.p, N, cfg, s);
+            if (best < 0) fail("cvFindFundamentalMat: RANSAC found no model with >= 8 inliers");
+            count = f_finalize(P, P.pts.p, N, cfg, best, Fm, P.mask.p, s);
+            if (mask) {
+                MCV_HIP(hipMemcpyAsync(mask, P.mask.p, (size_t)N, hipMemcpyDeviceToHost, s));
+                MCV_HIP(hipStreamSynchronize(s));
+            }
+        }
+        for (int k = 0; k < 9; ++k) F->M[k] = Fm[k];
+        return count;
+    })
+}

@@ -1,0 +1,156 @@
+// shim.cpp — the rest of the MiniCVNative C-ABI surface: error reporting, device query, and the
+// reference exports that are outside the hot path (they bind, and fail loudly with a message).
+//   cvDetectFeatures / cvFreeFeatures   MiniCVNative.cpp:221-365  (feature detection: out of scope)
+//   cvDetectQRCode / cvDetectArucoMarkers MiniCVNative.cpp:384-502 (fiducials: out of scope)
+//   cvTest                               MiniCVNative.cpp:504      (debug print: no-op)
+//   cvRecoverPose(s), cvFivePoint         MiniCVNative.cpp:165-215,368  (next)
+//   cvSolvePnP*, cvRefinePnP*, solveAp3p  MiniCVNative.cpp:48-163, ap3p.cpp:282 (row f2: next)
+#include "minicv_native.h"
+#include "mcv_runtime.h"
+#include <string>
+#include <cstring>
+
+namespace mcv {
+static thread_local std::string g_last_error;
+void set_last_error(const char* msg) { g_last_error = msg ? msg : ""; }
+void clear_last_error() { g_last_error.clear(); }
+}  // namespace mcv
+
+using namespace mcv;
+
+// ---- kernel timing (opt-in) ----
+#include "plan.h"
+#include <mutex>
+#include <vector>
+namespace {
+struct ProfRec { std::string name; hipEvent_t a, b; };
+std::mutex g_prof_mu;
+std::vector<ProfRec> g_prof;
+bool g_prof_on = false;
+}  // namespace
+namespace mcv {
+bool prof_enabled() { return g_prof_on; }
+void prof_record(const char* name, hipEvent_t a, hipEvent_t b) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof.push_back({name, a, b});
+}
+}  // namespace mcv
+
+extern "C" MCV_API void mcvProfileEnable(int on) { g_prof_on = on != 0; }
+
+extern "C" MCV_API void mcvProfileReset(void) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (auto& r : g_prof) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    g_prof.clear();
+}
+
+extern "C" MCV_API int mcvProfileRead(const char* name, double* total_ms) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    int n = 0;
+    double tot = 0;
+    for (auto& r : g_prof) {
+        if (r.name != name) continue;
+        if (hipEventSynchronize(r.b) != hipSuccess) return -1;
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) return -1;
+        tot += ms;
+        ++n;
+    }
+    if (total_ms) *total_ms = tot;
+    return n;
+}
+
+extern "C" MCV_API const char* mcvGetLastError(void) { return g_last_error.c_str(); }
+
+extern "C" MCV_API const char* mcvVersion(void) { return "minicv-mi355x 0.1.0 (gfx950)"; }
+
+extern "C" MCV_API int mcvDeviceCount(void) {
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice) return 0;
+    if (e != hipSuccess) {
+        set_last_error(hipGetErrorString(e));
+        return -1;
+    }
+    return n;
+}
+
+#define MCV_NOT_IN_SCOPE(name, why) set_last_error(name ": " why)
+
+extern "C" MCV_API int cvRecoverPose(const RecoverPoseConfig*, const int, const mcvV2d*, const mcvV2d*, mcvM33d*,
+                                     mcvV3d*, uint8_t*) {
+    MCV_NOT_IN_SCOPE("cvRecoverPose", "essential-matrix RANSAC is the next row (SURVEY 8f-1), not built yet");
+    return 0;
+}
+
+extern "C" MCV_API bool cvRecoverPoses(const RecoverPoseConfig*, const int, const mcvV2d*, const mcvV2d*, mcvM33d*,
+                                       mcvM33d*, mcvV3d*, uint8_t*) {
+    MCV_NOT_IN_SCOPE("cvRecoverPoses", "essential-matrix RANSAC is the next row (SURVEY 8f-1), not built yet");
+    return false;
+}
+
+extern "C" MCV_API DetectorResult* cvDetectFeatures(char*, int, int, int, int, void*) {
+    MCV_NOT_IN_SCOPE("cvDetectFeatures", "feature detection is outside the MI355X hot path (SURVEY 2 row 4)");
+    return nullptr;
+}
+
+extern "C" MCV_API void cvFreeFeatures(DetectorResult* res) {
+    // Frees a DetectorResult allocated with new[] members (fixes the reference's delete/new[]
+    // mismatch and the PointCount == 0 leak, MiniCVNative.cpp:349-358).
+    if (!res) return;
+    delete[] res->Descriptors;
+    delete[] res->Points;
+    delete res;
+}
+
+extern "C" MCV_API void cvTest(void) {}
+
+extern "C" MCV_API int cvFivePoint(const mcvV2d*, const mcvV2d*, mcvM33d*) {
+    MCV_NOT_IN_SCOPE("cvFivePoint", "five-point solver is the next row (SURVEY 8f-1), not built yet");
+    return 0;
+}
+
+extern "C" MCV_API bool cvSolvePnP(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*, const int,
+                                   mcvV3d*, mcvV3d*) {
+    MCV_NOT_IN_SCOPE("cvSolvePnP", "PnP is the next row (SURVEY 8f-2), not built yet");
+    return false;
+}
+
+extern "C" MCV_API bool cvSolvePnPRansac(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*,
+                                         const int, const int, const float, const double, mcvV3d*, mcvV3d*,
+                                         int* inlierCount, int*) {
+    if (inlierCount) *inlierCount = 0;
+    MCV_NOT_IN_SCOPE("cvSolvePnPRansac", "PnP-RANSAC is the next row (SURVEY 8f-2), not built yet");
+    return false;
+}
+
+extern "C" MCV_API void cvRefinePnPLM(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*, mcvV3d*,
+                                      mcvV3d*) {
+    MCV_NOT_IN_SCOPE("cvRefinePnPLM", "PnP refinement is the next row (SURVEY 8f-2), not built yet");
+}
+
+extern "C" MCV_API void cvRefinePnPVVS(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*, mcvV3d*,
+                                       mcvV3d*) {
+    MCV_NOT_IN_SCOPE("cvRefinePnPVVS", "PnP refinement is the next row (SURVEY 8f-2), not built yet");
+}
+
+extern "C" MCV_API int solveAp3p(mcvM33d*, mcvV3d*, float, float, float, float, float, float, float, float, float,
+                                 float, float, float, float, float, float, float, float, float, float) {
+    MCV_NOT_IN_SCOPE("solveAp3p", "AP3P is the next row (SURVEY 8f-2), not built yet");
+    return 0;
+}
+
+extern "C" MCV_API bool cvDetectQRCode(char*, int, int, int, int*, int* count) {
+    if (count) *count = 0;
+    MCV_NOT_IN_SCOPE("cvDetectQRCode", "QR detection is outside the MI355X hot path (SURVEY 2 row 7)");
+    return false;
+}
+
+extern "C" MCV_API bool cvDetectArucoMarkers(char*, int, int, int, int* infoCount, ArucoMarkerInfo*) {
+    if (infoCount) *infoCount = 0;
+    MCV_NOT_IN_SCOPE("cvDetectArucoMarkers", "ArUco detection is outside the MI355X hot path (SURVEY 2 row 8)");
+    return false;
+}

@@ -1,0 +1,83 @@
+"""Device-level API over torch-allocated HBM buffers (bench.py, multi-GPU ranks).
+
+PyTorch only provides device memory, streams and torch.distributed (RCCL); every kernel runs in
+libMiniCVNative.so. Pointers cross the C-ABI as plain integers (tensor.data_ptr()) and the
+stream as the raw hipStream_t handle of torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import native as N
+
+
+def _stream_handle(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+class RansacPlan:
+    """Workspace for one RANSAC problem family on the current device."""
+
+    def __init__(self, model: int, max_n: int, max_hyps: int):
+        self.model = model
+        self._p = N.lib().mcvRansacPlanCreate(model, int(max_n), int(max_hyps))
+        N.check(bool(self._p), "mcvRansacPlanCreate")
+
+    def close(self):
+        if self._p:
+            N.lib().mcvRansacPlanDestroy(self._p)
+            self._p = None
+
+    __del__ = close
+
+    def evaluate(self, pts4, n: int, cfg: N.RansacConfig, hyp_begin: int, hyp_count: int, key, counts=None,
+                 stream=None) -> None:
+        """Asynchronous: best packed key of [hyp_begin, hyp_begin + hyp_count) -> key[0] (int64 tensor),
+        first sampler failure -> key[1]."""
+        ok = N.lib().mcvRansacEvaluate(self._p, pts4.data_ptr(), int(n), C.addressof(cfg), int(hyp_begin),
+                                       int(hyp_count), key.data_ptr(),
+                                       counts.data_ptr() if counts is not None else None, _stream_handle(stream))
+        N.check(ok == 1, "mcvRansacEvaluate")
+
+    def finalize(self, pts4, n: int, cfg: N.RansacConfig, hyp: int, mask, stream=None):
+        """-> (inlier count, model 3x3 float64); writes the uint8 mask tensor. Synchronises the stream."""
+        m = (C.c_double * 9)()
+        cnt = N.lib().mcvRansacFinalize(self._p, pts4.data_ptr(), int(n), C.addressof(cfg), int(hyp), m,
+                                        mask.data_ptr(), _stream_handle(stream))
+        N.check(cnt > 0, "mcvRansacFinalize")
+        return cnt, np.array(m[:], dtype=np.float64).reshape(3, 3)
+
+
+def unpack_key(key: int):
+    """(count, hypothesis index) from the packed key (count << 32 | 0xFFFFFFFF - idx); (0, -1) if none."""
+    key = int(key) & 0xFFFFFFFFFFFFFFFF
+    if key == 0:
+        return 0, -1
+    return key >> 32, 0xFFFFFFFF - (key & 0xFFFFFFFF)
+
+
+def pack_points_tensor(src: np.ndarray, dst: np.ndarray, device):
+    """(N,2)+(N,2) fp64 -> device float32 [N,4] {x, y, x', y'} (float cast as convertTo(CV_32F))."""
+    import torch
+    p = np.concatenate([src, dst], axis=1).astype(np.float32)
+    return torch.from_numpy(np.ascontiguousarray(p)).to(device)
+
+
+def match_hamming(q, t, idx, dist, idx2=None, dist2=None, stream=None) -> None:
+    r = N.lib().mcvMatchHammingDevice(q.data_ptr(), q.shape[0], t.data_ptr(), t.shape[0], q.shape[1],
+                                      idx.data_ptr(), dist.data_ptr(),
+                                      idx2.data_ptr() if idx2 is not None else None,
+                                      dist2.data_ptr() if dist2 is not None else None, _stream_handle(stream))
+    N.check(r == q.shape[0], "mcvMatchHammingDevice")
+
+
+def match_l2(q, t, idx, dist, idx2=None, dist2=None, stream=None) -> None:
+    r = N.lib().mcvMatchL2Device(q.data_ptr(), q.shape[0], t.data_ptr(), t.shape[0], q.shape[1],
+                                 idx.data_ptr(), dist.data_ptr(),
+                                 idx2.data_ptr() if idx2 is not None else None,
+                                 dist2.data_ptr() if dist2 is not None else None, _stream_handle(stream))
+    N.check(r == q.shape[0], "mcvMatchL2Device")

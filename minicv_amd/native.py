@@ -1,0 +1,135 @@
+"""ctypes binding of libMiniCVNative.so — the same entry points the F# `module OpenCV.Native`
+binds with [<DllImport("MiniCVNative")>] (/root/reference/src/MiniCV/OpenCV.fs:339-382), plus the
+new hot-path exports declared in include/minicv_native.h.
+
+The library is the product: there is no Python or CPU fallback. If it is missing, importing the
+binding raises. Build it with `python -m minicv_amd.build` (or __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+LIB_PATH = Path(os.environ.get("MINICV_NATIVE_LIB",
+                               ROOT / "libs" / "Native" / "MiniCV" / "linux" / "AMD64" / "libMiniCVNative.so"))
+
+
+class V2d(C.Structure):
+    _fields_ = [("X", C.c_double), ("Y", C.c_double)]
+
+
+class V3d(C.Structure):
+    _fields_ = [("X", C.c_double), ("Y", C.c_double), ("Z", C.c_double)]
+
+
+class M33d(C.Structure):
+    _fields_ = [("M", C.c_double * 9)]
+
+
+class RecoverPoseConfig(C.Structure):
+    """MiniCVNative.cpp:39-46 / OpenCV.fs:16-36."""
+    _fields_ = [("FocalLength", C.c_double), ("PrincipalPoint", V2d), ("Probability", C.c_double),
+                ("InlierThreshold", C.c_double)]
+
+
+class RansacConfig(C.Structure):
+    _fields_ = [("threshold", C.c_double), ("confidence", C.c_double), ("maxIters", C.c_int),
+                ("method", C.c_int), ("seed", C.c_uint64), ("deviceCount", C.c_int), ("flags", C.c_int),
+                ("errorKind", C.c_int), ("reserved", C.c_int)]
+
+
+class ReplayState(C.Structure):
+    _fields_ = [("niters", C.c_int64), ("bestIndex", C.c_int64), ("bestCount", C.c_int32),
+                ("stopped", C.c_int32)]
+
+
+METHOD_LSQ = 0
+METHOD_RANSAC = 8
+FLAG_FIXED_ITERS = 1
+FLAG_NO_REFINE = 2
+FERR_SAMPSON = 0
+FERR_EPIPOLAR = 1
+MODEL_HOMOGRAPHY = 0
+MODEL_FUNDAMENTAL = 1
+
+_P = C.c_void_p
+_I = C.c_int
+_I64 = C.c_int64
+_U64 = C.c_uint64
+_D = C.c_double
+_F = C.c_float
+
+# name -> (restype, argtypes). Pointers are passed as void* (numpy .ctypes.data / device ints).
+SIGNATURES = {
+    # existing reference exports (OpenCV.fs:343-382)
+    "cvRecoverPose": (_I, [_P, _I, _P, _P, _P, _P, _P]),
+    "cvRecoverPoses": (C.c_bool, [_P, _I, _P, _P, _P, _P, _P, _P]),
+    "cvDetectFeatures": (_P, [_P, _I, _I, _I, _I, _P]),
+    "cvFreeFeatures": (None, [_P]),
+    "cvTest": (None, []),
+    "cvFivePoint": (_I, [_P, _P, _P]),
+    "cvSolvePnP": (C.c_bool, [_P, _P, _I, M33d, _P, _I, _P, _P]),
+    "cvSolvePnPRansac": (C.c_bool, [_P, _P, _I, M33d, _P, _I, _I, _F, _D, _P, _P, _P, _P]),
+    "cvRefinePnPLM": (None, [_P, _P, _I, M33d, _P, _P, _P]),
+    "cvRefinePnPVVS": (None, [_P, _P, _I, M33d, _P, _P, _P]),
+    "solveAp3p": (_I, [_P, _P] + [_F] * 19),
+    "cvDetectQRCode": (C.c_bool, [_P, _I, _I, _I, _P, _P]),
+    "cvDetectArucoMarkers": (C.c_bool, [_P, _I, _I, _I, _P, _P]),
+    # new hot-path exports
+    "cvFindHomography": (_I, [_P, _P, _I, _P, _P, _P]),
+    "cvFindFundamentalMat": (_I, [_P, _P, _I, _P, _P, _P]),
+    "cvMatchHamming": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
+    "cvMatchL2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
+    "mcvGetLastError": (C.c_char_p, []),
+    "mcvDeviceCount": (_I, []),
+    "mcvVersion": (C.c_char_p, []),
+    # device-level API
+    "mcvRansacPlanCreate": (_P, [_I, _I, _I64]),
+    "mcvRansacPlanDestroy": (None, [_P]),
+    "mcvPackCorrespondences": (_I, [_P, _P, _I, _P, _P]),
+    "mcvRansacEvaluate": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P, _P]),
+    "mcvRansacFinalize": (_I, [_P, _P, _I, _P, _I64, _P, _P, _P]),
+    "mcvReplayInit": (None, [_P, _I]),
+    "mcvReplayChunk": (_I, [_P, _P, _I64, _I64, _I, _I, _D, _I]),
+    "mcvMatchHammingDevice": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "mcvMatchL2Device": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "mcvProfileEnable": (None, [_I]),
+    "mcvProfileReset": (None, []),
+    "mcvProfileRead": (_I, [C.c_char_p, _P]),
+    # test hooks
+    "mcvHostHypothesis": (_I, [_I, _P, _I, _U64, _I64, _P, _P, _P]),
+    "mcvHostPhilox": (None, [C.c_uint32] * 6 + [_P]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libMiniCVNative.so (raises if it has not been built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"libMiniCVNative.so not found at {LIB_PATH}; run __graft_entry__.build()")
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    e = lib().mcvGetLastError()
+    return e.decode() if e else ""
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def check(ok: bool, what: str) -> None:
+    if not ok:
+        raise NativeError(f"{what}: {last_error()}")

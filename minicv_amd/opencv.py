@@ -1,0 +1,111 @@
+"""Host-side mirror of the reference's managed wrappers (module `OpenCV`,
+/root/reference/src/MiniCV/OpenCV.fs:855-1052): allocate caller-owned outputs, call the native
+export, map the byte mask to bool, return tuples. New wrappers for the hot-path exports follow
+the pattern of `OpenCV.recoverPose` (OpenCV.fs:855-861).
+
+Everything here calls libMiniCVNative.so; errors surface as NativeError with the native message.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import native as N
+
+
+@dataclass
+class RansacParams:
+    """RANSAC configuration (C struct RansacConfig). Defaults follow cv::findHomography
+    (thr 3, maxIters 2000, confidence 0.995)."""
+    threshold: float = 3.0
+    confidence: float = 0.995
+    max_iters: int = 2000
+    method: int = N.METHOD_RANSAC
+    seed: int = 0
+    device_count: int = 1
+    fixed_iters: bool = False
+    refine: bool = True
+    error_kind: int = N.FERR_SAMPSON
+
+    def to_c(self) -> N.RansacConfig:
+        flags = (N.FLAG_FIXED_ITERS if self.fixed_iters else 0) | (0 if self.refine else N.FLAG_NO_REFINE)
+        return N.RansacConfig(self.threshold, self.confidence, int(self.max_iters), int(self.method),
+                              int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(self.device_count), flags,
+                              int(self.error_kind), 0)
+
+
+def _v2d(a) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if a.ndim != 2 or a.shape[1] != 2:
+        raise ValueError("points must be an (N, 2) array")
+    return a
+
+
+def findHomography(src, dst, params: RansacParams | None = None):
+    """-> (inlierCount, H (3x3 float64), mask (bool[N])). Raises NativeError on failure."""
+    params = params or RansacParams()
+    a, b = _v2d(src), _v2d(dst)
+    n = a.shape[0]
+    if b.shape[0] != n:
+        raise ValueError("src/dst length mismatch")
+    H = N.M33d()
+    ms = np.zeros(max(n, 1), dtype=np.uint8)
+    cfg = params.to_c()
+    cnt = N.lib().cvFindHomography(a.ctypes.data, b.ctypes.data, n, N.C.addressof(cfg), N.C.addressof(H),
+                                   ms.ctypes.data)
+    N.check(cnt > 0, "cvFindHomography")
+    return cnt, np.array(H.M[:], dtype=np.float64).reshape(3, 3), ms[:n] != 0
+
+
+def findFundamentalMat(a, b, params: RansacParams | None = None):
+    """8-point RANSAC. -> (inlierCount, F (3x3 float64), mask (bool[N]))."""
+    params = params or RansacParams(threshold=3.0, confidence=0.99)
+    pa, pb = _v2d(a), _v2d(b)
+    n = pa.shape[0]
+    F = N.M33d()
+    ms = np.zeros(max(n, 1), dtype=np.uint8)
+    cfg = params.to_c()
+    cnt = N.lib().cvFindFundamentalMat(pa.ctypes.data, pb.ctypes.data, n, N.C.addressof(cfg), N.C.addressof(F),
+                                       ms.ctypes.data)
+    N.check(cnt > 0, "cvFindFundamentalMat")
+    return cnt, np.array(F.M[:], dtype=np.float64).reshape(3, 3), ms[:n] != 0
+
+
+def matchHamming(q, t):
+    """BFMatcher(NORM_HAMMING).knnMatch(k=2). q, t: uint8 [n][bytes]. -> (idx, dist, idx2, dist2)."""
+    q = np.ascontiguousarray(q, dtype=np.uint8)
+    t = np.ascontiguousarray(t, dtype=np.uint8)
+    if q.ndim != 2 or t.ndim != 2 or q.shape[1] != t.shape[1]:
+        raise ValueError("descriptor arrays must be [n][bytes] with equal widths")
+    nq, nt, nb = q.shape[0], t.shape[0], q.shape[1]
+    out = [np.empty(max(nq, 1), dtype=np.int32) for _ in range(4)]
+    r = N.lib().cvMatchHamming(q.ctypes.data, nq, t.ctypes.data, nt, nb, *[o.ctypes.data for o in out])
+    N.check(r == nq, "cvMatchHamming")
+    return tuple(o[:nq] for o in out)
+
+
+def matchL2(q, t):
+    """BFMatcher(NORM_L2).knnMatch(k=2). q, t: float32 [n][dim]. -> (idx, dist, idx2, dist2)."""
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    t = np.ascontiguousarray(t, dtype=np.float32)
+    if q.ndim != 2 or t.ndim != 2 or q.shape[1] != t.shape[1]:
+        raise ValueError("descriptor arrays must be [n][dim] with equal widths")
+    nq, nt, dim = q.shape[0], t.shape[0], q.shape[1]
+    idx, idx2 = np.empty(max(nq, 1), np.int32), np.empty(max(nq, 1), np.int32)
+    d, d2 = np.empty(max(nq, 1), np.float32), np.empty(max(nq, 1), np.float32)
+    r = N.lib().cvMatchL2(q.ctypes.data, nq, t.ctypes.data, nt, dim, idx.ctypes.data, d.ctypes.data,
+                          idx2.ctypes.data, d2.ctypes.data)
+    N.check(r == nq, "cvMatchL2")
+    return idx[:nq], d[:nq], idx2[:nq], d2[:nq]
+
+
+def recoverPose(cfg: N.RecoverPoseConfig, a, b):
+    """OpenCV.recoverPose (OpenCV.fs:855-861): -> (res, R, t, mask bytes)."""
+    pa, pb = _v2d(a), _v2d(b)
+    m, t = N.M33d(), N.V3d()
+    ms = np.zeros(max(pa.shape[0], 1), dtype=np.uint8)
+    res = N.lib().cvRecoverPose(N.C.addressof(cfg), pa.shape[0], pa.ctypes.data, pb.ctypes.data,
+                                N.C.addressof(m), N.C.addressof(t), ms.ctypes.data)
+    N.check(res > 0, "cvRecoverPose")
+    return res, np.array(m.M[:]).reshape(3, 3), np.array([t.X, t.Y, t.Z]), ms[:pa.shape[0]]

@@ -1,0 +1,112 @@
+"""Seeded synthetic workloads for the BASELINE.json configs (no datasets: no network).
+
+Shapes follow SURVEY.md §8d / BASELINE.md §2:
+  cfg1/cfg3  homography: src ~ U[-1,1]^2 (NDC convention, OpenCV.fs:873-876), dst = pi(H_true src)
+             with H_true = the matrix of the reference's cvTest export (MiniCVNative.cpp:506-511,
+             as cvTest builds it), inliers + N(0, sigma), a fraction of outliers ~ U[-1,1]^2
+             (50 % as in the authors' synthetic test, Program.fs:10-12), thr 5e-3 (OpenCV.fs:34).
+  cfg2       Hamming: train bits ~ Bernoulli(0.5); queries = planted train rows with 0-40 flipped
+             bits, 10 % pure random queries.
+  cfg4       fundamental: two lookAt cameras (src/Test/Camera.fs:171-184 model) viewing points in
+             a 6-unit cube (Program.fs:14), projections + N(0, sigma), 50 % outliers.
+  cfg5       SIFT-like fp32 descriptors: |N(0,1)| -> L2-normalise -> x512 -> clip 255, planted
+             near-duplicates.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# cvTest (MiniCVNative.cpp:506-511): arr1 is transposed into arr, and H = Mat(3,3,arr).
+_ARR1 = np.array([1.02736340896169, 0.0824668492092278, 0.399551267404442, -0.0921929548453944,
+                  1.03823834690651, 0.12968385038247, -0.159700861517284, -0.0688464520524622, 1.0])
+H_TRUE = _ARR1.reshape(3, 3).T.copy()
+
+
+def project(H: np.ndarray, p: np.ndarray) -> np.ndarray:
+    x = p @ H[:, :2].T + H[:, 2]
+    return x[:, :2] / x[:, 2:3]
+
+
+def homography_problem(n: int, seed: int, outlier_frac: float = 0.5, sigma: float = 1e-3, H: np.ndarray = H_TRUE):
+    """-> src (n,2) f64, dst (n,2) f64, is_inlier (n,) bool"""
+    rng = np.random.default_rng(seed)
+    src = rng.uniform(-1, 1, size=(n, 2))
+    dst = project(H, src) + rng.normal(0, sigma, size=(n, 2))
+    out = rng.random(n) < outlier_frac
+    dst[out] = rng.uniform(-1, 1, size=(int(out.sum()), 2))
+    return src, dst, ~out
+
+
+def hamming_problem(nq: int, nt: int, nbytes: int = 32, seed: int = 2, random_frac: float = 0.1,
+                    max_flips: int = 40):
+    """-> q (nq, nbytes) u8, t (nt, nbytes) u8, planted (nq,) int (-1 for random queries)"""
+    rng = np.random.default_rng(seed)
+    t = rng.integers(0, 256, size=(nt, nbytes), dtype=np.uint8)
+    planted = rng.integers(0, nt, size=nq)
+    q = t[planted].copy()
+    bits = np.unpackbits(q, axis=1)
+    flips = rng.integers(0, max_flips + 1, size=nq)
+    for i in range(nq):
+        pos = rng.choice(nbytes * 8, size=flips[i], replace=False)
+        bits[i, pos] ^= 1
+    q = np.packbits(bits, axis=1)
+    rnd = rng.random(nq) < random_frac
+    q[rnd] = rng.integers(0, 256, size=(int(rnd.sum()), nbytes), dtype=np.uint8)
+    planted[rnd] = -1
+    return q, t, planted
+
+
+def sift_like(n: int, dim: int, rng) -> np.ndarray:
+    d = np.abs(rng.normal(size=(n, dim)))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return np.minimum(d * 512.0, 255.0).astype(np.float32)
+
+
+def l2_problem(nq: int, nt: int, dim: int = 128, seed: int = 5, noise: float = 2.0, random_frac: float = 0.1):
+    rng = np.random.default_rng(seed)
+    t = sift_like(nt, dim, rng)
+    planted = rng.integers(0, nt, size=nq)
+    q = np.clip(t[planted] + rng.normal(0, noise, size=(nq, dim)), 0, 255).astype(np.float32)
+    rnd = rng.random(nq) < random_frac
+    q[rnd] = sift_like(int(rnd.sum()), dim, rng)
+    planted[rnd] = -1
+    return q, t, planted
+
+
+def look_at(eye, target, up):
+    """World->camera rotation/translation of a lookAt camera (camera looks down -z)."""
+    eye, target, up = map(lambda v: np.asarray(v, dtype=np.float64), (eye, target, up))
+    f = target - eye
+    f /= np.linalg.norm(f)
+    r = np.cross(f, up)
+    r /= np.linalg.norm(r)
+    u = np.cross(r, f)
+    R = np.stack([r, u, -f])
+    return R, -R @ eye
+
+
+def fundamental_problem(n: int, seed: int = 4, outlier_frac: float = 0.5, sigma: float = 1e-3):
+    """Two pinhole cameras (identity intrinsics, NDC image plane) viewing points in a 6-unit cube.
+    -> a (n,2), b (n,2), is_inlier, F_true (3x3, b^T F a = 0)"""
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(-3, 3, size=(n, 3))
+    R1, t1 = look_at([4.0, 5.0, 6.0], [0, 0, 0], [0, 0, 1])
+    R2, t2 = look_at([6.0, -3.0, 5.0], [0, 0, 0], [0, 0, 1])
+
+    def proj(R, t):
+        c = X @ R.T + t
+        return -c[:, :2] / c[:, 2:3]   # camera looks down -z; image coords (x, y) / depth
+
+    a = proj(R1, t1) + rng.normal(0, sigma, size=(n, 2))
+    b = proj(R2, t2) + rng.normal(0, sigma, size=(n, 2))
+    out = rng.random(n) < outlier_frac
+    lo, hi = b.min(axis=0), b.max(axis=0)
+    b[out] = rng.uniform(lo, hi, size=(int(out.sum()), 2))
+    # F from relative pose: x2 ~ K(R x1 + t); with the -z convention the image point is (-X/Z, -Y/Z)
+    R = R2 @ R1.T
+    t = t2 - R @ t1
+    tx = np.array([[0, -t[2], t[1]], [t[2], 0, -t[0]], [-t[1], t[0], 0]])
+    E = tx @ R
+    S = np.diag([1.0, 1.0, -1.0])   # image (x, y, 1) = S * normalised camera ray up to scale
+    F = S @ E @ S
+    return a, b, ~out, F / np.linalg.norm(F)

@@ -1,0 +1,560 @@
+/*
+ * oracle.c — CPU restatement of MiniCV's matching + RANSAC hot path. TEST INFRASTRUCTURE ONLY:
+ * imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the
+ * product (libMiniCVNative.so has no CPU fallback).
+ *
+ * PARITY STATUS: "parity unpinned" with respect to OpenCV. The reference delegates every
+ * computation of this path to third-party OpenCV (calib3d / features2d; call sites
+ * /root/reference/src/MiniCVNative/MiniCVNative.cpp:125,177,204), which is not installed in this
+ * container, is version-unpinned (vcpkg HEAD, /root/reference/buildnative.sh:15,48) and cannot be
+ * built offline; the reference ships no test that pins a number (/root/reference/src/Test/
+ * Program.fs:57-97 only prints detector counts). This file restates the OpenCV 4.x algorithms
+ * [ext, from the published source, unverifiable here] and is pinned instead by: Random123's
+ * Philox4x32-10 known-answer vectors, analytic known-answer problems (exact homographies /
+ * fundamental matrices, including the cvTest matrix MiniCVNative.cpp:506), cross-checks against
+ * independent numpy/scipy algebra, and committed golden fixtures (tests/golden/).
+ *
+ * It is written independently of minicv_amd/csrc (no shared header) but to the same definition,
+ * operation by operation, so that per-hypothesis models and inlier masks agree bit for bit.
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off: no FMA contraction, IEEE double/float).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include <float.h>
+#include <limits.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------------------------
+ * Philox4x32-10 (Salmon, Moraes, Dror, Shaw — "Parallel random numbers: as easy as 1, 2, 3").
+ * ---------------------------------------------------------------------------------------- */
+void orc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Per-hypothesis word stream: word s = philox({s/4, hyp_lo, hyp_hi, "MCV1"}, {seed_lo, seed_hi})[s%4] */
+typedef struct { uint64_t seed, hyp; uint64_t pos; uint32_t buf[4]; } Stream;
+
+static uint32_t stream_next(Stream* st) {
+    if ((st->pos & 3) == 0) {
+        uint32_t c[4] = {(uint32_t)(st->pos >> 2), (uint32_t)st->hyp, (uint32_t)(st->hyp >> 32), 0x4D435631u};
+        uint32_t k[2] = {(uint32_t)st->seed, (uint32_t)(st->seed >> 32)};
+        orc_philox(c, k, st->buf);
+    }
+    return st->buf[st->pos++ & 3];
+}
+
+static int stream_uniform(Stream* st, int n) { return (int)(((uint64_t)stream_next(st) * (uint32_t)n) >> 32); }
+
+#define ORC_MAX_ATTEMPTS 10000
+#define ORC_MAX_REDRAW 1000
+#define ORC_NO_MODEL (-1)
+#define ORC_NO_SAMPLE (-2)
+
+/* getSubset's inner loop: m distinct indices, duplicates redrawn (bounded). */
+static int draw_distinct(Stream* st, int N, int m, int* idx) {
+    for (int i = 0; i < m; ++i) {
+        int v = stream_uniform(st, N), tries = 0;
+        for (;;) {
+            int dup = 0;
+            for (int j = 0; j < i; ++j) dup |= (idx[j] == v);
+            if (!dup) break;
+            if (++tries >= ORC_MAX_REDRAW) return 0;
+            v = stream_uniform(st, N);
+        }
+        idx[i] = v;
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Homography. OpenCV 4.x calib3d/src/fundam.cpp HomographyEstimatorCallback [ext].
+ * ---------------------------------------------------------------------------------------- */
+static double det3(double a00, double a01, double a02, double a10, double a11, double a12, double a20, double a21,
+                   double a22) {
+    return a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
+}
+
+/* haveCollinearPoints(m, count=4): last point vs lines through earlier pairs. */
+static int collinear_last(const float* x, const float* y, int count) {
+    int i = count - 1;
+    for (int j = 0; j < i; ++j) {
+        double dx1 = (double)(float)(x[j] - x[i]), dy1 = (double)(float)(y[j] - y[i]);
+        for (int k = 0; k < j; ++k) {
+            double dx2 = (double)(float)(x[k] - x[i]), dy2 = (double)(float)(y[k] - y[i]);
+            if (fabs(dx2 * dy1 - dy2 * dx1) <= (double)FLT_EPSILON * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
+                return 1;
+        }
+    }
+    return 0;
+}
+
+static int h_subset_ok(const float* sx, const float* sy, const float* dx, const float* dy) {
+    static const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {0, 1, 3}};
+    if (collinear_last(sx, sy, 4) || collinear_last(dx, dy, 4)) return 0;
+    int negative = 0;
+    for (int i = 0; i < 4; ++i) {
+        int a = tt[i][0], b = tt[i][1], c = tt[i][2];
+        double dA = det3(sx[a], sy[a], 1., sx[b], sy[b], 1., sx[c], sy[c], 1.);
+        double dB = det3(dx[a], dy[a], 1., dx[b], dy[b], 1., dx[c], dy[c], 1.);
+        negative += dA * dB < 0;
+    }
+    return negative == 0 || negative == 4;
+}
+
+static void mul33(const double* A, const double* B, double* C) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+/* Minimal 4-point solve: runKernel's normalisation, then the 8x8 system (h22 = 1) by Gaussian
+ * elimination with partial pivoting (first maximum), back substitution, de-normalisation,
+ * H *= 1/H22. Returns 0 when degenerate. */
+static int h_solve4(const float* sx, const float* sy, const float* dx, const float* dy, double* H) {
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0, smx = 0, smy = 0, sMx = 0, sMy = 0;
+    for (int i = 0; i < 4; ++i) { cmx += dx[i]; cmy += dy[i]; cMx += sx[i]; cMy += sy[i]; }
+    cmx /= 4; cmy /= 4; cMx /= 4; cMy /= 4;
+    for (int i = 0; i < 4; ++i) {
+        smx += fabs(dx[i] - cmx); smy += fabs(dy[i] - cmy);
+        sMx += fabs(sx[i] - cMx); sMy += fabs(sy[i] - cMy);
+    }
+    if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
+        return 0;
+    smx = 4 / smx; smy = 4 / smy; sMx = 4 / sMx; sMy = 4 / sMy;
+    double a[8][9];
+    for (int i = 0; i < 4; ++i) {
+        double x = (dx[i] - cmx) * smx, y = (dy[i] - cmy) * smy;
+        double X = (sx[i] - cMx) * sMx, Y = (sy[i] - cMy) * sMy;
+        double r0[9] = {X, Y, 1, 0, 0, 0, -(x * X), -(x * Y), x};
+        double r1[9] = {0, 0, 0, X, Y, 1, -(y * X), -(y * Y), y};
+        memcpy(a[2 * i], r0, sizeof(r0));
+        memcpy(a[2 * i + 1], r1, sizeof(r1));
+    }
+    for (int c = 0; c < 8; ++c) {
+        int p = c;
+        double best = fabs(a[c][c]);
+        for (int r = c + 1; r < 8; ++r)
+            if (fabs(a[r][c]) > best) { best = fabs(a[r][c]); p = r; }
+        if (!(best > 0)) return 0;
+        if (p != c)
+            for (int k = c; k < 9; ++k) { double t = a[c][k]; a[c][k] = a[p][k]; a[p][k] = t; }
+        for (int r = c + 1; r < 8; ++r) {
+            double f = a[r][c] / a[c][c];
+            for (int k = c + 1; k < 9; ++k) a[r][k] = a[r][k] - f * a[c][k];
+        }
+    }
+    double h[8];
+    for (int i = 7; i >= 0; --i) {
+        double s = a[i][8];
+        for (int k = i + 1; k < 8; ++k) s = s - a[i][k] * h[k];
+        h[i] = s / a[i][i];
+    }
+    double Hn[9] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], 1.0};
+    double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double T[9];
+    mul33(invHnorm, Hn, T);
+    mul33(T, Hnorm2, H);
+    double s = 1. / H[8];
+    for (int i = 0; i < 9; ++i) {
+        H[i] = H[i] * s;
+        if (!isfinite(H[i])) return 0;
+    }
+    return 1;
+}
+
+/* One hypothesis: 1 = model, ORC_NO_MODEL, ORC_NO_SAMPLE. */
+int orc_h_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* H, float* hf, int* idx_out) {
+    Stream st;
+    st.seed = seed; st.hyp = (uint64_t)hyp; st.pos = 0;
+    int idx[4];
+    float sx[4], sy[4], dx[4], dy[4];
+    for (int attempt = 0; attempt < ORC_MAX_ATTEMPTS; ++attempt) {
+        if (!draw_distinct(&st, N, 4, idx)) continue;
+        for (int i = 0; i < 4; ++i) {
+            const float* p = pts4 + 4 * (size_t)idx[i];
+            sx[i] = p[0]; sy[i] = p[1]; dx[i] = p[2]; dy[i] = p[3];
+        }
+        if (!h_subset_ok(sx, sy, dx, dy)) continue;
+        if (idx_out) memcpy(idx_out, idx, sizeof(idx));
+        if (!h_solve4(sx, sy, dx, dy, H)) return ORC_NO_MODEL;
+        for (int i = 0; i < 8; ++i) {
+            hf[i] = (float)H[i];
+            if (!isfinite(hf[i])) return ORC_NO_MODEL;
+        }
+        return 1;
+    }
+    return ORC_NO_SAMPLE;
+}
+
+/* computeError + findInliers for one fp32 model. mask may be NULL. */
+int orc_h_count(const float* pts4, int N, const float* h, float thr2, uint8_t* mask) {
+    int n = 0;
+    for (int i = 0; i < N; ++i) {
+        const float* p = pts4 + 4 * (size_t)i;
+        float x = p[0], y = p[1];
+        float ww = 1.f / (h[6] * x + h[7] * y + 1.f);
+        float ex = (h[0] * x + h[1] * y + h[2]) * ww - p[2];
+        float ey = (h[3] * x + h[4] * y + h[5]) * ww - p[3];
+        int in = ex * ex + ey * ey <= thr2;
+        if (mask) mask[i] = (uint8_t)in;
+        n += in;
+    }
+    return n;
+}
+
+/* Status-or-count per hypothesis over [hypBegin, hypBegin+hypCount), threads over hypotheses. */
+void orc_h_counts(const float* pts4, int N, uint64_t seed, int64_t hypBegin, int64_t hypCount, float thr2,
+                  int* counts, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+    for (int64_t i = 0; i < hypCount; ++i) {
+        double H[9];
+        float hf[8];
+        int st = orc_h_hypothesis(pts4, N, seed, hypBegin + i, H, hf, NULL);
+        counts[i] = st == 1 ? orc_h_count(pts4, N, hf, thr2, NULL) : st;
+    }
+}
+
+/* RANSACUpdateNumIters [ext: OpenCV ptsetreg.cpp]. */
+int orc_update_num_iters(double p, double ep, int modelPoints, int maxIters) {
+    p = p > 0 ? p : 0.; p = p < 1 ? p : 1.;
+    ep = ep > 0 ? ep : 0.; ep = ep < 1 ? ep : 1.;
+    double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
+    double denom = 1. - pow(1. - ep, modelPoints);
+    if (denom < DBL_MIN) return 0;
+    num = log(num);
+    denom = log(denom);
+    return (denom >= 0 || -num >= (double)maxIters * (-denom)) ? maxIters : (int)lrint(num / denom);
+}
+
+/* Jacobi eigen-decomposition of symmetric A (n <= 9): eigenvalues descending in w, eigenvectors
+ * as rows of V. Independent implementation (threshold-free cyclic sweeps). */
+static void jacobi(double* A, int n, double* w, double* V) {
+    for (int i = 0; i < n * n; ++i) V[i] = (i / n == i % n);
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0, dg = 0;
+        for (int i = 0; i < n; ++i) {
+            dg += A[i * n + i] * A[i * n + i];
+            for (int j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
+        }
+        if (off <= DBL_MIN || off <= dg * 1e-32) break;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                double apq = A[p * n + q];
+                if (apq == 0) continue;
+                double theta = (A[q * n + q] - A[p * n + p]) / (2 * apq);
+                double t = (theta >= 0 ? 1. : -1.) / (fabs(theta) + sqrt(theta * theta + 1));
+                double c = 1 / sqrt(t * t + 1), s = t * c;
+                for (int k = 0; k < n; ++k) {
+                    double x = A[k * n + p], y = A[k * n + q];
+                    A[k * n + p] = c * x - s * y; A[k * n + q] = s * x + c * y;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double x = A[p * n + k], y = A[q * n + k];
+                    A[p * n + k] = c * x - s * y; A[q * n + k] = s * x + c * y;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double x = V[p * n + k], y = V[q * n + k];
+                    V[p * n + k] = c * x - s * y; V[q * n + k] = s * x + c * y;
+                }
+            }
+    }
+    for (int i = 0; i < n; ++i) w[i] = A[i * n + i];
+    for (int i = 0; i < n - 1; ++i) {
+        int m = i;
+        for (int j = i + 1; j < n; ++j)
+            if (w[j] > w[m]) m = j;
+        if (m != i) {
+            double t = w[i]; w[i] = w[m]; w[m] = t;
+            for (int k = 0; k < n; ++k) { t = V[i * n + k]; V[i * n + k] = V[m * n + k]; V[m * n + k] = t; }
+        }
+    }
+}
+
+static void eig_pinv_apply(const double* A, int n, const double* b, double* x, double* Ainv) {
+    double M[81], w[9], V[81], wmax = 0;
+    memcpy(M, A, sizeof(double) * n * n);
+    jacobi(M, n, w, V);
+    for (int i = 0; i < n; ++i) wmax = fabs(w[i]) > wmax ? fabs(w[i]) : wmax;
+    double thr = wmax * n * DBL_EPSILON;
+    if (x) for (int j = 0; j < n; ++j) x[j] = 0;
+    if (Ainv) for (int j = 0; j < n * n; ++j) Ainv[j] = 0;
+    for (int e = 0; e < n; ++e) {
+        if (fabs(w[e]) <= thr) continue;
+        if (x) {
+            double d = 0;
+            for (int k = 0; k < n; ++k) d += V[e * n + k] * b[k];
+            d /= w[e];
+            for (int j = 0; j < n; ++j) x[j] += d * V[e * n + j];
+        }
+        if (Ainv)
+            for (int i = 0; i < n; ++i)
+                for (int j = 0; j < n; ++j) Ainv[i * n + j] += V[e * n + i] * (1. / w[e]) * V[e * n + j];
+    }
+}
+
+/* HomographyEstimatorCallback::runKernel over the listed correspondences (sequential sums). */
+static int h_run_kernel(const float* pts4, const int* list, int count, double* H) {
+    double cmx = 0, cmy = 0, cMx = 0, cMy = 0, smx = 0, smy = 0, sMx = 0, sMy = 0;
+    for (int t = 0; t < count; ++t) {
+        const float* p = pts4 + 4 * (size_t)list[t];
+        cmx += p[2]; cmy += p[3]; cMx += p[0]; cMy += p[1];
+    }
+    cmx /= count; cmy /= count; cMx /= count; cMy /= count;
+    for (int t = 0; t < count; ++t) {
+        const float* p = pts4 + 4 * (size_t)list[t];
+        smx += fabs(p[2] - cmx); smy += fabs(p[3] - cmy); sMx += fabs(p[0] - cMx); sMy += fabs(p[1] - cMy);
+    }
+    if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
+        return 0;
+    smx = count / smx; smy = count / smy; sMx = count / sMx; sMy = count / sMy;
+    double L[81] = {0};
+    for (int t = 0; t < count; ++t) {
+        const float* p = pts4 + 4 * (size_t)list[t];
+        double x = (p[2] - cmx) * smx, y = (p[3] - cmy) * smy, X = (p[0] - cMx) * sMx, Y = (p[1] - cMy) * sMy;
+        double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
+        double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+        for (int j = 0; j < 9; ++j)
+            for (int k = j; k < 9; ++k) L[j * 9 + k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+    }
+    for (int j = 0; j < 9; ++j)
+        for (int k = 0; k < j; ++k) L[j * 9 + k] = L[k * 9 + j];
+    double w[9], V[81];
+    jacobi(L, 9, w, V);
+    double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double T[9], R[9];
+    mul33(invHnorm, V + 72, T);
+    mul33(T, Hnorm2, R);
+    for (int k = 0; k < 9; ++k) H[k] = R[k] * (1. / R[8]);
+    return 1;
+}
+
+/* HomographyRefineCallback::compute: returns |r|^2; A (8x8) and v (8) when non-NULL. */
+static double h_lm_compute(const float* pts4, const int* list, int count, const double* h, double* A, double* v) {
+    double S = 0;
+    if (A) { memset(A, 0, 64 * sizeof(double)); memset(v, 0, 8 * sizeof(double)); }
+    for (int t = 0; t < count; ++t) {
+        const float* p = pts4 + 4 * (size_t)list[t];
+        double Mx = p[0], My = p[1];
+        double ww = h[6] * Mx + h[7] * My + 1.;
+        ww = fabs(ww) > DBL_EPSILON ? 1. / ww : 0;
+        double xi = (h[0] * Mx + h[1] * My + h[2]) * ww, yi = (h[3] * Mx + h[4] * My + h[5]) * ww;
+        double rx = xi - p[2], ry = yi - p[3];
+        S += rx * rx + ry * ry;
+        if (A) {
+            double Jx[8] = {Mx * ww, My * ww, ww, 0, 0, 0, -Mx * ww * xi, -My * ww * xi};
+            double Jy[8] = {0, 0, 0, Mx * ww, My * ww, ww, -Mx * ww * yi, -My * ww * yi};
+            for (int j = 0; j < 8; ++j) {
+                for (int k = 0; k < 8; ++k) A[j * 8 + k] += Jx[j] * Jx[k] + Jy[j] * Jy[k];
+                v[j] += Jx[j] * rx + Jy[j] * ry;
+            }
+        }
+    }
+    return S;
+}
+
+/* LMSolverImpl::run [ext: OpenCV levmarq.cpp, classic version], maxIters, eps = FLT_EPSILON. */
+static void h_lm(const float* pts4, const int* list, int count, double* H, int maxIters) {
+    double x[8], xd[8], d[8], v[8], A[64], Ap[64], D[8];
+    memcpy(x, H, sizeof(x));
+    double S = h_lm_compute(pts4, list, count, x, A, v);
+    for (int i = 0; i < 8; ++i) D[i] = A[i * 9];
+    double lambda = 1, lc = 0.75;
+    int iter = 0;
+    for (;;) {
+        memcpy(Ap, A, sizeof(A));
+        for (int i = 0; i < 8; ++i) Ap[i * 9] += lambda * D[i];
+        eig_pinv_apply(Ap, 8, v, d, NULL);
+        for (int i = 0; i < 8; ++i) xd[i] = x[i] - d[i];
+        double Sd = h_lm_compute(pts4, list, count, xd, NULL, NULL);
+        double dS = 0;
+        for (int i = 0; i < 8; ++i) {
+            double ad = 0;
+            for (int k = 0; k < 8; ++k) ad += A[i * 8 + k] * d[k];
+            dS += d[i] * (-ad + 2 * v[i]);
+        }
+        double R = (S - Sd) / (fabs(dS) > DBL_EPSILON ? dS : 1);
+        if (R > 0.75) {
+            lambda *= 0.5;
+            if (lambda < lc) lambda = 0;
+        } else if (R < 0.25) {
+            double t = 0;
+            for (int i = 0; i < 8; ++i) t += d[i] * v[i];
+            double nu = (Sd - S) / (fabs(t) > DBL_EPSILON ? t : 1) + 2;
+            nu = nu < 2 ? 2 : (nu > 10 ? 10 : nu);
+            if (lambda == 0) {
+                eig_pinv_apply(A, 8, NULL, NULL, Ap);
+                double mx = DBL_EPSILON;
+                for (int i = 0; i < 8; ++i) mx = fabs(Ap[i * 9]) > mx ? fabs(Ap[i * 9]) : mx;
+                lambda = lc = 1. / mx;
+                nu *= 0.5;
+            }
+            lambda *= nu;
+        }
+        if (Sd < S) {
+            memcpy(x, xd, sizeof(x));
+            S = h_lm_compute(pts4, list, count, x, A, v);
+        }
+        ++iter;
+        double dn = 0;
+        for (int i = 0; i < 8; ++i) dn = fabs(d[i]) > dn ? fabs(d[i]) : dn;
+        if (!(iter < maxIters && dn >= FLT_EPSILON && S >= (double)FLT_EPSILON * FLT_EPSILON)) break;
+    }
+    memcpy(H, x, sizeof(x));
+}
+
+/* Sequential RANSAC replay over precomputed per-hypothesis statuses/counts (the loop of
+ * RANSACPointSetRegistrator::run). Returns best hypothesis index or -1. */
+int64_t orc_ransac_replay(const int* counts, int64_t ncounts, int N, int m, double conf, int maxIters, int fixed,
+                          int* bestCount) {
+    int64_t niters = maxIters > 1 ? maxIters : 1, best = -1;
+    int bc = 0;
+    for (int64_t it = 0; it < niters && it < ncounts; ++it) {
+        int c = counts[it];
+        if (c == ORC_NO_SAMPLE) break;
+        if (c < 0) continue;
+        if (c > (bc > m - 1 ? bc : m - 1)) {
+            bc = c; best = it;
+            if (!fixed) niters = orc_update_num_iters(conf, (double)(N - c) / N, m, (int)niters);
+        }
+    }
+    if (bestCount) *bestCount = bc;
+    return best;
+}
+
+#define ORC_FLAG_FIXED_ITERS 1
+#define ORC_FLAG_NO_REFINE 2
+
+/* cv::findHomography(src, dst, method, thr, mask, maxIters, conf) with the counter-based sampler.
+ * pts as fp64 AoS (converted to float as convertTo(CV_32F)). Returns inlier count, 0 on failure. */
+int orc_find_homography(const double* src, const double* dst, int N, double thr, double conf, int maxIters,
+                        int method, uint64_t seed, int flags, double* H, uint8_t* mask, int64_t* bestHypOut,
+                        int nthreads) {
+    if (mask) memset(mask, 0, (size_t)(N > 0 ? N : 0));
+    if (bestHypOut) *bestHypOut = -1;
+    if (N < 4) return 0;
+    if (thr <= 0) thr = 3;
+    float* pts = (float*)malloc(sizeof(float) * 4 * (size_t)N);
+    int* list = (int*)malloc(sizeof(int) * (size_t)N);
+    uint8_t* m8 = (uint8_t*)malloc((size_t)N);
+    for (int i = 0; i < N; ++i) {
+        pts[4 * i] = (float)src[2 * i]; pts[4 * i + 1] = (float)src[2 * i + 1];
+        pts[4 * i + 2] = (float)dst[2 * i]; pts[4 * i + 3] = (float)dst[2 * i + 1];
+    }
+    int result = 0, count = 0;
+    if (method == 0 || N == 4) {
+        for (int i = 0; i < N; ++i) { list[i] = i; m8[i] = 1; }
+        result = h_run_kernel(pts, list, N, H);
+        if (result && N > 4) h_lm(pts, list, N, H, 10);
+        count = N;
+    } else {
+        const float thr2 = (float)(thr * thr);
+        int64_t niters = maxIters > 1 ? maxIters : 1, best = -1;
+        int bc = 0;
+        int* cnts = (int*)malloc(sizeof(int) * (size_t)niters);
+        /* counts for every hypothesis up front (parallel), replay sequentially */
+        orc_h_counts(pts, N, seed, 0, niters, thr2, cnts, nthreads);
+        best = orc_ransac_replay(cnts, niters, N, 4, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0, &bc);
+        free(cnts);
+        if (best >= 0) {
+            double Hb[9];
+            float hf[8];
+            orc_h_hypothesis(pts, N, seed, best, Hb, hf, NULL);
+            count = orc_h_count(pts, N, hf, thr2, m8);
+            memcpy(H, Hb, sizeof(Hb));
+            result = 1;
+            if (!(flags & ORC_FLAG_NO_REFINE)) {
+                int k = 0;
+                for (int i = 0; i < N; ++i)
+                    if (m8[i]) list[k++] = i;
+                if (k > 0) {
+                    double Hr[9];
+                    if (h_run_kernel(pts, list, k, Hr)) memcpy(H, Hr, sizeof(Hr));
+                    h_lm(pts, list, k, H, 10);
+                }
+            }
+            if (bestHypOut) *bestHypOut = best;
+        }
+    }
+    if (result && mask) memcpy(mask, m8, (size_t)N);
+    free(pts); free(list); free(m8);
+    return result ? count : 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Brute-force matchers (BFMatcher NORM_HAMMING / NORM_L2, knn k = 2) [ext: OpenCV features2d].
+ * Ties: the lower train index wins (strict comparison while scanning trains in order).
+ * ---------------------------------------------------------------------------------------- */
+void orc_match_hamming(const uint8_t* q, int nq, const uint8_t* t, int nt, int bytes, int* idx, int* dist, int* idx2,
+                       int* dist2, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int i = 0; i < nq; ++i) {
+        int b1 = INT_MAX, b2 = INT_MAX, i1 = -1, i2 = -1;
+        const uint8_t* qi = q + (size_t)i * bytes;
+        for (int j = 0; j < nt; ++j) {
+            const uint8_t* tj = t + (size_t)j * bytes;
+            int d = 0;
+            for (int b = 0; b < bytes; ++b) d += __builtin_popcount((unsigned)(qi[b] ^ tj[b]));
+            if (d < b1) { b2 = b1; i2 = i1; b1 = d; i1 = j; }
+            else if (d < b2) { b2 = d; i2 = j; }
+        }
+        idx[i] = i1; dist[i] = b1;
+        if (idx2) idx2[i] = i2;
+        if (dist2) dist2[i] = b2;
+    }
+}
+
+/* Exact (fp64-accumulated) squared distances; returns sqrt like NORM_L2. */
+void orc_match_l2(const float* q, int nq, const float* t, int nt, int dim, int* idx, double* dist, int* idx2,
+                  double* dist2, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int i = 0; i < nq; ++i) {
+        double b1 = INFINITY, b2 = INFINITY;
+        int i1 = -1, i2 = -1;
+        const float* qi = q + (size_t)i * dim;
+        for (int j = 0; j < nt; ++j) {
+            const float* tj = t + (size_t)j * dim;
+            double d = 0;
+            for (int k = 0; k < dim; ++k) { double e = (double)qi[k] - (double)tj[k]; d += e * e; }
+            if (d < b1) { b2 = b1; i2 = i1; b1 = d; i1 = j; }
+            else if (d < b2) { b2 = d; i2 = j; }
+        }
+        idx[i] = i1; dist[i] = sqrt(b1);
+        if (idx2) idx2[i] = i2;
+        if (dist2) dist2[i] = sqrt(b2);
+    }
+}
+
+int orc_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

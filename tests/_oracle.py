@@ -1,0 +1,118 @@
+"""ctypes loader of oracle/liboracle.so — the CPU restatement used as the parity checker.
+Test infrastructure only (also imported by bench.py's cpu_baseline leg and smoke())."""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_SO = ORACLE_DIR / "liboracle.so"
+
+_P, _I, _I64, _U64, _D, _F = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double, C.c_float
+_SIGS = {
+    "orc_philox": (None, [_P, _P, _P]),
+    "orc_h_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P, _P]),
+    "orc_h_count": (_I, [_P, _I, _P, _F, _P]),
+    "orc_h_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _P, _I]),
+    "orc_update_num_iters": (_I, [_D, _D, _I, _I]),
+    "orc_ransac_replay": (_I64, [_P, _I64, _I, _I, _D, _I, _I, _P]),
+    "orc_find_homography": (_I, [_P, _P, _I, _D, _D, _I, _I, _U64, _I, _P, _P, _P, _I]),
+    "orc_match_hamming": (None, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I]),
+    "orc_match_l2": (None, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I]),
+    "orc_max_threads": (_I, []),
+}
+_OPTIONAL = {"orc_f_hypothesis", "orc_f_count", "orc_f_counts", "orc_find_fundamental"}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not ORACLE_SO.exists() or ORACLE_SO.stat().st_mtime < (ORACLE_DIR / "oracle.c").stat().st_mtime:
+            subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
+        L = C.CDLL(str(ORACLE_SO))
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def pack4(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
+    return np.ascontiguousarray(np.concatenate([src, dst], axis=1).astype(np.float32))
+
+
+def philox(ctr, key):
+    c = np.asarray(ctr, dtype=np.uint32)
+    k = np.asarray(key, dtype=np.uint32)
+    o = np.zeros(4, dtype=np.uint32)
+    load().orc_philox(ptr(c), ptr(k), ptr(o))
+    return [int(v) for v in o]
+
+
+def h_hypothesis(pts4: np.ndarray, seed: int, hyp: int):
+    H = np.zeros(9)
+    hf = np.zeros(8, dtype=np.float32)
+    idx = np.full(4, -1, dtype=np.int32)
+    st = load().orc_h_hypothesis(ptr(pts4), pts4.shape[0], seed, hyp, ptr(H), ptr(hf), ptr(idx))
+    return st, H, hf, idx
+
+
+def h_count(pts4: np.ndarray, hf: np.ndarray, thr2: float, want_mask: bool = False):
+    hf = np.ascontiguousarray(hf, dtype=np.float32)
+    m = np.zeros(pts4.shape[0], dtype=np.uint8) if want_mask else None
+    n = load().orc_h_count(ptr(pts4), pts4.shape[0], ptr(hf), thr2, ptr(m) if want_mask else None)
+    return (n, m) if want_mask else n
+
+
+def h_counts(pts4: np.ndarray, seed: int, begin: int, count: int, thr2: float, nthreads: int = 0) -> np.ndarray:
+    out = np.zeros(count, dtype=np.int32)
+    load().orc_h_counts(ptr(pts4), pts4.shape[0], seed, begin, count, thr2, ptr(out), nthreads)
+    return out
+
+
+def find_homography(src, dst, thr=3.0, conf=0.995, max_iters=2000, method=8, seed=0, flags=0, nthreads=0):
+    src = np.ascontiguousarray(src, dtype=np.float64)
+    dst = np.ascontiguousarray(dst, dtype=np.float64)
+    n = src.shape[0]
+    H = np.zeros(9)
+    mask = np.zeros(max(n, 1), dtype=np.uint8)
+    best = np.zeros(1, dtype=np.int64)
+    cnt = load().orc_find_homography(ptr(src), ptr(dst), n, thr, conf, max_iters, method, seed, flags, ptr(H),
+                                     ptr(mask), ptr(best), nthreads)
+    return cnt, H.reshape(3, 3), mask[:n], int(best[0])
+
+
+def replay(counts: np.ndarray, n: int, m: int, conf: float, max_iters: int, fixed: bool):
+    counts = np.ascontiguousarray(counts, dtype=np.int32)
+    bc = np.zeros(1, dtype=np.int32)
+    best = load().orc_ransac_replay(ptr(counts), counts.shape[0], n, m, conf, max_iters, int(fixed), ptr(bc))
+    return int(best), int(bc[0])
+
+
+def match_hamming(q, t, nthreads=0):
+    q = np.ascontiguousarray(q, dtype=np.uint8)
+    t = np.ascontiguousarray(t, dtype=np.uint8)
+    nq = q.shape[0]
+    out = [np.zeros(nq, dtype=np.int32) for _ in range(4)]
+    load().orc_match_hamming(ptr(q), nq, ptr(t), t.shape[0], q.shape[1], *[ptr(o) for o in out], nthreads)
+    return tuple(out)
+
+
+def match_l2(q, t, nthreads=0):
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    t = np.ascontiguousarray(t, dtype=np.float32)
+    nq = q.shape[0]
+    i1, i2 = np.zeros(nq, np.int32), np.zeros(nq, np.int32)
+    d1, d2 = np.zeros(nq), np.zeros(nq)
+    load().orc_match_l2(ptr(q), nq, ptr(t), t.shape[0], q.shape[1], ptr(i1), ptr(d1), ptr(i2), ptr(d2), nthreads)
+    return i1, d1, i2, d2

@@ -1,0 +1,103 @@
+"""Multi-rank path on CPU (gloo, world_size 2 and 3): hypothesis sharding + the one all-reduce that
+combines per-rank best keys (minicv_amd/dist.py) must reproduce the single-process sequential
+RANSAC answer, including the sampler-failure `break`. The per-rank "device" evaluation is played
+by precomputed per-hypothesis counts (from the oracle), reduced like mcv_best_* does."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from minicv_amd import dist as MD
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def local_key(counts, begin, count, m=4):
+    """What mcv_best_partial/final compute for one rank's range."""
+    seg = counts[begin:begin + count]
+    fail = np.nonzero(seg == -2)[0]
+    lim = int(fail[0]) if len(fail) else count
+    first_fail = begin + int(fail[0]) if len(fail) else MD.NO_FAIL
+    valid = seg[:lim] >= m
+    if not valid.any():
+        return 0, first_fail
+    c = int(seg[:lim].max())
+    i = int(np.nonzero(seg[:lim] == c)[0][0])
+    return (c << 32) | (0xFFFFFFFF - (begin + i)), first_fail
+
+
+def _worker(rank, world, port, counts, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def evaluate(begin, count):
+        return local_key(counts, begin, count)
+
+    def allreduce_max(vals):
+        t = torch.tensor(vals, dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [int(v) for v in t]
+
+    res = MD.global_best(evaluate, len(counts), rank, world, allreduce_max)
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def run_ranks(world, counts):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, counts, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    return out
+
+
+def test_shard_covers_range():
+    for total in (1, 7, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            spans = [MD.shard(total, r, world) for r in range(world)]
+            assert spans[0][0] == 0
+            assert sum(c for _, c in spans) == total
+            for (b0, c0), (b1, _) in zip(spans, spans[1:]):
+                assert b0 + c0 == b1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_best_matches_sequential(oracle, world):
+    from minicv_amd import synthetic as S
+    src, dst, _ = S.homography_problem(500, 31)
+    pts4 = oracle.pack4(src, dst)
+    counts = oracle.h_counts(pts4, 31, 0, 3000, float(np.float32(5e-3 ** 2)))
+    best, bc = oracle.replay(counts, 500, 4, 0.995, len(counts), fixed=True)
+    out = run_ranks(world, counts)
+    for r in range(world):
+        assert out[r][0] == bc and out[r][1] == best
+
+
+def test_distributed_sampler_failure_break(oracle):
+    rng = np.random.default_rng(5)
+    counts = rng.integers(0, 100, size=1000).astype(np.int32)
+    counts[700] = 500          # global max lies after the failure ...
+    counts[400] = -2           # ... which stops the sequential loop at 400
+    counts[100] = 99
+    counts[:100] = np.minimum(counts[:100], 50)
+    best, bc = oracle.replay(counts, 1000, 4, 0.99, len(counts), fixed=True)
+    assert best < 400
+    out = run_ranks(2, counts)
+    for r in range(2):
+        assert out[r][0] == bc and out[r][1] == best and out[r][2] == 400

@@ -1,0 +1,177 @@
+"""GPU parity of the homography RANSAC path against the oracle (needs an MI355X).
+
+Bar (north_star): bit-exact inlier masks / per-hypothesis counts for fixed hypothesis seeds;
+H within 1e-6 relative Frobenius of the oracle (the refit + LM sums run in a different order on
+the GPU); with MCV_FLAG_NO_REFINE the returned model is the device's fp64 minimal solve and must
+be bit-identical to the oracle's.
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from minicv_amd import native as N
+from minicv_amd import opencv, synthetic as S
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / "golden"
+REL_TOL = 1e-6   # relative Frobenius tolerance on refined H (north_star)
+
+
+def relf(A, B):
+    return np.linalg.norm(np.asarray(A) - np.asarray(B)) / np.linalg.norm(B)
+
+
+@pytest.fixture(scope="module")
+def torch_dev(gpu):
+    import torch
+    return torch, torch.device("cuda:0")
+
+
+def device_counts(torch_dev, src, dst, seed, begin, count, thr, model=N.MODEL_HOMOGRAPHY):
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    pts = D.pack_points_tensor(src, dst, dev)
+    plan = D.RansacPlan(model, src.shape[0], count)
+    cfg = opencv.RansacParams(threshold=thr, seed=seed).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(count, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, src.shape[0], cfg, begin, count, key, counts)
+    torch.cuda.synchronize()
+    out = counts.cpu().numpy(), [int(v) for v in key.cpu().numpy()]
+    plan.close()
+    return out
+
+
+@pytest.mark.parametrize("n,outl,seed,begin,count", [
+    (4, 0.0, 1, 0, 64), (5, 0.5, 2, 0, 300), (200, 0.5, 3, 0, 4096), (2000, 0.5, 4, 123456, 4096),
+    (3001, 0.8, 5, 2**31, 1000), (20000, 0.3, 6, 0, 1024)])
+def test_per_hypothesis_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count):
+    src, dst, _ = S.homography_problem(n, seed, outlier_frac=outl)
+    thr = 5e-3
+    got, key = device_counts(torch_dev, src, dst, seed, begin, count, thr)
+    ref = oracle.h_counts(oracle.pack4(src, dst), seed, begin, count, float(np.float32(thr * thr)))
+    np.testing.assert_array_equal(got, ref)
+    # best packed key: first strictly greater count among counts >= 4, before any sampler failure
+    fail = np.nonzero(ref == -2)[0]
+    lim = fail[0] if len(fail) else count
+    valid = ref[:lim] >= 4
+    if valid.any():
+        c = ref[:lim].max()
+        i = int(np.nonzero(ref[:lim] == c)[0][0])
+        assert key[0] == (int(c) << 32) | (0xFFFFFFFF - (begin + i))
+    else:
+        assert key[0] == 0
+    assert key[1] == (begin + int(fail[0]) if len(fail) else 2**63 - 1)
+
+
+def test_golden_cfg1(gpu, oracle):
+    g = np.load(GOLDEN / "cfg1_homography.npz")
+    p = opencv.RansacParams(threshold=float(g["thr"]), confidence=float(g["conf"]), max_iters=int(g["max_iters"]),
+                            seed=int(g["seed"]))
+    cnt, H, mask = opencv.findHomography(g["src"], g["dst"], p)
+    assert cnt == int(g["count"])
+    np.testing.assert_array_equal(mask, g["mask"].astype(bool))
+    assert relf(H, g["H"]) < REL_TOL
+
+
+CASES = [
+    # n, outlier fraction, sigma, thr, seed, maxIters, conf, flags
+    (4, 0.0, 1e-3, 5e-3, 1, 2000, 0.995, 0),
+    (5, 0.2, 1e-3, 5e-3, 2, 2000, 0.995, 0),
+    (8, 0.5, 1e-3, 5e-3, 3, 2000, 0.995, 0),
+    (50, 0.5, 1e-3, 5e-3, 4, 2000, 0.995, 0),
+    (200, 0.5, 1e-3, 5e-3, 5, 2000, 0.995, 0),
+    (1000, 0.7, 1e-3, 5e-3, 6, 5000, 0.999, 0),
+    (1000, 0.5, 1e-3, 5e-3, 7, 300, 0.995, N.FLAG_FIXED_ITERS),
+    (5000, 0.9, 2e-3, 1e-2, 8, 20000, 0.999, 0),
+    (777, 0.5, 0.0, 1e-4, 9, 2000, 0.995, 0),
+    (20000, 0.5, 1e-3, 5e-3, 10, 2000, 0.995, 0),
+]
+
+
+@pytest.mark.parametrize("n,outl,sigma,thr,seed,iters,conf,flags", CASES)
+def test_find_homography_vs_oracle(gpu, oracle, n, outl, sigma, thr, seed, iters, conf, flags):
+    src, dst, _ = S.homography_problem(n, seed, outlier_frac=outl, sigma=sigma)
+    cnt_o, H_o, mask_o, best_o = oracle.find_homography(src, dst, thr=thr, conf=conf, max_iters=iters, seed=seed,
+                                                        flags=flags)
+    p = opencv.RansacParams(threshold=thr, confidence=conf, max_iters=iters, seed=seed,
+                            fixed_iters=bool(flags & N.FLAG_FIXED_ITERS))
+    cnt, H, mask = opencv.findHomography(src, dst, p)
+    assert cnt == cnt_o
+    np.testing.assert_array_equal(mask, mask_o.astype(bool))
+    assert relf(H, H_o) < REL_TOL
+
+
+def test_no_refine_model_bit_exact(gpu, oracle):
+    src, dst, _ = S.homography_problem(3000, 12)
+    cnt_o, H_o, mask_o, _ = oracle.find_homography(src, dst, thr=5e-3, seed=12, flags=N.FLAG_NO_REFINE)
+    cnt, H, mask = opencv.findHomography(src, dst, opencv.RansacParams(threshold=5e-3, seed=12, refine=False))
+    assert cnt == cnt_o
+    np.testing.assert_array_equal(mask, mask_o.astype(bool))
+    np.testing.assert_array_equal(H, H_o)   # same fp64 minimal solve on both sides
+
+
+def test_least_squares_method(gpu, oracle):
+    src, dst, inl = S.homography_problem(500, 13, outlier_frac=0.0)
+    cnt_o, H_o, _, _ = oracle.find_homography(src, dst, method=0)
+    cnt, H, mask = opencv.findHomography(src, dst, opencv.RansacParams(method=N.METHOD_LSQ))
+    assert cnt == cnt_o == 500 and mask.all()
+    assert relf(H, H_o) < REL_TOL
+
+
+def test_degenerate_inputs_fail_like_oracle(gpu, oracle):
+    x = np.linspace(-1, 1, 30)
+    src = np.stack([x, 0.25 * x], axis=1)
+    dst = np.stack([x, -x], axis=1)
+    assert oracle.find_homography(src, dst, thr=0.01)[0] == 0
+    with pytest.raises(N.NativeError):
+        opencv.findHomography(src, dst, opencv.RansacParams(threshold=0.01))
+    with pytest.raises(N.NativeError):
+        opencv.findHomography(src[:3], dst[:3])
+
+
+def test_repeatable(gpu):
+    src, dst, _ = S.homography_problem(10000, 14)
+    r1 = opencv.findHomography(src, dst, opencv.RansacParams(threshold=5e-3, seed=3))
+    r2 = opencv.findHomography(src, dst, opencv.RansacParams(threshold=5e-3, seed=3))
+    assert r1[0] == r2[0]
+    np.testing.assert_array_equal(r1[1], r2[1])
+    np.testing.assert_array_equal(r1[2], r2[2])
+
+
+@pytest.mark.slow
+def test_full_size_bench_config_properties(torch_dev, oracle):
+    """BASELINE cfg3 size (N = 100k, 1M hypotheses): spot hypotheses match the oracle exactly, the
+    reduced key equals the argmax of the device's own counts, and the winner's mask has exactly
+    its count of inliers."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    n, H = 100_000, 1 << 20
+    src, dst, _ = S.homography_problem(n, 3)
+    thr = 5e-3
+    pts = D.pack_points_tensor(src, dst, dev)
+    plan = D.RansacPlan(N.MODEL_HOMOGRAPHY, n, H)
+    cfg = opencv.RansacParams(threshold=thr, seed=3, fixed_iters=True, max_iters=H).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(H, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, 0, H, key, counts)
+    c = counts.cpu().numpy()
+    k = int(key[0].item())
+    cnt, idx = D.unpack_key(k)
+    assert cnt == c.max() and idx == int(np.argmax(c))
+    rng = np.random.default_rng(0)
+    pick = np.sort(rng.choice(H, size=48, replace=False))
+    pts4 = oracle.pack4(src, dst)
+    for h in pick:
+        ref = oracle.h_counts(pts4, 3, int(h), 1, float(np.float32(thr * thr)))[0]
+        assert c[h] == ref
+    mask = torch.zeros(n, dtype=torch.uint8, device=dev)
+    cfg_nr = opencv.RansacParams(threshold=thr, seed=3, refine=False).to_c()
+    fc, _ = plan.finalize(pts, n, cfg_nr, idx, mask)
+    assert fc == cnt == int(mask.sum().item())
+    # determinism
+    counts2 = torch.zeros_like(counts)
+    plan.evaluate(pts, n, cfg, 0, H, key, counts2)
+    assert torch.equal(counts, counts2)
+    plan.close()
