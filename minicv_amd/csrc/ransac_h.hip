@@ -81,24 +81,18 @@ __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ p
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
 
-    int p = lane;
-    // Two correspondences per lane per trip: two independent loads in flight.
-    for (; p + 64 < N; p += 128) {
-        const float4 qa = pts[p];
-        const float4 qb = pts[p + 64];
+    // Wave-uniform trip count (the counts are per-wave SGPR sums of ballots: every lane must take
+    // part in every ballot). Two correspondences per lane per trip: two loads in flight.
+    for (int base = 0; base < N; base += 128) {
+        const int pa = base + lane, pb = pa + 64;
+        const bool va = pa < N, vb = pb < N;
+        const float4 qa = pts[va ? pa : 0];
+        const float4 qb = pts[vb ? pb : 0];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const float ea = h_error(hm[k], qa.x, qa.y, qa.z, qa.w);
             const float eb = h_error(hm[k], qb.x, qb.y, qb.z, qb.w);
-            cnt[k] += (uint32_t)__popcll(__ballot(ea <= thr2)) + (uint32_t)__popcll(__ballot(eb <= thr2));
-        }
-    }
-    if (p < N) {
-        const float4 qa = pts[p];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float ea = h_error(hm[k], qa.x, qa.y, qa.z, qa.w);
-            cnt[k] += (uint32_t)__popcll(__ballot(ea <= thr2));
+            cnt[k] += (uint32_t)__popcll(__ballot(va && ea <= thr2)) + (uint32_t)__popcll(__ballot(vb && eb <= thr2));
         }
     }
     if (lane == 0) {

@@ -45,7 +45,7 @@ def hamming_problem(nq: int, nt: int, nbytes: int = 32, seed: int = 2, random_fr
     planted = rng.integers(0, nt, size=nq)
     q = t[planted].copy()
     bits = np.unpackbits(q, axis=1)
-    flips = rng.integers(0, max_flips + 1, size=nq)
+    flips = rng.integers(0, min(max_flips, nbytes * 8) + 1, size=nq)
     for i in range(nq):
         pos = rng.choice(nbytes * 8, size=flips[i], replace=False)
         bits[i, pos] ^= 1
