@@ -120,6 +120,8 @@ MCV_API bool cvDetectArucoMarkers(char* data, int width, int height, int channel
 /* flags */
 #define MCV_FLAG_FIXED_ITERS  1   /* evaluate exactly maxIters hypotheses (no adaptive stop) */
 #define MCV_FLAG_NO_REFINE    2   /* return the best hypothesis' model (skip inlier refit + LM) */
+#define MCV_FLAG_UNFUSED_ERROR 4  /* inlier error evaluated unfused, op by op (OpenCV x86 SSE build
+                                     arithmetic); default: FMA-contracted definition */
 
 /* F error metric (cfg->errorKind, fundamental only) */
 #define MCV_FERR_SAMPSON   0   /* first-order geometric (Sampson) distance^2 (north_star) */
@@ -232,6 +234,12 @@ MCV_API int  mcvProfileRead(const char* kernel, double* total_ms);
  * ---------------------------------------------------------------------------------------- */
 MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, uint64_t seed, int64_t hyp,
                               double* model9, float* modelf9, int* sampleIdx);
+/* Device self-test: number of 32-bit patterns w where the sweep's reciprocal differs from 1.f/w
+ * (mode 0 = shipped rcp_rn; 1 = without the special-value fixup; 2 = raw v_rcp_f32). */
+MCV_API long long mcvTestRcpExhaustive(int mode, uint32_t* firstMismatches16);
+/* Device self-test: run the homography inlier sweep on caller-supplied fp32 models (8 floats each). */
+MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models8, int nModels, float thr2, int fused,
+                                   int* counts);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                            uint32_t* out4);
 

@@ -6,6 +6,9 @@ library lands where Aardvark's native loader looks for MiniCVNative
 
 -ffp-contract=off is global on purpose: the RANSAC error and minimal solvers must round exactly
 as written, on the GPU and in the host twin, for the inlier masks to be bit-exact.
+-fno-slp-vectorize: keep f32 VALU ops single-lane; SLP packing into v_pk_*_f32 needs v_mov to
+build operand pairs from scalar model coefficients and is an anti-lever beside the sweep's
+SGPR-operand arithmetic (cdna_hip_programming.md, packed f32 VALU).
 """
 from __future__ import annotations
 
@@ -26,7 +29,7 @@ ARCH = os.environ.get("MCV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = [
     "-x", "hip", "-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}",
-    "-ffp-contract=off", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+    "-ffp-contract=off", "-fno-slp-vectorize", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
     "-Wno-unused-variable", "-Wno-unused-but-set-variable",
     f"-I{INCLUDE}", f"-I{CSRC}",
 ]

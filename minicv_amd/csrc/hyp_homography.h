@@ -220,12 +220,34 @@ MCV_HD int h_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, d
     return kStatusNoSample;
 }
 
-// HomographyEstimatorCallback::computeError for one correspondence (fp32, as written).
+// HomographyEstimatorCallback::computeError for one correspondence, two bit-level definitions
+// (the reference's own arithmetic is build-dependent: OpenCV's x86 SSE baseline evaluates the
+// expression unfused, clang's default -ffp-contract=on on arm64 contracts it into FMAs):
+//   unfused (MCV_FLAG_UNFUSED_ERROR): every operation rounded as written, IEEE division;
+//   fused (default): w = fma(h6,x,fma(h7,y,1)); ww = RN(1/w);
+//                    ex = fma(fma(h0,x,fma(h1,y,h2)), ww, -mx); ey likewise; e = fma(ex,ex,ey*ey).
+// Inlier iff e <= (float)thr^2 in both.
 MCV_HD float h_error(const float* h, float x, float y, float mx, float my) {
     const float ww = 1.f / (h[6] * x + h[7] * y + 1.f);
     const float ex = (h[0] * x + h[1] * y + h[2]) * ww - mx;
     const float ey = (h[3] * x + h[4] * y + h[5]) * ww - my;
     return ex * ex + ey * ey;
 }
+
+MCV_HD float h_denominator_fused(const float* h, float x, float y) { return fmaf(h[6], x, fmaf(h[7], y, 1.f)); }
+
+MCV_HD float h_error_fused_ww(const float* h, float x, float y, float mx, float my, float ww) {
+    const float ex = fmaf(fmaf(h[0], x, fmaf(h[1], y, h[2])), ww, -mx);
+    const float ey = fmaf(fmaf(h[3], x, fmaf(h[4], y, h[5])), ww, -my);
+    return fmaf(ex, ex, ey * ey);
+}
+
+// Reference form of the fused error (IEEE division): host twin and rare-path fallback.
+MCV_HD float h_error_fused(const float* h, float x, float y, float mx, float my) {
+    return h_error_fused_ww(h, x, y, mx, my, 1.f / h_denominator_fused(h, x, y));
+}
+
+// |w| inside the range where rcp_newton(w) == 1.f / w (exhaustively verified).
+MCV_HD bool rcp_newton_ok(float w) { return fabsf(w) >= 0x1p-126f && fabsf(w) < 0x1p126f; }
 
 }  // namespace mcv

@@ -22,9 +22,10 @@ void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOu
 void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
                        int* d_counts, hipStream_t s);
 void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
-                     hipStream_t s);
-void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, uint8_t* d_mask, int* d_count,
-                   hipStream_t s);
+                     bool fused, const float* d_bbox, hipStream_t s);
+void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s);
+void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, bool fused, uint8_t* d_mask,
+                   int* d_count, hipStream_t s);
 void h_reduce_sums(const float* d_pts4, int N, const uint8_t* d_mask, double* d_part, double* d_out, hipStream_t s);
 void h_reduce_absdev(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, double* d_part,
                      double* d_out, hipStream_t s);

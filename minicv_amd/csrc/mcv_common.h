@@ -119,4 +119,31 @@ MCV_HD bool draw_distinct(HypStream& rs, int N, int (&idx)[M]) {
     return true;
 }
 
+// v_rcp_f32 + one FMA Newton step: equals the IEEE 1.f / w for every |w| in [2^-126, 2^126)
+// (exhaustive GPU check, mcvTestRcpExhaustive mode 3); callers guarantee that range.
+MCV_HD float rcp_newton(float w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float r = __builtin_amdgcn_rcpf(w);
+    const float e = __builtin_fmaf(-w, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+#else
+    return 1.0f / w;
+#endif
+}
+
+// Correctly rounded fp32 reciprocal. Device: v_rcp_f32 (1 ulp) + one FMA Newton step, with
+// v_div_fixup_f32 for 0 / inf / NaN operands — 4 VALU ops instead of the ~10 of the IEEE
+// division expansion; equality with 1.f / w is checked exhaustively over all 2^32 inputs on the
+// GPU (mcvTestRcpExhaustive, tests/test_gpu_selftest.py). Host: the IEEE division itself.
+MCV_HD float rcp_rn(float w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float r = __builtin_amdgcn_rcpf(w);
+    const float e = __builtin_fmaf(-w, r, 1.0f);
+    const float r1 = __builtin_fmaf(e, r, r);
+    return __builtin_amdgcn_div_fixupf(r1, w, 1.0f);
+#else
+    return 1.0f / w;
+#endif
+}
+
 }  // namespace mcv

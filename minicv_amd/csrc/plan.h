@@ -31,6 +31,7 @@ struct Plan {
     DevBuf<double> red;       // reduction result
     DevBuf<uint8_t> mask;
     DevBuf<int> count;
+    DevBuf<float> bbox;       // max |x|, max |y| of the source points (fused fast-path bound)
     DevBuf<uint8_t> one;      // single-hypothesis output record
     PinnedBuf<int> h_counts;
     PinnedBuf<double> h_red;
@@ -65,6 +66,7 @@ struct ProfScope {
 };
 void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst, hipStream_t s);
 double effective_threshold(const RansacConfig& cfg);
+bool fused_error(const RansacConfig& cfg);
 RansacConfig config_or_default(const RansacConfig* cfg);
 int64_t ransac_search(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, hipStream_t s);
 int finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,

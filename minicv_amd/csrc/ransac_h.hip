@@ -57,10 +57,76 @@ __global__ void mcv_h_one(const float* __restrict__ pts4, int N, uint64_t seed, 
 // wave-uniform (readfirstlane), so the models come in through scalar loads and every VALU op
 // reads its model coefficient straight from an SGPR; the counts accumulate in SGPRs too.
 // ------------------------------------------------------------------------------------------
-template <int K>
+// Class mask of v_cmp_class_f32 for "not a normal number" (sNaN, qNaN, +-inf, +-denormal, +-0).
+static constexpr int kClassNotNormal = 0x001 | 0x002 | 0x004 | 0x010 | 0x020 | 0x040 | 0x080 | 0x200;
+
+// Wave mask of lanes whose w falls in the classes `cls`: one v_cmp_class_f32 writing an SGPR pair
+// (the builtin + ballot pair lowers to cmp + cndmask + cmp on ROCm 7.2).
+__device__ __forceinline__ uint64_t class_mask(float w, int cls) {
+    uint64_t m;
+    asm("v_cmp_class_f32_e64 %0, %1, %2" : "=s"(m) : "v"(w), "s"(cls));
+    return m;
+}
+
+// One trip of the sweep: two correspondences per lane against the wave's K hypotheses.
+// PRED: lane predicates (ragged tail only). FUSED fast path: rcp_newton, with the trip redone by
+// IEEE division when any denominator is zero / denormal / non-finite.
+template <int K, bool FUSED, bool PRED>
+__device__ __forceinline__ void h_sweep_trip(const float (&hm)[K][8], const float4& qa, const float4& qb, bool va,
+                                             bool vb, float thr2, bool fast, uint32_t (&cnt)[K]) {
+    auto vote = [&](bool pa, bool pb) -> uint32_t {
+        if constexpr (PRED)
+            return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(va && pa)) +
+                   (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(vb && pb));
+        else
+            return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(pa)) +
+                   (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(pb));
+    };
+    if constexpr (FUSED) {
+        if (fast) {
+            uint64_t bad = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const float wa = h_denominator_fused(hm[k], qa.x, qa.y);
+                const float wb = h_denominator_fused(hm[k], qb.x, qb.y);
+                bad |= class_mask(wa, kClassNotNormal) | class_mask(wb, kClassNotNormal);
+                const float ea = h_error_fused_ww(hm[k], qa.x, qa.y, qa.z, qa.w, rcp_newton(wa));
+                const float eb = h_error_fused_ww(hm[k], qb.x, qb.y, qb.z, qb.w, rcp_newton(wb));
+                cnt[k] += vote(ea <= thr2, eb <= thr2);
+            }
+            if (__builtin_expect(bad == 0, 1)) return;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {   // replace this trip's fast counts by the exact ones
+                const float wa = h_denominator_fused(hm[k], qa.x, qa.y);
+                const float wb = h_denominator_fused(hm[k], qb.x, qb.y);
+                const float fa = h_error_fused_ww(hm[k], qa.x, qa.y, qa.z, qa.w, rcp_newton(wa));
+                const float fb = h_error_fused_ww(hm[k], qb.x, qb.y, qb.z, qb.w, rcp_newton(wb));
+                const float ea = h_error_fused_ww(hm[k], qa.x, qa.y, qa.z, qa.w, 1.f / wa);
+                const float eb = h_error_fused_ww(hm[k], qb.x, qb.y, qb.z, qb.w, 1.f / wb);
+                cnt[k] = cnt[k] - vote(fa <= thr2, fb <= thr2) + vote(ea <= thr2, eb <= thr2);
+            }
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {   // exact for the whole wave
+            const float ea = h_error_fused(hm[k], qa.x, qa.y, qa.z, qa.w);
+            const float eb = h_error_fused(hm[k], qb.x, qb.y, qb.z, qb.w);
+            cnt[k] += vote(ea <= thr2, eb <= thr2);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float ea = h_error(hm[k], qa.x, qa.y, qa.z, qa.w);
+            const float eb = h_error(hm[k], qb.x, qb.y, qb.z, qb.w);
+            cnt[k] += vote(ea <= thr2, eb <= thr2);
+        }
+    }
+}
+
+template <int K, bool FUSED>
 __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ pts, int N,
                                                     const HModelF* __restrict__ models, int* __restrict__ counts,
-                                                    int hypCount, float thr2) {
+                                                    int hypCount, float thr2, const float* __restrict__ bbox) {
     const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
     const int lane = threadIdx.x & 63;
     const int h0 = wave * K;
@@ -75,30 +141,77 @@ __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ p
         const HModelF m = models[valid[k] ? hk : h0];
 #pragma unroll
         for (int j = 0; j < 8; ++j) hm[k][j] = valid[k] ? m.h[j] : __builtin_nanf("");
+        // h2 and h5 meet another uniform operand in fma(h1, y, h2) / fma(h4, y, h5); a VALU op
+        // reads at most one SGPR (gfx9 constant-bus limit), so keep those two in VGPRs and the
+        // other six in SGPRs (no per-use v_mov, and SGPR pressure stays below the spill point).
+        asm volatile("" : "+v"(hm[k][2]));
+        asm volatile("" : "+v"(hm[k][5]));
     }
 
     uint32_t cnt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
 
+    // Fused fast path precondition, per hypothesis: max |w| over the points' bounding box stays
+    // below 2^125, so every denominator is below 2^126 (the exhaustively verified range of
+    // rcp_newton). The lower end (0, denormal, inf, NaN) is checked per point below.
+    bool fast = FUSED;
+    if constexpr (FUSED) {
+        const float X = bbox[0], Y = bbox[1];
+        bool anyValidBig = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float wmax = fabsf(hm[k][6]) * X + fabsf(hm[k][7]) * Y + 1.f;
+            anyValidBig = anyValidBig || (valid[k] && !(wmax < 0x1p125f));
+        }
+        fast = !anyValidBig;
+    }
+
     // Wave-uniform trip count (the counts are per-wave SGPR sums of ballots: every lane must take
-    // part in every ballot). Two correspondences per lane per trip: two loads in flight.
-    for (int base = 0; base < N; base += 128) {
-        const int pa = base + lane, pb = pa + 64;
+    // part in every ballot). Two correspondences per lane per trip: two loads in flight. Full
+    // 128-point trips run unpredicated; the ragged tail runs once with lane predicates.
+    const int nFull = N & ~127;
+    for (int base = 0; base < nFull; base += 128) {
+        const float4 qa = pts[base + lane];
+        const float4 qb = pts[base + lane + 64];
+        h_sweep_trip<K, FUSED, false>(hm, qa, qb, true, true, thr2, fast, cnt);
+    }
+    if (nFull < N) {
+        const int pa = nFull + lane, pb = pa + 64;
         const bool va = pa < N, vb = pb < N;
         const float4 qa = pts[va ? pa : 0];
         const float4 qb = pts[vb ? pb : 0];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float ea = h_error(hm[k], qa.x, qa.y, qa.z, qa.w);
-            const float eb = h_error(hm[k], qb.x, qb.y, qb.z, qb.w);
-            cnt[k] += (uint32_t)__popcll(__ballot(va && ea <= thr2)) + (uint32_t)__popcll(__ballot(vb && eb <= thr2));
-        }
+        h_sweep_trip<K, FUSED, true>(hm, qa, qb, va, vb, thr2, fast, cnt);
     }
     if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (valid[k]) counts[h0 + k] = (int)cnt[k];
+    }
+}
+
+// Bounding box of the source points: bbox[0] = max |x|, bbox[1] = max |y| (one block; the
+// ordering of float maxima is exact, so the result does not depend on the reduction order).
+__global__ __launch_bounds__(1024) void mcv_bbox(const float4* __restrict__ pts, int N, float* __restrict__ bbox) {
+    __shared__ float sx[16], sy[16];
+    float mx = 0, my = 0;
+    for (int i = threadIdx.x; i < N; i += 1024) {
+        const float4 q = pts[i];
+        mx = fmaxf(mx, fabsf(q.x));
+        my = fmaxf(my, fabsf(q.y));
+        if (q.x != q.x || q.y != q.y) mx = __builtin_inff();   // NaN coordinate: force exact path
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        my = fmaxf(my, __shfl_xor(my, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) { sx[threadIdx.x >> 6] = mx; sy[threadIdx.x >> 6] = my; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) { mx = fmaxf(mx, sx[w]); my = fmaxf(my, sy[w]); }
+        bbox[0] = mx;
+        bbox[1] = my;
     }
 }
 
@@ -200,12 +313,13 @@ __global__ __launch_bounds__(kBestThreads) void mcv_best_final(const uint64_t* _
 // Inlier mask of one model (count via per-wave ballot + one atomic per wave).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mcv_h_mask(const float4* __restrict__ pts, int N, HModelF m, float thr2,
-                                                  uint8_t* __restrict__ mask, int* __restrict__ count) {
+                                                  int fused, uint8_t* __restrict__ mask, int* __restrict__ count) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     bool in = false;
     if (i < N) {
         const float4 q = pts[i];
-        in = h_error(m.h, q.x, q.y, q.z, q.w) <= thr2;
+        const float e = fused ? h_error_fused(m.h, q.x, q.y, q.z, q.w) : h_error(m.h, q.x, q.y, q.z, q.w);
+        in = e <= thr2;
         mask[i] = in ? 1 : 0;
     }
     const uint64_t b = __ballot(in);
@@ -305,13 +419,21 @@ void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOu
     hipLaunchKernelGGL(mcv_h_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out);
 }
 
+void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_bbox, dim3(1), dim3(1024), 0, s, (const float4*)d_pts4, N, d_bbox);
+}
+
 void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
-                     hipStream_t s) {
+                     bool fused, const float* d_bbox, hipStream_t s) {
     constexpr int K = kVerifyHypPerWave;
     const int waves = (hypCount + K - 1) / K;
     const int blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL((mcv_h_verify<K>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
-                       (const HModelF*)d_models, d_counts, hypCount, thr2);
+    if (fused)
+        hipLaunchKernelGGL((mcv_h_verify<K, true>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
+                           (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox);
+    else
+        hipLaunchKernelGGL((mcv_h_verify<K, false>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
+                           (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox);
 }
 
 void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uint64_t* d_pkey, int64_t* d_pfail,
@@ -325,12 +447,12 @@ void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uin
                        minCount, d_out);
 }
 
-void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, uint8_t* d_mask, int* d_count,
-                   hipStream_t s) {
+void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, bool fused, uint8_t* d_mask,
+                   int* d_count, hipStream_t s) {
     HModelF m;
     for (int j = 0; j < 8; ++j) m.h[j] = hf8[j];
-    hipLaunchKernelGGL(mcv_h_mask, dim3((N + 255) / 256), dim3(256), 0, s, (const float4*)d_pts4, N, m, thr2, d_mask,
-                       d_count);
+    hipLaunchKernelGGL(mcv_h_mask, dim3((N + 255) / 256), dim3(256), 0, s, (const float4*)d_pts4, N, m, thr2,
+                       fused ? 1 : 0, d_mask, d_count);
 }
 
 void launch_fill_u8(uint8_t* d, int n, uint8_t v, hipStream_t s) {

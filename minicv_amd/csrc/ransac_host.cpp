@@ -89,6 +89,7 @@ void Plan::reserve(int n, int64_t hyps) {
     red.ensure(64);
     mask.ensure((size_t)maxN);
     count.ensure(1);
+    bbox.ensure(4);
     one.ensure(512);
     h_counts.ensure((size_t)maxHyps);
     h_red.ensure(64);
@@ -135,6 +136,7 @@ void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst,
 }
 
 double effective_threshold(const RansacConfig& cfg) { return cfg.threshold > 0 ? cfg.threshold : 3.0; }
+bool fused_error(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_UNFUSED_ERROR) == 0; }
 
 // Sum V doubles over (masked) correspondences: GPU two-stage reduction, result to host.
 template <class F>
@@ -256,9 +258,10 @@ void evaluate_chunk(Plan& P, const float* d_pts, int N, const RansacConfig& cfg,
     const double t = effective_threshold(cfg);
     const float thr2 = (float)(t * t);
     if (P.model == MCV_MODEL_HOMOGRAPHY) {
+        if (fused_error(cfg)) launch_bbox(d_pts, N, P.bbox.p, s);
         launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
         ProfScope ps("h_verify", s);
-        launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, s);
+        launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, fused_error(cfg), P.bbox.p, s);
     } else {
         f_evaluate_chunk(P, d_pts, N, cfg, hypBegin, hypCount, d_counts, s);
     }
@@ -282,7 +285,7 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     std::memcpy(&one, P.h_one.p, sizeof(HOneOut));
     if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
     MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
-    launch_h_mask(d_pts, N, one.hf, thr2, d_mask, P.count.p, s);
+    launch_h_mask(d_pts, N, one.hf, thr2, fused_error(cfg), d_mask, P.count.p, s);
     MCV_HIP(hipGetLastError());
     MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
     MCV_HIP(hipStreamSynchronize(s));

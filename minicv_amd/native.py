@@ -49,6 +49,7 @@ METHOD_LSQ = 0
 METHOD_RANSAC = 8
 FLAG_FIXED_ITERS = 1
 FLAG_NO_REFINE = 2
+FLAG_UNFUSED_ERROR = 4
 FERR_SAMPSON = 0
 FERR_EPIPOLAR = 1
 MODEL_HOMOGRAPHY = 0
@@ -101,6 +102,8 @@ SIGNATURES = {
     # test hooks
     "mcvHostHypothesis": (_I, [_I, _P, _I, _U64, _I64, _P, _P, _P]),
     "mcvHostPhilox": (None, [C.c_uint32] * 6 + [_P]),
+    "mcvTestRcpExhaustive": (C.c_longlong, [_I, _P]),
+    "mcvTestHomographySweep": (_I, [_P, _I, _P, _I, _F, _I, _P]),
 }
 
 _lib = None

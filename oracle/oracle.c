@@ -203,16 +203,27 @@ int orc_h_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, doubl
     return ORC_NO_SAMPLE;
 }
 
-/* computeError + findInliers for one fp32 model. mask may be NULL. */
-int orc_h_count(const float* pts4, int N, const float* h, float thr2, uint8_t* mask) {
+/* computeError + findInliers for one fp32 model. mask may be NULL.
+ * fused = 1 (default definition): w = fma(h6,x,fma(h7,y,1)); ww = 1/w (IEEE);
+ *   ex = fma(fma(h0,x,fma(h1,y,h2)), ww, -mx); ey likewise; e = fma(ex,ex,ey*ey)
+ * fused = 0: OpenCV's expression evaluated op by op (x86 SSE-baseline arithmetic). */
+int orc_h_count(const float* pts4, int N, const float* h, float thr2, uint8_t* mask, int fused) {
     int n = 0;
     for (int i = 0; i < N; ++i) {
         const float* p = pts4 + 4 * (size_t)i;
-        float x = p[0], y = p[1];
-        float ww = 1.f / (h[6] * x + h[7] * y + 1.f);
-        float ex = (h[0] * x + h[1] * y + h[2]) * ww - p[2];
-        float ey = (h[3] * x + h[4] * y + h[5]) * ww - p[3];
-        int in = ex * ex + ey * ey <= thr2;
+        float x = p[0], y = p[1], e;
+        if (fused) {
+            float ww = 1.f / fmaf(h[6], x, fmaf(h[7], y, 1.f));
+            float ex = fmaf(fmaf(h[0], x, fmaf(h[1], y, h[2])), ww, -p[2]);
+            float ey = fmaf(fmaf(h[3], x, fmaf(h[4], y, h[5])), ww, -p[3]);
+            e = fmaf(ex, ex, ey * ey);
+        } else {
+            float ww = 1.f / (h[6] * x + h[7] * y + 1.f);
+            float ex = (h[0] * x + h[1] * y + h[2]) * ww - p[2];
+            float ey = (h[3] * x + h[4] * y + h[5]) * ww - p[3];
+            e = ex * ex + ey * ey;
+        }
+        int in = e <= thr2;
         if (mask) mask[i] = (uint8_t)in;
         n += in;
     }
@@ -221,7 +232,7 @@ int orc_h_count(const float* pts4, int N, const float* h, float thr2, uint8_t* m
 
 /* Status-or-count per hypothesis over [hypBegin, hypBegin+hypCount), threads over hypotheses. */
 void orc_h_counts(const float* pts4, int N, uint64_t seed, int64_t hypBegin, int64_t hypCount, float thr2,
-                  int* counts, int nthreads) {
+                  int fused, int* counts, int nthreads) {
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(dynamic, 4)
@@ -230,7 +241,7 @@ void orc_h_counts(const float* pts4, int N, uint64_t seed, int64_t hypBegin, int
         double H[9];
         float hf[8];
         int st = orc_h_hypothesis(pts4, N, seed, hypBegin + i, H, hf, NULL);
-        counts[i] = st == 1 ? orc_h_count(pts4, N, hf, thr2, NULL) : st;
+        counts[i] = st == 1 ? orc_h_count(pts4, N, hf, thr2, NULL, fused) : st;
     }
 }
 
@@ -444,6 +455,7 @@ int64_t orc_ransac_replay(const int* counts, int64_t ncounts, int N, int m, doub
 
 #define ORC_FLAG_FIXED_ITERS 1
 #define ORC_FLAG_NO_REFINE 2
+#define ORC_FLAG_UNFUSED_ERROR 4
 
 /* cv::findHomography(src, dst, method, thr, mask, maxIters, conf) with the counter-based sampler.
  * pts as fp64 AoS (converted to float as convertTo(CV_32F)). Returns inlier count, 0 on failure. */
@@ -473,14 +485,15 @@ int orc_find_homography(const double* src, const double* dst, int N, double thr,
         int bc = 0;
         int* cnts = (int*)malloc(sizeof(int) * (size_t)niters);
         /* counts for every hypothesis up front (parallel), replay sequentially */
-        orc_h_counts(pts, N, seed, 0, niters, thr2, cnts, nthreads);
+        const int fused = (flags & ORC_FLAG_UNFUSED_ERROR) == 0;
+        orc_h_counts(pts, N, seed, 0, niters, thr2, fused, cnts, nthreads);
         best = orc_ransac_replay(cnts, niters, N, 4, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0, &bc);
         free(cnts);
         if (best >= 0) {
             double Hb[9];
             float hf[8];
             orc_h_hypothesis(pts, N, seed, best, Hb, hf, NULL);
-            count = orc_h_count(pts, N, hf, thr2, m8);
+            count = orc_h_count(pts, N, hf, thr2, m8, fused);
             memcpy(H, Hb, sizeof(Hb));
             result = 1;
             if (!(flags & ORC_FLAG_NO_REFINE)) {

@@ -16,8 +16,8 @@ _P, _I, _I64, _U64, _D, _F = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_dou
 _SIGS = {
     "orc_philox": (None, [_P, _P, _P]),
     "orc_h_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P, _P]),
-    "orc_h_count": (_I, [_P, _I, _P, _F, _P]),
-    "orc_h_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _P, _I]),
+    "orc_h_count": (_I, [_P, _I, _P, _F, _P, _I]),
+    "orc_h_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _I, _P, _I]),
     "orc_update_num_iters": (_I, [_D, _D, _I, _I]),
     "orc_ransac_replay": (_I64, [_P, _I64, _I, _I, _D, _I, _I, _P]),
     "orc_find_homography": (_I, [_P, _P, _I, _D, _D, _I, _I, _U64, _I, _P, _P, _P, _I]),
@@ -67,16 +67,17 @@ def h_hypothesis(pts4: np.ndarray, seed: int, hyp: int):
     return st, H, hf, idx
 
 
-def h_count(pts4: np.ndarray, hf: np.ndarray, thr2: float, want_mask: bool = False):
+def h_count(pts4: np.ndarray, hf: np.ndarray, thr2: float, want_mask: bool = False, fused: bool = True):
     hf = np.ascontiguousarray(hf, dtype=np.float32)
     m = np.zeros(pts4.shape[0], dtype=np.uint8) if want_mask else None
-    n = load().orc_h_count(ptr(pts4), pts4.shape[0], ptr(hf), thr2, ptr(m) if want_mask else None)
+    n = load().orc_h_count(ptr(pts4), pts4.shape[0], ptr(hf), thr2, ptr(m) if want_mask else None, int(fused))
     return (n, m) if want_mask else n
 
 
-def h_counts(pts4: np.ndarray, seed: int, begin: int, count: int, thr2: float, nthreads: int = 0) -> np.ndarray:
+def h_counts(pts4: np.ndarray, seed: int, begin: int, count: int, thr2: float, nthreads: int = 0,
+             fused: bool = True) -> np.ndarray:
     out = np.zeros(count, dtype=np.int32)
-    load().orc_h_counts(ptr(pts4), pts4.shape[0], seed, begin, count, thr2, ptr(out), nthreads)
+    load().orc_h_counts(ptr(pts4), pts4.shape[0], seed, begin, count, thr2, int(fused), ptr(out), nthreads)
     return out
 
 

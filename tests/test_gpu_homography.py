@@ -28,12 +28,12 @@ def torch_dev(gpu):
     return torch, torch.device("cuda:0")
 
 
-def device_counts(torch_dev, src, dst, seed, begin, count, thr, model=N.MODEL_HOMOGRAPHY):
+def device_counts(torch_dev, src, dst, seed, begin, count, thr, model=N.MODEL_HOMOGRAPHY, unfused=False):
     torch, dev = torch_dev
     from minicv_amd import device as D
     pts = D.pack_points_tensor(src, dst, dev)
     plan = D.RansacPlan(model, src.shape[0], count)
-    cfg = opencv.RansacParams(threshold=thr, seed=seed).to_c()
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     counts = torch.zeros(count, dtype=torch.int32, device=dev)
     plan.evaluate(pts, src.shape[0], cfg, begin, count, key, counts)
@@ -43,14 +43,16 @@ def device_counts(torch_dev, src, dst, seed, begin, count, thr, model=N.MODEL_HO
     return out
 
 
-@pytest.mark.parametrize("n,outl,seed,begin,count", [
-    (4, 0.0, 1, 0, 64), (5, 0.5, 2, 0, 300), (200, 0.5, 3, 0, 4096), (2000, 0.5, 4, 123456, 4096),
-    (3001, 0.8, 5, 2**31, 1000), (20000, 0.3, 6, 0, 1024)])
-def test_per_hypothesis_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count):
+@pytest.mark.parametrize("n,outl,seed,begin,count,unfused", [
+    (4, 0.0, 1, 0, 64, False), (5, 0.5, 2, 0, 300, False), (200, 0.5, 3, 0, 4096, False),
+    (2000, 0.5, 4, 123456, 4096, False), (3001, 0.8, 5, 2**31, 1000, False), (20000, 0.3, 6, 0, 1024, False),
+    (129, 0.5, 7, 0, 2048, True), (2000, 0.5, 8, 99, 4096, True), (20000, 0.3, 9, 0, 1024, True)])
+def test_per_hypothesis_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, unfused):
     src, dst, _ = S.homography_problem(n, seed, outlier_frac=outl)
     thr = 5e-3
-    got, key = device_counts(torch_dev, src, dst, seed, begin, count, thr)
-    ref = oracle.h_counts(oracle.pack4(src, dst), seed, begin, count, float(np.float32(thr * thr)))
+    got, key = device_counts(torch_dev, src, dst, seed, begin, count, thr, unfused=unfused)
+    ref = oracle.h_counts(oracle.pack4(src, dst), seed, begin, count, float(np.float32(thr * thr)),
+                          fused=not unfused)
     np.testing.assert_array_equal(got, ref)
     # best packed key: first strictly greater count among counts >= 4, before any sampler failure
     fail = np.nonzero(ref == -2)[0]
@@ -87,6 +89,8 @@ CASES = [
     (5000, 0.9, 2e-3, 1e-2, 8, 20000, 0.999, 0),
     (777, 0.5, 0.0, 1e-4, 9, 2000, 0.995, 0),
     (20000, 0.5, 1e-3, 5e-3, 10, 2000, 0.995, 0),
+    (3000, 0.5, 1e-3, 5e-3, 11, 2000, 0.995, N.FLAG_UNFUSED_ERROR),
+    (200, 0.6, 1e-3, 5e-3, 12, 500, 0.995, N.FLAG_UNFUSED_ERROR | N.FLAG_FIXED_ITERS),
 ]
 
 
@@ -96,7 +100,8 @@ def test_find_homography_vs_oracle(gpu, oracle, n, outl, sigma, thr, seed, iters
     cnt_o, H_o, mask_o, best_o = oracle.find_homography(src, dst, thr=thr, conf=conf, max_iters=iters, seed=seed,
                                                         flags=flags)
     p = opencv.RansacParams(threshold=thr, confidence=conf, max_iters=iters, seed=seed,
-                            fixed_iters=bool(flags & N.FLAG_FIXED_ITERS))
+                            fixed_iters=bool(flags & N.FLAG_FIXED_ITERS),
+                            unfused_error=bool(flags & N.FLAG_UNFUSED_ERROR))
     cnt, H, mask = opencv.findHomography(src, dst, p)
     assert cnt == cnt_o
     np.testing.assert_array_equal(mask, mask_o.astype(bool))
