@@ -31,6 +31,11 @@ HYPS_PER_GPU = 1 << 20
 THR = 5e-3
 SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# VALU issue model of mcv_h_verify (fused error): 15 VALU instructions per (hypothesis,
+# correspondence) evaluation, v_rcp_f32 at quarter rate -> 18 issue slots of 2 cycles (wave64 on
+# SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x 2.4 GHz / 2 x 64 lanes / 18.
+VALU_SLOTS_PER_EVAL = 18
+VALU_PEAK_EVALS = 256 * 4 * 2.4e9 / 2 * 64 / VALU_SLOTS_PER_EVAL
 
 
 def parse():
@@ -180,7 +185,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                          "kernel": "mcv_h_verify", "avg_launch_ms": avg_ms, "launches": launches,
-                         "algorithmic_bytes_per_launch": alg_bytes},
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 8 "
+                                 "hypotheses; the sweep's binding roof is VALU issue (see valu)",
+                         "valu": {"achieved": n * hyps / (avg_ms * 1e-3), "peak": VALU_PEAK_EVALS,
+                                  "unit": "evaluations/s", "frac": n * hyps / (avg_ms * 1e-3) / VALU_PEAK_EVALS,
+                                  "model": f"{VALU_SLOTS_PER_EVAL} VALU issue slots per (hypothesis, "
+                                           "correspondence) at 2.4 GHz"}},
             "result": {"best_count": result["count"], "best_hyp": result["idx"],
                        "refined_count": result["final_count"]},
         }
