@@ -34,6 +34,23 @@ void h_reduce_ltl(const float* d_pts4, int N, const uint8_t* d_mask, const doubl
 void h_reduce_lm(const float* d_pts4, int N, const uint8_t* d_mask, const double* h8, bool wantJ, double* d_part,
                  double* d_out, hipStream_t s);
 
+// ---- fundamental (ransac_f.hip)
+static const int kVerifyFHypPerWave = 4;
+struct FOneOut {
+    double F[9];
+    int status;
+    int idx[8];
+};
+void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+                       int* d_counts, hipStream_t s);
+void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s);
+void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
+                     int kind, hipStream_t s);
+void launch_f_mask(const float* d_pts4, int N, const double* F9, float thr2, int kind, uint8_t* d_mask, int* d_count,
+                   hipStream_t s);
+void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,
+                  double* d_part, double* d_out, hipStream_t s);
+
 // ---- shared (ransac_h.hip)
 void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uint64_t* d_pkey, int64_t* d_pfail,
                  uint64_t* d_out, hipStream_t s);

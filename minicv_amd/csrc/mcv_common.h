@@ -104,11 +104,13 @@ static const float kFltEpsilon = 1.19209290e-07f;
 // Returns false if the redraw bound is hit.
 template <int M>
 MCV_HD bool draw_distinct(HypStream& rs, int N, int (&idx)[M]) {
+#pragma unroll
     for (int i = 0; i < M; ++i) {
         int tries = 0;
         int v = rs.uniform(N);
         for (;;) {
             bool dup = false;
+#pragma unroll
             for (int j = 0; j < i; ++j) dup |= (idx[j] == v);
             if (!dup) break;
             if (++tries >= kMaxRedraw) return false;

@@ -46,6 +46,16 @@ struct Plan {
 
 Plan& thread_plan(int model);
 
+// Sum V doubles over (masked) correspondences: GPU two-stage reduction, result to host.
+template <class F>
+inline void reduce_to_host(Plan& P, hipStream_t s, int V, double* out, F launch) {
+    launch(P.part.p, P.red.p);
+    MCV_HIP(hipGetLastError());
+    MCV_HIP(hipMemcpyAsync(P.h_red.p, P.red.p, V * sizeof(double), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < V; ++i) out[i] = P.h_red.p[i];
+}
+
 // Opt-in kernel timing with HIP events recorded on the launch stream (bench.py's live roofline).
 bool prof_enabled();
 void prof_record(const char* name, hipEvent_t a, hipEvent_t b);
@@ -73,8 +83,7 @@ int finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_
              uint8_t* d_mask, hipStream_t s);
 
 // fundamental-matrix family (ransac_f.hip / ransac_f_host.cpp)
-void f_evaluate_chunk(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
-                      int* d_counts, hipStream_t s);
+int f_error_kind(const RansacConfig& cfg);
 int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* F, uint8_t* d_mask,
                hipStream_t s);
 int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F);

@@ -1,0 +1,158 @@
+// ransac_f.hip — gfx950 kernels of the fundamental-matrix RANSAC path.
+//
+//   mcv_f_generate      one lane per hypothesis: Philox sample of 8 -> collinearity check ->
+//                       8-point solve + rank 2 (fp64) -> FModelD (72 B) + status.
+//   mcv_f_verify<K, E>  inlier sweep: wave = K hypotheses (fp64 models in VGPRs), 64 lanes stream
+//                       the packed float4 correspondences; per (hypothesis, point) the fp64
+//                       Sampson / epipolar error E, cast to float, ballot + s_bcnt1 count.
+//   mcv_f_mask          inlier mask of the winner.
+//   OpFAtA              fixed-order fp64 reduction of A^T A (run8Point over all points).
+#include "mcv_common.h"
+#include "hyp_fundamental.h"
+#include "reduce.h"
+#include "kernels.h"
+
+namespace mcv {
+
+__global__ __launch_bounds__(256) void mcv_f_generate(const float* __restrict__ pts4, int N, uint64_t seed,
+                                                      int64_t hypBegin, int hypCount, FModelD* __restrict__ models,
+                                                      int* __restrict__ counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hypCount) return;
+    FModelD m;
+    const int st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr);
+    if (st == 1) {
+        models[i] = m;
+        counts[i] = 0;
+    } else {
+        counts[i] = st;
+    }
+}
+
+__global__ void mcv_f_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t hyp, FOneOut* __restrict__ out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    FOneOut o;
+    for (int j = 0; j < 9; ++j) o.F[j] = 0;
+    for (int j = 0; j < 8; ++j) o.idx[j] = -1;
+    o.status = f_hypothesis(pts4, N, seed, (uint64_t)hyp, o.F, o.idx);
+    *out = o;
+}
+
+template <int K, int KIND>
+__global__ __launch_bounds__(256) void mcv_f_verify(const float4* __restrict__ pts, int N,
+                                                    const FModelD* __restrict__ models, int* __restrict__ counts,
+                                                    int hypCount, float thr2) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    const int lane = threadIdx.x & 63;
+    const int h0 = wave * K;
+    if (h0 >= hypCount) return;
+    double fm[K][9];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int hk = h0 + k;
+        valid[k] = (hk < hypCount) && (counts[hk] >= 0);
+        const FModelD m = models[valid[k] ? hk : h0];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            fm[k][j] = valid[k] ? m.f[j] : __builtin_nan("");
+            asm volatile("" : "+v"(fm[k][j]));   // VGPR operands: no constant-bus moves in the fp64 FMAs
+        }
+    }
+    uint32_t cnt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt[k] = 0;
+    const int nFull = N & ~63;
+    for (int base = 0; base < nFull; base += 64) {
+        const float4 q = pts[base + lane];
+        const double x1 = q.x, y1 = q.y, x2 = q.z, y2 = q.w;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(f_error(KIND, fm[k], x1, y1, x2, y2) <= thr2));
+    }
+    if (nFull < N) {
+        const int p = nFull + lane;
+        const bool v = p < N;
+        const float4 q = pts[v ? p : 0];
+        const double x1 = q.x, y1 = q.y, x2 = q.z, y2 = q.w;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            cnt[k] += (uint32_t)__popcll(
+                __builtin_amdgcn_ballot_w64(v && f_error(KIND, fm[k], x1, y1, x2, y2) <= thr2));
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid[k]) counts[h0 + k] = (int)cnt[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void mcv_f_mask(const float4* __restrict__ pts, int N, FModelD m, float thr2,
+                                                  int kind, uint8_t* __restrict__ mask, int* __restrict__ count) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool in = false;
+    if (i < N) {
+        const float4 q = pts[i];
+        in = f_error(kind, m.f, q.x, q.y, q.z, q.w) <= thr2;
+        mask[i] = in ? 1 : 0;
+    }
+    const uint64_t b = __ballot(in);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (int)__popcll(b));
+}
+
+struct OpFAtA {   // 45: upper triangle of A^T A, rows (X2X1, X2Y1, X2, Y2X1, Y2Y1, Y2, X1, Y1, 1)
+    const float4* pts; const uint8_t* mask; double c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y;
+    __device__ void operator()(int i, double (&a)[45]) const {
+        if (mask && !mask[i]) return;
+        const float4 q = pts[i];
+        const double X1 = ((double)q.x - c1x) * s1x, Y1 = ((double)q.y - c1y) * s1y;
+        const double X2 = ((double)q.z - c2x) * s2x, Y2 = ((double)q.w - c2y) * s2y;
+        const double r[9] = {X2 * X1, X2 * Y1, X2, Y2 * X1, Y2 * Y1, Y2, X1, Y1, 1.0};
+        int o = 0;
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+#pragma unroll
+            for (int k = j; k < 9; ++k) a[o++] += r[j] * r[k];
+    }
+};
+
+void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+                       int* d_counts, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_f_generate, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, seed, hypBegin,
+                       hypCount, (FModelD*)d_models, d_counts);
+}
+
+void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_f_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out);
+}
+
+void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
+                     int kind, hipStream_t s) {
+    constexpr int K = kVerifyFHypPerWave;
+    const int blocks = ((hypCount + K - 1) / K + 3) / 4;
+    const float4* p = (const float4*)d_pts4;
+    const FModelD* m = (const FModelD*)d_models;
+    switch (kind) {
+        case 0: hipLaunchKernelGGL((mcv_f_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2); break;
+        case 1: hipLaunchKernelGGL((mcv_f_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2); break;
+        case 2: hipLaunchKernelGGL((mcv_f_verify<K, 2>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2); break;
+        default: hipLaunchKernelGGL((mcv_f_verify<K, 3>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2); break;
+    }
+}
+
+void launch_f_mask(const float* d_pts4, int N, const double* F9, float thr2, int kind, uint8_t* d_mask, int* d_count,
+                   hipStream_t s) {
+    FModelD m;
+    for (int j = 0; j < 9; ++j) m.f[j] = F9[j];
+    hipLaunchKernelGGL(mcv_f_mask, dim3((N + 255) / 256), dim3(256), 0, s, (const float4*)d_pts4, N, m, thr2, kind,
+                       d_mask, d_count);
+}
+
+void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,
+                  double* d_part, double* d_out, hipStream_t s) {
+    // c4 = {c2x, c2y, c1x, c1y} and s4 likewise (OpSums / OpAbsDev order: dst first)
+    OpFAtA op{(const float4*)d_pts4, d_mask, c4[2], c4[3], s4[2], s4[3], c4[0], c4[1], s4[0], s4[1]};
+    run_reduce<45>(N, op, d_part, d_out, s);
+}
+
+}  // namespace mcv

@@ -1,0 +1,78 @@
+// ransac_f_host.cpp — host side of cvFindFundamentalMat (new export; OpenCV 4.x
+// cv::findFundamentalMat(points1, points2, FM_RANSAC / FM_8POINT, thr, conf, maxIters, mask)
+// semantics, restated [ext]): the RANSAC result is the best hypothesis' model (OpenCV does not
+// refit F on the inliers); FM_8POINT (method 0 here) fits all points.
+#include "minicv_native.h"
+#include "mcv_runtime.h"
+#include "kernels.h"
+#include "linalg.h"
+#include "hyp_fundamental.h"
+#include "plan.h"
+
+#include <cmath>
+#include <cfloat>
+#include <cstring>
+
+namespace mcv {
+
+int f_error_kind(const RansacConfig& cfg) {
+    const int e = cfg.errorKind == MCV_FERR_EPIPOLAR ? 1 : 0;
+    return e * 2 + ((cfg.flags & MCV_FLAG_UNFUSED_ERROR) ? 1 : 0);
+}
+
+int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* F, uint8_t* d_mask,
+               hipStream_t s) {
+    const double t = effective_threshold(cfg);
+    const float thr2 = (float)(t * t);
+    FOneOut* d_one = (FOneOut*)P.one.p;
+    launch_f_one(d_pts, N, cfg.seed, hyp, d_one, s);
+    MCV_HIP(hipGetLastError());
+    FOneOut one;
+    MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(FOneOut), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    std::memcpy(&one, P.h_one.p, sizeof(FOneOut));
+    if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
+    MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
+    launch_f_mask(d_pts, N, one.F, thr2, f_error_kind(cfg), d_mask, P.count.p, s);
+    MCV_HIP(hipGetLastError());
+    MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < 9; ++k) F[k] = one.F[k];
+    return P.h_i.p[0];
+}
+
+// run8Point over all correspondences: GPU fp64 sums (centroids, mean |dev|, A^T A), then the 9x9
+// Jacobi eigen-solve, rank 2 and de-normalisation here. Returns N, or 0 if degenerate.
+int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F) {
+    double sums[5];
+    reduce_to_host(P, s, 5, sums, [&](double* part, double* red) { h_reduce_sums(d_pts, N, nullptr, part, red, s); });
+    const double n = sums[4];
+    double c4[4] = {sums[0] / n, sums[1] / n, sums[2] / n, sums[3] / n};   // c2x, c2y, c1x, c1y
+    double dev[4];
+    reduce_to_host(P, s, 4, dev, [&](double* part, double* red) { h_reduce_absdev(d_pts, N, nullptr, c4, part, red, s); });
+    for (int k = 0; k < 4; ++k)
+        if (std::fabs(dev[k]) < DBL_EPSILON) return 0;
+    double s4[4] = {n / dev[0], n / dev[1], n / dev[2], n / dev[3]};
+    double ata[45];
+    reduce_to_host(P, s, 45, ata, [&](double* part, double* red) { f_reduce_ata(d_pts, N, nullptr, c4, s4, part, red, s); });
+    double A[81], w[9], V[81];
+    int o = 0;
+    for (int j = 0; j < 9; ++j)
+        for (int k = j; k < 9; ++k) { A[j * 9 + k] = ata[o]; A[k * 9 + j] = ata[o]; ++o; }
+    jacobi_eigen(A, 9, w, V);
+    double F0[9];
+    for (int k = 0; k < 9; ++k) F0[k] = V[8 * 9 + k];
+    f_rank2(F0);
+    if (!f_denormalize(F0, c4[2], c4[3], s4[2], s4[3], c4[0], c4[1], s4[0], s4[1], F)) return 0;
+    return N;
+}
+
+int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F9, float* Ff9, int* sampleIdx) {
+    if (N < 8) fail("N < 8");
+    for (int k = 0; k < 9; ++k) F9[k] = 0;
+    const int st = f_hypothesis(pts4, N, seed, (uint64_t)hyp, F9, sampleIdx);
+    for (int k = 0; k < 9; ++k) Ff9[k] = (float)F9[k];
+    return st;
+}
+
+}  // namespace mcv

@@ -138,16 +138,6 @@ void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst,
 double effective_threshold(const RansacConfig& cfg) { return cfg.threshold > 0 ? cfg.threshold : 3.0; }
 bool fused_error(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_UNFUSED_ERROR) == 0; }
 
-// Sum V doubles over (masked) correspondences: GPU two-stage reduction, result to host.
-template <class F>
-static void reduce_to_host(Plan& P, hipStream_t s, int V, double* out, F launch) {
-    launch(P.part.p, P.red.p);
-    MCV_HIP(hipGetLastError());
-    MCV_HIP(hipMemcpyAsync(P.h_red.p, P.red.p, V * sizeof(double), hipMemcpyDeviceToHost, s));
-    MCV_HIP(hipStreamSynchronize(s));
-    std::memcpy(out, P.h_red.p, V * sizeof(double));
-}
-
 // HomographyEstimatorCallback::runKernel over the masked correspondences (mask == NULL: all).
 bool h_refit(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipStream_t s, double* H) {
     double sums[5];
@@ -263,7 +253,9 @@ void evaluate_chunk(Plan& P, const float* d_pts, int N, const RansacConfig& cfg,
         ProfScope ps("h_verify", s);
         launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, fused_error(cfg), P.bbox.p, s);
     } else {
-        f_evaluate_chunk(P, d_pts, N, cfg, hypBegin, hypCount, d_counts, s);
+        launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+        ProfScope ps("f_verify", s);
+        launch_f_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, f_error_kind(cfg), s);
     }
     if (d_key) launch_best(d_counts, hypCount, hypBegin, model_points(P.model), P.pkey.p, P.pfail.p, d_key, s);
     MCV_HIP(hipGetLastError());

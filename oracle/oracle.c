@@ -515,6 +515,263 @@ int orc_find_homography(const double* src, const double* dst, int N, double thr,
 }
 
 /* ------------------------------------------------------------------------------------------
+ * Fundamental matrix, 8-point minimal sets (north_star). OpenCV 4.x run8Point / FMEstimatorCallback
+ * and EMEstimatorCallback::computeError (Sampson) [ext]; same definition as
+ * minicv_amd/csrc/hyp_fundamental.h (mean-|dev| normalisation, f22 = 1 elimination, rank 2 by
+ * F (I - v v^T) with v from a cyclic 3x3 Jacobi of F^T F).
+ * ---------------------------------------------------------------------------------------- */
+static void jacobi3_orc(double* A, double* V) {
+    for (int i = 0; i < 9; ++i) V[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
+    static const int P[3] = {0, 0, 1}, Q[3] = {1, 2, 2};
+    for (int sweep = 0; sweep < 16; ++sweep) {
+        double off = A[1] * A[1] + A[2] * A[2] + A[5] * A[5];
+        double dg = A[0] * A[0] + A[4] * A[4] + A[8] * A[8];
+        if (!(off > dg * 1e-32)) break;
+        for (int r = 0; r < 3; ++r) {
+            int p = P[r], q = Q[r];
+            double apq = A[3 * p + q];
+            if (apq == 0) continue;
+            double theta = (A[3 * q + q] - A[3 * p + p]) / (2 * apq);
+            double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+            double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+            for (int k = 0; k < 3; ++k) {
+                double x = A[3 * k + p], y = A[3 * k + q];
+                A[3 * k + p] = c * x - s * y; A[3 * k + q] = s * x + c * y;
+            }
+            for (int k = 0; k < 3; ++k) {
+                double x = A[3 * p + k], y = A[3 * q + k];
+                A[3 * p + k] = c * x - s * y; A[3 * q + k] = s * x + c * y;
+            }
+            for (int k = 0; k < 3; ++k) {
+                double x = V[3 * k + p], y = V[3 * k + q];
+                V[3 * k + p] = c * x - s * y; V[3 * k + q] = s * x + c * y;
+            }
+        }
+    }
+}
+
+static void f_rank2_orc(double* F) {
+    double M[9], V[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) M[3 * i + j] = F[i] * F[j] + F[3 + i] * F[3 + j] + F[6 + i] * F[6 + j];
+    jacobi3_orc(M, V);
+    int m = 0;
+    double dmin = M[0];
+    if (M[4] < dmin) { m = 1; dmin = M[4]; }
+    if (M[8] < dmin) m = 2;
+    double v0 = V[m], v1 = V[3 + m], v2 = V[6 + m];
+    for (int i = 0; i < 3; ++i) {
+        double w = F[3 * i] * v0 + F[3 * i + 1] * v1 + F[3 * i + 2] * v2;
+        F[3 * i] = F[3 * i] - w * v0;
+        F[3 * i + 1] = F[3 * i + 1] - w * v1;
+        F[3 * i + 2] = F[3 * i + 2] - w * v2;
+    }
+}
+
+static int f_denorm_orc(const double* F0, double c1x, double c1y, double s1x, double s1y, double c2x, double c2y,
+                        double s2x, double s2y, double* F) {
+    double T1[9] = {s1x, 0, -s1x * c1x, 0, s1y, -s1y * c1y, 0, 0, 1};
+    double T2t[9] = {s2x, 0, 0, 0, s2y, 0, -s2x * c2x, -s2y * c2y, 1};
+    double T[9];
+    mul33(T2t, F0, T);
+    mul33(T, T1, F);
+    if (fabs(F[8]) > (double)FLT_EPSILON) {
+        double s = 1. / F[8];
+        for (int i = 0; i < 9; ++i) F[i] = F[i] * s;
+    }
+    for (int i = 0; i < 9; ++i)
+        if (!isfinite(F[i])) return 0;
+    return 1;
+}
+
+static int f_norm8(const float* x, const float* y, int m, double* cx, double* cy, double* sx, double* sy) {
+    double mx = 0, my = 0, ax = 0, ay = 0;
+    for (int i = 0; i < m; ++i) { mx += x[i]; my += y[i]; }
+    mx /= m; my /= m;
+    for (int i = 0; i < m; ++i) { ax += fabs(x[i] - mx); ay += fabs(y[i] - my); }
+    if (fabs(ax) < DBL_EPSILON || fabs(ay) < DBL_EPSILON) return 0;
+    *cx = mx; *cy = my; *sx = m / ax; *sy = m / ay;
+    return 1;
+}
+
+static int f_solve8_orc(const float* x1, const float* y1, const float* x2, const float* y2, double* F) {
+    double c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y;
+    if (!f_norm8(x1, y1, 8, &c1x, &c1y, &s1x, &s1y) || !f_norm8(x2, y2, 8, &c2x, &c2y, &s2x, &s2y)) return 0;
+    double a[8][9];
+    for (int i = 0; i < 8; ++i) {
+        double X1 = (x1[i] - c1x) * s1x, Y1 = (y1[i] - c1y) * s1y, X2 = (x2[i] - c2x) * s2x, Y2 = (y2[i] - c2y) * s2y;
+        double r[9] = {X2 * X1, X2 * Y1, X2, Y2 * X1, Y2 * Y1, Y2, X1, Y1, -1.0};
+        memcpy(a[i], r, sizeof(r));
+    }
+    for (int c = 0; c < 8; ++c) {
+        int p = c;
+        double best = fabs(a[c][c]);
+        for (int r = c + 1; r < 8; ++r)
+            if (fabs(a[r][c]) > best) { best = fabs(a[r][c]); p = r; }
+        if (!(best > 0)) return 0;
+        if (p != c)
+            for (int k = c; k < 9; ++k) { double t = a[c][k]; a[c][k] = a[p][k]; a[p][k] = t; }
+        for (int r = c + 1; r < 8; ++r) {
+            double f = a[r][c] / a[c][c];
+            for (int k = c + 1; k < 9; ++k) a[r][k] = a[r][k] - f * a[c][k];
+        }
+    }
+    double h[8];
+    for (int i = 7; i >= 0; --i) {
+        double s = a[i][8];
+        for (int k = i + 1; k < 8; ++k) s = s - a[i][k] * h[k];
+        h[i] = s / a[i][i];
+    }
+    double F0[9] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], 1.0};
+    f_rank2_orc(F0);
+    return f_denorm_orc(F0, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
+}
+
+int orc_f_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F, int* idx_out) {
+    Stream st;
+    st.seed = seed; st.hyp = (uint64_t)hyp; st.pos = 0;
+    int idx[8];
+    float x1[8], y1[8], x2[8], y2[8];
+    for (int attempt = 0; attempt < ORC_MAX_ATTEMPTS; ++attempt) {
+        if (!draw_distinct(&st, N, 8, idx)) continue;
+        for (int i = 0; i < 8; ++i) {
+            const float* p = pts4 + 4 * (size_t)idx[i];
+            x1[i] = p[0]; y1[i] = p[1]; x2[i] = p[2]; y2[i] = p[3];
+        }
+        if (collinear_last(x1, y1, 8) || collinear_last(x2, y2, 8)) continue;
+        if (idx_out) memcpy(idx_out, idx, sizeof(idx));
+        return f_solve8_orc(x1, y1, x2, y2, F) ? 1 : ORC_NO_MODEL;
+    }
+    return ORC_NO_SAMPLE;
+}
+
+/* kind = errorKind * 2 + unfused: 0 Sampson fused, 1 Sampson op-by-op, 2 epipolar fused, 3 epipolar. */
+static float f_err_orc(int kind, const double* F, double x1, double y1, double x2, double y2) {
+    if (kind == 0) {
+        double ax = fma(F[0], x1, fma(F[1], y1, F[2])), ay = fma(F[3], x1, fma(F[4], y1, F[5]));
+        double az = fma(F[6], x1, fma(F[7], y1, F[8]));
+        double bx = fma(F[0], x2, fma(F[3], y2, F[6])), by = fma(F[1], x2, fma(F[4], y2, F[7]));
+        double c = fma(x2, ax, fma(y2, ay, az));
+        double den = fma(ax, ax, fma(ay, ay, fma(bx, bx, by * by)));
+        return (float)(c * c / den);
+    }
+    if (kind == 1) {
+        double ax = F[0] * x1 + F[1] * y1 + F[2] * 1., ay = F[3] * x1 + F[4] * y1 + F[5] * 1.;
+        double az = F[6] * x1 + F[7] * y1 + F[8] * 1.;
+        double bx = F[0] * x2 + F[3] * y2 + F[6] * 1., by = F[1] * x2 + F[4] * y2 + F[7] * 1.;
+        double c = x2 * ax + y2 * ay + 1. * az;
+        double a2 = ax * ax, b2 = ay * ay, c2 = bx * bx, d2 = by * by;
+        return (float)(c * c / (a2 + b2 + c2 + d2));
+    }
+    double a, b, c, s1, s2, d1, d2;
+    if (kind == 2) {
+        a = fma(F[0], x1, fma(F[1], y1, F[2])); b = fma(F[3], x1, fma(F[4], y1, F[5]));
+        c = fma(F[6], x1, fma(F[7], y1, F[8]));
+        s2 = 1. / fma(a, a, b * b); d2 = fma(x2, a, fma(y2, b, c));
+        a = fma(F[0], x2, fma(F[3], y2, F[6])); b = fma(F[1], x2, fma(F[4], y2, F[7]));
+        c = fma(F[2], x2, fma(F[5], y2, F[8]));
+        s1 = 1. / fma(a, a, b * b); d1 = fma(x1, a, fma(y1, b, c));
+    } else {
+        a = F[0] * x1 + F[1] * y1 + F[2]; b = F[3] * x1 + F[4] * y1 + F[5]; c = F[6] * x1 + F[7] * y1 + F[8];
+        s2 = 1. / (a * a + b * b); d2 = x2 * a + y2 * b + c;
+        a = F[0] * x2 + F[3] * y2 + F[6]; b = F[1] * x2 + F[4] * y2 + F[7]; c = F[2] * x2 + F[5] * y2 + F[8];
+        s1 = 1. / (a * a + b * b); d1 = x1 * a + y1 * b + c;
+    }
+    double e1 = d1 * d1 * s1, e2 = d2 * d2 * s2;
+    return (float)(e1 < e2 ? e2 : e1);
+}
+
+int orc_f_count(const float* pts4, int N, const double* F, float thr2, int kind, uint8_t* mask) {
+    int n = 0;
+    for (int i = 0; i < N; ++i) {
+        const float* p = pts4 + 4 * (size_t)i;
+        int in = f_err_orc(kind, F, p[0], p[1], p[2], p[3]) <= thr2;
+        if (mask) mask[i] = (uint8_t)in;
+        n += in;
+    }
+    return n;
+}
+
+void orc_f_counts(const float* pts4, int N, uint64_t seed, int64_t hypBegin, int64_t hypCount, float thr2, int kind,
+                  int* counts, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+    for (int64_t i = 0; i < hypCount; ++i) {
+        double F[9];
+        int st = orc_f_hypothesis(pts4, N, seed, hypBegin + i, F, NULL);
+        counts[i] = st == 1 ? orc_f_count(pts4, N, F, thr2, kind, NULL) : st;
+    }
+}
+
+/* run8Point over all points (FM_8POINT / method 0): same normalisation, 9x9 Jacobi, rank 2. */
+static int f_fit_all_orc(const float* pts4, int N, double* F) {
+    double c1x = 0, c1y = 0, c2x = 0, c2y = 0, a1x = 0, a1y = 0, a2x = 0, a2y = 0;
+    for (int i = 0; i < N; ++i) { c1x += pts4[4 * i]; c1y += pts4[4 * i + 1]; c2x += pts4[4 * i + 2]; c2y += pts4[4 * i + 3]; }
+    c1x /= N; c1y /= N; c2x /= N; c2y /= N;
+    for (int i = 0; i < N; ++i) {
+        a1x += fabs(pts4[4 * i] - c1x); a1y += fabs(pts4[4 * i + 1] - c1y);
+        a2x += fabs(pts4[4 * i + 2] - c2x); a2y += fabs(pts4[4 * i + 3] - c2y);
+    }
+    if (a1x < DBL_EPSILON || a1y < DBL_EPSILON || a2x < DBL_EPSILON || a2y < DBL_EPSILON) return 0;
+    double s1x = N / a1x, s1y = N / a1y, s2x = N / a2x, s2y = N / a2y;
+    double A[81] = {0};
+    for (int i = 0; i < N; ++i) {
+        double X1 = (pts4[4 * i] - c1x) * s1x, Y1 = (pts4[4 * i + 1] - c1y) * s1y;
+        double X2 = (pts4[4 * i + 2] - c2x) * s2x, Y2 = (pts4[4 * i + 3] - c2y) * s2y;
+        double r[9] = {X2 * X1, X2 * Y1, X2, Y2 * X1, Y2 * Y1, Y2, X1, Y1, 1.0};
+        for (int j = 0; j < 9; ++j)
+            for (int k = j; k < 9; ++k) A[j * 9 + k] += r[j] * r[k];
+    }
+    for (int j = 0; j < 9; ++j)
+        for (int k = 0; k < j; ++k) A[j * 9 + k] = A[k * 9 + j];
+    double w[9], V[81], F0[9];
+    jacobi(A, 9, w, V);
+    memcpy(F0, V + 72, sizeof(F0));
+    f_rank2_orc(F0);
+    return f_denorm_orc(F0, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
+}
+
+/* cv::findFundamentalMat(a, b, FM_RANSAC (8-point kernel) | FM_8POINT, thr, conf, maxIters, mask). */
+int orc_find_fundamental(const double* a, const double* b, int N, double thr, double conf, int maxIters, int method,
+                         uint64_t seed, int flags, int errorKind, double* F, uint8_t* mask, int64_t* bestHypOut,
+                         int nthreads) {
+    if (mask) memset(mask, 0, (size_t)(N > 0 ? N : 0));
+    if (bestHypOut) *bestHypOut = -1;
+    if (N < 8) return 0;
+    if (thr <= 0) thr = 3;
+    float* pts = (float*)malloc(sizeof(float) * 4 * (size_t)N);
+    for (int i = 0; i < N; ++i) {
+        pts[4 * i] = (float)a[2 * i]; pts[4 * i + 1] = (float)a[2 * i + 1];
+        pts[4 * i + 2] = (float)b[2 * i]; pts[4 * i + 3] = (float)b[2 * i + 1];
+    }
+    int count = 0;
+    if (method == 0 || N == 8) {
+        if (f_fit_all_orc(pts, N, F)) {
+            count = N;
+            if (mask) memset(mask, 1, (size_t)N);
+        }
+    } else {
+        const float thr2 = (float)(thr * thr);
+        const int kind = (errorKind == 1 ? 2 : 0) + ((flags & ORC_FLAG_UNFUSED_ERROR) ? 1 : 0);
+        int64_t niters = maxIters > 1 ? maxIters : 1;
+        int* cnts = (int*)malloc(sizeof(int) * (size_t)niters);
+        orc_f_counts(pts, N, seed, 0, niters, thr2, kind, cnts, nthreads);
+        int bc = 0;
+        int64_t best = orc_ransac_replay(cnts, niters, N, 8, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0, &bc);
+        free(cnts);
+        if (best >= 0) {
+            orc_f_hypothesis(pts, N, seed, best, F, NULL);
+            count = orc_f_count(pts, N, F, thr2, kind, mask);
+            if (bestHypOut) *bestHypOut = best;
+        }
+    }
+    free(pts);
+    return count;
+}
+
+/* ------------------------------------------------------------------------------------------
  * Brute-force matchers (BFMatcher NORM_HAMMING / NORM_L2, knn k = 2) [ext: OpenCV features2d].
  * Ties: the lower train index wins (strict comparison while scanning trains in order).
  * ---------------------------------------------------------------------------------------- */

@@ -24,8 +24,11 @@ _SIGS = {
     "orc_match_hamming": (None, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I]),
     "orc_match_l2": (None, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I]),
     "orc_max_threads": (_I, []),
+    "orc_f_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P]),
+    "orc_f_count": (_I, [_P, _I, _P, _F, _I, _P]),
+    "orc_f_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _I, _P, _I]),
+    "orc_find_fundamental": (_I, [_P, _P, _I, _D, _D, _I, _I, _U64, _I, _I, _P, _P, _P, _I]),
 }
-_OPTIONAL = {"orc_f_hypothesis", "orc_f_count", "orc_f_counts", "orc_find_fundamental"}
 
 _lib = None
 
@@ -117,3 +120,39 @@ def match_l2(q, t, nthreads=0):
     d1, d2 = np.zeros(nq), np.zeros(nq)
     load().orc_match_l2(ptr(q), nq, ptr(t), t.shape[0], q.shape[1], ptr(i1), ptr(d1), ptr(i2), ptr(d2), nthreads)
     return i1, d1, i2, d2
+
+
+def f_hypothesis(pts4: np.ndarray, seed: int, hyp: int):
+    F = np.zeros(9)
+    idx = np.full(8, -1, dtype=np.int32)
+    st = load().orc_f_hypothesis(ptr(pts4), pts4.shape[0], seed, hyp, ptr(F), ptr(idx))
+    return st, F, idx
+
+
+def f_kind(error_kind: int = 0, unfused: bool = False) -> int:
+    return (2 if error_kind == 1 else 0) + (1 if unfused else 0)
+
+
+def f_count(pts4, F, thr2, kind=0, want_mask=False):
+    F = np.ascontiguousarray(F, dtype=np.float64).ravel()
+    m = np.zeros(pts4.shape[0], dtype=np.uint8) if want_mask else None
+    n = load().orc_f_count(ptr(pts4), pts4.shape[0], ptr(F), thr2, kind, ptr(m) if want_mask else None)
+    return (n, m) if want_mask else n
+
+
+def f_counts(pts4, seed, begin, count, thr2, kind=0, nthreads=0):
+    out = np.zeros(count, dtype=np.int32)
+    load().orc_f_counts(ptr(pts4), pts4.shape[0], seed, begin, count, thr2, kind, ptr(out), nthreads)
+    return out
+
+
+def find_fundamental(a, b, thr=3.0, conf=0.99, max_iters=1000, method=8, seed=0, flags=0, error_kind=0, nthreads=0):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    n = a.shape[0]
+    F = np.zeros(9)
+    mask = np.zeros(max(n, 1), dtype=np.uint8)
+    best = np.zeros(1, dtype=np.int64)
+    cnt = load().orc_find_fundamental(ptr(a), ptr(b), n, thr, conf, max_iters, method, seed, flags, error_kind,
+                                      ptr(F), ptr(mask), ptr(best), nthreads)
+    return cnt, F.reshape(3, 3), mask[:n], int(best[0])

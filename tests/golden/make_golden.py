@@ -50,7 +50,16 @@ def matchers():
                         lq=lq, lt=lt, l_idx=l[0], l_dist=l[1], l_idx2=l[2], l_dist2=l[3])
 
 
+def fundamental():
+    a, b, _, _ = S.fundamental_problem(500, 4)
+    thr, conf, iters, seed = 5e-3, 0.99, 1000, 4
+    cnt, F, mask, best = O.find_fundamental(a, b, thr=thr, conf=conf, max_iters=iters, seed=seed)
+    np.savez_compressed(OUT / "fundamental.npz", a=a, b=b, thr=thr, conf=conf, max_iters=iters, seed=seed,
+                        count=cnt, F=F, mask=mask, best_hyp=best)
+
+
 if __name__ == "__main__":
+    fundamental()
     cfg1()
     hypotheses()
     matchers()

@@ -147,3 +147,21 @@ def test_replay_chunks_match_oracle(native, oracle):
         assert st.bestIndex == best
         if best >= 0:
             assert st.bestCount == bc
+
+
+@pytest.mark.parametrize("n,outliers,seed", [(8, 0.0, 1), (9, 0.3, 2), (500, 0.5, 3), (5000, 0.7, 4)])
+def test_host_f_hypothesis_bit_exact_vs_oracle(native, oracle, n, outliers, seed):
+    a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=outliers)
+    pts4 = oracle.pack4(a, b)
+    L = native.lib()
+    F = np.zeros(9)
+    Ff = np.zeros(9, np.float32)
+    idx = np.full(8, -1, np.int32)
+    for hyp in list(range(200)) + [2**32 - 7]:
+        st = L.mcvHostHypothesis(1, pts4.ctypes.data, n, seed * 31, hyp, F.ctypes.data, Ff.ctypes.data,
+                                 idx.ctypes.data)
+        st2, F2, idx2 = oracle.f_hypothesis(pts4, seed * 31, hyp)
+        assert st == st2
+        if st == 1:
+            np.testing.assert_array_equal(F, F2)
+            np.testing.assert_array_equal(idx, idx2)

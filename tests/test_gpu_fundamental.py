@@ -1,0 +1,100 @@
+"""GPU parity of the fundamental-matrix RANSAC path (8-point minimal sets) against the oracle.
+Bar: per-hypothesis inlier counts and masks bit-exact for all four error definitions; the returned
+F (best hypothesis' fp64 model, no refit — as OpenCV's findFundamentalMat) bit-identical; the
+all-points 8-point fit within 1e-6 relative Frobenius (GPU fp64 sums in another order)."""
+import numpy as np
+import pytest
+
+from minicv_amd import native as N
+from minicv_amd import opencv, synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def relf_up_to_sign(A, B):
+    A = A / np.linalg.norm(A)
+    B = B / np.linalg.norm(B)
+    return min(np.linalg.norm(A - B), np.linalg.norm(A + B))
+
+
+@pytest.fixture(scope="module")
+def torch_dev(gpu):
+    import torch
+    return torch, torch.device("cuda:0")
+
+
+@pytest.mark.parametrize("n,outl,seed,begin,count,error_kind,unfused", [
+    (8, 0.0, 1, 0, 64, 0, False), (9, 0.3, 2, 0, 200, 0, False), (300, 0.5, 3, 0, 1024, 0, False),
+    (2000, 0.5, 4, 77777, 1024, 0, False), (1999, 0.5, 5, 0, 512, 0, True), (1000, 0.6, 6, 0, 512, 1, False),
+    (1000, 0.6, 7, 2**31, 512, 1, True), (65, 0.2, 8, 0, 300, 1, False)])
+def test_f_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, error_kind, unfused):
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=outl)
+    pts = D.pack_points_tensor(a, b, dev)
+    plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, n, count)
+    thr = 5e-3
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, error_kind=error_kind, unfused_error=unfused).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(count, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, begin, count, key, counts)
+    got = counts.cpu().numpy()
+    ref = oracle.f_counts(oracle.pack4(a, b), seed, begin, count, float(np.float32(thr * thr)),
+                          oracle.f_kind(error_kind, unfused))
+    np.testing.assert_array_equal(got, ref)
+    valid = ref >= 8
+    k = int(key[0].item())
+    if valid.any() and not (ref == -2).any():
+        c = ref.max()
+        i = int(np.nonzero(ref == c)[0][0])
+        assert k == (int(c) << 32) | (0xFFFFFFFF - (begin + i))
+    plan.close()
+
+
+@pytest.mark.parametrize("n,outl,seed,iters,conf,error_kind,flags", [
+    (8, 0.0, 1, 1000, 0.99, 0, 0), (50, 0.3, 2, 1000, 0.99, 0, 0), (500, 0.5, 4, 1000, 0.99, 0, 0),
+    (3000, 0.5, 5, 2000, 0.99, 0, 0), (3000, 0.5, 6, 2000, 0.99, 1, 0),
+    (2000, 0.5, 7, 500, 0.99, 0, N.FLAG_FIXED_ITERS), (2000, 0.5, 8, 1000, 0.999, 1, N.FLAG_UNFUSED_ERROR)])
+def test_find_fundamental_vs_oracle(gpu, oracle, n, outl, seed, iters, conf, error_kind, flags):
+    a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=outl)
+    thr = 5e-3
+    cnt_o, F_o, mask_o, _ = oracle.find_fundamental(a, b, thr=thr, conf=conf, max_iters=iters, seed=seed,
+                                                    flags=flags, error_kind=error_kind)
+    p = opencv.RansacParams(threshold=thr, confidence=conf, max_iters=iters, seed=seed, error_kind=error_kind,
+                            fixed_iters=bool(flags & N.FLAG_FIXED_ITERS),
+                            unfused_error=bool(flags & N.FLAG_UNFUSED_ERROR))
+    cnt, F, mask = opencv.findFundamentalMat(a, b, p)
+    assert cnt == cnt_o
+    np.testing.assert_array_equal(mask, mask_o.astype(bool))
+    if n == 8:
+        assert relf_up_to_sign(F, F_o) < 1e-6   # all-points fit path
+    else:
+        np.testing.assert_array_equal(F, F_o)
+
+
+def test_fundamental_lsq(gpu, oracle):
+    a, b, inl, Ft = S.fundamental_problem(4000, 9, outlier_frac=0.0)
+    cnt_o, F_o, _, _ = oracle.find_fundamental(a, b, method=0)
+    cnt, F, mask = opencv.findFundamentalMat(a, b, opencv.RansacParams(method=N.METHOD_LSQ))
+    assert cnt == cnt_o == 4000 and mask.all()
+    assert relf_up_to_sign(F, F_o) < 1e-6
+
+
+def test_fundamental_golden(gpu):
+    from pathlib import Path
+    g = np.load(Path(__file__).resolve().parent / "golden" / "fundamental.npz")
+    p = opencv.RansacParams(threshold=float(g["thr"]), confidence=float(g["conf"]), max_iters=int(g["max_iters"]),
+                            seed=int(g["seed"]))
+    cnt, F, mask = opencv.findFundamentalMat(g["a"], g["b"], p)
+    assert cnt == int(g["count"])
+    np.testing.assert_array_equal(mask, g["mask"].astype(bool))
+    np.testing.assert_array_equal(F, g["F"])
+
+
+def test_fundamental_degenerate(gpu):
+    x = np.linspace(-1, 1, 40)
+    a = np.stack([x, 0.5 * x], axis=1)
+    with pytest.raises(N.NativeError):
+        opencv.findFundamentalMat(a, a.copy(), opencv.RansacParams(threshold=0.01))
+    with pytest.raises(N.NativeError):
+        opencv.findFundamentalMat(a[:7], a[:7])
