@@ -13,6 +13,7 @@
 //   * a merge kernel folds the S partial top-2s per query.
 #include "kernels.h"
 #include "mcv_runtime.h"
+#include "plan.h"
 #include <climits>
 
 namespace mcv {
@@ -134,6 +135,7 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     const int chunkLen = nt > 0 ? (nt + nchunks - 1) / nchunks : 0;
     wk.part.ensure((size_t)nchunks * nq);
     dim3 grid((qwaves + 3) / 4, nchunks);
+    ProfScope ps("hamming", s);
     if (W == 8)
         hipLaunchKernelGGL((mcv_hamming_partial<8>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
     else
