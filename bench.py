@@ -28,6 +28,9 @@ sys.path.insert(0, str(ROOT))
 
 N_CORR = 100_000
 HYPS_PER_GPU = 1 << 20
+F_N_CORR = 500_000            # BASELINE config[3]: findFundamentalMat 8-pt, 500k correspondences
+F_HYPS_TOTAL = 1 << 16        # hypotheses per call, sharded over the ranks (strong scaling)
+F_SEED = 4
 THR = 5e-3
 SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -35,6 +38,10 @@ HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # correspondence) evaluation, v_rcp_f32 at quarter rate -> 18 issue slots of 2 cycles (wave64 on
 # SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x 2.4 GHz / 2 x 64 lanes / 18.
 VALU_SLOTS_PER_EVAL = 18
+F_FLOPS_PER_EVAL = 26          # fp64 Sampson (fused): 11 FMA + 2 mul + 1 div per (hypothesis, point)
+FP64_PEAK_TF = 78.6            # MI355X fp64 vector (spec)
+FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: fp32-input MFMA = fp32 vector peak
+HAMMING_PEAK_PAIRS = 256 * 4 * 2.4e9 / 2 * 64 / 20   # 20 VALU instructions per pair
 VALU_PEAK_EVALS = 256 * 4 * 2.4e9 / 2 * 64 / VALU_SLOTS_PER_EVAL
 
 
@@ -47,6 +54,8 @@ def parse():
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="homography", choices=["homography", "fundamental", "hamming", "l2"],
+                    help="homography = the headline (BASELINE config[2]); the others are config[1], [3], [4]")
     return ap.parse_args()
 
 
@@ -70,6 +79,130 @@ def cpu_baseline(src, dst, target_s: float):
                       f"oracle/oracle.c, OpenMP {threads} threads, {el:.1f} s"}
 
 
+def cpu_baseline_f(a, b, target_s: float):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import numpy as np
+    import _oracle as O
+    pts4 = O.pack4(a, b)
+    thr2 = float(np.float32(THR * THR))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    t = time.perf_counter()
+    O.f_counts(pts4, F_SEED, 0, 2 * threads, thr2, 0, threads)
+    cal = (time.perf_counter() - t) / (2 * threads)
+    sample = max(2 * threads, int(target_s / max(cal, 1e-6)))
+    t = time.perf_counter()
+    O.f_counts(pts4, F_SEED, 0, sample, thr2, 0, threads)
+    el = time.perf_counter() - t
+    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port",
+            "sample": f"{sample} hypotheses x {a.shape[0]} correspondences (8-pt sample+solve+fp64 Sampson "
+                      f"count), oracle/oracle.c, OpenMP {threads} threads, {el:.1f} s"}
+
+
+def bench_matcher(args):
+    """BASELINE config[1] (Hamming 10k x 10k x 256 bit) / config[4] (L2 SIFT-128 50k x 50k, fp32 MFMA).
+    Queries are sharded over ranks (no collective); the train set is replicated."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from minicv_amd import native as NL, synthetic as S, device as D
+    from minicv_amd import dist as MD
+    ham = args.workload == "hamming"
+    if ham:
+        nq, nt = 10_000, 10_000
+        q, t, _ = S.hamming_problem(nq, nt, seed=2)
+        qd, td = torch.from_numpy(q).to(dev), torch.from_numpy(t).to(dev)
+    else:
+        nq, nt = 50_000, 50_000
+        q, t, _ = S.l2_problem(nq, nt, dim=128, seed=5)
+        qd, td = torch.from_numpy(q).to(dev), torch.from_numpy(t).to(dev)
+    b0, cnt = MD.shard(nq, rank, world)
+    qs = qd[b0:b0 + cnt].contiguous()
+    idx = torch.empty(cnt, dtype=torch.int32, device=dev)
+    idx2 = torch.empty_like(idx)
+    dist_t = torch.empty(cnt, dtype=torch.int32 if ham else torch.float32, device=dev)
+    dist2 = torch.empty_like(dist_t)
+
+    def step():
+        (D.match_hamming if ham else D.match_l2)(qs, td, idx, dist_t, idx2, dist2)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    NL.lib().mcvProfileReset()
+    NL.lib().mcvProfileEnable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    NL.lib().mcvProfileEnable(0)
+    import ctypes as C
+    kms = C.c_double(0)
+    launches = NL.lib().mcvProfileRead(b"hamming" if ham else b"l2_mfma", C.addressof(kms))
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    if rank == 0:
+        avg_ms = kms.value / max(launches, 1)
+        if ham:
+            pairs = cnt * nt
+            ach = pairs / (avg_ms * 1e-3)
+            line = {"metric": "BF Hamming knn-2 queries/sec, 10k x 10k 256-bit (BASELINE config[1])",
+                    "value": nq * args.steps / el, "unit": "queries/s",
+                    "roofline": {"bound": "hbm", "achieved": 32.0 * pairs / (avg_ms * 1e-3) / 1e9,
+                                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                 "frac": 32.0 * pairs / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                                 "kernel": "mcv_hamming_partial", "avg_launch_ms": avg_ms,
+                                 "note": "algorithmic bytes = 32 B x Nt per query; data L2-resident, integer "
+                                         "VALU-bound (see valu)",
+                                 "valu": {"achieved": ach, "peak": HAMMING_PEAK_PAIRS, "unit": "pairs/s",
+                                          "frac": ach / HAMMING_PEAK_PAIRS,
+                                          "model": "20 VALU instructions per (query, train) pair"}},
+                    "dtype": "u32", "scaling": "strong"}
+        else:
+            flops = 2.0 * cnt * nt * 128
+            tf = flops / (avg_ms * 1e-3) / 1e12
+            line = {"metric": "BF L2 knn-2 TFLOP/s, SIFT-128 50k x 50k fp32 GEMM on MFMA (BASELINE config[4])",
+                    "value": 2.0 * nq * nt * 128 * args.steps / el / 1e12, "unit": "TFLOP/s",
+                    "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                                 "frac": tf / FP32_MFMA_PEAK_TF, "traffic": None, "kernel": "mcv_l2_mfma",
+                                 "avg_launch_ms": avg_ms},
+                    "dtype": "f32", "scaling": "strong"}
+        line.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                     "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "vs_baseline": None,
+                     "data": "synthetic (seeded, planted neighbours)",
+                     "config": {"workload": args.workload, "queries": nq, "train": nt,
+                                "parallelism": f"query-sharded dp{world}"},
+                     "cpu_baseline": None})
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, str(ROOT / "tests"))
+            import _oracle as O
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+            sq = 2000 if ham else 200
+            t1 = time.perf_counter()
+            (O.match_hamming if ham else O.match_l2)(q[:sq], t, nthreads=threads)
+            ct = time.perf_counter() - t1
+            line["cpu_baseline"] = {"value": sq / ct if ham else 2.0 * sq * nt * 128 / ct / 1e12,
+                                    "unit": "queries/s" if ham else "TFLOP/s", "cores": threads, "kind": "port",
+                                    "sample": f"{sq} queries x {nt} train, oracle/oracle.c, OpenMP {threads}"}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def load_traffic(n: int, hyps: int):
     """HBM bytes per mcv_h_verify launch from the committed rocprofv3 PMC summary, if present."""
     p = ROOT / "profiles" / "pmc_h_verify.json"
@@ -86,6 +219,12 @@ def load_traffic(n: int, hyps: int):
 
 def main():
     args = parse()
+    if args.workload in ("hamming", "l2"):
+        return bench_matcher(args)
+    return bench_ransac(args)
+
+
+def bench_ransac(args):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -105,12 +244,19 @@ def main():
     from minicv_amd import device as D
     from minicv_amd import dist as MD
 
+    fund = args.workload == "fundamental"
     n, hyps = args.n, args.hyps
-    src, dst, _ = S.homography_problem(n, SEED)
+    if fund:
+        n = args.n if args.n != N_CORR else F_N_CORR
+        hyps = args.hyps if args.hyps != HYPS_PER_GPU else F_HYPS_TOTAL // world
+        src, dst, _, _ = S.fundamental_problem(n, F_SEED)
+    else:
+        src, dst, _ = S.homography_problem(n, SEED)
     pts = D.pack_points_tensor(src, dst, dev)
-    plan = D.RansacPlan(NL.MODEL_HOMOGRAPHY, n, hyps)
+    plan = D.RansacPlan(NL.MODEL_FUNDAMENTAL if fund else NL.MODEL_HOMOGRAPHY, n, hyps)
     total = hyps * world
-    cfg = opencv.RansacParams(threshold=THR, confidence=0.995, max_iters=total, seed=SEED, fixed_iters=True).to_c()
+    cfg = opencv.RansacParams(threshold=THR, confidence=0.995, max_iters=total, seed=F_SEED if fund else SEED,
+                              fixed_iters=True).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = torch.zeros(n, dtype=torch.uint8, device=dev)
     red = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -153,7 +299,7 @@ def main():
     NL.lib().mcvProfileEnable(0)
     import ctypes as C
     kms = C.c_double(0)
-    launches = NL.lib().mcvProfileRead(b"h_verify", C.addressof(kms))
+    launches = NL.lib().mcvProfileRead(b"f_verify" if fund else b"h_verify", C.addressof(kms))
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -165,38 +311,68 @@ def main():
         alg_bytes = 16.0 * n * hyps            # per launch: every hypothesis reads all N float4 pairs
         achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
         traffic = load_traffic(n, hyps)
-        line = {
-            "metric": "RANSAC hypotheses/sec @100k corrs; achieved HBM GB/s vs roofline, 1/2/4/8 GPU",
-            "value": value,
-            "unit": "hypotheses/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": el / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (seeded cfg3 homography problem: cvTest H, 50% outliers, sigma 1e-3)",
-            "config": {"workload": f"findHomography RANSAC, {n} correspondences x {hyps} hypotheses per GPU "
-                                   f"(fixed iterations) + refit/LM, best model via RCCL all-reduce",
-                       "correspondences": n, "hypotheses_per_gpu": hyps, "threshold": THR,
-                       "parallelism": f"hypothesis-sharded dp{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "kernel": "mcv_h_verify", "avg_launch_ms": avg_ms, "launches": launches,
-                         "algorithmic_bytes_per_launch": alg_bytes,
-                         "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 8 "
-                                 "hypotheses; the sweep's binding roof is VALU issue (see valu)",
-                         "valu": {"achieved": n * hyps / (avg_ms * 1e-3), "peak": VALU_PEAK_EVALS,
-                                  "unit": "evaluations/s", "frac": n * hyps / (avg_ms * 1e-3) / VALU_PEAK_EVALS,
-                                  "model": f"{VALU_SLOTS_PER_EVAL} VALU issue slots per (hypothesis, "
-                                           "correspondence) at 2.4 GHz"}},
-            "result": {"best_count": result["count"], "best_hyp": result["idx"],
-                       "refined_count": result["final_count"]},
-        }
+        if not fund:
+            line = {
+                "metric": "RANSAC hypotheses/sec @100k corrs; achieved HBM GB/s vs roofline, 1/2/4/8 GPU",
+                "value": value,
+                "unit": "hypotheses/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": el / args.steps * 1e3,
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "f32",
+                "data": "synthetic (seeded cfg3 homography problem: cvTest H, 50% outliers, sigma 1e-3)",
+                "config": {"workload": f"findHomography RANSAC, {n} correspondences x {hyps} hypotheses per GPU "
+                                       f"(fixed iterations) + refit/LM, best model via RCCL all-reduce",
+                           "correspondences": n, "hypotheses_per_gpu": hyps, "threshold": THR,
+                           "parallelism": f"hypothesis-sharded dp{world}"},
+                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                             "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                             "kernel": "mcv_h_verify", "avg_launch_ms": avg_ms, "launches": launches,
+                             "algorithmic_bytes_per_launch": alg_bytes,
+                             "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 8 "
+                                     "hypotheses; the sweep's binding roof is VALU issue (see valu)",
+                             "valu": {"achieved": n * hyps / (avg_ms * 1e-3), "peak": VALU_PEAK_EVALS,
+                                      "unit": "evaluations/s",
+                                      "frac": n * hyps / (avg_ms * 1e-3) / VALU_PEAK_EVALS,
+                                      "model": f"{VALU_SLOTS_PER_EVAL} VALU issue slots per (hypothesis, "
+                                               "correspondence) at 2.4 GHz"}},
+                "result": {"best_count": result["count"], "best_hyp": result["idx"],
+                           "refined_count": result["final_count"]},
+            }
+        else:
+            fl = F_FLOPS_PER_EVAL * n * hyps / (avg_ms * 1e-3) / 1e12
+            line = {
+                "metric": "RANSAC hypotheses/sec, findFundamentalMat 8-pt @500k corrs (BASELINE config[3])",
+                "value": value,
+                "unit": "hypotheses/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": el / args.steps * 1e3,
+                "higher_is_better": True,
+                "scaling": "strong",
+                "vs_baseline": None,
+                "dtype": "f64",
+                "data": "synthetic (seeded two-view problem, 50% outliers, sigma 1e-3)",
+                "config": {"workload": f"findFundamentalMat 8-point RANSAC, {n} correspondences x {total} "
+                                       f"hypotheses per call sharded over {world} GPU(s), fp64 Sampson error",
+                           "correspondences": n, "hypotheses_total": total, "threshold": THR,
+                           "parallelism": f"hypothesis-sharded dp{world}"},
+                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                             "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                             "kernel": "mcv_f_verify", "avg_launch_ms": avg_ms, "launches": launches,
+                             "algorithmic_bytes_per_launch": alg_bytes,
+                             "fp64": {"achieved": fl, "peak": FP64_PEAK_TF, "unit": "TFLOP/s",
+                                      "frac": fl / FP64_PEAK_TF,
+                                      "model": f"{F_FLOPS_PER_EVAL} fp64 FLOP per (hypothesis, correspondence)"}},
+                "result": {"best_count": result["count"], "best_hyp": result["idx"]},
+            }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(src, dst, args.cpu_seconds)
+            line["cpu_baseline"] = (cpu_baseline_f if fund else cpu_baseline)(src, dst, args.cpu_seconds)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
