@@ -34,7 +34,7 @@ F_SEED = 4
 THR = 5e-3
 SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue model of mcv_h_verify (fused error): 15 VALU instructions per (hypothesis,
+# VALU issue model of mcv_h_verify<6,2> (fused error): 15 VALU instructions per (hypothesis,
 # correspondence) evaluation, v_rcp_f32 at quarter rate -> 18 issue slots of 2 cycles (wave64 on
 # SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x 2.4 GHz / 2 x 64 lanes / 18.
 VALU_SLOTS_PER_EVAL = 18
@@ -333,7 +333,7 @@ def bench_ransac(args):
                              "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                              "kernel": "mcv_h_verify", "avg_launch_ms": avg_ms, "launches": launches,
                              "algorithmic_bytes_per_launch": alg_bytes,
-                             "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 8 "
+                             "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 6 "
                                      "hypotheses; the sweep's binding roof is VALU issue (see valu)",
                              "valu": {"achieved": n * hyps / (avg_ms * 1e-3), "peak": VALU_PEAK_EVALS,
                                       "unit": "evaluations/s",

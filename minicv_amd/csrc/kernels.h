@@ -7,7 +7,9 @@
 namespace mcv {
 
 // Hypotheses per wave in the inlier sweep (models live in SGPRs: 8 per hypothesis).
-static const int kVerifyHypPerWave = 8;
+static const int kVerifyHypPerWave = 6;
+// Correspondences per lane per trip of the sweep (independent loads in flight).
+static const int kVerifyPtsPerLane = 2;
 // Upper bound of reduction partial blocks (reduce.h).
 static const int kReduceMaxBlocksHost = 1024;
 

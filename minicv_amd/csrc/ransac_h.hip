@@ -14,6 +14,7 @@
 //
 // Built with -ffp-contract=off (see hyp_homography.h): the fp32 error rounds exactly like the
 // host oracle, which is what makes the inlier masks bit-exact.
+#include <cstdlib>
 #include "mcv_common.h"
 #include "hyp_homography.h"
 #include "reduce.h"
@@ -68,62 +69,58 @@ __device__ __forceinline__ uint64_t class_mask(float w, int cls) {
     return m;
 }
 
-// One trip of the sweep: two correspondences per lane against the wave's K hypotheses.
+// One trip of the sweep: P correspondences per lane against the wave's K hypotheses.
 // PRED: lane predicates (ragged tail only). FUSED fast path: rcp_newton, with the trip redone by
 // IEEE division when any denominator is zero / denormal / non-finite.
-template <int K, bool FUSED, bool PRED>
-__device__ __forceinline__ void h_sweep_trip(const float (&hm)[K][8], const float4& qa, const float4& qb, bool va,
-                                             bool vb, float thr2, bool fast, uint32_t (&cnt)[K]) {
-    auto vote = [&](bool pa, bool pb) -> uint32_t {
+template <int K, int P, bool FUSED, bool PRED>
+__device__ __forceinline__ void h_sweep_trip(const float (&hm)[K][8], const float4 (&q)[P], const bool (&v)[P],
+                                             float thr2, bool fast, uint32_t (&cnt)[K]) {
+    auto vote = [&](int j, bool pred) -> uint32_t {
         if constexpr (PRED)
-            return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(va && pa)) +
-                   (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(vb && pb));
+            return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(v[j] && pred));
         else
-            return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(pa)) +
-                   (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(pb));
+            return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(pred));
     };
     if constexpr (FUSED) {
         if (fast) {
             uint64_t bad = 0;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                const float wa = h_denominator_fused(hm[k], qa.x, qa.y);
-                const float wb = h_denominator_fused(hm[k], qb.x, qb.y);
-                bad |= class_mask(wa, kClassNotNormal) | class_mask(wb, kClassNotNormal);
-                const float ea = h_error_fused_ww(hm[k], qa.x, qa.y, qa.z, qa.w, rcp_newton(wa));
-                const float eb = h_error_fused_ww(hm[k], qb.x, qb.y, qb.z, qb.w, rcp_newton(wb));
-                cnt[k] += vote(ea <= thr2, eb <= thr2);
+#pragma unroll
+                for (int j = 0; j < P; ++j) {
+                    const float w = h_denominator_fused(hm[k], q[j].x, q[j].y);
+                    bad |= class_mask(w, kClassNotNormal);
+                    const float e = h_error_fused_ww(hm[k], q[j].x, q[j].y, q[j].z, q[j].w, rcp_newton(w));
+                    cnt[k] += vote(j, e <= thr2);
+                }
             }
             if (__builtin_expect(bad == 0, 1)) return;
 #pragma unroll
             for (int k = 0; k < K; ++k) {   // replace this trip's fast counts by the exact ones
-                const float wa = h_denominator_fused(hm[k], qa.x, qa.y);
-                const float wb = h_denominator_fused(hm[k], qb.x, qb.y);
-                const float fa = h_error_fused_ww(hm[k], qa.x, qa.y, qa.z, qa.w, rcp_newton(wa));
-                const float fb = h_error_fused_ww(hm[k], qb.x, qb.y, qb.z, qb.w, rcp_newton(wb));
-                const float ea = h_error_fused_ww(hm[k], qa.x, qa.y, qa.z, qa.w, 1.f / wa);
-                const float eb = h_error_fused_ww(hm[k], qb.x, qb.y, qb.z, qb.w, 1.f / wb);
-                cnt[k] = cnt[k] - vote(fa <= thr2, fb <= thr2) + vote(ea <= thr2, eb <= thr2);
+#pragma unroll
+                for (int j = 0; j < P; ++j) {
+                    const float w = h_denominator_fused(hm[k], q[j].x, q[j].y);
+                    const float f = h_error_fused_ww(hm[k], q[j].x, q[j].y, q[j].z, q[j].w, rcp_newton(w));
+                    const float e = h_error_fused_ww(hm[k], q[j].x, q[j].y, q[j].z, q[j].w, 1.f / w);
+                    cnt[k] = cnt[k] - vote(j, f <= thr2) + vote(j, e <= thr2);
+                }
             }
             return;
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) {   // exact for the whole wave
-            const float ea = h_error_fused(hm[k], qa.x, qa.y, qa.z, qa.w);
-            const float eb = h_error_fused(hm[k], qb.x, qb.y, qb.z, qb.w);
-            cnt[k] += vote(ea <= thr2, eb <= thr2);
-        }
+        for (int k = 0; k < K; ++k)   // exact for the whole wave
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+                cnt[k] += vote(j, h_error_fused(hm[k], q[j].x, q[j].y, q[j].z, q[j].w) <= thr2);
     } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const float ea = h_error(hm[k], qa.x, qa.y, qa.z, qa.w);
-            const float eb = h_error(hm[k], qb.x, qb.y, qb.z, qb.w);
-            cnt[k] += vote(ea <= thr2, eb <= thr2);
-        }
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int j = 0; j < P; ++j) cnt[k] += vote(j, h_error(hm[k], q[j].x, q[j].y, q[j].z, q[j].w) <= thr2);
     }
 }
 
-template <int K, bool FUSED>
+template <int K, int P, bool FUSED>
 __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ pts, int N,
                                                     const HModelF* __restrict__ models, int* __restrict__ counts,
                                                     int hypCount, float thr2, const float* __restrict__ bbox) {
@@ -154,7 +151,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ p
 
     // Fused fast path precondition, per hypothesis: max |w| over the points' bounding box stays
     // below 2^125, so every denominator is below 2^126 (the exhaustively verified range of
-    // rcp_newton). The lower end (0, denormal, inf, NaN) is checked per point below.
+    // rcp_newton). The lower end (0, denormal, inf, NaN) is checked per point.
     bool fast = FUSED;
     if constexpr (FUSED) {
         const float X = bbox[0], Y = bbox[1];
@@ -168,20 +165,29 @@ __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ p
     }
 
     // Wave-uniform trip count (the counts are per-wave SGPR sums of ballots: every lane must take
-    // part in every ballot). Two correspondences per lane per trip: two loads in flight. Full
-    // 128-point trips run unpredicated; the ragged tail runs once with lane predicates.
-    const int nFull = N & ~127;
-    for (int base = 0; base < nFull; base += 128) {
-        const float4 qa = pts[base + lane];
-        const float4 qb = pts[base + lane + 64];
-        h_sweep_trip<K, FUSED, false>(hm, qa, qb, true, true, thr2, fast, cnt);
+    // part in every ballot). P correspondences per lane per trip (P loads in flight); full trips
+    // run unpredicated, the ragged tail once with lane predicates.
+    constexpr int TRIP = 64 * P;
+    const int nFull = N / TRIP * TRIP;
+    bool vt[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) vt[j] = true;
+    for (int base = 0; base < nFull; base += TRIP) {
+        float4 q[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) q[j] = pts[base + 64 * j + lane];
+        h_sweep_trip<K, P, FUSED, false>(hm, q, vt, thr2, fast, cnt);
     }
     if (nFull < N) {
-        const int pa = nFull + lane, pb = pa + 64;
-        const bool va = pa < N, vb = pb < N;
-        const float4 qa = pts[va ? pa : 0];
-        const float4 qb = pts[vb ? pb : 0];
-        h_sweep_trip<K, FUSED, true>(hm, qa, qb, va, vb, thr2, fast, cnt);
+        float4 q[P];
+        bool v[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int p = nFull + 64 * j + lane;
+            v[j] = p < N;
+            q[j] = pts[v[j] ? p : 0];
+        }
+        h_sweep_trip<K, P, FUSED, true>(hm, q, v, thr2, fast, cnt);
     }
     if (lane == 0) {
 #pragma unroll
@@ -423,17 +429,47 @@ void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s) {
     hipLaunchKernelGGL(mcv_bbox, dim3(1), dim3(1024), 0, s, (const float4*)d_pts4, N, d_bbox);
 }
 
-void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
-                     bool fused, const float* d_bbox, hipStream_t s) {
-    constexpr int K = kVerifyHypPerWave;
+template <int K, int P>
+static void launch_h_verify_kp(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount,
+                               float thr2, bool fused, const float* d_bbox, hipStream_t s) {
     const int waves = (hypCount + K - 1) / K;
     const int blocks = (waves + 3) / 4;
     if (fused)
-        hipLaunchKernelGGL((mcv_h_verify<K, true>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
+        hipLaunchKernelGGL((mcv_h_verify<K, P, true>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
                            (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox);
     else
-        hipLaunchKernelGGL((mcv_h_verify<K, false>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
+        hipLaunchKernelGGL((mcv_h_verify<K, P, false>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
                            (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox);
+}
+
+// Sweep shape (hypotheses per wave K, correspondences per lane per trip P). MCV_SWEEP_VARIANT
+// selects an alternative for tuning experiments (tests/bench only); the default is kVerify*.
+static int sweep_variant() {
+    static int v = [] {
+        const char* e = getenv("MCV_SWEEP_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
+                     bool fused, const float* d_bbox, hipStream_t s) {
+    switch (sweep_variant()) {
+        case 1: launch_h_verify_kp<8, 4>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 2: launch_h_verify_kp<4, 4>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 3: launch_h_verify_kp<8, 1>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 4: launch_h_verify_kp<6, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 5: launch_h_verify_kp<4, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 6: launch_h_verify_kp<6, 3>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 7: launch_h_verify_kp<5, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 8: launch_h_verify_kp<6, 1>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 9: launch_h_verify_kp<4, 3>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 10: launch_h_verify_kp<3, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 11: launch_h_verify_kp<7, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        default:
+            launch_h_verify_kp<kVerifyHypPerWave, kVerifyPtsPerLane>(d_pts4, N, d_models, d_counts, hypCount, thr2,
+                                                                     fused, d_bbox, s);
+    }
 }
 
 void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uint64_t* d_pkey, int64_t* d_pfail,
