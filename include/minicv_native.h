@@ -74,10 +74,14 @@ typedef struct {
     mcvV2f P0, P1, P2, P3;
 } ArucoMarkerInfo;
 
-/* Essential-matrix RANSAC — MiniCVNative.cpp:197-215 (next row f1; currently fails loudly). */
+/* Essential-matrix RANSAC + pose — MiniCVNative.cpp:197-215 (on the GPU):
+ * findEssentialMat(pa, pb, f, pp, RANSAC, Probability, InlierThreshold) -> ms = RANSAC mask ->
+ * recoverPose(E, ..., mask) (cheirality over the inliers, distance 50). Returns the number of
+ * inliers passing the cheirality test of the chosen (R, t); 0 on failure (ms untouched). */
 MCV_API int  cvRecoverPose(const RecoverPoseConfig* config, const int N, const mcvV2d* pa, const mcvV2d* pb,
                            mcvM33d* rMat, mcvV3d* tVec, uint8_t* ms);
-/* MiniCVNative.cpp:165-194 */
+/* MiniCVNative.cpp:165-194: findEssentialMat -> ms -> decomposeEssentialMat(E) -> R1, R2, t.
+ * false if N < 5 or no model (ms untouched then). */
 MCV_API bool cvRecoverPoses(const RecoverPoseConfig* config, const int N, const mcvV2d* pa, const mcvV2d* pb,
                             mcvM33d* rMat1, mcvM33d* rMat2, mcvV3d* tVec, uint8_t* ms);
 /* Feature detection — MiniCVNative.cpp:221-365 (out of scope: returns NULL). */
@@ -85,7 +89,8 @@ MCV_API DetectorResult* cvDetectFeatures(char* data, int width, int height, int 
 MCV_API void cvFreeFeatures(DetectorResult* res);
 /* Debug export — MiniCVNative.cpp:504 (no-op). */
 MCV_API void cvTest(void);
-/* Five-point minimal solver — MiniCVNative.cpp:368-382 (next row f1). */
+/* Five-point minimal solver — MiniCVNative.cpp:368-382 / fivepoint.cpp:233-339 (one GPU solve):
+ * Es: caller-allocated 10 x M33d, unit-Frobenius-norm E with pb^T E pa = 0. Returns the count. */
 MCV_API int  cvFivePoint(const mcvV2d* pa, const mcvV2d* pb, mcvM33d* Es);
 /* PnP — MiniCVNative.cpp:48-163 (next row f2). K passed by value as in the reference. */
 MCV_API bool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
@@ -150,6 +155,14 @@ MCV_API int cvFindHomography(const mcvV2d* src, const mcvV2d* dst, const int N, 
 MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, const int N, const RansacConfig* cfg,
                                  mcvM33d* F, uint8_t* mask);
 
+/* findEssentialMat (OpenCV focal/pp overload): a/b pixel points, normalised (x - pp) / focal in
+ * fp64; five-point minimal sets (<= 10 models per hypothesis), Sampson error, inlier iff
+ * err <= (float)(threshold / focal)^2. cfg NULL: threshold 1, confidence 0.999, maxIters 1000,
+ * seed 0. E: out, unit Frobenius norm. mask: uint8[N]. Returns the inlier count, 0 on failure.
+ * N == 5 runs one solve on all points (mask all 1) and succeeds only with a single solution. */
+MCV_API int cvFindEssentialMat(const mcvV2d* a, const mcvV2d* b, const int N, double focal, mcvV2d pp,
+                               const RansacConfig* cfg, mcvM33d* E, uint8_t* mask);
+
 /* Brute-force Hamming matcher (BFMatcher NORM_HAMMING, knn k = 2). q: [nq][bytesPerDesc],
  * t: [nt][bytesPerDesc] row-major bytes; bytesPerDesc in [1, 64]; nt < 2^22.
  * Outputs per query: best train index / distance and second best (idx2/dist2 may be NULL;
@@ -177,6 +190,9 @@ typedef struct mcvRansacPlan_ mcvRansacPlan;
 
 #define MCV_MODEL_HOMOGRAPHY   0
 #define MCV_MODEL_FUNDAMENTAL  1
+#define MCV_MODEL_ESSENTIAL    2   /* points: double4 {x1, y1, x2, y2} normalised (mcvPackEssential);
+                                      hypothesis h owns model slots 10h .. 10h+9: keys, counts and
+                                      indices below are slot indices for this model */
 
 /* Workspace for problems up to maxN correspondences and maxHyps hypotheses per evaluate call. */
 MCV_API mcvRansacPlan* mcvRansacPlanCreate(int model, int maxN, int64_t maxHyps);
@@ -184,6 +200,9 @@ MCV_API void mcvRansacPlanDestroy(mcvRansacPlan* plan);
 
 /* Pack host AoS fp64 pairs into the device float4 layout (synchronous H2D on `stream`). */
 MCV_API int mcvPackCorrespondences(const mcvV2d* a, const mcvV2d* b, int N, float* d_pts4, void* stream);
+/* Essential model: upload host pairs and normalise on the device into double4 (32 B each). */
+MCV_API int mcvPackEssential(const mcvV2d* a, const mcvV2d* b, int N, double focal, mcvV2d pp, double* d_pts4,
+                             void* stream);
 
 /* Evaluate hypotheses [hypBegin, hypBegin + hypCount) against all N correspondences:
  * sample + minimal solve + inlier count, then reduce to the best packed key
@@ -191,13 +210,13 @@ MCV_API int mcvPackCorrespondences(const mcvV2d* a, const mcvV2d* b, int N, floa
  * written to d_key[0]; d_key[1] = first hypothesis index whose sampler failed (or INT64 max).
  * d_counts (optional, may be NULL): per-hypothesis status/count (int32, -1 no model, -2 no sample).
  * Asynchronous on `stream`. Returns 1 on successful launch, 0 on error. */
-MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const float* d_pts4, int N, const RansacConfig* cfg,
+MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const void* d_pts4, int N, const RansacConfig* cfg,
                               int64_t hypBegin, int64_t hypCount, uint64_t* d_key, int* d_counts, void* stream);
 
 /* Recompute the best hypothesis' model (hypIndex), write the inlier mask (d_mask, uint8[N]),
  * optionally refit on the inliers + LM refine (per cfg->flags), model out to host `model9`.
  * Synchronises `stream`. Returns the inlier count, 0 on failure. */
-MCV_API int mcvRansacFinalize(mcvRansacPlan* plan, const float* d_pts4, int N, const RansacConfig* cfg,
+MCV_API int mcvRansacFinalize(mcvRansacPlan* plan, const void* d_pts4, int N, const RansacConfig* cfg,
                               int64_t hypIndex, double* model9, uint8_t* d_mask, void* stream);
 
 /* Sequential-RANSAC replay over per-hypothesis counts (host arrays), OpenCV semantics:
@@ -213,6 +232,11 @@ typedef struct {
 MCV_API void mcvReplayInit(mcvReplayState* st, int maxIters);
 MCV_API int  mcvReplayChunk(mcvReplayState* st, const int* counts, int64_t hypBegin, int64_t hypCount,
                             int N, int modelPoints, double confidence, int fixedIters);
+/* Multi-model hypotheses (essential: slotsPerHyp = 10): counts[h * slotsPerHyp + s], -2 at slot 0 =
+ * sampler failure, -1 = no model; models of one hypothesis are tried in slot order, niters is
+ * checked per hypothesis (RANSACPointSetRegistrator::run). bestIndex is the slot index. */
+MCV_API int  mcvReplayChunkModels(mcvReplayState* st, const int* counts, int64_t hypBegin, int64_t hypCount,
+                                  int slotsPerHyp, int N, int modelPoints, double confidence, int fixedIters);
 
 /* Device-level matchers: d_q/d_t device arrays, outputs device arrays. Asynchronous on stream. */
 MCV_API int mcvMatchHammingDevice(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc,
@@ -240,6 +264,11 @@ MCV_API long long mcvTestRcpExhaustive(int mode, uint32_t* firstMismatches16);
 /* Device self-test: run the homography inlier sweep on caller-supplied fp32 models (8 floats each). */
 MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models8, int nModels, float thr2, int fused,
                                    int* counts);
+/* Host twins of the essential path: hypothesis (double4 normalised points; E90 = 10 x 9) and the
+ * raw five-point solve (x1[5], y1[5], x2[5], y2[5] packed in p20). Return the model count / status. */
+MCV_API int mcvHostEssential(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90, int* sampleIdx);
+MCV_API int mcvHostFivePoint(const double* p20, double* E90);
+MCV_API void mcvHostDecomposeEssential(const double* E9, double* R1, double* R2, double* t3);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                            uint32_t* out4);
 

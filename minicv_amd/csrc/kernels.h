@@ -53,6 +53,27 @@ void launch_f_mask(const float* d_pts4, int N, const double* F9, float thr2, int
 void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,
                   double* d_part, double* d_out, hipStream_t s);
 
+// ---- essential (ransac_e.hip)
+static const int kVerifyEModelsPerWave = 4;
+static const int kEModelSlots = 10;
+struct EOneOut {
+    double E[10][9];
+    int status;    // model count (0 = no model) or -2 (no sample)
+    int idx[5];
+};
+struct EFiveIn { double x1[5], y1[5], x2[5], y2[5]; };
+void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, double* d_pts4, hipStream_t s);
+void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_dense,
+                       int* d_denseSlot, int* d_nDense, int* d_counts, hipStream_t s);
+void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
+                     int maxModels, int* d_counts, float thr2, int kind, hipStream_t s);
+void launch_e_one(const double* d_pts4, int N, uint64_t seed, int64_t hyp, EOneOut* d_out, hipStream_t s);
+void launch_e_mask(const double* d_pts4, int N, const double* E9, float thr2, int kind, uint8_t* d_mask, int* d_count,
+                   hipStream_t s);
+void launch_e_cheirality(const double* d_pts4, int N, const uint8_t* d_mask, const double* P4x12, double dist,
+                         int* d_good4, hipStream_t s);
+void launch_e_fivepoint(const EFiveIn& in, EOneOut* d_out, hipStream_t s);
+
 // ---- shared (ransac_h.hip)
 void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uint64_t* d_pkey, int64_t* d_pfail,
                  uint64_t* d_out, hipStream_t s);

@@ -11,8 +11,9 @@ namespace mcv {
 static const int64_t kChunkFirst = 4096;
 static const int64_t kChunkMax = 1 << 20;
 
-size_t model_bytes(int model);
+size_t model_bytes(int model);   // device model bytes per hypothesis
 int model_points(int model);
+int model_slots(int model);      // model slots per hypothesis (essential: 10)
 
 struct Plan {
     int model = MCV_MODEL_HOMOGRAPHY;
@@ -33,6 +34,10 @@ struct Plan {
     DevBuf<int> count;
     DevBuf<float> bbox;       // max |x|, max |y| of the source points (fused fast-path bound)
     DevBuf<uint8_t> one;      // single-hypothesis output record
+    DevBuf<double> ptsd;      // essential: double4 normalised correspondences
+    DevBuf<double> raw;       // essential: uploaded V2d pairs (a then b)
+    DevBuf<int> dslot;        // essential: slot of each dense model
+    DevBuf<int> ndense;       // essential: dense model count (+ 4 cheirality counters)
     PinnedBuf<int> h_counts;
     PinnedBuf<double> h_red;
     PinnedBuf<float> h_pack;
@@ -78,9 +83,11 @@ void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst,
 double effective_threshold(const RansacConfig& cfg);
 bool fused_error(const RansacConfig& cfg);
 RansacConfig config_or_default(const RansacConfig* cfg);
-int64_t ransac_search(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, hipStream_t s);
-int finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
+int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s);
+int finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
              uint8_t* d_mask, hipStream_t s);
+void evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
+                    int* d_counts, uint64_t* d_key, hipStream_t s);
 
 // fundamental-matrix family (ransac_f.hip / ransac_f_host.cpp)
 int f_error_kind(const RansacConfig& cfg);
@@ -88,5 +95,11 @@ int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
                hipStream_t s);
 int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F);
 int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F9, float* Ff9, int* sampleIdx);
+
+// essential-matrix family (ransac_e.hip / ransac_e_host.cpp)
+void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
+                      int* d_counts, hipStream_t s);
+int e_finalize(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int64_t slot, double* E,
+               uint8_t* d_mask, hipStream_t s);
 
 }  // namespace mcv

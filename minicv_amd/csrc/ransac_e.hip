@@ -1,0 +1,208 @@
+// ransac_e.hip — gfx950 kernels of the essential-matrix RANSAC path behind cvRecoverPose(s)
+// (reference MiniCVNative.cpp:165-215, fivepoint.cpp:233-339).
+//
+//   mcv_e_pack          V2d pairs -> double4 normalised camera coordinates (x - cx) / f.
+//   mcv_e_generate      one lane per hypothesis: Philox sample of 5 -> five-point solve (fp64,
+//                       up to 10 models) -> all 10 slot statuses + models appended to a dense
+//                       list (atomic slot allocation; results are keyed by slot, so the order of
+//                       the dense list never reaches an output).
+//   mcv_e_verify<K, E>  inlier sweep over the dense model list: wave = K models in VGPRs, 64
+//                       lanes stream the double4 correspondences, fp64 Sampson error cast to
+//                       float, ballot + popcount; the count lands in the model's slot.
+//   mcv_e_one           recompute one hypothesis (winner) -> all its models.
+//   mcv_e_mask          inlier mask of the winner.
+//   mcv_e_cheirality    recoverPose: per RANSAC inlier, the 4 (R, t) candidates' cheirality tests.
+//   mcv_e_fivepoint     cvFivePoint: one five-point solve on raw coordinates.
+#include "mcv_common.h"
+#include "hyp_essential.h"
+#include "kernels.h"
+
+namespace mcv {
+
+__global__ __launch_bounds__(256) void mcv_e_pack(const double2* __restrict__ a, const double2* __restrict__ b, int N,
+                                                  double f, double cx, double cy, double4* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const double2 p = a[i], q = b[i];
+    double4 o;
+    o.x = (p.x - cx) / f;
+    o.y = (p.y - cy) / f;
+    o.z = (q.x - cx) / f;
+    o.w = (q.y - cy) / f;
+    out[i] = o;
+}
+
+__global__ __launch_bounds__(64) void mcv_e_generate(const double* __restrict__ pts4, int N, uint64_t seed,
+                                                     int64_t hypBegin, int hypCount, EModel* __restrict__ dense,
+                                                     int* __restrict__ denseSlot, int* __restrict__ nDense,
+                                                     int* __restrict__ counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hypCount) return;
+    double E[kEMaxModels][9];
+    const int n = e_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), E, nullptr);
+    const int m = n > 0 ? n : 0;
+    for (int s = 0; s < kEMaxModels; ++s)
+        counts[(int64_t)i * kEMaxModels + s] = s < m ? 0 : (s == 0 && n == kStatusNoSample ? kStatusNoSample : kStatusNoModel);
+    if (m == 0) return;
+    const int base = atomicAdd(nDense, m);
+    for (int s = 0; s < m; ++s) {
+        EModel em;
+        for (int k = 0; k < 9; ++k) em.e[k] = E[s][k];
+        dense[base + s] = em;
+        denseSlot[base + s] = i * kEMaxModels + s;
+    }
+}
+
+template <int K, int KIND>
+__global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ pts, int N,
+                                                    const EModel* __restrict__ dense,
+                                                    const int* __restrict__ denseSlot, const int* __restrict__ nDense,
+                                                    int* __restrict__ counts, float thr2) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    const int lane = threadIdx.x & 63;
+    const int total = __builtin_amdgcn_readfirstlane(*nDense);
+    const int m0 = wave * K;
+    if (m0 >= total) return;
+    double em[K][9];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        valid[k] = m0 + k < total;
+        const EModel m = dense[valid[k] ? m0 + k : m0];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            em[k][j] = valid[k] ? m.e[j] : __builtin_nan("");
+            asm volatile("" : "+v"(em[k][j]));
+        }
+    }
+    uint32_t cnt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt[k] = 0;
+    const int nFull = N & ~63;
+    for (int base = 0; base < nFull; base += 64) {
+        const double4 q = pts[base + lane];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(f_error(KIND, em[k], q.x, q.y, q.z, q.w) <= thr2));
+    }
+    if (nFull < N) {
+        const int p = nFull + lane;
+        const bool v = p < N;
+        const double4 q = pts[v ? p : 0];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            cnt[k] += (uint32_t)__popcll(
+                __builtin_amdgcn_ballot_w64(v && f_error(KIND, em[k], q.x, q.y, q.z, q.w) <= thr2));
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid[k]) counts[denseSlot[m0 + k]] = (int)cnt[k];
+    }
+}
+
+__global__ void mcv_e_one(const double* __restrict__ pts4, int N, uint64_t seed, int64_t hyp,
+                          EOneOut* __restrict__ out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    double E[kEMaxModels][9];
+    int idx[5] = {-1, -1, -1, -1, -1};
+    const int n = e_hypothesis(pts4, N, seed, (uint64_t)hyp, E, idx);
+    out->status = n;
+    for (int i = 0; i < 5; ++i) out->idx[i] = idx[i];
+    for (int s = 0; s < kEMaxModels; ++s)
+        for (int k = 0; k < 9; ++k) out->E[s][k] = s < n ? E[s][k] : 0.0;
+}
+
+__global__ __launch_bounds__(256) void mcv_e_mask(const double4* __restrict__ pts, int N, EModel m, float thr2,
+                                                  int kind, uint8_t* __restrict__ mask, int* __restrict__ count) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool in = false;
+    if (i < N) {
+        const double4 q = pts[i];
+        in = f_error(kind, m.e, q.x, q.y, q.z, q.w) <= thr2;
+        mask[i] = in ? 1 : 0;
+    }
+    const uint64_t b = __ballot(in);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (int)__popcll(b));
+}
+
+struct EPoseCands { double P[4][12]; };
+
+__global__ __launch_bounds__(256) void mcv_e_cheirality(const double4* __restrict__ pts, int N,
+                                                        const uint8_t* __restrict__ mask, EPoseCands c, double dist,
+                                                        int* __restrict__ good4) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const bool act = i < N && (!mask || mask[i]);
+    double4 q = {0, 0, 0, 0};
+    if (act) q = pts[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool g = act && e_cheirality(c.P[k], q.x, q.y, q.z, q.w, dist);
+        const uint64_t b = __ballot(g);
+        if ((threadIdx.x & 63) == 0 && b) atomicAdd(good4 + k, (int)__popcll(b));
+    }
+}
+
+__global__ void mcv_e_fivepoint(EFiveIn in, EOneOut* __restrict__ out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    double E[kEMaxModels][9];
+    const int n = e_solve5(in.x1, in.y1, in.x2, in.y2, E);
+    out->status = n;
+    for (int s = 0; s < kEMaxModels; ++s)
+        for (int k = 0; k < 9; ++k) out->E[s][k] = s < n ? E[s][k] : 0.0;
+}
+
+// ---- launchers ---------------------------------------------------------------------------------
+void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, double* d_pts4, hipStream_t s) {
+    if (N <= 0) return;
+    const double2* a = (const double2*)d_ab;
+    hipLaunchKernelGGL(mcv_e_pack, dim3((N + 255) / 256), dim3(256), 0, s, a, a + N, N, f, cx, cy,
+                       (double4*)d_pts4);
+}
+
+void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_dense,
+                       int* d_denseSlot, int* d_nDense, int* d_counts, hipStream_t s) {
+    (void)hipMemsetAsync(d_nDense, 0, sizeof(int), s);
+    hipLaunchKernelGGL(mcv_e_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+                       hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+}
+
+void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
+                     int maxModels, int* d_counts, float thr2, int kind, hipStream_t s) {
+    constexpr int K = kVerifyEModelsPerWave;
+    const int blocks = ((maxModels + K - 1) / K + 3) / 4;
+    const double4* p = (const double4*)d_pts4;
+    const EModel* m = (const EModel*)d_dense;
+    switch (kind) {
+        case 0: hipLaunchKernelGGL((mcv_e_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2); break;
+        default: hipLaunchKernelGGL((mcv_e_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2); break;
+    }
+}
+
+void launch_e_one(const double* d_pts4, int N, uint64_t seed, int64_t hyp, EOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_e_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out);
+}
+
+void launch_e_mask(const double* d_pts4, int N, const double* E9, float thr2, int kind, uint8_t* d_mask, int* d_count,
+                   hipStream_t s) {
+    EModel m;
+    for (int j = 0; j < 9; ++j) m.e[j] = E9[j];
+    hipLaunchKernelGGL(mcv_e_mask, dim3((N + 255) / 256), dim3(256), 0, s, (const double4*)d_pts4, N, m, thr2, kind,
+                       d_mask, d_count);
+}
+
+void launch_e_cheirality(const double* d_pts4, int N, const uint8_t* d_mask, const double* P4x12, double dist,
+                         int* d_good4, hipStream_t s) {
+    EPoseCands c;
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 12; ++j) c.P[k][j] = P4x12[12 * k + j];
+    (void)hipMemsetAsync(d_good4, 0, 4 * sizeof(int), s);
+    hipLaunchKernelGGL(mcv_e_cheirality, dim3((N + 255) / 256), dim3(256), 0, s, (const double4*)d_pts4, N, d_mask,
+                       c, dist, d_good4);
+}
+
+void launch_e_fivepoint(const EFiveIn& in, EOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_e_fivepoint, dim3(1), dim3(64), 0, s, in, d_out);
+}
+
+}  // namespace mcv

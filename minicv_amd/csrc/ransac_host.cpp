@@ -51,24 +51,43 @@ extern "C" MCV_API void mcvReplayInit(mcvReplayState* st, int maxIters) {
     st->stopped = 0;
 }
 
-extern "C" MCV_API int mcvReplayChunk(mcvReplayState* st, const int* counts, int64_t hypBegin, int64_t hypCount,
-                                      int N, int modelPoints, double confidence, int fixedIters) {
+namespace mcv {
+// One chunk of the RANSACPointSetRegistrator::run loop: hypothesis `it` = one getSubset +
+// runKernel; its models (slots) are tried in order, each improvement updates niters; the loop
+// condition is checked per hypothesis.
+static int replay_chunk(mcvReplayState* st, const int* counts, int64_t hypBegin, int64_t hypCount, int slots, int N,
+                        int modelPoints, double confidence, int fixedIters) {
     if (st->stopped) return 1;
     for (int64_t i = 0; i < hypCount; ++i) {
         const int64_t it = hypBegin + i;
         if (it >= st->niters) { st->stopped = 1; return 1; }
-        const int c = counts[i];
-        if (c == kStatusNoSample) { st->stopped = 1; return 1; }
-        if (c < 0) continue;
-        if (c > std::max(st->bestCount, modelPoints - 1)) {
-            st->bestCount = c;
-            st->bestIndex = it;
-            if (!fixedIters)
-                st->niters = ransac_update_num_iters(confidence, (double)(N - c) / N, modelPoints, st->niters);
+        const int* c = counts + i * slots;
+        if (c[0] == kStatusNoSample) { st->stopped = 1; return 1; }
+        for (int k = 0; k < slots; ++k) {
+            if (c[k] < 0) continue;
+            if (c[k] > std::max(st->bestCount, modelPoints - 1)) {
+                st->bestCount = c[k];
+                st->bestIndex = it * slots + k;
+                if (!fixedIters)
+                    st->niters = ransac_update_num_iters(confidence, (double)(N - c[k]) / N, modelPoints, st->niters);
+            }
         }
     }
     if (hypBegin + hypCount >= st->niters) { st->stopped = 1; return 1; }
     return 0;
+}
+}  // namespace mcv
+
+extern "C" MCV_API int mcvReplayChunk(mcvReplayState* st, const int* counts, int64_t hypBegin, int64_t hypCount,
+                                      int N, int modelPoints, double confidence, int fixedIters) {
+    return replay_chunk(st, counts, hypBegin, hypCount, 1, N, modelPoints, confidence, fixedIters);
+}
+
+extern "C" MCV_API int mcvReplayChunkModels(mcvReplayState* st, const int* counts, int64_t hypBegin,
+                                            int64_t hypCount, int slotsPerHyp, int N, int modelPoints,
+                                            double confidence, int fixedIters) {
+    if (slotsPerHyp < 1) slotsPerHyp = 1;
+    return replay_chunk(st, counts, hypBegin, hypCount, slotsPerHyp, N, modelPoints, confidence, fixedIters);
 }
 
 namespace mcv {
@@ -79,9 +98,17 @@ namespace mcv {
 void Plan::reserve(int n, int64_t hyps) {
     if (n > maxN) maxN = n;
     if (hyps > maxHyps) maxHyps = hyps;
-    pts.ensure((size_t)maxN * 4);
+    const size_t slots = (size_t)model_slots(model);
+    if (model == MCV_MODEL_ESSENTIAL) {
+        ptsd.ensure((size_t)maxN * 4);
+        raw.ensure((size_t)maxN * 4);
+        dslot.ensure((size_t)maxHyps * slots);
+        ndense.ensure(8);
+    } else {
+        pts.ensure((size_t)maxN * 4);
+    }
     models.ensure((size_t)maxHyps * model_bytes(model));
-    counts.ensure((size_t)maxHyps);
+    counts.ensure((size_t)maxHyps * slots);
     pkey.ensure(512);
     pfail.ensure(512);
     key.ensure(2);
@@ -91,14 +118,18 @@ void Plan::reserve(int n, int64_t hyps) {
     count.ensure(1);
     bbox.ensure(4);
     one.ensure(512);
-    h_counts.ensure((size_t)maxHyps);
+    h_counts.ensure((size_t)maxHyps * slots);
     h_red.ensure(64);
-    h_pack.ensure((size_t)maxN * 4);
-    h_one.ensure(512);
+    if (model != MCV_MODEL_ESSENTIAL) h_pack.ensure((size_t)maxN * 4);
+    one.ensure(sizeof(EOneOut));
+    h_one.ensure(sizeof(EOneOut));
     h_i.ensure(4);
 }
 
-size_t model_bytes(int model) { return model == MCV_MODEL_FUNDAMENTAL ? 80 : 32; }
+size_t model_bytes(int model) {
+    return model == MCV_MODEL_ESSENTIAL ? 72 * kEModelSlots : (model == MCV_MODEL_FUNDAMENTAL ? 80 : 32);
+}
+int model_slots(int model) { return model == MCV_MODEL_ESSENTIAL ? kEModelSlots : 1; }
 
 hipStream_t Plan::own_stream() {
     if (!stream) MCV_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -243,8 +274,17 @@ void h_lm_refine(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipS
 }
 
 // Evaluate one chunk of hypotheses on the device (generate + verify [+ best key]).
-void evaluate_chunk(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
+void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
                     int* d_counts, uint64_t* d_key, hipStream_t s) {
+    if (P.model == MCV_MODEL_ESSENTIAL) {
+        e_evaluate_chunk(P, (const double*)d_ptsv, N, cfg, hypBegin, hypCount, d_counts, s);
+        if (d_key)
+            launch_best(d_counts, hypCount * kEModelSlots, hypBegin * kEModelSlots, model_points(P.model), P.pkey.p,
+                        P.pfail.p, d_key, s);
+        MCV_HIP(hipGetLastError());
+        return;
+    }
+    const float* d_pts = (const float*)d_ptsv;
     const double t = effective_threshold(cfg);
     const float thr2 = (float)(t * t);
     if (P.model == MCV_MODEL_HOMOGRAPHY) {
@@ -261,7 +301,7 @@ void evaluate_chunk(Plan& P, const float* d_pts, int N, const RansacConfig& cfg,
     MCV_HIP(hipGetLastError());
 }
 
-int model_points(int model) { return model == MCV_MODEL_FUNDAMENTAL ? 8 : 4; }
+int model_points(int model) { return model == MCV_MODEL_FUNDAMENTAL ? 8 : (model == MCV_MODEL_ESSENTIAL ? 5 : 4); }
 
 // Winner -> mask (+ refit + LM). Returns inlier count, 0 on failure. Synchronises s.
 int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* H, uint8_t* d_mask,
@@ -293,16 +333,19 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     return count;
 }
 
-int finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
+int finalize(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
              uint8_t* d_mask, hipStream_t s) {
+    if (P.model == MCV_MODEL_ESSENTIAL) return e_finalize(P, (const double*)d_ptsv, N, cfg, hyp, model9, d_mask, s);
+    const float* d_pts = (const float*)d_ptsv;
     if (P.model == MCV_MODEL_HOMOGRAPHY) return h_finalize(P, d_pts, N, cfg, hyp, model9, d_mask, s);
     return f_finalize(P, d_pts, N, cfg, hyp, model9, d_mask, s);
 }
 
 // Full RANSAC on device-resident points with the OpenCV sequential-replay semantics.
 // Returns the best hypothesis index or -1.
-int64_t ransac_search(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, hipStream_t s) {
+int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s) {
     const int m = model_points(P.model);
+    const int slots = model_slots(P.model);
     mcvReplayState st;
     mcvReplayInit(&st, cfg.maxIters);
     const bool fixed = (cfg.flags & MCV_FLAG_FIXED_ITERS) != 0;
@@ -314,9 +357,9 @@ int64_t ransac_search(Plan& P, const float* d_pts, int N, const RansacConfig& cf
         const int cnt = (int)std::min<int64_t>(remaining, chunk);
         P.reserve(N, cnt);
         evaluate_chunk(P, d_pts, N, cfg, begin, cnt, P.counts.p, nullptr, s);
-        MCV_HIP(hipMemcpyAsync(P.h_counts.p, P.counts.p, (size_t)cnt * sizeof(int), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipMemcpyAsync(P.h_counts.p, P.counts.p, (size_t)cnt * slots * sizeof(int), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
-        mcvReplayChunk(&st, P.h_counts.p, begin, cnt, N, m, cfg.confidence, fixed ? 1 : 0);
+        replay_chunk(&st, P.h_counts.p, begin, cnt, slots, N, m, cfg.confidence, fixed ? 1 : 0);
         begin += cnt;
         chunk = std::min<int64_t>(chunk * 2, kChunkMax);
     }
@@ -386,7 +429,8 @@ extern "C" MCV_API int cvFindHomography(const mcvV2d* src, const mcvV2d* dst, co
 
 extern "C" MCV_API mcvRansacPlan* mcvRansacPlanCreate(int model, int maxN, int64_t maxHyps) {
     MCV_GUARD(nullptr, {
-        if (model != MCV_MODEL_HOMOGRAPHY && model != MCV_MODEL_FUNDAMENTAL) fail("unknown model %d", model);
+        if (model != MCV_MODEL_HOMOGRAPHY && model != MCV_MODEL_FUNDAMENTAL && model != MCV_MODEL_ESSENTIAL)
+            fail("unknown model %d", model);
         require_device();
         std::unique_ptr<Plan> p(new Plan());
         MCV_HIP(hipGetDevice(&p->device));
@@ -413,7 +457,7 @@ extern "C" MCV_API int mcvPackCorrespondences(const mcvV2d* a, const mcvV2d* b, 
     })
 }
 
-extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const float* d_pts4, int N, const RansacConfig* cfg,
+extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const void* d_pts4, int N, const RansacConfig* cfg,
                                          int64_t hypBegin, int64_t hypCount, uint64_t* d_key, int* d_counts,
                                          void* stream) {
     MCV_GUARD(0, {
@@ -422,14 +466,15 @@ extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const float* d_pts
         if (N < model_points(P->model)) fail("mcvRansacEvaluate: N=%d below the minimal sample", N);
         if (hypCount <= 0 || hypCount > P->maxHyps) fail("mcvRansacEvaluate: hypCount %lld outside plan capacity %lld",
                                                          (long long)hypCount, (long long)P->maxHyps);
-        if (hypBegin < 0 || hypBegin + hypCount > 0xFFFFFFFFll) fail("mcvRansacEvaluate: hypothesis index beyond 2^32");
+        if (hypBegin < 0 || (hypBegin + hypCount) * model_slots(P->model) > 0xFFFFFFFFll)
+            fail("mcvRansacEvaluate: hypothesis (slot) index beyond 2^32");
         evaluate_chunk(*P, d_pts4, N, *cfg, hypBegin, (int)hypCount, d_counts ? d_counts : P->counts.p, d_key,
                        (hipStream_t)stream);
         return 1;
     })
 }
 
-extern "C" MCV_API int mcvRansacFinalize(mcvRansacPlan* plan, const float* d_pts4, int N, const RansacConfig* cfg,
+extern "C" MCV_API int mcvRansacFinalize(mcvRansacPlan* plan, const void* d_pts4, int N, const RansacConfig* cfg,
                                          int64_t hypIndex, double* model9, uint8_t* d_mask, void* stream) {
     MCV_GUARD(0, {
         Plan* P = reinterpret_cast<Plan*>(plan);

@@ -3,7 +3,6 @@
 //   cvDetectFeatures / cvFreeFeatures   MiniCVNative.cpp:221-365  (feature detection: out of scope)
 //   cvDetectQRCode / cvDetectArucoMarkers MiniCVNative.cpp:384-502 (fiducials: out of scope)
 //   cvTest                               MiniCVNative.cpp:504      (debug print: no-op)
-//   cvRecoverPose(s), cvFivePoint         MiniCVNative.cpp:165-215,368  (next)
 //   cvSolvePnP*, cvRefinePnP*, solveAp3p  MiniCVNative.cpp:48-163, ap3p.cpp:282 (row f2: next)
 #include "minicv_native.h"
 #include "mcv_runtime.h"
@@ -80,18 +79,6 @@ extern "C" MCV_API int mcvDeviceCount(void) {
 
 #define MCV_NOT_IN_SCOPE(name, why) set_last_error(name ": " why)
 
-extern "C" MCV_API int cvRecoverPose(const RecoverPoseConfig*, const int, const mcvV2d*, const mcvV2d*, mcvM33d*,
-                                     mcvV3d*, uint8_t*) {
-    MCV_NOT_IN_SCOPE("cvRecoverPose", "essential-matrix RANSAC is the next row (SURVEY 8f-1), not built yet");
-    return 0;
-}
-
-extern "C" MCV_API bool cvRecoverPoses(const RecoverPoseConfig*, const int, const mcvV2d*, const mcvV2d*, mcvM33d*,
-                                       mcvM33d*, mcvV3d*, uint8_t*) {
-    MCV_NOT_IN_SCOPE("cvRecoverPoses", "essential-matrix RANSAC is the next row (SURVEY 8f-1), not built yet");
-    return false;
-}
-
 extern "C" MCV_API DetectorResult* cvDetectFeatures(char*, int, int, int, int, void*) {
     MCV_NOT_IN_SCOPE("cvDetectFeatures", "feature detection is outside the MI355X hot path (SURVEY 2 row 4)");
     return nullptr;
@@ -107,11 +94,6 @@ extern "C" MCV_API void cvFreeFeatures(DetectorResult* res) {
 }
 
 extern "C" MCV_API void cvTest(void) {}
-
-extern "C" MCV_API int cvFivePoint(const mcvV2d*, const mcvV2d*, mcvM33d*) {
-    MCV_NOT_IN_SCOPE("cvFivePoint", "five-point solver is the next row (SURVEY 8f-1), not built yet");
-    return 0;
-}
 
 extern "C" MCV_API bool cvSolvePnP(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*, const int,
                                    mcvV3d*, mcvV3d*) {

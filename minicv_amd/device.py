@@ -81,3 +81,16 @@ def match_l2(q, t, idx, dist, idx2=None, dist2=None, stream=None) -> None:
                                  idx2.data_ptr() if idx2 is not None else None,
                                  dist2.data_ptr() if dist2 is not None else None, _stream_handle(stream))
     N.check(r == q.shape[0], "mcvMatchL2Device")
+
+
+def pack_essential_tensor(a: np.ndarray, b: np.ndarray, focal: float, pp, device, stream=None):
+    """(N,2)+(N,2) fp64 pixels -> device float64 [N,4] normalised (x - pp) / focal, computed on the GPU
+    (mcvPackEssential; synchronises the stream)."""
+    import torch
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    out = torch.empty((a.shape[0], 4), dtype=torch.float64, device=device)
+    ok = N.lib().mcvPackEssential(a.ctypes.data, b.ctypes.data, a.shape[0], float(focal),
+                                  N.V2d(float(pp[0]), float(pp[1])), out.data_ptr(), _stream_handle(stream))
+    N.check(ok == 1, "mcvPackEssential")
+    return out

@@ -54,6 +54,8 @@ FERR_SAMPSON = 0
 FERR_EPIPOLAR = 1
 MODEL_HOMOGRAPHY = 0
 MODEL_FUNDAMENTAL = 1
+MODEL_ESSENTIAL = 2
+E_SLOTS = 10
 
 _P = C.c_void_p
 _I = C.c_int
@@ -81,6 +83,7 @@ SIGNATURES = {
     # new hot-path exports
     "cvFindHomography": (_I, [_P, _P, _I, _P, _P, _P]),
     "cvFindFundamentalMat": (_I, [_P, _P, _I, _P, _P, _P]),
+    "cvFindEssentialMat": (_I, [_P, _P, _I, _D, V2d, _P, _P, _P]),
     "cvMatchHamming": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
     "cvMatchL2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
     "mcvGetLastError": (C.c_char_p, []),
@@ -90,10 +93,12 @@ SIGNATURES = {
     "mcvRansacPlanCreate": (_P, [_I, _I, _I64]),
     "mcvRansacPlanDestroy": (None, [_P]),
     "mcvPackCorrespondences": (_I, [_P, _P, _I, _P, _P]),
+    "mcvPackEssential": (_I, [_P, _P, _I, _D, V2d, _P, _P]),
     "mcvRansacEvaluate": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P, _P]),
     "mcvRansacFinalize": (_I, [_P, _P, _I, _P, _I64, _P, _P, _P]),
     "mcvReplayInit": (None, [_P, _I]),
     "mcvReplayChunk": (_I, [_P, _P, _I64, _I64, _I, _I, _D, _I]),
+    "mcvReplayChunkModels": (_I, [_P, _P, _I64, _I64, _I, _I, _I, _D, _I]),
     "mcvMatchHammingDevice": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
     "mcvMatchL2Device": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
     "mcvProfileEnable": (None, [_I]),
@@ -102,6 +107,9 @@ SIGNATURES = {
     # test hooks
     "mcvHostHypothesis": (_I, [_I, _P, _I, _U64, _I64, _P, _P, _P]),
     "mcvHostPhilox": (None, [C.c_uint32] * 6 + [_P]),
+    "mcvHostEssential": (_I, [_P, _I, _U64, _I64, _P, _P]),
+    "mcvHostFivePoint": (_I, [_P, _P]),
+    "mcvHostDecomposeEssential": (None, [_P, _P, _P, _P]),
     "mcvTestRcpExhaustive": (C.c_longlong, [_I, _P]),
     "mcvTestHomographySweep": (_I, [_P, _I, _P, _I, _F, _I, _P]),
 }
@@ -115,6 +123,13 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not LIB_PATH.exists():
             raise RuntimeError(f"libMiniCVNative.so not found at {LIB_PATH}; run __graft_entry__.build()")
+        # torch bundles its own libamdhip64.so.7 / libhsa-runtime64.so.1 (same SONAMEs as /opt/rocm's).
+        # Whichever process-wide copy loads first serves both; if ours loaded first, torch would bring
+        # a second HIP/HSA runtime whose device init fails. So let torch's copy load first when present.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

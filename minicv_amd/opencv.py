@@ -102,12 +102,83 @@ def matchL2(q, t):
     return idx[:nq], d[:nq], idx2[:nq], d2[:nq]
 
 
-def recoverPose(cfg: N.RecoverPoseConfig, a, b):
-    """OpenCV.recoverPose (OpenCV.fs:855-861): -> (res, R, t, mask bytes)."""
+def recoverPoseConfig(focal: float = 1.0, pp=(0.0, 0.0), probability: float = 0.999,
+                      threshold: float = 0.005) -> N.RecoverPoseConfig:
+    """RecoverPoseConfig (OpenCV.fs:16-36); defaults = RecoverPoseConfig.Default (:33-34)."""
+    return N.RecoverPoseConfig(float(focal), N.V2d(float(pp[0]), float(pp[1])), float(probability), float(threshold))
+
+
+def findEssentialMat(a, b, focal: float = 1.0, pp=(0.0, 0.0), params: RansacParams | None = None):
+    """cv::findEssentialMat(a, b, focal, pp, RANSAC, ...) on the GPU.
+    -> (inlierCount, E (3x3 float64, unit Frobenius norm), mask (bool[N]))."""
+    params = params or RansacParams(threshold=1.0, confidence=0.999, max_iters=1000)
     pa, pb = _v2d(a), _v2d(b)
-    m, t = N.M33d(), N.V3d()
+    n = pa.shape[0]
+    if pb.shape[0] != n:
+        raise ValueError("a/b length mismatch")
+    E = N.M33d()
+    ms = np.zeros(max(n, 1), dtype=np.uint8)
+    cfg = params.to_c()
+    cnt = N.lib().cvFindEssentialMat(pa.ctypes.data, pb.ctypes.data, n, float(focal), N.V2d(*map(float, pp)),
+                                     N.C.addressof(cfg), N.C.addressof(E), ms.ctypes.data)
+    N.check(cnt > 0, "cvFindEssentialMat")
+    return cnt, np.array(E.M[:], dtype=np.float64).reshape(3, 3), ms[:n] != 0
+
+
+def recoverPose(cfg: N.RecoverPoseConfig, a, b):
+    """OpenCV.recoverPose (OpenCV.fs:855-861): -> (res, R, t, mask bytes). res is the number of
+    RANSAC inliers passing the cheirality test; the mask is the RANSAC mask (MiniCVNative.cpp:206-210).
+    Raises NativeError when the export reports an error (the reference would throw inside OpenCV)."""
+    pa, pb = _v2d(a), _v2d(b)
+    m, t = N.M33d(), N.V3d(100, 123, 432)
     ms = np.zeros(max(pa.shape[0], 1), dtype=np.uint8)
     res = N.lib().cvRecoverPose(N.C.addressof(cfg), pa.shape[0], pa.ctypes.data, pb.ctypes.data,
                                 N.C.addressof(m), N.C.addressof(t), ms.ctypes.data)
-    N.check(res > 0, "cvRecoverPose")
+    if res <= 0 and N.last_error():
+        raise N.NativeError(f"cvRecoverPose: {N.last_error()}")
     return res, np.array(m.M[:]).reshape(3, 3), np.array([t.X, t.Y, t.Z]), ms[:pa.shape[0]]
+
+
+def recoverPoses(cfg: N.RecoverPoseConfig, a, b):
+    """OpenCV.recoverPoses (OpenCV.fs:863-870): -> (R1, R2, t, mask bytes); the bool result is
+    ignored like the F# wrapper does (outputs keep their initial values on failure)."""
+    pa, pb = _v2d(a), _v2d(b)
+    m1, m2 = N.M33d(), N.M33d()
+    m1.M[:] = [1.0, 0, 0, 0, 1.0, 0, 0, 0, 1.0]
+    m2.M[:] = [1.0, 0, 0, 0, 1.0, 0, 0, 0, 1.0]
+    t = N.V3d(100, 123, 432)
+    ms = np.zeros(max(pa.shape[0], 1), dtype=np.uint8)
+    N.lib().cvRecoverPoses(N.C.addressof(cfg), pa.shape[0], pa.ctypes.data, pb.ctypes.data, N.C.addressof(m1),
+                           N.C.addressof(m2), N.C.addressof(t), ms.ctypes.data)
+    return (np.array(m1.M[:]).reshape(3, 3), np.array(m2.M[:]).reshape(3, 3), np.array([t.X, t.Y, t.Z]),
+            ms[:pa.shape[0]])
+
+
+def recoverPoses2(cfg: N.RecoverPoseConfig, a, b):
+    """OpenCV.recoverPoses2 (OpenCV.fs:872-909): NDC-like input (x, y) -> (x, -y), focal and
+    threshold rescaled, result mapped back with C = diag(1, -1, -1).
+    -> (list of (R, t) candidate poses, mask bool[N])."""
+    scale = 2.0
+    pa = np.stack([(0.5 * _v2d(a)[:, 0]) * scale, (-0.5 * _v2d(a)[:, 1]) * scale], axis=1)
+    pb = np.stack([(0.5 * _v2d(b)[:, 0]) * scale, (-0.5 * _v2d(b)[:, 1]) * scale], axis=1)
+    c = N.RecoverPoseConfig(scale * cfg.FocalLength / 2.0, N.V2d(0.0, 0.0), cfg.Probability,
+                            scale * 0.5 * cfg.InlierThreshold)
+    m1, m2, t, ms = recoverPoses(c, pa, pb)
+    Cm = np.diag([1.0, -1.0, -1.0])
+    m1 = Cm @ m1.T @ Cm
+    m2 = Cm @ m2.T @ Cm
+    t = Cm @ t
+    poses = [(m1, t)] if np.array_equal(m1, m2) else [(m1, t), (m2, t)]
+    return poses, ms != 0
+
+
+def fivepoint(a, b):
+    """OpenCV.fivepoint (OpenCV.fs:912-920): -> list of up to 10 essential matrices (3x3)."""
+    pa, pb = _v2d(a), _v2d(b)
+    if pa.shape[0] < 5 or pb.shape[0] < 5:
+        raise ValueError("fivepoint needs 5 correspondences")
+    Es = (N.M33d * 10)()
+    cnt = N.lib().cvFivePoint(pa.ctypes.data, pb.ctypes.data, Es)
+    if cnt <= 0 and N.last_error():
+        raise N.NativeError(f"cvFivePoint: {N.last_error()}")
+    return [np.array(Es[i].M[:]).reshape(3, 3) for i in range(max(cnt, 0))]

@@ -110,3 +110,33 @@ def fundamental_problem(n: int, seed: int = 4, outlier_frac: float = 0.5, sigma:
     S = np.diag([1.0, 1.0, -1.0])   # image (x, y, 1) = S * normalised camera ray up to scale
     F = S @ E @ S
     return a, b, ~out, F / np.linalg.norm(F)
+
+
+def rotation(axis, angle_rad: float) -> np.ndarray:
+    """Rodrigues rotation matrix."""
+    k = np.asarray(axis, dtype=np.float64)
+    k = k / np.linalg.norm(k)
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(angle_rad) * K + (1 - np.cos(angle_rad)) * K @ K
+
+
+def essential_problem(n: int, seed: int = 6, outlier_frac: float = 0.5, sigma: float = 0.3, focal: float = 800.0,
+                      pp=(640.0, 360.0), R: np.ndarray | None = None, t=None):
+    """Calibrated two-view pixels (OpenCV convention: camera looks down +z, x = f X/Z + pp).
+    Camera 1 = [I | 0]; camera 2 = [R | t] (X2 = R X1 + t). Points at depth 4..12.
+    -> a (n,2), b (n,2), is_inlier, R, t_unit, E_true (unit norm, x2n^T E x1n = 0)"""
+    rng = np.random.default_rng(seed)
+    R = rotation([0.2, 1.0, 0.1], np.deg2rad(8.0)) if R is None else np.asarray(R, dtype=np.float64)
+    t = np.array([1.0, 0.15, 0.1]) if t is None else np.asarray(t, dtype=np.float64)
+    X = np.stack([rng.uniform(-3, 3, n), rng.uniform(-2, 2, n), rng.uniform(4, 12, n)], axis=1)
+    Y = X @ R.T + t
+    ppa = np.asarray(pp, dtype=np.float64)
+    a = focal * X[:, :2] / X[:, 2:3] + ppa + rng.normal(0, sigma, size=(n, 2))
+    b = focal * Y[:, :2] / Y[:, 2:3] + ppa + rng.normal(0, sigma, size=(n, 2))
+    out = rng.random(n) < outlier_frac
+    lo, hi = b.min(axis=0), b.max(axis=0)
+    b[out] = rng.uniform(lo, hi, size=(int(out.sum()), 2))
+    tu = t / np.linalg.norm(t)
+    tx = np.array([[0, -tu[2], tu[1]], [tu[2], 0, -tu[0]], [-tu[1], tu[0], 0]])
+    E = tx @ R
+    return a, b, ~out, R, tu, E / np.linalg.norm(E)

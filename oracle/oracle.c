@@ -48,10 +48,9 @@ void orc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-/* Per-hypothesis word stream: word s = philox({s/4, hyp_lo, hyp_hi, "MCV1"}, {seed_lo, seed_hi})[s%4] */
-typedef struct { uint64_t seed, hyp; uint64_t pos; uint32_t buf[4]; } Stream;
+#include "oracle_int.h"
 
-static uint32_t stream_next(Stream* st) {
+uint32_t stream_next(Stream* st) {
     if ((st->pos & 3) == 0) {
         uint32_t c[4] = {(uint32_t)(st->pos >> 2), (uint32_t)st->hyp, (uint32_t)(st->hyp >> 32), 0x4D435631u};
         uint32_t k[2] = {(uint32_t)st->seed, (uint32_t)(st->seed >> 32)};
@@ -60,15 +59,11 @@ static uint32_t stream_next(Stream* st) {
     return st->buf[st->pos++ & 3];
 }
 
-static int stream_uniform(Stream* st, int n) { return (int)(((uint64_t)stream_next(st) * (uint32_t)n) >> 32); }
+int stream_uniform(Stream* st, int n) { return (int)(((uint64_t)stream_next(st) * (uint32_t)n) >> 32); }
 
-#define ORC_MAX_ATTEMPTS 10000
-#define ORC_MAX_REDRAW 1000
-#define ORC_NO_MODEL (-1)
-#define ORC_NO_SAMPLE (-2)
 
 /* getSubset's inner loop: m distinct indices, duplicates redrawn (bounded). */
-static int draw_distinct(Stream* st, int N, int m, int* idx) {
+int draw_distinct(Stream* st, int N, int m, int* idx) {
     for (int i = 0; i < m; ++i) {
         int v = stream_uniform(st, N), tries = 0;
         for (;;) {
@@ -453,9 +448,6 @@ int64_t orc_ransac_replay(const int* counts, int64_t ncounts, int N, int m, doub
     return best;
 }
 
-#define ORC_FLAG_FIXED_ITERS 1
-#define ORC_FLAG_NO_REFINE 2
-#define ORC_FLAG_UNFUSED_ERROR 4
 
 /* cv::findHomography(src, dst, method, thr, mask, maxIters, conf) with the counter-based sampler.
  * pts as fp64 AoS (converted to float as convertTo(CV_32F)). Returns inlier count, 0 on failure. */
@@ -520,7 +512,7 @@ int orc_find_homography(const double* src, const double* dst, int N, double thr,
  * minicv_amd/csrc/hyp_fundamental.h (mean-|dev| normalisation, f22 = 1 elimination, rank 2 by
  * F (I - v v^T) with v from a cyclic 3x3 Jacobi of F^T F).
  * ---------------------------------------------------------------------------------------- */
-static void jacobi3_orc(double* A, double* V) {
+void jacobi3_orc(double* A, double* V) {
     for (int i = 0; i < 9; ++i) V[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
     static const int P[3] = {0, 0, 1}, Q[3] = {1, 2, 2};
     for (int sweep = 0; sweep < 16; ++sweep) {
@@ -646,7 +638,7 @@ int orc_f_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, doubl
 }
 
 /* kind = errorKind * 2 + unfused: 0 Sampson fused, 1 Sampson op-by-op, 2 epipolar fused, 3 epipolar. */
-static float f_err_orc(int kind, const double* F, double x1, double y1, double x2, double y2) {
+float f_err_orc(int kind, const double* F, double x1, double y1, double x2, double y2) {
     if (kind == 0) {
         double ax = fma(F[0], x1, fma(F[1], y1, F[2])), ay = fma(F[3], x1, fma(F[4], y1, F[5]));
         double az = fma(F[6], x1, fma(F[7], y1, F[8]));

@@ -28,6 +28,15 @@ _SIGS = {
     "orc_f_count": (_I, [_P, _I, _P, _F, _I, _P]),
     "orc_f_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _I, _P, _I]),
     "orc_find_fundamental": (_I, [_P, _P, _I, _D, _D, _I, _I, _U64, _I, _I, _P, _P, _P, _I]),
+    "orc_poly_real_roots": (_I, [_P, _I, _P]),
+    "orc_e_solve5": (_I, [_P, _P, _P, _P, _P]),
+    "orc_e_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P]),
+    "orc_e_count": (_I, [_P, _I, _P, _F, _I, _P]),
+    "orc_e_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _I, _P, _I]),
+    "orc_ransac_replay_slots": (_I64, [_P, _I64, _I, _I, _I, _D, _I, _I, _P]),
+    "orc_find_essential": (_I, [_P, _P, _I, _D, _D, _D, _D, _D, _I, _U64, _I, _P, _P, _P, _I]),
+    "orc_e_decompose": (None, [_P, _P, _P, _P]),
+    "orc_recover_pose": (_I, [_P, _P, _I, _D, _D, _D, _P, _P, _P, _P, _P]),
 }
 
 _lib = None
@@ -36,7 +45,8 @@ _lib = None
 def load() -> C.CDLL:
     global _lib
     if _lib is None:
-        if not ORACLE_SO.exists() or ORACLE_SO.stat().st_mtime < (ORACLE_DIR / "oracle.c").stat().st_mtime:
+        srcs = [ORACLE_DIR / n for n in ("oracle.c", "oracle_e.c", "oracle_int.h")]
+        if not ORACLE_SO.exists() or ORACLE_SO.stat().st_mtime < max(p.stat().st_mtime for p in srcs):
             subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
         L = C.CDLL(str(ORACLE_SO))
         for name, (res, args) in _SIGS.items():
@@ -156,3 +166,86 @@ def find_fundamental(a, b, thr=3.0, conf=0.99, max_iters=1000, method=8, seed=0,
     cnt = load().orc_find_fundamental(ptr(a), ptr(b), n, thr, conf, max_iters, method, seed, flags, error_kind,
                                       ptr(F), ptr(mask), ptr(best), nthreads)
     return cnt, F.reshape(3, 3), mask[:n], int(best[0])
+
+
+# ---- essential matrix (oracle_e.c) ---------------------------------------------------------
+E_SLOTS = 10
+
+
+def pack_e(a, b, focal=1.0, pp=(0.0, 0.0)) -> np.ndarray:
+    """double4 normalised correspondences, (x - pp) / focal in fp64 (same as mcv_e_pack)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    ppa = np.asarray(pp, dtype=np.float64)
+    return np.ascontiguousarray(np.concatenate([(a - ppa) / focal, (b - ppa) / focal], axis=1))
+
+
+def poly_real_roots(c):
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    r = np.zeros(10)
+    n = load().orc_poly_real_roots(ptr(c), len(c) - 1, ptr(r))
+    return r[:n]
+
+
+def e_solve5(x1, y1, x2, y2):
+    arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (x1, y1, x2, y2)]
+    E = np.zeros(90)
+    n = load().orc_e_solve5(*[ptr(v) for v in arrs], ptr(E))
+    return E.reshape(10, 3, 3)[:max(n, 0)]
+
+
+def e_hypothesis(pts4d, seed, hyp):
+    E = np.zeros(90)
+    idx = np.full(5, -1, dtype=np.int32)
+    n = load().orc_e_hypothesis(ptr(pts4d), pts4d.shape[0], seed, hyp, ptr(E), ptr(idx))
+    return n, E.reshape(10, 9), idx
+
+
+def e_count(pts4d, E, thr2, kind=0, want_mask=False):
+    E = np.ascontiguousarray(E, dtype=np.float64).ravel()
+    m = np.zeros(pts4d.shape[0], dtype=np.uint8) if want_mask else None
+    n = load().orc_e_count(ptr(pts4d), pts4d.shape[0], ptr(E), thr2, kind, ptr(m) if want_mask else None)
+    return (n, m) if want_mask else n
+
+
+def e_counts(pts4d, seed, begin, count, thr2, kind=0, nthreads=0):
+    out = np.zeros(count * E_SLOTS, dtype=np.int32)
+    load().orc_e_counts(ptr(pts4d), pts4d.shape[0], seed, begin, count, thr2, kind, ptr(out), nthreads)
+    return out
+
+
+def replay_slots(counts, nhyp, n, m, conf, max_iters, fixed, slots=E_SLOTS):
+    counts = np.ascontiguousarray(counts, dtype=np.int32)
+    bc = np.zeros(1, dtype=np.int32)
+    best = load().orc_ransac_replay_slots(ptr(counts), nhyp, slots, n, m, conf, max_iters, int(fixed), ptr(bc))
+    return int(best), int(bc[0])
+
+
+def find_essential(a, b, focal=1.0, pp=(0.0, 0.0), thr=1.0, conf=0.999, max_iters=1000, seed=0, flags=0, nthreads=0):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    n = a.shape[0]
+    E = np.zeros(9)
+    mask = np.zeros(max(n, 1), dtype=np.uint8)
+    best = np.zeros(1, dtype=np.int64)
+    cnt = load().orc_find_essential(ptr(a), ptr(b), n, focal, pp[0], pp[1], thr, conf, max_iters, seed, flags,
+                                    ptr(E), ptr(mask), ptr(best), nthreads)
+    return cnt, E.reshape(3, 3), mask[:n], int(best[0])
+
+
+def e_decompose(E):
+    E = np.ascontiguousarray(E, dtype=np.float64).ravel()
+    R1, R2, t = np.zeros(9), np.zeros(9), np.zeros(3)
+    load().orc_e_decompose(ptr(E), ptr(R1), ptr(R2), ptr(t))
+    return R1.reshape(3, 3), R2.reshape(3, 3), t
+
+
+def recover_pose(a, b, E, mask=None, focal=1.0, pp=(0.0, 0.0)):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    E = np.ascontiguousarray(E, dtype=np.float64).ravel()
+    m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+    R, t, g = np.zeros(9), np.zeros(3), np.zeros(4, dtype=np.int32)
+    res = load().orc_recover_pose(ptr(a), ptr(b), a.shape[0], focal, pp[0], pp[1], ptr(E),
+                                  None if m is None else ptr(m), ptr(R), ptr(t), ptr(g))
+    return res, R.reshape(3, 3), t, g

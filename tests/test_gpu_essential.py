@@ -1,0 +1,170 @@
+"""GPU parity of the essential-matrix path behind the reference's own exports
+cvRecoverPose / cvRecoverPoses / cvFivePoint (MiniCVNative.cpp:165-215, 368-382) and the new
+cvFindEssentialMat, against the oracle (oracle/oracle_e.c).
+Bar: five-point models, per-slot inlier counts, masks and the returned E bit-exact; the pose from
+recoverPose (R, t, cheirality count) bit-exact; plus geometric truth on synthetic two-view data."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from minicv_amd import native as N
+from minicv_amd import opencv, synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+FOCAL, PP = 800.0, (640.0, 360.0)
+
+
+@pytest.fixture(scope="module")
+def torch_dev(gpu):
+    import torch
+    return torch, torch.device("cuda:0")
+
+
+def test_five_point_bit_exact(gpu, oracle):
+    rng = np.random.default_rng(3)
+    for trial in range(60):
+        if trial % 3 == 0:
+            a, b = rng.normal(size=(5, 2)), rng.normal(size=(5, 2))
+        else:
+            a, b, *_ = S.essential_problem(5, seed=trial, outlier_frac=0, sigma=0.0 if trial % 2 else 0.4,
+                                           focal=1.0, pp=(0, 0))
+        Es = opencv.fivepoint(a, b)
+        ref = oracle.e_solve5(a[:, 0], a[:, 1], b[:, 0], b[:, 1])
+        assert len(Es) == len(ref)
+        for e, r in zip(Es, ref):
+            np.testing.assert_array_equal(e, r)
+
+
+def test_five_point_exact_geometry(gpu):
+    a, b, _, R, tu, E = S.essential_problem(5, seed=21, outlier_frac=0, sigma=0, focal=1.0, pp=(0, 0))
+    Es = opencv.fivepoint(a, b)
+    assert min(min(np.abs(e - E).max(), np.abs(e + E).max()) for e in Es) < 1e-8
+
+
+@pytest.mark.parametrize("n,outl,seed,begin,count,unfused", [
+    (5, 0.0, 1, 0, 64, False), (6, 0.3, 2, 0, 100, False), (300, 0.5, 3, 0, 512, False),
+    (2000, 0.5, 4, 123457, 512, False), (1999, 0.6, 5, 0, 256, True), (64, 0.2, 6, 2**28, 300, False)])
+def test_e_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, unfused):
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    a, b, *_ = S.essential_problem(n, seed=seed, outlier_frac=outl)
+    pts = D.pack_essential_tensor(a, b, FOCAL, PP, dev)
+    ref_pts = oracle.pack_e(a, b, FOCAL, PP)
+    np.testing.assert_array_equal(pts.cpu().numpy(), ref_pts)          # normalisation on the GPU
+    plan = D.RansacPlan(N.MODEL_ESSENTIAL, n, count)
+    thr = 1.0 / FOCAL                                                  # device API: normalised units
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(count * N.E_SLOTS, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, begin, count, key, counts)
+    got = counts.cpu().numpy()
+    ref = oracle.e_counts(ref_pts, seed, begin, count, float(np.float32(thr * thr)), 1 if unfused else 0)
+    np.testing.assert_array_equal(got, ref)
+    if (ref >= 5).any() and not (ref == -2).any():
+        c = ref.max()
+        i = int(np.nonzero(ref == c)[0][0])
+        assert int(key[0].item()) == (int(c) << 32) | (0xFFFFFFFF - (begin * N.E_SLOTS + i))
+    plan.close()
+
+
+@pytest.mark.parametrize("n,outl,seed,iters,conf,flags", [
+    (6, 0.0, 1, 1000, 0.999, 0), (50, 0.3, 2, 1000, 0.999, 0), (500, 0.5, 3, 1000, 0.999, 0),
+    (3000, 0.5, 4, 1000, 0.999, 0), (3000, 0.6, 5, 300, 0.999, N.FLAG_FIXED_ITERS),
+    (2000, 0.5, 6, 1000, 0.99, N.FLAG_UNFUSED_ERROR), (20000, 0.5, 7, 1000, 0.999, 0)])
+def test_find_essential_vs_oracle(gpu, oracle, n, outl, seed, iters, conf, flags):
+    a, b, inl, R, tu, E = S.essential_problem(n, seed=seed, outlier_frac=outl)
+    p = opencv.RansacParams(threshold=1.0, confidence=conf, max_iters=iters, seed=seed,
+                            fixed_iters=bool(flags & N.FLAG_FIXED_ITERS),
+                            unfused_error=bool(flags & N.FLAG_UNFUSED_ERROR))
+    cnt, Eg, mask = opencv.findEssentialMat(a, b, FOCAL, PP, p)
+    rc, Er, rmask, best = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=conf, max_iters=iters, seed=seed,
+                                                flags=flags)
+    assert cnt == rc
+    np.testing.assert_array_equal(Eg, Er)
+    np.testing.assert_array_equal(mask, rmask != 0)
+    if n >= 500:
+        assert min(np.abs(Eg - E).max(), np.abs(Eg + E).max()) < 0.15   # best minimal-sample model, no refit
+
+
+def test_find_essential_n5(gpu, oracle):
+    for seed in range(12):
+        a, b, *_ = S.essential_problem(5, seed=seed, outlier_frac=0)
+        ref = oracle.find_essential(a, b, FOCAL, PP)
+        if ref[0] == 5:
+            cnt, Eg, mask = opencv.findEssentialMat(a, b, FOCAL, PP)
+            assert cnt == 5 and mask.all()
+            np.testing.assert_array_equal(Eg, ref[1])
+        else:
+            with pytest.raises(N.NativeError, match="solutions"):
+                opencv.findEssentialMat(a, b, FOCAL, PP)
+
+
+@pytest.mark.parametrize("n,outl,seed,thr", [(200, 0.3, 1, 0.5), (5000, 0.5, 2, 1.0), (30000, 0.4, 3, 2.0)])
+def test_recover_pose_vs_oracle(gpu, oracle, n, outl, seed, thr):
+    a, b, inl, R, tu, E = S.essential_problem(n, seed=seed, outlier_frac=outl, sigma=0.2)
+    cfg = opencv.recoverPoseConfig(FOCAL, PP, 0.999, thr)
+    res, Rg, tg, ms = opencv.recoverPose(cfg, a, b)
+    rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=thr, conf=0.999, max_iters=1000, seed=0)
+    np.testing.assert_array_equal(ms, rmask)                          # ms = RANSAC mask (:206-210)
+    rres, Rr, tr, g = oracle.recover_pose(a, b, Er, rmask, FOCAL, PP)
+    assert res == rres
+    np.testing.assert_array_equal(Rg, Rr)
+    np.testing.assert_array_equal(tg, tr)
+    assert np.abs(Rg - R).max() < 0.03 and np.abs(tg - tu).max() < 0.08
+    assert res > 0.9 * ms.sum()
+
+
+def test_recover_poses_vs_oracle(gpu, oracle):
+    a, b, inl, R, tu, E = S.essential_problem(4000, seed=9, outlier_frac=0.5, sigma=0.2)
+    cfg = opencv.recoverPoseConfig(FOCAL, PP, 0.999, 1.0)
+    R1, R2, t, ms = opencv.recoverPoses(cfg, a, b)
+    rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=0.999, max_iters=1000, seed=0)
+    np.testing.assert_array_equal(ms, rmask)
+    oR1, oR2, ot = oracle.e_decompose(Er)
+    np.testing.assert_array_equal(R1, oR1)
+    np.testing.assert_array_equal(R2, oR2)
+    np.testing.assert_array_equal(t, ot)
+    assert min(np.abs(R1 - R).max(), np.abs(R2 - R).max()) < 0.03
+
+
+def test_recover_poses2_convention(gpu):
+    # NDC-like input of OpenCV.fs:872-909: (x, y) in [-1, 1], y up
+    a, b, inl, R, tu, E = S.essential_problem(2000, seed=4, outlier_frac=0.3, sigma=0.1, focal=400.0, pp=(0, 0))
+    poses, mask = opencv.recoverPoses2(opencv.recoverPoseConfig(1.0, (0, 0), 0.999, 1.0 / 400.0), a / 400.0,
+                                       b / 400.0)
+    assert 1 <= len(poses) <= 2 and mask.sum() > 0.8 * inl.sum()
+
+
+def test_recover_edge_cases(gpu):
+    cfg = opencv.recoverPoseConfig(FOCAL, PP, 0.999, 1.0)
+    a, b, *_ = S.essential_problem(4, seed=1, outlier_frac=0)
+    R1, R2, t, ms = opencv.recoverPoses(cfg, a, b)                     # N < 5: false, outputs untouched
+    np.testing.assert_array_equal(R1, np.eye(3))
+    assert list(t) == [100, 123, 432] and not ms.any()
+    with pytest.raises(N.NativeError, match="at least 5"):
+        opencv.recoverPose(cfg, a, b)
+    # all points identical: every sample is degenerate -> no model
+    a = np.tile([[100.0, 200.0]], (50, 1))
+    b = np.tile([[110.0, 190.0]], (50, 1))
+    R1, R2, t, ms = opencv.recoverPoses(cfg, a, b)
+    assert list(t) == [100, 123, 432] and not ms.any()
+    with pytest.raises(N.NativeError):
+        opencv.recoverPose(cfg, a, b)
+    with pytest.raises(N.NativeError, match="confidence"):
+        opencv.recoverPose(opencv.recoverPoseConfig(FOCAL, PP, 1.5, 1.0), *S.essential_problem(50, seed=2)[:2])
+
+
+def test_raw_export_marshalling(native, gpu):
+    """cvRecoverPose through ctypes exactly like the F# P/Invoke (OpenCV.fs:855-861)."""
+    a, b, *_ = S.essential_problem(500, seed=12, outlier_frac=0.2)
+    cfg = N.RecoverPoseConfig(FOCAL, N.V2d(*PP), 0.999, 1.0)
+    m, t = N.M33d(), N.V3d(100, 123, 432)
+    ms = np.zeros(500, np.uint8)
+    pa, pb = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    res = native.lib().cvRecoverPose(C.addressof(cfg), 500, pa.ctypes.data, pb.ctypes.data, C.addressof(m),
+                                     C.addressof(t), ms.ctypes.data)
+    assert res > 300 and set(np.unique(ms)) <= {0, 1}
+    Rm = np.array(m.M[:]).reshape(3, 3)
+    np.testing.assert_allclose(Rm @ Rm.T, np.eye(3), atol=1e-12)
