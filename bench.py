@@ -31,6 +31,10 @@ HYPS_PER_GPU = 1 << 20
 F_N_CORR = 500_000            # BASELINE config[3]: findFundamentalMat 8-pt, 500k correspondences
 F_HYPS_TOTAL = 1 << 16        # hypotheses per call, sharded over the ranks (strong scaling)
 F_SEED = 4
+E_N_CORR = 100_000            # essential (cvRecoverPose path): not a BASELINE config
+E_HYPS_TOTAL = 1 << 16
+E_SEED = 6
+E_FOCAL, E_PP, E_THR_PX = 800.0, (640.0, 360.0), 1.0
 THR = 5e-3
 SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -54,7 +58,7 @@ def parse():
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="homography", choices=["homography", "fundamental", "hamming", "l2"],
+    ap.add_argument("--workload", default="homography", choices=["homography", "fundamental", "essential", "hamming", "l2"],
                     help="homography = the headline (BASELINE config[2]); the others are config[1], [3], [4]")
     return ap.parse_args()
 
@@ -245,6 +249,9 @@ def bench_ransac(args):
     from minicv_amd import dist as MD
 
     fund = args.workload == "fundamental"
+    ess = args.workload == "essential"
+    if ess:
+        return bench_essential(args, world, rank, dev)
     n, hyps = args.n, args.hyps
     if fund:
         n = args.n if args.n != N_CORR else F_N_CORR
@@ -379,6 +386,121 @@ def bench_ransac(args):
     plan.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_baseline_e(pts4d, target_s: float):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import numpy as np
+    import _oracle as O
+    thr = E_THR_PX / E_FOCAL
+    thr2 = float(np.float32(thr * thr))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    t = time.perf_counter()
+    O.e_counts(pts4d, E_SEED, 0, 2 * threads, thr2, 0, threads)
+    cal = (time.perf_counter() - t) / (2 * threads)
+    sample = max(2 * threads, int(target_s / max(cal, 1e-6)))
+    t = time.perf_counter()
+    O.e_counts(pts4d, E_SEED, 0, sample, thr2, 0, threads)
+    el = time.perf_counter() - t
+    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port",
+            "sample": f"{sample} hypotheses x {pts4d.shape[0]} correspondences (5-pt sample+solve, <= 10 models, "
+                      f"fp64 Sampson count), oracle/oracle_e.c, OpenMP {threads} threads, {el:.1f} s"}
+
+
+def bench_essential(args, world, rank, dev):
+    """E-RANSAC (the cvRecoverPose path): a step = one findEssentialMat RANSAC call over a fixed
+    hypothesis budget on HBM-resident normalised correspondences (hypotheses sharded over ranks,
+    one all-reduce), then the winner's mask and the recoverPose cheirality pass."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from minicv_amd import native as NL, opencv, synthetic as S
+    from minicv_amd import device as D
+    from minicv_amd import dist as MD
+
+    n = args.n if args.n != N_CORR else E_N_CORR
+    hyps = args.hyps if args.hyps != HYPS_PER_GPU else E_HYPS_TOTAL // world
+    total = hyps * world
+    a, b, *_ = S.essential_problem(n, seed=E_SEED, outlier_frac=0.5)
+    pts = D.pack_essential_tensor(a, b, E_FOCAL, E_PP, dev)
+    plan = D.RansacPlan(NL.MODEL_ESSENTIAL, n, hyps)
+    cfg = opencv.RansacParams(threshold=E_THR_PX / E_FOCAL, confidence=0.999, max_iters=total, seed=E_SEED,
+                              fixed_iters=True).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    mask = torch.zeros(n, dtype=torch.uint8, device=dev)
+    red = torch.zeros(2, dtype=torch.int64, device=dev)
+
+    def evaluate(begin, count):
+        plan.evaluate(pts, n, cfg, begin, count, key)
+        k = key.cpu()
+        return int(k[0]), int(k[1])
+
+    def allreduce_max(vals):
+        if world == 1:
+            return vals
+        red.copy_(torch.tensor(vals, dtype=torch.int64))
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+        return [int(v) for v in red.cpu()]
+
+    result = {}
+
+    def step():
+        cnt, slot, _ = MD.global_best(evaluate, total, rank, world, allreduce_max, slots=NL.E_SLOTS)
+        if slot < 0:
+            raise RuntimeError("no model found")
+        fc, E = plan.finalize(pts, n, cfg, slot, mask)
+        result.update(count=cnt, slot=slot, final_count=fc)
+
+    for _ in range(args.warmup):
+        step()
+    NL.lib().mcvProfileReset()
+    NL.lib().mcvProfileEnable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    NL.lib().mcvProfileEnable(0)
+    vms, gms = C.c_double(0), C.c_double(0)
+    vl = NL.lib().mcvProfileRead(b"e_verify", C.addressof(vms))
+    gl = NL.lib().mcvProfileRead(b"e_generate", C.addressof(gms))
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        models = int(result.get("models", 0))
+        v_ms = vms.value / max(vl, 1)
+        g_ms = gms.value / max(gl, 1)
+        line = {
+            "metric": "RANSAC hypotheses/sec, findEssentialMat 5-pt (cvRecoverPose path) @100k corrs",
+            "value": total * args.steps / el, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded calibrated two-view problem, 50% outliers, sigma 0.3 px, f 800)",
+            "config": {"workload": f"findEssentialMat five-point RANSAC, {n} correspondences x {total} hypotheses "
+                                   f"(<= 10 models each) per call sharded over {world} GPU(s)",
+                       "correspondences": n, "hypotheses_total": total, "threshold_px": E_THR_PX,
+                       "parallelism": f"hypothesis-sharded dp{world}"},
+            "kernels": {"mcv_e_generate": {"avg_launch_ms": g_ms, "launches": gl},
+                        "mcv_e_verify": {"avg_launch_ms": v_ms, "launches": vl}},
+            "result": {"best_count": result["count"], "best_slot": result["slot"],
+                       "final_count": result["final_count"]},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, str(ROOT / "tests"))
+            import _oracle as O
+            line["cpu_baseline"] = cpu_baseline_e(O.pack_e(a, b, E_FOCAL, E_PP), args.cpu_seconds)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    plan.close()
 
 
 if __name__ == "__main__":

@@ -30,7 +30,10 @@ static int e_kind(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_UNFUSE
 void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
                       int* d_counts, hipStream_t s) {
     const float thr2 = (float)(cfg.threshold * cfg.threshold);
-    launch_e_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts, s);
+    {
+        ProfScope pg("e_generate", s);
+        launch_e_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts, s);
+    }
     ProfScope ps("e_verify", s);
     launch_e_verify(d_pts, N, P.models.p, P.dslot.p, P.ndense.p, hypCount * kEModelSlots, d_counts, thr2, e_kind(cfg),
                     s);

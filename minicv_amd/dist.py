@@ -33,16 +33,18 @@ def unpack(key: int) -> Tuple[int, int]:
 
 
 def global_best(evaluate: Callable[[int, int], Tuple[int, int]], total: int, rank: int, world: int,
-                allreduce_max: Callable[[list], list]) -> Tuple[int, int, int]:
-    """evaluate(begin, count) -> (key, first_fail) for this rank's range (device work);
-    allreduce_max([a, b]) -> elementwise MAX over ranks. Returns (count, hypIndex, first_fail)."""
+                allreduce_max: Callable[[list], list], slots: int = 1) -> Tuple[int, int, int]:
+    """evaluate(begin, count) -> (key, first_fail) for this rank's range of hypotheses (device work);
+    allreduce_max([a, b]) -> elementwise MAX over ranks. Returns (count, index, first_fail).
+    With multi-model hypotheses (essential: slots = 10) keys, index and first_fail are slot indices
+    (hypothesis h owns slots h * slots .. h * slots + slots - 1)."""
     begin, count = shard(total, rank, world)
     key, fail = evaluate(begin, count) if count > 0 else (0, NO_FAIL)
     g = allreduce_max([key, -fail])
     gkey, gfail = g[0], -g[1]
     cnt, idx = unpack(gkey)
     if gfail != NO_FAIL and idx >= 0 and idx > gfail:
-        end = min(begin + count, gfail)
+        end = min(begin + count, gfail // slots)
         key2, _ = evaluate(begin, end - begin) if end > begin else (0, NO_FAIL)
         g2 = allreduce_max([key2, 0])
         cnt, idx = unpack(g2[0])

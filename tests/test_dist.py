@@ -20,8 +20,9 @@ def _free_port():
     return p
 
 
-def local_key(counts, begin, count, m=4):
-    """What mcv_best_partial/final compute for one rank's range."""
+def local_key(counts, begin, count, m=4, slots=1):
+    """What mcv_best_partial/final compute for one rank's range (slot indices when slots > 1)."""
+    begin, count = begin * slots, count * slots
     seg = counts[begin:begin + count]
     fail = np.nonzero(seg == -2)[0]
     lim = int(fail[0]) if len(fail) else count
@@ -34,7 +35,7 @@ def local_key(counts, begin, count, m=4):
     return (c << 32) | (0xFFFFFFFF - (begin + i)), first_fail
 
 
-def _worker(rank, world, port, counts, q):
+def _worker(rank, world, port, counts, q, m=4, slots=1):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -42,23 +43,23 @@ def _worker(rank, world, port, counts, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def evaluate(begin, count):
-        return local_key(counts, begin, count)
+        return local_key(counts, begin, count, m, slots)
 
     def allreduce_max(vals):
         t = torch.tensor(vals, dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return [int(v) for v in t]
 
-    res = MD.global_best(evaluate, len(counts), rank, world, allreduce_max)
+    res = MD.global_best(evaluate, len(counts) // slots, rank, world, allreduce_max, slots=slots)
     q.put((rank, res))
     dist.destroy_process_group()
 
 
-def run_ranks(world, counts):
+def run_ranks(world, counts, m=4, slots=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, counts, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, counts, q, m, slots)) for r in range(world)]
     for p in ps:
         p.start()
     out = dict(q.get(timeout=120) for _ in ps)
@@ -101,3 +102,23 @@ def test_distributed_sampler_failure_break(oracle):
     out = run_ranks(2, counts)
     for r in range(2):
         assert out[r][0] == bc and out[r][1] == best and out[r][2] == 400
+
+
+def test_distributed_essential_slots(oracle):
+    """Multi-model hypotheses (five-point: <= 10 E per sample): slot-indexed keys over 2 ranks equal
+    the sequential replay, also when a sampler failure truncates the stream."""
+    from minicv_amd import synthetic as S
+    a, b, *_ = S.essential_problem(400, seed=8, outlier_frac=0.5)
+    p = oracle.pack_e(a, b, 800.0, (640.0, 360.0))
+    counts = oracle.e_counts(p, 8, 0, 600, float(np.float32((1.0 / 800.0) ** 2)))
+    best, bc = oracle.replay_slots(counts, 600, 400, 5, 0.999, 600, True)
+    out = run_ranks(2, counts, m=5, slots=10)
+    for r in range(2):
+        assert out[r][0] == bc and out[r][1] == best
+    c2 = counts.copy()
+    c2[10 * 450] = -2
+    c2[10 * 500] = 400           # best after the failure must be ignored
+    best2, bc2 = oracle.replay_slots(c2, 600, 400, 5, 0.999, 600, True)
+    out = run_ranks(2, c2, m=5, slots=10)
+    for r in range(2):
+        assert out[r][0] == bc2 and out[r][1] == best2 and out[r][2] == 4500
