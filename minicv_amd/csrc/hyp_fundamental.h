@@ -224,8 +224,58 @@ MCV_HD int f_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, d
 }
 
 // ---- errors (fp64, cast to float) ----------------------------------------------------------
-// Sampson, fused (default): Fx1 = (fma(f0,x1,fma(f1,y1,f2)), ...), F^T x2 likewise,
-// c = fma(x2, Fx1_0, fma(y2, Fx1_1, Fx1_2)), den = fma(a,a,fma(b,b,fma(g,g,h*h))), e = c*c/den.
+// Sampson numerator c^2 and denominator, fused (default): Fx1 = (fma(f0,x1,fma(f1,y1,f2)), ...),
+// F^T x2 likewise, c = fma(x2, Fx1_0, fma(y2, Fx1_1, Fx1_2)), den = fma(a,a,fma(b,b,fma(g,g,h*h))).
+MCV_HD void f_sampson_parts_fused(const double* F, double x1, double y1, double x2, double y2, double& c2,
+                                  double& den) {
+    const double ax = fma(F[0], x1, fma(F[1], y1, F[2]));
+    const double ay = fma(F[3], x1, fma(F[4], y1, F[5]));
+    const double az = fma(F[6], x1, fma(F[7], y1, F[8]));
+    const double bx = fma(F[0], x2, fma(F[3], y2, F[6]));
+    const double by = fma(F[1], x2, fma(F[4], y2, F[7]));
+    const double c = fma(x2, ax, fma(y2, ay, az));
+    den = fma(ax, ax, fma(ay, ay, fma(bx, bx, by * by)));
+    c2 = c * c;
+}
+
+// Sampson parts, op by op (OpenCV Matx*Vec / dot order).
+MCV_HD void f_sampson_parts(const double* F, double x1, double y1, double x2, double y2, double& c2, double& den) {
+    const double ax = F[0] * x1 + F[1] * y1 + F[2] * 1.;
+    const double ay = F[3] * x1 + F[4] * y1 + F[5] * 1.;
+    const double az = F[6] * x1 + F[7] * y1 + F[8] * 1.;
+    const double bx = F[0] * x2 + F[3] * y2 + F[6] * 1.;
+    const double by = F[1] * x2 + F[4] * y2 + F[7] * 1.;
+    const double c = x2 * ax + y2 * ay + 1. * az;
+    const double a2 = ax * ax, b2 = ay * ay, c2_ = bx * bx, d2 = by * by;
+    den = a2 + b2 + c2_ + d2;
+    c2 = c * c;
+}
+
+// Certified inlier test of a Sampson error without the fp64 division (the sweep's hot path):
+// err = (float)(c2 / den) <= thr2  is decided exactly by
+//   c2 < den * lo  -> inlier,   c2 > den * hi  -> outlier,   otherwise (or den < 2^-960) undecided,
+// with mid = the double midpoint between thr2 and the next float up, lo = mid (1 - 2^-49),
+// hi = mid (1 + 2^-49): a correctly rounded quotient below mid(1 - 2^-50) rounds (to double, then
+// to float) to <= thr2, one above mid(1 + 2^-50) to > thr2, and the products' rounding (2^-53
+// relative while den * lo stays normal) cannot cross those margins. Undecided lanes (probability
+// ~1e-14 per evaluation) take the exact division.
+struct SampsonCut { double lo, hi; };
+static const double kSampsonDenMin = 0x1p-960;
+
+MCV_HD SampsonCut sampson_cut(float thr2) {
+    SampsonCut c;
+    c.lo = -1.0;              // disabled: nothing certified inside ...
+    c.hi = __builtin_inf();   // ... or outside -> every evaluation divides
+    if (!(thr2 >= 0.0f) || !(thr2 <= 1e30f)) return c;
+    const float nx = nextafterf(thr2, __builtin_inff());
+    const double mid = ((double)thr2 + (double)nx) * 0.5;   // exact in fp64
+    if (!(mid >= 0x1p-60)) return c;
+    c.lo = mid * (1.0 - 0x1p-49);
+    c.hi = mid * (1.0 + 0x1p-49);
+    return c;
+}
+
+// Sampson, fused (default): e = (float)(c*c/den).
 MCV_HD float f_err_sampson_fused(const double* F, double x1, double y1, double x2, double y2) {
     const double ax = fma(F[0], x1, fma(F[1], y1, F[2]));
     const double ay = fma(F[3], x1, fma(F[4], y1, F[5]));
@@ -281,6 +331,10 @@ MCV_HD float f_err_epipolar(const double* F, double x1, double y1, double x2, do
     return (float)(e1 < e2 ? e2 : e1);   // std::max(d1*d1*s1, d2*d2*s2)
 }
 
+// Dummy model for padded / invalid sweep slots: den = 1, c^2 >= 1e20 -> certified outlier everywhere.
+MCV_HD double f_dummy_model(int j) { return j == 2 ? 1.0 : (j == 8 ? 1e10 : 0.0); }
+
+
 // Error selector: kind = errorKind * 2 + unfused.
 MCV_HD float f_error(int kind, const double* F, double x1, double y1, double x2, double y2) {
     switch (kind) {
@@ -290,5 +344,32 @@ MCV_HD float f_error(int kind, const double* F, double x1, double y1, double x2,
         default: return f_err_epipolar(F, x1, y1, x2, y2);
     }
 }
+
+#if defined(__HIPCC__)
+// One sweep step for K models at one correspondence per lane: inlier ballots into cnt[k].
+// KIND 0/1 (Sampson) use the certified division-free test with an exact fallback for undecided
+// lanes (wave-uniform branch, rare); KIND 2/3 (epipolar) evaluate f_error directly.
+template <int K, int KIND>
+__device__ __forceinline__ void f_sweep_point(const double (&fm)[K][9], double x1, double y1, double x2, double y2,
+                                              bool v, float thr2, double lo, double hi, uint32_t (&cnt)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if constexpr (KIND <= 1) {
+            double c2, den;
+            if constexpr (KIND == 0) f_sampson_parts_fused(fm[k], x1, y1, x2, y2, c2, den);
+            else f_sampson_parts(fm[k], x1, y1, x2, y2, c2, den);
+            const bool ok = den >= kSampsonDenMin;
+            const bool in = ok && c2 < den * lo;
+            const bool out = ok && c2 > den * hi;
+            const bool amb = v && !(in || out);
+            bool res = v && in;
+            if (__builtin_amdgcn_ballot_w64(amb)) res = res || (amb && (float)(c2 / den) <= thr2);
+            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(res));
+        } else {
+            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(v && f_error(KIND, fm[k], x1, y1, x2, y2) <= thr2));
+        }
+    }
+}
+#endif
 
 }  // namespace mcv

@@ -57,7 +57,7 @@ template <int K, int KIND>
 __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ pts, int N,
                                                     const EModel* __restrict__ dense,
                                                     const int* __restrict__ denseSlot, const int* __restrict__ nDense,
-                                                    int* __restrict__ counts, float thr2) {
+                                                    int* __restrict__ counts, float thr2, double lo, double hi) {
     const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
     const int lane = threadIdx.x & 63;
     const int total = __builtin_amdgcn_readfirstlane(*nDense);
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ 
         const EModel m = dense[valid[k] ? m0 + k : m0];
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
-            em[k][j] = valid[k] ? m.e[j] : __builtin_nan("");
+            em[k][j] = valid[k] ? m.e[j] : f_dummy_model(j);
             asm volatile("" : "+v"(em[k][j]));
         }
     }
@@ -81,18 +81,13 @@ __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ 
     const int nFull = N & ~63;
     for (int base = 0; base < nFull; base += 64) {
         const double4 q = pts[base + lane];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(f_error(KIND, em[k], q.x, q.y, q.z, q.w) <= thr2));
+        f_sweep_point<K, KIND>(em, q.x, q.y, q.z, q.w, true, thr2, lo, hi, cnt);
     }
     if (nFull < N) {
         const int p = nFull + lane;
         const bool v = p < N;
         const double4 q = pts[v ? p : 0];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            cnt[k] += (uint32_t)__popcll(
-                __builtin_amdgcn_ballot_w64(v && f_error(KIND, em[k], q.x, q.y, q.z, q.w) <= thr2));
+        f_sweep_point<K, KIND>(em, q.x, q.y, q.z, q.w, v, thr2, lo, hi, cnt);
     }
     if (lane == 0) {
 #pragma unroll
@@ -173,9 +168,10 @@ void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int
     const int blocks = ((maxModels + K - 1) / K + 3) / 4;
     const double4* p = (const double4*)d_pts4;
     const EModel* m = (const EModel*)d_dense;
+    const SampsonCut c = sampson_cut(thr2);
     switch (kind) {
-        case 0: hipLaunchKernelGGL((mcv_e_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2); break;
-        default: hipLaunchKernelGGL((mcv_e_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2); break;
+        case 0: hipLaunchKernelGGL((mcv_e_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2, c.lo, c.hi); break;
+        default: hipLaunchKernelGGL((mcv_e_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2, c.lo, c.hi); break;
     }
 }
 

@@ -41,7 +41,7 @@ __global__ void mcv_f_one(const float* __restrict__ pts4, int N, uint64_t seed, 
 template <int K, int KIND>
 __global__ __launch_bounds__(256) void mcv_f_verify(const float4* __restrict__ pts, int N,
                                                     const FModelD* __restrict__ models, int* __restrict__ counts,
-                                                    int hypCount, float thr2) {
+                                                    int hypCount, float thr2, double lo, double hi) {
     const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
     const int lane = threadIdx.x & 63;
     const int h0 = wave * K;
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void mcv_f_verify(const float4* __restrict__ p
         const FModelD m = models[valid[k] ? hk : h0];
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
-            fm[k][j] = valid[k] ? m.f[j] : __builtin_nan("");
+            fm[k][j] = valid[k] ? m.f[j] : f_dummy_model(j);
             asm volatile("" : "+v"(fm[k][j]));   // VGPR operands: no constant-bus moves in the fp64 FMAs
         }
     }
@@ -65,20 +65,13 @@ __global__ __launch_bounds__(256) void mcv_f_verify(const float4* __restrict__ p
     const int nFull = N & ~63;
     for (int base = 0; base < nFull; base += 64) {
         const float4 q = pts[base + lane];
-        const double x1 = q.x, y1 = q.y, x2 = q.z, y2 = q.w;
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(f_error(KIND, fm[k], x1, y1, x2, y2) <= thr2));
+        f_sweep_point<K, KIND>(fm, q.x, q.y, q.z, q.w, true, thr2, lo, hi, cnt);
     }
     if (nFull < N) {
         const int p = nFull + lane;
         const bool v = p < N;
         const float4 q = pts[v ? p : 0];
-        const double x1 = q.x, y1 = q.y, x2 = q.z, y2 = q.w;
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            cnt[k] += (uint32_t)__popcll(
-                __builtin_amdgcn_ballot_w64(v && f_error(KIND, fm[k], x1, y1, x2, y2) <= thr2));
+        f_sweep_point<K, KIND>(fm, q.x, q.y, q.z, q.w, v, thr2, lo, hi, cnt);
     }
     if (lane == 0) {
 #pragma unroll
@@ -132,11 +125,12 @@ void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_co
     const int blocks = ((hypCount + K - 1) / K + 3) / 4;
     const float4* p = (const float4*)d_pts4;
     const FModelD* m = (const FModelD*)d_models;
+    const SampsonCut c = sampson_cut(thr2);
     switch (kind) {
-        case 0: hipLaunchKernelGGL((mcv_f_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2); break;
-        case 1: hipLaunchKernelGGL((mcv_f_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2); break;
-        case 2: hipLaunchKernelGGL((mcv_f_verify<K, 2>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2); break;
-        default: hipLaunchKernelGGL((mcv_f_verify<K, 3>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2); break;
+        case 0: hipLaunchKernelGGL((mcv_f_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, c.lo, c.hi); break;
+        case 1: hipLaunchKernelGGL((mcv_f_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, c.lo, c.hi); break;
+        case 2: hipLaunchKernelGGL((mcv_f_verify<K, 2>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, c.lo, c.hi); break;
+        default: hipLaunchKernelGGL((mcv_f_verify<K, 3>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, c.lo, c.hi); break;
     }
 }
 

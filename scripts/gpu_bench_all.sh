@@ -15,3 +15,4 @@ step bench_homography 300 python bench.py --steps 10 --warmup 3 --cpu-seconds 8
 step bench_fundamental 300 python bench.py --workload fundamental --steps 5 --warmup 1 --cpu-seconds 8
 step bench_hamming 300 python bench.py --workload hamming --steps 20 --warmup 3
 step bench_l2 300 python bench.py --workload l2 --steps 5 --warmup 2
+step bench_essential 300 python bench.py --workload essential --steps 5 --warmup 2 --cpu-seconds 8

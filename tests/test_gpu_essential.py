@@ -168,3 +168,37 @@ def test_raw_export_marshalling(native, gpu):
     assert res > 300 and set(np.unique(ms)) <= {0, 1}
     Rm = np.array(m.M[:]).reshape(3, 3)
     np.testing.assert_allclose(Rm @ Rm.T, np.eye(3), atol=1e-12)
+
+
+def test_e_counts_at_exact_threshold_boundary(torch_dev, oracle):
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    from test_gpu_fundamental import _sampson_unfused_np, _thr_for
+    a, b, *_ = S.essential_problem(3000, seed=13, outlier_frac=0.3)
+    p = oracle.pack_e(a, b, FOCAL, PP)
+    n0, E90, _ = oracle.e_hypothesis(p, 13, 0)
+    assert n0 >= 1
+    x = p.astype(np.float64)
+    F = E90[0]
+    ax = F[0] * x[:, 0] + F[1] * x[:, 1] + F[2] * 1.0
+    ay = F[3] * x[:, 0] + F[4] * x[:, 1] + F[5] * 1.0
+    az = F[6] * x[:, 0] + F[7] * x[:, 1] + F[8] * 1.0
+    bx = F[0] * x[:, 2] + F[3] * x[:, 3] + F[6] * 1.0
+    by = F[1] * x[:, 2] + F[4] * x[:, 3] + F[7] * 1.0
+    c = x[:, 2] * ax + x[:, 3] * ay + 1.0 * az
+    err = (c * c / (ax * ax + ay * ay + bx * bx + by * by)).astype(np.float32)
+    pts = D.pack_essential_tensor(a, b, FOCAL, PP, dev)
+    plan = D.RansacPlan(N.MODEL_ESSENTIAL, 3000, 32)
+    for q in (0.2, 0.6):
+        target = np.float32(np.quantile(err, q, method="nearest"))
+        thr = _thr_for(target)
+        for unfused in (True, False):
+            cfg = opencv.RansacParams(threshold=thr, seed=13, unfused_error=unfused).to_c()
+            key = torch.zeros(2, dtype=torch.int64, device=dev)
+            counts = torch.zeros(32 * N.E_SLOTS, dtype=torch.int32, device=dev)
+            plan.evaluate(pts, 3000, cfg, 0, 32, key, counts)
+            ref = oracle.e_counts(p, 13, 0, 32, float(target), 1 if unfused else 0)
+            np.testing.assert_array_equal(counts.cpu().numpy(), ref)
+            if unfused:
+                assert ref[0] == int((err <= target).sum())
+    plan.close()

@@ -98,3 +98,54 @@ def test_fundamental_degenerate(gpu):
         opencv.findFundamentalMat(a, a.copy(), opencv.RansacParams(threshold=0.01))
     with pytest.raises(N.NativeError):
         opencv.findFundamentalMat(a[:7], a[:7])
+
+
+def _sampson_unfused_np(F, p4):
+    """Op-by-op Sampson error exactly as f_err_sampson (numpy float64 has no FMA contraction)."""
+    F = np.asarray(F, dtype=np.float64).ravel()
+    x1, y1, x2, y2 = (p4[:, k].astype(np.float64) for k in range(4))
+    ax = F[0] * x1 + F[1] * y1 + F[2] * 1.0
+    ay = F[3] * x1 + F[4] * y1 + F[5] * 1.0
+    az = F[6] * x1 + F[7] * y1 + F[8] * 1.0
+    bx = F[0] * x2 + F[3] * y2 + F[6] * 1.0
+    by = F[1] * x2 + F[4] * y2 + F[7] * 1.0
+    c = x2 * ax + y2 * ay + 1.0 * az
+    return (c * c / (ax * ax + ay * ay + bx * bx + by * by)).astype(np.float32)
+
+
+def _thr_for(target: np.float32) -> float:
+    """A double thr with (float)(thr * thr) == target."""
+    t = float(np.sqrt(np.float64(target)))
+    for _ in range(200):
+        got = np.float32(t * t)
+        if got == target:
+            return t
+        t = float(np.nextafter(t, np.inf if got < target else -np.inf))
+    raise AssertionError("no threshold maps to the target")
+
+
+@pytest.mark.parametrize("unfused", [True, False])
+def test_f_counts_at_exact_threshold_boundary(torch_dev, oracle, unfused):
+    """Thresholds equal to actual float errors of many points: the certified division-free compare
+    must hand these boundary cases to the exact path (err == thr2 is an inlier)."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    a, b, _, _ = S.fundamental_problem(3000, 12, outlier_frac=0.3)
+    p4 = oracle.pack4(a, b)
+    st, F, _ = oracle.f_hypothesis(p4, 12, 0)
+    assert st == 1
+    err = _sampson_unfused_np(F, p4)
+    pts = D.pack_points_tensor(a, b, dev)
+    plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, 3000, 64)
+    for q in (0.1, 0.5, 0.9):
+        target = np.float32(np.quantile(err, q, method="nearest"))
+        thr = _thr_for(target)
+        cfg = opencv.RansacParams(threshold=thr, seed=12, unfused_error=unfused).to_c()
+        key = torch.zeros(2, dtype=torch.int64, device=dev)
+        counts = torch.zeros(64, dtype=torch.int32, device=dev)
+        plan.evaluate(pts, 3000, cfg, 0, 64, key, counts)
+        ref = oracle.f_counts(p4, 12, 0, 64, float(target), oracle.f_kind(0, unfused))
+        np.testing.assert_array_equal(counts.cpu().numpy(), ref)
+        if unfused:
+            assert ref[0] == int((err <= target).sum())
+    plan.close()
