@@ -67,6 +67,8 @@ void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBe
                        int* d_denseSlot, int* d_nDense, int* d_counts, hipStream_t s);
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
                      int maxModels, int* d_counts, float thr2, int kind, hipStream_t s);
+void launch_e_fetch(const void* d_dense, const int* d_denseSlot, const int* d_nDense, int maxModels, int slot,
+                    void* d_out, int* d_found, hipStream_t s);
 void launch_e_one(const double* d_pts4, int N, uint64_t seed, int64_t hyp, EOneOut* d_out, hipStream_t s);
 void launch_e_mask(const double* d_pts4, int N, const double* E9, float thr2, int kind, uint8_t* d_mask, int* d_count,
                    hipStream_t s);

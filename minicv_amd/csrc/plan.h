@@ -37,7 +37,11 @@ struct Plan {
     DevBuf<double> ptsd;      // essential: double4 normalised correspondences
     DevBuf<double> raw;       // essential: uploaded V2d pairs (a then b)
     DevBuf<int> dslot;        // essential: slot of each dense model
-    DevBuf<int> ndense;       // essential: dense model count (+ 4 cheirality counters)
+    DevBuf<int> ndense;       // essential: dense model count, 4 cheirality counters, fetch flag
+    int64_t eLastBegin = -1;  // essential: hypothesis range of the dense list's last chunk
+    int64_t eLastCount = 0;
+    uint64_t eLastSeed = 0;
+    const void* eLastPts = nullptr;
     PinnedBuf<int> h_counts;
     PinnedBuf<double> h_red;
     PinnedBuf<float> h_pack;

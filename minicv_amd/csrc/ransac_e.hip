@@ -96,6 +96,18 @@ __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ 
     }
 }
 
+// Winner's model straight from the dense list of the last evaluated chunk (slot -> model), instead
+// of a single-lane five-point re-solve (the same code produced it, so the model is identical).
+__global__ __launch_bounds__(256) void mcv_e_fetch(const EModel* __restrict__ dense, const int* __restrict__ denseSlot,
+                                                   const int* __restrict__ nDense, int slot,
+                                                   EModel* __restrict__ out, int* __restrict__ found) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < *nDense && denseSlot[i] == slot) {
+        *out = dense[i];
+        *found = 1;
+    }
+}
+
 __global__ void mcv_e_one(const double* __restrict__ pts4, int N, uint64_t seed, int64_t hyp,
                           EOneOut* __restrict__ out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -173,6 +185,13 @@ void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int
         case 0: hipLaunchKernelGGL((mcv_e_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2, c.lo, c.hi); break;
         default: hipLaunchKernelGGL((mcv_e_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2, c.lo, c.hi); break;
     }
+}
+
+void launch_e_fetch(const void* d_dense, const int* d_denseSlot, const int* d_nDense, int maxModels, int slot,
+                    void* d_out, int* d_found, hipStream_t s) {
+    (void)hipMemsetAsync(d_found, 0, sizeof(int), s);
+    hipLaunchKernelGGL(mcv_e_fetch, dim3((maxModels + 255) / 256), dim3(256), 0, s, (const EModel*)d_dense,
+                       d_denseSlot, d_nDense, slot, (EModel*)d_out, d_found);
 }
 
 void launch_e_one(const double* d_pts4, int N, uint64_t seed, int64_t hyp, EOneOut* d_out, hipStream_t s) {

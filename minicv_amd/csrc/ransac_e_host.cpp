@@ -34,6 +34,10 @@ void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& c
         ProfScope pg("e_generate", s);
         launch_e_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts, s);
     }
+    P.eLastBegin = hypBegin;
+    P.eLastCount = hypCount;
+    P.eLastSeed = cfg.seed;
+    P.eLastPts = d_pts;
     ProfScope ps("e_verify", s);
     launch_e_verify(d_pts, N, P.models.p, P.dslot.p, P.ndense.p, hypCount * kEModelSlots, d_counts, thr2, e_kind(cfg),
                     s);
@@ -66,9 +70,26 @@ int e_finalize(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int
                uint8_t* d_mask, hipStream_t s) {
     const int64_t hyp = slot / kEModelSlots;
     const int k = (int)(slot % kEModelSlots);
-    const EOneOut one = e_one(P, d_pts, N, cfg.seed, hyp, s);
-    if (one.status <= k) fail("winning slot %lld has no model (status %d)", (long long)slot, one.status);
-    for (int j = 0; j < 9; ++j) E[j] = one.E[k][j];
+    bool have = false;
+    if (hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount && P.eLastSeed == cfg.seed && P.eLastPts == d_pts) {
+        const int local = (int)((hyp - P.eLastBegin) * kEModelSlots + k);
+        int* d_found = P.ndense.p + 7;
+        uint8_t* d_out = P.one.p;
+        launch_e_fetch(P.models.p, P.dslot.p, P.ndense.p, (int)(P.eLastCount * kEModelSlots), local, d_out, d_found, s);
+        MCV_HIP(hipGetLastError());
+        MCV_HIP(hipMemcpyAsync(P.h_one.p, d_out, 9 * sizeof(double), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipMemcpyAsync(P.h_i.p, d_found, sizeof(int), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        if (P.h_i.p[0] == 1) {
+            std::memcpy(E, P.h_one.p, 9 * sizeof(double));
+            have = true;
+        }
+    }
+    if (!have) {
+        const EOneOut one = e_one(P, d_pts, N, cfg.seed, hyp, s);
+        if (one.status <= k) fail("winning slot %lld has no model (status %d)", (long long)slot, one.status);
+        for (int j = 0; j < 9; ++j) E[j] = one.E[k][j];
+    }
     return e_mask_count(P, d_pts, N, cfg, E, d_mask, s);
 }
 
