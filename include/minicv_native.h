@@ -92,18 +92,29 @@ MCV_API void cvTest(void);
 /* Five-point minimal solver — MiniCVNative.cpp:368-382 / fivepoint.cpp:233-339 (one GPU solve):
  * Es: caller-allocated 10 x M33d, unit-Frobenius-norm E with pb^T E pa = 0. Returns the count. */
 MCV_API int  cvFivePoint(const mcvV2d* pa, const mcvV2d* pb, mcvM33d* Es);
-/* PnP — MiniCVNative.cpp:48-163 (next row f2). K passed by value as in the reference. */
+/* PnP — MiniCVNative.cpp:48-163 (on the GPU). K passed by value as in the
+ * reference; distortion = 4 doubles (k1, k2, p1, p2; MiniCVNative.cpp:78,120).
+ * cvSolvePnPRansac: 4-point AP3P minimal sets (every solverKind; OpenCV uses EPnP with 5 points
+ * for kinds 0/1/3/4 — DESIGN.md §3), fp32 reprojection error of projectPoints, inlier iff
+ * err <= reprojectionError^2, sequential-RANSAC semantics with seed 0; then Levenberg-Marquardt
+ * on the inliers from the best hypothesis. outInliers (caller: N ints) = RANSAC inlier indices.
+ * cvSolvePnP: kinds 2/5 (P3P/AP3P) need N == 4 (AP3P, the 4th point picks the solution); other
+ * kinds: AP3P-RANSAC initialisation (256 hypotheses, 4 px) + LM over all points. */
 MCV_API bool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                         const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec);
 MCV_API bool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                               const double* distortionCoeffs, const int solverKind, const int iterationsCount,
                               const float reprojectionError, const double confidence, mcvV3d* tVec, mcvV3d* rVec,
                               int* inlierCount, int* outInliers);
+/* In/out pose (t, r): 20 LM iterations over all points (solvePnPRefineLM) / 20 VVS iterations with
+ * lambda 1 on the normalised image plane (solvePnPRefineVVS). */
 MCV_API void cvRefinePnPLM(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                            const double* distortionCoeffs, mcvV3d* tVec, mcvV3d* rVec);
 MCV_API void cvRefinePnPVVS(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                             const double* distortionCoeffs, mcvV3d* tVec, mcvV3d* rVec);
-/* AP3P — ap3p.cpp:282-317 (next row f2). */
+/* AP3P — ap3p.cpp:282-317, float arguments as the F# P/Invoke passes them (OpenCV.fs:373-374;
+ * the reference's C++ definition takes doubles — an ABI mismatch in the reference). Rs/ts:
+ * caller arrays of 4; R as the reference returns it (ap3p.cpp:245-250). Returns the count. */
 MCV_API int  solveAp3p(mcvM33d* Rs, mcvV3d* ts, float mu0, float mv0, float X0, float Y0, float Z0,
                        float mu1, float mv1, float X1, float Y1, float Z1,
                        float mu2, float mv2, float X2, float Y2, float Z2,
@@ -163,6 +174,11 @@ MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, const int N, 
 MCV_API int cvFindEssentialMat(const mcvV2d* a, const mcvV2d* b, const int N, double focal, mcvV2d pp,
                                const RansacConfig* cfg, mcvM33d* E, uint8_t* mask);
 
+/* cvSolvePnPRansac with a full RansacConfig (threshold = reprojection error in pixels; seed, fixed iterations, unfused error, NO_REFINE). */
+MCV_API bool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+                                 const double* distortionCoeffs, const RansacConfig* cfg, mcvV3d* tVec, mcvV3d* rVec,
+                                 int* inlierCount, int* outInliers);
+
 /* Brute-force Hamming matcher (BFMatcher NORM_HAMMING, knn k = 2). q: [nq][bytesPerDesc],
  * t: [nt][bytesPerDesc] row-major bytes; bytesPerDesc in [1, 64]; nt < 2^22.
  * Outputs per query: best train index / distance and second best (idx2/dist2 may be NULL;
@@ -193,6 +209,10 @@ typedef struct mcvRansacPlan_ mcvRansacPlan;
 #define MCV_MODEL_ESSENTIAL    2   /* points: double4 {x1, y1, x2, y2} normalised (mcvPackEssential);
                                       hypothesis h owns model slots 10h .. 10h+9: keys, counts and
                                       indices below are slot indices for this model */
+#define MCV_MODEL_PNP          3   /* points: PnpPoint {X, Y, Z, u, v, pad[3]} fp32 (mcvPackPnP); camera
+                                      via mcvRansacPlanSetCamera; threshold in pixels; finalize
+                                      writes model9 = {rvec[3], tvec[3], 0, 0, 0} (LM-refined unless
+                                      MCV_FLAG_NO_REFINE) */
 
 /* Workspace for problems up to maxN correspondences and maxHyps hypotheses per evaluate call. */
 MCV_API mcvRansacPlan* mcvRansacPlanCreate(int model, int maxN, int64_t maxHyps);
@@ -200,6 +220,11 @@ MCV_API void mcvRansacPlanDestroy(mcvRansacPlan* plan);
 
 /* Pack host AoS fp64 pairs into the device float4 layout (synchronous H2D on `stream`). */
 MCV_API int mcvPackCorrespondences(const mcvV2d* a, const mcvV2d* b, int N, float* d_pts4, void* stream);
+/* PnP model: upload image V2d[N] + world V3d[N] and pack them on the device (32 B each). */
+MCV_API int mcvPackPnP(const mcvV2d* img, const mcvV3d* world, int N, void* d_pts, void* stream);
+/* PnP plans: camera matrix (row-major 3x3; fx = K[0], fy = K[4], cx = K[2], cy = K[5]) and
+ * distortion (k1, k2, p1, p2; NULL = none). */
+MCV_API int mcvRansacPlanSetCamera(mcvRansacPlan* plan, const double* K9, const double* dist4);
 /* Essential model: upload host pairs and normalise on the device into double4 (32 B each). */
 MCV_API int mcvPackEssential(const mcvV2d* a, const mcvV2d* b, int N, double focal, mcvV2d pp, double* d_pts4,
                              void* stream);
@@ -269,6 +294,12 @@ MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models
 MCV_API int mcvHostEssential(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90, int* sampleIdx);
 MCV_API int mcvHostFivePoint(const double* p20, double* E90);
 MCV_API void mcvHostDecomposeEssential(const double* E9, double* R1, double* R2, double* t3);
+/* Host twins of the PnP path: one hypothesis on packed PnpPoint[N] (cam8 = fx, fy, cx, cy, k1, k2,
+ * p1, p2), and the Rodrigues maps used by the LM refit. */
+MCV_API int mcvHostPnP(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9, double* t3,
+                       int* idx4);
+MCV_API void mcvHostRodrigues(const double* r, double* R, double* dR27);
+MCV_API void mcvHostRodriguesInv(const double* R, double* r);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                            uint32_t* out4);
 

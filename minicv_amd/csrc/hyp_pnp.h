@@ -1,0 +1,257 @@
+// hyp_pnp.h — per-hypothesis code of the PnP-RANSAC path behind
+// cvSolvePnPRansac / cvSolvePnP / solveAp3p (MiniCVNative.cpp:48-139, ap3p.cpp:282-317).
+// Compiled for gfx950 (ransac_pnp.hip) and for the host (mcvHostPnP* test hooks) with
+// -ffp-contract=off: +,-,*,/ and sqrt round identically on both sides.
+//
+// Restated behaviour:
+//  * AP3P (Ke & Roumeliotis, CVPR 2017) exactly as the reference's computePoses
+//    (ap3p.cpp:123-255): bearing vectors, the f1i / f2i / g1..g7 terms, the quartic in
+//    cos(theta1'), C13, R = Ck1nl C13 Cb1k3tz^T, t = sin(theta1') b3' - R^T w3. The quartic's real
+//    roots come from e_poly_real_roots (derivative-interval bisection, hyp_essential.h) instead
+//    of solveQuartic's complex Ferrari formulas + polishQuarticRoots (ap3p.cpp:10-74): those use
+//    complex sqrt / cbrt / pow, whose last bits differ between libm and the GPU's ocml, and they
+//    return the real parts of complex roots as spurious candidates.
+//  * Camera-from-world rotation of a solution is R^T (OpenCV's ap3p stores the transpose;
+//    the reference's solveAp3p export returns R itself, ap3p.cpp:245-250 — kept for that export).
+//  * OpenCV 4.x solvePnPRansac / PnPRansacCallback [ext]: 4-point minimal sets for P3P / AP3P
+//    (the first three solve, the fourth picks the solution of least reprojection error), image
+//    points undistorted first (undistortPoints, 5 fixed iterations), error = squared pixel
+//    distance between the observed point and projectPoints (k1, k2, p1, p2 model, fp64 inside,
+//    fp32 output), inlier iff err <= (float)thr^2 (thr is a float: the reference's
+//    reprojectionError argument).
+#pragma once
+
+#include "mcv_common.h"
+#include "hyp_essential.h"   // e_poly_real_roots
+
+namespace mcv {
+
+static const int kPnpMaxSolutions = 4;
+static const int kUndistortIters = 5;
+
+// Camera: K (fx, fy, cx, cy; skew ignored as projectPoints does) + distortion (k1, k2, p1, p2).
+struct PnpCamera { double fx, fy, cx, cy, k1, k2, p1, p2; };
+
+// Pose: X_cam = R X_world + t (row-major R).
+struct PnpPose { double R[9]; double t[3]; };
+
+// undistortPoints (OpenCV cvUndistortPointsInternal, fixed 5 iterations) -> normalised (x, y).
+MCV_HD void pnp_undistort(const PnpCamera& c, double u, double v, double& x, double& y) {
+    const double x0 = (u - c.cx) / c.fx, y0 = (v - c.cy) / c.fy;
+    x = x0;
+    y = y0;
+    for (int it = 0; it < kUndistortIters; ++it) {
+        const double r2 = x * x + y * y;
+        const double icdist = 1.0 / (1.0 + (c.k2 * r2 + c.k1) * r2);
+        if (icdist < 0) { x = x0; y = y0; break; }
+        const double dx = 2.0 * c.p1 * x * y + c.p2 * (r2 + 2.0 * x * x);
+        const double dy = c.p1 * (r2 + 2.0 * y * y) + 2.0 * c.p2 * x * y;
+        x = (x0 - dx) * icdist;
+        y = (y0 - dy) * icdist;
+    }
+}
+
+// projectPoints for one point (k1, k2, p1, p2): pixel (u, v) in fp64, returned as float like the
+// CV_32F projpoints of PnPRansacCallback::computeError. Returns false if Zc == 0 (OpenCV then
+// divides by 1; here the point is an outlier).
+MCV_HD void pnp_project(const PnpCamera& c, const double* R, const double* t, double X, double Y, double Z,
+                        double& u, double& v) {
+    const double Xc = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    const double Yc = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    const double Zc = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    const double iz = Zc != 0 ? 1.0 / Zc : 1.0;
+    const double x = Xc * iz, y = Yc * iz;
+    const double r2 = x * x + y * y, r4 = r2 * r2;
+    const double a1 = 2.0 * x * y, a2 = r2 + 2.0 * x * x, a3 = r2 + 2.0 * y * y;
+    const double cdist = 1.0 + c.k1 * r2 + c.k2 * r4;
+    const double xd = x * cdist + c.p1 * a1 + c.p2 * a2;
+    const double yd = y * cdist + c.p1 * a3 + c.p2 * a1;
+    u = xd * c.fx + c.cx;
+    v = yd * c.fy + c.cy;
+}
+
+// Reprojection error: float observed point minus the float projection, squared norm in fp32
+// (fused: fmaf(dx, dx, dy * dy); unfused: dx * dx + dy * dy).
+MCV_HD float pnp_error(const PnpCamera& c, const double* R, const double* t, float X, float Y, float Z, float uo,
+                       float vo, bool fused) {
+    double u, v;
+    pnp_project(c, R, t, X, Y, Z, u, v);
+    const float dx = uo - (float)u, dy = vo - (float)v;
+#if defined(__HIP_DEVICE_COMPILE__)
+    return fused ? __builtin_fmaf(dx, dx, dy * dy) : dx * dx + dy * dy;
+#else
+    return fused ? fmaf(dx, dx, dy * dy) : dx * dx + dy * dy;
+#endif
+}
+
+// ---- AP3P (reference computePoses, restated) --------------------------------------------------
+MCV_HD void v3_cross(const double* a, const double* b, double* r) {
+    r[0] = a[1] * b[2] - a[2] * b[1];
+    r[1] = -(a[0] * b[2] - a[2] * b[0]);
+    r[2] = a[0] * b[1] - a[1] * b[0];
+}
+MCV_HD double v3_dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+MCV_HD double v3_norm(const double* a) { return sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
+
+// b[3][3]: bearing vectors (unit) b1, b2, b3; w[3][3]: world points. Outputs up to 4 solutions
+// (Rr = the reference's R, row-major; tr = translation). Returns the count.
+MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3]) {
+    const double* w1 = w[0];
+    const double* w2 = w[1];
+    const double* w3 = w[2];
+    const double* b1 = b[0];
+    const double* b2 = b[1];
+    const double* b3 = b[2];
+    double u0[3] = {w1[0] - w2[0], w1[1] - w2[1], w1[2] - w2[2]};
+    const double nu0 = v3_norm(u0);
+    double k1[3] = {u0[0] / nu0, u0[1] / nu0, u0[2] / nu0};
+    double k3[3];
+    v3_cross(b1, b2, k3);
+    const double nk3 = v3_norm(k3);
+    k3[0] = k3[0] / nk3; k3[1] = k3[1] / nk3; k3[2] = k3[2] / nk3;
+    double tz[3], v1[3], v2[3];
+    v3_cross(b1, k3, tz);
+    v3_cross(b1, b3, v1);
+    v3_cross(b2, b3, v2);
+    double u1[3] = {w1[0] - w3[0], w1[1] - w3[1], w1[2] - w3[2]};
+    const double u1k1 = v3_dot(u1, k1);
+    const double k3b3 = v3_dot(k3, b3);
+    double f11 = k3b3;
+    double f13 = v3_dot(k3, v1);
+    const double f15 = -u1k1 * f11;
+    double nl[3];
+    v3_cross(u1, k1, nl);
+    const double delta = v3_norm(nl);
+    nl[0] = nl[0] / delta; nl[1] = nl[1] / delta; nl[2] = nl[2] / delta;
+    f11 = f11 * delta;
+    f13 = f13 * delta;
+    const double u2k1 = u1k1 - nu0;
+    double f21 = v3_dot(tz, v2);
+    double f22 = nk3 * k3b3;
+    double f23 = v3_dot(k3, v2);
+    const double f24 = u2k1 * f22;
+    const double f25 = -u2k1 * f21;
+    f21 = f21 * delta;
+    f22 = f22 * delta;
+    f23 = f23 * delta;
+    const double g1 = f13 * f22;
+    const double g2 = f13 * f25 - f15 * f23;
+    const double g3 = f11 * f23 - f13 * f21;
+    const double g4 = -f13 * f24;
+    const double g5 = f11 * f22;
+    const double g6 = f11 * f25 - f15 * f21;
+    const double g7 = -f15 * f24;
+    // quartic a4 s^4 + a3 s^3 + a2 s^2 + a1 s + a0, stored ascending for the root finder
+    double c[5];
+    c[4] = g5 * g5 + g1 * g1 + g3 * g3;
+    c[3] = 2 * (g5 * g6 + g1 * g2 + g3 * g4);
+    c[2] = g6 * g6 + 2 * g5 * g7 + g2 * g2 + g4 * g4 - g1 * g1 - g3 * g3;
+    c[1] = 2 * (g6 * g7 - g1 * g2 - g3 * g4);
+    c[0] = g7 * g7 - g2 * g2 - g4 * g4;
+    bool finite = true;
+    for (int k = 0; k < 5; ++k) finite = finite && isfinite(c[k]);
+    if (!finite || !isfinite(delta) || !isfinite(k3b3) || !(nk3 > 0) || !(nu0 > 0) || !(delta > 0)) return 0;
+    double s[10];
+    const int ns = e_poly_real_roots(c, 4, s);
+    double temp[3];
+    v3_cross(k1, nl, temp);
+    const double Ck1nl[9] = {k1[0], nl[0], temp[0], k1[1], nl[1], temp[1], k1[2], nl[2], temp[2]};
+    const double Cb1k3tzT[9] = {b1[0], b1[1], b1[2], k3[0], k3[1], k3[2], tz[0], tz[1], tz[2]};
+    const double sc = delta / k3b3;
+    const double b3p[3] = {b3[0] * sc, b3[1] * sc, b3[2] * sc};
+    int n = 0;
+    for (int i = 0; i < ns && n < kPnpMaxSolutions; ++i) {
+        const double ct1 = s[i];
+        if (fabs(ct1) > 1) continue;
+        double st1 = sqrt(1 - ct1 * ct1);
+        st1 = (k3b3 > 0) ? st1 : -st1;
+        double ct3 = g1 * ct1 + g2;
+        double st3 = g3 * ct1 + g4;
+        const double nt3 = st1 / ((g5 * ct1 + g6) * ct1 + g7);
+        ct3 = ct3 * nt3;
+        st3 = st3 * nt3;
+        const double C13[9] = {ct3, 0, -st3, st1 * st3, ct1, st1 * ct3, ct1 * st3, -st1, ct1 * ct3};
+        double T[9], R[9];
+        for (int r = 0; r < 3; ++r)
+            for (int q = 0; q < 3; ++q)
+                T[3 * r + q] = Ck1nl[3 * r] * C13[q] + Ck1nl[3 * r + 1] * C13[3 + q] + Ck1nl[3 * r + 2] * C13[6 + q];
+        for (int r = 0; r < 3; ++r)
+            for (int q = 0; q < 3; ++q)
+                R[3 * r + q] = T[3 * r] * Cb1k3tzT[q] + T[3 * r + 1] * Cb1k3tzT[3 + q] + T[3 * r + 2] * Cb1k3tzT[6 + q];
+        const double rp3[3] = {w3[0] * R[0] + w3[1] * R[3] + w3[2] * R[6], w3[0] * R[1] + w3[1] * R[4] + w3[2] * R[7],
+                               w3[0] * R[2] + w3[1] * R[5] + w3[2] * R[8]};
+        bool ok = isfinite(nt3);
+        for (int k = 0; k < 9; ++k) { Rr[n][k] = R[k]; ok = ok && isfinite(R[k]); }
+        for (int k = 0; k < 3; ++k) { tr[n][k] = st1 * b3p[k] - rp3[k]; ok = ok && isfinite(tr[n][k]); }
+        if (ok) ++n;
+    }
+    return n;
+}
+
+// Bearing vector of a normalised image point (x, y): (x, y, 1) / |(x, y, 1)| as the reference
+// builds it (ap3p.cpp:285-301: mk = 1 / norm, then mu *= mk, mv *= mk).
+MCV_HD void pnp_bearing(double x, double y, double* b) {
+    const double nrm = sqrt(x * x + y * y + 1);
+    const double mk = 1. / nrm;
+    b[0] = x * mk;
+    b[1] = y * mk;
+    b[2] = mk;
+}
+
+// Four-point AP3P pose: points 0..2 solve, point 3 (pixel reprojection error, distortion-free on
+// the undistorted point) picks the solution; first minimum on ties. x/y: undistorted normalised
+// image coordinates; W: world points. Returns 1 and the camera-from-world pose, or 0.
+MCV_HD int pnp_ap3p4(const PnpCamera& c, const double* x, const double* y, const double (*W)[3], PnpPose& pose) {
+    double b[3][3], w[3][3];
+    for (int i = 0; i < 3; ++i) {
+        pnp_bearing(x[i], y[i], b[i]);
+        for (int k = 0; k < 3; ++k) w[i][k] = W[i][k];
+    }
+    double Rr[kPnpMaxSolutions][9], tr[kPnpMaxSolutions][3];
+    const int n = ap3p_compute_poses(b, w, Rr, tr);
+    if (n == 0) return 0;
+    int best = 0;
+    double bestErr = 0;
+    for (int i = 0; i < n; ++i) {
+        // camera-from-world rotation = Rr^T
+        const double* R = Rr[i];
+        const double X = R[0] * W[3][0] + R[3] * W[3][1] + R[6] * W[3][2] + tr[i][0];
+        const double Y = R[1] * W[3][0] + R[4] * W[3][1] + R[7] * W[3][2] + tr[i][1];
+        const double Z = R[2] * W[3][0] + R[5] * W[3][1] + R[8] * W[3][2] + tr[i][2];
+        const double du = c.fx * (X / Z - x[3]);
+        const double dv = c.fy * (Y / Z - y[3]);
+        const double e = du * du + dv * dv;
+        if (i == 0 || bestErr > e) { best = i; bestErr = e; }
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q) pose.R[3 * r + q] = Rr[best][3 * q + r];
+    for (int k = 0; k < 3; ++k) pose.t[k] = tr[best][k];
+    return 1;
+}
+
+// Packed PnP correspondence on the device: float4 {X, Y, Z, u} + float4 {v, 0, 0, 0} (32 B),
+// fp32 as solvePnPRansac's convertTo(CV_32F).
+struct PnpPoint { float X, Y, Z, u, v, pad0, pad1, pad2; };
+
+// One hypothesis: 4 distinct indices (Philox stream), undistort, AP3P + 4th-point selection.
+// Returns 1 (model), kStatusNoModel or kStatusNoSample.
+MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, uint64_t seed, uint64_t hyp, PnpPose& pose,
+                          int* idx_out) {
+    HypStream rs;
+    rs.init(seed, hyp);
+    int idx[4];
+    for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
+        if (!draw_distinct<4>(rs, N, idx)) continue;
+        double x[4], y[4], W[4][3];
+        for (int i = 0; i < 4; ++i) {
+            const PnpPoint p = pts[idx[i]];
+            pnp_undistort(c, (double)p.u, (double)p.v, x[i], y[i]);
+            W[i][0] = p.X; W[i][1] = p.Y; W[i][2] = p.Z;
+        }
+        if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
+        return pnp_ap3p4(c, x, y, W, pose) ? 1 : kStatusNoModel;
+    }
+    return kStatusNoSample;
+}
+
+}  // namespace mcv

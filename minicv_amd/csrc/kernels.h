@@ -76,6 +76,36 @@ void launch_e_cheirality(const double* d_pts4, int N, const uint8_t* d_mask, con
                          int* d_good4, hipStream_t s);
 void launch_e_fivepoint(const EFiveIn& in, EOneOut* d_out, hipStream_t s);
 
+// ---- PnP (ransac_pnp.hip); cam8 = {fx, fy, cx, cy, k1, k2, p1, p2}
+static const int kVerifyPnpPosesPerWave = 4;
+struct PnpOneOut {
+    double R[9];
+    double t[3];
+    int status;
+    int idx[4];
+};
+struct Ap3pIn { double mu[3], mv[3], W[3][3], inv_fx, inv_fy, cx_fx, cy_fy; };
+struct Ap3pOut {
+    double R[4][9];
+    double t[4][3];
+    int count;
+};
+void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_pts, hipStream_t s);
+void launch_pnp_generate(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin, int hypCount,
+                         void* d_models, int* d_counts, hipStream_t s);
+void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
+                       float thr2, bool fused, hipStream_t s);
+void launch_pnp_one(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hyp, PnpOneOut* d_out,
+                    hipStream_t s);
+void launch_pnp_solve4(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s);
+void launch_pnp_mask(const void* d_pts, int N, const double* cam8, const double* R9, const double* t3, float thr2,
+                     bool fused, uint8_t* d_mask, int* d_count, hipStream_t s);
+void launch_pnp_ap3p(const Ap3pIn& in, Ap3pOut* d_out, hipStream_t s);
+void pnp_reduce_lm(const void* d_pts, int N, const uint8_t* d_mask, const double* cam8, const double* R9,
+                   const double* t3, const double* dR27, bool wantJ, double* d_part, double* d_out, hipStream_t s);
+void pnp_reduce_vvs(const void* d_pts, int N, const uint8_t* d_mask, const double* cam8, const double* R9,
+                    const double* t3, double* d_part, double* d_out, hipStream_t s);
+
 // ---- shared (ransac_h.hip)
 void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uint64_t* d_pkey, int64_t* d_pfail,
                  uint64_t* d_out, hipStream_t s);

@@ -38,6 +38,7 @@ struct Plan {
     DevBuf<double> raw;       // essential: uploaded V2d pairs (a then b)
     DevBuf<int> dslot;        // essential: slot of each dense model
     DevBuf<int> ndense;       // essential: dense model count, 4 cheirality counters, fetch flag
+    double pnpCam[8] = {1, 1, 0, 0, 0, 0, 0, 0};   // PnP: fx, fy, cx, cy, k1, k2, p1, p2
     int64_t eLastBegin = -1;  // essential: hypothesis range of the dense list's last chunk
     int64_t eLastCount = 0;
     uint64_t eLastSeed = 0;
@@ -99,6 +100,12 @@ int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
                hipStream_t s);
 int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F);
 int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F9, float* Ff9, int* sampleIdx);
+
+// PnP family (ransac_pnp.hip / pnp_host.cpp)
+void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
+                      int* d_counts, hipStream_t s);
+int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
+               uint8_t* d_mask, hipStream_t s);
 
 // essential-matrix family (ransac_e.hip / ransac_e_host.cpp)
 void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,

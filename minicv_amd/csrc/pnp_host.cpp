@@ -1,0 +1,496 @@
+// pnp_host.cpp — host side of the PnP path behind the reference's exports
+// cvSolvePnPRansac, cvSolvePnP, cvRefinePnPLM, cvRefinePnPVVS, solveAp3p
+// (MiniCVNative.cpp:48-163, ap3p.cpp:282-317) plus cvSolvePnPRansacCfg.
+//
+// solvePnPRansac (OpenCV 4.x, restated [ext]): points -> fp32; N == 4 -> one minimal solve, all
+// inliers; else RANSACPointSetRegistrator(PnPRansacCallback, 4, reprojectionError, confidence,
+// iterationsCount) -> the best model's mask -> solvePnP on the inliers. Here the hypotheses run
+// on the GPU (ransac_pnp.hip) with the sequential replay of ransac_host.cpp, and the final solve
+// on the inliers is Levenberg-Marquardt from the best hypothesis' pose (the ITERATIVE refinement
+// OpenCV uses with an extrinsic guess) with its O(N) sums on the GPU.
+#include "minicv_native.h"
+#include "mcv_runtime.h"
+#include "kernels.h"
+#include "linalg.h"
+#include "plan.h"
+#include "hyp_pnp.h"
+
+#include <cmath>
+#include <cfloat>
+#include <cstring>
+#include <vector>
+#include <algorithm>
+
+namespace mcv {
+
+// ---- rotation algebra (host) --------------------------------------------------------------------
+static void skew(const double* v, double* S) {
+    S[0] = 0; S[1] = -v[2]; S[2] = v[1];
+    S[3] = v[2]; S[4] = 0; S[5] = -v[0];
+    S[6] = -v[1]; S[7] = v[0]; S[8] = 0;
+}
+static void mul33(const double* A, const double* B, double* C) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+// Rodrigues r -> R (row-major) and dR/dr_j (dR + 9 j), Gallego & Yezzi (2015):
+//   dR/dr_j = (r_j [r]x + [r x ((I - R) e_j)]x) R / |r|^2;  [e_j]x for |r| -> 0.
+void rodrigues(const double* r, double* R, double* dR) {
+    const double th2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+    const double th = std::sqrt(th2);
+    double S[9];
+    skew(r, S);
+    if (th < 1e-12) {
+        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0 ? 1.0 : 0.0) + S[k];
+        if (dR)
+            for (int j = 0; j < 3; ++j) {
+                double e[3] = {0, 0, 0};
+                e[j] = 1;
+                skew(e, dR + 9 * j);
+            }
+        return;
+    }
+    const double s = std::sin(th), c = std::cos(th);
+    double S2[9];
+    mul33(S, S, S2);
+    for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0 ? 1.0 : 0.0) + (s / th) * S[k] + ((1 - c) / th2) * S2[k];
+    if (!dR) return;
+    for (int j = 0; j < 3; ++j) {
+        double w[3];   // (I - R) e_j
+        for (int i = 0; i < 3; ++i) w[i] = (i == j ? 1.0 : 0.0) - R[3 * i + j];
+        double rx[3] = {r[1] * w[2] - r[2] * w[1], r[2] * w[0] - r[0] * w[2], r[0] * w[1] - r[1] * w[0]};
+        double A[9], B[9];
+        skew(rx, A);
+        for (int k = 0; k < 9; ++k) A[k] = (r[j] * S[k] + A[k]) / th2;
+        mul33(A, R, B);
+        for (int k = 0; k < 9; ++k) dR[9 * j + k] = B[k];
+    }
+}
+
+// R -> r (axis * angle); robust near 0 and pi.
+void rodrigues_inv(const double* R, double* r) {
+    const double w[3] = {(R[7] - R[5]) * 0.5, (R[2] - R[6]) * 0.5, (R[3] - R[1]) * 0.5};
+    const double s = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = std::max(-1.0, std::min(1.0, c));
+    if (s > 1e-7) {
+        const double th = std::atan2(s, c);
+        for (int k = 0; k < 3; ++k) r[k] = w[k] * (th / s);
+        return;
+    }
+    if (c > 0) {
+        for (int k = 0; k < 3; ++k) r[k] = w[k];
+        return;
+    }
+    // theta ~ pi: axis from the largest diagonal of (R + I) / 2
+    int m = 0;
+    for (int k = 1; k < 3; ++k)
+        if (R[4 * k] > R[4 * m]) m = k;
+    double ax[3];
+    for (int k = 0; k < 3; ++k) ax[k] = (R[3 * m + k] + R[3 * k + m]) * 0.25 + (k == m ? 0.5 : 0.0);
+    double n = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+    for (int k = 0; k < 3; ++k) ax[k] /= n;
+    if (ax[0] * w[0] + ax[1] * w[1] + ax[2] * w[2] < 0)
+        for (int k = 0; k < 3; ++k) ax[k] = -ax[k];
+    const double th = std::atan2(s, c);
+    for (int k = 0; k < 3; ++k) r[k] = ax[k] * th;
+}
+
+// ---- plan helpers -----------------------------------------------------------------------------
+static void set_camera(Plan& P, const double* K9, const double* dist4) {
+    P.pnpCam[0] = K9[0]; P.pnpCam[1] = K9[4]; P.pnpCam[2] = K9[2]; P.pnpCam[3] = K9[5];
+    for (int k = 0; k < 4; ++k) P.pnpCam[4 + k] = dist4 ? dist4[k] : 0.0;
+    if (!(K9[0] != 0) || !(K9[4] != 0) || !std::isfinite(K9[0]) || !std::isfinite(K9[4]))
+        fail("camera matrix needs finite non-zero fx, fy");
+}
+
+static void pnp_pack(Plan& P, const mcvV2d* img, const mcvV3d* world, int N, void* d_out, hipStream_t s) {
+    P.raw.ensure((size_t)N * 5);
+    MCV_HIP(hipMemcpyAsync(P.raw.p, img, (size_t)N * sizeof(mcvV2d), hipMemcpyHostToDevice, s));
+    MCV_HIP(hipMemcpyAsync(P.raw.p + 2 * (size_t)N, world, (size_t)N * sizeof(mcvV3d), hipMemcpyHostToDevice, s));
+    launch_pnp_pack(P.raw.p, P.raw.p + 2 * (size_t)N, N, d_out, s);
+    MCV_HIP(hipGetLastError());
+}
+
+static bool fused_pnp(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_UNFUSED_ERROR) == 0; }
+
+void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
+                      int* d_counts, hipStream_t s) {
+    const float thr2 = (float)(cfg.threshold * cfg.threshold);
+    launch_pnp_generate(d_pts, N, P.pnpCam, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+    ProfScope ps("pnp_verify", s);
+    launch_pnp_verify(d_pts, N, P.pnpCam, P.models.p, d_counts, hypCount, thr2, fused_pnp(cfg), s);
+}
+
+static PnpOneOut pnp_fetch_one(Plan& P, hipStream_t s) {
+    PnpOneOut one;
+    MCV_HIP(hipMemcpyAsync(P.h_one.p, P.one.p, sizeof(PnpOneOut), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    std::memcpy(&one, P.h_one.p, sizeof(PnpOneOut));
+    return one;
+}
+
+static int pnp_mask_count(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, const double* R, const double* t,
+                          uint8_t* d_mask, hipStream_t s) {
+    const float thr2 = (float)(cfg.threshold * cfg.threshold);
+    MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
+    launch_pnp_mask(d_pts, N, P.pnpCam, R, t, thr2, fused_pnp(cfg), d_mask, P.count.p, s);
+    MCV_HIP(hipGetLastError());
+    MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    return P.h_i.p[0];
+}
+
+// Levenberg-Marquardt on (rvec, t) over the (masked) correspondences: damping A + lambda diag(A),
+// lambda from 1e-3 (x10 on rejection, /10 on acceptance), at most maxIters accepted-or-rejected
+// steps, stop when the step is below FLT_EPSILON relative to the parameters or the cost stalls.
+void pnp_lm(Plan& P, const void* d_pts, int N, const uint8_t* d_mask, double* rvec, double* t, int maxIters,
+            hipStream_t s) {
+    double p[6] = {rvec[0], rvec[1], rvec[2], t[0], t[1], t[2]};
+    auto eval = [&](const double* q, bool wantJ, double* A, double* g) -> double {
+        double R[9], dR[27], buf[28];
+        rodrigues(q, R, wantJ ? dR : nullptr);
+        reduce_to_host(P, s, 28, buf, [&](double* part, double* red) {
+            pnp_reduce_lm(d_pts, N, d_mask, P.pnpCam, R, q + 3, wantJ ? dR : nullptr, wantJ, part, red, s);
+        });
+        if (wantJ) {
+            int o = 0;
+            for (int j = 0; j < 6; ++j)
+                for (int k = j; k < 6; ++k) { A[6 * j + k] = buf[o]; A[6 * k + j] = buf[o]; ++o; }
+            for (int j = 0; j < 6; ++j) g[j] = buf[21 + j];
+        }
+        return buf[27];
+    };
+    double A[36], g[6];
+    double S = eval(p, true, A, g);
+    double lambda = 1e-3;
+    for (int it = 0; it < maxIters; ++it) {
+        double M[36], rhs[6], d[6];
+        for (int k = 0; k < 36; ++k) M[k] = A[k];
+        for (int k = 0; k < 6; ++k) {
+            M[7 * k] = A[7 * k] + lambda * std::max(A[7 * k], DBL_EPSILON);
+            rhs[k] = -g[k];
+        }
+        eig_solve(M, 6, rhs, d);
+        double q[6], dn = 0, pn = 0;
+        for (int k = 0; k < 6; ++k) {
+            q[k] = p[k] + d[k];
+            dn = std::max(dn, std::fabs(d[k]));
+            pn = std::max(pn, std::fabs(p[k]));
+        }
+        const double Sq = eval(q, false, nullptr, nullptr);
+        if (Sq < S) {
+            const bool stall = (S - Sq) <= FLT_EPSILON * S;
+            for (int k = 0; k < 6; ++k) p[k] = q[k];
+            lambda = std::max(lambda * 0.1, 1e-12);
+            S = eval(p, true, A, g);
+            if (stall || dn <= FLT_EPSILON * (pn + FLT_EPSILON)) break;
+        } else {
+            lambda *= 10;
+            if (dn <= FLT_EPSILON * (pn + FLT_EPSILON) || lambda > 1e16) break;
+        }
+    }
+    for (int k = 0; k < 3; ++k) { rvec[k] = p[k]; t[k] = p[3 + k]; }
+}
+
+// Virtual visual servoing (solvePnPRefineVVS restated): v = -lambda (L^T L)^+ L^T e on the
+// normalised image plane, cMo <- exp(v)^-1 cMo, 20 iterations or |v| < FLT_EPSILON.
+void pnp_vvs(Plan& P, const void* d_pts, int N, double* rvec, double* t, int maxIters, double lambda, hipStream_t s) {
+    double R[9];
+    rodrigues(rvec, R, nullptr);
+    for (int it = 0; it < maxIters; ++it) {
+        double buf[28];
+        reduce_to_host(P, s, 28, buf, [&](double* part, double* red) {
+            pnp_reduce_vvs(d_pts, N, nullptr, P.pnpCam, R, t, part, red, s);
+        });
+        double A[36], g[6], v[6];
+        int o = 0;
+        for (int j = 0; j < 6; ++j)
+            for (int k = j; k < 6; ++k) { A[6 * j + k] = buf[o]; A[6 * k + j] = buf[o]; ++o; }
+        for (int j = 0; j < 6; ++j) g[j] = buf[21 + j];
+        eig_solve(A, 6, g, v);
+        double vn = 0;
+        for (int k = 0; k < 6; ++k) { v[k] = -lambda * v[k]; vn += v[k] * v[k]; }
+        // T = exp(v): rotation Rodrigues(w), translation V u
+        const double* u = v;
+        const double* w = v + 3;
+        double Rw[9], S[9], S2[9], V[9];
+        rodrigues(w, Rw, nullptr);
+        skew(w, S);
+        mul33(S, S, S2);
+        const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2], th = std::sqrt(th2);
+        const double a = th < 1e-8 ? 0.5 : (1 - std::cos(th)) / th2;
+        const double b = th < 1e-8 ? 1.0 / 6.0 : (th - std::sin(th)) / (th2 * th);
+        for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * S[k] + b * S2[k];
+        double tt[3];
+        for (int i = 0; i < 3; ++i) tt[i] = V[3 * i] * u[0] + V[3 * i + 1] * u[1] + V[3 * i + 2] * u[2];
+        // cMo <- T^-1 cMo: R' = Rw^T R, t' = Rw^T (t - tt)
+        double Rn[9], tn[3];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Rn[3 * i + j] = Rw[i] * R[j] + Rw[3 + i] * R[3 + j] + Rw[6 + i] * R[6 + j];
+        for (int i = 0; i < 3; ++i)
+            tn[i] = Rw[i] * (t[0] - tt[0]) + Rw[3 + i] * (t[1] - tt[1]) + Rw[6 + i] * (t[2] - tt[2]);
+        std::memcpy(R, Rn, sizeof(R));
+        std::memcpy(t, tn, sizeof(tn));
+        if (std::sqrt(vn) < FLT_EPSILON) break;
+    }
+    rodrigues_inv(R, rvec);
+}
+
+// Device API finalize: winner -> mask -> LM on the inliers; model9 = {rvec, tvec, 0, 0, 0}.
+int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
+               uint8_t* d_mask, hipStream_t s) {
+    launch_pnp_one(d_pts, N, P.pnpCam, cfg.seed, hyp, (PnpOneOut*)P.one.p, s);
+    MCV_HIP(hipGetLastError());
+    const PnpOneOut one = pnp_fetch_one(P, s);
+    if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
+    const int count = pnp_mask_count(P, d_pts, N, cfg, one.R, one.t, d_mask, s);
+    double r[3], t[3] = {one.t[0], one.t[1], one.t[2]};
+    rodrigues_inv(one.R, r);
+    if (!(cfg.flags & MCV_FLAG_NO_REFINE) && count > 0) pnp_lm(P, d_pts, N, d_mask, r, t, 20, s);
+    for (int k = 0; k < 3; ++k) { model9[k] = r[k]; model9[3 + k] = t[k]; model9[6 + k] = 0; }
+    return count;
+}
+
+struct PnpResult {
+    bool ok = false;
+    int count = 0;
+    double r[3] = {0, 0, 0}, t[3] = {0, 0, 0};
+};
+
+// The RANSAC export body. Mask of the best hypothesis stays in P.mask (d_mask).
+static PnpResult pnp_ransac(Plan& P, const mcvV2d* img, const mcvV3d* world, int N, const double* K9,
+                            const double* dist, const RansacConfig& cfg, hipStream_t s) {
+    PnpResult res;
+    set_camera(P, K9, dist);
+    P.reserve(N, 1);
+    pnp_pack(P, img, world, N, P.ptsd.p, s);
+    if (N == 4) {
+        launch_pnp_solve4(P.ptsd.p, P.pnpCam, (PnpOneOut*)P.one.p, s);
+        MCV_HIP(hipGetLastError());
+        const PnpOneOut one = pnp_fetch_one(P, s);
+        if (one.status != 1) return res;
+        rodrigues_inv(one.R, res.r);
+        for (int k = 0; k < 3; ++k) res.t[k] = one.t[k];
+        launch_fill_u8(P.mask.p, N, 1, s);
+        res.count = 4;
+        res.ok = true;
+        return res;
+    }
+    const int64_t best = ransac_search(P, P.ptsd.p, N, cfg, s);
+    if (best < 0) return res;
+    double model9[9];
+    res.count = p_finalize(P, P.ptsd.p, N, cfg, best, model9, P.mask.p, s);
+    for (int k = 0; k < 3; ++k) { res.r[k] = model9[k]; res.t[k] = model9[3 + k]; }
+    res.ok = true;
+    return res;
+}
+
+static RansacConfig pnp_config(int iters, float thr, double conf) {
+    RansacConfig c;
+    std::memset(&c, 0, sizeof(c));
+    c.threshold = (double)thr;
+    c.confidence = conf;
+    c.maxIters = iters;
+    c.method = MCV_METHOD_RANSAC;
+    return c;
+}
+
+static bool pnp_ransac_export(const mcvV2d* img, const mcvV3d* world, int N, const mcvM33d& K, const double* dist,
+                              const RansacConfig& cfg, mcvV3d* tVec, mcvV3d* rVec, int* inlierCount,
+                              int* outInliers) {
+    if (inlierCount) *inlierCount = 0;
+    if (!img || !world || !tVec || !rVec || !inlierCount) fail("cvSolvePnPRansac: null argument");
+    if (N < 4) fail("cvSolvePnPRansac: need at least 4 correspondences (N=%d)", N);
+    if (!(cfg.confidence > 0 && cfg.confidence < 1)) fail("cvSolvePnPRansac: confidence must be in (0,1)");
+    require_device();
+    Plan& P = thread_plan(MCV_MODEL_PNP);
+    hipStream_t s = P.own_stream();
+    const PnpResult r = pnp_ransac(P, img, world, N, K.M, dist, cfg, s);
+    if (!r.ok) {
+        set_last_error("cvSolvePnPRansac: RANSAC found no pose with >= 4 inliers");
+        return false;
+    }
+    rVec->X = r.r[0]; rVec->Y = r.r[1]; rVec->Z = r.r[2];
+    tVec->X = r.t[0]; tVec->Y = r.t[1]; tVec->Z = r.t[2];
+    std::vector<uint8_t> m(N);
+    MCV_HIP(hipMemcpyAsync(m.data(), P.mask.p, (size_t)N, hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    int c = 0;
+    for (int i = 0; i < N; ++i)
+        if (m[i]) {
+            if (outInliers) outInliers[c] = i;
+            ++c;
+        }
+    *inlierCount = c;
+    return true;
+}
+
+}  // namespace mcv
+
+using namespace mcv;
+
+extern "C" MCV_API bool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N,
+                                         const mcvM33d K, const double* distortionCoeffs, const int solverKind,
+                                         const int iterationsCount, const float reprojectionError,
+                                         const double confidence, mcvV3d* tVec, mcvV3d* rVec, int* inlierCount,
+                                         int* outInliers) {
+    (void)solverKind;   // every kind uses the AP3P 4-point kernel (header comment)
+    MCV_GUARD(false, {
+        const RansacConfig cfg = pnp_config(iterationsCount, reprojectionError, confidence);
+        return pnp_ransac_export(imgPoints, worldPoints, N, K, distortionCoeffs, cfg, tVec, rVec, inlierCount,
+                                 outInliers);
+    })
+}
+
+extern "C" MCV_API bool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N,
+                                            const mcvM33d K, const double* distortionCoeffs, const RansacConfig* cfgp,
+                                            mcvV3d* tVec, mcvV3d* rVec, int* inlierCount, int* outInliers) {
+    MCV_GUARD(false, {
+        RansacConfig cfg = cfgp ? *cfgp : pnp_config(100, 8.0f, 0.99);
+        if (cfg.method != MCV_METHOD_RANSAC) fail("cvSolvePnPRansacCfg: only RANSAC (method 8)");
+        return pnp_ransac_export(imgPoints, worldPoints, N, K, distortionCoeffs, cfg, tVec, rVec, inlierCount,
+                                 outInliers);
+    })
+}
+
+extern "C" MCV_API bool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+                                   const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec) {
+    MCV_GUARD(false, {
+        if (!imgPoints || !worldPoints || !tVec || !rVec) fail("cvSolvePnP: null argument");
+        if (N < 4) fail("cvSolvePnP: need at least 4 correspondences (N=%d)", N);
+        const bool p3p = solverKind == 2 || solverKind == 5;
+        if (p3p && N != 4) fail("cvSolvePnP: P3P / AP3P need exactly 4 points (N=%d)", N);
+        require_device();
+        Plan& P = thread_plan(MCV_MODEL_PNP);
+        hipStream_t s = P.own_stream();
+        PnpResult r;
+        if (p3p) {
+            r = pnp_ransac(P, imgPoints, worldPoints, N, K.M, distortionCoeffs, pnp_config(1, 1.f, 0.99), s);
+        } else {
+            // AP3P-RANSAC initialisation (fixed 256 hypotheses, 4 px), then LM over all points
+            RansacConfig cfg = pnp_config(256, 4.0f, 0.99);
+            cfg.flags = MCV_FLAG_FIXED_ITERS | MCV_FLAG_NO_REFINE;
+            r = pnp_ransac(P, imgPoints, worldPoints, N, K.M, distortionCoeffs, cfg, s);
+            if (r.ok && N > 4) pnp_lm(P, P.ptsd.p, N, nullptr, r.r, r.t, 20, s);
+        }
+        if (!r.ok) {
+            set_last_error("cvSolvePnP: no pose");
+            return false;
+        }
+        rVec->X = r.r[0]; rVec->Y = r.r[1]; rVec->Z = r.r[2];
+        tVec->X = r.t[0]; tVec->Y = r.t[1]; tVec->Z = r.t[2];
+        return true;
+    })
+}
+
+static void refine_common(const mcvV2d* img, const mcvV3d* world, int N, const mcvM33d& K, const double* dist,
+                          mcvV3d* tVec, mcvV3d* rVec, bool vvs) {
+    if (!img || !world || !tVec || !rVec) fail("cvRefinePnP: null argument");
+    if (N < 3) fail("cvRefinePnP: need at least 3 correspondences (N=%d)", N);
+    require_device();
+    Plan& P = thread_plan(MCV_MODEL_PNP);
+    hipStream_t s = P.own_stream();
+    set_camera(P, K.M, dist);
+    P.reserve(N, 1);
+    pnp_pack(P, img, world, N, P.ptsd.p, s);
+    double r[3] = {rVec->X, rVec->Y, rVec->Z}, t[3] = {tVec->X, tVec->Y, tVec->Z};
+    if (vvs) pnp_vvs(P, P.ptsd.p, N, r, t, 20, 1.0, s);
+    else pnp_lm(P, P.ptsd.p, N, nullptr, r, t, 20, s);
+    rVec->X = r[0]; rVec->Y = r[1]; rVec->Z = r[2];
+    tVec->X = t[0]; tVec->Y = t[1]; tVec->Z = t[2];
+}
+
+extern "C" MCV_API void cvRefinePnPLM(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+                                      const double* distortionCoeffs, mcvV3d* tVec, mcvV3d* rVec) {
+    try {
+        clear_last_error();
+        refine_common(imgPoints, worldPoints, N, K, distortionCoeffs, tVec, rVec, false);
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+    }
+}
+
+extern "C" MCV_API void cvRefinePnPVVS(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N,
+                                       const mcvM33d K, const double* distortionCoeffs, mcvV3d* tVec, mcvV3d* rVec) {
+    try {
+        clear_last_error();
+        refine_common(imgPoints, worldPoints, N, K, distortionCoeffs, tVec, rVec, true);
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+    }
+}
+
+extern "C" MCV_API int solveAp3p(mcvM33d* Rs, mcvV3d* ts, float mu0, float mv0, float X0, float Y0, float Z0,
+                                 float mu1, float mv1, float X1, float Y1, float Z1, float mu2, float mv2, float X2,
+                                 float Y2, float Z2, float inv_fx, float inv_fy, float cx_fx, float cy_fy) {
+    MCV_GUARD(0, {
+        if (!Rs || !ts) fail("solveAp3p: null argument");
+        require_device();
+        Plan& P = thread_plan(MCV_MODEL_PNP);
+        hipStream_t s = P.own_stream();
+        P.reserve(4, 1);
+        Ap3pIn in;
+        const float mu[3] = {mu0, mu1, mu2}, mv[3] = {mv0, mv1, mv2};
+        const float W[3][3] = {{X0, Y0, Z0}, {X1, Y1, Z1}, {X2, Y2, Z2}};
+        for (int i = 0; i < 3; ++i) {
+            in.mu[i] = mu[i];
+            in.mv[i] = mv[i];
+            for (int k = 0; k < 3; ++k) in.W[i][k] = W[i][k];
+        }
+        in.inv_fx = inv_fx; in.inv_fy = inv_fy; in.cx_fx = cx_fx; in.cy_fy = cy_fy;
+        P.one.ensure(sizeof(Ap3pOut));
+        P.h_one.ensure(sizeof(Ap3pOut));
+        launch_pnp_ap3p(in, (Ap3pOut*)P.one.p, s);
+        MCV_HIP(hipGetLastError());
+        Ap3pOut out;
+        MCV_HIP(hipMemcpyAsync(P.h_one.p, P.one.p, sizeof(Ap3pOut), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        std::memcpy(&out, P.h_one.p, sizeof(Ap3pOut));
+        for (int k = 0; k < out.count; ++k) {
+            for (int j = 0; j < 9; ++j) Rs[k].M[j] = out.R[k][j];
+            ts[k].X = out.t[k][0]; ts[k].Y = out.t[k][1]; ts[k].Z = out.t[k][2];
+        }
+        return out.count;
+    })
+}
+
+extern "C" MCV_API int mcvPackPnP(const mcvV2d* img, const mcvV3d* world, int N, void* d_pts, void* stream) {
+    MCV_GUARD(0, {
+        if (!img || !world || !d_pts || N < 0) fail("mcvPackPnP: bad argument");
+        require_device();
+        Plan& P = thread_plan(MCV_MODEL_PNP);
+        pnp_pack(P, img, world, N, d_pts, (hipStream_t)stream);
+        MCV_HIP(hipStreamSynchronize((hipStream_t)stream));
+        return 1;
+    })
+}
+
+extern "C" MCV_API int mcvRansacPlanSetCamera(mcvRansacPlan* plan, const double* K9, const double* dist4) {
+    MCV_GUARD(0, {
+        Plan* P = reinterpret_cast<Plan*>(plan);
+        if (!P || !K9) fail("mcvRansacPlanSetCamera: null argument");
+        set_camera(*P, K9, dist4);
+        return 1;
+    })
+}
+
+// ---- host twins (test hooks) ------------------------------------------------------------------
+extern "C" MCV_API void mcvHostRodrigues(const double* r, double* R, double* dR27) { rodrigues(r, R, dR27); }
+extern "C" MCV_API void mcvHostRodriguesInv(const double* R, double* r) { rodrigues_inv(R, r); }
+
+extern "C" MCV_API int mcvHostPnP(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9,
+                                  double* t3, int* idx4) {
+    MCV_GUARD(kStatusNoSample - 1, {
+        if (!pts || !cam8 || !R9 || !t3 || N < 4) fail("mcvHostPnP: bad argument");
+        PnpCamera c{cam8[0], cam8[1], cam8[2], cam8[3], cam8[4], cam8[5], cam8[6], cam8[7]};
+        PnpPose p;
+        for (int k = 0; k < 9; ++k) p.R[k] = 0;
+        for (int k = 0; k < 3; ++k) p.t[k] = 0;
+        const int st = pnp_hypothesis((const PnpPoint*)pts, N, c, seed, (uint64_t)hyp, p, idx4);
+        for (int k = 0; k < 9; ++k) R9[k] = p.R[k];
+        for (int k = 0; k < 3; ++k) t3[k] = p.t[k];
+        return st;
+    })
+}

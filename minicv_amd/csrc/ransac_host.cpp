@@ -99,7 +99,7 @@ void Plan::reserve(int n, int64_t hyps) {
     if (n > maxN) maxN = n;
     if (hyps > maxHyps) maxHyps = hyps;
     const size_t slots = (size_t)model_slots(model);
-    if (model == MCV_MODEL_ESSENTIAL) {
+    if (model == MCV_MODEL_ESSENTIAL || model == MCV_MODEL_PNP) {
         ptsd.ensure((size_t)maxN * 4);
         raw.ensure((size_t)maxN * 4);
         dslot.ensure((size_t)maxHyps * slots);
@@ -120,13 +120,14 @@ void Plan::reserve(int n, int64_t hyps) {
     one.ensure(512);
     h_counts.ensure((size_t)maxHyps * slots);
     h_red.ensure(64);
-    if (model != MCV_MODEL_ESSENTIAL) h_pack.ensure((size_t)maxN * 4);
+    if (model != MCV_MODEL_ESSENTIAL && model != MCV_MODEL_PNP) h_pack.ensure((size_t)maxN * 4);
     one.ensure(sizeof(EOneOut));
     h_one.ensure(sizeof(EOneOut));
     h_i.ensure(4);
 }
 
 size_t model_bytes(int model) {
+    if (model == MCV_MODEL_PNP) return 96;
     return model == MCV_MODEL_ESSENTIAL ? 72 * kEModelSlots : (model == MCV_MODEL_FUNDAMENTAL ? 80 : 32);
 }
 int model_slots(int model) { return model == MCV_MODEL_ESSENTIAL ? kEModelSlots : 1; }
@@ -284,6 +285,12 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         MCV_HIP(hipGetLastError());
         return;
     }
+    if (P.model == MCV_MODEL_PNP) {
+        p_evaluate_chunk(P, d_ptsv, N, cfg, hypBegin, hypCount, d_counts, s);
+        if (d_key) launch_best(d_counts, hypCount, hypBegin, model_points(P.model), P.pkey.p, P.pfail.p, d_key, s);
+        MCV_HIP(hipGetLastError());
+        return;
+    }
     const float* d_pts = (const float*)d_ptsv;
     const double t = effective_threshold(cfg);
     const float thr2 = (float)(t * t);
@@ -302,6 +309,7 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
 }
 
 int model_points(int model) { return model == MCV_MODEL_FUNDAMENTAL ? 8 : (model == MCV_MODEL_ESSENTIAL ? 5 : 4); }
+// (homography and PnP: 4)
 
 // Winner -> mask (+ refit + LM). Returns inlier count, 0 on failure. Synchronises s.
 int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* H, uint8_t* d_mask,
@@ -336,6 +344,7 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
 int finalize(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
              uint8_t* d_mask, hipStream_t s) {
     if (P.model == MCV_MODEL_ESSENTIAL) return e_finalize(P, (const double*)d_ptsv, N, cfg, hyp, model9, d_mask, s);
+    if (P.model == MCV_MODEL_PNP) return p_finalize(P, d_ptsv, N, cfg, hyp, model9, d_mask, s);
     const float* d_pts = (const float*)d_ptsv;
     if (P.model == MCV_MODEL_HOMOGRAPHY) return h_finalize(P, d_pts, N, cfg, hyp, model9, d_mask, s);
     return f_finalize(P, d_pts, N, cfg, hyp, model9, d_mask, s);
@@ -429,7 +438,7 @@ extern "C" MCV_API int cvFindHomography(const mcvV2d* src, const mcvV2d* dst, co
 
 extern "C" MCV_API mcvRansacPlan* mcvRansacPlanCreate(int model, int maxN, int64_t maxHyps) {
     MCV_GUARD(nullptr, {
-        if (model != MCV_MODEL_HOMOGRAPHY && model != MCV_MODEL_FUNDAMENTAL && model != MCV_MODEL_ESSENTIAL)
+        if (model < MCV_MODEL_HOMOGRAPHY || model > MCV_MODEL_PNP)
             fail("unknown model %d", model);
         require_device();
         std::unique_ptr<Plan> p(new Plan());

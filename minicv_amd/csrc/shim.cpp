@@ -3,7 +3,6 @@
 //   cvDetectFeatures / cvFreeFeatures   MiniCVNative.cpp:221-365  (feature detection: out of scope)
 //   cvDetectQRCode / cvDetectArucoMarkers MiniCVNative.cpp:384-502 (fiducials: out of scope)
 //   cvTest                               MiniCVNative.cpp:504      (debug print: no-op)
-//   cvSolvePnP*, cvRefinePnP*, solveAp3p  MiniCVNative.cpp:48-163, ap3p.cpp:282 (row f2: next)
 #include "minicv_native.h"
 #include "mcv_runtime.h"
 #include <string>
@@ -94,36 +93,6 @@ extern "C" MCV_API void cvFreeFeatures(DetectorResult* res) {
 }
 
 extern "C" MCV_API void cvTest(void) {}
-
-extern "C" MCV_API bool cvSolvePnP(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*, const int,
-                                   mcvV3d*, mcvV3d*) {
-    MCV_NOT_IN_SCOPE("cvSolvePnP", "PnP is the next row (SURVEY 8f-2), not built yet");
-    return false;
-}
-
-extern "C" MCV_API bool cvSolvePnPRansac(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*,
-                                         const int, const int, const float, const double, mcvV3d*, mcvV3d*,
-                                         int* inlierCount, int*) {
-    if (inlierCount) *inlierCount = 0;
-    MCV_NOT_IN_SCOPE("cvSolvePnPRansac", "PnP-RANSAC is the next row (SURVEY 8f-2), not built yet");
-    return false;
-}
-
-extern "C" MCV_API void cvRefinePnPLM(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*, mcvV3d*,
-                                      mcvV3d*) {
-    MCV_NOT_IN_SCOPE("cvRefinePnPLM", "PnP refinement is the next row (SURVEY 8f-2), not built yet");
-}
-
-extern "C" MCV_API void cvRefinePnPVVS(const mcvV2d*, const mcvV3d*, const int, const mcvM33d, const double*, mcvV3d*,
-                                       mcvV3d*) {
-    MCV_NOT_IN_SCOPE("cvRefinePnPVVS", "PnP refinement is the next row (SURVEY 8f-2), not built yet");
-}
-
-extern "C" MCV_API int solveAp3p(mcvM33d*, mcvV3d*, float, float, float, float, float, float, float, float, float,
-                                 float, float, float, float, float, float, float, float, float, float) {
-    MCV_NOT_IN_SCOPE("solveAp3p", "AP3P is the next row (SURVEY 8f-2), not built yet");
-    return 0;
-}
 
 extern "C" MCV_API bool cvDetectQRCode(char*, int, int, int, int*, int* count) {
     if (count) *count = 0;

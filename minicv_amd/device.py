@@ -27,6 +27,13 @@ class RansacPlan:
         self._p = N.lib().mcvRansacPlanCreate(model, int(max_n), int(max_hyps))
         N.check(bool(self._p), "mcvRansacPlanCreate")
 
+    def set_camera(self, K, dist=None) -> None:
+        """PnP plans: camera matrix (3x3) and distortion (k1, k2, p1, p2)."""
+        K9 = np.ascontiguousarray(np.asarray(K, dtype=np.float64).ravel())
+        d = None if dist is None else np.ascontiguousarray(np.asarray(dist, dtype=np.float64))
+        ok = N.lib().mcvRansacPlanSetCamera(self._p, K9.ctypes.data, None if d is None else d.ctypes.data)
+        N.check(ok == 1, "mcvRansacPlanSetCamera")
+
     def close(self):
         if self._p:
             N.lib().mcvRansacPlanDestroy(self._p)
@@ -93,4 +100,15 @@ def pack_essential_tensor(a: np.ndarray, b: np.ndarray, focal: float, pp, device
     ok = N.lib().mcvPackEssential(a.ctypes.data, b.ctypes.data, a.shape[0], float(focal),
                                   N.V2d(float(pp[0]), float(pp[1])), out.data_ptr(), _stream_handle(stream))
     N.check(ok == 1, "mcvPackEssential")
+    return out
+
+
+def pack_pnp_tensor(img: np.ndarray, world: np.ndarray, device, stream=None):
+    """(N,2) image + (N,3) world fp64 -> device PnpPoint [N][8] float32 (packed on the GPU)."""
+    import torch
+    img = np.ascontiguousarray(img, dtype=np.float64)
+    world = np.ascontiguousarray(world, dtype=np.float64)
+    out = torch.empty((img.shape[0], 8), dtype=torch.float32, device=device)
+    ok = N.lib().mcvPackPnP(img.ctypes.data, world.ctypes.data, img.shape[0], out.data_ptr(), _stream_handle(stream))
+    N.check(ok == 1, "mcvPackPnP")
     return out

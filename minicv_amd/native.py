@@ -55,6 +55,7 @@ FERR_EPIPOLAR = 1
 MODEL_HOMOGRAPHY = 0
 MODEL_FUNDAMENTAL = 1
 MODEL_ESSENTIAL = 2
+MODEL_PNP = 3
 E_SLOTS = 10
 
 _P = C.c_void_p
@@ -84,6 +85,7 @@ SIGNATURES = {
     "cvFindHomography": (_I, [_P, _P, _I, _P, _P, _P]),
     "cvFindFundamentalMat": (_I, [_P, _P, _I, _P, _P, _P]),
     "cvFindEssentialMat": (_I, [_P, _P, _I, _D, V2d, _P, _P, _P]),
+    "cvSolvePnPRansacCfg": (C.c_bool, [_P, _P, _I, M33d, _P, _P, _P, _P, _P, _P]),
     "cvMatchHamming": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
     "cvMatchL2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
     "mcvGetLastError": (C.c_char_p, []),
@@ -94,6 +96,8 @@ SIGNATURES = {
     "mcvRansacPlanDestroy": (None, [_P]),
     "mcvPackCorrespondences": (_I, [_P, _P, _I, _P, _P]),
     "mcvPackEssential": (_I, [_P, _P, _I, _D, V2d, _P, _P]),
+    "mcvPackPnP": (_I, [_P, _P, _I, _P, _P]),
+    "mcvRansacPlanSetCamera": (_I, [_P, _P, _P]),
     "mcvRansacEvaluate": (_I, [_P, _P, _I, _P, _I64, _I64, _P, _P, _P]),
     "mcvRansacFinalize": (_I, [_P, _P, _I, _P, _I64, _P, _P, _P]),
     "mcvReplayInit": (None, [_P, _I]),
@@ -110,6 +114,9 @@ SIGNATURES = {
     "mcvHostEssential": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostFivePoint": (_I, [_P, _P]),
     "mcvHostDecomposeEssential": (None, [_P, _P, _P, _P]),
+    "mcvHostPnP": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
+    "mcvHostRodrigues": (None, [_P, _P, _P]),
+    "mcvHostRodriguesInv": (None, [_P, _P]),
     "mcvTestRcpExhaustive": (C.c_longlong, [_I, _P]),
     "mcvTestHomographySweep": (_I, [_P, _I, _P, _I, _F, _I, _P]),
 }

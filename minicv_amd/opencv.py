@@ -182,3 +182,103 @@ def fivepoint(a, b):
     if cnt <= 0 and N.last_error():
         raise N.NativeError(f"cvFivePoint: {N.last_error()}")
     return [np.array(Es[i].M[:]).reshape(3, 3) for i in range(max(cnt, 0))]
+
+
+# ---- PnP (OpenCV.fs:922-1052; exports MiniCVNative.cpp:48-163, ap3p.cpp:282) -----------------
+SOLVER_KIND = {"Iterative": 0, "EPNP": 1, "P3P": 2, "AP3P": 5, "SQPNP": 6}
+
+
+def _m33(K) -> N.M33d:
+    K = np.ascontiguousarray(np.asarray(K, dtype=np.float64).reshape(9))
+    m = N.M33d()
+    m.M[:] = K.tolist()
+    return m
+
+
+def _dist4(d):
+    d = np.zeros(4) if d is None else np.ascontiguousarray(np.asarray(d, dtype=np.float64).reshape(4))
+    return d
+
+
+def _v3d(a) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if a.ndim != 2 or a.shape[1] != 3:
+        raise ValueError("world points must be an (N, 3) array")
+    return a
+
+
+def solvePnPRansac(img, world, K, dist=None, kind: str = "AP3P", iterations: int = 100, reproj_error: float = 8.0,
+                   confidence: float = 0.99, params: RansacParams | None = None):
+    """cvSolvePnPRansac (solvePnPInternal with `ransac`, OpenCV.fs:976-1038).
+    -> (ok, rvec, tvec, inlier indices int32[count]). With `params` the seeded cvSolvePnPRansacCfg
+    export is used (threshold = reprojection error in pixels)."""
+    pi, pw = _v2d(img), _v3d(world)
+    n = pi.shape[0]
+    if pw.shape[0] != n:
+        raise ValueError("img/world length mismatch")
+    d = _dist4(dist)
+    t, r = N.V3d(), N.V3d()
+    cnt = N.C.c_int(0)
+    inl = np.zeros(max(n, 1), dtype=np.int32)
+    if params is None:
+        ok = N.lib().cvSolvePnPRansac(pi.ctypes.data, pw.ctypes.data, n, _m33(K), d.ctypes.data, SOLVER_KIND[kind],
+                                      int(iterations), float(reproj_error), float(confidence), N.C.addressof(t),
+                                      N.C.addressof(r), N.C.addressof(cnt), inl.ctypes.data)
+    else:
+        cfg = params.to_c()
+        ok = N.lib().cvSolvePnPRansacCfg(pi.ctypes.data, pw.ctypes.data, n, _m33(K), d.ctypes.data,
+                                         N.C.addressof(cfg), N.C.addressof(t), N.C.addressof(r), N.C.addressof(cnt),
+                                         inl.ctypes.data)
+    if not ok and N.last_error() and "no pose" not in N.last_error():
+        raise N.NativeError(f"cvSolvePnPRansac: {N.last_error()}")
+    return bool(ok), np.array([r.X, r.Y, r.Z]), np.array([t.X, t.Y, t.Z]), inl[:cnt.value].copy()
+
+
+def solvePnP(img, world, K, dist=None, kind: str = "AP3P"):
+    """cvSolvePnP -> (ok, rvec, tvec)."""
+    pi, pw = _v2d(img), _v3d(world)
+    d = _dist4(dist)
+    t, r = N.V3d(), N.V3d()
+    ok = N.lib().cvSolvePnP(pi.ctypes.data, pw.ctypes.data, pi.shape[0], _m33(K), d.ctypes.data, SOLVER_KIND[kind],
+                            N.C.addressof(t), N.C.addressof(r))
+    if not ok and N.last_error() and "no pose" not in N.last_error():
+        raise N.NativeError(f"cvSolvePnP: {N.last_error()}")
+    return bool(ok), np.array([r.X, r.Y, r.Z]), np.array([t.X, t.Y, t.Z])
+
+
+def _refine(fn, img, world, K, dist, rvec, tvec):
+    pi, pw = _v2d(img), _v3d(world)
+    d = _dist4(dist)
+    t, r = N.V3d(*map(float, tvec)), N.V3d(*map(float, rvec))
+    fn(pi.ctypes.data, pw.ctypes.data, pi.shape[0], _m33(K), d.ctypes.data, N.C.addressof(t), N.C.addressof(r))
+    if N.last_error():
+        raise N.NativeError(N.last_error())
+    return np.array([r.X, r.Y, r.Z]), np.array([t.X, t.Y, t.Z])
+
+
+def refinePnPLM(img, world, K, dist, rvec, tvec):
+    """cvRefinePnPLM with the given initial pose -> (rvec, tvec)."""
+    return _refine(N.lib().cvRefinePnPLM, img, world, K, dist, rvec, tvec)
+
+
+def refinePnPVVS(img, world, K, dist, rvec, tvec):
+    """cvRefinePnPVVS -> (rvec, tvec)."""
+    return _refine(N.lib().cvRefinePnPVVS, img, world, K, dist, rvec, tvec)
+
+
+def solveAp3p(img, world, K):
+    """OpenCV.solveAp3p (OpenCV.fs:385-431): 3 points, float arguments -> list of (R, t) as the
+    reference returns them (R as stored by ap3p.cpp:245-250)."""
+    img = np.asarray(img, dtype=np.float64)
+    world = np.asarray(world, dtype=np.float64)
+    K = np.asarray(K, dtype=np.float64).reshape(3, 3)
+    Rs, ts = (N.M33d * 4)(), (N.V3d * 4)()
+    inv_fx, inv_fy = 1.0 / K[0, 0], 1.0 / K[1, 1]
+    args = []
+    for i in range(3):
+        args += [img[i, 0], img[i, 1], world[i, 0], world[i, 1], world[i, 2]]
+    args += [inv_fx, inv_fy, K[0, 2] * inv_fx, K[1, 2] * inv_fy]
+    cnt = N.lib().solveAp3p(Rs, ts, *[float(a) for a in args])
+    if cnt <= 0 and N.last_error():
+        raise N.NativeError(f"solveAp3p: {N.last_error()}")
+    return [(np.array(Rs[i].M[:]).reshape(3, 3), np.array([ts[i].X, ts[i].Y, ts[i].Z])) for i in range(max(cnt, 0))]

@@ -140,3 +140,27 @@ def essential_problem(n: int, seed: int = 6, outlier_frac: float = 0.5, sigma: f
     tx = np.array([[0, -tu[2], tu[1]], [tu[2], 0, -tu[0]], [-tu[1], tu[0], 0]])
     E = tx @ R
     return a, b, ~out, R, tu, E / np.linalg.norm(E)
+
+
+def pnp_problem(n: int, seed: int = 8, outlier_frac: float = 0.5, sigma: float = 0.5, K=None, dist=None,
+                R: np.ndarray | None = None, t=None):
+    """2D-3D correspondences (OpenCV camera: x = K (R X + t), +z forward) after the reference's
+    testPnp recipe (Program.fs:8-24: points in a 6-unit cube). Optional distortion (k1, k2, p1, p2)
+    is applied with the projectPoints model. -> img (n,2), world (n,3), is_inlier, K, dist, R, t"""
+    rng = np.random.default_rng(seed)
+    K = np.array([[800.0, 0, 640.0], [0, 820.0, 360.0], [0, 0, 1]]) if K is None else np.asarray(K, np.float64)
+    dist = np.zeros(4) if dist is None else np.asarray(dist, np.float64)
+    R = rotation([0.3, -1.0, 0.2], np.deg2rad(25.0)) if R is None else np.asarray(R, np.float64)
+    t = np.array([0.2, -0.1, 9.0]) if t is None else np.asarray(t, np.float64)
+    W = rng.uniform(-3, 3, size=(n, 3))
+    Xc = W @ R.T + t
+    x, y = Xc[:, 0] / Xc[:, 2], Xc[:, 1] / Xc[:, 2]
+    r2 = x * x + y * y
+    cd = 1 + dist[0] * r2 + dist[1] * r2 * r2
+    xd = x * cd + dist[2] * 2 * x * y + dist[3] * (r2 + 2 * x * x)
+    yd = y * cd + dist[2] * (r2 + 2 * y * y) + dist[3] * 2 * x * y
+    img = np.stack([xd * K[0, 0] + K[0, 2], yd * K[1, 1] + K[1, 2]], axis=1) + rng.normal(0, sigma, size=(n, 2))
+    out = rng.random(n) < outlier_frac
+    lo, hi = img.min(axis=0), img.max(axis=0)
+    img[out] = rng.uniform(lo, hi, size=(int(out.sum()), 2))
+    return img, W, ~out, K, dist, R, t

@@ -296,7 +296,7 @@ static void jacobi(double* A, int n, double* w, double* V) {
     }
 }
 
-static void eig_pinv_apply(const double* A, int n, const double* b, double* x, double* Ainv) {
+void eig_pinv_apply(const double* A, int n, const double* b, double* x, double* Ainv) {
     double M[81], w[9], V[81], wmax = 0;
     memcpy(M, A, sizeof(double) * n * n);
     jacobi(M, n, w, V);

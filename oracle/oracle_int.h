@@ -21,5 +21,9 @@ int draw_distinct(Stream* st, int N, int m, int* idx);
 void jacobi3_orc(double* A, double* V);
 float f_err_orc(int kind, const double* F, double x1, double y1, double x2, double y2);
 int orc_update_num_iters(double p, double ep, int modelPoints, int maxIters);
+int64_t orc_ransac_replay(const int* counts, int64_t ncounts, int N, int m, double conf, int maxIters, int fixed,
+                          int* bestCount);
+void eig_pinv_apply(const double* A, int n, const double* b, double* x, double* Ainv);
+int orc_poly_real_roots(const double* cin, int deg, double* roots);
 
 #endif

@@ -37,6 +37,15 @@ _SIGS = {
     "orc_find_essential": (_I, [_P, _P, _I, _D, _D, _D, _D, _D, _I, _U64, _I, _P, _P, _P, _I]),
     "orc_e_decompose": (None, [_P, _P, _P, _P]),
     "orc_recover_pose": (_I, [_P, _P, _I, _D, _D, _D, _P, _P, _P, _P, _P]),
+    "orc_ap3p_poses": (_I, [_P, _P, _P, _P]),
+    "orc_solve_ap3p": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _P]),
+    "orc_pnp_hypothesis": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
+    "orc_pnp_count": (_I, [_P, _I, _P, _P, _P, _F, _I, _P]),
+    "orc_pnp_counts": (None, [_P, _I, _P, _U64, _I64, _I64, _F, _I, _P, _I]),
+    "orc_pnp_lm": (None, [_P, _I, _P, _P, _P, _P, _I]),
+    "orc_solve_pnp_ransac": (_I, [_P, _P, _I, _P, _P, _D, _D, _I, _U64, _I, _P, _P, _P, _P, _I]),
+    "orc_rodrigues": (None, [_P, _P, _P]),
+    "orc_rodrigues_inv": (None, [_P, _P]),
 }
 
 _lib = None
@@ -45,7 +54,7 @@ _lib = None
 def load() -> C.CDLL:
     global _lib
     if _lib is None:
-        srcs = [ORACLE_DIR / n for n in ("oracle.c", "oracle_e.c", "oracle_int.h")]
+        srcs = [ORACLE_DIR / n for n in ("oracle.c", "oracle_e.c", "oracle_pnp.c", "oracle_int.h")]
         if not ORACLE_SO.exists() or ORACLE_SO.stat().st_mtime < max(p.stat().st_mtime for p in srcs):
             subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
         L = C.CDLL(str(ORACLE_SO))
@@ -249,3 +258,77 @@ def recover_pose(a, b, E, mask=None, focal=1.0, pp=(0.0, 0.0)):
     res = load().orc_recover_pose(ptr(a), ptr(b), a.shape[0], focal, pp[0], pp[1], ptr(E),
                                   None if m is None else ptr(m), ptr(R), ptr(t), ptr(g))
     return res, R.reshape(3, 3), t, g
+
+
+# ---- PnP (oracle_pnp.c) ---------------------------------------------------------------------
+def cam8(K, dist=None):
+    K = np.asarray(K, dtype=np.float64).reshape(3, 3)
+    d = np.zeros(4) if dist is None else np.asarray(dist, dtype=np.float64)
+    return np.ascontiguousarray([K[0, 0], K[1, 1], K[0, 2], K[1, 2], d[0], d[1], d[2], d[3]], dtype=np.float64)
+
+
+def pack_pnp(img, world) -> np.ndarray:
+    """PnpPoint layout: float32 [N][8] {X, Y, Z, u, v, 0, 0, 0}."""
+    img = np.asarray(img, dtype=np.float64)
+    world = np.asarray(world, dtype=np.float64)
+    p = np.zeros((img.shape[0], 8), dtype=np.float32)
+    p[:, 0:3] = world.astype(np.float32)
+    p[:, 3:5] = img.astype(np.float32)
+    return np.ascontiguousarray(p)
+
+
+def pnp_hypothesis(pts8, c8, seed, hyp):
+    R, t, idx = np.zeros(9), np.zeros(3), np.full(4, -1, dtype=np.int32)
+    st = load().orc_pnp_hypothesis(ptr(pts8), pts8.shape[0], ptr(c8), seed, hyp, ptr(R), ptr(t), ptr(idx))
+    return st, R.reshape(3, 3), t, idx
+
+
+def pnp_counts(pts8, c8, seed, begin, count, thr2, fused=True, nthreads=0):
+    out = np.zeros(count, dtype=np.int32)
+    load().orc_pnp_counts(ptr(pts8), pts8.shape[0], ptr(c8), seed, begin, count, thr2, int(fused), ptr(out), nthreads)
+    return out
+
+
+def pnp_count(pts8, c8, R, t, thr2, fused=True):
+    R = np.ascontiguousarray(R, dtype=np.float64).ravel()
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    m = np.zeros(pts8.shape[0], dtype=np.uint8)
+    n = load().orc_pnp_count(ptr(pts8), pts8.shape[0], ptr(c8), ptr(R), ptr(t), thr2, int(fused), ptr(m))
+    return n, m
+
+
+def solve_pnp_ransac(img, world, K, dist=None, thr=8.0, conf=0.99, max_iters=100, seed=0, flags=0, nthreads=0):
+    img = np.ascontiguousarray(img, dtype=np.float64)
+    world = np.ascontiguousarray(world, dtype=np.float64)
+    K9 = np.ascontiguousarray(np.asarray(K, dtype=np.float64).ravel())
+    d = np.ascontiguousarray(np.zeros(4) if dist is None else np.asarray(dist, dtype=np.float64))
+    n = img.shape[0]
+    r, t = np.zeros(3), np.zeros(3)
+    mask = np.zeros(max(n, 1), dtype=np.uint8)
+    best = np.zeros(1, dtype=np.int64)
+    cnt = load().orc_solve_pnp_ransac(ptr(img), ptr(world), n, ptr(K9), ptr(d), float(thr), conf, max_iters, seed,
+                                      flags, ptr(r), ptr(t), ptr(mask), ptr(best), nthreads)
+    return cnt, r, t, mask[:n], int(best[0])
+
+
+def solve_ap3p(mu, mv, W, inv_fx, inv_fy, cx_fx, cy_fy):
+    mu = np.ascontiguousarray(mu, dtype=np.float64)
+    mv = np.ascontiguousarray(mv, dtype=np.float64)
+    W = np.ascontiguousarray(np.asarray(W, dtype=np.float64).ravel())
+    Rs, ts = np.zeros(36), np.zeros(12)
+    n = load().orc_solve_ap3p(ptr(mu), ptr(mv), ptr(W), inv_fx, inv_fy, cx_fx, cy_fy, ptr(Rs), ptr(ts))
+    return [(Rs[9 * i:9 * i + 9].reshape(3, 3), ts[3 * i:3 * i + 3]) for i in range(n)]
+
+
+def rodrigues(r):
+    r = np.ascontiguousarray(r, dtype=np.float64)
+    R, dR = np.zeros(9), np.zeros(27)
+    load().orc_rodrigues(ptr(r), ptr(R), ptr(dR))
+    return R.reshape(3, 3), dR.reshape(3, 3, 3)
+
+
+def rodrigues_inv(R):
+    R = np.ascontiguousarray(np.asarray(R, dtype=np.float64).ravel())
+    r = np.zeros(3)
+    load().orc_rodrigues_inv(ptr(R), ptr(r))
+    return r

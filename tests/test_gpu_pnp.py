@@ -1,0 +1,152 @@
+"""GPU parity of the PnP path behind cvSolvePnPRansac / cvSolvePnP /
+cvRefinePnPLM / cvRefinePnPVVS / solveAp3p (MiniCVNative.cpp:48-163, ap3p.cpp:282-317) against
+the oracle (oracle/oracle_pnp.c).
+Bar: per-hypothesis inlier counts and the RANSAC inlier set bit-exact; AP3P solutions bit-exact;
+the LM-refined pose within 1e-6 (relative) of the oracle's (GPU sums in another order); refined
+poses reach the ground truth on synthetic data."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from minicv_amd import native as N
+from minicv_amd import opencv, synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+DIST = [-0.12, 0.03, 0.001, -0.002]
+
+
+@pytest.fixture(scope="module")
+def torch_dev(gpu):
+    import torch
+    return torch, torch.device("cuda:0")
+
+
+def rot(r):
+    return S.rotation(r / np.linalg.norm(r), np.linalg.norm(r)) if np.linalg.norm(r) > 0 else np.eye(3)
+
+
+@pytest.mark.parametrize("n,outl,seed,begin,count,dist,unfused", [
+    (4, 0.0, 1, 0, 32, None, False), (5, 0.2, 2, 0, 100, None, False), (300, 0.5, 3, 0, 256, DIST, False),
+    (5000, 0.5, 4, 77777, 100, DIST, False), (2001, 0.6, 5, 0, 300, None, True), (20000, 0.5, 6, 2**31, 64, DIST,
+                                                                                  False)])
+def test_pnp_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, dist, unfused):
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=seed, outlier_frac=outl, dist=dist)
+    pts = D.pack_pnp_tensor(img, W, dev)
+    pts8 = oracle.pack_pnp(img, W)
+    np.testing.assert_array_equal(pts.cpu().numpy(), pts8)
+    plan = D.RansacPlan(N.MODEL_PNP, n, count)
+    plan.set_camera(K, d)
+    thr = 2.0
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(count, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, begin, count, key, counts)
+    ref = oracle.pnp_counts(pts8, oracle.cam8(K, d), seed, begin, count, float(np.float32(thr * thr)), not unfused)
+    np.testing.assert_array_equal(counts.cpu().numpy(), ref)
+    if (ref >= 4).any() and not (ref == -2).any():
+        c = ref.max()
+        i = int(np.nonzero(ref == c)[0][0])
+        assert int(key[0].item()) == (int(c) << 32) | (0xFFFFFFFF - (begin + i))
+    plan.close()
+
+
+@pytest.mark.parametrize("n,outl,seed,iters,thr,dist,flags", [
+    (50, 0.3, 1, 100, 2.0, None, 0), (3000, 0.5, 2, 100, 2.0, DIST, 0), (3000, 0.6, 3, 300, 3.0, None, 0),
+    (20000, 0.5, 4, 100, 2.0, DIST, 0), (2000, 0.5, 5, 200, 2.0, None, N.FLAG_FIXED_ITERS | N.FLAG_UNFUSED_ERROR),
+    (2000, 0.5, 6, 200, 2.0, DIST, N.FLAG_NO_REFINE)])
+def test_solve_pnp_ransac_vs_oracle(gpu, oracle, n, outl, seed, iters, thr, dist, flags):
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=seed, outlier_frac=outl, sigma=0.3, dist=dist)
+    p = opencv.RansacParams(threshold=thr, confidence=0.99, max_iters=iters, seed=seed,
+                            fixed_iters=bool(flags & N.FLAG_FIXED_ITERS), refine=not (flags & N.FLAG_NO_REFINE),
+                            unfused_error=bool(flags & N.FLAG_UNFUSED_ERROR))
+    ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, d, params=p)
+    rc, rr, rt, rmask, best = oracle.solve_pnp_ransac(img, W, K, d, thr=thr, conf=0.99, max_iters=iters, seed=seed,
+                                                      flags=flags)
+    assert ok and rc > 0
+    np.testing.assert_array_equal(inliers, np.nonzero(rmask)[0])
+    if flags & N.FLAG_NO_REFINE:
+        np.testing.assert_array_equal(r, rr)
+        np.testing.assert_array_equal(tt, rt)
+    else:
+        np.testing.assert_allclose(r, rr, rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(tt, rt, rtol=1e-6, atol=1e-9)
+    if n >= 1000:
+        assert np.abs(rot(r) - R).max() < 2e-3 and np.abs(tt - t).max() < 2e-2
+
+
+def test_solve_pnp_ransac_reference_signature(native, gpu):
+    """cvSolvePnPRansac through ctypes exactly like the F# P/Invoke (OpenCV.fs:364-365, :999)."""
+    img, W, inl, K, d, R, t = S.pnp_problem(5000, seed=11, outlier_frac=0.5, sigma=0.3)
+    for kind in ("Iterative", "EPNP", "P3P", "AP3P"):
+        ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, None, kind=kind, iterations=100, reproj_error=2.0,
+                                                   confidence=0.99)
+        assert ok and len(inliers) > 0.95 * inl.sum() and inl[inliers].mean() > 0.99
+        assert np.abs(rot(r) - R).max() < 2e-3
+
+
+def test_n4_and_solve_pnp(gpu, oracle):
+    img, W, inl, K, d, R, t = S.pnp_problem(4, seed=12, outlier_frac=0, sigma=0)
+    ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, None, iterations=100, reproj_error=2.0)
+    rc, rr, rt, rmask, _ = oracle.solve_pnp_ransac(img, W, K, None, thr=2.0)
+    assert ok and list(inliers) == [0, 1, 2, 3] and rc == 4
+    np.testing.assert_array_equal(r, rr)
+    np.testing.assert_array_equal(tt, rt)
+    ok2, r2, t2 = opencv.solvePnP(img, W, K, None, kind="AP3P")
+    assert ok2
+    np.testing.assert_array_equal(r2, rr)
+    with pytest.raises(N.NativeError, match="exactly 4"):
+        opencv.solvePnP(np.vstack([img, img[:1]]), np.vstack([W, W[:1]]), K, None, kind="P3P")
+    # iterative kind on a clean cloud converges to the truth
+    img, W, inl, K, d, R, t = S.pnp_problem(500, seed=13, outlier_frac=0, sigma=0.1, dist=DIST)
+    ok3, r3, t3 = opencv.solvePnP(img, W, K, d, kind="Iterative")
+    assert ok3 and np.abs(rot(r3) - R).max() < 1e-3 and np.abs(t3 - t).max() < 1e-2
+
+
+@pytest.mark.parametrize("vvs", [False, True])
+def test_refine_converges(gpu, vvs):
+    img, W, inl, K, d, R, t = S.pnp_problem(2000, seed=14, outlier_frac=0, sigma=0.05, dist=DIST)
+    from minicv_amd.synthetic import rotation
+    R0 = rotation([1, 0, 0], 0.05) @ R
+    r0 = _rvec(R0)
+    t0 = t + np.array([0.05, -0.03, 0.2])
+    fn = opencv.refinePnPVVS if vvs else opencv.refinePnPLM
+    r, tt = fn(img, W, K, d, r0, t0)
+    assert np.abs(rot(r) - R).max() < 1e-3 and np.abs(tt - t).max() < 1e-2
+
+
+def _rvec(R):
+    ang = np.arccos(np.clip((np.trace(R) - 1) / 2, -1, 1))
+    w = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    return w / (2 * np.sin(ang)) * ang
+
+
+def test_solve_ap3p_vs_oracle(gpu, oracle):
+    for seed in range(20):
+        img, W, inl, K, d, R, t = S.pnp_problem(3, seed=seed, outlier_frac=0, sigma=0)
+        sols = opencv.solveAp3p(img, W, K)
+        # the export takes float arguments (OpenCV.fs:374): the oracle gets the same float values
+        f = lambda v: np.float64(np.float32(v))
+        inv_fx, inv_fy = f(1 / K[0, 0]), f(1 / K[1, 1])
+        ref = oracle.solve_ap3p(np.array([f(v) for v in img[:, 0]]), np.array([f(v) for v in img[:, 1]]),
+                                np.array([[f(v) for v in row] for row in W]), inv_fx, inv_fy,
+                                f(K[0, 2] * (1 / K[0, 0])), f(K[1, 2] * (1 / K[1, 1])))
+        assert len(sols) == len(ref)
+        for (Rg, tg), (Ro, to) in zip(sols, ref):
+            np.testing.assert_array_equal(Rg, Ro)
+            np.testing.assert_array_equal(tg, to)
+        assert min(np.abs(Rg.T - R).max() for Rg, _ in sols) < 1e-4
+
+
+def test_pnp_edge_cases(gpu):
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    with pytest.raises(N.NativeError, match="at least 4"):
+        opencv.solvePnPRansac(np.zeros((3, 2)), np.zeros((3, 3)), K)
+    # all world points identical: every AP3P sample is degenerate
+    ok, r, t, inl = opencv.solvePnPRansac(np.tile([[600.0, 300.0]], (50, 1)), np.tile([[1.0, 2.0, 3.0]], (50, 1)), K)
+    assert not ok and len(inl) == 0
+    with pytest.raises(N.NativeError, match="confidence"):
+        opencv.solvePnPRansac(*S.pnp_problem(50, seed=1)[:2], K, confidence=1.0)
