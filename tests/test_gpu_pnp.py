@@ -75,7 +75,8 @@ def test_solve_pnp_ransac_vs_oracle(gpu, oracle, n, outl, seed, iters, thr, dist
         np.testing.assert_allclose(r, rr, rtol=1e-6, atol=1e-9)
         np.testing.assert_allclose(tt, rt, rtol=1e-6, atol=1e-9)
     if n >= 1000:
-        assert np.abs(rot(r) - R).max() < 2e-3 and np.abs(tt - t).max() < 2e-2
+        tol = 2e-2 if flags & N.FLAG_NO_REFINE else 2e-3     # unrefined: best minimal-sample pose
+        assert np.abs(rot(r) - R).max() < tol and np.abs(tt - t).max() < 10 * tol
 
 
 def test_solve_pnp_ransac_reference_signature(native, gpu):
