@@ -35,6 +35,10 @@ E_N_CORR = 100_000            # essential (cvRecoverPose path): not
 E_HYPS_TOTAL = 1 << 16
 E_SEED = 6
 E_FOCAL, E_PP, E_THR_PX = 800.0, (640.0, 360.0), 1.0
+P_N_CORR = 20_000             # PnP (cvSolvePnPRansac path): reference testPnp size (Program.fs:14)
+P_HYPS_TOTAL = 1 << 16
+P_SEED = 8
+P_THR_PX = 2.0
 THR = 5e-3
 SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -58,7 +62,7 @@ def parse():
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="homography", choices=["homography", "fundamental", "essential", "hamming", "l2"],
+    ap.add_argument("--workload", default="homography", choices=["homography", "fundamental", "essential", "pnp", "hamming", "l2"],
                     help="homography = the headline (BASELINE config[2]); the others are config[1], [3], [4]")
     return ap.parse_args()
 
@@ -252,6 +256,8 @@ def bench_ransac(args):
     ess = args.workload == "essential"
     if ess:
         return bench_essential(args, world, rank, dev)
+    if args.workload == "pnp":
+        return bench_pnp(args, world, rank, dev)
     n, hyps = args.n, args.hyps
     if fund:
         n = args.n if args.n != N_CORR else F_N_CORR
@@ -499,6 +505,119 @@ def bench_essential(args, world, rank, dev):
             line["cpu_baseline"] = cpu_baseline_e(O.pack_e(a, b, E_FOCAL, E_PP), args.cpu_seconds)
         else:
             line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    plan.close()
+
+
+def cpu_baseline_p(img, W, K, d, target_s: float):
+    sys.path.insert(0, str(ROOT / "tests"))
+    import numpy as np
+    import _oracle as O
+    pts8, c8 = O.pack_pnp(img, W), O.cam8(K, d)
+    thr2 = float(np.float32(P_THR_PX * P_THR_PX))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    t = time.perf_counter()
+    O.pnp_counts(pts8, c8, P_SEED, 0, 4 * threads, thr2, True, threads)
+    cal = (time.perf_counter() - t) / (4 * threads)
+    sample = max(4 * threads, int(target_s / max(cal, 1e-6)))
+    t = time.perf_counter()
+    O.pnp_counts(pts8, c8, P_SEED, 0, sample, thr2, True, threads)
+    el = time.perf_counter() - t
+    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port",
+            "sample": f"{sample} hypotheses x {img.shape[0]} correspondences (4-pt AP3P sample+solve, projectPoints "
+                      f"fp32 error count), oracle/oracle_pnp.c, OpenMP {threads} threads, {el:.1f} s"}
+
+
+def bench_pnp(args, world, rank, dev):
+    """PnP-RANSAC (the cvSolvePnPRansac path): a step = one solvePnPRansac call over a fixed
+    hypothesis budget (AP3P hypotheses, projectPoints sweep with distortion) on HBM-resident 2D-3D
+    correspondences, sharded over ranks with one all-reduce, then mask + LM refit on the inliers."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from minicv_amd import native as NL, opencv, synthetic as S
+    from minicv_amd import device as D
+    from minicv_amd import dist as MD
+
+    n = args.n if args.n != N_CORR else P_N_CORR
+    hyps = args.hyps if args.hyps != HYPS_PER_GPU else P_HYPS_TOTAL // world
+    total = hyps * world
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=P_SEED, outlier_frac=0.5, sigma=0.5,
+                                            dist=[-0.12, 0.03, 0.001, -0.002])
+    pts = D.pack_pnp_tensor(img, W, dev)
+    plan = D.RansacPlan(NL.MODEL_PNP, n, hyps)
+    plan.set_camera(K, d)
+    cfg = opencv.RansacParams(threshold=P_THR_PX, confidence=0.99, max_iters=total, seed=P_SEED,
+                              fixed_iters=True).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    mask = torch.zeros(n, dtype=torch.uint8, device=dev)
+    red = torch.zeros(2, dtype=torch.int64, device=dev)
+
+    def evaluate(begin, count):
+        plan.evaluate(pts, n, cfg, begin, count, key)
+        k = key.cpu()
+        return int(k[0]), int(k[1])
+
+    def allreduce_max(vals):
+        if world == 1:
+            return vals
+        red.copy_(torch.tensor(vals, dtype=torch.int64))
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+        return [int(v) for v in red.cpu()]
+
+    result = {}
+
+    def step():
+        cnt, idx, _ = MD.global_best(evaluate, total, rank, world, allreduce_max)
+        if idx < 0:
+            raise RuntimeError("no model found")
+        m = (C.c_double * 9)()
+        fc = NL.lib().mcvRansacFinalize(plan._p, pts.data_ptr(), n, C.addressof(cfg), idx, m, mask.data_ptr(),
+                                        D._stream_handle())
+        NL.check(fc > 0, "mcvRansacFinalize")
+        result.update(count=cnt, idx=idx, final_count=fc, pose=list(m[:6]))
+
+    for _ in range(args.warmup):
+        step()
+    NL.lib().mcvProfileReset()
+    NL.lib().mcvProfileEnable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    NL.lib().mcvProfileEnable(0)
+    vms = C.c_double(0)
+    vl = NL.lib().mcvProfileRead(b"pnp_verify", C.addressof(vms))
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    if rank == 0:
+        v_ms = vms.value / max(vl, 1)
+        line = {
+            "metric": "RANSAC hypotheses/sec, solvePnPRansac AP3P (cvSolvePnPRansac path) @20k corrs",
+            "value": total * args.steps / el, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded 2D-3D problem after Program.fs:8-24, 50% outliers, sigma 0.5 px, k1 k2 p1 p2)",
+            "config": {"workload": f"solvePnPRansac AP3P, {n} correspondences x {total} hypotheses per call sharded "
+                                   f"over {world} GPU(s) + LM refit", "correspondences": n,
+                       "hypotheses_total": total, "threshold_px": P_THR_PX,
+                       "parallelism": f"hypothesis-sharded dp{world}"},
+            "kernels": {"mcv_pnp_verify": {"avg_launch_ms": v_ms, "launches": vl,
+                                           "evaluations_per_s": n * hyps / max(v_ms * 1e-3, 1e-12)}},
+            "result": {"best_count": result["count"], "best_hyp": result["idx"],
+                       "final_count": result["final_count"], "true_inliers": int(inl.sum())},
+        }
+        line["cpu_baseline"] = (cpu_baseline_p(img, W, K, d, args.cpu_seconds)
+                                if world == 1 and not args.no_cpu_baseline else None)
         print(json.dumps(line), flush=True)
     plan.close()
 

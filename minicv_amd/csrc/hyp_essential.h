@@ -16,8 +16,9 @@
 // Deterministic replacements: the null space by Gauss-Jordan with full pivoting
 // + modified Gram-Schmidt (not SVD); the coefficient matrix by generic polynomial products (not
 // the expanded getCoeffMat formulas); the elimination by Gauss-Jordan with partial pivoting (not
-// Mat::inv); the real roots by derivative-interval bisection over the ordered bit patterns of
-// doubles (not solvePoly's complex iteration; tangent double roots are not reported); the null
+// Mat::inv); the real roots by derivative-interval (Rolle) bracketing and Illinois regula falsi
+// to a 1-ulp bracket, safeguarded by bisection over the ordered bit patterns of doubles (not
+// solvePoly's complex iteration; tangent double roots are not reported); the null
 // vector of B(z) by the largest of the three row cross products (not SVD::solveZ).
 #pragma once
 
@@ -48,29 +49,58 @@ MCV_HD double e_falling(int m, int j) {
     return r;
 }
 
-// j-th derivative of the monic polynomial c[0..n] (c[n] = 1) at x, Horner from the top.
-MCV_HD double e_deriv_eval(const double* c, int n, int j, double x) {
-    double f = c[n] * e_falling(n, j);
-    for (int k = n - 1; k >= j; --k) f = f * x + c[k] * e_falling(k, j);
+// Horner on ascending coefficients q[0..d].
+MCV_HD double e_poly_eval(const double* q, int d, double x) {
+    double f = q[d];
+    for (int k = d - 1; k >= 0; --k) f = f * x + q[k];
     return f;
 }
 
-// Root of p^(j) in (a, b) where p^(j)(a) has sign `aNeg`: bisection on the ordered bit patterns.
-MCV_HD double e_bisect(const double* c, int n, int j, double a, double b, bool aNeg) {
-    int64_t klo = e_dkey(a), khi = e_dkey(b);
-    for (int it = 0; it < 70; ++it) {
-        const int64_t km = (klo >> 1) + (khi >> 1) + (klo & khi & 1);
-        if (km == klo || km == khi) break;
-        const double m = e_dval(km);
-        const double f = e_deriv_eval(c, n, j, m);
-        if (f == 0) return m;
-        if ((f < 0) == aNeg) klo = km; else khi = km;
+// Root of q (degree d) in (lo, hi) given opposite signs flo = q(lo), fhi = q(hi), to adjacent
+// doubles: Illinois regula falsi (the retained end's value is halved when it is kept twice), a
+// bisection step on the ordered bit patterns whenever the point falls outside the bracket or the
+// bracket failed to halve (in bit-pattern distance) twice in a row. Returns an exact zero if hit,
+// else the lower end of the final 1-ulp bracket.
+MCV_HD double e_root_bracketed(const double* q, int d, double lo, double hi, double flo, double fhi) {
+    int side = 0, stall = 0;
+    for (int it = 0; it < 256; ++it) {
+        const int64_t klo = e_dkey(lo), khi = e_dkey(hi);
+        const int64_t kmid = (klo >> 1) + (khi >> 1) + (klo & khi & 1);
+        if (kmid == klo || kmid == khi) break;
+        double m;
+        if (stall >= 2) {
+            m = e_dval(kmid);
+            stall = 0;
+        } else {
+            m = lo - flo * ((hi - lo) / (fhi - flo));
+            if (!(m > lo && m < hi)) m = e_dval(kmid);
+        }
+        const double fm = e_poly_eval(q, d, m);
+        if (fm == 0) return m;
+        const uint64_t w0 = (uint64_t)khi - (uint64_t)klo;
+        const int64_t km = e_dkey(m);
+        uint64_t w1;
+        if ((fm < 0) == (flo < 0)) {
+            w1 = (uint64_t)khi - (uint64_t)km;
+            lo = m;
+            flo = fm;
+            if (side == -1) fhi = fhi * 0.5;
+            side = -1;
+        } else {
+            w1 = (uint64_t)km - (uint64_t)klo;
+            hi = m;
+            fhi = fm;
+            if (side == 1) flo = flo * 0.5;
+            side = 1;
+        }
+        stall = (w1 > w0 / 2) ? stall + 1 : 0;
     }
-    return e_dval(klo);
+    return lo;
 }
 
 // Real roots (ascending) of sum_k cin[k] z^k, degree <= 10. The real roots of p^(j) are separated
-// by those of p^(j+1) (Rolle), all inside the Cauchy bound R of p (Gauss-Lucas); walk j = n-1..0.
+// by those of p^(j+1) (Rolle), all inside the Cauchy bound R of p (Gauss-Lucas); walk j = n-1..0,
+// with p^(j)'s coefficients c[k + j] (k + j)! / k! formed once per level.
 MCV_HD int e_poly_real_roots(const double* cin, int deg, double* roots) {
     int n = deg;
     while (n > 0 && cin[n] == 0) --n;
@@ -84,19 +114,21 @@ MCV_HD int e_poly_real_roots(const double* cin, int deg, double* roots) {
     }
     R = 1.0 + R;
     if (!isfinite(R)) return 0;
-    double rp[10], rc[10];
+    double rp[10], rc[10], q[11];
     int np = 0;
     for (int j = n - 1; j >= 0; --j) {
+        const int d = n - j;
+        for (int k = 0; k <= d; ++k) q[k] = c[k + j] * e_falling(k + j, j);
         int nc = 0;
         double a = -R;
-        double fa = e_deriv_eval(c, n, j, a);
+        double fa = e_poly_eval(q, d, a);
         for (int s = 0; s <= np; ++s) {
             const double b = s < np ? rp[s] : R;
-            const double fb = e_deriv_eval(c, n, j, b);
+            const double fb = e_poly_eval(q, d, b);
             if (fb == 0) {
                 if (nc == 0 || rc[nc - 1] != b) rc[nc++] = b;
             } else if (fa != 0 && ((fa < 0) != (fb < 0))) {
-                rc[nc++] = e_bisect(c, n, j, a, b, fa < 0);
+                rc[nc++] = e_root_bracketed(q, d, a, b, fa, fb);
             }
             a = b;
             fa = fb;

@@ -50,23 +50,44 @@ static double falling(int m, int j) {
     return r;
 }
 
-/* j-th derivative of monic c (degree n) at x */
-static double dpoly(const double* c, int n, int j, double x) {
-    double f = c[n] * falling(n, j);
-    for (int k = n - 1; k >= j; --k) f = f * x + c[k] * falling(k, j);
+static double horner(const double* q, int d, double x) {
+    double f = q[d];
+    for (int k = d - 1; k >= 0; --k) f = f * x + q[k];
     return f;
 }
 
-static double bisect(const double* c, int n, int j, double a, double b, int aNeg) {
-    int64_t lo = key_of(a), hi = key_of(b);
-    for (int it = 0; it < 70; ++it) {
-        int64_t mid = (lo >> 1) + (hi >> 1) + (lo & hi & 1);
-        if (mid == lo || mid == hi) break;
-        double m = val_of(mid), f = dpoly(c, n, j, m);
-        if (f == 0) return m;
-        if ((f < 0) == aNeg) lo = mid; else hi = mid;
+/* Illinois regula falsi with bit-pattern bisection safeguards, to a 1-ulp bracket */
+static double root_in(const double* q, int d, double lo, double hi, double flo, double fhi) {
+    int side = 0, stall = 0;
+    for (int it = 0; it < 256; ++it) {
+        int64_t a = key_of(lo), b = key_of(hi), mid = (a >> 1) + (b >> 1) + (a & b & 1);
+        if (mid == a || mid == b) break;
+        double m;
+        if (stall >= 2) {
+            m = val_of(mid);
+            stall = 0;
+        } else {
+            m = lo - flo * ((hi - lo) / (fhi - flo));
+            if (!(m > lo && m < hi)) m = val_of(mid);
+        }
+        double fm = horner(q, d, m);
+        if (fm == 0) return m;
+        uint64_t before = (uint64_t)b - (uint64_t)a, after;
+        int64_t km = key_of(m);
+        if ((fm < 0) == (flo < 0)) {
+            after = (uint64_t)b - (uint64_t)km;
+            lo = m; flo = fm;
+            if (side == -1) fhi = fhi * 0.5;
+            side = -1;
+        } else {
+            after = (uint64_t)km - (uint64_t)a;
+            hi = m; fhi = fm;
+            if (side == 1) flo = flo * 0.5;
+            side = 1;
+        }
+        stall = after > before / 2 ? stall + 1 : 0;
     }
-    return val_of(lo);
+    return lo;
 }
 
 /* real roots ascending of sum cin[k] z^k (deg <= 10): Rolle intervals from the derivatives */
@@ -79,17 +100,18 @@ int orc_poly_real_roots(const double* cin, int deg, double* roots) {
     for (int k = 0; k < n; ++k) R = fabs(c[k]) > R ? fabs(c[k]) : R;
     R = 1.0 + R;
     if (!isfinite(R)) return 0;
-    double crit[10], cur[10];
+    double crit[10], cur[10], q[11];
     int ncrit = 0;
     for (int j = n - 1; j >= 0; --j) {
-        int nc = 0;
-        double a = -R, fa = dpoly(c, n, j, a);
+        int d = n - j, nc = 0;
+        for (int k = 0; k <= d; ++k) q[k] = c[k + j] * falling(k + j, j);
+        double a = -R, fa = horner(q, d, a);
         for (int s = 0; s <= ncrit; ++s) {
-            double b = s < ncrit ? crit[s] : R, fb = dpoly(c, n, j, b);
+            double b = s < ncrit ? crit[s] : R, fb = horner(q, d, b);
             if (fb == 0) {
                 if (nc == 0 || cur[nc - 1] != b) cur[nc++] = b;
             } else if (fa != 0 && ((fa < 0) != (fb < 0))) {
-                cur[nc++] = bisect(c, n, j, a, b, fa < 0);
+                cur[nc++] = root_in(q, d, a, b, fa, fb);
             }
             a = b;
             fa = fb;

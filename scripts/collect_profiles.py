@@ -16,7 +16,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "gpurun_out"
 PROF = ROOT / "profiles"
-WORKLOADS = ["homography", "fundamental", "essential", "hamming", "l2"]
+WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2"]
 
 
 def last_json(path: Path):
