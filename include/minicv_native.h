@@ -179,6 +179,30 @@ MCV_API bool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3d* worldPoi
                                  const double* distortionCoeffs, const RansacConfig* cfg, mcvV3d* tVec, mcvV3d* rVec,
                                  int* inlierCount, int* outInliers);
 
+/* Device-resident match -> RANSAC hand-off. Inputs are the reference's
+ * DetectorResult (MiniCVNative.h:23-29: KeyPoint2d[PointCount] + row-major descriptors,
+ * DescriptorElementType 0 = uint8 -> Hamming, 5 = float32 -> L2). Matching a -> b (knn 2), then
+ * on the GPU: Lowe ratio test (d1 < ratio d2; ratio <= 0: off), mutual-nearest check, max
+ * distance (<= 0: off), order-preserving compaction, keypoint gather into the RANSAC layout. */
+typedef struct {
+    float ratio;
+    int   crossCheck;
+    float maxDistance;
+    int   model;        /* MCV_MODEL_HOMOGRAPHY or MCV_MODEL_FUNDAMENTAL (cvMatchAndFindModel) */
+} MatchConfig;          /* 16 bytes */
+
+/* Matches only: pairs[2k] = index in a, pairs[2k+1] = index in b (ascending in a), dist[k]
+ * (Hamming distance or L2 distance; may be NULL). Returns the match count, -1 on failure
+ * (maxPairs >= a->PointCount is always enough). */
+MCV_API int cvMatchFeatures(const DetectorResult* a, const DetectorResult* b, const MatchConfig* cfg, int* pairs,
+                            float* dist, int maxPairs);
+/* Matches + RANSAC on the matched keypoints (cvFindHomography / cvFindFundamentalMat semantics,
+ * cfg->method RANSAC) without leaving the GPU. M: model; pairs as above; mask[k]: inlier flag of
+ * match k; *matchCount: number of matches written. Returns the inlier count, 0 on failure. */
+MCV_API int cvMatchAndFindModel(const DetectorResult* a, const DetectorResult* b, const MatchConfig* mcfg,
+                                const RansacConfig* rcfg, mcvM33d* M, int* pairs, uint8_t* mask, int maxPairs,
+                                int* matchCount);
+
 /* Brute-force Hamming matcher (BFMatcher NORM_HAMMING, knn k = 2). q: [nq][bytesPerDesc],
  * t: [nt][bytesPerDesc] row-major bytes; bytesPerDesc in [1, 64]; nt < 2^22.
  * Outputs per query: best train index / distance and second best (idx2/dist2 may be NULL;

@@ -111,6 +111,12 @@ void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uin
                  uint64_t* d_out, hipStream_t s);
 void launch_fill_u8(uint8_t* d, int n, uint8_t v, hipStream_t s);
 
+// ---- match -> RANSAC hand-off (match_pipeline.hip)
+void launch_match_compact(const int* d_idx, const int* d_di1, const int* d_di2, const float* d_df1,
+                          const float* d_df2, const int* d_idxBack, int nq, float ratio, float maxDist,
+                          const uint8_t* d_kpA, const uint8_t* d_kpB, int kpStride, uint8_t* d_keep, int* d_cnt,
+                          int* d_off, int* d_pairs, float* d_dist, float* d_pts4, hipStream_t s);
+
 // ---- matchers (match_hamming.hip, match_l2.hip)
 int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc, int* d_idx,
                          int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s);

@@ -40,6 +40,22 @@ class RansacConfig(C.Structure):
                 ("errorKind", C.c_int), ("reserved", C.c_int)]
 
 
+class KeyPoint2d(C.Structure):
+    """MiniCVNative.h:14-21 / OpenCV.fs:300-310 (28 bytes)."""
+    _fields_ = [("X", C.c_float), ("Y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int), ("class_id", C.c_int)]
+
+
+class DetectorResult(C.Structure):
+    """MiniCVNative.h:23-29 / OpenCV.fs:329-337."""
+    _fields_ = [("PointCount", C.c_int), ("DescriptorEntries", C.c_int), ("DescriptorElementType", C.c_int),
+                ("Points", C.c_void_p), ("Descriptors", C.c_void_p)]
+
+
+class MatchConfig(C.Structure):
+    _fields_ = [("ratio", C.c_float), ("crossCheck", C.c_int), ("maxDistance", C.c_float), ("model", C.c_int)]
+
+
 class ReplayState(C.Structure):
     _fields_ = [("niters", C.c_int64), ("bestIndex", C.c_int64), ("bestCount", C.c_int32),
                 ("stopped", C.c_int32)]
@@ -86,6 +102,8 @@ SIGNATURES = {
     "cvFindFundamentalMat": (_I, [_P, _P, _I, _P, _P, _P]),
     "cvFindEssentialMat": (_I, [_P, _P, _I, _D, V2d, _P, _P, _P]),
     "cvSolvePnPRansacCfg": (C.c_bool, [_P, _P, _I, M33d, _P, _P, _P, _P, _P, _P]),
+    "cvMatchFeatures": (_I, [_P, _P, _P, _P, _P, _I]),
+    "cvMatchAndFindModel": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "cvMatchHamming": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
     "cvMatchL2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
     "mcvGetLastError": (C.c_char_p, []),

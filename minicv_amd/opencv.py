@@ -282,3 +282,58 @@ def solveAp3p(img, world, K):
     if cnt <= 0 and N.last_error():
         raise N.NativeError(f"solveAp3p: {N.last_error()}")
     return [(np.array(Rs[i].M[:]).reshape(3, 3), np.array([ts[i].X, ts[i].Y, ts[i].Z])) for i in range(max(cnt, 0))]
+
+
+# ---- device-resident match -> RANSAC hand-off ------------------------------
+class Features:
+    """A DetectorResult (MiniCVNative.h:23-29) built from keypoint coordinates and descriptors, as
+    cvDetectFeatures returns it: KeyPoint2d[N] + row-major descriptors (uint8 -> Hamming,
+    float32 -> L2). Keeps the backing arrays alive while the struct is in use."""
+
+    def __init__(self, points, descriptors):
+        pts = np.asarray(points, dtype=np.float64)
+        d = np.ascontiguousarray(descriptors)
+        if d.dtype not in (np.uint8, np.float32):
+            raise ValueError("descriptors must be uint8 (Hamming) or float32 (L2)")
+        n = pts.shape[0]
+        self._kp = (N.KeyPoint2d * max(n, 1))()
+        for i in range(n):
+            self._kp[i].X, self._kp[i].Y = float(pts[i, 0]), float(pts[i, 1])
+        self._d = d
+        self.struct = N.DetectorResult(n, int(d.size), 0 if d.dtype == np.uint8 else 5,
+                                       N.C.cast(self._kp, N.C.c_void_p), d.ctypes.data)
+
+
+def _mcfg(ratio, cross_check, max_distance, model):
+    return N.MatchConfig(float(ratio), int(bool(cross_check)), float(max_distance), int(model))
+
+
+def matchFeatures(a: Features, b: Features, ratio: float = 0.8, cross_check: bool = False,
+                  max_distance: float = 0.0):
+    """cvMatchFeatures -> (pairs int32 [k][2] (index in a, index in b), dist float32 [k])."""
+    n = a.struct.PointCount
+    pairs = np.zeros((max(n, 1), 2), dtype=np.int32)
+    dist = np.zeros(max(n, 1), dtype=np.float32)
+    cfg = _mcfg(ratio, cross_check, max_distance, N.MODEL_HOMOGRAPHY)
+    k = N.lib().cvMatchFeatures(N.C.addressof(a.struct), N.C.addressof(b.struct), N.C.addressof(cfg),
+                                pairs.ctypes.data, dist.ctypes.data, max(n, 1))
+    N.check(k >= 0, "cvMatchFeatures")
+    return pairs[:k].copy(), dist[:k].copy()
+
+
+def matchAndFindModel(a: Features, b: Features, model: int = N.MODEL_HOMOGRAPHY, ratio: float = 0.8,
+                      cross_check: bool = False, max_distance: float = 0.0, params: RansacParams | None = None):
+    """cvMatchAndFindModel -> (inliers, M 3x3, pairs [k][2], mask bool[k])."""
+    n = a.struct.PointCount
+    pairs = np.zeros((max(n, 1), 2), dtype=np.int32)
+    mask = np.zeros(max(n, 1), dtype=np.uint8)
+    M = N.M33d()
+    mc = N.C.c_int(0)
+    cfg = _mcfg(ratio, cross_check, max_distance, model)
+    rc = (params or (RansacParams() if model == N.MODEL_HOMOGRAPHY else RansacParams(confidence=0.99))).to_c()
+    cnt = N.lib().cvMatchAndFindModel(N.C.addressof(a.struct), N.C.addressof(b.struct), N.C.addressof(cfg),
+                                      N.C.addressof(rc), N.C.addressof(M), pairs.ctypes.data, mask.ctypes.data,
+                                      max(n, 1), N.C.addressof(mc))
+    N.check(cnt > 0, "cvMatchAndFindModel")
+    k = mc.value
+    return cnt, np.array(M.M[:]).reshape(3, 3), pairs[:k].copy(), mask[:k] != 0

@@ -164,3 +164,23 @@ def pnp_problem(n: int, seed: int = 8, outlier_frac: float = 0.5, sigma: float =
     lo, hi = img.min(axis=0), img.max(axis=0)
     img[out] = rng.uniform(lo, hi, size=(int(out.sum()), 2))
     return img, W, ~out, K, dist, R, t
+
+
+H_PIX = np.array([[1.05, 0.02, 15.0], [-0.03, 0.98, -10.0], [1e-5, 2e-5, 1.0]])
+
+
+def feature_pair_problem(na: int, nb: int, seed: int = 9, kind: str = "hamming", match_frac: float = 0.6,
+                         sigma: float = 0.5, H: np.ndarray = H_PIX, size=(640.0, 480.0)):
+    """Two 'images' of keypoints + descriptors: a fraction of a's keypoints reappear in b at
+    H(a) + N(0, sigma) px with a perturbed copy of their descriptor (binary: bit flips; SIFT-like:
+    additive noise); the rest of b is random. -> (pts_a, desc_a, pts_b, desc_b, planted)"""
+    rng = np.random.default_rng(seed)
+    if kind == "hamming":
+        da, db, planted = hamming_problem(na, nb, seed=seed, random_frac=1.0 - match_frac)
+    else:
+        da, db, planted = l2_problem(na, nb, seed=seed, random_frac=1.0 - match_frac)
+    pa = rng.uniform([0, 0], size, size=(na, 2))
+    pb = rng.uniform([0, 0], size, size=(nb, 2))
+    ok = planted >= 0
+    pb[planted[ok]] = project(H, pa[ok]) + rng.normal(0, sigma, size=(int(ok.sum()), 2))
+    return pa, da, pb, db, planted
