@@ -27,6 +27,11 @@ def expected_pairs(oracle, da, db, ratio, cross, maxd):
     return np.stack([q, idx[q]], axis=1).astype(np.int32), d1f[q]
 
 
+def reproj_px(H, pts):
+    """median distance (px) between H(pts) and the true H_PIX(pts)"""
+    return float(np.median(np.linalg.norm(S.project(H, pts) - S.project(S.H_PIX, pts), axis=1)))
+
+
 @pytest.mark.parametrize("na,nb,ratio,cross,maxd", [(1000, 1200, 0.8, False, 0), (3000, 2500, 0.75, True, 0),
                                                     (777, 333, 0.0, True, 60.0), (5000, 5000, 0.9, False, 40.0)])
 def test_match_features_hamming_exact(gpu, oracle, na, nb, ratio, cross, maxd):
@@ -52,8 +57,7 @@ def test_match_and_find_homography_vs_oracle(gpu, oracle):
     np.testing.assert_array_equal(mask, rmask != 0)
     Hn, rHn = H / np.linalg.norm(H), rH / np.linalg.norm(rH)
     assert np.linalg.norm(Hn - rHn) < 1e-6
-    Ht = S.H_PIX / np.linalg.norm(S.H_PIX)
-    assert np.linalg.norm(Hn - Ht) < 1e-3
+    assert reproj_px(H, pa) < 0.5
     # every inlier is a planted correspondence
     assert (planted[pairs[mask, 0]] == pairs[mask, 1]).mean() > 0.99
 
@@ -82,8 +86,7 @@ def test_match_features_l2(gpu):
     assert np.all(np.diff(pairs[:, 0]) > 0)
     cnt, H, pr, mask = opencv.matchAndFindModel(A, B, ratio=0.8, cross_check=True,
                                                 params=opencv.RansacParams(threshold=3.0, seed=1))
-    Hn = H / np.linalg.norm(H)
-    assert np.linalg.norm(Hn - S.H_PIX / np.linalg.norm(S.H_PIX)) < 1e-3
+    assert reproj_px(H, pa) < 0.5
 
 
 def test_pipeline_edge_cases(gpu):
@@ -95,4 +98,4 @@ def test_pipeline_edge_cases(gpu):
     with pytest.raises(N.NativeError, match="element types differ"):
         opencv.matchFeatures(A, opencv.Features(pb, db.astype(np.float32)))
     with pytest.raises(N.NativeError, match="need at least"):
-        opencv.matchAndFindModel(A, opencv.Features(pb[:2], db[:2]), ratio=0.0)
+        opencv.matchAndFindModel(opencv.Features(pa[:3], da[:3]), opencv.Features(pb, db), ratio=0.0)
