@@ -76,7 +76,7 @@ struct PinnedBuf {
         if (p) (void)hipHostFree(p);
         p = nullptr;
         n = 0;
-        MCV_HIP(hipHostMalloc((void**)&p, (count ? count : 1) * sizeof(T), hipHostMallocDefault));
+        MCV_HIP(hipHostMalloc((void**)&p, (count ? count : 1) * sizeof(T), hipHostMallocPortable));
         n = count;
     }
     ~PinnedBuf() {

@@ -18,6 +18,7 @@ int model_slots(int model);      // model slots per hypothesis (essential: 10)
 struct Plan {
     int model = MCV_MODEL_HOMOGRAPHY;
     int device = 0;
+    int shard = 0;
     int maxN = 0;
     int64_t maxHyps = 0;
     hipStream_t stream = nullptr;   // only for the host-pointer exports
@@ -54,7 +55,8 @@ struct Plan {
     ~Plan();
 };
 
-Plan& thread_plan(int model);
+Plan& thread_plan(int model, int shard = 0);   // current device; shard > 0: extra per-device workspaces
+static const int kMaxShards = 16;
 
 // Sum V doubles over (masked) correspondences: GPU two-stage reduction, result to host.
 template <class F>

@@ -142,16 +142,27 @@ Plan::~Plan() {
 }
 
 // Per-thread cached plans for the host-pointer exports (one per device and model).
-Plan& thread_plan(int model) {
+Plan& thread_plan(int model, int shard) {
     int dev = 0;
     MCV_HIP(hipGetDevice(&dev));
     thread_local std::vector<std::unique_ptr<Plan>> plans;
     for (auto& p : plans)
-        if (p->device == dev && p->model == model) return *p;
+        if (p->device == dev && p->model == model && p->shard == shard) return *p;
     plans.emplace_back(new Plan());
     plans.back()->device = dev;
     plans.back()->model = model;
+    plans.back()->shard = shard;
     return *plans.back();
+}
+
+// Device-resident point buffer of a plan (layout per model) and its size in bytes.
+static void* plan_points(Plan& P, int N, size_t* bytes) {
+    if (P.model == MCV_MODEL_ESSENTIAL || P.model == MCV_MODEL_PNP) {
+        *bytes = (size_t)N * 32;
+        return P.ptsd.p;
+    }
+    *bytes = (size_t)N * 16;
+    return P.pts.p;
 }
 
 void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst, hipStream_t s) {
@@ -351,13 +362,40 @@ int finalize(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg, int64_
 }
 
 // Full RANSAC on device-resident points with the OpenCV sequential-replay semantics.
-// Returns the best hypothesis index or -1.
+// cfg.deviceCount > 1: every chunk is split into that many contiguous hypothesis ranges evaluated
+// concurrently by per-shard workspaces on devices 0, 1, ... (round-robin over the visible GPUs;
+// points replicated once by peer copy), counts concatenated in order, then the same replay — the
+// answer is identical to one device. Returns the best hypothesis (slot) index or -1.
 int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s) {
     const int m = model_points(P.model);
     const int slots = model_slots(P.model);
     mcvReplayState st;
     mcvReplayInit(&st, cfg.maxIters);
     const bool fixed = (cfg.flags & MCV_FLAG_FIXED_ITERS) != 0;
+    int ndev = 1;
+    MCV_HIP(hipGetDeviceCount(&ndev));
+    const int shards = std::max(1, std::min(cfg.deviceCount, kMaxShards));
+    int home = 0;
+    MCV_HIP(hipGetDevice(&home));
+    struct Shard { Plan* P; const void* pts; hipStream_t s; int dev; };
+    std::vector<Shard> sh;
+    sh.push_back({&P, d_pts, s, home});
+    if (shards > 1) {
+        size_t bytes = 0;
+        MCV_HIP(hipStreamSynchronize(s));
+        for (int k = 1; k < shards; ++k) {
+            const int dev = (home + k) % ndev;
+            MCV_HIP(hipSetDevice(dev));
+            Plan& Pk = thread_plan(P.model, k);
+            Pk.reserve(N, 1);
+            std::memcpy(Pk.pnpCam, P.pnpCam, sizeof(P.pnpCam));
+            void* dst = plan_points(Pk, N, &bytes);
+            hipStream_t sk = Pk.own_stream();
+            MCV_HIP(hipMemcpyPeerAsync(dst, dev, d_pts, home, bytes, sk));
+            sh.push_back({&Pk, dst, sk, dev});
+        }
+        MCV_HIP(hipSetDevice(home));
+    }
     int64_t begin = 0;
     int64_t chunk = std::min<int64_t>(std::max<int64_t>(st.niters, 1), kChunkFirst);
     while (!st.stopped) {
@@ -365,9 +403,25 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
         if (remaining <= 0) break;
         const int cnt = (int)std::min<int64_t>(remaining, chunk);
         P.reserve(N, cnt);
-        evaluate_chunk(P, d_pts, N, cfg, begin, cnt, P.counts.p, nullptr, s);
-        MCV_HIP(hipMemcpyAsync(P.h_counts.p, P.counts.p, (size_t)cnt * slots * sizeof(int), hipMemcpyDeviceToHost, s));
-        MCV_HIP(hipStreamSynchronize(s));
+        const int nsh = std::min<int>((int)sh.size(), cnt);
+        int64_t off = 0;
+        for (int k = 0; k < nsh; ++k) {
+            const int ck = (int)(cnt / nsh + (k < cnt % nsh ? 1 : 0));
+            Shard& x = sh[k];
+            if (k > 0) {
+                MCV_HIP(hipSetDevice(x.dev));
+                x.P->reserve(N, ck);
+            }
+            evaluate_chunk(*x.P, x.pts, N, cfg, begin + off, ck, x.P->counts.p, nullptr, x.s);
+            MCV_HIP(hipMemcpyAsync(P.h_counts.p + off * slots, x.P->counts.p, (size_t)ck * slots * sizeof(int),
+                                   hipMemcpyDeviceToHost, x.s));
+            off += ck;
+        }
+        for (int k = 0; k < nsh; ++k) {
+            if (k > 0) MCV_HIP(hipSetDevice(sh[k].dev));
+            MCV_HIP(hipStreamSynchronize(sh[k].s));
+        }
+        if (nsh > 1) MCV_HIP(hipSetDevice(home));
         replay_chunk(&st, P.h_counts.p, begin, cnt, slots, N, m, cfg.confidence, fixed ? 1 : 0);
         begin += cnt;
         chunk = std::min<int64_t>(chunk * 2, kChunkMax);
