@@ -38,6 +38,7 @@ void h_reduce_lm(const float* d_pts4, int N, const uint8_t* d_mask, const double
 
 // ---- fundamental (ransac_f.hip)
 static const int kVerifyFHypPerWave = 4;
+static const int kVerifyFPtsPerLane = 2;
 struct FOneOut {
     double F[9];
     int status;

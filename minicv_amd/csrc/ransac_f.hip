@@ -11,6 +11,7 @@
 #include "hyp_fundamental.h"
 #include "reduce.h"
 #include "kernels.h"
+#include <cstdlib>
 
 namespace mcv {
 
@@ -38,7 +39,7 @@ __global__ void mcv_f_one(const float* __restrict__ pts4, int N, uint64_t seed, 
     *out = o;
 }
 
-template <int K, int KIND>
+template <int K, int P, int KIND>
 __global__ __launch_bounds__(256) void mcv_f_verify(const float4* __restrict__ pts, int N,
                                                     const FModelD* __restrict__ models, int* __restrict__ counts,
                                                     int hypCount, float thr2, double lo, double hi) {
@@ -62,13 +63,17 @@ __global__ __launch_bounds__(256) void mcv_f_verify(const float4* __restrict__ p
     uint32_t cnt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
-    const int nFull = N & ~63;
-    for (int base = 0; base < nFull; base += 64) {
-        const float4 q = pts[base + lane];
-        f_sweep_point<K, KIND>(fm, q.x, q.y, q.z, q.w, true, thr2, lo, hi, cnt);
+    const int step = 64 * P;
+    const int nFull = N - N % step;
+    for (int base = 0; base < nFull; base += step) {
+        float4 q[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) q[p] = pts[base + 64 * p + lane];
+#pragma unroll
+        for (int p = 0; p < P; ++p) f_sweep_point<K, KIND>(fm, q[p].x, q[p].y, q[p].z, q[p].w, true, thr2, lo, hi, cnt);
     }
-    if (nFull < N) {
-        const int p = nFull + lane;
+    for (int base = nFull; base < N; base += 64) {
+        const int p = base + lane;
         const bool v = p < N;
         const float4 q = pts[v ? p : 0];
         f_sweep_point<K, KIND>(fm, q.x, q.y, q.z, q.w, v, thr2, lo, hi, cnt);
@@ -119,18 +124,43 @@ void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOu
     hipLaunchKernelGGL(mcv_f_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out);
 }
 
+template <int K, int P>
+static void launch_f_verify_kp(const float4* p, int N, const FModelD* m, int* d_counts, int hypCount, float thr2,
+                               int kind, double lo, double hi, hipStream_t s) {
+    const int blocks = ((hypCount + K - 1) / K + 3) / 4;
+    switch (kind) {
+        case 0: hipLaunchKernelGGL((mcv_f_verify<K, P, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, lo, hi); break;
+        case 1: hipLaunchKernelGGL((mcv_f_verify<K, P, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, lo, hi); break;
+        case 2: hipLaunchKernelGGL((mcv_f_verify<K, P, 2>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, lo, hi); break;
+        default: hipLaunchKernelGGL((mcv_f_verify<K, P, 3>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, lo, hi); break;
+    }
+}
+
+// Sweep shape; MCV_F_VARIANT selects alternatives for tuning experiments only.
+static int f_variant() {
+    static int v = [] {
+        const char* e = getenv("MCV_F_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
                      int kind, hipStream_t s) {
-    constexpr int K = kVerifyFHypPerWave;
-    const int blocks = ((hypCount + K - 1) / K + 3) / 4;
     const float4* p = (const float4*)d_pts4;
     const FModelD* m = (const FModelD*)d_models;
     const SampsonCut c = sampson_cut(thr2);
-    switch (kind) {
-        case 0: hipLaunchKernelGGL((mcv_f_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, c.lo, c.hi); break;
-        case 1: hipLaunchKernelGGL((mcv_f_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, c.lo, c.hi); break;
-        case 2: hipLaunchKernelGGL((mcv_f_verify<K, 2>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, c.lo, c.hi); break;
-        default: hipLaunchKernelGGL((mcv_f_verify<K, 3>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, c.lo, c.hi); break;
+    switch (f_variant()) {
+        case 1: launch_f_verify_kp<4, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
+        case 2: launch_f_verify_kp<6, 1>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
+        case 3: launch_f_verify_kp<6, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
+        case 4: launch_f_verify_kp<8, 1>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
+        case 5: launch_f_verify_kp<2, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
+        case 6: launch_f_verify_kp<3, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
+        case 7: launch_f_verify_kp<2, 4>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
+        default:
+            launch_f_verify_kp<kVerifyFHypPerWave, kVerifyFPtsPerLane>(p, N, m, d_counts, hypCount, thr2, kind, c.lo,
+                                                                       c.hi, s);
     }
 }
 
