@@ -10,7 +10,7 @@ finalize: mask of the winner, refit on its inliers and 10 LM iterations.
 Scaling: weak — each GPU evaluates its own 1M-hypothesis batch of the same problem (the union is
 one RANSAC call over N x 1M hypotheses), one 16-byte all-reduce per step.
 
-Printed JSON carries the live roofline of the dominant kernel (mcv_h_verify, HIP events on its
+Printed JSON carries the live roofline of the dominant kernel (mcv_h_verify_pk, HIP events on its
 launch stream; algorithmic bytes = 16 B x N correspondences per hypothesis) and the oracle's CPU
 throughput on a bounded sample of the same workload (rank 0, N = 1 only).
 """
@@ -42,14 +42,19 @@ P_THR_PX = 2.0
 THR = 5e-3
 SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue model of mcv_h_verify<6,2> (fused error): 15 VALU instructions per (hypothesis,
-# correspondence) evaluation, v_rcp_f32 at quarter rate -> 18 issue slots of 2 cycles (wave64 on
-# SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x 2.4 GHz / 2 x 64 lanes / 18.
+# VALU issue model of the packed sweep mcv_h_verify_pk<6,2> (fused error), per (hypothesis, pair of
+# correspondences): 12 v_pk_fma/mul_f32 (4 cycles each: two 32-lane passes per half), 2 v_rcp_f32
+# (quarter rate, 8 cycles), 2 v_cmp + 2 v_cmp_class (2 cycles) = 72 cycles = 36 per evaluation,
+# i.e. 18 issue slots of 2 cycles (wave64 on SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x
+# 2.4 GHz / 2 x 64 lanes / 18.
 VALU_SLOTS_PER_EVAL = 18
 F_FLOPS_PER_EVAL = 26          # fp64 Sampson (fused): 11 FMA + 2 mul + 1 div per (hypothesis, point)
 FP64_PEAK_TF = 78.6            # MI355X fp64 vector (spec)
 FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: fp32-input MFMA = fp32 vector peak
-HAMMING_PEAK_PAIRS = 256 * 4 * 2.4e9 / 2 * 64 / 20   # 20 VALU instructions per pair
+# Hamming issue model (measured per-instruction costs, scripts/exp/valu_rate.hip): per 64 pairs
+# 8 x (v_xor_b32 2 + v_bcnt_u32_b32 4) + v_lshl_or_b32 4 + v_med3_u32 4 + v_min_u32 2 = 58 cycles.
+HAMMING_CYC_PER_WAVE_PAIR = 58
+HAMMING_PEAK_PAIRS = 256 * 4 * 2.4e9 / HAMMING_CYC_PER_WAVE_PAIR * 64
 VALU_PEAK_EVALS = 256 * 4 * 2.4e9 / 2 * 64 / VALU_SLOTS_PER_EVAL
 
 
@@ -172,13 +177,15 @@ def bench_matcher(args):
                     "value": nq * args.steps / el, "unit": "queries/s",
                     "roofline": {"bound": "hbm", "achieved": 32.0 * pairs / (avg_ms * 1e-3) / 1e9,
                                  "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                 "frac": 32.0 * pairs / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                                 "frac": 32.0 * pairs / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                 "traffic": load_traffic("mcv_hamming_partial", f"{nq}x{nt}"),
                                  "kernel": "mcv_hamming_partial", "avg_launch_ms": avg_ms,
                                  "note": "algorithmic bytes = 32 B x Nt per query; data L2-resident, integer "
                                          "VALU-bound (see valu)",
                                  "valu": {"achieved": ach, "peak": HAMMING_PEAK_PAIRS, "unit": "pairs/s",
                                           "frac": ach / HAMMING_PEAK_PAIRS,
-                                          "model": "20 VALU instructions per (query, train) pair"}},
+                                          "model": f"{HAMMING_CYC_PER_WAVE_PAIR} SIMD cycles per 64 (query, "
+                                                   "train) pairs at 2.4 GHz"}},
                     "dtype": "u32", "scaling": "strong"}
         else:
             flops = 2.0 * cnt * nt * 128
@@ -186,7 +193,8 @@ def bench_matcher(args):
             line = {"metric": "BF L2 knn-2 TFLOP/s, SIFT-128 50k x 50k fp32 GEMM on MFMA (BASELINE config[4])",
                     "value": 2.0 * nq * nt * 128 * args.steps / el / 1e12, "unit": "TFLOP/s",
                     "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                                 "frac": tf / FP32_MFMA_PEAK_TF, "traffic": None, "kernel": "mcv_l2_mfma",
+                                 "frac": tf / FP32_MFMA_PEAK_TF,
+                                 "traffic": load_traffic("mcv_l2_mfma", f"{nq}x{nt}"), "kernel": "mcv_l2_mfma",
                                  "avg_launch_ms": avg_ms},
                     "dtype": "f32", "scaling": "strong"}
         line.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -211,14 +219,15 @@ def bench_matcher(args):
         dist.destroy_process_group()
 
 
-def load_traffic(n: int, hyps: int):
-    """HBM bytes per mcv_h_verify launch from the committed rocprofv3 PMC summary, if present."""
-    p = ROOT / "profiles" / "pmc_h_verify.json"
+def load_traffic(kernel: str, config: str):
+    """HBM bytes per launch of `kernel` on workload `config` from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json, written by scripts/collect_profiles.py), if present."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
         return None
     try:
-        d = json.loads(p.read_text())
-        if d.get("n") == n and d.get("hyps") == hyps:
+        d = json.loads(p.read_text()).get(kernel)
+        if d and d.get("config") == config:
             return d.get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -323,7 +332,7 @@ def bench_ransac(args):
         avg_ms = kms.value / max(launches, 1)
         alg_bytes = 16.0 * n * hyps            # per launch: every hypothesis reads all N float4 pairs
         achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-        traffic = load_traffic(n, hyps)
+        traffic = load_traffic("mcv_f_verify" if fund else "mcv_h_verify_pk", f"{n}x{hyps}")
         if not fund:
             line = {
                 "metric": "RANSAC hypotheses/sec @100k corrs; achieved HBM GB/s vs roofline, 1/2/4/8 GPU",
@@ -344,7 +353,7 @@ def bench_ransac(args):
                            "parallelism": f"hypothesis-sharded dp{world}"},
                 "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                              "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                             "kernel": "mcv_h_verify", "avg_launch_ms": avg_ms, "launches": launches,
+                             "kernel": "mcv_h_verify_pk", "avg_launch_ms": avg_ms, "launches": launches,
                              "algorithmic_bytes_per_launch": alg_bytes,
                              "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 6 "
                                      "hypotheses; the sweep's binding roof is VALU issue (see valu)",
@@ -376,7 +385,7 @@ def bench_ransac(args):
                            "correspondences": n, "hypotheses_total": total, "threshold": THR,
                            "parallelism": f"hypothesis-sharded dp{world}"},
                 "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                             "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                             "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                              "kernel": "mcv_f_verify", "avg_launch_ms": avg_ms, "launches": launches,
                              "algorithmic_bytes_per_launch": alg_bytes,
                              "fp64": {"achieved": fl, "peak": FP64_PEAK_TF, "unit": "TFLOP/s",

@@ -26,6 +26,10 @@ void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBeg
 void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
                      bool fused, const float* d_bbox, hipStream_t s);
 void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s);
+// Packed-f32 sweep of the fused error over the paired layout (ransac_h.hip, HPair: 32 B per 2).
+void launch_h_pair(const float* d_pts4, int N, void* d_pairs, hipStream_t s);
+bool launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
+                            int hypCount, float thr2, const float* d_bbox, hipStream_t s);
 void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, bool fused, uint8_t* d_mask,
                    int* d_count, hipStream_t s);
 void h_reduce_sums(const float* d_pts4, int N, const uint8_t* d_mask, double* d_part, double* d_out, hipStream_t s);

@@ -7,65 +7,151 @@
 //   * lane = query: each lane keeps its query's W words in VGPRs;
 //   * wave-uniform train index: the train descriptor arrives by scalar loads (SGPRs), so each
 //     XOR reads it as its scalar operand — no LDS traffic at all;
-//   * the train set is split into S chunks over the grid (>= ~4k waves to fill 256 CUs), each
+//   * train descriptors are staged in two ping-pong SGPR groups of 32 dwords by hand-issued
+//     s_load_dwordx16 bursts, so the scalar-load latency hides behind a group of VALU work;
+//   * the train set is split into S chunks over the grid (~8k waves: variant screen in
+//     scripts/sweep_hamming.sh), each
 //     (query-wave, chunk) keeps a top-2 of packed keys key = dist << 22 | trainIdx, so
 //     min(key) is "smallest distance, then lowest train index" (BFMatcher's first-minimum rule);
 //   * a merge kernel folds the S partial top-2s per query.
+// Issue cost per (query, train) pair on gfx950, measured (scripts/exp/valu_rate.hip): the VOP2
+// v_xor_b32 / v_min_u32 take 2 cycles per wave64 instruction, the VOP3-only v_bcnt_u32_b32 /
+// v_med3_u32 / v_lshl_or_b32 take 4 — 8 x (2 + 4) + 4 + 4 + 2 = 58 SIMD cycles per 64 pairs.
 #include "kernels.h"
 #include "mcv_runtime.h"
 #include "plan.h"
 #include <climits>
+#include <cstdlib>
 
 namespace mcv {
 
 static const int kIdxBits = 22;
 static const uint32_t kIdxMask = (1u << kIdxBits) - 1;
 
+// Top-2 of packed keys: with m1 <= m2 the new second best is med3(m1, k, m2) (one VALU op).
+__device__ __forceinline__ void top2_push(uint32_t& m1, uint32_t& m2, uint32_t k) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(m1), "v"(k), "v"(m2));
+    m2 = r;
+    m1 = min(m1, k);
+}
+
+// popcount(a ^ b) + acc as one v_xor_b32 + one accumulating v_bcnt_u32_b32 (the compiler would
+// otherwise re-associate the sum into v_bcnt(x, 0) + v_add3 trees: 1/3 more adds).
+__device__ __forceinline__ uint32_t xor_bcnt(uint32_t a, uint32_t b, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(a ^ b), "v"(acc));
+    return r;
+}
+
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+// 16 dwords (two 256-bit descriptors, or one 512-bit one) into SGPRs by one s_load_dwordx16,
+// issued by hand. The waitcnt pass does not see it: every use goes through sgpr_wait() first.
+// `live0/live1` (the other buffer) are tied to the load so the scheduler can neither consume the
+// other buffer above it nor hand its registers to this one.
+__device__ __forceinline__ u32x16 sload16(const uint32_t* p, u32x16& live0, u32x16& live1) {
+    u32x16 r;
+    asm volatile("s_load_dwordx16 %0, %3, 0x0" : "=&s"(r), "+s"(live0), "+s"(live1) : "s"(p));
+    return r;
+}
+// Scalar loads return out of order: only lgkmcnt(0) is a valid wait. The buffers are tied to the
+// wait (no use above it) and so is the running top-2 (the previous group's VALU work stays above).
+template <int Q>
+__device__ __forceinline__ void sgpr_wait(u32x16& a, u32x16& b, uint32_t (&m1)[Q], uint32_t (&m2)[Q]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a), "+s"(b), "+v"(m1[0]), "+v"(m2[0]));
+    if (Q > 1) asm volatile("; keep %0 %1" : "+v"(m1[Q - 1]), "+v"(m2[Q - 1]));
+}
+
 template <int W>
+__device__ __forceinline__ uint32_t hamming_key_v(const uint32_t* qv, const u32x16& v, int off, int j) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) d = xor_bcnt(qv[w], v[off + w], d);
+    return (d << kIdxBits) | (uint32_t)j;
+}
+
+// Lane = Q queries (their W words each in VGPRs); a wave covers 64 Q consecutive queries.
+// A group = 32 dwords (4 x 256-bit or 2 x 512-bit descriptors) in two SGPR vectors. Two groups
+// ping-pong: wait(A) -> issue B -> consume A -> wait(B) -> issue A' -> consume B, so each burst's
+// latency (K$ miss -> L2) hides behind a whole group of VALU work.
+template <int W, int Q>
 __global__ __launch_bounds__(256) void mcv_hamming_partial(const uint32_t* __restrict__ q, int nq,
                                                            const uint32_t* __restrict__ t, int nt, int chunkLen,
                                                            uint2* __restrict__ part) {
+    constexpr int G = 32 / W;  // descriptors per group
     const int lane = threadIdx.x & 63;
     const int qwave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     const int chunk = blockIdx.y;
-    const int qi = qwave * 64 + lane;
     const int tBegin = chunk * chunkLen;
     const int tEnd = min(tBegin + chunkLen, nt);
-    if (qwave * 64 >= nq) return;
+    if (qwave * 64 * Q >= nq) return;
 
-    uint32_t qv[W];
-    const int qsafe = qi < nq ? qi : nq - 1;
+    uint32_t qv[Q][W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) qv[w] = q[(size_t)qsafe * W + w];
+    for (int r = 0; r < Q; ++r) {
+        const int qi = (qwave * Q + r) * 64 + lane;
+        const int qsafe = qi < nq ? qi : nq - 1;
+#pragma unroll
+        for (int w = 0; w < W; ++w) qv[r][w] = q[(size_t)qsafe * W + w];
+    }
 
-    uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+    uint32_t m1[Q], m2[Q];
+#pragma unroll
+    for (int r = 0; r < Q; ++r) m1[r] = m2[r] = 0xFFFFFFFFu;
+    const int nGroups = (tEnd - tBegin) / G;
     int j = tBegin;
-    for (; j + 1 < tEnd; j += 2) {
-        const uint32_t* ta = t + (size_t)j * W;
-        const uint32_t* tb = ta + W;
-        uint32_t da = 0, db = 0;
+    auto consume = [&](const u32x16& lo, const u32x16& hi, int jj) {
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            da = da + __popc(qv[w] ^ ta[w]);
-            db = db + __popc(qv[w] ^ tb[w]);
+        for (int k = 0; k < G; ++k) {
+            const int off = k * W;
+#pragma unroll
+            for (int r = 0; r < Q; ++r) {
+                const uint32_t key = off < 16 ? hamming_key_v<W>(qv[r], lo, off, jj + k)
+                                               : hamming_key_v<W>(qv[r], hi, off - 16, jj + k);
+                top2_push(m1[r], m2[r], key);
+            }
         }
-        const uint32_t ka = (da << kIdxBits) | (uint32_t)j;
-        const uint32_t kb = (db << kIdxBits) | (uint32_t)(j + 1);
-        m2 = min(m2, max(m1, ka));
-        m1 = min(m1, ka);
-        m2 = min(m2, max(m1, kb));
-        m1 = min(m1, kb);
+    };
+    if (nGroups > 0) {
+        const uint32_t* tp = t + (size_t)j * W;
+        u32x16 a0 = {}, a1 = {}, b0 = {}, b1 = {};
+        a0 = sload16(tp, b0, b1);
+        a1 = sload16(tp + 16, b0, b1);
+        int g = 0;
+        for (; g + 1 < nGroups; g += 2, j += 2 * G) {
+            sgpr_wait<Q>(a0, a1, m1, m2);
+            const uint32_t* tb = t + (size_t)(j + G) * W;
+            b0 = sload16(tb, a0, a1);
+            b1 = sload16(tb + 16, a0, a1);
+            consume(a0, a1, j);
+            sgpr_wait<Q>(b0, b1, m1, m2);
+            const uint32_t* ta = t + (size_t)(g + 2 < nGroups ? j + 2 * G : j) * W;
+            a0 = sload16(ta, b0, b1);
+            a1 = sload16(ta + 16, b0, b1);
+            consume(b0, b1, j + G);
+        }
+        sgpr_wait<Q>(a0, a1, m1, m2);
+        if (g < nGroups) {
+            consume(a0, a1, j);
+            j += G;
+        }
     }
-    if (j < tEnd) {
-        const uint32_t* ta = t + (size_t)j * W;
-        uint32_t da = 0;
+    for (; j < tEnd; ++j) {
+        const uint32_t* td = t + (size_t)j * W;
 #pragma unroll
-        for (int w = 0; w < W; ++w) da += __popc(qv[w] ^ ta[w]);
-        const uint32_t ka = (da << kIdxBits) | (uint32_t)j;
-        m2 = min(m2, max(m1, ka));
-        m1 = min(m1, ka);
+        for (int r = 0; r < Q; ++r) {
+            uint32_t d = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) d = xor_bcnt(qv[r][w], td[w], d);
+            top2_push(m1[r], m2[r], (d << kIdxBits) | (uint32_t)j);
+        }
     }
-    if (qi < nq) part[(size_t)chunk * nq + qi] = make_uint2(m1, m2);
+#pragma unroll
+    for (int r = 0; r < Q; ++r) {
+        const int qi = (qwave * Q + r) * 64 + lane;
+        if (qi < nq) part[(size_t)chunk * nq + qi] = make_uint2(m1[r], m2[r]);
+    }
 }
 
 __global__ __launch_bounds__(256) void mcv_hamming_merge(const uint2* __restrict__ part, int nq, int nchunks,
@@ -127,8 +213,16 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         q = wk.qpack.p;
         t = wk.tpack.p;
     }
-    const int qwaves = (nq + 63) / 64;
-    int nchunks = (4096 + qwaves - 1) / qwaves;
+    static const int targetWaves = [] {
+        const char* e = getenv("MCV_HAMMING_WAVES");  // variant screen (scripts/sweep_hamming.sh)
+        return e ? atoi(e) : 8192;
+    }();
+    static const int Q = [] {
+        const char* e = getenv("MCV_HAMMING_Q");  // queries per lane (1 or 2; 2 screened slower)
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+    const int qwaves = (nq + 64 * Q - 1) / (64 * Q);
+    int nchunks = (targetWaves + qwaves - 1) / qwaves;
     const int maxChunks = nt > 0 ? (nt + 63) / 64 : 1;
     if (nchunks > maxChunks) nchunks = maxChunks;
     if (nchunks < 1) nchunks = 1;
@@ -136,10 +230,14 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     wk.part.ensure((size_t)nchunks * nq);
     dim3 grid((qwaves + 3) / 4, nchunks);
     ProfScope ps("hamming", s);
-    if (W == 8)
-        hipLaunchKernelGGL((mcv_hamming_partial<8>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
+    if (W == 8 && Q == 1)
+        hipLaunchKernelGGL((mcv_hamming_partial<8, 1>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
+    else if (W == 8)
+        hipLaunchKernelGGL((mcv_hamming_partial<8, 2>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
+    else if (Q == 1)
+        hipLaunchKernelGGL((mcv_hamming_partial<16, 1>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
     else
-        hipLaunchKernelGGL((mcv_hamming_partial<16>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
+        hipLaunchKernelGGL((mcv_hamming_partial<16, 2>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
     hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nchunks, d_idx,
                        d_dist, d_idx2, d_dist2);
     MCV_HIP(hipGetLastError());

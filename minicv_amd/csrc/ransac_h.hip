@@ -37,6 +37,9 @@ __global__ __launch_bounds__(256) void mcv_h_generate(const float* __restrict__ 
         models[i] = mf;
         counts[i] = 0;
     } else {
+        // the zero model (w = 1 everywhere) keeps the packed sweep's slot well-defined
+        for (int j = 0; j < 8; ++j) mf.h[j] = 0.f;
+        models[i] = mf;
         counts[i] = st;
     }
 }
@@ -120,10 +123,12 @@ __device__ __forceinline__ void h_sweep_trip(const float (&hm)[K][8], const floa
     }
 }
 
+// redo: count only the slots the packed sweep marked kStatusRedo (a wave with none exits).
 template <int K, int P, bool FUSED>
 __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ pts, int N,
                                                     const HModelF* __restrict__ models, int* __restrict__ counts,
-                                                    int hypCount, float thr2, const float* __restrict__ bbox) {
+                                                    int hypCount, float thr2, const float* __restrict__ bbox,
+                                                    int redo) {
     const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
     const int lane = threadIdx.x & 63;
     const int h0 = wave * K;
@@ -131,10 +136,12 @@ __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ p
 
     float hm[K][8];
     bool valid[K];
+    bool any = false;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int hk = h0 + k;
-        valid[k] = (hk < hypCount) && (counts[hk] >= 0);
+        valid[k] = (hk < hypCount) && (redo ? counts[hk] == kStatusRedo : counts[hk] >= 0);
+        any = any || valid[k];
         const HModelF m = models[valid[k] ? hk : h0];
 #pragma unroll
         for (int j = 0; j < 8; ++j) hm[k][j] = valid[k] ? m.h[j] : __builtin_nanf("");
@@ -145,6 +152,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ p
         asm volatile("" : "+v"(hm[k][5]));
     }
 
+    if (!any) return;
     uint32_t cnt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
@@ -193,6 +201,151 @@ __global__ __launch_bounds__(256) void mcv_h_verify(const float4* __restrict__ p
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (valid[k]) counts[h0 + k] = (int)cnt[k];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Packed-f32 inlier sweep (fused error). Two correspondences share a 64-bit VGPR pair per
+// coordinate, so every FMA of the error runs as one v_pk_fma_f32 over both (a VOP3 v_fma_f32
+// issues at the same cost as a v_pk_fma_f32 on gfx950: the packed form halves the FMA issue).
+// Layout: HPair p = correspondences (2p, 2p+1) as {x, y, x', y'} pairs, 32 B; an odd N is padded
+// with {0, 0, NaN, NaN}, whose error is NaN (never an inlier) and whose w is 1 (never "bad").
+// Model coefficients stay in SGPRs and are broadcast to both halves with op_sel / op_sel_hi.
+// Every operation rounds exactly like h_denominator_fused / rcp_newton / h_error_fused_ww.
+// ------------------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct HPair {
+    f2 x, y, mx, my;
+};
+
+__global__ __launch_bounds__(256) void mcv_h_pair(const float4* __restrict__ pts, int N, HPair* __restrict__ out) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= (N + 1) / 2) return;
+    const float4 a = pts[2 * p];
+    const float nan = __builtin_nanf("");
+    const float4 b = 2 * p + 1 < N ? pts[2 * p + 1] : make_float4(0.f, 0.f, nan, nan);
+    HPair o;
+    o.x = f2{a.x, b.x};
+    o.y = f2{a.y, b.y};
+    o.mx = f2{a.z, b.z};
+    o.my = f2{a.w, b.w};
+    out[p] = o;
+}
+
+// Packed FMA through the compiler (llvm.fma.v2f32 -> v_pk_fma_f32): it folds a splat of an SGPR
+// coefficient into op_sel / op_sel_hi and inserts the wait states between dependent packed ops
+// (hand-written asm would not get them: the hazard recognizer does not see into inline asm).
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// Broadcast one half of a coefficient pair: a shuffle the backend folds into op_sel / op_sel_hi.
+__device__ __forceinline__ f2 lo(f2 v) { return __builtin_shufflevector(v, v, 0, 0); }
+__device__ __forceinline__ f2 hi(f2 v) { return __builtin_shufflevector(v, v, 1, 1); }
+
+// One trip: NP pairs per lane against the wave's K hypotheses.
+template <int K, int NP, bool PRED>
+__device__ __forceinline__ void h_pk_trip(const f2 (&hp)[K][4], const f2 (&hc)[K], const HPair (&q)[NP],
+                                          const bool (&v)[NP], float thr2, f2 one, uint32_t (&cnt)[K],
+                                          uint64_t& bad) {
+    auto vote = [&](int j, bool pred) -> uint32_t {
+        if constexpr (PRED)
+            return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(v[j] && pred));
+        else
+            return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(pred));
+    };
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        // Re-define the pairs in the trip (no instruction): a broadcast is then built per use and
+        // folds into op_sel / op_sel_hi, instead of being hoisted out of the loop as a splat pair
+        // (which doubles the SGPRs the models take and spills them).
+        f2 p0 = hp[k][0], p1 = hp[k][1], p2 = hp[k][2], p3 = hp[k][3];   // (h0,h1) .. (h6,h7)
+        f2 c = hc[k];                                                       // (h2, h5)
+        asm volatile("" : "+s"(p0), "+s"(p1), "+s"(p2), "+s"(p3), "+v"(c));
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            f2 W = pk_fma(lo(p3), q[j].x, pk_fma(hi(p3), q[j].y, one));
+            const f2 U = pk_fma(lo(p0), q[j].x, pk_fma(hi(p0), q[j].y, lo(c)));
+            const f2 V = pk_fma(hi(p1), q[j].x, pk_fma(lo(p2), q[j].y, hi(c)));
+            bad |= class_mask(W.x, kClassNotNormal) | class_mask(W.y, kClassNotNormal);
+            f2 R = f2{__builtin_amdgcn_rcpf(W.x), __builtin_amdgcn_rcpf(W.y)};
+            const f2 E = pk_fma(-W, R, one);              // fma(-w, r, 1)
+            R = pk_fma(E, R, R);                          // fma(e, r, r)
+            const f2 DX = pk_fma(U, R, -q[j].mx);         // fma(u, r, -x')
+            const f2 DY = pk_fma(V, R, -q[j].my);         // fma(v, r, -y')
+            const f2 ERR = pk_fma(DX, DX, DY * DY);       // fma(ex, ex, ey * ey)
+            cnt[k] += vote(j, ERR.x <= thr2) + vote(j, ERR.y <= thr2);
+        }
+    }
+}
+
+// A wave whose hypotheses fail the bounding-box precondition, or which meets a "bad" denominator
+// (0, denormal, inf, NaN) in any trip, marks its valid slots kStatusRedo instead of writing
+// counts; mcv_h_verify<.., redo = true> then recounts exactly those slots with the scalar sweep
+// (IEEE division fallback). Keeping the exact path out of this kernel keeps its registers free.
+template <int K, int NP>
+__global__ __launch_bounds__(256) void mcv_h_verify_pk(const HPair* __restrict__ pairs, int nPairs,
+                                                       const HModelF* __restrict__ models, int* __restrict__ counts,
+                                                       int hypCount, float thr2, const float* __restrict__ bbox) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    const int lane = threadIdx.x & 63;
+    const int h0 = wave * K;
+    if (h0 >= hypCount) return;
+
+    // Every slot below hypCount holds a model (mcv_h_generate writes the zero model, w = 1, for a
+    // failed hypothesis); slots past hypCount re-read the last one. Reading the models unselected
+    // keeps the (h0,h1) .. (h6,h7) SGPR pairs intact: coefficients broadcast by op_sel.
+    f2 hp[K][4], hc[K];
+    bool valid[K];
+    const float X = bbox[0], Y = bbox[1];
+    bool fast = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int hk = h0 + k;
+        valid[k] = (hk < hypCount) && (counts[hk] >= 0);
+        const f2* mp = (const f2*)&models[hk < hypCount ? hk : hypCount - 1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hp[k][j] = mp[j];
+        // h2, h5 are the addends of fma(h1, y, h2) / fma(h4, y, h5), beside an SGPR multiplier:
+        // one VGPR pair per hypothesis (constant-bus limit), broadcast by op_sel as well.
+        hc[k] = f2{hp[k][1].x, hp[k][2].y};
+        asm volatile("" : "+v"(hc[k]));
+        // precondition (as mcv_h_verify): max |w| over the bounding box below 2^125
+        const float wmax = fabsf(hp[k][3].x) * X + fabsf(hp[k][3].y) * Y + 1.f;
+        fast = fast && !(valid[k] && !(wmax < 0x1p125f));
+    }
+    const f2 one = f2{1.f, 1.f};
+
+    uint32_t cnt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt[k] = 0;
+    uint64_t bad = 0;
+    if (fast) {
+        constexpr int TRIP = 64 * NP;
+        const int nFull = nPairs / TRIP * TRIP;
+        bool vt[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) vt[j] = true;
+        for (int base = 0; base < nFull; base += TRIP) {
+            HPair q[NP];
+#pragma unroll
+            for (int j = 0; j < NP; ++j) q[j] = pairs[base + 64 * j + lane];
+            h_pk_trip<K, NP, false>(hp, hc, q, vt, thr2, one, cnt, bad);
+        }
+        if (nFull < nPairs) {
+            HPair q[NP];
+            bool v[NP];
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {
+                const int p = nFull + 64 * j + lane;
+                v[j] = p < nPairs;
+                q[j] = pairs[v[j] ? p : 0];
+            }
+            h_pk_trip<K, NP, true>(hp, hc, q, v, thr2, one, cnt, bad);
+        }
+    }
+    const bool redo = !fast || bad != 0;
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid[k]) counts[h0 + k] = redo ? kStatusRedo : (int)cnt[k];
     }
 }
 
@@ -431,15 +584,15 @@ void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s) {
 
 template <int K, int P>
 static void launch_h_verify_kp(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount,
-                               float thr2, bool fused, const float* d_bbox, hipStream_t s) {
+                               float thr2, bool fused, const float* d_bbox, hipStream_t s, int redo = 0) {
     const int waves = (hypCount + K - 1) / K;
     const int blocks = (waves + 3) / 4;
     if (fused)
         hipLaunchKernelGGL((mcv_h_verify<K, P, true>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
-                           (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox);
+                           (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox, redo);
     else
         hipLaunchKernelGGL((mcv_h_verify<K, P, false>), dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
-                           (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox);
+                           (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox, redo);
 }
 
 // Sweep shape (hypotheses per wave K, correspondences per lane per trip P). MCV_SWEEP_VARIANT
@@ -466,9 +619,52 @@ void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_co
         case 9: launch_h_verify_kp<4, 3>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
         case 10: launch_h_verify_kp<3, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
         case 11: launch_h_verify_kp<7, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
+        case 19: launch_h_verify_kp<6, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
         default:
             launch_h_verify_kp<kVerifyHypPerWave, kVerifyPtsPerLane>(d_pts4, N, d_models, d_counts, hypCount, thr2,
                                                                      fused, d_bbox, s);
+    }
+}
+
+template <int K, int NP>
+static void launch_h_verify_pk_k(const void* d_pairs, int N, const void* d_models, int* d_counts, int hypCount,
+                                 float thr2, const float* d_bbox, hipStream_t s) {
+    const int waves = (hypCount + K - 1) / K;
+    const int blocks = (waves + 3) / 4;
+    hipLaunchKernelGGL((mcv_h_verify_pk<K, NP>), dim3(blocks), dim3(256), 0, s, (const HPair*)d_pairs, (N + 1) / 2,
+                       (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox);
+}
+
+void launch_h_pair(const float* d_pts4, int N, void* d_pairs, hipStream_t s) {
+    const int np = (N + 1) / 2;
+    hipLaunchKernelGGL(mcv_h_pair, dim3((np + 255) / 256), dim3(256), 0, s, (const float4*)d_pts4, N,
+                       (HPair*)d_pairs);
+}
+
+static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d_models, int* d_counts,
+                                       int hypCount, float thr2, const float* d_bbox, hipStream_t s);
+
+// Packed sweep (fused error) + the exact recount of the slots it marked kStatusRedo. Returns false
+// when the variant screen selects the scalar sweep.
+bool launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
+                            int hypCount, float thr2, const float* d_bbox, hipStream_t s) {
+    if (!launch_h_verify_pk_variant(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s)) return false;
+    launch_h_verify_kp<kVerifyHypPerWave, kVerifyPtsPerLane>(d_pts4, N, d_models, d_counts, hypCount, thr2, true,
+                                                             d_bbox, s, 1);
+    return true;
+}
+
+static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d_models, int* d_counts,
+                                       int hypCount, float thr2, const float* d_bbox, hipStream_t s) {
+    switch (sweep_variant()) {
+        case 0: launch_h_verify_pk_k<6, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 26: launch_h_verify_pk_k<6, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 20: launch_h_verify_pk_k<4, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 21: launch_h_verify_pk_k<8, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 22: launch_h_verify_pk_k<4, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 24: launch_h_verify_pk_k<3, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 25: launch_h_verify_pk_k<5, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        default: return false;
     }
 }
 

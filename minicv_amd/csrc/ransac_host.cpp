@@ -306,10 +306,16 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
     const double t = effective_threshold(cfg);
     const float thr2 = (float)(t * t);
     if (P.model == MCV_MODEL_HOMOGRAPHY) {
-        if (fused_error(cfg)) launch_bbox(d_pts, N, P.bbox.p, s);
+        const bool fused = fused_error(cfg);
+        if (fused) {
+            launch_bbox(d_pts, N, P.bbox.p, s);
+            P.pairs.ensure((size_t)(N + 1) / 2 * 8);
+            launch_h_pair(d_pts, N, P.pairs.p, s);
+        }
         launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
         ProfScope ps("h_verify", s);
-        launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, fused_error(cfg), P.bbox.p, s);
+        if (!fused || !launch_h_verify_packed(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bbox.p, s))
+            launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, fused, P.bbox.p, s);
     } else {
         launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
         ProfScope ps("f_verify", s);

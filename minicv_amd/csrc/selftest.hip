@@ -66,7 +66,8 @@ extern "C" MCV_API long long mcvTestRcpExhaustive(int mode, uint32_t* firstMisma
 
 // Run the homography inlier sweep on caller-supplied fp32 models (host arrays): exercises the
 // rare exact-division paths of mcv_h_verify with crafted models (zero / denormal / huge
-// denominators) that random hypotheses practically never produce.
+// denominators) that random hypotheses practically never produce. fused: 0 = op-by-op error,
+// 1 = fused error (scalar sweep), 2 = fused error through the packed sweep mcv_h_verify_pk.
 extern "C" MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models8, int nModels,
                                               float thr2, int fused, int* counts) {
     MCV_GUARD(0, {
@@ -82,7 +83,16 @@ extern "C" MCV_API int mcvTestHomographySweep(const float* pts4, int N, const fl
         MCV_HIP(hipMemcpy(m.p, models8, (size_t)nModels * 32, hipMemcpyHostToDevice));
         MCV_HIP(hipMemset(c.p, 0, (size_t)nModels * 4));
         launch_bbox(p.p, N, bb.p, 0);
-        launch_h_verify(p.p, N, m.p, c.p, nModels, thr2, fused != 0, bb.p, 0);
+        if (fused == 2) {   // packed sweep + exact recount of the slots it marks kStatusRedo
+            DevBuf<float> pairs;
+            pairs.ensure((size_t)(N + 1) / 2 * 8);
+            launch_h_pair(p.p, N, pairs.p, 0);
+            if (!launch_h_verify_packed(p.p, pairs.p, N, m.p, c.p, nModels, thr2, bb.p, 0))
+                fail("packed sweep disabled by MCV_SWEEP_VARIANT");
+            MCV_HIP(hipDeviceSynchronize());
+        } else {
+            launch_h_verify(p.p, N, m.p, c.p, nModels, thr2, fused != 0, bb.p, 0);
+        }
         MCV_HIP(hipGetLastError());
         MCV_HIP(hipMemcpy(counts, c.p, (size_t)nModels * 4, hipMemcpyDeviceToHost));
         return 1;

@@ -2,9 +2,12 @@
 """Copy the judged evidence from gpurun_out/ (scratch) into profiles/ (tracked):
   gpurun_out/bench_<w>.log           -> profiles/<round>_bench_<w>.json   (the bench JSON line)
   gpurun_out/prof_<w>/run_kernel_stats.csv -> profiles/<round>/kernel_stats_<w>.csv
-  gpurun_out/pmc_{fetch,write,sq}/run_counter_collection.csv -> profiles/<round>/pmc_*_counters.csv
-and derive profiles/pmc_h_verify.json (HBM bytes per mcv_h_verify launch with the gfx950
-FETCH_SIZE x2 correction of MI355X_MICROARCH.md, plus SQ counters). Usage: collect_profiles.py r01
+  gpurun_out/pmc_{fetch,write}_<w>/run_counter_collection.csv -> profiles/<round>/pmc_{fetch,write}_<w>.csv
+  gpurun_out/pmc_sq/run_counter_collection.csv -> profiles/<round>/pmc_sq_homography.csv
+and derive profiles/pmc_traffic.json: HBM bytes per launch of each workload's dominant kernel
+(FETCH_SIZE x2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), keyed by kernel with
+the workload config it was measured on (bench.py reads it for `roofline.traffic`), plus the SQ
+counters of the homography sweep. Usage: collect_profiles.py r01
 """
 import csv
 import json
@@ -17,6 +20,9 @@ ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "gpurun_out"
 PROF = ROOT / "profiles"
 WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2"]
+# dominant kernel per BASELINE workload (substring of the demangled rocprofv3 kernel name)
+KERNELS = {"homography": "mcv_h_verify_pk", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
+           "l2": "mcv_l2_mfma"}
 
 
 def last_json(path: Path):
@@ -52,37 +58,59 @@ def main():
         ks = OUT / f"prof_{w}" / "run_kernel_stats.csv"
         if ks.exists():
             shutil.copy(ks, PROF / rnd / f"kernel_stats_{w}.csv")
-    pmc = {}
-    for name in ("fetch", "write", "sq"):
-        src = OUT / f"pmc_{name}" / "run_counter_collection.csv"
-        if src.exists():
-            shutil.copy(src, PROF / rnd / f"pmc_{name}_counters.csv")
-            pmc[name] = pmc_sums(src, "mcv_h_verify")
-    if {"fetch", "write"} <= pmc.keys() and pmc["fetch"].get("FETCH_SIZE"):
-        hb = json.loads((PROF / f"{rnd}_bench_homography.json").read_text())
-        n = hb["config"]["correspondences"]
-        hyps = hb["config"]["hypotheses_per_gpu"]
-        mean = lambda xs: sum(xs) / len(xs)
-        fetch_kb = mean(pmc["fetch"]["FETCH_SIZE"])
-        write_kb = mean(pmc["write"]["WRITE_SIZE"])
-        sq = {k: mean(v) for k, v in sorted(pmc.get("sq", {}).items())}
-        d = {
-            "kernel": "mcv_h_verify (default variant)", "n": n, "hyps": hyps,
-            "FETCH_SIZE_KB": fetch_kb, "WRITE_SIZE_KB": write_kb,
-            "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024.0,
-            "correction": "FETCH_SIZE x2 (gfx950 counts half of a wide streaming read, MI355X_MICROARCH.md HBM); "
-                          "WRITE_SIZE as reported; units KB",
-            "algorithmic_bytes_per_launch": 16 * n * hyps,
-            "sq": sq,
-            "source": f"rocprofv3 --kernel-trace --pmc (three separate passes), bench.py --steps 3, round {rnd}",
+    traffic = {}
+    mean = lambda xs: sum(xs) / len(xs)
+    for w, kernel in KERNELS.items():
+        fetch = OUT / f"pmc_fetch_{w}" / "run_counter_collection.csv"
+        write = OUT / f"pmc_write_{w}" / "run_counter_collection.csv"
+        if not (fetch.exists() and write.exists()):
+            continue
+        shutil.copy(fetch, PROF / rnd / f"pmc_fetch_{w}.csv")
+        shutil.copy(write, PROF / rnd / f"pmc_write_{w}.csv")
+        f = pmc_sums(fetch, kernel).get("FETCH_SIZE")
+        wr = pmc_sums(write, kernel).get("WRITE_SIZE")
+        if not f or not wr:
+            continue
+        j = last_json(PROF / f"{rnd}_bench_{w}.json") if (PROF / f"{rnd}_bench_{w}.json").exists() else None
+        c = j["config"] if j else {}
+        if w == "homography":
+            config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_per_gpu')}", \
+                16.0 * c.get("correspondences", 0) * c.get("hypotheses_per_gpu", 0)
+        elif w == "fundamental":
+            config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
+                16.0 * c.get("correspondences", 0) * c.get("hypotheses_total", 0)
+        else:
+            config = f"{c.get('queries')}x{c.get('train')}"
+            dim_bytes = 32.0 if w == "hamming" else 512.0
+            alg = dim_bytes * c.get("queries", 0) * c.get("train", 0)
+        traffic[kernel] = {
+            "workload": w, "config": config,
+            "FETCH_SIZE_KB": mean(f), "WRITE_SIZE_KB": mean(wr), "dispatches": len(f),
+            "hbm_bytes_per_launch": (2 * mean(f) + mean(wr)) * 1024.0,
+            "algorithmic_bytes_per_launch": alg,
         }
-        if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_INSTS_VALU"):
-            ms = hb["roofline"]["avg_launch_ms"]
-            # GRBM_GUI_ACTIVE is summed over the 8 XCDs' GRBM instances
-            d["derived"] = {"clock_GHz": sq["GRBM_GUI_ACTIVE"] / 8 / (ms * 1e-3) / 1e9,
-                            "valu_instr_per_eval": sq["SQ_INSTS_VALU"] * 64 / (n * hyps)}
-        (PROF / "pmc_h_verify.json").write_text(json.dumps(d, indent=1) + "\n")
-        print("pmc", d["hbm_bytes_per_launch"], d.get("derived"))
+        print("traffic", kernel, traffic[kernel]["hbm_bytes_per_launch"])
+    sq_src = OUT / "pmc_sq" / "run_counter_collection.csv"
+    if sq_src.exists():
+        shutil.copy(sq_src, PROF / rnd / "pmc_sq_homography.csv")
+        sq = {k: mean(v) for k, v in sorted(pmc_sums(sq_src, KERNELS["homography"]).items())}
+        if "mcv_h_verify_pk" in traffic:
+            t = traffic["mcv_h_verify_pk"]
+            d = {"sq": sq}
+            hb = last_json(PROF / f"{rnd}_bench_homography.json")
+            if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_INSTS_VALU") and hb:
+                ms = hb["roofline"]["avg_launch_ms"]
+                evals = t["algorithmic_bytes_per_launch"] / 16.0
+                # GRBM_GUI_ACTIVE is summed over the 8 XCDs' GRBM instances
+                d["derived"] = {"clock_GHz": sq["GRBM_GUI_ACTIVE"] / 8 / (ms * 1e-3) / 1e9,
+                                "valu_instr_per_eval": sq["SQ_INSTS_VALU"] * 64 / evals}
+            t["counters"] = d
+    if traffic:
+        for v in traffic.values():
+            v["correction"] = ("FETCH_SIZE x2 (gfx950 counts half of a wide streaming read, MI355X_MICROARCH.md "
+                               "HBM) + WRITE_SIZE; units KB")
+            v["source"] = f"rocprofv3 --kernel-trace --pmc (one counter per pass), bench.py, round {rnd}"
+        (PROF / "pmc_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
 
 
 if __name__ == "__main__":

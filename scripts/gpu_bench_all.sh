@@ -10,7 +10,7 @@ step() {   # name timeout cmd...
     echo "$name rc=$rc"; tail -2 "gpurun_out/$name.log"
     if [ $rc -gt 1 ]; then exit $rc; fi
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -q
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step bench_homography 300 python bench.py --steps 10 --warmup 3 --cpu-seconds 8
 step bench_fundamental 300 python bench.py --workload fundamental --steps 5 --warmup 1 --cpu-seconds 8
 step bench_hamming 300 python bench.py --workload hamming --steps 20 --warmup 3

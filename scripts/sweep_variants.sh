@@ -1,7 +1,8 @@
 #!/bin/bash
 # Screen sweep shapes (MCV_SWEEP_VARIANT) on the headline bench; one process per variant.
+#   0 / 20-26: packed-f32 sweep mcv_h_verify_pk<K, pairs per lane> (0 = <6, 2>); 19: scalar mcv_h_verify<6, 2>.
 mkdir -p gpurun_out
-for v in ${VARIANTS:-0 1 2 3 4 5 0}; do
+for v in ${VARIANTS:-0 19 20 21 22 24 25 26}; do
     MCV_SWEEP_VARIANT=$v timeout -k 10 200 python bench.py --steps 8 --warmup 2 --no-cpu-baseline > gpurun_out/variant_$v.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { tail -3 gpurun_out/variant_$v.log; exit $rc; }
     python -c "import json,sys; d=json.loads([l for l in open('gpurun_out/variant_$v.log') if l.startswith('{')][0]); print('variant $v', round(d['value']/1e6,2), 'Mhyp/s', round(d['roofline']['avg_launch_ms'],2), 'ms', d['result']['best_count'])"

@@ -41,8 +41,9 @@ def crafted_models():
     return np.stack(ms)
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_sweep_rare_paths_bit_exact(native, gpu, oracle, fused):
+@pytest.mark.parametrize("mode", [0, 1, 2])   # op-by-op, fused scalar sweep, fused packed sweep
+def test_sweep_rare_paths_bit_exact(native, gpu, oracle, mode):
+    fused = mode != 0
     rng = np.random.default_rng(1)
     n = 1000 + 77
     pts = rng.uniform(-1, 1, size=(n, 4)).astype(np.float32)
@@ -55,7 +56,7 @@ def test_sweep_rare_paths_bit_exact(native, gpu, oracle, fused):
     counts = np.zeros(len(models), np.int32)
     thr2 = np.float32(0.05 ** 2)
     ok = native.lib().mcvTestHomographySweep(pts.ctypes.data, n, models.ctypes.data, len(models), float(thr2),
-                                             int(fused), counts.ctypes.data)
+                                             mode, counts.ctypes.data)
     assert ok == 1, native.last_error()
     ref = np.array([oracle.h_count(pts, m, float(thr2), fused=fused) for m in models], np.int32)
     np.testing.assert_array_equal(counts, ref)
