@@ -67,7 +67,8 @@ def parse():
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="homography", choices=["homography", "fundamental", "essential", "pnp", "hamming", "l2"],
+    ap.add_argument("--workload", default="homography",
+                    choices=["homography", "fundamental", "essential", "pnp", "hamming", "l2", "scaled"],
                     help="homography = the headline (BASELINE config[2]); the others are config[1], [3], [4]")
     return ap.parse_args()
 
@@ -238,6 +239,8 @@ def main():
     args = parse()
     if args.workload in ("hamming", "l2"):
         return bench_matcher(args)
+    if args.workload == "scaled":
+        return bench_scaled(args)
     return bench_ransac(args)
 
 
@@ -629,6 +632,110 @@ def bench_pnp(args, world, rank, dev):
                                 if world == 1 and not args.no_cpu_baseline else None)
         print(json.dumps(line), flush=True)
     plan.close()
+
+
+S_N_OBS = 20_000              # CameraPose.findScaled: observations per call (2 N candidates)
+S_SEED = 11
+S_FLOPS_PER_TERM = 30         # per (candidate, observation): 28 fp64 add/sub/mul + 2 divisions
+
+
+def bench_scaled(args):
+    """CameraPose.findScaled (the managed O(N^2) scale search, on the GPU behind cvFindScaledPose):
+    a step = one call on HBM-resident observations: 2 N candidate scales, each verified against all
+    N observations, then the first-minimum selection. Ranks run independent replicas (the path has
+    no exchange step; weak scaling)."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from minicv_amd import native as NL, synthetic as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    n = args.n if args.n != N_CORR else S_N_OBS
+    src, pose, W, O, inl = S.scaled_problem(n, seed=S_SEED, outlier_frac=0.3, sigma=1e-3, true_scale=2.5)
+    Wd = torch.from_numpy(np.ascontiguousarray(W)).to(dev)
+    Od = torch.from_numpy(np.ascontiguousarray(O)).to(dev)
+    cam = src.to_c()
+    R = NL.M33d()
+    R.M[:] = pose.Rotation.reshape(9)
+    t = NL.V3d(*pose.Translation)
+    cost, sc = C.c_double(0), C.c_double(0)
+    stream = torch.cuda.current_stream().cuda_stream
+    res = {}
+
+    def step():
+        k = NL.lib().mcvFindScaledPoseDevice(C.addressof(cam), Wd.data_ptr(), Od.data_ptr(), n, C.addressof(R),
+                                             C.addressof(t), C.addressof(cost), C.addressof(sc), stream)
+        NL.check(k >= 0, "mcvFindScaledPoseDevice")
+        res.update(candidates=k, cost=cost.value, scale=sc.value)
+
+    for _ in range(args.warmup):
+        step()
+    NL.lib().mcvProfileReset()
+    NL.lib().mcvProfileEnable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    NL.lib().mcvProfileEnable(0)
+    kms = C.c_double(0)
+    launches = NL.lib().mcvProfileRead(b"scaled_costs", C.addressof(kms))
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    if rank == 0:
+        avg_ms = kms.value / max(launches, 1)
+        cands = 2 * n
+        terms = cands * n
+        tf = S_FLOPS_PER_TERM * terms / (avg_ms * 1e-3) / 1e12
+        line = {
+            "metric": "CameraPose.findScaled candidate scales/sec (2 N candidates x N observations)",
+            "value": world * cands * args.steps / el, "unit": "candidates/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded lookAt camera + relative pose, 30% outlier observations, sigma 1e-3)",
+            "config": {"workload": f"findScaled, {n} observations -> {cands} candidate scales, replicas on {world} "
+                                   f"GPU(s)", "observations": n, "parallelism": f"replicas x{world}"},
+            "roofline": {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TF, "unit": "TFLOP/s",
+                         "frac": tf / FP64_PEAK_TF, "traffic": None, "kernel": "mcv_scaled_costs",
+                         "avg_launch_ms": avg_ms, "launches": launches,
+                         "model": f"{S_FLOPS_PER_TERM} fp64 FLOP per (candidate, observation), a division "
+                                  "counted as one", "terms_per_launch": terms},
+            "result": {"evaluated_candidates": res["candidates"], "cost": res["cost"], "scale": res["scale"]},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, str(ROOT / "tests"))
+            import _oracle as O_
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+            cam14 = np.concatenate([src.location, src.forward, src.up, src.right, src.focal])
+            t1 = time.perf_counter()
+            O_.scaled_costs_sample(cam14, W, O, pose.Rotation, pose.Translation, threads, threads)
+            cal = (time.perf_counter() - t1) / threads
+            sample = int(min(cands, max(threads, args.cpu_seconds / max(cal, 1e-9))))
+            t1 = time.perf_counter()
+            O_.scaled_costs_sample(cam14, W, O, pose.Rotation, pose.Translation, sample, threads)
+            ct = time.perf_counter() - t1
+            line["cpu_baseline"] = {"value": sample / ct, "unit": "candidates/s", "cores": threads, "kind": "port",
+                                    "sample": f"{sample} candidates x {n} observations, oracle/oracle_scaled.c, "
+                                              f"OpenMP {threads} threads, {ct:.1f} s"}
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -221,6 +221,36 @@ MCV_API const char* mcvGetLastError(void);
 MCV_API int mcvDeviceCount(void);
 MCV_API const char* mcvVersion(void);
 
+/* CameraPose.findScaled — src/MiniCV/CameraPose.fs:39-134, the managed
+ * O(N^2) scale hypothesize-and-verify, moved onto the GPU behind a new export. The F# wrapper keeps
+ * its signature `findScaled inlierThreshold srcCam worldObservations pose` and passes the tuple
+ * list as two arrays; it builds `scale bestScale pose` itself from *outScale.
+ *   candidates: for observation i (list order), the pose scales s = -z / n from the dst0 frame
+ *     (CameraPose.fs:103-117), s.X then s.Y; skipped when |n.X| or |n.Y| < 1e-5 (Fun.IsTiny);
+ *   cost(s) = avgReprojectionError s (CameraPose.fs:71-87): mean of |project1 dstCam(s) w - obs|^2
+ *     over the observations visible in dstCam(s) (Camera.fs:72-83), +inf if none;
+ *   selection: first strictly smaller cost wins (CameraPose.fs:119-125).
+ * inlierThreshold is accepted and unused, as in the reference (only the dead countInliers uses it).
+ * Writes *outCost = best cost (+inf when no candidate improves on +inf) and *outScale = its scale
+ * (0 then). Returns the number of candidate scales evaluated (2 per non-tiny observation), -1 on
+ * failure. N == 0 returns 0 with *outCost = +inf, *outScale = 0 (the reference's empty-list case). */
+typedef struct {             /* Camera.fs:7-14, F# record field order: 13 doubles */
+    mcvV3d location;
+    mcvV3d forward;
+    mcvV3d up;
+    mcvV3d right;
+    mcvV2d focal;
+} mcvCamera;
+MCV_API int cvFindScaledPose(double inlierThreshold, const mcvCamera* srcCam, const mcvV3d* worldPoints,
+                             const mcvV2d* observations, int N, const mcvM33d* rotation, const mcvV3d* translation,
+                             double* outCost, double* outScale);
+/* Per-candidate costs of cvFindScaledPose (test / analysis helper): scales[2N] and costs[2N] in
+ * candidate order (slot 2i = s.X, 2i+1 = s.Y of observation i; a skipped observation has NaN scales
+ * and +inf costs). Returns N, -1 on failure. */
+MCV_API int cvFindScaledPoseCosts(const mcvCamera* srcCam, const mcvV3d* worldPoints, const mcvV2d* observations,
+                                  int N, const mcvM33d* rotation, const mcvV3d* translation, double* scales,
+                                  double* costs);
+
 /* ------------------------------------------------------------------------------------------
  * (3) Device-level API: device pointers, caller's stream (hipStream_t as void*), current device.
  *     Points on device are packed fp32 correspondences float4 {x, y, x', y'} (16 B each).
@@ -293,6 +323,12 @@ MCV_API int mcvMatchHammingDevice(const uint8_t* d_q, int nq, const uint8_t* d_t
 MCV_API int mcvMatchL2Device(const float* d_q, int nq, const float* d_t, int nt, int dim,
                              int* d_idx, float* d_dist, int* d_idx2, float* d_dist2, void* stream);
 
+/* Device-level CameraPose.findScaled: d_world V3d[N], d_obs V2d[N] on the device. Synchronises
+ * `stream`; same outputs and return value as cvFindScaledPose. */
+MCV_API int mcvFindScaledPoseDevice(const mcvCamera* srcCam, const mcvV3d* d_world, const mcvV2d* d_obs, int N,
+                                    const mcvM33d* rotation, const mcvV3d* translation, double* outCost,
+                                    double* outScale, void* stream);
+
 /* Opt-in kernel timing: HIP events recorded around the inlier-sweep launches on their stream.
  * mcvProfileRead returns the number of launches of `kernel` ("h_verify", "f_verify") and their
  * summed duration in ms (synchronises the recorded events). */
@@ -327,6 +363,10 @@ MCV_API void mcvHostRodrigues(const double* r, double* R, double* dR27);
 MCV_API void mcvHostRodriguesInv(const double* R, double* r);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                            uint32_t* out4);
+/* Host twin of CameraPose.findScaled: the same candidates and costs as cvFindScaledPoseCosts,
+ * computed by the host-compiled kernel code with the reference's sequential sums (list order). */
+MCV_API int mcvHostScaledCosts(const mcvCamera* srcCam, const mcvV3d* worldPoints, const mcvV2d* observations, int N,
+                               const mcvM33d* rotation, const mcvV3d* translation, double* scales, double* costs);
 
 #ifdef __cplusplus
 }

@@ -128,4 +128,9 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
 int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim, int* d_idx, float* d_dist,
                     int* d_idx2, float* d_dist2, hipStream_t s);
 
+// ---- CameraPose.findScaled (scaled_pose.hip)
+struct ScaledSetup;
+void launch_scaled(const ScaledSetup& S, const double* d_w3, const double* d_o2, int N, double* d_soa,
+                   double* d_scales, uint8_t* d_used, double* d_costs, long long* d_out, hipStream_t s);
+
 }  // namespace mcv

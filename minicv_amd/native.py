@@ -28,6 +28,11 @@ class M33d(C.Structure):
     _fields_ = [("M", C.c_double * 9)]
 
 
+class Camera(C.Structure):
+    """mcvCamera: the MiniCV Camera record (src/MiniCV/Camera.fs:7-14), field order kept."""
+    _fields_ = [("location", V3d), ("forward", V3d), ("up", V3d), ("right", V3d), ("focal", V2d)]
+
+
 class RecoverPoseConfig(C.Structure):
     """MiniCVNative.cpp:39-46 / OpenCV.fs:16-36."""
     _fields_ = [("FocalLength", C.c_double), ("PrincipalPoint", V2d), ("Probability", C.c_double),
@@ -106,6 +111,8 @@ SIGNATURES = {
     "cvMatchAndFindModel": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "cvMatchHamming": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
     "cvMatchL2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
+    "cvFindScaledPose": (_I, [_D, _P, _P, _P, _I, _P, _P, _P, _P]),
+    "cvFindScaledPoseCosts": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "mcvGetLastError": (C.c_char_p, []),
     "mcvDeviceCount": (_I, []),
     "mcvVersion": (C.c_char_p, []),
@@ -123,6 +130,7 @@ SIGNATURES = {
     "mcvReplayChunkModels": (_I, [_P, _P, _I64, _I64, _I, _I, _I, _D, _I]),
     "mcvMatchHammingDevice": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
     "mcvMatchL2Device": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "mcvFindScaledPoseDevice": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P]),
     "mcvProfileEnable": (None, [_I]),
     "mcvProfileReset": (None, []),
     "mcvProfileRead": (_I, [C.c_char_p, _P]),
@@ -137,6 +145,7 @@ SIGNATURES = {
     "mcvHostRodriguesInv": (None, [_P, _P]),
     "mcvTestRcpExhaustive": (C.c_longlong, [_I, _P]),
     "mcvTestHomographySweep": (_I, [_P, _I, _P, _I, _F, _I, _P]),
+    "mcvHostScaledCosts": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
 }
 
 _lib = None

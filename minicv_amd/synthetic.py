@@ -184,3 +184,32 @@ def feature_pair_problem(na: int, nb: int, seed: int = 9, kind: str = "hamming",
     ok = planted >= 0
     pb[planted[ok]] = project(H, pa[ok]) + rng.normal(0, sigma, size=(int(ok.sum()), 2))
     return pa, da, pb, db, planted
+
+
+def scaled_problem(n: int, seed: int = 10, outlier_frac: float = 0.3, sigma: float = 1e-3, true_scale: float = 2.5,
+                   focal=(1.0, 1.0)):
+    """CameraPose.findScaled inputs: a lookAt source camera (Camera.fs:93-104), a
+    relative pose (rotation, unit translation) and world points seen by the destination camera
+    transformedView (transformation (scale true_scale pose)) srcCam; observations = project1 of
+    that camera (Camera.fs:72-83) + N(0, sigma), a fraction replaced by uniform [-1, 1]^2 outliers.
+    -> (srcCam, pose, world[n,3], obs[n,2], is_inlier)"""
+    from . import camera as CM
+    rng = np.random.default_rng(seed)
+    src = CM.lookAt([0.0, -10.0, 1.0], [0.0, 0.0, 0.0], [0.0, 0.0, 1.0], focal)
+    R = rotation([0.2, 0.3, 1.0], np.deg2rad(12.0))
+    t = np.array([0.6, 0.1, -0.2])
+    t = t / np.linalg.norm(t)
+    pose = CM.CameraPose(1, 1, R, t, False)
+    dst = CM.transformed_view(CM.transformation(CM.scale(true_scale, pose)), src)
+    world = np.empty((0, 3))
+    while world.shape[0] < n:
+        w = rng.uniform(-3, 3, size=(4 * n, 3))
+        _, v1 = CM.project1(dst, w)
+        _, v0 = CM.project1(src, w)
+        world = np.concatenate([world, w[v1 & v0]])
+    world = world[:n]
+    obs, _ = CM.project1(dst, world)
+    obs = obs + rng.normal(0, sigma, size=obs.shape)
+    out = rng.random(n) < outlier_frac
+    obs[out] = rng.uniform(-1, 1, size=(int(out.sum()), 2))
+    return src, pose, world, obs, ~out

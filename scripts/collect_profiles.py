@@ -19,7 +19,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "gpurun_out"
 PROF = ROOT / "profiles"
-WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2"]
+WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2", "scaled"]
 # dominant kernel per BASELINE workload (substring of the demangled rocprofv3 kernel name)
 KERNELS = {"homography": "mcv_h_verify_pk", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
            "l2": "mcv_l2_mfma"}

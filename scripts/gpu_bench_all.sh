@@ -17,3 +17,4 @@ step bench_hamming 300 python bench.py --workload hamming --steps 20 --warmup 3
 step bench_l2 300 python bench.py --workload l2 --steps 5 --warmup 2
 step bench_essential 300 python bench.py --workload essential --steps 5 --warmup 2 --cpu-seconds 8
 step bench_pnp 300 python bench.py --workload pnp --steps 5 --warmup 2 --cpu-seconds 8
+step bench_scaled 300 python bench.py --workload scaled --steps 5 --warmup 2 --cpu-seconds 8

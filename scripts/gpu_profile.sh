@@ -11,7 +11,7 @@ run() {   # name timeout args...
     echo "$name rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 "$R/gpurun_out/$name.log"; exit $rc; fi
 }
-for w in homography fundamental essential pnp hamming l2; do
+for w in homography fundamental essential pnp hamming l2 scaled; do
     run prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$w" -o run -- \
         python3 "$R/bench.py" --workload $w --steps 5 --warmup 2 --no-cpu-baseline
 done

@@ -46,6 +46,9 @@ _SIGS = {
     "orc_solve_pnp_ransac": (_I, [_P, _P, _I, _P, _P, _D, _D, _I, _U64, _I, _P, _P, _P, _P, _I]),
     "orc_rodrigues": (None, [_P, _P, _P]),
     "orc_rodrigues_inv": (None, [_P, _P]),
+    "orc_scaled_costs": (None, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I]),
+    "orc_find_scaled": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I]),
+    "orc_scaled_costs_sample": (None, [_P, _P, _P, _I, _P, _P, _I, _P, _P, _P, _I]),
 }
 
 _lib = None
@@ -54,7 +57,7 @@ _lib = None
 def load() -> C.CDLL:
     global _lib
     if _lib is None:
-        srcs = [ORACLE_DIR / n for n in ("oracle.c", "oracle_e.c", "oracle_pnp.c", "oracle_int.h")]
+        srcs = [ORACLE_DIR / n for n in ("oracle.c", "oracle_e.c", "oracle_pnp.c", "oracle_scaled.c", "oracle_int.h")]
         if not ORACLE_SO.exists() or ORACLE_SO.stat().st_mtime < max(p.stat().st_mtime for p in srcs):
             subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
         L = C.CDLL(str(ORACLE_SO))
@@ -332,3 +335,46 @@ def rodrigues_inv(R):
     r = np.zeros(3)
     load().orc_rodrigues_inv(ptr(R), ptr(r))
     return r
+
+
+def _scaled_args(cam14, world, obs, R, t):
+    cam = np.ascontiguousarray(cam14, np.float64).reshape(14)
+    W = np.ascontiguousarray(world, np.float64).reshape(-1, 3)
+    O = np.ascontiguousarray(obs, np.float64).reshape(-1, 2)
+    R9 = np.ascontiguousarray(R, np.float64).reshape(9)
+    T3 = np.ascontiguousarray(t, np.float64).reshape(3)
+    return cam, W, O, R9, T3
+
+
+def scaled_costs(cam14, world, obs, R, t, nthreads=0):
+    """CameraPose.findScaled candidates: (scales[2N], costs[2N], used[N])."""
+    cam, W, O, R9, T3 = _scaled_args(cam14, world, obs, R, t)
+    n = W.shape[0]
+    sc = np.empty(2 * n)
+    co = np.empty(2 * n)
+    used = np.zeros(n, np.uint8)
+    load().orc_scaled_costs(ptr(cam), ptr(W), ptr(O), n, ptr(R9), ptr(T3), ptr(sc), ptr(co), ptr(used), nthreads)
+    return sc, co, used
+
+
+def find_scaled(cam14, world, obs, R, t, nthreads=0):
+    """CameraPose.findScaled: (cost, scale, evaluated candidates)."""
+    cam, W, O, R9, T3 = _scaled_args(cam14, world, obs, R, t)
+    n = W.shape[0]
+    sc = np.empty(max(2 * n, 1))
+    co = np.empty(max(2 * n, 1))
+    used = np.zeros(max(n, 1), np.uint8)
+    cost, scale = C.c_double(0), C.c_double(0)
+    k = load().orc_find_scaled(ptr(cam), ptr(W), ptr(O), n, ptr(R9), ptr(T3), ptr(sc), ptr(co), ptr(used),
+                               C.addressof(cost), C.addressof(scale), nthreads)
+    return cost.value, scale.value, k
+
+
+def scaled_costs_sample(cam14, world, obs, R, t, n_cand, nthreads=0):
+    """Costs of the first n_cand candidates (CPU baseline sample)."""
+    cam, W, O, R9, T3 = _scaled_args(cam14, world, obs, R, t)
+    n = W.shape[0]
+    sc, co, used = np.empty(2 * n), np.empty(2 * n), np.zeros(n, np.uint8)
+    load().orc_scaled_costs_sample(ptr(cam), ptr(W), ptr(O), n, ptr(R9), ptr(T3), n_cand, ptr(sc), ptr(co),
+                                   ptr(used), nthreads)
+    return co[:n_cand]
