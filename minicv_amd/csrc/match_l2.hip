@@ -4,8 +4,8 @@
 //
 //   |q - t|^2 = |q|^2 + |t|^2 - 2 q.t ; argmin over t needs only s(t) = |t|^2 - 2 q.t.
 //
-// mcv_l2_mfma<DP>: v_mfma_f32_32x32x2_f32 (exact f32 FMA chain, 64 FLOP/clk/SIMD = the fp32 peak).
-//   A = 32 train rows of a tile (from LDS), B = 32 queries (resident in VGPRs for the whole
+// mcv_l2_mfma<DP, TR>: v_mfma_f32_32x32x2_f32 (exact f32 FMA chain, 64 FLOP/clk/SIMD = the fp32
+//   peak). A = TR train rows of a tile (from LDS), B = 32 queries (resident in VGPRs for the whole
 //   kernel), D[i][j] = t_i . q_j. The 32x32 accumulator puts one query on each lane (col = lane & 31)
 //   and 16 train rows in its registers, so the top-2 epilogue is lane-local: no cross-lane
 //   reduction per tile, one shuffle at the end to merge the two lane halves.
@@ -13,13 +13,16 @@
 //   2s + h, so 4 consecutive k-steps are one 16-byte read (ds_read_b128 / global_load_dwordx4).
 //   Train tiles are double-buffered in LDS (row stride DP + 4 floats: conflict-free b128 reads),
 //   register-staged: the next tile's global loads are issued before this tile's MFMAs and written
-//   to LDS after them; one barrier per tile.
+//   to LDS after them; one barrier per tile. The epilogue takes the tile's norms as 4 b128 reads
+//   and inserts each score with 2 v_cmp + 6 v_cndmask (no divergent branch per score: the branchy
+//   form the compiler chose cost 7 % of the kernel, 5.80 -> 5.38 ms at cfg5).
 //   Grid = (query blocks of 128) x (train chunks); a merge kernel folds the per-chunk top-2s.
 // Ties: scores compared as (score, train index) pairs — lowest index wins, like BFMatcher's scan.
 #include "kernels.h"
 #include "mcv_runtime.h"
 #include "plan.h"
 #include <cmath>
+#include <cstdlib>
 
 namespace mcv {
 
@@ -41,6 +44,27 @@ __device__ __forceinline__ void top2_push(float& b1, int& i1, float& b2, int& i2
     i1 = c1 ? i : i1;
     b2 = nb2;
     i2 = ni2;
+}
+
+// Epilogue form of the same insertion for one lane's scores in ascending train-index order: a later
+// index never wins a tie, so strict < decides; NaN scores (padding rows) never enter. Written as
+// 2 v_cmp + 6 v_cndmask on VCC: the compiler turns the equivalent selects into a divergent branch
+// per score (s_and_saveexec / s_cbranch_execz), which serialised the MFMA tile loop.
+__device__ __forceinline__ void top2_push_asc(float& b1, int& i1, float& b2, int& i2, float s, int i) {
+    float tb;
+    int ti;
+    asm volatile(
+        "v_cmp_lt_f32_e32 vcc, %[s], %[b2]\n\t"
+        "v_cndmask_b32_e32 %[tb], %[b2], %[s], vcc\n\t"
+        "v_cndmask_b32_e32 %[ti], %[i2], %[i], vcc\n\t"
+        "v_cmp_lt_f32_e32 vcc, %[s], %[b1]\n\t"
+        "v_cndmask_b32_e32 %[b2], %[tb], %[b1], vcc\n\t"
+        "v_cndmask_b32_e32 %[i2], %[ti], %[i1], vcc\n\t"
+        "v_cndmask_b32_e32 %[b1], %[b1], %[s], vcc\n\t"
+        "v_cndmask_b32_e32 %[i1], %[i1], %[i], vcc"
+        : [b1] "+v"(b1), [i1] "+v"(i1), [b2] "+v"(b2), [i2] "+v"(i2), [tb] "=&v"(tb), [ti] "=&v"(ti)
+        : [s] "v"(s), [i] "v"(i)
+        : "vcc");
 }
 
 // Parity-split, zero-padded copy [nPad][DP] + squared norms (fp32 FMA chain in dim order).
@@ -65,38 +89,43 @@ __global__ void mcv_l2_prep(const float* __restrict__ src, int n, int dim, int D
     }
 }
 
-template <int DP>
+// Stage TR train rows x DP floats (TR * DP / 1024 float4 per thread) + their norms.
+template <int DP, int TR>
 __device__ __forceinline__ void l2_gload(const float* __restrict__ tp, const float* __restrict__ tnorm, int tile,
-                                         float4 (&stg)[DP / 32], float& nstg) {
+                                         float4 (&stg)[TR * DP / 1024], float& nstg) {
     constexpr int ROWS_PER_PASS = 256 / (DP / 4);
     const int srow = threadIdx.x / (DP / 4), sc4 = threadIdx.x % (DP / 4);
 #pragma unroll
-    for (int r = 0; r < DP / 32; ++r)
-        stg[r] = reinterpret_cast<const float4*>(tp + (size_t)(tile * 32 + srow + r * ROWS_PER_PASS) * DP)[sc4];
-    if (threadIdx.x < 32) nstg = tnorm[tile * 32 + threadIdx.x];
+    for (int r = 0; r < TR * DP / 1024; ++r)
+        stg[r] = reinterpret_cast<const float4*>(tp + (size_t)(tile * TR + srow + r * ROWS_PER_PASS) * DP)[sc4];
+    if (threadIdx.x < TR) nstg = tnorm[tile * TR + threadIdx.x];
 }
 
-template <int DP>
+template <int DP, int TR>
 __device__ __forceinline__ void l2_lstore(float* __restrict__ lds, float* __restrict__ lnorm,
-                                          const float4 (&stg)[DP / 32], float nstg) {
+                                          const float4 (&stg)[TR * DP / 1024], float nstg) {
     constexpr int ROWF = DP + 4;
     constexpr int ROWS_PER_PASS = 256 / (DP / 4);
     const int srow = threadIdx.x / (DP / 4), sc4 = threadIdx.x % (DP / 4);
 #pragma unroll
-    for (int r = 0; r < DP / 32; ++r)
+    for (int r = 0; r < TR * DP / 1024; ++r)
         *reinterpret_cast<float4*>(&lds[(srow + r * ROWS_PER_PASS) * ROWF + sc4 * 4]) = stg[r];
-    if (threadIdx.x < 32) lnorm[threadIdx.x] = nstg;
+    if (threadIdx.x < TR) lnorm[threadIdx.x] = nstg;
 }
 
-template <int DP>
+// TR train rows per tile = TR / 32 independent 32x32 accumulator chains per wave, interleaved
+// k-step by k-step (they share the query operands b[]): the matrix pipe never waits on one
+// chain's dependent-accumulator latency.
+template <int DP, int TR>
 __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ qp, const float* __restrict__ tp,
                                                      const float* __restrict__ tnorm, int ntTiles,
                                                      int tilesPerChunk, int nqPad, L2Part* __restrict__ part) {
     constexpr int KS = DP / 2;          // MFMA k-steps (2 dims each)
     constexpr int ROWF = DP + 4;        // padded LDS row, floats
-    constexpr int PER = DP / 32;        // float4 staging loads per thread per tile (32 rows x DP)
-    __shared__ __attribute__((aligned(16))) float lds[2][32 * ROWF];
-    __shared__ float lnorm[2][32];
+    constexpr int PER = TR * DP / 1024; // float4 staging loads per thread per tile (TR rows x DP)
+    constexpr int NC = TR / 32;         // accumulator chains
+    __shared__ __attribute__((aligned(16))) float lds[2][TR * ROWF];
+    __shared__ __attribute__((aligned(16))) float lnorm[2][TR];
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
@@ -118,13 +147,13 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
     float b1 = INFINITY, b2 = INFINITY;
     int i1 = -1, i2 = -1;
 
-    // Register staging of the next train tile (32 rows x DP floats = PER float4 per thread).
+    // Register staging of the next train tile.
     float4 stg[PER];
     float nstg = 0.f;
 
     if (tBegin < tEnd) {
-        l2_gload<DP>(tp, tnorm, tBegin, stg, nstg);
-        l2_lstore<DP>(lds[0], lnorm[0], stg, nstg);
+        l2_gload<DP, TR>(tp, tnorm, tBegin, stg, nstg);
+        l2_lstore<DP, TR>(lds[0], lnorm[0], stg, nstg);
     }
     __syncthreads();
     for (int t = tBegin; t < tEnd; ++t) {
@@ -132,27 +161,47 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
         const bool more = t + 1 < tEnd;
         // next tile's loads in flight under this tile's MFMAs (the last trip reloads its own tile
         // into the idle buffer: no branch around the staging registers)
-        l2_gload<DP>(tp, tnorm, more ? t + 1 : t, stg, nstg);
-        floatx16 acc;
+        l2_gload<DP, TR>(tp, tnorm, more ? t + 1 : t, stg, nstg);
+        // the tile's norms for this lane's rows (8j + 4h .. 8j + 4h + 3 of each chain: 4 b128 reads),
+        // fetched ahead of the MFMA chain so the epilogue never waits on LDS
+        float4 nv[NC][4];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        const float* arow = &lds[buf][col * ROWF + h * KS];
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) nv[c][j] = *reinterpret_cast<const float4*>(&lnorm[buf][32 * c + 8 * j + 4 * h]);
+        floatx16 acc[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
 #pragma unroll
         for (int s4 = 0; s4 < KS / 4; ++s4) {
-            const float4 a = *reinterpret_cast<const float4*>(arow + 4 * s4);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[4 * s4 + 0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[4 * s4 + 1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[4 * s4 + 2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[4 * s4 + 3], acc, 0, 0, 0);
-        }
-        // epilogue: lane = query col, register r = train row (r&3) + 8(r>>2) + 4h, rows ascending
+            float4 a[NC];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float s = fmaf(-2.f, acc[r], lnorm[buf][row]);
-            top2_push(b1, i1, b2, i2, s, t * 32 + row);
+            for (int c = 0; c < NC; ++c)
+                a[c] = *reinterpret_cast<const float4*>(&lds[buf][(32 * c + col) * ROWF + h * KS + 4 * s4]);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c].x, b[4 * s4 + 0], acc[c], 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c].y, b[4 * s4 + 1], acc[c], 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c].z, b[4 * s4 + 2], acc[c], 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c].w, b[4 * s4 + 3], acc[c], 0, 0, 0);
         }
-        l2_lstore<DP>(lds[buf ^ 1], lnorm[buf ^ 1], stg, nstg);
+        // epilogue: lane = query col, register r of chain c = train row 32c + (r&3) + 8(r>>2) + 4h;
+        // chains in order, rows ascending within a chain: ascending train index per lane
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = 32 * c + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float4 n4 = nv[c][r >> 2];
+                const float nrm = (r & 3) == 0 ? n4.x : (r & 3) == 1 ? n4.y : (r & 3) == 2 ? n4.z : n4.w;
+                const float s = fmaf(-2.f, acc[c][r], nrm);
+                top2_push_asc(b1, i1, b2, i2, s, t * TR + row);
+            }
+        l2_lstore<DP, TR>(lds[buf ^ 1], lnorm[buf ^ 1], stg, nstg);
         __syncthreads();
     }
     // merge the two lane halves that hold the same query
@@ -198,8 +247,13 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     thread_local L2Work wk;
     const int DP = dim <= 32 ? 32 : dim <= 64 ? 64 : dim <= 128 ? 128 : 256;
     const int nqPad = (nq + 127) / 128 * 128;
-    const int ntPad = nt > 0 ? (nt + 31) / 32 * 32 : 32;
-    const int ntTiles = ntPad / 32;
+    static const int TRsel = [] {   // train rows per tile (variant screen: 32 or 64)
+        const char* e = getenv("MCV_L2_TR");
+        return e && atoi(e) == 64 ? 64 : 32;   // screened equal (scripts/sweep_l2.sh): keep one chain
+    }();
+    const int TR = DP <= 128 ? TRsel : 32;
+    const int ntPad = nt > 0 ? (nt + TR - 1) / TR * TR : TR;
+    const int ntTiles = ntPad / TR;
     wk.qp.ensure((size_t)nqPad * DP);
     wk.tp.ensure((size_t)ntPad * DP);
     wk.qn.ensure(nqPad);
@@ -219,12 +273,15 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     dim3 grid(qblocks, nchunks);
     {
         ProfScope ps("l2_mfma", s);
+#define MCV_L2_LAUNCH(D, T) hipLaunchKernelGGL((mcv_l2_mfma<D, T>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, \
+                                               ntTiles, tilesPerChunk, nqPad, wk.part.p)
         switch (DP) {
-            case 32: hipLaunchKernelGGL((mcv_l2_mfma<32>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p); break;
-            case 64: hipLaunchKernelGGL((mcv_l2_mfma<64>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p); break;
-            case 128: hipLaunchKernelGGL((mcv_l2_mfma<128>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p); break;
-            default: hipLaunchKernelGGL((mcv_l2_mfma<256>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p); break;
+            case 32: if (TR == 64) MCV_L2_LAUNCH(32, 64); else MCV_L2_LAUNCH(32, 32); break;
+            case 64: if (TR == 64) MCV_L2_LAUNCH(64, 64); else MCV_L2_LAUNCH(64, 32); break;
+            case 128: if (TR == 64) MCV_L2_LAUNCH(128, 64); else MCV_L2_LAUNCH(128, 32); break;
+            default: MCV_L2_LAUNCH(256, 32); break;
         }
+#undef MCV_L2_LAUNCH
     }
     hipLaunchKernelGGL(mcv_l2_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nqPad, nchunks, wk.qn.p,
                        d_idx, d_dist, d_idx2, d_dist2);
