@@ -347,27 +347,47 @@ MCV_HD float f_error(int kind, const double* F, double x1, double y1, double x2,
 
 #if defined(__HIPCC__)
 // One sweep step for K models at one correspondence per lane: inlier ballots into cnt[k].
-// KIND 0/1 (Sampson) use the certified division-free test with an exact fallback for undecided
-// lanes (wave-uniform branch, rare); KIND 2/3 (epipolar) evaluate f_error directly.
+// KIND 0/1 (Sampson) use the certified division-free test: per model two lane masks (certified
+// inliers, undecided lanes) straight from the fp64 compares, and ONE wave-uniform branch for the
+// whole step into the exact division of the undecided lanes (rare). Keeping the fallback out of
+// the per-model path leaves the common case as compares + scalar mask logic, with no exec-mask
+// round trips through VGPRs. KIND 2/3 (epipolar) evaluate f_error directly.
 template <int K, int KIND>
 __device__ __forceinline__ void f_sweep_point(const double (&fm)[K][9], double x1, double y1, double x2, double y2,
                                               bool v, float thr2, double lo, double hi, uint32_t (&cnt)[K]) {
+    if constexpr (KIND <= 1) {
+        // each compare straight into a lane mask (v_cmp -> SGPR pair), combined by scalar ops
+        const uint64_t vm = __builtin_amdgcn_ballot_w64(v);
+        uint64_t inm[K], amb[K], anyAmb = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        if constexpr (KIND <= 1) {
+        for (int k = 0; k < K; ++k) {
             double c2, den;
             if constexpr (KIND == 0) f_sampson_parts_fused(fm[k], x1, y1, x2, y2, c2, den);
             else f_sampson_parts(fm[k], x1, y1, x2, y2, c2, den);
-            const bool ok = den >= kSampsonDenMin;
-            const bool in = ok && c2 < den * lo;
-            const bool out = ok && c2 > den * hi;
-            const bool amb = v && !(in || out);
-            bool res = v && in;
-            if (__builtin_amdgcn_ballot_w64(amb)) res = res || (amb && (float)(c2 / den) <= thr2);
-            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(res));
-        } else {
-            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(v && f_error(KIND, fm[k], x1, y1, x2, y2) <= thr2));
+            const uint64_t ok = __builtin_amdgcn_ballot_w64(den >= kSampsonDenMin);
+            const uint64_t in = ok & __builtin_amdgcn_ballot_w64(c2 < den * lo);
+            const uint64_t out = ok & __builtin_amdgcn_ballot_w64(c2 > den * hi);
+            inm[k] = vm & in;
+            amb[k] = vm & ~(in | out);
+            anyAmb |= amb[k];
         }
+        if (__builtin_expect(anyAmb != 0, 0)) {
+            const uint64_t me = 1ull << (__lane_id() & 63);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (amb[k] == 0) continue;
+                double c2, den;
+                if constexpr (KIND == 0) f_sampson_parts_fused(fm[k], x1, y1, x2, y2, c2, den);
+                else f_sampson_parts(fm[k], x1, y1, x2, y2, c2, den);
+                inm[k] |= __builtin_amdgcn_ballot_w64((amb[k] & me) != 0 && (float)(c2 / den) <= thr2);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) cnt[k] += (uint32_t)__popcll(inm[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(v && f_error(KIND, fm[k], x1, y1, x2, y2) <= thr2));
     }
 }
 #endif

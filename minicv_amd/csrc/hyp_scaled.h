@@ -42,7 +42,8 @@ MCV_HD void scaled_location(const ScaledSetup& S, double s, double (&loc)[3]) {
 }
 
 // One observation against dstCam(s): Camera.project1 (Camera.fs:72-83) and the squared distance
-// to the observation (CameraPose.fs:80-82). Returns false when the point is not visible.
+// to the observation (CameraPose.fs:80-82). Returns false when the point is not visible; err is
+// computed either way (no branch: the caller selects it), meaningful only when visible.
 MCV_HD bool scaled_term(const ScaledSetup& S, const double (&loc)[3], double wx, double wy, double wz, double ox,
                         double oy, double& err) {
     const double o0 = wx - loc[0], o1 = wy - loc[1], o2 = wz - loc[2];
@@ -50,10 +51,9 @@ MCV_HD bool scaled_term(const ScaledSetup& S, const double (&loc)[3], double wx,
     const double p1 = o0 * S.up[0] + o1 * S.up[1] + o2 * S.up[2];
     const double p2 = o0 * S.fwd[0] + o1 * S.fwd[1] + o2 * S.fwd[2];
     const double cx = S.fx * p0 / p2, cy = S.fy * p1 / p2;
-    if (!(p2 >= 0.0 && cx >= -1.0 && cy >= -1.0 && cx <= 1.0 && cy <= 1.0)) return false;
     const double dx = cx - ox, dy = cy - oy;
     err = dx * dx + dy * dy;
-    return true;
+    return p2 >= 0.0 && cx >= -1.0 && cy >= -1.0 && cx <= 1.0 && cy <= 1.0;
 }
 
 // Candidate scales of observation (w, obs) (CameraPose.fs:103-117). Returns false when the

@@ -67,6 +67,11 @@ __global__ __launch_bounds__(256) void mcv_pnp_verify(const PnpPoint* __restrict
         for (int j = 0; j < 9; ++j) R[k][j] = valid[k] ? m.R[j] : (j % 4 == 0 ? 1.0 : 0.0);
 #pragma unroll
         for (int j = 0; j < 3; ++j) t[k][j] = valid[k] ? m.t[j] : 1e30;
+        // poses in VGPRs: 4 x 12 doubles in SGPRs spill into VGPR lanes (v_readlane per use)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) asm volatile("" : "+v"(R[k][j]));
+#pragma unroll
+        for (int j = 0; j < 3; ++j) asm volatile("" : "+v"(t[k][j]));
     }
     const int p0 = blockIdx.y * chunk;
     const int p1 = min(N, p0 + chunk);
@@ -77,10 +82,14 @@ __global__ __launch_bounds__(256) void mcv_pnp_verify(const PnpPoint* __restrict
         const int p = base + lane;
         const bool v = p < p1;
         const PnpPoint q = pts[v ? p : p0];
+        // every lane evaluates (the padding lanes re-read point p0): `v && err <= thr2` would
+        // short-circuit into a divergent branch around the whole projection
+        const uint64_t vm = __builtin_amdgcn_ballot_w64(v);
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            cnt[k] += (uint32_t)__popcll(
-                __builtin_amdgcn_ballot_w64(v && pnp_error(cam, R[k], t[k], q.X, q.Y, q.Z, q.u, q.v, FUSED) <= thr2));
+        for (int k = 0; k < K; ++k) {
+            const float e = pnp_error(cam, R[k], t[k], q.X, q.Y, q.Z, q.u, q.v, FUSED);
+            cnt[k] += (uint32_t)__popcll(vm & __builtin_amdgcn_ballot_w64(e <= thr2));
+        }
     }
     if (lane == 0) {
 #pragma unroll

@@ -92,10 +92,9 @@ __global__ __launch_bounds__(256) void mcv_scaled_costs(ScaledSetup S, const dou
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             double e;
-            if (scaled_term(S, loc[k], x, y, z, u, v, e)) {
-                sum[k] += e;
-                cnt[k] += 1;
-            }
+            const bool vis = scaled_term(S, loc[k], x, y, z, u, v, e);
+            sum[k] += vis ? e : 0.0;   // select, not a branch (an invisible e may be NaN / inf)
+            cnt[k] += vis ? 1 : 0;
         }
     }
 #pragma unroll
