@@ -7,13 +7,14 @@
 //   * lane = query: each lane keeps its query's W words in VGPRs;
 //   * wave-uniform train index: the train descriptor arrives by scalar loads (SGPRs), so each
 //     XOR reads it as its scalar operand — no LDS traffic at all;
-//   * train descriptors are staged in two ping-pong SGPR groups of 32 dwords by hand-issued
-//     s_load_dwordx16 bursts, so the scalar-load latency hides behind a group of VALU work;
-//   * the train set is split into S chunks over the grid (~8k waves: variant screen in
-//     scripts/sweep_hamming.sh), each
+//   * train descriptors are staged in two ping-pong SGPR groups of 16 dwords (NB = 1, default) or
+//     32 (NB = 2) by hand-issued s_load_dwordx16 bursts, so the scalar-load latency hides behind a
+//     group of VALU work;
+//   * the train set is split into S chunks over the grid (~16k waves; NB, waves and queries per
+//     lane screened in scripts/sweep_hamming.sh); a block = one query-wave x 4 consecutive chunks, each
 //     (query-wave, chunk) keeps a top-2 of packed keys key = dist << 22 | trainIdx, so
 //     min(key) is "smallest distance, then lowest train index" (BFMatcher's first-minimum rule);
-//   * a merge kernel folds the S partial top-2s per query.
+//   * the block merges its 4 waves' top-2s in LDS; a merge kernel folds the S/4 partials per query.
 // Issue cost per (query, train) pair on gfx950, measured (scripts/exp/valu_rate.hip): the VOP2
 // v_xor_b32 / v_min_u32 take 2 cycles per wave64 instruction, the VOP3-only v_bcnt_u32_b32 /
 // v_med3_u32 / v_lshl_or_b32 take 4 — 8 x (2 + 4) + 4 + 4 + 2 = 58 SIMD cycles per 64 pairs.
@@ -55,11 +56,21 @@ __device__ __forceinline__ u32x16 sload16(const uint32_t* p, u32x16& live0, u32x
     asm volatile("s_load_dwordx16 %0, %3, 0x0" : "=&s"(r), "+s"(live0), "+s"(live1) : "s"(p));
     return r;
 }
+__device__ __forceinline__ u32x16 sload16(const uint32_t* p, u32x16& live0) {
+    u32x16 r;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0" : "=&s"(r), "+s"(live0) : "s"(p));
+    return r;
+}
 // Scalar loads return out of order: only lgkmcnt(0) is a valid wait. The buffers are tied to the
 // wait (no use above it) and so is the running top-2 (the previous group's VALU work stays above).
 template <int Q>
 __device__ __forceinline__ void sgpr_wait(u32x16& a, u32x16& b, uint32_t (&m1)[Q], uint32_t (&m2)[Q]) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a), "+s"(b), "+v"(m1[0]), "+v"(m2[0]));
+    if (Q > 1) asm volatile("; keep %0 %1" : "+v"(m1[Q - 1]), "+v"(m2[Q - 1]));
+}
+template <int Q>
+__device__ __forceinline__ void sgpr_wait(u32x16& a, uint32_t (&m1)[Q], uint32_t (&m2)[Q]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a), "+v"(m1[0]), "+v"(m2[0]));
     if (Q > 1) asm volatile("; keep %0 %1" : "+v"(m1[Q - 1]), "+v"(m2[Q - 1]));
 }
 
@@ -72,20 +83,24 @@ __device__ __forceinline__ uint32_t hamming_key_v(const uint32_t* qv, const u32x
 }
 
 // Lane = Q queries (their W words each in VGPRs); a wave covers 64 Q consecutive queries.
-// A group = 32 dwords (4 x 256-bit or 2 x 512-bit descriptors) in two SGPR vectors. Two groups
-// ping-pong: wait(A) -> issue B -> consume A -> wait(B) -> issue A' -> consume B, so each burst's
-// latency (K$ miss -> L2) hides behind a whole group of VALU work.
-template <int W, int Q>
+// A group = 16 NB dwords (NB = 2: 4 x 256-bit or 2 x 512-bit descriptors; NB = 1: half that) in NB
+// SGPR vectors. Two groups ping-pong: wait(A) -> issue B -> consume A -> wait(B) -> issue A' ->
+// consume B, so each burst's latency (K$ miss -> L2) hides behind a whole group of VALU work.
+// NB = 1 halves the SGPRs the buffers take (occupancy: 8 waves per SIMD instead of 7).
+template <int W, int Q, int NB>
 __global__ __launch_bounds__(256) void mcv_hamming_partial(const uint32_t* __restrict__ q, int nq,
                                                            const uint32_t* __restrict__ t, int nt, int chunkLen,
                                                            uint2* __restrict__ part) {
-    constexpr int G = 32 / W;  // descriptors per group
+    constexpr int G = 16 * NB / W;  // descriptors per group
     const int lane = threadIdx.x & 63;
-    const int qwave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    const int chunk = blockIdx.y;
-    const int tBegin = chunk * chunkLen;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    // block = one query-wave x 4 consecutive train chunks (one per wave), merged in LDS at the end:
+    // a quarter of the partial top-2s for the merge kernel to read
+    const int qwave = blockIdx.x;
+    const int chunk = blockIdx.y * 4 + wv;
+    const int tBegin = min(chunk * chunkLen, nt);
     const int tEnd = min(tBegin + chunkLen, nt);
-    if (qwave * 64 * Q >= nq) return;
+    if (qwave * 64 * Q >= nq) return;   // block-uniform
 
     uint32_t qv[Q][W];
 #pragma unroll
@@ -113,7 +128,7 @@ __global__ __launch_bounds__(256) void mcv_hamming_partial(const uint32_t* __res
             }
         }
     };
-    if (nGroups > 0) {
+    if (nGroups > 0 && NB == 2) {
         const uint32_t* tp = t + (size_t)j * W;
         u32x16 a0 = {}, a1 = {}, b0 = {}, b1 = {};
         a0 = sload16(tp, b0, b1);
@@ -136,6 +151,24 @@ __global__ __launch_bounds__(256) void mcv_hamming_partial(const uint32_t* __res
             consume(a0, a1, j);
             j += G;
         }
+    } else if (nGroups > 0) {   // NB == 1: one 16-dword vector per group
+        const uint32_t* tp = t + (size_t)j * W;
+        u32x16 a0 = {}, b0 = {};
+        a0 = sload16(tp, b0);
+        int g = 0;
+        for (; g + 1 < nGroups; g += 2, j += 2 * G) {
+            sgpr_wait<Q>(a0, m1, m2);
+            b0 = sload16(t + (size_t)(j + G) * W, a0);
+            consume(a0, a0, j);
+            sgpr_wait<Q>(b0, m1, m2);
+            a0 = sload16(t + (size_t)(g + 2 < nGroups ? j + 2 * G : j) * W, b0);
+            consume(b0, b0, j + G);
+        }
+        sgpr_wait<Q>(a0, m1, m2);
+        if (g < nGroups) {
+            consume(a0, a0, j);
+            j += G;
+        }
     }
     for (; j < tEnd; ++j) {
         const uint32_t* td = t + (size_t)j * W;
@@ -147,10 +180,21 @@ __global__ __launch_bounds__(256) void mcv_hamming_partial(const uint32_t* __res
             top2_push(m1[r], m2[r], (d << kIdxBits) | (uint32_t)j);
         }
     }
+    __shared__ uint2 sm[4][64 * Q];
+#pragma unroll
+    for (int r = 0; r < Q; ++r) sm[wv][r * 64 + lane] = make_uint2(m1[r], m2[r]);
+    __syncthreads();
+    if (wv != 0) return;
 #pragma unroll
     for (int r = 0; r < Q; ++r) {
+#pragma unroll
+        for (int o = 1; o < 4; ++o) {
+            const uint2 p = sm[o][r * 64 + lane];
+            top2_push(m1[r], m2[r], p.x);
+            top2_push(m1[r], m2[r], p.y);
+        }
         const int qi = (qwave * Q + r) * 64 + lane;
-        if (qi < nq) part[(size_t)chunk * nq + qi] = make_uint2(m1[r], m2[r]);
+        if (qi < nq) part[(size_t)blockIdx.y * nq + qi] = make_uint2(m1[r], m2[r]);
     }
 }
 
@@ -215,7 +259,7 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     }
     static const int targetWaves = [] {
         const char* e = getenv("MCV_HAMMING_WAVES");  // variant screen (scripts/sweep_hamming.sh)
-        return e ? atoi(e) : 8192;
+        return e ? atoi(e) : 16384;
     }();
     static const int Q = [] {
         const char* e = getenv("MCV_HAMMING_Q");  // queries per lane (1 or 2; 2 screened slower)
@@ -227,18 +271,22 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     if (nchunks > maxChunks) nchunks = maxChunks;
     if (nchunks < 1) nchunks = 1;
     const int chunkLen = nt > 0 ? (nt + nchunks - 1) / nchunks : 0;
-    wk.part.ensure((size_t)nchunks * nq);
-    dim3 grid((qwaves + 3) / 4, nchunks);
+    const int nparts = (nchunks + 3) / 4;
+    wk.part.ensure((size_t)nparts * nq);
+    dim3 grid(qwaves, nparts);
     ProfScope ps("hamming", s);
-    if (W == 8 && Q == 1)
-        hipLaunchKernelGGL((mcv_hamming_partial<8, 1>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
-    else if (W == 8)
-        hipLaunchKernelGGL((mcv_hamming_partial<8, 2>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
-    else if (Q == 1)
-        hipLaunchKernelGGL((mcv_hamming_partial<16, 1>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
-    else
-        hipLaunchKernelGGL((mcv_hamming_partial<16, 2>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p);
-    hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nchunks, d_idx,
+    static const int NB = [] {
+        const char* e = getenv("MCV_HAMMING_NB");  // SGPR vectors per staged group (1 or 2)
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+#define MCV_HAM_LAUNCH(W_, Q_, NB_) \
+    hipLaunchKernelGGL((mcv_hamming_partial<W_, Q_, NB_>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p)
+    if (W == 8 && Q == 1) { if (NB == 2) MCV_HAM_LAUNCH(8, 1, 2); else MCV_HAM_LAUNCH(8, 1, 1); }
+    else if (W == 8) { if (NB == 2) MCV_HAM_LAUNCH(8, 2, 2); else MCV_HAM_LAUNCH(8, 2, 1); }
+    else if (Q == 1) { if (NB == 2) MCV_HAM_LAUNCH(16, 1, 2); else MCV_HAM_LAUNCH(16, 1, 1); }
+    else { if (NB == 2) MCV_HAM_LAUNCH(16, 2, 2); else MCV_HAM_LAUNCH(16, 2, 1); }
+#undef MCV_HAM_LAUNCH
+    hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nparts, d_idx,
                        d_dist, d_idx2, d_dist2);
     MCV_HIP(hipGetLastError());
     return nq;
