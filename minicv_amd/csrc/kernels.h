@@ -60,6 +60,7 @@ void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const doubl
 
 // ---- essential (ransac_e.hip)
 static const int kVerifyEModelsPerWave = 4;
+static const int kVerifyEPtsPerLane = 2;   // correspondences per lane per trip (variant screen)
 static const int kEModelSlots = 10;
 struct EOneOut {
     double E[10][9];

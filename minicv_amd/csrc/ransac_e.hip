@@ -6,7 +6,7 @@
 //                       up to 10 models) -> all 10 slot statuses + models appended to a dense
 //                       list (atomic slot allocation; results are keyed by slot, so the order of
 //                       the dense list never reaches an output).
-//   mcv_e_verify<K, E>  inlier sweep over the dense model list: wave = K models in VGPRs, 64
+//   mcv_e_verify<K,P,E> inlier sweep over the dense model list: wave = K models in VGPRs, 64
 //                       lanes stream the double4 correspondences, fp64 Sampson error cast to
 //                       float, ballot + popcount; the count lands in the model's slot.
 //   mcv_e_one           recompute one hypothesis (winner) -> all its models.
@@ -16,6 +16,7 @@
 #include "mcv_common.h"
 #include "hyp_essential.h"
 #include "kernels.h"
+#include <cstdlib>
 
 namespace mcv {
 
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(64) void mcv_e_generate(const double* __restrict__ 
     }
 }
 
-template <int K, int KIND>
+template <int K, int P, int KIND>
 __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ pts, int N,
                                                     const EModel* __restrict__ dense,
                                                     const int* __restrict__ denseSlot, const int* __restrict__ nDense,
@@ -78,13 +79,18 @@ __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ 
     uint32_t cnt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
-    const int nFull = N & ~63;
-    for (int base = 0; base < nFull; base += 64) {
-        const double4 q = pts[base + lane];
-        f_sweep_point<K, KIND>(em, q.x, q.y, q.z, q.w, true, thr2, lo, hi, cnt);
+    // P correspondences per lane per trip (loads in flight), then a 64-wide predicated tail
+    const int step = 64 * P;
+    const int nFull = N - N % step;
+    for (int base = 0; base < nFull; base += step) {
+        double4 q[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) q[j] = pts[base + 64 * j + lane];
+#pragma unroll
+        for (int j = 0; j < P; ++j) f_sweep_point<K, KIND>(em, q[j].x, q[j].y, q[j].z, q[j].w, true, thr2, lo, hi, cnt);
     }
-    if (nFull < N) {
-        const int p = nFull + lane;
+    for (int base = nFull; base < N; base += 64) {
+        const int p = base + lane;
         const bool v = p < N;
         const double4 q = pts[v ? p : 0];
         f_sweep_point<K, KIND>(em, q.x, q.y, q.z, q.w, v, thr2, lo, hi, cnt);
@@ -174,16 +180,39 @@ void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBe
                        hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
 }
 
+template <int K, int P>
+static void launch_e_verify_kp(const double4* p, int N, const EModel* m, const int* d_denseSlot, const int* d_nDense,
+                               int maxModels, int* d_counts, float thr2, int kind, double lo, double hi,
+                               hipStream_t s) {
+    const int blocks = ((maxModels + K - 1) / K + 3) / 4;
+    if (kind == 0)
+        hipLaunchKernelGGL((mcv_e_verify<K, P, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense,
+                           d_counts, thr2, lo, hi);
+    else
+        hipLaunchKernelGGL((mcv_e_verify<K, P, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense,
+                           d_counts, thr2, lo, hi);
+}
+
+// Sweep shape (models per wave K, correspondences per lane per trip P); MCV_E_VARIANT selects
+// alternatives for the variant screen (scripts/sweep_e_variants.sh) only.
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
                      int maxModels, int* d_counts, float thr2, int kind, hipStream_t s) {
-    constexpr int K = kVerifyEModelsPerWave;
-    const int blocks = ((maxModels + K - 1) / K + 3) / 4;
+    static const int variant = [] {
+        const char* e = getenv("MCV_E_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
     const double4* p = (const double4*)d_pts4;
     const EModel* m = (const EModel*)d_dense;
     const SampsonCut c = sampson_cut(thr2);
-    switch (kind) {
-        case 0: hipLaunchKernelGGL((mcv_e_verify<K, 0>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2, c.lo, c.hi); break;
-        default: hipLaunchKernelGGL((mcv_e_verify<K, 1>), dim3(blocks), dim3(256), 0, s, p, N, m, d_denseSlot, d_nDense, d_counts, thr2, c.lo, c.hi); break;
+    switch (variant) {
+        case 1: launch_e_verify_kp<4, 1>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
+        case 2: launch_e_verify_kp<6, 1>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
+        case 3: launch_e_verify_kp<2, 2>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
+        case 4: launch_e_verify_kp<6, 2>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
+        case 5: launch_e_verify_kp<8, 1>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
+        default:
+            launch_e_verify_kp<kVerifyEModelsPerWave, kVerifyEPtsPerLane>(p, N, m, d_denseSlot, d_nDense, maxModels,
+                                                                          d_counts, thr2, kind, c.lo, c.hi, s);
     }
 }
 

@@ -16,6 +16,7 @@
 #include "hyp_pnp.h"
 #include "reduce.h"
 #include "kernels.h"
+#include <cstdlib>
 
 namespace mcv {
 
@@ -267,9 +268,9 @@ void launch_pnp_generate(const void* d_pts, int N, const double* cam8, uint64_t 
                        to_cam(cam8), seed, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
 }
 
-void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
-                       float thr2, bool fused, hipStream_t s) {
-    constexpr int K = kVerifyPnpPosesPerWave;
+template <int K>
+static void launch_pnp_verify_k(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts,
+                                int hypCount, float thr2, bool fused, hipStream_t s) {
     const int waves = (hypCount + K - 1) / K;
     // split the correspondences so that waves x chunks >= ~8 waves per SIMD, chunks >= 2048 points
     int chunks = (8192 + waves - 1) / waves;
@@ -289,6 +290,21 @@ void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void*
     else
         hipLaunchKernelGGL((mcv_pnp_verify<K, false>), grid, dim3(256), 0, s, p, N, chunk, to_cam(cam8), m, d_counts,
                            hypCount, thr2);
+}
+
+// Poses per wave; MCV_PNP_K selects alternatives for the variant screen only.
+void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
+                       float thr2, bool fused, hipStream_t s) {
+    static const int k = [] {
+        const char* e = getenv("MCV_PNP_K");
+        return e ? atoi(e) : kVerifyPnpPosesPerWave;
+    }();
+    switch (k) {
+        case 2: launch_pnp_verify_k<2>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s); break;
+        case 6: launch_pnp_verify_k<6>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s); break;
+        case 8: launch_pnp_verify_k<8>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s); break;
+        default: launch_pnp_verify_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s);
+    }
 }
 
 void launch_pnp_one(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hyp, PnpOneOut* d_out,
