@@ -10,7 +10,7 @@ from pathlib import Path
 import numpy as np
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-from minicv_amd import opencv, synthetic as S  # noqa: E402
+from minicv_amd import camera as CM, opencv, synthetic as S  # noqa: E402
 
 
 def timed(fn, reps=20, warm=3):
@@ -38,6 +38,8 @@ def main():
         out.append(("cvFindFundamentalMat", n, timed(lambda: opencv.findFundamentalMat(fa, fb))))
         q, t, _ = S.hamming_problem(n, n, seed=5)
         out.append(("cvMatchHamming", n, timed(lambda: opencv.matchHamming(q, t))))
+        cam, pose, W3, O2, _ = S.scaled_problem(n, seed=7)
+        out.append(("cvFindScaledPose", n, timed(lambda: CM.findScaled(0.01, cam, (W3, O2), pose))))
     a, b, *_ = S.essential_problem(5, seed=6, outlier_frac=0)
     out.append(("cvFivePoint", 5, timed(lambda: opencv.fivepoint(a, b))))
     for name, n, ms in out:
