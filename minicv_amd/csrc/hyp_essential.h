@@ -61,7 +61,10 @@ MCV_HD double e_poly_eval(const double* q, int d, double x) {
 // bisection step on the ordered bit patterns whenever the point falls outside the bracket or the
 // bracket failed to halve (in bit-pattern distance) twice in a row. Returns an exact zero if hit,
 // else the lower end of the final 1-ulp bracket.
-MCV_HD double e_root_bracketed(const double* q, int d, double lo, double hi, double flo, double fhi) {
+// Eval is any callable returning q(x) with exactly e_poly_eval's rounding (the wave solver passes
+// a fixed-length Horner over zero-padded coefficients, which rounds identically).
+template <class Eval>
+MCV_HD double e_root_bracketed_f(const Eval& eval, double lo, double hi, double flo, double fhi) {
     int side = 0, stall = 0;
     for (int it = 0; it < 256; ++it) {
         const int64_t klo = e_dkey(lo), khi = e_dkey(hi);
@@ -75,7 +78,7 @@ MCV_HD double e_root_bracketed(const double* q, int d, double lo, double hi, dou
             m = lo - flo * ((hi - lo) / (fhi - flo));
             if (!(m > lo && m < hi)) m = e_dval(kmid);
         }
-        const double fm = e_poly_eval(q, d, m);
+        const double fm = eval(m);
         if (fm == 0) return m;
         const uint64_t w0 = (uint64_t)khi - (uint64_t)klo;
         const int64_t km = e_dkey(m);
@@ -96,6 +99,10 @@ MCV_HD double e_root_bracketed(const double* q, int d, double lo, double hi, dou
         stall = (w1 > w0 / 2) ? stall + 1 : 0;
     }
     return lo;
+}
+
+MCV_HD double e_root_bracketed(const double* q, int d, double lo, double hi, double flo, double fhi) {
+    return e_root_bracketed_f([q, d](double x) { return e_poly_eval(q, d, x); }, lo, hi, flo, fhi);
 }
 
 // Real roots (ascending) of sum_k cin[k] z^k, degree <= 10. The real roots of p^(j) are separated
@@ -347,6 +354,73 @@ MCV_HD double e_horner(const double* c, int n, double z) {
     return f;
 }
 
+// B(z): per row i, polynomials in z (ascending): bx (deg 3), by (deg 3), bc (deg 4).
+// Row = C[4+2i] - z * C[5+2i] over the tail monomials [xz^2, xz, x, yz^2, yz, y, z^3, z^2, z, 1];
+// C points at C[0][0], rows `stride` doubles apart.
+MCV_HD void e_bz(const double* C, int stride, double (*bx)[4], double (*by)[4], double (*bc)[5]) {
+    for (int i = 0; i < 3; ++i) {
+        const double* e = C + (4 + 2 * i) * stride;
+        const double* f = C + (5 + 2 * i) * stride;
+        bx[i][3] = 0.0 - f[0]; bx[i][2] = e[0] - f[1]; bx[i][1] = e[1] - f[2]; bx[i][0] = e[2] - 0.0;
+        by[i][3] = 0.0 - f[3]; by[i][2] = e[3] - f[4]; by[i][1] = e[4] - f[5]; by[i][0] = e[5] - 0.0;
+        bc[i][4] = 0.0 - f[6]; bc[i][3] = e[6] - f[7]; bc[i][2] = e[7] - f[8]; bc[i][1] = e[8] - f[9];
+        bc[i][0] = e[9] - 0.0;
+    }
+}
+
+// det B = bx0 (by1 bc2 - by2 bc1) - by0 (bx1 bc2 - bx2 bc1) + bc0 (bx1 by2 - bx2 by1)
+MCV_HD void e_detpoly(const double (*bx)[4], const double (*by)[4], const double (*bc)[5], double* det) {
+    double t1[8], t2[8], m7[8], p1[11], p2[11], q6[7], q6b[7], m6[7], p3[11];
+    e_polymul(by[1], 3, bc[2], 4, t1);
+    e_polymul(by[2], 3, bc[1], 4, t2);
+    for (int k = 0; k < 8; ++k) m7[k] = t1[k] - t2[k];
+    e_polymul(bx[0], 3, m7, 7, p1);
+    e_polymul(bx[1], 3, bc[2], 4, t1);
+    e_polymul(bx[2], 3, bc[1], 4, t2);
+    for (int k = 0; k < 8; ++k) m7[k] = t1[k] - t2[k];
+    e_polymul(by[0], 3, m7, 7, p2);
+    e_polymul(bx[1], 3, by[2], 3, q6);
+    e_polymul(bx[2], 3, by[1], 3, q6b);
+    for (int k = 0; k < 7; ++k) m6[k] = q6[k] - q6b[k];
+    e_polymul(bc[0], 4, m6, 6, p3);
+    for (int k = 0; k < 11; ++k) det[k] = p1[k] - p2[k] + p3[k];
+}
+
+// Null vector of B(z) for one real root z (the largest of the row-pair cross products, first on
+// ties) -> unit-norm E. False if the root gives no model.
+MCV_HD bool e_model_at(const double (*bx)[4], const double (*by)[4], const double (*bc)[5], const double* nb0,
+                       const double* nb1, const double* nb2, const double* nb3, double z, double* E) {
+    double r[3][3];
+    for (int i = 0; i < 3; ++i) {
+        r[i][0] = e_horner(bx[i], 3, z);
+        r[i][1] = e_horner(by[i], 3, z);
+        r[i][2] = e_horner(bc[i], 4, z);
+    }
+    double v[3] = {0, 0, 0}, best = -1;
+    const int pa[3] = {0, 0, 1}, pb[3] = {1, 2, 2};
+    for (int q = 0; q < 3; ++q) {
+        const double* u = r[pa[q]];
+        const double* w = r[pb[q]];
+        const double c0 = u[1] * w[2] - u[2] * w[1];
+        const double c1 = u[2] * w[0] - u[0] * w[2];
+        const double c2 = u[0] * w[1] - u[1] * w[0];
+        const double n2 = c0 * c0 + c1 * c1 + c2 * c2;
+        if (n2 > best) { best = n2; v[0] = c0; v[1] = c1; v[2] = c2; }
+    }
+    const double nv = sqrt(best);
+    if (!(nv > 0) || !(fabs(v[2]) >= 1e-10 * nv)) return false;
+    const double x = v[0] / v[2], y = v[1] / v[2];
+    double e[9], ss = 0;
+    for (int k = 0; k < 9; ++k) {
+        e[k] = x * nb0[k] + y * nb1[k] + z * nb2[k] + nb3[k];
+        ss = ss + e[k] * e[k];
+    }
+    const double ns = sqrt(ss);
+    if (!(ns > 0) || !isfinite(ns)) return false;
+    for (int k = 0; k < 9; ++k) E[k] = e[k] / ns;
+    return true;
+}
+
 // Five-point solve on normalised coordinates: up to 10 unit-norm E (row-major) in E[10][9].
 MCV_HD int e_solve5(const double* x1, const double* y1, const double* x2, const double* y2, double (*E)[9]) {
     double nb[4][9];
@@ -357,71 +431,15 @@ MCV_HD int e_solve5(const double* x1, const double* y1, const double* x2, const 
         e_coeffs(nb, A);
         if (!e_eliminate(A, C)) return 0;
     }
-    // B(z): per row i, polynomials in z (ascending): bx (deg 3), by (deg 3), bc (deg 4).
-    // Row = C[4+2i] - z * C[5+2i] over the tail monomials [xz^2, xz, x, yz^2, yz, y, z^3, z^2, z, 1].
     double bx[3][4], by[3][4], bc[3][5];
-    for (int i = 0; i < 3; ++i) {
-        const double* e = C[4 + 2 * i];
-        const double* f = C[5 + 2 * i];
-        bx[i][3] = 0.0 - f[0]; bx[i][2] = e[0] - f[1]; bx[i][1] = e[1] - f[2]; bx[i][0] = e[2] - 0.0;
-        by[i][3] = 0.0 - f[3]; by[i][2] = e[3] - f[4]; by[i][1] = e[4] - f[5]; by[i][0] = e[5] - 0.0;
-        bc[i][4] = 0.0 - f[6]; bc[i][3] = e[6] - f[7]; bc[i][2] = e[7] - f[8]; bc[i][1] = e[8] - f[9];
-        bc[i][0] = e[9] - 0.0;
-    }
-    // det B = bx0 (by1 bc2 - by2 bc1) - by0 (bx1 bc2 - bx2 bc1) + bc0 (bx1 by2 - bx2 by1)
+    e_bz(&C[0][0], 10, bx, by, bc);
     double det[11];
-    {
-        double t1[8], t2[8], m7[8], p1[11], p2[11], q6[7], q6b[7], m6[7], p3[11];
-        e_polymul(by[1], 3, bc[2], 4, t1);
-        e_polymul(by[2], 3, bc[1], 4, t2);
-        for (int k = 0; k < 8; ++k) m7[k] = t1[k] - t2[k];
-        e_polymul(bx[0], 3, m7, 7, p1);
-        e_polymul(bx[1], 3, bc[2], 4, t1);
-        e_polymul(bx[2], 3, bc[1], 4, t2);
-        for (int k = 0; k < 8; ++k) m7[k] = t1[k] - t2[k];
-        e_polymul(by[0], 3, m7, 7, p2);
-        e_polymul(bx[1], 3, by[2], 3, q6);
-        e_polymul(bx[2], 3, by[1], 3, q6b);
-        for (int k = 0; k < 7; ++k) m6[k] = q6[k] - q6b[k];
-        e_polymul(bc[0], 4, m6, 6, p3);
-        for (int k = 0; k < 11; ++k) det[k] = p1[k] - p2[k] + p3[k];
-    }
+    e_detpoly(bx, by, bc, det);
     double roots[10];
     const int nr = e_poly_real_roots(det, 10, roots);
     int count = 0;
-    for (int s = 0; s < nr; ++s) {
-        const double z = roots[s];
-        double r[3][3];
-        for (int i = 0; i < 3; ++i) {
-            r[i][0] = e_horner(bx[i], 3, z);
-            r[i][1] = e_horner(by[i], 3, z);
-            r[i][2] = e_horner(bc[i], 4, z);
-        }
-        // null vector of B(z): the largest of the row-pair cross products (first on ties)
-        double v[3], best = -1;
-        const int pa[3] = {0, 0, 1}, pb[3] = {1, 2, 2};
-        for (int q = 0; q < 3; ++q) {
-            const double* u = r[pa[q]];
-            const double* w = r[pb[q]];
-            const double c0 = u[1] * w[2] - u[2] * w[1];
-            const double c1 = u[2] * w[0] - u[0] * w[2];
-            const double c2 = u[0] * w[1] - u[1] * w[0];
-            const double n2 = c0 * c0 + c1 * c1 + c2 * c2;
-            if (n2 > best) { best = n2; v[0] = c0; v[1] = c1; v[2] = c2; }
-        }
-        const double nv = sqrt(best);
-        if (!(nv > 0) || !(fabs(v[2]) >= 1e-10 * nv)) continue;
-        const double x = v[0] / v[2], y = v[1] / v[2];
-        double e[9], ss = 0;
-        for (int k = 0; k < 9; ++k) {
-            e[k] = x * nb[0][k] + y * nb[1][k] + z * nb[2][k] + nb[3][k];
-            ss = ss + e[k] * e[k];
-        }
-        const double ns = sqrt(ss);
-        if (!(ns > 0) || !isfinite(ns)) continue;
-        for (int k = 0; k < 9; ++k) E[count][k] = e[k] / ns;
-        ++count;
-    }
+    for (int s = 0; s < nr; ++s)
+        if (e_model_at(bx, by, bc, nb[0], nb[1], nb[2], nb[3], roots[s], E[count])) ++count;
     return count;
 }
 

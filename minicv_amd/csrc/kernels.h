@@ -60,6 +60,7 @@ void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const doubl
 
 // ---- essential (ransac_e.hip)
 static const int kVerifyEModelsPerWave = 4;
+static const int kEGenLanes = 16;   // lanes per hypothesis of mcv_e_generate_wave (five_point_wave.h)
 static const int kVerifyEPtsPerLane = 2;   // correspondences per lane per trip (variant screen)
 static const int kEModelSlots = 10;
 struct EOneOut {
@@ -68,9 +69,19 @@ struct EOneOut {
     int idx[5];
 };
 struct EFiveIn { double x1[5], y1[5], x2[5], y2[5]; };
+// Five-point solve split at the root finder (mcv_e_stage -> mcv_e_roots): the null basis, B(z) and
+// det B(z) of one hypothesis; status 1 = solved up to the roots, 0 = degenerate, -2 = no sample.
+struct EStage {
+    double nb[4][9];
+    double bx[3][4], by[3][4], bc[3][5];
+    double det[11];
+    int status, pad;
+};
+static const int kEStageMinHyps = 49152;   // hypCount from which generate takes the split path
+static const int kEStageLanes = 16;        // lanes per hypothesis of its matrix phases
 void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, double* d_pts4, hipStream_t s);
 void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_dense,
-                       int* d_denseSlot, int* d_nDense, int* d_counts, hipStream_t s);
+                       int* d_denseSlot, int* d_nDense, int* d_counts, void* d_stage, hipStream_t s);
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
                      int maxModels, int* d_counts, float thr2, int kind, hipStream_t s);
 void launch_e_fetch(const void* d_dense, const int* d_denseSlot, const int* d_nDense, int maxModels, int slot,

@@ -39,6 +39,7 @@ struct Plan {
     DevBuf<double> ptsd;      // essential: double4 normalised correspondences
     DevBuf<double> raw;       // essential: uploaded V2d pairs (a then b)
     DevBuf<int> dslot;        // essential: slot of each dense model
+    DevBuf<uint8_t> estage;   // essential: per-hypothesis EStage of the split five-point solve
     DevBuf<int> ndense;       // essential: dense model count, 4 cheirality counters, fetch flag
     double pnpCam[8] = {1, 1, 0, 0, 0, 0, 0, 0};   // PnP: fx, fy, cx, cy, k1, k2, p1, p2
     int64_t eLastBegin = -1;  // essential: hypothesis range of the dense list's last chunk

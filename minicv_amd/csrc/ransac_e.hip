@@ -2,19 +2,23 @@
 // (reference MiniCVNative.cpp:165-215, fivepoint.cpp:233-339).
 //
 //   mcv_e_pack          V2d pairs -> double4 normalised camera coordinates (x - cx) / f.
-//   mcv_e_generate      one lane per hypothesis: Philox sample of 5 -> five-point solve (fp64,
-//                       up to 10 models) -> all 10 slot statuses + models appended to a dense
-//                       list (atomic slot allocation; results are keyed by slot, so the order of
-//                       the dense list never reaches an output).
+//   mcv_e_generate_wave one wave per hypothesis: Philox sample of 5 -> five-point solve (fp64, up to
+//                       10 models; five_point_wave.h spreads each step over the 64 lanes with the
+//                       working matrices in LDS) -> all 10 slot statuses + models appended to a
+//                       dense list (atomic slot allocation; results are keyed by slot, so the order
+//                       of the dense list never reaches an output).
+//   mcv_e_generate      the same, one lane per hypothesis running e_solve5 (MCV_E_GEN=1; kept for
+//                       the A/B screen).
 //   mcv_e_verify<K,P,E> inlier sweep over the dense model list: wave = K models in VGPRs, 64
 //                       lanes stream the double4 correspondences, fp64 Sampson error cast to
 //                       float, ballot + popcount; the count lands in the model's slot.
-//   mcv_e_one           recompute one hypothesis (winner) -> all its models.
+//   mcv_e_one           recompute one hypothesis (winner) -> all its models (one wave).
 //   mcv_e_mask          inlier mask of the winner.
 //   mcv_e_cheirality    recoverPose: per RANSAC inlier, the 4 (R, t) candidates' cheirality tests.
-//   mcv_e_fivepoint     cvFivePoint: one five-point solve on raw coordinates.
+//   mcv_e_fivepoint     cvFivePoint: one five-point solve on raw coordinates (one wave).
 #include "mcv_common.h"
 #include "hyp_essential.h"
+#include "five_point_wave.h"
 #include "kernels.h"
 #include <cstdlib>
 
@@ -51,6 +55,93 @@ __global__ __launch_bounds__(64) void mcv_e_generate(const double* __restrict__ 
         for (int k = 0; k < 9; ++k) em.e[k] = E[s][k];
         dense[base + s] = em;
         denseSlot[base + s] = i * kEMaxModels + s;
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(64) void mcv_e_generate_wave(const double* __restrict__ pts4, int N, uint64_t seed,
+                                                          int64_t hypBegin, int hypCount, EModel* __restrict__ dense,
+                                                          int* __restrict__ denseSlot, int* __restrict__ nDense,
+                                                          int* __restrict__ counts) {
+    __shared__ EWave S[64 / G];
+    const EGroup<G> g(threadIdx.x);
+    EWave& W = S[g.base / G];
+    const int i = blockIdx.x * (64 / G) + g.base / G;
+    if (i >= hypCount) return;
+    double E[9];
+    const int n = ew_hypothesis(W, g, pts4, N, seed, (uint64_t)(hypBegin + i), E, nullptr);
+    const int m = n > 0 ? n : 0;
+    if (g.sub < kEMaxModels)
+        counts[(int64_t)i * kEMaxModels + g.sub] =
+            g.sub < m ? 0 : (g.sub == 0 && n == kStatusNoSample ? kStatusNoSample : kStatusNoModel);
+    int base = 0;
+    if (g.sub == 0 && m > 0) base = atomicAdd(nDense, m);
+    base = __shfl(base, g.base);
+    if (g.sub < m) {
+        EModel em;
+        for (int k = 0; k < 9; ++k) em.e[k] = E[k];
+        dense[base + g.sub] = em;
+        denseSlot[base + g.sub] = i * kEMaxModels + g.sub;
+    }
+}
+
+// Split path, part 1: matrix phases of G-lane groups -> EStage per hypothesis.
+template <int G>
+__global__ __launch_bounds__(64) void mcv_e_stage(const double* __restrict__ pts4, int N, uint64_t seed,
+                                                  int64_t hypBegin, int hypCount, EStage* __restrict__ st) {
+    __shared__ EWave S[64 / G];
+    const EGroup<G> g(threadIdx.x);
+    const int i = blockIdx.x * (64 / G) + g.base / G;
+    if (i >= hypCount) return;
+    ew_stage_hypothesis(S[g.base / G], g, pts4, N, seed, (uint64_t)(hypBegin + i), st + i);
+}
+
+// Split path, part 2: one lane per hypothesis — real roots of det B(z) (e_poly_real_roots, root
+// lists in LDS columns), one model per root, statuses + dense append (one atomic per wave).
+__global__ __launch_bounds__(64) void mcv_e_roots(const EStage* __restrict__ st, int hypCount,
+                                                  EModel* __restrict__ dense, int* __restrict__ denseSlot,
+                                                  int* __restrict__ nDense, int* __restrict__ counts) {
+    __shared__ double Lc[11][64];
+    __shared__ double Lr[2][10][64];
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * 64 + lane;
+    const bool act = i < hypCount;
+    const EStage* h = st + (act ? i : 0);
+    const int status = act ? h->status : 0;
+    int nr = 0, which = 0;
+    if (status == 1) nr = ew_lane_roots(h->det, Lc, Lr, lane, &which);
+    uint32_t okm = 0;
+    int m = 0;
+    for (int r = 0; r < nr; ++r) {
+        double E[9];
+        if (e_model_at(h->bx, h->by, h->bc, h->nb[0], h->nb[1], h->nb[2], h->nb[3], Lr[which][r][lane], E)) {
+            okm |= 1u << r;
+            ++m;
+        }
+    }
+    if (act)
+        for (int s = 0; s < kEMaxModels; ++s)
+            counts[(int64_t)i * kEMaxModels + s] =
+                s < m ? 0 : (s == 0 && status == kStatusNoSample ? kStatusNoSample : kStatusNoModel);
+    // wave-exclusive scan of m -> one atomic per wave
+    int incl = m;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        incl += lane >= o ? y : 0;
+    }
+    const int total = __shfl(incl, 63);
+    int base = 0;
+    if (lane == 63 && total > 0) base = atomicAdd(nDense, total);
+    base = __shfl(base, 63) + incl - m;
+    int t = 0;
+    for (int r = 0; r < nr; ++r) {
+        if (!((okm >> r) & 1u)) continue;
+        EModel em;
+        (void)e_model_at(h->bx, h->by, h->bc, h->nb[0], h->nb[1], h->nb[2], h->nb[3], Lr[which][r][lane], em.e);
+        dense[base + t] = em;
+        denseSlot[base + t] = i * kEMaxModels + t;
+        ++t;
     }
 }
 
@@ -114,16 +205,20 @@ __global__ __launch_bounds__(256) void mcv_e_fetch(const EModel* __restrict__ de
     }
 }
 
-__global__ void mcv_e_one(const double* __restrict__ pts4, int N, uint64_t seed, int64_t hyp,
-                          EOneOut* __restrict__ out) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    double E[kEMaxModels][9];
+__global__ __launch_bounds__(64) void mcv_e_one(const double* __restrict__ pts4, int N, uint64_t seed, int64_t hyp,
+                                                EOneOut* __restrict__ out) {
+    __shared__ EWave S;
+    const EGroup<64> g(threadIdx.x);
+    const int lane = threadIdx.x;
+    double E[9];
     int idx[5] = {-1, -1, -1, -1, -1};
-    const int n = e_hypothesis(pts4, N, seed, (uint64_t)hyp, E, idx);
-    out->status = n;
-    for (int i = 0; i < 5; ++i) out->idx[i] = idx[i];
-    for (int s = 0; s < kEMaxModels; ++s)
-        for (int k = 0; k < 9; ++k) out->E[s][k] = s < n ? E[s][k] : 0.0;
+    const int n = ew_hypothesis(S, g, pts4, N, seed, (uint64_t)hyp, E, idx);
+    if (lane == 0) {
+        out->status = n;
+        for (int i = 0; i < 5; ++i) out->idx[i] = idx[i];
+    }
+    if (lane < kEMaxModels)
+        for (int k = 0; k < 9; ++k) out->E[lane][k] = lane < n ? E[k] : 0.0;
 }
 
 __global__ __launch_bounds__(256) void mcv_e_mask(const double4* __restrict__ pts, int N, EModel m, float thr2,
@@ -156,13 +251,16 @@ __global__ __launch_bounds__(256) void mcv_e_cheirality(const double4* __restric
     }
 }
 
-__global__ void mcv_e_fivepoint(EFiveIn in, EOneOut* __restrict__ out) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    double E[kEMaxModels][9];
-    const int n = e_solve5(in.x1, in.y1, in.x2, in.y2, E);
-    out->status = n;
-    for (int s = 0; s < kEMaxModels; ++s)
-        for (int k = 0; k < 9; ++k) out->E[s][k] = s < n ? E[s][k] : 0.0;
+__global__ __launch_bounds__(64) void mcv_e_fivepoint(EFiveIn in, EOneOut* __restrict__ out) {
+    __shared__ EWave S;
+    const EGroup<64> g(threadIdx.x);
+    const int lane = threadIdx.x;
+    ew_stage(S, g, in.x1, in.y1, in.x2, in.y2);
+    double E[9];
+    const int n = ew_solve5(S, g, E);
+    if (lane == 0) out->status = n;
+    if (lane < kEMaxModels)
+        for (int k = 0; k < 9; ++k) out->E[lane][k] = lane < n ? E[k] : 0.0;
 }
 
 // ---- launchers ---------------------------------------------------------------------------------
@@ -174,10 +272,40 @@ void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, do
 }
 
 void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_dense,
-                       int* d_denseSlot, int* d_nDense, int* d_counts, hipStream_t s) {
+                       int* d_denseSlot, int* d_nDense, int* d_counts, void* d_stage, hipStream_t s) {
+    // MCV_E_GEN: lanes per hypothesis of the five-point solve (16 / 32 / 64; 1 = the one-lane
+    // e_solve5 kernel), for the A/B screen only
+    static const int group = [] {
+        const char* e = getenv("MCV_E_GEN");
+        return e ? atoi(e) : kEGenLanes;
+    }();
     (void)hipMemsetAsync(d_nDense, 0, sizeof(int), s);
-    hipLaunchKernelGGL(mcv_e_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
-                       hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+    if (hypCount <= 0) return;
+    if (d_stage && group == kEGenLanes) {   // many hypotheses: matrix phases per group, roots per lane
+        EStage* st = (EStage*)d_stage;
+        hipLaunchKernelGGL(mcv_e_stage<kEStageLanes>, dim3((hypCount + 64 / kEStageLanes - 1) / (64 / kEStageLanes)),
+                           dim3(64), 0, s, d_pts4, N, seed, hypBegin, hypCount, st);
+        hipLaunchKernelGGL(mcv_e_roots, dim3((hypCount + 63) / 64), dim3(64), 0, s, st, hypCount, (EModel*)d_dense,
+                           d_denseSlot, d_nDense, d_counts);
+        return;
+    }
+    switch (group) {
+        case 1:
+            hipLaunchKernelGGL(mcv_e_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+                               hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+            break;
+        case 64:
+            hipLaunchKernelGGL(mcv_e_generate_wave<64>, dim3(hypCount), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+                               hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+            break;
+        case 32:
+            hipLaunchKernelGGL(mcv_e_generate_wave<32>, dim3((hypCount + 1) / 2), dim3(64), 0, s, d_pts4, N, seed,
+                               hypBegin, hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+            break;
+        default:
+            hipLaunchKernelGGL(mcv_e_generate_wave<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, seed,
+                               hypBegin, hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+    }
 }
 
 template <int K, int P>

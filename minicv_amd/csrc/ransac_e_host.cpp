@@ -32,7 +32,9 @@ void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& c
     const float thr2 = (float)(cfg.threshold * cfg.threshold);
     {
         ProfScope pg("e_generate", s);
-        launch_e_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts, s);
+        if (hypCount >= kEStageMinHyps) P.estage.ensure((size_t)hypCount * sizeof(EStage));
+        launch_e_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts,
+                          hypCount >= kEStageMinHyps ? P.estage.p : nullptr, s);
     }
     P.eLastBegin = hypBegin;
     P.eLastCount = hypCount;

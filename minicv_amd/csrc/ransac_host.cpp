@@ -104,6 +104,7 @@ void Plan::reserve(int n, int64_t hyps) {
         raw.ensure((size_t)maxN * 4);
         dslot.ensure((size_t)maxHyps * slots);
         ndense.ensure(8);
+        if (model == MCV_MODEL_ESSENTIAL && maxHyps >= kEStageMinHyps) estage.ensure((size_t)maxHyps * sizeof(EStage));
     } else {
         pts.ensure((size_t)maxN * 4);
     }
