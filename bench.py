@@ -37,6 +37,7 @@ E_SEED = 6
 E_FOCAL, E_PP, E_THR_PX = 800.0, (640.0, 360.0), 1.0
 P_N_CORR = 20_000             # PnP (cvSolvePnPRansac path): reference testPnp size (Program.fs:14)
 P_HYPS_TOTAL = 1 << 16
+P_FLOPS_PER_EVAL = 51         # pnp_project: R X + t (18), 1 / Zc (1), distortion + intrinsics (32)
 P_SEED = 8
 P_THR_PX = 2.0
 THR = 5e-3
@@ -492,10 +493,15 @@ def bench_essential(args, world, rank, dev):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    # models per verify launch (the sweep runs over the dense model list): count them once, untimed
+    slots = torch.zeros(hyps * NL.E_SLOTS, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, rank * hyps, hyps, key, slots)
+    models = int((slots >= 0).sum().item())
     if rank == 0:
-        models = int(result.get("models", 0))
         v_ms = vms.value / max(vl, 1)
         g_ms = gms.value / max(gl, 1)
+        alg_bytes = 32.0 * n * models            # each model reads all N double4 correspondences
+        fl = F_FLOPS_PER_EVAL * n * models / (v_ms * 1e-3) / 1e12
         line = {
             "metric": "RANSAC hypotheses/sec, findEssentialMat 5-pt (cvRecoverPose path) @100k corrs",
             "value": total * args.steps / el, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
@@ -508,6 +514,15 @@ def bench_essential(args, world, rank, dev):
                        "parallelism": f"hypothesis-sharded dp{world}"},
             "kernels": {"mcv_e_generate": {"avg_launch_ms": g_ms, "launches": gl},
                         "mcv_e_verify": {"avg_launch_ms": v_ms, "launches": vl}},
+            "roofline": {"bound": "hbm", "achieved": alg_bytes / (v_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": alg_bytes / (v_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                         "traffic": load_traffic("mcv_e_verify", f"{n}x{hyps}"), "kernel": "mcv_e_verify",
+                         "avg_launch_ms": v_ms, "launches": vl, "models_per_launch": models,
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "note": "frac > 1: the 32 N-byte point set is L2-resident and each load serves 4 models; "
+                                 "the sweep is fp64-VALU-bound (see fp64)",
+                         "fp64": {"achieved": fl, "peak": FP64_PEAK_TF, "unit": "TFLOP/s", "frac": fl / FP64_PEAK_TF,
+                                  "model": f"{F_FLOPS_PER_EVAL} fp64 FLOP per (model, correspondence)"}},
             "result": {"best_count": result["count"], "best_slot": result["slot"],
                        "final_count": result["final_count"]},
         }
@@ -613,6 +628,8 @@ def bench_pnp(args, world, rank, dev):
         el = float(tt.item())
     if rank == 0:
         v_ms = vms.value / max(vl, 1)
+        p_bytes = 20.0 * n * hyps                # PnpPoint {X, Y, Z, u, v} f32 per (hypothesis, correspondence)
+        p_fl = P_FLOPS_PER_EVAL * n * hyps / (v_ms * 1e-3) / 1e12
         line = {
             "metric": "RANSAC hypotheses/sec, solvePnPRansac AP3P (cvSolvePnPRansac path) @20k corrs",
             "value": total * args.steps / el, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
@@ -625,6 +642,15 @@ def bench_pnp(args, world, rank, dev):
                        "parallelism": f"hypothesis-sharded dp{world}"},
             "kernels": {"mcv_pnp_verify": {"avg_launch_ms": v_ms, "launches": vl,
                                            "evaluations_per_s": n * hyps / max(v_ms * 1e-3, 1e-12)}},
+            "roofline": {"bound": "hbm", "achieved": p_bytes / (v_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": p_bytes / (v_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                         "traffic": load_traffic("mcv_pnp_verify", f"{n}x{hyps}"), "kernel": "mcv_pnp_verify",
+                         "avg_launch_ms": v_ms, "launches": vl, "algorithmic_bytes_per_launch": p_bytes,
+                         "note": "frac > 1: the 20 N-byte point set is L2-resident and each load serves 4 poses; "
+                                 "the sweep is fp64-VALU-bound (see fp64)",
+                         "fp64": {"achieved": p_fl, "peak": FP64_PEAK_TF, "unit": "TFLOP/s", "frac": p_fl / FP64_PEAK_TF,
+                                  "model": f"{P_FLOPS_PER_EVAL} fp64 FLOP per (hypothesis, correspondence), "
+                                           "a division counted as one"}},
             "result": {"best_count": result["count"], "best_hyp": result["idx"],
                        "final_count": result["final_count"], "true_inliers": int(inl.sum())},
         }

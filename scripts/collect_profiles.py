@@ -22,7 +22,7 @@ PROF = ROOT / "profiles"
 WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2", "scaled"]
 # dominant kernel per BASELINE workload (substring of the demangled rocprofv3 kernel name)
 KERNELS = {"homography": "mcv_h_verify_pk", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
-           "l2": "mcv_l2_mfma"}
+           "l2": "mcv_l2_mfma", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify"}
 
 
 def last_json(path: Path):
@@ -79,6 +79,13 @@ def main():
         elif w == "fundamental":
             config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
                 16.0 * c.get("correspondences", 0) * c.get("hypotheses_total", 0)
+        elif w == "essential":
+            models = (j or {}).get("roofline", {}).get("models_per_launch", 0)
+            config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
+                32.0 * c.get("correspondences", 0) * models
+        elif w == "pnp":
+            config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
+                20.0 * c.get("correspondences", 0) * c.get("hypotheses_total", 0)
         else:
             config = f"{c.get('queries')}x{c.get('train')}"
             dim_bytes = 32.0 if w == "hamming" else 512.0
