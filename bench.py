@@ -49,7 +49,6 @@ HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # i.e. 18 issue slots of 2 cycles (wave64 on SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x
 # 2.4 GHz / 2 x 64 lanes / 18.
 VALU_SLOTS_PER_EVAL = 18
-F_FLOPS_PER_EVAL = 26          # fp64 Sampson (fused): 11 FMA + 2 mul + 1 div per (hypothesis, point)
 FP64_PEAK_TF = 78.6            # MI355X fp64 vector (spec)
 FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: fp32-input MFMA = fp32 vector peak
 # Hamming issue model (measured per-instruction costs, scripts/exp/valu_rate.hip): per 64 pairs
@@ -57,6 +56,12 @@ FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: fp32-input MFMA = fp32 vec
 HAMMING_CYC_PER_WAVE_PAIR = 58
 HAMMING_PEAK_PAIRS = 256 * 4 * 2.4e9 / HAMMING_CYC_PER_WAVE_PAIR * 64
 VALU_PEAK_EVALS = 256 * 4 * 2.4e9 / 2 * 64 / VALU_SLOTS_PER_EVAL
+# VALU issue model of the certified packed-fp32 Sampson prefilter (sampson_pk.h; F and E sweeps),
+# per (model pair, correspondence): 17 v_pk_fma + 3 v_pk_mul + 2 v_pk_add (4 cycles each), 2 v_and
+# + 2 v_max_f32 (2 cycles), 4 v_cmp_f32 (VOP3, 4 cycles) = 112 cycles, i.e. 56 SIMD cycles per
+# 64 (model, correspondence) evaluations; the fp64 re-test of undecided lanes is ~1e-4 of them.
+SPK_CYC_PER_WAVE_EVAL = 56
+SPK_PEAK_EVALS = 256 * 4 * 2.4e9 / SPK_CYC_PER_WAVE_EVAL * 64
 
 
 def parse():
@@ -370,7 +375,6 @@ def bench_ransac(args):
                            "refined_count": result["final_count"]},
             }
         else:
-            fl = F_FLOPS_PER_EVAL * n * hyps / (avg_ms * 1e-3) / 1e12
             line = {
                 "metric": "RANSAC hypotheses/sec, findFundamentalMat 8-pt @500k corrs (BASELINE config[3])",
                 "value": value,
@@ -392,9 +396,12 @@ def bench_ransac(args):
                              "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                              "kernel": "mcv_f_verify", "avg_launch_ms": avg_ms, "launches": launches,
                              "algorithmic_bytes_per_launch": alg_bytes,
-                             "fp64": {"achieved": fl, "peak": FP64_PEAK_TF, "unit": "TFLOP/s",
-                                      "frac": fl / FP64_PEAK_TF,
-                                      "model": f"{F_FLOPS_PER_EVAL} fp64 FLOP per (hypothesis, correspondence)"}},
+                             "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 8 "
+                                     "models; the sweep's binding roof is VALU issue (see valu)",
+                             "valu": {"achieved": n * hyps / (avg_ms * 1e-3), "peak": SPK_PEAK_EVALS,
+                                      "unit": "evaluations/s", "frac": n * hyps / (avg_ms * 1e-3) / SPK_PEAK_EVALS,
+                                      "model": f"certified packed-fp32 Sampson prefilter: {SPK_CYC_PER_WAVE_EVAL} "
+                                               "SIMD cycles per 64 (model, correspondence) at 2.4 GHz"}},
                 "result": {"best_count": result["count"], "best_hyp": result["idx"]},
             }
         if world == 1 and not args.no_cpu_baseline:
@@ -500,8 +507,7 @@ def bench_essential(args, world, rank, dev):
     if rank == 0:
         v_ms = vms.value / max(vl, 1)
         g_ms = gms.value / max(gl, 1)
-        alg_bytes = 32.0 * n * models            # each model reads all N double4 correspondences
-        fl = F_FLOPS_PER_EVAL * n * models / (v_ms * 1e-3) / 1e12
+        alg_bytes = 16.0 * n * models            # each model reads all N float4 correspondences
         line = {
             "metric": "RANSAC hypotheses/sec, findEssentialMat 5-pt (cvRecoverPose path) @100k corrs",
             "value": total * args.steps / el, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
@@ -519,10 +525,13 @@ def bench_essential(args, world, rank, dev):
                          "traffic": load_traffic("mcv_e_verify", f"{n}x{hyps}"), "kernel": "mcv_e_verify",
                          "avg_launch_ms": v_ms, "launches": vl, "models_per_launch": models,
                          "algorithmic_bytes_per_launch": alg_bytes,
-                         "note": "frac > 1: the 32 N-byte point set is L2-resident and each load serves 4 models; "
-                                 "the sweep is fp64-VALU-bound (see fp64)",
-                         "fp64": {"achieved": fl, "peak": FP64_PEAK_TF, "unit": "TFLOP/s", "frac": fl / FP64_PEAK_TF,
-                                  "model": f"{F_FLOPS_PER_EVAL} fp64 FLOP per (model, correspondence)"}},
+                         "note": "frac > 1: the point set is L2-resident and each load serves 6 models; the "
+                                 "sweep reads the 16 N-byte float4 copy (32 N-byte double4 only for undecided "
+                                 "lanes) and is VALU-issue-bound (see valu)",
+                         "valu": {"achieved": n * models / (v_ms * 1e-3), "peak": SPK_PEAK_EVALS,
+                                  "unit": "evaluations/s", "frac": n * models / (v_ms * 1e-3) / SPK_PEAK_EVALS,
+                                  "model": f"certified packed-fp32 Sampson prefilter: {SPK_CYC_PER_WAVE_EVAL} SIMD "
+                                           "cycles per 64 (model, correspondence) at 2.4 GHz"}},
             "result": {"best_count": result["count"], "best_slot": result["slot"],
                        "final_count": result["final_count"]},
         }

@@ -52,7 +52,10 @@ void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBeg
                        int* d_counts, hipStream_t s);
 void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s);
 void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
-                     int kind, hipStream_t s);
+                     int kind, hipStream_t s, const double* d_bb = nullptr);
+// max |x1|, |y1|, |x2|, |y2| of float4 (fp64 = false) or double4 points -> d_bb[4] (fp64); with
+// d_out32 (double4 input) also the float4-rounded copy of the points.
+void launch_abs_bound4(const void* d_pts4, bool fp64, int N, double* d_bb, float* d_out32, hipStream_t s);
 void launch_f_mask(const float* d_pts4, int N, const double* F9, float thr2, int kind, uint8_t* d_mask, int* d_count,
                    hipStream_t s);
 void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,
@@ -83,7 +86,8 @@ void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, do
 void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_dense,
                        int* d_denseSlot, int* d_nDense, int* d_counts, void* d_stage, hipStream_t s);
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
-                     int maxModels, int* d_counts, float thr2, int kind, hipStream_t s);
+                     int maxModels, int* d_counts, float thr2, int kind, hipStream_t s, const float* d_pts32 = nullptr,
+                     const double* d_bb = nullptr);
 void launch_e_fetch(const void* d_dense, const int* d_denseSlot, const int* d_nDense, int maxModels, int slot,
                     void* d_out, int* d_found, hipStream_t s);
 void launch_e_one(const double* d_pts4, int N, uint64_t seed, int64_t hyp, EOneOut* d_out, hipStream_t s);

@@ -34,6 +34,7 @@ struct Plan {
     DevBuf<uint8_t> mask;
     DevBuf<int> count;
     DevBuf<float> bbox;       // max |x|, max |y| of the source points (fused fast-path bound)
+    DevBuf<double> bb4;       // F / E: max |x1|, |y1|, |x2|, |y2| (packed-fp32 Sampson prefilter bound)
     DevBuf<float> pairs;      // homography: paired layout of the packed sweep (8 floats per 2)
     DevBuf<uint8_t> one;      // single-hypothesis output record
     DevBuf<double> ptsd;      // essential: double4 normalised correspondences

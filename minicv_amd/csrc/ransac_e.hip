@@ -12,6 +12,8 @@
 //   mcv_e_verify<K,P,E> inlier sweep over the dense model list: wave = K models in VGPRs, 64
 //                       lanes stream the double4 correspondences, fp64 Sampson error cast to
 //                       float, ballot + popcount; the count lands in the model's slot.
+//   mcv_e_verify_pk     the same sweep through the certified packed-fp32 prefilter (sampson_pk.h)
+//                       over a float4 copy of the points; undecided lanes re-tested in fp64.
 //   mcv_e_one           recompute one hypothesis (winner) -> all its models (one wave).
 //   mcv_e_mask          inlier mask of the winner.
 //   mcv_e_cheirality    recoverPose: per RANSAC inlier, the 4 (R, t) candidates' cheirality tests.
@@ -19,6 +21,7 @@
 #include "mcv_common.h"
 #include "hyp_essential.h"
 #include "five_point_wave.h"
+#include "sampson_pk.h"
 #include "kernels.h"
 #include <cstdlib>
 
@@ -193,6 +196,84 @@ __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ 
     }
 }
 
+template <int KP, int P>
+__global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict__ pts32,
+                                                       const double4* __restrict__ pts, int N,
+                                                       const EModel* __restrict__ dense,
+                                                       const int* __restrict__ denseSlot,
+                                                       const int* __restrict__ nDense, int* __restrict__ counts,
+                                                       float thr2, int kind, SampsonPkCut cut,
+                                                       const double* __restrict__ bb) {
+    constexpr int K = 2 * KP;
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    const int lane = threadIdx.x & 63;
+    const int total = __builtin_amdgcn_readfirstlane(*nDense);
+    const int m0 = wave * K;
+    if (m0 >= total) return;
+    const double B[4] = {bb[0], bb[1], bb[2], bb[3]};
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) valid[k] = m0 + k < total;
+    SampsonPkPair pr[KP];
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+        double Fa[9], Fb[9];
+        const EModel ma = dense[valid[2 * kp] ? m0 + 2 * kp : m0];
+        const EModel mb = dense[valid[2 * kp + 1] ? m0 + 2 * kp + 1 : m0];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            Fa[j] = valid[2 * kp] ? ma.e[j] : f_dummy_model(j);
+            Fb[j] = valid[2 * kp + 1] ? mb.e[j] : f_dummy_model(j);
+        }
+        spk_make_pair(pr[kp], Fa, Fb, B, cut);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) asm volatile("" : "+v"(pr[kp].f[j]));
+        asm volatile("" : "+v"(pr[kp].ec));
+        asm volatile("" : "+v"(pr[kp].nedl));
+        asm volatile("" : "+v"(pr[kp].edh));
+    }
+    auto f64 = [&](int k, double (&F)[9]) {
+        const int mk = valid[k] ? m0 + k : -1;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) F[j] = mk >= 0 ? dense[mk].e[j] : f_dummy_model(j);
+    };
+    uint32_t cnt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt[k] = 0;
+    const int step = 64 * P;
+    const int nFull = N - N % step;
+    for (int base = 0; base < nFull; base += step) {
+        float4 q[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) q[p] = pts32[base + 64 * p + lane];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const int idx = base + 64 * p + lane;
+            auto x64 = [&](double& x1, double& y1, double& x2, double& y2) {
+                const double4 d = pts[idx];
+                x1 = d.x; y1 = d.y; x2 = d.z; y2 = d.w;
+            };
+            spk_sweep_point<KP>(pr, q[p], true, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
+        }
+    }
+    for (int base = nFull; base < N; base += 64) {
+        const int p = base + lane;
+        const bool v = p < N;
+        const int idx = v ? p : 0;
+        const float4 q = pts32[idx];
+        auto x64 = [&](double& x1, double& y1, double& x2, double& y2) {
+            const double4 d = pts[idx];
+            x1 = d.x; y1 = d.y; x2 = d.z; y2 = d.w;
+        };
+        spk_sweep_point<KP>(pr, q, v, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid[k]) counts[denseSlot[m0 + k]] = (int)cnt[k];
+    }
+}
+
 // Winner's model straight from the dense list of the last evaluated chunk (slot -> model), instead
 // of a single-lane five-point re-solve (the same code produced it, so the model is identical).
 __global__ __launch_bounds__(256) void mcv_e_fetch(const EModel* __restrict__ dense, const int* __restrict__ denseSlot,
@@ -323,8 +404,34 @@ static void launch_e_verify_kp(const double4* p, int N, const EModel* m, const i
 
 // Sweep shape (models per wave K, correspondences per lane per trip P); MCV_E_VARIANT selects
 // alternatives for the variant screen (scripts/sweep_e_variants.sh) only.
+template <int KP, int P>
+static void launch_e_verify_pk_kp(const float4* p32, const double4* p, int N, const EModel* m, const int* d_denseSlot,
+                                  const int* d_nDense, int maxModels, int* d_counts, float thr2, int kind,
+                                  const SampsonPkCut& cut, const double* d_bb, hipStream_t s) {
+    const int blocks = ((maxModels + 2 * KP - 1) / (2 * KP) + 3) / 4;
+    hipLaunchKernelGGL((mcv_e_verify_pk<KP, P>), dim3(blocks), dim3(256), 0, s, p32, p, N, m, d_denseSlot, d_nDense,
+                       d_counts, thr2, kind, cut, d_bb);
+}
+
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
-                     int maxModels, int* d_counts, float thr2, int kind, hipStream_t s) {
+                     int maxModels, int* d_counts, float thr2, int kind, hipStream_t s, const float* d_pts32,
+                     const double* d_bb) {
+    static const int pkv = [] {
+        const char* e = getenv("MCV_E_PK");
+        return e ? atoi(e) : 0;
+    }();
+    if (d_pts32 && d_bb && pkv != 9) {   // certified packed-fp32 prefilter
+        const SampsonPkCut cut = sampson_pk_cut_host(sampson_cut(thr2));
+        const float4* p32 = (const float4*)d_pts32;
+        const double4* p = (const double4*)d_pts4;
+        const EModel* m = (const EModel*)d_dense;
+        switch (pkv) {
+            case 1: launch_e_verify_pk_kp<2, 2>(p32, p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, cut, d_bb, s); return;
+            case 2: launch_e_verify_pk_kp<4, 1>(p32, p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, cut, d_bb, s); return;
+            case 3: launch_e_verify_pk_kp<2, 1>(p32, p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, cut, d_bb, s); return;
+            default: launch_e_verify_pk_kp<3, 2>(p32, p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, cut, d_bb, s); return;
+        }
+    }
     static const int variant = [] {
         const char* e = getenv("MCV_E_VARIANT");
         return e ? atoi(e) : 0;

@@ -40,9 +40,12 @@ void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& c
     P.eLastCount = hypCount;
     P.eLastSeed = cfg.seed;
     P.eLastPts = d_pts;
+    P.bb4.ensure(4);
+    P.pts.ensure((size_t)N * 4);
+    launch_abs_bound4(d_pts, true, N, P.bb4.p, P.pts.p, s);   // fp32 copy + bounds for the prefilter
     ProfScope ps("e_verify", s);
     launch_e_verify(d_pts, N, P.models.p, P.dslot.p, P.ndense.p, hypCount * kEModelSlots, d_counts, thr2, e_kind(cfg),
-                    s);
+                    s, P.pts.p, P.bb4.p);
 }
 
 static EOneOut e_one(Plan& P, const double* d_pts, int N, uint64_t seed, int64_t hyp, hipStream_t s) {

@@ -5,13 +5,19 @@
 //   mcv_f_verify<K, E>  inlier sweep: wave = K hypotheses (fp64 models in VGPRs), 64 lanes stream
 //                       the packed float4 correspondences; per (hypothesis, point) the fp64
 //                       Sampson / epipolar error E, cast to float, ballot + s_bcnt1 count.
+//   mcv_f_verify_pk<KP,P> the Sampson sweep with the certified packed-fp32 prefilter
+//                       (sampson_pk.h): wave = KP model pairs, undecided lanes re-tested in fp64.
+//   mcv_abs_bound4      max |x1|, |y1|, |x2|, |y2| over the point set (the prefilter's bound).
 //   mcv_f_mask          inlier mask of the winner.
 //   OpFAtA              fixed-order fp64 reduction of A^T A (run8Point over all points).
 #include "mcv_common.h"
 #include "hyp_fundamental.h"
+#include "sampson_pk.h"
 #include "reduce.h"
 #include "kernels.h"
 #include <cstdlib>
+#include <algorithm>
+#include <cmath>
 
 namespace mcv {
 
@@ -85,6 +91,105 @@ __global__ __launch_bounds__(256) void mcv_f_verify(const float4* __restrict__ p
     }
 }
 
+// Point-set bounds for the packed prefilter: bb = max |x1|, |y1|, |x2|, |y2| as fp64 bit patterns
+// (non-negative doubles order like their bits; NaN coordinates force +inf, i.e. no certification).
+// With out32 (double4 input) the points are also written rounded to float4 for the fp32 sweep.
+template <class T4>
+__global__ __launch_bounds__(256) void mcv_abs_bound4(const T4* __restrict__ pts, int N,
+                                                      unsigned long long* __restrict__ bb, float4* __restrict__ out32) {
+    double m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
+        const T4 q = pts[i];
+        const double x = q.x, y = q.y, z = q.z, w = q.w;
+        m0 = x == x ? fmax(m0, fabs(x)) : __builtin_inf();
+        m1 = y == y ? fmax(m1, fabs(y)) : __builtin_inf();
+        m2 = z == z ? fmax(m2, fabs(z)) : __builtin_inf();
+        m3 = w == w ? fmax(m3, fabs(w)) : __builtin_inf();
+        if (out32) out32[i] = float4{(float)q.x, (float)q.y, (float)q.z, (float)q.w};
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        m0 = fmax(m0, __shfl_xor(m0, off, 64));
+        m1 = fmax(m1, __shfl_xor(m1, off, 64));
+        m2 = fmax(m2, __shfl_xor(m2, off, 64));
+        m3 = fmax(m3, __shfl_xor(m3, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(bb + 0, (unsigned long long)__double_as_longlong(m0));
+        atomicMax(bb + 1, (unsigned long long)__double_as_longlong(m1));
+        atomicMax(bb + 2, (unsigned long long)__double_as_longlong(m2));
+        atomicMax(bb + 3, (unsigned long long)__double_as_longlong(m3));
+    }
+}
+
+template <int KP, int P>
+__global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict__ pts, int N,
+                                                       const FModelD* __restrict__ models, int* __restrict__ counts,
+                                                       int hypCount, float thr2, int kind, SampsonPkCut cut,
+                                                       const double* __restrict__ bb) {
+    constexpr int K = 2 * KP;
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    const int lane = threadIdx.x & 63;
+    const int h0 = wave * K;
+    if (h0 >= hypCount) return;
+    const double B[4] = {bb[0], bb[1], bb[2], bb[3]};
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) valid[k] = (h0 + k < hypCount) && (counts[h0 + k] >= 0);
+    SampsonPkPair pr[KP];
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+        double Fa[9], Fb[9];
+        const FModelD ma = models[valid[2 * kp] ? h0 + 2 * kp : h0];
+        const FModelD mb = models[valid[2 * kp + 1] ? h0 + 2 * kp + 1 : h0];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            Fa[j] = valid[2 * kp] ? ma.f[j] : f_dummy_model(j);
+            Fb[j] = valid[2 * kp + 1] ? mb.f[j] : f_dummy_model(j);
+        }
+        spk_make_pair(pr[kp], Fa, Fb, B, cut);
+        // VGPR operands (the pairs are wave-uniform): no constant-bus moves inside the packed ops
+#pragma unroll
+        for (int j = 0; j < 9; ++j) asm volatile("" : "+v"(pr[kp].f[j]));
+        asm volatile("" : "+v"(pr[kp].ec));
+        asm volatile("" : "+v"(pr[kp].nedl));
+        asm volatile("" : "+v"(pr[kp].edh));
+    }
+    auto f64 = [&](int k, double (&F)[9]) {
+        const int hk = valid[k] ? h0 + k : -1;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) F[j] = hk >= 0 ? models[hk].f[j] : f_dummy_model(j);
+    };
+    uint32_t cnt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt[k] = 0;
+    const int step = 64 * P;
+    const int nFull = N - N % step;
+    for (int base = 0; base < nFull; base += step) {
+        float4 q[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) q[p] = pts[base + 64 * p + lane];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const float4 qp = q[p];
+            auto x64 = [&](double& x1, double& y1, double& x2, double& y2) { x1 = qp.x; y1 = qp.y; x2 = qp.z; y2 = qp.w; };
+            spk_sweep_point<KP>(pr, qp, true, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
+        }
+    }
+    for (int base = nFull; base < N; base += 64) {
+        const int p = base + lane;
+        const bool v = p < N;
+        const float4 q = pts[v ? p : 0];
+        auto x64 = [&](double& x1, double& y1, double& x2, double& y2) { x1 = q.x; y1 = q.y; x2 = q.z; y2 = q.w; };
+        spk_sweep_point<KP>(pr, q, v, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid[k]) counts[h0 + k] = (int)cnt[k];
+    }
+}
+
 __global__ __launch_bounds__(256) void mcv_f_mask(const float4* __restrict__ pts, int N, FModelD m, float thr2,
                                                   int kind, uint8_t* __restrict__ mask, int* __restrict__ count) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -145,11 +250,46 @@ static int f_variant() {
     return v;
 }
 
+void launch_abs_bound4(const void* d_pts4, bool fp64, int N, double* d_bb, float* d_out32, hipStream_t s) {
+    (void)hipMemsetAsync(d_bb, 0, 4 * sizeof(double), s);
+    if (N <= 0) return;
+    const int blocks = std::min(1024, (N + 255) / 256);
+    if (fp64)
+        hipLaunchKernelGGL(mcv_abs_bound4<double4>, dim3(blocks), dim3(256), 0, s, (const double4*)d_pts4, N,
+                           (unsigned long long*)d_bb, (float4*)d_out32);
+    else
+        hipLaunchKernelGGL(mcv_abs_bound4<float4>, dim3(blocks), dim3(256), 0, s, (const float4*)d_pts4, N,
+                           (unsigned long long*)d_bb, (float4*)nullptr);
+}
+
+template <int KP, int P>
+static void launch_f_verify_pk_kp(const float4* p, int N, const FModelD* m, int* d_counts, int hypCount, float thr2,
+                                  int kind, const SampsonPkCut& cut, const double* d_bb, hipStream_t s) {
+    const int blocks = ((hypCount + 2 * KP - 1) / (2 * KP) + 3) / 4;
+    hipLaunchKernelGGL((mcv_f_verify_pk<KP, P>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, kind,
+                       cut, d_bb);
+}
+
 void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
-                     int kind, hipStream_t s) {
+                     int kind, hipStream_t s, const double* d_bb) {
     const float4* p = (const float4*)d_pts4;
     const FModelD* m = (const FModelD*)d_models;
     const SampsonCut c = sampson_cut(thr2);
+    if (d_bb && kind <= 1 && f_variant() == 0) {   // Sampson: certified packed-fp32 prefilter
+        const SampsonPkCut cut = sampson_pk_cut_host(c);
+        static const int pkv = [] {
+            const char* e = getenv("MCV_F_PK");
+            return e ? atoi(e) : 0;
+        }();
+        switch (pkv) {
+            case 1: launch_f_verify_pk_kp<2, 2>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
+            case 2: launch_f_verify_pk_kp<3, 2>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
+            case 3: launch_f_verify_pk_kp<4, 2>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
+            case 4: launch_f_verify_pk_kp<3, 1>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
+            case 9: break;   // fp64 sweep
+            default: launch_f_verify_pk_kp<4, 1>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
+        }
+    }
     switch (f_variant()) {
         case 1: launch_f_verify_kp<4, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
         case 2: launch_f_verify_kp<6, 1>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;

@@ -319,8 +319,10 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
             launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, fused, P.bbox.p, s);
     } else {
         launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+        P.bb4.ensure(4);
+        launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         ProfScope ps("f_verify", s);
-        launch_f_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, f_error_kind(cfg), s);
+        launch_f_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, f_error_kind(cfg), s, P.bb4.p);
     }
     if (d_key) launch_best(d_counts, hypCount, hypBegin, model_points(P.model), P.pkey.p, P.pfail.p, d_key, s);
     MCV_HIP(hipGetLastError());

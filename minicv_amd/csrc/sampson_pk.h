@@ -1,0 +1,166 @@
+// sampson_pk.h — certified packed-fp32 prefilter of the fp64 Sampson inlier test (F and E sweeps).
+//
+// The reference decides inlier <=> (float)(c * c / den) <= thr2 with c, den evaluated in fp64
+// (f_err_sampson[_fused]). The sweep evaluates c and den in fp32 instead — two models per
+// v_pk_fma_f32, so 14 issue slots per (model, correspondence) against 22 for the fp64 test — and
+// decides every lane whose fp32 values are far enough from the threshold to make the fp64 answer
+// certain; the rest (a fraction ~1e-4 of evaluations) take the exact fp64 test.
+//
+// Error bound (u = 2^-24; inputs |x1| <= X1, |y1| <= Y1, |x2| <= X2, |y2| <= Y2 over the point set):
+//   Ax = |F0| X1 + |F1| Y1 + |F2|, Ay, Az likewise, Bx = |F0| X2 + |F3| Y2 + |F6|, By = |F1| X2 + ...,
+//   Mc = X2 Ax + Y2 Ay + Az, Dm = Ax^2 + Ay^2 + Bx^2 + By^2.
+// Rounding the model (and, for E, the points) to fp32 and the fma chain give |ax32 - ax| <= 6u Ax
+// and so on, |c32 - c| <= 10u Mc, |den32 - den| <= 16u Dm against the exact values, and the fp64
+// evaluation sits within 1e-15 of them. We use Ec = 16u Mc, Ed = 24u Dm. Then, with
+// L <= lo (1 - 2^-20) and H >= hi (1 + 2^-20) in fp32 (lo, hi: SampsonCut), and every remaining
+// fp32 rounding (< 2^-21 relative in total) inside that 2^-20 margin:
+//   (|c32| + Ec)^2 < den32 L - Ed L                 => c64^2 < den64 lo (1 - 2^-21)  => inlier
+//   max(|c32| - Ec, 0)^2 > den32 H + Ed H           => c64^2 > den64 hi (1 + 2^-21)  => outlier
+// (SampsonCut's argument: a quotient below mid (1 - 2^-50) rounds to <= thr2, above mid (1 + 2^-50)
+// to > thr2). The bound holds while every magnitude is a normal fp32 far from overflow: a model with
+// Mc or Dm outside [2^-90, 2^60] (or a non-finite bound) gets Ec = inf — every lane undecided.
+// NaN / inf values fail both compares and so also fall back to fp64.
+#pragma once
+
+#include "mcv_common.h"
+#include "hyp_fundamental.h"
+#include <cmath>
+
+namespace mcv {
+
+struct SampsonPkBound { double Ec, Ed; };
+
+MCV_HD SampsonPkBound sampson_pk_bound(const double* F, double X1, double Y1, double X2, double Y2) {
+    const double a0 = fabs(F[0]), a1 = fabs(F[1]), a2 = fabs(F[2]), a3 = fabs(F[3]), a4 = fabs(F[4]);
+    const double a5 = fabs(F[5]), a6 = fabs(F[6]), a7 = fabs(F[7]), a8 = fabs(F[8]);
+    const double Ax = a0 * X1 + a1 * Y1 + a2, Ay = a3 * X1 + a4 * Y1 + a5, Az = a6 * X1 + a7 * Y1 + a8;
+    const double Bx = a0 * X2 + a3 * Y2 + a6, By = a1 * X2 + a4 * Y2 + a7;
+    const double Mc = X2 * Ax + Y2 * Ay + Az;
+    const double Dm = Ax * Ax + Ay * Ay + Bx * Bx + By * By;
+    SampsonPkBound b;
+    const double u = 0x1p-24;
+    b.Ec = 16.0 * u * Mc * (1.0 + 0x1p-30);
+    b.Ed = 24.0 * u * Dm * (1.0 + 0x1p-30);
+    const bool ok = Mc >= 0x1p-90 && Mc <= 0x1p60 && Dm >= 0x1p-90 && Dm <= 0x1p60 && Ax <= 0x1p60 &&
+                    Ay <= 0x1p60 && Bx <= 0x1p60 && By <= 0x1p60;   // false for NaN too
+    if (!ok) b.Ec = b.Ed = __builtin_inf();
+    return b;
+}
+
+#if defined(__HIPCC__)
+typedef float sf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ sf2 spk_fma(sf2 a, sf2 b, sf2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ sf2 spk_lo(sf2 v) { return __builtin_shufflevector(v, v, 0, 0); }
+__device__ __forceinline__ sf2 spk_hi(sf2 v) { return __builtin_shufflevector(v, v, 1, 1); }
+
+// fp32 constants of the certified cut: L32 <= lo (1 - 2^-20), H32 >= hi (1 + 2^-20); the bound
+// products are taken against those fp32 values and rounded outward, so that
+// den32 L32 - Ed L32 <= den64 L32 and den32 H32 + Ed H32 >= den64 H32 hold exactly.
+struct SampsonPkCut { float L32, H32; };
+inline SampsonPkCut sampson_pk_cut_host(const SampsonCut& c) {
+    SampsonPkCut k;
+    k.L32 = -1.0f;   // lo <= 0: nothing certified inside
+    if (c.lo > 0) {
+        const double L = c.lo * (1.0 - 0x1p-20);
+        float f = (float)L;
+        if ((double)f > L) f = std::nextafter(f, 0.0f);
+        k.L32 = f;
+    }
+    const double H = c.hi * (1.0 + 0x1p-20);
+    float h = (float)H;
+    if ((double)h < H) h = std::nextafter(h, __builtin_inff());
+    k.H32 = h;
+    return k;
+}
+
+// Two models (one pair) in packed fp32, plus their bound terms: Ec, -Ed L32, Ed H32 (rounded up in
+// magnitude, so that the tests stay conservative).
+struct SampsonPkPair {
+    sf2 f[9];
+    sf2 ec, nedl, edh;
+};
+
+__device__ __forceinline__ float spk_f32_up(double v) { return __double2float_ru(v); }
+
+// Build one pair from two fp64 models (F row-major) and the point-set bounds bb = {X1, Y1, X2, Y2}.
+__device__ __forceinline__ void spk_make_pair(SampsonPkPair& P, const double* Fa, const double* Fb, const double* bb,
+                                              const SampsonPkCut& k) {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) P.f[j] = sf2{(float)Fa[j], (float)Fb[j]};
+    const SampsonPkBound ba = sampson_pk_bound(Fa, bb[0], bb[1], bb[2], bb[3]);
+    const SampsonPkBound bbn = sampson_pk_bound(Fb, bb[0], bb[1], bb[2], bb[3]);
+    const double L = k.L32 > 0 ? (double)k.L32 : 0.0;
+    P.ec = sf2{spk_f32_up(ba.Ec), spk_f32_up(bbn.Ec)};
+    P.nedl = sf2{-spk_f32_up(ba.Ed * L), -spk_f32_up(bbn.Ed * L)};
+    P.edh = sf2{spk_f32_up(ba.Ed * (double)k.H32), spk_f32_up(bbn.Ed * (double)k.H32)};
+}
+
+// One correspondence (p01 = {x1, y1}, p23 = {x2, y2}) against one model pair: lane masks of the
+// certified inliers and of the undecided lanes, for model 2k (lo) and 2k + 1 (hi).
+__device__ __forceinline__ void spk_test(const SampsonPkPair& P, sf2 p01, sf2 p23, float L32, float H32,
+                                         uint64_t& in0, uint64_t& in1, uint64_t& amb0, uint64_t& amb1) {
+    const sf2 x1 = spk_lo(p01), y1 = spk_hi(p01), x2 = spk_lo(p23), y2 = spk_hi(p23);
+    const sf2 ax = spk_fma(P.f[0], x1, spk_fma(P.f[1], y1, P.f[2]));
+    const sf2 ay = spk_fma(P.f[3], x1, spk_fma(P.f[4], y1, P.f[5]));
+    const sf2 az = spk_fma(P.f[6], x1, spk_fma(P.f[7], y1, P.f[8]));
+    const sf2 bx = spk_fma(P.f[0], x2, spk_fma(P.f[3], y2, P.f[6]));
+    const sf2 by = spk_fma(P.f[1], x2, spk_fma(P.f[4], y2, P.f[7]));
+    const sf2 c = spk_fma(x2, ax, spk_fma(y2, ay, az));
+    const sf2 den = spk_fma(ax, ax, spk_fma(ay, ay, spk_fma(bx, bx, by * by)));
+    const sf2 ac = __builtin_elementwise_max(c, -c);
+    const sf2 b = ac + P.ec;
+    const sf2 b2 = b * b;
+    const sf2 r = spk_fma(den, sf2{L32, L32}, P.nedl);
+    const sf2 a = __builtin_elementwise_max(ac - P.ec, sf2{0.0f, 0.0f});
+    const sf2 a2 = a * a;
+    const sf2 q = spk_fma(den, sf2{H32, H32}, P.edh);
+    const uint64_t i0 = __builtin_amdgcn_ballot_w64(b2.x < r.x);
+    const uint64_t i1 = __builtin_amdgcn_ballot_w64(b2.y < r.y);
+    const uint64_t o0 = __builtin_amdgcn_ballot_w64(a2.x > q.x);
+    const uint64_t o1 = __builtin_amdgcn_ballot_w64(a2.y > q.y);
+    in0 = i0;
+    in1 = i1;
+    amb0 = ~(i0 | o0);
+    amb1 = ~(i1 | o1);
+}
+
+
+// One sweep step of KP model pairs at one correspondence per lane (v: lane holds a point):
+// certified inliers counted, undecided lanes re-tested in fp64 (f_error, kind 0/1) in one
+// wave-uniform branch. F64 fetches model k's fp64 coefficients (global memory; the fallback is
+// rare, so they are not kept in registers); X64 the lane's fp64 point.
+template <int KP, class F64, class X64>
+__device__ __forceinline__ void spk_sweep_point(const SampsonPkPair (&pr)[KP], float4 q, bool v, float L32, float H32,
+                                                int kind, float thr2, const F64& f64, const X64& x64,
+                                                uint32_t (&cnt)[2 * KP]) {
+    const uint64_t vm = __builtin_amdgcn_ballot_w64(v);
+    const sf2 p01 = sf2{q.x, q.y}, p23 = sf2{q.z, q.w};
+    uint64_t inm[2 * KP], amb[2 * KP], anyAmb = 0;
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+        uint64_t i0, i1, a0, a1;
+        spk_test(pr[kp], p01, p23, L32, H32, i0, i1, a0, a1);
+        inm[2 * kp] = vm & i0;
+        inm[2 * kp + 1] = vm & i1;
+        amb[2 * kp] = vm & a0;
+        amb[2 * kp + 1] = vm & a1;
+        anyAmb |= amb[2 * kp] | amb[2 * kp + 1];
+    }
+    if (__builtin_expect(anyAmb != 0, 0)) {
+        const uint64_t me = 1ull << (__lane_id() & 63);
+        double x1, y1, x2, y2;
+        x64(x1, y1, x2, y2);
+#pragma unroll
+        for (int k = 0; k < 2 * KP; ++k) {
+            if (amb[k] == 0) continue;
+            double F[9];
+            f64(k, F);
+            inm[k] |= __builtin_amdgcn_ballot_w64((amb[k] & me) != 0 && f_error(kind, F, x1, y1, x2, y2) <= thr2);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 2 * KP; ++k) cnt[k] += (uint32_t)__popcll(inm[k]);
+}
+#endif
+
+}  // namespace mcv

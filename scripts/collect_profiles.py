@@ -82,7 +82,7 @@ def main():
         elif w == "essential":
             models = (j or {}).get("roofline", {}).get("models_per_launch", 0)
             config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
-                32.0 * c.get("correspondences", 0) * models
+                16.0 * c.get("correspondences", 0) * models
         elif w == "pnp":
             config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
                 20.0 * c.get("correspondences", 0) * c.get("hypotheses_total", 0)

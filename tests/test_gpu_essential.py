@@ -205,3 +205,31 @@ def test_e_counts_at_exact_threshold_boundary(torch_dev, oracle):
             if unfused:
                 assert ref[0] == int((err <= target).sum())
     plan.close()
+
+
+@pytest.mark.parametrize("case", ["nan", "wide_thr"])
+def test_e_counts_prefilter_extremes(torch_dev, oracle, case):
+    """E sweep through the packed-fp32 prefilter: a NaN coordinate (no certification at all) and a
+    threshold wide enough to put many correspondences near the cut; bit-exact against the oracle."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    n, count, seed = 1200, 128, 23
+    a, b, *_ = S.essential_problem(n, seed=seed, outlier_frac=0.4)
+    a, b = a.copy(), b.copy()
+    thr = 1.0 / FOCAL
+    if case == "nan":
+        b[7, 1] = np.nan
+    else:
+        thr = 20.0 / FOCAL
+    pts = D.pack_essential_tensor(a, b, FOCAL, PP, dev)
+    ref_pts = oracle.pack_e(a, b, FOCAL, PP)
+    plan = D.RansacPlan(N.MODEL_ESSENTIAL, n, count)
+    for unfused in (False, True):
+        cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+        key = torch.zeros(2, dtype=torch.int64, device=dev)
+        counts = torch.zeros(count * N.E_SLOTS, dtype=torch.int32, device=dev)
+        plan.evaluate(pts, n, cfg, 0, count, key, counts)
+        ref = oracle.e_counts(ref_pts, seed, 0, count, float(np.float32(thr * thr)), 1 if unfused else 0)
+        np.testing.assert_array_equal(counts.cpu().numpy(), ref)
+        assert (ref > 0).any()
+    plan.close()

@@ -149,3 +149,40 @@ def test_f_counts_at_exact_threshold_boundary(torch_dev, oracle, unfused):
         if unfused:
             assert ref[0] == int((err <= target).sum())
     plan.close()
+
+
+@pytest.mark.parametrize("case", ["nan", "huge", "tiny", "wide_thr"])
+def test_f_counts_prefilter_extremes(torch_dev, oracle, case):
+    """The packed-fp32 prefilter (sampson_pk.h) against the fp64 oracle where its bound must give
+    up: a NaN coordinate (bound -> inf: every lane re-tested in fp64), a 1e30 coordinate (bound out
+    of range), a point set scaled by 1e-30 (magnitudes below the bound's range), and a threshold
+    wide enough to put many correspondences near the cut."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    n, count, seed = 1500, 256, 21
+    a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=0.4)
+    a, b = a.copy(), b.copy()
+    thr = 5e-3
+    if case == "nan":
+        a[10, 0] = np.nan
+    elif case == "huge":
+        b[20, 0] = 1e30
+    elif case == "tiny":
+        a *= 1e-30
+        b *= 1e-30
+        thr = 5e-33
+    else:
+        thr = 0.5
+    pts = D.pack_points_tensor(a, b, dev)
+    plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, n, count)
+    for unfused in (False, True):
+        cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+        key = torch.zeros(2, dtype=torch.int64, device=dev)
+        counts = torch.zeros(count, dtype=torch.int32, device=dev)
+        plan.evaluate(pts, n, cfg, 0, count, key, counts)
+        ref = oracle.f_counts(oracle.pack4(a, b), seed, 0, count, float(np.float32(thr * thr)),
+                              oracle.f_kind(0, unfused))
+        np.testing.assert_array_equal(counts.cpu().numpy(), ref)
+        # (tiny: the 8-point sampler's absolute degeneracy tests reject every sample — parity only)
+        assert case == "tiny" or (ref > 0).any()
+    plan.close()
