@@ -21,6 +21,8 @@ struct HOneOut {
     int idx[4];
 };
 void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOut* d_out, hipStream_t s);
+void launch_h_mask_one(const float* d_pts4, int N, const HOneOut* d_one, float thr2, bool fused, uint8_t* d_mask,
+                       int* d_count, hipStream_t s);
 void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
                        int* d_counts, hipStream_t s);
 void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
@@ -33,6 +35,7 @@ bool launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, con
 void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, bool fused, uint8_t* d_mask,
                    int* d_count, hipStream_t s);
 void h_reduce_sums(const float* d_pts4, int N, const uint8_t* d_mask, double* d_part, double* d_out, hipStream_t s);
+void h_refit_chain(const float* d_pts4, int N, const uint8_t* d_mask, double* d_part, double* d_red, hipStream_t s);
 void h_reduce_absdev(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, double* d_part,
                      double* d_out, hipStream_t s);
 void h_reduce_ltl(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,

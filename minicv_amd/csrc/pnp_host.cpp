@@ -179,12 +179,17 @@ void pnp_lm(Plan& P, const void* d_pts, int N, const uint8_t* d_mask, double* rv
             dn = std::max(dn, std::fabs(d[k]));
             pn = std::max(pn, std::fabs(p[k]));
         }
-        const double Sq = eval(q, false, nullptr, nullptr);
+        // the normal equations at q ride along with its cost (one synchronisation per step); on
+        // acceptance they equal the re-evaluation at the new p (same sums, same order)
+        double Aq[36], gq[6];
+        const double Sq = eval(q, true, Aq, gq);
         if (Sq < S) {
             const bool stall = (S - Sq) <= FLT_EPSILON * S;
             for (int k = 0; k < 6; ++k) p[k] = q[k];
             lambda = std::max(lambda * 0.1, 1e-12);
-            S = eval(p, true, A, g);
+            S = Sq;
+            std::memcpy(A, Aq, sizeof(Aq));
+            std::memcpy(g, gq, sizeof(gq));
             if (stall || dn <= FLT_EPSILON * (pn + FLT_EPSILON)) break;
         } else {
             lambda *= 10;

@@ -485,6 +485,25 @@ __global__ __launch_bounds__(256) void mcv_h_mask(const float4* __restrict__ pts
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (int)__popcll(b));
 }
 
+// The same, with the model read from the winner record mcv_h_one wrote (no host round trip).
+__global__ __launch_bounds__(256) void mcv_h_mask_one(const float4* __restrict__ pts, int N,
+                                                      const HOneOut* __restrict__ one, float thr2, int fused,
+                                                      uint8_t* __restrict__ mask, int* __restrict__ count) {
+    HModelF m;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m.h[j] = one->hf[j];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool in = false;
+    if (i < N) {
+        const float4 q = pts[i];
+        const float e = fused ? h_error_fused(m.h, q.x, q.y, q.z, q.w) : h_error(m.h, q.x, q.y, q.z, q.w);
+        in = e <= thr2;
+        mask[i] = in ? 1 : 0;
+    }
+    const uint64_t b = __ballot(in);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (int)__popcll(b));
+}
+
 __global__ void mcv_fill_u8(uint8_t* __restrict__ p, int n, uint8_t v) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) p[i] = v;
@@ -509,6 +528,15 @@ struct OpAbsDev {  // 4: sum |dst - cm|, |src - cM|
         const float4 q = pts[i];
         a[0] += fabs((double)q.z - cmx); a[1] += fabs((double)q.w - cmy);
         a[2] += fabs((double)q.x - cMx); a[3] += fabs((double)q.y - cMy);
+    }
+};
+struct OpAbsDevD {  // OpAbsDev with the centroids read from device memory (chained refit)
+    const float4* pts; const uint8_t* mask; const double* c4;
+    __device__ void operator()(int i, double (&a)[4]) const {
+        if (mask && !mask[i]) return;
+        const float4 q = pts[i];
+        a[0] += fabs((double)q.z - c4[0]); a[1] += fabs((double)q.w - c4[1]);
+        a[2] += fabs((double)q.x - c4[2]); a[3] += fabs((double)q.y - c4[3]);
     }
 };
 struct OpLtL {     // 45: upper triangle of LtL, row-major
@@ -687,6 +715,12 @@ void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, boo
                        fused ? 1 : 0, d_mask, d_count);
 }
 
+void launch_h_mask_one(const float* d_pts4, int N, const HOneOut* d_one, float thr2, bool fused, uint8_t* d_mask,
+                       int* d_count, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_h_mask_one, dim3((N + 255) / 256), dim3(256), 0, s, (const float4*)d_pts4, N, d_one, thr2,
+                       fused ? 1 : 0, d_mask, d_count);
+}
+
 void launch_fill_u8(uint8_t* d, int n, uint8_t v, hipStream_t s) {
     hipLaunchKernelGGL(mcv_fill_u8, dim3((n + 255) / 256), dim3(256), 0, s, d, n, v);
 }
@@ -705,6 +739,35 @@ void h_reduce_ltl(const float* d_pts4, int N, const uint8_t* d_mask, const doubl
     OpLtL op{(const float4*)d_pts4, d_mask, c4[0], c4[1], c4[2], c4[3], s4[0], s4[1], s4[2], s4[3]};
     run_reduce<45>(N, op, d_part, d_out, s);
 }
+struct OpLtLD {    // OpLtL with centroids / scales read from device memory (chained refit)
+    const float4* pts; const uint8_t* mask; const double* c4; const double* s4;
+    __device__ void operator()(int i, double (&a)[45]) const {
+        OpLtL op{pts, mask, c4[0], c4[1], c4[2], c4[3], s4[0], s4[1], s4[2], s4[3]};
+        op(i, a);
+    }
+};
+
+// refit statistics between the chained passes: c4 = sums / count, s4 = count / absdev (the same
+// IEEE divisions the host performs, so the passes see bit-identical constants)
+__global__ void mcv_refit_stats(double* __restrict__ red, int stage) {
+    if (threadIdx.x >= 4) return;
+    const int k = threadIdx.x;
+    if (stage == 0) red[5 + k] = red[k] / red[4];
+    else red[13 + k] = red[4] / red[9 + k];
+}
+
+// HomographyEstimatorCallback::runKernel's three passes chained on the device (no host round trip):
+// red[0..4] = sums, red[5..8] = centroids, red[9..12] = |dev| sums, red[13..16] = scales,
+// red[17..61] = LtL.
+void h_refit_chain(const float* d_pts4, int N, const uint8_t* d_mask, double* d_part, double* d_red, hipStream_t s) {
+    const float4* p = (const float4*)d_pts4;
+    run_reduce<5>(N, OpSums{p, d_mask}, d_part, d_red, s);
+    hipLaunchKernelGGL(mcv_refit_stats, dim3(1), dim3(64), 0, s, d_red, 0);
+    run_reduce<4>(N, OpAbsDevD{p, d_mask, d_red + 5}, d_part, d_red + 9, s);
+    hipLaunchKernelGGL(mcv_refit_stats, dim3(1), dim3(64), 0, s, d_red, 1);
+    run_reduce<45>(N, OpLtLD{p, d_mask, d_red + 5, d_red + 13}, d_part, d_red + 17, s);
+}
+
 void h_reduce_lm(const float* d_pts4, int N, const uint8_t* d_mask, const double* h8, bool wantJ, double* d_part,
                  double* d_out, hipStream_t s) {
     if (wantJ) {

@@ -184,18 +184,19 @@ bool fused_error(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_UNFUSED
 
 // HomographyEstimatorCallback::runKernel over the masked correspondences (mask == NULL: all).
 bool h_refit(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipStream_t s, double* H) {
-    double sums[5];
-    reduce_to_host(P, s, 5, sums, [&](double* part, double* red) { h_reduce_sums(d_pts, N, d_mask, part, red, s); });
+    // the three passes (sums -> centroids -> |deviations| -> scales -> LtL) chained on the device,
+    // one read-back; the host re-derives c4 / s4 with the same divisions and checks them
+    double r[62];
+    reduce_to_host(P, s, 62, r, [&](double* part, double* red) { h_refit_chain(d_pts, N, d_mask, part, red, s); });
+    const double* sums = r;
     const double count = sums[4];
     if (count <= 0) return false;
     double c4[4] = {sums[0] / count, sums[1] / count, sums[2] / count, sums[3] / count};   // cm.x, cm.y, cM.x, cM.y
-    double dev[4];
-    reduce_to_host(P, s, 4, dev, [&](double* part, double* red) { h_reduce_absdev(d_pts, N, d_mask, c4, part, red, s); });
+    const double* dev = r + 9;
     for (int k = 0; k < 4; ++k)
         if (std::fabs(dev[k]) < DBL_EPSILON) return false;
     double s4[4] = {count / dev[0], count / dev[1], count / dev[2], count / dev[3]};   // sm.x, sm.y, sM.x, sM.y
-    double ltl[45];
-    reduce_to_host(P, s, 45, ltl, [&](double* part, double* red) { h_reduce_ltl(d_pts, N, d_mask, c4, s4, part, red, s); });
+    const double* ltl = r + 17;
     double A[81], w[9], V[81];
     int o = 0;
     for (int j = 0; j < 9; ++j)
@@ -246,7 +247,11 @@ void h_lm_refine(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipS
         for (int i = 0; i < lx; ++i) Ap[i * lx + i] += lambda * D[i];
         eig_solve(Ap, lx, v, d);
         for (int i = 0; i < lx; ++i) xd[i] = x[i] - d[i];
-        const double Sd = compute(xd, false, nullptr, nullptr);
+        // JtJ / Jtr at xd ride along with its cost (one synchronisation per step): on acceptance they
+        // are exactly what LMSolverImpl's re-evaluation at the new x returns (same sums, same order;
+        // the cost is summed identically by OpLM and OpLMErr)
+        double Ad[64], vd[8];
+        const double Sd = compute(xd, true, Ad, vd);
         for (int i = 0; i < lx; ++i) {   // temp_d = -A d + 2 v
             double acc = 0;
             for (int k = 0; k < lx; ++k) acc += A[i * lx + k] * d[k];
@@ -275,7 +280,8 @@ void h_lm_refine(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipS
         if (Sd < S) {
             S = Sd;
             for (int i = 0; i < lx; ++i) x[i] = xd[i];
-            S = compute(x, true, A, v);
+            std::memcpy(A, Ad, sizeof(Ad));
+            std::memcpy(v, vd, sizeof(vd));
         }
         ++iter;
         double dn = 0;
@@ -336,19 +342,18 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
                hipStream_t s) {
     const double t = effective_threshold(cfg);
     const float thr2 = (float)(t * t);
+    // winner re-solve -> mask from the device-side record -> one read-back of both
     HOneOut* d_one = (HOneOut*)P.one.p;
     launch_h_one(d_pts, N, cfg.seed, hyp, d_one, s);
+    MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
+    launch_h_mask_one(d_pts, N, d_one, thr2, fused_error(cfg), d_mask, P.count.p, s);
     MCV_HIP(hipGetLastError());
     HOneOut one;
     MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(HOneOut), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
     MCV_HIP(hipStreamSynchronize(s));
     std::memcpy(&one, P.h_one.p, sizeof(HOneOut));
     if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
-    MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
-    launch_h_mask(d_pts, N, one.hf, thr2, fused_error(cfg), d_mask, P.count.p, s);
-    MCV_HIP(hipGetLastError());
-    MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    MCV_HIP(hipStreamSynchronize(s));
     const int count = P.h_i.p[0];
     for (int k = 0; k < 9; ++k) H[k] = one.H[k];
     if (cfg.flags & MCV_FLAG_NO_REFINE) return count;
