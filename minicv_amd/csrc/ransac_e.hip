@@ -2,11 +2,12 @@
 // (reference MiniCVNative.cpp:165-215, fivepoint.cpp:233-339).
 //
 //   mcv_e_pack          V2d pairs -> double4 normalised camera coordinates (x - cx) / f.
-//   mcv_e_generate_wave one wave per hypothesis: Philox sample of 5 -> five-point solve (fp64, up to
-//                       10 models; five_point_wave.h spreads each step over the 64 lanes with the
-//                       working matrices in LDS) -> all 10 slot statuses + models appended to a
-//                       dense list (atomic slot allocation; results are keyed by slot, so the order
-//                       of the dense list never reaches an output).
+//   mcv_e_generate_wave<G> one G-lane group per hypothesis (4 per wave at G = 16): Philox sample of
+//                       5 -> five-point solve (fp64, up to 10 models; five_point_wave.h spreads each
+//                       step over the group's lanes with the working matrices in LDS) -> all 10
+//                       slot statuses + models appended to a dense list (atomic slot allocation;
+//                       results are keyed by slot, so the order of the dense list never reaches an
+//                       output). mcv_e_stage + mcv_e_roots: the split form for large chunks.
 //   mcv_e_generate      the same, one lane per hypothesis running e_solve5 (MCV_E_GEN=1; kept for
 //                       the A/B screen).
 //   mcv_e_verify<K,P,E> inlier sweep over the dense model list: wave = K models in VGPRs, 64
@@ -16,7 +17,7 @@
 //                       over a float4 copy of the points; undecided lanes re-tested in fp64.
 //   mcv_e_one           recompute one hypothesis (winner) -> all its models (one wave).
 //   mcv_e_mask          inlier mask of the winner.
-//   mcv_e_cheirality    recoverPose: per RANSAC inlier, the 4 (R, t) candidates' cheirality tests.
+//   mcv_e_cheirality    recoverPose: one lane per (RANSAC inlier, (R, t) candidate) cheirality test.
 //   mcv_e_fivepoint     cvFivePoint: one five-point solve on raw coordinates (one wave).
 #include "mcv_common.h"
 #include "hyp_essential.h"
@@ -320,15 +321,22 @@ struct EPoseCands { double P[4][12]; };
 __global__ __launch_bounds__(256) void mcv_e_cheirality(const double4* __restrict__ pts, int N,
                                                         const uint8_t* __restrict__ mask, EPoseCands c, double dist,
                                                         int* __restrict__ good4) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    // one lane per (correspondence, candidate): the four 4x4 Jacobi solves of a correspondence run
+    // side by side instead of one after another (this kernel is on cvRecoverPose's latency path)
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int i = t >> 2, k = t & 3;
     const bool act = i < N && (!mask || mask[i]);
     double4 q = {0, 0, 0, 0};
     if (act) q = pts[i];
+    double P[12];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const bool g = act && e_cheirality(c.P[k], q.x, q.y, q.z, q.w, dist);
-        const uint64_t b = __ballot(g);
-        if ((threadIdx.x & 63) == 0 && b) atomicAdd(good4 + k, (int)__popcll(b));
+    for (int j = 0; j < 12; ++j)
+        P[j] = k == 0 ? c.P[0][j] : (k == 1 ? c.P[1][j] : (k == 2 ? c.P[2][j] : c.P[3][j]));
+    const bool g = e_cheirality(P, q.x, q.y, q.z, q.w, dist) && act;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        const uint64_t b = __ballot(g && k == kk);
+        if ((threadIdx.x & 63) == 0 && b) atomicAdd(good4 + kk, (int)__popcll(b));
     }
 }
 
@@ -476,8 +484,8 @@ void launch_e_cheirality(const double* d_pts4, int N, const uint8_t* d_mask, con
     for (int k = 0; k < 4; ++k)
         for (int j = 0; j < 12; ++j) c.P[k][j] = P4x12[12 * k + j];
     (void)hipMemsetAsync(d_good4, 0, 4 * sizeof(int), s);
-    hipLaunchKernelGGL(mcv_e_cheirality, dim3((N + 255) / 256), dim3(256), 0, s, (const double4*)d_pts4, N, d_mask,
-                       c, dist, d_good4);
+    hipLaunchKernelGGL(mcv_e_cheirality, dim3((4 * (int64_t)N + 255) / 256), dim3(256), 0, s, (const double4*)d_pts4,
+                       N, d_mask, c, dist, d_good4);
 }
 
 void launch_e_fivepoint(const EFiveIn& in, EOneOut* d_out, hipStream_t s) {
