@@ -502,10 +502,11 @@ __device__ __forceinline__ int ew_hypothesis(EWave& S, const EGroup<G>& g, const
     return kStatusNoSample;
 }
 
-// ---- split path: the matrix phases per group, the root finder per lane ---------------------------
+// ---- split path: the matrix phases per 16-lane group, the root finder on fewer lanes -------------
 // With many hypotheses in flight the root finder (~400 Illinois steps on the critical path of
-// one solve, a few active lanes per group) dominates; one lane per hypothesis runs it at full
-// lane occupancy instead, with its root lists in LDS columns (no scratch).
+// one solve, a few active lanes per 16-lane group) dominates; the split path runs it on a small
+// lane group per hypothesis (ew_group_roots, below; the default) or on one lane (ew_lane_roots),
+// with the matrix phases' results (EStage) handed over through HBM.
 
 // Matrix phases of hypothesis `hyp` -> EStage (lanes of the group share the writes).
 template <int G>
@@ -617,6 +618,93 @@ __device__ __forceinline__ int ew_lane_roots(const double* cin, double (*Lc)[64]
         cur ^= 1;
     }
     *which = cur;
+    return np;
+}
+
+
+// ---- split path, root finder over a small lane group (GR = 4 or 8 lanes per hypothesis) ----------
+// One hypothesis per GR lanes: each level's intervals are dealt round-robin to the group's lanes
+// (lane sub brackets s = sub, sub + GR, ...), so a level costs the longest per-lane sum of
+// Illinois runs rather than the sum over all intervals, and 64 / GR hypotheses share a wave. The
+// kept-root list is rebuilt by the group's first lane in interval order (the serial rule).
+struct ERootLds {
+    double c[11];
+    double rp[10];
+    double val[11], b[11];
+    int type[11];
+    int np;
+};
+
+template <int D, int GR>
+__device__ __forceinline__ int ew_group_level(ERootLds& S, int sub, int j, int np, double R) {
+    EPolyD<D> P;
+#pragma unroll
+    for (int k = 0; k <= D; ++k) P.q[k] = S.c[k + j] * e_falling(k + j, j);
+    for (int s = sub; s <= np; s += GR) {
+        const double a = s == 0 ? -R : S.rp[s - 1];
+        const double b = s < np ? S.rp[s] : R;
+        const double fa = P(a), fb = P(b);
+        int type = 0;
+        double val = 0.0;
+        if (fb == 0) {
+            type = 1;
+            val = b;
+        } else if (fa != 0 && ((fa < 0) != (fb < 0))) {
+            type = 2;
+            val = e_root_bracketed_f(P, a, b, fa, fb);
+        }
+        S.type[s] = type;
+        S.val[s] = val;
+        S.b[s] = b;
+    }
+    ew_sync();
+    if (sub == 0) {
+        int nc = 0;
+        for (int s = 0; s <= np; ++s) {
+            const int t = S.type[s];
+            if (t == 1) {
+                if (nc == 0 || S.rp[nc - 1] != S.b[s]) S.rp[nc++] = S.b[s];
+            } else if (t == 2) {
+                S.rp[nc++] = S.val[s];
+            }
+        }
+        S.np = nc;
+    }
+    ew_sync();
+    return S.np;
+}
+
+// e_poly_real_roots of cin for one group; the roots end in S.rp (count returned).
+template <int GR>
+__device__ __forceinline__ int ew_group_roots(ERootLds& S, const double* cin, int sub) {
+    int n = 10;
+    while (n > 0 && cin[n] == 0) --n;
+    if (n < 1) return 0;
+    const double lead = cin[n];
+    for (int k = sub; k <= n; k += GR) S.c[k] = cin[k] / lead;
+    ew_sync();
+    double R = 0;
+    for (int k = 0; k < n; ++k) {
+        const double a = fabs(S.c[k]);
+        R = a > R ? a : R;
+    }
+    R = 1.0 + R;
+    if (!isfinite(R)) return 0;
+    int np = 0;
+    for (int j = n - 1; j >= 0; --j) {
+        switch (n - j) {
+            case 1: np = ew_group_level<1, GR>(S, sub, j, np, R); break;
+            case 2: np = ew_group_level<2, GR>(S, sub, j, np, R); break;
+            case 3: np = ew_group_level<3, GR>(S, sub, j, np, R); break;
+            case 4: np = ew_group_level<4, GR>(S, sub, j, np, R); break;
+            case 5: np = ew_group_level<5, GR>(S, sub, j, np, R); break;
+            case 6: np = ew_group_level<6, GR>(S, sub, j, np, R); break;
+            case 7: np = ew_group_level<7, GR>(S, sub, j, np, R); break;
+            case 8: np = ew_group_level<8, GR>(S, sub, j, np, R); break;
+            case 9: np = ew_group_level<9, GR>(S, sub, j, np, R); break;
+            default: np = ew_group_level<10, GR>(S, sub, j, np, R); break;
+        }
+    }
     return np;
 }
 

@@ -83,8 +83,9 @@ struct EStage {
     double det[11];
     int status, pad;
 };
-static const int kEStageMinHyps = 49152;   // hypCount from which generate takes the split path
+static const int kEStageMinHyps = 32768;   // hypCount from which generate takes the split path
 static const int kEStageLanes = 16;        // lanes per hypothesis of its matrix phases
+static const int kERootLanes = 4;          // lanes per hypothesis of its root finder (1: one lane)
 void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, double* d_pts4, hipStream_t s);
 void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_dense,
                        int* d_denseSlot, int* d_nDense, int* d_counts, void* d_stage, hipStream_t s);

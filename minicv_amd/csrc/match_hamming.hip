@@ -204,6 +204,8 @@ __global__ __launch_bounds__(256) void mcv_hamming_merge(const uint2* __restrict
     const int qi = blockIdx.x * 256 + threadIdx.x;
     if (qi >= nq) return;
     uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
+    // unrolled so that several partials are in flight per lane (the merge is load-latency-bound)
+#pragma unroll 8
     for (int c = 0; c < nchunks; ++c) {
         const uint2 p = part[(size_t)c * nq + qi];
         m2 = min(m2, max(m1, p.x));

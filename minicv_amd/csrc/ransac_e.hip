@@ -149,6 +149,52 @@ __global__ __launch_bounds__(64) void mcv_e_roots(const EStage* __restrict__ st,
     }
 }
 
+// Split path, part 2 (default): GR lanes per hypothesis — the derivative levels' intervals dealt
+// over the group (ew_group_roots), models by root over the group's lanes, statuses + dense append.
+template <int GR>
+__global__ __launch_bounds__(64) void mcv_e_roots_g(const EStage* __restrict__ st, int hypCount,
+                                                    EModel* __restrict__ dense, int* __restrict__ denseSlot,
+                                                    int* __restrict__ nDense, int* __restrict__ counts) {
+    __shared__ ERootLds L[64 / GR];
+    __shared__ int okAll[64 / GR][kEMaxModels];
+    const int sub = threadIdx.x & (GR - 1), grp = threadIdx.x / GR;
+    const int i = blockIdx.x * (64 / GR) + grp;
+    if (i >= hypCount) return;
+    ERootLds& S = L[grp];
+    const EStage* h = st + i;
+    const int status = h->status;
+    const int nr = status == 1 ? ew_group_roots<GR>(S, h->det, sub) : 0;
+    double E[kEMaxModels / GR + 1][9];
+    bool ok[kEMaxModels / GR + 1];
+#pragma unroll
+    for (int u = 0; u <= kEMaxModels / GR; ++u) {
+        const int r = sub + GR * u;
+        ok[u] = r < nr && e_model_at(h->bx, h->by, h->bc, h->nb[0], h->nb[1], h->nb[2], h->nb[3], S.rp[r], E[u]);
+        if (r < kEMaxModels) okAll[grp][r] = ok[u] ? 1 : 0;
+    }
+    ew_sync();
+    int m = 0;
+    for (int r = 0; r < nr; ++r) m += okAll[grp][r];
+    for (int s = sub; s < kEMaxModels; s += GR)
+        counts[(int64_t)i * kEMaxModels + s] =
+            s < m ? 0 : (s == 0 && status == kStatusNoSample ? kStatusNoSample : kStatusNoModel);
+    int base = 0;
+    if (sub == 0 && m > 0) base = atomicAdd(nDense, m);
+    base = __shfl(base, grp * GR);
+#pragma unroll
+    for (int u = 0; u <= kEMaxModels / GR; ++u) {
+        const int r = sub + GR * u;
+        if (!ok[u]) continue;
+        int pos = 0;
+        for (int t = 0; t < r; ++t) pos += okAll[grp][t];
+        EModel em;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) em.e[k] = E[u][k];
+        dense[base + pos] = em;
+        denseSlot[base + pos] = i * kEMaxModels + pos;
+    }
+}
+
 template <int K, int P, int KIND>
 __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ pts, int N,
                                                     const EModel* __restrict__ dense,
@@ -374,8 +420,19 @@ void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBe
         EStage* st = (EStage*)d_stage;
         hipLaunchKernelGGL(mcv_e_stage<kEStageLanes>, dim3((hypCount + 64 / kEStageLanes - 1) / (64 / kEStageLanes)),
                            dim3(64), 0, s, d_pts4, N, seed, hypBegin, hypCount, st);
-        hipLaunchKernelGGL(mcv_e_roots, dim3((hypCount + 63) / 64), dim3(64), 0, s, st, hypCount, (EModel*)d_dense,
-                           d_denseSlot, d_nDense, d_counts);
+        static const int rootLanes = [] {
+            const char* e = getenv("MCV_E_ROOTS");
+            return e ? atoi(e) : kERootLanes;
+        }();
+        if (rootLanes == 1)
+            hipLaunchKernelGGL(mcv_e_roots, dim3((hypCount + 63) / 64), dim3(64), 0, s, st, hypCount,
+                               (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+        else if (rootLanes == 8)
+            hipLaunchKernelGGL(mcv_e_roots_g<8>, dim3((hypCount + 7) / 8), dim3(64), 0, s, st, hypCount,
+                               (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+        else
+            hipLaunchKernelGGL(mcv_e_roots_g<4>, dim3((hypCount + 15) / 16), dim3(64), 0, s, st, hypCount,
+                               (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
         return;
     }
     switch (group) {

@@ -46,9 +46,10 @@ def test_five_point_exact_geometry(gpu):
 @pytest.mark.parametrize("n,outl,seed,begin,count,unfused", [
     (5, 0.0, 1, 0, 64, False), (6, 0.3, 2, 0, 100, False), (300, 0.5, 3, 0, 512, False),
     (2000, 0.5, 4, 123457, 512, False), (1999, 0.6, 5, 0, 256, True), (64, 0.2, 6, 2**28, 300, False),
-    (1000, 0.5, 11, 5, 33000, True),
-    # >= kEStageMinHyps hypotheses per chunk: the split path (matrix phases per lane group, roots per lane)
-    (300, 0.5, 8, 77, 50000, False), (5, 0.0, 10, 0, 49152, False)])
+    (1000, 0.5, 11, 5, 20000, True),
+    # >= kEStageMinHyps hypotheses per chunk: the split path (matrix phases per 16-lane group, roots
+    # per 4-lane group)
+    (1000, 0.5, 12, 5, 33000, True), (300, 0.5, 8, 77, 50000, False), (5, 0.0, 10, 0, 32768, False)])
 def test_e_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, unfused):
     torch, dev = torch_dev
     from minicv_amd import device as D
