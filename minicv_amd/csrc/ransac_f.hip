@@ -114,11 +114,18 @@ __global__ __launch_bounds__(256) void mcv_abs_bound4(const T4* __restrict__ pts
         m2 = fmax(m2, __shfl_xor(m2, off, 64));
         m3 = fmax(m3, __shfl_xor(m3, off, 64));
     }
+    // block maximum first: one atomic per block and coordinate (per-wave atomics on 4 addresses
+    // serialised to ~190 us at 500k points)
+    __shared__ double sm[4][4];
+    const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        atomicMax(bb + 0, (unsigned long long)__double_as_longlong(m0));
-        atomicMax(bb + 1, (unsigned long long)__double_as_longlong(m1));
-        atomicMax(bb + 2, (unsigned long long)__double_as_longlong(m2));
-        atomicMax(bb + 3, (unsigned long long)__double_as_longlong(m3));
+        sm[wv][0] = m0; sm[wv][1] = m1; sm[wv][2] = m2; sm[wv][3] = m3;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const int c = threadIdx.x;
+        const double m = fmax(fmax(sm[0][c], sm[1][c]), fmax(sm[2][c], sm[3][c]));
+        atomicMax(bb + c, (unsigned long long)__double_as_longlong(m));
     }
 }
 
@@ -190,17 +197,26 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
     }
 }
 
+// Grid-stride, one count atomic per block (per-wave atomics on the one counter serialised to
+// ~90 us at 500k correspondences).
 __global__ __launch_bounds__(256) void mcv_f_mask(const float4* __restrict__ pts, int N, FModelD m, float thr2,
                                                   int kind, uint8_t* __restrict__ mask, int* __restrict__ count) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    bool in = false;
-    if (i < N) {
+    int c = 0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
         const float4 q = pts[i];
-        in = f_error(kind, m.f, q.x, q.y, q.z, q.w) <= thr2;
+        const bool in = f_error(kind, m.f, q.x, q.y, q.z, q.w) <= thr2;
         mask[i] = in ? 1 : 0;
+        c += in ? 1 : 0;
     }
-    const uint64_t b = __ballot(in);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (int)__popcll(b));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+    __shared__ int sc[4];
+    if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int t = sc[0] + sc[1] + sc[2] + sc[3];
+        if (t) atomicAdd(count, t);
+    }
 }
 
 struct OpFAtA {   // 45: upper triangle of A^T A, rows (X2X1, X2Y1, X2, Y2X1, Y2Y1, Y2, X1, Y1, 1)
@@ -253,7 +269,7 @@ static int f_variant() {
 void launch_abs_bound4(const void* d_pts4, bool fp64, int N, double* d_bb, float* d_out32, hipStream_t s) {
     (void)hipMemsetAsync(d_bb, 0, 4 * sizeof(double), s);
     if (N <= 0) return;
-    const int blocks = std::min(1024, (N + 255) / 256);
+    const int blocks = std::min(256, (N + 255) / 256);
     if (fp64)
         hipLaunchKernelGGL(mcv_abs_bound4<double4>, dim3(blocks), dim3(256), 0, s, (const double4*)d_pts4, N,
                            (unsigned long long*)d_bb, (float4*)d_out32);
@@ -308,8 +324,9 @@ void launch_f_mask(const float* d_pts4, int N, const double* F9, float thr2, int
                    hipStream_t s) {
     FModelD m;
     for (int j = 0; j < 9; ++j) m.f[j] = F9[j];
-    hipLaunchKernelGGL(mcv_f_mask, dim3((N + 255) / 256), dim3(256), 0, s, (const float4*)d_pts4, N, m, thr2, kind,
-                       d_mask, d_count);
+    if (N <= 0) return;
+    hipLaunchKernelGGL(mcv_f_mask, dim3(std::min(512, (N + 255) / 256)), dim3(256), 0, s, (const float4*)d_pts4, N, m,
+                       thr2, kind, d_mask, d_count);
 }
 
 void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,
