@@ -43,7 +43,7 @@ struct Plan {
     DevBuf<uint8_t> estage;   // essential: per-hypothesis EStage of the split five-point solve
     DevBuf<int> ndense;       // essential: dense model count, 4 cheirality counters, fetch flag
     double pnpCam[8] = {1, 1, 0, 0, 0, 0, 0, 0};   // PnP: fx, fy, cx, cy, k1, k2, p1, p2
-    int64_t eLastBegin = -1;  // essential: hypothesis range of the dense list's last chunk
+    int64_t eLastBegin = -1;  // essential / PnP: hypothesis range of the last evaluated chunk
     int64_t eLastCount = 0;
     uint64_t eLastSeed = 0;
     const void* eLastPts = nullptr;

@@ -119,6 +119,10 @@ void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
                       int* d_counts, hipStream_t s) {
     const float thr2 = (float)(cfg.threshold * cfg.threshold);
     launch_pnp_generate(d_pts, N, P.pnpCam, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+    P.eLastBegin = hypBegin;
+    P.eLastCount = hypCount;
+    P.eLastSeed = cfg.seed;
+    P.eLastPts = d_pts;
     ProfScope ps("pnp_verify", s);
     launch_pnp_verify(d_pts, N, P.pnpCam, P.models.p, d_counts, hypCount, thr2, fused_pnp(cfg), s);
 }
@@ -246,9 +250,23 @@ void pnp_vvs(Plan& P, const void* d_pts, int N, double* rvec, double* t, int max
 // Device API finalize: winner -> mask -> LM on the inliers; model9 = {rvec, tvec, 0, 0, 0}.
 int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
                uint8_t* d_mask, hipStream_t s) {
-    launch_pnp_one(d_pts, N, P.pnpCam, cfg.seed, hyp, (PnpOneOut*)P.one.p, s);
-    MCV_HIP(hipGetLastError());
-    const PnpOneOut one = pnp_fetch_one(P, s);
+    PnpOneOut one;
+    if (hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount && P.eLastSeed == cfg.seed && P.eLastPts == d_pts) {
+        // the winner's pose straight from the last chunk's model buffer (the same code produced it)
+        // instead of a single-lane AP3P re-solve
+        const PnpPose* d_m = (const PnpPose*)P.models.p + (hyp - P.eLastBegin);
+        MCV_HIP(hipMemcpyAsync(P.h_one.p, d_m, sizeof(PnpPose), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        PnpPose pose;
+        std::memcpy(&pose, P.h_one.p, sizeof(PnpPose));
+        std::memcpy(one.R, pose.R, sizeof(one.R));
+        std::memcpy(one.t, pose.t, sizeof(one.t));
+        one.status = 1;
+    } else {
+        launch_pnp_one(d_pts, N, P.pnpCam, cfg.seed, hyp, (PnpOneOut*)P.one.p, s);
+        MCV_HIP(hipGetLastError());
+        one = pnp_fetch_one(P, s);
+    }
     if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
     const int count = pnp_mask_count(P, d_pts, N, cfg, one.R, one.t, d_mask, s);
     double r[3], t[3] = {one.t[0], one.t[1], one.t[2]};
