@@ -147,6 +147,84 @@ MCV_HD int e_poly_real_roots(const double* cin, int deg, double* roots) {
     return np;
 }
 
+// e_poly_real_roots for a fixed maximum degree NMAX with no dynamically indexed arrays (so the
+// device keeps everything in registers; the AP3P quartic): levels and intervals unrolled, pushes
+// into the root list as select chains, every level's Horner over coefficients zero-padded to
+// degree NMAX — +0 * x + (+0) stays +0 and (+-0) + q[d] = q[d], so it rounds exactly like the
+// degree-d loop. Bit-identical to e_poly_real_roots(cin, NMAX, roots).
+template <int NMAX>
+struct EPolyPad {
+    double q[NMAX + 1];
+    MCV_HD double operator()(double x) const {
+        double f = q[NMAX];
+        for (int k = NMAX - 1; k >= 0; --k) f = f * x + q[k];
+        return f;
+    }
+};
+
+template <int NMAX>
+MCV_HD int e_poly_real_roots_fixed(const double (&cin)[NMAX + 1], double (&roots)[NMAX]) {
+    int n = 0;
+#pragma unroll
+    for (int k = 1; k <= NMAX; ++k) n = cin[k] != 0 ? k : n;   // highest non-zero coefficient
+    if (n < 1) return 0;
+    double lead = cin[1];
+#pragma unroll
+    for (int k = 2; k <= NMAX; ++k) lead = n == k ? cin[k] : lead;
+    double c[NMAX + 1];
+#pragma unroll
+    for (int k = 0; k <= NMAX; ++k) c[k] = k <= n ? cin[k] / lead : 0.0;
+    double R = 0;
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) {
+        const double a = fabs(c[k]);
+        R = (k < n && a > R) ? a : R;
+    }
+    R = 1.0 + R;
+    if (!isfinite(R)) return 0;
+    double rp[NMAX], rc[NMAX];
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) rp[k] = rc[k] = 0.0;
+    int np = 0;
+#pragma unroll
+    for (int j = NMAX - 1; j >= 0; --j) {
+        if (j > n - 1) continue;
+        const int d = n - j;
+        EPolyPad<NMAX> P;
+#pragma unroll
+        for (int k = 0; k <= NMAX; ++k) P.q[k] = (k + j <= NMAX && k <= d) ? c[k + j <= NMAX ? k + j : 0] * e_falling(k + j, j) : 0.0;
+        int nc = 0;
+        double last = 0.0;
+        auto push = [&](double v) {
+#pragma unroll
+            for (int t = 0; t < NMAX; ++t) rc[t] = t == nc ? v : rc[t];
+            last = v;
+            ++nc;
+        };
+        double a = -R;
+        double fa = P(a);
+#pragma unroll
+        for (int s = 0; s < NMAX; ++s) {
+            if (s > np) break;
+            const double b = s < np ? rp[s] : R;
+            const double fb = P(b);
+            if (fb == 0) {
+                if (nc == 0 || last != b) push(b);
+            } else if (fa != 0 && ((fa < 0) != (fb < 0))) {
+                push(e_root_bracketed_f(P, a, b, fa, fb));
+            }
+            a = b;
+            fa = fb;
+        }
+#pragma unroll
+        for (int t = 0; t < NMAX; ++t) rp[t] = rc[t];
+        np = nc;
+    }
+#pragma unroll
+    for (int t = 0; t < NMAX; ++t) roots[t] = rp[t];
+    return np;
+}
+
 // ---- polynomial algebra in (x, y, z, w = 1) -------------------------------------------------
 // Linear form: 4 coefficients (x, y, z, w). Quadratic: pairs (a <= b) in the order
 // (0,0) (0,1) (0,2) (0,3) (1,1) (1,2) (1,3) (2,2) (2,3) (3,3). Cubic: 20 coefficients in the

@@ -151,8 +151,8 @@ MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double
     bool finite = true;
     for (int k = 0; k < 5; ++k) finite = finite && isfinite(c[k]);
     if (!finite || !isfinite(delta) || !isfinite(k3b3) || !(nk3 > 0) || !(nu0 > 0) || !(delta > 0)) return 0;
-    double s[10];
-    const int ns = e_poly_real_roots(c, 4, s);
+    double s[4];
+    const int ns = e_poly_real_roots_fixed<4>(c, s);   // = e_poly_real_roots(c, 4, s), register-resident
     double temp[3];
     v3_cross(k1, nl, temp);
     const double Ck1nl[9] = {k1[0], nl[0], temp[0], k1[1], nl[1], temp[1], k1[2], nl[2], temp[2]};
@@ -160,7 +160,9 @@ MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double
     const double sc = delta / k3b3;
     const double b3p[3] = {b3[0] * sc, b3[1] * sc, b3[2] * sc};
     int n = 0;
-    for (int i = 0; i < ns && n < kPnpMaxSolutions; ++i) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // ns <= 4 = kPnpMaxSolutions: no solution is ever cut off
+        if (i >= ns) break;
         const double ct1 = s[i];
         if (fabs(ct1) > 1) continue;
         double st1 = sqrt(1 - ct1 * ct1);
@@ -181,8 +183,18 @@ MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double
         const double rp3[3] = {w3[0] * R[0] + w3[1] * R[3] + w3[2] * R[6], w3[0] * R[1] + w3[1] * R[4] + w3[2] * R[7],
                                w3[0] * R[2] + w3[1] * R[5] + w3[2] * R[8]};
         bool ok = isfinite(nt3);
-        for (int k = 0; k < 9; ++k) { Rr[n][k] = R[k]; ok = ok && isfinite(R[k]); }
-        for (int k = 0; k < 3; ++k) { tr[n][k] = st1 * b3p[k] - rp3[k]; ok = ok && isfinite(tr[n][k]); }
+        double tv[3];
+        for (int k = 0; k < 9; ++k) ok = ok && isfinite(R[k]);
+        for (int k = 0; k < 3; ++k) { tv[k] = st1 * b3p[k] - rp3[k]; ok = ok && isfinite(tv[k]); }
+        // append to slot n as selects (a dynamically indexed store would put Rr / tr in scratch)
+#pragma unroll
+        for (int slot = 0; slot < kPnpMaxSolutions; ++slot) {
+            const bool w = ok && slot == n;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Rr[slot][k] = w ? R[k] : Rr[slot][k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) tr[slot][k] = w ? tv[k] : tr[slot][k];
+        }
         if (ok) ++n;
     }
     return n;
@@ -208,11 +220,16 @@ MCV_HD int pnp_ap3p4(const PnpCamera& c, const double* x, const double* y, const
         for (int k = 0; k < 3; ++k) w[i][k] = W[i][k];
     }
     double Rr[kPnpMaxSolutions][9], tr[kPnpMaxSolutions][3];
+    for (int i = 0; i < kPnpMaxSolutions; ++i) {
+        for (int k = 0; k < 9; ++k) Rr[i][k] = 0.0;
+        for (int k = 0; k < 3; ++k) tr[i][k] = 0.0;
+    }
     const int n = ap3p_compute_poses(b, w, Rr, tr);
     if (n == 0) return 0;
-    int best = 0;
-    double bestErr = 0;
-    for (int i = 0; i < n; ++i) {
+    double bestErr = 0, bR[9], bt[3];
+#pragma unroll
+    for (int i = 0; i < kPnpMaxSolutions; ++i) {
+        if (i >= n) break;
         // camera-from-world rotation = Rr^T
         const double* R = Rr[i];
         const double X = R[0] * W[3][0] + R[3] * W[3][1] + R[6] * W[3][2] + tr[i][0];
@@ -221,11 +238,14 @@ MCV_HD int pnp_ap3p4(const PnpCamera& c, const double* x, const double* y, const
         const double du = c.fx * (X / Z - x[3]);
         const double dv = c.fy * (Y / Z - y[3]);
         const double e = du * du + dv * dv;
-        if (i == 0 || bestErr > e) { best = i; bestErr = e; }
+        const bool take = i == 0 || bestErr > e;   // first minimum
+        bestErr = take ? e : bestErr;
+        for (int k = 0; k < 9; ++k) bR[k] = take ? R[k] : bR[k];
+        for (int k = 0; k < 3; ++k) bt[k] = take ? tr[i][k] : bt[k];
     }
     for (int r = 0; r < 3; ++r)
-        for (int q = 0; q < 3; ++q) pose.R[3 * r + q] = Rr[best][3 * q + r];
-    for (int k = 0; k < 3; ++k) pose.t[k] = tr[best][k];
+        for (int q = 0; q < 3; ++q) pose.R[3 * r + q] = bR[3 * q + r];
+    for (int k = 0; k < 3; ++k) pose.t[k] = bt[k];
     return 1;
 }
 
