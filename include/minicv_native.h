@@ -355,6 +355,10 @@ MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models
 MCV_API int mcvHostEssential(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90, int* sampleIdx);
 MCV_API int mcvHostFivePoint(const double* p20, double* E90);
 MCV_API void mcvHostDecomposeEssential(const double* E9, double* R1, double* R2, double* t3);
+/* Host twin of the real-root finder (Rolle brackets + Illinois) of sum c[k] x^k, deg <= 10;
+ * fixed = 1 (deg == 4 only) runs the register-resident fixed-size form the AP3P quartic uses.
+ * Writes the ascending roots, returns their count (-1 on bad arguments). */
+MCV_API int mcvHostRealRoots(const double* c, int deg, int fixed, double* roots);
 /* Host twins of the PnP path: one hypothesis on packed PnpPoint[N] (cam8 = fx, fy, cx, cy, k1, k2,
  * p1, p2), and the Rodrigues maps used by the LM refit. */
 MCV_API int mcvHostPnP(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9, double* t3,

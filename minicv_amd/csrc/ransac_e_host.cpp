@@ -343,6 +343,20 @@ extern "C" MCV_API int mcvHostFivePoint(const double* p20, double* E90) {
     })
 }
 
+extern "C" MCV_API int mcvHostRealRoots(const double* c, int deg, int fixed, double* roots) {
+    MCV_GUARD(-1, {
+        if (!c || !roots || deg < 0 || deg > 10 || (fixed && deg != 4)) fail("mcvHostRealRoots: bad arguments");
+        if (fixed) {
+            const double c5[5] = {c[0], c[1], c[2], c[3], c[4]};
+            double r4[4];
+            const int n = e_poly_real_roots_fixed<4>(c5, r4);
+            for (int k = 0; k < n; ++k) roots[k] = r4[k];
+            return n;
+        }
+        return e_poly_real_roots(c, deg, roots);
+    })
+}
+
 extern "C" MCV_API void mcvHostDecomposeEssential(const double* E9, double* R1, double* R2, double* t3) {
     e_decompose(E9, R1, R2, t3);
 }

@@ -140,6 +140,7 @@ SIGNATURES = {
     "mcvHostEssential": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostFivePoint": (_I, [_P, _P]),
     "mcvHostDecomposeEssential": (None, [_P, _P, _P, _P]),
+    "mcvHostRealRoots": (_I, [_P, _I, _I, _P]),
     "mcvHostPnP": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
     "mcvHostRodrigues": (None, [_P, _P, _P]),
     "mcvHostRodriguesInv": (None, [_P, _P]),

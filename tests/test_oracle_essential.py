@@ -166,3 +166,34 @@ def test_replay_models_export_matches_oracle(native, oracle):
         assert st.bestIndex == best
         if best >= 0:
             assert st.bestCount == bc
+
+
+def _host_roots(native, c, fixed):
+    import ctypes as C
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    r = np.zeros(10, dtype=np.float64)
+    n = native.lib().mcvHostRealRoots(c.ctypes.data_as(C.c_void_p), len(c) - 1, int(fixed),
+                                      r.ctypes.data_as(C.c_void_p))
+    assert n >= 0
+    return r[:n]
+
+
+def test_host_real_roots_fixed_form_bit_exact(native, oracle):
+    """The register-resident fixed-size root finder (AP3P's quartic) equals the generic one and the
+    oracle bit for bit: random quartics, leading zeros (degree 3..0), repeated and clustered roots,
+    zero / huge / tiny coefficients, non-finite input."""
+    rng = np.random.default_rng(7)
+    cases = [rng.normal(size=5) * 10.0 ** rng.integers(-6, 7, size=5) for _ in range(3000)]
+    cases += [np.poly1d(rng.normal(size=4), r=True).coeffs[::-1] for _ in range(500)]
+    cases += [np.poly1d([r, r, s, s], r=True).coeffs[::-1] for r, s in rng.normal(size=(300, 2))]
+    cases += [np.poly1d([1.0, 1.0 + 1e-12, -2.0, 3.0], r=True).coeffs[::-1]]
+    for d in range(4):
+        cases += [np.concatenate([rng.normal(size=d + 1), np.zeros(4 - d)]) for _ in range(100)]
+    cases += [np.array([0.0, 0, 0, 0, 0]), np.array([1.0, 0, 0, 0, 1e-300]), np.array([1e300, -1e300, 1, 0, 1]),
+              np.array([np.nan, 1, 2, 3, 4]), np.array([1, 2, 3, 4, np.inf]), np.array([-1.0, 0, 0, 0, 1])]
+    for c in cases:
+        c = np.asarray(c, dtype=np.float64)
+        fx = _host_roots(native, c, True)
+        gen = _host_roots(native, c, False)
+        np.testing.assert_array_equal(fx, gen)
+        np.testing.assert_array_equal(fx, oracle.poly_real_roots(c))
