@@ -64,6 +64,26 @@ SPK_CYC_PER_WAVE_EVAL = 56
 SPK_PEAK_EVALS = 256 * 4 * 2.4e9 / SPK_CYC_PER_WAVE_EVAL * 64
 
 
+
+def dist_setup(torch, dist):
+    """(world, rank, device) for this process. The driver runs N ranks on N GPUs over RCCL
+    ("nccl"); MCV_DIST_BACKEND=gloo rehearses N ranks on the GPUs this box has (ranks share a
+    device, the one all-reduce goes through gloo) — a test of the multi-rank path, not a benchmark."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("MCV_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return world, rank, dev
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,13 +144,7 @@ def bench_matcher(args):
     import numpy as np
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, dev = dist_setup(torch, dist)
     from minicv_amd import native as NL, synthetic as S, device as D
     from minicv_amd import dist as MD
     ham = args.workload == "hamming"
@@ -256,15 +270,10 @@ def bench_ransac(args):
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, dev = dist_setup(torch, dist)
 
     from minicv_amd import native as NL, opencv, synthetic as S
     from minicv_amd import device as D
@@ -685,13 +694,7 @@ def bench_scaled(args):
     import torch.distributed as dist
     from minicv_amd import native as NL, synthetic as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, dev = dist_setup(torch, dist)
     n = args.n if args.n != N_CORR else S_N_OBS
     src, pose, W, O, inl = S.scaled_problem(n, seed=S_SEED, outlier_frac=0.3, sigma=1e-3, true_scale=2.5)
     Wd = torch.from_numpy(np.ascontiguousarray(W)).to(dev)
