@@ -90,7 +90,9 @@ __device__ __forceinline__ void ew_sync() { __syncthreads(); }
 // Lanes [base, base + G) of the wave work on one hypothesis; sub = lane - base.
 template <int G>
 struct EGroup {
-    static_assert(G == 16 || G == 32 || G == 64, "group of 16, 32 or 64 lanes");
+    // 8-lane groups serve the matrix phases only (ew_stage_hypothesis); the root bracketing by
+    // interval needs >= 11 lanes (ew_real_roots), so a full solve takes 16, 32 or 64
+    static_assert(G == 8 || G == 16 || G == 32 || G == 64, "group of 8, 16, 32 or 64 lanes");
     int sub, base;
     __device__ explicit EGroup(int lane) : sub(lane & (G - 1)), base(lane & ~(G - 1)) {}
     __device__ uint64_t ballot(bool p) const {

@@ -418,8 +418,19 @@ void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBe
     if (hypCount <= 0) return;
     if (d_stage && group == kEGenLanes) {   // many hypotheses: matrix phases per group, roots per lane
         EStage* st = (EStage*)d_stage;
-        hipLaunchKernelGGL(mcv_e_stage<kEStageLanes>, dim3((hypCount + 64 / kEStageLanes - 1) / (64 / kEStageLanes)),
-                           dim3(64), 0, s, d_pts4, N, seed, hypBegin, hypCount, st);
+        static const int stageLanes = [] {
+            const char* e = getenv("MCV_E_STAGE");   // 8 / 16 / 32 lanes per hypothesis (screen)
+            return e ? atoi(e) : kEStageLanes;
+        }();
+        if (stageLanes == 8)
+            hipLaunchKernelGGL(mcv_e_stage<8>, dim3((hypCount + 7) / 8), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+                               hypCount, st);
+        else if (stageLanes == 32)
+            hipLaunchKernelGGL(mcv_e_stage<32>, dim3((hypCount + 1) / 2), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+                               hypCount, st);
+        else
+            hipLaunchKernelGGL(mcv_e_stage<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+                               hypCount, st);
         static const int rootLanes = [] {
             const char* e = getenv("MCV_E_ROOTS");
             return e ? atoi(e) : kERootLanes;
