@@ -692,6 +692,10 @@ static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d
         case 22: launch_h_verify_pk_k<4, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         case 24: launch_h_verify_pk_k<3, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         case 25: launch_h_verify_pk_k<5, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 27: launch_h_verify_pk_k<5, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 28: launch_h_verify_pk_k<7, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 29: launch_h_verify_pk_k<6, 3>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 30: launch_h_verify_pk_k<8, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         default: return false;
     }
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Screen sweep shapes (MCV_SWEEP_VARIANT) on the headline bench; one process per variant.
-#   0 / 20-26: packed-f32 sweep mcv_h_verify_pk<K, pairs per lane> (0 = <6, 2>); 19: scalar mcv_h_verify<6, 2>.
+#   0 / 20-30: packed-f32 sweep mcv_h_verify_pk<K, pairs per lane> (0 = <6, 2>; 27-30 = <5,2> <7,2> <6,3> <8,2>,
+#   screened at 30.40 / 32.14 / 34.67 / 34.22 ms vs 30.44); 19: scalar mcv_h_verify<6, 2>.
 mkdir -p gpurun_out
 for v in ${VARIANTS:-0 19 20 21 22 24 25 26}; do
     MCV_SWEEP_VARIANT=$v timeout -k 10 200 python bench.py --steps 8 --warmup 2 --no-cpu-baseline > gpurun_out/variant_$v.log 2>&1
