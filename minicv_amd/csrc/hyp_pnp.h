@@ -59,7 +59,13 @@ MCV_HD void pnp_project(const PnpCamera& c, const double* R, const double* t, do
     const double Xc = R[0] * X + R[1] * Y + R[2] * Z + t[0];
     const double Yc = R[3] * X + R[4] * Y + R[5] * Z + t[1];
     const double Zc = R[6] * X + R[7] * Y + R[8] * Z + t[2];
-    const double iz = 1.0 / (Zc != 0 ? Zc : 1.0);   // = (Zc != 0 ? 1 / Zc : 1), without a divergent branch
+#if defined(__HIP_DEVICE_COMPILE__)
+    // refined reciprocal (mcv_common.h): 1 / Zc bit for bit for |Zc| in [2^-64, 2^64]
+    double iz = rcp_f64_refined(Zc);
+    if (!div_f64_refined_domain(Zc)) iz = 1.0 / (Zc != 0 ? Zc : 1.0);   // = (Zc != 0 ? 1 / Zc : 1)
+#else
+    const double iz = 1.0 / (Zc != 0 ? Zc : 1.0);   // = (Zc != 0 ? 1 / Zc : 1)
+#endif
     const double x = Xc * iz, y = Yc * iz;
     const double r2 = x * x + y * y, r4 = r2 * r2;
     const double a1 = 2.0 * x * y, a2 = r2 + 2.0 * x * x, a3 = r2 + 2.0 * y * y;

@@ -50,7 +50,20 @@ MCV_HD bool scaled_term(const ScaledSetup& S, const double (&loc)[3], double wx,
     const double p0 = o0 * S.right[0] + o1 * S.right[1] + o2 * S.right[2];
     const double p1 = o0 * S.up[0] + o1 * S.up[1] + o2 * S.up[2];
     const double p2 = o0 * S.fwd[0] + o1 * S.fwd[1] + o2 * S.fwd[2];
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Both quotients share one refined reciprocal (mcv_common.h): equal to the IEEE divisions for
+    // p2 in [2^-64, 2^64] and every numerator whose quotient can be visible (|c| <= 1); a numerator
+    // below 2^-900 gives |c| < 2^-836 either way, and c - o then rounds identically (to -o, or to
+    // a value whose square is +0). A visible p2 outside that range takes the IEEE divisions.
+    const double rp2 = rcp_f64_refined(p2);
+    double cx = div_f64_refined(S.fx * p0, p2, rp2), cy = div_f64_refined(S.fy * p1, p2, rp2);
+    if (p2 >= 0.0 && !div_f64_refined_domain(p2)) {
+        cx = S.fx * p0 / p2;
+        cy = S.fy * p1 / p2;
+    }
+#else
     const double cx = S.fx * p0 / p2, cy = S.fy * p1 / p2;
+#endif
     const double dx = cx - ox, dy = cy - oy;
     err = dx * dx + dy * dy;
     return p2 >= 0.0 && cx >= -1.0 && cy >= -1.0 && cx <= 1.0 && cy <= 1.0;

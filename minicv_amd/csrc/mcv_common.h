@@ -149,4 +149,37 @@ MCV_HD float rcp_rn(float w) {
 #endif
 }
 
+// fp64 division without the v_div_scale / v_div_fixup wrapper. The IEEE expansion gfx950 runs
+// for n / d is div_scale(d), div_scale(n), rcp, two Newton steps, q = n r, rem = fma(-d, q, n),
+// div_fmas(rem, r, q), div_fixup: 11 VALU ops. When no operand needs scaling the div_scale ops
+// return their inputs (VCC = 0, div_fmas = fma) and div_fixup passes a normal result through, so
+//   rcp_f64_refined(d) = the refined reciprocal (5 ops, shared by every quotient over d)
+//   div_f64_refined(n, d, r) = n / d bit for bit (3 ops)
+// whenever d in +-[2^-64, 2^64] and 2^-900 <= |n| < 2^700 (or n = 0, up to the sign of the zero).
+// Callers guard d and argue the n range (mcvTestDivF64 samples both: tests/test_gpu_selftest.py).
+// Host: the IEEE division itself.
+MCV_HD double rcp_f64_refined(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(r, e, r);
+#else
+    return 1.0 / d;
+#endif
+}
+MCV_HD double div_f64_refined(double n, double d, double r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double q = n * r;
+    const double rem = __builtin_fma(-d, q, n);
+    return __builtin_fma(rem, r, q);
+#else
+    (void)r;
+    return n / d;
+#endif
+}
+// The denominator domain of the two helpers above.
+MCV_HD bool div_f64_refined_domain(double d) { return __builtin_fabs(d) >= 0x1p-64 && __builtin_fabs(d) <= 0x1p64; }
+
 }  // namespace mcv

@@ -42,6 +42,49 @@ __global__ __launch_bounds__(256) void mcv_rcp_check(uint64_t begin, uint64_t co
     if (local) atomicAdd(mism, local);
 }
 
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+// fp64 with a random sign and mantissa and a binary exponent uniform in [lo, hi] (normal range).
+__device__ __forceinline__ double random_f64(uint64_t bits, uint64_t ebits, int lo, int hi) {
+    const int e = lo + (int)(ebits % (uint64_t)(hi - lo + 1));
+    return __longlong_as_double((long long)((bits & 0x800FFFFFFFFFFFFFull) | ((uint64_t)(e + 1023) << 52)));
+}
+
+// Samples (n, d) with d in +-[2^-64, 2^64] and compares div_f64_refined against n / d.
+//   mode 0: |n| in [2^-900, 2^699]      mode 1: n = 1 (the reciprocal)
+//   mode 2: n = d * k, k a small integer (exact quotients)   mode 3: d at the domain ends
+__global__ __launch_bounds__(256) void mcv_div_check(uint64_t seed, uint64_t count, int mode,
+                                                     unsigned long long* mism, double* first) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    unsigned long long local = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += stride) {
+        const uint64_t a = splitmix64(seed ^ (i * 4 + 0)), b = splitmix64(seed ^ (i * 4 + 1));
+        const uint64_t c = splitmix64(seed ^ (i * 4 + 2)), g = splitmix64(seed ^ (i * 4 + 3));
+        double d = random_f64(a, b, -64, 63);
+        if (mode == 3) d = (g & 1) ? random_f64(a, b, -64, -64) : random_f64(a, b, 63, 63);
+        double n;
+        if (mode == 1) n = 1.0;
+        else if (mode == 2) n = d * (double)(int)(g % 2001 - 1000);
+        else n = random_f64(c, g, -900, 699);
+        const double q = div_f64_refined(n, d, rcp_f64_refined(d));
+        const double ref = n / d;
+        const bool same = __double_as_longlong(q) == __double_as_longlong(ref) || (q == 0.0 && ref == 0.0);
+        if (!same) {
+            ++local;
+            const unsigned long long slot = atomicAdd(mism + 1, 1ull);
+            if (slot < 16) {
+                first[2 * slot] = n;
+                first[2 * slot + 1] = d;
+            }
+        }
+    }
+    if (local) atomicAdd(mism, local);
+}
+
 }  // namespace mcv
 
 using namespace mcv;
@@ -60,6 +103,27 @@ extern "C" MCV_API long long mcvTestRcpExhaustive(int mode, uint32_t* firstMisma
         unsigned long long h[2];
         MCV_HIP(hipMemcpy(h, m.p, 16, hipMemcpyDeviceToHost));
         if (firstMismatches16) MCV_HIP(hipMemcpy(firstMismatches16, f.p, 64, hipMemcpyDeviceToHost));
+        return (long long)h[0];
+    })
+}
+
+extern "C" MCV_API long long mcvTestDivF64(int mode, unsigned long long seed, long long count,
+                                           double* firstMismatches32) {
+    MCV_GUARD(-1, {
+        require_device();
+        if (count < 0) return -1LL;
+        DevBuf<unsigned long long> m;
+        DevBuf<double> f;
+        m.ensure(2);
+        f.ensure(32);
+        MCV_HIP(hipMemset(m.p, 0, 16));
+        MCV_HIP(hipMemset(f.p, 0, 256));
+        hipLaunchKernelGGL(mcv_div_check, dim3(8192), dim3(256), 0, 0, (uint64_t)seed, (uint64_t)count, mode, m.p,
+                           f.p);
+        MCV_HIP(hipGetLastError());
+        unsigned long long h[2];
+        MCV_HIP(hipMemcpy(h, m.p, 16, hipMemcpyDeviceToHost));
+        if (firstMismatches32) MCV_HIP(hipMemcpy(firstMismatches32, f.p, 256, hipMemcpyDeviceToHost));
         return (long long)h[0];
     })
 }

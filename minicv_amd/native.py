@@ -145,6 +145,7 @@ SIGNATURES = {
     "mcvHostRodrigues": (None, [_P, _P, _P]),
     "mcvHostRodriguesInv": (None, [_P, _P]),
     "mcvTestRcpExhaustive": (C.c_longlong, [_I, _P]),
+    "mcvTestDivF64": (C.c_longlong, [_I, C.c_ulonglong, C.c_longlong, _P]),
     "mcvTestHomographySweep": (_I, [_P, _I, _P, _I, _F, _I, _P]),
     "mcvHostScaledCosts": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
 }

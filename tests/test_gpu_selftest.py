@@ -60,3 +60,13 @@ def test_sweep_rare_paths_bit_exact(native, gpu, oracle, mode):
     assert ok == 1, native.last_error()
     ref = np.array([oracle.h_count(pts, m, float(thr2), fused=fused) for m in models], np.int32)
     np.testing.assert_array_equal(counts, ref)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])   # random n / reciprocal / exact quotients / domain ends
+def test_unscaled_f64_division_matches_ieee(native, gpu, mode):
+    """rcp_f64_refined + div_f64_refined (the fp64 division without v_div_scale / v_div_fixup that the
+    findScaled and PnP sweeps run) equal the IEEE quotient over 2^26 sampled (n, d) per mode, d in
+    +-[2^-64, 2^64]."""
+    first = np.zeros(32, np.float64)
+    n = native.lib().mcvTestDivF64(mode, 0x5EED + mode, 1 << 26, first.ctypes.data)
+    assert n == 0, first[:2 * min(n, 16)].reshape(-1, 2).tolist()
