@@ -45,7 +45,7 @@ SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # VALU issue model of the packed sweep mcv_h_verify_pk<6,2> (fused error), per (hypothesis, pair of
 # correspondences): 12 v_pk_fma/mul_f32 (4 cycles each: two 32-lane passes per half), 2 v_rcp_f32
-# (quarter rate, 8 cycles), 2 v_cmp + 2 v_cmp_class (2 cycles) = 72 cycles = 36 per evaluation,
+# (quarter rate, 8 cycles), 2 v_cmp (2 cycles) + 1 v_min3_f32 of |w| (4 cycles) = 72 cycles = 36 per evaluation,
 # i.e. 18 issue slots of 2 cycles (wave64 on SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x
 # 2.4 GHz / 2 x 64 lanes / 18.
 VALU_SLOTS_PER_EVAL = 18

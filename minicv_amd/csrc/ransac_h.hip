@@ -244,7 +244,7 @@ __device__ __forceinline__ f2 hi(f2 v) { return __builtin_shufflevector(v, v, 1,
 template <int K, int NP, bool PRED>
 __device__ __forceinline__ void h_pk_trip(const f2 (&hp)[K][4], const f2 (&hc)[K], const HPair (&q)[NP],
                                           const bool (&v)[NP], float thr2, f2 one, uint32_t (&cnt)[K],
-                                          uint64_t& bad) {
+                                          float (&wmin)[NP]) {
     auto vote = [&](int j, bool pred) -> uint32_t {
         if constexpr (PRED)
             return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(v[j] && pred));
@@ -264,7 +264,13 @@ __device__ __forceinline__ void h_pk_trip(const f2 (&hp)[K][4], const f2 (&hc)[K
             f2 W = pk_fma(lo(p3), q[j].x, pk_fma(hi(p3), q[j].y, one));
             const f2 U = pk_fma(lo(p0), q[j].x, pk_fma(hi(p0), q[j].y, lo(c)));
             const f2 V = pk_fma(hi(p1), q[j].x, pk_fma(lo(p2), q[j].y, hi(c)));
-            bad |= class_mask(W.x, kClassNotNormal) | class_mask(W.y, kClassNotNormal);
+            // smallest |w| per lane and pair slot (one v_min3_f32 with |.| modifiers; an fma result
+            // is canonical, so no quieting op): |w| < 2^-126 (0, denormal) is a "bad" denominator.
+            // One accumulator per slot j keeps the min chains short (a single running min was
+            // 4% slower than the two v_cmp_class per pair it replaces; two chains are 4% faster).
+            // A NaN w (NaN point) is not tracked: the fast and the exact error are both NaN there
+            // (outlier); the bounding-box precondition rules out an infinite w.
+            wmin[j] = __builtin_fminf(__builtin_fminf(wmin[j], __builtin_fabsf(W.x)), __builtin_fabsf(W.y));
             f2 R = f2{__builtin_amdgcn_rcpf(W.x), __builtin_amdgcn_rcpf(W.y)};
             const f2 E = pk_fma(-W, R, one);              // fma(-w, r, 1)
             R = pk_fma(E, R, R);                          // fma(e, r, r)
@@ -316,7 +322,9 @@ __global__ __launch_bounds__(256) void mcv_h_verify_pk(const HPair* __restrict__
     uint32_t cnt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
-    uint64_t bad = 0;
+    float wmin[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) wmin[j] = 1.0f;
     if (fast) {
         constexpr int TRIP = 64 * NP;
         const int nFull = nPairs / TRIP * TRIP;
@@ -327,7 +335,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify_pk(const HPair* __restrict__
             HPair q[NP];
 #pragma unroll
             for (int j = 0; j < NP; ++j) q[j] = pairs[base + 64 * j + lane];
-            h_pk_trip<K, NP, false>(hp, hc, q, vt, thr2, one, cnt, bad);
+            h_pk_trip<K, NP, false>(hp, hc, q, vt, thr2, one, cnt, wmin);
         }
         if (nFull < nPairs) {
             HPair q[NP];
@@ -338,10 +346,13 @@ __global__ __launch_bounds__(256) void mcv_h_verify_pk(const HPair* __restrict__
                 v[j] = p < nPairs;
                 q[j] = pairs[v[j] ? p : 0];
             }
-            h_pk_trip<K, NP, true>(hp, hc, q, v, thr2, one, cnt, bad);
+            h_pk_trip<K, NP, true>(hp, hc, q, v, thr2, one, cnt, wmin);
         }
     }
-    const bool redo = !fast || bad != 0;
+    float wm = wmin[0];
+#pragma unroll
+    for (int j = 1; j < NP; ++j) wm = __builtin_fminf(wm, wmin[j]);
+    const bool redo = !fast || __builtin_amdgcn_ballot_w64(!(wm >= 0x1p-126f)) != 0;
     if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k)
