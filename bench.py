@@ -43,7 +43,7 @@ P_THR_PX = 2.0
 THR = 5e-3
 SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue model of the packed sweep mcv_h_verify_pk<6,2> (fused error), per (hypothesis, pair of
+# VALU issue model of the packed sweep mcv_h_verify_pk<8,2> (fused error), per (hypothesis, pair of
 # correspondences): 12 v_pk_fma/mul_f32 (4 cycles each: two 32-lane passes per half), 2 v_rcp_f32
 # (quarter rate, 8 cycles), 2 v_cmp (2 cycles) + 1 v_min3_f32 of |w| (4 cycles) = 72 cycles = 36 per evaluation,
 # i.e. 18 issue slots of 2 cycles (wave64 on SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x

@@ -696,7 +696,7 @@ bool launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, con
 static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d_models, int* d_counts,
                                        int hypCount, float thr2, const float* d_bbox, hipStream_t s) {
     switch (sweep_variant()) {
-        case 0: launch_h_verify_pk_k<6, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 0: launch_h_verify_pk_k<8, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         case 26: launch_h_verify_pk_k<6, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         case 20: launch_h_verify_pk_k<4, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         case 21: launch_h_verify_pk_k<8, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
@@ -706,7 +706,7 @@ static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d
         case 27: launch_h_verify_pk_k<5, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         case 28: launch_h_verify_pk_k<7, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         case 29: launch_h_verify_pk_k<6, 3>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 30: launch_h_verify_pk_k<8, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
+        case 30: launch_h_verify_pk_k<6, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         default: return false;
     }
 }
