@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fused", action="store_true",
+                    help="opt-in FMA-contracted inlier error (default: OpenCV's op-by-op order, the reference's)")
     ap.add_argument("--workload", default="homography",
                     choices=["homography", "fundamental", "essential", "pnp", "hamming", "l2", "scaled"],
                     help="homography = the headline (BASELINE config[2]); the others are config[1], [3], [4]")
@@ -296,7 +298,7 @@ def bench_ransac(args):
     plan = D.RansacPlan(NL.MODEL_FUNDAMENTAL if fund else NL.MODEL_HOMOGRAPHY, n, hyps)
     total = hyps * world
     cfg = opencv.RansacParams(threshold=THR, confidence=0.995, max_iters=total, seed=F_SEED if fund else SEED,
-                              fixed_iters=True).to_c()
+                              fixed_iters=True, fused_error=args.fused).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = torch.zeros(n, dtype=torch.uint8, device=dev)
     red = torch.zeros(2, dtype=torch.int64, device=dev)

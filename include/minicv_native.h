@@ -136,8 +136,10 @@ MCV_API bool cvDetectArucoMarkers(char* data, int width, int height, int channel
 /* flags */
 #define MCV_FLAG_FIXED_ITERS  1   /* evaluate exactly maxIters hypotheses (no adaptive stop) */
 #define MCV_FLAG_NO_REFINE    2   /* return the best hypothesis' model (skip inlier refit + LM) */
-#define MCV_FLAG_UNFUSED_ERROR 4  /* inlier error evaluated unfused, op by op (OpenCV x86 SSE build
-                                     arithmetic); default: FMA-contracted definition */
+#define MCV_FLAG_FUSED_ERROR  4   /* opt-in: FMA-contracted inlier error (what a compiler contracting
+                                     OpenCV's computeError produces, e.g. clang on arm64). Default:
+                                     op-by-op, every operation rounded as written = OpenCV's x86-64
+                                     (SSE baseline) build, the reference's Linux/AMD64 target. */
 
 /* F error metric (cfg->errorKind, fundamental only) */
 #define MCV_FERR_SAMPSON   0   /* first-order geometric (Sampson) distance^2 (north_star) */
@@ -174,7 +176,7 @@ MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, const int N, 
 MCV_API int cvFindEssentialMat(const mcvV2d* a, const mcvV2d* b, const int N, double focal, mcvV2d pp,
                                const RansacConfig* cfg, mcvM33d* E, uint8_t* mask);
 
-/* cvSolvePnPRansac with a full RansacConfig (threshold = reprojection error in pixels; seed, fixed iterations, unfused error, NO_REFINE). */
+/* cvSolvePnPRansac with a full RansacConfig (threshold = reprojection error in pixels; seed, fixed iterations, fused error, NO_REFINE). */
 MCV_API bool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                                  const double* distortionCoeffs, const RansacConfig* cfg, mcvV3d* tVec, mcvV3d* rVec,
                                  int* inlierCount, int* outInliers);
@@ -351,7 +353,8 @@ MCV_API long long mcvTestRcpExhaustive(int mode, uint32_t* firstMismatches16);
  * 1: n = 1; 2: n = k d, |k| <= 1000; 3: d at the domain ends); first 16 (n, d) pairs returned. */
 MCV_API long long mcvTestDivF64(int mode, unsigned long long seed, long long count, double* firstMismatches32);
 /* Device self-test: run the homography inlier sweep on caller-supplied fp32 models (8 floats each);
- * fused: 0 = op-by-op error, 1 = fused (scalar sweep), 2 = fused through the packed-f32 sweep. */
+ * fused: 0 = op-by-op error (scalar sweep), 1 = fused (scalar sweep), 2 = fused through the packed-f32
+ * sweep, 3 = op-by-op through the certified division-free sweep (the default path). */
 MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models8, int nModels, float thr2, int fused,
                                    int* counts);
 /* Host twins of the essential path: hypothesis (double4 normalised points; E90 = 10 x 9) and the

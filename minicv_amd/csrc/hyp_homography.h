@@ -221,10 +221,12 @@ MCV_HD int h_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, d
 }
 
 // HomographyEstimatorCallback::computeError for one correspondence, two bit-level definitions
-// (the reference's own arithmetic is build-dependent: OpenCV's x86 SSE baseline evaluates the
-// expression unfused, clang's default -ffp-contract=on on arm64 contracts it into FMAs):
-//   unfused (MCV_FLAG_UNFUSED_ERROR): every operation rounded as written, IEEE division;
-//   fused (default): w = fma(h6,x,fma(h7,y,1)); ww = RN(1/w);
+// (the reference's own arithmetic is build-dependent: OpenCV's x86-64 SSE baseline — the
+// reference's Linux/AMD64 target — evaluates the expression unfused, clang's default
+// -ffp-contract=on on arm64 contracts it into FMAs):
+//   op by op (default): every operation rounded as written, IEEE division (h_error); the sweep
+//                    decides it without dividing (mcv_h_verify_cert, ransac_h.hip);
+//   fused (MCV_FLAG_FUSED_ERROR): w = fma(h6,x,fma(h7,y,1)); ww = RN(1/w);
 //                    ex = fma(fma(h0,x,fma(h1,y,h2)), ww, -mx); ey likewise; e = fma(ex,ex,ey*ey).
 // Inlier iff e <= (float)thr^2 in both.
 MCV_HD float h_error(const float* h, float x, float y, float mx, float my) {

@@ -32,6 +32,10 @@ void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s);
 void launch_h_pair(const float* d_pts4, int N, void* d_pairs, hipStream_t s);
 bool launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
                             int hypCount, float thr2, const float* d_bbox, hipStream_t s);
+// Certified division-free sweep of the op-by-op error (the default) + exact recount of its redo slots;
+// d_bb = launch_abs_bound4 of the float4 points.
+void launch_h_verify_certified(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
+                               int hypCount, float thr2, const double* d_bb, hipStream_t s);
 void launch_h_mask(const float* d_pts4, int N, const float* hf8, float thr2, bool fused, uint8_t* d_mask,
                    int* d_count, hipStream_t s);
 void h_reduce_sums(const float* d_pts4, int N, const uint8_t* d_mask, double* d_part, double* d_out, hipStream_t s);

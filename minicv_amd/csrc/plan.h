@@ -92,6 +92,7 @@ struct ProfScope {
 void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst, hipStream_t s);
 double effective_threshold(const RansacConfig& cfg);
 bool fused_error(const RansacConfig& cfg);
+bool h_sweep_scalar_only();
 RansacConfig config_or_default(const RansacConfig* cfg);
 int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s);
 int finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,

@@ -113,7 +113,7 @@ static void pnp_pack(Plan& P, const mcvV2d* img, const mcvV3d* world, int N, voi
     MCV_HIP(hipGetLastError());
 }
 
-static bool fused_pnp(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_UNFUSED_ERROR) == 0; }
+static bool fused_pnp(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_ERROR) != 0; }
 
 void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
                       int* d_counts, hipStream_t s) {

@@ -25,7 +25,7 @@ namespace mcv {
 
 static const double kCheiralityDist = 50.0;   // recoverPose's distanceThresh for the focal/pp overload
 
-static int e_kind(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_UNFUSED_ERROR) ? 1 : 0; }
+static int e_kind(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_ERROR) ? 0 : 1; }
 
 void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
                       int* d_counts, hipStream_t s) {

@@ -17,7 +17,7 @@ namespace mcv {
 
 int f_error_kind(const RansacConfig& cfg) {
     const int e = cfg.errorKind == MCV_FERR_EPIPOLAR ? 1 : 0;
-    return e * 2 + ((cfg.flags & MCV_FLAG_UNFUSED_ERROR) ? 1 : 0);
+    return e * 2 + ((cfg.flags & MCV_FLAG_FUSED_ERROR) ? 0 : 1);
 }
 
 int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* F, uint8_t* d_mask,

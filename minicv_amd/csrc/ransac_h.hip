@@ -15,6 +15,7 @@
 // Built with -ffp-contract=off (see hyp_homography.h): the fp32 error rounds exactly like the
 // host oracle, which is what makes the inlier masks bit-exact.
 #include <cstdlib>
+#include <cmath>
 #include "mcv_common.h"
 #include "hyp_homography.h"
 #include "reduce.h"
@@ -357,6 +358,258 @@ __global__ __launch_bounds__(256) void mcv_h_verify_pk(const HPair* __restrict__
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (valid[k]) counts[h0 + k] = redo ? kStatusRedo : (int)cnt[k];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Certified division-free sweep of the op-by-op error (the default: OpenCV's computeError as an
+// x86-64 SSE build evaluates it, h_error). Per (hypothesis, correspondence) in packed f32:
+//   W = fma(h6,x,fma(h7,y,1)), U = fma(h0,x,fma(h1,y,h2)), V likewise,
+//   DX = fma(-x',W,U), DY = fma(-y',W,V), L = fma(DX,DX,DY*DY), W2 = W*W,
+//   certified inlier   <=  fma(W2, a_in, L)  < -b_in
+//   certified outlier  <=  fma(W2, a_out, L) >  b_out
+// with per-model constants from h_cert_consts (the derivation is in DESIGN.md §4): the reference
+// error times w^2 lies within relative (t + O(u)) and absolute O(u^2 G^2 / t) of L, and w^2 within
+// the same of W2, so a decided lane has the answer of the op-by-op fp32 error bit for bit. Lanes
+// left undecided (~1e-7 of evaluations on these workloads) take h_error with IEEE division in one
+// wave-uniform branch per trip. 13 packed ops + 4 compares per pair of correspondences, no
+// reciprocal: against the fused sweep's 12 packed + 2 v_rcp_f32 + v_min3 + 2 compares.
+// ------------------------------------------------------------------------------------------
+// Band parameter of the certified tests: relative half-width ~ t + O(u) around thr2 w^2, absolute
+// part ~ (7.5 u G)^2 / t. One t for every model keeps the slopes a_in / a_out launch constants.
+static constexpr double kCertT = 0x1p-12;
+static constexpr double kCertSlop = 0x1p-18;   // covers the O(u) terms (< 15 u = 2^-20.1 in total)
+
+struct HCertSlopes { f2 a; };   // {a_in, a_out}, both <= 0 (kernel argument)
+
+HCertSlopes h_cert_slopes_host(float thr2) {
+    const double T = (double)thr2, t = kCertT;
+    const double ain = -T * (1.0 - t) / (1.0 + t) * (1.0 - kCertSlop);
+    const double aout = -T * (1.0 + t) / (1.0 - t) * (1.0 + kCertSlop);
+    // rounded towards the conservative side of each test: |a_in| down, |a_out| up
+    float fi = (float)ain, fo = (float)aout;
+    if ((double)fi < ain) fi = std::nextafter(fi, 0.0f);
+    if ((double)fo > aout) fo = std::nextafter(fo, -__builtin_inff());
+    HCertSlopes c;
+    c.a = f2{fi, fo};
+    return c;
+}
+
+// Per-model offsets b = {-b_in, b_out}; false when the model or the point set leaves the domain of
+// the error bound (the wave then hands its slots to the exact scalar sweep). bb = {max|x|, max|y|,
+// max|x'|, max|y'|} of the correspondences (inf when any is NaN / inf).
+__device__ __forceinline__ bool h_cert_offsets(const float* h, const double* bb, float thr2, f2& b) {
+    const double X = bb[0], Y = bb[1], MX = bb[2], MY = bb[3];
+    const double u = 0x1p-24, t = kCertT;
+    const double Bu = fabs((double)h[0]) * X + fabs((double)h[1]) * Y + fabs((double)h[2]);
+    const double Bv = fabs((double)h[3]) * X + fabs((double)h[4]) * Y + fabs((double)h[5]);
+    const double Bw = fabs((double)h[6]) * X + fabs((double)h[7]) * Y + 1.0;
+    const double Gx = Bu + MX * Bw + 0x1p-40, Gy = Bv + MY * Bw + 0x1p-40;
+    const double T = (double)thr2;
+    const bool ok = X <= 0x1p40 && Y <= 0x1p40 && MX <= 0x1p40 && MY <= 0x1p40 && Bw <= 0x1p50 &&
+                    Gx <= 0x1p50 && Gy <= 0x1p50 && T >= 0x1p-100 && T <= 0x1p20;   // false for NaN
+    const double cx = 7.5 * u * Gx, cy = 7.5 * u * Gy, cw = 5.1 * u * Bw;
+    const double C = cx * cx + cy * cy, Cw = cw * cw;
+    const double tiny = 0x1p-120 + 0x1p-140 * Bw * Bw;
+    const double bin = (1.0 + 2 * kCertSlop) * ((1.0 + 1.0 / t) * C + T * Cw / t) + tiny;
+    const double bout = (1.0 + 2 * kCertSlop) / (1.0 - t) * (C / t + T * (1.0 + 1.0 / t) * Cw) + tiny;
+    b = f2{__double2float_rd(-bin), __double2float_ru(bout)};
+    return ok;
+}
+
+// Unpacked model k (for the exact fallback): h[0..7] from the coefficient pairs.
+template <int K>
+__device__ __forceinline__ void h_cert_model(const f2 (&hp)[K][4], int k, float (&h)[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        h[2 * j] = hp[k][j].x;
+        h[2 * j + 1] = hp[k][j].y;
+    }
+}
+
+// One pair of correspondences against one model: certified in / out lane masks per half.
+// a = {a_in, a_out} (shared), b = the model's {-b_in, b_out}.
+__device__ __forceinline__ void h_cert_eval(f2 p0, f2 p1, f2 p2, f2 p3, f2 c, f2 a, f2 b, const HPair& q, f2 one,
+                                            uint64_t& inx, uint64_t& iny, uint64_t& outx, uint64_t& outy) {
+    const f2 W = pk_fma(lo(p3), q.x, pk_fma(hi(p3), q.y, one));      // fma(h6,x,fma(h7,y,1))
+    const f2 U = pk_fma(lo(p0), q.x, pk_fma(hi(p0), q.y, lo(c)));    // fma(h0,x,fma(h1,y,h2))
+    const f2 V = pk_fma(hi(p1), q.x, pk_fma(lo(p2), q.y, hi(c)));    // fma(h3,x,fma(h4,y,h5))
+    const f2 DX = pk_fma(-q.mx, W, U);
+    const f2 DY = pk_fma(-q.my, W, V);
+    const f2 L = pk_fma(DX, DX, DY * DY);
+    const f2 W2 = W * W;
+    const f2 I = pk_fma(W2, lo(a), L);
+    const f2 O = pk_fma(W2, hi(a), L);
+    inx = __builtin_amdgcn_ballot_w64(I.x < b.x);
+    iny = __builtin_amdgcn_ballot_w64(I.y < b.x);
+    outx = __builtin_amdgcn_ballot_w64(O.x > b.y);
+    outy = __builtin_amdgcn_ballot_w64(O.y > b.y);
+}
+
+// One trip: NP pairs per lane against the wave's K models. vx / vy: lanes whose first / second
+// correspondence of pair slot j exists (all ones in full trips).
+// One trip: NP pairs per lane against the wave's K models. vx / vy: lanes whose first / second
+// correspondence of pair slot j exists (all ones in full trips). Returns the mask of models with
+// an undecided lane in this trip (bit k); their certified counts are already in cnt.
+template <int K, int NP, bool PRED, int DIAG = 0>
+__device__ __forceinline__ uint32_t h_cert_trip(f2 (&hp)[K][4], const f2 (&hc)[K], f2 a, const f2 (&cb)[K],
+                                                const HPair (&q)[NP], const uint64_t (&vx)[NP],
+                                                const uint64_t (&vy)[NP], f2 one, uint32_t (&cnt)[K]) {
+    uint32_t undecided = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        // re-defined in place every trip (no copy): the loop cannot hoist the broadcasts, so each use
+        // reads the SGPR pair through op_sel
+        asm volatile("" : "+s"(hp[k][0]), "+s"(hp[k][1]), "+s"(hp[k][2]), "+s"(hp[k][3]));
+        uint64_t dec = ~0ull;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            uint64_t inx, iny, outx, outy;
+            h_cert_eval(hp[k][0], hp[k][1], hp[k][2], hp[k][3], hc[k], a, cb[k], q[j], one, inx, iny, outx, outy);
+            if constexpr (PRED) {
+                inx &= vx[j];
+                iny &= vy[j];
+                dec &= (inx | outx | ~vx[j]) & (iny | outy | ~vy[j]);
+            } else if constexpr (DIAG < 2) {
+                dec &= (inx | outx) & (iny | outy);
+            }
+            cnt[k] += (uint32_t)__popcll(inx) + (uint32_t)__popcll(iny);
+        }
+        undecided |= (dec != ~0ull) ? (1u << k) : 0u;
+    }
+    return DIAG >= 1 ? 0u : undecided;
+}
+
+// The exact op-by-op error (IEEE division) for the undecided lanes of model k at the trip starting
+// at pair `base` (re-read from memory; validity from the pair counts). Returns their inlier count.
+template <int NP>
+__device__ __noinline__ uint32_t h_cert_resolve(const HPair* __restrict__ pairs, int nPairs, int nComplete, int base,
+                                                const HModelF* __restrict__ models, int hk, f2 a, f2 b, float thr2) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t me = 1ull << lane;
+    const f2* mp = (const f2*)&models[hk];
+    const f2 m0 = mp[0], m1 = mp[1], m2 = mp[2], m3 = mp[3];
+    const float h[8] = {m0.x, m0.y, m1.x, m1.y, m2.x, m2.y, m3.x, m3.y};
+    const f2 one = f2{1.f, 1.f};
+    uint32_t add = 0;
+    for (int j = 0; j < NP; ++j) {
+        const int p = base + 64 * j + lane;
+        const uint64_t vx = __builtin_amdgcn_ballot_w64(p < nPairs), vy = __builtin_amdgcn_ballot_w64(p < nComplete);
+        const HPair q = pairs[p < nPairs ? p : 0];
+        uint64_t inx, iny, outx, outy;
+        h_cert_eval(m0, m1, m2, m3, f2{m1.x, m2.y}, a, b, q, one, inx, iny, outx, outy);
+        const uint64_t ax = vx & ~(inx | outx), ay = vy & ~(iny | outy);
+        bool ex = false, ey = false;
+        if (ax & me) ex = h_error(h, q.x.x, q.y.x, q.mx.x, q.my.x) <= thr2;
+        if (ay & me) ey = h_error(h, q.x.y, q.y.y, q.mx.y, q.my.y) <= thr2;
+        add += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(ex)) + (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(ey));
+    }
+    return add;
+}
+
+// A wave whose models or point set leave the bound's domain marks its valid slots kStatusRedo
+// (recounted by the exact scalar sweep mcv_h_verify<.., false> with redo = 1), as does a wave
+// whose undecided trips overflow its event list. Trips with undecided lanes are only recorded in
+// the sweep (LDS event list: trip base << 8 | model mask) and resolved after it, so the exact
+// division stays out of the sweep's registers.
+// nComplete = N / 2 pairs hold two correspondences; pair nComplete (odd N) holds one.
+static constexpr int kCertEvents = 256;   // per wave
+
+template <int K, int NP, int DIAG = 0>
+__global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict__ pairs, int nPairs, int nComplete,
+                                                         const HModelF* __restrict__ models, int* __restrict__ counts,
+                                                         int hypCount, float thr2, HCertSlopes slopes,
+                                                         const double* __restrict__ bb) {
+    static_assert(K <= 8, "model mask in 8 bits");
+    __shared__ uint32_t events[4][kCertEvents];
+    __shared__ f2 offsets[4][K];
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    const int wib = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int h0 = wave * K;
+    if (h0 >= hypCount) return;
+
+    f2 hp[K][4], hc[K], cb[K];
+    bool valid[K];
+    bool fast = true;
+    double b4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b4[j] = bb[j];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int hk = h0 + k;
+        valid[k] = (hk < hypCount) && (counts[hk] >= 0);
+        const f2* mp = (const f2*)&models[hk < hypCount ? hk : hypCount - 1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hp[k][j] = mp[j];
+        hc[k] = f2{hp[k][1].x, hp[k][2].y};
+        float h[8];
+        h_cert_model<K>(hp, k, h);
+        const bool ok = h_cert_offsets(h, b4, thr2, cb[k]);
+        fast = fast && (ok || !valid[k]);
+        if (lane == 0) offsets[wib][k] = cb[k];
+        // VGPR-resident: hc meets an SGPR coefficient in the same op (constant-bus limit), cb is
+        // the VGPR operand of the e32 compares
+        asm volatile("" : "+v"(hc[k]), "+v"(cb[k]));
+    }
+    const f2 one = f2{1.f, 1.f};
+    uint32_t cnt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt[k] = 0;
+    int nev = 0;
+    if (fast) {
+        constexpr int TRIP = 64 * NP;
+        const int nFull = nComplete / TRIP * TRIP;
+        uint64_t all[NP];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) all[j] = ~0ull;
+        for (int base = 0; base < nFull; base += TRIP) {
+            HPair q[NP];
+#pragma unroll
+            for (int j = 0; j < NP; ++j) q[j] = pairs[base + 64 * j + lane];
+            const uint32_t und = h_cert_trip<K, NP, false, DIAG>(hp, hc, slopes.a, cb, q, all, all, one, cnt);
+            if (__builtin_expect(und != 0, 0)) {
+                if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)base << 8) | und;
+                ++nev;
+            }
+        }
+        for (int base = nFull; base < nPairs; base += TRIP) {
+            HPair q[NP];
+            uint64_t vx[NP], vy[NP];
+#pragma unroll
+            for (int j = 0; j < NP; ++j) {
+                const int p = base + 64 * j + lane;
+                vx[j] = __builtin_amdgcn_ballot_w64(p < nPairs);
+                vy[j] = __builtin_amdgcn_ballot_w64(p < nComplete);
+                q[j] = pairs[p < nPairs ? p : 0];
+            }
+            const uint32_t und = h_cert_trip<K, NP, true, DIAG>(hp, hc, slopes.a, cb, q, vx, vy, one, cnt);
+            if (und != 0) {
+                if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)base << 8) | und;
+                ++nev;
+            }
+        }
+        if (nev > kCertEvents) fast = false;   // too many to resolve here: exact recount of the wave
+        else if (nev > 0) {
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            for (int e = 0; e < nev; ++e) {
+                const uint32_t ev = __builtin_amdgcn_readfirstlane(events[wib][e]);
+                const int base = (int)(ev >> 8);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    if (!(ev & (1u << k))) continue;
+                    const int hk = h0 + k < hypCount ? h0 + k : hypCount - 1;
+                    cnt[k] += h_cert_resolve<NP>(pairs, nPairs, nComplete, base, models, hk, slopes.a,
+                                                 offsets[wib][k], thr2);
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid[k]) counts[h0 + k] = fast ? (int)cnt[k] : kStatusRedo;
     }
 }
 
@@ -709,6 +962,49 @@ static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d
         case 30: launch_h_verify_pk_k<6, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
         default: return false;
     }
+}
+
+template <int K, int NP, int DIAG = 0>
+static void launch_h_verify_cert_k(const void* d_pairs, int N, const void* d_models, int* d_counts, int hypCount,
+                                   float thr2, const double* d_bb, hipStream_t s) {
+    const int waves = (hypCount + K - 1) / K;
+    const int blocks = (waves + 3) / 4;
+    hipLaunchKernelGGL((mcv_h_verify_cert<K, NP, DIAG>), dim3(blocks), dim3(256), 0, s, (const HPair*)d_pairs, (N + 1) / 2,
+                       N / 2, (const HModelF*)d_models, d_counts, hypCount, thr2, h_cert_slopes_host(thr2), d_bb);
+}
+
+// Certified sweep shape (models per wave K, pairs per lane per trip NP); MCV_HCERT_VARIANT selects
+// an alternative for the variant screen (tests / bench only).
+static int cert_variant() {
+    static int v = [] {
+        const char* e = getenv("MCV_HCERT_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+// Certified sweep of the op-by-op error + the exact recount of the slots it marks kStatusRedo.
+void launch_h_verify_certified(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
+                               int hypCount, float thr2, const double* d_bb, hipStream_t s) {
+    switch (cert_variant()) {
+        case 1: launch_h_verify_cert_k<6, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 2: launch_h_verify_cert_k<4, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 3: launch_h_verify_cert_k<8, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 4: launch_h_verify_cert_k<4, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 5: launch_h_verify_cert_k<6, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 6: launch_h_verify_cert_k<5, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 7: launch_h_verify_cert_k<3, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 8: launch_h_verify_cert_k<4, 4>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 20: launch_h_verify_cert_k<4, 2, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 21: launch_h_verify_cert_k<4, 2, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 22: launch_h_verify_cert_k<8, 2, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 23: launch_h_verify_cert_k<6, 2, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        default: launch_h_verify_cert_k<8, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s);
+    }
+    static const bool noredo = getenv("MCV_HCERT_NOREDO") != nullptr;   // diagnostics only
+    if (noredo) return;
+    launch_h_verify_kp<kVerifyHypPerWave, kVerifyPtsPerLane>(d_pts4, N, d_models, d_counts, hypCount, thr2, false,
+                                                             nullptr, s, 1);
 }
 
 void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uint64_t* d_pkey, int64_t* d_pfail,

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cfloat>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 #include <algorithm>
 #include <memory>
@@ -180,7 +181,15 @@ void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst,
 }
 
 double effective_threshold(const RansacConfig& cfg) { return cfg.threshold > 0 ? cfg.threshold : 3.0; }
-bool fused_error(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_UNFUSED_ERROR) == 0; }
+bool fused_error(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_ERROR) != 0; }
+// MCV_HCERT_VARIANT=-1: run the scalar op-by-op sweep instead of the certified one (screen / A-B only)
+bool h_sweep_scalar_only() {
+    static const bool v = [] {
+        const char* e = getenv("MCV_HCERT_VARIANT");
+        return e && atoi(e) < 0;
+    }();
+    return v;
+}
 
 // HomographyEstimatorCallback::runKernel over the masked correspondences (mask == NULL: all).
 bool h_refit(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipStream_t s, double* H) {
@@ -314,15 +323,25 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
     const float thr2 = (float)(t * t);
     if (P.model == MCV_MODEL_HOMOGRAPHY) {
         const bool fused = fused_error(cfg);
+        P.pairs.ensure((size_t)(N + 1) / 2 * 8);
+        launch_h_pair(d_pts, N, P.pairs.p, s);
         if (fused) {
             launch_bbox(d_pts, N, P.bbox.p, s);
-            P.pairs.ensure((size_t)(N + 1) / 2 * 8);
-            launch_h_pair(d_pts, N, P.pairs.p, s);
+        } else {
+            P.bb4.ensure(4);
+            launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         }
         launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
         ProfScope ps("h_verify", s);
-        if (!fused || !launch_h_verify_packed(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bbox.p, s))
-            launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, fused, P.bbox.p, s);
+        if (!fused) {
+            // default: OpenCV's op-by-op error, certified division-free packed sweep
+            if (h_sweep_scalar_only())
+                launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, false, nullptr, s);
+            else
+                launch_h_verify_certified(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bb4.p, s);
+        } else if (!launch_h_verify_packed(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bbox.p, s)) {
+            launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, true, P.bbox.p, s);
+        }
     } else {
         launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
         P.bb4.ensure(4);

@@ -131,7 +131,8 @@ extern "C" MCV_API long long mcvTestDivF64(int mode, unsigned long long seed, lo
 // Run the homography inlier sweep on caller-supplied fp32 models (host arrays): exercises the
 // rare exact-division paths of mcv_h_verify with crafted models (zero / denormal / huge
 // denominators) that random hypotheses practically never produce. fused: 0 = op-by-op error,
-// 1 = fused error (scalar sweep), 2 = fused error through the packed sweep mcv_h_verify_pk.
+// 1 = fused error (scalar sweep), 2 = fused error through the packed sweep mcv_h_verify_pk,
+// 3 = op-by-op error through the certified sweep mcv_h_verify_cert (the default path).
 extern "C" MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models8, int nModels,
                                               float thr2, int fused, int* counts) {
     MCV_GUARD(0, {
@@ -147,7 +148,16 @@ extern "C" MCV_API int mcvTestHomographySweep(const float* pts4, int N, const fl
         MCV_HIP(hipMemcpy(m.p, models8, (size_t)nModels * 32, hipMemcpyHostToDevice));
         MCV_HIP(hipMemset(c.p, 0, (size_t)nModels * 4));
         launch_bbox(p.p, N, bb.p, 0);
-        if (fused == 2) {   // packed sweep + exact recount of the slots it marks kStatusRedo
+        if (fused == 3) {   // certified op-by-op sweep + exact recount of the slots it marks kStatusRedo
+            DevBuf<float> pairs;
+            DevBuf<double> b4;
+            pairs.ensure((size_t)(N + 1) / 2 * 8);
+            b4.ensure(4);
+            launch_h_pair(p.p, N, pairs.p, 0);
+            launch_abs_bound4(p.p, false, N, b4.p, nullptr, 0);
+            launch_h_verify_certified(p.p, pairs.p, N, m.p, c.p, nModels, thr2, b4.p, 0);
+            MCV_HIP(hipDeviceSynchronize());
+        } else if (fused == 2) {   // packed sweep + exact recount of the slots it marks kStatusRedo
             DevBuf<float> pairs;
             pairs.ensure((size_t)(N + 1) / 2 * 8);
             launch_h_pair(p.p, N, pairs.p, 0);

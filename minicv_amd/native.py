@@ -70,7 +70,7 @@ METHOD_LSQ = 0
 METHOD_RANSAC = 8
 FLAG_FIXED_ITERS = 1
 FLAG_NO_REFINE = 2
-FLAG_UNFUSED_ERROR = 4
+FLAG_FUSED_ERROR = 4
 FERR_SAMPSON = 0
 FERR_EPIPOLAR = 1
 MODEL_HOMOGRAPHY = 0

@@ -27,11 +27,11 @@ class RansacParams:
     fixed_iters: bool = False
     refine: bool = True
     error_kind: int = N.FERR_SAMPSON
-    unfused_error: bool = False
+    fused_error: bool = False   # opt-in FMA-contracted error (default: OpenCV op-by-op order)
 
     def to_c(self) -> N.RansacConfig:
         flags = (N.FLAG_FIXED_ITERS if self.fixed_iters else 0) | (0 if self.refine else N.FLAG_NO_REFINE) | \
-            (N.FLAG_UNFUSED_ERROR if self.unfused_error else 0)
+            (N.FLAG_FUSED_ERROR if self.fused_error else 0)
         return N.RansacConfig(self.threshold, self.confidence, int(self.max_iters), int(self.method),
                               int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(self.device_count), flags,
                               int(self.error_kind), 0)

@@ -477,7 +477,7 @@ int orc_find_homography(const double* src, const double* dst, int N, double thr,
         int bc = 0;
         int* cnts = (int*)malloc(sizeof(int) * (size_t)niters);
         /* counts for every hypothesis up front (parallel), replay sequentially */
-        const int fused = (flags & ORC_FLAG_UNFUSED_ERROR) == 0;
+        const int fused = (flags & ORC_FLAG_FUSED_ERROR) != 0;
         orc_h_counts(pts, N, seed, 0, niters, thr2, fused, cnts, nthreads);
         best = orc_ransac_replay(cnts, niters, N, 4, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0, &bc);
         free(cnts);
@@ -746,7 +746,7 @@ int orc_find_fundamental(const double* a, const double* b, int N, double thr, do
         }
     } else {
         const float thr2 = (float)(thr * thr);
-        const int kind = (errorKind == 1 ? 2 : 0) + ((flags & ORC_FLAG_UNFUSED_ERROR) ? 1 : 0);
+        const int kind = (errorKind == 1 ? 2 : 0) + ((flags & ORC_FLAG_FUSED_ERROR) ? 0 : 1);
         int64_t niters = maxIters > 1 ? maxIters : 1;
         int* cnts = (int*)malloc(sizeof(int) * (size_t)niters);
         orc_f_counts(pts, N, seed, 0, niters, thr2, kind, cnts, nthreads);

@@ -421,7 +421,7 @@ int orc_find_essential(const double* a, const double* b, int N, double focal, do
     }
     double t = thr / ((focal + focal) / 2);
     float thr2 = (float)(t * t);
-    int kind = (flags & ORC_FLAG_UNFUSED_ERROR) ? 1 : 0, result = 0;
+    int kind = (flags & ORC_FLAG_FUSED_ERROR) ? 0 : 1, result = 0;
     if (N == 5) {
         double x1[5], y1[5], x2[5], y2[5], Es[EMAX * 9];
         for (int i = 0; i < 5; ++i) { x1[i] = pts[4 * i]; y1[i] = pts[4 * i + 1]; x2[i] = pts[4 * i + 2]; y2[i] = pts[4 * i + 3]; }

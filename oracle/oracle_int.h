@@ -10,7 +10,7 @@
 
 #define ORC_FLAG_FIXED_ITERS 1
 #define ORC_FLAG_NO_REFINE 2
-#define ORC_FLAG_UNFUSED_ERROR 4
+#define ORC_FLAG_FUSED_ERROR 4
 
 /* Per-hypothesis word stream: word s = philox({s/4, hyp_lo, hyp_hi, "MCV1"}, {seed_lo, seed_hi})[s%4] */
 typedef struct { uint64_t seed, hyp; uint64_t pos; uint32_t buf[4]; } Stream;

@@ -399,7 +399,7 @@ int orc_solve_pnp_ransac(const double* img, const double* world, int N, const do
         p[3] = (float)img[2 * i]; p[4] = (float)img[2 * i + 1];
     }
     Cam c = cam_of(cam8);
-    int fused = !(flags & ORC_FLAG_UNFUSED_ERROR), result = 0;
+    int fused = (flags & ORC_FLAG_FUSED_ERROR) != 0, result = 0;
     float thr2 = (float)(thr * thr);
     double R[9], t[3];
     if (N == 4) {

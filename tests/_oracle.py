@@ -92,7 +92,7 @@ def h_hypothesis(pts4: np.ndarray, seed: int, hyp: int):
     return st, H, hf, idx
 
 
-def h_count(pts4: np.ndarray, hf: np.ndarray, thr2: float, want_mask: bool = False, fused: bool = True):
+def h_count(pts4: np.ndarray, hf: np.ndarray, thr2: float, want_mask: bool = False, fused: bool = False):
     hf = np.ascontiguousarray(hf, dtype=np.float32)
     m = np.zeros(pts4.shape[0], dtype=np.uint8) if want_mask else None
     n = load().orc_h_count(ptr(pts4), pts4.shape[0], ptr(hf), thr2, ptr(m) if want_mask else None, int(fused))
@@ -100,7 +100,7 @@ def h_count(pts4: np.ndarray, hf: np.ndarray, thr2: float, want_mask: bool = Fal
 
 
 def h_counts(pts4: np.ndarray, seed: int, begin: int, count: int, thr2: float, nthreads: int = 0,
-             fused: bool = True) -> np.ndarray:
+             fused: bool = False) -> np.ndarray:
     out = np.zeros(count, dtype=np.int32)
     load().orc_h_counts(ptr(pts4), pts4.shape[0], seed, begin, count, thr2, int(fused), ptr(out), nthreads)
     return out
@@ -286,13 +286,13 @@ def pnp_hypothesis(pts8, c8, seed, hyp):
     return st, R.reshape(3, 3), t, idx
 
 
-def pnp_counts(pts8, c8, seed, begin, count, thr2, fused=True, nthreads=0):
+def pnp_counts(pts8, c8, seed, begin, count, thr2, fused=False, nthreads=0):
     out = np.zeros(count, dtype=np.int32)
     load().orc_pnp_counts(ptr(pts8), pts8.shape[0], ptr(c8), seed, begin, count, thr2, int(fused), ptr(out), nthreads)
     return out
 
 
-def pnp_count(pts8, c8, R, t, thr2, fused=True):
+def pnp_count(pts8, c8, R, t, thr2, fused=False):
     R = np.ascontiguousarray(R, dtype=np.float64).ravel()
     t = np.ascontiguousarray(t, dtype=np.float64)
     m = np.zeros(pts8.shape[0], dtype=np.uint8)

@@ -59,7 +59,7 @@ def test_e_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count,
     np.testing.assert_array_equal(pts.cpu().numpy(), ref_pts)          # normalisation on the GPU
     plan = D.RansacPlan(N.MODEL_ESSENTIAL, n, count)
     thr = 1.0 / FOCAL                                                  # device API: normalised units
-    cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     counts = torch.zeros(count * N.E_SLOTS, dtype=torch.int32, device=dev)
     plan.evaluate(pts, n, cfg, begin, count, key, counts)
@@ -76,12 +76,12 @@ def test_e_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count,
 @pytest.mark.parametrize("n,outl,seed,iters,conf,flags", [
     (6, 0.0, 1, 1000, 0.999, 0), (50, 0.3, 2, 1000, 0.999, 0), (500, 0.5, 3, 1000, 0.999, 0),
     (3000, 0.5, 4, 1000, 0.999, 0), (3000, 0.6, 5, 300, 0.999, N.FLAG_FIXED_ITERS),
-    (2000, 0.5, 6, 1000, 0.99, N.FLAG_UNFUSED_ERROR), (20000, 0.5, 7, 1000, 0.999, 0)])
+    (2000, 0.5, 6, 1000, 0.99, N.FLAG_FUSED_ERROR), (20000, 0.5, 7, 1000, 0.999, 0)])
 def test_find_essential_vs_oracle(gpu, oracle, n, outl, seed, iters, conf, flags):
     a, b, inl, R, tu, E = S.essential_problem(n, seed=seed, outlier_frac=outl)
     p = opencv.RansacParams(threshold=1.0, confidence=conf, max_iters=iters, seed=seed,
                             fixed_iters=bool(flags & N.FLAG_FIXED_ITERS),
-                            unfused_error=bool(flags & N.FLAG_UNFUSED_ERROR))
+                            fused_error=bool(flags & N.FLAG_FUSED_ERROR))
     cnt, Eg, mask = opencv.findEssentialMat(a, b, FOCAL, PP, p)
     rc, Er, rmask, best = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=conf, max_iters=iters, seed=seed,
                                                 flags=flags)
@@ -197,7 +197,7 @@ def test_e_counts_at_exact_threshold_boundary(torch_dev, oracle):
         target = np.float32(np.quantile(err, q, method="nearest"))
         thr = _thr_for(target)
         for unfused in (True, False):
-            cfg = opencv.RansacParams(threshold=thr, seed=13, unfused_error=unfused).to_c()
+            cfg = opencv.RansacParams(threshold=thr, seed=13, fused_error=not unfused).to_c()
             key = torch.zeros(2, dtype=torch.int64, device=dev)
             counts = torch.zeros(32 * N.E_SLOTS, dtype=torch.int32, device=dev)
             plan.evaluate(pts, 3000, cfg, 0, 32, key, counts)
@@ -226,7 +226,7 @@ def test_e_counts_prefilter_extremes(torch_dev, oracle, case):
     ref_pts = oracle.pack_e(a, b, FOCAL, PP)
     plan = D.RansacPlan(N.MODEL_ESSENTIAL, n, count)
     for unfused in (False, True):
-        cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+        cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused).to_c()
         key = torch.zeros(2, dtype=torch.int64, device=dev)
         counts = torch.zeros(count * N.E_SLOTS, dtype=torch.int32, device=dev)
         plan.evaluate(pts, n, cfg, 0, count, key, counts)

@@ -34,7 +34,7 @@ def test_f_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, erro
     pts = D.pack_points_tensor(a, b, dev)
     plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, n, count)
     thr = 5e-3
-    cfg = opencv.RansacParams(threshold=thr, seed=seed, error_kind=error_kind, unfused_error=unfused).to_c()
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, error_kind=error_kind, fused_error=not unfused).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     counts = torch.zeros(count, dtype=torch.int32, device=dev)
     plan.evaluate(pts, n, cfg, begin, count, key, counts)
@@ -54,7 +54,7 @@ def test_f_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, erro
 @pytest.mark.parametrize("n,outl,seed,iters,conf,error_kind,flags", [
     (8, 0.0, 1, 1000, 0.99, 0, 0), (50, 0.3, 2, 1000, 0.99, 0, 0), (500, 0.5, 4, 1000, 0.99, 0, 0),
     (3000, 0.5, 5, 2000, 0.99, 0, 0), (3000, 0.5, 6, 2000, 0.99, 1, 0),
-    (2000, 0.5, 7, 500, 0.99, 0, N.FLAG_FIXED_ITERS), (2000, 0.5, 8, 1000, 0.999, 1, N.FLAG_UNFUSED_ERROR)])
+    (2000, 0.5, 7, 500, 0.99, 0, N.FLAG_FIXED_ITERS), (2000, 0.5, 8, 1000, 0.999, 1, N.FLAG_FUSED_ERROR)])
 def test_find_fundamental_vs_oracle(gpu, oracle, n, outl, seed, iters, conf, error_kind, flags):
     a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=outl)
     thr = 5e-3
@@ -62,7 +62,7 @@ def test_find_fundamental_vs_oracle(gpu, oracle, n, outl, seed, iters, conf, err
                                                     flags=flags, error_kind=error_kind)
     p = opencv.RansacParams(threshold=thr, confidence=conf, max_iters=iters, seed=seed, error_kind=error_kind,
                             fixed_iters=bool(flags & N.FLAG_FIXED_ITERS),
-                            unfused_error=bool(flags & N.FLAG_UNFUSED_ERROR))
+                            fused_error=bool(flags & N.FLAG_FUSED_ERROR))
     cnt, F, mask = opencv.findFundamentalMat(a, b, p)
     assert cnt == cnt_o
     np.testing.assert_array_equal(mask, mask_o.astype(bool))
@@ -140,7 +140,7 @@ def test_f_counts_at_exact_threshold_boundary(torch_dev, oracle, unfused):
     for q in (0.1, 0.5, 0.9):
         target = np.float32(np.quantile(err, q, method="nearest"))
         thr = _thr_for(target)
-        cfg = opencv.RansacParams(threshold=thr, seed=12, unfused_error=unfused).to_c()
+        cfg = opencv.RansacParams(threshold=thr, seed=12, fused_error=not unfused).to_c()
         key = torch.zeros(2, dtype=torch.int64, device=dev)
         counts = torch.zeros(64, dtype=torch.int32, device=dev)
         plan.evaluate(pts, 3000, cfg, 0, 64, key, counts)
@@ -176,7 +176,7 @@ def test_f_counts_prefilter_extremes(torch_dev, oracle, case):
     pts = D.pack_points_tensor(a, b, dev)
     plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, n, count)
     for unfused in (False, True):
-        cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+        cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused).to_c()
         key = torch.zeros(2, dtype=torch.int64, device=dev)
         counts = torch.zeros(count, dtype=torch.int32, device=dev)
         plan.evaluate(pts, n, cfg, 0, count, key, counts)

@@ -33,7 +33,7 @@ def device_counts(torch_dev, src, dst, seed, begin, count, thr, model=N.MODEL_HO
     from minicv_amd import device as D
     pts = D.pack_points_tensor(src, dst, dev)
     plan = D.RansacPlan(model, src.shape[0], count)
-    cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     counts = torch.zeros(count, dtype=torch.int32, device=dev)
     plan.evaluate(pts, src.shape[0], cfg, begin, count, key, counts)
@@ -89,8 +89,8 @@ CASES = [
     (5000, 0.9, 2e-3, 1e-2, 8, 20000, 0.999, 0),
     (777, 0.5, 0.0, 1e-4, 9, 2000, 0.995, 0),
     (20000, 0.5, 1e-3, 5e-3, 10, 2000, 0.995, 0),
-    (3000, 0.5, 1e-3, 5e-3, 11, 2000, 0.995, N.FLAG_UNFUSED_ERROR),
-    (200, 0.6, 1e-3, 5e-3, 12, 500, 0.995, N.FLAG_UNFUSED_ERROR | N.FLAG_FIXED_ITERS),
+    (3000, 0.5, 1e-3, 5e-3, 11, 2000, 0.995, N.FLAG_FUSED_ERROR),
+    (200, 0.6, 1e-3, 5e-3, 12, 500, 0.995, N.FLAG_FUSED_ERROR | N.FLAG_FIXED_ITERS),
 ]
 
 
@@ -101,7 +101,7 @@ def test_find_homography_vs_oracle(gpu, oracle, n, outl, sigma, thr, seed, iters
                                                         flags=flags)
     p = opencv.RansacParams(threshold=thr, confidence=conf, max_iters=iters, seed=seed,
                             fixed_iters=bool(flags & N.FLAG_FIXED_ITERS),
-                            unfused_error=bool(flags & N.FLAG_UNFUSED_ERROR))
+                            fused_error=bool(flags & N.FLAG_FUSED_ERROR))
     cnt, H, mask = opencv.findHomography(src, dst, p)
     assert cnt == cnt_o
     np.testing.assert_array_equal(mask, mask_o.astype(bool))

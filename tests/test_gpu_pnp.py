@@ -41,7 +41,7 @@ def test_pnp_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, di
     plan = D.RansacPlan(N.MODEL_PNP, n, count)
     plan.set_camera(K, d)
     thr = 2.0
-    cfg = opencv.RansacParams(threshold=thr, seed=seed, unfused_error=unfused).to_c()
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     counts = torch.zeros(count, dtype=torch.int32, device=dev)
     plan.evaluate(pts, n, cfg, begin, count, key, counts)
@@ -56,13 +56,13 @@ def test_pnp_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, di
 
 @pytest.mark.parametrize("n,outl,seed,iters,thr,dist,flags", [
     (50, 0.3, 1, 100, 2.0, None, 0), (3000, 0.5, 2, 100, 2.0, DIST, 0), (3000, 0.6, 3, 300, 3.0, None, 0),
-    (20000, 0.5, 4, 100, 2.0, DIST, 0), (2000, 0.5, 5, 200, 2.0, None, N.FLAG_FIXED_ITERS | N.FLAG_UNFUSED_ERROR),
+    (20000, 0.5, 4, 100, 2.0, DIST, 0), (2000, 0.5, 5, 200, 2.0, None, N.FLAG_FIXED_ITERS | N.FLAG_FUSED_ERROR),
     (2000, 0.5, 6, 200, 2.0, DIST, N.FLAG_NO_REFINE)])
 def test_solve_pnp_ransac_vs_oracle(gpu, oracle, n, outl, seed, iters, thr, dist, flags):
     img, W, inl, K, d, R, t = S.pnp_problem(n, seed=seed, outlier_frac=outl, sigma=0.3, dist=dist)
     p = opencv.RansacParams(threshold=thr, confidence=0.99, max_iters=iters, seed=seed,
                             fixed_iters=bool(flags & N.FLAG_FIXED_ITERS), refine=not (flags & N.FLAG_NO_REFINE),
-                            unfused_error=bool(flags & N.FLAG_UNFUSED_ERROR))
+                            fused_error=bool(flags & N.FLAG_FUSED_ERROR))
     ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, d, params=p)
     rc, rr, rt, rmask, best = oracle.solve_pnp_ransac(img, W, K, d, thr=thr, conf=0.99, max_iters=iters, seed=seed,
                                                       flags=flags)

@@ -41,9 +41,9 @@ def crafted_models():
     return np.stack(ms)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])   # op-by-op, fused scalar sweep, fused packed sweep
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])   # op-by-op scalar, fused scalar, fused packed, op-by-op certified
 def test_sweep_rare_paths_bit_exact(native, gpu, oracle, mode):
-    fused = mode != 0
+    fused = mode in (1, 2)
     rng = np.random.default_rng(1)
     n = 1000 + 77
     pts = rng.uniform(-1, 1, size=(n, 4)).astype(np.float32)
@@ -60,6 +60,84 @@ def test_sweep_rare_paths_bit_exact(native, gpu, oracle, mode):
     assert ok == 1, native.last_error()
     ref = np.array([oracle.h_count(pts, m, float(thr2), fused=fused) for m in models], np.int32)
     np.testing.assert_array_equal(counts, ref)
+
+
+def h_err_opcv(pts, h):
+    """HomographyEstimatorCallback::computeError op by op in float32 (numpy rounds every operation)."""
+    x, y, mx, my = (pts[:, i].astype(np.float32) for i in range(4))
+    h = h.astype(np.float32)
+    one = np.float32(1)
+    with np.errstate(all="ignore"):
+        ww = one / (h[6] * x + h[7] * y + one)
+        dx = (h[0] * x + h[1] * y + h[2]) * ww - mx
+        dy = (h[3] * x + h[4] * y + h[5]) * ww - my
+        return dx * dx + dy * dy
+
+
+def sweep(native, pts, models, thr2, mode):
+    counts = np.zeros(len(models), np.int32)
+    pts = np.ascontiguousarray(pts, np.float32)
+    models = np.ascontiguousarray(models, np.float32)
+    ok = native.lib().mcvTestHomographySweep(pts.ctypes.data, pts.shape[0], models.ctypes.data, len(models),
+                                             float(thr2), mode, counts.ctypes.data)
+    assert ok == 1, native.last_error()
+    return counts
+
+
+@pytest.mark.parametrize("n,scale,seed", [(1077, 1.0, 3), (4096, 1.0, 4), (2049, 640.0, 5), (33, 1.0, 6)])
+def test_certified_sweep_at_exact_thresholds(native, gpu, oracle, n, scale, seed):
+    """The certified division-free sweep (the default op-by-op path) against the oracle with thresholds
+    equal to actual float errors of the points, so that lanes sit exactly on the cut and the exact
+    fallback decides them; pixel-scale coordinates included."""
+    rng = np.random.default_rng(seed)
+    src = rng.uniform(-1, 1, size=(n, 2))
+    H = np.array([[1.02, -0.09, -0.16], [0.08, 1.04, -0.07], [0.40, 0.13, 1.0]])
+    p = np.c_[src, np.ones(n)] @ H.T
+    dst = p[:, :2] / p[:, 2:] + rng.normal(scale=2e-3, size=(n, 2))
+    dst[: n // 3] = rng.uniform(-1, 1, size=(n // 3, 2))
+    pts = (np.c_[src, dst] * scale).astype(np.float32)
+    ms = [H.ravel()[:8] / H[2, 2]]
+    for _ in range(31):
+        ms.append(ms[0] + rng.normal(scale=1e-3, size=8))
+    for _ in range(16):   # random hypotheses, some with the horizon w = 0 crossing the point set
+        ms.append(rng.normal(size=8) * np.array([1, 1, 1, 1, 1, 1, 2, 2]))
+    models = np.array(ms, np.float64)
+    if scale != 1.0:   # same geometry in pixel units: H' = S H S^-1
+        models[:, [2, 5]] *= scale
+        models[:, [6, 7]] /= scale
+    models = models.astype(np.float32)
+    for m in models[:4]:
+        e = h_err_opcv(pts, m)
+        for thr2 in (np.float32(np.median(e)), np.sort(e)[n // 2 + 3], np.float32((5e-3 * scale) ** 2)):
+            got = sweep(native, pts, models, thr2, 3)
+            ref = np.array([oracle.h_count(pts, mm, float(thr2), fused=False) for mm in models], np.int32)
+            np.testing.assert_array_equal(got, ref)
+            np.testing.assert_array_equal(ref, [(h_err_opcv(pts, mm) <= thr2).sum() for mm in models])
+
+
+def test_certified_sweep_near_horizon(native, gpu, oracle):
+    """Points on both sides of and right at the line w = 0 of each model (huge projected errors, w of
+    either sign, w = +-0 and denormal w): decided by the certified tests or the exact fallback."""
+    rng = np.random.default_rng(7)
+    n = 3001
+    models, pts = [], []
+    for _ in range(24):
+        h = rng.normal(size=8).astype(np.float32)
+        models.append(h)
+    models = np.array(models, np.float32)
+    x = rng.uniform(-1, 1, size=n).astype(np.float32)
+    h = models[0]
+    with np.errstate(all="ignore"):
+        y = ((-np.float32(1) - h[6] * x) / h[7]).astype(np.float32)   # on the horizon of model 0
+    y[::2] = np.nextafter(y[::2], np.float32(np.inf))
+    y[::3] = rng.uniform(-1, 1, size=y[::3].shape).astype(np.float32)
+    dst = rng.uniform(-50, 50, size=(n, 2)).astype(np.float32)
+    pts = np.c_[x, y, dst].astype(np.float32)
+    pts = pts[np.isfinite(pts).all(axis=1)]
+    for thr2 in (np.float32(1e-2), np.float32(25.0), np.float32(1e6)):
+        got = sweep(native, pts, models, thr2, 3)
+        ref = np.array([oracle.h_count(pts, m, float(thr2), fused=False) for m in models], np.int32)
+        np.testing.assert_array_equal(got, ref)
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])   # random n / reciprocal / exact quotients / domain ends
