@@ -43,26 +43,61 @@ P_THR_PX = 2.0
 THR = 5e-3
 SEED = 3
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue model of the packed sweep mcv_h_verify_pk<8,2> (fused error), per (hypothesis, pair of
-# correspondences): 12 v_pk_fma/mul_f32 (4 cycles each: two 32-lane passes per half), 2 v_rcp_f32
-# (quarter rate, 8 cycles), 2 v_cmp (2 cycles) + 1 v_min3_f32 of |w| (4 cycles) = 72 cycles = 36 per evaluation,
-# i.e. 18 issue slots of 2 cycles (wave64 on SIMD32). Peak evaluations/s = 256 CUs x 4 SIMDs x
-# 2.4 GHz / 2 x 64 lanes / 18.
-VALU_SLOTS_PER_EVAL = 18
-FP64_PEAK_TF = 78.6            # MI355X fp64 vector (spec)
-FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: fp32-input MFMA = fp32 vector peak
-# Hamming issue model (measured per-instruction costs, scripts/exp/valu_rate.hip): per 64 pairs
-# 8 x (v_xor_b32 2 + v_bcnt_u32_b32 4) + v_lshl_or_b32 4 + v_med3_u32 4 + v_min_u32 2 = 58 cycles.
-HAMMING_CYC_PER_WAVE_PAIR = 58
-HAMMING_PEAK_PAIRS = 256 * 4 * 2.4e9 / HAMMING_CYC_PER_WAVE_PAIR * 64
-VALU_PEAK_EVALS = 256 * 4 * 2.4e9 / 2 * 64 / VALU_SLOTS_PER_EVAL
-# VALU issue model of the certified packed-fp32 Sampson prefilter (sampson_pk.h; F and E sweeps),
-# per (model pair, correspondence): 17 v_pk_fma + 3 v_pk_mul + 2 v_pk_add (4 cycles each), 2 v_and
-# + 2 v_max_f32 (2 cycles), 4 v_cmp_f32 (VOP3, 4 cycles) = 112 cycles, i.e. 56 SIMD cycles per
-# 64 (model, correspondence) evaluations; the fp64 re-test of undecided lanes is ~1e-4 of them.
+# Roofs (MI355X_MICROARCH.md): fp32 vector = fp32-input MFMA = 157.3 TFLOP/s dense, fp64 vector 78.6;
+# the int32 VALU op rate is the fp32 FMA lane rate counted once per op (256 CUs x 4 SIMDs x 32 lanes
+# x 2.4 GHz).
+FP32_PEAK_TF = 157.3
+FP64_PEAK_TF = 78.6
+FP32_MFMA_PEAK_TF = 157.3
+INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# Algorithmic work per unit: homography computeError = 25 flops per (hypothesis,
+# correspondence) (3 dot products, 1 reciprocal, 2 sub, 2 mul, 1 add, 1 compare); Sampson error =
+# 34 fp64 flops per (model, correspondence) (F x1 12, F^T x2 8, x2^T F x1 4, denominator 7, c^2,
+# division, compare); Hamming = 24 int32 ops per (query, train) pair of 256-bit descriptors
+# (8 xor + 8 popcount + 7 add + 1 compare).
+H_FLOPS_PER_EVAL = 25
+SAMPSON_FLOPS_PER_EVAL = 34
+HAM_OPS_PER_PAIR = 24
+# Issue models (secondary: what the kernels' instruction streams allow at 2.4 GHz, SIMD cycles per
+# 64 evaluations; measured issue costs: VOP3/VOP3P 4 cycles, VOP2/VOPC e32 2, transcendental 8):
+#   mcv_h_verify_cert (default op-by-op error): per pair of correspondences 13 packed ops + 4 e32
+#     compares = 60 cycles -> 30 per evaluation;
+#   mcv_h_verify_pk (--fused): 12 packed + 2 v_rcp_f32 + v_min3 + 2 compares = 72 -> 36;
+#   Sampson prefilter (F, E): 56 per (model, correspondence); Hamming 58 per pair.
+H_CERT_CYC_PER_EVAL = 30
+H_PK_CYC_PER_EVAL = 36
 SPK_CYC_PER_WAVE_EVAL = 56
-SPK_PEAK_EVALS = 256 * 4 * 2.4e9 / SPK_CYC_PER_WAVE_EVAL * 64
+HAMMING_CYC_PER_WAVE_PAIR = 58
+SIMD_CYC_PER_S = 256 * 4 * 2.4e9
 
+
+def issue_peak(cycles_per_64: float) -> float:
+    """Evaluations / s when every SIMD issues the kernel's stream back to back (64 lanes per wave)."""
+    return SIMD_CYC_PER_S / cycles_per_64 * 64
+
+
+def host_cpu():
+    """The host the CPU baseline runs on: threads used (OMP_NUM_THREADS, which the GPU box sets to
+    its CPU share, else every core this process may run on), nproc and the CPU model."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return {"threads": env or aff, "nproc": os.cpu_count(), "affinity": aff, "model": model,
+            "threads_from": "OMP_NUM_THREADS" if env else "sched_getaffinity"}
+
+
+def cpu_threads() -> int:
+    return host_cpu()["threads"]
 
 
 def dist_setup(torch, dist):
@@ -108,7 +143,7 @@ def cpu_baseline(src, dst, target_s: float):
     import _oracle as O
     pts4 = O.pack4(src, dst)
     thr2 = float(np.float32(THR * THR))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    threads = cpu_threads()
     t = time.perf_counter()
     O.h_counts(pts4, SEED, 0, 4 * threads, thr2, threads)
     cal = (time.perf_counter() - t) / (4 * threads)
@@ -116,8 +151,8 @@ def cpu_baseline(src, dst, target_s: float):
     t = time.perf_counter()
     O.h_counts(pts4, SEED, 0, sample, thr2, threads)
     el = time.perf_counter() - t
-    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} hypotheses x {src.shape[0]} correspondences (sample+solve+fp32 count), "
+    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port", "host": host_cpu(),
+            "sample": f"{sample} hypotheses x {src.shape[0]} correspondences (sample+solve+fp32 op-by-op count), "
                       f"oracle/oracle.c, OpenMP {threads} threads, {el:.1f} s"}
 
 
@@ -127,15 +162,15 @@ def cpu_baseline_f(a, b, target_s: float):
     import _oracle as O
     pts4 = O.pack4(a, b)
     thr2 = float(np.float32(THR * THR))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    threads = cpu_threads()
     t = time.perf_counter()
-    O.f_counts(pts4, F_SEED, 0, 2 * threads, thr2, 0, threads)
+    O.f_counts(pts4, F_SEED, 0, 2 * threads, thr2, 1, threads)
     cal = (time.perf_counter() - t) / (2 * threads)
     sample = max(2 * threads, int(target_s / max(cal, 1e-6)))
     t = time.perf_counter()
-    O.f_counts(pts4, F_SEED, 0, sample, thr2, 0, threads)
+    O.f_counts(pts4, F_SEED, 0, sample, thr2, 1, threads)
     el = time.perf_counter() - t
-    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port",
+    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port", "host": host_cpu(),
             "sample": f"{sample} hypotheses x {a.shape[0]} correspondences (8-pt sample+solve+fp64 Sampson "
                       f"count), oracle/oracle.c, OpenMP {threads} threads, {el:.1f} s"}
 
@@ -198,17 +233,21 @@ def bench_matcher(args):
             ach = pairs / (avg_ms * 1e-3)
             line = {"metric": "BF Hamming knn-2 queries/sec, 10k x 10k 256-bit (BASELINE config[1])",
                     "value": nq * args.steps / el, "unit": "queries/s",
-                    "roofline": {"bound": "hbm", "achieved": 32.0 * pairs / (avg_ms * 1e-3) / 1e9,
-                                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                                 "frac": 32.0 * pairs / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                    "roofline": {"bound": "int-valu", "achieved": HAM_OPS_PER_PAIR * ach / 1e12,
+                                 "peak": INT32_PEAK_TOPS, "unit": "Tops/s",
+                                 "frac": HAM_OPS_PER_PAIR * ach / 1e12 / INT32_PEAK_TOPS,
                                  "traffic": load_traffic("mcv_hamming_partial", f"{nq}x{nt}"),
                                  "kernel": "mcv_hamming_partial", "avg_launch_ms": avg_ms,
-                                 "note": "algorithmic bytes = 32 B x Nt per query; data L2-resident, integer "
-                                         "VALU-bound (see valu)",
-                                 "valu": {"achieved": ach, "peak": HAMMING_PEAK_PAIRS, "unit": "pairs/s",
-                                          "frac": ach / HAMMING_PEAK_PAIRS,
-                                          "model": f"{HAMMING_CYC_PER_WAVE_PAIR} SIMD cycles per 64 (query, "
-                                                   "train) pairs at 2.4 GHz"}},
+                                 "model": f"{HAM_OPS_PER_PAIR} int32 ops per (query, train) pair of 256-bit "
+                                          "descriptors",
+                                 "hbm": {"effective_GBps": 32.0 * pairs / (avg_ms * 1e-3) / 1e9,
+                                         "peak": HBM_PEAK_GBPS,
+                                         "note": "32 B x Nt per query as if streamed; the 640 KB sets are "
+                                                 "L2-resident"},
+                                 "issue": {"achieved": ach, "peak": issue_peak(HAMMING_CYC_PER_WAVE_PAIR),
+                                           "unit": "pairs/s", "frac": ach / issue_peak(HAMMING_CYC_PER_WAVE_PAIR),
+                                           "model": f"{HAMMING_CYC_PER_WAVE_PAIR} SIMD cycles per 64 (query, "
+                                                    "train) pairs at 2.4 GHz"}},
                     "dtype": "u32", "scaling": "strong"}
         else:
             flops = 2.0 * cnt * nt * 128
@@ -229,13 +268,14 @@ def bench_matcher(args):
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, str(ROOT / "tests"))
             import _oracle as O
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+            threads = cpu_threads()
             sq = 2000 if ham else 200
             t1 = time.perf_counter()
             (O.match_hamming if ham else O.match_l2)(q[:sq], t, nthreads=threads)
             ct = time.perf_counter() - t1
             line["cpu_baseline"] = {"value": sq / ct if ham else 2.0 * sq * nt * 128 / ct / 1e12,
                                     "unit": "queries/s" if ham else "TFLOP/s", "cores": threads, "kind": "port",
+                                    "host": host_cpu(),
                                     "sample": f"{sq} queries x {nt} train, oracle/oracle.c, OpenMP {threads}"}
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -352,8 +392,12 @@ def bench_ransac(args):
         avg_ms = kms.value / max(launches, 1)
         alg_bytes = 16.0 * n * hyps            # per launch: every hypothesis reads all N float4 pairs
         achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-        traffic = load_traffic("mcv_f_verify" if fund else "mcv_h_verify_pk", f"{n}x{hyps}")
+        hkern = "mcv_h_verify_pk" if args.fused else "mcv_h_verify_cert"
+        traffic = load_traffic("mcv_f_verify_pk" if fund else hkern, f"{n}x{hyps}")
+        evals_per_s = n * hyps / (avg_ms * 1e-3)
         if not fund:
+            tf = H_FLOPS_PER_EVAL * evals_per_s / 1e12
+            cyc = H_PK_CYC_PER_EVAL if args.fused else H_CERT_CYC_PER_EVAL
             line = {
                 "metric": "RANSAC hypotheses/sec @100k corrs; achieved HBM GB/s vs roofline, 1/2/4/8 GPU",
                 "value": value,
@@ -370,22 +414,27 @@ def bench_ransac(args):
                 "config": {"workload": f"findHomography RANSAC, {n} correspondences x {hyps} hypotheses per GPU "
                                        f"(fixed iterations) + refit/LM, best model via RCCL all-reduce",
                            "correspondences": n, "hypotheses_per_gpu": hyps, "threshold": THR,
+                           "error": "fused (opt-in)" if args.fused else "OpenCV op-by-op (default)",
                            "parallelism": f"hypothesis-sharded dp{world}"},
-                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                             "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                             "kernel": "mcv_h_verify_pk", "avg_launch_ms": avg_ms, "launches": launches,
-                             "algorithmic_bytes_per_launch": alg_bytes,
-                             "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 6 "
-                                     "hypotheses; the sweep's binding roof is VALU issue (see valu)",
-                             "valu": {"achieved": n * hyps / (avg_ms * 1e-3), "peak": VALU_PEAK_EVALS,
-                                      "unit": "evaluations/s",
-                                      "frac": n * hyps / (avg_ms * 1e-3) / VALU_PEAK_EVALS,
-                                      "model": f"{VALU_SLOTS_PER_EVAL} VALU issue slots per (hypothesis, "
-                                               "correspondence) at 2.4 GHz"}},
+                "roofline": {"bound": "fp32-valu", "achieved": tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
+                             "frac": tf / FP32_PEAK_TF, "traffic": traffic,
+                             "kernel": hkern, "avg_launch_ms": avg_ms, "launches": launches,
+                             "flops_per_launch": H_FLOPS_PER_EVAL * n * hyps,
+                             "model": f"{H_FLOPS_PER_EVAL} flops per (hypothesis, correspondence) x {n} x {hyps} per "
+                                      "launch (SURVEY.md 8d)",
+                             "hbm": {"effective_GBps": alg_bytes / (avg_ms * 1e-3) / 1e9,
+                                     "algorithmic_bytes_per_launch": alg_bytes, "peak": HBM_PEAK_GBPS,
+                                     "note": "16 B x N per hypothesis as if streamed from HBM; the 1.6 MB point "
+                                             "set is L2-resident, measured HBM bytes per launch are `traffic`"},
+                             "issue": {"achieved": evals_per_s, "peak": issue_peak(2 * cyc), "unit": "evaluations/s",
+                                       "frac": evals_per_s / issue_peak(2 * cyc),
+                                       "model": f"{cyc} SIMD cycles per 32 (hypothesis, correspondence) "
+                                                "evaluations of the kernel's instruction stream at 2.4 GHz"}},
                 "result": {"best_count": result["count"], "best_hyp": result["idx"],
                            "refined_count": result["final_count"]},
             }
         else:
+            tf = SAMPSON_FLOPS_PER_EVAL * evals_per_s / 1e12
             line = {
                 "metric": "RANSAC hypotheses/sec, findFundamentalMat 8-pt @500k corrs (BASELINE config[3])",
                 "value": value,
@@ -403,16 +452,19 @@ def bench_ransac(args):
                                        f"hypotheses per call sharded over {world} GPU(s), fp64 Sampson error",
                            "correspondences": n, "hypotheses_total": total, "threshold": THR,
                            "parallelism": f"hypothesis-sharded dp{world}"},
-                "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                             "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                             "kernel": "mcv_f_verify", "avg_launch_ms": avg_ms, "launches": launches,
-                             "algorithmic_bytes_per_launch": alg_bytes,
-                             "note": "frac > 1: the 16 N-byte point set is L2-resident and each load serves 8 "
-                                     "models; the sweep's binding roof is VALU issue (see valu)",
-                             "valu": {"achieved": n * hyps / (avg_ms * 1e-3), "peak": SPK_PEAK_EVALS,
-                                      "unit": "evaluations/s", "frac": n * hyps / (avg_ms * 1e-3) / SPK_PEAK_EVALS,
-                                      "model": f"certified packed-fp32 Sampson prefilter: {SPK_CYC_PER_WAVE_EVAL} "
-                                               "SIMD cycles per 64 (model, correspondence) at 2.4 GHz"}},
+                "roofline": {"bound": "fp32-valu", "achieved": tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
+                             "frac": tf / FP32_PEAK_TF, "traffic": traffic,
+                             "kernel": "mcv_f_verify_pk", "avg_launch_ms": avg_ms, "launches": launches,
+                             "model": f"{SAMPSON_FLOPS_PER_EVAL} (fp64-definition) flops per (model, correspondence); "
+                                      "the sweep decides them with a certified packed-fp32 prefilter, so the fp32 "
+                                      "vector roof binds",
+                             "hbm": {"effective_GBps": alg_bytes / (avg_ms * 1e-3) / 1e9,
+                                     "algorithmic_bytes_per_launch": alg_bytes, "peak": HBM_PEAK_GBPS},
+                             "issue": {"achieved": evals_per_s, "peak": issue_peak(SPK_CYC_PER_WAVE_EVAL),
+                                       "unit": "evaluations/s",
+                                       "frac": evals_per_s / issue_peak(SPK_CYC_PER_WAVE_EVAL),
+                                       "model": f"certified packed-fp32 Sampson prefilter: {SPK_CYC_PER_WAVE_EVAL} "
+                                                "SIMD cycles per 64 (model, correspondence) at 2.4 GHz"}},
                 "result": {"best_count": result["count"], "best_hyp": result["idx"]},
             }
         if world == 1 and not args.no_cpu_baseline:
@@ -431,15 +483,15 @@ def cpu_baseline_e(pts4d, target_s: float):
     import _oracle as O
     thr = E_THR_PX / E_FOCAL
     thr2 = float(np.float32(thr * thr))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    threads = cpu_threads()
     t = time.perf_counter()
-    O.e_counts(pts4d, E_SEED, 0, 2 * threads, thr2, 0, threads)
+    O.e_counts(pts4d, E_SEED, 0, 2 * threads, thr2, 1, threads)
     cal = (time.perf_counter() - t) / (2 * threads)
     sample = max(2 * threads, int(target_s / max(cal, 1e-6)))
     t = time.perf_counter()
-    O.e_counts(pts4d, E_SEED, 0, sample, thr2, 0, threads)
+    O.e_counts(pts4d, E_SEED, 0, sample, thr2, 1, threads)
     el = time.perf_counter() - t
-    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port",
+    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port", "host": host_cpu(),
             "sample": f"{sample} hypotheses x {pts4d.shape[0]} correspondences (5-pt sample+solve, <= 10 models, "
                       f"fp64 Sampson count), oracle/oracle_e.c, OpenMP {threads} threads, {el:.1f} s"}
 
@@ -463,7 +515,7 @@ def bench_essential(args, world, rank, dev):
     pts = D.pack_essential_tensor(a, b, E_FOCAL, E_PP, dev)
     plan = D.RansacPlan(NL.MODEL_ESSENTIAL, n, hyps)
     cfg = opencv.RansacParams(threshold=E_THR_PX / E_FOCAL, confidence=0.999, max_iters=total, seed=E_SEED,
-                              fixed_iters=True).to_c()
+                              fixed_iters=True, fused_error=args.fused).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = torch.zeros(n, dtype=torch.uint8, device=dev)
     red = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -519,6 +571,7 @@ def bench_essential(args, world, rank, dev):
         v_ms = vms.value / max(vl, 1)
         g_ms = gms.value / max(gl, 1)
         alg_bytes = 16.0 * n * models            # each model reads all N float4 correspondences
+        e_tf = SAMPSON_FLOPS_PER_EVAL * n * models / (v_ms * 1e-3) / 1e12
         line = {
             "metric": "RANSAC hypotheses/sec, findEssentialMat 5-pt (cvRecoverPose path) @100k corrs",
             "value": total * args.steps / el, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
@@ -531,18 +584,19 @@ def bench_essential(args, world, rank, dev):
                        "parallelism": f"hypothesis-sharded dp{world}"},
             "kernels": {"mcv_e_generate": {"avg_launch_ms": g_ms, "launches": gl},
                         "mcv_e_verify": {"avg_launch_ms": v_ms, "launches": vl}},
-            "roofline": {"bound": "hbm", "achieved": alg_bytes / (v_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": alg_bytes / (v_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                         "traffic": load_traffic("mcv_e_verify", f"{n}x{hyps}"), "kernel": "mcv_e_verify",
+            "roofline": {"bound": "fp32-valu", "achieved": e_tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
+                         "frac": e_tf / FP32_PEAK_TF,
+                         "traffic": load_traffic("mcv_e_verify_pk", f"{n}x{hyps}"), "kernel": "mcv_e_verify_pk",
                          "avg_launch_ms": v_ms, "launches": vl, "models_per_launch": models,
-                         "algorithmic_bytes_per_launch": alg_bytes,
-                         "note": "frac > 1: the point set is L2-resident and each load serves 6 models; the "
-                                 "sweep reads the 16 N-byte float4 copy (32 N-byte double4 only for undecided "
-                                 "lanes) and is VALU-issue-bound (see valu)",
-                         "valu": {"achieved": n * models / (v_ms * 1e-3), "peak": SPK_PEAK_EVALS,
-                                  "unit": "evaluations/s", "frac": n * models / (v_ms * 1e-3) / SPK_PEAK_EVALS,
-                                  "model": f"certified packed-fp32 Sampson prefilter: {SPK_CYC_PER_WAVE_EVAL} SIMD "
-                                           "cycles per 64 (model, correspondence) at 2.4 GHz"}},
+                         "model": f"{SAMPSON_FLOPS_PER_EVAL} (fp64-definition) flops per (model, correspondence); "
+                                  "certified packed-fp32 prefilter, fp64 only for undecided lanes",
+                         "hbm": {"effective_GBps": alg_bytes / (v_ms * 1e-3) / 1e9,
+                                 "algorithmic_bytes_per_launch": alg_bytes, "peak": HBM_PEAK_GBPS},
+                         "issue": {"achieved": n * models / (v_ms * 1e-3), "peak": issue_peak(SPK_CYC_PER_WAVE_EVAL),
+                                   "unit": "evaluations/s",
+                                   "frac": n * models / (v_ms * 1e-3) / issue_peak(SPK_CYC_PER_WAVE_EVAL),
+                                   "model": f"certified packed-fp32 Sampson prefilter: {SPK_CYC_PER_WAVE_EVAL} SIMD "
+                                            "cycles per 64 (model, correspondence) at 2.4 GHz"}},
             "result": {"best_count": result["count"], "best_slot": result["slot"],
                        "final_count": result["final_count"]},
         }
@@ -562,15 +616,15 @@ def cpu_baseline_p(img, W, K, d, target_s: float):
     import _oracle as O
     pts8, c8 = O.pack_pnp(img, W), O.cam8(K, d)
     thr2 = float(np.float32(P_THR_PX * P_THR_PX))
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    threads = cpu_threads()
     t = time.perf_counter()
-    O.pnp_counts(pts8, c8, P_SEED, 0, 4 * threads, thr2, True, threads)
+    O.pnp_counts(pts8, c8, P_SEED, 0, 4 * threads, thr2, False, threads)
     cal = (time.perf_counter() - t) / (4 * threads)
     sample = max(4 * threads, int(target_s / max(cal, 1e-6)))
     t = time.perf_counter()
-    O.pnp_counts(pts8, c8, P_SEED, 0, sample, thr2, True, threads)
+    O.pnp_counts(pts8, c8, P_SEED, 0, sample, thr2, False, threads)
     el = time.perf_counter() - t
-    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port",
+    return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port", "host": host_cpu(),
             "sample": f"{sample} hypotheses x {img.shape[0]} correspondences (4-pt AP3P sample+solve, projectPoints "
                       f"fp32 error count), oracle/oracle_pnp.c, OpenMP {threads} threads, {el:.1f} s"}
 
@@ -596,7 +650,7 @@ def bench_pnp(args, world, rank, dev):
     plan = D.RansacPlan(NL.MODEL_PNP, n, hyps)
     plan.set_camera(K, d)
     cfg = opencv.RansacParams(threshold=P_THR_PX, confidence=0.99, max_iters=total, seed=P_SEED,
-                              fixed_iters=True).to_c()
+                              fixed_iters=True, fused_error=args.fused).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = torch.zeros(n, dtype=torch.uint8, device=dev)
     red = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -662,15 +716,14 @@ def bench_pnp(args, world, rank, dev):
                        "parallelism": f"hypothesis-sharded dp{world}"},
             "kernels": {"mcv_pnp_verify": {"avg_launch_ms": v_ms, "launches": vl,
                                            "evaluations_per_s": n * hyps / max(v_ms * 1e-3, 1e-12)}},
-            "roofline": {"bound": "hbm", "achieved": p_bytes / (v_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": p_bytes / (v_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "roofline": {"bound": "fp64-valu", "achieved": p_fl, "peak": FP64_PEAK_TF, "unit": "TFLOP/s",
+                         "frac": p_fl / FP64_PEAK_TF,
                          "traffic": load_traffic("mcv_pnp_verify", f"{n}x{hyps}"), "kernel": "mcv_pnp_verify",
-                         "avg_launch_ms": v_ms, "launches": vl, "algorithmic_bytes_per_launch": p_bytes,
-                         "note": "frac > 1: the 20 N-byte point set is L2-resident and each load serves 4 poses; "
-                                 "the sweep is fp64-VALU-bound (see fp64)",
-                         "fp64": {"achieved": p_fl, "peak": FP64_PEAK_TF, "unit": "TFLOP/s", "frac": p_fl / FP64_PEAK_TF,
-                                  "model": f"{P_FLOPS_PER_EVAL} fp64 FLOP per (hypothesis, correspondence), "
-                                           "a division counted as one"}},
+                         "avg_launch_ms": v_ms, "launches": vl,
+                         "model": f"{P_FLOPS_PER_EVAL} fp64 FLOP per (hypothesis, correspondence), a division "
+                                  "counted as one",
+                         "hbm": {"effective_GBps": p_bytes / (v_ms * 1e-3) / 1e9,
+                                 "algorithmic_bytes_per_launch": p_bytes, "peak": HBM_PEAK_GBPS}},
             "result": {"best_count": result["count"], "best_hyp": result["idx"],
                        "final_count": result["final_count"], "true_inliers": int(inl.sum())},
         }
@@ -749,7 +802,7 @@ def bench_scaled(args):
             "data": "synthetic (seeded lookAt camera + relative pose, 30% outlier observations, sigma 1e-3)",
             "config": {"workload": f"findScaled, {n} observations -> {cands} candidate scales, replicas on {world} "
                                    f"GPU(s)", "observations": n, "parallelism": f"replicas x{world}"},
-            "roofline": {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TF, "unit": "TFLOP/s",
+            "roofline": {"bound": "fp64-valu", "achieved": tf, "peak": FP64_PEAK_TF, "unit": "TFLOP/s",
                          "frac": tf / FP64_PEAK_TF, "traffic": None, "kernel": "mcv_scaled_costs",
                          "avg_launch_ms": avg_ms, "launches": launches,
                          "model": f"{S_FLOPS_PER_TERM} fp64 FLOP per (candidate, observation), a division "
@@ -759,7 +812,7 @@ def bench_scaled(args):
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, str(ROOT / "tests"))
             import _oracle as O_
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+            threads = cpu_threads()
             cam14 = np.concatenate([src.location, src.forward, src.up, src.right, src.focal])
             t1 = time.perf_counter()
             O_.scaled_costs_sample(cam14, W, O, pose.Rotation, pose.Translation, threads, threads)
@@ -769,6 +822,7 @@ def bench_scaled(args):
             O_.scaled_costs_sample(cam14, W, O, pose.Rotation, pose.Translation, sample, threads)
             ct = time.perf_counter() - t1
             line["cpu_baseline"] = {"value": sample / ct, "unit": "candidates/s", "cores": threads, "kind": "port",
+                                    "host": host_cpu(),
                                     "sample": f"{sample} candidates x {n} observations, oracle/oracle_scaled.c, "
                                               f"OpenMP {threads} threads, {ct:.1f} s"}
         else:

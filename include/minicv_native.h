@@ -38,6 +38,11 @@ typedef struct { double X, Y; } mcvV2d;
 typedef struct { double X, Y, Z; } mcvV3d;
 typedef struct { double M[9]; } mcvM33d;       /* row-major */
 typedef struct { float X, Y; } mcvV2f;
+/* The reference's `bool` exports (MiniCVNative.cpp:48,93,165,384,439) return a 1-byte C++ bool,
+ * while the F# P/Invoke side (OpenCV.fs:343-382, no MarshalAs) reads a 4-byte Win32 BOOL: only the
+ * low byte is defined there. This library returns them as a 32-bit 0/1, so the upper bytes are
+ * zero and both readings agree. */
+typedef int32_t mcvBool;
 
 /* ------------------------------------------------------------------------------------------
  * (1) Existing exports of the reference (same names, same argument meaning).
@@ -82,7 +87,7 @@ MCV_API int  cvRecoverPose(const RecoverPoseConfig* config, const int N, const m
                            mcvM33d* rMat, mcvV3d* tVec, uint8_t* ms);
 /* MiniCVNative.cpp:165-194: findEssentialMat -> ms -> decomposeEssentialMat(E) -> R1, R2, t.
  * false if N < 5 or no model (ms untouched then). */
-MCV_API bool cvRecoverPoses(const RecoverPoseConfig* config, const int N, const mcvV2d* pa, const mcvV2d* pb,
+MCV_API mcvBool cvRecoverPoses(const RecoverPoseConfig* config, const int N, const mcvV2d* pa, const mcvV2d* pb,
                             mcvM33d* rMat1, mcvM33d* rMat2, mcvV3d* tVec, uint8_t* ms);
 /* Feature detection — MiniCVNative.cpp:221-365 (out of scope: returns NULL). */
 MCV_API DetectorResult* cvDetectFeatures(char* data, int width, int height, int channels, int mode, void* config);
@@ -100,9 +105,9 @@ MCV_API int  cvFivePoint(const mcvV2d* pa, const mcvV2d* pb, mcvM33d* Es);
  * on the inliers from the best hypothesis. outInliers (caller: N ints) = RANSAC inlier indices.
  * cvSolvePnP: kinds 2/5 (P3P/AP3P) need N == 4 (AP3P, the 4th point picks the solution); other
  * kinds: AP3P-RANSAC initialisation (256 hypotheses, 4 px) + LM over all points. */
-MCV_API bool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                         const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec);
-MCV_API bool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+MCV_API mcvBool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                               const double* distortionCoeffs, const int solverKind, const int iterationsCount,
                               const float reprojectionError, const double confidence, mcvV3d* tVec, mcvV3d* rVec,
                               int* inlierCount, int* outInliers);
@@ -120,8 +125,8 @@ MCV_API int  solveAp3p(mcvM33d* Rs, mcvV3d* ts, float mu0, float mv0, float X0, 
                        float mu2, float mv2, float X2, float Y2, float Z2,
                        float inv_fx, float inv_fy, float cx_fx, float cy_fy);
 /* Fiducials — MiniCVNative.cpp:384-502 (out of scope: return false). */
-MCV_API bool cvDetectQRCode(char* data, int width, int height, int channels, int* positions, int* count);
-MCV_API bool cvDetectArucoMarkers(char* data, int width, int height, int channels, int* infoCount,
+MCV_API mcvBool cvDetectQRCode(char* data, int width, int height, int channels, int* positions, int* count);
+MCV_API mcvBool cvDetectArucoMarkers(char* data, int width, int height, int channels, int* infoCount,
                                   ArucoMarkerInfo* infos);
 
 /* ------------------------------------------------------------------------------------------
@@ -163,7 +168,8 @@ typedef struct {
 MCV_API int cvFindHomography(const mcvV2d* src, const mcvV2d* dst, const int N, const RansacConfig* cfg,
                              mcvM33d* H, uint8_t* mask);
 
-/* findFundamentalMat, 8-point minimal sets. a/b: N AoS fp64 points. F: out (||F||_F = 1 scale, F[8] >= 0).
+/* findFundamentalMat, 8-point minimal sets. a/b: N AoS fp64 points. F: out, scaled so that F[8] = 1 when
+ * |F[8]| > FLT_EPSILON (run8Point's normalisation), otherwise as solved.
  * mask: caller-allocated uint8[N]. Returns inlier count (>= 8), 0 on failure. */
 MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, const int N, const RansacConfig* cfg,
                                  mcvM33d* F, uint8_t* mask);
@@ -177,7 +183,7 @@ MCV_API int cvFindEssentialMat(const mcvV2d* a, const mcvV2d* b, const int N, do
                                const RansacConfig* cfg, mcvM33d* E, uint8_t* mask);
 
 /* cvSolvePnPRansac with a full RansacConfig (threshold = reprojection error in pixels; seed, fixed iterations, fused error, NO_REFINE). */
-MCV_API bool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+MCV_API mcvBool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                                  const double* distortionCoeffs, const RansacConfig* cfg, mcvV3d* tVec, mcvV3d* rVec,
                                  int* inlierCount, int* outInliers);
 
@@ -345,8 +351,9 @@ MCV_API int  mcvProfileRead(const char* kernel, double* total_ms);
  * ---------------------------------------------------------------------------------------- */
 MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, uint64_t seed, int64_t hyp,
                               double* model9, float* modelf9, int* sampleIdx);
-/* Device self-test: number of 32-bit patterns w where the sweep's reciprocal differs from 1.f/w
- * (mode 0 = shipped rcp_rn; 1 = without the special-value fixup; 2 = raw v_rcp_f32). */
+/* Device self-test: number of 32-bit patterns w where a reciprocal differs from 1.f/w (mode 0 =
+ * rcp_exact; 1 = rcp_newton everywhere; 2 = rcp_newton + v_div_fixup; 3 = rcp_newton on its domain
+ * |w| in [2^-126, 2^126) only; 4 = raw v_rcp_f32). */
 MCV_API long long mcvTestRcpExhaustive(int mode, uint32_t* firstMismatches16);
 /* Device self-test: number of sampled (n, d), d in +-[2^-64, 2^64], where the unscaled fp64
  * division (rcp_f64_refined + div_f64_refined) differs from n / d (mode 0: 2^-900 <= |n| < 2^700;

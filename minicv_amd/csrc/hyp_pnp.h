@@ -60,8 +60,10 @@ MCV_HD void pnp_project(const PnpCamera& c, const double* R, const double* t, do
     const double Yc = R[3] * X + R[4] * Y + R[5] * Z + t[1];
     const double Zc = R[6] * X + R[7] * Y + R[8] * Z + t[2];
 #if defined(__HIP_DEVICE_COMPILE__)
-    // refined reciprocal (mcv_common.h): 1 / Zc bit for bit for |Zc| in [2^-64, 2^64]
-    double iz = rcp_f64_refined(Zc);
+    // 1 / Zc bit for bit for |Zc| in [2^-64, 2^64]: the refined reciprocal followed by the quotient
+    // correction of the IEEE sequence (div_f64_refined with n = 1, mcvTestDivF64 mode 1); the two
+    // Newton steps alone are not a correctly rounded reciprocal for every significand
+    double iz = div_f64_refined(1.0, Zc, rcp_f64_refined(Zc));
     if (!div_f64_refined_domain(Zc)) iz = 1.0 / (Zc != 0 ? Zc : 1.0);   // = (Zc != 0 ? 1 / Zc : 1)
 #else
     const double iz = 1.0 / (Zc != 0 ? Zc : 1.0);   // = (Zc != 0 ? 1 / Zc : 1)

@@ -134,16 +134,19 @@ MCV_HD float rcp_newton(float w) {
 #endif
 }
 
-// Correctly rounded fp32 reciprocal. Device: v_rcp_f32 (1 ulp) + one FMA Newton step, with
-// v_div_fixup_f32 for 0 / inf / NaN operands — 4 VALU ops instead of the ~10 of the IEEE
-// division expansion; equality with 1.f / w is checked exhaustively over all 2^32 inputs on the
-// GPU (mcvTestRcpExhaustive, tests/test_gpu_selftest.py). Host: the IEEE division itself.
-MCV_HD float rcp_rn(float w) {
+// Correctly rounded fp32 reciprocal for every w, without the division expansion: rcp_newton (equal
+// to 1.f / w on |w| in [2^-126, 2^126), exhaustively) on w scaled by 2^24 when |w| is denormal (an
+// exact power-of-two scaling into that domain; the product by 2^24 afterwards rounds the same way,
+// overflow to inf included), +-inf for +-0, NaN for NaN. |w| >= 2^126 takes the IEEE division.
+// rcp_newton with v_div_fixup alone misrounds denormal inputs (mcvTestRcpExhaustive mode 2); this
+// form is checked over all 2^32 inputs (mode 0). Host: the IEEE division itself.
+MCV_HD float rcp_exact(float w) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const float r = __builtin_amdgcn_rcpf(w);
-    const float e = __builtin_fmaf(-w, r, 1.0f);
-    const float r1 = __builtin_fmaf(e, r, r);
-    return __builtin_amdgcn_div_fixupf(r1, w, 1.0f);
+    const float aw = __builtin_fabsf(w);
+    if (__builtin_expect(aw >= 0x1p126f, 0)) return 1.0f / w;
+    const float sc = aw < 0x1p-126f ? 0x1p24f : 1.0f;
+    const float r = rcp_newton(w * sc) * sc;
+    return w == 0.0f ? __builtin_copysignf(__builtin_inff(), w) : r;
 #else
     return 1.0f / w;
 #endif

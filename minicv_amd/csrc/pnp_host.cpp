@@ -354,7 +354,7 @@ static bool pnp_ransac_export(const mcvV2d* img, const mcvV3d* world, int N, con
 
 using namespace mcv;
 
-extern "C" MCV_API bool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N,
+extern "C" MCV_API mcvBool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N,
                                          const mcvM33d K, const double* distortionCoeffs, const int solverKind,
                                          const int iterationsCount, const float reprojectionError,
                                          const double confidence, mcvV3d* tVec, mcvV3d* rVec, int* inlierCount,
@@ -367,7 +367,7 @@ extern "C" MCV_API bool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* 
     })
 }
 
-extern "C" MCV_API bool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N,
+extern "C" MCV_API mcvBool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N,
                                             const mcvM33d K, const double* distortionCoeffs, const RansacConfig* cfgp,
                                             mcvV3d* tVec, mcvV3d* rVec, int* inlierCount, int* outInliers) {
     MCV_GUARD(false, {
@@ -378,7 +378,7 @@ extern "C" MCV_API bool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mcvV3
     })
 }
 
-extern "C" MCV_API bool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
+extern "C" MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                                    const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec) {
     MCV_GUARD(false, {
         if (!imgPoints || !worldPoints || !tVec || !rVec) fail("cvSolvePnP: null argument");

@@ -240,7 +240,7 @@ extern "C" MCV_API int cvFindEssentialMat(const mcvV2d* a, const mcvV2d* b, cons
     })
 }
 
-extern "C" MCV_API bool cvRecoverPoses(const RecoverPoseConfig* config, const int N, const mcvV2d* pa,
+extern "C" MCV_API mcvBool cvRecoverPoses(const RecoverPoseConfig* config, const int N, const mcvV2d* pa,
                                        const mcvV2d* pb, mcvM33d* rMat1, mcvM33d* rMat2, mcvV3d* tVec, uint8_t* ms) {
     MCV_GUARD(false, {
         if (N < 5) return false;   // MiniCVNative.cpp:167

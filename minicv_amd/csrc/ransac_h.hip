@@ -363,41 +363,46 @@ __global__ __launch_bounds__(256) void mcv_h_verify_pk(const HPair* __restrict__
 
 // ------------------------------------------------------------------------------------------
 // Certified division-free sweep of the op-by-op error (the default: OpenCV's computeError as an
-// x86-64 SSE build evaluates it, h_error). Per (hypothesis, correspondence) in packed f32:
+// x86-64 SSE build evaluates it, h_error). Per pair of correspondences in packed f32:
 //   W = fma(h6,x,fma(h7,y,1)), U = fma(h0,x,fma(h1,y,h2)), V likewise,
-//   DX = fma(-x',W,U), DY = fma(-y',W,V), L = fma(DX,DX,DY*DY), W2 = W*W,
-//   certified inlier   <=  fma(W2, a_in, L)  < -b_in
-//   certified outlier  <=  fma(W2, a_out, L) >  b_out
-// with per-model constants from h_cert_consts (the derivation is in DESIGN.md §4): the reference
-// error times w^2 lies within relative (t + O(u)) and absolute O(u^2 G^2 / t) of L, and w^2 within
-// the same of W2, so a decided lane has the answer of the op-by-op fp32 error bit for bit. Lanes
-// left undecided (~1e-7 of evaluations on these workloads) take h_error with IEEE division in one
-// wave-uniform branch per trip. 13 packed ops + 4 compares per pair of correspondences, no
-// reciprocal: against the fused sweep's 12 packed + 2 v_rcp_f32 + v_min3 + 2 compares.
+//   DX = fma(-x',W,U), DY = fma(-y',W,V), L = fma(DX,DX,fma(DY,DY,b_in)), W2 = W*W,
+//   I = fma(W2, a_in, L), X = fma(W2, d, b_x);
+//   I < 0                     -> certified inlier
+//   bits(I) <= bits(X)        -> undecided (0 <= I <= X as floats); otherwise certified outlier.
+// The reference error times w^2 lies within relative (t + O(u)) and absolute O(u^2 G^2 / t) of
+// DX^2 + DY^2, and w^2 within the same of W2 (derivation in DESIGN.md §4); a_in, d (launch) and
+// b_in, b_x (per model) put the two cuts outside those intervals, so a decided lane has the answer
+// of the op-by-op fp32 error bit for bit. 13 packed ops + 4 VOPC e32 compares per pair, no
+// reciprocal (the fused sweep: 12 packed + 2 v_rcp_f32 + v_min3 + 2 compares). Undecided lanes
+// (where points crowd the threshold, ~1e-4 of evaluations on the cfg3 data) are recorded per trip
+// and resolved after the sweep with the exact error and IEEE division.
 // ------------------------------------------------------------------------------------------
-// Band parameter of the certified tests: relative half-width ~ t + O(u) around thr2 w^2, absolute
-// part ~ (7.5 u G)^2 / t. One t for every model keeps the slopes a_in / a_out launch constants.
+// Band parameter: relative half-width ~ t + O(u) around thr2 w^2, absolute part ~ (7.5 u G)^2 / t.
+// One t for every model keeps the slopes launch constants.
 static constexpr double kCertT = 0x1p-12;
-static constexpr double kCertSlop = 0x1p-18;   // covers the O(u) terms (< 15 u = 2^-20.1 in total)
+static constexpr double kCertSlop = 0x1p-18;   // covers the O(u) factors (< 16 u = 2^-20 in total)
 
-struct HCertSlopes { f2 a; };   // {a_in, a_out}, both <= 0 (kernel argument)
+struct HCertSlopes { f2 a; };   // {a_in (<= 0), d (>= 0)} (kernel argument)
 
 HCertSlopes h_cert_slopes_host(float thr2) {
-    const double T = (double)thr2, t = kCertT;
+    const double T = (double)thr2, t = kCertT, u = 0x1p-24;
+    // inlier cut: |a_in| <= T (1-t)/(1+t) (1 - slop), rounded towards zero
     const double ain = -T * (1.0 - t) / (1.0 + t) * (1.0 - kCertSlop);
-    const double aout = -T * (1.0 + t) / (1.0 - t) * (1.0 + kCertSlop);
-    // rounded towards the conservative side of each test: |a_in| down, |a_out| up
-    float fi = (float)ain, fo = (float)aout;
+    float fi = (float)ain;
     if ((double)fi < ain) fi = std::nextafter(fi, 0.0f);
-    if ((double)fo > aout) fo = std::nextafter(fo, -__builtin_inff());
+    // outlier cut: |a_in| + d (1 - 2u) >= T (1+t)/(1-t) (1 + slop), d rounded up
+    const double need = T * (1.0 + t) / (1.0 - t) * (1.0 + kCertSlop);
+    const double d = (need + (double)fi) / (1.0 - 2 * u);
+    float fd = (float)d;
+    if ((double)fd < d) fd = std::nextafter(fd, __builtin_inff());
     HCertSlopes c;
-    c.a = f2{fi, fo};
+    c.a = f2{fi, fd};
     return c;
 }
 
-// Per-model offsets b = {-b_in, b_out}; false when the model or the point set leaves the domain of
-// the error bound (the wave then hands its slots to the exact scalar sweep). bb = {max|x|, max|y|,
-// max|x'|, max|y'|} of the correspondences (inf when any is NaN / inf).
+// Per-model offsets b = {b_in, b_x} (both > 0); false when the model or the point set leaves the
+// domain of the error bound (the wave then hands its slots to the exact scalar sweep).
+// bb = {max|x|, max|y|, max|x'|, max|y'|} of the correspondences (inf when any is NaN / inf).
 __device__ __forceinline__ bool h_cert_offsets(const float* h, const double* bb, float thr2, f2& b) {
     const double X = bb[0], Y = bb[1], MX = bb[2], MY = bb[3];
     const double u = 0x1p-24, t = kCertT;
@@ -411,13 +416,15 @@ __device__ __forceinline__ bool h_cert_offsets(const float* h, const double* bb,
     const double cx = 7.5 * u * Gx, cy = 7.5 * u * Gy, cw = 5.1 * u * Bw;
     const double C = cx * cx + cy * cy, Cw = cw * cw;
     const double tiny = 0x1p-120 + 0x1p-140 * Bw * Bw;
-    const double bin = (1.0 + 2 * kCertSlop) * ((1.0 + 1.0 / t) * C + T * Cw / t) + tiny;
-    const double bout = (1.0 + 2 * kCertSlop) / (1.0 - t) * (C / t + T * (1.0 + 1.0 / t) * Cw) + tiny;
-    b = f2{__double2float_rd(-bin), __double2float_ru(bout)};
+    const double K1 = (1.0 + 2 * kCertSlop) * ((1.0 + 1.0 / t) * C + T * Cw / t) + tiny;
+    const double K2 = (1.0 + 2 * kCertSlop) / (1.0 - t) * (C / t + T * (1.0 + 1.0 / t) * Cw) + tiny;
+    const float bin = __double2float_ru(K1);
+    const double bx = (K2 + (double)bin) * (1.0 + kCertSlop);
+    b = f2{bin, __double2float_ru(bx)};
     return ok;
 }
 
-// Unpacked model k (for the exact fallback): h[0..7] from the coefficient pairs.
+// Unpacked model k (for the exact path): h[0..7] from the coefficient pairs.
 template <int K>
 __device__ __forceinline__ void h_cert_model(const f2 (&hp)[K][4], int k, float (&h)[8]) {
 #pragma unroll
@@ -427,31 +434,67 @@ __device__ __forceinline__ void h_cert_model(const f2 (&hp)[K][4], int k, float 
     }
 }
 
-// One pair of correspondences against one model: certified in / out lane masks per half.
-// a = {a_in, a_out} (shared), b = the model's {-b_in, b_out}.
-__device__ __forceinline__ void h_cert_eval(f2 p0, f2 p1, f2 p2, f2 p3, f2 c, f2 a, f2 b, const HPair& q, f2 one,
-                                            uint64_t& inx, uint64_t& iny, uint64_t& outx, uint64_t& outy) {
+// The certified values of one pair of correspondences against one model: I and X (see above).
+// a = {a_in, d} (shared), b = the model's {b_in, b_x}, c = {h2, h5}.
+__device__ __forceinline__ void h_cert_values(f2 p0, f2 p1, f2 p2, f2 p3, f2 c, f2 a, f2 b, const HPair& q, f2 one,
+                                              f2& I, f2& X) {
     const f2 W = pk_fma(lo(p3), q.x, pk_fma(hi(p3), q.y, one));      // fma(h6,x,fma(h7,y,1))
     const f2 U = pk_fma(lo(p0), q.x, pk_fma(hi(p0), q.y, lo(c)));    // fma(h0,x,fma(h1,y,h2))
     const f2 V = pk_fma(hi(p1), q.x, pk_fma(lo(p2), q.y, hi(c)));    // fma(h3,x,fma(h4,y,h5))
     const f2 DX = pk_fma(-q.mx, W, U);
     const f2 DY = pk_fma(-q.my, W, V);
-    const f2 L = pk_fma(DX, DX, DY * DY);
+    const f2 L = pk_fma(DX, DX, pk_fma(DY, DY, lo(b)));
     const f2 W2 = W * W;
-    const f2 I = pk_fma(W2, lo(a), L);
-    const f2 O = pk_fma(W2, hi(a), L);
-    inx = __builtin_amdgcn_ballot_w64(I.x < b.x);
-    iny = __builtin_amdgcn_ballot_w64(I.y < b.x);
-    outx = __builtin_amdgcn_ballot_w64(O.x > b.y);
-    outy = __builtin_amdgcn_ballot_w64(O.y > b.y);
+    I = pk_fma(W2, lo(a), L);
+    X = pk_fma(W2, hi(a), hi(b));
+}
+
+// Lane masks from the certified values, C++ form (tail trips and the resolve pass): inliers and
+// undecided lanes per half. The sweep's asm form (h_cert_masks_asm) computes the same predicates.
+__device__ __forceinline__ void h_cert_masks(f2 I, f2 X, uint64_t& inx, uint64_t& iny, uint64_t& ux,
+                                             uint64_t& uy) {
+    inx = __builtin_amdgcn_ballot_w64(I.x < 0.0f);
+    iny = __builtin_amdgcn_ballot_w64(I.y < 0.0f);
+    ux = __builtin_amdgcn_ballot_w64(__float_as_uint(I.x) <= __float_as_uint(X.x));
+    uy = __builtin_amdgcn_ballot_w64(__float_as_uint(I.y) <= __float_as_uint(X.y));
+}
+
+// The same four compares as VOPC e32 (2-cycle issue; the compiler picks the 4-cycle VOP3 form when
+// several lane masks are live at once). Wait states: the leading s_nop 0 covers a packed-op result
+// read right at the statement's start (the compiler places 1 state between dependent packed ops);
+// SALU reads of VCC after a VALU write need none.
+__device__ __forceinline__ void h_cert_masks_asm(f2 I, f2 X, uint64_t& inx, uint64_t& iny, uint64_t& ux,
+                                                 uint64_t& uy) {
+    asm volatile(
+        "s_nop 0\n\t"
+        "v_cmp_gt_f32_e32 vcc, 0, %4\n\t"
+        "s_mov_b64 %0, vcc\n\t"
+        "v_cmp_gt_f32_e32 vcc, 0, %5\n\t"
+        "s_mov_b64 %1, vcc\n\t"
+        "v_cmp_le_u32_e32 vcc, %4, %6\n\t"
+        "s_mov_b64 %2, vcc\n\t"
+        "v_cmp_le_u32_e32 vcc, %5, %7\n\t"
+        "s_mov_b64 %3, vcc"
+        : "=&s"(inx), "=&s"(iny), "=&s"(ux), "=&s"(uy)
+        : "v"(I.x), "v"(I.y), "v"(X.x), "v"(X.y)
+        : "vcc");
+}
+
+// h_error of both correspondences of a pair, packed, operation for operation (every product and sum
+// rounded as written) with the reciprocal by rcp_exact, which equals the IEEE 1.f / w for every w
+// (exhaustive GPU check, mcvTestRcpExhaustive mode 0): bit-identical to h_error.
+__device__ __forceinline__ f2 h_error_pk(f2 p0, f2 p1, f2 p2, f2 p3, const HPair& q) {
+    const f2 w = (lo(p3) * q.x + hi(p3) * q.y) + f2{1.f, 1.f};
+    const f2 ww = f2{rcp_exact(w.x), rcp_exact(w.y)};
+    const f2 ex = ((lo(p0) * q.x + hi(p0) * q.y) + lo(p1)) * ww - q.mx;
+    const f2 ey = ((hi(p1) * q.x + lo(p2) * q.y) + hi(p2)) * ww - q.my;
+    return ex * ex + ey * ey;
 }
 
 // One trip: NP pairs per lane against the wave's K models. vx / vy: lanes whose first / second
-// correspondence of pair slot j exists (all ones in full trips).
-// One trip: NP pairs per lane against the wave's K models. vx / vy: lanes whose first / second
-// correspondence of pair slot j exists (all ones in full trips). Returns the mask of models with
-// an undecided lane in this trip (bit k); their certified counts are already in cnt.
-template <int K, int NP, bool PRED, int DIAG = 0>
+// correspondence of pair slot j exists (tail trip only). Returns the mask of models with an
+// undecided lane in this trip (bit k); their certified counts are already in cnt.
+template <int K, int NP, bool PRED, bool ASMCMP = false>
 __device__ __forceinline__ uint32_t h_cert_trip(f2 (&hp)[K][4], const f2 (&hc)[K], f2 a, const f2 (&cb)[K],
                                                 const HPair (&q)[NP], const uint64_t (&vx)[NP],
                                                 const uint64_t (&vy)[NP], f2 one, uint32_t (&cnt)[K]) {
@@ -461,26 +504,95 @@ __device__ __forceinline__ uint32_t h_cert_trip(f2 (&hp)[K][4], const f2 (&hc)[K
         // re-defined in place every trip (no copy): the loop cannot hoist the broadcasts, so each use
         // reads the SGPR pair through op_sel
         asm volatile("" : "+s"(hp[k][0]), "+s"(hp[k][1]), "+s"(hp[k][2]), "+s"(hp[k][3]));
-        uint64_t dec = ~0ull;
+        uint64_t und = 0;
 #pragma unroll
         for (int j = 0; j < NP; ++j) {
-            uint64_t inx, iny, outx, outy;
-            h_cert_eval(hp[k][0], hp[k][1], hp[k][2], hp[k][3], hc[k], a, cb[k], q[j], one, inx, iny, outx, outy);
+            f2 I, X;
+            h_cert_values(hp[k][0], hp[k][1], hp[k][2], hp[k][3], hc[k], a, cb[k], q[j], one, I, X);
+            uint64_t inx, iny, ux, uy;
             if constexpr (PRED) {
+                h_cert_masks(I, X, inx, iny, ux, uy);
                 inx &= vx[j];
                 iny &= vy[j];
-                dec &= (inx | outx | ~vx[j]) & (iny | outy | ~vy[j]);
-            } else if constexpr (DIAG < 2) {
-                dec &= (inx | outx) & (iny | outy);
+                und |= (ux & vx[j]) | (uy & vy[j]);
+            } else {
+                if constexpr (ASMCMP) h_cert_masks_asm(I, X, inx, iny, ux, uy);
+                else h_cert_masks(I, X, inx, iny, ux, uy);
+                und |= ux | uy;
             }
             cnt[k] += (uint32_t)__popcll(inx) + (uint32_t)__popcll(iny);
         }
-        undecided |= (dec != ~0ull) ? (1u << k) : 0u;
+        undecided |= (und != 0) ? (1u << k) : 0u;
     }
-    return DIAG >= 1 ? 0u : undecided;
+    return undecided;
 }
 
-// The exact op-by-op error (IEEE division) for the undecided lanes of model k at the trip starting
+// The exact op-by-op error for the undecided lanes of the models in `und`, on the trip's pairs still
+// in registers: a rolled loop over the models, each re-read through the scalar cache with its
+// offsets from LDS, so that this rare path adds little register pressure to the sweep.
+template <int K, int NP, bool PRED>
+__device__ __forceinline__ void h_cert_fix(uint32_t und, const HModelF* __restrict__ models, int h0, int hypCount,
+                                           const f2* __restrict__ offs, f2 a, const HPair (&q)[NP],
+                                           const uint64_t (&vx)[NP], const uint64_t (&vy)[NP], float thr2, f2 one,
+                                           uint32_t (&cnt)[K]) {
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+        if (!(und & (1u << k))) continue;
+        const int hk = h0 + k < hypCount ? h0 + k : hypCount - 1;
+        const f2* mp = (const f2*)&models[hk];
+        const f2 m0 = mp[0], m1 = mp[1], m2 = mp[2], m3 = mp[3];
+        const f2 b = offs[k];
+        uint32_t add = 0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            f2 I, X;
+            h_cert_values(m0, m1, m2, m3, f2{m1.x, m2.y}, a, b, q[j], one, I, X);
+            uint64_t inx, iny, ux, uy;
+            h_cert_masks(I, X, inx, iny, ux, uy);
+            if constexpr (PRED) {
+                ux &= vx[j];
+                uy &= vy[j];
+            }
+            if ((ux | uy) == 0) continue;
+            const f2 e = h_error_pk(m0, m1, m2, m3, q[j]);
+            const uint64_t me = 1ull << (__lane_id() & 63);
+            add += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64((ux & me) != 0 && e.x <= thr2)) +
+                   (uint32_t)__popcll(__builtin_amdgcn_ballot_w64((uy & me) != 0 && e.y <= thr2));
+        }
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) cnt[kk] += (kk == k) ? add : 0u;   // no dynamic register indexing
+    }
+}
+
+// The same with the models still in registers (compile-time model index; the branch per model is
+// wave-uniform and rarely taken).
+template <int K, int NP, bool PRED>
+__device__ __forceinline__ void h_cert_fix_regs(uint32_t und, const f2 (&hp)[K][4], const f2 (&hc)[K], f2 a,
+                                                const f2 (&cb)[K], const HPair (&q)[NP], const uint64_t (&vx)[NP],
+                                                const uint64_t (&vy)[NP], float thr2, f2 one, uint32_t (&cnt)[K]) {
+    const uint64_t me = 1ull << (__lane_id() & 63);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (!(und & (1u << k))) continue;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            f2 I, X;
+            h_cert_values(hp[k][0], hp[k][1], hp[k][2], hp[k][3], hc[k], a, cb[k], q[j], one, I, X);
+            uint64_t inx, iny, ux, uy;
+            h_cert_masks(I, X, inx, iny, ux, uy);
+            if constexpr (PRED) {
+                ux &= vx[j];
+                uy &= vy[j];
+            }
+            if ((ux | uy) == 0) continue;
+            const f2 e = h_error_pk(hp[k][0], hp[k][1], hp[k][2], hp[k][3], q[j]);
+            cnt[k] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64((ux & me) != 0 && e.x <= thr2)) +
+                      (uint32_t)__popcll(__builtin_amdgcn_ballot_w64((uy & me) != 0 && e.y <= thr2));
+        }
+    }
+}
+
+// The exact op-by-op error (IEEE division) for the undecided lanes of model hk at the trip starting
 // at pair `base` (re-read from memory; validity from the pair counts). Returns their inlier count.
 template <int NP>
 __device__ __noinline__ uint32_t h_cert_resolve(const HPair* __restrict__ pairs, int nPairs, int nComplete, int base,
@@ -496,12 +608,15 @@ __device__ __noinline__ uint32_t h_cert_resolve(const HPair* __restrict__ pairs,
         const int p = base + 64 * j + lane;
         const uint64_t vx = __builtin_amdgcn_ballot_w64(p < nPairs), vy = __builtin_amdgcn_ballot_w64(p < nComplete);
         const HPair q = pairs[p < nPairs ? p : 0];
-        uint64_t inx, iny, outx, outy;
-        h_cert_eval(m0, m1, m2, m3, f2{m1.x, m2.y}, a, b, q, one, inx, iny, outx, outy);
-        const uint64_t ax = vx & ~(inx | outx), ay = vy & ~(iny | outy);
+        f2 I, X;
+        h_cert_values(m0, m1, m2, m3, f2{m1.x, m2.y}, a, b, q, one, I, X);
+        uint64_t inx, iny, ux, uy;
+        h_cert_masks(I, X, inx, iny, ux, uy);
+        ux &= vx;
+        uy &= vy;
         bool ex = false, ey = false;
-        if (ax & me) ex = h_error(h, q.x.x, q.y.x, q.mx.x, q.my.x) <= thr2;
-        if (ay & me) ey = h_error(h, q.x.y, q.y.y, q.mx.y, q.my.y) <= thr2;
+        if (ux & me) ex = h_error(h, q.x.x, q.y.x, q.mx.x, q.my.x) <= thr2;
+        if (uy & me) ey = h_error(h, q.x.y, q.y.y, q.mx.y, q.my.y) <= thr2;
         add += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(ex)) + (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(ey));
     }
     return add;
@@ -515,7 +630,7 @@ __device__ __noinline__ uint32_t h_cert_resolve(const HPair* __restrict__ pairs,
 // nComplete = N / 2 pairs hold two correspondences; pair nComplete (odd N) holds one.
 static constexpr int kCertEvents = 256;   // per wave
 
-template <int K, int NP, int DIAG = 0>
+template <int K, int NP, int FIX, bool ASMCMP>
 __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict__ pairs, int nPairs, int nComplete,
                                                          const HModelF* __restrict__ models, int* __restrict__ counts,
                                                          int hypCount, float thr2, HCertSlopes slopes,
@@ -548,8 +663,9 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
         const bool ok = h_cert_offsets(h, b4, thr2, cb[k]);
         fast = fast && (ok || !valid[k]);
         if (lane == 0) offsets[wib][k] = cb[k];
-        // VGPR-resident: hc meets an SGPR coefficient in the same op (constant-bus limit), cb is
-        // the VGPR operand of the e32 compares
+        __builtin_amdgcn_wave_barrier();
+        // VGPR-resident: hc and cb meet an SGPR coefficient or another model operand in the same
+        // packed op (constant-bus limit)
         asm volatile("" : "+v"(hc[k]), "+v"(cb[k]));
     }
     const f2 one = f2{1.f, 1.f};
@@ -567,10 +683,17 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
             HPair q[NP];
 #pragma unroll
             for (int j = 0; j < NP; ++j) q[j] = pairs[base + 64 * j + lane];
-            const uint32_t und = h_cert_trip<K, NP, false, DIAG>(hp, hc, slopes.a, cb, q, all, all, one, cnt);
-            if (__builtin_expect(und != 0, 0)) {
-                if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)base << 8) | und;
-                ++nev;
+            const uint32_t und = h_cert_trip<K, NP, false, ASMCMP>(hp, hc, slopes.a, cb, q, all, all, one, cnt);
+            if (FIX >= 0 && __builtin_expect(und != 0, 0)) {   // FIX < 0: timing diagnostics only
+                if constexpr (FIX == 2) {
+                    h_cert_fix_regs<K, NP, false>(und, hp, hc, slopes.a, cb, q, all, all, thr2, one, cnt);
+                } else if constexpr (FIX == 1) {
+                    h_cert_fix<K, NP, false>(und, models, h0, hypCount, offsets[wib], slopes.a, q, all, all, thr2,
+                                             one, cnt);
+                } else {
+                    if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)base << 8) | und;
+                    ++nev;
+                }
             }
         }
         for (int base = nFull; base < nPairs; base += TRIP) {
@@ -583,7 +706,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
                 vy[j] = __builtin_amdgcn_ballot_w64(p < nComplete);
                 q[j] = pairs[p < nPairs ? p : 0];
             }
-            const uint32_t und = h_cert_trip<K, NP, true, DIAG>(hp, hc, slopes.a, cb, q, vx, vy, one, cnt);
+            const uint32_t und = h_cert_trip<K, NP, true>(hp, hc, slopes.a, cb, q, vx, vy, one, cnt);
             if (und != 0) {
                 if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)base << 8) | und;
                 ++nev;
@@ -591,8 +714,8 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
         }
         if (nev > kCertEvents) fast = false;   // too many to resolve here: exact recount of the wave
         else if (nev > 0) {
-            __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
             for (int e = 0; e < nev; ++e) {
                 const uint32_t ev = __builtin_amdgcn_readfirstlane(events[wib][e]);
                 const int base = (int)(ev >> 8);
@@ -964,12 +1087,12 @@ static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d
     }
 }
 
-template <int K, int NP, int DIAG = 0>
+template <int K, int NP, int FIX = 1, bool ASMCMP = false>
 static void launch_h_verify_cert_k(const void* d_pairs, int N, const void* d_models, int* d_counts, int hypCount,
                                    float thr2, const double* d_bb, hipStream_t s) {
     const int waves = (hypCount + K - 1) / K;
     const int blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL((mcv_h_verify_cert<K, NP, DIAG>), dim3(blocks), dim3(256), 0, s, (const HPair*)d_pairs, (N + 1) / 2,
+    hipLaunchKernelGGL((mcv_h_verify_cert<K, NP, FIX, ASMCMP>), dim3(blocks), dim3(256), 0, s, (const HPair*)d_pairs, (N + 1) / 2,
                        N / 2, (const HModelF*)d_models, d_counts, hypCount, thr2, h_cert_slopes_host(thr2), d_bb);
 }
 
@@ -987,19 +1110,17 @@ static int cert_variant() {
 void launch_h_verify_certified(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
                                int hypCount, float thr2, const double* d_bb, hipStream_t s) {
     switch (cert_variant()) {
-        case 1: launch_h_verify_cert_k<6, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 2: launch_h_verify_cert_k<4, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 3: launch_h_verify_cert_k<8, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 4: launch_h_verify_cert_k<4, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 5: launch_h_verify_cert_k<6, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 6: launch_h_verify_cert_k<5, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 7: launch_h_verify_cert_k<3, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 8: launch_h_verify_cert_k<4, 4>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 20: launch_h_verify_cert_k<4, 2, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 21: launch_h_verify_cert_k<4, 2, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 22: launch_h_verify_cert_k<8, 2, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 23: launch_h_verify_cert_k<6, 2, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        default: launch_h_verify_cert_k<8, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s);
+        case 1: launch_h_verify_cert_k<4, 2, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 2: launch_h_verify_cert_k<4, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 3: launch_h_verify_cert_k<6, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 4: launch_h_verify_cert_k<3, 2, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 5: launch_h_verify_cert_k<4, 2, 1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 6: launch_h_verify_cert_k<4, 2, 2, true>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 7: launch_h_verify_cert_k<6, 1, 2, true>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 8: launch_h_verify_cert_k<5, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 90: launch_h_verify_cert_k<4, 2, -1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        case 91: launch_h_verify_cert_k<6, 1, -1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
+        default: launch_h_verify_cert_k<4, 2, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s);
     }
     static const bool noredo = getenv("MCV_HCERT_NOREDO") != nullptr;   // diagnostics only
     if (noredo) return;

@@ -410,6 +410,12 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
     const int shards = std::max(1, std::min(cfg.deviceCount, kMaxShards));
     int home = 0;
     MCV_HIP(hipGetDevice(&home));
+    // the calling thread's device is restored on every exit, exceptions included (later calls on
+    // this thread resolve their plans and allocations by the current device)
+    struct DeviceRestore {
+        int dev;
+        ~DeviceRestore() { (void)hipSetDevice(dev); }
+    } restore{home};
     struct Shard { Plan* P; const void* pts; hipStream_t s; int dev; };
     std::vector<Shard> sh;
     sh.push_back({&P, d_pts, s, home});

@@ -1,7 +1,7 @@
 // selftest.hip — device self-tests exported as test hooks (never on a product path).
-//   mcvTestRcpExhaustive: checks, over every 32-bit pattern, that the fused reciprocal used by the
-//   inlier sweep (v_rcp_f32 + one FMA Newton step + v_div_fixup) equals the correctly rounded
-//   IEEE quotient 1.f / w — the property that lets the host oracle reproduce it with a division.
+//   mcvTestRcpExhaustive: counts, over every 32-bit pattern, where the reciprocals the inlier sweeps
+//   use (rcp_newton: v_rcp_f32 + one FMA Newton step; rcp_exact) differ from the correctly rounded
+//   IEEE quotient 1.f / w — the property that lets the host oracle reproduce them with a division.
 #include "mcv_common.h"
 #include "minicv_native.h"
 #include "mcv_runtime.h"
@@ -9,13 +9,15 @@
 
 namespace mcv {
 
+// mode 0: rcp_exact; 1 / 3: rcp_newton (everywhere / on its domain only); 2: rcp_newton with
+// v_div_fixup_f32 (the special-value fixup alone does not repair denormal inputs); 4: raw v_rcp_f32
 __device__ __forceinline__ float rcp_variant(float w, int mode) {
-    if (mode == 0) return rcp_rn(w);
-    if (mode == 3) return rcp_newton(w);
+    if (mode == 0) return rcp_exact(w);
+    if (mode == 1 || mode == 3) return rcp_newton(w);
     const float r = __builtin_amdgcn_rcpf(w);
-    if (mode == 2) return r;
+    if (mode == 4) return r;
     const float e = __builtin_fmaf(-w, r, 1.0f);
-    return __builtin_fmaf(e, r, r);
+    return __builtin_amdgcn_div_fixupf(__builtin_fmaf(e, r, r), w, 1.0f);
 }
 
 __global__ __launch_bounds__(256) void mcv_rcp_check(uint64_t begin, uint64_t count, int mode,

@@ -94,13 +94,13 @@ extern "C" MCV_API void cvFreeFeatures(DetectorResult* res) {
 
 extern "C" MCV_API void cvTest(void) {}
 
-extern "C" MCV_API bool cvDetectQRCode(char*, int, int, int, int*, int* count) {
+extern "C" MCV_API mcvBool cvDetectQRCode(char*, int, int, int, int*, int* count) {
     if (count) *count = 0;
     MCV_NOT_IN_SCOPE("cvDetectQRCode", "QR detection is outside the MI355X hot path (SURVEY 2 row 7)");
     return false;
 }
 
-extern "C" MCV_API bool cvDetectArucoMarkers(char*, int, int, int, int* infoCount, ArucoMarkerInfo*) {
+extern "C" MCV_API mcvBool cvDetectArucoMarkers(char*, int, int, int, int* infoCount, ArucoMarkerInfo*) {
     if (infoCount) *infoCount = 0;
     MCV_NOT_IN_SCOPE("cvDetectArucoMarkers", "ArUco detection is outside the MI355X hot path (SURVEY 2 row 8)");
     return false;

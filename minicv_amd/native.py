@@ -90,23 +90,23 @@ _F = C.c_float
 SIGNATURES = {
     # existing reference exports (OpenCV.fs:343-382)
     "cvRecoverPose": (_I, [_P, _I, _P, _P, _P, _P, _P]),
-    "cvRecoverPoses": (C.c_bool, [_P, _I, _P, _P, _P, _P, _P, _P]),
+    "cvRecoverPoses": (_I, [_P, _I, _P, _P, _P, _P, _P, _P]),
     "cvDetectFeatures": (_P, [_P, _I, _I, _I, _I, _P]),
     "cvFreeFeatures": (None, [_P]),
     "cvTest": (None, []),
     "cvFivePoint": (_I, [_P, _P, _P]),
-    "cvSolvePnP": (C.c_bool, [_P, _P, _I, M33d, _P, _I, _P, _P]),
-    "cvSolvePnPRansac": (C.c_bool, [_P, _P, _I, M33d, _P, _I, _I, _F, _D, _P, _P, _P, _P]),
+    "cvSolvePnP": (_I, [_P, _P, _I, M33d, _P, _I, _P, _P]),
+    "cvSolvePnPRansac": (_I, [_P, _P, _I, M33d, _P, _I, _I, _F, _D, _P, _P, _P, _P]),
     "cvRefinePnPLM": (None, [_P, _P, _I, M33d, _P, _P, _P]),
     "cvRefinePnPVVS": (None, [_P, _P, _I, M33d, _P, _P, _P]),
     "solveAp3p": (_I, [_P, _P] + [_F] * 19),
-    "cvDetectQRCode": (C.c_bool, [_P, _I, _I, _I, _P, _P]),
-    "cvDetectArucoMarkers": (C.c_bool, [_P, _I, _I, _I, _P, _P]),
+    "cvDetectQRCode": (_I, [_P, _I, _I, _I, _P, _P]),
+    "cvDetectArucoMarkers": (_I, [_P, _I, _I, _I, _P, _P]),
     # new hot-path exports
     "cvFindHomography": (_I, [_P, _P, _I, _P, _P, _P]),
     "cvFindFundamentalMat": (_I, [_P, _P, _I, _P, _P, _P]),
     "cvFindEssentialMat": (_I, [_P, _P, _I, _D, V2d, _P, _P, _P]),
-    "cvSolvePnPRansacCfg": (C.c_bool, [_P, _P, _I, M33d, _P, _P, _P, _P, _P, _P]),
+    "cvSolvePnPRansacCfg": (_I, [_P, _P, _I, M33d, _P, _P, _P, _P, _P, _P]),
     "cvMatchFeatures": (_I, [_P, _P, _P, _P, _P, _I]),
     "cvMatchAndFindModel": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "cvMatchHamming": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),

@@ -162,7 +162,7 @@ def f_count(pts4, F, thr2, kind=0, want_mask=False):
     return (n, m) if want_mask else n
 
 
-def f_counts(pts4, seed, begin, count, thr2, kind=0, nthreads=0):
+def f_counts(pts4, seed, begin, count, thr2, kind=1, nthreads=0):
     out = np.zeros(count, dtype=np.int32)
     load().orc_f_counts(ptr(pts4), pts4.shape[0], seed, begin, count, thr2, kind, ptr(out), nthreads)
     return out
@@ -220,7 +220,7 @@ def e_count(pts4d, E, thr2, kind=0, want_mask=False):
     return (n, m) if want_mask else n
 
 
-def e_counts(pts4d, seed, begin, count, thr2, kind=0, nthreads=0):
+def e_counts(pts4d, seed, begin, count, thr2, kind=1, nthreads=0):
     out = np.zeros(count * E_SLOTS, dtype=np.int32)
     load().orc_e_counts(ptr(pts4d), pts4d.shape[0], seed, begin, count, thr2, kind, ptr(out), nthreads)
     return out

@@ -35,6 +35,37 @@ def local_key(counts, begin, count, m=4, slots=1):
     return (c << 32) | (0xFFFFFFFF - (begin + i)), first_fail
 
 
+def _worker_replay(rank, world, port, counts, q, n, m, conf, max_iters, fixed, slots):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    evaluated = []
+
+    def evaluate_counts(begin, count):
+        evaluated.append((begin, count))
+        return counts[begin * slots:(begin + count) * slots]
+
+    res = MD.global_replay(evaluate_counts, n, m, conf, max_iters, rank, world, MD.torch_allgather(dist),
+                           fixed=fixed, slots=slots)
+    q.put((rank, (res, sum(c for _, c in evaluated))))
+    dist.destroy_process_group()
+
+
+def run_replay(world, counts, n, m, conf, max_iters, fixed, slots=1):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_replay, args=(r, world, port, counts, q, n, m, conf, max_iters, fixed, slots))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    return out
+
+
 def _worker(rank, world, port, counts, q, m=4, slots=1):
     import torch
     import torch.distributed as dist
@@ -122,3 +153,43 @@ def test_distributed_essential_slots(oracle):
     out = run_ranks(2, c2, m=5, slots=10)
     for r in range(2):
         assert out[r][0] == bc2 and out[r][1] == best2 and out[r][2] == 4500
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_adaptive_replay_matches_sequential(oracle, world):
+    """Adaptive termination across ranks (no FIXED_ITERS): chunked sharding + all-gather of the counts
+    + the sequential replay on every rank equals the single-process replay (winner and stopping
+    point); the ranks evaluate no more than the chunks up to the stop."""
+    from minicv_amd import synthetic as S
+    n = 2000
+    src, dst, _ = S.homography_problem(n, 33, outlier_frac=0.6)
+    pts4 = oracle.pack4(src, dst)
+    max_iters = 20000
+    counts = oracle.h_counts(pts4, 33, 0, max_iters, float(np.float32(5e-3 ** 2)))
+    best, bc = oracle.replay(counts, n, 4, 0.995, max_iters, fixed=False)
+    out = run_replay(world, counts, n, 4, 0.995, max_iters, False)
+    total = sum(v[1] for v in out.values())
+    assert total < max_iters          # stopped early, like the sequential loop
+    for r in range(world):
+        assert out[r][0] == (bc, best)
+    best_f, bc_f = oracle.replay(counts, n, 4, 0.995, 3000, fixed=True)
+    out = run_replay(world, counts[:3000], n, 4, 0.995, 3000, True)
+    for r in range(world):
+        assert out[r][0] == (bc_f, best_f)
+
+
+def test_distributed_adaptive_replay_essential_slots_and_failure(oracle):
+    from minicv_amd import synthetic as S
+    a, b, *_ = S.essential_problem(400, seed=9, outlier_frac=0.5)
+    p = oracle.pack_e(a, b, 800.0, (640.0, 360.0))
+    counts = oracle.e_counts(p, 9, 0, 1000, float(np.float32((1.0 / 800.0) ** 2)))
+    best, bc = oracle.replay_slots(counts, 1000, 400, 5, 0.999, 1000, False)
+    out = run_replay(2, counts, 400, 5, 0.999, 1000, False, slots=10)
+    for r in range(2):
+        assert out[r][0] == (bc, best)
+    c2 = counts.copy()
+    c2[10 * 37] = -2                      # sampler failure: the loop breaks there
+    best2, bc2 = oracle.replay_slots(c2, 1000, 400, 5, 0.999, 1000, False)
+    out = run_replay(3, c2, 400, 5, 0.999, 1000, False, slots=10)
+    for r in range(3):
+        assert out[r][0] == (bc2, best2)

@@ -13,6 +13,26 @@ def test_fused_reciprocal_is_correctly_rounded_on_its_domain(native, gpu):
     assert n == 0, [hex(v) for v in first[:min(n, 16)]]
 
 
+def test_rcp_exact_is_ieee_everywhere(native, gpu):
+    """rcp_exact == IEEE 1.f/w for every 32-bit pattern, zeros / denormals / infinities / NaNs
+    included — what the certified sweep's exact path (h_error_pk) relies on to reproduce h_error's
+    division bit for bit."""
+    first = np.zeros(16, np.uint32)
+    n = native.lib().mcvTestRcpExhaustive(0, first.ctypes.data)
+    assert n == 0, [hex(v) for v in first[:min(n, 16)]]
+
+
+def test_div_fixup_does_not_repair_denormal_reciprocals(native, gpu):
+    """v_div_fixup_f32 after rcp_newton handles zeros / infinities / NaNs but not denormal inputs:
+    the mismatches of that form are exactly denormal w (why rcp_exact takes the IEEE division there)."""
+    first = np.zeros(16, np.uint32)
+    n = native.lib().mcvTestRcpExhaustive(2, first.ctypes.data)
+    assert n > 0
+    for v in first[:16]:
+        w = abs(float(np.array([v], np.uint32).view(np.float32)[0]))
+        assert w < 2.0**-126 or w >= 2.0**126
+
+
 def test_reciprocal_mismatches_only_outside_domain(native, gpu):
     """Outside that domain rcp_newton differs from 1.f/w for exactly the 3 * 2^24 patterns with
     |w| < 2^-126 or |w| >= 2^126 (zero/denormal: 2 * 2^23, huge/inf: 2 * 2^23 plus NaNs that
