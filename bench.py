@@ -250,6 +250,7 @@ def bench_matcher(args):
                                                     "train) pairs at 2.4 GHz"}},
                     "dtype": "u32", "scaling": "strong"}
         else:
+            exact_scans = NL.lib().mcvL2LastExactScans()
             flops = 2.0 * cnt * nt * 128
             tf = flops / (avg_ms * 1e-3) / 1e12
             line = {"metric": "BF L2 knn-2 TFLOP/s, SIFT-128 50k x 50k fp32 GEMM on MFMA (BASELINE config[4])",
@@ -258,6 +259,9 @@ def bench_matcher(args):
                                  "frac": tf / FP32_MFMA_PEAK_TF,
                                  "traffic": load_traffic("mcv_l2_mfma", f"{nq}x{nt}"), "kernel": "mcv_l2_mfma",
                                  "avg_launch_ms": avg_ms},
+                    "exact_rerank": {"queries_to_exact_scan": exact_scans,
+                                     "note": "idx / dist are the exact direct-sum answer (fp64, ties -> lowest "
+                                             "index); the GEMM form only nominates candidates"},
                     "dtype": "f32", "scaling": "strong"}
         line.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                      "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "vs_baseline": None,

@@ -223,6 +223,10 @@ MCV_API int cvMatchHamming(const uint8_t* q, const int nq, const uint8_t* t, con
 MCV_API int cvMatchL2(const float* q, const int nq, const float* t, const int nt, const int dim,
                       int* idx, float* dist, int* idx2, float* dist2);
 
+/* Diagnostics of the exact L2 re-rank: queries the calling thread's last L2 match sent to the exact
+ * full scan (near-ties the GEMM form cannot separate); synchronises the device. */
+MCV_API int mcvL2LastExactScans(void);
+
 /* Last error message of the calling thread ("" if none). */
 MCV_API const char* mcvGetLastError(void);
 /* Library / device info: number of visible HIP devices (0 when none), -1 on runtime error. */

@@ -95,3 +95,7 @@ extern "C" MCV_API int mcvMatchL2Device(const float* d_q, int nq, const float* d
         return launch_match_l2(d_q, nq, d_t, nt, dim, d_idx, d_dist, d_idx2, d_dist2, (hipStream_t)stream);
     })
 }
+
+extern "C" MCV_API int mcvL2LastExactScans(void) {
+    MCV_GUARD(-1, { return l2_last_exact_scans(); })
+}

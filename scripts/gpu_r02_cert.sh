@@ -1,10 +1,9 @@
 #!/bin/bash
 set -o pipefail
-mkdir -p gpurun_out/r02i
+mkdir -p gpurun_out/r02j
 export PYTHONUNBUFFERED=1
-MCV_HCERT_VARIANT=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
-    tests/test_gpu_selftest.py tests/test_gpu_homography.py > gpurun_out/r02i/pytest_v1.log 2>&1 || exit 2
-for v in 1 2 3 4 5 8 90 91; do
-  MCV_HCERT_VARIANT=$v timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu-baseline \
-      > gpurun_out/r02i/bench_h_v$v.json 2> gpurun_out/r02i/bench_h_v$v.err || exit 3
-done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+    tests/test_gpu_matchers.py tests/test_gpu_pipeline.py > gpurun_out/r02j/pytest_m.log 2>&1 || exit 2
+timeout -k 10 120 python bench.py --workload l2 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/r02j/bench_l2.json 2>&1 || exit 4
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r02j/prof_l2 -o run -- python3 bench.py --workload l2 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/r02j/prof_l2.log 2>&1 || exit 5

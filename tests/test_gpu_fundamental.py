@@ -186,3 +186,42 @@ def test_f_counts_prefilter_extremes(torch_dev, oracle, case):
         # (tiny: the 8-point sampler's absolute degeneracy tests reject every sample — parity only)
         assert case == "tiny" or (ref > 0).any()
     plan.close()
+
+
+@pytest.mark.slow
+def test_full_size_cfg4(torch_dev, oracle):
+    """BASELINE config[3] at full size: F-RANSAC over 500k correspondences, 65536 fixed hypotheses.
+    32 spot hypotheses equal the oracle's counts, the reduced key is the argmax of the device's own
+    counts, the winner's mask holds exactly its count, and the host export sharded over 8 workspaces
+    (deviceCount = 8; round-robin over the visible GPUs) is bit-identical to deviceCount = 1."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    n, H = 500_000, 1 << 16
+    a, b, _, _ = S.fundamental_problem(n, 4)
+    thr = 5e-3
+    pts = D.pack_points_tensor(a, b, dev)
+    plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, n, H)
+    cfg = opencv.RansacParams(threshold=thr, seed=4, fixed_iters=True, max_iters=H).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(H, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, 0, H, key, counts)
+    c = counts.cpu().numpy()
+    cnt, idx = D.unpack_key(int(key[0].item()))
+    assert cnt == c.max() and idx == int(np.argmax(c))
+    rng = np.random.default_rng(1)
+    pick = np.sort(rng.choice(H, size=32, replace=False))
+    p4 = oracle.pack4(a, b)
+    thr2 = float(np.float32(thr * thr))
+    for h in list(pick) + [idx]:
+        assert c[h] == oracle.f_counts(p4, 4, int(h), 1, thr2)[0], h
+    mask = torch.zeros(n, dtype=torch.uint8, device=dev)
+    fc, F = plan.finalize(pts, n, opencv.RansacParams(threshold=thr, seed=4).to_c(), idx, mask)
+    assert fc == cnt == int(mask.sum().item())
+    plan.close()
+    p1 = opencv.RansacParams(threshold=thr, seed=4, fixed_iters=True, max_iters=H)
+    p8 = opencv.RansacParams(threshold=thr, seed=4, fixed_iters=True, max_iters=H, device_count=8)
+    r1, r8 = opencv.findFundamentalMat(a, b, p1), opencv.findFundamentalMat(a, b, p8)
+    assert r1[0] == r8[0] == cnt
+    np.testing.assert_array_equal(r1[1], r8[1])
+    np.testing.assert_array_equal(r1[2], r8[2])
+    np.testing.assert_array_equal(r1[1], np.asarray(F).reshape(r1[1].shape))
