@@ -357,7 +357,7 @@ MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, uint64_t seed
                               double* model9, float* modelf9, int* sampleIdx);
 /* Device self-test: number of 32-bit patterns w where a reciprocal differs from 1.f/w (mode 0 =
  * rcp_exact; 1 = rcp_newton everywhere; 2 = rcp_newton + v_div_fixup; 3 = rcp_newton on its domain
- * |w| in [2^-126, 2^126) only; 4 = raw v_rcp_f32). */
+ * |w| in [2^-126, 2^126) only; 4 = raw v_rcp_f32; 5 = rcp_exact_bounded on |w| < 2^126 and NaN). */
 MCV_API long long mcvTestRcpExhaustive(int mode, uint32_t* firstMismatches16);
 /* Device self-test: number of sampled (n, d), d in +-[2^-64, 2^64], where the unscaled fp64
  * division (rcp_f64_refined + div_f64_refined) differs from n / d (mode 0: 2^-900 <= |n| < 2^700;

@@ -140,6 +140,18 @@ MCV_HD float rcp_newton(float w) {
 // overflow to inf included), +-inf for +-0, NaN for NaN. |w| >= 2^126 takes the IEEE division.
 // rcp_newton with v_div_fixup alone misrounds denormal inputs (mcvTestRcpExhaustive mode 2); this
 // form is checked over all 2^32 inputs (mode 0). Host: the IEEE division itself.
+// rcp_exact for |w| < 2^126 (or NaN) only — callers that bound |w| (the certified sweep's exact
+// path: |w| <= Bw (1 + 2^-20) <= 2^50) skip the division branch.
+MCV_HD float rcp_exact_bounded(float w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float sc = __builtin_fabsf(w) < 0x1p-126f ? 0x1p24f : 1.0f;
+    const float r = rcp_newton(w * sc) * sc;
+    return w == 0.0f ? __builtin_copysignf(__builtin_inff(), w) : r;
+#else
+    return 1.0f / w;
+#endif
+}
+
 MCV_HD float rcp_exact(float w) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const float aw = __builtin_fabsf(w);

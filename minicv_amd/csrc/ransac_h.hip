@@ -379,13 +379,25 @@ __global__ __launch_bounds__(256) void mcv_h_verify_pk(const HPair* __restrict__
 // ------------------------------------------------------------------------------------------
 // Band parameter: relative half-width ~ t + O(u) around thr2 w^2, absolute part ~ (7.5 u G)^2 / t.
 // One t for every model keeps the slopes launch constants.
-static constexpr double kCertT = 0x1p-12;
+static constexpr double kCertT = 0x1p-11;   // default band parameter (MCV_HCERT_T overrides: screens)
 static constexpr double kCertSlop = 0x1p-18;   // covers the O(u) factors (< 16 u = 2^-20 in total)
 
-struct HCertSlopes { f2 a; };   // {a_in (<= 0), d (>= 0)} (kernel argument)
+struct HCertSlopes {
+    f2 a;       // {a_in (<= 0), d (>= 0)}
+    double t;   // band parameter the per-model offsets use
+};
+
+static double cert_t() {
+    static const double t = [] {
+        const char* e = getenv("MCV_HCERT_T");
+        const double v = e ? atof(e) : 0.0;
+        return v > 0x1p-20 && v < 0x1p-4 ? v : kCertT;
+    }();
+    return t;
+}
 
 HCertSlopes h_cert_slopes_host(float thr2) {
-    const double T = (double)thr2, t = kCertT, u = 0x1p-24;
+    const double T = (double)thr2, t = cert_t(), u = 0x1p-24;
     // inlier cut: |a_in| <= T (1-t)/(1+t) (1 - slop), rounded towards zero
     const double ain = -T * (1.0 - t) / (1.0 + t) * (1.0 - kCertSlop);
     float fi = (float)ain;
@@ -397,15 +409,16 @@ HCertSlopes h_cert_slopes_host(float thr2) {
     if ((double)fd < d) fd = std::nextafter(fd, __builtin_inff());
     HCertSlopes c;
     c.a = f2{fi, fd};
+    c.t = t;
     return c;
 }
 
 // Per-model offsets b = {b_in, b_x} (both > 0); false when the model or the point set leaves the
 // domain of the error bound (the wave then hands its slots to the exact scalar sweep).
 // bb = {max|x|, max|y|, max|x'|, max|y'|} of the correspondences (inf when any is NaN / inf).
-__device__ __forceinline__ bool h_cert_offsets(const float* h, const double* bb, float thr2, f2& b) {
+__device__ __forceinline__ bool h_cert_offsets(const float* h, const double* bb, float thr2, double t, f2& b) {
     const double X = bb[0], Y = bb[1], MX = bb[2], MY = bb[3];
-    const double u = 0x1p-24, t = kCertT;
+    const double u = 0x1p-24;
     const double Bu = fabs((double)h[0]) * X + fabs((double)h[1]) * Y + fabs((double)h[2]);
     const double Bv = fabs((double)h[3]) * X + fabs((double)h[4]) * Y + fabs((double)h[5]);
     const double Bw = fabs((double)h[6]) * X + fabs((double)h[7]) * Y + 1.0;
@@ -481,11 +494,12 @@ __device__ __forceinline__ void h_cert_masks_asm(f2 I, f2 X, uint64_t& inx, uint
 }
 
 // h_error of both correspondences of a pair, packed, operation for operation (every product and sum
-// rounded as written) with the reciprocal by rcp_exact, which equals the IEEE 1.f / w for every w
-// (exhaustive GPU check, mcvTestRcpExhaustive mode 0): bit-identical to h_error.
+// rounded as written) with the reciprocal by rcp_exact_bounded, which equals the IEEE 1.f / w for
+// every |w| < 2^126 (exhaustive GPU check, mcvTestRcpExhaustive mode 5): bit-identical to h_error in
+// the certified sweep's domain (|w| <= Bw (1 + 2^-20), Bw <= 2^50).
 __device__ __forceinline__ f2 h_error_pk(f2 p0, f2 p1, f2 p2, f2 p3, const HPair& q) {
     const f2 w = (lo(p3) * q.x + hi(p3) * q.y) + f2{1.f, 1.f};
-    const f2 ww = f2{rcp_exact(w.x), rcp_exact(w.y)};
+    const f2 ww = f2{rcp_exact_bounded(w.x), rcp_exact_bounded(w.y)};   // |w| <= 2^51 in the certified domain
     const f2 ex = ((lo(p0) * q.x + hi(p0) * q.y) + lo(p1)) * ww - q.mx;
     const f2 ey = ((hi(p1) * q.x + lo(p2) * q.y) + hi(p2)) * ww - q.my;
     return ex * ex + ey * ey;
@@ -660,7 +674,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
         hc[k] = f2{hp[k][1].x, hp[k][2].y};
         float h[8];
         h_cert_model<K>(hp, k, h);
-        const bool ok = h_cert_offsets(h, b4, thr2, cb[k]);
+        const bool ok = h_cert_offsets(h, b4, thr2, slopes.t, cb[k]);
         fast = fast && (ok || !valid[k]);
         if (lane == 0) offsets[wib][k] = cb[k];
         __builtin_amdgcn_wave_barrier();
@@ -1112,7 +1126,6 @@ void launch_h_verify_certified(const float* d_pts4, const void* d_pairs, int N, 
     switch (cert_variant()) {
         case 1: launch_h_verify_cert_k<4, 2, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
         case 2: launch_h_verify_cert_k<4, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 3: launch_h_verify_cert_k<6, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
         case 4: launch_h_verify_cert_k<3, 2, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
         case 5: launch_h_verify_cert_k<4, 2, 1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
         case 6: launch_h_verify_cert_k<4, 2, 2, true>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
@@ -1120,7 +1133,9 @@ void launch_h_verify_certified(const float* d_pts4, const void* d_pairs, int N, 
         case 8: launch_h_verify_cert_k<5, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
         case 90: launch_h_verify_cert_k<4, 2, -1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
         case 91: launch_h_verify_cert_k<6, 1, -1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        default: launch_h_verify_cert_k<4, 2, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s);
+        // default <6, 1>: screened against <4, 2>, <4, 1>, <5, 1>, <3, 2>, <8, 2> and t = 2^-12 / 2^-11 / 2^-10
+        // (28.8 ms vs 29.6-33 ms at cfg3; scripts/gpu_r02_cert.sh)
+        default: launch_h_verify_cert_k<6, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s);
     }
     static const bool noredo = getenv("MCV_HCERT_NOREDO") != nullptr;   // diagnostics only
     if (noredo) return;

@@ -13,6 +13,7 @@ namespace mcv {
 // v_div_fixup_f32 (the special-value fixup alone does not repair denormal inputs); 4: raw v_rcp_f32
 __device__ __forceinline__ float rcp_variant(float w, int mode) {
     if (mode == 0) return rcp_exact(w);
+    if (mode == 5) return rcp_exact_bounded(w);
     if (mode == 1 || mode == 3) return rcp_newton(w);
     const float r = __builtin_amdgcn_rcpf(w);
     if (mode == 4) return r;
@@ -31,6 +32,7 @@ __global__ __launch_bounds__(256) void mcv_rcp_check(uint64_t begin, uint64_t co
             const float aw = fabsf(w);
             if (!(aw >= 0x1p-126f && aw < 0x1p126f)) continue;
         }
+        if (mode == 5 && fabsf(w) >= 0x1p126f) continue;   // rcp_exact_bounded's domain: |w| < 2^126, NaN
         const float a = rcp_variant(w, mode);
         const float b = 1.0f / w;
         const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);

@@ -1,9 +1,12 @@
 #!/bin/bash
 set -o pipefail
-mkdir -p gpurun_out/r02j
+mkdir -p gpurun_out/r02k
 export PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
-    tests/test_gpu_matchers.py tests/test_gpu_pipeline.py > gpurun_out/r02j/pytest_m.log 2>&1 || exit 2
-timeout -k 10 120 python bench.py --workload l2 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/r02j/bench_l2.json 2>&1 || exit 4
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r02j/prof_l2 -o run -- python3 bench.py --workload l2 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/r02j/prof_l2.log 2>&1 || exit 5
+MCV_HCERT_VARIANT=3 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+    tests/test_gpu_selftest.py tests/test_gpu_homography.py > gpurun_out/r02k/pytest_v3.log 2>&1 || exit 2
+for t in 0.000244140625 0.00048828125 0.0009765625; do
+for v in 3 8 2; do
+  MCV_HCERT_T=$t MCV_HCERT_VARIANT=$v timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu-baseline \
+      > gpurun_out/r02k/bench_h_v${v}_t$t.json 2> gpurun_out/r02k/bench_h_v${v}_t$t.err || exit 3
+done
+done

@@ -22,6 +22,13 @@ def test_rcp_exact_is_ieee_everywhere(native, gpu):
     assert n == 0, [hex(v) for v in first[:min(n, 16)]]
 
 
+def test_rcp_exact_bounded_is_ieee_on_its_domain(native, gpu):
+    """rcp_exact_bounded (no division branch) == IEEE 1.f/w for every pattern with |w| < 2^126 or NaN."""
+    first = np.zeros(16, np.uint32)
+    n = native.lib().mcvTestRcpExhaustive(5, first.ctypes.data)
+    assert n == 0, [hex(v) for v in first[:min(n, 16)]]
+
+
 def test_div_fixup_does_not_repair_denormal_reciprocals(native, gpu):
     """v_div_fixup_f32 after rcp_newton handles zeros / infinities / NaNs but not denormal inputs:
     the mismatches of that form are exactly denormal w (why rcp_exact takes the IEEE division there)."""
