@@ -128,6 +128,8 @@ def parse():
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pnp-kind", default="EPNP", choices=["Iterative", "EPNP", "P3P", "DLS", "UPNP", "AP3P"],
+                    help="pnp workload: the reference's solverKind (EPNP = its own testPnp, Program.fs:27-32)")
     ap.add_argument("--fused", action="store_true",
                     help="opt-in FMA-contracted inlier error (default: OpenCV's op-by-op order, the reference's)")
     ap.add_argument("--workload", default="homography",
@@ -614,7 +616,7 @@ def bench_essential(args, world, rank, dev):
     plan.close()
 
 
-def cpu_baseline_p(img, W, K, d, target_s: float):
+def cpu_baseline_p(img, W, K, d, target_s: float, kind: int = 1):
     sys.path.insert(0, str(ROOT / "tests"))
     import numpy as np
     import _oracle as O
@@ -622,15 +624,16 @@ def cpu_baseline_p(img, W, K, d, target_s: float):
     thr2 = float(np.float32(P_THR_PX * P_THR_PX))
     threads = cpu_threads()
     t = time.perf_counter()
-    O.pnp_counts(pts8, c8, P_SEED, 0, 4 * threads, thr2, False, threads)
+    O.pnp_counts(pts8, c8, P_SEED, 0, 4 * threads, thr2, False, threads, kind=kind)
     cal = (time.perf_counter() - t) / (4 * threads)
     sample = max(4 * threads, int(target_s / max(cal, 1e-6)))
     t = time.perf_counter()
-    O.pnp_counts(pts8, c8, P_SEED, 0, sample, thr2, False, threads)
+    O.pnp_counts(pts8, c8, P_SEED, 0, sample, thr2, False, threads, kind=kind)
     el = time.perf_counter() - t
+    solver = "4-pt AP3P" if kind in (2, 5) else "5-pt EPnP"
     return {"value": sample / el, "unit": "hypotheses/s", "cores": threads, "kind": "port", "host": host_cpu(),
-            "sample": f"{sample} hypotheses x {img.shape[0]} correspondences (4-pt AP3P sample+solve, projectPoints "
-                      f"fp32 error count), oracle/oracle_pnp.c, OpenMP {threads} threads, {el:.1f} s"}
+            "sample": f"{sample} hypotheses x {img.shape[0]} correspondences ({solver} sample+solve, projectPoints "
+                      f"fp32 error count), oracle/oracle_pnp.c + oracle_epnp.c, OpenMP {threads} threads, {el:.1f} s"}
 
 
 def bench_pnp(args, world, rank, dev):
@@ -655,6 +658,8 @@ def bench_pnp(args, world, rank, dev):
     plan.set_camera(K, d)
     cfg = opencv.RansacParams(threshold=P_THR_PX, confidence=0.99, max_iters=total, seed=P_SEED,
                               fixed_iters=True, fused_error=args.fused).to_c()
+    kind = opencv.SOLVER_KIND[args.pnp_kind]
+    cfg.pnpKind = kind
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = torch.zeros(n, dtype=torch.uint8, device=dev)
     red = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -709,13 +714,15 @@ def bench_pnp(args, world, rank, dev):
         p_bytes = 20.0 * n * hyps                # PnpPoint {X, Y, Z, u, v} f32 per (hypothesis, correspondence)
         p_fl = P_FLOPS_PER_EVAL * n * hyps / (v_ms * 1e-3) / 1e12
         line = {
-            "metric": "RANSAC hypotheses/sec, solvePnPRansac AP3P (cvSolvePnPRansac path) @20k corrs",
+            "metric": f"RANSAC hypotheses/sec, solvePnPRansac {args.pnp_kind} (cvSolvePnPRansac path) @20k corrs",
             "value": total * args.steps / el, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded 2D-3D problem after Program.fs:8-24, 50% outliers, sigma 0.5 px, k1 k2 p1 p2)",
-            "config": {"workload": f"solvePnPRansac AP3P, {n} correspondences x {total} hypotheses per call sharded "
-                                   f"over {world} GPU(s) + LM refit", "correspondences": n,
+            "config": {"workload": f"solvePnPRansac {args.pnp_kind} ({'4-pt AP3P' if kind in (2, 5) else '5-pt EPnP'}"
+                                   f" minimal sets), {n} correspondences x {total} hypotheses per call sharded over "
+                                   f"{world} GPU(s) + {'LM' if kind == 0 else 'EPnP'} inlier solve",
+                       "correspondences": n, "solver_kind": kind,
                        "hypotheses_total": total, "threshold_px": P_THR_PX,
                        "parallelism": f"hypothesis-sharded dp{world}"},
             "kernels": {"mcv_pnp_verify": {"avg_launch_ms": v_ms, "launches": vl,
@@ -731,7 +738,7 @@ def bench_pnp(args, world, rank, dev):
             "result": {"best_count": result["count"], "best_hyp": result["idx"],
                        "final_count": result["final_count"], "true_inliers": int(inl.sum())},
         }
-        line["cpu_baseline"] = (cpu_baseline_p(img, W, K, d, args.cpu_seconds)
+        line["cpu_baseline"] = (cpu_baseline_p(img, W, K, d, args.cpu_seconds, kind)
                                 if world == 1 and not args.no_cpu_baseline else None)
         print(json.dumps(line), flush=True)
     plan.close()

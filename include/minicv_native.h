@@ -159,7 +159,9 @@ typedef struct {
     int    deviceCount;   /* 0/1: one GPU; >1 shard hypotheses over that many local GPUs */
     int    flags;         /* MCV_FLAG_* */
     int    errorKind;     /* MCV_FERR_* (fundamental only) */
-    int    reserved;
+    int    pnpKind;       /* PnP only: the reference's solverKind (0 ITERATIVE, 1 EPNP, 2 P3P, 3 DLS, 4 UPNP,
+                             5 AP3P; others = 0). 2 / 5: AP3P on 4-point sets; else EPnP on 5-point sets.
+                             Final pose on the inliers: LM from the RANSAC pose (0), EPnP (1-5). */
 } RansacConfig;           /* 48 bytes */
 
 /* findHomography. src/dst: N AoS fp64 points (converted to fp32 like OpenCV's convertTo(CV_32F)).
@@ -276,9 +278,10 @@ typedef struct mcvRansacPlan_ mcvRansacPlan;
                                       hypothesis h owns model slots 10h .. 10h+9: keys, counts and
                                       indices below are slot indices for this model */
 #define MCV_MODEL_PNP          3   /* points: PnpPoint {X, Y, Z, u, v, pad[3]} fp32 (mcvPackPnP); camera
-                                      via mcvRansacPlanSetCamera; threshold in pixels; finalize
-                                      writes model9 = {rvec[3], tvec[3], 0, 0, 0} (LM-refined unless
-                                      MCV_FLAG_NO_REFINE) */
+                                      via mcvRansacPlanSetCamera; threshold in pixels; cfg->pnpKind
+                                      picks the minimal solver; finalize writes model9 = {rvec[3],
+                                      tvec[3], 0, 0, 0}, the inlier solve of cfg->pnpKind unless
+                                      MCV_FLAG_NO_REFINE */
 
 /* Workspace for problems up to maxN correspondences and maxHyps hypotheses per evaluate call. */
 MCV_API mcvRansacPlan* mcvRansacPlanCreate(int model, int maxN, int64_t maxHyps);
@@ -381,6 +384,16 @@ MCV_API int mcvHostRealRoots(const double* c, int deg, int fixed, double* roots)
  * p1, p2), and the Rodrigues maps used by the LM refit. */
 MCV_API int mcvHostPnP(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9, double* t3,
                        int* idx4);
+/* EPnP twins: a 5-point EPnP hypothesis (idx5: the sample), and epnp_solve_small<5> on given world
+ * points pw15 (5 x 3) and pixel observations us10 (5 x 2), cam4 = fu, fv, uc, vc. */
+MCV_API int mcvHostPnPEpnp(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9,
+                           double* t3, int* idx5);
+MCV_API void mcvHostEpnp5(const double* pw15, const double* us10, const double* cam4, double* R9, double* t3);
+/* Device self-test: the PnP generate kernel's poses for hypotheses [hypBegin, hypBegin + hypCount) on
+ * host PnpPoint[N] (kind: solverKind, EPnP kernel unless 2 / 5). poses12[h] = {R (9), t (3)},
+ * status[h] = 1 or -1 / -2. Returns hypCount, -1 on failure. */
+MCV_API int mcvTestPnpHypotheses(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin,
+                                 int hypCount, int kind, double* poses12, int* status);
 MCV_API void mcvHostRodrigues(const double* r, double* R, double* dR27);
 MCV_API void mcvHostRodriguesInv(const double* R, double* r);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,

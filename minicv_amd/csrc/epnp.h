@@ -1,0 +1,558 @@
+// epnp.h — EPnP (Lepetit, Moreno-Noguer, Fua, IJCV 2009) as OpenCV 4.x's epnp.cpp computes it
+// [ext: OpenCV calib3d, not vendored in /root/reference], for the solverKind 0/1/3/4 paths of
+// cvSolvePnPRansac / cvSolvePnP (reference MiniCVNative.cpp:48-139; SOLVEPNP_DLS / UPNP fall back
+// to EPnP in OpenCV 4.x). Compiled for gfx950 (one RANSAC hypothesis per lane, 5 points) and for
+// the host (the O(1) dense algebra of the inlier solve) with -ffp-contract=off, so both sides
+// round every operation identically; oracle/oracle_epnp.c restates the same algorithm in C.
+//
+// Restated pieces (operation order as written in the OpenCV sources):
+//  * compute_pose: control points (centroid + PCA of the centred world points through cvSVD),
+//    barycentric alphas (cvInvert DECOMP_SVD), M^T M (cvMulTransposed), its SVD, L_6x10 / rho,
+//    betas of the three approximations (cvSolve DECOMP_SVD), 5 Gauss-Newton steps each
+//    (epnp::qr_solve, Householder, including its pivot-scan that skips the last row), then
+//    compute_R_and_t (ccs, pcs, solve_for_sign, estimate_R_and_t via the SVD of ABt) and the
+//    mean reprojection error picking N = 1, 2 or 3 (first minimum).
+//  * cv::SVD / cv::solve / cv::invert: JacobiSVDImpl_<double> (one-sided cyclic Jacobi on the
+//    transposed matrix, eps = 10 DBL_EPSILON, at most max(m, 30) sweeps, descending selection
+//    sort, cv::RNG(0x12345678) fill of null singular vectors) and SVBkSb (threshold 2 DBL_EPSILON
+//    x sum w). The scalar loop order of the generic template is restated; x86 builds may run
+//    some of those loops through SIMD helpers (VBLAS) with other partial-sum orders [ext].
+//  * std::hypot is replaced by hypot_fma (Borges' FMA-corrected square root), identical on both
+//    sides; libm's hypot may differ from it in the last bit.
+// Large point sets (the inlier solve) sum per-point terms in blocks of kEpnpBlock consecutive
+// points, each block sequentially from 0, the block sums sequentially: for n <= kEpnpBlock this
+// is exactly the sequential order of the OpenCV loops.
+#pragma once
+
+#include "mcv_common.h"
+
+namespace mcv {
+
+static const double kDblMin = 2.2250738585072014e-308;
+static const int kEpnpBlock = 1024;
+
+// cv::RNG: multiply-with-carry, state = (uint32)state * 4164903690 + (state >> 32).
+struct CvRng {
+    uint64_t s;
+    MCV_HD uint32_t next() {
+        s = (uint64_t)(uint32_t)s * 4164903690u + (uint32_t)(s >> 32);
+        return (uint32_t)s;
+    }
+};
+
+// sqrt(x^2 + y^2) with one FMA-based correction step (Borges 2019); power-of-two scaling keeps the
+// squares inside the normal range. Deterministic: only +, -, *, /, sqrt and fma.
+MCV_HD double hypot_fma(double x, double y) {
+    x = __builtin_fabs(x);
+    y = __builtin_fabs(y);
+    if (!(x <= 1.7976931348623157e308) || !(y <= 1.7976931348623157e308)) {
+        if (x == __builtin_inf() || y == __builtin_inf()) return __builtin_inf();
+        return x + y;   // NaN
+    }
+    if (x < y) { const double t = x; x = y; y = t; }
+    if (y == 0) return x;
+    double sc = 1.0;
+    if (x > 0x1p500) { x *= 0x1p-600; y *= 0x1p-600; sc = 0x1p600; }
+    else if (x < 0x1p-500) { x *= 0x1p600; y *= 0x1p600; sc = 0x1p-600; }
+    double h = __builtin_sqrt(__builtin_fma(x, x, y * y));
+    const double h2 = h * h, x2 = x * x;
+    h -= (__builtin_fma(-y, y, h2 - x2) + __builtin_fma(h, h, -h2) - __builtin_fma(x, x, -x2)) / (2 * h);
+    return h * sc;
+}
+
+// JacobiSVDImpl_<double>: A holds the N rows of length M of the TRANSPOSED input (At). On return
+// A's rows are the left singular vectors (normalised), Wo the singular values (descending), and
+// Vt (if non-null) the right singular vectors as rows. The A result does not depend on Vt.
+template <int M, int N>
+MCV_HD void jacobi_svd(double (&A)[N][M], double (&Wo)[N], double (*Vt)[N]) {
+    const double eps = kDblEpsilon * 10, minval = kDblMin;
+    double W[N];
+    for (int i = 0; i < N; ++i) {
+        double sd = 0;
+        for (int k = 0; k < M; ++k) sd += A[i][k] * A[i][k];
+        W[i] = sd;
+        if (Vt)
+            for (int k = 0; k < N; ++k) Vt[i][k] = k == i ? 1.0 : 0.0;
+    }
+    const int maxIter = M > 30 ? M : 30;
+    for (int iter = 0; iter < maxIter; ++iter) {
+        bool changed = false;
+        for (int i = 0; i < N - 1; ++i)
+            for (int j = i + 1; j < N; ++j) {
+                double a = W[i], b = W[j], p = 0;
+                for (int k = 0; k < M; ++k) p += A[i][k] * A[j][k];
+                if (__builtin_fabs(p) <= eps * __builtin_sqrt(a * b)) continue;
+                p *= 2;
+                const double beta = a - b, gamma = hypot_fma(p, beta);
+                double c, s;
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = __builtin_sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = __builtin_sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                a = b = 0;
+                for (int k = 0; k < M; ++k) {
+                    const double t0 = c * A[i][k] + s * A[j][k];
+                    const double t1 = -s * A[i][k] + c * A[j][k];
+                    A[i][k] = t0;
+                    A[j][k] = t1;
+                    a += t0 * t0;
+                    b += t1 * t1;
+                }
+                W[i] = a;
+                W[j] = b;
+                changed = true;
+                if (Vt)
+                    for (int k = 0; k < N; ++k) {
+                        const double t0 = c * Vt[i][k] + s * Vt[j][k];
+                        const double t1 = -s * Vt[i][k] + c * Vt[j][k];
+                        Vt[i][k] = t0;
+                        Vt[j][k] = t1;
+                    }
+            }
+        if (!changed) break;
+    }
+    for (int i = 0; i < N; ++i) {
+        double sd = 0;
+        for (int k = 0; k < M; ++k) sd += A[i][k] * A[i][k];
+        W[i] = __builtin_sqrt(sd);
+    }
+    for (int i = 0; i < N - 1; ++i) {
+        int j = i;
+        for (int k = i + 1; k < N; ++k)
+            if (W[j] < W[k]) j = k;
+        if (i != j) {
+            const double tw = W[i]; W[i] = W[j]; W[j] = tw;
+            for (int k = 0; k < M; ++k) { const double t = A[i][k]; A[i][k] = A[j][k]; A[j][k] = t; }
+            if (Vt)
+                for (int k = 0; k < N; ++k) { const double t = Vt[i][k]; Vt[i][k] = Vt[j][k]; Vt[j][k] = t; }
+        }
+    }
+    for (int i = 0; i < N; ++i) Wo[i] = W[i];
+    CvRng rng{0x12345678u};
+    for (int i = 0; i < N; ++i) {
+        double sd = W[i];
+        for (int ii = 0; ii < 100 && sd <= minval; ++ii) {
+            // null singular value: random +-1/M vector orthogonalised against the previous rows
+            const double val0 = 1. / M;
+            for (int k = 0; k < M; ++k) A[i][k] = (rng.next() & 256) != 0 ? val0 : -val0;
+            for (int it = 0; it < 2; ++it)
+                for (int j = 0; j < i; ++j) {
+                    sd = 0;
+                    for (int k = 0; k < M; ++k) sd += A[i][k] * A[j][k];
+                    double asum = 0;
+                    for (int k = 0; k < M; ++k) {
+                        const double t = A[i][k] - sd * A[j][k];
+                        A[i][k] = t;
+                        asum += __builtin_fabs(t);
+                    }
+                    asum = asum > eps * 100 ? 1 / asum : 0;
+                    for (int k = 0; k < M; ++k) A[i][k] *= asum;
+                }
+            sd = 0;
+            for (int k = 0; k < M; ++k) sd += A[i][k] * A[i][k];
+            sd = __builtin_sqrt(sd);
+        }
+        const double s = sd > minval ? 1 / sd : 0.;
+        for (int k = 0; k < M; ++k) A[i][k] *= s;
+    }
+}
+
+// SVBkSb for one right-hand side: x = sum_i [|w_i| > 2 eps sum w] (u_i . b / w_i) v_i, with
+// u_i = U[i] (rows of the jacobi_svd A result) and v_i = Vt[i].
+template <int M, int N>
+MCV_HD void svd_backsubst(const double (&U)[N][M], const double (&w)[N], const double (&Vt)[N][N],
+                          const double (&b)[M], double (&x)[N]) {
+    double thr = 0;
+    for (int i = 0; i < N; ++i) thr += w[i];
+    thr *= kDblEpsilon * 2;
+    for (int j = 0; j < N; ++j) x[j] = 0;
+    for (int i = 0; i < N; ++i) {
+        double wi = w[i];
+        if (__builtin_fabs(wi) <= thr) continue;
+        wi = 1 / wi;
+        double s = 0;
+        for (int j = 0; j < M; ++j) s += U[i][j] * b[j];
+        s *= wi;
+        for (int j = 0; j < N; ++j) x[j] = x[j] + s * Vt[i][j];
+    }
+}
+
+// cv::invert(DECOMP_SVD) of a square matrix given its decomposition (SVBkSb with b = I).
+template <int N>
+MCV_HD void svd_pinv(const double (&U)[N][N], const double (&w)[N], const double (&Vt)[N][N], double (&X)[N][N]) {
+    double thr = 0;
+    for (int i = 0; i < N; ++i) thr += w[i];
+    thr *= kDblEpsilon * 2;
+    for (int r = 0; r < N; ++r)
+        for (int c = 0; c < N; ++c) X[r][c] = 0;
+    for (int i = 0; i < N; ++i) {
+        double wi = w[i];
+        if (__builtin_fabs(wi) <= thr) continue;
+        wi = 1 / wi;
+        double buf[N];
+        for (int c = 0; c < N; ++c) buf[c] = U[i][c] * wi;
+        for (int r = 0; r < N; ++r) {
+            const double s = Vt[i][r];
+            for (int c = 0; c < N; ++c) X[r][c] = X[r][c] + s * buf[c];
+        }
+    }
+}
+
+// cv::solve(L, rho, x, DECOMP_SVD) for a 6 x K system.
+template <int K>
+MCV_HD void svd_solve6(const double (&L)[6][K], const double (&rho)[6], double (&x)[K]) {
+    double A[K][6], w[K], Vt[K][K];
+    for (int i = 0; i < K; ++i)
+        for (int r = 0; r < 6; ++r) A[i][r] = L[r][i];
+    jacobi_svd<6, K>(A, w, Vt);
+    svd_backsubst<6, K>(A, w, Vt, rho, x);
+}
+
+MCV_HD double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+struct EpnpCam { double fu, fv, uc, vc; };
+
+// Control points and the inverse of their difference matrix (choose_control_points +
+// compute_barycentric_coordinates' cvInvert).
+struct EpnpCtrl {
+    double cws[4][3];
+    double ccinv[3][3];
+};
+
+// cws[0] = sum / n; PCA of the centred points: PW0^T PW0 (symmetric, full) -> cvSVD(U^T).
+MCV_HD void epnp_control(const double (&sum)[3], const double (&pw0tpw0)[3][3], int n, EpnpCtrl& C) {
+    for (int j = 0; j < 3; ++j) C.cws[0][j] = sum[j] / n;
+    double A[3][3], dc[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A[i][j] = pw0tpw0[j][i];
+    jacobi_svd<3, 3>(A, dc, (double(*)[3])nullptr);   // A = U^T (uct)
+    for (int i = 1; i < 4; ++i) {
+        const double k = __builtin_sqrt(dc[i - 1] / n);
+        for (int j = 0; j < 3; ++j) C.cws[i][j] = C.cws[0][j] + k * A[i - 1][j];
+    }
+    double B[3][3], w[3], Vt[3][3];
+    for (int i = 0; i < 3; ++i)            // B = CC^T; CC[i][j - 1] = cws[j][i] - cws[0][i]
+        for (int j = 1; j < 4; ++j) B[j - 1][i] = C.cws[j][i] - C.cws[0][i];
+    jacobi_svd<3, 3>(B, w, Vt);
+    svd_pinv<3>(B, w, Vt, C.ccinv);
+}
+
+MCV_HD void epnp_alphas(const EpnpCtrl& C, const double* p, double (&a)[4]) {
+    for (int j = 0; j < 3; ++j)
+        a[1 + j] = C.ccinv[j][0] * (p[0] - C.cws[0][0]) + C.ccinv[j][1] * (p[1] - C.cws[0][1]) +
+                   C.ccinv[j][2] * (p[2] - C.cws[0][2]);
+    a[0] = 1.0 - a[1] - a[2] - a[3];
+}
+
+// The two rows of M for one point (fill_M).
+MCV_HD void epnp_m_rows(const double (&a)[4], double u, double v, const EpnpCam& c, double (&r1)[12],
+                        double (&r2)[12]) {
+    for (int i = 0; i < 4; ++i) {
+        r1[3 * i] = a[i] * c.fu;
+        r1[3 * i + 1] = 0.0;
+        r1[3 * i + 2] = a[i] * (c.uc - u);
+        r2[3 * i] = 0.0;
+        r2[3 * i + 1] = a[i] * c.fv;
+        r2[3 * i + 2] = a[i] * (c.vc - v);
+    }
+}
+
+// Upper triangle of M^T M, row-major (a <= b): 78 sums.
+static const int kMtmSums = 78;
+MCV_HD int mtm_index(int a, int b) { return a * 12 - a * (a - 1) / 2 + (b - a); }
+
+// The four null-space vectors (rows 11, 10, 9, 8 of U^T of M^T M) and everything that depends
+// only on them and the control points: L_6x10, rho and the betas of the three approximations
+// after Gauss-Newton.
+struct EpnpBetas {
+    double v[4][12];
+    double betas[4][4];   // [N][.] for N = 1, 2, 3 (index 0 unused)
+};
+
+MCV_HD void epnp_qr_solve(double (&A)[6][4], double (&b)[6], double (&X)[4]) {
+    const int nr = 6, nc = 4;
+    double A1[4], A2[4];
+    for (int k = 0; k < nc; ++k) {
+        // epnp::qr_solve's pivot scan: |A[k][k]| twice, then rows k+1 .. nr-2 (never row nr-1)
+        double eta = __builtin_fabs(A[k][k]);
+        for (int i = k + 1; i < nr; ++i) {
+            const double elt = __builtin_fabs(A[i - 1][k]);
+            if (eta < elt) eta = elt;
+        }
+        if (eta == 0) return;   // A1[k] = A2[k] = 0 and X unchanged
+        double sum2 = 0.0;
+        const double inv_eta = 1. / eta;
+        for (int i = k; i < nr; ++i) {
+            A[i][k] *= inv_eta;
+            sum2 += A[i][k] * A[i][k];
+        }
+        double sigma = __builtin_sqrt(sum2);
+        if (A[k][k] < 0) sigma = -sigma;
+        A[k][k] += sigma;
+        A1[k] = sigma * A[k][k];
+        A2[k] = -eta * sigma;
+        for (int j = k + 1; j < nc; ++j) {
+            double sum = 0;
+            for (int i = k; i < nr; ++i) sum += A[i][k] * A[i][j];
+            const double tau = sum / A1[k];
+            for (int i = k; i < nr; ++i) A[i][j] -= tau * A[i][k];
+        }
+    }
+    for (int j = 0; j < nc; ++j) {
+        double tau = 0;
+        for (int i = j; i < nr; ++i) tau += A[i][j] * b[i];
+        tau /= A1[j];
+        for (int i = j; i < nr; ++i) b[i] -= tau * A[i][j];
+    }
+    X[nc - 1] = b[nc - 1] / A2[nc - 1];
+    for (int i = nc - 2; i >= 0; --i) {
+        double sum = 0;
+        for (int j = i + 1; j < nc; ++j) sum += A[i][j] * X[j];
+        X[i] = (b[i] - sum) / A2[i];
+    }
+}
+
+MCV_HD void epnp_gauss_newton(const double (&L)[6][10], const double (&rho)[6], double (&be)[4]) {
+    double X[4] = {0, 0, 0, 0};   // kept across iterations, as epnp::gauss_newton's x
+    for (int it = 0; it < 5; ++it) {
+        double A[6][4], b[6];
+        for (int i = 0; i < 6; ++i) {
+            const double* l = L[i];
+            A[i][0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
+            A[i][1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
+            A[i][2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
+            A[i][3] = l[6] * be[0] + l[7] * be[1] + l[8] * be[2] + 2 * l[9] * be[3];
+            b[i] = rho[i] - (l[0] * be[0] * be[0] + l[1] * be[0] * be[1] + l[2] * be[1] * be[1] +
+                             l[3] * be[0] * be[2] + l[4] * be[1] * be[2] + l[5] * be[2] * be[2] +
+                             l[6] * be[0] * be[3] + l[7] * be[1] * be[3] + l[8] * be[2] * be[3] +
+                             l[9] * be[3] * be[3]);
+        }
+        epnp_qr_solve(A, b, X);
+        for (int i = 0; i < 4; ++i) be[i] += X[i];
+    }
+}
+
+MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBetas& B) {
+    {
+        // cvSVD(MtM, D, Ut, 0, MODIFY_A | U_T): Jacobi on transpose(MtM) (= MtM after completeSymm)
+        double A[12][12], w[12];
+        for (int a = 0; a < 12; ++a)
+            for (int b = a; b < 12; ++b) A[a][b] = A[b][a] = mtm[mtm_index(a, b)];
+        jacobi_svd<12, 12>(A, w, (double(*)[12])nullptr);
+        for (int i = 0; i < 4; ++i)
+            for (int k = 0; k < 12; ++k) B.v[i][k] = A[11 - i][k];
+    }
+    double L[6][10], rho[6];
+    {
+        double dv[4][6][3];
+        for (int i = 0; i < 4; ++i) {
+            int a = 0, b = 1;
+            for (int j = 0; j < 6; ++j) {
+                for (int k = 0; k < 3; ++k) dv[i][j][k] = B.v[i][3 * a + k] - B.v[i][3 * b + k];
+                ++b;
+                if (b > 3) { ++a; b = a + 1; }
+            }
+        }
+        for (int i = 0; i < 6; ++i) {
+            L[i][0] = dot3(dv[0][i], dv[0][i]);
+            L[i][1] = 2.0 * dot3(dv[0][i], dv[1][i]);
+            L[i][2] = dot3(dv[1][i], dv[1][i]);
+            L[i][3] = 2.0 * dot3(dv[0][i], dv[2][i]);
+            L[i][4] = 2.0 * dot3(dv[1][i], dv[2][i]);
+            L[i][5] = dot3(dv[2][i], dv[2][i]);
+            L[i][6] = 2.0 * dot3(dv[0][i], dv[3][i]);
+            L[i][7] = 2.0 * dot3(dv[1][i], dv[3][i]);
+            L[i][8] = 2.0 * dot3(dv[2][i], dv[3][i]);
+            L[i][9] = dot3(dv[3][i], dv[3][i]);
+        }
+        const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
+        for (int i = 0; i < 6; ++i) {
+            const double* p1 = C.cws[pa[i]];
+            const double* p2 = C.cws[pb[i]];
+            rho[i] = (p1[0] - p2[0]) * (p1[0] - p2[0]) + (p1[1] - p2[1]) * (p1[1] - p2[1]) +
+                     (p1[2] - p2[2]) * (p1[2] - p2[2]);
+        }
+    }
+    for (int k = 0; k < 4; ++k) B.betas[0][k] = 0;
+    {   // approximation 1: [B11 B12 B13 B14]
+        double L4[6][4], b4[4];
+        for (int i = 0; i < 6; ++i) { L4[i][0] = L[i][0]; L4[i][1] = L[i][1]; L4[i][2] = L[i][3]; L4[i][3] = L[i][6]; }
+        svd_solve6<4>(L4, rho, b4);
+        double* be = B.betas[1];
+        if (b4[0] < 0) {
+            be[0] = __builtin_sqrt(-b4[0]);
+            be[1] = -b4[1] / be[0];
+            be[2] = -b4[2] / be[0];
+            be[3] = -b4[3] / be[0];
+        } else {
+            be[0] = __builtin_sqrt(b4[0]);
+            be[1] = b4[1] / be[0];
+            be[2] = b4[2] / be[0];
+            be[3] = b4[3] / be[0];
+        }
+        epnp_gauss_newton(L, rho, B.betas[1]);
+    }
+    {   // approximation 2: [B11 B12 B22]
+        double L3[6][3], b3[3];
+        for (int i = 0; i < 6; ++i) { L3[i][0] = L[i][0]; L3[i][1] = L[i][1]; L3[i][2] = L[i][2]; }
+        svd_solve6<3>(L3, rho, b3);
+        double* be = B.betas[2];
+        if (b3[0] < 0) {
+            be[0] = __builtin_sqrt(-b3[0]);
+            be[1] = (b3[2] < 0) ? __builtin_sqrt(-b3[2]) : 0.0;
+        } else {
+            be[0] = __builtin_sqrt(b3[0]);
+            be[1] = (b3[2] > 0) ? __builtin_sqrt(b3[2]) : 0.0;
+        }
+        if (b3[1] < 0) be[0] = -be[0];
+        be[2] = 0.0;
+        be[3] = 0.0;
+        epnp_gauss_newton(L, rho, B.betas[2]);
+    }
+    {   // approximation 3: [B11 B12 B22 B13 B23]
+        double L5[6][5], b5[5];
+        for (int i = 0; i < 6; ++i)
+            for (int k = 0; k < 5; ++k) L5[i][k] = L[i][k];
+        svd_solve6<5>(L5, rho, b5);
+        double* be = B.betas[3];
+        if (b5[0] < 0) {
+            be[0] = __builtin_sqrt(-b5[0]);
+            be[1] = (b5[2] < 0) ? __builtin_sqrt(-b5[2]) : 0.0;
+        } else {
+            be[0] = __builtin_sqrt(b5[0]);
+            be[1] = (b5[2] > 0) ? __builtin_sqrt(b5[2]) : 0.0;
+        }
+        if (b5[1] < 0) be[0] = -be[0];
+        be[2] = b5[3] / be[0];
+        be[3] = 0.0;
+        epnp_gauss_newton(L, rho, B.betas[3]);
+    }
+}
+
+// Control points in the camera frame for one beta vector (compute_ccs).
+MCV_HD void epnp_ccs(const EpnpBetas& B, const double (&be)[4], double (&ccs)[4][3]) {
+    for (int j = 0; j < 4; ++j)
+        for (int k = 0; k < 3; ++k) ccs[j][k] = 0.0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            for (int k = 0; k < 3; ++k) ccs[j][k] += be[i] * B.v[i][3 * j + k];
+}
+
+MCV_HD void epnp_pc(const double (&a)[4], const double (&ccs)[4][3], double (&pc)[3]) {
+    for (int j = 0; j < 3; ++j) pc[j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
+}
+
+// estimate_R_and_t's tail: R = U V^T of ABt (cvSVD, no transposes), det fix, t = pc0 - R pw0.
+MCV_HD void epnp_rt(const double (&abt)[3][3], const double (&pc0)[3], const double (&pw0)[3], double (&R)[3][3],
+                    double (&t)[3]) {
+    double A[3][3], w[3], Vt[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A[i][j] = abt[j][i];
+    jacobi_svd<3, 3>(A, w, Vt);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[i][j] = A[0][i] * Vt[0][j] + A[1][i] * Vt[1][j] + A[2][i] * Vt[2][j];
+    const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
+                       R[0][2] * R[1][1] * R[2][0] - R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
+    if (det < 0) {
+        R[2][0] = -R[2][0];
+        R[2][1] = -R[2][1];
+        R[2][2] = -R[2][2];
+    }
+    for (int i = 0; i < 3; ++i) t[i] = pc0[i] - dot3(R[i], pw0);
+}
+
+// One term of reprojection_error.
+MCV_HD double epnp_reproj_term(const double (&R)[3][3], const double (&t)[3], const EpnpCam& c, const double* pw,
+                               double u, double v) {
+    const double Xc = dot3(R[0], pw) + t[0];
+    const double Yc = dot3(R[1], pw) + t[1];
+    const double inv_Zc = 1.0 / (dot3(R[2], pw) + t[2]);
+    const double ue = c.uc + c.fu * Xc * inv_Zc;
+    const double ve = c.vc + c.fv * Yc * inv_Zc;
+    return __builtin_sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+}
+
+// compute_pose's final choice: N = 1, then 2 / 3 if strictly smaller.
+MCV_HD int epnp_pick(const double (&rep)[4]) {
+    int N = 1;
+    if (rep[2] < rep[1]) N = 2;
+    if (rep[3] < rep[N]) N = 3;
+    return N;
+}
+
+// Whole EPnP for a small point set held by the caller (RANSAC minimal sets, n = NP):
+// pw[i] world points, us[i] pixel coordinates (undistorted normalised * f + c).
+template <int NP>
+MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
+                             double (&Rout)[3][3], double (&tout)[3]) {
+    EpnpCtrl C;
+    {
+        double sum[3] = {0, 0, 0};
+        for (int i = 0; i < NP; ++i)
+            for (int j = 0; j < 3; ++j) sum[j] += pw[i][j];
+        double c0[3];
+        for (int j = 0; j < 3; ++j) c0[j] = sum[j] / NP;
+        double P[3][3];
+        for (int a = 0; a < 3; ++a)
+            for (int b = a; b < 3; ++b) {
+                double s = 0;
+                for (int i = 0; i < NP; ++i) s += (pw[i][a] - c0[a]) * (pw[i][b] - c0[b]);
+                P[a][b] = P[b][a] = s;
+            }
+        epnp_control(sum, P, NP, C);
+    }
+    double al[NP][4];
+    for (int i = 0; i < NP; ++i) epnp_alphas(C, pw[i], al[i]);
+    double mtm[kMtmSums];
+    for (int k = 0; k < kMtmSums; ++k) mtm[k] = 0;
+    for (int i = 0; i < NP; ++i) {
+        double r1[12], r2[12];
+        epnp_m_rows(al[i], us[i][0], us[i][1], cam, r1, r2);
+        int o = 0;
+        for (int a = 0; a < 12; ++a)
+            for (int b = a; b < 12; ++b, ++o) {
+                mtm[o] += r1[a] * r1[b];
+                mtm[o] += r2[a] * r2[b];
+            }
+    }
+    EpnpBetas B;
+    epnp_betas(mtm, C, B);
+    double pw0[3] = {0, 0, 0};
+    for (int i = 0; i < NP; ++i)
+        for (int j = 0; j < 3; ++j) pw0[j] += pw[i][j];
+    for (int j = 0; j < 3; ++j) pw0[j] /= NP;
+    double rep[4] = {0, 0, 0, 0}, Rs[4][3][3], ts[4][3];
+    for (int N = 1; N <= 3; ++N) {
+        double ccs[4][3], pc[NP][3];
+        epnp_ccs(B, B.betas[N], ccs);
+        for (int i = 0; i < NP; ++i) epnp_pc(al[i], ccs, pc[i]);
+        if (pc[0][2] < 0.0)   // solve_for_sign
+            for (int i = 0; i < NP; ++i)
+                for (int j = 0; j < 3; ++j) pc[i][j] = -pc[i][j];
+        double pc0[3] = {0, 0, 0};
+        for (int i = 0; i < NP; ++i)
+            for (int j = 0; j < 3; ++j) pc0[j] += pc[i][j];
+        for (int j = 0; j < 3; ++j) pc0[j] /= NP;
+        double abt[3][3];
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) abt[j][k] = 0;
+        for (int i = 0; i < NP; ++i)
+            for (int j = 0; j < 3; ++j)
+                for (int k = 0; k < 3; ++k) abt[j][k] += (pc[i][j] - pc0[j]) * (pw[i][k] - pw0[k]);
+        epnp_rt(abt, pc0, pw0, Rs[N], ts[N]);
+        double s = 0.0;
+        for (int i = 0; i < NP; ++i) s += epnp_reproj_term(Rs[N], ts[N], cam, pw[i], us[i][0], us[i][1]);
+        rep[N] = s / NP;
+    }
+    const int N = epnp_pick(rep);
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) Rout[i][j] = Rs[N][i][j];
+        tout[i] = ts[N][i];
+    }
+}
+
+}  // namespace mcv

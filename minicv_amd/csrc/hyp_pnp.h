@@ -23,6 +23,7 @@
 
 #include "mcv_common.h"
 #include "hyp_essential.h"   // e_poly_real_roots
+#include "epnp.h"
 
 namespace mcv {
 
@@ -35,9 +36,11 @@ struct PnpCamera { double fx, fy, cx, cy, k1, k2, p1, p2; };
 // Pose: X_cam = R X_world + t (row-major R).
 struct PnpPose { double R[9]; double t[3]; };
 
-// undistortPoints (OpenCV cvUndistortPointsInternal, fixed 5 iterations) -> normalised (x, y).
+// undistortPoints (OpenCV cvUndistortPointsInternal, fixed 5 iterations) -> normalised (x, y);
+// x0 = (u - cx) * (1 / fx) as that function scales by ifx = 1./fx.
 MCV_HD void pnp_undistort(const PnpCamera& c, double u, double v, double& x, double& y) {
-    const double x0 = (u - c.cx) / c.fx, y0 = (v - c.cy) / c.fy;
+    const double ifx = 1. / c.fx, ify = 1. / c.fy;
+    const double x0 = (u - c.cx) * ifx, y0 = (v - c.cy) * ify;
     x = x0;
     y = y0;
     for (int it = 0; it < kUndistortIters; ++it) {
@@ -278,6 +281,54 @@ MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, uint64
         }
         if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
         return pnp_ap3p4(c, x, y, W, pose) ? 1 : kStatusNoModel;
+    }
+    return kStatusNoSample;
+}
+
+// PnP solver kinds (the reference's solverKind, MiniCVNative.cpp:99-116): 0 ITERATIVE, 1 EPNP,
+// 2 P3P, 3 DLS, 4 UPNP, 5 AP3P; other values select ITERATIVE there (kind stays 0).
+MCV_HD int pnp_kind(int solverKind) { return solverKind >= 0 && solverKind <= 5 ? solverKind : 0; }
+// solvePnPRansac's minimal-set solver: P3P / AP3P keep their 4-point kernel (AP3P here for both),
+// every other kind samples 5 points for EPnP.
+MCV_HD bool pnp_kind_epnp(int kind) { return kind != 2 && kind != 5; }
+
+// EPnP on 5 float correspondences as PnPRansacCallback::runKernel feeds it: the float subset's
+// image points go through undistortPoints with a CV_32F result (the normalised coordinates are
+// rounded to float), epnp::init_points maps them back to pixels (x * fu + uc in double), world
+// points are the float coordinates.
+MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose) {
+    double pw[5][3], us[5][2];
+    for (int i = 0; i < 5; ++i) {
+        const PnpPoint p = p5[i];
+        double x, y;
+        pnp_undistort(c, (double)p.u, (double)p.v, x, y);
+        us[i][0] = (double)(float)x * c.fx + c.cx;
+        us[i][1] = (double)(float)y * c.fy + c.cy;
+        pw[i][0] = p.X; pw[i][1] = p.Y; pw[i][2] = p.Z;
+    }
+    const EpnpCam ec{c.fx, c.fy, c.cx, c.cy};
+    double R[3][3], t[3];
+    epnp_solve_small<5>(pw, us, ec, R, t);
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) pose.R[3 * i + j] = R[i][j];
+        pose.t[i] = t[i];
+    }
+}
+
+// One EPnP hypothesis: 5 distinct indices (Philox stream) -> pnp_epnp5. EPnP always yields a
+// model (possibly non-finite, which then counts no inliers), as solvePnP(EPNP) returns true.
+MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, uint64_t seed, uint64_t hyp,
+                               PnpPose& pose, int* idx_out) {
+    HypStream rs;
+    rs.init(seed, hyp);
+    int idx[5];
+    for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
+        if (!draw_distinct<5>(rs, N, idx)) continue;
+        PnpPoint p5[5];
+        for (int i = 0; i < 5; ++i) p5[i] = pts[idx[i]];
+        if (idx_out) for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
+        pnp_epnp5(c, p5, pose);
+        return 1;
     }
     return kStatusNoSample;
 }

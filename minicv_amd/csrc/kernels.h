@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "epnp.h"
 
 namespace mcv {
 
@@ -111,7 +112,7 @@ struct PnpOneOut {
     double R[9];
     double t[3];
     int status;
-    int idx[4];
+    int idx[5];
 };
 struct Ap3pIn { double mu[3], mv[3], W[3][3], inv_fx, inv_fy, cx_fx, cy_fy; };
 struct Ap3pOut {
@@ -121,11 +122,29 @@ struct Ap3pOut {
 };
 void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_pts, hipStream_t s);
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin, int hypCount,
-                         void* d_models, int* d_counts, hipStream_t s);
+                         bool epnp, void* d_models, int* d_counts, hipStream_t s);
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
                        float thr2, bool fused, hipStream_t s);
-void launch_pnp_one(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hyp, PnpOneOut* d_out,
-                    hipStream_t s);
+void launch_pnp_one(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hyp, bool epnp,
+                    PnpOneOut* d_out, hipStream_t s);
+void launch_pnp_solve5(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s);
+void launch_mask_compact(const uint8_t* d_mask, int N, int* d_idx, int* d_count, hipStream_t s);
+// EPnP over n points: d_pts (+ optional index list d_idx) fp32 PnpPoints, or d_img / d_world fp64.
+void launch_epnp_prep(const void* d_pts, const int* d_idx, const double* d_img, const double* d_world, int n,
+                      const double* cam8, double* d_pw, double* d_us, hipStream_t s);
+enum { kEpnpPassSumPw = 0, kEpnpPassPw0 = 1, kEpnpPassMtm = 2, kEpnpPassPc = 3, kEpnpPassAbt = 4, kEpnpPassReproj = 5 };
+struct EpnpPassArgs {
+    EpnpCtrl C;
+    EpnpCam cam;
+    double c0[3];            // Pw0: centroid
+    double ccs[3][4][3];     // Pc / Abt: sign-fixed control points of N = 1, 2, 3
+    double pc0[3][3];        // Abt
+    double pw0[3];           // Abt
+    double R[3][3][3];       // Reproj
+    double t[3][3];
+};
+void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, const EpnpPassArgs& a, int nacc,
+                      double* d_part, hipStream_t s);
 void launch_pnp_solve4(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s);
 void launch_pnp_mask(const void* d_pts, int N, const double* cam8, const double* R9, const double* t3, float thr2,
                      bool fused, uint8_t* d_mask, int* d_count, hipStream_t s);

@@ -13,6 +13,7 @@ static const int64_t kChunkMax = 1 << 20;
 
 size_t model_bytes(int model);   // device model bytes per hypothesis
 int model_points(int model);
+int model_points_cfg(int model, const RansacConfig& cfg);   // PnP: 5 with the EPnP kernel
 int model_slots(int model);      // model slots per hypothesis (essential: 10)
 
 struct Plan {
@@ -43,6 +44,10 @@ struct Plan {
     DevBuf<uint8_t> estage;   // essential: per-hypothesis EStage of the split five-point solve
     DevBuf<int> ndense;       // essential: dense model count, 4 cheirality counters, fetch flag
     double pnpCam[8] = {1, 1, 0, 0, 0, 0, 0, 0};   // PnP: fx, fy, cx, cy, k1, k2, p1, p2
+    DevBuf<double> epw;       // PnP: EPnP solve points (world, double)
+    DevBuf<double> eus;       // PnP: EPnP solve points (pixels of the undistorted observations)
+    DevBuf<int> eidx;         // PnP: inlier indices of the EPnP solve
+    int eLastKind = -1;       // PnP: minimal solver of the last evaluated chunk (1 EPnP, 0 AP3P)
     int64_t eLastBegin = -1;  // essential / PnP: hypothesis range of the last evaluated chunk
     int64_t eLastCount = 0;
     uint64_t eLastSeed = 0;
@@ -112,6 +117,7 @@ void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
                       int* d_counts, hipStream_t s);
 int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
                uint8_t* d_mask, hipStream_t s);
+bool pnp_cfg_epnp(const RansacConfig& cfg);   // minimal sets of 5 for EPnP (solverKind 0/1/3/4)
 
 // essential-matrix family (ransac_e.hip / ransac_e_host.cpp)
 void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,

@@ -114,15 +114,18 @@ static void pnp_pack(Plan& P, const mcvV2d* img, const mcvV3d* world, int N, voi
 }
 
 static bool fused_pnp(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_ERROR) != 0; }
+bool pnp_cfg_epnp(const RansacConfig& cfg) { return pnp_kind_epnp(pnp_kind(cfg.pnpKind)); }
 
 void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
                       int* d_counts, hipStream_t s) {
     const float thr2 = (float)(cfg.threshold * cfg.threshold);
-    launch_pnp_generate(d_pts, N, P.pnpCam, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+    const bool epnp = pnp_cfg_epnp(cfg);
+    launch_pnp_generate(d_pts, N, P.pnpCam, cfg.seed, hypBegin, hypCount, epnp, P.models.p, d_counts, s);
     P.eLastBegin = hypBegin;
     P.eLastCount = hypCount;
     P.eLastSeed = cfg.seed;
     P.eLastPts = d_pts;
+    P.eLastKind = epnp ? 1 : 0;
     ProfScope ps("pnp_verify", s);
     launch_pnp_verify(d_pts, N, P.pnpCam, P.models.p, d_counts, hypCount, thr2, fused_pnp(cfg), s);
 }
@@ -247,13 +250,99 @@ void pnp_vvs(Plan& P, const void* d_pts, int N, double* rvec, double* t, int max
     rodrigues_inv(R, rvec);
 }
 
-// Device API finalize: winner -> mask -> LM on the inliers; model9 = {rvec, tvec, 0, 0, 0}.
+// EPnP (epnp.h, OpenCV compute_pose) over n points already on the device as double world points
+// d_pw[3n] and pixel observations d_us[2n]: the O(n) loops run as blocked fixed-order passes
+// (mcv_epnp_pass), the 3x3 / 12x12 / 6xK algebra between them here on the host.
+static void epnp_device(Plan& P, const double* d_pw, const double* d_us, int n, double* R9, double* t3,
+                        hipStream_t s) {
+    if (n < 4) fail("EPnP needs at least 4 points (n=%d)", n);
+    EpnpPassArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.cam = EpnpCam{P.pnpCam[0], P.pnpCam[1], P.pnpCam[2], P.pnpCam[3]};
+    const int nblk = (n + kEpnpBlock - 1) / kEpnpBlock;
+    std::vector<double> part;
+    auto pass = [&](int mode, int nacc, double* out) {
+        P.part.ensure((size_t)nacc * nblk);
+        launch_epnp_pass(mode, d_pw, d_us, n, A, nacc, P.part.p, s);
+        MCV_HIP(hipGetLastError());
+        part.resize((size_t)nacc * nblk);
+        MCV_HIP(hipMemcpyAsync(part.data(), P.part.p, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        for (int a = 0; a < nacc; ++a) {
+            double t = 0;
+            for (int b = 0; b < nblk; ++b) t += part[(size_t)a * nblk + b];
+            out[a] = t;
+        }
+    };
+    double sum[3], p6[6], mtm[kMtmSums], pcs[9], abt[27], rep3[3];
+    pass(kEpnpPassSumPw, 3, sum);
+    for (int j = 0; j < 3; ++j) A.c0[j] = sum[j] / n;
+    pass(kEpnpPassPw0, 6, p6);
+    const double P3[3][3] = {{p6[0], p6[1], p6[2]}, {p6[1], p6[3], p6[4]}, {p6[2], p6[4], p6[5]}};
+    epnp_control(sum, P3, n, A.C);
+    pass(kEpnpPassMtm, kMtmSums, mtm);
+    EpnpBetas B;
+    epnp_betas(mtm, A.C, B);
+    double p0[3], al0[4];
+    MCV_HIP(hipMemcpyAsync(p0, d_pw, sizeof(p0), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    epnp_alphas(A.C, p0, al0);
+    for (int N = 0; N < 3; ++N) {
+        epnp_ccs(B, B.betas[N + 1], A.ccs[N]);
+        double pc[3];
+        epnp_pc(al0, A.ccs[N], pc);
+        if (pc[2] < 0.0)   // solve_for_sign on the first point; -ccs gives exactly the negated pcs
+            for (int j = 0; j < 4; ++j)
+                for (int k = 0; k < 3; ++k) A.ccs[N][j][k] = -A.ccs[N][j][k];
+    }
+    pass(kEpnpPassPc, 9, pcs);
+    for (int N = 0; N < 3; ++N)
+        for (int j = 0; j < 3; ++j) A.pc0[N][j] = pcs[3 * N + j] / n;
+    for (int j = 0; j < 3; ++j) A.pw0[j] = sum[j] / n;
+    pass(kEpnpPassAbt, 27, abt);
+    for (int N = 0; N < 3; ++N) {
+        double ab[3][3];
+        for (int j = 0; j < 3; ++j)
+            for (int k = 0; k < 3; ++k) ab[j][k] = abt[9 * N + 3 * j + k];
+        epnp_rt(ab, A.pc0[N], A.pw0, A.R[N], A.t[N]);
+    }
+    pass(kEpnpPassReproj, 3, rep3);
+    const double rep[4] = {0, rep3[0] / n, rep3[1] / n, rep3[2] / n};
+    const int N = epnp_pick(rep) - 1;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) R9[3 * i + j] = A.R[N][i][j];
+        t3[i] = A.t[N][i];
+    }
+}
+
+// solvePnPRansac's final EPnP: the inliers (compressElems order) of the float points as doubles,
+// image points through undistortPoints with a double result.
+static void epnp_inliers(Plan& P, const void* d_pts, int N, const uint8_t* d_mask, double* R9, double* t3,
+                         hipStream_t s) {
+    P.eidx.ensure((size_t)std::max(N, 1));
+    launch_mask_compact(d_mask, N, P.eidx.p, P.count.p, s);
+    MCV_HIP(hipGetLastError());
+    MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    const int n = P.h_i.p[0];
+    P.epw.ensure((size_t)3 * std::max(n, 1));
+    P.eus.ensure((size_t)2 * std::max(n, 1));
+    launch_epnp_prep(d_pts, P.eidx.p, nullptr, nullptr, n, P.pnpCam, P.epw.p, P.eus.p, s);
+    MCV_HIP(hipGetLastError());
+    epnp_device(P, P.epw.p, P.eus.p, n, R9, t3, s);
+}
+
+// Device API finalize: winner -> mask -> the inlier solve of the kind (solvePnPRansac's tail):
+// ITERATIVE refines the RANSAC pose with LM (useExtrinsicGuess = true), every other kind runs EPnP
+// on the inliers (P3P / AP3P switch to EPnP there). model9 = {rvec, tvec, 0, 0, 0}.
 int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
                uint8_t* d_mask, hipStream_t s) {
     PnpOneOut one;
-    if (hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount && P.eLastSeed == cfg.seed && P.eLastPts == d_pts) {
+    const bool epnp = pnp_cfg_epnp(cfg);
+    if (hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount && P.eLastSeed == cfg.seed && P.eLastPts == d_pts &&
+        P.eLastKind == (epnp ? 1 : 0)) {
         // the winner's pose straight from the last chunk's model buffer (the same code produced it)
-        // instead of a single-lane AP3P re-solve
+        // instead of a single-lane re-solve
         const PnpPose* d_m = (const PnpPose*)P.models.p + (hyp - P.eLastBegin);
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_m, sizeof(PnpPose), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
@@ -263,7 +352,7 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
         std::memcpy(one.t, pose.t, sizeof(one.t));
         one.status = 1;
     } else {
-        launch_pnp_one(d_pts, N, P.pnpCam, cfg.seed, hyp, (PnpOneOut*)P.one.p, s);
+        launch_pnp_one(d_pts, N, P.pnpCam, cfg.seed, hyp, epnp, (PnpOneOut*)P.one.p, s);
         MCV_HIP(hipGetLastError());
         one = pnp_fetch_one(P, s);
     }
@@ -271,7 +360,15 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
     const int count = pnp_mask_count(P, d_pts, N, cfg, one.R, one.t, d_mask, s);
     double r[3], t[3] = {one.t[0], one.t[1], one.t[2]};
     rodrigues_inv(one.R, r);
-    if (!(cfg.flags & MCV_FLAG_NO_REFINE) && count > 0) pnp_lm(P, d_pts, N, d_mask, r, t, 20, s);
+    if (!(cfg.flags & MCV_FLAG_NO_REFINE) && count > 0) {
+        if (pnp_kind(cfg.pnpKind) == 0) {
+            pnp_lm(P, d_pts, N, d_mask, r, t, 20, s);
+        } else {
+            double R2[9];
+            epnp_inliers(P, d_pts, N, d_mask, R2, t, s);
+            rodrigues_inv(R2, r);
+        }
+    }
     for (int k = 0; k < 3; ++k) { model9[k] = r[k]; model9[3 + k] = t[k]; model9[6 + k] = 0; }
     return count;
 }
@@ -289,15 +386,18 @@ static PnpResult pnp_ransac(Plan& P, const mcvV2d* img, const mcvV3d* world, int
     set_camera(P, K9, dist);
     P.reserve(N, 1);
     pnp_pack(P, img, world, N, P.ptsd.p, s);
-    if (N == 4) {
-        launch_pnp_solve4(P.ptsd.p, P.pnpCam, (PnpOneOut*)P.one.p, s);
+    const bool epnp = pnp_cfg_epnp(cfg);
+    if (N == 4 || (epnp && N == 5)) {
+        // npoints == model_points: one solvePnP on all points (P3P for 4, here AP3P; EPnP for 5)
+        if (N == 4) launch_pnp_solve4(P.ptsd.p, P.pnpCam, (PnpOneOut*)P.one.p, s);
+        else launch_pnp_solve5(P.ptsd.p, P.pnpCam, (PnpOneOut*)P.one.p, s);
         MCV_HIP(hipGetLastError());
         const PnpOneOut one = pnp_fetch_one(P, s);
         if (one.status != 1) return res;
         rodrigues_inv(one.R, res.r);
         for (int k = 0; k < 3; ++k) res.t[k] = one.t[k];
         launch_fill_u8(P.mask.p, N, 1, s);
-        res.count = 4;
+        res.count = N;
         res.ok = true;
         return res;
     }
@@ -310,13 +410,14 @@ static PnpResult pnp_ransac(Plan& P, const mcvV2d* img, const mcvV3d* world, int
     return res;
 }
 
-static RansacConfig pnp_config(int iters, float thr, double conf) {
+static RansacConfig pnp_config(int iters, float thr, double conf, int kind) {
     RansacConfig c;
     std::memset(&c, 0, sizeof(c));
     c.threshold = (double)thr;
     c.confidence = conf;
     c.maxIters = iters;
     c.method = MCV_METHOD_RANSAC;
+    c.pnpKind = kind;
     return c;
 }
 
@@ -359,9 +460,8 @@ extern "C" MCV_API mcvBool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3
                                          const int iterationsCount, const float reprojectionError,
                                          const double confidence, mcvV3d* tVec, mcvV3d* rVec, int* inlierCount,
                                          int* outInliers) {
-    (void)solverKind;   // every kind uses the AP3P 4-point kernel (header comment)
     MCV_GUARD(false, {
-        const RansacConfig cfg = pnp_config(iterationsCount, reprojectionError, confidence);
+        const RansacConfig cfg = pnp_config(iterationsCount, reprojectionError, confidence, pnp_kind(solverKind));
         return pnp_ransac_export(imgPoints, worldPoints, N, K, distortionCoeffs, cfg, tVec, rVec, inlierCount,
                                  outInliers);
     })
@@ -371,7 +471,7 @@ extern "C" MCV_API mcvBool cvSolvePnPRansacCfg(const mcvV2d* imgPoints, const mc
                                             const mcvM33d K, const double* distortionCoeffs, const RansacConfig* cfgp,
                                             mcvV3d* tVec, mcvV3d* rVec, int* inlierCount, int* outInliers) {
     MCV_GUARD(false, {
-        RansacConfig cfg = cfgp ? *cfgp : pnp_config(100, 8.0f, 0.99);
+        RansacConfig cfg = cfgp ? *cfgp : pnp_config(100, 8.0f, 0.99, 0);
         if (cfg.method != MCV_METHOD_RANSAC) fail("cvSolvePnPRansacCfg: only RANSAC (method 8)");
         return pnp_ransac_export(imgPoints, worldPoints, N, K, distortionCoeffs, cfg, tVec, rVec, inlierCount,
                                  outInliers);
@@ -383,20 +483,33 @@ extern "C" MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* wor
     MCV_GUARD(false, {
         if (!imgPoints || !worldPoints || !tVec || !rVec) fail("cvSolvePnP: null argument");
         if (N < 4) fail("cvSolvePnP: need at least 4 correspondences (N=%d)", N);
-        const bool p3p = solverKind == 2 || solverKind == 5;
+        // solverKind as MiniCVNative.cpp:54-75 maps it (6 = SQPNP, unknown = ITERATIVE)
+        const int kind = solverKind >= 0 && solverKind <= 6 ? solverKind : 0;
+        const bool p3p = kind == 2 || kind == 5;
         if (p3p && N != 4) fail("cvSolvePnP: P3P / AP3P need exactly 4 points (N=%d)", N);
         require_device();
         Plan& P = thread_plan(MCV_MODEL_PNP);
         hipStream_t s = P.own_stream();
         PnpResult r;
         if (p3p) {
-            r = pnp_ransac(P, imgPoints, worldPoints, N, K.M, distortionCoeffs, pnp_config(1, 1.f, 0.99), s);
+            r = pnp_ransac(P, imgPoints, worldPoints, N, K.M, distortionCoeffs, pnp_config(1, 1.f, 0.99, kind), s);
         } else {
-            // AP3P-RANSAC initialisation (fixed 256 hypotheses, 4 px), then LM over all points
-            RansacConfig cfg = pnp_config(256, 4.0f, 0.99);
-            cfg.flags = MCV_FLAG_FIXED_ITERS | MCV_FLAG_NO_REFINE;
-            r = pnp_ransac(P, imgPoints, worldPoints, N, K.M, distortionCoeffs, cfg, s);
-            if (r.ok && N > 4) pnp_lm(P, P.ptsd.p, N, nullptr, r.r, r.t, 20, s);
+            // EPnP on all points in double (solvePnPGeneric keeps the caller's CV_64F points);
+            // ITERATIVE / SQPNP: then LM over all points from that pose (the reference's DLT or
+            // homography initialisation and SQPnP's global search are not restated)
+            set_camera(P, K.M, distortionCoeffs);
+            P.reserve(N, 1);
+            pnp_pack(P, imgPoints, worldPoints, N, P.ptsd.p, s);
+            P.epw.ensure((size_t)3 * N);
+            P.eus.ensure((size_t)2 * N);
+            launch_epnp_prep(nullptr, nullptr, P.raw.p, P.raw.p + 2 * (size_t)N, N, P.pnpCam, P.epw.p, P.eus.p, s);
+            MCV_HIP(hipGetLastError());
+            double R9[9];
+            epnp_device(P, P.epw.p, P.eus.p, N, R9, r.t, s);
+            rodrigues_inv(R9, r.r);
+            r.ok = std::isfinite(r.r[0]) && std::isfinite(r.r[1]) && std::isfinite(r.r[2]) && std::isfinite(r.t[0]) &&
+                   std::isfinite(r.t[1]) && std::isfinite(r.t[2]);
+            if (r.ok && (kind == 0 || kind == 6)) pnp_lm(P, P.ptsd.p, N, nullptr, r.r, r.t, 20, s);
         }
         if (!r.ok) {
             set_last_error("cvSolvePnP: no pose");
@@ -515,5 +628,66 @@ extern "C" MCV_API int mcvHostPnP(const void* pts, int N, const double* cam8, ui
         for (int k = 0; k < 9; ++k) R9[k] = p.R[k];
         for (int k = 0; k < 3; ++k) t3[k] = p.t[k];
         return st;
+    })
+}
+
+extern "C" MCV_API int mcvHostPnPEpnp(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp,
+                                      double* R9, double* t3, int* idx5) {
+    MCV_GUARD(kStatusNoSample - 1, {
+        if (!pts || !cam8 || !R9 || !t3 || N < 5) fail("mcvHostPnPEpnp: bad argument");
+        PnpCamera c{cam8[0], cam8[1], cam8[2], cam8[3], cam8[4], cam8[5], cam8[6], cam8[7]};
+        PnpPose p;
+        for (int k = 0; k < 9; ++k) p.R[k] = 0;
+        for (int k = 0; k < 3; ++k) p.t[k] = 0;
+        const int st = pnp_hypothesis_epnp((const PnpPoint*)pts, N, c, seed, (uint64_t)hyp, p, idx5);
+        for (int k = 0; k < 9; ++k) R9[k] = p.R[k];
+        for (int k = 0; k < 3; ++k) t3[k] = p.t[k];
+        return st;
+    })
+}
+
+// Host build of epnp_solve_small<5> (pw: 5 x 3 world points, us: 5 x 2 pixels, cam4 = fu, fv, uc, vc).
+extern "C" MCV_API void mcvHostEpnp5(const double* pw15, const double* us10, const double* cam4, double* R9,
+                                     double* t3) {
+    double pw[5][3], us[5][2], R[3][3], t[3];
+    for (int i = 0; i < 5; ++i) {
+        for (int k = 0; k < 3; ++k) pw[i][k] = pw15[3 * i + k];
+        for (int k = 0; k < 2; ++k) us[i][k] = us10[2 * i + k];
+    }
+    epnp_solve_small<5>(pw, us, EpnpCam{cam4[0], cam4[1], cam4[2], cam4[3]}, R, t);
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) R9[3 * i + j] = R[i][j];
+        t3[i] = t[i];
+    }
+}
+
+// Test hook: the device's per-hypothesis poses. pts: host PnpPoint[N] (8 floats each); kind: the
+// solverKind (EPnP kernel unless 2 / 5). Writes poses12[h] = {R (9), t (3)} and status[h] (1 or a
+// kStatus* code). Returns hypCount, -1 on failure.
+extern "C" MCV_API int mcvTestPnpHypotheses(const float* pts, int N, const double* cam8, uint64_t seed,
+                                            int64_t hypBegin, int hypCount, int kind, double* poses12,
+                                            int* status) {
+    MCV_GUARD(-1, {
+        if (!pts || !cam8 || !poses12 || !status || N < 5 || hypCount <= 0) fail("mcvTestPnpHypotheses: bad argument");
+        require_device();
+        Plan& P = thread_plan(MCV_MODEL_PNP);
+        hipStream_t s = P.own_stream();
+        P.reserve(N, hypCount);
+        for (int k = 0; k < 8; ++k) P.pnpCam[k] = cam8[k];
+        MCV_HIP(hipMemcpyAsync(P.ptsd.p, pts, (size_t)N * sizeof(PnpPoint), hipMemcpyHostToDevice, s));
+        launch_pnp_generate(P.ptsd.p, N, P.pnpCam, seed, hypBegin, hypCount, pnp_kind_epnp(pnp_kind(kind)), P.models.p,
+                            P.counts.p, s);
+        MCV_HIP(hipGetLastError());
+        std::vector<PnpPose> m((size_t)hypCount);
+        MCV_HIP(hipMemcpyAsync(m.data(), P.models.p, m.size() * sizeof(PnpPose), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipMemcpyAsync(status, P.counts.p, (size_t)hypCount * sizeof(int), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        P.eLastBegin = -1;
+        for (int h = 0; h < hypCount; ++h) {
+            if (status[h] == 0) status[h] = 1;
+            for (int k = 0; k < 9; ++k) poses12[12 * (size_t)h + k] = status[h] == 1 ? m[h].R[k] : 0.0;
+            for (int k = 0; k < 3; ++k) poses12[12 * (size_t)h + 9 + k] = status[h] == 1 ? m[h].t[k] : 0.0;
+        }
+        return hypCount;
     })
 }

@@ -314,7 +314,8 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
     }
     if (P.model == MCV_MODEL_PNP) {
         p_evaluate_chunk(P, d_ptsv, N, cfg, hypBegin, hypCount, d_counts, s);
-        if (d_key) launch_best(d_counts, hypCount, hypBegin, model_points(P.model), P.pkey.p, P.pfail.p, d_key, s);
+        if (d_key)
+            launch_best(d_counts, hypCount, hypBegin, model_points_cfg(P.model, cfg), P.pkey.p, P.pfail.p, d_key, s);
         MCV_HIP(hipGetLastError());
         return;
     }
@@ -354,7 +355,10 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
 }
 
 int model_points(int model) { return model == MCV_MODEL_FUNDAMENTAL ? 8 : (model == MCV_MODEL_ESSENTIAL ? 5 : 4); }
-// (homography and PnP: 4)
+// (homography and PnP with the AP3P kernel: 4)
+int model_points_cfg(int model, const RansacConfig& cfg) {
+    return model == MCV_MODEL_PNP && pnp_cfg_epnp(cfg) ? 5 : model_points(model);
+}
 
 // Winner -> mask (+ refit + LM). Returns inlier count, 0 on failure. Synchronises s.
 int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* H, uint8_t* d_mask,
@@ -400,7 +404,7 @@ int finalize(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg, int64_
 // points replicated once by peer copy), counts concatenated in order, then the same replay — the
 // answer is identical to one device. Returns the best hypothesis (slot) index or -1.
 int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s) {
-    const int m = model_points(P.model);
+    const int m = model_points_cfg(P.model, cfg);
     const int slots = model_slots(P.model);
     mcvReplayState st;
     mcvReplayInit(&st, cfg.maxIters);
@@ -565,7 +569,7 @@ extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const void* d_pts4
     MCV_GUARD(0, {
         Plan* P = reinterpret_cast<Plan*>(plan);
         if (!P || !d_pts4 || !cfg || !d_key) fail("mcvRansacEvaluate: null argument");
-        if (N < model_points(P->model)) fail("mcvRansacEvaluate: N=%d below the minimal sample", N);
+        if (N < model_points_cfg(P->model, *cfg)) fail("mcvRansacEvaluate: N=%d below the minimal sample", N);
         if (hypCount <= 0 || hypCount > P->maxHyps) fail("mcvRansacEvaluate: hypCount %lld outside plan capacity %lld",
                                                          (long long)hypCount, (long long)P->maxHyps);
         if (hypBegin < 0 || (hypBegin + hypCount) * model_slots(P->model) > 0xFFFFFFFFll)

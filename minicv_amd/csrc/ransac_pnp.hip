@@ -9,7 +9,10 @@
 //                        squared pixel error, ballot + popcount; chunk partial counts are added
 //                        with integer atomics (order-free, exact). The 2-D split keeps the chip
 //                        busy at the reference's default 100 iterations.
+//   mcv_pnp_generate<1>  EPnP kernels (solverKind 0/1/3/4): 5-point samples, epnp.h per lane.
 //   mcv_pnp_one / _mask  winner recompute, inlier mask.
+//   mcv_epnp_pass<MODE>  EPnP over the inliers / all points: blocked fixed-order fp64 sums of the
+//                        O(n) loops; the O(1) algebra between the passes runs on the host (epnp.h).
 //   OpPnpLM / OpPnpVVS   fixed-order fp64 reductions for the LM refit / VVS refinement.
 //   mcv_pnp_ap3p         solveAp3p export: one AP3P solve (3 points).
 #include "mcv_common.h"
@@ -34,13 +37,15 @@ __global__ __launch_bounds__(256) void mcv_pnp_pack(const double* __restrict__ i
     out[i] = p;
 }
 
+template <bool EPNP>
 __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
                                                        uint64_t seed, int64_t hypBegin, int hypCount,
                                                        PnpPose* __restrict__ models, int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     PnpPose p;
-    const int st = pnp_hypothesis(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr);
+    const int st = EPNP ? pnp_hypothesis_epnp(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr)
+                        : pnp_hypothesis(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr);
     if (st == 1) {
         models[i] = p;
         counts[i] = 0;
@@ -100,16 +105,30 @@ __global__ __launch_bounds__(256) void mcv_pnp_verify(const PnpPoint* __restrict
 }
 
 __global__ void mcv_pnp_one(const PnpPoint* __restrict__ pts, int N, PnpCamera cam, uint64_t seed, int64_t hyp,
-                            PnpOneOut* __restrict__ out) {
+                            bool epnp, PnpOneOut* __restrict__ out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     PnpPose p;
     for (int k = 0; k < 9; ++k) p.R[k] = 0;
     for (int k = 0; k < 3; ++k) p.t[k] = 0;
-    int idx[4] = {-1, -1, -1, -1};
-    out->status = pnp_hypothesis(pts, N, cam, seed, (uint64_t)hyp, p, idx);
+    int idx[5] = {-1, -1, -1, -1, -1};
+    out->status = epnp ? pnp_hypothesis_epnp(pts, N, cam, seed, (uint64_t)hyp, p, idx)
+                       : pnp_hypothesis(pts, N, cam, seed, (uint64_t)hyp, p, idx);
     for (int k = 0; k < 9; ++k) out->R[k] = p.R[k];
     for (int k = 0; k < 3; ++k) out->t[k] = p.t[k];
-    for (int k = 0; k < 4; ++k) out->idx[k] = idx[k];
+    for (int k = 0; k < 5; ++k) out->idx[k] = idx[k];
+}
+
+// solvePnP(EPNP) on exactly 5 float correspondences (solvePnPRansac's npoints == model_points case).
+__global__ void mcv_pnp_solve5(const PnpPoint* __restrict__ pts, PnpCamera cam, PnpOneOut* __restrict__ out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    PnpPoint p5[5];
+    for (int i = 0; i < 5; ++i) p5[i] = pts[i];
+    PnpPose p;
+    pnp_epnp5(cam, p5, p);
+    out->status = 1;
+    for (int k = 0; k < 9; ++k) out->R[k] = p.R[k];
+    for (int k = 0; k < 3; ++k) out->t[k] = p.t[k];
+    for (int k = 0; k < 5; ++k) out->idx[k] = k;
 }
 
 // Direct four-point solve on given normalised points (N == 4 path of solvePnPRansac / solvePnP).
@@ -128,6 +147,7 @@ __global__ void mcv_pnp_solve4(const PnpPoint* __restrict__ pts, PnpCamera cam, 
     for (int k = 0; k < 9; ++k) out->R[k] = p.R[k];
     for (int k = 0; k < 3; ++k) out->t[k] = p.t[k];
     for (int k = 0; k < 4; ++k) out->idx[k] = k;
+    out->idx[4] = -1;
 }
 
 __global__ __launch_bounds__(256) void mcv_pnp_mask(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
@@ -249,6 +269,116 @@ struct OpPnpVVS {
     }
 };
 
+// ---- EPnP on a large point set (the inlier solve of solvePnPRansac, solvePnP(EPNP)) ----------
+// Mask -> ascending index list (one block, 1024 threads, chunked ballot scan): the inliers in the
+// order compressElems keeps them.
+__global__ __launch_bounds__(1024) void mcv_mask_compact(const uint8_t* __restrict__ mask, int N,
+                                                         int* __restrict__ idx, int* __restrict__ count) {
+    __shared__ int wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int base = 0;
+    for (int c0 = 0; c0 < N; c0 += 1024) {
+        const int i = c0 + tid;
+        const bool f = i < N && mask[i] != 0;
+        const uint64_t b = __ballot(f);
+        const int below = (int)__popcll(b & ((1ull << lane) - 1));
+        if (lane == 0) wsum[wv] = (int)__popcll(b);
+        __syncthreads();
+        int off = 0, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            off += w < wv ? wsum[w] : 0;
+            tot += wsum[w];
+        }
+        if (f) idx[base + off + below] = i;
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) *count = base;
+}
+
+// Points of the solve in double: pw = world, us = undistortPoints (double result) * f + c.
+__global__ __launch_bounds__(256) void mcv_epnp_prep_f32(const PnpPoint* __restrict__ pts, const int* __restrict__ idx,
+                                                         int n, PnpCamera c, double* __restrict__ pw,
+                                                         double* __restrict__ us) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const PnpPoint p = pts[idx ? idx[i] : i];
+    double x, y;
+    pnp_undistort(c, (double)p.u, (double)p.v, x, y);
+    us[2 * (size_t)i] = x * c.fx + c.cx;
+    us[2 * (size_t)i + 1] = y * c.fy + c.cy;
+    pw[3 * (size_t)i] = p.X;
+    pw[3 * (size_t)i + 1] = p.Y;
+    pw[3 * (size_t)i + 2] = p.Z;
+}
+
+__global__ __launch_bounds__(256) void mcv_epnp_prep_f64(const double* __restrict__ img, const double* __restrict__ world,
+                                                         int n, PnpCamera c, double* __restrict__ pw,
+                                                         double* __restrict__ us) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double x, y;
+    pnp_undistort(c, img[2 * (size_t)i], img[2 * (size_t)i + 1], x, y);
+    us[2 * (size_t)i] = x * c.fx + c.cx;
+    us[2 * (size_t)i + 1] = y * c.fy + c.cy;
+    for (int k = 0; k < 3; ++k) pw[3 * (size_t)i + k] = world[3 * (size_t)i + k];
+}
+
+// One thread per (accumulator, block of kEpnpBlock points): the block's terms summed in point
+// order from 0 (the O(n) loops of epnp.cpp); partials part[acc * nblk + blk], summed over blocks
+// in order on the host. Threads of one block index are adjacent, so a wave reads each point once.
+template <int MODE>
+__global__ __launch_bounds__(256) void mcv_epnp_pass(const double* __restrict__ pw, const double* __restrict__ us,
+                                                     int n, EpnpPassArgs A, int nacc, int nblk,
+                                                     double* __restrict__ part) {
+    const int tid = blockIdx.x * 256 + threadIdx.x;
+    if (tid >= nacc * nblk) return;
+    const int acc = tid % nacc, blk = tid / nacc;
+    const int i0 = blk * kEpnpBlock;
+    const int i1 = min(n, i0 + kEpnpBlock);
+    double s = 0;
+    if (MODE == kEpnpPassSumPw) {
+        for (int i = i0; i < i1; ++i) s += pw[3 * (size_t)i + acc];
+    } else if (MODE == kEpnpPassPw0) {
+        const int a = acc < 3 ? 0 : (acc < 5 ? 1 : 2);
+        const int b = acc < 3 ? acc : (acc < 5 ? acc - 2 : 2);
+        for (int i = i0; i < i1; ++i)
+            s += (pw[3 * (size_t)i + a] - A.c0[a]) * (pw[3 * (size_t)i + b] - A.c0[b]);
+    } else if (MODE == kEpnpPassMtm) {
+        int a = 0, r = acc;
+        while (r >= 12 - a) { r -= 12 - a; ++a; }
+        const int b = a + r;
+        for (int i = i0; i < i1; ++i) {
+            double al[4], r1[12], r2[12];
+            epnp_alphas(A.C, pw + 3 * (size_t)i, al);
+            epnp_m_rows(al, us[2 * (size_t)i], us[2 * (size_t)i + 1], A.cam, r1, r2);
+            s += r1[a] * r1[b];
+            s += r2[a] * r2[b];
+        }
+    } else if (MODE == kEpnpPassPc) {
+        const int N = acc / 3, j = acc % 3;
+        for (int i = i0; i < i1; ++i) {
+            double al[4], pc[3];
+            epnp_alphas(A.C, pw + 3 * (size_t)i, al);
+            epnp_pc(al, A.ccs[N], pc);
+            s += pc[j];
+        }
+    } else if (MODE == kEpnpPassAbt) {
+        const int N = acc / 9, j = (acc % 9) / 3, k = acc % 3;
+        for (int i = i0; i < i1; ++i) {
+            double al[4], pc[3];
+            epnp_alphas(A.C, pw + 3 * (size_t)i, al);
+            epnp_pc(al, A.ccs[N], pc);
+            s += (pc[j] - A.pc0[N][j]) * (pw[3 * (size_t)i + k] - A.pw0[k]);
+        }
+    } else {
+        for (int i = i0; i < i1; ++i)
+            s += epnp_reproj_term(A.R[acc], A.t[acc], A.cam, pw + 3 * (size_t)i, us[2 * (size_t)i],
+                                  us[2 * (size_t)i + 1]);
+    }
+    part[(size_t)acc * nblk + blk] = s;
+}
+
 // ---- launchers --------------------------------------------------------------------------------
 static PnpCamera to_cam(const double* cam8) {
     PnpCamera c;
@@ -263,9 +393,13 @@ void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_
 }
 
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin, int hypCount,
-                         void* d_models, int* d_counts, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_pnp_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts, N,
-                       to_cam(cam8), seed, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
+                         bool epnp, void* d_models, int* d_counts, hipStream_t s) {
+    if (epnp)
+        hipLaunchKernelGGL(mcv_pnp_generate<true>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
+                           N, to_cam(cam8), seed, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
+    else
+        hipLaunchKernelGGL(mcv_pnp_generate<false>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
+                           N, to_cam(cam8), seed, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
 }
 
 template <int K>
@@ -307,9 +441,43 @@ void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void*
     }
 }
 
-void launch_pnp_one(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hyp, PnpOneOut* d_out,
-                    hipStream_t s) {
-    hipLaunchKernelGGL(mcv_pnp_one, dim3(1), dim3(64), 0, s, (const PnpPoint*)d_pts, N, to_cam(cam8), seed, hyp, d_out);
+void launch_pnp_one(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hyp, bool epnp,
+                    PnpOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_pnp_one, dim3(1), dim3(64), 0, s, (const PnpPoint*)d_pts, N, to_cam(cam8), seed, hyp, epnp,
+                       d_out);
+}
+
+void launch_pnp_solve5(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_pnp_solve5, dim3(1), dim3(64), 0, s, (const PnpPoint*)d_pts, to_cam(cam8), d_out);
+}
+
+void launch_mask_compact(const uint8_t* d_mask, int N, int* d_idx, int* d_count, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_mask_compact, dim3(1), dim3(1024), 0, s, d_mask, N, d_idx, d_count);
+}
+
+void launch_epnp_prep(const void* d_pts, const int* d_idx, const double* d_img, const double* d_world, int n,
+                      const double* cam8, double* d_pw, double* d_us, hipStream_t s) {
+    if (n <= 0) return;
+    if (d_pts)
+        hipLaunchKernelGGL(mcv_epnp_prep_f32, dim3((n + 255) / 256), dim3(256), 0, s, (const PnpPoint*)d_pts, d_idx, n,
+                           to_cam(cam8), d_pw, d_us);
+    else
+        hipLaunchKernelGGL(mcv_epnp_prep_f64, dim3((n + 255) / 256), dim3(256), 0, s, d_img, d_world, n, to_cam(cam8),
+                           d_pw, d_us);
+}
+
+void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, const EpnpPassArgs& a, int nacc,
+                      double* d_part, hipStream_t s) {
+    const int nblk = (n + kEpnpBlock - 1) / kEpnpBlock;
+    const dim3 grid((nacc * nblk + 255) / 256), block(256);
+    switch (mode) {
+        case kEpnpPassSumPw: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSumPw>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
+        case kEpnpPassPw0: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassPw0>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
+        case kEpnpPassMtm: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassMtm>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
+        case kEpnpPassPc: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassPc>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
+        case kEpnpPassAbt: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassAbt>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
+        default: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassReproj>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part);
+    }
 }
 
 void launch_pnp_solve4(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s) {

@@ -42,7 +42,7 @@ class RecoverPoseConfig(C.Structure):
 class RansacConfig(C.Structure):
     _fields_ = [("threshold", C.c_double), ("confidence", C.c_double), ("maxIters", C.c_int),
                 ("method", C.c_int), ("seed", C.c_uint64), ("deviceCount", C.c_int), ("flags", C.c_int),
-                ("errorKind", C.c_int), ("reserved", C.c_int)]
+                ("errorKind", C.c_int), ("pnpKind", C.c_int)]
 
 
 class KeyPoint2d(C.Structure):
@@ -143,6 +143,9 @@ SIGNATURES = {
     "mcvHostDecomposeEssential": (None, [_P, _P, _P, _P]),
     "mcvHostRealRoots": (_I, [_P, _I, _I, _P]),
     "mcvHostPnP": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
+    "mcvHostPnPEpnp": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
+    "mcvHostEpnp5": (None, [_P, _P, _P, _P, _P]),
+    "mcvTestPnpHypotheses": (_I, [_P, _I, _P, _U64, _I64, _I, _I, _P, _P]),
     "mcvHostRodrigues": (None, [_P, _P, _P]),
     "mcvHostRodriguesInv": (None, [_P, _P]),
     "mcvTestRcpExhaustive": (C.c_longlong, [_I, _P]),

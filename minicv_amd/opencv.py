@@ -185,7 +185,7 @@ def fivepoint(a, b):
 
 
 # ---- PnP (OpenCV.fs:922-1052; exports MiniCVNative.cpp:48-163, ap3p.cpp:282) -----------------
-SOLVER_KIND = {"Iterative": 0, "EPNP": 1, "P3P": 2, "AP3P": 5, "SQPNP": 6}
+SOLVER_KIND = {"Iterative": 0, "EPNP": 1, "P3P": 2, "DLS": 3, "UPNP": 4, "AP3P": 5, "SQPNP": 6}
 
 
 def _m33(K) -> N.M33d:
@@ -226,6 +226,7 @@ def solvePnPRansac(img, world, K, dist=None, kind: str = "AP3P", iterations: int
                                       N.C.addressof(r), N.C.addressof(cnt), inl.ctypes.data)
     else:
         cfg = params.to_c()
+        cfg.pnpKind = SOLVER_KIND[kind]
         ok = N.lib().cvSolvePnPRansacCfg(pi.ctypes.data, pw.ctypes.data, n, _m33(K), d.ctypes.data,
                                          N.C.addressof(cfg), N.C.addressof(t), N.C.addressof(r), N.C.addressof(cnt),
                                          inl.ctypes.data)

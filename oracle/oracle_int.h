@@ -25,5 +25,19 @@ int64_t orc_ransac_replay(const int* counts, int64_t ncounts, int N, int m, doub
                           int* bestCount);
 void eig_pinv_apply(const double* A, int n, const double* b, double* x, double* Ainv);
 int orc_poly_real_roots(const double* cin, int deg, double* roots);
+/* PnP (oracle_pnp.c / oracle_epnp.c) */
+void orc_undistort(const double* cam8, double u, double v, double* x, double* y);
+int orc_pnp_hypothesis(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R, double* t,
+                       int* idx_out);
+int orc_pnp_count(const float* pts, int N, const double* cam8, const double* R, const double* t, float thr2, int fused,
+                  uint8_t* mask);
+void orc_pnp_lm(const float* pts, int N, const uint8_t* mask, const double* cam8, double* rvec, double* t,
+                int maxIters);
+void orc_rodrigues_inv(const double* R, double* r);
+void orc_epnp(const double* pw, const double* us, int n, const double* cam4, double* R, double* t);
+void orc_epnp5_f32(const float* p5, const double* cam8, double* R, double* t);
+int orc_pnp_hypothesis_epnp(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R,
+                            double* t, int* idx_out);
+void orc_epnp_points(const double* img, const double* world, int n, const double* cam8, double* R, double* t);
 
 #endif

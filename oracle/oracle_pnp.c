@@ -33,8 +33,10 @@ static Cam cam_of(const double* c8) {
     return c;
 }
 
+/* cvUndistortPointsInternal: x0 = (u - cx) * ifx with ifx = 1./fx, 5 fixed iterations */
 static void undistort(const Cam* c, double u, double v, double* xo, double* yo) {
-    double x0 = (u - c->cx) / c->fx, y0 = (v - c->cy) / c->fy, x = x0, y = y0;
+    double ifx = 1. / c->fx, ify = 1. / c->fy;
+    double x0 = (u - c->cx) * ifx, y0 = (v - c->cy) * ify, x = x0, y = y0;
     for (int it = 0; it < 5; ++it) {
         double r2 = x * x + y * y;
         double ic = 1.0 / (1.0 + (c->k2 * r2 + c->k1) * r2);
@@ -46,6 +48,11 @@ static void undistort(const Cam* c, double u, double v, double* xo, double* yo) 
     }
     *xo = x;
     *yo = y;
+}
+
+void orc_undistort(const double* cam8, double u, double v, double* x, double* y) {
+    Cam c = cam_of(cam8);
+    undistort(&c, u, v, x, y);
 }
 
 static void project(const Cam* c, const double* R, const double* t, double X, double Y, double Z, double* u, double* v) {
@@ -242,6 +249,27 @@ void orc_pnp_counts(const float* pts, int N, const double* cam8, uint64_t seed, 
     }
 }
 
+/* counts with the minimal solver of solverKind `kind` (EPnP on 5 points unless 2 / 5) */
+static int kind_epnp(int kind) {
+    if (kind < 0 || kind > 5) kind = 0;
+    return kind != 2 && kind != 5;
+}
+
+void orc_pnp_counts_k(const float* pts, int N, const double* cam8, uint64_t seed, int64_t begin, int64_t count,
+                      float thr2, int fused, int kind, int* out, int nthreads) {
+    const int ep = kind_epnp(kind);
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+    for (int64_t h = 0; h < count; ++h) {
+        double R[9], t[3];
+        int st = ep ? orc_pnp_hypothesis_epnp(pts, N, cam8, seed, begin + h, R, t, NULL)
+                    : orc_pnp_hypothesis(pts, N, cam8, seed, begin + h, R, t, NULL);
+        out[h] = st == 1 ? orc_pnp_count(pts, N, cam8, R, t, thr2, fused, NULL) : st;
+    }
+}
+
 /* ---- rotation algebra + LM (independent restatement of pnp_host.cpp's definition) -------- */
 static void skew3(const double* v, double* S) {
     S[0] = 0; S[1] = -v[2]; S[2] = v[1]; S[3] = v[2]; S[4] = 0; S[5] = -v[0]; S[6] = -v[1]; S[7] = v[0]; S[8] = 0;
@@ -384,12 +412,69 @@ void orc_pnp_lm(const float* pts, int N, const uint8_t* mask, const double* cam8
     for (int k = 0; k < 3; ++k) { rvec[k] = p[k]; t[k] = p[3 + k]; }
 }
 
-/* cvSolvePnPRansac semantics (seeded): returns the inlier count (0 on failure); mask, rvec, tvec out. */
-int orc_solve_pnp_ransac(const double* img, const double* world, int N, const double* K9, const double* dist4,
-                         double thr, double conf, int maxIters, uint64_t seed, int flags, double* rvec, double* tvec,
-                         uint8_t* mask, int64_t* bestOut, int nthreads) {
+/* Virtual visual servoing refinement, restating pnp_host.cpp's pnp_vvs definition
+ * (solvePnPRefineVVS [ext]): normalised-plane error e = projection - undistorted observation,
+ * interaction matrix L (camera twist (v, w)), v = -lambda pinv(L^T L) L^T e, cMo <- exp(v)^-1 cMo,
+ * at most maxIters steps or |v| < FLT_EPSILON; sums in point order. */
+void orc_pnp_vvs(const float* pts, int N, const double* cam8, double* rvec, double* t, int maxIters, double lambda) {
+    Cam c = cam_of(cam8);
+    double R[9];
+    orc_rodrigues(rvec, R, NULL);
+    for (int it = 0; it < maxIters; ++it) {
+        double A[36], g[6], v[6];
+        memset(A, 0, sizeof(A));
+        memset(g, 0, sizeof(g));
+        for (int i = 0; i < N; ++i) {
+            const float* p = pts + 8 * (size_t)i;
+            double X = p[0], Y = p[1], Z = p[2];
+            double Xc = R[0] * X + R[1] * Y + R[2] * Z + t[0], Yc = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+            double Zc = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+            double iz = Zc != 0 ? 1.0 / Zc : 1.0, x = Xc * iz, y = Yc * iz, xo, yo;
+            undistort(&c, (double)p[3], (double)p[4], &xo, &yo);
+            double ex = x - xo, ey = y - yo;
+            double Lx[6] = {-iz, 0.0, x * iz, x * y, -(1.0 + x * x), y};
+            double Ly[6] = {0.0, -iz, y * iz, 1.0 + y * y, -x * y, -x};
+            for (int j = 0; j < 6; ++j) {
+                for (int k = 0; k < 6; ++k) A[6 * j + k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+                g[j] += Lx[j] * ex + Ly[j] * ey;
+            }
+        }
+        eig_pinv_apply(A, 6, g, v, NULL);
+        double vn = 0;
+        for (int k = 0; k < 6; ++k) { v[k] = -lambda * v[k]; vn += v[k] * v[k]; }
+        const double *u = v, *w = v + 3;
+        double Rw[9], S[9], S2[9], V[9], tt[3], Rn[9], tn[3];
+        orc_rodrigues(w, Rw, NULL);
+        skew3(w, S);
+        mm3(S, S, S2);
+        double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2], th = sqrt(th2);
+        double a = th < 1e-8 ? 0.5 : (1 - cos(th)) / th2;
+        double b = th < 1e-8 ? 1.0 / 6.0 : (th - sin(th)) / (th2 * th);
+        for (int k = 0; k < 9; ++k) V[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * S[k] + b * S2[k];
+        for (int i = 0; i < 3; ++i) tt[i] = V[3 * i] * u[0] + V[3 * i + 1] * u[1] + V[3 * i + 2] * u[2];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Rn[3 * i + j] = Rw[i] * R[j] + Rw[3 + i] * R[3 + j] + Rw[6 + i] * R[6 + j];
+        for (int i = 0; i < 3; ++i)
+            tn[i] = Rw[i] * (t[0] - tt[0]) + Rw[3 + i] * (t[1] - tt[1]) + Rw[6 + i] * (t[2] - tt[2]);
+        memcpy(R, Rn, sizeof(R));
+        memcpy(t, tn, sizeof(tn));
+        if (sqrt(vn) < FLT_EPSILON) break;
+    }
+    orc_rodrigues_inv(R, rvec);
+}
+
+/* cvSolvePnPRansac semantics (seeded), solverKind `kind` (OpenCV solvePnPRansac):
+ * P3P / AP3P (2, 5): AP3P on 4-point sets; every other kind EPnP on 5-point sets; npoints ==
+ * model_points: one solve on all points; final pose: LM from the RANSAC pose for ITERATIVE (0),
+ * EPnP on the inliers (float points as doubles) for the others.
+ * Returns the inlier count (0 on failure); mask, rvec, tvec out. */
+int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const double* K9, const double* dist4,
+                           double thr, double conf, int maxIters, uint64_t seed, int flags, int kind, double* rvec,
+                           double* tvec, uint8_t* mask, int64_t* bestOut, int nthreads) {
     if (bestOut) *bestOut = -1;
     if (N < 4) return 0;
+    if (kind < 0 || kind > 5) kind = 0;
+    const int ep = kind_epnp(kind);
     double cam8[8] = {K9[0], K9[4], K9[2], K9[5], dist4 ? dist4[0] : 0, dist4 ? dist4[1] : 0, dist4 ? dist4[2] : 0,
                       dist4 ? dist4[3] : 0};
     float* pts = (float*)calloc((size_t)N * 8, sizeof(float));
@@ -402,37 +487,98 @@ int orc_solve_pnp_ransac(const double* img, const double* world, int N, const do
     int fused = (flags & ORC_FLAG_FUSED_ERROR) != 0, result = 0;
     float thr2 = (float)(thr * thr);
     double R[9], t[3];
-    if (N == 4) {
-        double x[4], y[4], W[12];
-        for (int i = 0; i < 4; ++i) {
-            undistort(&c, (double)pts[8 * i + 3], (double)pts[8 * i + 4], &x[i], &y[i]);
-            W[3 * i] = pts[8 * i]; W[3 * i + 1] = pts[8 * i + 1]; W[3 * i + 2] = pts[8 * i + 2];
+    if (N == 4 || (ep && N == 5)) {
+        int ok = 1;
+        if (N == 4) {
+            double x[4], y[4], W[12];
+            for (int i = 0; i < 4; ++i) {
+                undistort(&c, (double)pts[8 * i + 3], (double)pts[8 * i + 4], &x[i], &y[i]);
+                W[3 * i] = pts[8 * i]; W[3 * i + 1] = pts[8 * i + 1]; W[3 * i + 2] = pts[8 * i + 2];
+            }
+            ok = ap3p4(&c, x, y, W, R, t);
+        } else {
+            orc_epnp5_f32(pts, cam8, R, t);
         }
-        if (ap3p4(&c, x, y, W, R, t)) {
+        if (ok) {
             orc_rodrigues_inv(R, rvec);
             memcpy(tvec, t, sizeof(t));
-            if (mask) memset(mask, 1, 4);
-            result = 4;
+            if (mask) memset(mask, 1, (size_t)N);
+            result = N;
         }
         free(pts);
         return result;
     }
     int64_t niters = maxIters > 1 ? maxIters : 1;
     int* cnt = (int*)malloc(sizeof(int) * (size_t)niters);
-    orc_pnp_counts(pts, N, cam8, seed, 0, niters, thr2, fused, cnt, nthreads);
+    orc_pnp_counts_k(pts, N, cam8, seed, 0, niters, thr2, fused, kind, cnt, nthreads);
     int bc = 0;
-    int64_t best = orc_ransac_replay(cnt, niters, N, 4, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0, &bc);
+    int64_t best = orc_ransac_replay(cnt, niters, N, ep ? 5 : 4, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0,
+                                     &bc);
     free(cnt);
-    if (best >= 0 && orc_pnp_hypothesis(pts, N, cam8, seed, best, R, t, NULL) == 1) {
+    int st = best < 0 ? 0
+             : ep     ? orc_pnp_hypothesis_epnp(pts, N, cam8, seed, best, R, t, NULL)
+                      : orc_pnp_hypothesis(pts, N, cam8, seed, best, R, t, NULL);
+    if (st == 1) {
         uint8_t* m = (uint8_t*)malloc((size_t)N);
         result = orc_pnp_count(pts, N, cam8, R, t, thr2, fused, m);
         orc_rodrigues_inv(R, rvec);
         memcpy(tvec, t, sizeof(t));
-        if (!(flags & ORC_FLAG_NO_REFINE) && result > 0) orc_pnp_lm(pts, N, m, cam8, rvec, tvec, 20);
+        if (!(flags & ORC_FLAG_NO_REFINE) && result > 0) {
+            if (kind == 0) {
+                orc_pnp_lm(pts, N, m, cam8, rvec, tvec, 20);
+            } else {
+                double* ii = (double*)malloc(sizeof(double) * 2 * (size_t)result);
+                double* ww = (double*)malloc(sizeof(double) * 3 * (size_t)result);
+                int k = 0;
+                for (int i = 0; i < N; ++i)
+                    if (m[i]) {
+                        const float* p = pts + 8 * (size_t)i;
+                        ii[2 * k] = p[3]; ii[2 * k + 1] = p[4];
+                        ww[3 * k] = p[0]; ww[3 * k + 1] = p[1]; ww[3 * k + 2] = p[2];
+                        ++k;
+                    }
+                double R2[9];
+                orc_epnp_points(ii, ww, result, cam8, R2, tvec);
+                orc_rodrigues_inv(R2, rvec);
+                free(ii);
+                free(ww);
+            }
+        }
         if (mask) memcpy(mask, m, (size_t)N);
         free(m);
         if (bestOut) *bestOut = best;
     }
     free(pts);
     return result;
+}
+
+int orc_solve_pnp_ransac(const double* img, const double* world, int N, const double* K9, const double* dist4,
+                         double thr, double conf, int maxIters, uint64_t seed, int flags, double* rvec, double* tvec,
+                         uint8_t* mask, int64_t* bestOut, int nthreads) {
+    return orc_solve_pnp_ransac_k(img, world, N, K9, dist4, thr, conf, maxIters, seed, flags, 5, rvec, tvec, mask,
+                                  bestOut, nthreads);
+}
+
+/* cvSolvePnP for the EPnP family (1, 3, 4: EPnP on all double points) and ITERATIVE / SQPNP (0, 6:
+ * that pose, then LM over all points as float PnpPoints). Returns 1, or 0 for a non-finite pose. */
+int orc_solve_pnp(const double* img, const double* world, int N, const double* K9, const double* dist4, int kind,
+                  double* rvec, double* tvec) {
+    double cam8[8] = {K9[0], K9[4], K9[2], K9[5], dist4 ? dist4[0] : 0, dist4 ? dist4[1] : 0, dist4 ? dist4[2] : 0,
+                      dist4 ? dist4[3] : 0};
+    double R[9];
+    orc_epnp_points(img, world, N, cam8, R, tvec);
+    orc_rodrigues_inv(R, rvec);
+    for (int k = 0; k < 3; ++k)
+        if (!isfinite(rvec[k]) || !isfinite(tvec[k])) return 0;
+    if (kind == 0 || kind == 6 || kind < 0 || kind > 6) {
+        float* pts = (float*)calloc((size_t)N * 8, sizeof(float));
+        for (int i = 0; i < N; ++i) {
+            float* p = pts + 8 * (size_t)i;
+            p[0] = (float)world[3 * i]; p[1] = (float)world[3 * i + 1]; p[2] = (float)world[3 * i + 2];
+            p[3] = (float)img[2 * i]; p[4] = (float)img[2 * i + 1];
+        }
+        orc_pnp_lm(pts, N, NULL, cam8, rvec, tvec, 20);
+        free(pts);
+    }
+    return 1;
 }

@@ -44,6 +44,14 @@ _SIGS = {
     "orc_pnp_counts": (None, [_P, _I, _P, _U64, _I64, _I64, _F, _I, _P, _I]),
     "orc_pnp_lm": (None, [_P, _I, _P, _P, _P, _P, _I]),
     "orc_solve_pnp_ransac": (_I, [_P, _P, _I, _P, _P, _D, _D, _I, _U64, _I, _P, _P, _P, _P, _I]),
+    "orc_pnp_vvs": (None, [_P, _I, _P, _P, _P, _I, _D]),
+    "orc_pnp_counts_k": (None, [_P, _I, _P, _U64, _I64, _I64, _F, _I, _I, _P, _I]),
+    "orc_solve_pnp_ransac_k": (_I, [_P, _P, _I, _P, _P, _D, _D, _I, _U64, _I, _I, _P, _P, _P, _P, _I]),
+    "orc_solve_pnp": (_I, [_P, _P, _I, _P, _P, _I, _P, _P]),
+    "orc_epnp": (None, [_P, _P, _I, _P, _P, _P]),
+    "orc_epnp5_f32": (None, [_P, _P, _P, _P]),
+    "orc_pnp_hypothesis_epnp": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
+    "orc_epnp_points": (None, [_P, _P, _I, _P, _P, _P]),
     "orc_rodrigues": (None, [_P, _P, _P]),
     "orc_rodrigues_inv": (None, [_P, _P]),
     "orc_scaled_costs": (None, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _I]),
@@ -286,10 +294,66 @@ def pnp_hypothesis(pts8, c8, seed, hyp):
     return st, R.reshape(3, 3), t, idx
 
 
-def pnp_counts(pts8, c8, seed, begin, count, thr2, fused=False, nthreads=0):
+def pnp_counts(pts8, c8, seed, begin, count, thr2, fused=False, nthreads=0, kind=5):
+    """Per-hypothesis counts with the minimal solver of solverKind `kind` (AP3P for 2 / 5, else EPnP)."""
     out = np.zeros(count, dtype=np.int32)
-    load().orc_pnp_counts(ptr(pts8), pts8.shape[0], ptr(c8), seed, begin, count, thr2, int(fused), ptr(out), nthreads)
+    load().orc_pnp_counts_k(ptr(pts8), pts8.shape[0], ptr(c8), seed, begin, count, thr2, int(fused), int(kind),
+                            ptr(out), nthreads)
     return out
+
+
+def pnp_lm(pts8, c8, rvec, tvec, mask=None, max_iters=20):
+    """cvRefinePnPLM's definition (pnp_host.cpp pnp_lm) -> (rvec, tvec)."""
+    r = np.ascontiguousarray(rvec, dtype=np.float64).copy()
+    t = np.ascontiguousarray(tvec, dtype=np.float64).copy()
+    m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+    load().orc_pnp_lm(ptr(pts8), pts8.shape[0], None if m is None else ptr(m), ptr(c8), ptr(r), ptr(t), max_iters)
+    return r, t
+
+
+def pnp_vvs(pts8, c8, rvec, tvec, max_iters=20, lam=1.0):
+    """cvRefinePnPVVS's definition (pnp_host.cpp pnp_vvs) -> (rvec, tvec)."""
+    r = np.ascontiguousarray(rvec, dtype=np.float64).copy()
+    t = np.ascontiguousarray(tvec, dtype=np.float64).copy()
+    load().orc_pnp_vvs(ptr(pts8), pts8.shape[0], ptr(c8), ptr(r), ptr(t), max_iters, lam)
+    return r, t
+
+
+def pnp_hypothesis_epnp(pts8, c8, seed, hyp):
+    R, t, idx = np.zeros(9), np.zeros(3), np.full(5, -1, dtype=np.int32)
+    st = load().orc_pnp_hypothesis_epnp(ptr(pts8), pts8.shape[0], ptr(c8), seed, hyp, ptr(R), ptr(t), ptr(idx))
+    return st, R.reshape(3, 3), t, idx
+
+
+def epnp(pw, us, cam4):
+    """compute_pose on n points: pw (n, 3) world, us (n, 2) pixels, cam4 = (fu, fv, uc, vc)."""
+    pw = np.ascontiguousarray(pw, dtype=np.float64)
+    us = np.ascontiguousarray(us, dtype=np.float64)
+    c = np.ascontiguousarray(cam4, dtype=np.float64)
+    R, t = np.zeros(9), np.zeros(3)
+    load().orc_epnp(ptr(pw), ptr(us), pw.shape[0], ptr(c), ptr(R), ptr(t))
+    return R.reshape(3, 3), t
+
+
+def epnp_points(img, world, c8):
+    """solvePnP(EPNP) on double points: undistortPoints (double) then compute_pose."""
+    img = np.ascontiguousarray(img, dtype=np.float64)
+    world = np.ascontiguousarray(world, dtype=np.float64)
+    R, t = np.zeros(9), np.zeros(3)
+    load().orc_epnp_points(ptr(img), ptr(world), img.shape[0], ptr(np.ascontiguousarray(c8, dtype=np.float64)),
+                           ptr(R), ptr(t))
+    return R.reshape(3, 3), t
+
+
+def solve_pnp(img, world, K, dist=None, kind=1):
+    """cvSolvePnP for kinds 0 / 1 / 3 / 4 / 6 -> (ok, rvec, tvec)."""
+    img = np.ascontiguousarray(img, dtype=np.float64)
+    world = np.ascontiguousarray(world, dtype=np.float64)
+    K9 = np.ascontiguousarray(np.asarray(K, dtype=np.float64).ravel())
+    d = np.ascontiguousarray(np.zeros(4) if dist is None else np.asarray(dist, dtype=np.float64))
+    r, t = np.zeros(3), np.zeros(3)
+    ok = load().orc_solve_pnp(ptr(img), ptr(world), img.shape[0], ptr(K9), ptr(d), int(kind), ptr(r), ptr(t))
+    return bool(ok), r, t
 
 
 def pnp_count(pts8, c8, R, t, thr2, fused=False):
@@ -300,7 +364,7 @@ def pnp_count(pts8, c8, R, t, thr2, fused=False):
     return n, m
 
 
-def solve_pnp_ransac(img, world, K, dist=None, thr=8.0, conf=0.99, max_iters=100, seed=0, flags=0, nthreads=0):
+def solve_pnp_ransac(img, world, K, dist=None, thr=8.0, conf=0.99, max_iters=100, seed=0, flags=0, nthreads=0, kind=5):
     img = np.ascontiguousarray(img, dtype=np.float64)
     world = np.ascontiguousarray(world, dtype=np.float64)
     K9 = np.ascontiguousarray(np.asarray(K, dtype=np.float64).ravel())
@@ -309,8 +373,8 @@ def solve_pnp_ransac(img, world, K, dist=None, thr=8.0, conf=0.99, max_iters=100
     r, t = np.zeros(3), np.zeros(3)
     mask = np.zeros(max(n, 1), dtype=np.uint8)
     best = np.zeros(1, dtype=np.int64)
-    cnt = load().orc_solve_pnp_ransac(ptr(img), ptr(world), n, ptr(K9), ptr(d), float(thr), conf, max_iters, seed,
-                                      flags, ptr(r), ptr(t), ptr(mask), ptr(best), nthreads)
+    cnt = load().orc_solve_pnp_ransac_k(ptr(img), ptr(world), n, ptr(K9), ptr(d), float(thr), conf, max_iters, seed,
+                                        flags, int(kind), ptr(r), ptr(t), ptr(mask), ptr(best), nthreads)
     return cnt, r, t, mask[:n], int(best[0])
 
 

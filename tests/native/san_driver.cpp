@@ -28,6 +28,13 @@ int orc_f_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, doubl
 int orc_e_hypothesis(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90, int* idx_out);
 int orc_pnp_hypothesis(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R, double* t,
                        int* idx_out);
+int orc_pnp_hypothesis_epnp(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R,
+                            double* t, int* idx_out);
+int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const double* K9, const double* dist4,
+                           double thr, double conf, int maxIters, uint64_t seed, int flags, int kind, double* rvec,
+                           double* tvec, uint8_t* mask, int64_t* bestOut, int nthreads);
+int orc_solve_pnp(const double* img, const double* world, int N, const double* K9, const double* dist4, int kind,
+                  double* rvec, double* tvec);
 int orc_find_homography(const double* src, const double* dst, int N, double thr, double conf, int maxIters, int method,
                         uint64_t seed, int flags, double* H, uint8_t* mask, int64_t* bestHypOut, int nthreads);
 int orc_find_fundamental(const double* a, const double* b, int N, double thr, double conf, int maxIters, int method,
@@ -138,6 +145,18 @@ int main() {
             const int s2 = orc_pnp_hypothesis(reinterpret_cast<const float*>(pts.data()), N, cam8, 5, h, R2, t2, i2);
             expect(s1 == s2, "pnp status", s1, s2);
             if (s1 == 1 && s2 == 1) expect(same_bits(p1.R, R2, 9) && same_bits(p1.t, t2, 3), "pnp pose", h, N);
+            // EPnP hypotheses (epnp.h: JacobiSVD, SVBkSb, Gauss-Newton); every 4th on a planar copy
+            std::vector<mcv::PnpPoint> q = pts;
+            if (h % 4 == 3)
+                for (auto& p : q) p.Z = 0.f;
+            mcv::PnpPose e1;
+            std::memset(&e1, 0, sizeof(e1));
+            double R3[9] = {0}, t3[3] = {0};
+            int j1[5], j2[5];
+            const int u1 = mcv::pnp_hypothesis_epnp(q.data(), N, cam, 6, (uint64_t)h, e1, j1);
+            const int u2 = orc_pnp_hypothesis_epnp(reinterpret_cast<const float*>(q.data()), N, cam8, 6, h, R3, t3, j2);
+            expect(u1 == u2, "epnp status", u1, u2);
+            if (u1 == 1 && u2 == 1) expect(same_bits(e1.R, R3, 9) && same_bits(e1.t, t3, 3), "epnp pose", h, N);
         }
     }
 
@@ -174,6 +193,13 @@ int main() {
         k = orc_solve_pnp_ransac(img.data(), w3.data(), N, K9, d4, 8.0, 0.99, 100, 1, 0, rv, tv, mask.data(), &best,
                                  threads);
         expect(k >= 0, "solve_pnp_ransac", k, 0);
+        for (int kind : {0, 1}) {
+            k = orc_solve_pnp_ransac_k(img.data(), w3.data(), N, K9, d4, 8.0, 0.99, 100, 1, 0, kind, rv, tv, mask.data(),
+                                       &best, threads);
+            expect(k >= 0, "solve_pnp_ransac_k", k, kind);
+        }
+        k = orc_solve_pnp(img.data(), w3.data(), N, K9, d4, 1, rv, tv);
+        expect(k >= 0, "solve_pnp", k, 0);
         // matchers
         std::vector<uint8_t> qb(64 * 32), tb(80 * 32);
         for (auto& v : qb) v = (uint8_t)(rng() & 0xFF);

@@ -1,9 +1,10 @@
 """GPU parity of the PnP path behind cvSolvePnPRansac / cvSolvePnP /
 cvRefinePnPLM / cvRefinePnPVVS / solveAp3p (MiniCVNative.cpp:48-163, ap3p.cpp:282-317) against
 the oracle (oracle/oracle_pnp.c).
-Bar: per-hypothesis inlier counts and the RANSAC inlier set bit-exact; AP3P solutions bit-exact;
-the LM-refined pose within 1e-6 (relative) of the oracle's (GPU sums in another order); refined
-poses reach the ground truth on synthetic data."""
+Bar: per-hypothesis poses (AP3P and EPnP kernels), inlier counts and the RANSAC inlier set
+bit-exact; the EPnP inlier solve bit-exact in t (the rvec through the host Rodrigues map to 1e-14);
+the LM / VVS refined poses within 1e-6 (relative) of the oracle's (GPU sums in another order);
+refined poses reach the ground truth on synthetic data."""
 import ctypes as C
 
 import numpy as np
@@ -27,11 +28,14 @@ def rot(r):
     return S.rotation(r / np.linalg.norm(r), np.linalg.norm(r)) if np.linalg.norm(r) > 0 else np.eye(3)
 
 
+@pytest.mark.parametrize("kind", [5, 1])
 @pytest.mark.parametrize("n,outl,seed,begin,count,dist,unfused", [
     (4, 0.0, 1, 0, 32, None, False), (5, 0.2, 2, 0, 100, None, False), (300, 0.5, 3, 0, 256, DIST, False),
     (5000, 0.5, 4, 77777, 100, DIST, False), (2001, 0.6, 5, 0, 300, None, True), (20000, 0.5, 6, 2**31, 64, DIST,
                                                                                   False)])
-def test_pnp_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, dist, unfused):
+def test_pnp_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, dist, unfused, kind):
+    if kind == 1 and n < 5:
+        pytest.skip("EPnP samples 5 points")
     torch, dev = torch_dev
     from minicv_amd import device as D
     img, W, inl, K, d, R, t = S.pnp_problem(n, seed=seed, outlier_frac=outl, dist=dist)
@@ -42,34 +46,81 @@ def test_pnp_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, di
     plan.set_camera(K, d)
     thr = 2.0
     cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused).to_c()
+    cfg.pnpKind = kind
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     counts = torch.zeros(count, dtype=torch.int32, device=dev)
     plan.evaluate(pts, n, cfg, begin, count, key, counts)
-    ref = oracle.pnp_counts(pts8, oracle.cam8(K, d), seed, begin, count, float(np.float32(thr * thr)), not unfused)
+    ref = oracle.pnp_counts(pts8, oracle.cam8(K, d), seed, begin, count, float(np.float32(thr * thr)), not unfused,
+                            kind=kind)
     np.testing.assert_array_equal(counts.cpu().numpy(), ref)
-    if (ref >= 4).any() and not (ref == -2).any():
+    m = 5 if kind == 1 else 4
+    if (ref >= m).any() and not (ref == -2).any():
         c = ref.max()
         i = int(np.nonzero(ref == c)[0][0])
         assert int(key[0].item()) == (int(c) << 32) | (0xFFFFFFFF - (begin + i))
     plan.close()
 
 
+@pytest.mark.parametrize("n,seed,dist,planar", [(1000, 1, DIST, False), (37, 2, None, False), (500, 3, DIST, True),
+                                                (6, 4, None, False)])
+def test_epnp_hypotheses_bit_exact(native, gpu, oracle, n, seed, dist, planar):
+    """The EPnP kernel's poses (one lane per hypothesis, epnp.h) equal the C restatement bit for bit,
+    planar targets (zero singular values, cv::RNG branch) and degenerate samples included."""
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=seed, outlier_frac=0.4, dist=dist)
+    if planar:
+        W[:, 2] = 0.0
+        W[::7] = W[0]                                   # duplicated world points
+    pts8 = oracle.pack_pnp(img, W)
+    c8 = oracle.cam8(K, d)
+    count = 512
+    poses = np.zeros((count, 12))
+    status = np.zeros(count, np.int32)
+    got = native.lib().mcvTestPnpHypotheses(pts8.ctypes.data, n, c8.ctypes.data, 77, 1000, count, 1,
+                                            poses.ctypes.data, status.ctypes.data)
+    assert got == count, native.last_error()
+    for h in range(count):
+        st, Ro, to, _ = oracle.pnp_hypothesis_epnp(pts8, c8, 77, 1000 + h)
+        assert status[h] == st
+        np.testing.assert_array_equal(poses[h, :9], Ro.ravel(), err_msg=f"hyp {h}")
+        np.testing.assert_array_equal(poses[h, 9:], to, err_msg=f"hyp {h}")
+
+
+def test_ap3p_hypotheses_bit_exact(native, gpu, oracle):
+    img, W, inl, K, d, R, t = S.pnp_problem(800, seed=5, outlier_frac=0.5, dist=DIST)
+    pts8 = oracle.pack_pnp(img, W)
+    c8 = oracle.cam8(K, d)
+    count = 512
+    poses = np.zeros((count, 12))
+    status = np.zeros(count, np.int32)
+    assert native.lib().mcvTestPnpHypotheses(pts8.ctypes.data, 800, c8.ctypes.data, 3, 0, count, 5,
+                                             poses.ctypes.data, status.ctypes.data) == count
+    for h in range(count):
+        st, Ro, to, _ = oracle.pnp_hypothesis(pts8, c8, 3, h)
+        assert status[h] == st
+        if st == 1:
+            np.testing.assert_array_equal(poses[h, :9], Ro.ravel())
+            np.testing.assert_array_equal(poses[h, 9:], to)
+
+
+@pytest.mark.parametrize("kind", [5, 1, 0])
 @pytest.mark.parametrize("n,outl,seed,iters,thr,dist,flags", [
     (50, 0.3, 1, 100, 2.0, None, 0), (3000, 0.5, 2, 100, 2.0, DIST, 0), (3000, 0.6, 3, 300, 3.0, None, 0),
     (20000, 0.5, 4, 100, 2.0, DIST, 0), (2000, 0.5, 5, 200, 2.0, None, N.FLAG_FIXED_ITERS | N.FLAG_FUSED_ERROR),
     (2000, 0.5, 6, 200, 2.0, DIST, N.FLAG_NO_REFINE)])
-def test_solve_pnp_ransac_vs_oracle(gpu, oracle, n, outl, seed, iters, thr, dist, flags):
+def test_solve_pnp_ransac_vs_oracle(gpu, oracle, n, outl, seed, iters, thr, dist, flags, kind):
     img, W, inl, K, d, R, t = S.pnp_problem(n, seed=seed, outlier_frac=outl, sigma=0.3, dist=dist)
     p = opencv.RansacParams(threshold=thr, confidence=0.99, max_iters=iters, seed=seed,
                             fixed_iters=bool(flags & N.FLAG_FIXED_ITERS), refine=not (flags & N.FLAG_NO_REFINE),
                             fused_error=bool(flags & N.FLAG_FUSED_ERROR))
-    ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, d, params=p)
+    name = {0: "Iterative", 1: "EPNP", 5: "AP3P"}[kind]
+    ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, d, kind=name, params=p)
     rc, rr, rt, rmask, best = oracle.solve_pnp_ransac(img, W, K, d, thr=thr, conf=0.99, max_iters=iters, seed=seed,
-                                                      flags=flags)
+                                                      flags=flags, kind=kind)
     assert ok and rc > 0
     np.testing.assert_array_equal(inliers, np.nonzero(rmask)[0])
-    if flags & N.FLAG_NO_REFINE:
-        np.testing.assert_array_equal(r, rr)
+    if flags & N.FLAG_NO_REFINE or kind != 0:
+        # the hypothesis pose, or EPnP on the inliers: same bits; rvec via two Rodrigues restatements
+        np.testing.assert_allclose(r, rr, rtol=0, atol=1e-14)
         np.testing.assert_array_equal(tt, rt)
     else:
         np.testing.assert_allclose(r, rr, rtol=1e-6, atol=1e-9)
@@ -79,10 +130,22 @@ def test_solve_pnp_ransac_vs_oracle(gpu, oracle, n, outl, seed, iters, thr, dist
         assert np.abs(rot(r) - R).max() < tol and np.abs(tt - t).max() < 10 * tol
 
 
+@pytest.mark.parametrize("kind", ["EPNP", "Iterative", "DLS"])
+def test_five_points_direct_epnp(gpu, oracle, kind):
+    """npoints == model_points (5): one EPnP on the float points, all inliers (solvePnPRansac)."""
+    img, W, inl, K, d, R, t = S.pnp_problem(5, seed=31, outlier_frac=0, sigma=0, dist=DIST)
+    ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, d, kind=kind, iterations=100, reproj_error=2.0)
+    rc, rr, rt, rmask, _ = oracle.solve_pnp_ransac(img, W, K, d, thr=2.0, kind=opencv.SOLVER_KIND[kind])
+    assert ok and rc == 5 and list(inliers) == [0, 1, 2, 3, 4]
+    np.testing.assert_array_equal(tt, rt)
+    np.testing.assert_allclose(r, rr, rtol=0, atol=1e-14)
+    assert np.abs(rot(r) - R).max() < 1e-4
+
+
 def test_solve_pnp_ransac_reference_signature(native, gpu):
     """cvSolvePnPRansac through ctypes exactly like the F# P/Invoke (OpenCV.fs:364-365, :999)."""
     img, W, inl, K, d, R, t = S.pnp_problem(5000, seed=11, outlier_frac=0.5, sigma=0.3)
-    for kind in ("Iterative", "EPNP", "P3P", "AP3P"):
+    for kind in ("Iterative", "EPNP", "P3P", "DLS", "UPNP", "AP3P"):
         ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, None, kind=kind, iterations=100, reproj_error=2.0,
                                                    confidence=0.99)
         assert ok and len(inliers) > 0.95 * inl.sum() and inl[inliers].mean() > 0.99
@@ -105,10 +168,29 @@ def test_n4_and_solve_pnp(gpu, oracle):
     img, W, inl, K, d, R, t = S.pnp_problem(500, seed=13, outlier_frac=0, sigma=0.1, dist=DIST)
     ok3, r3, t3 = opencv.solvePnP(img, W, K, d, kind="Iterative")
     assert ok3 and np.abs(rot(r3) - R).max() < 1e-3 and np.abs(t3 - t).max() < 1e-2
+    ok4, r4, t4 = oracle.solve_pnp(img, W, K, d, kind=0)
+    np.testing.assert_allclose(r3, r4, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(t3, t4, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("n,kind", [(6, "EPNP"), (500, "EPNP"), (3000, "UPNP"), (20000, "DLS"), (4, "EPNP")])
+def test_solve_pnp_epnp_vs_oracle(gpu, oracle, n, kind):
+    """cvSolvePnP with the EPnP family: compute_pose on all double points, bit-exact t (blocked sums
+    beyond 1024 points, the device passes against the C restatement)."""
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=40 + n, outlier_frac=0, sigma=0.2, dist=DIST)
+    ok, r, tt = opencv.solvePnP(img, W, K, d, kind=kind)
+    ok2, rr, rt = oracle.solve_pnp(img, W, K, d, kind=opencv.SOLVER_KIND[kind])
+    assert ok == ok2
+    np.testing.assert_array_equal(tt, rt)
+    np.testing.assert_allclose(r, rr, rtol=0, atol=1e-14)
+    if n >= 500:
+        assert np.abs(rot(r) - R).max() < 1e-3
 
 
 @pytest.mark.parametrize("vvs", [False, True])
-def test_refine_converges(gpu, vvs):
+def test_refine_converges(gpu, oracle, vvs):
+    """cvRefinePnPLM / cvRefinePnPVVS from a perturbed pose: the truth is reached, and the result equals
+    the oracle's restatement of the same iteration (sequential sums) to 1e-6 relative."""
     img, W, inl, K, d, R, t = S.pnp_problem(2000, seed=14, outlier_frac=0, sigma=0.05, dist=DIST)
     from minicv_amd.synthetic import rotation
     R0 = rotation([1, 0, 0], 0.05) @ R
@@ -117,6 +199,10 @@ def test_refine_converges(gpu, vvs):
     fn = opencv.refinePnPVVS if vvs else opencv.refinePnPLM
     r, tt = fn(img, W, K, d, r0, t0)
     assert np.abs(rot(r) - R).max() < 1e-3 and np.abs(tt - t).max() < 1e-2
+    pts8, c8 = oracle.pack_pnp(img, W), oracle.cam8(K, d)
+    rr, rt = oracle.pnp_vvs(pts8, c8, r0, t0) if vvs else oracle.pnp_lm(pts8, c8, r0, t0)
+    np.testing.assert_allclose(r, rr, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(tt, rt, rtol=1e-6, atol=1e-9)
 
 
 def _rvec(R):

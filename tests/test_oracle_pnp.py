@@ -97,3 +97,110 @@ def test_host_rodrigues_matches_oracle(native, oracle):
         r2 = np.zeros(3)
         L.mcvHostRodriguesInv(np.ascontiguousarray(R).ctypes.data, r2.ctypes.data)
         np.testing.assert_allclose(r2, oracle.rodrigues_inv(Ro), atol=1e-14)
+
+
+# ---- EPnP (oracle/oracle_epnp.c; product twin minicv_amd/csrc/epnp.h) ---------------------------
+def _project_px(W, K, R, t):
+    Xc = W @ R.T + t
+    return np.c_[Xc[:, 0] / Xc[:, 2] * K[0, 0] + K[0, 2], Xc[:, 1] / Xc[:, 2] * K[1, 1] + K[1, 2]]
+
+
+@pytest.mark.parametrize("n", [5, 6, 12, 200, 1024, 1025, 5000])
+def test_epnp_exact_recovery(oracle, n):
+    """Noise-free pixels of a known pose: compute_pose returns it (n > 1024 exercises the blocked sums)."""
+    rng = np.random.default_rng(n)
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    for trial in range(20):
+        R, t = _pose(rng)
+        W = rng.uniform(-3, 3, size=(n, 3))
+        us = _project_px(W, K, R, t)
+        Re, te = oracle.epnp(W, us, (K[0, 0], K[1, 1], K[0, 2], K[1, 2]))
+        assert np.abs(Re - R).max() < 1e-8 and np.abs(te - t).max() < 1e-7, (trial, Re - R, te - t)
+        np.testing.assert_allclose(Re @ Re.T, np.eye(3), atol=1e-12)
+
+
+@pytest.mark.parametrize("n", [5, 40, 3000])
+def test_epnp_planar_target(oracle, n):
+    """Near-planar targets (|Z| <= 1e-2) are recovered exactly. On an exactly planar one (Z = 0)
+    PW0^T PW0 has a zero singular value: the null-singular-vector branch of JacobiSVD (cv::RNG fill)
+    runs, the fourth control point coincides with the centroid and OpenCV's general-case EPnP (no
+    planar variant) is ill-posed; the restatement only has to stay finite and return a rotation."""
+    rng = np.random.default_rng(100 + n)
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    cam4 = (K[0, 0], K[1, 1], K[0, 2], K[1, 2])
+    for trial in range(10):
+        R, t = _pose(rng)
+        W = np.c_[rng.uniform(-3, 3, size=(n, 2)), rng.uniform(-1e-2, 1e-2, size=n)]
+        Re, te = oracle.epnp(W, _project_px(W, K, R, t), cam4)
+        assert np.abs(Re - R).max() < 1e-9 and np.abs(te - t).max() < 1e-8, trial
+        W[:, 2] = 0.0
+        Re, te = oracle.epnp(W, _project_px(W, K, R, t), cam4)
+        assert np.isfinite(Re).all() and np.isfinite(te).all()
+        np.testing.assert_allclose(Re @ Re.T, np.eye(3), atol=1e-9)
+        assert abs(np.linalg.det(Re) - 1) < 1e-9
+
+
+def _epnp_cases(rng, count):
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    cam4 = np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]])
+    for c in range(count):
+        R, t = _pose(rng)
+        W = rng.uniform(-3, 3, size=(5, 3))
+        if c % 5 == 1:
+            W[:, 2] = 0.0                                      # planar
+        if c % 5 == 2:
+            W[3] = W[0] + 1e-7 * rng.normal(size=3)            # near-duplicate point
+        us = _project_px(W, K, R, t)
+        if c % 5 == 3:
+            us = us + rng.normal(scale=2.0, size=us.shape)     # noisy
+        if c % 5 == 4:
+            us = rng.uniform(0, 1000, size=us.shape)           # garbage
+        yield np.ascontiguousarray(W), np.ascontiguousarray(us), cam4
+
+
+def test_host_epnp5_bit_exact(native, oracle):
+    """The x86 build of epnp_solve_small<5> (the code every GPU lane runs) equals the C restatement
+    bit for bit on regular, planar, near-degenerate, noisy and garbage 5-point sets."""
+    L = native.lib()
+    rng = np.random.default_rng(7)
+    for W, us, cam4 in _epnp_cases(rng, 400):
+        R9, t3 = np.zeros(9), np.zeros(3)
+        L.mcvHostEpnp5(W.ctypes.data, us.ctypes.data, cam4.ctypes.data, R9.ctypes.data, t3.ctypes.data)
+        Ro, to = oracle.epnp(W, us, cam4)
+        np.testing.assert_array_equal(R9, Ro.ravel())
+        np.testing.assert_array_equal(t3, to)
+
+
+def test_host_epnp_hypothesis_bit_exact(native, oracle):
+    img, W, inl, K, d, R, t = S.pnp_problem(1000, seed=6, outlier_frac=0.5, dist=[-0.1, 0.01, 0.002, 0.001])
+    pts8 = oracle.pack_pnp(img, W)
+    c8 = oracle.cam8(K, d)
+    L = native.lib()
+    for hyp in list(range(200)) + [2**32 - 2]:
+        st, Ro, to, io = oracle.pnp_hypothesis_epnp(pts8, c8, 9, hyp)
+        R9, t3, i5 = np.zeros(9), np.zeros(3), np.zeros(5, np.int32)
+        st2 = L.mcvHostPnPEpnp(pts8.ctypes.data, pts8.shape[0], c8.ctypes.data, 9, hyp, R9.ctypes.data,
+                               t3.ctypes.data, i5.ctypes.data)
+        assert st == st2 == 1
+        np.testing.assert_array_equal(Ro.ravel(), R9)
+        np.testing.assert_array_equal(to, t3)
+        np.testing.assert_array_equal(io, i5)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 5])
+def test_ransac_kinds_recover_pose(oracle, kind):
+    """solvePnPRansac per kind: EPnP-5 kernel (0, 1) or AP3P-4 (2, 5); final LM (0) or EPnP on the inliers."""
+    img, W, inl, K, d, R, t = S.pnp_problem(2000, seed=21, outlier_frac=0.4, sigma=0.3, dist=[-0.1, 0.01, 0.0, 0.0])
+    cnt, r, tt, mask, best = oracle.solve_pnp_ransac(img, W, K, d, thr=2.0, conf=0.99, max_iters=300, seed=3,
+                                                     kind=kind)
+    assert cnt == mask.sum() and cnt > 0.95 * inl.sum() and ((mask != 0) & ~inl).sum() < 0.01 * len(img)
+    Rr, _ = oracle.rodrigues(r)
+    assert np.abs(Rr - R).max() < 2e-3 and np.abs(tt - t).max() < 2e-2
+
+
+@pytest.mark.parametrize("kind", [0, 1, 6])
+def test_solve_pnp_all_points(oracle, kind):
+    img, W, inl, K, d, R, t = S.pnp_problem(500, seed=22, outlier_frac=0.0, sigma=0.0, dist=[-0.1, 0.01, 0.002, 0.0])
+    ok, r, tt = oracle.solve_pnp(img, W, K, d, kind=kind)
+    Rr, _ = oracle.rodrigues(r)
+    assert ok and np.abs(Rr - R).max() < 1e-6 and np.abs(tt - t).max() < 1e-5
