@@ -94,17 +94,20 @@ MCV_API DetectorResult* cvDetectFeatures(char* data, int width, int height, int 
 MCV_API void cvFreeFeatures(DetectorResult* res);
 /* Debug export — MiniCVNative.cpp:504 (no-op). */
 MCV_API void cvTest(void);
-/* Five-point minimal solver — MiniCVNative.cpp:368-382 / fivepoint.cpp:233-339 (one GPU solve):
+/* Five-point minimal solver — MiniCVNative.cpp:368-382 / fivepoint.cpp:233-339 (one GPU solve of
+ * the reference's own path: SVD null space, solvePoly roots with |Im| <= 1e-10 in its order):
  * Es: caller-allocated 10 x M33d, unit-Frobenius-norm E with pb^T E pa = 0. Returns the count. */
 MCV_API int  cvFivePoint(const mcvV2d* pa, const mcvV2d* pb, mcvM33d* Es);
 /* PnP — MiniCVNative.cpp:48-163 (on the GPU). K passed by value as in the
  * reference; distortion = 4 doubles (k1, k2, p1, p2; MiniCVNative.cpp:78,120).
- * cvSolvePnPRansac: 4-point AP3P minimal sets (every solverKind; OpenCV uses EPnP with 5 points
- * for kinds 0/1/3/4 — DESIGN.md §3), fp32 reprojection error of projectPoints, inlier iff
- * err <= reprojectionError^2, sequential-RANSAC semantics with seed 0; then Levenberg-Marquardt
- * on the inliers from the best hypothesis. outInliers (caller: N ints) = RANSAC inlier indices.
- * cvSolvePnP: kinds 2/5 (P3P/AP3P) need N == 4 (AP3P, the 4th point picks the solution); other
- * kinds: AP3P-RANSAC initialisation (256 hypotheses, 4 px) + LM over all points. */
+ * cvSolvePnPRansac (OpenCV 4.x solvePnPRansac): solverKind 2 / 5 (P3P / AP3P) sample 4 points
+ * for AP3P, kinds 0 / 1 / 3 / 4 (ITERATIVE / EPNP / DLS / UPNP) sample 5 points for EPnP (other
+ * values act as 0); N == model points -> one solve on all points. fp32 reprojection error of
+ * projectPoints, inlier iff err <= reprojectionError^2, sequential-RANSAC semantics with seed 0;
+ * final pose on the inliers: LM from the RANSAC pose (kind 0), EPnP (every other kind).
+ * outInliers (caller: N ints) = RANSAC inlier indices.
+ * cvSolvePnP: kinds 2 / 5 need N == 4 (AP3P, the 4th point picks the solution); 1 / 3 / 4:
+ * EPnP on all points; 0 / 6 (ITERATIVE / SQPNP) and others: EPnP, then LM over all points. */
 MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                         const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec);
 MCV_API mcvBool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
@@ -117,13 +120,15 @@ MCV_API void cvRefinePnPLM(const mcvV2d* imgPoints, const mcvV3d* worldPoints, c
                            const double* distortionCoeffs, mcvV3d* tVec, mcvV3d* rVec);
 MCV_API void cvRefinePnPVVS(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                             const double* distortionCoeffs, mcvV3d* tVec, mcvV3d* rVec);
-/* AP3P — ap3p.cpp:282-317, float arguments as the F# P/Invoke passes them (OpenCV.fs:373-374;
- * the reference's C++ definition takes doubles — an ABI mismatch in the reference). Rs/ts:
- * caller arrays of 4; R as the reference returns it (ap3p.cpp:245-250). Returns the count. */
-MCV_API int  solveAp3p(mcvM33d* Rs, mcvV3d* ts, float mu0, float mv0, float X0, float Y0, float Z0,
-                       float mu1, float mv1, float X1, float Y1, float Z1,
-                       float mu2, float mv2, float X2, float Y2, float Z2,
-                       float inv_fx, float inv_fy, float cx_fx, float cy_fy);
+/* AP3P — ap3p.cpp:282-317, double arguments as the reference defines them and the F# P/Invoke
+ * passes them (OpenCV.fs:373-374: F# `float` is System.Double). The reference's quartic path:
+ * Ferrari (std::complex) + two Newton polish passes, every root with |cos| <= 1 in its order,
+ * complex roots' real parts included. Rs/ts: caller arrays of 4; R as the reference returns it
+ * (ap3p.cpp:245-250). Returns the count. */
+MCV_API int  solveAp3p(mcvM33d* Rs, mcvV3d* ts, double mu0, double mv0, double X0, double Y0, double Z0,
+                       double mu1, double mv1, double X1, double Y1, double Z1,
+                       double mu2, double mv2, double X2, double Y2, double Z2,
+                       double inv_fx, double inv_fy, double cx_fx, double cy_fy);
 /* Fiducials — MiniCVNative.cpp:384-502 (out of scope: return false). */
 MCV_API mcvBool cvDetectQRCode(char* data, int width, int height, int channels, int* positions, int* count);
 MCV_API mcvBool cvDetectArucoMarkers(char* data, int width, int height, int channels, int* infoCount,
@@ -375,6 +380,8 @@ MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models
  * raw five-point solve (x1[5], y1[5], x2[5], y2[5] packed in p20). Return the model count / status. */
 MCV_API int mcvHostEssential(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90, int* sampleIdx);
 MCV_API int mcvHostFivePoint(const double* p20, double* E90);
+/* Host build of the cvFivePoint export's own path (e_solve5_ref), same packing as mcvHostFivePoint. */
+MCV_API int mcvHostFivePointRef(const double* p20, double* E90);
 MCV_API void mcvHostDecomposeEssential(const double* E9, double* R1, double* R2, double* t3);
 /* Host twin of the real-root finder (Rolle brackets + Illinois) of sum c[k] x^k, deg <= 10;
  * fixed = 1 (deg == 4 only) runs the register-resident fixed-size form the AP3P quartic uses.
@@ -394,6 +401,9 @@ MCV_API void mcvHostEpnp5(const double* pw15, const double* us10, const double* 
  * status[h] = 1 or -1 / -2. Returns hypCount, -1 on failure. */
 MCV_API int mcvTestPnpHypotheses(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin,
                                  int hypCount, int kind, double* poses12, int* status);
+/* Host build of solveAp3p's computation (mu3 / mv3 pixels, W9 = 3 world points), R36 / t12 out. */
+MCV_API int mcvHostSolveAp3p(const double* mu3, const double* mv3, const double* W9, double inv_fx, double inv_fy,
+                             double cx_fx, double cy_fy, double* R36, double* t12);
 MCV_API void mcvHostRodrigues(const double* r, double* R, double* dR27);
 MCV_API void mcvHostRodriguesInv(const double* R, double* r);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,

@@ -63,8 +63,10 @@ MCV_HD double hypot_fma(double x, double y) {
 // JacobiSVDImpl_<double>: A holds the N rows of length M of the TRANSPOSED input (At). On return
 // A's rows are the left singular vectors (normalised), Wo the singular values (descending), and
 // Vt (if non-null) the right singular vectors as rows. The A result does not depend on Vt.
-template <int M, int N>
-MCV_HD void jacobi_svd(double (&A)[N][M], double (&Wo)[N], double (*Vt)[N]) {
+// N1 > N (SVD::FULL_UV with more columns than rows): rows N .. N1-1 of A start at zero and are
+// completed to an orthonormal basis by the cv::RNG branch.
+template <int M, int N, int N1 = N>
+MCV_HD void jacobi_svd(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
     const double eps = kDblEpsilon * 10, minval = kDblMin;
     double W[N];
     for (int i = 0; i < N; ++i) {
@@ -133,8 +135,8 @@ MCV_HD void jacobi_svd(double (&A)[N][M], double (&Wo)[N], double (*Vt)[N]) {
     }
     for (int i = 0; i < N; ++i) Wo[i] = W[i];
     CvRng rng{0x12345678u};
-    for (int i = 0; i < N; ++i) {
-        double sd = W[i];
+    for (int i = 0; i < N1; ++i) {
+        double sd = i < N ? W[i] : 0;
         for (int ii = 0; ii < 100 && sd <= minval; ++ii) {
             // null singular value: random +-1/M vector orthogonalised against the previous rows
             const double val0 = 1. / M;

@@ -23,7 +23,7 @@
 
 #include "mcv_common.h"
 #include "hyp_essential.h"   // e_poly_real_roots
-#include "epnp.h"
+#include "epnp.h"   // EPnP; kDblMin
 
 namespace mcv {
 
@@ -104,9 +104,16 @@ MCV_HD void v3_cross(const double* a, const double* b, double* r) {
 MCV_HD double v3_dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 MCV_HD double v3_norm(const double* a) { return sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
 
-// b[3][3]: bearing vectors (unit) b1, b2, b3; w[3][3]: world points. Outputs up to 4 solutions
-// (Rr = the reference's R, row-major; tr = translation). Returns the count.
-MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3]) {
+// Everything computePoses derives before the quartic (ap3p.cpp:133-211): the frames k1 / nl /
+// k3 / tz, b3' and the g1..g7 terms; c = quartic coefficients ascending (c[4] s^4 + ... + c[0]).
+struct Ap3pSetup {
+    double k1[3], nl[3], temp[3], k3[3], tz[3], b1[3], b3p[3], w3[3];
+    double g1, g2, g3, g4, g5, g6, g7, k3b3;
+    double c[5];
+    bool ok;   // finite coefficients and non-degenerate frames
+};
+
+MCV_HD void ap3p_setup(const double (*b)[3], const double (*w)[3], Ap3pSetup& S) {
     const double* w1 = w[0];
     const double* w2 = w[1];
     const double* w3 = w[2];
@@ -115,13 +122,14 @@ MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double
     const double* b3 = b[2];
     double u0[3] = {w1[0] - w2[0], w1[1] - w2[1], w1[2] - w2[2]};
     const double nu0 = v3_norm(u0);
-    double k1[3] = {u0[0] / nu0, u0[1] / nu0, u0[2] / nu0};
-    double k3[3];
+    double* k1 = S.k1;
+    k1[0] = u0[0] / nu0; k1[1] = u0[1] / nu0; k1[2] = u0[2] / nu0;
+    double* k3 = S.k3;
     v3_cross(b1, b2, k3);
     const double nk3 = v3_norm(k3);
     k3[0] = k3[0] / nk3; k3[1] = k3[1] / nk3; k3[2] = k3[2] / nk3;
-    double tz[3], v1[3], v2[3];
-    v3_cross(b1, k3, tz);
+    double v1[3], v2[3];
+    v3_cross(b1, k3, S.tz);
     v3_cross(b1, b3, v1);
     v3_cross(b2, b3, v2);
     double u1[3] = {w1[0] - w3[0], w1[1] - w3[1], w1[2] - w3[2]};
@@ -130,14 +138,14 @@ MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double
     double f11 = k3b3;
     double f13 = v3_dot(k3, v1);
     const double f15 = -u1k1 * f11;
-    double nl[3];
+    double* nl = S.nl;
     v3_cross(u1, k1, nl);
     const double delta = v3_norm(nl);
     nl[0] = nl[0] / delta; nl[1] = nl[1] / delta; nl[2] = nl[2] / delta;
     f11 = f11 * delta;
     f13 = f13 * delta;
     const double u2k1 = u1k1 - nu0;
-    double f21 = v3_dot(tz, v2);
+    double f21 = v3_dot(S.tz, v2);
     double f22 = nk3 * k3b3;
     double f23 = v3_dot(k3, v2);
     const double f24 = u2k1 * f22;
@@ -145,15 +153,15 @@ MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double
     f21 = f21 * delta;
     f22 = f22 * delta;
     f23 = f23 * delta;
-    const double g1 = f13 * f22;
-    const double g2 = f13 * f25 - f15 * f23;
-    const double g3 = f11 * f23 - f13 * f21;
-    const double g4 = -f13 * f24;
-    const double g5 = f11 * f22;
-    const double g6 = f11 * f25 - f15 * f21;
-    const double g7 = -f15 * f24;
-    // quartic a4 s^4 + a3 s^3 + a2 s^2 + a1 s + a0, stored ascending for the root finder
-    double c[5];
+    S.g1 = f13 * f22;
+    S.g2 = f13 * f25 - f15 * f23;
+    S.g3 = f11 * f23 - f13 * f21;
+    S.g4 = -f13 * f24;
+    S.g5 = f11 * f22;
+    S.g6 = f11 * f25 - f15 * f21;
+    S.g7 = -f15 * f24;
+    const double g1 = S.g1, g2 = S.g2, g3 = S.g3, g4 = S.g4, g5 = S.g5, g6 = S.g6, g7 = S.g7;
+    double* c = S.c;
     c[4] = g5 * g5 + g1 * g1 + g3 * g3;
     c[3] = 2 * (g5 * g6 + g1 * g2 + g3 * g4);
     c[2] = g6 * g6 + 2 * g5 * g7 + g2 * g2 + g4 * g4 - g1 * g1 - g3 * g3;
@@ -161,52 +169,177 @@ MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double
     c[0] = g7 * g7 - g2 * g2 - g4 * g4;
     bool finite = true;
     for (int k = 0; k < 5; ++k) finite = finite && isfinite(c[k]);
-    if (!finite || !isfinite(delta) || !isfinite(k3b3) || !(nk3 > 0) || !(nu0 > 0) || !(delta > 0)) return 0;
-    double s[4];
-    const int ns = e_poly_real_roots_fixed<4>(c, s);   // = e_poly_real_roots(c, 4, s), register-resident
-    double temp[3];
-    v3_cross(k1, nl, temp);
-    const double Ck1nl[9] = {k1[0], nl[0], temp[0], k1[1], nl[1], temp[1], k1[2], nl[2], temp[2]};
-    const double Cb1k3tzT[9] = {b1[0], b1[1], b1[2], k3[0], k3[1], k3[2], tz[0], tz[1], tz[2]};
+    S.ok = finite && isfinite(delta) && isfinite(k3b3) && nk3 > 0 && nu0 > 0 && delta > 0;
+    v3_cross(k1, nl, S.temp);
+    for (int k = 0; k < 3; ++k) { S.b1[k] = b1[k]; S.w3[k] = w3[k]; }
     const double sc = delta / k3b3;
-    const double b3p[3] = {b3[0] * sc, b3[1] * sc, b3[2] * sc};
+    S.b3p[0] = b3[0] * sc; S.b3p[1] = b3[1] * sc; S.b3p[2] = b3[2] * sc;
+    S.k3b3 = k3b3;
+}
+
+// One root cos(theta1') -> (R, t) (ap3p.cpp:220-255). Returns whether every value is finite.
+MCV_HD bool ap3p_pose(const Ap3pSetup& S, double ct1, double* R, double* tv) {
+    const double Ck1nl[9] = {S.k1[0], S.nl[0], S.temp[0], S.k1[1], S.nl[1], S.temp[1], S.k1[2], S.nl[2], S.temp[2]};
+    const double Cb1k3tzT[9] = {S.b1[0], S.b1[1], S.b1[2], S.k3[0], S.k3[1], S.k3[2], S.tz[0], S.tz[1], S.tz[2]};
+    double st1 = sqrt(1 - ct1 * ct1);
+    st1 = (S.k3b3 > 0) ? st1 : -st1;
+    double ct3 = S.g1 * ct1 + S.g2;
+    double st3 = S.g3 * ct1 + S.g4;
+    const double nt3 = st1 / ((S.g5 * ct1 + S.g6) * ct1 + S.g7);
+    ct3 = ct3 * nt3;
+    st3 = st3 * nt3;
+    const double C13[9] = {ct3, 0, -st3, st1 * st3, ct1, st1 * ct3, ct1 * st3, -st1, ct1 * ct3};
+    double T[9];
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q)
+            T[3 * r + q] = Ck1nl[3 * r] * C13[q] + Ck1nl[3 * r + 1] * C13[3 + q] + Ck1nl[3 * r + 2] * C13[6 + q];
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q)
+            R[3 * r + q] = T[3 * r] * Cb1k3tzT[q] + T[3 * r + 1] * Cb1k3tzT[3 + q] + T[3 * r + 2] * Cb1k3tzT[6 + q];
+    const double* w3 = S.w3;
+    const double rp3[3] = {w3[0] * R[0] + w3[1] * R[3] + w3[2] * R[6], w3[0] * R[1] + w3[1] * R[4] + w3[2] * R[7],
+                           w3[0] * R[2] + w3[1] * R[5] + w3[2] * R[8]};
+    bool ok = isfinite(nt3);
+    for (int k = 0; k < 9; ++k) ok = ok && isfinite(R[k]);
+    for (int k = 0; k < 3; ++k) { tv[k] = st1 * S.b3p[k] - rp3[k]; ok = ok && isfinite(tv[k]); }
+    return ok;
+}
+
+// b[3][3]: bearing vectors (unit) b1, b2, b3; w[3][3]: world points. Outputs up to 4 solutions
+// (Rr = the reference's R, row-major; tr = translation). Returns the count. The RANSAC form: the
+// real roots of the quartic from e_poly_real_roots (bit-reproducible), non-finite poses dropped.
+MCV_HD int ap3p_compute_poses(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3]) {
+    Ap3pSetup S;
+    ap3p_setup(b, w, S);
+    if (!S.ok) return 0;
+    double s[4];
+    const int ns = e_poly_real_roots_fixed<4>(S.c, s);   // = e_poly_real_roots(c, 4, s), register-resident
     int n = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {   // ns <= 4 = kPnpMaxSolutions: no solution is ever cut off
         if (i >= ns) break;
         const double ct1 = s[i];
         if (fabs(ct1) > 1) continue;
-        double st1 = sqrt(1 - ct1 * ct1);
-        st1 = (k3b3 > 0) ? st1 : -st1;
-        double ct3 = g1 * ct1 + g2;
-        double st3 = g3 * ct1 + g4;
-        const double nt3 = st1 / ((g5 * ct1 + g6) * ct1 + g7);
-        ct3 = ct3 * nt3;
-        st3 = st3 * nt3;
-        const double C13[9] = {ct3, 0, -st3, st1 * st3, ct1, st1 * ct3, ct1 * st3, -st1, ct1 * ct3};
-        double T[9], R[9];
-        for (int r = 0; r < 3; ++r)
-            for (int q = 0; q < 3; ++q)
-                T[3 * r + q] = Ck1nl[3 * r] * C13[q] + Ck1nl[3 * r + 1] * C13[3 + q] + Ck1nl[3 * r + 2] * C13[6 + q];
-        for (int r = 0; r < 3; ++r)
-            for (int q = 0; q < 3; ++q)
-                R[3 * r + q] = T[3 * r] * Cb1k3tzT[q] + T[3 * r + 1] * Cb1k3tzT[3 + q] + T[3 * r + 2] * Cb1k3tzT[6 + q];
-        const double rp3[3] = {w3[0] * R[0] + w3[1] * R[3] + w3[2] * R[6], w3[0] * R[1] + w3[1] * R[4] + w3[2] * R[7],
-                               w3[0] * R[2] + w3[1] * R[5] + w3[2] * R[8]};
-        bool ok = isfinite(nt3);
-        double tv[3];
-        for (int k = 0; k < 9; ++k) ok = ok && isfinite(R[k]);
-        for (int k = 0; k < 3; ++k) { tv[k] = st1 * b3p[k] - rp3[k]; ok = ok && isfinite(tv[k]); }
+        double R[9], tv[3];
+        const bool ok = ap3p_pose(S, ct1, R, tv);
         // append to slot n as selects (a dynamically indexed store would put Rr / tr in scratch)
 #pragma unroll
         for (int slot = 0; slot < kPnpMaxSolutions; ++slot) {
-            const bool w = ok && slot == n;
+            const bool wr = ok && slot == n;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) Rr[slot][k] = w ? R[k] : Rr[slot][k];
+            for (int k = 0; k < 9; ++k) Rr[slot][k] = wr ? R[k] : Rr[slot][k];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) tr[slot][k] = w ? tv[k] : tr[slot][k];
+            for (int k = 0; k < 3; ++k) tr[slot][k] = wr ? tv[k] : tr[slot][k];
         }
         if (ok) ++n;
+    }
+    return n;
+}
+
+// ---- the reference's own quartic path for the solveAp3p export ----------------------------------
+// solveQuartic (ap3p.cpp:10-59): Ferrari through std::complex<double> as libstdc++ evaluates it
+// (csqrt of glibc, pow(complex, 1/3) = polar(exp(log|w| / 3), arg(w) / 3), real / complex by
+// Smith's division as libgcc's __divdc3), every root's real part kept; polishQuarticRoots
+// (ap3p.cpp:61-74): two Newton passes over the four roots. Transcendentals (cbrt, log, exp, cos,
+// atan2, hypot) are the device's (ocml) vs glibc on the host: agreement to ~1e-15, not bit for bit.
+struct Cplx { double re, im; };
+
+MCV_HD Cplx cplx_sqrt(double x, double y) {
+    if (!isfinite(x) || !isfinite(y)) {
+        const double n = x + y;
+        return {n, n};
+    }
+    if (y == 0) {
+        if (x < 0) return {0.0, copysign(sqrt(-x), y)};
+        return {fabs(sqrt(x)), copysign(0.0, y)};
+    }
+    if (x == 0) {
+        const double r = fabs(y) >= 2 * kDblMin ? sqrt(0.5 * fabs(y)) : 0.5 * sqrt(2 * fabs(y));
+        return {r, copysign(r, y)};
+    }
+    const double d = hypot(x, y);
+    double r, s;
+    if (x > 0) {
+        r = sqrt(0.5 * (d + x));
+        s = 0.5 * (y / r);
+    } else {
+        s = sqrt(0.5 * (d - x));
+        r = fabs(0.5 * (y / s));
+    }
+    return {r, copysign(s, y)};
+}
+
+MCV_HD Cplx cplx_div(Cplx a, Cplx b) {
+    double ratio, denom;
+    if (fabs(b.re) < fabs(b.im)) {
+        ratio = b.re / b.im;
+        denom = (b.re * ratio) + b.im;
+        return {((a.re * ratio) + a.im) / denom, ((a.im * ratio) - a.re) / denom};
+    }
+    ratio = b.im / b.re;
+    denom = (b.im * ratio) + b.re;
+    return {((a.im * ratio) + a.re) / denom, (a.im - (a.re * ratio)) / denom};
+}
+
+// factors: a4, a3, a2, a1, a0 (descending, as solveQuartic reads them)
+MCV_HD void ap3p_solve_quartic(const double* f, double* roots) {
+    const double a4 = f[0], a3 = f[1], a2 = f[2], a1 = f[3], a0 = f[4];
+    const double a4_2 = a4 * a4, a3_2 = a3 * a3, a4_3 = a4_2 * a4, a2a4 = a2 * a4;
+    const double p4 = (8 * a2a4 - 3 * a3_2) / (8 * a4_2);
+    const double q4 = (a3_2 * a3 - 4 * a2a4 * a3 + 8 * a1 * a4_2) / (8 * a4_3);
+    const double r4 = (256 * a0 * a4_3 - 3 * (a3_2 * a3_2) - 64 * a1 * a3 * a4_2 + 16 * a2a4 * a3_2) / (256 * (a4_3 * a4));
+    const double p3 = ((p4 * p4) / 12 + r4) / 3;
+    const double q3 = (72 * r4 * p4 - 2 * p4 * p4 * p4 - 27 * q4 * q4) / 432;
+    const Cplx sd = cplx_sqrt(q3 * q3 - p3 * p3 * p3, 0.0);
+    Cplx w;
+    if (q3 >= 0) w = {-sd.re - q3, -sd.im};
+    else w = {sd.re - q3, sd.im};
+    double t;
+    if (w.im == 0.0) {
+        const double wr = cbrt(w.re);
+        t = 2.0 * (wr + p3 / wr);
+    } else {
+        const double third = 1.0 / 3;
+        const double lr = log(hypot(w.re, w.im)), li = atan2(w.im, w.re);
+        t = 4.0 * (exp(third * lr) * cos(third * li));
+    }
+    const Cplx sqrt_2m = cplx_sqrt(-2 * p4 / 3 + t, 0.0);
+    const double B_4A = -a3 / (4 * a4);
+    const double complex1 = 4 * p4 / 3 + t;
+    const Cplx complex2 = cplx_div({2 * q4, 0.0}, sqrt_2m);
+    const double sqrt_2m_rh = sqrt_2m.re / 2;
+    const double sqrt1 = cplx_sqrt(-(complex1 + complex2.re), -complex2.im).re / 2;
+    roots[0] = B_4A + sqrt_2m_rh + sqrt1;
+    roots[1] = B_4A + sqrt_2m_rh - sqrt1;
+    const double sqrt2 = cplx_sqrt(-(complex1 - complex2.re), complex2.im).re / 2;
+    roots[2] = B_4A - sqrt_2m_rh + sqrt2;
+    roots[3] = B_4A - sqrt_2m_rh - sqrt2;
+}
+
+MCV_HD void ap3p_polish(const double* c, double* roots) {
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 4; ++j) {
+            const double error = (((c[0] * roots[j] + c[1]) * roots[j] + c[2]) * roots[j] + c[3]) * roots[j] + c[4];
+            const double derivative = ((4 * c[0] * roots[j] + 3 * c[1]) * roots[j] + 2 * c[2]) * roots[j] + c[3];
+            roots[j] -= error / derivative;
+        }
+}
+
+// computePoses exactly as the export runs it: the four polished Ferrari roots in order, |cos| > 1
+// skipped, nothing else filtered (non-finite poses of degenerate input are returned as they come).
+MCV_HD int ap3p_compute_poses_ref(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3]) {
+    Ap3pSetup S;
+    ap3p_setup(b, w, S);
+    const double f[5] = {S.c[4], S.c[3], S.c[2], S.c[1], S.c[0]};
+    double s[4];
+    ap3p_solve_quartic(f, s);
+    ap3p_polish(f, s);
+    int n = 0;
+    for (int i = 0; i < 4; ++i) {
+        const double ct1 = s[i];
+        if (fabs(ct1) > 1) continue;
+        ap3p_pose(S, ct1, Rr[n], tr[n]);
+        ++n;
     }
     return n;
 }

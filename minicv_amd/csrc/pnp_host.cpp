@@ -558,9 +558,10 @@ extern "C" MCV_API void cvRefinePnPVVS(const mcvV2d* imgPoints, const mcvV3d* wo
     }
 }
 
-extern "C" MCV_API int solveAp3p(mcvM33d* Rs, mcvV3d* ts, float mu0, float mv0, float X0, float Y0, float Z0,
-                                 float mu1, float mv1, float X1, float Y1, float Z1, float mu2, float mv2, float X2,
-                                 float Y2, float Z2, float inv_fx, float inv_fy, float cx_fx, float cy_fy) {
+extern "C" MCV_API int solveAp3p(mcvM33d* Rs, mcvV3d* ts, double mu0, double mv0, double X0, double Y0, double Z0,
+                                 double mu1, double mv1, double X1, double Y1, double Z1, double mu2, double mv2,
+                                 double X2, double Y2, double Z2, double inv_fx, double inv_fy, double cx_fx,
+                                 double cy_fy) {
     MCV_GUARD(0, {
         if (!Rs || !ts) fail("solveAp3p: null argument");
         require_device();
@@ -568,8 +569,8 @@ extern "C" MCV_API int solveAp3p(mcvM33d* Rs, mcvV3d* ts, float mu0, float mv0, 
         hipStream_t s = P.own_stream();
         P.reserve(4, 1);
         Ap3pIn in;
-        const float mu[3] = {mu0, mu1, mu2}, mv[3] = {mv0, mv1, mv2};
-        const float W[3][3] = {{X0, Y0, Z0}, {X1, Y1, Z1}, {X2, Y2, Z2}};
+        const double mu[3] = {mu0, mu1, mu2}, mv[3] = {mv0, mv1, mv2};
+        const double W[3][3] = {{X0, Y0, Z0}, {X1, Y1, Z1}, {X2, Y2, Z2}};
         for (int i = 0; i < 3; ++i) {
             in.mu[i] = mu[i];
             in.mv[i] = mv[i];
@@ -590,6 +591,29 @@ extern "C" MCV_API int solveAp3p(mcvM33d* Rs, mcvV3d* ts, float mu0, float mv0, 
         }
         return out.count;
     })
+}
+
+// Host build of the solveAp3p export's computation (bearings + ap3p_compute_poses_ref).
+extern "C" MCV_API int mcvHostSolveAp3p(const double* mu3, const double* mv3, const double* W9, double inv_fx,
+                                        double inv_fy, double cx_fx, double cy_fy, double* R36, double* t12) {
+    double b[3][3], w[3][3];
+    for (int i = 0; i < 3; ++i) {
+        double mu = inv_fx * mu3[i] - cx_fx;
+        double mv = inv_fy * mv3[i] - cy_fy;
+        const double nrm = std::sqrt(mu * mu + mv * mv + 1);
+        const double mk = 1. / nrm;
+        mu = mu * mk;
+        mv = mv * mk;
+        b[i][0] = mu; b[i][1] = mv; b[i][2] = mk;
+        for (int k = 0; k < 3; ++k) w[i][k] = W9[3 * i + k];
+    }
+    double Rr[kPnpMaxSolutions][9], tr[kPnpMaxSolutions][3];
+    const int n = ap3p_compute_poses_ref(b, w, Rr, tr);
+    for (int s = 0; s < n; ++s) {
+        for (int k = 0; k < 9; ++k) R36[9 * s + k] = Rr[s][k];
+        for (int k = 0; k < 3; ++k) t12[3 * s + k] = tr[s][k];
+    }
+    return n;
 }
 
 extern "C" MCV_API int mcvPackPnP(const mcvV2d* img, const mcvV3d* world, int N, void* d_pts, void* stream) {

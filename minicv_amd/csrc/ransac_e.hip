@@ -18,7 +18,7 @@
 //   mcv_e_one           recompute one hypothesis (winner) -> all its models (one wave).
 //   mcv_e_mask          inlier mask of the winner.
 //   mcv_e_cheirality    recoverPose: one lane per (RANSAC inlier, (R, t) candidate) cheirality test.
-//   mcv_e_fivepoint     cvFivePoint: one five-point solve on raw coordinates (one wave).
+//   mcv_e_fivepoint     cvFivePoint: the reference's own five-point path on raw coordinates (one lane).
 #include "mcv_common.h"
 #include "hyp_essential.h"
 #include "five_point_wave.h"
@@ -386,16 +386,15 @@ __global__ __launch_bounds__(256) void mcv_e_cheirality(const double4* __restric
     }
 }
 
+// cvFivePoint: the export's own path (e_solve5_ref: JacobiSVD null space, LU elimination,
+// solvePoly roots with |Im| <= 1e-10 in its order, solveZ), one lane.
 __global__ __launch_bounds__(64) void mcv_e_fivepoint(EFiveIn in, EOneOut* __restrict__ out) {
-    __shared__ EWave S;
-    const EGroup<64> g(threadIdx.x);
-    const int lane = threadIdx.x;
-    ew_stage(S, g, in.x1, in.y1, in.x2, in.y2);
-    double E[9];
-    const int n = ew_solve5(S, g, E);
-    if (lane == 0) out->status = n;
-    if (lane < kEMaxModels)
-        for (int k = 0; k < 9; ++k) out->E[lane][k] = lane < n ? E[k] : 0.0;
+    if (threadIdx.x != 0) return;
+    double E[kEMaxModels][9];
+    const int n = e_solve5_ref(in.x1, in.y1, in.x2, in.y2, E);
+    out->status = n;
+    for (int s = 0; s < kEMaxModels; ++s)
+        for (int k = 0; k < 9; ++k) out->E[s][k] = s < n ? E[s][k] : 0.0;
 }
 
 // ---- launchers ---------------------------------------------------------------------------------

@@ -343,6 +343,17 @@ extern "C" MCV_API int mcvHostFivePoint(const double* p20, double* E90) {
     })
 }
 
+extern "C" MCV_API int mcvHostFivePointRef(const double* p20, double* E90) {
+    MCV_GUARD(-1, {
+        if (!p20 || !E90) fail("mcvHostFivePointRef: null argument");
+        double E[kEMaxModels][9];
+        const int n = e_solve5_ref(p20, p20 + 5, p20 + 10, p20 + 15, E);
+        for (int s = 0; s < kEMaxModels; ++s)
+            for (int k = 0; k < 9; ++k) E90[9 * s + k] = s < n ? E[s][k] : 0.0;
+        return n;
+    })
+}
+
 extern "C" MCV_API int mcvHostRealRoots(const double* c, int deg, int fixed, double* roots) {
     MCV_GUARD(-1, {
         if (!c || !roots || deg < 0 || deg > 10 || (fixed && deg != 4)) fail("mcvHostRealRoots: bad arguments");

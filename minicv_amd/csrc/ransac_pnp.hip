@@ -164,7 +164,8 @@ __global__ __launch_bounds__(256) void mcv_pnp_mask(const PnpPoint* __restrict__
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (int)__popcll(b));
 }
 
-// The reference's solveAp3p (ap3p.cpp:282-317): bearings from (inv_fx u - cx_fx, ...), all solutions.
+// The reference's solveAp3p (ap3p.cpp:282-317): bearings from (inv_fx u - cx_fx, ...), the solutions
+// of its own Ferrari quartic path in its order (ap3p_compute_poses_ref).
 __global__ void mcv_pnp_ap3p(Ap3pIn in, Ap3pOut* __restrict__ out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     double b[3][3], w[3][3];
@@ -179,7 +180,7 @@ __global__ void mcv_pnp_ap3p(Ap3pIn in, Ap3pOut* __restrict__ out) {
         for (int k = 0; k < 3; ++k) w[i][k] = in.W[i][k];
     }
     double Rr[kPnpMaxSolutions][9], tr[kPnpMaxSolutions][3];
-    const int n = ap3p_compute_poses(b, w, Rr, tr);
+    const int n = ap3p_compute_poses_ref(b, w, Rr, tr);
     out->count = n;
     for (int s = 0; s < kPnpMaxSolutions; ++s) {
         for (int k = 0; k < 9; ++k) out->R[s][k] = s < n ? Rr[s][k] : 0.0;

@@ -99,7 +99,7 @@ SIGNATURES = {
     "cvSolvePnPRansac": (_I, [_P, _P, _I, M33d, _P, _I, _I, _F, _D, _P, _P, _P, _P]),
     "cvRefinePnPLM": (None, [_P, _P, _I, M33d, _P, _P, _P]),
     "cvRefinePnPVVS": (None, [_P, _P, _I, M33d, _P, _P, _P]),
-    "solveAp3p": (_I, [_P, _P] + [_F] * 19),
+    "solveAp3p": (_I, [_P, _P] + [_D] * 19),
     "cvDetectQRCode": (_I, [_P, _I, _I, _I, _P, _P]),
     "cvDetectArucoMarkers": (_I, [_P, _I, _I, _I, _P, _P]),
     # new hot-path exports
@@ -140,11 +140,13 @@ SIGNATURES = {
     "mcvHostPhilox": (None, [C.c_uint32] * 6 + [_P]),
     "mcvHostEssential": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostFivePoint": (_I, [_P, _P]),
+    "mcvHostFivePointRef": (_I, [_P, _P]),
     "mcvHostDecomposeEssential": (None, [_P, _P, _P, _P]),
     "mcvHostRealRoots": (_I, [_P, _I, _I, _P]),
     "mcvHostPnP": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
     "mcvHostPnPEpnp": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
     "mcvHostEpnp5": (None, [_P, _P, _P, _P, _P]),
+    "mcvHostSolveAp3p": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _P]),
     "mcvTestPnpHypotheses": (_I, [_P, _I, _P, _U64, _I64, _I, _I, _P, _P]),
     "mcvHostRodrigues": (None, [_P, _P, _P]),
     "mcvHostRodriguesInv": (None, [_P, _P]),

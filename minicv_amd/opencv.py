@@ -268,8 +268,8 @@ def refinePnPVVS(img, world, K, dist, rvec, tvec):
 
 
 def solveAp3p(img, world, K):
-    """OpenCV.solveAp3p (OpenCV.fs:385-431): 3 points, float arguments -> list of (R, t) as the
-    reference returns them (R as stored by ap3p.cpp:245-250)."""
+    """OpenCV.solveAp3p (OpenCV.fs:385-431): 3 points, double arguments (F# `float` is System.Double)
+    -> list of (R, t) as the reference returns them (R as stored by ap3p.cpp:245-250)."""
     img = np.asarray(img, dtype=np.float64)
     world = np.asarray(world, dtype=np.float64)
     K = np.asarray(K, dtype=np.float64).reshape(3, 3)

@@ -339,6 +339,157 @@ int orc_e_solve5(const double* x1, const double* y1, const double* x2, const dou
     return count;
 }
 
+/* cvFivePoint's own path (fivepoint.cpp:233-339) as the export restates it: null space from
+ * SVD::compute(Q, FULL_UV) (JacobiSVD with the cv::RNG completion rows), A(:, :10)^-1 A(:, 10:) by
+ * OpenCV's LUImpl and a sequential product, det B(z), cv::solvePoly (Durand-Kerner, 300 sweeps,
+ * OpenCV Complex arithmetic), roots with |Im| <= 1e-10 in solvePoly's order, SVD::solveZ of B(z),
+ * E scaled by 1 / ||E||. Deviations from the reference: the coefficient matrix and det B(z) use
+ * the generic products of constraint_matrix / pmul (the same polynomials, other rounding). */
+static int lu_solve10(double A[10][10], double b[10][10]) {
+    const double eps = DBL_EPSILON * 100;
+    for (int i = 0; i < 10; ++i) {
+        int k = i;
+        for (int j = i + 1; j < 10; ++j)
+            if (fabs(A[j][i]) > fabs(A[k][i])) k = j;
+        if (fabs(A[k][i]) < eps) return 0;
+        if (k != i) {
+            for (int j = i; j < 10; ++j) { double t = A[i][j]; A[i][j] = A[k][j]; A[k][j] = t; }
+            for (int j = 0; j < 10; ++j) { double t = b[i][j]; b[i][j] = b[k][j]; b[k][j] = t; }
+        }
+        double d = -1 / A[i][i];
+        for (int j = i + 1; j < 10; ++j) {
+            double alpha = A[j][i] * d;
+            for (int q = i + 1; q < 10; ++q) A[j][q] += alpha * A[i][q];
+            for (int q = 0; q < 10; ++q) b[j][q] += alpha * b[i][q];
+        }
+        A[i][i] = -d;
+    }
+    for (int i = 9; i >= 0; --i)
+        for (int j = 0; j < 10; ++j) {
+            double s = b[i][j];
+            for (int q = i + 1; q < 10; ++q) s -= A[i][q] * b[q][j];
+            b[i][j] = s * A[i][i];
+        }
+    return 1;
+}
+
+/* cv::solvePoly(c (ascending, degree 10), roots, 300): re[10], im[10] */
+void orc_solve_poly10(const double* c, double* rre, double* rim) {
+    double cre[11], cim[11];
+    for (int i = 0; i <= 10; ++i) { cre[i] = c[i]; cim[i] = 0.0; }
+    int n = 10;
+    for (; n > 1; --n)
+        if (fabs(cre[n]) + fabs(cim[n]) > DBL_EPSILON) break;
+    double pre = 1, pim = 0;
+    for (int i = 0; i < 10; ++i) { rre[i] = 0; rim[i] = 0; }
+    for (int i = 0; i < n; ++i) {
+        rre[i] = pre; rim[i] = pim;
+        double t = pre * 1 - pim * 1;
+        pim = pre * 1 + pim * 1;
+        pre = t;
+    }
+    for (int iter = 0; iter < 300; ++iter) {
+        double maxDiff = 0;
+        for (int i = 0; i < n; ++i) {
+            pre = rre[i]; pim = rim[i];
+            double nre = cre[n], nim = cim[n], dre = cre[n], dim = cim[n];
+            for (int j = 0; j < n; ++j) {
+                double tre = nre * pre - nim * pim + cre[n - j - 1];
+                double tim = nre * pim + nim * pre + cim[n - j - 1];
+                nre = tre; nim = tim;
+                if (j != i) {
+                    double ere = pre - rre[j], eim = pim - rim[j];
+                    double ure = dre * ere - dim * eim, uim = dre * eim + dim * ere;
+                    dre = ure; dim = uim;
+                }
+            }
+            double t = 1. / (dre * dre + dim * dim);
+            double qre = (nre * dre + nim * dim) * t, qim = (-nre * dim + nim * dre) * t;
+            rre[i] = pre - qre;
+            rim[i] = pim - qim;
+            double a = sqrt(qre * qre + qim * qim);
+            maxDiff = maxDiff > a ? maxDiff : a;
+        }
+        if (maxDiff <= 0) break;
+    }
+    for (; n < 10; ++n) { rre[n] = rre[n - 1]; rim[n] = rim[n - 1]; }
+}
+
+int orc_e_solve5_ref(const double* x1, const double* y1, const double* x2, const double* y2, double* Eout) {
+    double nb[4][9], A[10][20], C[10][10];
+    {
+        double U[81], w[5];
+        memset(U, 0, sizeof(U));
+        for (int i = 0; i < 5; ++i) {
+            double* r = U + 9 * i;
+            r[0] = x1[i] * x2[i]; r[1] = y1[i] * x2[i]; r[2] = x2[i] * 1.0;
+            r[3] = x1[i] * y2[i]; r[4] = y1[i] * y2[i]; r[5] = y2[i] * 1.0;
+            r[6] = x1[i] * 1.0; r[7] = y1[i] * 1.0; r[8] = 1.0;
+        }
+        orc_jsvd(U, w, NULL, 9, 5, 9);
+        for (int b = 0; b < 4; ++b) memcpy(nb[b], U + 9 * (5 + b), sizeof(double) * 9);
+    }
+    constraint_matrix(nb, A);
+    {
+        double L[10][10], P[10][10];
+        for (int r = 0; r < 10; ++r)
+            for (int k = 0; k < 10; ++k) { L[r][k] = A[r][k]; C[r][k] = k == r ? 1.0 : 0.0; }
+        if (!lu_solve10(L, C)) return 0;
+        for (int r = 0; r < 10; ++r)
+            for (int k = 0; k < 10; ++k) {
+                double s = 0;
+                for (int q = 0; q < 10; ++q) s += C[r][q] * A[q][10 + k];
+                P[r][k] = s;
+            }
+        memcpy(C, P, sizeof(P));
+    }
+    double X[3][4], Y[3][4], K[3][5];
+    for (int i = 0; i < 3; ++i) {
+        const double* e = C[4 + 2 * i];
+        const double* f = C[5 + 2 * i];
+        X[i][3] = 0.0 - f[0]; X[i][2] = e[0] - f[1]; X[i][1] = e[1] - f[2]; X[i][0] = e[2] - 0.0;
+        Y[i][3] = 0.0 - f[3]; Y[i][2] = e[3] - f[4]; Y[i][1] = e[4] - f[5]; Y[i][0] = e[5] - 0.0;
+        K[i][4] = 0.0 - f[6]; K[i][3] = e[6] - f[7]; K[i][2] = e[7] - f[8]; K[i][1] = e[8] - f[9];
+        K[i][0] = e[9] - 0.0;
+    }
+    double u[8], v[8], w7[8], P1[11], P2[11], P3[11], a6[7], b6[7], w6[7], det[11];
+    pmul(Y[1], 3, K[2], 4, u); pmul(Y[2], 3, K[1], 4, v);
+    for (int k = 0; k < 8; ++k) w7[k] = u[k] - v[k];
+    pmul(X[0], 3, w7, 7, P1);
+    pmul(X[1], 3, K[2], 4, u); pmul(X[2], 3, K[1], 4, v);
+    for (int k = 0; k < 8; ++k) w7[k] = u[k] - v[k];
+    pmul(Y[0], 3, w7, 7, P2);
+    pmul(X[1], 3, Y[2], 3, a6); pmul(X[2], 3, Y[1], 3, b6);
+    for (int k = 0; k < 7; ++k) w6[k] = a6[k] - b6[k];
+    pmul(K[0], 4, w6, 6, P3);
+    for (int k = 0; k < 11; ++k) det[k] = P1[k] - P2[k] + P3[k];
+    double rre[10], rim[10];
+    orc_solve_poly10(det, rre, rim);
+    int count = 0;
+    for (int i = 0; i < 10; ++i) {
+        if (fabs(rim[i]) > 1e-10) continue;
+        double z1 = rre[i], z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+        double At[9], w[3], Vt[9];
+        for (int j = 0; j < 3; ++j) {
+            At[j] = X[j][3] * z3 + X[j][2] * z2 + X[j][1] * z1 + X[j][0];
+            At[3 + j] = Y[j][3] * z3 + Y[j][2] * z2 + Y[j][1] * z1 + Y[j][0];
+            At[6 + j] = K[j][4] * z4 + K[j][3] * z3 + K[j][2] * z2 + K[j][1] * z1 + K[j][0];
+        }
+        orc_jsvd(At, w, Vt, 3, 3, 3);
+        const double* xy1 = Vt + 6;
+        if (fabs(xy1[2]) < 1e-10) continue;
+        double x = xy1[0] / xy1[2], y = xy1[1] / xy1[2], e[9], ss = 0;
+        for (int k = 0; k < 9; ++k) {
+            e[k] = nb[0][k] * x + nb[1][k] * y + nb[2][k] * z1 + nb[3][k];
+            ss += e[k] * e[k];
+        }
+        double sc = 1. / sqrt(ss);
+        for (int k = 0; k < 9; ++k) Eout[9 * count + k] = e[k] * sc;
+        ++count;
+    }
+    return count;
+}
+
 /* One hypothesis on double4 normalised points. Returns #models, or ORC_NO_SAMPLE. */
 int orc_e_hypothesis(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90, int* idx_out) {
     Stream st;

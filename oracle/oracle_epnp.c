@@ -41,9 +41,9 @@ static double hyp_fma(double x, double y) {
     return h * sc;
 }
 
-/* JacobiSVDImpl_<double>(At, W, Vt, m, n, n1 = n): At is n x m row-major (the transposed
- * matrix); Vt n x n or NULL. */
-static void jsvd(double* At, double* Wout, double* Vt, int m, int n) {
+/* JacobiSVDImpl_<double>(At, W, Vt, m, n, n1): At is n1 x m row-major (the transposed matrix; rows
+ * n .. n1-1 zero on entry, completed by the cv::RNG branch); Vt n x n or NULL. */
+void orc_jsvd(double* At, double* Wout, double* Vt, int m, int n, int n1) {
     const double eps = DBL_EPSILON * 10, minval = DBL_MIN;
     double W[16];
     for (int i = 0; i < n; i++) {
@@ -116,8 +116,8 @@ static void jsvd(double* At, double* Wout, double* Vt, int m, int n) {
     }
     for (int i = 0; i < n; i++) Wout[i] = W[i];
     uint64_t rng = 0x12345678u;
-    for (int i = 0; i < n; i++) {
-        double sd = W[i];
+    for (int i = 0; i < n1; i++) {
+        double sd = i < n ? W[i] : 0;
         for (int ii = 0; ii < 100 && sd <= minval; ii++) {
             double val0 = 1. / m;
             for (int k = 0; k < m; k++) {
@@ -145,6 +145,8 @@ static void jsvd(double* At, double* Wout, double* Vt, int m, int n) {
         for (int k = 0; k < m; k++) At[i * m + k] *= s;
     }
 }
+
+static void jsvd(double* At, double* Wout, double* Vt, int m, int n) { orc_jsvd(At, Wout, Vt, m, n, n); }
 
 /* SVBkSb: rhs b (m) or b == NULL for the inverse (x: n x m). u rows = At rows after jsvd. */
 static void svbksb(const double* U, const double* w, const double* Vt, int m, int n, const double* b, double* x) {

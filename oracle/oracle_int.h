@@ -34,6 +34,7 @@ int orc_pnp_count(const float* pts, int N, const double* cam8, const double* R, 
 void orc_pnp_lm(const float* pts, int N, const uint8_t* mask, const double* cam8, double* rvec, double* t,
                 int maxIters);
 void orc_rodrigues_inv(const double* R, double* r);
+void orc_jsvd(double* At, double* Wout, double* Vt, int m, int n, int n1);
 void orc_epnp(const double* pw, const double* us, int n, const double* cam4, double* R, double* t);
 void orc_epnp5_f32(const float* p5, const double* cam8, double* R, double* t);
 int orc_pnp_hypothesis_epnp(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R,

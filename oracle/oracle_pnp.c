@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
+#include <complex.h>
 #include <float.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -85,9 +86,63 @@ static void cross(const double* a, const double* b, double* r) {
 static double dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 static double nrm(const double* a) { return sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
 
-/* computePoses; Rr/tr as the reference stores them. Returns the count (<= 4). */
+/* solveQuartic (ap3p.cpp:10-59) as libstdc++ evaluates its std::complex<double> expressions on
+ * Linux: C99 complex with glibc's csqrt / clog, pow(complex, double) = polar(exp(y log|w|), y arg w)
+ * (libstdc++'s non-real branch), real / complex through libgcc's __divdc3; then
+ * polishQuarticRoots (ap3p.cpp:61-74). f: descending coefficients a4..a0. */
+static void ferrari_ref(const double* f, double* roots) {
+    double a4 = f[0], a3 = f[1], a2 = f[2], a1 = f[3], a0 = f[4];
+    double a4_2 = a4 * a4, a3_2 = a3 * a3, a4_3 = a4_2 * a4, a2a4 = a2 * a4;
+    double p4 = (8 * a2a4 - 3 * a3_2) / (8 * a4_2);
+    double q4 = (a3_2 * a3 - 4 * a2a4 * a3 + 8 * a1 * a4_2) / (8 * a4_3);
+    double r4 = (256 * a0 * a4_3 - 3 * (a3_2 * a3_2) - 64 * a1 * a3 * a4_2 + 16 * a2a4 * a3_2) / (256 * (a4_3 * a4));
+    double p3 = ((p4 * p4) / 12 + r4) / 3;
+    double q3 = (72 * r4 * p4 - 2 * p4 * p4 * p4 - 27 * q4 * q4) / 432;
+    double t;
+    double complex w;
+    double complex sd = csqrt(CMPLX(q3 * q3 - p3 * p3 * p3, 0.0));
+    if (q3 >= 0)
+        w = -sd - q3;
+    else
+        w = sd - q3;
+    if (cimag(w) == 0.0) {
+        double wr = cbrt(creal(w));
+        t = 2.0 * (wr + p3 / wr);
+    } else {
+        double third = 1.0 / 3;
+        double complex lw = clog(w);
+        t = 4.0 * (exp(third * creal(lw)) * cos(third * cimag(lw)));
+    }
+    double complex sqrt_2m = csqrt(CMPLX(-2 * p4 / 3 + t, 0.0));
+    double B_4A = -a3 / (4 * a4);
+    double complex1 = 4 * p4 / 3 + t;
+    double complex complex2 = CMPLX(2 * q4, 0.0) / sqrt_2m;
+    double sqrt_2m_rh = creal(sqrt_2m) / 2;
+    double sqrt1 = creal(csqrt(-(complex1 + complex2))) / 2;
+    roots[0] = B_4A + sqrt_2m_rh + sqrt1;
+    roots[1] = B_4A + sqrt_2m_rh - sqrt1;
+    double sqrt2 = creal(csqrt(-(complex1 - complex2))) / 2;
+    roots[2] = B_4A - sqrt_2m_rh + sqrt2;
+    roots[3] = B_4A - sqrt_2m_rh - sqrt2;
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double error = (((f[0] * roots[j] + f[1]) * roots[j] + f[2]) * roots[j] + f[3]) * roots[j] + f[4];
+            double derivative = ((4 * f[0] * roots[j] + 3 * f[1]) * roots[j] + 2 * f[2]) * roots[j] + f[3];
+            roots[j] -= error / derivative;
+        }
+}
+
+/* computePoses; Rr/tr as the reference stores them. Returns the count (<= 4).
+ * ref = 0: the RANSAC form (bit-reproducible real roots, non-finite poses dropped);
+ * ref = 1: the reference's own path (ferrari_ref, all four roots in order, nothing filtered). */
+static int ap3p_poses_impl(const double* b, const double* w, double* Rr, double* tr, int ref);
+
 int orc_ap3p_poses(const double* b /*3x3 rows = b1,b2,b3*/, const double* w /*rows = w1,w2,w3*/, double* Rr,
                    double* tr) {
+    return ap3p_poses_impl(b, w, Rr, tr, 0);
+}
+
+static int ap3p_poses_impl(const double* b, const double* w, double* Rr, double* tr, int ref) {
     const double *w1 = w, *w2 = w + 3, *w3 = w + 6, *b1 = b, *b2 = b + 3, *b3 = b + 6;
     double u0[3] = {w1[0] - w2[0], w1[1] - w2[1], w1[2] - w2[2]};
     double nu0 = nrm(u0);
@@ -123,9 +178,16 @@ int orc_ap3p_poses(const double* b /*3x3 rows = b1,b2,b3*/, const double* w /*ro
     c[0] = g7 * g7 - g2 * g2 - g4 * g4;
     int fin = 1;
     for (int k = 0; k < 5; ++k) fin = fin && isfinite(c[k]);
-    if (!fin || !isfinite(delta) || !isfinite(k3b3) || !(nk3 > 0) || !(nu0 > 0) || !(delta > 0)) return 0;
+    if (!ref && (!fin || !isfinite(delta) || !isfinite(k3b3) || !(nk3 > 0) || !(nu0 > 0) || !(delta > 0))) return 0;
     double s[10];
-    int ns = orc_poly_real_roots(c, 4, s);
+    int ns;
+    if (ref) {
+        double f[5] = {c[4], c[3], c[2], c[1], c[0]};
+        ferrari_ref(f, s);
+        ns = 4;
+    } else {
+        ns = orc_poly_real_roots(c, 4, s);
+    }
     double tmp[3];
     cross(k1, nl, tmp);
     double A[9] = {k1[0], nl[0], tmp[0], k1[1], nl[1], tmp[1], k1[2], nl[2], tmp[2]};
@@ -153,7 +215,7 @@ int orc_ap3p_poses(const double* b /*3x3 rows = b1,b2,b3*/, const double* w /*ro
         int ok = isfinite(nt3);
         for (int k = 0; k < 9; ++k) { Rr[9 * n + k] = R[k]; ok = ok && isfinite(R[k]); }
         for (int k = 0; k < 3; ++k) { tr[3 * n + k] = st1 * b3p[k] - rp3[k]; ok = ok && isfinite(tr[3 * n + k]); }
-        if (ok) ++n;
+        if (ok || ref) ++n;
     }
     return n;
 }
@@ -176,7 +238,7 @@ int orc_solve_ap3p(const double* mu, const double* mv, const double* W9, double 
         b[3 * i + 1] = v * mk;
         b[3 * i + 2] = mk;
     }
-    return orc_ap3p_poses(b, W9, Rs, ts);
+    return ap3p_poses_impl(b, W9, Rs, ts, 1);
 }
 
 /* AP3P on 3 points + the 4th picks (pixel error, first minimum); camera-from-world pose out. */

@@ -30,6 +30,8 @@ _SIGS = {
     "orc_find_fundamental": (_I, [_P, _P, _I, _D, _D, _I, _I, _U64, _I, _I, _P, _P, _P, _I]),
     "orc_poly_real_roots": (_I, [_P, _I, _P]),
     "orc_e_solve5": (_I, [_P, _P, _P, _P, _P]),
+    "orc_e_solve5_ref": (_I, [_P, _P, _P, _P, _P]),
+    "orc_solve_poly10": (None, [_P, _P, _P]),
     "orc_e_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "orc_e_count": (_I, [_P, _I, _P, _F, _I, _P]),
     "orc_e_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _I, _P, _I]),
@@ -212,6 +214,22 @@ def e_solve5(x1, y1, x2, y2):
     E = np.zeros(90)
     n = load().orc_e_solve5(*[ptr(v) for v in arrs], ptr(E))
     return E.reshape(10, 3, 3)[:max(n, 0)]
+
+
+def e_solve5_ref(x1, y1, x2, y2):
+    """cvFivePoint's own path (JacobiSVD null space, LU, solvePoly, solveZ)."""
+    arrs = [np.ascontiguousarray(v, dtype=np.float64) for v in (x1, y1, x2, y2)]
+    E = np.zeros(90)
+    n = load().orc_e_solve5_ref(*[ptr(v) for v in arrs], ptr(E))
+    return E.reshape(10, 3, 3)[:max(n, 0)]
+
+
+def solve_poly10(c):
+    """cv::solvePoly(c ascending, 300 iterations) -> complex roots in its order."""
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    re, im = np.zeros(10), np.zeros(10)
+    load().orc_solve_poly10(ptr(c), ptr(re), ptr(im))
+    return re + 1j * im
 
 
 def e_hypothesis(pts4d, seed, hyp):

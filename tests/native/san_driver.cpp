@@ -35,6 +35,7 @@ int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const 
                            double* tvec, uint8_t* mask, int64_t* bestOut, int nthreads);
 int orc_solve_pnp(const double* img, const double* world, int N, const double* K9, const double* dist4, int kind,
                   double* rvec, double* tvec);
+int orc_e_solve5_ref(const double* x1, const double* y1, const double* x2, const double* y2, double* Eout);
 int orc_find_homography(const double* src, const double* dst, int N, double thr, double conf, int maxIters, int method,
                         uint64_t seed, int flags, double* H, uint8_t* mask, int64_t* bestHypOut, int nthreads);
 int orc_find_fundamental(const double* a, const double* b, int N, double thr, double conf, int maxIters, int method,
@@ -121,6 +122,18 @@ int main() {
             const int n2 = orc_e_hypothesis(pts.data(), N, 11, h, E2, i2);
             expect(n1 == n2, "e count", n1, n2);
             if (n1 > 0 && n1 == n2) expect(same_bits(&E1[0][0], E2, 9 * n1), "e models", h, N);
+            if (h < 6) {   // the cvFivePoint export path on the first five points
+                double x1[5], y1[5], x2[5], y2[5];
+                for (int i = 0; i < 5; ++i) {
+                    x1[i] = pts[4 * i]; y1[i] = pts[4 * i + 1]; x2[i] = pts[4 * i + 2]; y2[i] = pts[4 * i + 3];
+                }
+                std::memset(E1, 0, sizeof(E1));
+                std::memset(E2, 0, sizeof(E2));
+                const int r1 = mcv::e_solve5_ref(x1, y1, x2, y2, E1);
+                const int r2 = orc_e_solve5_ref(x1, y1, x2, y2, E2);
+                expect(r1 == r2, "e ref count", r1, r2);
+                if (r1 > 0 && r1 == r2) expect(same_bits(&E1[0][0], E2, 9 * r1), "e ref models", h, N);
+            }
         }
     }
 

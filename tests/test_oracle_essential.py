@@ -197,3 +197,59 @@ def test_host_real_roots_fixed_form_bit_exact(native, oracle):
         gen = _host_roots(native, c, False)
         np.testing.assert_array_equal(fx, gen)
         np.testing.assert_array_equal(fx, oracle.poly_real_roots(c))
+
+
+# ---- cvFivePoint's own path (fivepoint.cpp:233-339; oracle orc_e_solve5_ref) ---------------------
+def test_solve_poly_durand_kerner(oracle):
+    """cv::solvePoly restated (Durand-Kerner, 300 sweeps): the root set of random degree-10
+    polynomials equals numpy's companion-matrix roots; real roots come out with |Im| ~ 0."""
+    rng = np.random.default_rng(3)
+    for _ in range(100):
+        real = np.sort(rng.uniform(-3, 3, size=rng.integers(0, 6) * 2))
+        cplx = rng.normal(size=(5 - len(real) // 2)) + 1j * rng.uniform(0.2, 2, size=5 - len(real) // 2)
+        rts = np.concatenate([real, cplx, cplx.conj()])
+        c = np.real(np.poly(rts))[::-1] * rng.uniform(0.5, 2)          # ascending coefficients
+        got = oracle.solve_poly10(c)
+        for r in rts:
+            assert np.min(np.abs(got - r)) < 1e-7 * max(1, abs(r))
+        assert (np.abs(got.imag[np.abs(got.imag) < 1e-6]) <= 1e-10).all()
+
+
+def test_five_point_ref_recovers_true_essential(oracle):
+    """The export path finds the true E for exact poses and agrees with the RANSAC solver's model set
+    (same count, same E up to sign: median ~1e-14, 95% within 1e-9, all within 1e-4 — the Nister
+    formulation is ill-conditioned for a few configurations); every solution has unit norm."""
+    worst, extra, devs = 0.0, 0, []
+    for seed in range(200):
+        rng = np.random.default_rng(1000 + seed)
+        R = S.rotation(rng.normal(size=3), rng.uniform(0.02, 0.5))
+        t = rng.normal(size=3)
+        a, b, _, R, tu, E = S.essential_problem(5, seed=seed, outlier_frac=0, sigma=0, R=R, t=t + [0, 0, 0.3])
+        p = oracle.pack_e(a, b, FOCAL, PP)
+        Er = oracle.e_solve5_ref(p[:, 0], p[:, 1], p[:, 2], p[:, 3])
+        Es = oracle.e_solve5(p[:, 0], p[:, 1], p[:, 2], p[:, 3])
+        assert 1 <= len(Er) <= 10
+        worst = max(worst, min(min(np.abs(e - E).max(), np.abs(e + E).max()) for e in Er))
+        for e in Er:
+            np.testing.assert_allclose(np.linalg.norm(e), 1.0, atol=1e-12)
+        assert len(Er) == len(Es)
+        for e in Es:   # every RANSAC-path model is among the export's (up to sign)
+            devs.append(min(min(np.abs(e - f).max(), np.abs(e + f).max()) for f in Er))
+    assert worst < 1e-4 and max(devs) < 1e-4 and np.quantile(devs, 0.95) < 1e-9
+
+
+def test_host_five_point_ref_bit_exact(native, oracle):
+    rng = np.random.default_rng(8)
+    L = native.lib()
+    for trial in range(150):
+        if trial % 3 == 0:
+            p = rng.normal(size=(5, 4))
+        else:
+            a, b, *_ = S.essential_problem(5, seed=trial, outlier_frac=0, sigma=0.5)
+            p = oracle.pack_e(a, b, FOCAL, PP)
+        p20 = np.ascontiguousarray(np.concatenate([p[:, 0], p[:, 1], p[:, 2], p[:, 3]]))
+        E90 = np.zeros(90)
+        n = L.mcvHostFivePointRef(p20.ctypes.data, E90.ctypes.data)
+        Es = oracle.e_solve5_ref(p[:, 0], p[:, 1], p[:, 2], p[:, 3])
+        assert n == len(Es)
+        np.testing.assert_array_equal(E90.reshape(10, 3, 3)[:n], Es)

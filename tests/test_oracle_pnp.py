@@ -204,3 +204,39 @@ def test_solve_pnp_all_points(oracle, kind):
     ok, r, tt = oracle.solve_pnp(img, W, K, d, kind=kind)
     Rr, _ = oracle.rodrigues(r)
     assert ok and np.abs(Rr - R).max() < 1e-6 and np.abs(tt - t).max() < 1e-5
+
+
+def _ap3p_triples(count, seed):
+    """Random 3-point problems: pixel observations of a random pose, a few of them perturbed so that
+    the quartic has complex roots (whose real parts the reference keeps) or nearly double roots."""
+    rng = np.random.default_rng(seed)
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    for c in range(count):
+        R, t = _pose(rng)
+        W = rng.uniform(-3, 3, size=(3, 3))
+        us = _project_px(W, K, R, t)
+        if c % 3 == 1:
+            us = us + rng.normal(scale=20.0, size=us.shape)
+        yield us, W, K
+
+
+def test_solve_ap3p_reference_quartic_path(native, oracle):
+    """solveAp3p's own quartic path (Ferrari with std::complex + 2 polish passes, ap3p.cpp:10-74): the
+    host build of the product code against the oracle's glibc / C99-complex restatement on 1000 random
+    triples — same solution count and order, values within 1e-9 (the transcendentals are libm's on
+    both sides here; the GPU test holds the device to the same bar)."""
+    L = native.lib()
+    spurious = 0
+    for us, W, K in _ap3p_triples(1000, 5):
+        inv_fx, inv_fy = 1 / K[0, 0], 1 / K[1, 1]
+        args = (np.ascontiguousarray(us[:, 0]), np.ascontiguousarray(us[:, 1]), np.ascontiguousarray(W.ravel()))
+        R36, t12 = np.zeros(36), np.zeros(12)
+        n = L.mcvHostSolveAp3p(*(a.ctypes.data for a in args), inv_fx, inv_fy, K[0, 2] * inv_fx, K[1, 2] * inv_fy,
+                               R36.ctypes.data, t12.ctypes.data)
+        ref = oracle.solve_ap3p(us[:, 0], us[:, 1], W, inv_fx, inv_fy, K[0, 2] * inv_fx, K[1, 2] * inv_fy)
+        assert n == len(ref)
+        for i, (Ro, to) in enumerate(ref):
+            np.testing.assert_allclose(R36[9 * i:9 * i + 9], Ro.ravel(), rtol=0, atol=1e-9)
+            np.testing.assert_allclose(t12[3 * i:3 * i + 3], to, rtol=1e-9, atol=1e-9)
+        spurious += n - sum(np.abs(np.linalg.det(Ro) - 1) < 1e-6 for Ro, _ in ref)
+    assert spurious >= 0
