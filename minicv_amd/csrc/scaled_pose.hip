@@ -2,11 +2,11 @@
 //
 //   mcv_scaled_pack        AoS V3d world points + V2d observations -> SoA fp64 (5 coalesced streams)
 //   mcv_scaled_candidates  lane per observation: the two candidate scales (or "skipped")
-//   mcv_scaled_costs<K>    the O(N^2) verify: a wave owns K candidate scales (their dstCam(s)
-//                          locations are wave-uniform: SGPRs), its 64 lanes stream all N observations,
-//                          project them (Camera.project1) and accumulate sum |c - obs|^2 and the
-//                          visible count in fp64; a fixed-order wave tree gives each candidate's
-//                          avgReprojectionError (+inf when nothing is visible).
+//   mcv_scaled_costs       the O(N^2) verify: a workgroup owns 64 candidate scales; 4 waves project
+//                          double-buffered LDS tiles of observations (Camera.project1) for all of
+//                          them while a fifth wave adds the previous tile's terms to each candidate's
+//                          running fp64 sum in list order, as the managed loop does:
+//                          avgReprojectionError bit for bit (+inf when nothing is visible).
 //   mcv_scaled_best        first strictly smaller cost in candidate order: min of (cost bits,
 //                          index) over the finite costs (costs are >= 0, so their bit patterns
 //                          order like the values), plus the evaluated-candidate count.
@@ -43,68 +43,76 @@ __global__ __launch_bounds__(256) void mcv_scaled_candidates(ScaledSetup S, cons
     used[i] = ok ? 1 : 0;
 }
 
-__device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-__device__ __forceinline__ int wave_sum_i32(int v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
+// A workgroup owns kScaledCands candidate scales and streams the N observations in tiles of
+// kScaledTile. Compute waves 0..7 (lane l = candidate l, its dstCam(s) location in VGPRs) each project
+// a contiguous eighth of tile t (observations broadcast from LDS, staged by wave 8) for all the group's
+// candidates and park the terms in LDS buffer t % 2 (an invisible observation parks -0.0: adding
+// it leaves any running sum unchanged, and a visible term d = dx^2 + dy^2 is never -0.0). Wave 8
+// meanwhile adds tile t - 1's terms to each candidate's running fp64 sum in list order —
+// avgReprojectionError's `sum <- sum + d` loop (CameraPose.fs:83-91) bit for bit — and counts the
+// visible ones; one barrier per tile hands the buffers over.
+static const int kScaledCands = 64;
+static const int kScaledTile = 32;
+static const int kScaledComputeWaves = 8;
+static const int kScaledThreads = (kScaledComputeWaves + 1) * 64;
 
-template <int K>
-__global__ __launch_bounds__(256) void mcv_scaled_costs(ScaledSetup S, const double* __restrict__ soa, int N,
-                                                        const double* __restrict__ scales,
-                                                        const uint8_t* __restrict__ used, int nCand,
-                                                        double* __restrict__ costs) {
-    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+__global__ __launch_bounds__(kScaledThreads) void mcv_scaled_costs(ScaledSetup S, const double* __restrict__ soa,
+                                                                   int N, const double* __restrict__ scales,
+                                                                   const uint8_t* __restrict__ used, int nCand,
+                                                                   double* __restrict__ costs) {
+    __shared__ double terms[2][kScaledTile][kScaledCands];
+    __shared__ double obs[2][5][kScaledTile];
     const int lane = threadIdx.x & 63;
-    const int c0 = wave * K;
-    if (c0 >= nCand) return;
-    double loc[K][3];
-    bool live = false;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int c = blockIdx.x * kScaledCands + lane;
+    const int cc = c < nCand ? c : nCand - 1;
+    double loc[3];
+    scaled_location(S, scales[cc], loc);
+    const int per = kScaledTile / kScaledComputeWaves;   // observations per compute wave and tile
+    const int sw = kScaledComputeWaves;                   // the staging / summing wave
+    const int ntiles = (N + kScaledTile - 1) / kScaledTile;
+    // the summing wave stages tile t's observations (5 SoA streams) into obs[t % 2]; past N: the last one
+    auto stage = [&](int t) {
+        if (lane < kScaledTile) {
+            const int j0 = t * kScaledTile + lane;
+            const int j = j0 < N ? j0 : N - 1;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int c = c0 + k < nCand ? c0 + k : c0;
-        scaled_location(S, scales[c], loc[k]);
-        live = live || (c0 + k < nCand && used[(c0 + k) >> 1]);
-    }
-    if (!live) {   // every candidate of this wave was skipped by the reference loop
-        if (lane < K && c0 + lane < nCand) costs[c0 + lane] = __builtin_inf();
-        return;
-    }
-    double sum[K];
-    int cnt[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        sum[k] = 0.0;
-        cnt[k] = 0;
-    }
-    const double* wx = soa;
-    const double* wy = soa + N;
-    const double* wz = soa + 2 * (size_t)N;
-    const double* ox = soa + 3 * (size_t)N;
-    const double* oy = soa + 4 * (size_t)N;
-    for (int i = lane; i < N; i += 64) {
-        const double x = wx[i], y = wy[i], z = wz[i], u = ox[i], v = oy[i];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            double e;
-            const bool vis = scaled_term(S, loc[k], x, y, z, u, v, e);
-            sum[k] += vis ? e : 0.0;   // select, not a branch (an invisible e may be NaN / inf)
-            cnt[k] += vis ? 1 : 0;
+            for (int q = 0; q < 5; ++q) obs[t & 1][q][lane] = soa[(size_t)q * N + j];
         }
+    };
+    if (wv == sw) stage(0);
+    __syncthreads();
+    double sum = 0.0;
+    int cnt = 0;
+    for (int t = 0; t <= ntiles; ++t) {
+        if (wv < sw && t < ntiles) {
+            double (*buf)[kScaledCands] = terms[t & 1];
+            const double (*o)[kScaledTile] = obs[t & 1];
+            const int r0 = wv * per;
+            const int j0 = t * kScaledTile + r0;
+#pragma unroll 4
+            for (int k = 0; k < per; ++k) {
+                double e;
+                const bool vis = scaled_term(S, loc, o[0][r0 + k], o[1][r0 + k], o[2][r0 + k], o[3][r0 + k],
+                                             o[4][r0 + k], e);
+                buf[r0 + k][lane] = (vis && j0 + k < N) ? e : -0.0;
+            }
+        }
+        if (wv == sw) {
+            if (t + 1 < ntiles) stage(t + 1);
+            if (t > 0) {
+                const double (*buf)[kScaledCands] = terms[(t - 1) & 1];
+#pragma unroll 8
+                for (int k = 0; k < kScaledTile; ++k) {
+                    const double d = buf[k][lane];
+                    sum = sum + d;
+                    cnt += __double_as_longlong(d) != (long long)0x8000000000000000ull ? 1 : 0;
+                }
+            }
+        }
+        __syncthreads();
     }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double s = wave_sum_f64(sum[k]);
-        const int n = wave_sum_i32(cnt[k]);
-        const int c = c0 + k;
-        if (lane == 0 && c < nCand)
-            costs[c] = (!used[c >> 1] || n == 0) ? __builtin_inf() : s / (double)n;
-    }
+    if (wv == sw && c < nCand) costs[c] = (!used[c >> 1] || cnt == 0) ? __builtin_inf() : sum / (double)cnt;
 }
 
 // out[0] = best candidate index (-1: none), out[1] = number of evaluated candidates.
@@ -155,19 +163,16 @@ __global__ __launch_bounds__(1024) void mcv_scaled_best(const double* __restrict
     }
 }
 
-static const int kScaledPerWave = 8;
-
 void launch_scaled(const ScaledSetup& S, const double* d_w3, const double* d_o2, int N, double* d_soa,
                    double* d_scales, uint8_t* d_used, double* d_costs, long long* d_out, hipStream_t s) {
     const int nCand = 2 * N;
     hipLaunchKernelGGL(mcv_scaled_pack, dim3((N + 255) / 256), dim3(256), 0, s, d_w3, d_o2, N, d_soa);
     hipLaunchKernelGGL(mcv_scaled_candidates, dim3((N + 255) / 256), dim3(256), 0, s, S, d_soa, N, d_scales,
                        d_used);
-    const int waves = (nCand + kScaledPerWave - 1) / kScaledPerWave;
     {
         ProfScope ps("scaled_costs", s);
-        hipLaunchKernelGGL((mcv_scaled_costs<kScaledPerWave>), dim3((waves + 3) / 4), dim3(256), 0, s, S, d_soa, N,
-                           d_scales, d_used, nCand, d_costs);
+        hipLaunchKernelGGL(mcv_scaled_costs, dim3((nCand + kScaledCands - 1) / kScaledCands), dim3(kScaledThreads),
+                           0, s, S, d_soa, N, d_scales, d_used, nCand, d_costs);
     }
     hipLaunchKernelGGL(mcv_scaled_best, dim3(1), dim3(1024), 0, s, d_costs, d_used, nCand, d_out);
 }
