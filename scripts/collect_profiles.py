@@ -21,8 +21,9 @@ OUT = ROOT / "gpurun_out"
 PROF = ROOT / "profiles"
 WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2", "scaled"]
 # dominant kernel per BASELINE workload (substring of the demangled rocprofv3 kernel name)
-KERNELS = {"homography": "mcv_h_verify_pk", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
+KERNELS = {"homography": "mcv_h_verify_cert", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
            "l2": "mcv_l2_mfma", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify"}
+EXTRA_BENCH = ["homography_fused", "pnp_ap3p"]   # second bench lines (bench_<name>.log)
 
 
 def last_json(path: Path):
@@ -50,7 +51,7 @@ def pmc_sums(path: Path, kernel_prefix: str):
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
     (PROF / rnd).mkdir(parents=True, exist_ok=True)
-    for w in WORKLOADS:
+    for w in WORKLOADS + EXTRA_BENCH:
         log = OUT / f"bench_{w}.log"
         if log.exists() and (j := last_json(log)):
             (PROF / f"{rnd}_bench_{w}.json").write_text(json.dumps(j) + "\n")
@@ -101,8 +102,8 @@ def main():
     if sq_src.exists():
         shutil.copy(sq_src, PROF / rnd / "pmc_sq_homography.csv")
         sq = {k: mean(v) for k, v in sorted(pmc_sums(sq_src, KERNELS["homography"]).items())}
-        if "mcv_h_verify_pk" in traffic:
-            t = traffic["mcv_h_verify_pk"]
+        if KERNELS["homography"] in traffic:
+            t = traffic[KERNELS["homography"]]
             d = {"sq": sq}
             hb = last_json(PROF / f"{rnd}_bench_homography.json")
             if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_INSTS_VALU") and hb:
