@@ -150,6 +150,11 @@ MCV_API mcvBool cvDetectArucoMarkers(char* data, int width, int height, int chan
                                      OpenCV's computeError produces, e.g. clang on arm64). Default:
                                      op-by-op, every operation rounded as written = OpenCV's x86-64
                                      (SSE baseline) build, the reference's Linux/AMD64 target. */
+#define MCV_FLAG_SEVEN_POINT  8   /* fundamental only: OpenCV FM_RANSAC's minimal solver (run7Point: 7-point
+                                     samples, up to 3 models each, model slots 3h .. 3h+2 in the device
+                                     API) instead of the 8-point default; with errorKind EPIPOLAR it is
+                                     cv::findFundamentalMat(FM_RANSAC). Needs N >= 15 (OpenCV switches to
+                                     LMeDS below that, not provided) or N == 7 (one solve, first model). */
 
 /* F error metric (cfg->errorKind, fundamental only) */
 #define MCV_FERR_SAMPSON   0   /* first-order geometric (Sampson) distance^2 (north_star) */
@@ -382,6 +387,9 @@ MCV_API int mcvHostEssential(const double* pts4, int N, uint64_t seed, int64_t h
 MCV_API int mcvHostFivePoint(const double* p20, double* E90);
 /* Host build of the cvFivePoint export's own path (e_solve5_ref), same packing as mcvHostFivePoint. */
 MCV_API int mcvHostFivePointRef(const double* p20, double* E90);
+/* Host twin of one 7-point fundamental hypothesis (MCV_FLAG_SEVEN_POINT): F27 = up to 3 models,
+ * idx7 = the accepted sample (may be NULL). Returns the model count or the kStatus code. */
+MCV_API int mcvHostF7(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F27, int* idx7);
 MCV_API void mcvHostDecomposeEssential(const double* E9, double* R1, double* R2, double* t3);
 /* Host twin of the real-root finder (Rolle brackets + Illinois) of sum c[k] x^k, deg <= 10;
  * fixed = 1 (deg == 4 only) runs the register-resident fixed-size form the AP3P quartic uses.

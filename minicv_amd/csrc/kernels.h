@@ -59,6 +59,11 @@ struct FOneOut {
 void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
                        int* d_counts, hipStream_t s);
 void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s);
+// 7-point (MCV_FLAG_SEVEN_POINT): 3 model slots per hypothesis (models[3h + s], counts[3h + s]).
+void launch_f7_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+                        int* d_counts, hipStream_t s);
+void launch_f7_one(const float* d_pts4, int N, uint64_t seed, int64_t slot, FOneOut* d_out, hipStream_t s);
+void launch_f7_direct(const float* d_pts4, FOneOut* d_out, hipStream_t s);   // N == 7: run7Point, first model
 void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
                      int kind, hipStream_t s, const double* d_bb = nullptr);
 // max |x1|, |y1|, |x2|, |y2| of float4 (fp64 = false) or double4 points -> d_bb[4] (fp64); with

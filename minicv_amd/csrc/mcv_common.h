@@ -97,6 +97,7 @@ static const int kMaxRedraw = 1000;
 static const int kStatusNoModel = -1;   // minimal solver degenerate -> OpenCV `continue`
 static const int kStatusNoSample = -2;  // sampler exhausted attempts -> OpenCV `break`
 static const int kStatusRedo = -3;      // packed H sweep: count this slot again with the exact sweep
+static const int kF7Slots = 3;          // 7-point fundamental (run7Point): model slots per hypothesis
 
 static const double kDblEpsilon = 2.2204460492503131e-16;
 static const float kFltEpsilon = 1.19209290e-07f;

@@ -13,7 +13,8 @@ static const int64_t kChunkMax = 1 << 20;
 
 size_t model_bytes(int model);   // device model bytes per hypothesis
 int model_points(int model);
-int model_points_cfg(int model, const RansacConfig& cfg);   // PnP: 5 with the EPnP kernel
+int model_points_cfg(int model, const RansacConfig& cfg);   // PnP: 5 with the EPnP kernel; F 7-point: 7
+int model_slots_cfg(int model, const RansacConfig& cfg);    // F 7-point: 3 model slots per hypothesis
 int model_slots(int model);      // model slots per hypothesis (essential: 10)
 
 struct Plan {

@@ -2,6 +2,8 @@
 //
 //   mcv_f_generate      one lane per hypothesis: Philox sample of 8 -> collinearity check ->
 //                       8-point solve + rank 2 (fp64) -> FModelD (72 B) + status.
+//   mcv_f7_generate     MCV_FLAG_SEVEN_POINT: lane per hypothesis, 7-point sample -> run7Point (JacobiSVD
+//                       null space, cubic) -> up to 3 FModelD slots + per-slot status.
 //   mcv_f_verify<K, E>  inlier sweep: wave = K hypotheses (fp64 models in VGPRs), 64 lanes stream
 //                       the packed float4 correspondences; per (hypothesis, point) the fp64
 //                       Sampson / epipolar error E, cast to float, ballot + s_bcnt1 count.
@@ -12,6 +14,7 @@
 //   OpFAtA              fixed-order fp64 reduction of A^T A (run8Point over all points).
 #include "mcv_common.h"
 #include "hyp_fundamental.h"
+#include "hyp_f7.h"
 #include "sampson_pk.h"
 #include "reduce.h"
 #include "kernels.h"
@@ -234,6 +237,68 @@ struct OpFAtA {   // 45: upper triangle of A^T A, rows (X2X1, X2Y1, X2, Y2X1, Y2
             for (int k = j; k < 9; ++k) a[o++] += r[j] * r[k];
     }
 };
+
+__global__ __launch_bounds__(64) void mcv_f7_generate(const float* __restrict__ pts4, int N, uint64_t seed,
+                                                      int64_t hypBegin, int hypCount, FModelD* __restrict__ models,
+                                                      int* __restrict__ counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hypCount) return;
+    double F[kF7Slots][9];
+    const int st = f7_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), F, nullptr);
+    for (int s = 0; s < kF7Slots; ++s) {
+        if (st > s) {
+            FModelD m;
+            for (int j = 0; j < 9; ++j) m.f[j] = F[s][j];
+            models[kF7Slots * (size_t)i + s] = m;
+            counts[kF7Slots * (size_t)i + s] = 0;
+        } else {
+            counts[kF7Slots * (size_t)i + s] = (s == 0 && st == kStatusNoSample) ? kStatusNoSample : kStatusNoModel;
+        }
+    }
+}
+
+__global__ void mcv_f7_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t slot,
+                           FOneOut* __restrict__ out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    double F[kF7Slots][9];
+    int idx[7] = {-1, -1, -1, -1, -1, -1, -1};
+    const int s = (int)(slot % kF7Slots);
+    const int st = f7_hypothesis(pts4, N, seed, (uint64_t)(slot / kF7Slots), F, idx);
+    FOneOut o;
+    o.status = st > s ? 1 : (st < 0 ? st : kStatusNoModel);
+    for (int j = 0; j < 9; ++j) o.F[j] = st > s ? F[s][j] : 0.0;
+    for (int j = 0; j < 8; ++j) o.idx[j] = j < 7 ? idx[j] : -1;
+    *out = o;
+}
+
+__global__ void mcv_f7_direct(const float* __restrict__ pts4, FOneOut* __restrict__ out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    float x1[7], y1[7], x2[7], y2[7];
+    for (int i = 0; i < 7; ++i) {
+        x1[i] = pts4[4 * i]; y1[i] = pts4[4 * i + 1]; x2[i] = pts4[4 * i + 2]; y2[i] = pts4[4 * i + 3];
+    }
+    double F[kF7Slots][9];
+    const int n = f_solve7(x1, y1, x2, y2, F);
+    FOneOut o;
+    o.status = n > 0 ? n : kStatusNoModel;
+    for (int j = 0; j < 9; ++j) o.F[j] = n > 0 ? F[0][j] : 0.0;
+    for (int j = 0; j < 8; ++j) o.idx[j] = j < 7 ? j : -1;
+    *out = o;
+}
+
+void launch_f7_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+                        int* d_counts, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_f7_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+                       hypCount, (FModelD*)d_models, d_counts);
+}
+
+void launch_f7_one(const float* d_pts4, int N, uint64_t seed, int64_t slot, FOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_f7_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, slot, d_out);
+}
+
+void launch_f7_direct(const float* d_pts4, FOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_f7_direct, dim3(1), dim3(64), 0, s, d_pts4, d_out);
+}
 
 void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
                        int* d_counts, hipStream_t s) {

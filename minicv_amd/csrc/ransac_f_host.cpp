@@ -7,6 +7,7 @@
 #include "kernels.h"
 #include "linalg.h"
 #include "hyp_fundamental.h"
+#include "hyp_f7.h"
 #include "plan.h"
 
 #include <cmath>
@@ -25,7 +26,8 @@ int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     const double t = effective_threshold(cfg);
     const float thr2 = (float)(t * t);
     FOneOut* d_one = (FOneOut*)P.one.p;
-    launch_f_one(d_pts, N, cfg.seed, hyp, d_one, s);
+    if (cfg.flags & MCV_FLAG_SEVEN_POINT) launch_f7_one(d_pts, N, cfg.seed, hyp, d_one, s);   // hyp = model slot
+    else launch_f_one(d_pts, N, cfg.seed, hyp, d_one, s);
     MCV_HIP(hipGetLastError());
     FOneOut one;
     MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(FOneOut), hipMemcpyDeviceToHost, s));
@@ -76,3 +78,19 @@ int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, doub
 }
 
 }  // namespace mcv
+
+using namespace mcv;
+
+// Host build of one 7-point hypothesis (f7_hypothesis): F27 = up to 3 models, idx7 = the sample.
+extern "C" MCV_API int mcvHostF7(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F27, int* idx7) {
+    MCV_GUARD(kStatusNoSample - 1, {
+        if (!pts4 || !F27 || N < 7) fail("mcvHostF7: bad argument");
+        double F[kF7Slots][9];
+        for (int s = 0; s < kF7Slots; ++s)
+            for (int k = 0; k < 9; ++k) F[s][k] = 0.0;
+        const int n = f7_hypothesis(pts4, N, seed, (uint64_t)hyp, F, idx7);
+        for (int s = 0; s < kF7Slots; ++s)
+            for (int k = 0; k < 9; ++k) F27[9 * s + k] = F[s][k];
+        return n;
+    })
+}

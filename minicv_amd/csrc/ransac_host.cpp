@@ -133,6 +133,10 @@ size_t model_bytes(int model) {
     return model == MCV_MODEL_ESSENTIAL ? 72 * kEModelSlots : (model == MCV_MODEL_FUNDAMENTAL ? 80 : 32);
 }
 int model_slots(int model) { return model == MCV_MODEL_ESSENTIAL ? kEModelSlots : 1; }
+static bool f_seven(int model, const RansacConfig& cfg) {
+    return model == MCV_MODEL_FUNDAMENTAL && (cfg.flags & MCV_FLAG_SEVEN_POINT) != 0;
+}
+int model_slots_cfg(int model, const RansacConfig& cfg) { return f_seven(model, cfg) ? kF7Slots : model_slots(model); }
 
 hipStream_t Plan::own_stream() {
     if (!stream) MCV_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -343,6 +347,19 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         } else if (!launch_h_verify_packed(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bbox.p, s)) {
             launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, true, P.bbox.p, s);
         }
+    } else if (f_seven(P.model, cfg)) {
+        // OpenCV FM_RANSAC: 7-point samples, 3 model slots per hypothesis (slot keys like essential)
+        launch_f7_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+        P.bb4.ensure(4);
+        launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
+        {
+            ProfScope ps("f_verify", s);
+            launch_f_verify(d_pts, N, P.models.p, d_counts, hypCount * kF7Slots, thr2, f_error_kind(cfg), s, P.bb4.p);
+        }
+        if (d_key)
+            launch_best(d_counts, hypCount * kF7Slots, hypBegin * kF7Slots, 7, P.pkey.p, P.pfail.p, d_key, s);
+        MCV_HIP(hipGetLastError());
+        return;
     } else {
         launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
         P.bb4.ensure(4);
@@ -357,6 +374,7 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
 int model_points(int model) { return model == MCV_MODEL_FUNDAMENTAL ? 8 : (model == MCV_MODEL_ESSENTIAL ? 5 : 4); }
 // (homography and PnP with the AP3P kernel: 4)
 int model_points_cfg(int model, const RansacConfig& cfg) {
+    if (f_seven(model, cfg)) return 7;
     return model == MCV_MODEL_PNP && pnp_cfg_epnp(cfg) ? 5 : model_points(model);
 }
 
@@ -405,7 +423,10 @@ int finalize(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg, int64_
 // answer is identical to one device. Returns the best hypothesis (slot) index or -1.
 int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s) {
     const int m = model_points_cfg(P.model, cfg);
-    const int slots = model_slots(P.model);
+    const int slots = model_slots_cfg(P.model, cfg);
+    // plans size their slot buffers by model_slots(model): a mode with more slots per hypothesis
+    // (7-point F) reserves that many times the hypotheses
+    const int64_t slotScale = slots / model_slots(P.model);
     mcvReplayState st;
     mcvReplayInit(&st, cfg.maxIters);
     const bool fixed = (cfg.flags & MCV_FLAG_FIXED_ITERS) != 0;
@@ -430,7 +451,7 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
             const int dev = (home + k) % ndev;
             MCV_HIP(hipSetDevice(dev));
             Plan& Pk = thread_plan(P.model, k);
-            Pk.reserve(N, 1);
+            Pk.reserve(N, slotScale);
             std::memcpy(Pk.pnpCam, P.pnpCam, sizeof(P.pnpCam));
             void* dst = plan_points(Pk, N, &bytes);
             hipStream_t sk = Pk.own_stream();
@@ -445,7 +466,7 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
         const int64_t remaining = st.niters - begin;
         if (remaining <= 0) break;
         const int cnt = (int)std::min<int64_t>(remaining, chunk);
-        P.reserve(N, cnt);
+        P.reserve(N, cnt * slotScale);
         const int nsh = std::min<int>((int)sh.size(), cnt);
         int64_t off = 0;
         for (int k = 0; k < nsh; ++k) {
@@ -453,7 +474,7 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
             Shard& x = sh[k];
             if (k > 0) {
                 MCV_HIP(hipSetDevice(x.dev));
-                x.P->reserve(N, ck);
+                x.P->reserve(N, ck * slotScale);
             }
             evaluate_chunk(*x.P, x.pts, N, cfg, begin + off, ck, x.P->counts.p, nullptr, x.s);
             MCV_HIP(hipMemcpyAsync(P.h_counts.p + off * slots, x.P->counts.p, (size_t)ck * slots * sizeof(int),
@@ -570,9 +591,11 @@ extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const void* d_pts4
         Plan* P = reinterpret_cast<Plan*>(plan);
         if (!P || !d_pts4 || !cfg || !d_key) fail("mcvRansacEvaluate: null argument");
         if (N < model_points_cfg(P->model, *cfg)) fail("mcvRansacEvaluate: N=%d below the minimal sample", N);
-        if (hypCount <= 0 || hypCount > P->maxHyps) fail("mcvRansacEvaluate: hypCount %lld outside plan capacity %lld",
-                                                         (long long)hypCount, (long long)P->maxHyps);
-        if (hypBegin < 0 || (hypBegin + hypCount) * model_slots(P->model) > 0xFFFFFFFFll)
+        const int64_t scale = model_slots_cfg(P->model, *cfg) / model_slots(P->model);
+        if (hypCount <= 0 || hypCount * scale > P->maxHyps)
+            fail("mcvRansacEvaluate: hypCount %lld (x%lld slots) outside plan capacity %lld", (long long)hypCount,
+                 (long long)scale, (long long)P->maxHyps);
+        if (hypBegin < 0 || (hypBegin + hypCount) * model_slots_cfg(P->model, *cfg) > 0xFFFFFFFFll)
             fail("mcvRansacEvaluate: hypothesis (slot) index beyond 2^32");
         evaluate_chunk(*P, d_pts4, N, *cfg, hypBegin, (int)hypCount, d_counts ? d_counts : P->counts.p, d_key,
                        (hipStream_t)stream);
@@ -622,9 +645,13 @@ extern "C" MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, co
     MCV_GUARD(0, {
         if (!a || !b || !F || N < 0) fail("cvFindFundamentalMat: null argument or negative N");
         if (mask) std::memset(mask, 0, (size_t)N);
-        if (N < 8) fail("cvFindFundamentalMat: need at least 8 correspondences (N=%d)", N);
         RansacConfig cfg = config_or_default(cfgp);
         if (!cfgp) cfg.confidence = 0.99;
+        const bool seven = (cfg.flags & MCV_FLAG_SEVEN_POINT) != 0;
+        if (seven && cfg.method == MCV_METHOD_RANSAC && N != 7 && N < 15)
+            fail("cvFindFundamentalMat: 7-point FM_RANSAC needs N >= 15 (OpenCV uses LMeDS below that; N=%d)", N);
+        if (!seven && N < 8) fail("cvFindFundamentalMat: need at least 8 correspondences (N=%d)", N);
+        if (seven && N < 7) fail("cvFindFundamentalMat: need at least 7 correspondences (N=%d)", N);
         if (cfg.method != MCV_METHOD_RANSAC && cfg.method != MCV_METHOD_LSQ)
             fail("cvFindFundamentalMat: unsupported method %d", cfg.method);
         if (cfg.method == MCV_METHOD_RANSAC && !(cfg.confidence > 0 && cfg.confidence < 1))
@@ -636,13 +663,25 @@ extern "C" MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, co
         pack_points(P, a, b, N, P.pts.p, s);
         double Fm[9];
         int count = 0;
-        if (cfg.method == MCV_METHOD_LSQ || N == 8) {
+        if (seven && N == 7) {
+            // findFundamentalMat with npoints == 7: run7Point once (the first of its models), mask all 1
+            launch_f7_direct(P.pts.p, (FOneOut*)P.one.p, s);
+            MCV_HIP(hipGetLastError());
+            FOneOut one;
+            MCV_HIP(hipMemcpyAsync(P.h_one.p, P.one.p, sizeof(FOneOut), hipMemcpyDeviceToHost, s));
+            MCV_HIP(hipStreamSynchronize(s));
+            std::memcpy(&one, P.h_one.p, sizeof(FOneOut));
+            if (one.status <= 0) fail("cvFindFundamentalMat: degenerate 7-point set");
+            for (int k = 0; k < 9; ++k) Fm[k] = one.F[k];
+            if (mask) std::memset(mask, 1, (size_t)N);
+            count = N;
+        } else if (cfg.method == MCV_METHOD_LSQ || N == 8) {
             count = f_fit_all(P, P.pts.p, N, s, Fm);
             if (count <= 0) fail("cvFindFundamentalMat: degenerate point set");
             if (mask) std::memset(mask, 1, (size_t)N);
         } else {
             const int64_t best = ransac_search(P, P.pts.p, N, cfg, s);
-            if (best < 0) fail("cvFindFundamentalMat: RANSAC found no model with >= 8 inliers");
+            if (best < 0) fail("cvFindFundamentalMat: RANSAC found no model with >= %d inliers", seven ? 7 : 8);
             count = f_finalize(P, P.pts.p, N, cfg, best, Fm, P.mask.p, s);
             if (mask) {
                 MCV_HIP(hipMemcpyAsync(mask, P.mask.p, (size_t)N, hipMemcpyDeviceToHost, s));

@@ -71,6 +71,7 @@ METHOD_RANSAC = 8
 FLAG_FIXED_ITERS = 1
 FLAG_NO_REFINE = 2
 FLAG_FUSED_ERROR = 4
+FLAG_SEVEN_POINT = 8
 FERR_SAMPSON = 0
 FERR_EPIPOLAR = 1
 MODEL_HOMOGRAPHY = 0
@@ -141,6 +142,7 @@ SIGNATURES = {
     "mcvHostEssential": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostFivePoint": (_I, [_P, _P]),
     "mcvHostFivePointRef": (_I, [_P, _P]),
+    "mcvHostF7": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostDecomposeEssential": (None, [_P, _P, _P, _P]),
     "mcvHostRealRoots": (_I, [_P, _I, _I, _P]),
     "mcvHostPnP": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),

@@ -28,10 +28,11 @@ class RansacParams:
     refine: bool = True
     error_kind: int = N.FERR_SAMPSON
     fused_error: bool = False   # opt-in FMA-contracted error (default: OpenCV op-by-op order)
+    seven_point: bool = False   # fundamental: OpenCV FM_RANSAC's 7-point minimal sets (<= 3 models each)
 
     def to_c(self) -> N.RansacConfig:
         flags = (N.FLAG_FIXED_ITERS if self.fixed_iters else 0) | (0 if self.refine else N.FLAG_NO_REFINE) | \
-            (N.FLAG_FUSED_ERROR if self.fused_error else 0)
+            (N.FLAG_FUSED_ERROR if self.fused_error else 0) | (N.FLAG_SEVEN_POINT if self.seven_point else 0)
         return N.RansacConfig(self.threshold, self.confidence, int(self.max_iters), int(self.method),
                               int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(self.device_count), flags,
                               int(self.error_kind), 0)
@@ -61,7 +62,8 @@ def findHomography(src, dst, params: RansacParams | None = None):
 
 
 def findFundamentalMat(a, b, params: RansacParams | None = None):
-    """8-point RANSAC. -> (inlierCount, F (3x3 float64), mask (bool[N]))."""
+    """8-point RANSAC (default), or OpenCV FM_RANSAC with params.seven_point (+ error_kind EPIPOLAR).
+    -> (inlierCount, F (3x3 float64), mask (bool[N]))."""
     params = params or RansacParams(threshold=3.0, confidence=0.99)
     pa, pb = _v2d(a), _v2d(b)
     n = pa.shape[0]

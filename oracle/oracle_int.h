@@ -34,6 +34,9 @@ int orc_pnp_count(const float* pts, int N, const double* cam8, const double* R, 
 void orc_pnp_lm(const float* pts, int N, const uint8_t* mask, const double* cam8, double* rvec, double* t,
                 int maxIters);
 void orc_rodrigues_inv(const double* R, double* r);
+int orc_f_count(const float* pts4, int N, const double* F, float thr2, int kind, uint8_t* mask);
+int64_t orc_ransac_replay_slots(const int* counts, int64_t nhyp, int slots, int N, int m, double conf, int maxIters,
+                                int fixed, int* bestCount);
 void orc_jsvd(double* At, double* Wout, double* Vt, int m, int n, int n1);
 void orc_epnp(const double* pw, const double* us, int n, const double* cam4, double* R, double* t);
 void orc_epnp5_f32(const float* p5, const double* cam8, double* R, double* t);

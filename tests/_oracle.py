@@ -30,6 +30,10 @@ _SIGS = {
     "orc_find_fundamental": (_I, [_P, _P, _I, _D, _D, _I, _I, _U64, _I, _I, _P, _P, _P, _I]),
     "orc_poly_real_roots": (_I, [_P, _I, _P]),
     "orc_e_solve5": (_I, [_P, _P, _P, _P, _P]),
+    "orc_f7_solve": (_I, [_P, _P, _P, _P, _P]),
+    "orc_f7_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P]),
+    "orc_f7_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _I, _P, _I]),
+    "orc_find_fundamental7": (_I, [_P, _P, _I, _D, _D, _I, _U64, _I, _I, _P, _P, _P, _I]),
     "orc_e_solve5_ref": (_I, [_P, _P, _P, _P, _P]),
     "orc_solve_poly10": (None, [_P, _P, _P]),
     "orc_e_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P]),
@@ -192,6 +196,32 @@ def find_fundamental(a, b, thr=3.0, conf=0.99, max_iters=1000, method=8, seed=0,
 
 # ---- essential matrix (oracle_e.c) ---------------------------------------------------------
 E_SLOTS = 10
+
+
+F7_SLOTS = 3
+
+
+def f7_hypothesis(pts4, seed, hyp):
+    """7-point hypothesis -> (n or status, F[3,3,3], idx[7])."""
+    F, idx = np.zeros(27), np.full(7, -1, dtype=np.int32)
+    n = load().orc_f7_hypothesis(ptr(pts4), pts4.shape[0], seed, hyp, ptr(F), ptr(idx))
+    return n, F.reshape(3, 3, 3), idx
+
+
+def f7_counts(pts4, seed, begin, count, thr2, kind=3, nthreads=0):
+    out = np.zeros(count * F7_SLOTS, dtype=np.int32)
+    load().orc_f7_counts(ptr(pts4), pts4.shape[0], seed, begin, count, thr2, kind, ptr(out), nthreads)
+    return out
+
+
+def find_fundamental7(a, b, thr=3.0, conf=0.99, max_iters=1000, seed=0, flags=0, error_kind=1, nthreads=0):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    n = a.shape[0]
+    F, mask, best = np.zeros(9), np.zeros(max(n, 1), dtype=np.uint8), np.zeros(1, dtype=np.int64)
+    cnt = load().orc_find_fundamental7(ptr(a), ptr(b), n, thr, conf, max_iters, seed, flags, error_kind, ptr(F),
+                                       ptr(mask), ptr(best), nthreads)
+    return cnt, F.reshape(3, 3), mask[:n], int(best[0])
 
 
 def pack_e(a, b, focal=1.0, pp=(0.0, 0.0)) -> np.ndarray:

@@ -225,3 +225,62 @@ def test_full_size_cfg4(torch_dev, oracle):
     np.testing.assert_array_equal(r1[1], r8[1])
     np.testing.assert_array_equal(r1[2], r8[2])
     np.testing.assert_array_equal(r1[1], np.asarray(F).reshape(r1[1].shape))
+
+
+# ---- OpenCV FM_RANSAC: 7-point minimal sets, up to 3 models per sample (MCV_FLAG_SEVEN_POINT) -----
+@pytest.mark.parametrize("n,outl,seed,begin,count,error_kind,unfused", [
+    (15, 0.0, 1, 0, 64, 1, True), (300, 0.5, 3, 0, 1024, 1, True), (2000, 0.5, 4, 77777, 512, 1, True),
+    (1999, 0.5, 5, 0, 512, 0, True), (1000, 0.6, 6, 2**30, 256, 1, False), (64, 0.2, 8, 0, 300, 0, False)])
+def test_f7_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, error_kind, unfused):
+    """Per-slot counts (3 model slots per hypothesis) equal the run7Point restatement's; the best key is
+    the first maximum over slots."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=outl)
+    pts = D.pack_points_tensor(a, b, dev)
+    plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, n, 3 * count)
+    thr = 5e-3
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, error_kind=error_kind, fused_error=not unfused,
+                              seven_point=True).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(3 * count, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, begin, count, key, counts)
+    got = counts.cpu().numpy()
+    ref = oracle.f7_counts(oracle.pack4(a, b), seed, begin, count, float(np.float32(thr * thr)),
+                           oracle.f_kind(error_kind, unfused))
+    np.testing.assert_array_equal(got, ref)
+    if (ref >= 7).any() and not (ref == -2).any():
+        c = ref.max()
+        i = int(np.nonzero(ref == c)[0][0])
+        assert int(key[0].item()) == (int(c) << 32) | (0xFFFFFFFF - (3 * begin + i))
+    plan.close()
+
+
+@pytest.mark.parametrize("n,outl,seed,iters,fixed", [(15, 0.0, 1, 200, False), (500, 0.5, 2, 1000, False),
+                                                     (3000, 0.5, 3, 2000, False), (2000, 0.5, 4, 300, True)])
+def test_find_fundamental7_vs_oracle(gpu, oracle, n, outl, seed, iters, fixed):
+    """cvFindFundamentalMat with FM_RANSAC semantics (7-point sets, epipolar error, op-by-op): the
+    winning slot, its F (no refit) and the mask equal the oracle's exactly."""
+    a, b, inl, F = S.fundamental_problem(n, seed, outlier_frac=outl)
+    p = opencv.RansacParams(threshold=5e-3, confidence=0.99, max_iters=iters, seed=seed, error_kind=N.FERR_EPIPOLAR,
+                            seven_point=True, fixed_iters=fixed)
+    cnt, Fg, mask = opencv.findFundamentalMat(a, b, p)
+    rc, Fo, rmask, best = oracle.find_fundamental7(a, b, thr=5e-3, conf=0.99, max_iters=iters, seed=seed,
+                                                   flags=N.FLAG_FIXED_ITERS if fixed else 0, error_kind=1)
+    assert cnt == rc and best >= 0
+    np.testing.assert_array_equal(Fg, Fo)
+    np.testing.assert_array_equal(mask, rmask != 0)
+    if n >= 500:   # the winning minimal-sample model (no refit, sigma 1e-3 vs thr 5e-3) keeps most
+        assert mask[inl].mean() > 0.6 and mask[~inl].mean() < 0.05   # inliers (0.83 at seed 2)
+
+
+def test_find_fundamental7_edges(gpu, oracle):
+    a, b, _, F = S.fundamental_problem(7, 5, outlier_frac=0.0, sigma=0.0)
+    p = opencv.RansacParams(threshold=5e-3, seven_point=True, error_kind=N.FERR_EPIPOLAR)
+    cnt, Fg, mask = opencv.findFundamentalMat(a, b, p)      # N == 7: run7Point once, first model
+    rc, Fo, rmask, _ = oracle.find_fundamental7(a, b, thr=5e-3)
+    assert cnt == rc == 7 and mask.all()
+    np.testing.assert_array_equal(Fg, Fo)
+    a, b, _, _ = S.fundamental_problem(12, 5, outlier_frac=0.0)
+    with pytest.raises(N.NativeError, match="N >= 15"):
+        opencv.findFundamentalMat(a, b, p)
