@@ -17,8 +17,7 @@
 //    sort, cv::RNG(0x12345678) fill of null singular vectors) and SVBkSb (threshold 2 DBL_EPSILON
 //    x sum w). The scalar loop order of the generic template is restated; x86 builds may run
 //    some of those loops through SIMD helpers (VBLAS) with other partial-sum orders [ext].
-//  * std::hypot is replaced by hypot_fma (Borges' FMA-corrected square root), identical on both
-//    sides; libm's hypot may differ from it in the last bit.
+//  * hypot is lapack.cpp's own template (cv_hypot below), not libm's.
 // Large point sets (the inlier solve) sum per-point terms in blocks of kEpnpBlock consecutive
 // points, each block sequentially from 0, the block sums sequentially: for n <= kEpnpBlock this
 // is exactly the sequential order of the OpenCV loops.
@@ -40,24 +39,21 @@ struct CvRng {
     }
 };
 
-// sqrt(x^2 + y^2) with one FMA-based correction step (Borges 2019); power-of-two scaling keeps the
-// squares inside the normal range. Deterministic: only +, -, *, /, sqrt and fma.
-MCV_HD double hypot_fma(double x, double y) {
-    x = __builtin_fabs(x);
-    y = __builtin_fabs(y);
-    if (!(x <= 1.7976931348623157e308) || !(y <= 1.7976931348623157e308)) {
-        if (x == __builtin_inf() || y == __builtin_inf()) return __builtin_inf();
-        return x + y;   // NaN
+// The hypot template of OpenCV's core lapack.cpp (the one JacobiSVDImpl_ calls — an unqualified
+// hypot inside namespace cv): the larger magnitude times sqrt(1 + ratio^2). Only |.|, /, *, + and
+// sqrt, so host and device round it identically.
+MCV_HD double cv_hypot(double a, double b) {
+    a = __builtin_fabs(a);
+    b = __builtin_fabs(b);
+    if (a > b) {
+        b /= a;
+        return a * __builtin_sqrt(1 + b * b);
     }
-    if (x < y) { const double t = x; x = y; y = t; }
-    if (y == 0) return x;
-    double sc = 1.0;
-    if (x > 0x1p500) { x *= 0x1p-600; y *= 0x1p-600; sc = 0x1p600; }
-    else if (x < 0x1p-500) { x *= 0x1p600; y *= 0x1p600; sc = 0x1p-600; }
-    double h = __builtin_sqrt(__builtin_fma(x, x, y * y));
-    const double h2 = h * h, x2 = x * x;
-    h -= (__builtin_fma(-y, y, h2 - x2) + __builtin_fma(h, h, -h2) - __builtin_fma(x, x, -x2)) / (2 * h);
-    return h * sc;
+    if (b > 0) {
+        a /= b;
+        return b * __builtin_sqrt(1 + a * a);
+    }
+    return 0;
 }
 
 // JacobiSVDImpl_<double>: A holds the N rows of length M of the TRANSPOSED input (At). On return
@@ -85,7 +81,7 @@ MCV_HD void jacobi_svd(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
                 for (int k = 0; k < M; ++k) p += A[i][k] * A[j][k];
                 if (__builtin_fabs(p) <= eps * __builtin_sqrt(a * b)) continue;
                 p *= 2;
-                const double beta = a - b, gamma = hypot_fma(p, beta);
+                const double beta = a - b, gamma = cv_hypot(p, beta);
                 double c, s;
                 if (beta < 0) {
                     const double delta = (gamma - beta) * 0.5;

@@ -7,10 +7,10 @@
  *
  * OpenCV is not vendored in /root/reference and not installed here [ext]: this restates the
  * published algorithm and the scalar loop order of those functions; x86 OpenCV builds run some
- * JacobiSVD loops through SIMD helpers, and std::hypot is replaced by an FMA-corrected hypot, so
- * the last bits of OpenCV's own result are not claimed (parity with OpenCV unpinned; the EPnP
- * solution itself is pinned by exact synthetic geometry: noise-free correspondences of a known
- * pose give that pose back to ~1e-10, tests/test_oracle_pnp.py). The GPU path
+ * JacobiSVD loops through SIMD helpers (other partial-sum orders), so the last bits of OpenCV's
+ * own result are not claimed (parity with OpenCV unpinned; the EPnP solution itself is pinned by
+ * exact synthetic geometry: noise-free correspondences of a known pose give that pose back to
+ * ~1e-10, tests/test_oracle_pnp.py). The GPU path
  * (minicv_amd/csrc/epnp.h) must equal this file bit for bit.
  *
  * Sums over the points of a large set run in blocks of EPNP_BLOCK consecutive points (each block
@@ -26,19 +26,19 @@
 
 #define EPNP_BLOCK 1024
 
-static double hyp_fma(double x, double y) {
-    x = fabs(x);
-    y = fabs(y);
-    if (!(x <= DBL_MAX) || !(y <= DBL_MAX)) return (isinf(x) || isinf(y)) ? INFINITY : x + y;
-    if (x < y) { double t = x; x = y; y = t; }
-    if (y == 0) return x;
-    double sc = 1.0;
-    if (x > 0x1p500) { x *= 0x1p-600; y *= 0x1p-600; sc = 0x1p600; }
-    else if (x < 0x1p-500) { x *= 0x1p600; y *= 0x1p600; sc = 0x1p-600; }
-    double h = sqrt(fma(x, x, y * y));
-    double h2 = h * h, x2 = x * x;
-    h -= (fma(-y, y, h2 - x2) + fma(h, h, -h2) - fma(x, x, -x2)) / (2 * h);
-    return h * sc;
+/* core lapack.cpp's hypot template (what JacobiSVDImpl_'s unqualified hypot resolves to). */
+static double cv_hypot(double a, double b) {
+    a = fabs(a);
+    b = fabs(b);
+    if (a > b) {
+        b /= a;
+        return a * sqrt(1 + b * b);
+    }
+    if (b > 0) {
+        a /= b;
+        return b * sqrt(1 + a * a);
+    }
+    return 0;
 }
 
 /* JacobiSVDImpl_<double>(At, W, Vt, m, n, n1): At is n1 x m row-major (the transposed matrix; rows
@@ -65,7 +65,7 @@ void orc_jsvd(double* At, double* Wout, double* Vt, int m, int n, int n1) {
                 for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
                 if (fabs(p) <= eps * sqrt(a * b)) continue;
                 p *= 2;
-                double beta = a - b, gamma = hyp_fma(p, beta), c, s;
+                double beta = a - b, gamma = cv_hypot(p, beta), c, s;
                 if (beta < 0) {
                     double delta = (gamma - beta) * 0.5;
                     s = sqrt(delta / gamma);
