@@ -313,9 +313,10 @@ def load_traffic(kernel: str, config: str):
     if not p.exists():
         return None
     try:
-        d = json.loads(p.read_text()).get(kernel)
-        if d and d.get("config") == config:
-            return d.get("hbm_bytes_per_launch")
+        # keys are kernel-name prefixes as rocprofv3 reports them (mcv_f_verify covers mcv_f_verify_pk<..>)
+        for key, d in json.loads(p.read_text()).items():
+            if (kernel == key or kernel.startswith(key + "_")) and d.get("config") == config:
+                return d.get("hbm_bytes_per_launch")
     except Exception:
         return None
     return None
@@ -830,8 +831,8 @@ def bench_scaled(args):
                                    f"GPU(s)", "observations": n, "parallelism": f"replicas x{world}"},
             "roofline": {"bound": "fp64-valu (unfused: the managed code's op-by-op arithmetic)", "achieved": tf,
                          "peak": FP64_NOFMA_PEAK_TF, "unit": "TFLOP/s", "frac": tf / FP64_NOFMA_PEAK_TF,
-                         "peak_fma": FP64_PEAK_TF, "frac_fma": tf / FP64_PEAK_TF, "traffic": None,
-                         "kernel": "mcv_scaled_costs",
+                         "peak_fma": FP64_PEAK_TF, "frac_fma": tf / FP64_PEAK_TF,
+                         "traffic": load_traffic("mcv_scaled_costs", f"{n}"), "kernel": "mcv_scaled_costs",
                          "avg_launch_ms": avg_ms, "launches": launches,
                          "model": f"{S_FLOPS_PER_TERM} fp64 FLOP per (candidate, observation), a division "
                                   "counted as one", "terms_per_launch": terms},

@@ -22,7 +22,8 @@ PROF = ROOT / "profiles"
 WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2", "scaled"]
 # dominant kernel per BASELINE workload (substring of the demangled rocprofv3 kernel name)
 KERNELS = {"homography": "mcv_h_verify_cert", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
-           "l2": "mcv_l2_mfma", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify"}
+           "l2": "mcv_l2_mfma", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify",
+           "scaled": "mcv_scaled_costs"}
 EXTRA_BENCH = ["homography_fused", "pnp_ap3p"]   # second bench lines (bench_<name>.log)
 
 
@@ -87,6 +88,8 @@ def main():
         elif w == "pnp":
             config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
                 20.0 * c.get("correspondences", 0) * c.get("hypotheses_total", 0)
+        elif w == "scaled":   # 2 N candidates x N observations x 40 B (world point + observation)
+            config, alg = f"{c.get('observations')}", 80.0 * c.get("observations", 0) ** 2
         else:
             config = f"{c.get('queries')}x{c.get('train')}"
             dim_bytes = 32.0 if w == "hamming" else 512.0

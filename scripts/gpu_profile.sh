@@ -16,7 +16,7 @@ for w in homography fundamental essential pnp hamming l2 scaled; do
         python3 "$R/bench.py" --workload $w --steps 5 --warmup 2 --no-cpu-baseline
 done
 # PMC passes (one counter per run) on each BASELINE workload's bench, then SQ counters of the H sweep
-for w in homography fundamental essential pnp hamming l2; do
+for w in homography fundamental essential pnp hamming l2 scaled; do
     run pmc_fetch_$w 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch_$w" -o run -- \
         python3 "$R/bench.py" --workload $w --steps 3 --warmup 1 --no-cpu-baseline
     run pmc_write_$w 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write_$w" -o run -- \

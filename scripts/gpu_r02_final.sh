@@ -34,7 +34,7 @@ for w in homography fundamental essential pnp hamming l2 scaled; do
     step prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$w" -o run -- \
         python3 "$R/bench.py" --workload $w --steps 5 --warmup 2 --no-cpu-baseline
 done
-for w in homography fundamental essential pnp hamming l2; do
+for w in homography fundamental essential pnp hamming l2 scaled; do
     step pmc_fetch_$w 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch_$w" -o run -- \
         python3 "$R/bench.py" --workload $w --steps 3 --warmup 1 --no-cpu-baseline
     step pmc_write_$w 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write_$w" -o run -- \
