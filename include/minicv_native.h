@@ -409,6 +409,16 @@ MCV_API void mcvHostEpnp5(const double* pw15, const double* us10, const double* 
  * status[h] = 1 or -1 / -2. Returns hypCount, -1 on failure. */
 MCV_API int mcvTestPnpHypotheses(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin,
                                  int hypCount, int kind, double* poses12, int* status);
+/* Device self-test: the PnP inlier sweep on caller-supplied poses (poses12[h] = {R (9), t (3)}) over
+ * host PnpPoint[N]; mode 0 = the certified packed-fp32 sweep (the default path), 1 = the all-fp64
+ * sweep. counts[h] = inliers. Returns nPoses, -1 on failure. */
+MCV_API int mcvTestPnpSweep(const float* pts, int N, const double* cam8, const double* poses12, int nPoses,
+                            float thr2, int fused, int mode, int* counts);
+/* Host twin of the certified PnP prefilter (pnp_pk.h) for one pose over host PnpPoint[N]: decision[i]
+ * = 1 certified inlier, 0 certified outlier, -1 undecided; exact[i] = the fp64 test (pnp_error).
+ * Returns the number of decided points whose decision differs from the exact test (must be 0). */
+MCV_API int mcvHostPnpCert(const float* pts, int N, const double* cam8, const double* R9, const double* t3,
+                           float thr2, int fused, int* decision, int* exact);
 /* Host build of solveAp3p's computation (mu3 / mv3 pixels, W9 = 3 world points), R36 / t12 out. */
 MCV_API int mcvHostSolveAp3p(const double* mu3, const double* mv3, const double* W9, double inv_fx, double inv_fy,
                              double cx_fx, double cy_fy, double* R36, double* t12);

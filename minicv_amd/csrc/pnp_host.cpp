@@ -14,6 +14,7 @@
 #include "linalg.h"
 #include "plan.h"
 #include "hyp_pnp.h"
+#include "pnp_pk.h"
 
 #include <cmath>
 #include <cfloat>
@@ -126,8 +127,10 @@ void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
     P.eLastSeed = cfg.seed;
     P.eLastPts = d_pts;
     P.eLastKind = epnp ? 1 : 0;
+    P.bb4.ensure(4);
+    launch_pnp_extent(d_pts, N, P.bb4.p, s);
     ProfScope ps("pnp_verify", s);
-    launch_pnp_verify(d_pts, N, P.pnpCam, P.models.p, d_counts, hypCount, thr2, fused_pnp(cfg), s);
+    launch_pnp_verify(d_pts, N, P.pnpCam, P.models.p, d_counts, hypCount, thr2, fused_pnp(cfg), P.bb4.p, s);
 }
 
 static PnpOneOut pnp_fetch_one(Plan& P, hipStream_t s) {
@@ -715,3 +718,56 @@ extern "C" MCV_API int mcvTestPnpHypotheses(const float* pts, int N, const doubl
         return hypCount;
     })
 }
+
+extern "C" MCV_API int mcvTestPnpSweep(const float* pts, int N, const double* cam8, const double* poses12, int nPoses,
+                                       float thr2, int fused, int mode, int* counts) {
+    MCV_GUARD(-1, {
+        if (!pts || !cam8 || !poses12 || !counts || N <= 0 || nPoses <= 0) fail("mcvTestPnpSweep: bad argument");
+        require_device();
+        Plan& P = thread_plan(MCV_MODEL_PNP);
+        hipStream_t s = P.own_stream();
+        P.reserve(N, nPoses);
+        for (int k = 0; k < 8; ++k) P.pnpCam[k] = cam8[k];
+        MCV_HIP(hipMemcpyAsync(P.ptsd.p, pts, (size_t)N * sizeof(PnpPoint), hipMemcpyHostToDevice, s));
+        std::vector<PnpPose> m((size_t)nPoses);
+        for (int h = 0; h < nPoses; ++h) {
+            for (int k = 0; k < 9; ++k) m[h].R[k] = poses12[12 * (size_t)h + k];
+            for (int k = 0; k < 3; ++k) m[h].t[k] = poses12[12 * (size_t)h + 9 + k];
+        }
+        MCV_HIP(hipMemcpyAsync(P.models.p, m.data(), m.size() * sizeof(PnpPose), hipMemcpyHostToDevice, s));
+        MCV_HIP(hipMemsetAsync(P.counts.p, 0, (size_t)nPoses * sizeof(int), s));
+        P.bb4.ensure(4);
+        launch_pnp_extent(P.ptsd.p, N, P.bb4.p, s);
+        launch_pnp_verify(P.ptsd.p, N, P.pnpCam, P.models.p, P.counts.p, nPoses, thr2, fused != 0,
+                          mode == 0 ? P.bb4.p : nullptr, s);
+        MCV_HIP(hipGetLastError());
+        MCV_HIP(hipMemcpyAsync(counts, P.counts.p, (size_t)nPoses * sizeof(int), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        P.eLastBegin = -1;
+        return nPoses;
+    });
+}
+
+extern "C" MCV_API int mcvHostPnpCert(const float* pts, int N, const double* cam8, const double* R9, const double* t3,
+                                      float thr2, int fused, int* decision, int* exact) {
+    const PnpPoint* q = (const PnpPoint*)pts;
+    double ext[3] = {0, 0, 0};
+    for (int i = 0; i < N; ++i) {
+        const double v[3] = {q[i].X, q[i].Y, q[i].Z};
+        for (int k = 0; k < 3; ++k) ext[k] = std::isfinite(v[k]) ? std::fmax(ext[k], std::fabs(v[k])) : INFINITY;
+    }
+    const PnpPkCam pc = pnp_pk_cam_host(cam8, thr2);
+    PnpPkPose pp;
+    pnp_pk_pose(R9, t3, ext, pp);
+    PnpCamera cam{cam8[0], cam8[1], cam8[2], cam8[3], cam8[4], cam8[5], cam8[6], cam8[7]};
+    int bad = 0;
+    for (int i = 0; i < N; ++i) {
+        const int d = pc.ok ? pnp_pk_decide_host(pc, pp, q[i].X, q[i].Y, q[i].Z, q[i].u, q[i].v) : -1;
+        const int e = pnp_error(cam, R9, t3, q[i].X, q[i].Y, q[i].Z, q[i].u, q[i].v, fused != 0) <= thr2 ? 1 : 0;
+        decision[i] = d;
+        exact[i] = e;
+        if (d >= 0 && d != e) ++bad;
+    }
+    return bad;
+}
+

@@ -1,0 +1,228 @@
+// pnp_pk.h — certified packed-fp32 prefilter of the PnP inlier test (the
+// sweep behind cvSolvePnPRansac, MiniCVNative.cpp:125).
+//
+// The exact decision (hyp_pnp.h pnp_error, the reference's PnPRansacCallback::computeError):
+// (u, v) = projectPoints(X) in fp64 (pnp_project), U = (float)u, dx = uo - U, dy likewise in fp32,
+// e = dx * dx + dy * dy (or fmaf), inlier iff e <= thr2. That costs ~60 fp64 instructions per
+// (pose, point). This prefilter evaluates the same projection in fp32 — two points per
+// v_pk_fma_f32, the pose in wave-uniform registers — together with a per-lane bound g on the
+// distance between its pixel and the exact one, and decides every lane whose distance is certainly
+// inside or outside the threshold circle; the rest take the exact fp64 test.
+//
+// Bound (u = 2^-24; extents Xm, Ym, Zm = max |X|, |Y|, |Z| over the points; M_r = sum_j |R_rj| Xm_j
+// + |t_r| per row r of the pose):
+//   Xc, Yc, Zc: three FMAs on fp32-rounded R, t:  |Xc32 - Xc| <= eX = 5u M_0 (eY, eZ likewise).
+//   x = Xc / Zc by v_rcp_f32 (<= 1 ulp) and a multiply: with |Zc32| >= zmin = 2^10 eZ,
+//     |x32 - x| <= delta = |1/Zc32| (c1 + m c2), c1 = max(eX, eY)(1 + 2^-10)(1 + 2^-7),
+//     c2 = 1.6 eZ (1 + 2^-7) (the 1.6 also covers the reciprocal's and the product's rounding,
+//     since eZ / |Zc32| >= 5u); m >= max(|x32|, |y32|) is taken as (1 + r2) / 2 (AM-GM; no abs in
+//     packed arithmetic).
+//   distortion (xd, yd) = x (1 + k1 r2 + k2 r2^2 + 2 p1 y + 2 p2 x) + (p2, p1) r2 (the factored form
+//     evaluated here): on the box |x|, |y| <= rho = m + delta its gradient's row sums are bounded by
+//     L = 1 + rho (8 (|p1| + |p2|) + rho^2 (6 |k1| + 20 |k2| rho^2)), and its fp32 evaluation (depth 8
+//     with the coefficient rounding) by 10 u rho L; so |xd32 - xd| <= L (delta + 10 u rho).
+//   pixels: |u32 - u| + |(float)u - u| <= F L (delta + 13 u rho) + 3 u C, F = max |f|, C = max |c|
+//     (fx / cx rounding, the FMA, the cast of the exact u to float); the fp64 path's own error is
+//     ~2^-29 of that, inside the (1 + 2^-16) slack on F and C.
+//   g = sqrt(2) (F L (delta + 13 u rho) + 4 u C) (1 + 2^-16) >= the Euclidean pixel distance.
+// Decision (S = fl(D^2 + E^2), D = uo - u32, E = vo - v32; the exact e is within (1 +- 11u) of the
+// squared distance of uo to the exact pixel, which is within g of sqrt(S)):
+//   S < thr2 (1 - 2^-17) - 2T' g                     -> certified inlier (sqrt(S) + g < T)
+//   S > thr2 (1 + 2^-17) + g (g (1 + 2^-17) + 2T')   -> certified outlier (sqrt(S) - g > T)
+// with T' = sqrt(thr2) (1 + 2^-17): the 2^-17 margins cover every fp32 rounding of S, lo and hi and
+// the (1 +- 11u) factors. NaN or inf anywhere fails both compares (undecided), as does a lane with
+// |Zc32| < zmin (the domain of the 1/Zc bound) and every lane of a pose whose bound is not finite.
+#pragma once
+
+#include "mcv_common.h"
+#include "hyp_pnp.h"
+#include <cmath>
+
+namespace mcv {
+
+// Launch constants (host-built, pnp_pk_cam_host): the camera in fp32 and the bound's slopes.
+struct PnpPkCam {
+    float fx, fy, cx, cy, k1, k2, tp1, tp2, p1, p2;   // tp1 = 2 p1, tp2 = 2 p2 (exact)
+    float A2, A4, cp;      // 6 |k1|, 20 |k2|, 8 (|p1| + |p2|), rounded up
+    float half;            // 0.5 (1 + 2^-20), rounded up: m = fma(r2, half, half)
+    float u13;             // 13 u (1 + 2^-16)
+    float Fg, Cg;          // sqrt(2) F (1 + 2^-16), sqrt(2) 4u C (1 + 2^-16) + 2^-100, rounded up
+    float twoT, thrLo, thrHi, gk;   // 2T', thr2 (1 - 2^-17) down, thr2 (1 + 2^-17) up, 1 + 2^-17
+    int ok;                // 0: outside the bound's domain (the launch takes the exact fp64 sweep)
+};
+
+// Per-pose constants (computed per wave from the fp64 pose and the point extents).
+struct PnpPkPose {
+    float R[9], t[3];
+    float c1, c2, zmin;
+};
+
+MCV_HD float pk_f32_ru(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __double2float_ru(v);
+#else
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, __builtin_inff());
+    return f;
+#endif
+}
+MCV_HD float pk_f32_rd(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __double2float_rd(v);
+#else
+    float f = (float)v;
+    if ((double)f > v) f = std::nextafter(f, -__builtin_inff());
+    return f;
+#endif
+}
+
+inline PnpPkCam pnp_pk_cam_host(const double* cam8, float thr2) {
+    const double fx = cam8[0], fy = cam8[1], cx = cam8[2], cy = cam8[3];
+    const double k1 = cam8[4], k2 = cam8[5], p1 = cam8[6], p2 = cam8[7];
+    PnpPkCam c;
+    c.fx = (float)fx; c.fy = (float)fy; c.cx = (float)cx; c.cy = (float)cy;
+    c.k1 = (float)k1; c.k2 = (float)k2; c.p1 = (float)p1; c.p2 = (float)p2;
+    c.tp1 = 2.0f * c.p1; c.tp2 = 2.0f * c.p2;
+    c.A2 = pk_f32_ru(6.0 * std::fabs(k1) * (1 + 0x1p-30));
+    c.A4 = pk_f32_ru(20.0 * std::fabs(k2) * (1 + 0x1p-30));
+    c.cp = pk_f32_ru(8.0 * (std::fabs(p1) + std::fabs(p2)) * (1 + 0x1p-30));
+    c.half = pk_f32_ru(0.5 * (1 + 0x1p-20));
+    const double u = 0x1p-24, s = 1.0 + 0x1p-16;
+    c.u13 = pk_f32_ru(13.0 * u * s);
+    const double F = std::fmax(std::fabs(fx), std::fabs(fy)), C = std::fmax(std::fabs(cx), std::fabs(cy));
+    c.Fg = pk_f32_ru(std::sqrt(2.0) * F * s * (1 + 0x1p-30));
+    c.Cg = pk_f32_ru(std::sqrt(2.0) * 4.0 * u * C * s * (1 + 0x1p-30) + 0x1p-100);
+    const double T2 = (double)thr2, T = std::sqrt(T2);
+    c.twoT = pk_f32_ru(2.0 * T * (1 + 0x1p-17) * (1 + 0x1p-30));
+    c.thrLo = pk_f32_rd(T2 * (1 - 0x1p-17));
+    c.thrHi = pk_f32_ru(T2 * (1 + 0x1p-17));
+    c.gk = 1.0f + 0x1p-17f;
+    // domain: finite camera (fp32-representable well away from overflow), finite non-negative thr2
+    const double lim = 0x1p40;
+    c.ok = std::fabs(fx) < lim && std::fabs(fy) < lim && std::fabs(cx) < lim && std::fabs(cy) < lim &&
+           std::fabs(k1) < lim && std::fabs(k2) < lim && std::fabs(p1) < lim && std::fabs(p2) < lim &&
+           T2 >= 0 && T2 < 0x1p60 && std::isfinite(c.Fg) && std::isfinite(c.twoT);
+    return c;
+}
+
+// ext = {Xm, Ym, Zm} (inf when any coordinate is not finite).
+MCV_HD void pnp_pk_pose(const double* R, const double* t, const double* ext, PnpPkPose& p) {
+    for (int j = 0; j < 9; ++j) p.R[j] = (float)R[j];
+    for (int j = 0; j < 3; ++j) p.t[j] = (float)t[j];
+    double M[3];
+    for (int r = 0; r < 3; ++r)
+        M[r] = (fabs(R[3 * r]) * ext[0] + fabs(R[3 * r + 1]) * ext[1] + fabs(R[3 * r + 2]) * ext[2] + fabs(t[r])) *
+               (1 + 0x1p-40);
+    const double u = 0x1p-24;
+    const double eXY = 5.0 * u * fmax(M[0], M[1]), eZ = 5.0 * u * M[2];
+    const bool ok = M[0] <= 0x1p60 && M[1] <= 0x1p60 && M[2] <= 0x1p60;   // false for NaN
+    p.c1 = ok ? pk_f32_ru(eXY * (1 + 0x1p-10) * (1 + 0x1p-7)) : __builtin_inff();
+    p.c2 = ok ? pk_f32_ru(1.6 * eZ * (1 + 0x1p-7)) : __builtin_inff();
+    p.zmin = ok ? pk_f32_ru(fmax(eZ * 0x1p10, 0x1p-100)) : __builtin_inff();
+}
+
+// Elementwise helpers: V = float (host twin, one point) or f2 (device, two points).
+MCV_HD float pkv_fma(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_fmaf(a, b, c);
+#else
+    return std::fma(a, b, c);
+#endif
+}
+MCV_HD float pkv_splat(float c, float) { return c; }
+MCV_HD float pkv_rcp(float a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(a);
+#else
+    return 1.0f / a;
+#endif
+}
+MCV_HD float pkv_absmul(float a, float b) { return fabsf(a) * b; }
+
+#if defined(__HIPCC__)
+typedef float pkf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pkf2 pkv_fma(pkf2 a, pkf2 b, pkf2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ pkf2 pkv_splat(float c, pkf2) { return pkf2{c, c}; }
+__device__ __forceinline__ pkf2 pkv_rcp(pkf2 a) { return pkf2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)}; }
+__device__ __forceinline__ pkf2 pkv_absmul(pkf2 a, pkf2 b) { return pkf2{fabsf(a.x) * b.x, fabsf(a.y) * b.y}; }
+#endif
+
+// The launch and pose constants splatted to the evaluation's vector type once, outside the sweep
+// (V = f2: VGPR pairs; no per-use v_mov and no two-scalar operand pairs inside the loop).
+template <class V>
+struct PnpPkCamV {
+    V fx, fy, cx, cy, k1, k2, tp1, tp2, p1, p2, A2, A4, cp, half, u13, Fg, Cg, ntwoT, twoT, thrLo, thrHi, gk, one;
+};
+template <class V>
+MCV_HD PnpPkCamV<V> pnp_pk_cam_v(const PnpPkCam& c, V z) {
+    PnpPkCamV<V> v;
+    v.fx = pkv_splat(c.fx, z); v.fy = pkv_splat(c.fy, z); v.cx = pkv_splat(c.cx, z); v.cy = pkv_splat(c.cy, z);
+    v.k1 = pkv_splat(c.k1, z); v.k2 = pkv_splat(c.k2, z); v.tp1 = pkv_splat(c.tp1, z); v.tp2 = pkv_splat(c.tp2, z);
+    v.p1 = pkv_splat(c.p1, z); v.p2 = pkv_splat(c.p2, z); v.A2 = pkv_splat(c.A2, z); v.A4 = pkv_splat(c.A4, z);
+    v.cp = pkv_splat(c.cp, z); v.half = pkv_splat(c.half, z); v.u13 = pkv_splat(c.u13, z); v.Fg = pkv_splat(c.Fg, z);
+    v.Cg = pkv_splat(c.Cg, z); v.ntwoT = pkv_splat(-c.twoT, z); v.twoT = pkv_splat(c.twoT, z);
+    v.thrLo = pkv_splat(c.thrLo, z); v.thrHi = pkv_splat(c.thrHi, z); v.gk = pkv_splat(c.gk, z);
+    v.one = pkv_splat(1.0f, z);
+    return v;
+}
+// Pose: R as scalars (one wave-uniform operand per FMA), t and the bound slopes splatted.
+template <class V>
+struct PnpPkPoseV {
+    float R[9];
+    V t0, t1, t2, c1, c2;
+    float zmin;
+};
+template <class V>
+MCV_HD PnpPkPoseV<V> pnp_pk_pose_v(const PnpPkPose& p, V z) {
+    PnpPkPoseV<V> v;
+    for (int j = 0; j < 9; ++j) v.R[j] = p.R[j];
+    v.t0 = pkv_splat(p.t[0], z); v.t1 = pkv_splat(p.t[1], z); v.t2 = pkv_splat(p.t[2], z);
+    v.c1 = pkv_splat(p.c1, z); v.c2 = pkv_splat(p.c2, z);
+    v.zmin = p.zmin;
+    return v;
+}
+
+// The certified quantities of one point (V = float) or two points (V = f2) against one pose:
+// S (squared fp32 pixel distance), lo / hi (the two cuts) and Zc (for the domain test |Zc| >= zmin).
+// 20 FMA-class operations + 2 reciprocals + 2 |.|-products per point (halved per point when packed).
+template <class V>
+MCV_HD void pnp_pk_eval(const PnpPkCamV<V>& c, const PnpPkPoseV<V>& p, V X, V Y, V Z, V uo, V vo, V& S, V& lo, V& hi,
+                        V& Zc) {
+    const V z = X - X;
+    const V Xc = pkv_fma(pkv_splat(p.R[0], z), X, pkv_fma(pkv_splat(p.R[1], z), Y, pkv_fma(pkv_splat(p.R[2], z), Z, p.t0)));
+    const V Yc = pkv_fma(pkv_splat(p.R[3], z), X, pkv_fma(pkv_splat(p.R[4], z), Y, pkv_fma(pkv_splat(p.R[5], z), Z, p.t1)));
+    Zc = pkv_fma(pkv_splat(p.R[6], z), X, pkv_fma(pkv_splat(p.R[7], z), Y, pkv_fma(pkv_splat(p.R[8], z), Z, p.t2)));
+    const V iz = pkv_rcp(Zc);
+    const V x = Xc * iz, y = Yc * iz;
+    const V r2 = pkv_fma(x, x, y * y);
+    const V cd = pkv_fma(r2, pkv_fma(c.k2, r2, c.k1), c.one);
+    const V w = pkv_fma(c.tp1, y, pkv_fma(c.tp2, x, cd));
+    const V xd = pkv_fma(x, w, c.p2 * r2);
+    const V yd = pkv_fma(y, w, c.p1 * r2);
+    const V u = pkv_fma(c.fx, xd, c.cx);
+    const V v = pkv_fma(c.fy, yd, c.cy);
+    const V D = uo - u, E = vo - v;
+    S = pkv_fma(D, D, E * E);
+    // bound
+    const V m = pkv_fma(r2, c.half, c.half);
+    const V delta = pkv_absmul(iz, pkv_fma(m, p.c2, p.c1));
+    const V rho = m + delta;
+    const V rho2 = rho * rho;
+    const V L = pkv_fma(rho, pkv_fma(rho2, pkv_fma(rho2, c.A4, c.A2), c.cp), c.one);
+    const V q = pkv_fma(rho, c.u13, delta);
+    const V g = pkv_fma(L * q, c.Fg, c.Cg);
+    lo = pkv_fma(g, c.ntwoT, c.thrLo);
+    hi = pkv_fma(g, pkv_fma(g, c.gk, c.twoT), c.thrHi);
+}
+
+// Host twin of the decision for one point: 1 certified inlier, 0 certified outlier, -1 undecided.
+inline int pnp_pk_decide_host(const PnpPkCam& c, const PnpPkPose& p, float X, float Y, float Z, float uo, float vo) {
+    float S, lo, hi, Zc;
+    pnp_pk_eval<float>(pnp_pk_cam_v<float>(c, 0.0f), pnp_pk_pose_v<float>(p, 0.0f), X, Y, Z, uo, vo, S, lo, hi, Zc);
+    if (!(std::fabs(Zc) >= p.zmin)) return -1;
+    if (S < lo) return 1;
+    if (S > hi) return 0;
+    return -1;
+}
+
+}  // namespace mcv

@@ -17,6 +17,7 @@
 //   mcv_pnp_ap3p         solveAp3p export: one AP3P solve (3 points).
 #include "mcv_common.h"
 #include "hyp_pnp.h"
+#include "pnp_pk.h"
 #include "reduce.h"
 #include "kernels.h"
 #include <cstdlib>
@@ -95,6 +96,168 @@ __global__ __launch_bounds__(256) void mcv_pnp_verify(const PnpPoint* __restrict
         for (int k = 0; k < K; ++k) {
             const float e = pnp_error(cam, R[k], t[k], q.X, q.Y, q.Z, q.u, q.v, FUSED);
             cnt[k] += (uint32_t)__popcll(vm & __builtin_amdgcn_ballot_w64(e <= thr2));
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (valid[k] && cnt[k]) atomicAdd(counts + h0 + k, (int)cnt[k]);
+    }
+}
+
+// Point extents for the prefilter's bound: ext = {max |X|, max |Y|, max |Z|} as the ordered bit
+// patterns of non-negative doubles (atomicMax; zeroed by the caller), inf for a non-finite coordinate.
+__global__ __launch_bounds__(256) void mcv_pnp_extent(const PnpPoint* __restrict__ pts, int N,
+                                                      unsigned long long* __restrict__ ext) {
+    double m0 = 0, m1 = 0, m2 = 0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
+        const PnpPoint q = pts[i];
+        const double x = q.X, y = q.Y, z = q.Z;
+        m0 = x - x == 0 ? fmax(m0, fabs(x)) : __builtin_inf();
+        m1 = y - y == 0 ? fmax(m1, fabs(y)) : __builtin_inf();
+        m2 = z - z == 0 ? fmax(m2, fabs(z)) : __builtin_inf();
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        m0 = fmax(m0, __shfl_xor(m0, off, 64));
+        m1 = fmax(m1, __shfl_xor(m1, off, 64));
+        m2 = fmax(m2, __shfl_xor(m2, off, 64));
+    }
+    __shared__ double sm[4][3];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sm[w][0] = m0; sm[w][1] = m1; sm[w][2] = m2; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        double m = sm[0][threadIdx.x];
+        for (int k = 1; k < 4; ++k) m = fmax(m, sm[k][threadIdx.x]);
+        atomicMax(ext + threadIdx.x, (unsigned long long)__double_as_longlong(m));
+    }
+}
+
+// Exact inlier count of one pose over the 128 points [base, base + 128) n [p0, p1) (two per lane):
+// the reference's fp64 projection + fp32 error (pnp_error). The prefilter's undecided trips.
+__device__ __noinline__ uint32_t pnp_exact_trip(const PnpPoint* __restrict__ pts, int base, int p0, int p1,
+                                                PnpCamera cam, const PnpPose* __restrict__ models, int hk,
+                                                float thr2, bool fused) {
+    const int lane = threadIdx.x & 63;
+    double R[9], t[3];
+    const PnpPose m = models[hk];
+    for (int j = 0; j < 9; ++j) R[j] = m.R[j];
+    for (int j = 0; j < 3; ++j) t[j] = m.t[j];
+    uint32_t c = 0;
+    for (int h = 0; h < 2; ++h) {
+        const int i = base + 2 * lane + h;
+        const bool v = i < p1;
+        const PnpPoint q = pts[v ? i : p0];
+        const bool in = v && pnp_error(cam, R, t, q.X, q.Y, q.Z, q.u, q.v, fused) <= thr2;
+        c += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(in));
+    }
+    return c;
+}
+
+// Certified packed-fp32 sweep (pnp_pk.h): a wave holds K poses (fp32 copies + bound constants, wave-
+// uniform) and streams a chunk of the points two per lane (lane l of a trip reads points base + 2l,
+// base + 2l + 1: 64 contiguous bytes). Per (pose, point pair): the packed projection, the bound, two
+// cuts; a trip whose lanes are all decided adds its certified inliers, a trip with an undecided lane
+// is recorded (LDS event list: trip << 8 | pose mask) and recounted exactly after the sweep. An
+// event-list overflow recounts the wave's chunk exactly. Partial counts by integer atomics.
+static constexpr int kPnpEvents = 192;   // per wave
+
+template <int K>
+__global__ __launch_bounds__(256) void mcv_pnp_verify_pk(const PnpPoint* __restrict__ pts, int N, int chunk,
+                                                         PnpCamera cam, PnpPkCam pc, const PnpPose* __restrict__ models,
+                                                         int* __restrict__ counts, int hypCount, float thr2, bool fused,
+                                                         const double* __restrict__ ext) {
+    static_assert(K <= 8, "pose mask in 8 bits");
+    __shared__ uint32_t events[4][kPnpEvents];
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    const int wib = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int h0 = wave * K;
+    if (h0 >= hypCount) return;
+    const double e3[3] = {ext[0], ext[1], ext[2]};
+    const pkf2 z2 = pkf2{0.0f, 0.0f};
+    PnpPkCamV<pkf2> cv = pnp_pk_cam_v<pkf2>(pc, z2);
+    // the splatted constants live in VGPR pairs: kept as SGPR pairs, every FMA that meets two of them
+    // (or a pose coefficient) would copy one into a VGPR inside the loop
+    asm volatile("" : "+v"(cv.fx), "+v"(cv.fy), "+v"(cv.cx), "+v"(cv.cy), "+v"(cv.k1), "+v"(cv.k2), "+v"(cv.tp1),
+                 "+v"(cv.tp2), "+v"(cv.p1), "+v"(cv.p2), "+v"(cv.A2), "+v"(cv.A4));
+    asm volatile("" : "+v"(cv.cp), "+v"(cv.half), "+v"(cv.u13), "+v"(cv.Fg), "+v"(cv.Cg), "+v"(cv.ntwoT),
+                 "+v"(cv.twoT), "+v"(cv.thrLo), "+v"(cv.thrHi), "+v"(cv.gk), "+v"(cv.one));
+    PnpPkPoseV<pkf2> pp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int hk = h0 + k;
+        valid[k] = hk < hypCount && counts[hk] >= 0;
+        const PnpPose m = models[valid[k] ? hk : h0];
+        PnpPkPose p;
+        pnp_pk_pose(m.R, m.t, e3, p);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) p.R[j] = __builtin_amdgcn_readfirstlane(p.R[j]);   // wave-uniform: SGPRs
+        pp[k] = pnp_pk_pose_v<pkf2>(p, z2);
+        asm volatile("" : "+v"(pp[k].t0), "+v"(pp[k].t1), "+v"(pp[k].t2), "+v"(pp[k].c1), "+v"(pp[k].c2));
+    }
+    uint32_t validMask = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) validMask |= valid[k] ? 1u << k : 0u;
+    const int p0 = blockIdx.y * chunk;
+    const int p1 = min(N, p0 + chunk);
+    uint32_t cnt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cnt[k] = 0;
+    int nev = 0;
+    for (int base = p0; base < p1; base += 128) {
+        const int i0 = base + 2 * lane, i1 = i0 + 1;
+        const bool v0 = i0 < p1, v1 = i1 < p1;
+        const PnpPoint a = pts[v0 ? i0 : p0];
+        const PnpPoint b = pts[v1 ? i1 : p0];
+        const uint64_t vm0 = __builtin_amdgcn_ballot_w64(v0), vm1 = __builtin_amdgcn_ballot_w64(v1);
+        const pkf2 X = pkf2{a.X, b.X}, Y = pkf2{a.Y, b.Y}, Z = pkf2{a.Z, b.Z};
+        const pkf2 U = pkf2{a.u, b.u}, V = pkf2{a.v, b.v};
+        uint32_t und = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            pkf2 S, lo, hi, Zc;
+            pnp_pk_eval<pkf2>(cv, pp[k], X, Y, Z, U, V, S, lo, hi, Zc);
+            const uint64_t d0 = __builtin_amdgcn_ballot_w64(fabsf(Zc.x) >= pp[k].zmin);
+            const uint64_t d1 = __builtin_amdgcn_ballot_w64(fabsf(Zc.y) >= pp[k].zmin);
+            const uint64_t in0 = __builtin_amdgcn_ballot_w64(S.x < lo.x) & d0;
+            const uint64_t in1 = __builtin_amdgcn_ballot_w64(S.y < lo.y) & d1;
+            const uint64_t out0 = __builtin_amdgcn_ballot_w64(S.x > hi.x) & d0;
+            const uint64_t out1 = __builtin_amdgcn_ballot_w64(S.y > hi.y) & d1;
+            const uint64_t u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
+            // branch-free: a trip with an undecided lane adds nothing here (recounted exactly later)
+            const uint32_t bit = u != 0 ? 1u << k : 0u;
+            und |= bit;
+            const uint32_t c = (uint32_t)__popcll(in0 & vm0) + (uint32_t)__popcll(in1 & vm1);
+            cnt[k] += bit ? 0u : c;
+        }
+        und &= validMask;
+        if (__builtin_expect(und != 0, 0)) {
+            if (nev < kPnpEvents && lane == 0) events[wib][nev] = ((uint32_t)((base - p0) >> 7) << 8) | und;
+            ++nev;
+        }
+    }
+    if (nev > kPnpEvents) {
+        // too many undecided trips (a pose outside the bound's domain): exact recount of the chunk
+#pragma unroll 1
+        for (int k = 0; k < K; ++k) {
+            if (!valid[k]) continue;
+            uint32_t c = 0;
+            for (int base = p0; base < p1; base += 128) c += pnp_exact_trip(pts, base, p0, p1, cam, models, h0 + k, thr2, fused);
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk) cnt[kk] = kk == k ? c : cnt[kk];
+        }
+    } else if (nev > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int e = 0; e < nev; ++e) {
+            const uint32_t ev = __builtin_amdgcn_readfirstlane(events[wib][e]);
+            const int base = p0 + (int)(ev >> 8) * 128;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (ev & (1u << k)) cnt[k] += pnp_exact_trip(pts, base, p0, p1, cam, models, h0 + k, thr2, fused);
         }
     }
     if (lane == 0) {
@@ -403,20 +566,27 @@ void launch_pnp_generate(const void* d_pts, int N, const double* cam8, uint64_t 
                            N, to_cam(cam8), seed, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
 }
 
-template <int K>
-static void launch_pnp_verify_k(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts,
-                                int hypCount, float thr2, bool fused, hipStream_t s) {
+// Grid of a pose-wave x point-chunk sweep: waves x chunks >= ~8 waves per SIMD, chunks >= 2048
+// points, chunk a multiple of `align`.
+static void pnp_verify_grid(int N, int hypCount, int K, int align, dim3& grid, int& chunk) {
     const int waves = (hypCount + K - 1) / K;
-    // split the correspondences so that waves x chunks >= ~8 waves per SIMD, chunks >= 2048 points
     int chunks = (8192 + waves - 1) / waves;
     const int maxChunks = (N + 2047) / 2048;
     if (chunks > maxChunks) chunks = maxChunks;
     if (chunks < 1) chunks = 1;
-    int chunk = (N + chunks - 1) / chunks;
-    chunk = (chunk + 63) & ~63;
+    chunk = (N + chunks - 1) / chunks;
+    chunk = (chunk + align - 1) / align * align;
     chunks = (N + chunk - 1) / chunk;
     if (chunks < 1) chunks = 1;
-    const dim3 grid((waves + 3) / 4, chunks);
+    grid = dim3((waves + 3) / 4, chunks);
+}
+
+template <int K>
+static void launch_pnp_verify_k(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts,
+                                int hypCount, float thr2, bool fused, hipStream_t s) {
+    dim3 grid;
+    int chunk;
+    pnp_verify_grid(N, hypCount, K, 64, grid, chunk);
     const PnpPoint* p = (const PnpPoint*)d_pts;
     const PnpPose* m = (const PnpPose*)d_models;
     if (fused)
@@ -427,13 +597,49 @@ static void launch_pnp_verify_k(const void* d_pts, int N, const double* cam8, co
                            hypCount, thr2);
 }
 
-// Poses per wave; MCV_PNP_K selects alternatives for the variant screen only.
+template <int K>
+static void launch_pnp_verify_pk_k(const void* d_pts, int N, const double* cam8, const PnpPkCam& pc,
+                                   const void* d_models, int* d_counts, int hypCount, float thr2, bool fused,
+                                   const double* d_ext, hipStream_t s) {
+    dim3 grid;
+    int chunk;
+    pnp_verify_grid(N, hypCount, K, 128, grid, chunk);
+    hipLaunchKernelGGL((mcv_pnp_verify_pk<K>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
+                       pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
+}
+
+void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s) {
+    (void)hipMemsetAsync(d_ext, 0, 3 * sizeof(double), s);   // errors surface at the caller's hipGetLastError
+    if (N <= 0) return;
+    int blocks = (N + 255) / 256;
+    if (blocks > 256) blocks = 256;
+    hipLaunchKernelGGL(mcv_pnp_extent, dim3(blocks), dim3(256), 0, s, (const PnpPoint*)d_pts, N,
+                       (unsigned long long*)d_ext);
+}
+
+// Poses per wave; MCV_PNP_K selects alternatives for the variant screen only. MCV_PNP_FP64=1 forces
+// the all-fp64 sweep (the certified sweep's comparison point). d_ext = launch_pnp_extent's output.
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
-                       float thr2, bool fused, hipStream_t s) {
+                       float thr2, bool fused, const double* d_ext, hipStream_t s) {
     static const int k = [] {
         const char* e = getenv("MCV_PNP_K");
         return e ? atoi(e) : kVerifyPnpPosesPerWave;
     }();
+    static const bool fp64 = [] {
+        const char* e = getenv("MCV_PNP_FP64");
+        return e && atoi(e) != 0;
+    }();
+    const PnpPkCam pc = pnp_pk_cam_host(cam8, thr2);
+    if (!fp64 && pc.ok && d_ext) {
+        switch (k) {
+            case 2: launch_pnp_verify_pk_k<2>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
+            case 6: launch_pnp_verify_pk_k<6>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
+            case 8: launch_pnp_verify_pk_k<8>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
+            default: launch_pnp_verify_pk_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2,
+                                                                   fused, d_ext, s);
+        }
+        return;
+    }
     switch (k) {
         case 2: launch_pnp_verify_k<2>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s); break;
         case 6: launch_pnp_verify_k<6>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s); break;

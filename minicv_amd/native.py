@@ -147,6 +147,8 @@ SIGNATURES = {
     "mcvHostRealRoots": (_I, [_P, _I, _I, _P]),
     "mcvHostPnP": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
     "mcvHostPnPEpnp": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
+    "mcvHostPnpCert": (_I, [_P, _I, _P, _P, _P, C.c_float, _I, _P, _P]),
+    "mcvTestPnpSweep": (_I, [_P, _I, _P, _P, _I, C.c_float, _I, _I, _P]),
     "mcvHostEpnp5": (None, [_P, _P, _P, _P, _P]),
     "mcvHostSolveAp3p": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _P]),
     "mcvTestPnpHypotheses": (_I, [_P, _I, _P, _U64, _I64, _I, _I, _P, _P]),

@@ -247,3 +247,69 @@ def test_pnp_edge_cases(gpu):
     assert not ok and len(inl) == 0
     with pytest.raises(N.NativeError, match="confidence"):
         opencv.solvePnPRansac(*S.pnp_problem(50, seed=1)[:2], K, confidence=1.0)
+
+
+def _ring_obs(rng, R, t, K, d, W, thr):
+    """Observations on / just inside / just outside the threshold circle of pose (R, t)."""
+    from test_pnp_cert import _project
+    proj = _project(R, t, K, d, W)
+    ang = rng.uniform(0, 2 * np.pi, W.shape[0])
+    rad = thr * (1 + rng.choice([-1e-6, -1e-7, 0.0, 1e-7, 1e-6, 1e-3], W.shape[0]))
+    return proj + np.stack([np.cos(ang), np.sin(ang)], 1) * rad[:, None]
+
+
+def _sweep(L, pts8, c8, poses, thr2, fused, mode):
+    P = np.ascontiguousarray(np.concatenate([np.concatenate([R.ravel(), t]) for R, t in poses]), np.float64)
+    counts = np.zeros(len(poses), np.int32)
+    r = L.mcvTestPnpSweep(pts8.ctypes.data, pts8.shape[0], c8.ctypes.data, P.ctypes.data, len(poses), thr2,
+                          int(fused), int(mode), counts.ctypes.data)
+    assert r == len(poses)
+    return counts
+
+
+@pytest.mark.parametrize("n", [1, 2, 127, 128, 129, 1001, 5000])
+@pytest.mark.parametrize("fused", [False, True])
+def test_pnp_certified_sweep_crafted(native, gpu, oracle, n, fused):
+    """The certified packed-fp32 sweep (default) and the all-fp64 sweep on crafted poses — truth,
+    perturbed, wild (points behind the camera / on its plane), NaN — over observations crafted onto
+    each pose's threshold circle: counts bit-exact against the oracle's exact test per pose."""
+    L = native.lib()
+    rng = np.random.default_rng(n + 7 * fused)
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=n, outlier_frac=0.4, sigma=1.0, dist=DIST)
+    c8 = oracle.cam8(K, d)
+    thr = 2.0
+    thr2 = float(np.float32(thr * thr))
+    poses = [(R, t)]
+    poses += [(S.rotation(rng.normal(size=3), rng.uniform(0, 0.05)) @ R, t + rng.normal(size=3) * 0.05)
+              for _ in range(6)]
+    poses += [(S.rotation(rng.normal(size=3), rng.uniform(0, np.pi)), rng.normal(size=3) * s) for s in (0.1, 3, 30)]
+    poses.append((np.full((3, 3), np.nan), np.zeros(3)))
+    poses.append((np.eye(3), np.array([0.0, 0.0, 1e30])))
+    for obs in (img, _ring_obs(rng, R, t, K, d, W, thr), _ring_obs(rng, *poses[2], K, d, W, thr)):
+        pts8 = oracle.pack_pnp(obs, W)
+        ref = np.array([oracle.pnp_count(pts8, c8, Rp, tp, thr2, fused)[0] for Rp, tp in poses])
+        for mode in (0, 1):
+            np.testing.assert_array_equal(_sweep(L, pts8, c8, poses, thr2, fused, mode), ref)
+
+
+def test_pnp_certified_sweep_event_overflow(native, gpu, oracle):
+    """65536 poses over 30000 points (one point chunk per wave, 235 trips): poses outside the bound's
+    domain (non-finite bound) mark every trip undecided, overflow the wave's event list and take the
+    exact recount of the chunk; ring observations put undecided lanes into ordinary poses' trips."""
+    L = native.lib()
+    rng = np.random.default_rng(3)
+    n = 30000
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=11, outlier_frac=0.5, sigma=1.0, dist=DIST)
+    c8 = oracle.cam8(K, d)
+    thr2 = float(np.float32(4.0))
+    obs = img.copy()
+    ring = _ring_obs(rng, R, t, K, d, W, 2.0)
+    sel = rng.random(n) < 0.02
+    obs[sel] = ring[sel]
+    pts8 = oracle.pack_pnp(obs, W)
+    distinct = [(R, t), (np.eye(3), np.array([0.0, 0.0, 1e30])),
+                (S.rotation(rng.normal(size=3), 0.02) @ R, t + 0.02), (np.full((3, 3), np.nan), np.zeros(3))]
+    ref = np.array([oracle.pnp_count(pts8, c8, Rp, tp, thr2, False)[0] for Rp, tp in distinct])
+    idx = rng.integers(0, len(distinct), 65536)
+    counts = _sweep(L, pts8, c8, [distinct[i] for i in idx], thr2, False, 0)
+    np.testing.assert_array_equal(counts, ref[idx])
