@@ -15,8 +15,9 @@
 //   x = Xc / Zc by v_rcp_f32 (<= 1 ulp) and a multiply: with |Zc32| >= zmin = 2^10 eZ,
 //     |x32 - x| <= delta = |1/Zc32| (c1 + m c2), c1 = max(eX, eY)(1 + 2^-10)(1 + 2^-7),
 //     c2 = 1.6 eZ (1 + 2^-7) (the 1.6 also covers the reciprocal's and the product's rounding,
-//     since eZ / |Zc32| >= 5u); m >= max(|x32|, |y32|) is taken as (1 + r2) / 2 (AM-GM; no abs in
-//     packed arithmetic).
+//     since eZ / |Zc32| >= 5u); m = max(|x32|, |y32|) (two VOP3 v_max_f32 with |.| modifiers per
+//     point pair: packed arithmetic has no abs, and the AM-GM form (1 + r2) / 2 overstates m by
+//     r2 / (2 m) where points project far off-image, which the rho^5 of L then multiplies).
 //   distortion (xd, yd) = x (1 + k1 r2 + k2 r2^2 + 2 p1 y + 2 p2 x) + (p2, p1) r2 (the factored form
 //     evaluated here): on the box |x|, |y| <= rho = m + delta its gradient's row sums are bounded by
 //     L = 1 + rho (8 (|p1| + |p2|) + rho^2 (6 |k1| + 20 |k2| rho^2)), and its fp32 evaluation (depth 8
@@ -138,6 +139,7 @@ MCV_HD float pkv_rcp(float a) {
 #endif
 }
 MCV_HD float pkv_absmul(float a, float b) { return fabsf(a) * b; }
+MCV_HD float pkv_absmax(float a, float b) { return fmaxf(fabsf(a), fabsf(b)); }
 
 #if defined(__HIPCC__)
 typedef float pkf2 __attribute__((ext_vector_type(2)));
@@ -145,74 +147,95 @@ __device__ __forceinline__ pkf2 pkv_fma(pkf2 a, pkf2 b, pkf2 c) { return __built
 __device__ __forceinline__ pkf2 pkv_splat(float c, pkf2) { return pkf2{c, c}; }
 __device__ __forceinline__ pkf2 pkv_rcp(pkf2 a) { return pkf2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)}; }
 __device__ __forceinline__ pkf2 pkv_absmul(pkf2 a, pkf2 b) { return pkf2{fabsf(a.x) * b.x, fabsf(a.y) * b.y}; }
+__device__ __forceinline__ pkf2 pkv_absmax(pkf2 a, pkf2 b) {
+    return pkf2{fmaxf(fabsf(a.x), fabsf(b.x)), fmaxf(fabsf(a.y), fabsf(b.y))};
+}
 #endif
 
-// The launch and pose constants splatted to the evaluation's vector type once, outside the sweep
-// (V = f2: VGPR pairs; no per-use v_mov and no two-scalar operand pairs inside the loop).
+// Coefficient pairs: two different wave-uniform constants in one 64-bit register pair, either half
+// broadcast to both lanes of a packed op by op_sel (no per-use copy). Host twin: a plain struct.
+struct PkPairH { float x, y; };
+MCV_HD PkPairH pkp_make(float a, float b, float) { return PkPairH{a, b}; }
+MCV_HD float pkp_lo(PkPairH p, float) { return p.x; }
+MCV_HD float pkp_hi(PkPairH p, float) { return p.y; }
+template <class V> struct PkPairOf { typedef PkPairH type; };
+#if defined(__HIPCC__)
+__device__ __forceinline__ pkf2 pkp_make(float a, float b, pkf2) { return pkf2{a, b}; }
+__device__ __forceinline__ pkf2 pkp_lo(pkf2 p, pkf2) { return __builtin_shufflevector(p, p, 0, 0); }
+__device__ __forceinline__ pkf2 pkp_hi(pkf2 p, pkf2) { return __builtin_shufflevector(p, p, 1, 1); }
+template <> struct PkPairOf<pkf2> { typedef pkf2 type; };
+#endif
+
+// Launch constants, built once outside the sweep. Constant-bus rule (one scalar operand per VALU
+// op): of two constants that meet in one FMA, one is a splatted vector (VGPR pair on the device),
+// the other comes from a coefficient pair (SGPR pair).
 template <class V>
 struct PnpPkCamV {
-    V fx, fy, cx, cy, k1, k2, tp1, tp2, p1, p2, A2, A4, cp, half, u13, Fg, Cg, ntwoT, twoT, thrLo, thrHi, gk, one;
+    typedef typename PkPairOf<V>::type P;
+    P k2tp1, tp2p1, p2fx, fyA4, cpu13, Fgnt, gkHi;   // {k2, tp1}, {tp2, p1}, {p2, fx}, {fy, A4}, {cp, u13}, {Fg, -twoT}, {gk, thrHi}
+    V k1, cx, cy, A2, Cg, thrLo, twoT, one;
 };
 template <class V>
 MCV_HD PnpPkCamV<V> pnp_pk_cam_v(const PnpPkCam& c, V z) {
     PnpPkCamV<V> v;
-    v.fx = pkv_splat(c.fx, z); v.fy = pkv_splat(c.fy, z); v.cx = pkv_splat(c.cx, z); v.cy = pkv_splat(c.cy, z);
-    v.k1 = pkv_splat(c.k1, z); v.k2 = pkv_splat(c.k2, z); v.tp1 = pkv_splat(c.tp1, z); v.tp2 = pkv_splat(c.tp2, z);
-    v.p1 = pkv_splat(c.p1, z); v.p2 = pkv_splat(c.p2, z); v.A2 = pkv_splat(c.A2, z); v.A4 = pkv_splat(c.A4, z);
-    v.cp = pkv_splat(c.cp, z); v.half = pkv_splat(c.half, z); v.u13 = pkv_splat(c.u13, z); v.Fg = pkv_splat(c.Fg, z);
-    v.Cg = pkv_splat(c.Cg, z); v.ntwoT = pkv_splat(-c.twoT, z); v.twoT = pkv_splat(c.twoT, z);
-    v.thrLo = pkv_splat(c.thrLo, z); v.thrHi = pkv_splat(c.thrHi, z); v.gk = pkv_splat(c.gk, z);
+    v.k2tp1 = pkp_make(c.k2, c.tp1, z); v.tp2p1 = pkp_make(c.tp2, c.p1, z); v.p2fx = pkp_make(c.p2, c.fx, z);
+    v.fyA4 = pkp_make(c.fy, c.A4, z); v.cpu13 = pkp_make(c.cp, c.u13, z); v.Fgnt = pkp_make(c.Fg, -c.twoT, z);
+    v.gkHi = pkp_make(c.gk, c.thrHi, z);
+    v.k1 = pkv_splat(c.k1, z); v.cx = pkv_splat(c.cx, z); v.cy = pkv_splat(c.cy, z); v.A2 = pkv_splat(c.A2, z);
+    v.Cg = pkv_splat(c.Cg, z); v.thrLo = pkv_splat(c.thrLo, z); v.twoT = pkv_splat(c.twoT, z);
     v.one = pkv_splat(1.0f, z);
     return v;
 }
-// Pose: R as scalars (one wave-uniform operand per FMA), t and the bound slopes splatted.
+// Pose: R and c2 as coefficient pairs, t and c1 splatted (each meets a pose coefficient in an FMA).
 template <class V>
 struct PnpPkPoseV {
-    float R[9];
-    V t0, t1, t2, c1, c2;
+    typedef typename PkPairOf<V>::type P;
+    P r01, r23, r45, r67, r8c2;
+    V t0, t1, t2, c1;
     float zmin;
 };
 template <class V>
 MCV_HD PnpPkPoseV<V> pnp_pk_pose_v(const PnpPkPose& p, V z) {
     PnpPkPoseV<V> v;
-    for (int j = 0; j < 9; ++j) v.R[j] = p.R[j];
+    v.r01 = pkp_make(p.R[0], p.R[1], z); v.r23 = pkp_make(p.R[2], p.R[3], z); v.r45 = pkp_make(p.R[4], p.R[5], z);
+    v.r67 = pkp_make(p.R[6], p.R[7], z); v.r8c2 = pkp_make(p.R[8], p.c2, z);
     v.t0 = pkv_splat(p.t[0], z); v.t1 = pkv_splat(p.t[1], z); v.t2 = pkv_splat(p.t[2], z);
-    v.c1 = pkv_splat(p.c1, z); v.c2 = pkv_splat(p.c2, z);
+    v.c1 = pkv_splat(p.c1, z);
     v.zmin = p.zmin;
     return v;
 }
 
 // The certified quantities of one point (V = float) or two points (V = f2) against one pose:
 // S (squared fp32 pixel distance), lo / hi (the two cuts) and Zc (for the domain test |Zc| >= zmin).
-// 20 FMA-class operations + 2 reciprocals + 2 |.|-products per point (halved per point when packed).
+// Per point pair (packed): 40 packed ops, 2 v_rcp_f32, 2 v_max_f32 and 2 v_mul_f32 with |.|.
 template <class V>
 MCV_HD void pnp_pk_eval(const PnpPkCamV<V>& c, const PnpPkPoseV<V>& p, V X, V Y, V Z, V uo, V vo, V& S, V& lo, V& hi,
                         V& Zc) {
-    const V z = X - X;
-    const V Xc = pkv_fma(pkv_splat(p.R[0], z), X, pkv_fma(pkv_splat(p.R[1], z), Y, pkv_fma(pkv_splat(p.R[2], z), Z, p.t0)));
-    const V Yc = pkv_fma(pkv_splat(p.R[3], z), X, pkv_fma(pkv_splat(p.R[4], z), Y, pkv_fma(pkv_splat(p.R[5], z), Z, p.t1)));
-    Zc = pkv_fma(pkv_splat(p.R[6], z), X, pkv_fma(pkv_splat(p.R[7], z), Y, pkv_fma(pkv_splat(p.R[8], z), Z, p.t2)));
+    const V z = X;   // type tag only
+    const V Xc = pkv_fma(pkp_lo(p.r01, z), X, pkv_fma(pkp_hi(p.r01, z), Y, pkv_fma(pkp_lo(p.r23, z), Z, p.t0)));
+    const V Yc = pkv_fma(pkp_hi(p.r23, z), X, pkv_fma(pkp_lo(p.r45, z), Y, pkv_fma(pkp_hi(p.r45, z), Z, p.t1)));
+    Zc = pkv_fma(pkp_lo(p.r67, z), X, pkv_fma(pkp_hi(p.r67, z), Y, pkv_fma(pkp_lo(p.r8c2, z), Z, p.t2)));
     const V iz = pkv_rcp(Zc);
     const V x = Xc * iz, y = Yc * iz;
     const V r2 = pkv_fma(x, x, y * y);
-    const V cd = pkv_fma(r2, pkv_fma(c.k2, r2, c.k1), c.one);
-    const V w = pkv_fma(c.tp1, y, pkv_fma(c.tp2, x, cd));
-    const V xd = pkv_fma(x, w, c.p2 * r2);
-    const V yd = pkv_fma(y, w, c.p1 * r2);
-    const V u = pkv_fma(c.fx, xd, c.cx);
-    const V v = pkv_fma(c.fy, yd, c.cy);
+    const V cd = pkv_fma(r2, pkv_fma(pkp_lo(c.k2tp1, z), r2, c.k1), c.one);
+    const V w = pkv_fma(pkp_hi(c.k2tp1, z), y, pkv_fma(pkp_lo(c.tp2p1, z), x, cd));
+    const V xd = pkv_fma(x, w, pkp_lo(c.p2fx, z) * r2);
+    const V yd = pkv_fma(y, w, pkp_hi(c.tp2p1, z) * r2);
+    const V u = pkv_fma(pkp_hi(c.p2fx, z), xd, c.cx);
+    const V v = pkv_fma(pkp_lo(c.fyA4, z), yd, c.cy);
     const V D = uo - u, E = vo - v;
     S = pkv_fma(D, D, E * E);
     // bound
-    const V m = pkv_fma(r2, c.half, c.half);
-    const V delta = pkv_absmul(iz, pkv_fma(m, p.c2, p.c1));
+    const V m = pkv_absmax(x, y);
+    const V delta = pkv_absmul(iz, pkv_fma(m, pkp_hi(p.r8c2, z), p.c1));
     const V rho = m + delta;
     const V rho2 = rho * rho;
-    const V L = pkv_fma(rho, pkv_fma(rho2, pkv_fma(rho2, c.A4, c.A2), c.cp), c.one);
-    const V q = pkv_fma(rho, c.u13, delta);
-    const V g = pkv_fma(L * q, c.Fg, c.Cg);
-    lo = pkv_fma(g, c.ntwoT, c.thrLo);
-    hi = pkv_fma(g, pkv_fma(g, c.gk, c.twoT), c.thrHi);
+    const V L = pkv_fma(rho, pkv_fma(rho2, pkv_fma(rho2, pkp_hi(c.fyA4, z), c.A2), pkp_lo(c.cpu13, z)), c.one);
+    const V q = pkv_fma(rho, pkp_hi(c.cpu13, z), delta);
+    const V g = pkv_fma(L * q, pkp_lo(c.Fgnt, z), c.Cg);
+    lo = pkv_fma(g, pkp_hi(c.Fgnt, z), c.thrLo);
+    hi = pkv_fma(g, pkv_fma(g, pkp_lo(c.gkHi, z), c.twoT), pkp_hi(c.gkHi, z));
 }
 
 // Host twin of the decision for one point: 1 certified inlier, 0 certified outlier, -1 undecided.

@@ -163,8 +163,14 @@ __device__ __noinline__ uint32_t pnp_exact_trip(const PnpPoint* __restrict__ pts
 // event-list overflow recounts the wave's chunk exactly. Partial counts by integer atomics.
 static constexpr int kPnpEvents = 192;   // per wave
 
-template <int K>
-__global__ __launch_bounds__(256) void mcv_pnp_verify_pk(const PnpPoint* __restrict__ pts, int N, int chunk,
+// A wave-uniform pair into SGPRs (readfirstlane is an int builtin: bit copies).
+__device__ __forceinline__ pkf2 pk_uniform(pkf2 v) {
+    return pkf2{__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
+                __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y)))};
+}
+
+template <int K, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void mcv_pnp_verify_pk(const PnpPoint* __restrict__ pts, int N, int chunk,
                                                          PnpCamera cam, PnpPkCam pc, const PnpPose* __restrict__ models,
                                                          int* __restrict__ counts, int hypCount, float thr2, bool fused,
                                                          const double* __restrict__ ext) {
@@ -178,12 +184,10 @@ __global__ __launch_bounds__(256) void mcv_pnp_verify_pk(const PnpPoint* __restr
     const double e3[3] = {ext[0], ext[1], ext[2]};
     const pkf2 z2 = pkf2{0.0f, 0.0f};
     PnpPkCamV<pkf2> cv = pnp_pk_cam_v<pkf2>(pc, z2);
-    // the splatted constants live in VGPR pairs: kept as SGPR pairs, every FMA that meets two of them
-    // (or a pose coefficient) would copy one into a VGPR inside the loop
-    asm volatile("" : "+v"(cv.fx), "+v"(cv.fy), "+v"(cv.cx), "+v"(cv.cy), "+v"(cv.k1), "+v"(cv.k2), "+v"(cv.tp1),
-                 "+v"(cv.tp2), "+v"(cv.p1), "+v"(cv.p2), "+v"(cv.A2), "+v"(cv.A4));
-    asm volatile("" : "+v"(cv.cp), "+v"(cv.half), "+v"(cv.u13), "+v"(cv.Fg), "+v"(cv.Cg), "+v"(cv.ntwoT),
-                 "+v"(cv.twoT), "+v"(cv.thrLo), "+v"(cv.thrHi), "+v"(cv.gk), "+v"(cv.one));
+    asm volatile("" : "+v"(cv.k1), "+v"(cv.cx), "+v"(cv.cy), "+v"(cv.A2), "+v"(cv.Cg), "+v"(cv.thrLo), "+v"(cv.twoT));
+    cv.k2tp1 = pk_uniform(cv.k2tp1); cv.tp2p1 = pk_uniform(cv.tp2p1); cv.p2fx = pk_uniform(cv.p2fx);
+    cv.fyA4 = pk_uniform(cv.fyA4); cv.cpu13 = pk_uniform(cv.cpu13); cv.Fgnt = pk_uniform(cv.Fgnt);
+    cv.gkHi = pk_uniform(cv.gkHi);
     PnpPkPoseV<pkf2> pp[K];
     bool valid[K];
 #pragma unroll
@@ -193,10 +197,14 @@ __global__ __launch_bounds__(256) void mcv_pnp_verify_pk(const PnpPoint* __restr
         const PnpPose m = models[valid[k] ? hk : h0];
         PnpPkPose p;
         pnp_pk_pose(m.R, m.t, e3, p);
-#pragma unroll
-        for (int j = 0; j < 9; ++j) p.R[j] = __builtin_amdgcn_readfirstlane(p.R[j]);   // wave-uniform: SGPRs
         pp[k] = pnp_pk_pose_v<pkf2>(p, z2);
-        asm volatile("" : "+v"(pp[k].t0), "+v"(pp[k].t1), "+v"(pp[k].t2), "+v"(pp[k].c1), "+v"(pp[k].c2));
+        pp[k].zmin = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(pp[k].zmin)));
+        asm volatile("" : "+v"(pp[k].t0), "+v"(pp[k].t1), "+v"(pp[k].t2), "+v"(pp[k].c1));
+        // pose coefficient pairs in SGPRs, read through op_sel. (K = 4 poses' pairs plus the ballot masks
+        // of their interleaved tests overflow the SGPR file by ~15 spilled dwords per trip; the VGPR-pair
+        // placement that avoids it measured slower: 1.92 vs 1.79 ms at the PnP bench)
+        pp[k].r01 = pk_uniform(pp[k].r01); pp[k].r23 = pk_uniform(pp[k].r23); pp[k].r45 = pk_uniform(pp[k].r45);
+        pp[k].r67 = pk_uniform(pp[k].r67); pp[k].r8c2 = pk_uniform(pp[k].r8c2);
     }
     uint32_t validMask = 0;
 #pragma unroll
@@ -216,8 +224,11 @@ __global__ __launch_bounds__(256) void mcv_pnp_verify_pk(const PnpPoint* __restr
         const pkf2 X = pkf2{a.X, b.X}, Y = pkf2{a.Y, b.Y}, Z = pkf2{a.Z, b.Z};
         const pkf2 U = pkf2{a.u, b.u}, V = pkf2{a.v, b.v};
         uint32_t und = 0;
+        asm volatile("" : "+s"(cv.k2tp1), "+s"(cv.tp2p1), "+s"(cv.p2fx), "+s"(cv.fyA4), "+s"(cv.cpu13), "+s"(cv.Fgnt),
+                     "+s"(cv.gkHi));
 #pragma unroll
         for (int k = 0; k < K; ++k) {
+            asm volatile("" : "+s"(pp[k].r01), "+s"(pp[k].r23), "+s"(pp[k].r45), "+s"(pp[k].r67), "+s"(pp[k].r8c2));
             pkf2 S, lo, hi, Zc;
             pnp_pk_eval<pkf2>(cv, pp[k], X, Y, Z, U, V, S, lo, hi, Zc);
             const uint64_t d0 = __builtin_amdgcn_ballot_w64(fabsf(Zc.x) >= pp[k].zmin);
@@ -604,7 +615,21 @@ static void launch_pnp_verify_pk_k(const void* d_pts, int N, const double* cam8,
     dim3 grid;
     int chunk;
     pnp_verify_grid(N, hypCount, K, 128, grid, chunk);
-    hipLaunchKernelGGL((mcv_pnp_verify_pk<K>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
+    static const int wpe = [] {
+        const char* e = getenv("MCV_PNP_WPE");
+        return e ? atoi(e) : 3;
+    }();
+    if (wpe >= 5)
+        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 5>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
+                           pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
+    else if (wpe == 4)
+        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 4>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
+                           pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
+    else if (wpe == 3)
+        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
+                           pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
+    else
+    hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 2>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
                        pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
 }
 
