@@ -6,10 +6,11 @@
 // Semantics restated from OpenCV 4.x calib3d [ext, unverifiable here; SURVEY.md §8a row a9]:
 //   run8Point: centre + scale each point set, linear system (x2,1)^T F (x1,1) = 0, null vector,
 //   rank 2 by zeroing the smallest singular value, de-normalise, F *= 1/F22 if |F22| > FLT_EPSILON.
-// Differences: with exactly 8 points the 8x9 system has a 1-D null space, solved
-// with f22 = 1 by Gaussian elimination (partial pivoting) instead of a 9x9 eigen-decomposition;
-// normalisation uses the mean absolute deviation (no sqrt); rank 2 via the eigenvector of the
-// smallest eigenvalue of F^T F (3x3 cyclic Jacobi), F <- F (I - v v^T) = U diag(s1, s2, 0) V^T.
+// Restated as run8Point: centroid + sqrt(2) / mean Euclidean distance normalisation, rank 2 through
+// SVD::compute (JacobiSVDImpl_) with w[2] = 0, T2^T F0 T1, F *= 1/F22.
+// Difference: with exactly 8 points the 8x9 system has a 1-D null space, solved with
+// f22 = 1 by Gaussian elimination (partial pivoting) instead of the 9x9 eigen-decomposition of A^T A
+// (the same null vector up to rounding; 65536 hypotheses per call).
 // Errors: MCV_FERR_SAMPSON = first-order geometric error x2'Fx1^2 / (|Fx1|_12^2 + |F'x2|_12^2)
 // (OpenCV EMEstimatorCallback::computeError's formula), MCV_FERR_EPIPOLAR = OpenCV
 // FMEstimatorCallback::computeError (max of the two squared point-to-epipolar-line distances);
@@ -18,6 +19,7 @@
 
 #include "mcv_common.h"
 #include "hyp_homography.h"   // det3, mat3_mul, have_collinear (point-set checks)
+#include "epnp.h"             // jacobi_svd (JacobiSVDImpl_)
 
 namespace mcv {
 
@@ -78,42 +80,54 @@ MCV_HD void jacobi3(double* A, double* V) {
     }
 }
 
-// Rank-2 projection F <- F - (F v)(v^T), v = eigenvector of F^T F with the smallest eigenvalue.
+// run8Point's rank-2 step: SVD::compute(F0, w, U, Vt) — JacobiSVDImpl_ on F0^T (jacobi_svd, epnp.h),
+// U = the transposed left-vector rows — then w[2] = 0 and F0 = U * diag(w) * Vt as two Matx products
+// (s = 0; s += a(i,k) b(k,j) in k order).
 MCV_HD void f_rank2(double* F) {
-    double M[9];
+    double At[3][3];
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) M[3 * i + j] = F[i] * F[j] + F[3 + i] * F[3 + j] + F[6 + i] * F[6 + j];
-    double V[9];
-    jacobi3(M, V);
-    // eigenvector (column of V) of the smallest eigenvalue; first minimum on ties
-    const bool m1 = M[4] < M[0];
-    const double dmin = m1 ? M[4] : M[0];
-    const bool m2 = M[8] < dmin;
-    const double v0 = m2 ? V[2] : (m1 ? V[1] : V[0]);
-    const double v1 = m2 ? V[5] : (m1 ? V[4] : V[3]);
-    const double v2 = m2 ? V[8] : (m1 ? V[7] : V[6]);
-    for (int i = 0; i < 3; ++i) {
-        const double w = F[3 * i] * v0 + F[3 * i + 1] * v1 + F[3 * i + 2] * v2;
-        F[3 * i + 0] = F[3 * i + 0] - w * v0;
-        F[3 * i + 1] = F[3 * i + 1] - w * v1;
-        F[3 * i + 2] = F[3 * i + 2] - w * v2;
-    }
+        for (int j = 0; j < 3; ++j) At[i][j] = F[3 * j + i];
+    double w[3], Vt[3][3];
+    jacobi_svd<3, 3>(At, w, Vt);
+    w[2] = 0.;
+    double UD[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double acc = 0;
+            for (int k = 0; k < 3; ++k) acc += At[k][i] * (k == j ? w[j] : 0.0);   // U(i, k) = At[k][i]
+            UD[i][j] = acc;
+        }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double acc = 0;
+            for (int k = 0; k < 3; ++k) acc += UD[i][k] * Vt[k][j];
+            F[3 * i + j] = acc;
+        }
 }
 
-// Normalising transform of a point set: centroid + mean absolute deviation per axis.
-// T = [[sx, 0, -sx cx], [0, sy, -sy cy], [0, 0, 1]]. Returns false if degenerate.
+// run8Point's normalising transform of a point set: centroid (the sum times t = 1 / count), mean
+// Euclidean distance to it (norm(Point2d) summed, times t), scale = sqrt(2) / that distance, the same
+// for both axes. T = [[s, 0, -s cx], [0, s, -s cy], [0, 0, 1]]. false when the distance is below
+// FLT_EPSILON (run8Point returns 0).
 template <int M>
 MCV_HD bool f_norm(const float* x, const float* y, double* cx, double* cy, double* sx, double* sy) {
     double mx = 0, my = 0;
 #pragma unroll
     for (int i = 0; i < M; ++i) { mx += (double)x[i]; my += (double)y[i]; }
-    mx /= M; my /= M;
-    double ax = 0, ay = 0;
+    const double t = 1. / M;
+    mx *= t;
+    my *= t;
+    double sc = 0;
 #pragma unroll
-    for (int i = 0; i < M; ++i) { ax += fabs((double)x[i] - mx); ay += fabs((double)y[i] - my); }
-    if (fabs(ax) < kDblEpsilon || fabs(ay) < kDblEpsilon) return false;
+    for (int i = 0; i < M; ++i) {
+        const double dx = (double)x[i] - mx, dy = (double)y[i] - my;
+        sc += sqrt(dx * dx + dy * dy);
+    }
+    sc *= t;
+    if (sc < (double)kFltEpsilon) return false;
+    sc = sqrt(2.) / sc;
     *cx = mx; *cy = my;
-    *sx = M / ax; *sy = M / ay;
+    *sx = sc; *sy = sc;
     return true;
 }
 

@@ -71,6 +71,9 @@ void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_co
 void launch_abs_bound4(const void* d_pts4, bool fp64, int N, double* d_bb, float* d_out32, hipStream_t s);
 void launch_f_mask(const float* d_pts4, int N, const double* F9, float thr2, int kind, uint8_t* d_mask, int* d_count,
                    hipStream_t s);
+// c4 = {c2x, c2y, c1x, c1y}; d_out = {sum |p2 - c2|, sum |p1 - c1|} (Euclidean).
+void f_reduce_eucdev(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, double* d_part,
+                     double* d_out, hipStream_t s);
 void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,
                   double* d_part, double* d_out, hipStream_t s);
 

@@ -394,6 +394,25 @@ void launch_f_mask(const float* d_pts4, int N, const double* F9, float thr2, int
                        thr2, kind, d_mask, d_count);
 }
 
+// run8Point's scale sums: sum of the Euclidean distances to the centroids, {image 2, image 1}.
+struct OpFEucDev {
+    const float4* pts; const uint8_t* mask; double c2x, c2y, c1x, c1y;
+    __device__ void operator()(int i, double (&a)[2]) const {
+        if (mask && !mask[i]) return;
+        const float4 q = pts[i];
+        const double dx2 = (double)q.z - c2x, dy2 = (double)q.w - c2y;
+        const double dx1 = (double)q.x - c1x, dy1 = (double)q.y - c1y;
+        a[0] += sqrt(dx2 * dx2 + dy2 * dy2);
+        a[1] += sqrt(dx1 * dx1 + dy1 * dy1);
+    }
+};
+
+void f_reduce_eucdev(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, double* d_part,
+                     double* d_out, hipStream_t s) {
+    OpFEucDev op{(const float4*)d_pts4, d_mask, c4[0], c4[1], c4[2], c4[3]};
+    run_reduce<2>(N, op, d_part, d_out, s);
+}
+
 void f_reduce_ata(const float* d_pts4, int N, const uint8_t* d_mask, const double* c4, const double* s4,
                   double* d_part, double* d_out, hipStream_t s) {
     // c4 = {c2x, c2y, c1x, c1y} and s4 likewise (OpSums / OpAbsDev order: dst first)

@@ -43,18 +43,23 @@ int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     return P.h_i.p[0];
 }
 
-// run8Point over all correspondences: GPU fp64 sums (centroids, mean |dev|, A^T A), then the 9x9
-// Jacobi eigen-solve, rank 2 and de-normalisation here. Returns N, or 0 if degenerate.
+// run8Point over all correspondences: GPU fp64 sums (centroids, Euclidean distances, A^T A), then the
+// 9x9 eigen-solve (JacobiImpl_), rank 2 (JacobiSVD) and de-normalisation here. Returns N, or 0 if
+// degenerate (a mean distance below FLT_EPSILON, or one of the 8 largest eigenvalues below
+// DBL_EPSILON).
 int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F) {
     double sums[5];
     reduce_to_host(P, s, 5, sums, [&](double* part, double* red) { h_reduce_sums(d_pts, N, nullptr, part, red, s); });
     const double n = sums[4];
-    double c4[4] = {sums[0] / n, sums[1] / n, sums[2] / n, sums[3] / n};   // c2x, c2y, c1x, c1y
-    double dev[4];
-    reduce_to_host(P, s, 4, dev, [&](double* part, double* red) { h_reduce_absdev(d_pts, N, nullptr, c4, part, red, s); });
-    for (int k = 0; k < 4; ++k)
-        if (std::fabs(dev[k]) < DBL_EPSILON) return 0;
-    double s4[4] = {n / dev[0], n / dev[1], n / dev[2], n / dev[3]};
+    const double t = 1. / n;
+    double c4[4] = {sums[0] * t, sums[1] * t, sums[2] * t, sums[3] * t};   // c2x, c2y, c1x, c1y
+    double dev[2];
+    reduce_to_host(P, s, 2, dev, [&](double* part, double* red) { f_reduce_eucdev(d_pts, N, nullptr, c4, part, red, s); });
+    double scale2 = dev[0] * t, scale1 = dev[1] * t;
+    if (scale1 < FLT_EPSILON || scale2 < FLT_EPSILON) return 0;
+    scale1 = std::sqrt(2.) / scale1;
+    scale2 = std::sqrt(2.) / scale2;
+    double s4[4] = {scale2, scale2, scale1, scale1};
     double ata[45];
     reduce_to_host(P, s, 45, ata, [&](double* part, double* red) { f_reduce_ata(d_pts, N, nullptr, c4, s4, part, red, s); });
     double A[81], w[9], V[81];
@@ -62,6 +67,10 @@ int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F) {
     for (int j = 0; j < 9; ++j)
         for (int k = j; k < 9; ++k) { A[j * 9 + k] = ata[o]; A[k * 9 + j] = ata[o]; ++o; }
     jacobi_eigen(A, 9, w, V);
+    int i = 0;
+    for (; i < 9; ++i)
+        if (std::fabs(w[i]) < DBL_EPSILON) break;
+    if (i < 8) return 0;
     double F0[9];
     for (int k = 0; k < 9; ++k) F0[k] = V[8 * 9 + k];
     f_rank2(F0);

@@ -252,69 +252,111 @@ int orc_update_num_iters(double p, double ep, int modelPoints, int maxIters) {
     return (denom >= 0 || -num >= (double)maxIters * (-denom)) ? maxIters : (int)lrint(num / denom);
 }
 
-/* Jacobi eigen-decomposition of symmetric A (n <= 9): eigenvalues descending in w, eigenvectors
- * as rows of V. Independent implementation (threshold-free cyclic sweeps). */
+/* cv::eigen of a symmetric double matrix: JacobiImpl_<double> of OpenCV 4.x core lapack.cpp [ext],
+ * restated — classical Jacobi, pivot = the largest strict-upper element found through the per-row
+ * (indR) and per-column (indC) maxima (first maximum on ties), stop at |pivot| <= DBL_EPSILON or after
+ * n*n*30 rotations, lapack.cpp's hypot, eigenvalues sorted descending by selection with the rows of V
+ * (the eigenvectors) swapped along. A (n <= 9, row-major) is destroyed. */
+static double lp_hypot(double a, double b) {
+    a = fabs(a);
+    b = fabs(b);
+    if (a > b) { b /= a; return a * sqrt(1 + b * b); }
+    if (b > 0) { a /= b; return b * sqrt(1 + a * a); }
+    return 0;
+}
+
+static int row_argmax(const double* A, int n, int r) {   /* argmax_{c > r} |A[r][c]| */
+    int m = r + 1;
+    double mv = fabs(A[n * r + m]);
+    for (int c = r + 2; c < n; ++c)
+        if (mv < fabs(A[n * r + c])) { mv = fabs(A[n * r + c]); m = c; }
+    return m;
+}
+
+static int col_argmax(const double* A, int n, int c) {   /* argmax_{r < c} |A[r][c]| */
+    int m = 0;
+    double mv = fabs(A[c]);
+    for (int r = 1; r < c; ++r)
+        if (mv < fabs(A[n * r + c])) { mv = fabs(A[n * r + c]); m = r; }
+    return m;
+}
+
 static void jacobi(double* A, int n, double* w, double* V) {
+    int indR[9], indC[9];
     for (int i = 0; i < n * n; ++i) V[i] = (i / n == i % n);
-    for (int sweep = 0; sweep < 100; ++sweep) {
-        double off = 0, dg = 0;
-        for (int i = 0; i < n; ++i) {
-            dg += A[i * n + i] * A[i * n + i];
-            for (int j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
-        }
-        if (off <= DBL_MIN || off <= dg * 1e-32) break;
-        for (int p = 0; p < n; ++p)
-            for (int q = p + 1; q < n; ++q) {
-                double apq = A[p * n + q];
-                if (apq == 0) continue;
-                double theta = (A[q * n + q] - A[p * n + p]) / (2 * apq);
-                double t = (theta >= 0 ? 1. : -1.) / (fabs(theta) + sqrt(theta * theta + 1));
-                double c = 1 / sqrt(t * t + 1), s = t * c;
-                for (int k = 0; k < n; ++k) {
-                    double x = A[k * n + p], y = A[k * n + q];
-                    A[k * n + p] = c * x - s * y; A[k * n + q] = s * x + c * y;
-                }
-                for (int k = 0; k < n; ++k) {
-                    double x = A[p * n + k], y = A[q * n + k];
-                    A[p * n + k] = c * x - s * y; A[q * n + k] = s * x + c * y;
-                }
-                for (int k = 0; k < n; ++k) {
-                    double x = V[p * n + k], y = V[q * n + k];
-                    V[p * n + k] = c * x - s * y; V[q * n + k] = s * x + c * y;
-                }
-            }
+    for (int k = 0; k < n; ++k) {
+        w[k] = A[(n + 1) * k];
+        if (k < n - 1) indR[k] = row_argmax(A, n, k);
+        if (k > 0) indC[k] = col_argmax(A, n, k);
     }
-    for (int i = 0; i < n; ++i) w[i] = A[i * n + i];
-    for (int i = 0; i < n - 1; ++i) {
-        int m = i;
-        for (int j = i + 1; j < n; ++j)
-            if (w[j] > w[m]) m = j;
-        if (m != i) {
-            double t = w[i]; w[i] = w[m]; w[m] = t;
-            for (int k = 0; k < n; ++k) { t = V[i * n + k]; V[i * n + k] = V[m * n + k]; V[m * n + k] = t; }
+    for (int it = 0; n > 1 && it < n * n * 30; ++it) {
+        int k = 0, l;
+        double mv = fabs(A[indR[0]]);
+        for (int i = 1; i < n - 1; ++i)
+            if (mv < fabs(A[n * i + indR[i]])) { mv = fabs(A[n * i + indR[i]]); k = i; }
+        l = indR[k];
+        for (int i = 1; i < n; ++i)
+            if (mv < fabs(A[n * indC[i] + i])) { mv = fabs(A[n * indC[i] + i]); k = indC[i]; l = i; }
+        double p = A[n * k + l];
+        if (fabs(p) <= DBL_EPSILON) break;
+        double y = (w[l] - w[k]) * 0.5;
+        double t = fabs(y) + lp_hypot(p, y);
+        double s = lp_hypot(p, t);
+        double c = t / s;
+        s = p / s;
+        t = (p / t) * p;
+        if (y < 0) { s = -s; t = -t; }
+        A[n * k + l] = 0;
+        w[k] -= t;
+        w[l] += t;
+#define ORC_ROT(v0, v1) do { double a0_ = (v0), b0_ = (v1); (v0) = a0_ * c - b0_ * s; (v1) = a0_ * s + b0_ * c; } while (0)
+        for (int i = 0; i < k; ++i) ORC_ROT(A[n * i + k], A[n * i + l]);
+        for (int i = k + 1; i < l; ++i) ORC_ROT(A[n * k + i], A[n * i + l]);
+        for (int i = l + 1; i < n; ++i) ORC_ROT(A[n * k + i], A[n * l + i]);
+        for (int i = 0; i < n; ++i) ORC_ROT(V[n * k + i], V[n * l + i]);
+#undef ORC_ROT
+        for (int j = 0; j < 2; ++j) {
+            int idx = j == 0 ? k : l;
+            if (idx < n - 1) indR[idx] = row_argmax(A, n, idx);
+            if (idx > 0) indC[idx] = col_argmax(A, n, idx);
+        }
+    }
+    for (int k = 0; k < n - 1; ++k) {
+        int m = k;
+        for (int i = k + 1; i < n; ++i)
+            if (w[m] < w[i]) m = i;
+        if (m != k) {
+            double t = w[k]; w[k] = w[m]; w[m] = t;
+            for (int i = 0; i < n; ++i) { t = V[n * k + i]; V[n * k + i] = V[n * m + i]; V[n * m + i] = t; }
         }
     }
 }
 
+/* cv::solve / cv::invert with DECOMP_EIG: eigen (above) then SVBkSb (u = v = eigenvector rows,
+ * threshold 2 DBL_EPSILON x sum of the signed w). */
 void eig_pinv_apply(const double* A, int n, const double* b, double* x, double* Ainv) {
-    double M[81], w[9], V[81], wmax = 0;
+    double M[81], w[9], V[81], thr = 0;
     memcpy(M, A, sizeof(double) * n * n);
     jacobi(M, n, w, V);
-    for (int i = 0; i < n; ++i) wmax = fabs(w[i]) > wmax ? fabs(w[i]) : wmax;
-    double thr = wmax * n * DBL_EPSILON;
+    for (int i = 0; i < n; ++i) thr += w[i];
+    thr *= DBL_EPSILON * 2;
     if (x) for (int j = 0; j < n; ++j) x[j] = 0;
     if (Ainv) for (int j = 0; j < n * n; ++j) Ainv[j] = 0;
     for (int e = 0; e < n; ++e) {
         if (fabs(w[e]) <= thr) continue;
+        double wi = 1 / w[e];
         if (x) {
             double d = 0;
             for (int k = 0; k < n; ++k) d += V[e * n + k] * b[k];
-            d /= w[e];
-            for (int j = 0; j < n; ++j) x[j] += d * V[e * n + j];
+            d *= wi;
+            for (int j = 0; j < n; ++j) x[j] = x[j] + d * V[e * n + j];
         }
-        if (Ainv)
+        if (Ainv) {
+            double buf[9];
+            for (int j = 0; j < n; ++j) buf[j] = V[e * n + j] * wi;
             for (int i = 0; i < n; ++i)
-                for (int j = 0; j < n; ++j) Ainv[i * n + j] += V[e * n + i] * (1. / w[e]) * V[e * n + j];
+                for (int j = 0; j < n; ++j) Ainv[i * n + j] = Ainv[i * n + j] + V[e * n + i] * buf[j];
+        }
     }
 }
 
@@ -509,8 +551,8 @@ int orc_find_homography(const double* src, const double* dst, int N, double thr,
 /* ------------------------------------------------------------------------------------------
  * Fundamental matrix, 8-point minimal sets (north_star). OpenCV 4.x run8Point / FMEstimatorCallback
  * and EMEstimatorCallback::computeError (Sampson) [ext]; same definition as
- * minicv_amd/csrc/hyp_fundamental.h (mean-|dev| normalisation, f22 = 1 elimination, rank 2 by
- * F (I - v v^T) with v from a cyclic 3x3 Jacobi of F^T F).
+ * minicv_amd/csrc/hyp_fundamental.h (run8Point's sqrt(2) / mean-distance normalisation, f22 = 1
+ * elimination for the null vector, rank 2 through JacobiSVD with w[2] = 0).
  * ---------------------------------------------------------------------------------------- */
 void jacobi3_orc(double* A, double* V) {
     for (int i = 0; i < 9; ++i) V[i] = (i == 0 || i == 4 || i == 8) ? 1.0 : 0.0;
@@ -542,22 +584,26 @@ void jacobi3_orc(double* A, double* V) {
     }
 }
 
+/* run8Point's rank-2 step: cv::SVD::compute(F0) = JacobiSVDImpl_ on F0^T (orc_jsvd), w[2] = 0,
+ * F0 = (U diag(w)) Vt with Matx products (s = 0; s += a b in k order). */
 static void f_rank2_orc(double* F) {
-    double M[9], V[9];
+    double At[9], w[3], Vt[9], UD[9];
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) M[3 * i + j] = F[i] * F[j] + F[3 + i] * F[3 + j] + F[6 + i] * F[6 + j];
-    jacobi3_orc(M, V);
-    int m = 0;
-    double dmin = M[0];
-    if (M[4] < dmin) { m = 1; dmin = M[4]; }
-    if (M[8] < dmin) m = 2;
-    double v0 = V[m], v1 = V[3 + m], v2 = V[6 + m];
-    for (int i = 0; i < 3; ++i) {
-        double w = F[3 * i] * v0 + F[3 * i + 1] * v1 + F[3 * i + 2] * v2;
-        F[3 * i] = F[3 * i] - w * v0;
-        F[3 * i + 1] = F[3 * i + 1] - w * v1;
-        F[3 * i + 2] = F[3 * i + 2] - w * v2;
-    }
+        for (int j = 0; j < 3; ++j) At[3 * i + j] = F[3 * j + i];
+    orc_jsvd(At, w, Vt, 3, 3, 3);
+    w[2] = 0.;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double acc = 0;
+            for (int k = 0; k < 3; ++k) acc += At[3 * k + i] * (k == j ? w[j] : 0.0);
+            UD[3 * i + j] = acc;
+        }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double acc = 0;
+            for (int k = 0; k < 3; ++k) acc += UD[3 * i + k] * Vt[3 * k + j];
+            F[3 * i + j] = acc;
+        }
 }
 
 static int f_denorm_orc(const double* F0, double c1x, double c1y, double s1x, double s1y, double c2x, double c2y,
@@ -576,13 +622,20 @@ static int f_denorm_orc(const double* F0, double c1x, double c1y, double s1x, do
     return 1;
 }
 
+/* run8Point's normalisation: centroid = sum * (1 / m), mean Euclidean distance (times 1 / m),
+ * scale = sqrt(2) / distance for both axes; 0 when the distance is below FLT_EPSILON. */
 static int f_norm8(const float* x, const float* y, int m, double* cx, double* cy, double* sx, double* sy) {
-    double mx = 0, my = 0, ax = 0, ay = 0;
+    double mx = 0, my = 0, d = 0, t = 1. / m;
     for (int i = 0; i < m; ++i) { mx += x[i]; my += y[i]; }
-    mx /= m; my /= m;
-    for (int i = 0; i < m; ++i) { ax += fabs(x[i] - mx); ay += fabs(y[i] - my); }
-    if (fabs(ax) < DBL_EPSILON || fabs(ay) < DBL_EPSILON) return 0;
-    *cx = mx; *cy = my; *sx = m / ax; *sy = m / ay;
+    mx *= t; my *= t;
+    for (int i = 0; i < m; ++i) {
+        double dx = x[i] - mx, dy = y[i] - my;
+        d += sqrt(dx * dx + dy * dy);
+    }
+    d *= t;
+    if (d < FLT_EPSILON) return 0;
+    d = sqrt(2.) / d;
+    *cx = mx; *cy = my; *sx = d; *sy = d;
     return 1;
 }
 
@@ -697,17 +750,20 @@ void orc_f_counts(const float* pts4, int N, uint64_t seed, int64_t hypBegin, int
     }
 }
 
-/* run8Point over all points (FM_8POINT / method 0): same normalisation, 9x9 Jacobi, rank 2. */
+/* run8Point over all points (FM_8POINT / method 0): same normalisation, eigen (JacobiImpl_), the
+ * eigenvalue check, rank 2. */
 static int f_fit_all_orc(const float* pts4, int N, double* F) {
-    double c1x = 0, c1y = 0, c2x = 0, c2y = 0, a1x = 0, a1y = 0, a2x = 0, a2y = 0;
+    double c1x = 0, c1y = 0, c2x = 0, c2y = 0, d1 = 0, d2 = 0, t = 1. / N;
     for (int i = 0; i < N; ++i) { c1x += pts4[4 * i]; c1y += pts4[4 * i + 1]; c2x += pts4[4 * i + 2]; c2y += pts4[4 * i + 3]; }
-    c1x /= N; c1y /= N; c2x /= N; c2y /= N;
+    c1x *= t; c1y *= t; c2x *= t; c2y *= t;
     for (int i = 0; i < N; ++i) {
-        a1x += fabs(pts4[4 * i] - c1x); a1y += fabs(pts4[4 * i + 1] - c1y);
-        a2x += fabs(pts4[4 * i + 2] - c2x); a2y += fabs(pts4[4 * i + 3] - c2y);
+        double ax = pts4[4 * i] - c1x, ay = pts4[4 * i + 1] - c1y, bx = pts4[4 * i + 2] - c2x, by = pts4[4 * i + 3] - c2y;
+        d1 += sqrt(ax * ax + ay * ay);
+        d2 += sqrt(bx * bx + by * by);
     }
-    if (a1x < DBL_EPSILON || a1y < DBL_EPSILON || a2x < DBL_EPSILON || a2y < DBL_EPSILON) return 0;
-    double s1x = N / a1x, s1y = N / a1y, s2x = N / a2x, s2y = N / a2y;
+    d1 *= t; d2 *= t;
+    if (d1 < FLT_EPSILON || d2 < FLT_EPSILON) return 0;
+    double s1x = sqrt(2.) / d1, s1y = s1x, s2x = sqrt(2.) / d2, s2y = s2x;
     double A[81] = {0};
     for (int i = 0; i < N; ++i) {
         double X1 = (pts4[4 * i] - c1x) * s1x, Y1 = (pts4[4 * i + 1] - c1y) * s1y;
@@ -720,6 +776,10 @@ static int f_fit_all_orc(const float* pts4, int N, double* F) {
         for (int k = 0; k < j; ++k) A[j * 9 + k] = A[k * 9 + j];
     double w[9], V[81], F0[9];
     jacobi(A, 9, w, V);
+    int i = 0;
+    for (; i < 9; ++i)
+        if (fabs(w[i]) < DBL_EPSILON) break;
+    if (i < 8) return 0;
     memcpy(F0, V + 72, sizeof(F0));
     f_rank2_orc(F0);
     return f_denorm_orc(F0, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
