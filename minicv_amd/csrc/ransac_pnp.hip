@@ -499,59 +499,91 @@ __global__ __launch_bounds__(256) void mcv_epnp_prep_f64(const double* __restric
     for (int k = 0; k < 3; ++k) pw[3 * (size_t)i + k] = world[3 * (size_t)i + k];
 }
 
-// One thread per (accumulator, block of kEpnpBlock points): the block's terms summed in point
-// order from 0 (the O(n) loops of epnp.cpp); partials part[acc * nblk + blk], summed over blocks
-// in order on the host. Threads of one block index are adjacent, so a wave reads each point once.
+// One workgroup per block of kEpnpBlock points, one lane per accumulator: each accumulator adds its
+// block's terms in point order from 0 (the O(n) loops of epnp.cpp), exactly as a sequential loop
+// would. The per-point inputs of those terms (world / image point, barycentric alphas, the two M
+// rows) are computed for a tile of kEpnpTile points by all lanes into LDS first, so the ordered
+// chains read LDS instead of waiting on a global load per point. Partials part[acc * nblk + blk],
+// summed over blocks in order on the host.
+static constexpr int kEpnpTile = 64;
+
+template <int MODE>
+struct EpnpRec {   // per-point record of a pass
+    static constexpr int W = MODE == kEpnpPassMtm ? 24 : (MODE == kEpnpPassPc ? 4 : (MODE == kEpnpPassAbt ? 7 : 5));
+};
+
 template <int MODE>
 __global__ __launch_bounds__(256) void mcv_epnp_pass(const double* __restrict__ pw, const double* __restrict__ us,
                                                      int n, EpnpPassArgs A, int nacc, int nblk,
                                                      double* __restrict__ part) {
-    const int tid = blockIdx.x * 256 + threadIdx.x;
-    if (tid >= nacc * nblk) return;
-    const int acc = tid % nacc, blk = tid / nacc;
+    constexpr int W = EpnpRec<MODE>::W;
+    __shared__ double rec[kEpnpTile][W];
+    const int blk = blockIdx.x;
     const int i0 = blk * kEpnpBlock;
     const int i1 = min(n, i0 + kEpnpBlock);
-    double s = 0;
-    if (MODE == kEpnpPassSumPw) {
-        for (int i = i0; i < i1; ++i) s += pw[3 * (size_t)i + acc];
-    } else if (MODE == kEpnpPassPw0) {
-        const int a = acc < 3 ? 0 : (acc < 5 ? 1 : 2);
-        const int b = acc < 3 ? acc : (acc < 5 ? acc - 2 : 2);
-        for (int i = i0; i < i1; ++i)
-            s += (pw[3 * (size_t)i + a] - A.c0[a]) * (pw[3 * (size_t)i + b] - A.c0[b]);
+    const int acc = threadIdx.x;
+    int a = 0, b = 0;
+    if (MODE == kEpnpPassPw0) {
+        a = acc < 3 ? 0 : (acc < 5 ? 1 : 2);
+        b = acc < 3 ? acc : (acc < 5 ? acc - 2 : 2);
     } else if (MODE == kEpnpPassMtm) {
-        int a = 0, r = acc;
-        while (r >= 12 - a) { r -= 12 - a; ++a; }
-        const int b = a + r;
-        for (int i = i0; i < i1; ++i) {
-            double al[4], r1[12], r2[12];
-            epnp_alphas(A.C, pw + 3 * (size_t)i, al);
-            epnp_m_rows(al, us[2 * (size_t)i], us[2 * (size_t)i + 1], A.cam, r1, r2);
-            s += r1[a] * r1[b];
-            s += r2[a] * r2[b];
-        }
-    } else if (MODE == kEpnpPassPc) {
-        const int N = acc / 3, j = acc % 3;
-        for (int i = i0; i < i1; ++i) {
-            double al[4], pc[3];
-            epnp_alphas(A.C, pw + 3 * (size_t)i, al);
-            epnp_pc(al, A.ccs[N], pc);
-            s += pc[j];
-        }
-    } else if (MODE == kEpnpPassAbt) {
-        const int N = acc / 9, j = (acc % 9) / 3, k = acc % 3;
-        for (int i = i0; i < i1; ++i) {
-            double al[4], pc[3];
-            epnp_alphas(A.C, pw + 3 * (size_t)i, al);
-            epnp_pc(al, A.ccs[N], pc);
-            s += (pc[j] - A.pc0[N][j]) * (pw[3 * (size_t)i + k] - A.pw0[k]);
-        }
-    } else {
-        for (int i = i0; i < i1; ++i)
-            s += epnp_reproj_term(A.R[acc], A.t[acc], A.cam, pw + 3 * (size_t)i, us[2 * (size_t)i],
-                                  us[2 * (size_t)i + 1]);
+        int r = acc;
+        while (a < 12 && r >= 12 - a) { r -= 12 - a; ++a; }
+        b = a + r;
     }
-    part[(size_t)acc * nblk + blk] = s;
+    double s = 0;
+    for (int t0 = i0; t0 < i1; t0 += kEpnpTile) {
+        const int tn = min(kEpnpTile, i1 - t0);
+        // inputs of the tile's terms, one point per lane
+        for (int j = threadIdx.x; j < tn; j += 256) {
+            const int i = t0 + j;
+            if (MODE == kEpnpPassMtm) {
+                double al[4], r1[12], r2[12];
+                epnp_alphas(A.C, pw + 3 * (size_t)i, al);
+                epnp_m_rows(al, us[2 * (size_t)i], us[2 * (size_t)i + 1], A.cam, r1, r2);
+                for (int k = 0; k < 12; ++k) { rec[j][k] = r1[k]; rec[j][12 + k] = r2[k]; }
+            } else if (MODE == kEpnpPassPc || MODE == kEpnpPassAbt) {
+                double al[4];
+                epnp_alphas(A.C, pw + 3 * (size_t)i, al);
+                for (int k = 0; k < 4; ++k) rec[j][k] = al[k];
+                if (MODE == kEpnpPassAbt)
+                    for (int k = 0; k < 3; ++k) rec[j][4 + k] = pw[3 * (size_t)i + k];
+            } else {
+                for (int k = 0; k < 3; ++k) rec[j][k] = pw[3 * (size_t)i + k];
+                rec[j][3] = us[2 * (size_t)i];
+                rec[j][4] = us[2 * (size_t)i + 1];
+            }
+        }
+        __syncthreads();
+        if (acc < nacc) {
+            for (int j = 0; j < tn; ++j) {
+                if (MODE == kEpnpPassSumPw) {
+                    s += rec[j][acc];
+                } else if (MODE == kEpnpPassPw0) {
+                    s += (rec[j][a] - A.c0[a]) * (rec[j][b] - A.c0[b]);
+                } else if (MODE == kEpnpPassMtm) {
+                    s += rec[j][a] * rec[j][b];
+                    s += rec[j][12 + a] * rec[j][12 + b];
+                } else if (MODE == kEpnpPassPc) {
+                    const double al[4] = {rec[j][0], rec[j][1], rec[j][2], rec[j][3]};
+                    double pc[3];
+                    epnp_pc(al, A.ccs[acc / 3], pc);
+                    s += pc[acc % 3];
+                } else if (MODE == kEpnpPassAbt) {
+                    const int N = acc / 9, jj = (acc % 9) / 3, k = acc % 3;
+                    const double al[4] = {rec[j][0], rec[j][1], rec[j][2], rec[j][3]};
+                    double pc[3];
+                    epnp_pc(al, A.ccs[N], pc);
+                    s += (pc[jj] - A.pc0[N][jj]) * (rec[j][4 + k] - A.pw0[k]);
+                } else {
+                    const double p3[3] = {rec[j][0], rec[j][1], rec[j][2]};
+                    s += epnp_reproj_term(A.R[acc], A.t[acc], A.cam, p3, rec[j][3], rec[j][4]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (acc < nacc) part[(size_t)acc * nblk + blk] = s;
 }
 
 // ---- launchers --------------------------------------------------------------------------------
@@ -701,7 +733,7 @@ void launch_epnp_prep(const void* d_pts, const int* d_idx, const double* d_img, 
 void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, const EpnpPassArgs& a, int nacc,
                       double* d_part, hipStream_t s) {
     const int nblk = (n + kEpnpBlock - 1) / kEpnpBlock;
-    const dim3 grid((nacc * nblk + 255) / 256), block(256);
+    const dim3 grid(nblk), block(256);   // nacc <= 78 accumulators, one lane each
     switch (mode) {
         case kEpnpPassSumPw: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSumPw>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
         case kEpnpPassPw0: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassPw0>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
