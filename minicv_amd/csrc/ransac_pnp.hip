@@ -499,87 +499,95 @@ __global__ __launch_bounds__(256) void mcv_epnp_prep_f64(const double* __restric
     for (int k = 0; k < 3; ++k) pw[3 * (size_t)i + k] = world[3 * (size_t)i + k];
 }
 
+static constexpr int kEpnpTile = 32;
+
+// One (point, accumulator) term of a pass — the body of the corresponding epnp.cpp loop; the MtM
+// pass adds two products per point (r1 and r2 rows), the others one (t[1] unused).
+template <int MODE>
+__device__ __forceinline__ void epnp_pass_term(const double* __restrict__ pw, const double* __restrict__ us,
+                                               const EpnpPassArgs& A, int i, int acc, double (&t)[2]) {
+    const double* p = pw + 3 * (size_t)i;
+    if (MODE == kEpnpPassSumPw) {
+        t[0] = p[acc];
+    } else if (MODE == kEpnpPassPw0) {
+        const int a = acc < 3 ? 0 : (acc < 5 ? 1 : 2);
+        const int b = acc < 3 ? acc : (acc < 5 ? acc - 2 : 2);
+        t[0] = (p[a] - A.c0[a]) * (p[b] - A.c0[b]);
+    } else if (MODE == kEpnpPassMtm) {
+        int a = 0, r = acc;
+        while (a < 12 && r >= 12 - a) { r -= 12 - a; ++a; }
+        const int b = a + r;
+        double al[4], r1[12], r2[12];
+        epnp_alphas(A.C, p, al);
+        epnp_m_rows(al, us[2 * (size_t)i], us[2 * (size_t)i + 1], A.cam, r1, r2);
+        t[0] = r1[a] * r1[b];
+        t[1] = r2[a] * r2[b];
+    } else if (MODE == kEpnpPassPc) {
+        double al[4], pc[3];
+        epnp_alphas(A.C, p, al);
+        epnp_pc(al, A.ccs[acc / 3], pc);
+        t[0] = pc[acc % 3];
+    } else if (MODE == kEpnpPassAbt) {
+        const int N = acc / 9, j = (acc % 9) / 3, k = acc % 3;
+        double al[4], pc[3];
+        epnp_alphas(A.C, p, al);
+        epnp_pc(al, A.ccs[N], pc);
+        t[0] = (pc[j] - A.pc0[N][j]) * (p[k] - A.pw0[k]);
+    } else {
+        t[0] = epnp_reproj_term(A.R[acc], A.t[acc], A.cam, p, us[2 * (size_t)i], us[2 * (size_t)i + 1]);
+    }
+}
+
 // One workgroup per block of kEpnpBlock points, one lane per accumulator: each accumulator adds its
 // block's terms in point order from 0 (the O(n) loops of epnp.cpp), exactly as a sequential loop
-// would. The per-point inputs of those terms (world / image point, barycentric alphas, the two M
-// rows) are computed for a tile of kEpnpTile points by all lanes into LDS first, so the ordered
-// chains read LDS instead of waiting on a global load per point. Partials part[acc * nblk + blk],
-// summed over blocks in order on the host.
-static constexpr int kEpnpTile = 64;
-
-template <int MODE>
-struct EpnpRec {   // per-point record of a pass
-    static constexpr int W = MODE == kEpnpPassMtm ? 24 : (MODE == kEpnpPassPc ? 4 : (MODE == kEpnpPassAbt ? 7 : 5));
-};
-
+// would. The terms of a tile of kEpnpTile points are computed by all lanes in parallel into LDS
+// first, so the ordered chains only add. Partials part[acc * nblk + blk], summed over blocks in
+// order on the host.
 template <int MODE>
 __global__ __launch_bounds__(256) void mcv_epnp_pass(const double* __restrict__ pw, const double* __restrict__ us,
                                                      int n, EpnpPassArgs A, int nacc, int nblk,
                                                      double* __restrict__ part) {
-    constexpr int W = EpnpRec<MODE>::W;
-    __shared__ double rec[kEpnpTile][W];
+    __shared__ double term[kEpnpTile * 78];
+    int ma = 0, mb = 0;   // MtM: the accumulator's (row, column) of the upper triangle
+    if (MODE == kEpnpPassMtm) {
+        int r = threadIdx.x;
+        while (ma < 12 && r >= 12 - ma) { r -= 12 - ma; ++ma; }
+        mb = ma + r;
+    }
     const int blk = blockIdx.x;
     const int i0 = blk * kEpnpBlock;
     const int i1 = min(n, i0 + kEpnpBlock);
     const int acc = threadIdx.x;
-    int a = 0, b = 0;
-    if (MODE == kEpnpPassPw0) {
-        a = acc < 3 ? 0 : (acc < 5 ? 1 : 2);
-        b = acc < 3 ? acc : (acc < 5 ? acc - 2 : 2);
-    } else if (MODE == kEpnpPassMtm) {
-        int r = acc;
-        while (a < 12 && r >= 12 - a) { r -= 12 - a; ++a; }
-        b = a + r;
-    }
     double s = 0;
     for (int t0 = i0; t0 < i1; t0 += kEpnpTile) {
         const int tn = min(kEpnpTile, i1 - t0);
-        // inputs of the tile's terms, one point per lane
-        for (int j = threadIdx.x; j < tn; j += 256) {
-            const int i = t0 + j;
-            if (MODE == kEpnpPassMtm) {
+        if (MODE == kEpnpPassMtm) {
+            // 78 accumulators share a point's two M rows: one lane per point computes them, the
+            // ordered lanes form their products from LDS
+            double* rows = term;   // [kEpnpTile][24]
+            for (int j = threadIdx.x; j < tn; j += 256) {
+                const int i = t0 + j;
                 double al[4], r1[12], r2[12];
                 epnp_alphas(A.C, pw + 3 * (size_t)i, al);
                 epnp_m_rows(al, us[2 * (size_t)i], us[2 * (size_t)i + 1], A.cam, r1, r2);
-                for (int k = 0; k < 12; ++k) { rec[j][k] = r1[k]; rec[j][12 + k] = r2[k]; }
-            } else if (MODE == kEpnpPassPc || MODE == kEpnpPassAbt) {
-                double al[4];
-                epnp_alphas(A.C, pw + 3 * (size_t)i, al);
-                for (int k = 0; k < 4; ++k) rec[j][k] = al[k];
-                if (MODE == kEpnpPassAbt)
-                    for (int k = 0; k < 3; ++k) rec[j][4 + k] = pw[3 * (size_t)i + k];
-            } else {
-                for (int k = 0; k < 3; ++k) rec[j][k] = pw[3 * (size_t)i + k];
-                rec[j][3] = us[2 * (size_t)i];
-                rec[j][4] = us[2 * (size_t)i + 1];
+                for (int k = 0; k < 12; ++k) { rows[j * 24 + k] = r1[k]; rows[j * 24 + 12 + k] = r2[k]; }
             }
-        }
-        __syncthreads();
-        if (acc < nacc) {
-            for (int j = 0; j < tn; ++j) {
-                if (MODE == kEpnpPassSumPw) {
-                    s += rec[j][acc];
-                } else if (MODE == kEpnpPassPw0) {
-                    s += (rec[j][a] - A.c0[a]) * (rec[j][b] - A.c0[b]);
-                } else if (MODE == kEpnpPassMtm) {
-                    s += rec[j][a] * rec[j][b];
-                    s += rec[j][12 + a] * rec[j][12 + b];
-                } else if (MODE == kEpnpPassPc) {
-                    const double al[4] = {rec[j][0], rec[j][1], rec[j][2], rec[j][3]};
-                    double pc[3];
-                    epnp_pc(al, A.ccs[acc / 3], pc);
-                    s += pc[acc % 3];
-                } else if (MODE == kEpnpPassAbt) {
-                    const int N = acc / 9, jj = (acc % 9) / 3, k = acc % 3;
-                    const double al[4] = {rec[j][0], rec[j][1], rec[j][2], rec[j][3]};
-                    double pc[3];
-                    epnp_pc(al, A.ccs[N], pc);
-                    s += (pc[jj] - A.pc0[N][jj]) * (rec[j][4 + k] - A.pw0[k]);
-                } else {
-                    const double p3[3] = {rec[j][0], rec[j][1], rec[j][2]};
-                    s += epnp_reproj_term(A.R[acc], A.t[acc], A.cam, p3, rec[j][3], rec[j][4]);
+            __syncthreads();
+            if (acc < nacc)
+                for (int j = 0; j < tn; ++j) {
+                    s += rows[j * 24 + ma] * rows[j * 24 + mb];
+                    s += rows[j * 24 + 12 + ma] * rows[j * 24 + 12 + mb];
                 }
+        } else {
+            for (int w = threadIdx.x; w < tn * nacc; w += 256) {
+                const int j = w / nacc, a = w - j * nacc;
+                double t[2];
+                epnp_pass_term<MODE>(pw, us, A, t0 + j, a, t);
+                term[j * nacc + a] = t[0];
             }
+            __syncthreads();
+            if (acc < nacc)
+                for (int j = 0; j < tn; ++j) s += term[j * nacc + acc];
         }
         __syncthreads();
     }

@@ -9,8 +9,9 @@ if [[ ${PARTS:-} == *t* ]]; then
       > gpurun_out/pnpsweep/pytest.log 2>&1 || { tail -30 gpurun_out/pnpsweep/pytest.log; exit 1; }
   tail -1 gpurun_out/pnpsweep/pytest.log
 fi
-for v in ${VARIANTS:-"2 3" "2 4" "2 5" "4 3" "4 4"}; do
-  set -- $v
+# VARIANTS: space-separated K_WPE tokens
+for v in ${VARIANTS:-2_3 2_4 2_5 4_3 4_4}; do
+  set -- ${v/_/ }
   timeout -k 10 300 env MCV_PNP_K=$1 MCV_PNP_WPE=$2 python bench.py --workload pnp --steps 5 --warmup 2 --no-cpu-baseline \
       > gpurun_out/pnpsweep/k$1_w$2.log 2>&1 || { tail -5 gpurun_out/pnpsweep/k$1_w$2.log; exit 1; }
   python - gpurun_out/pnpsweep/k$1_w$2.log K=$1 WPE=$2 <<'PY'
