@@ -334,10 +334,13 @@ MCV_HD void epnp_gauss_newton(const double (&L)[6][10], const double (&rho)[6], 
     }
 }
 
-MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBetas& B) {
+// A: the 12 x 12 working matrix of the SVD (caller storage: a register / scratch array on the host,
+// a per-lane LDS slice in the GPU hypothesis kernel).
+typedef double EpnpWs[12][12];
+MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBetas& B, EpnpWs& A) {
     {
         // cvSVD(MtM, D, Ut, 0, MODIFY_A | U_T): Jacobi on transpose(MtM) (= MtM after completeSymm)
-        double A[12][12], w[12];
+        double w[12];
         for (int a = 0; a < 12; ++a)
             for (int b = a; b < 12; ++b) A[a][b] = A[b][a] = mtm[mtm_index(a, b)];
         jacobi_svd<12, 12>(A, w, (double(*)[12])nullptr);
@@ -431,6 +434,11 @@ MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBet
     }
 }
 
+MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBetas& B) {
+    EpnpWs A;
+    epnp_betas(mtm, C, B, A);
+}
+
 // Control points in the camera frame for one beta vector (compute_ccs).
 MCV_HD void epnp_ccs(const EpnpBetas& B, const double (&be)[4], double (&ccs)[4][3]) {
     for (int j = 0; j < 4; ++j)
@@ -486,7 +494,7 @@ MCV_HD int epnp_pick(const double (&rep)[4]) {
 // pw[i] world points, us[i] pixel coordinates (undistorted normalised * f + c).
 template <int NP>
 MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
-                             double (&Rout)[3][3], double (&tout)[3]) {
+                             double (&Rout)[3][3], double (&tout)[3], EpnpWs& ws) {
     EpnpCtrl C;
     {
         double sum[3] = {0, 0, 0};
@@ -518,7 +526,7 @@ MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2
             }
     }
     EpnpBetas B;
-    epnp_betas(mtm, C, B);
+    epnp_betas(mtm, C, B, ws);
     double pw0[3] = {0, 0, 0};
     for (int i = 0; i < NP; ++i)
         for (int j = 0; j < 3; ++j) pw0[j] += pw[i][j];
@@ -551,6 +559,13 @@ MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2
         for (int j = 0; j < 3; ++j) Rout[i][j] = Rs[N][i][j];
         tout[i] = ts[N][i];
     }
+}
+
+template <int NP>
+MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
+                             double (&Rout)[3][3], double (&tout)[3]) {
+    EpnpWs ws;
+    epnp_solve_small<NP>(pw, us, cam, Rout, tout, ws);
 }
 
 }  // namespace mcv

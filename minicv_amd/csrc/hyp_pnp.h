@@ -429,7 +429,7 @@ MCV_HD bool pnp_kind_epnp(int kind) { return kind != 2 && kind != 5; }
 // image points go through undistortPoints with a CV_32F result (the normalised coordinates are
 // rounded to float), epnp::init_points maps them back to pixels (x * fu + uc in double), world
 // points are the float coordinates.
-MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose) {
+MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose, EpnpWs& ws) {
     double pw[5][3], us[5][2];
     for (int i = 0; i < 5; ++i) {
         const PnpPoint p = p5[i];
@@ -441,17 +441,21 @@ MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose) {
     }
     const EpnpCam ec{c.fx, c.fy, c.cx, c.cy};
     double R[3][3], t[3];
-    epnp_solve_small<5>(pw, us, ec, R, t);
+    epnp_solve_small<5>(pw, us, ec, R, t, ws);
     for (int i = 0; i < 3; ++i) {
         for (int j = 0; j < 3; ++j) pose.R[3 * i + j] = R[i][j];
         pose.t[i] = t[i];
     }
 }
+MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose) {
+    EpnpWs ws;
+    pnp_epnp5(c, p5, pose, ws);
+}
 
 // One EPnP hypothesis: 5 distinct indices (Philox stream) -> pnp_epnp5. EPnP always yields a
 // model (possibly non-finite, which then counts no inliers), as solvePnP(EPNP) returns true.
 MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, uint64_t seed, uint64_t hyp,
-                               PnpPose& pose, int* idx_out) {
+                               PnpPose& pose, int* idx_out, EpnpWs& ws) {
     HypStream rs;
     rs.init(seed, hyp);
     int idx[5];
@@ -460,10 +464,15 @@ MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, u
         PnpPoint p5[5];
         for (int i = 0; i < 5; ++i) p5[i] = pts[idx[i]];
         if (idx_out) for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
-        pnp_epnp5(c, p5, pose);
+        pnp_epnp5(c, p5, pose, ws);
         return 1;
     }
     return kStatusNoSample;
+}
+MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, uint64_t seed, uint64_t hyp,
+                               PnpPose& pose, int* idx_out) {
+    EpnpWs ws;
+    return pnp_hypothesis_epnp(pts, N, c, seed, hyp, pose, idx_out, ws);
 }
 
 }  // namespace mcv

@@ -38,6 +38,10 @@ __global__ __launch_bounds__(256) void mcv_pnp_pack(const double* __restrict__ i
     out[i] = p;
 }
 
+// EPnP's 12 x 12 SVD working matrix lives in LDS, one padded slice per lane (a private array with
+// the SVD's data-dependent row pairs went to scratch: 2.4 KB per lane at one wave per SIMD).
+static constexpr int kEpnpWsStride = 145;   // doubles per lane (12 x 12 + 1: bank spread)
+
 template <bool EPNP>
 __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
                                                        uint64_t seed, int64_t hypBegin, int hypCount,
@@ -45,8 +49,14 @@ __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restric
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     PnpPose p;
-    const int st = EPNP ? pnp_hypothesis_epnp(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr)
-                        : pnp_hypothesis(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr);
+    int st;
+    if constexpr (EPNP) {
+        __shared__ double ws[64 * kEpnpWsStride];
+        EpnpWs& A = *reinterpret_cast<EpnpWs*>(ws + (size_t)threadIdx.x * kEpnpWsStride);
+        st = pnp_hypothesis_epnp(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr, A);
+    } else {
+        st = pnp_hypothesis(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr);
+    }
     if (st == 1) {
         models[i] = p;
         counts[i] = 0;
