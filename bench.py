@@ -134,6 +134,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pnp-kind", default="EPNP", choices=["Iterative", "EPNP", "P3P", "DLS", "UPNP", "AP3P"],
                     help="pnp workload: the reference's solverKind (EPNP = its own testPnp, Program.fs:27-32)")
+    ap.add_argument("--fast-minimal", action="store_true",
+                    help="opt-in elimination minimal solver for H / 8-point F (default: OpenCV's cv::eigen runKernel)")
     ap.add_argument("--fused", action="store_true",
                     help="opt-in FMA-contracted inlier error (default: OpenCV's op-by-op order, the reference's)")
     ap.add_argument("--workload", default="homography",
@@ -367,7 +369,7 @@ def bench_ransac(args):
     plan = D.RansacPlan(NL.MODEL_FUNDAMENTAL if fund else NL.MODEL_HOMOGRAPHY, n, hyps)
     total = hyps * world
     cfg = opencv.RansacParams(threshold=THR, confidence=0.995, max_iters=total, seed=F_SEED if fund else SEED,
-                              fixed_iters=True, fused_error=args.fused).to_c()
+                              fixed_iters=True, fused_error=args.fused, fast_minimal=args.fast_minimal).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = torch.zeros(n, dtype=torch.uint8, device=dev)
     red = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -411,6 +413,11 @@ def bench_ransac(args):
     import ctypes as C
     kms = C.c_double(0)
     launches = NL.lib().mcvProfileRead(b"f_verify" if fund else b"h_verify", C.addressof(kms))
+    gms = C.c_double(0)
+    glaunches = NL.lib().mcvProfileRead(b"f_generate" if fund else b"h_generate", C.addressof(gms))
+    minimal = {"solver": "elimination, h22 / f22 = 1 (opt-in MCV_FLAG_FAST_MINIMAL)" if args.fast_minimal else
+               "OpenCV runKernel / run8Point: 9x9 cv::eigen (JacobiImpl_) (default)",
+               "generate_avg_ms": gms.value / max(glaunches, 1)}
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -443,7 +450,9 @@ def bench_ransac(args):
                                        f"(fixed iterations) + refit/LM, best model via RCCL all-reduce",
                            "correspondences": n, "hypotheses_per_gpu": hyps, "threshold": THR,
                            "error": "fused (opt-in)" if args.fused else "OpenCV op-by-op (default)",
+                           "minimal_solver": minimal["solver"],
                            "parallelism": f"hypothesis-sharded dp{world}"},
+                "kernels": {"generate": minimal["generate_avg_ms"], "verify": avg_ms},
                 "roofline": {"bound": "fp32-valu", "achieved": tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
                              "frac": tf / FP32_PEAK_TF, "traffic": traffic,
                              "kernel": hkern, "avg_launch_ms": avg_ms, "launches": launches,
@@ -476,7 +485,9 @@ def bench_ransac(args):
                 "config": {"workload": f"findFundamentalMat 8-point RANSAC, {n} correspondences x {total} "
                                        f"hypotheses per call sharded over {world} GPU(s), fp64 Sampson error",
                            "correspondences": n, "hypotheses_total": total, "threshold": THR,
+                           "minimal_solver": minimal["solver"],
                            "parallelism": f"hypothesis-sharded dp{world}"},
+                "kernels": {"generate": minimal["generate_avg_ms"], "verify": avg_ms},
                 "roofline": {"bound": "fp32-valu", "achieved": tf, "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
                              "frac": tf / FP32_PEAK_TF, "traffic": traffic,
                              "kernel": "mcv_f_verify_pk", "avg_launch_ms": avg_ms, "launches": launches,

@@ -155,6 +155,11 @@ MCV_API mcvBool cvDetectArucoMarkers(char* data, int width, int height, int chan
                                      API) instead of the 8-point default; with errorKind EPIPOLAR it is
                                      cv::findFundamentalMat(FM_RANSAC). Needs N >= 15 (OpenCV switches to
                                      LMeDS below that, not provided) or N == 7 (one solve, first model). */
+#define MCV_FLAG_FAST_MINIMAL 16  /* homography / 8-point fundamental: opt-in minimal solve by 8x8 Gaussian
+                                     elimination with h22 = 1 / f22 = 1 (no eigenvalue check for F).
+                                     Default: OpenCV's own runKernel / run8Point, the 9x9 cv::eigen
+                                     (JacobiImpl_) of LtL / A^T A. The two agree to ~1e-11 relative; the
+                                     default costs ~50x more per hypothesis on the GPU. */
 
 /* F error metric (cfg->errorKind, fundamental only) */
 #define MCV_FERR_SAMPSON   0   /* first-order geometric (Sampson) distance^2 (north_star) */
@@ -366,6 +371,7 @@ MCV_API int  mcvProfileRead(const char* kernel, double* total_ms);
  * (sampler + subset check + minimal solver + error), so CPU tests can check it against the
  * oracle bit for bit without a GPU. Never on a product path.
  * ---------------------------------------------------------------------------------------- */
+#define MCV_HOST_FAST_MINIMAL 0x100   /* or-ed into mcvHostHypothesis' model: the elimination solver */
 MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, uint64_t seed, int64_t hyp,
                               double* model9, float* modelf9, int* sampleIdx);
 /* Device self-test: number of 32-bit patterns w where a reciprocal differs from 1.f/w (mode 0 =

@@ -6,11 +6,9 @@
 // Semantics restated from OpenCV 4.x calib3d [ext, unverifiable here; SURVEY.md §8a row a9]:
 //   run8Point: centre + scale each point set, linear system (x2,1)^T F (x1,1) = 0, null vector,
 //   rank 2 by zeroing the smallest singular value, de-normalise, F *= 1/F22 if |F22| > FLT_EPSILON.
-// Restated as run8Point: centroid + sqrt(2) / mean Euclidean distance normalisation, rank 2 through
-// SVD::compute (JacobiSVDImpl_) with w[2] = 0, T2^T F0 T1, F *= 1/F22.
-// Difference: with exactly 8 points the 8x9 system has a 1-D null space, solved with
-// f22 = 1 by Gaussian elimination (partial pivoting) instead of the 9x9 eigen-decomposition of A^T A
-// (the same null vector up to rounding; 65536 hypotheses per call).
+// Restated as run8Point: centroid + sqrt(2) / mean Euclidean distance normalisation, A = sum r r^T,
+// cv::eigen (JacobiImpl_, jacobi_eig.h) with its eigenvalue check, rank 2 through SVD::compute
+// (JacobiSVDImpl_) with w[2] = 0, T2^T F0 T1, F *= 1/F22.
 // Errors: MCV_FERR_SAMPSON = first-order geometric error x2'Fx1^2 / (|Fx1|_12^2 + |F'x2|_12^2)
 // (OpenCV EMEstimatorCallback::computeError's formula), MCV_FERR_EPIPOLAR = OpenCV
 // FMEstimatorCallback::computeError (max of the two squared point-to-epipolar-line distances);
@@ -20,6 +18,7 @@
 #include "mcv_common.h"
 #include "hyp_homography.h"   // det3, mat3_mul, have_collinear (point-set checks)
 #include "epnp.h"             // jacobi_svd (JacobiSVDImpl_)
+#include "jacobi_eig.h"       // eig9_jacobi (JacobiImpl_)
 
 namespace mcv {
 
@@ -148,8 +147,10 @@ MCV_HD bool f_denormalize(const double* F0, double c1x, double c1y, double s1x, 
     return ok;
 }
 
-// Minimal 8-point solve; a = image-1 points (x1, y1), b = image-2 points (x2, y2).
-MCV_HD bool f_solve8(const float* x1, const float* y1, const float* x2, const float* y2, double* F) {
+// MCV_FLAG_FAST_MINIMAL (opt-in): the 8x9 system's null vector with f22 = 1 by Gaussian elimination
+// (partial pivoting) instead of the eigen-solve of A^T A (no eigenvalue check), then rank 2 and
+// de-normalisation as below.
+MCV_HD bool f_solve8_elim(const float* x1, const float* y1, const float* x2, const float* y2, double* F) {
     double c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y;
     if (!f_norm<8>(x1, y1, &c1x, &c1y, &s1x, &s1y) || !f_norm<8>(x2, y2, &c2x, &c2y, &s2x, &s2y)) return false;
     double a[8][9];
@@ -217,8 +218,63 @@ MCV_HD bool f_solve8(const float* x1, const float* y1, const float* x2, const fl
     return f_denormalize(F0, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
 }
 
+// Minimal 8-point solve = run8Point on the sample; a = image-1 points (x1, y1), b = image-2 points
+// (x2, y2): normalisation, A += r r^T (points in order, upper triangle: A is symmetric exactly),
+// cv::eigen (eig9_jacobi), the eigenvalue check (the first 8 sorted eigenvalues must not fall below
+// DBL_EPSILON in magnitude, else run8Point returns 0), F0 = the last eigenvector, rank 2,
+// de-normalisation.
+template <class WS>
+MCV_HD bool f_solve8(const float* x1, const float* y1, const float* x2, const float* y2, double* F, WS& ws,
+                     bool fast = false) {
+    if (fast) return f_solve8_elim(x1, y1, x2, y2, F);
+    double c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y;
+    if (!f_norm<8>(x1, y1, &c1x, &c1y, &s1x, &s1y) || !f_norm<8>(x2, y2, &c2x, &c2y, &s2x, &s2y)) return false;
+    double dg[9], up[36];
+#pragma unroll
+    for (int e = 0; e < 36; ++e) up[e] = 0.0;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) dg[e] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double X1 = ((double)x1[i] - c1x) * s1x, Y1 = ((double)y1[i] - c1y) * s1y;
+        const double X2 = ((double)x2[i] - c2x) * s2x, Y2 = ((double)y2[i] - c2y) * s2y;
+        const double r[9] = {X2 * X1, X2 * Y1, X2, Y2 * X1, Y2 * Y1, Y2, X1, Y1, 1.0};
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            dg[j] += r[j] * r[j];
+#pragma unroll
+            for (int k = j + 1; k < 9; ++k) up[eig_tri(j, k)] += r[j] * r[k];
+        }
+    }
+    bool fin = true;
+#pragma unroll
+    for (int e = 0; e < 36; ++e) {
+        fin = fin && isfinite(up[e]);
+        ws[kEigA + e] = up[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        fin = fin && isfinite(dg[e]);
+        ws[kEigW + e] = dg[e];
+    }
+    if (!fin) return false;
+    double w[9];
+    const int r = eig9_jacobi(ws, w, 8);
+    bool rank8 = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rank8 = rank8 && !(fabs(w[i]) < kDblEpsilon);
+    if (!rank8) return false;
+    double F0[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) F0[j] = ws[kEigV + 9 * r + j];
+    f_rank2(F0);
+    return f_denormalize(F0, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
+}
+
 // One hypothesis: 1 (model), kStatusNoModel, kStatusNoSample.
-MCV_HD int f_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, double* F, int* idx_out) {
+template <class WS>
+MCV_HD int f_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, double* F, int* idx_out, WS& ws,
+                        bool fast = false) {
     HypStream rs;
     rs.init(seed, hyp);
     float x1[8], y1[8], x2[8], y2[8];
@@ -232,7 +288,7 @@ MCV_HD int f_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, d
         }
         if (have_collinear_last<8>(x1, y1) || have_collinear_last<8>(x2, y2)) continue;
         if (idx_out) for (int i = 0; i < 8; ++i) idx_out[i] = idx[i];
-        return f_solve8(x1, y1, x2, y2, F) ? 1 : kStatusNoModel;
+        return f_solve8(x1, y1, x2, y2, F, ws, fast) ? 1 : kStatusNoModel;
     }
     return kStatusNoSample;
 }

@@ -9,15 +9,15 @@
 //   * subset check   = HomographyEstimatorCallback::checkSubset: haveCollinearPoints on both point
 //                      sets (last point vs lines through earlier pairs, FLT_EPSILON test), then the
 //                      4-triangle orientation-consistency test (Marquez-Neila et al. 2013);
-//   * minimal solver = normalised DLT of runKernel (centroid + mean-|dev| scaling). For exactly 4
-//                      points the 8x9 system has a 1-D null space, solved here with h22 = 1 by 8x8
-//                      Gaussian elimination with partial pivoting instead of the 9x9 Jacobi
-//                      eigen-solve (identical model up to rounding; documented in DESIGN.md §3);
+//   * minimal solver = runKernel itself: centroid + mean-|dev| scaling, the 9x9 LtL, cv::eigen
+//                      (JacobiImpl_, jacobi_eig.h), de-normalisation, 1/H22 (MCV_FLAG_FAST_MINIMAL:
+//                      8x8 elimination with h22 = 1, opt-in);
 //   * error          = HomographyEstimatorCallback::computeError: fp32, model cast to float,
 //                      ww = 1/(h6 x + h7 y + 1), err = dx^2 + dy^2; inlier iff err <= (float)thr^2.
 #pragma once
 
 #include "mcv_common.h"
+#include "jacobi_eig.h"
 
 namespace mcv {
 
@@ -81,9 +81,11 @@ MCV_HD void mat3_mul(const double* A, const double* B, double* C) {
             C[3 * i + j] = A[3 * i + 0] * B[0 * 3 + j] + A[3 * i + 1] * B[1 * 3 + j] + A[3 * i + 2] * B[2 * 3 + j];
 }
 
-// Minimal 4-point homography src -> dst. Returns false when degenerate (zero scale, zero pivot,
-// non-finite result). H: row-major, scaled by 1/H22 (OpenCV convertTo(..., 1./H(2,2))).
-MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const float* dy, double* H) {
+// MCV_FLAG_FAST_MINIMAL (opt-in): runKernel's normalisation, then the 8x8 system (h22 = 1) by
+// Gaussian elimination with partial pivoting instead of the eigen-solve — the same null vector up to
+// the eigen-solve's convergence error (~1e-11 relative), 50x cheaper on the GPU.
+// Returns false when degenerate (zero scale, zero pivot, non-finite result).
+MCV_HD bool h_solve4_elim(const float* sx, const float* sy, const float* dx, const float* dy, double* H) {
     // Normalisation (runKernel): centroids and mean absolute deviations, in double.
     double cMx = 0, cMy = 0, cmx = 0, cmy = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -190,10 +192,112 @@ MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const fl
     return ok;
 }
 
+// Minimal 4-point homography src -> dst = HomographyEstimatorCallback::runKernel on the sample:
+// centroid + mean-|dev| normalisation, LtL[j][k] += Lx[j] Lx[k] + Ly[j] Ly[k] (k >= j, points in
+// order, from +0), cv::eigen (eig9_jacobi, jacobi_eig.h) -> H0 = the eigenvector of the smallest
+// eigenvalue, H = invHnorm H0 Hnorm2 (3x3 gemm order), scaled by 1/H22 (convertTo). Returns false
+// when the scales vanish (runKernel returns 0) or the result is not finite (a non-finite model
+// counts no inlier in OpenCV: the same RANSAC outcome as no model).
+template <class WS>
+MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const float* dy, double* H, WS& ws,
+                     bool fast = false) {
+    if (fast) return h_solve4_elim(sx, sy, dx, dy, H);
+    // Normalisation (runKernel): centroids and mean absolute deviations, in double.
+    double cMx = 0, cMy = 0, cmx = 0, cmy = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 4; ++i) {
+        cmx += (double)dx[i]; cmy += (double)dy[i];
+        cMx += (double)sx[i]; cMy += (double)sy[i];
+    }
+    cmx /= 4; cmy /= 4; cMx /= 4; cMy /= 4;
+    double smx = 0, smy = 0, sMx = 0, sMy = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 4; ++i) {
+        smx += fabs((double)dx[i] - cmx); smy += fabs((double)dy[i] - cmy);
+        sMx += fabs((double)sx[i] - cMx); sMy += fabs((double)sy[i] - cMy);
+    }
+    if (fabs(smx) < kDblEpsilon || fabs(smy) < kDblEpsilon || fabs(sMx) < kDblEpsilon || fabs(sMy) < kDblEpsilon)
+        return false;
+    smx = 4 / smx; smy = 4 / smy; sMx = 4 / sMx; sMy = 4 / sMy;
+
+    // LtL: diagonal -> W slots, strict upper triangle -> packed A slots of the eigen workspace.
+    double dg[9], up[36];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int e = 0; e < 36; ++e) up[e] = 0.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int e = 0; e < 9; ++e) dg[e] = 0.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 4; ++i) {
+        const double x = ((double)dx[i] - cmx) * smx, y = ((double)dy[i] - cmy) * smy;
+        const double X = ((double)sx[i] - cMx) * sMx, Y = ((double)sy[i] - cMy) * sMy;
+        const double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
+        const double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int j = 0; j < 9; ++j) {
+            dg[j] += Lx[j] * Lx[j] + Ly[j] * Ly[j];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+            for (int k = j + 1; k < 9; ++k) up[eig_tri(j, k)] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+        }
+    }
+    bool fin = true;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int e = 0; e < 36; ++e) {
+        fin = fin && isfinite(up[e]);
+        ws[kEigA + e] = up[e];
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int e = 0; e < 9; ++e) {
+        fin = fin && isfinite(dg[e]);
+        ws[kEigW + e] = dg[e];
+    }
+    if (!fin) return false;
+    double w[9];
+    const int r = eig9_jacobi(ws, w, 8);
+    double H0[9];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int j = 0; j < 9; ++j) H0[j] = ws[kEigV + 9 * r + j];
+    const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
+    const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
+    double T[9];
+    mat3_mul(invHnorm, H0, T);
+    mat3_mul(T, Hnorm2, H);
+    const double s = 1. / H[8];
+    bool ok = true;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < 9; ++i) {
+        H[i] = H[i] * s;
+        ok = ok && isfinite(H[i]);
+    }
+    return ok;
+}
+
 // One hypothesis: returns 1 (model written), kStatusNoModel, or kStatusNoSample.
 // pts4: N packed {x, y, x', y'}. idx_out (optional) receives the accepted sample.
+template <class WS>
 MCV_HD int h_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, double* H, HModelF* mf,
-                        int* idx_out) {
+                        int* idx_out, WS& ws, bool fast = false) {
     HypStream rs;
     rs.init(seed, hyp);
     float sx[4], sy[4], dx[4], dy[4];
@@ -209,7 +313,7 @@ MCV_HD int h_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, d
         }
         if (!h_check_subset(sx, sy, dx, dy)) continue;
         if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
-        if (!h_solve4(sx, sy, dx, dy, H)) return kStatusNoModel;
+        if (!h_solve4(sx, sy, dx, dy, H, ws, fast)) return kStatusNoModel;
         bool ok = true;
         for (int i = 0; i < 8; ++i) {
             mf->h[i] = (float)H[i];

@@ -1,0 +1,301 @@
+// jacobi_eig.h — cv::eigen of a 9x9 symmetric matrix exactly as OpenCV 4.x computes it
+// (hal::Jacobi -> JacobiImpl_<double>, core lapack.cpp [ext, restated]) for the minimal solvers
+// of the RANSAC hypothesis kernels: HomographyEstimatorCallback::runKernel (LtL, 4 points) and
+// run8Point (A = sum r r^T, 8 points) take the eigenvector of the smallest eigenvalue.
+//
+// JacobiImpl_ (the same algorithm as linalg.h's host jacobi_eigen, restated here in the form a
+// GPU lane runs): classical Jacobi. The pivot (k, l) is the first maximum |A(i, indR[i])| over
+// rows 0..n-2, then |A(indC[i], i)| over columns 1..n-1 — indR / indC hold per-row / per-column
+// argmaxes of the strict upper triangle and are refreshed only for rows / columns k and l after a
+// rotation (the others go stale, as in OpenCV). Stop when |p| <= DBL_EPSILON or after n*n*30
+// rotations; y = (W[l] - W[k]) / 2, t = |y| + hypot(p, y), s = hypot(p, t), c = t / s, s = p / s,
+// t = (p / t) p, signs flipped for y < 0; lapack.cpp's own hypot (cv_hypot, epnp.h). Only the strict
+// upper triangle is read or written. Then a descending selection sort of W, rows of V swapped along.
+//
+// Layout: the working set is 127 doubles — [0, 36) the strict upper triangle packed by rows
+// (eig_tri), [36, 45) W (the running diagonal), [45, 126) V row-major, a junk slot. On the GPU it lives in LDS,
+// one column per lane of a [element][64 lanes] block (EigWsLane: element e of lane L at
+// lds[e * 64 + L], so a wave's accesses to one element are 64 consecutive doubles — conflict-free
+// ds_read_b64 / ds_write_b64, and a compile-time element index is an immediate offset); the data-
+// dependent (k, l) indexing would otherwise put the matrices in scratch. On the host (twins, the
+// single-lane winner kernels) it is a private array (EigWsLocal). Both run the same code and round
+// identically (-ffp-contract=off; division and sqrt are IEEE on both sides).
+// indR / indC are kept in registers as 4-bit fields of one 32-bit word each. The quotients run
+// gfx950's refined-reciprocal division inside its exact domain (eig_div), the hypot branch-free.
+#pragma once
+
+#include <cstdlib>
+#include "mcv_common.h"
+#include "epnp.h"   // cv_hypot (lapack.cpp's hypot)
+
+namespace mcv {
+
+// [0, 36) strict upper triangle, [36, 45) W, [45, 126) V, 126 = a junk slot (the rotation's
+// branch-free form sends the two skipped indices there).
+static constexpr int kEigA = 0, kEigW = 36, kEigV = 45, kEigJunk = 126, kEigWs = 127;
+// Lanes per hypothesis-kernel block: the 1016-byte working set per lane makes LDS the occupancy
+// limit (160 KB per CU). 39 lanes = 4 blocks per CU, one wave on every SIMD (screened on cfg3:
+// 32 / 39 / 48 / 64 lanes -> 14.9 / 11.5 / 12.5 / 13.9 ms for 2^20 hypotheses); MCV_EIG_LANES =
+// 32 / 48 / 64 re-screens.
+static constexpr int kEigLanes = 39;
+inline int eig_lanes() {   // host: the launchers' screen knob
+    static const int v = [] {
+        const char* e = getenv("MCV_EIG_LANES");
+        return e ? atoi(e) : kEigLanes;
+    }();
+    return v;
+}
+
+// Packed index of A(r, c), r < c < 9: row r starts at 7r - r(r-1)/2 - 1 + (r + 1).
+MCV_HD int eig_row_base(int r) { return 7 * r - ((r * (r - 1)) >> 1) - 1; }
+MCV_HD int eig_tri(int r, int c) { return eig_row_base(r) + c; }
+
+struct EigWsLocal {
+    double d[kEigWs];
+    MCV_HD double& operator[](int e) { return d[e]; }
+};
+
+template <int L = 64>
+struct EigWsLane {
+    double* p;   // &block[lane] of a __shared__ double[kEigWs * L] (L lanes per block)
+    MCV_HD double& operator[](int e) { return p[e * L]; }
+};
+
+// 4-bit fields: indR[i] at field i (i = 0..7), indC[i] at field i - 1 (i = 1..8).
+MCV_HD int eig_nib(uint32_t x, int i) { return (int)((x >> (4 * i)) & 15u); }
+MCV_HD uint32_t eig_set_nib(uint32_t x, int i, int v) {
+    const uint32_t m = 15u << (4 * i);
+    return (x & ~m) | (((uint32_t)v << (4 * i)) & m);
+}
+
+// x / y exactly as the IEEE division. Device: gfx950's refined-reciprocal quotient without the
+// div_scale / div_fixup wrapper (mcv_common.h) inside its proven domain, the IEEE division outside.
+MCV_HD double eig_div(double x, double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double ax = __builtin_fabs(x);
+    if (__builtin_expect(div_f64_refined_domain(y) && (ax == 0.0 || (ax >= 0x1p-900 && ax < 0x1p700)), 1))
+        return div_f64_refined(x, y, rcp_f64_refined(y));
+    return x / y;
+#else
+    return x / y;
+#endif
+}
+
+// lapack.cpp's hypot (cv_hypot) in branch-free form: the same quotient, product and root for every
+// input (a > b: b / a, a sqrt(1 + r^2); b > 0: a / b, b sqrt(1 + r^2); else 0).
+MCV_HD double eig_hypot(double a, double b) {
+    a = __builtin_fabs(a);
+    b = __builtin_fabs(b);
+    const bool ag = a > b;
+    const double hi = ag ? a : b, lo = ag ? b : a;
+    const double r = eig_div(lo, hi);
+    const double h = hi * __builtin_sqrt(1 + r * r);
+    return (ag || b > 0) ? h : 0.0;
+}
+
+// First maximum of a candidate pair in scan order: the later one wins only when strictly greater.
+MCV_HD void eig_pick(double& v, int& kl, double v2, int kl2) {
+    const bool t = v < v2;
+    v = t ? v2 : v;
+    kl = t ? kl2 : kl;
+}
+
+// cv::eigen on the 9x9 symmetric matrix whose strict upper triangle (packed) and diagonal the caller
+// stored at ws[kEigA..] and ws[kEigW..]. On return w[] holds the eigenvalues in descending order and
+// the function returns the workspace row of V (the original row index) that the sort moved to
+// position `pos` — V row `pos` of OpenCV's result is ws[kEigV + 9 * ret + j]. Returns the rotation
+// count through *iters when non-null (diagnostics).
+template <class WS>
+MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
+    constexpr int n = 9;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < n * n; ++i) ws[kEigV + i] = (i / n == i % n) ? 1.0 : 0.0;
+    uint32_t indR = 0, indC = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int k = 0; k < n; ++k) {
+        if (k < n - 1) {
+            int m = k + 1;
+            double mv = __builtin_fabs(ws[eig_tri(k, k + 1)]);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+            for (int i = k + 2; i < n; ++i) {
+                const double val = __builtin_fabs(ws[eig_tri(k, i)]);
+                if (mv < val) mv = val, m = i;
+            }
+            indR = eig_set_nib(indR, k, m);
+        }
+        if (k > 0) {
+            int m = 0;
+            double mv = __builtin_fabs(ws[eig_tri(0, k)]);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+            for (int i = 1; i < k; ++i) {
+                const double val = __builtin_fabs(ws[eig_tri(i, k)]);
+                if (mv < val) mv = val, m = i;
+            }
+            indC = eig_set_nib(indC, k - 1, m);
+        }
+    }
+    int it = 0;
+    for (; it < n * n * 30; ++it) {
+        // pivot (k, l): the first maximum over the 16 candidates in OpenCV's scan order (rows 0..7
+        // through indR, then columns 1..8 through indC), as a pairwise tree (first wins on ties)
+        double cv[16];
+        int ck[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = 0; i < n - 1; ++i) {
+            const int c = eig_nib(indR, i);
+            cv[i] = __builtin_fabs(ws[eig_row_base(i) + c]);
+            ck[i] = i * 16 + c;
+        }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = 1; i < n; ++i) {
+            const int r = eig_nib(indC, i - 1);
+            cv[7 + i] = __builtin_fabs(ws[eig_row_base(r) + i]);
+            ck[7 + i] = r * 16 + i;
+        }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int h = 1; h < 16; h *= 2)
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+            for (int i = 0; i < 16; i += 2 * h) eig_pick(cv[i], ck[i], cv[i + h], ck[i + h]);
+        const int k = ck[0] >> 4, l = ck[0] & 15;
+        const int ekl = eig_tri(k, l);
+        const double p = ws[ekl];
+        if (__builtin_fabs(p) <= kDblEpsilon) break;
+        // every operand of the rotation is read before anything is written back (the reads do not
+        // depend on the scalar chain, so their LDS latency hides behind it): W[k], W[l], for every
+        // other i the pair (A(k|i), A(l|i)) of the upper triangle (i = k, l read and write the junk
+        // slot), and V rows k and l
+        const double wk = ws[kEigW + k], wl = ws[kEigW + l];
+        const int rk = eig_row_base(k), rl = eig_row_base(l);
+        int e0[n], e1[n];
+        double a0[n], b0[n], va[n], vb[n];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = 0; i < n; ++i) {
+            // branch-free index selection (a select of LDS addresses feeding a load is otherwise
+            // turned into control flow around each load)
+            const int mk = -(int)(i < k), ml = -(int)(i < l), ms = -(int)(i == k || i == l);
+            const int x0 = ((eig_row_base(i) + k) & mk) | ((rk + i) & ~mk);
+            const int x1 = ((eig_row_base(i) + l) & ml) | ((rl + i) & ~ml);
+            e0[i] = (kEigJunk & ms) | (x0 & ~ms);
+            e1[i] = (kEigJunk & ms) | (x1 & ~ms);
+            a0[i] = ws[e0[i]];
+            b0[i] = ws[e1[i]];
+        }
+        const int vk = kEigV + n * k, vl = kEigV + n * l;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = 0; i < n; ++i) {
+            va[i] = ws[vk + i];
+            vb[i] = ws[vl + i];
+        }
+        const double y = (wl - wk) * 0.5;
+        double t = __builtin_fabs(y) + eig_hypot(p, y);
+        double s = eig_hypot(p, t);
+        const double c = eig_div(t, s);
+        s = eig_div(p, s);
+        t = eig_div(p, t) * p;
+        if (y < 0) s = -s, t = -t;
+        ws[ekl] = 0;
+        ws[kEigW + k] = wk - t;
+        ws[kEigW + l] = wl + t;
+        // rotate rows and columns k and l; nk / nl keep the new values (A(k, l) = 0 at i = l / i = k)
+        // for the rescans
+        double nk[n], nl[n];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = 0; i < n; ++i) {
+            const bool skip = i == k || i == l;
+            const double v0 = a0[i] * c - b0[i] * s, v1 = a0[i] * s + b0[i] * c;
+            ws[e0[i]] = v0;
+            ws[e1[i]] = v1;
+            nk[i] = skip ? 0.0 : v0;
+            nl[i] = skip ? 0.0 : v1;
+        }
+        // rotate eigenvectors
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = 0; i < n; ++i) {
+            ws[vk + i] = va[i] * c - vb[i] * s;
+            ws[vl + i] = va[i] * s + vb[i] * c;
+        }
+        // refresh indR / indC of rows and columns k and l (first maximum; every |value| >= 0 beats
+        // the -1 start, so the first in-range element is taken unconditionally as in OpenCV)
+        int mRk = 0, mCk = 0, mRl = 0, mCl = 0;
+        double vRk = -1, vCk = -1, vRl = -1, vCl = -1;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = 0; i < n; ++i) {
+            const double ak = __builtin_fabs(nk[i]), al = __builtin_fabs(nl[i]);
+            const bool tRk = i > k && vRk < ak, tCk = i < k && vCk < ak;
+            const bool tRl = i > l && vRl < al, tCl = i < l && vCl < al;
+            vRk = tRk ? ak : vRk; mRk = tRk ? i : mRk;
+            vCk = tCk ? ak : vCk; mCk = tCk ? i : mCk;
+            vRl = tRl ? al : vRl; mRl = tRl ? i : mRl;
+            vCl = tCl ? al : vCl; mCl = tCl ? i : mCl;
+        }
+        if (k < n - 1) indR = eig_set_nib(indR, k, mRk);
+        if (k > 0) indC = eig_set_nib(indC, k - 1, mCk);
+        if (l < n - 1) indR = eig_set_nib(indR, l, mRl);
+        indC = eig_set_nib(indC, l - 1, mCl);   // l >= 1
+    }
+    if (iters) *iters = it;
+    // descending selection sort, rows of V swapped along (tracked as a permutation)
+    int perm[n];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < n; ++i) {
+        w[i] = ws[kEigW + i];
+        perm[i] = i;
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int k = 0; k < n - 1; ++k) {
+        int m = k;
+        double wm = w[k];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = k + 1; i < n; ++i)
+            if (wm < w[i]) m = i, wm = w[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int i = k + 1; i < n; ++i)
+            if (i == m) {
+                const double tw = w[k]; w[k] = w[i]; w[i] = tw;
+                const int tp = perm[k]; perm[k] = perm[i]; perm[i] = tp;
+            }
+    }
+    int r = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int i = 0; i < n; ++i)
+        if (i == pos) r = perm[i];
+    return r;
+}
+
+}  // namespace mcv

@@ -21,11 +21,11 @@ struct HOneOut {
     int status;
     int idx[4];
 };
-void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOut* d_out, hipStream_t s);
+void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast);
 void launch_h_mask_one(const float* d_pts4, int N, const HOneOut* d_one, float thr2, bool fused, uint8_t* d_mask,
                        int* d_count, hipStream_t s);
 void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
-                       int* d_counts, hipStream_t s);
+                       int* d_counts, hipStream_t s, bool fast);
 void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
                      bool fused, const float* d_bbox, hipStream_t s);
 void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s);
@@ -57,8 +57,8 @@ struct FOneOut {
     int idx[8];
 };
 void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
-                       int* d_counts, hipStream_t s);
-void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s);
+                       int* d_counts, hipStream_t s, bool fast);
+void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s, bool fast);
 // 7-point (MCV_FLAG_SEVEN_POINT): 3 model slots per hypothesis (models[3h + s], counts[3h + s]).
 void launch_f7_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
                         int* d_counts, hipStream_t s);

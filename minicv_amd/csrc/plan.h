@@ -111,7 +111,8 @@ int f_error_kind(const RansacConfig& cfg);
 int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* F, uint8_t* d_mask,
                hipStream_t s);
 int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F);
-int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F9, float* Ff9, int* sampleIdx);
+int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F9, float* Ff9, int* sampleIdx,
+                      bool fast);
 
 // PnP family (ransac_pnp.hip / pnp_host.cpp)
 void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,

@@ -24,13 +24,24 @@
 
 namespace mcv {
 
-__global__ __launch_bounds__(256) void mcv_f_generate(const float* __restrict__ pts4, int N, uint64_t seed,
-                                                      int64_t hypBegin, int hypCount, FModelD* __restrict__ models,
-                                                      int* __restrict__ counts) {
+// One lane per hypothesis; run8Point's eigen-solve working set in LDS, one column per lane.
+// FAST = MCV_FLAG_FAST_MINIMAL (no workspace).
+template <bool FAST, int L = kEigLanes>
+__global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __restrict__ pts4, int N, uint64_t seed,
+                                                     int64_t hypBegin, int hypCount, FModelD* __restrict__ models,
+                                                     int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     FModelD m;
-    const int st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr);
+    int st;
+    if constexpr (FAST) {
+        EigWsLocal unused;   // the elimination never touches it (folded away)
+        st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr, unused, true);
+    } else {
+        __shared__ double lds[kEigWs * L];
+        EigWsLane<L> ws{lds + threadIdx.x};
+        st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
+    }
     if (st == 1) {
         models[i] = m;
         counts[i] = 0;
@@ -39,12 +50,15 @@ __global__ __launch_bounds__(256) void mcv_f_generate(const float* __restrict__ 
     }
 }
 
-__global__ void mcv_f_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t hyp, FOneOut* __restrict__ out) {
+__global__ void mcv_f_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t hyp, FOneOut* __restrict__ out,
+                          bool fast) {
+    __shared__ double lds[kEigWs];
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    EigWsLane<1> ws{lds};
     FOneOut o;
     for (int j = 0; j < 9; ++j) o.F[j] = 0;
     for (int j = 0; j < 8; ++j) o.idx[j] = -1;
-    o.status = f_hypothesis(pts4, N, seed, (uint64_t)hyp, o.F, o.idx);
+    o.status = f_hypothesis(pts4, N, seed, (uint64_t)hyp, o.F, o.idx, ws, fast);
     *out = o;
 }
 
@@ -301,13 +315,32 @@ void launch_f7_direct(const float* d_pts4, FOneOut* d_out, hipStream_t s) {
 }
 
 void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
-                       int* d_counts, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_f_generate, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, seed, hypBegin,
-                       hypCount, (FModelD*)d_models, d_counts);
+                       int* d_counts, hipStream_t s, bool fast) {
+    if (fast)
+        hipLaunchKernelGGL(mcv_f_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, seed, hypBegin,
+                           hypCount, (FModelD*)d_models, d_counts);
+    else
+        switch (eig_lanes()) {
+            case 64:
+                hipLaunchKernelGGL((mcv_f_generate<false, 64>), dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N,
+                                   seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+                break;
+            case 48:
+                hipLaunchKernelGGL((mcv_f_generate<false, 48>), dim3((hypCount + 47) / 48), dim3(48), 0, s, d_pts4, N,
+                                   seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+                break;
+            case 32:
+                hipLaunchKernelGGL((mcv_f_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
+                                   seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+                break;
+            default:
+                hipLaunchKernelGGL((mcv_f_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
+                                   seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+        }
 }
 
-void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_f_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out);
+void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s, bool fast) {
+    hipLaunchKernelGGL(mcv_f_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out, fast);
 }
 
 template <int K, int P>

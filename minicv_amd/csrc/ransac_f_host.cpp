@@ -27,7 +27,7 @@ int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     const float thr2 = (float)(t * t);
     FOneOut* d_one = (FOneOut*)P.one.p;
     if (cfg.flags & MCV_FLAG_SEVEN_POINT) launch_f7_one(d_pts, N, cfg.seed, hyp, d_one, s);   // hyp = model slot
-    else launch_f_one(d_pts, N, cfg.seed, hyp, d_one, s);
+    else launch_f_one(d_pts, N, cfg.seed, hyp, d_one, s, (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0);
     MCV_HIP(hipGetLastError());
     FOneOut one;
     MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(FOneOut), hipMemcpyDeviceToHost, s));
@@ -78,10 +78,12 @@ int f_fit_all(Plan& P, const float* d_pts, int N, hipStream_t s, double* F) {
     return N;
 }
 
-int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F9, float* Ff9, int* sampleIdx) {
+int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F9, float* Ff9, int* sampleIdx,
+                      bool fast) {
     if (N < 8) fail("N < 8");
     for (int k = 0; k < 9; ++k) F9[k] = 0;
-    const int st = f_hypothesis(pts4, N, seed, (uint64_t)hyp, F9, sampleIdx);
+    EigWsLocal ws;
+    const int st = f_hypothesis(pts4, N, seed, (uint64_t)hyp, F9, sampleIdx, ws, fast);
     for (int k = 0; k < 9; ++k) Ff9[k] = (float)F9[k];
     return st;
 }

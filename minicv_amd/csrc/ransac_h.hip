@@ -26,14 +26,25 @@ namespace mcv {
 // ------------------------------------------------------------------------------------------
 // Hypothesis generation
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void mcv_h_generate(const float* __restrict__ pts4, int N, uint64_t seed,
-                                                      int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
-                                                      int* __restrict__ counts) {
+// One lane per hypothesis; the runKernel eigen-solve's working set (127 doubles) in LDS, one column
+// per lane (jacobi_eig.h): 64 KB per 64-lane block. FAST = MCV_FLAG_FAST_MINIMAL (no workspace).
+template <bool FAST, int L = kEigLanes>
+__global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __restrict__ pts4, int N, uint64_t seed,
+                                                     int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
+                                                     int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     double H[9];
     HModelF mf;
-    const int st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr);
+    int st;
+    if constexpr (FAST) {
+        EigWsLocal unused;   // the elimination never touches it (folded away)
+        st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr, unused, true);
+    } else {
+        __shared__ double lds[kEigWs * L];
+        EigWsLane<L> ws{lds + threadIdx.x};
+        st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
+    }
     if (st == 1) {
         models[i] = mf;
         counts[i] = 0;
@@ -46,13 +57,16 @@ __global__ __launch_bounds__(256) void mcv_h_generate(const float* __restrict__ 
 }
 
 // One hypothesis in full (finalize path): fp64 model, fp32 model, status, sample.
-__global__ void mcv_h_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t hyp, HOneOut* __restrict__ out) {
+__global__ void mcv_h_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t hyp, HOneOut* __restrict__ out,
+                          bool fast) {
+    __shared__ double lds[kEigWs];
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    EigWsLane<1> ws{lds};
     HOneOut o;
     HModelF mf;
     for (int j = 0; j < 9; ++j) o.H[j] = 0;
     for (int j = 0; j < 8; ++j) mf.h[j] = 0;
-    o.status = h_hypothesis(pts4, N, seed, (uint64_t)hyp, o.H, &mf, o.idx);
+    o.status = h_hypothesis(pts4, N, seed, (uint64_t)hyp, o.H, &mf, o.idx, ws, fast);
     for (int j = 0; j < 8; ++j) o.hf[j] = mf.h[j];
     *out = o;
 }
@@ -997,14 +1011,32 @@ struct OpLMErr {   // 1: |r|^2 only
 // Launchers (host side, called from ransac_host.cpp)
 // ------------------------------------------------------------------------------------------
 void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
-                       int* d_counts, hipStream_t s) {
-    const int blocks = (hypCount + 255) / 256;
-    hipLaunchKernelGGL(mcv_h_generate, dim3(blocks), dim3(256), 0, s, d_pts4, N, seed, hypBegin, hypCount,
-                       (HModelF*)d_models, d_counts);
+                       int* d_counts, hipStream_t s, bool fast) {
+    if (fast)
+        hipLaunchKernelGGL(mcv_h_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, seed, hypBegin,
+                           hypCount, (HModelF*)d_models, d_counts);
+    else
+        switch (eig_lanes()) {
+            case 64:
+                hipLaunchKernelGGL((mcv_h_generate<false, 64>), dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N,
+                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_counts);
+                break;
+            case 48:
+                hipLaunchKernelGGL((mcv_h_generate<false, 48>), dim3((hypCount + 47) / 48), dim3(48), 0, s, d_pts4, N,
+                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_counts);
+                break;
+            case 32:
+                hipLaunchKernelGGL((mcv_h_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
+                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_counts);
+                break;
+            default:
+                hipLaunchKernelGGL((mcv_h_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
+                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_counts);
+        }
 }
 
-void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOut* d_out, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_h_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out);
+void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast) {
+    hipLaunchKernelGGL(mcv_h_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out, fast);
 }
 
 void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s) {

@@ -186,6 +186,7 @@ void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst,
 
 double effective_threshold(const RansacConfig& cfg) { return cfg.threshold > 0 ? cfg.threshold : 3.0; }
 bool fused_error(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_ERROR) != 0; }
+bool fast_minimal(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0; }
 // MCV_HCERT_VARIANT=-1: run the scalar op-by-op sweep instead of the certified one (screen / A-B only)
 bool h_sweep_scalar_only() {
     static const bool v = [] {
@@ -336,7 +337,10 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
             P.bb4.ensure(4);
             launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         }
-        launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+        {
+            ProfScope pg("h_generate", s);
+            launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s, fast_minimal(cfg));
+        }
         ProfScope ps("h_verify", s);
         if (!fused) {
             // default: OpenCV's op-by-op error, certified division-free packed sweep
@@ -361,7 +365,10 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         MCV_HIP(hipGetLastError());
         return;
     } else {
-        launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+        {
+            ProfScope pg("f_generate", s);
+            launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s, fast_minimal(cfg));
+        }
         P.bb4.ensure(4);
         launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         ProfScope ps("f_verify", s);
@@ -385,7 +392,7 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     const float thr2 = (float)(t * t);
     // winner re-solve -> mask from the device-side record -> one read-back of both
     HOneOut* d_one = (HOneOut*)P.one.p;
-    launch_h_one(d_pts, N, cfg.seed, hyp, d_one, s);
+    launch_h_one(d_pts, N, cfg.seed, hyp, d_one, s, fast_minimal(cfg));
     MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
     launch_h_mask_one(d_pts, N, d_one, thr2, fused_error(cfg), d_mask, P.count.p, s);
     MCV_HIP(hipGetLastError());
@@ -618,17 +625,20 @@ extern "C" MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, ui
                                          double* model9, float* modelf9, int* sampleIdx) {
     MCV_GUARD(kStatusNoSample - 1, {
         if (!pts4 || !model9 || !modelf9) fail("mcvHostHypothesis: null argument");
+        const bool fast = (model & MCV_HOST_FAST_MINIMAL) != 0;
+        model &= ~MCV_HOST_FAST_MINIMAL;
         if (model == MCV_MODEL_HOMOGRAPHY) {
             if (N < 4) fail("N < 4");
             HModelF mf;
             for (int k = 0; k < 9; ++k) model9[k] = 0;
             for (int k = 0; k < 8; ++k) mf.h[k] = 0;
-            const int st = h_hypothesis(pts4, N, seed, (uint64_t)hyp, model9, &mf, sampleIdx);
+            EigWsLocal ws;
+            const int st = h_hypothesis(pts4, N, seed, (uint64_t)hyp, model9, &mf, sampleIdx, ws, fast);
             for (int k = 0; k < 8; ++k) modelf9[k] = mf.h[k];
             modelf9[8] = 1.f;
             return st;
         }
-        return f_host_hypothesis(pts4, N, seed, hyp, model9, modelf9, sampleIdx);
+        return f_host_hypothesis(pts4, N, seed, hyp, model9, modelf9, sampleIdx, fast);
     })
 }
 

@@ -72,6 +72,7 @@ FLAG_FIXED_ITERS = 1
 FLAG_NO_REFINE = 2
 FLAG_FUSED_ERROR = 4
 FLAG_SEVEN_POINT = 8
+FLAG_FAST_MINIMAL = 16
 FERR_SAMPSON = 0
 FERR_EPIPOLAR = 1
 MODEL_HOMOGRAPHY = 0

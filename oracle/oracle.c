@@ -118,10 +118,15 @@ static void mul33(const double* A, const double* B, double* C) {
         for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
 }
 
-/* Minimal 4-point solve: runKernel's normalisation, then the 8x8 system (h22 = 1) by Gaussian
+/* The minimal solver of the H / 8-point F hypotheses: 0 = OpenCV's eigen path (default), 1 = the
+ * MCV_FLAG_FAST_MINIMAL elimination. Test infrastructure: set before the (OpenMP) calls. */
+static int g_fast_minimal = 0;
+void orc_set_fast_minimal(int v) { g_fast_minimal = v; }
+
+/* MCV_FLAG_FAST_MINIMAL (opt-in): runKernel's normalisation, then the 8x8 system (h22 = 1) by Gaussian
  * elimination with partial pivoting (first maximum), back substitution, de-normalisation,
  * H *= 1/H22. Returns 0 when degenerate. */
-static int h_solve4(const float* sx, const float* sy, const float* dx, const float* dy, double* H) {
+static int h_solve4_elim(const float* sx, const float* sy, const float* dx, const float* dy, double* H) {
     double cMx = 0, cMy = 0, cmx = 0, cmy = 0, smx = 0, smy = 0, sMx = 0, sMy = 0;
     for (int i = 0; i < 4; ++i) { cmx += dx[i]; cmy += dy[i]; cMx += sx[i]; cMy += sy[i]; }
     cmx /= 4; cmy /= 4; cMx /= 4; cMy /= 4;
@@ -171,6 +176,17 @@ static int h_solve4(const float* sx, const float* sy, const float* dx, const flo
         H[i] = H[i] * s;
         if (!isfinite(H[i])) return 0;
     }
+    return 1;
+}
+
+/* Minimal 4-point solve = HomographyEstimatorCallback::runKernel on the sample (h_run_kernel_xy,
+ * below: LtL, cv::eigen, de-normalisation, 1/H22). 0 when the scales vanish or H is not finite. */
+static int h_run_kernel_xy(const float* sx, const float* sy, const float* dx, const float* dy, int count, double* H);
+static int h_solve4(const float* sx, const float* sy, const float* dx, const float* dy, double* H) {
+    if (g_fast_minimal) return h_solve4_elim(sx, sy, dx, dy, H);
+    if (!h_run_kernel_xy(sx, sy, dx, dy, 4, H)) return 0;
+    for (int i = 0; i < 9; ++i)
+        if (!isfinite(H[i])) return 0;
     return 1;
 }
 
@@ -360,25 +376,23 @@ void eig_pinv_apply(const double* A, int n, const double* b, double* x, double* 
     }
 }
 
-/* HomographyEstimatorCallback::runKernel over the listed correspondences (sequential sums). */
-static int h_run_kernel(const float* pts4, const int* list, int count, double* H) {
+/* HomographyEstimatorCallback::runKernel [ext: OpenCV fundam.cpp] on count correspondences
+ * M = (sx, sy) -> m = (dx, dy), sequential sums: centroids, mean |deviation| scales (0 when one
+ * vanishes), LtL[j][k] += Lx[j] Lx[k] + Ly[j] Ly[k] (k >= j) then completeSymm, cv::eigen, H0 = the
+ * last eigenvector row, invHnorm H0 Hnorm2, times 1/H22 (convertTo). */
+static int h_run_kernel_xy(const float* sx, const float* sy, const float* dx, const float* dy, int count, double* H) {
     double cmx = 0, cmy = 0, cMx = 0, cMy = 0, smx = 0, smy = 0, sMx = 0, sMy = 0;
-    for (int t = 0; t < count; ++t) {
-        const float* p = pts4 + 4 * (size_t)list[t];
-        cmx += p[2]; cmy += p[3]; cMx += p[0]; cMy += p[1];
-    }
+    for (int t = 0; t < count; ++t) { cmx += dx[t]; cmy += dy[t]; cMx += sx[t]; cMy += sy[t]; }
     cmx /= count; cmy /= count; cMx /= count; cMy /= count;
     for (int t = 0; t < count; ++t) {
-        const float* p = pts4 + 4 * (size_t)list[t];
-        smx += fabs(p[2] - cmx); smy += fabs(p[3] - cmy); sMx += fabs(p[0] - cMx); sMy += fabs(p[1] - cMy);
+        smx += fabs(dx[t] - cmx); smy += fabs(dy[t] - cmy); sMx += fabs(sx[t] - cMx); sMy += fabs(sy[t] - cMy);
     }
     if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
         return 0;
     smx = count / smx; smy = count / smy; sMx = count / sMx; sMy = count / sMy;
     double L[81] = {0};
     for (int t = 0; t < count; ++t) {
-        const float* p = pts4 + 4 * (size_t)list[t];
-        double x = (p[2] - cmx) * smx, y = (p[3] - cmy) * smy, X = (p[0] - cMx) * sMx, Y = (p[1] - cMy) * sMy;
+        double x = (dx[t] - cmx) * smx, y = (dy[t] - cmy) * smy, X = (sx[t] - cMx) * sMx, Y = (sy[t] - cMy) * sMy;
         double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
         double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
         for (int j = 0; j < 9; ++j)
@@ -386,6 +400,8 @@ static int h_run_kernel(const float* pts4, const int* list, int count, double* H
     }
     for (int j = 0; j < 9; ++j)
         for (int k = 0; k < j; ++k) L[j * 9 + k] = L[k * 9 + j];
+    for (int j = 0; j < 81; ++j)
+        if (!isfinite(L[j])) return 0;   /* NaN input: OpenCV's NaN model counts no inlier either */
     double w[9], V[81];
     jacobi(L, 9, w, V);
     double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
@@ -393,8 +409,21 @@ static int h_run_kernel(const float* pts4, const int* list, int count, double* H
     double T[9], R[9];
     mul33(invHnorm, V + 72, T);
     mul33(T, Hnorm2, R);
-    for (int k = 0; k < 9; ++k) H[k] = R[k] * (1. / R[8]);
+    double sc = 1. / R[8];
+    for (int k = 0; k < 9; ++k) H[k] = R[k] * sc;
     return 1;
+}
+
+/* The same over listed correspondences of a float4 set (refit over the inliers). */
+static int h_run_kernel(const float* pts4, const int* list, int count, double* H) {
+    float* b = (float*)malloc(sizeof(float) * 4 * (size_t)(count > 0 ? count : 1));
+    for (int t = 0; t < count; ++t) {
+        const float* p = pts4 + 4 * (size_t)list[t];
+        b[t] = p[0]; b[count + t] = p[1]; b[2 * (size_t)count + t] = p[2]; b[3 * (size_t)count + t] = p[3];
+    }
+    int r = h_run_kernel_xy(b, b + count, b + 2 * (size_t)count, b + 3 * (size_t)count, count, H);
+    free(b);
+    return r;
 }
 
 /* HomographyRefineCallback::compute: returns |r|^2; A (8x8) and v (8) when non-NULL. */
@@ -639,7 +668,28 @@ static int f_norm8(const float* x, const float* y, int m, double* cx, double* cy
     return 1;
 }
 
-static int f_solve8_orc(const float* x1, const float* y1, const float* x2, const float* y2, double* F) {
+/* run8Point's eigen step on the accumulated A (upper triangle filled; completed here): cv::eigen, the
+ * eigenvalue check (0 when one of the 8 largest is below DBL_EPSILON in magnitude), F0 = the last
+ * eigenvector row, rank 2, de-normalisation. */
+static int f_from_ata(double* A, double c1x, double c1y, double s1x, double s1y, double c2x, double c2y, double s2x,
+                      double s2y, double* F) {
+    for (int j = 0; j < 9; ++j)
+        for (int k = 0; k < j; ++k) A[j * 9 + k] = A[k * 9 + j];
+    for (int j = 0; j < 81; ++j)
+        if (!isfinite(A[j])) return 0;
+    double w[9], V[81], F0[9];
+    jacobi(A, 9, w, V);
+    int i = 0;
+    for (; i < 9; ++i)
+        if (fabs(w[i]) < DBL_EPSILON) break;
+    if (i < 8) return 0;
+    memcpy(F0, V + 72, sizeof(F0));
+    f_rank2_orc(F0);
+    return f_denorm_orc(F0, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
+}
+
+/* MCV_FLAG_FAST_MINIMAL (opt-in): the 8x9 system with f22 = 1 by Gaussian elimination. */
+static int f_solve8_elim_orc(const float* x1, const float* y1, const float* x2, const float* y2, double* F) {
     double c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y;
     if (!f_norm8(x1, y1, 8, &c1x, &c1y, &s1x, &s1y) || !f_norm8(x2, y2, 8, &c2x, &c2y, &s2x, &s2y)) return 0;
     double a[8][9];
@@ -670,6 +720,21 @@ static int f_solve8_orc(const float* x1, const float* y1, const float* x2, const
     double F0[9] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], 1.0};
     f_rank2_orc(F0);
     return f_denorm_orc(F0, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
+}
+
+/* run8Point on the 8-point sample: normalisation, A += r r^T, f_from_ata. */
+static int f_solve8_orc(const float* x1, const float* y1, const float* x2, const float* y2, double* F) {
+    if (g_fast_minimal) return f_solve8_elim_orc(x1, y1, x2, y2, F);
+    double c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y;
+    if (!f_norm8(x1, y1, 8, &c1x, &c1y, &s1x, &s1y) || !f_norm8(x2, y2, 8, &c2x, &c2y, &s2x, &s2y)) return 0;
+    double A[81] = {0};
+    for (int i = 0; i < 8; ++i) {
+        double X1 = (x1[i] - c1x) * s1x, Y1 = (y1[i] - c1y) * s1y, X2 = (x2[i] - c2x) * s2x, Y2 = (y2[i] - c2y) * s2y;
+        double r[9] = {X2 * X1, X2 * Y1, X2, Y2 * X1, Y2 * Y1, Y2, X1, Y1, 1.0};
+        for (int j = 0; j < 9; ++j)
+            for (int k = j; k < 9; ++k) A[j * 9 + k] += r[j] * r[k];
+    }
+    return f_from_ata(A, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
 }
 
 int orc_f_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* F, int* idx_out) {
@@ -772,17 +837,7 @@ static int f_fit_all_orc(const float* pts4, int N, double* F) {
         for (int j = 0; j < 9; ++j)
             for (int k = j; k < 9; ++k) A[j * 9 + k] += r[j] * r[k];
     }
-    for (int j = 0; j < 9; ++j)
-        for (int k = 0; k < j; ++k) A[j * 9 + k] = A[k * 9 + j];
-    double w[9], V[81], F0[9];
-    jacobi(A, 9, w, V);
-    int i = 0;
-    for (; i < 9; ++i)
-        if (fabs(w[i]) < DBL_EPSILON) break;
-    if (i < 8) return 0;
-    memcpy(F0, V + 72, sizeof(F0));
-    f_rank2_orc(F0);
-    return f_denorm_orc(F0, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
+    return f_from_ata(A, c1x, c1y, s1x, s1y, c2x, c2y, s2x, s2y, F);
 }
 
 /* cv::findFundamentalMat(a, b, FM_RANSAC (8-point kernel) | FM_8POINT, thr, conf, maxIters, mask). */

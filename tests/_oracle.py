@@ -15,6 +15,7 @@ ORACLE_SO = ORACLE_DIR / "liboracle.so"
 _P, _I, _I64, _U64, _D, _F = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double, C.c_float
 _SIGS = {
     "orc_philox": (None, [_P, _P, _P]),
+    "orc_set_fast_minimal": (None, [_I]),
     "orc_h_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P, _P]),
     "orc_h_count": (_I, [_P, _I, _P, _F, _P, _I]),
     "orc_h_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _I, _P, _I]),
@@ -80,6 +81,20 @@ def load() -> C.CDLL:
             f.restype, f.argtypes = res, args
         _lib = L
     return _lib
+
+
+class fast_minimal:
+    """Context: the H / 8-point F hypotheses use the MCV_FLAG_FAST_MINIMAL elimination solver."""
+
+    def __init__(self, on: bool = True):
+        self.on = on
+
+    def __enter__(self):
+        load().orc_set_fast_minimal(int(self.on))
+        return self
+
+    def __exit__(self, *exc):
+        load().orc_set_fast_minimal(0)
 
 
 def ptr(a: np.ndarray) -> int:

@@ -83,7 +83,8 @@ int main() {
             float hf2[8] = {0};
             std::memset(&m1, 0, sizeof(m1));
             int i1[4] = {-1, -1, -1, -1}, i2[4] = {-1, -1, -1, -1};
-            const int s1 = mcv::h_hypothesis(pts.data(), N, 7, (uint64_t)h, H1, &m1, i1);
+            mcv::EigWsLocal ws;
+            const int s1 = mcv::h_hypothesis(pts.data(), N, 7, (uint64_t)h, H1, &m1, i1, ws);
             const int s2 = orc_h_hypothesis(pts.data(), N, 7, h, H2, hf2, i2);
             expect(s1 == s2, "h status", s1, s2);
             if (s1 == 1 && s2 == 1) {
@@ -93,7 +94,7 @@ int main() {
             if (N >= 8) {
                 double F1[9] = {0}, F2[9] = {0};
                 int j1[8], j2[8];
-                const int t1 = mcv::f_hypothesis(pts.data(), N, 9, (uint64_t)h, F1, j1);
+                const int t1 = mcv::f_hypothesis(pts.data(), N, 9, (uint64_t)h, F1, j1, ws);
                 const int t2 = orc_f_hypothesis(pts.data(), N, 9, h, F2, j2);
                 expect(t1 == t2, "f status", t1, t2);
                 if (t1 == 1 && t2 == 1) expect(same_bits(F1, F2, 9), "f model", h, N);

@@ -102,20 +102,24 @@ def test_host_philox_matches_oracle(native, oracle, ctr, key):
     assert list(out) == oracle.philox(ctr, key)
 
 
+@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("n,outliers,seed", [(4, 0.0, 1), (7, 0.5, 2), (200, 0.5, 3), (5000, 0.7, 4)])
-def test_host_hypothesis_bit_exact_vs_oracle(native, oracle, n, outliers, seed):
+def test_host_hypothesis_bit_exact_vs_oracle(native, oracle, n, outliers, seed, fast):
     """The exact code the kernel runs (hyp_homography.h), compiled for the host, vs the independent
-    C restatement: status, sample, fp64 model and fp32 model all bit-identical."""
+    C restatement: status, sample, fp64 model and fp32 model all bit-identical — for OpenCV's
+    eigen-based runKernel (default) and the MCV_FLAG_FAST_MINIMAL elimination."""
     src, dst, _ = S.homography_problem(n, seed, outlier_frac=outliers)
     pts4 = oracle.pack4(src, dst)
     L = native.lib()
     H = np.zeros(9)
     hf = np.zeros(9, np.float32)
     idx = np.full(4, -1, np.int32)
+    model = 0 | (0x100 if fast else 0)
     for hyp in list(range(300)) + [2**31 + 5, 2**32 - 1]:
-        st = L.mcvHostHypothesis(0, pts4.ctypes.data, n, seed * 7919, hyp, H.ctypes.data, hf.ctypes.data,
+        st = L.mcvHostHypothesis(model, pts4.ctypes.data, n, seed * 7919, hyp, H.ctypes.data, hf.ctypes.data,
                                  idx.ctypes.data)
-        st2, H2, hf2, idx2 = oracle.h_hypothesis(pts4, seed * 7919, hyp)
+        with oracle.fast_minimal(fast):
+            st2, H2, hf2, idx2 = oracle.h_hypothesis(pts4, seed * 7919, hyp)
         assert st == st2
         if st == 1:
             np.testing.assert_array_equal(H, H2)
@@ -149,18 +153,21 @@ def test_replay_chunks_match_oracle(native, oracle):
             assert st.bestCount == bc
 
 
+@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("n,outliers,seed", [(8, 0.0, 1), (9, 0.3, 2), (500, 0.5, 3), (5000, 0.7, 4)])
-def test_host_f_hypothesis_bit_exact_vs_oracle(native, oracle, n, outliers, seed):
+def test_host_f_hypothesis_bit_exact_vs_oracle(native, oracle, n, outliers, seed, fast):
     a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=outliers)
     pts4 = oracle.pack4(a, b)
     L = native.lib()
     F = np.zeros(9)
     Ff = np.zeros(9, np.float32)
     idx = np.full(8, -1, np.int32)
+    model = 1 | (0x100 if fast else 0)
     for hyp in list(range(200)) + [2**32 - 7]:
-        st = L.mcvHostHypothesis(1, pts4.ctypes.data, n, seed * 31, hyp, F.ctypes.data, Ff.ctypes.data,
+        st = L.mcvHostHypothesis(model, pts4.ctypes.data, n, seed * 31, hyp, F.ctypes.data, Ff.ctypes.data,
                                  idx.ctypes.data)
-        st2, F2, idx2 = oracle.f_hypothesis(pts4, seed * 31, hyp)
+        with oracle.fast_minimal(fast):
+            st2, F2, idx2 = oracle.f_hypothesis(pts4, seed * 31, hyp)
         assert st == st2
         if st == 1:
             np.testing.assert_array_equal(F, F2)

@@ -51,6 +51,36 @@ def test_f_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, erro
     plan.close()
 
 
+@pytest.mark.parametrize("n,outl,seed,begin,count", [(8, 0.0, 31, 0, 64), (2000, 0.5, 32, 5, 1024)])
+def test_f_counts_fast_minimal(torch_dev, oracle, n, outl, seed, begin, count):
+    """MCV_FLAG_FAST_MINIMAL (elimination null vector) against the oracle's elimination."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=outl)
+    pts = D.pack_points_tensor(a, b, dev)
+    plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, n, count)
+    thr = 5e-3
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, fast_minimal=True).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(count, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, begin, count, key, counts)
+    got = counts.cpu().numpy()
+    with oracle.fast_minimal():
+        ref = oracle.f_counts(oracle.pack4(a, b), seed, begin, count, float(np.float32(thr * thr)),
+                              oracle.f_kind(0, True))
+    np.testing.assert_array_equal(got, ref)
+    plan.close()
+    if n == 8:
+        return   # N == 8 is one all-points fit (GPU sums, 1e-6 bar: test_find_fundamental_vs_oracle)
+    with oracle.fast_minimal():
+        cnt_o, F_o, mask_o, _ = oracle.find_fundamental(a, b, thr=thr, seed=seed, max_iters=300)
+    cnt, F, mask = opencv.findFundamentalMat(a, b, opencv.RansacParams(threshold=thr, seed=seed, max_iters=300,
+                                                                       confidence=0.99, fast_minimal=True))
+    assert cnt == cnt_o
+    np.testing.assert_array_equal(mask, mask_o.astype(bool))
+    np.testing.assert_array_equal(F, F_o)
+
+
 @pytest.mark.parametrize("n,outl,seed,iters,conf,error_kind,flags", [
     (8, 0.0, 1, 1000, 0.99, 0, 0), (50, 0.3, 2, 1000, 0.99, 0, 0), (500, 0.5, 4, 1000, 0.99, 0, 0),
     (3000, 0.5, 5, 2000, 0.99, 0, 0), (3000, 0.5, 6, 2000, 0.99, 1, 0),

@@ -28,12 +28,12 @@ def torch_dev(gpu):
     return torch, torch.device("cuda:0")
 
 
-def device_counts(torch_dev, src, dst, seed, begin, count, thr, model=N.MODEL_HOMOGRAPHY, unfused=False):
+def device_counts(torch_dev, src, dst, seed, begin, count, thr, model=N.MODEL_HOMOGRAPHY, unfused=False, fast=False):
     torch, dev = torch_dev
     from minicv_amd import device as D
     pts = D.pack_points_tensor(src, dst, dev)
     plan = D.RansacPlan(model, src.shape[0], count)
-    cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused).to_c()
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused, fast_minimal=fast).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     counts = torch.zeros(count, dtype=torch.int32, device=dev)
     plan.evaluate(pts, src.shape[0], cfg, begin, count, key, counts)
@@ -65,6 +65,30 @@ def test_per_hypothesis_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin
     else:
         assert key[0] == 0
     assert key[1] == (begin + int(fail[0]) if len(fail) else 2**63 - 1)
+
+
+@pytest.mark.parametrize("n,outl,seed,begin,count", [(4, 0.0, 21, 0, 64), (200, 0.5, 22, 0, 4096),
+                                                    (20000, 0.3, 23, 2**31, 1024)])
+def test_per_hypothesis_counts_fast_minimal(torch_dev, oracle, n, outl, seed, begin, count):
+    """MCV_FLAG_FAST_MINIMAL (elimination minimal solver): counts bit-exact against the oracle's
+    elimination; the default path is covered above."""
+    src, dst, _ = S.homography_problem(n, seed, outlier_frac=outl)
+    thr = 5e-3
+    got, _ = device_counts(torch_dev, src, dst, seed, begin, count, thr, unfused=True, fast=True)
+    with oracle.fast_minimal():
+        ref = oracle.h_counts(oracle.pack4(src, dst), seed, begin, count, float(np.float32(thr * thr)))
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_find_homography_fast_minimal(gpu, oracle):
+    src, dst, _ = S.homography_problem(3000, 24)
+    with oracle.fast_minimal():
+        cnt_o, H_o, mask_o, _ = oracle.find_homography(src, dst, thr=5e-3, seed=24, flags=N.FLAG_NO_REFINE)
+    cnt, H, mask = opencv.findHomography(src, dst, opencv.RansacParams(threshold=5e-3, seed=24, refine=False,
+                                                                       fast_minimal=True))
+    assert cnt == cnt_o
+    np.testing.assert_array_equal(mask, mask_o.astype(bool))
+    np.testing.assert_array_equal(H, H_o)
 
 
 def test_golden_cfg1(gpu, oracle):
