@@ -24,7 +24,7 @@ WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2", "
 KERNELS = {"homography": "mcv_h_verify_cert", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
            "l2": "mcv_l2_mfma", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify",
            "scaled": "mcv_scaled_costs"}
-EXTRA_BENCH = ["homography_fused", "pnp_ap3p"]   # second bench lines (bench_<name>.log)
+EXTRA_BENCH = ["homography_fused", "homography_fast", "pnp_ap3p"]   # second bench lines (bench_<name>.log)
 
 
 def last_json(path: Path):

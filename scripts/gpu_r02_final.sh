@@ -20,6 +20,7 @@ fi
 if [[ $PARTS == *b* ]]; then
 step bench_homography 300 python bench.py --steps 10 --warmup 3 --cpu-seconds 8
 step bench_homography_fused 300 python bench.py --steps 10 --warmup 3 --fused --no-cpu-baseline
+step bench_homography_fast 300 python bench.py --steps 10 --warmup 3 --fast-minimal --no-cpu-baseline
 step bench_fundamental 300 python bench.py --workload fundamental --steps 5 --warmup 1 --cpu-seconds 8
 step bench_hamming 300 python bench.py --workload hamming --steps 20 --warmup 3
 step bench_l2 300 python bench.py --workload l2 --steps 5 --warmup 2
