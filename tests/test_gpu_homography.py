@@ -204,3 +204,24 @@ def test_full_size_bench_config_properties(torch_dev, oracle):
     plan.evaluate(pts, n, cfg, 0, H, key, counts2)
     assert torch.equal(counts, counts2)
     plan.close()
+
+
+@pytest.mark.parametrize("fast", [False, True])
+def test_counts_extreme_points(torch_dev, oracle, fast):
+    """Minimal-solver edge inputs: duplicated, near-collinear, huge and tiny coordinates and non-finite
+    points in the sample. The eigen path rejects a non-finite LtL (OpenCV's NaN model counts no
+    inlier: the same RANSAC outcome); every status and count equals the oracle's."""
+    src, dst, _ = S.homography_problem(300, 25, outlier_frac=0.3)
+    rng = np.random.default_rng(25)
+    src[:40] = src[40:80] * (1 + 1e-7 * rng.standard_normal((40, 2)))   # near-duplicates
+    src[80:90, 1] = 0.5 * src[80:90, 0] + 0.1                           # collinear run
+    src[90:95] *= 1e6
+    dst[95:100] *= 1e-6
+    src[100, 0] = np.nan
+    dst[101, 1] = np.inf
+    src[102] = [1e30, -1e30]
+    thr = 5e-3
+    got, _ = device_counts(torch_dev, src, dst, 25, 0, 4096, thr, unfused=True, fast=fast)
+    with oracle.fast_minimal(fast):
+        ref = oracle.h_counts(oracle.pack4(src, dst), 25, 0, 4096, float(np.float32(thr * thr)))
+    np.testing.assert_array_equal(got, ref)
