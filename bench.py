@@ -507,6 +507,23 @@ def bench_ransac(args):
             line["cpu_baseline"] = (cpu_baseline_f if fund else cpu_baseline)(src, dst, args.cpu_seconds)
         else:
             line["cpu_baseline"] = None
+        if world == 1 and not args.fast_minimal:
+            # the same step with the opt-in elimination minimal solver (a secondary figure, not `value`)
+            cfg_default = cfg
+            cfg = opencv.RansacParams(threshold=THR, confidence=0.995, max_iters=total,
+                                      seed=F_SEED if fund else SEED, fixed_iters=True, fused_error=args.fused,
+                                      fast_minimal=True).to_c()
+            step()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            fe = (time.perf_counter() - t1) / 3
+            cfg = cfg_default
+            line["fast_minimal"] = {"value": total / fe, "ms_per_step": fe * 1e3,
+                                    "note": "opt-in MCV_FLAG_FAST_MINIMAL (elimination minimal solver), 3 steps; "
+                                            "`value` above is the default (OpenCV's cv::eigen runKernel / run8Point)"}
         print(json.dumps(line), flush=True)
     plan.close()
     if world > 1:
