@@ -20,8 +20,8 @@
 // dependent (k, l) indexing would otherwise put the matrices in scratch. On the host (twins, the
 // single-lane winner kernels) it is a private array (EigWsLocal). Both run the same code and round
 // identically (-ffp-contract=off; division and sqrt are IEEE on both sides).
-// indR / indC are kept in registers as 4-bit fields of one 32-bit word each. The quotients run
-// gfx950's refined-reciprocal division inside its exact domain (eig_div), the hypot branch-free.
+// indR / indC are kept in registers as 4-bit fields of one 32-bit word each. The rotation's five
+// quotients run gfx950's refined-reciprocal division inside its exact domain (eig_rotation).
 #pragma once
 
 #include <cstdlib>
@@ -68,29 +68,44 @@ MCV_HD uint32_t eig_set_nib(uint32_t x, int i, int v) {
     return (x & ~m) | (((uint32_t)v << (4 * i)) & m);
 }
 
-// x / y exactly as the IEEE division. Device: gfx950's refined-reciprocal quotient without the
-// div_scale / div_fixup wrapper (mcv_common.h) inside its proven domain, the IEEE division outside.
-MCV_HD double eig_div(double x, double y) {
+// JacobiImpl_'s rotation from the pivot p (|p| > DBL_EPSILON) and y = (W[l] - W[k]) / 2:
+//   t = |y| + hypot(p, y); s = hypot(p, t); c = t / s; s = p / s; t = (p / t) p; signs for y < 0.
+// Here t >= |p| and s >= t, so the second hypot's quotient is |p| / t and every divisor is at least
+// |p| > 2^-64. Device: when the first hypot's larger operand stays below 2^60 and its quotient's
+// numerator is 0 or at least 2^-900 (always, for the normalised systems of the minimal solvers),
+// all five quotients take gfx950's refined-reciprocal form (bit-identical to IEEE there) behind
+// one wave-uniform branch; otherwise the IEEE divisions. Host: the IEEE divisions.
+MCV_HD void eig_rotation(double p, double y, double& c, double& s, double& t) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const double ax = __builtin_fabs(x);
-    if (__builtin_expect(div_f64_refined_domain(y) && (ax == 0.0 || (ax >= 0x1p-900 && ax < 0x1p700)), 1))
-        return div_f64_refined(x, y, rcp_f64_refined(y));
-    return x / y;
+    const double ap = __builtin_fabs(p), ay = __builtin_fabs(y);
+    const bool ag = ap > ay;
+    const double hi = ag ? ap : ay, lo = ag ? ay : ap;
+    if (__builtin_expect(hi <= 0x1p60 && (lo == 0.0 || lo >= 0x1p-900), 1)) {
+        const double r1 = div_f64_refined(lo, hi, rcp_f64_refined(hi));
+        const double h1 = hi * __builtin_sqrt(1 + r1 * r1);
+        double tt = ay + h1;          // hypot(p, y): hi > 0 here, so the `else 0` case cannot occur
+        const double rt = rcp_f64_refined(tt);
+        const double r2 = div_f64_refined(ap, tt, rt);
+        const double ss = tt * __builtin_sqrt(1 + r2 * r2);   // hypot(p, t) with t >= |p|
+        const double rs = rcp_f64_refined(ss);
+        c = div_f64_refined(tt, ss, rs);
+        s = div_f64_refined(p, ss, rs);
+        t = div_f64_refined(p, tt, rt) * p;
+    } else {
+        t = ay + cv_hypot(p, y);
+        s = cv_hypot(p, t);
+        c = t / s;
+        s = p / s;
+        t = (p / t) * p;
+    }
 #else
-    return x / y;
+    t = __builtin_fabs(y) + cv_hypot(p, y);
+    s = cv_hypot(p, t);
+    c = t / s;
+    s = p / s;
+    t = (p / t) * p;
 #endif
-}
-
-// lapack.cpp's hypot (cv_hypot) in branch-free form: the same quotient, product and root for every
-// input (a > b: b / a, a sqrt(1 + r^2); b > 0: a / b, b sqrt(1 + r^2); else 0).
-MCV_HD double eig_hypot(double a, double b) {
-    a = __builtin_fabs(a);
-    b = __builtin_fabs(b);
-    const bool ag = a > b;
-    const double hi = ag ? a : b, lo = ag ? b : a;
-    const double r = eig_div(lo, hi);
-    const double h = hi * __builtin_sqrt(1 + r * r);
-    return (ag || b > 0) ? h : 0.0;
+    if (y < 0) s = -s, t = -t;
 }
 
 // First maximum of a candidate pair in scan order: the later one wins only when strictly greater.
@@ -207,12 +222,8 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
             vb[i] = ws[vl + i];
         }
         const double y = (wl - wk) * 0.5;
-        double t = __builtin_fabs(y) + eig_hypot(p, y);
-        double s = eig_hypot(p, t);
-        const double c = eig_div(t, s);
-        s = eig_div(p, s);
-        t = eig_div(p, t) * p;
-        if (y < 0) s = -s, t = -t;
+        double c, s, t;
+        eig_rotation(p, y, c, s, t);
         ws[ekl] = 0;
         ws[kEigW + k] = wk - t;
         ws[kEigW + l] = wl + t;
