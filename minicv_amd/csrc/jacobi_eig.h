@@ -14,9 +14,8 @@
 //
 // Layout: the working set is 127 doubles — [0, 36) the strict upper triangle packed by rows
 // (eig_tri), [36, 45) W (the running diagonal), [45, 126) V row-major, a junk slot. On the GPU it lives in LDS,
-// one column per lane of a [element][64 lanes] block (EigWsLane: element e of lane L at
-// lds[e * 64 + L], so a wave's accesses to one element are 64 consecutive doubles — conflict-free
-// ds_read_b64 / ds_write_b64, and a compile-time element index is an immediate offset); the data-
+// one 127-double slice per lane (EigWsLane; the odd stride keeps a half-wave's accesses to one
+// element bank-conflict-free, a compile-time element index is an immediate offset); the data-
 // dependent (k, l) indexing would otherwise put the matrices in scratch. On the host (twins, the
 // single-lane winner kernels) it is a private array (EigWsLocal). Both run the same code and round
 // identically (-ffp-contract=off; division and sqrt are IEEE on both sides).
@@ -55,10 +54,14 @@ struct EigWsLocal {
     MCV_HD double& operator[](int e) { return d[e]; }
 };
 
+// Lane-private slices of a __shared__ double[kEigWs * L] block: p = block + lane * kEigWs. The odd
+// stride (127 doubles) puts a half-wave's 64-bit accesses to one element on distinct bank pairs, and
+// every address is lane base + 8 e (a compile-time element is an immediate offset, a dynamic one a
+// shift-add: no multiply by a non-power-of-two lane count).
 template <int L = 64>
 struct EigWsLane {
-    double* p;   // &block[lane] of a __shared__ double[kEigWs * L] (L lanes per block)
-    MCV_HD double& operator[](int e) { return p[e * L]; }
+    double* p;
+    MCV_HD double& operator[](int e) { return p[e]; }
 };
 
 // 4-bit fields: indR[i] at field i (i = 0..7), indC[i] at field i - 1 (i = 1..8).

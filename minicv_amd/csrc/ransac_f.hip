@@ -39,7 +39,7 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __
         st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
-        EigWsLane<L> ws{lds + threadIdx.x};
+        EigWsLane<L> ws{lds + threadIdx.x * kEigWs};
         st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
     }
     if (st == 1) {

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
         st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
-        EigWsLane<L> ws{lds + threadIdx.x};
+        EigWsLane<L> ws{lds + threadIdx.x * kEigWs};
         st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
     }
     if (st == 1) {
