@@ -314,3 +314,27 @@ def test_find_fundamental7_edges(gpu, oracle):
     a, b, _, _ = S.fundamental_problem(12, 5, outlier_frac=0.0)
     with pytest.raises(N.NativeError, match="N >= 15"):
         opencv.findFundamentalMat(a, b, p)
+
+
+@pytest.mark.parametrize("seed", [41, 42, 43])
+def test_f_eigen_minimal_solver_stress(torch_dev, oracle, seed):
+    """run8Point's eigen-solve (JacobiImpl_ per lane) and its eigenvalue check against the oracle over
+    many 8-point samples: every status and count identical."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(200, 2500))
+    a, b, _, _ = S.fundamental_problem(n, seed, outlier_frac=float(rng.uniform(0.1, 0.7)))
+    pts = D.pack_points_tensor(a, b, dev)
+    count = 8192
+    plan = D.RansacPlan(N.MODEL_FUNDAMENTAL, n, count)
+    thr = 5e-3
+    begin = int(rng.integers(0, 2**31))
+    cfg = opencv.RansacParams(threshold=thr, seed=seed).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(count, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, begin, count, key, counts)
+    got = counts.cpu().numpy()
+    plan.close()
+    ref = oracle.f_counts(oracle.pack4(a, b), seed, begin, count, float(np.float32(thr * thr)), oracle.f_kind(0, True))
+    np.testing.assert_array_equal(got, ref)

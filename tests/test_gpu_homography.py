@@ -225,3 +225,20 @@ def test_counts_extreme_points(torch_dev, oracle, fast):
     with oracle.fast_minimal(fast):
         ref = oracle.h_counts(oracle.pack4(src, dst), 25, 0, 4096, float(np.float32(thr * thr)))
     np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("seed", [31, 32, 33, 34])
+def test_eigen_minimal_solver_stress(torch_dev, oracle, seed):
+    """The per-lane JacobiImpl_ kernel against the oracle's restatement over many hypotheses and point
+    geometries (perspective-heavy scenes, wide coordinate ranges): every status and count identical."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(300, 3000))
+    src, dst, _ = S.homography_problem(n, seed, outlier_frac=float(rng.uniform(0.1, 0.8)),
+                                       sigma=float(rng.choice([0.0, 1e-3, 1e-2])))
+    scale = float(rng.choice([1e-3, 1.0, 640.0]))
+    src, dst = src * scale, dst * scale
+    thr = 5e-3 * scale
+    begin = int(rng.integers(0, 2**31))
+    got, _ = device_counts(torch_dev, src, dst, seed, begin, 16384, thr, unfused=True)
+    ref = oracle.h_counts(oracle.pack4(src, dst), seed, begin, 16384, float(np.float32(thr * thr)))
+    np.testing.assert_array_equal(got, ref)
