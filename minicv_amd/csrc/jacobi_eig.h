@@ -54,11 +54,10 @@ struct EigWsLocal {
     MCV_HD double& operator[](int e) { return d[e]; }
 };
 
-// Lane-private slices of a __shared__ double[kEigWs * L] block: p = block + lane * kEigWs. The odd
-// stride (127 doubles) puts a half-wave's 64-bit accesses to one element on distinct bank pairs, and
-// every address is lane base + 8 e (a compile-time element is an immediate offset, a dynamic one a
-// shift-add: no multiply by a non-power-of-two lane count).
-template <int L = 64>
+// Lane-private slices of a __shared__ double[kEigWs * lanes] block: p = block + lane * kEigWs. The
+// odd stride (127 doubles) puts a half-wave's 64-bit accesses to one element on distinct bank pairs,
+// and every address is lane base + 8 e (a compile-time element is an immediate offset, a dynamic one
+// a shift-add: no multiply by a non-power-of-two lane count).
 struct EigWsLane {
     double* p;
     MCV_HD double& operator[](int e) { return p[e]; }
@@ -76,8 +75,9 @@ MCV_HD uint32_t eig_set_nib(uint32_t x, int i, int v) {
 // Here t >= |p| and s >= t, so the second hypot's quotient is |p| / t and every divisor is at least
 // |p| > 2^-64. Device: when the first hypot's larger operand stays below 2^60 and its quotient's
 // numerator is 0 or at least 2^-900 (always, for the normalised systems of the minimal solvers),
-// all five quotients take gfx950's refined-reciprocal form (bit-identical to IEEE there) behind
-// one wave-uniform branch; otherwise the IEEE divisions. Host: the IEEE divisions.
+// all five quotients take gfx950's refined-reciprocal form (bit-identical to IEEE there); a lane
+// outside that domain takes the IEEE divisions (a branch no lane takes on these systems, so the
+// wave skips it). Host: the IEEE divisions.
 MCV_HD void eig_rotation(double p, double y, double& c, double& s, double& t) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double ap = __builtin_fabs(p), ay = __builtin_fabs(y);

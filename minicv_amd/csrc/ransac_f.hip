@@ -39,7 +39,7 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __
         st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
-        EigWsLane<L> ws{lds + threadIdx.x * kEigWs};
+        EigWsLane ws{lds + threadIdx.x * kEigWs};
         st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
     }
     if (st == 1) {
@@ -54,7 +54,7 @@ __global__ void mcv_f_one(const float* __restrict__ pts4, int N, uint64_t seed, 
                           bool fast) {
     __shared__ double lds[kEigWs];
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    EigWsLane<1> ws{lds};
+    EigWsLane ws{lds};
     FOneOut o;
     for (int j = 0; j < 9; ++j) o.F[j] = 0;
     for (int j = 0; j < 8; ++j) o.idx[j] = -1;

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
         st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
-        EigWsLane<L> ws{lds + threadIdx.x * kEigWs};
+        EigWsLane ws{lds + threadIdx.x * kEigWs};
         st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
     }
     if (st == 1) {
@@ -61,7 +61,7 @@ __global__ void mcv_h_one(const float* __restrict__ pts4, int N, uint64_t seed, 
                           bool fast) {
     __shared__ double lds[kEigWs];
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    EigWsLane<1> ws{lds};
+    EigWsLane ws{lds};
     HOneOut o;
     HModelF mf;
     for (int j = 0; j < 9; ++j) o.H[j] = 0;
