@@ -568,9 +568,45 @@ MCV_HD bool e_lu_solve(double (&A)[N][N], double (&b)[N][NB]) {
 
 struct ECplx { double re, im; };
 
+// Durand-Kerner sweeps of cv::solvePoly on a polynomial of fixed degree NN (co[0..NN], roots[0..NN)):
+// the same in-place updates in the same order as the generic loop below, with compile-time indices so
+// the GPU keeps roots and coefficients in registers. solvePoly stops only when a whole sweep leaves
+// every root unchanged (maxDiff <= 0), which in practice never happens: all 300 sweeps run.
+template <int NN>
+MCV_HD void e_dk_sweeps(ECplx (&co)[11], ECplx (&roots)[10]) {
+    ECplx cc[NN + 1], rr[NN];
+#pragma unroll
+    for (int i = 0; i <= NN; ++i) cc[i] = co[i];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) rr[i] = roots[i];
+    for (int iter = 0; iter < 300; ++iter) {
+        double maxDiff = 0;
+#pragma unroll
+        for (int i = 0; i < NN; ++i) {
+            const ECplx p = rr[i];
+            ECplx num = cc[NN], den = cc[NN];
+#pragma unroll
+            for (int j = 0; j < NN; ++j) {
+                num = {num.re * p.re - num.im * p.im + cc[NN - j - 1].re, num.re * p.im + num.im * p.re + cc[NN - j - 1].im};
+                if (j != i) {
+                    const ECplx d = {p.re - rr[j].re, p.im - rr[j].im};
+                    den = {den.re * d.re - den.im * d.im, den.re * d.im + den.im * d.re};
+                }
+            }
+            const double t = 1. / (den.re * den.re + den.im * den.im);
+            num = {(num.re * den.re + num.im * den.im) * t, (-num.re * den.im + num.im * den.re) * t};
+            rr[i] = {p.re - num.re, p.im - num.im};
+            const double a = sqrt(num.re * num.re + num.im * num.im);
+            maxDiff = maxDiff > a ? maxDiff : a;
+        }
+        if (maxDiff <= 0) break;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) roots[i] = rr[i];
+}
+
 // cv::solvePoly(coeffs, roots, 300) for a degree-10 real polynomial (coeffs ascending).
-MCV_HD void e_solve_poly10(const double* c, ECplx (&roots)[10]) {
-    ECplx co[11];
+MCV_HD void e_solve_poly10(const double* c, ECplx (&roots)[10], ECplx (&co)[11]) {
     for (int i = 0; i <= 10; ++i) co[i] = {c[i], 0.0};
     int n = 10;
     for (; n > 1; --n)
@@ -581,6 +617,10 @@ MCV_HD void e_solve_poly10(const double* c, ECplx (&roots)[10]) {
     for (int i = 0; i < n; ++i) {
         roots[i] = p;
         p = {p.re * r.re - p.im * r.im, p.re * r.im + p.im * r.re};
+    }
+    if (n == 10) {   // the full degree (the leading coefficient of det B(z) is not ~0)
+        e_dk_sweeps<10>(co, roots);
+        return;
     }
     for (int iter = 0; iter < 300; ++iter) {
         double maxDiff = 0;
@@ -605,11 +645,22 @@ MCV_HD void e_solve_poly10(const double* c, ECplx (&roots)[10]) {
     for (; n < 10; ++n) roots[n] = roots[n - 1];
 }
 
+// Working set of the export's five-point solve: a private array on the host; on the GPU one
+// __shared__ copy for the single solving lane (its data-dependent pivoting and root loops otherwise
+// run from 4 KB of scratch).
+struct E5RefWs {
+    double U[9][9];
+    double A[10][20], L[10][10], C[10][10], P[10][10];
+    ECplx co[11], roots[10];
+};
+
 // The export's five-point solve (normalised coordinates as given): E[10][9] row-major, count.
-MCV_HD int e_solve5_ref(const double* x1, const double* y1, const double* x2, const double* y2, double (*E)[9]) {
+MCV_HD int e_solve5_ref(const double* x1, const double* y1, const double* x2, const double* y2, double (*E)[9],
+                        E5RefWs& ws) {
     double nb[4][9];
     {
-        double U[9][9], w[5];
+        double (&U)[9][9] = ws.U;
+        double w[5];
         for (int i = 0; i < 9; ++i)
             for (int k = 0; k < 9; ++k) U[i][k] = 0.0;
         for (int i = 0; i < 5; ++i) {
@@ -621,14 +672,15 @@ MCV_HD int e_solve5_ref(const double* x1, const double* y1, const double* x2, co
         for (int b = 0; b < 4; ++b)
             for (int k = 0; k < 9; ++k) nb[b][k] = U[5 + b][k];
     }
-    double C[10][10];
+    double (&C)[10][10] = ws.C;
     {
-        double A[10][20], L[10][10];
+        double (&A)[10][20] = ws.A;
+        double (&L)[10][10] = ws.L;
         e_coeffs(nb, A);
         for (int r = 0; r < 10; ++r)
             for (int k = 0; k < 10; ++k) { L[r][k] = A[r][k]; C[r][k] = k == r ? 1.0 : 0.0; }
         if (!e_lu_solve<10, 10>(L, C)) return 0;    // C = A(:, 0:10)^-1
-        double P[10][10];
+        double (&P)[10][10] = ws.P;
         for (int r = 0; r < 10; ++r)
             for (int k = 0; k < 10; ++k) {
                 double s = 0;
@@ -642,8 +694,8 @@ MCV_HD int e_solve5_ref(const double* x1, const double* y1, const double* x2, co
     e_bz(&C[0][0], 10, bx, by, bc);
     double det[11];
     e_detpoly(bx, by, bc, det);
-    ECplx roots[10];
-    e_solve_poly10(det, roots);
+    ECplx (&roots)[10] = ws.roots;
+    e_solve_poly10(det, roots, ws.co);
     int count = 0;
     for (int i = 0; i < 10; ++i) {
         if (fabs(roots[i].im) > 1e-10) continue;

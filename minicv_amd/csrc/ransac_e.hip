@@ -389,12 +389,12 @@ __global__ __launch_bounds__(256) void mcv_e_cheirality(const double4* __restric
 // cvFivePoint: the export's own path (e_solve5_ref: JacobiSVD null space, LU elimination,
 // solvePoly roots with |Im| <= 1e-10 in its order, solveZ), one lane.
 __global__ __launch_bounds__(64) void mcv_e_fivepoint(EFiveIn in, EOneOut* __restrict__ out) {
+    __shared__ E5RefWs ws;
     if (threadIdx.x != 0) return;
-    double E[kEMaxModels][9];
-    const int n = e_solve5_ref(in.x1, in.y1, in.x2, in.y2, E);
+    const int n = e_solve5_ref(in.x1, in.y1, in.x2, in.y2, out->E, ws);   // models straight to the record
     out->status = n;
-    for (int s = 0; s < kEMaxModels; ++s)
-        for (int k = 0; k < 9; ++k) out->E[s][k] = s < n ? E[s][k] : 0.0;
+    for (int s = n > 0 ? n : 0; s < kEMaxModels; ++s)
+        for (int k = 0; k < 9; ++k) out->E[s][k] = 0.0;
 }
 
 // ---- launchers ---------------------------------------------------------------------------------

@@ -347,7 +347,8 @@ extern "C" MCV_API int mcvHostFivePointRef(const double* p20, double* E90) {
     MCV_GUARD(-1, {
         if (!p20 || !E90) fail("mcvHostFivePointRef: null argument");
         double E[kEMaxModels][9];
-        const int n = e_solve5_ref(p20, p20 + 5, p20 + 10, p20 + 15, E);
+        E5RefWs ws;
+        const int n = e_solve5_ref(p20, p20 + 5, p20 + 10, p20 + 15, E, ws);
         for (int s = 0; s < kEMaxModels; ++s)
             for (int k = 0; k < 9; ++k) E90[9 * s + k] = s < n ? E[s][k] : 0.0;
         return n;

@@ -130,7 +130,8 @@ int main() {
                 }
                 std::memset(E1, 0, sizeof(E1));
                 std::memset(E2, 0, sizeof(E2));
-                const int r1 = mcv::e_solve5_ref(x1, y1, x2, y2, E1);
+                mcv::E5RefWs ws5;
+                const int r1 = mcv::e_solve5_ref(x1, y1, x2, y2, E1, ws5);
                 const int r2 = orc_e_solve5_ref(x1, y1, x2, y2, E2);
                 expect(r1 == r2, "e ref count", r1, r2);
                 if (r1 > 0 && r1 == r2) expect(same_bits(&E1[0][0], E2, 9 * r1), "e ref models", h, N);
