@@ -48,8 +48,8 @@ struct Plan {
     DevBuf<double> epw;       // PnP: EPnP solve points (world, double)
     DevBuf<double> eus;       // PnP: EPnP solve points (pixels of the undistorted observations)
     DevBuf<int> eidx;         // PnP: inlier indices of the EPnP solve
-    int eLastKind = -1;       // PnP: minimal solver of the last evaluated chunk (1 EPnP, 0 AP3P)
-    int64_t eLastBegin = -1;  // essential / PnP: hypothesis range of the last evaluated chunk
+    int eLastKind = -1;       // minimal solver of the last evaluated chunk (PnP: 1 EPnP, 0 AP3P; F: 10 eigen, 11 elimination)
+    int64_t eLastBegin = -1;  // essential / PnP / 8-point F: hypothesis range of the last evaluated chunk
     int64_t eLastCount = 0;
     uint64_t eLastSeed = 0;
     const void* eLastPts = nullptr;

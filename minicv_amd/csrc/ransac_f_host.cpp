@@ -26,13 +26,25 @@ int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     const double t = effective_threshold(cfg);
     const float thr2 = (float)(t * t);
     FOneOut* d_one = (FOneOut*)P.one.p;
-    if (cfg.flags & MCV_FLAG_SEVEN_POINT) launch_f7_one(d_pts, N, cfg.seed, hyp, d_one, s);   // hyp = model slot
-    else launch_f_one(d_pts, N, cfg.seed, hyp, d_one, s, (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0);
-    MCV_HIP(hipGetLastError());
+    const bool fast = (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0;
     FOneOut one;
-    MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(FOneOut), hipMemcpyDeviceToHost, s));
-    MCV_HIP(hipStreamSynchronize(s));
-    std::memcpy(&one, P.h_one.p, sizeof(FOneOut));
+    if (!(cfg.flags & MCV_FLAG_SEVEN_POINT) && hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount &&
+        P.eLastSeed == cfg.seed && P.eLastPts == d_pts && P.eLastKind == (fast ? 11 : 10)) {
+        // the winner's model straight from the last chunk's buffer (the same code produced it) instead
+        // of a single-lane re-solve (the eigen-solve's ~0.5 ms latency)
+        const FModelD* d_m = (const FModelD*)P.models.p + (hyp - P.eLastBegin);
+        MCV_HIP(hipMemcpyAsync(P.h_one.p, d_m, sizeof(FModelD), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        std::memcpy(one.F, P.h_one.p, sizeof(FModelD));
+        one.status = 1;
+    } else {
+        if (cfg.flags & MCV_FLAG_SEVEN_POINT) launch_f7_one(d_pts, N, cfg.seed, hyp, d_one, s);   // hyp = model slot
+        else launch_f_one(d_pts, N, cfg.seed, hyp, d_one, s, fast);
+        MCV_HIP(hipGetLastError());
+        MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(FOneOut), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        std::memcpy(&one, P.h_one.p, sizeof(FOneOut));
+    }
     if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
     MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
     launch_f_mask(d_pts, N, one.F, thr2, f_error_kind(cfg), d_mask, P.count.p, s);

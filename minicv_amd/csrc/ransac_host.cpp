@@ -353,6 +353,7 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         }
     } else if (f_seven(P.model, cfg)) {
         // OpenCV FM_RANSAC: 7-point samples, 3 model slots per hypothesis (slot keys like essential)
+        P.eLastBegin = -1;
         launch_f7_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
         P.bb4.ensure(4);
         launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
@@ -369,6 +370,12 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
             ProfScope pg("f_generate", s);
             launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s, fast_minimal(cfg));
         }
+        // the winner's fp64 model can come straight from this chunk's buffer (f_finalize)
+        P.eLastBegin = hypBegin;
+        P.eLastCount = hypCount;
+        P.eLastSeed = cfg.seed;
+        P.eLastPts = d_pts;
+        P.eLastKind = fast_minimal(cfg) ? 11 : 10;
         P.bb4.ensure(4);
         launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         ProfScope ps("f_verify", s);
