@@ -31,7 +31,7 @@ namespace mcv {
 template <bool FAST, int L = kEigLanes>
 __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __restrict__ pts4, int N, uint64_t seed,
                                                      int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
-                                                     int* __restrict__ counts) {
+                                                     double* __restrict__ h64, int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     double H[9];
@@ -47,6 +47,7 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
     }
     if (st == 1) {
         models[i] = mf;
+        for (int j = 0; j < 9; ++j) h64[9 * (int64_t)i + j] = H[j];
         counts[i] = 0;
     } else {
         // the zero model (w = 1 everywhere) keeps the packed sweep's slot well-defined
@@ -1011,27 +1012,27 @@ struct OpLMErr {   // 1: |r|^2 only
 // Launchers (host side, called from ransac_host.cpp)
 // ------------------------------------------------------------------------------------------
 void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
-                       int* d_counts, hipStream_t s, bool fast) {
+                       double* d_h64, int* d_counts, hipStream_t s, bool fast) {
     if (fast)
         hipLaunchKernelGGL(mcv_h_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, seed, hypBegin,
-                           hypCount, (HModelF*)d_models, d_counts);
+                           hypCount, (HModelF*)d_models, d_h64, d_counts);
     else
         switch (eig_lanes()) {
             case 64:
                 hipLaunchKernelGGL((mcv_h_generate<false, 64>), dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_counts);
+                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
             case 48:
                 hipLaunchKernelGGL((mcv_h_generate<false, 48>), dim3((hypCount + 47) / 48), dim3(48), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_counts);
+                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
             case 32:
                 hipLaunchKernelGGL((mcv_h_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_counts);
+                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
             default:
                 hipLaunchKernelGGL((mcv_h_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_counts);
+                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
         }
 }
 

@@ -110,6 +110,7 @@ void Plan::reserve(int n, int64_t hyps) {
         pts.ensure((size_t)maxN * 4);
     }
     models.ensure((size_t)maxHyps * model_bytes(model));
+    if (model == MCV_MODEL_HOMOGRAPHY) h64.ensure((size_t)maxHyps * 9);
     counts.ensure((size_t)maxHyps * slots);
     pkey.ensure(512);
     pfail.ensure(512);
@@ -339,8 +340,15 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         }
         {
             ProfScope pg("h_generate", s);
-            launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s, fast_minimal(cfg));
+            launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, P.h64.p, d_counts, s,
+                              fast_minimal(cfg));
         }
+        // the winner's models can come straight from this chunk's buffers (h_finalize)
+        P.eLastBegin = hypBegin;
+        P.eLastCount = hypCount;
+        P.eLastSeed = cfg.seed;
+        P.eLastPts = d_pts;
+        P.eLastKind = fast_minimal(cfg) ? 21 : 20;
         ProfScope ps("h_verify", s);
         if (!fused) {
             // default: OpenCV's op-by-op error, certified division-free packed sweep
@@ -399,7 +407,19 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     const float thr2 = (float)(t * t);
     // winner re-solve -> mask from the device-side record -> one read-back of both
     HOneOut* d_one = (HOneOut*)P.one.p;
-    launch_h_one(d_pts, N, cfg.seed, hyp, d_one, s, fast_minimal(cfg));
+    if (hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount && P.eLastSeed == cfg.seed && P.eLastPts == d_pts &&
+        P.eLastKind == (fast_minimal(cfg) ? 21 : 20)) {
+        // the winner's fp64 and fp32 models straight from the last chunk's buffers (the same code
+        // produced them) instead of a single-lane eigen re-solve (~0.4 ms); a winner has status 1
+        const int64_t local = hyp - P.eLastBegin;
+        MCV_HIP(hipMemcpyAsync(d_one->H, P.h64.p + 9 * local, 9 * sizeof(double), hipMemcpyDeviceToDevice, s));
+        MCV_HIP(hipMemcpyAsync(d_one->hf, P.models.p + local * sizeof(HModelF), sizeof(HModelF),
+                               hipMemcpyDeviceToDevice, s));
+        P.h_i.p[1] = 1;
+        MCV_HIP(hipMemcpyAsync(&d_one->status, P.h_i.p + 1, sizeof(int), hipMemcpyHostToDevice, s));
+    } else {
+        launch_h_one(d_pts, N, cfg.seed, hyp, d_one, s, fast_minimal(cfg));
+    }
     MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
     launch_h_mask_one(d_pts, N, d_one, thr2, fused_error(cfg), d_mask, P.count.p, s);
     MCV_HIP(hipGetLastError());
