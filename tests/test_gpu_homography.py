@@ -242,3 +242,40 @@ def test_eigen_minimal_solver_stress(torch_dev, oracle, seed):
     got, _ = device_counts(torch_dev, src, dst, seed, begin, 16384, thr, unfused=True)
     ref = oracle.h_counts(oracle.pack4(src, dst), seed, begin, 16384, float(np.float32(thr * thr)))
     np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("model", [N.MODEL_HOMOGRAPHY, N.MODEL_FUNDAMENTAL])
+def test_finalize_fetch_and_resolve_paths(torch_dev, oracle, model):
+    """finalize takes the winner's fp64 model from the last evaluated chunk's buffers, or re-solves the
+    hypothesis on one lane when it lies outside that chunk: both give the oracle's model bit for bit
+    (no refine) and its inlier count."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    n = 1500
+    if model == N.MODEL_HOMOGRAPHY:
+        src, dst, _ = S.homography_problem(n, 26)
+    else:
+        src, dst, _, _ = S.fundamental_problem(n, 26)
+    pts4 = oracle.pack4(src, dst)
+    pts = D.pack_points_tensor(src, dst, dev)
+    plan = D.RansacPlan(model, n, 512)
+    thr = 5e-3
+    cfg = opencv.RansacParams(threshold=thr, seed=26, refine=False).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(512, dtype=torch.int32, device=dev)
+    mask = torch.zeros(n, dtype=torch.uint8, device=dev)
+    plan.evaluate(pts, n, cfg, 1000, 512, key, counts)     # last chunk = [1000, 1512)
+    c = counts.cpu().numpy()
+    inside = 1000 + int(np.argmax(c))
+    for hyp in (inside, 77):                                # fetch path, then the re-solve path
+        fc, M = plan.finalize(pts, n, cfg, hyp, mask)
+        if model == N.MODEL_HOMOGRAPHY:
+            st, H, hf, _ = oracle.h_hypothesis(pts4, 26, hyp)
+            ref_count = oracle.h_count(pts4, hf, float(np.float32(thr * thr)))
+            np.testing.assert_array_equal(M.ravel(), H)
+        else:
+            st, F, _ = oracle.f_hypothesis(pts4, 26, hyp)
+            ref_count = oracle.f_count(pts4, F, float(np.float32(thr * thr)), oracle.f_kind(0, True))
+            np.testing.assert_array_equal(M.ravel(), F)
+        assert st == 1 and fc == ref_count == int(mask.sum().item())
+    plan.close()
