@@ -134,6 +134,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pnp-kind", default="EPNP", choices=["Iterative", "EPNP", "P3P", "DLS", "UPNP", "AP3P"],
                     help="pnp workload: the reference's solverKind (EPNP = its own testPnp, Program.fs:27-32)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary fast_minimal leg of the H / F lines (profiling runs: one solver per process)")
     ap.add_argument("--fast-minimal", action="store_true",
                     help="opt-in elimination minimal solver for H / 8-point F (default: OpenCV's cv::eigen runKernel)")
     ap.add_argument("--fused", action="store_true",
@@ -507,7 +509,7 @@ def bench_ransac(args):
             line["cpu_baseline"] = (cpu_baseline_f if fund else cpu_baseline)(src, dst, args.cpu_seconds)
         else:
             line["cpu_baseline"] = None
-        if world == 1 and not args.fast_minimal:
+        if world == 1 and not args.fast_minimal and not args.no_secondary:
             # the same step with the opt-in elimination minimal solver (a secondary figure, not `value`)
             cfg_default = cfg
             cfg = opencv.RansacParams(threshold=THR, confidence=0.995, max_iters=total,

@@ -33,13 +33,13 @@ fi
 cd /tmp && export TMPDIR=/tmp
 for w in homography fundamental essential pnp hamming l2 scaled; do
     step prof_$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$w" -o run -- \
-        python3 "$R/bench.py" --workload $w --steps 5 --warmup 2 --no-cpu-baseline
+        python3 "$R/bench.py" --workload $w --steps 5 --warmup 2 --no-cpu-baseline --no-secondary
 done
 for w in homography fundamental essential pnp hamming l2 scaled; do
     step pmc_fetch_$w 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch_$w" -o run -- \
-        python3 "$R/bench.py" --workload $w --steps 3 --warmup 1 --no-cpu-baseline
+        python3 "$R/bench.py" --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-secondary
     step pmc_write_$w 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write_$w" -o run -- \
-        python3 "$R/bench.py" --workload $w --steps 3 --warmup 1 --no-cpu-baseline
+        python3 "$R/bench.py" --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-secondary
 done
 step pmc_sq 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d "$R/gpurun_out/pmc_sq" -o run -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
+    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-secondary
