@@ -234,3 +234,23 @@ def test_e_counts_prefilter_extremes(torch_dev, oracle, case):
         np.testing.assert_array_equal(counts.cpu().numpy(), ref)
         assert (ref > 0).any()
     plan.close()
+
+
+@pytest.mark.slow
+def test_e_counts_bench_workload_full(torch_dev, oracle):
+    """bench.py's essential workload at full size (100k correspondences, 65536 hypotheses, <= 10 model
+    slots each): every slot's status / count equals the oracle's (OpenMP over the box's threads)."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    n, H, focal, pp = 100_000, 1 << 16, 800.0, (640.0, 360.0)
+    a, b, *_ = S.essential_problem(n, seed=6, outlier_frac=0.5)
+    pts = D.pack_essential_tensor(a, b, focal, pp, dev)
+    plan = D.RansacPlan(N.MODEL_ESSENTIAL, n, H)
+    thr = 1.0 / focal
+    cfg = opencv.RansacParams(threshold=thr, seed=6, fixed_iters=True, max_iters=H).to_c()
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(H * N.E_SLOTS, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, 0, H, key, counts)
+    ref = oracle.e_counts(oracle.pack_e(a, b, focal, pp), 6, 0, H, float(np.float32(thr * thr)), 1)
+    np.testing.assert_array_equal(counts.cpu().numpy(), ref)
+    plan.close()

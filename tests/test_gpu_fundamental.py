@@ -221,7 +221,7 @@ def test_f_counts_prefilter_extremes(torch_dev, oracle, case):
 @pytest.mark.slow
 def test_full_size_cfg4(torch_dev, oracle):
     """BASELINE config[3] at full size: F-RANSAC over 500k correspondences, 65536 fixed hypotheses.
-    32 spot hypotheses equal the oracle's counts, the reduced key is the argmax of the device's own
+    every hypothesis' count equals the oracle's, the reduced key is the argmax of the device's own
     counts, the winner's mask holds exactly its count, and the host export sharded over 8 workspaces
     (deviceCount = 8; round-robin over the visible GPUs) is bit-identical to deviceCount = 1."""
     torch, dev = torch_dev
@@ -238,12 +238,10 @@ def test_full_size_cfg4(torch_dev, oracle):
     c = counts.cpu().numpy()
     cnt, idx = D.unpack_key(int(key[0].item()))
     assert cnt == c.max() and idx == int(np.argmax(c))
-    rng = np.random.default_rng(1)
-    pick = np.sort(rng.choice(H, size=32, replace=False))
+    # every one of the 65536 hypotheses against the oracle (OpenMP over the box's threads, ~5 s)
     p4 = oracle.pack4(a, b)
     thr2 = float(np.float32(thr * thr))
-    for h in list(pick) + [idx]:
-        assert c[h] == oracle.f_counts(p4, 4, int(h), 1, thr2)[0], h
+    np.testing.assert_array_equal(c, oracle.f_counts(p4, 4, 0, H, thr2))
     mask = torch.zeros(n, dtype=torch.uint8, device=dev)
     fc, F = plan.finalize(pts, n, opencv.RansacParams(threshold=thr, seed=4).to_c(), idx, mask)
     assert fc == cnt == int(mask.sum().item())

@@ -313,3 +313,26 @@ def test_pnp_certified_sweep_event_overflow(native, gpu, oracle):
     idx = rng.integers(0, len(distinct), 65536)
     counts = _sweep(L, pts8, c8, [distinct[i] for i in idx], thr2, False, 0)
     np.testing.assert_array_equal(counts, ref[idx])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", [1, 5])
+def test_pnp_counts_bench_workload_full(torch_dev, oracle, kind):
+    """bench.py's PnP workload at full size (20k correspondences with k1 k2 p1 p2, 65536 EPnP / AP3P
+    hypotheses): every hypothesis' status / count equals the oracle's."""
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    n, H = 20_000, 1 << 16
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=8, outlier_frac=0.5, sigma=0.5, dist=DIST)
+    pts = D.pack_pnp_tensor(img, W, dev)
+    plan = D.RansacPlan(N.MODEL_PNP, n, H)
+    plan.set_camera(K, d)
+    cfg = opencv.RansacParams(threshold=2.0, confidence=0.99, max_iters=H, seed=8, fixed_iters=True).to_c()
+    cfg.pnpKind = kind
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(H, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, 0, H, key, counts)
+    ref = oracle.pnp_counts(oracle.pack_pnp(img, W), oracle.cam8(K, d), 8, 0, H, float(np.float32(4.0)), False,
+                            kind=kind)
+    np.testing.assert_array_equal(counts.cpu().numpy(), ref)
+    plan.close()
