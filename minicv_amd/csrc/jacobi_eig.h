@@ -33,10 +33,10 @@ namespace mcv {
 // branch-free form sends the two skipped indices there).
 static constexpr int kEigA = 0, kEigW = 36, kEigV = 45, kEigJunk = 126, kEigWs = 127;
 // Lanes per hypothesis-kernel block: the 1016-byte working set per lane makes LDS the occupancy
-// limit (160 KB per CU). 39 lanes = 4 blocks per CU, one wave on every SIMD (screened on cfg3:
-// 32 / 39 / 48 / 64 lanes -> 14.9 / 11.5 / 12.5 / 13.9 ms for 2^20 hypotheses); MCV_EIG_LANES =
-// 32 / 48 / 64 re-screens.
-static constexpr int kEigLanes = 39;
+// limit (160 KB per CU). 40 lanes = 4 blocks of 40.6 KB per CU, one wave on every SIMD (cfg3 screen,
+// 2^20 hypotheses: 64 -> 39 lanes took the H generate 13.9 -> 11.4 ms; 39 vs 40 lanes 9.63 vs 9.34 ms
+// in scripts/eig_lanes_screen.sh); MCV_EIG_LANES = 32 / 39 / 48 / 64 re-screens.
+static constexpr int kEigLanes = 40;
 inline int eig_lanes() {   // host: the launchers' screen knob
     static const int v = [] {
         const char* e = getenv("MCV_EIG_LANES");

@@ -333,9 +333,14 @@ void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBeg
                 hipLaunchKernelGGL((mcv_f_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
                                    seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
                 break;
-            default:
+            case 39:
                 hipLaunchKernelGGL((mcv_f_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
                                    seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+                break;
+            default:
+                hipLaunchKernelGGL((mcv_f_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
+                                   dim3(kEigLanes), 0, s, d_pts4, N, seed, hypBegin, hypCount, (FModelD*)d_models,
+                                   d_counts);
         }
 }
 

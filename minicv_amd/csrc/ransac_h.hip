@@ -1026,13 +1026,19 @@ void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBeg
                 hipLaunchKernelGGL((mcv_h_generate<false, 48>), dim3((hypCount + 47) / 48), dim3(48), 0, s, d_pts4, N,
                                    seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
+
             case 32:
                 hipLaunchKernelGGL((mcv_h_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
                                    seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
-            default:
+            case 39:
                 hipLaunchKernelGGL((mcv_h_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
                                    seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
+                break;
+            default:
+                hipLaunchKernelGGL((mcv_h_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
+                                   dim3(kEigLanes), 0, s, d_pts4, N, seed, hypBegin, hypCount, (HModelF*)d_models, d_h64,
+                                   d_counts);
         }
 }
 
