@@ -45,8 +45,15 @@ inline int eig_lanes() {   // host: the launchers' screen knob
     return v;
 }
 
-// Packed index of A(r, c), r < c < 9: row r starts at 7r - r(r-1)/2 - 1 + (r + 1).
-MCV_HD int eig_row_base(int r) { return 7 * r - ((r * (r - 1)) >> 1) - 1; }
+// Packed index of A(r, c), r < c < 9: row r starts at 7r - r(r-1)/2 - 1 + (r + 1); the base is
+// r(15 - r)/2 - 1 (r(15 - r) is even), one 24-bit multiply for a dynamic r.
+MCV_HD int eig_row_base(int r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (int)(__umul24((unsigned)r, (unsigned)(15 - r)) >> 1) - 1;
+#else
+    return ((r * (15 - r)) >> 1) - 1;
+#endif
+}
 MCV_HD int eig_tri(int r, int c) { return eig_row_base(r) + c; }
 
 struct EigWsLocal {
@@ -111,9 +118,10 @@ MCV_HD void eig_rotation(double p, double y, double& c, double& s, double& t) {
     if (y < 0) s = -s, t = -t;
 }
 
-// First maximum of a candidate pair in scan order: the later one wins only when strictly greater.
+// First maximum (by magnitude) of a candidate pair in scan order: the later one wins only when
+// strictly greater. Values stay signed; the compare takes the magnitudes (operand modifiers).
 MCV_HD void eig_pick(double& v, int& kl, double v2, int kl2) {
-    const bool t = v < v2;
+    const bool t = __builtin_fabs(v) < __builtin_fabs(v2);
     v = t ? v2 : v;
     kl = t ? kl2 : kl;
 }
@@ -130,6 +138,7 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
 #pragma unroll
 #endif
     for (int i = 0; i < n * n; ++i) ws[kEigV + i] = (i / n == i % n) ? 1.0 : 0.0;
+    ws[kEigJunk] = 0.0;   // stays +0: the skipped pair rotates (0, 0) into (+0, +0)
     uint32_t indR = 0, indC = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
@@ -171,7 +180,7 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
 #endif
         for (int i = 0; i < n - 1; ++i) {
             const int c = eig_nib(indR, i);
-            cv[i] = __builtin_fabs(ws[eig_row_base(i) + c]);
+            cv[i] = ws[eig_row_base(i) + c];
             ck[i] = i * 16 + c;
         }
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -179,7 +188,7 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
 #endif
         for (int i = 1; i < n; ++i) {
             const int r = eig_nib(indC, i - 1);
-            cv[7 + i] = __builtin_fabs(ws[eig_row_base(r) + i]);
+            cv[7 + i] = ws[eig_row_base(r) + i];
             ck[7 + i] = r * 16 + i;
         }
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -192,7 +201,7 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
             for (int i = 0; i < 16; i += 2 * h) eig_pick(cv[i], ck[i], cv[i + h], ck[i + h]);
         const int k = ck[0] >> 4, l = ck[0] & 15;
         const int ekl = eig_tri(k, l);
-        const double p = ws[ekl];
+        const double p = cv[0];   // = A(k, l)
         if (__builtin_fabs(p) <= kDblEpsilon) break;
         // every operand of the rotation is read before anything is written back (the reads do not
         // depend on the scalar chain, so their LDS latency hides behind it): W[k], W[l], for every
@@ -216,7 +225,7 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
             a0[i] = ws[e0[i]];
             b0[i] = ws[e1[i]];
         }
-        const int vk = kEigV + n * k, vl = kEigV + n * l;
+        const int vk = kEigV + (k << 3) + k, vl = kEigV + (l << 3) + l;   // + 9 k, + 9 l
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
@@ -230,19 +239,17 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
         ws[ekl] = 0;
         ws[kEigW + k] = wk - t;
         ws[kEigW + l] = wl + t;
-        // rotate rows and columns k and l; nk / nl keep the new values (A(k, l) = 0 at i = l / i = k)
-        // for the rescans
+        // rotate rows and columns k and l; nk / nl keep the new values for the rescans (at i = k, l the
+        // junk pair (0, 0) rotates to (+0, +0): A(k, l) = 0 without a select)
         double nk[n], nl[n];
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
         for (int i = 0; i < n; ++i) {
-            const bool skip = i == k || i == l;
-            const double v0 = a0[i] * c - b0[i] * s, v1 = a0[i] * s + b0[i] * c;
-            ws[e0[i]] = v0;
-            ws[e1[i]] = v1;
-            nk[i] = skip ? 0.0 : v0;
-            nl[i] = skip ? 0.0 : v1;
+            nk[i] = a0[i] * c - b0[i] * s;
+            nl[i] = a0[i] * s + b0[i] * c;
+            ws[e0[i]] = nk[i];
+            ws[e1[i]] = nl[i];
         }
         // rotate eigenvectors
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -252,21 +259,23 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
             ws[vk + i] = va[i] * c - vb[i] * s;
             ws[vl + i] = va[i] * s + vb[i] * c;
         }
-        // refresh indR / indC of rows and columns k and l (first maximum; every |value| >= 0 beats
-        // the -1 start, so the first in-range element is taken unconditionally as in OpenCV)
-        int mRk = 0, mCk = 0, mRl = 0, mCl = 0;
-        double vRk = -1, vCk = -1, vRl = -1, vCl = -1;
+        // refresh indR / indC of rows and columns k and l (first maximum by magnitude). OpenCV takes
+        // the first in-range element unconditionally; here the index starts there (k + 1 for a row,
+        // 0 for a column) with a running value of 0, which only a strictly larger |value| replaces —
+        // the same index for finite values. Values stay signed (magnitudes through the compare).
+        int mRk = k + 1, mCk = 0, mRl = l + 1, mCl = 0;
+        double vRk = 0, vCk = 0, vRl = 0, vCl = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
         for (int i = 0; i < n; ++i) {
             const double ak = __builtin_fabs(nk[i]), al = __builtin_fabs(nl[i]);
-            const bool tRk = i > k && vRk < ak, tCk = i < k && vCk < ak;
-            const bool tRl = i > l && vRl < al, tCl = i < l && vCl < al;
-            vRk = tRk ? ak : vRk; mRk = tRk ? i : mRk;
-            vCk = tCk ? ak : vCk; mCk = tCk ? i : mCk;
-            vRl = tRl ? al : vRl; mRl = tRl ? i : mRl;
-            vCl = tCl ? al : vCl; mCl = tCl ? i : mCl;
+            const bool tRk = i > k && __builtin_fabs(vRk) < ak, tCk = i < k && __builtin_fabs(vCk) < ak;
+            const bool tRl = i > l && __builtin_fabs(vRl) < al, tCl = i < l && __builtin_fabs(vCl) < al;
+            vRk = tRk ? nk[i] : vRk; mRk = tRk ? i : mRk;
+            vCk = tCk ? nk[i] : vCk; mCk = tCk ? i : mCk;
+            vRl = tRl ? nl[i] : vRl; mRl = tRl ? i : mRl;
+            vCl = tCl ? nl[i] : vCl; mCl = tCl ? i : mCl;
         }
         if (k < n - 1) indR = eig_set_nib(indR, k, mRk);
         if (k > 0) indC = eig_set_nib(indC, k - 1, mCk);
