@@ -380,7 +380,8 @@ MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, uint64_t seed
 MCV_API long long mcvTestRcpExhaustive(int mode, uint32_t* firstMismatches16);
 /* Device self-test: number of sampled (n, d), d in +-[2^-64, 2^64], where the unscaled fp64
  * division (rcp_f64_refined + div_f64_refined) differs from n / d (mode 0: 2^-900 <= |n| < 2^700;
- * 1: n = 1; 2: n = k d, |k| <= 1000; 3: d at the domain ends); first 16 (n, d) pairs returned. */
+ * 1: n = 1; 2: n = k d, |k| <= 1000; 3: d at the domain ends); first 16 (n, d) pairs returned.
+ * Mode 4: sampled x in [1, 2] where the rotation's unscaled sqrt_f64_1to2 differs from sqrt (pairs (x, 0)). */
 MCV_API long long mcvTestDivF64(int mode, unsigned long long seed, long long count, double* firstMismatches32);
 /* Device self-test: run the homography inlier sweep on caller-supplied fp32 models (8 floats each);
  * fused: 0 = op-by-op error (scalar sweep), 1 = fused (scalar sweep), 2 = fused through the packed-f32

@@ -92,11 +92,11 @@ MCV_HD void eig_rotation(double p, double y, double& c, double& s, double& t) {
     const double hi = ag ? ap : ay, lo = ag ? ay : ap;
     if (__builtin_expect(hi <= 0x1p60 && (lo == 0.0 || lo >= 0x1p-900), 1)) {
         const double r1 = div_f64_refined(lo, hi, rcp_f64_refined(hi));
-        const double h1 = hi * __builtin_sqrt(1 + r1 * r1);
+        const double h1 = hi * sqrt_f64_1to2(1 + r1 * r1);   // r1 <= 1
         double tt = ay + h1;          // hypot(p, y): hi > 0 here, so the `else 0` case cannot occur
         const double rt = rcp_f64_refined(tt);
         const double r2 = div_f64_refined(ap, tt, rt);
-        const double ss = tt * __builtin_sqrt(1 + r2 * r2);   // hypot(p, t) with t >= |p|
+        const double ss = tt * sqrt_f64_1to2(1 + r2 * r2);   // hypot(p, t) with t >= |p|
         const double rs = rcp_f64_refined(ss);
         c = div_f64_refined(tt, ss, rs);
         s = div_f64_refined(p, ss, rs);

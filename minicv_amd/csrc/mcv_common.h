@@ -198,4 +198,25 @@ MCV_HD double div_f64_refined(double n, double d, double r) {
 // The denominator domain of the two helpers above.
 MCV_HD bool div_f64_refined_domain(double d) { return __builtin_fabs(d) >= 0x1p-64 && __builtin_fabs(d) <= 0x1p64; }
 
+// sqrt(x) for x in [1, 2] (the 1 + r^2, r <= 1, of a hypot): gfx950's correctly rounded fp64 sqrt
+// expansion (v_rsq_f64, then g = x y, h = y / 2 and three fma refinement rounds) without its
+// denormal scaling (ldexp by 0 here) and zero / infinity class select (never taken here) — the same
+// bits as sqrt(x) on that range, 4 ops shorter on the rotation's dependent chain
+// (mcvTestDivF64 mode 4 samples it: tests/test_gpu_selftest.py). Host: sqrt.
+MCV_HD double sqrt_f64_1to2(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+#else
+    return __builtin_sqrt(x);
+#endif
+}
+
 }  // namespace mcv

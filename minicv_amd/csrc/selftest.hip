@@ -61,6 +61,7 @@ __device__ __forceinline__ double random_f64(uint64_t bits, uint64_t ebits, int 
 // Samples (n, d) with d in +-[2^-64, 2^64] and compares div_f64_refined against n / d.
 //   mode 0: |n| in [2^-900, 2^699]      mode 1: n = 1 (the reciprocal)
 //   mode 2: n = d * k, k a small integer (exact quotients)   mode 3: d at the domain ends
+//   mode 4: sqrt_f64_1to2(x) against sqrt(x), x in [1, 2] (the pair records (x, 0))
 __global__ __launch_bounds__(256) void mcv_div_check(uint64_t seed, uint64_t count, int mode,
                                                      unsigned long long* mism, double* first) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
@@ -68,6 +69,19 @@ __global__ __launch_bounds__(256) void mcv_div_check(uint64_t seed, uint64_t cou
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += stride) {
         const uint64_t a = splitmix64(seed ^ (i * 4 + 0)), b = splitmix64(seed ^ (i * 4 + 1));
         const uint64_t c = splitmix64(seed ^ (i * 4 + 2)), g = splitmix64(seed ^ (i * 4 + 3));
+        if (mode == 4) {
+            const double x = (g & 0xFFFF) == 0 ? 2.0 : random_f64(a & 0x000FFFFFFFFFFFFFull, b, 0, 0);
+            const double r = sqrt_f64_1to2(x), ref = __builtin_sqrt(x);
+            if (__double_as_longlong(r) != __double_as_longlong(ref)) {
+                ++local;
+                const unsigned long long slot = atomicAdd(mism + 1, 1ull);
+                if (slot < 16) {
+                    first[2 * slot] = x;
+                    first[2 * slot + 1] = 0.0;
+                }
+            }
+            continue;
+        }
         double d = random_f64(a, b, -64, 63);
         if (mode == 3) d = (g & 1) ? random_f64(a, b, -64, -64) : random_f64(a, b, 63, 63);
         double n;
