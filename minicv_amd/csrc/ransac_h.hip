@@ -26,8 +26,9 @@ namespace mcv {
 // ------------------------------------------------------------------------------------------
 // Hypothesis generation
 // ------------------------------------------------------------------------------------------
-// One lane per hypothesis; the runKernel eigen-solve's working set (127 doubles) in LDS, one column
-// per lane (jacobi_eig.h): 64 KB per 64-lane block. FAST = MCV_FLAG_FAST_MINIMAL (no workspace).
+// One lane per hypothesis; the runKernel eigen-solve's working set (127 doubles) in LDS, one slice
+// per lane (jacobi_eig.h): 40.6 KB per 40-lane block, 4 blocks per CU. FAST = MCV_FLAG_FAST_MINIMAL
+// (no workspace).
 template <bool FAST, int L = kEigLanes>
 __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __restrict__ pts4, int N, uint64_t seed,
                                                      int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
