@@ -146,15 +146,24 @@ MCV_API mcvBool cvDetectArucoMarkers(char* data, int width, int height, int chan
 /* flags */
 #define MCV_FLAG_FIXED_ITERS  1   /* evaluate exactly maxIters hypotheses (no adaptive stop) */
 #define MCV_FLAG_NO_REFINE    2   /* return the best hypothesis' model (skip inlier refit + LM) */
-#define MCV_FLAG_FUSED_ERROR  4   /* opt-in: FMA-contracted inlier error (what a compiler contracting
-                                     OpenCV's computeError produces, e.g. clang on arm64). Default:
-                                     op-by-op, every operation rounded as written = OpenCV's x86-64
-                                     (SSE baseline) build, the reference's Linux/AMD64 target. */
+#define MCV_FLAG_RETIRED_4    4   /* retired: meant "unfused error" in the round-1 header (now the default);
+                                     rejected with an error so an old caller cannot silently get the
+                                     opposite definition */
 #define MCV_FLAG_SEVEN_POINT  8   /* fundamental only: OpenCV FM_RANSAC's minimal solver (run7Point: 7-point
                                      samples, up to 3 models each, model slots 3h .. 3h+2 in the device
                                      API) instead of the 8-point default; with errorKind EPIPOLAR it is
                                      cv::findFundamentalMat(FM_RANSAC). Needs N >= 15 (OpenCV switches to
                                      LMeDS below that, not provided) or N == 7 (one solve, first model). */
+#define MCV_FLAG_CV_SAMPLER   32  /* OpenCV's own sample stream instead of the counter-based Philox one:
+                                     cv::RNG((uint64)-1) per call, getSubset's duplicate rejection and
+                                     checkSubset, 10000 attempts (RANSACPointSetRegistrator::run), generated
+                                     on the host before the GPU evaluates the hypotheses; cfg->seed is then
+                                     unused. The default of cvRecoverPose(s) / cvSolvePnPRansac and of the
+                                     NULL-config defaults; sequential by definition: <= 2^24 hypotheses */
+#define MCV_FLAG_FUSED_ERROR  64  /* opt-in: FMA-contracted inlier error (what a compiler contracting
+                                     OpenCV's computeError produces, e.g. clang on arm64). Default:
+                                     op-by-op, every operation rounded as written = OpenCV's x86-64
+                                     (SSE baseline) build, the reference's Linux/AMD64 target. */
 #define MCV_FLAG_FAST_MINIMAL 16  /* homography / 8-point fundamental: opt-in minimal solve by 8x8 Gaussian
                                      elimination with h22 = 1 / f22 = 1 (no eigenvalue check for F).
                                      Default: OpenCV's own runKernel / run8Point, the 9x9 cv::eigen
@@ -249,6 +258,10 @@ MCV_API const char* mcvGetLastError(void);
 /* Library / device info: number of visible HIP devices (0 when none), -1 on runtime error. */
 MCV_API int mcvDeviceCount(void);
 MCV_API const char* mcvVersion(void);
+/* ABI revision of this header: 3 (round 3: MCV_FLAG_FUSED_ERROR moved from 4 to 64, bit 4 rejected,
+ * MCV_FLAG_CV_SAMPLER added, RansacConfig unchanged at 48 bytes). */
+#define MCV_ABI_VERSION 3
+MCV_API int mcvAbiVersion(void);
 
 /* CameraPose.findScaled — src/MiniCV/CameraPose.fs:39-134, the managed
  * O(N^2) scale hypothesize-and-verify, moved onto the GPU behind a new export. The F# wrapper keeps
@@ -431,6 +444,11 @@ MCV_API int mcvHostSolveAp3p(const double* mu3, const double* mv3, const double*
                              double cx_fx, double cy_fy, double* R36, double* t12);
 MCV_API void mcvHostRodrigues(const double* r, double* R, double* dR27);
 MCV_API void mcvHostRodriguesInv(const double* R, double* r);
+/* OpenCV's sample stream (MCV_FLAG_CV_SAMPLER) on the host: rows [0, rows) of m indices each for the
+ * model family (homography / fundamental: pts4 = the float4 points their checkSubset reads; essential /
+ * PnP: no check, pts4 may be NULL). Rows from the first failed getSubset on are -1. Returns the number
+ * of accepted rows, -1 on bad arguments. */
+MCV_API int64_t mcvCvSubsets(int model, int m, const float* pts4, int N, int64_t rows, int* out);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                            uint32_t* out4);
 /* Host twin of CameraPose.findScaled: the same candidates and costs as cvFindScaledPoseCosts,

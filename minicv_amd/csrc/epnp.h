@@ -30,15 +30,6 @@ namespace mcv {
 static const double kDblMin = 2.2250738585072014e-308;
 static const int kEpnpBlock = 1024;
 
-// cv::RNG: multiply-with-carry, state = (uint32)state * 4164903690 + (state >> 32).
-struct CvRng {
-    uint64_t s;
-    MCV_HD uint32_t next() {
-        s = (uint64_t)(uint32_t)s * 4164903690u + (uint32_t)(s >> 32);
-        return (uint32_t)s;
-    }
-};
-
 // The hypot template of OpenCV's core lapack.cpp (the one JacobiSVDImpl_ calls — an unqualified
 // hypot inside namespace cv): the larger magnitude times sqrt(1 + ratio^2). Only |.|, /, *, + and
 // sqrt, so host and device round it identically.

@@ -482,13 +482,14 @@ __device__ __forceinline__ void ew_stage(EWave& S, const EGroup<G>& g, const dou
 // lanes 0..19 fetch the sample. Returns the model count (0 = no model) or kStatusNoSample; lane
 // sub < count holds model sub.
 template <int G>
-__device__ __forceinline__ int ew_hypothesis(EWave& S, const EGroup<G>& g, const double* pts4, int N, uint64_t seed,
-                                             uint64_t hyp, double (&E)[9], int* idx_out) {
-    HypStream rs;
-    rs.init(seed, hyp);
+__device__ __forceinline__ int ew_hypothesis(EWave& S, const EGroup<G>& g, const double* pts4, int N,
+                                             const Sampler& smp, uint64_t hyp, double (&E)[9], int* idx_out) {
+    SubsetSrc<5> src(smp, hyp);
     int idx[5];
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        if (!draw_distinct<5>(rs, N, idx)) continue;
+        const int got = src.next(N, idx);
+        if (got < 0) break;
+        if (got == 0) continue;
         if (idx_out)
             for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
         for (int e = g.sub; e < 20; e += G) {
@@ -513,13 +514,14 @@ __device__ __forceinline__ int ew_hypothesis(EWave& S, const EGroup<G>& g, const
 // Matrix phases of hypothesis `hyp` -> EStage (lanes of the group share the writes).
 template <int G>
 __device__ __forceinline__ void ew_stage_hypothesis(EWave& S, const EGroup<G>& g, const double* pts4, int N,
-                                                    uint64_t seed, uint64_t hyp, EStage* out) {
-    HypStream rs;
-    rs.init(seed, hyp);
+                                                    const Sampler& smp, uint64_t hyp, EStage* out) {
+    SubsetSrc<5> src(smp, hyp);
     int idx[5];
     int status = kStatusNoSample;
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        if (!draw_distinct<5>(rs, N, idx)) continue;
+        const int got = src.next(N, idx);
+        if (got < 0) break;
+        if (got == 0) continue;
         for (int e = g.sub; e < 20; e += G) {
             const int c = e / 5, i = e - 5 * (e / 5);
             int id = idx[0];

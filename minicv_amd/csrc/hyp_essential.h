@@ -728,12 +728,13 @@ MCV_HD int e_solve5_ref(const double* x1, const double* y1, const double* x2, co
 // One hypothesis on packed double4 normalised correspondences {x1, y1, x2, y2}: 5 distinct
 // indices from the Philox stream (no subset check: EMEstimatorCallback has none), five-point
 // solve. Returns the number of models (0 = kStatusNoModel) or kStatusNoSample.
-MCV_HD int e_hypothesis(const double* pts4, int N, uint64_t seed, uint64_t hyp, double (*E)[9], int* idx_out) {
-    HypStream rs;
-    rs.init(seed, hyp);
+MCV_HD int e_hypothesis(const double* pts4, int N, const Sampler& smp, uint64_t hyp, double (*E)[9], int* idx_out) {
+    SubsetSrc<5> src(smp, hyp);
     int idx[5];
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        if (!draw_distinct<5>(rs, N, idx)) continue;
+        const int got = src.next(N, idx);
+        if (got < 0) break;
+        if (got == 0) continue;
         double x1[5], y1[5], x2[5], y2[5];
         for (int i = 0; i < 5; ++i) {
             const double* p = pts4 + 4 * (int64_t)idx[i];

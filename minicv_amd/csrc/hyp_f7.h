@@ -79,18 +79,19 @@ MCV_HD int f_solve7(const float* x1, const float* y1, const float* x2, const flo
 }
 
 // One 7-point hypothesis: the number of models (0 = kStatusNoModel) or kStatusNoSample.
-MCV_HD int f7_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, double (*F)[9], int* idx_out) {
-    HypStream rs;
-    rs.init(seed, hyp);
+MCV_HD int f7_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t hyp, double (*F)[9], int* idx_out) {
+    SubsetSrc<7> src(smp, hyp);
     float x1[7], y1[7], x2[7], y2[7];
     int idx[7];
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        if (!draw_distinct<7>(rs, N, idx)) continue;
+        const int got = src.next(N, idx);
+        if (got < 0) break;
+        if (got == 0) continue;
         for (int i = 0; i < 7; ++i) {
             const float* p = pts4 + 4 * (int64_t)idx[i];
             x1[i] = p[0]; y1[i] = p[1]; x2[i] = p[2]; y2[i] = p[3];
         }
-        if (have_collinear_last<7>(x1, y1) || have_collinear_last<7>(x2, y2)) continue;
+        if (!src.tabled() && (have_collinear_last<7>(x1, y1) || have_collinear_last<7>(x2, y2))) continue;
         if (idx_out) for (int i = 0; i < 7; ++i) idx_out[i] = idx[i];
         return f_solve7(x1, y1, x2, y2, F);
     }

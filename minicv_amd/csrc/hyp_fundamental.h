@@ -273,20 +273,21 @@ MCV_HD bool f_solve8(const float* x1, const float* y1, const float* x2, const fl
 
 // One hypothesis: 1 (model), kStatusNoModel, kStatusNoSample.
 template <class WS>
-MCV_HD int f_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, double* F, int* idx_out, WS& ws,
+MCV_HD int f_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t hyp, double* F, int* idx_out, WS& ws,
                         bool fast = false) {
-    HypStream rs;
-    rs.init(seed, hyp);
+    SubsetSrc<8> src(smp, hyp);
     float x1[8], y1[8], x2[8], y2[8];
     int idx[8];
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        if (!draw_distinct<8>(rs, N, idx)) continue;
+        const int got = src.next(N, idx);
+        if (got < 0) break;
+        if (got == 0) continue;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const float* p = pts4 + 4 * (int64_t)idx[i];
             x1[i] = p[0]; y1[i] = p[1]; x2[i] = p[2]; y2[i] = p[3];
         }
-        if (have_collinear_last<8>(x1, y1) || have_collinear_last<8>(x2, y2)) continue;
+        if (!src.tabled() && (have_collinear_last<8>(x1, y1) || have_collinear_last<8>(x2, y2))) continue;
         if (idx_out) for (int i = 0; i < 8; ++i) idx_out[i] = idx[i];
         return f_solve8(x1, y1, x2, y2, F, ws, fast) ? 1 : kStatusNoModel;
     }

@@ -296,14 +296,15 @@ MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const fl
 // One hypothesis: returns 1 (model written), kStatusNoModel, or kStatusNoSample.
 // pts4: N packed {x, y, x', y'}. idx_out (optional) receives the accepted sample.
 template <class WS>
-MCV_HD int h_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, double* H, HModelF* mf,
+MCV_HD int h_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t hyp, double* H, HModelF* mf,
                         int* idx_out, WS& ws, bool fast = false) {
-    HypStream rs;
-    rs.init(seed, hyp);
+    SubsetSrc<4> src(smp, hyp);
     float sx[4], sy[4], dx[4], dy[4];
     int idx[4];
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        if (!draw_distinct<4>(rs, N, idx)) continue;
+        const int got = src.next(N, idx);
+        if (got < 0) break;
+        if (got == 0) continue;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
@@ -311,7 +312,7 @@ MCV_HD int h_hypothesis(const float* pts4, int N, uint64_t seed, uint64_t hyp, d
             const float* p = pts4 + 4 * (int64_t)idx[i];
             sx[i] = p[0]; sy[i] = p[1]; dx[i] = p[2]; dy[i] = p[3];
         }
-        if (!h_check_subset(sx, sy, dx, dy)) continue;
+        if (!src.tabled() && !h_check_subset(sx, sy, dx, dy)) continue;
         if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
         if (!h_solve4(sx, sy, dx, dy, H, ws, fast)) return kStatusNoModel;
         bool ok = true;

@@ -399,13 +399,14 @@ struct PnpPoint { float X, Y, Z, u, v, pad0, pad1, pad2; };
 
 // One hypothesis: 4 distinct indices (Philox stream), undistort, AP3P + 4th-point selection.
 // Returns 1 (model), kStatusNoModel or kStatusNoSample.
-MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, uint64_t seed, uint64_t hyp, PnpPose& pose,
-                          int* idx_out) {
-    HypStream rs;
-    rs.init(seed, hyp);
+MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
+                          PnpPose& pose, int* idx_out) {
+    SubsetSrc<4> src(smp, hyp);
     int idx[4];
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        if (!draw_distinct<4>(rs, N, idx)) continue;
+        const int got = src.next(N, idx);
+        if (got < 0) break;
+        if (got == 0) continue;
         double x[4], y[4], W[4][3];
         for (int i = 0; i < 4; ++i) {
             const PnpPoint p = pts[idx[i]];
@@ -454,13 +455,14 @@ MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose) {
 
 // One EPnP hypothesis: 5 distinct indices (Philox stream) -> pnp_epnp5. EPnP always yields a
 // model (possibly non-finite, which then counts no inliers), as solvePnP(EPNP) returns true.
-MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, uint64_t seed, uint64_t hyp,
+MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
                                PnpPose& pose, int* idx_out, EpnpWs& ws) {
-    HypStream rs;
-    rs.init(seed, hyp);
+    SubsetSrc<5> src(smp, hyp);
     int idx[5];
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        if (!draw_distinct<5>(rs, N, idx)) continue;
+        const int got = src.next(N, idx);
+        if (got < 0) break;
+        if (got == 0) continue;
         PnpPoint p5[5];
         for (int i = 0; i < 5; ++i) p5[i] = pts[idx[i]];
         if (idx_out) for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
@@ -469,10 +471,10 @@ MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, u
     }
     return kStatusNoSample;
 }
-MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, uint64_t seed, uint64_t hyp,
+MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
                                PnpPose& pose, int* idx_out) {
     EpnpWs ws;
-    return pnp_hypothesis_epnp(pts, N, c, seed, hyp, pose, idx_out, ws);
+    return pnp_hypothesis_epnp(pts, N, c, smp, hyp, pose, idx_out, ws);
 }
 
 }  // namespace mcv

@@ -21,10 +21,10 @@ struct HOneOut {
     int status;
     int idx[4];
 };
-void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast);
+void launch_h_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast);
 void launch_h_mask_one(const float* d_pts4, int N, const HOneOut* d_one, float thr2, bool fused, uint8_t* d_mask,
                        int* d_count, hipStream_t s);
-void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_models,
                        double* d_h64, int* d_counts, hipStream_t s, bool fast);
 void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
                      bool fused, const float* d_bbox, hipStream_t s);
@@ -56,13 +56,13 @@ struct FOneOut {
     int status;
     int idx[8];
 };
-void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+void launch_f_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_models,
                        int* d_counts, hipStream_t s, bool fast);
-void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s, bool fast);
+void launch_f_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, FOneOut* d_out, hipStream_t s, bool fast);
 // 7-point (MCV_FLAG_SEVEN_POINT): 3 model slots per hypothesis (models[3h + s], counts[3h + s]).
-void launch_f7_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+void launch_f7_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_models,
                         int* d_counts, hipStream_t s);
-void launch_f7_one(const float* d_pts4, int N, uint64_t seed, int64_t slot, FOneOut* d_out, hipStream_t s);
+void launch_f7_one(const float* d_pts4, int N, Sampler smp, int64_t slot, FOneOut* d_out, hipStream_t s);
 void launch_f7_direct(const float* d_pts4, FOneOut* d_out, hipStream_t s);   // N == 7: run7Point, first model
 void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
                      int kind, hipStream_t s, const double* d_bb = nullptr);
@@ -100,14 +100,14 @@ static const int kEStageMinHyps = 32768;   // hypCount from which generate takes
 static const int kEStageLanes = 16;        // lanes per hypothesis of its matrix phases
 static const int kERootLanes = 4;          // lanes per hypothesis of its root finder (1: one lane)
 void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, double* d_pts4, hipStream_t s);
-void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_dense,
+void launch_e_generate(const double* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_dense,
                        int* d_denseSlot, int* d_nDense, int* d_counts, void* d_stage, hipStream_t s);
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
                      int maxModels, int* d_counts, float thr2, int kind, hipStream_t s, const float* d_pts32 = nullptr,
                      const double* d_bb = nullptr);
 void launch_e_fetch(const void* d_dense, const int* d_denseSlot, const int* d_nDense, int maxModels, int slot,
                     void* d_out, int* d_found, hipStream_t s);
-void launch_e_one(const double* d_pts4, int N, uint64_t seed, int64_t hyp, EOneOut* d_out, hipStream_t s);
+void launch_e_one(const double* d_pts4, int N, Sampler smp, int64_t hyp, EOneOut* d_out, hipStream_t s);
 void launch_e_mask(const double* d_pts4, int N, const double* E9, float thr2, int kind, uint8_t* d_mask, int* d_count,
                    hipStream_t s);
 void launch_e_cheirality(const double* d_pts4, int N, const uint8_t* d_mask, const double* P4x12, double dist,
@@ -129,13 +129,13 @@ struct Ap3pOut {
     int count;
 };
 void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_pts, hipStream_t s);
-void launch_pnp_generate(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin, int hypCount,
+void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
                          bool epnp, void* d_models, int* d_counts, hipStream_t s);
 // d_ext: 3 doubles of device scratch filled by launch_pnp_extent (the certified sweep's bound).
 void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s);
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
                        float thr2, bool fused, const double* d_ext, hipStream_t s);
-void launch_pnp_one(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hyp, bool epnp,
+void launch_pnp_one(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hyp, bool epnp,
                     PnpOneOut* d_out, hipStream_t s);
 void launch_pnp_solve5(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s);
 void launch_mask_compact(const uint8_t* d_mask, int N, int* d_idx, int* d_count, hipStream_t s);

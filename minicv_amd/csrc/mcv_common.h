@@ -93,6 +93,44 @@ struct HypStream {
 static const int kMaxAttempts = 10000;
 static const int kMaxRedraw = 1000;
 
+// cv::RNG (OpenCV core, [ext]): multiply-with-carry on a 64-bit state,
+//   next() : state = (uint64)(unsigned)state * 4164903690 + (unsigned)(state >> 32), returns (unsigned)state
+//   uniform(a, b) = a == b ? a : (int)(next() % (b - a) + a)
+// RANSACPointSetRegistrator::run seeds one per call with (uint64)-1 and getSubset draws every index
+// of every attempt from it, in order (cv_sampler.cpp generates that stream on the host).
+struct CvRng {
+    uint64_t s;
+    MCV_HD uint32_t next() {
+        s = (uint64_t)(uint32_t)s * 4164903690u + (uint32_t)(s >> 32);
+        return (uint32_t)s;
+    }
+    MCV_HD int uniform(int a, int b) { return a == b ? a : (int)(next() % (uint32_t)(b - a) + (uint32_t)a); }
+};
+
+// Where a hypothesis' minimal sample comes from:
+//   table == nullptr: the counter-based Philox stream of (seed, hypothesis) — any order, any GPU;
+//   table != nullptr: OpenCV's own sequential stream, precomputed on the host (cv_sampler.cpp,
+//     MCV_FLAG_CV_SAMPLER): row `hyp` holds the m indices getSubset accepted for that hypothesis
+//     (its duplicate rejection and checkSubset already applied), or -1 in column 0 when getSubset
+//     gave up after its 10000 attempts (the loop's `break`).
+struct Sampler {
+    uint64_t seed;
+    const int* table;
+};
+
+// Subset source of one hypothesis. next(): 1 = a subset in idx (Philox: the caller still runs
+// checkSubset and asks again on failure), 0 = draw again (Philox redraw bound), -1 = no subset.
+template <int M>
+struct SubsetSrc {
+    HypStream rs;
+    const int* row;
+    MCV_HD SubsetSrc(const Sampler& smp, uint64_t hyp) : row(smp.table ? smp.table + (int64_t)M * (int64_t)hyp : nullptr) {
+        rs.init(smp.seed, hyp);
+    }
+    MCV_HD bool tabled() const { return row != nullptr; }
+    MCV_HD int next(int N, int (&idx)[M]);
+};
+
 // Per-hypothesis status codes stored in the counts array.
 static const int kStatusNoModel = -1;   // minimal solver degenerate -> OpenCV `continue`
 static const int kStatusNoSample = -2;  // sampler exhausted attempts -> OpenCV `break`
@@ -121,6 +159,16 @@ MCV_HD bool draw_distinct(HypStream& rs, int N, int (&idx)[M]) {
         idx[i] = v;
     }
     return true;
+}
+
+template <int M>
+MCV_HD int SubsetSrc<M>::next(int N, int (&idx)[M]) {
+    if (row) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) idx[i] = row[i];
+        return idx[0] >= 0 ? 1 : -1;
+    }
+    return draw_distinct<M>(rs, N, idx) ? 1 : 0;
 }
 
 // v_rcp_f32 + one FMA Newton step: equals the IEEE 1.f / w for every |w| in [2^-126, 2^126)

@@ -139,6 +139,7 @@ extern "C" MCV_API int cvMatchAndFindModel(const DetectorResult* a, const Detect
         RansacConfig rcfg = config_or_default(rcfgp);
         if (!rcfgp && mcfg.model == MCV_MODEL_FUNDAMENTAL) rcfg.confidence = 0.99;
         if (rcfg.method != MCV_METHOD_RANSAC) fail("cvMatchAndFindModel: only RANSAC (method 8)");
+        check_flags(rcfg, "cvMatchAndFindModel");
         if (!(rcfg.confidence > 0 && rcfg.confidence < 1)) fail("cvMatchAndFindModel: confidence must be in (0,1)");
         require_device();
         Plan& P = thread_plan(mcfg.model);

@@ -3,7 +3,9 @@
 
 #include "minicv_native.h"
 #include "mcv_runtime.h"
+#include "mcv_common.h"
 #include <stdint.h>
+#include <vector>
 
 namespace mcv {
 
@@ -16,6 +18,27 @@ int model_points(int model);
 int model_points_cfg(int model, const RansacConfig& cfg);   // PnP: 5 with the EPnP kernel; F 7-point: 7
 int model_slots_cfg(int model, const RansacConfig& cfg);    // F 7-point: 3 model slots per hypothesis
 int model_slots(int model);      // model slots per hypothesis (essential: 10)
+
+// Key of the last evaluated chunk. A winner inside it takes its model from the chunk's buffers
+// instead of a re-solve; the key names everything that produced those buffers (the hypothesis
+// range, the sample source, the point buffer and N, the minimal solver) plus an evaluation
+// generation, so any other evaluate in between, or a different solver / sampler, invalidates it.
+struct LastChunk {
+    int64_t begin = -1, count = 0;
+    uint64_t seed = 0;
+    const int* table = nullptr;
+    const void* pts = nullptr;
+    int N = 0;
+    int kind = -1;            // H: 20 eigen, 21 elimination; F: 10 / 11; E: 30 / 31; PnP: 1 EPnP, 0 AP3P
+    void set(int64_t b, int64_t c, const Sampler& smp, const void* p, int n, int k) {
+        begin = b; count = c; seed = smp.seed; table = smp.table; pts = p; N = n; kind = k;
+    }
+    void clear() { *this = LastChunk(); }
+    bool covers(int64_t hyp, const Sampler& smp, const void* p, int n, int k) const {
+        return begin >= 0 && hyp >= begin && hyp < begin + count && seed == smp.seed && table == smp.table &&
+               pts == p && N == n && kind == k;
+    }
+};
 
 struct Plan {
     int model = MCV_MODEL_HOMOGRAPHY;
@@ -49,11 +72,11 @@ struct Plan {
     DevBuf<double> epw;       // PnP: EPnP solve points (world, double)
     DevBuf<double> eus;       // PnP: EPnP solve points (pixels of the undistorted observations)
     DevBuf<int> eidx;         // PnP: inlier indices of the EPnP solve
-    int eLastKind = -1;       // minimal solver of the last evaluated chunk (PnP: 1 EPnP, 0 AP3P; F: 10 eigen, 11 elimination)
-    int64_t eLastBegin = -1;  // essential / PnP / 8-point F: hypothesis range of the last evaluated chunk
-    int64_t eLastCount = 0;
-    uint64_t eLastSeed = 0;
-    const void* eLastPts = nullptr;
+    LastChunk last;           // the last evaluated chunk (finalize takes the winner's model from its buffers)
+    DevBuf<int> subsets;      // MCV_FLAG_CV_SAMPLER: OpenCV's getSubset stream, subsetM ints per hypothesis
+    int64_t subsetRows = 0;   // hypotheses [0, subsetRows) covered by `subsets`
+    int subsetM = 0;
+    Sampler sampler(const RansacConfig& cfg) const;
     PinnedBuf<int> h_counts;
     PinnedBuf<double> h_red;
     PinnedBuf<float> h_pack;
@@ -98,10 +121,19 @@ struct ProfScope {
 };
 void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst, hipStream_t s);
 double effective_threshold(const RansacConfig& cfg);
+bool cv_sampler(const RansacConfig& cfg);   // MCV_FLAG_CV_SAMPLER
+void check_flags(const RansacConfig& cfg, const char* who);   // rejects the retired bit 4
+// OpenCV's subset stream (cv_sampler.cpp): rows [0, rows) for P's model / cfg, uploaded to P.subsets.
+// h_pts4: host float4 points for the models with a checkSubset (H, F); nullptr = read from d_pts.
+void cv_table_build(int model, const RansacConfig& cfg, const float* h_pts4, int N, int64_t rows, std::vector<int>& out);
+void cv_table_upload(Plan& P, const std::vector<int>& t, int m, int64_t rows, hipStream_t s);
+void cv_table_prepare(Plan& P, const void* d_pts, const float* h_pts4, int N, const RansacConfig& cfg, int64_t rows,
+                      hipStream_t s);
 bool fused_error(const RansacConfig& cfg);
 bool h_sweep_scalar_only();
 RansacConfig config_or_default(const RansacConfig* cfg);
-int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s);
+int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s,
+                      const float* h_pts4 = nullptr);
 int finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hyp, double* model9,
              uint8_t* d_mask, hipStream_t s);
 void evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,

@@ -121,12 +121,9 @@ void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
                       int* d_counts, hipStream_t s) {
     const float thr2 = (float)(cfg.threshold * cfg.threshold);
     const bool epnp = pnp_cfg_epnp(cfg);
-    launch_pnp_generate(d_pts, N, P.pnpCam, cfg.seed, hypBegin, hypCount, epnp, P.models.p, d_counts, s);
-    P.eLastBegin = hypBegin;
-    P.eLastCount = hypCount;
-    P.eLastSeed = cfg.seed;
-    P.eLastPts = d_pts;
-    P.eLastKind = epnp ? 1 : 0;
+    const Sampler smp = P.sampler(cfg);
+    launch_pnp_generate(d_pts, N, P.pnpCam, smp, hypBegin, hypCount, epnp, P.models.p, d_counts, s);
+    P.last.set(hypBegin, hypCount, smp, d_pts, N, epnp ? 1 : 0);
     P.bb4.ensure(4);
     launch_pnp_extent(d_pts, N, P.bb4.p, s);
     ProfScope ps("pnp_verify", s);
@@ -342,11 +339,11 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
                uint8_t* d_mask, hipStream_t s) {
     PnpOneOut one;
     const bool epnp = pnp_cfg_epnp(cfg);
-    if (hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount && P.eLastSeed == cfg.seed && P.eLastPts == d_pts &&
-        P.eLastKind == (epnp ? 1 : 0)) {
+    const Sampler smp = P.sampler(cfg);
+    if (P.last.covers(hyp, smp, d_pts, N, epnp ? 1 : 0)) {
         // the winner's pose straight from the last chunk's model buffer (the same code produced it)
         // instead of a single-lane re-solve
-        const PnpPose* d_m = (const PnpPose*)P.models.p + (hyp - P.eLastBegin);
+        const PnpPose* d_m = (const PnpPose*)P.models.p + (hyp - P.last.begin);
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_m, sizeof(PnpPose), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
         PnpPose pose;
@@ -355,7 +352,7 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
         std::memcpy(one.t, pose.t, sizeof(one.t));
         one.status = 1;
     } else {
-        launch_pnp_one(d_pts, N, P.pnpCam, cfg.seed, hyp, epnp, (PnpOneOut*)P.one.p, s);
+        launch_pnp_one(d_pts, N, P.pnpCam, smp, hyp, epnp, (PnpOneOut*)P.one.p, s);
         MCV_HIP(hipGetLastError());
         one = pnp_fetch_one(P, s);
     }
@@ -421,6 +418,7 @@ static RansacConfig pnp_config(int iters, float thr, double conf, int kind) {
     c.maxIters = iters;
     c.method = MCV_METHOD_RANSAC;
     c.pnpKind = kind;
+    c.flags = MCV_FLAG_CV_SAMPLER;   // solvePnPRansac's own sample stream (the reference's API has no seed)
     return c;
 }
 
@@ -431,6 +429,7 @@ static bool pnp_ransac_export(const mcvV2d* img, const mcvV3d* world, int N, con
     if (!img || !world || !tVec || !rVec || !inlierCount) fail("cvSolvePnPRansac: null argument");
     if (N < 4) fail("cvSolvePnPRansac: need at least 4 correspondences (N=%d)", N);
     if (!(cfg.confidence > 0 && cfg.confidence < 1)) fail("cvSolvePnPRansac: confidence must be in (0,1)");
+    check_flags(cfg, "cvSolvePnPRansac");
     require_device();
     Plan& P = thread_plan(MCV_MODEL_PNP);
     hipStream_t s = P.own_stream();
@@ -651,7 +650,7 @@ extern "C" MCV_API int mcvHostPnP(const void* pts, int N, const double* cam8, ui
         PnpPose p;
         for (int k = 0; k < 9; ++k) p.R[k] = 0;
         for (int k = 0; k < 3; ++k) p.t[k] = 0;
-        const int st = pnp_hypothesis((const PnpPoint*)pts, N, c, seed, (uint64_t)hyp, p, idx4);
+        const int st = pnp_hypothesis((const PnpPoint*)pts, N, c, Sampler{seed, nullptr}, (uint64_t)hyp, p, idx4);
         for (int k = 0; k < 9; ++k) R9[k] = p.R[k];
         for (int k = 0; k < 3; ++k) t3[k] = p.t[k];
         return st;
@@ -666,7 +665,7 @@ extern "C" MCV_API int mcvHostPnPEpnp(const void* pts, int N, const double* cam8
         PnpPose p;
         for (int k = 0; k < 9; ++k) p.R[k] = 0;
         for (int k = 0; k < 3; ++k) p.t[k] = 0;
-        const int st = pnp_hypothesis_epnp((const PnpPoint*)pts, N, c, seed, (uint64_t)hyp, p, idx5);
+        const int st = pnp_hypothesis_epnp((const PnpPoint*)pts, N, c, Sampler{seed, nullptr}, (uint64_t)hyp, p, idx5);
         for (int k = 0; k < 9; ++k) R9[k] = p.R[k];
         for (int k = 0; k < 3; ++k) t3[k] = p.t[k];
         return st;
@@ -702,14 +701,15 @@ extern "C" MCV_API int mcvTestPnpHypotheses(const float* pts, int N, const doubl
         P.reserve(N, hypCount);
         for (int k = 0; k < 8; ++k) P.pnpCam[k] = cam8[k];
         MCV_HIP(hipMemcpyAsync(P.ptsd.p, pts, (size_t)N * sizeof(PnpPoint), hipMemcpyHostToDevice, s));
-        launch_pnp_generate(P.ptsd.p, N, P.pnpCam, seed, hypBegin, hypCount, pnp_kind_epnp(pnp_kind(kind)), P.models.p,
+        launch_pnp_generate(P.ptsd.p, N, P.pnpCam, Sampler{seed, nullptr}, hypBegin, hypCount,
+                            pnp_kind_epnp(pnp_kind(kind)), P.models.p,
                             P.counts.p, s);
         MCV_HIP(hipGetLastError());
         std::vector<PnpPose> m((size_t)hypCount);
         MCV_HIP(hipMemcpyAsync(m.data(), P.models.p, m.size() * sizeof(PnpPose), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipMemcpyAsync(status, P.counts.p, (size_t)hypCount * sizeof(int), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
-        P.eLastBegin = -1;
+        P.last.clear();
         for (int h = 0; h < hypCount; ++h) {
             if (status[h] == 0) status[h] = 1;
             for (int k = 0; k < 9; ++k) poses12[12 * (size_t)h + k] = status[h] == 1 ? m[h].R[k] : 0.0;
@@ -743,7 +743,7 @@ extern "C" MCV_API int mcvTestPnpSweep(const float* pts, int N, const double* ca
         MCV_HIP(hipGetLastError());
         MCV_HIP(hipMemcpyAsync(counts, P.counts.p, (size_t)nPoses * sizeof(int), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
-        P.eLastBegin = -1;
+        P.last.clear();
         return nPoses;
     });
 }

@@ -41,14 +41,14 @@ __global__ __launch_bounds__(256) void mcv_e_pack(const double2* __restrict__ a,
     out[i] = o;
 }
 
-__global__ __launch_bounds__(64) void mcv_e_generate(const double* __restrict__ pts4, int N, uint64_t seed,
+__global__ __launch_bounds__(64) void mcv_e_generate(const double* __restrict__ pts4, int N, Sampler smp,
                                                      int64_t hypBegin, int hypCount, EModel* __restrict__ dense,
                                                      int* __restrict__ denseSlot, int* __restrict__ nDense,
                                                      int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     double E[kEMaxModels][9];
-    const int n = e_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), E, nullptr);
+    const int n = e_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), E, nullptr);
     const int m = n > 0 ? n : 0;
     for (int s = 0; s < kEMaxModels; ++s)
         counts[(int64_t)i * kEMaxModels + s] = s < m ? 0 : (s == 0 && n == kStatusNoSample ? kStatusNoSample : kStatusNoModel);
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(64) void mcv_e_generate(const double* __restrict__ 
 }
 
 template <int G>
-__global__ __launch_bounds__(64) void mcv_e_generate_wave(const double* __restrict__ pts4, int N, uint64_t seed,
+__global__ __launch_bounds__(64) void mcv_e_generate_wave(const double* __restrict__ pts4, int N, Sampler smp,
                                                           int64_t hypBegin, int hypCount, EModel* __restrict__ dense,
                                                           int* __restrict__ denseSlot, int* __restrict__ nDense,
                                                           int* __restrict__ counts) {
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(64) void mcv_e_generate_wave(const double* __restri
     const int i = blockIdx.x * (64 / G) + g.base / G;
     if (i >= hypCount) return;
     double E[9];
-    const int n = ew_hypothesis(W, g, pts4, N, seed, (uint64_t)(hypBegin + i), E, nullptr);
+    const int n = ew_hypothesis(W, g, pts4, N, smp, (uint64_t)(hypBegin + i), E, nullptr);
     const int m = n > 0 ? n : 0;
     if (g.sub < kEMaxModels)
         counts[(int64_t)i * kEMaxModels + g.sub] =
@@ -91,13 +91,13 @@ __global__ __launch_bounds__(64) void mcv_e_generate_wave(const double* __restri
 
 // Split path, part 1: matrix phases of G-lane groups -> EStage per hypothesis.
 template <int G>
-__global__ __launch_bounds__(64) void mcv_e_stage(const double* __restrict__ pts4, int N, uint64_t seed,
+__global__ __launch_bounds__(64) void mcv_e_stage(const double* __restrict__ pts4, int N, Sampler smp,
                                                   int64_t hypBegin, int hypCount, EStage* __restrict__ st) {
     __shared__ EWave S[64 / G];
     const EGroup<G> g(threadIdx.x);
     const int i = blockIdx.x * (64 / G) + g.base / G;
     if (i >= hypCount) return;
-    ew_stage_hypothesis(S[g.base / G], g, pts4, N, seed, (uint64_t)(hypBegin + i), st + i);
+    ew_stage_hypothesis(S[g.base / G], g, pts4, N, smp, (uint64_t)(hypBegin + i), st + i);
 }
 
 // Split path, part 2: one lane per hypothesis — real roots of det B(z) (e_poly_real_roots, root
@@ -333,14 +333,14 @@ __global__ __launch_bounds__(256) void mcv_e_fetch(const EModel* __restrict__ de
     }
 }
 
-__global__ __launch_bounds__(64) void mcv_e_one(const double* __restrict__ pts4, int N, uint64_t seed, int64_t hyp,
+__global__ __launch_bounds__(64) void mcv_e_one(const double* __restrict__ pts4, int N, Sampler smp, int64_t hyp,
                                                 EOneOut* __restrict__ out) {
     __shared__ EWave S;
     const EGroup<64> g(threadIdx.x);
     const int lane = threadIdx.x;
     double E[9];
     int idx[5] = {-1, -1, -1, -1, -1};
-    const int n = ew_hypothesis(S, g, pts4, N, seed, (uint64_t)hyp, E, idx);
+    const int n = ew_hypothesis(S, g, pts4, N, smp, (uint64_t)hyp, E, idx);
     if (lane == 0) {
         out->status = n;
         for (int i = 0; i < 5; ++i) out->idx[i] = idx[i];
@@ -405,7 +405,7 @@ void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, do
                        (double4*)d_pts4);
 }
 
-void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_dense,
+void launch_e_generate(const double* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_dense,
                        int* d_denseSlot, int* d_nDense, int* d_counts, void* d_stage, hipStream_t s) {
     // MCV_E_GEN: lanes per hypothesis of the five-point solve (16 / 32 / 64; 1 = the one-lane
     // e_solve5 kernel), for the A/B screen only
@@ -422,13 +422,13 @@ void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBe
             return e ? atoi(e) : kEStageLanes;
         }();
         if (stageLanes == 8)
-            hipLaunchKernelGGL(mcv_e_stage<8>, dim3((hypCount + 7) / 8), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+            hipLaunchKernelGGL(mcv_e_stage<8>, dim3((hypCount + 7) / 8), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
                                hypCount, st);
         else if (stageLanes == 32)
-            hipLaunchKernelGGL(mcv_e_stage<32>, dim3((hypCount + 1) / 2), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+            hipLaunchKernelGGL(mcv_e_stage<32>, dim3((hypCount + 1) / 2), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
                                hypCount, st);
         else
-            hipLaunchKernelGGL(mcv_e_stage<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+            hipLaunchKernelGGL(mcv_e_stage<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
                                hypCount, st);
         static const int rootLanes = [] {
             const char* e = getenv("MCV_E_ROOTS");
@@ -447,19 +447,19 @@ void launch_e_generate(const double* d_pts4, int N, uint64_t seed, int64_t hypBe
     }
     switch (group) {
         case 1:
-            hipLaunchKernelGGL(mcv_e_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+            hipLaunchKernelGGL(mcv_e_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
                                hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
             break;
         case 64:
-            hipLaunchKernelGGL(mcv_e_generate_wave<64>, dim3(hypCount), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+            hipLaunchKernelGGL(mcv_e_generate_wave<64>, dim3(hypCount), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
                                hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
             break;
         case 32:
-            hipLaunchKernelGGL(mcv_e_generate_wave<32>, dim3((hypCount + 1) / 2), dim3(64), 0, s, d_pts4, N, seed,
+            hipLaunchKernelGGL(mcv_e_generate_wave<32>, dim3((hypCount + 1) / 2), dim3(64), 0, s, d_pts4, N, smp,
                                hypBegin, hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
             break;
         default:
-            hipLaunchKernelGGL(mcv_e_generate_wave<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, seed,
+            hipLaunchKernelGGL(mcv_e_generate_wave<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, smp,
                                hypBegin, hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
     }
 }
@@ -533,8 +533,8 @@ void launch_e_fetch(const void* d_dense, const int* d_denseSlot, const int* d_nD
                        d_denseSlot, d_nDense, slot, (EModel*)d_out, d_found);
 }
 
-void launch_e_one(const double* d_pts4, int N, uint64_t seed, int64_t hyp, EOneOut* d_out, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_e_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out);
+void launch_e_one(const double* d_pts4, int N, Sampler smp, int64_t hyp, EOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_e_one, dim3(1), dim3(64), 0, s, d_pts4, N, smp, hyp, d_out);
 }
 
 void launch_e_mask(const double* d_pts4, int N, const double* E9, float thr2, int kind, uint8_t* d_mask, int* d_count,

@@ -30,16 +30,14 @@ static int e_kind(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_
 void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
                       int* d_counts, hipStream_t s) {
     const float thr2 = (float)(cfg.threshold * cfg.threshold);
+    const Sampler smp = P.sampler(cfg);
     {
         ProfScope pg("e_generate", s);
         if (hypCount >= kEStageMinHyps) P.estage.ensure((size_t)hypCount * sizeof(EStage));
-        launch_e_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts,
+        launch_e_generate(d_pts, N, smp, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts,
                           hypCount >= kEStageMinHyps ? P.estage.p : nullptr, s);
     }
-    P.eLastBegin = hypBegin;
-    P.eLastCount = hypCount;
-    P.eLastSeed = cfg.seed;
-    P.eLastPts = d_pts;
+    P.last.set(hypBegin, hypCount, smp, d_pts, N, 30);
     P.bb4.ensure(4);
     P.pts.ensure((size_t)N * 4);
     launch_abs_bound4(d_pts, true, N, P.bb4.p, P.pts.p, s);   // fp32 copy + bounds for the prefilter
@@ -48,9 +46,9 @@ void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& c
                     s, P.pts.p, P.bb4.p);
 }
 
-static EOneOut e_one(Plan& P, const double* d_pts, int N, uint64_t seed, int64_t hyp, hipStream_t s) {
+static EOneOut e_one(Plan& P, const double* d_pts, int N, const Sampler& smp, int64_t hyp, hipStream_t s) {
     EOneOut* d_one = (EOneOut*)P.one.p;
-    launch_e_one(d_pts, N, seed, hyp, d_one, s);
+    launch_e_one(d_pts, N, smp, hyp, d_one, s);
     MCV_HIP(hipGetLastError());
     EOneOut one;
     MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(EOneOut), hipMemcpyDeviceToHost, s));
@@ -76,11 +74,12 @@ int e_finalize(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int
     const int64_t hyp = slot / kEModelSlots;
     const int k = (int)(slot % kEModelSlots);
     bool have = false;
-    if (hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount && P.eLastSeed == cfg.seed && P.eLastPts == d_pts) {
-        const int local = (int)((hyp - P.eLastBegin) * kEModelSlots + k);
+    const Sampler smp = P.sampler(cfg);
+    if (P.last.covers(hyp, smp, d_pts, N, 30)) {
+        const int local = (int)((hyp - P.last.begin) * kEModelSlots + k);
         int* d_found = P.ndense.p + 7;
         uint8_t* d_out = P.one.p;
-        launch_e_fetch(P.models.p, P.dslot.p, P.ndense.p, (int)(P.eLastCount * kEModelSlots), local, d_out, d_found, s);
+        launch_e_fetch(P.models.p, P.dslot.p, P.ndense.p, (int)(P.last.count * kEModelSlots), local, d_out, d_found, s);
         MCV_HIP(hipGetLastError());
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_out, 9 * sizeof(double), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipMemcpyAsync(P.h_i.p, d_found, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -91,7 +90,7 @@ int e_finalize(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int
         }
     }
     if (!have) {
-        const EOneOut one = e_one(P, d_pts, N, cfg.seed, hyp, s);
+        const EOneOut one = e_one(P, d_pts, N, smp, hyp, s);
         if (one.status <= k) fail("winning slot %lld has no model (status %d)", (long long)slot, one.status);
         for (int j = 0; j < 9; ++j) E[j] = one.E[k][j];
     }
@@ -169,6 +168,7 @@ static RansacConfig e_config(const RansacConfig* cfgp) {
     c.confidence = 0.999;
     c.maxIters = 1000;
     c.method = MCV_METHOD_RANSAC;
+    c.flags = MCV_FLAG_CV_SAMPLER;   // OpenCV's own sample stream (no seed in the reference's API)
     return c;
 }
 
@@ -180,6 +180,7 @@ static RansacConfig e_config(const RecoverPoseConfig* rc) {
 }
 
 static void e_check(const RansacConfig& cfg, const char* who) {
+    check_flags(cfg, who);
     if (cfg.method != MCV_METHOD_RANSAC) fail("%s: only RANSAC (method 8) is supported for E", who);
     if (!(cfg.confidence > 0 && cfg.confidence < 1)) fail("%s: confidence must be in (0,1)", who);
 }
@@ -325,7 +326,7 @@ extern "C" MCV_API int mcvHostEssential(const double* pts4, int N, uint64_t seed
     MCV_GUARD(kStatusNoSample - 1, {
         if (!pts4 || !E90 || N < 5) fail("mcvHostEssential: bad argument");
         double E[kEMaxModels][9];
-        const int n = e_hypothesis(pts4, N, seed, (uint64_t)hyp, E, sampleIdx);
+        const int n = e_hypothesis(pts4, N, Sampler{seed, nullptr}, (uint64_t)hyp, E, sampleIdx);
         for (int s = 0; s < kEMaxModels; ++s)
             for (int k = 0; k < 9; ++k) E90[9 * s + k] = s < n ? E[s][k] : 0.0;
         return n;

@@ -27,7 +27,7 @@ namespace mcv {
 // One lane per hypothesis; run8Point's eigen-solve working set in LDS, one column per lane.
 // FAST = MCV_FLAG_FAST_MINIMAL (no workspace).
 template <bool FAST, int L = kEigLanes>
-__global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __restrict__ pts4, int N, uint64_t seed,
+__global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __restrict__ pts4, int N, Sampler smp,
                                                      int64_t hypBegin, int hypCount, FModelD* __restrict__ models,
                                                      int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -36,11 +36,11 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __
     int st;
     if constexpr (FAST) {
         EigWsLocal unused;   // the elimination never touches it (folded away)
-        st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr, unused, true);
+        st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
         EigWsLane ws{lds + threadIdx.x * kEigWs};
-        st = f_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
+        st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
     }
     if (st == 1) {
         models[i] = m;
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __
     }
 }
 
-__global__ void mcv_f_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t hyp, FOneOut* __restrict__ out,
+__global__ void mcv_f_one(const float* __restrict__ pts4, int N, Sampler smp, int64_t hyp, FOneOut* __restrict__ out,
                           bool fast) {
     __shared__ double lds[kEigWs];
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -58,7 +58,7 @@ __global__ void mcv_f_one(const float* __restrict__ pts4, int N, uint64_t seed, 
     FOneOut o;
     for (int j = 0; j < 9; ++j) o.F[j] = 0;
     for (int j = 0; j < 8; ++j) o.idx[j] = -1;
-    o.status = f_hypothesis(pts4, N, seed, (uint64_t)hyp, o.F, o.idx, ws, fast);
+    o.status = f_hypothesis(pts4, N, smp, (uint64_t)hyp, o.F, o.idx, ws, fast);
     *out = o;
 }
 
@@ -252,13 +252,13 @@ struct OpFAtA {   // 45: upper triangle of A^T A, rows (X2X1, X2Y1, X2, Y2X1, Y2
     }
 };
 
-__global__ __launch_bounds__(64) void mcv_f7_generate(const float* __restrict__ pts4, int N, uint64_t seed,
+__global__ __launch_bounds__(64) void mcv_f7_generate(const float* __restrict__ pts4, int N, Sampler smp,
                                                       int64_t hypBegin, int hypCount, FModelD* __restrict__ models,
                                                       int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     double F[kF7Slots][9];
-    const int st = f7_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), F, nullptr);
+    const int st = f7_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), F, nullptr);
     for (int s = 0; s < kF7Slots; ++s) {
         if (st > s) {
             FModelD m;
@@ -271,13 +271,13 @@ __global__ __launch_bounds__(64) void mcv_f7_generate(const float* __restrict__ 
     }
 }
 
-__global__ void mcv_f7_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t slot,
+__global__ void mcv_f7_one(const float* __restrict__ pts4, int N, Sampler smp, int64_t slot,
                            FOneOut* __restrict__ out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     double F[kF7Slots][9];
     int idx[7] = {-1, -1, -1, -1, -1, -1, -1};
     const int s = (int)(slot % kF7Slots);
-    const int st = f7_hypothesis(pts4, N, seed, (uint64_t)(slot / kF7Slots), F, idx);
+    const int st = f7_hypothesis(pts4, N, smp, (uint64_t)(slot / kF7Slots), F, idx);
     FOneOut o;
     o.status = st > s ? 1 : (st < 0 ? st : kStatusNoModel);
     for (int j = 0; j < 9; ++j) o.F[j] = st > s ? F[s][j] : 0.0;
@@ -300,52 +300,52 @@ __global__ void mcv_f7_direct(const float* __restrict__ pts4, FOneOut* __restric
     *out = o;
 }
 
-void launch_f7_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+void launch_f7_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_models,
                         int* d_counts, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_f7_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, seed, hypBegin,
+    hipLaunchKernelGGL(mcv_f7_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
                        hypCount, (FModelD*)d_models, d_counts);
 }
 
-void launch_f7_one(const float* d_pts4, int N, uint64_t seed, int64_t slot, FOneOut* d_out, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_f7_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, slot, d_out);
+void launch_f7_one(const float* d_pts4, int N, Sampler smp, int64_t slot, FOneOut* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(mcv_f7_one, dim3(1), dim3(64), 0, s, d_pts4, N, smp, slot, d_out);
 }
 
 void launch_f7_direct(const float* d_pts4, FOneOut* d_out, hipStream_t s) {
     hipLaunchKernelGGL(mcv_f7_direct, dim3(1), dim3(64), 0, s, d_pts4, d_out);
 }
 
-void launch_f_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+void launch_f_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_models,
                        int* d_counts, hipStream_t s, bool fast) {
     if (fast)
-        hipLaunchKernelGGL(mcv_f_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, seed, hypBegin,
+        hipLaunchKernelGGL(mcv_f_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, smp, hypBegin,
                            hypCount, (FModelD*)d_models, d_counts);
     else
         switch (eig_lanes()) {
             case 64:
                 hipLaunchKernelGGL((mcv_f_generate<false, 64>), dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+                                   smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
                 break;
             case 48:
                 hipLaunchKernelGGL((mcv_f_generate<false, 48>), dim3((hypCount + 47) / 48), dim3(48), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+                                   smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
                 break;
             case 32:
                 hipLaunchKernelGGL((mcv_f_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+                                   smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
                 break;
             case 39:
                 hipLaunchKernelGGL((mcv_f_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (FModelD*)d_models, d_counts);
+                                   smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
                 break;
             default:
                 hipLaunchKernelGGL((mcv_f_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
-                                   dim3(kEigLanes), 0, s, d_pts4, N, seed, hypBegin, hypCount, (FModelD*)d_models,
+                                   dim3(kEigLanes), 0, s, d_pts4, N, smp, hypBegin, hypCount, (FModelD*)d_models,
                                    d_counts);
         }
 }
 
-void launch_f_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, FOneOut* d_out, hipStream_t s, bool fast) {
-    hipLaunchKernelGGL(mcv_f_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out, fast);
+void launch_f_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, FOneOut* d_out, hipStream_t s, bool fast) {
+    hipLaunchKernelGGL(mcv_f_one, dim3(1), dim3(64), 0, s, d_pts4, N, smp, hyp, d_out, fast);
 }
 
 template <int K, int P>

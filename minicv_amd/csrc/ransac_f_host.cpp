@@ -28,18 +28,18 @@ int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     FOneOut* d_one = (FOneOut*)P.one.p;
     const bool fast = (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0;
     FOneOut one;
-    if (!(cfg.flags & MCV_FLAG_SEVEN_POINT) && hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount &&
-        P.eLastSeed == cfg.seed && P.eLastPts == d_pts && P.eLastKind == (fast ? 11 : 10)) {
+    const Sampler smp = P.sampler(cfg);
+    if (!(cfg.flags & MCV_FLAG_SEVEN_POINT) && P.last.covers(hyp, smp, d_pts, N, fast ? 11 : 10)) {
         // the winner's model straight from the last chunk's buffer (the same code produced it) instead
         // of a single-lane re-solve (the eigen-solve's ~0.5 ms latency)
-        const FModelD* d_m = (const FModelD*)P.models.p + (hyp - P.eLastBegin);
+        const FModelD* d_m = (const FModelD*)P.models.p + (hyp - P.last.begin);
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_m, sizeof(FModelD), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
         std::memcpy(one.F, P.h_one.p, sizeof(FModelD));
         one.status = 1;
     } else {
-        if (cfg.flags & MCV_FLAG_SEVEN_POINT) launch_f7_one(d_pts, N, cfg.seed, hyp, d_one, s);   // hyp = model slot
-        else launch_f_one(d_pts, N, cfg.seed, hyp, d_one, s, fast);
+        if (cfg.flags & MCV_FLAG_SEVEN_POINT) launch_f7_one(d_pts, N, smp, hyp, d_one, s);   // hyp = model slot
+        else launch_f_one(d_pts, N, smp, hyp, d_one, s, fast);
         MCV_HIP(hipGetLastError());
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(FOneOut), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
@@ -95,7 +95,7 @@ int f_host_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, doub
     if (N < 8) fail("N < 8");
     for (int k = 0; k < 9; ++k) F9[k] = 0;
     EigWsLocal ws;
-    const int st = f_hypothesis(pts4, N, seed, (uint64_t)hyp, F9, sampleIdx, ws, fast);
+    const int st = f_hypothesis(pts4, N, Sampler{seed, nullptr}, (uint64_t)hyp, F9, sampleIdx, ws, fast);
     for (int k = 0; k < 9; ++k) Ff9[k] = (float)F9[k];
     return st;
 }
@@ -111,7 +111,7 @@ extern "C" MCV_API int mcvHostF7(const float* pts4, int N, uint64_t seed, int64_
         double F[kF7Slots][9];
         for (int s = 0; s < kF7Slots; ++s)
             for (int k = 0; k < 9; ++k) F[s][k] = 0.0;
-        const int n = f7_hypothesis(pts4, N, seed, (uint64_t)hyp, F, idx7);
+        const int n = f7_hypothesis(pts4, N, Sampler{seed, nullptr}, (uint64_t)hyp, F, idx7);
         for (int s = 0; s < kF7Slots; ++s)
             for (int k = 0; k < 9; ++k) F27[9 * s + k] = F[s][k];
         return n;

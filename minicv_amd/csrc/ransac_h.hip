@@ -30,7 +30,7 @@ namespace mcv {
 // per lane (jacobi_eig.h): 40.6 KB per 40-lane block, 4 blocks per CU. FAST = MCV_FLAG_FAST_MINIMAL
 // (no workspace).
 template <bool FAST, int L = kEigLanes>
-__global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __restrict__ pts4, int N, uint64_t seed,
+__global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __restrict__ pts4, int N, Sampler smp,
                                                      int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
                                                      double* __restrict__ h64, int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -40,11 +40,11 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
     int st;
     if constexpr (FAST) {
         EigWsLocal unused;   // the elimination never touches it (folded away)
-        st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr, unused, true);
+        st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
         EigWsLane ws{lds + threadIdx.x * kEigWs};
-        st = h_hypothesis(pts4, N, seed, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
+        st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
     }
     if (st == 1) {
         models[i] = mf;
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
 }
 
 // One hypothesis in full (finalize path): fp64 model, fp32 model, status, sample.
-__global__ void mcv_h_one(const float* __restrict__ pts4, int N, uint64_t seed, int64_t hyp, HOneOut* __restrict__ out,
+__global__ void mcv_h_one(const float* __restrict__ pts4, int N, Sampler smp, int64_t hyp, HOneOut* __restrict__ out,
                           bool fast) {
     __shared__ double lds[kEigWs];
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -68,7 +68,7 @@ __global__ void mcv_h_one(const float* __restrict__ pts4, int N, uint64_t seed, 
     HModelF mf;
     for (int j = 0; j < 9; ++j) o.H[j] = 0;
     for (int j = 0; j < 8; ++j) mf.h[j] = 0;
-    o.status = h_hypothesis(pts4, N, seed, (uint64_t)hyp, o.H, &mf, o.idx, ws, fast);
+    o.status = h_hypothesis(pts4, N, smp, (uint64_t)hyp, o.H, &mf, o.idx, ws, fast);
     for (int j = 0; j < 8; ++j) o.hf[j] = mf.h[j];
     *out = o;
 }
@@ -1012,39 +1012,39 @@ struct OpLMErr {   // 1: |r|^2 only
 // ------------------------------------------------------------------------------------------
 // Launchers (host side, called from ransac_host.cpp)
 // ------------------------------------------------------------------------------------------
-void launch_h_generate(const float* d_pts4, int N, uint64_t seed, int64_t hypBegin, int hypCount, void* d_models,
+void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_models,
                        double* d_h64, int* d_counts, hipStream_t s, bool fast) {
     if (fast)
-        hipLaunchKernelGGL(mcv_h_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, seed, hypBegin,
+        hipLaunchKernelGGL(mcv_h_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, smp, hypBegin,
                            hypCount, (HModelF*)d_models, d_h64, d_counts);
     else
         switch (eig_lanes()) {
             case 64:
                 hipLaunchKernelGGL((mcv_h_generate<false, 64>), dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
+                                   smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
             case 48:
                 hipLaunchKernelGGL((mcv_h_generate<false, 48>), dim3((hypCount + 47) / 48), dim3(48), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
+                                   smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
 
             case 32:
                 hipLaunchKernelGGL((mcv_h_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
+                                   smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
             case 39:
                 hipLaunchKernelGGL((mcv_h_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
-                                   seed, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
+                                   smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
                 break;
             default:
                 hipLaunchKernelGGL((mcv_h_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
-                                   dim3(kEigLanes), 0, s, d_pts4, N, seed, hypBegin, hypCount, (HModelF*)d_models, d_h64,
+                                   dim3(kEigLanes), 0, s, d_pts4, N, smp, hypBegin, hypCount, (HModelF*)d_models, d_h64,
                                    d_counts);
         }
 }
 
-void launch_h_one(const float* d_pts4, int N, uint64_t seed, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast) {
-    hipLaunchKernelGGL(mcv_h_one, dim3(1), dim3(64), 0, s, d_pts4, N, seed, hyp, d_out, fast);
+void launch_h_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast) {
+    hipLaunchKernelGGL(mcv_h_one, dim3(1), dim3(64), 0, s, d_pts4, N, smp, hyp, d_out, fast);
 }
 
 void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s) {

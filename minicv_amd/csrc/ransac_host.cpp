@@ -338,17 +338,14 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
             P.bb4.ensure(4);
             launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         }
+        const Sampler smp = P.sampler(cfg);
         {
             ProfScope pg("h_generate", s);
-            launch_h_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, P.h64.p, d_counts, s,
+            launch_h_generate(d_pts, N, smp, hypBegin, hypCount, P.models.p, P.h64.p, d_counts, s,
                               fast_minimal(cfg));
         }
         // the winner's models can come straight from this chunk's buffers (h_finalize)
-        P.eLastBegin = hypBegin;
-        P.eLastCount = hypCount;
-        P.eLastSeed = cfg.seed;
-        P.eLastPts = d_pts;
-        P.eLastKind = fast_minimal(cfg) ? 21 : 20;
+        P.last.set(hypBegin, hypCount, smp, d_pts, N, fast_minimal(cfg) ? 21 : 20);
         ProfScope ps("h_verify", s);
         if (!fused) {
             // default: OpenCV's op-by-op error, certified division-free packed sweep
@@ -361,8 +358,8 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         }
     } else if (f_seven(P.model, cfg)) {
         // OpenCV FM_RANSAC: 7-point samples, 3 model slots per hypothesis (slot keys like essential)
-        P.eLastBegin = -1;
-        launch_f7_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s);
+        P.last.clear();
+        launch_f7_generate(d_pts, N, P.sampler(cfg), hypBegin, hypCount, P.models.p, d_counts, s);
         P.bb4.ensure(4);
         launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         {
@@ -374,16 +371,13 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         MCV_HIP(hipGetLastError());
         return;
     } else {
+        const Sampler smp = P.sampler(cfg);
         {
             ProfScope pg("f_generate", s);
-            launch_f_generate(d_pts, N, cfg.seed, hypBegin, hypCount, P.models.p, d_counts, s, fast_minimal(cfg));
+            launch_f_generate(d_pts, N, smp, hypBegin, hypCount, P.models.p, d_counts, s, fast_minimal(cfg));
         }
         // the winner's fp64 model can come straight from this chunk's buffer (f_finalize)
-        P.eLastBegin = hypBegin;
-        P.eLastCount = hypCount;
-        P.eLastSeed = cfg.seed;
-        P.eLastPts = d_pts;
-        P.eLastKind = fast_minimal(cfg) ? 11 : 10;
+        P.last.set(hypBegin, hypCount, smp, d_pts, N, fast_minimal(cfg) ? 11 : 10);
         P.bb4.ensure(4);
         launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         ProfScope ps("f_verify", s);
@@ -407,18 +401,18 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     const float thr2 = (float)(t * t);
     // winner re-solve -> mask from the device-side record -> one read-back of both
     HOneOut* d_one = (HOneOut*)P.one.p;
-    if (hyp >= P.eLastBegin && hyp < P.eLastBegin + P.eLastCount && P.eLastSeed == cfg.seed && P.eLastPts == d_pts &&
-        P.eLastKind == (fast_minimal(cfg) ? 21 : 20)) {
+    const Sampler smp = P.sampler(cfg);
+    if (P.last.covers(hyp, smp, d_pts, N, fast_minimal(cfg) ? 21 : 20)) {
         // the winner's fp64 and fp32 models straight from the last chunk's buffers (the same code
         // produced them) instead of a single-lane eigen re-solve (~0.4 ms); a winner has status 1
-        const int64_t local = hyp - P.eLastBegin;
+        const int64_t local = hyp - P.last.begin;
         MCV_HIP(hipMemcpyAsync(d_one->H, P.h64.p + 9 * local, 9 * sizeof(double), hipMemcpyDeviceToDevice, s));
         MCV_HIP(hipMemcpyAsync(d_one->hf, P.models.p + local * sizeof(HModelF), sizeof(HModelF),
                                hipMemcpyDeviceToDevice, s));
         P.h_i.p[1] = 1;
         MCV_HIP(hipMemcpyAsync(&d_one->status, P.h_i.p + 1, sizeof(int), hipMemcpyHostToDevice, s));
     } else {
-        launch_h_one(d_pts, N, cfg.seed, hyp, d_one, s, fast_minimal(cfg));
+        launch_h_one(d_pts, N, smp, hyp, d_one, s, fast_minimal(cfg));
     }
     MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
     launch_h_mask_one(d_pts, N, d_one, thr2, fused_error(cfg), d_mask, P.count.p, s);
@@ -455,7 +449,8 @@ int finalize(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg, int64_
 // concurrently by per-shard workspaces on devices 0, 1, ... (round-robin over the visible GPUs;
 // points replicated once by peer copy), counts concatenated in order, then the same replay — the
 // answer is identical to one device. Returns the best hypothesis (slot) index or -1.
-int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s) {
+int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s,
+                      const float* h_pts4) {
     const int m = model_points_cfg(P.model, cfg);
     const int slots = model_slots_cfg(P.model, cfg);
     // plans size their slot buffers by model_slots(model): a mode with more slots per hypothesis
@@ -478,6 +473,21 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
     struct Shard { Plan* P; const void* pts; hipStream_t s; int dev; };
     std::vector<Shard> sh;
     sh.push_back({&P, d_pts, s, home});
+    // OpenCV's sample stream: the whole budget's subsets up front (niters only shrinks), uploaded to
+    // every shard's workspace
+    std::vector<int> table;
+    const int64_t tableRows = std::max(cfg.maxIters, 1);
+    if (cv_sampler(cfg)) {
+        std::vector<float> host;
+        if (!h_pts4 && P.model != MCV_MODEL_ESSENTIAL && P.model != MCV_MODEL_PNP) {
+            host.resize((size_t)N * 4);
+            MCV_HIP(hipMemcpyAsync(host.data(), d_pts, (size_t)N * 16, hipMemcpyDeviceToHost, s));
+            MCV_HIP(hipStreamSynchronize(s));
+            h_pts4 = host.data();
+        }
+        cv_table_build(P.model, cfg, h_pts4, N, tableRows, table);
+        cv_table_upload(P, table, m, tableRows, s);
+    }
     if (shards > 1) {
         size_t bytes = 0;
         MCV_HIP(hipStreamSynchronize(s));
@@ -490,6 +500,7 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
             void* dst = plan_points(Pk, N, &bytes);
             hipStream_t sk = Pk.own_stream();
             MCV_HIP(hipMemcpyPeerAsync(dst, dev, d_pts, home, bytes, sk));
+            if (cv_sampler(cfg)) cv_table_upload(Pk, table, m, tableRows, sk);
             sh.push_back({&Pk, dst, sk, dev});
         }
         MCV_HIP(hipSetDevice(home));
@@ -543,6 +554,7 @@ RansacConfig config_or_default(const RansacConfig* cfg) {
     c.confidence = 0.995;
     c.maxIters = 2000;
     c.method = MCV_METHOD_RANSAC;
+    c.flags = MCV_FLAG_CV_SAMPLER;   // no seed given: OpenCV's own sample stream
     return c;
 }
 
@@ -558,6 +570,7 @@ extern "C" MCV_API int cvFindHomography(const mcvV2d* src, const mcvV2d* dst, co
         if (mask) std::memset(mask, 0, (size_t)N);
         if (N < 4) fail("cvFindHomography: need at least 4 correspondences (N=%d)", N);
         const RansacConfig cfg = config_or_default(cfgp);
+        check_flags(cfg, "cvFindHomography");
         if (cfg.method != MCV_METHOD_RANSAC && cfg.method != MCV_METHOD_LSQ)
             fail("cvFindHomography: unsupported method %d", cfg.method);
         if (cfg.method == MCV_METHOD_RANSAC && !(cfg.confidence > 0 && cfg.confidence < 1))
@@ -575,7 +588,7 @@ extern "C" MCV_API int cvFindHomography(const mcvV2d* src, const mcvV2d* dst, co
             if (mask) std::memset(mask, 1, (size_t)N);
             count = N;
         } else {
-            const int64_t best = ransac_search(P, P.pts.p, N, cfg, s);
+            const int64_t best = ransac_search(P, P.pts.p, N, cfg, s, P.h_pack.p);
             if (best < 0) fail("cvFindHomography: RANSAC found no model with >= 4 inliers");
             count = h_finalize(P, P.pts.p, N, cfg, best, Hm, P.mask.p, s);
             if (mask) {
@@ -631,6 +644,12 @@ extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const void* d_pts4
                  (long long)scale, (long long)P->maxHyps);
         if (hypBegin < 0 || (hypBegin + hypCount) * model_slots_cfg(P->model, *cfg) > 0xFFFFFFFFll)
             fail("mcvRansacEvaluate: hypothesis (slot) index beyond 2^32");
+        check_flags(*cfg, "mcvRansacEvaluate");
+        if (cv_sampler(*cfg) && (hypBegin == 0 || P->subsetRows < hypBegin + hypCount ||
+                                 P->subsetM != model_points_cfg(P->model, *cfg)))
+            // a search starts at hypothesis 0: the stream is rebuilt from the current points
+            cv_table_prepare(*P, d_pts4, nullptr, N, *cfg, std::max<int64_t>(hypBegin + hypCount, cfg->maxIters),
+                             (hipStream_t)stream);
         evaluate_chunk(*P, d_pts4, N, *cfg, hypBegin, (int)hypCount, d_counts ? d_counts : P->counts.p, d_key,
                        (hipStream_t)stream);
         return 1;
@@ -643,7 +662,12 @@ extern "C" MCV_API int mcvRansacFinalize(mcvRansacPlan* plan, const void* d_pts4
         Plan* P = reinterpret_cast<Plan*>(plan);
         if (!P || !d_pts4 || !cfg || !model9 || !d_mask) fail("mcvRansacFinalize: null argument");
         if (hypIndex < 0) fail("mcvRansacFinalize: no winning hypothesis");
+        check_flags(*cfg, "mcvRansacFinalize");
         P->reserve(N, 1);
+        const int64_t hyp = hypIndex / model_slots_cfg(P->model, *cfg);
+        if (cv_sampler(*cfg) && (P->subsetRows <= hyp || P->subsetM != model_points_cfg(P->model, *cfg)))
+            cv_table_prepare(*P, d_pts4, nullptr, N, *cfg, std::max<int64_t>(hyp + 1, cfg->maxIters),
+                             (hipStream_t)stream);
         return finalize(*P, d_pts4, N, *cfg, hypIndex, model9, d_mask, (hipStream_t)stream);
     })
 }
@@ -660,7 +684,8 @@ extern "C" MCV_API int mcvHostHypothesis(int model, const float* pts4, int N, ui
             for (int k = 0; k < 9; ++k) model9[k] = 0;
             for (int k = 0; k < 8; ++k) mf.h[k] = 0;
             EigWsLocal ws;
-            const int st = h_hypothesis(pts4, N, seed, (uint64_t)hyp, model9, &mf, sampleIdx, ws, fast);
+            const int st = h_hypothesis(pts4, N, Sampler{seed, nullptr}, (uint64_t)hyp, model9, &mf, sampleIdx, ws,
+                                        fast);
             for (int k = 0; k < 8; ++k) modelf9[k] = mf.h[k];
             modelf9[8] = 1.f;
             return st;
@@ -684,6 +709,7 @@ extern "C" MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, co
         if (mask) std::memset(mask, 0, (size_t)N);
         RansacConfig cfg = config_or_default(cfgp);
         if (!cfgp) cfg.confidence = 0.99;
+        check_flags(cfg, "cvFindFundamentalMat");
         const bool seven = (cfg.flags & MCV_FLAG_SEVEN_POINT) != 0;
         if (seven && cfg.method == MCV_METHOD_RANSAC && N != 7 && N < 15)
             fail("cvFindFundamentalMat: 7-point FM_RANSAC needs N >= 15 (OpenCV uses LMeDS below that; N=%d)", N);
@@ -717,7 +743,7 @@ extern "C" MCV_API int cvFindFundamentalMat(const mcvV2d* a, const mcvV2d* b, co
             if (count <= 0) fail("cvFindFundamentalMat: degenerate point set");
             if (mask) std::memset(mask, 1, (size_t)N);
         } else {
-            const int64_t best = ransac_search(P, P.pts.p, N, cfg, s);
+            const int64_t best = ransac_search(P, P.pts.p, N, cfg, s, P.h_pack.p);
             if (best < 0) fail("cvFindFundamentalMat: RANSAC found no model with >= %d inliers", seven ? 7 : 8);
             count = f_finalize(P, P.pts.p, N, cfg, best, Fm, P.mask.p, s);
             if (mask) {

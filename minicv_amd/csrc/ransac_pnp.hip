@@ -44,7 +44,7 @@ static constexpr int kEpnpWsStride = 145;   // doubles per lane (12 x 12 + 1: ba
 
 template <bool EPNP>
 __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
-                                                       uint64_t seed, int64_t hypBegin, int hypCount,
+                                                       Sampler smp, int64_t hypBegin, int hypCount,
                                                        PnpPose* __restrict__ models, int* __restrict__ counts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
@@ -53,9 +53,9 @@ __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restric
     if constexpr (EPNP) {
         __shared__ double ws[64 * kEpnpWsStride];
         EpnpWs& A = *reinterpret_cast<EpnpWs*>(ws + (size_t)threadIdx.x * kEpnpWsStride);
-        st = pnp_hypothesis_epnp(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr, A);
+        st = pnp_hypothesis_epnp(pts, N, cam, smp, (uint64_t)(hypBegin + i), p, nullptr, A);
     } else {
-        st = pnp_hypothesis(pts, N, cam, seed, (uint64_t)(hypBegin + i), p, nullptr);
+        st = pnp_hypothesis(pts, N, cam, smp, (uint64_t)(hypBegin + i), p, nullptr);
     }
     if (st == 1) {
         models[i] = p;
@@ -288,15 +288,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
-__global__ void mcv_pnp_one(const PnpPoint* __restrict__ pts, int N, PnpCamera cam, uint64_t seed, int64_t hyp,
+__global__ void mcv_pnp_one(const PnpPoint* __restrict__ pts, int N, PnpCamera cam, Sampler smp, int64_t hyp,
                             bool epnp, PnpOneOut* __restrict__ out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     PnpPose p;
     for (int k = 0; k < 9; ++k) p.R[k] = 0;
     for (int k = 0; k < 3; ++k) p.t[k] = 0;
     int idx[5] = {-1, -1, -1, -1, -1};
-    out->status = epnp ? pnp_hypothesis_epnp(pts, N, cam, seed, (uint64_t)hyp, p, idx)
-                       : pnp_hypothesis(pts, N, cam, seed, (uint64_t)hyp, p, idx);
+    out->status = epnp ? pnp_hypothesis_epnp(pts, N, cam, smp, (uint64_t)hyp, p, idx)
+                       : pnp_hypothesis(pts, N, cam, smp, (uint64_t)hyp, p, idx);
     for (int k = 0; k < 9; ++k) out->R[k] = p.R[k];
     for (int k = 0; k < 3; ++k) out->t[k] = p.t[k];
     for (int k = 0; k < 5; ++k) out->idx[k] = idx[k];
@@ -617,14 +617,14 @@ void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_
     hipLaunchKernelGGL(mcv_pnp_pack, dim3((N + 255) / 256), dim3(256), 0, s, d_img, d_world, N, (PnpPoint*)d_pts);
 }
 
-void launch_pnp_generate(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin, int hypCount,
+void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
                          bool epnp, void* d_models, int* d_counts, hipStream_t s) {
     if (epnp)
         hipLaunchKernelGGL(mcv_pnp_generate<true>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
-                           N, to_cam(cam8), seed, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
+                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
     else
         hipLaunchKernelGGL(mcv_pnp_generate<false>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
-                           N, to_cam(cam8), seed, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
+                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
 }
 
 // Grid of a pose-wave x point-chunk sweep: waves x chunks >= ~8 waves per SIMD, chunks >= 2048
@@ -723,9 +723,9 @@ void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void*
     }
 }
 
-void launch_pnp_one(const void* d_pts, int N, const double* cam8, uint64_t seed, int64_t hyp, bool epnp,
+void launch_pnp_one(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hyp, bool epnp,
                     PnpOneOut* d_out, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_pnp_one, dim3(1), dim3(64), 0, s, (const PnpPoint*)d_pts, N, to_cam(cam8), seed, hyp, epnp,
+    hipLaunchKernelGGL(mcv_pnp_one, dim3(1), dim3(64), 0, s, (const PnpPoint*)d_pts, N, to_cam(cam8), smp, hyp, epnp,
                        d_out);
 }
 

@@ -63,7 +63,8 @@ extern "C" MCV_API int mcvProfileRead(const char* name, double* total_ms) {
 
 extern "C" MCV_API const char* mcvGetLastError(void) { return g_last_error.c_str(); }
 
-extern "C" MCV_API const char* mcvVersion(void) { return "minicv-mi355x 0.1.0 (gfx950)"; }
+extern "C" MCV_API const char* mcvVersion(void) { return "minicv-mi355x 0.3.0 (gfx950)"; }
+extern "C" MCV_API int mcvAbiVersion(void) { return MCV_ABI_VERSION; }
 
 extern "C" MCV_API int mcvDeviceCount(void) {
     int n = 0;

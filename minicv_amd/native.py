@@ -70,7 +70,8 @@ METHOD_LSQ = 0
 METHOD_RANSAC = 8
 FLAG_FIXED_ITERS = 1
 FLAG_NO_REFINE = 2
-FLAG_FUSED_ERROR = 4
+FLAG_FUSED_ERROR = 64   # bit 4 is retired (rejected by the library)
+FLAG_CV_SAMPLER = 32    # OpenCV's own sample stream (cv::RNG(-1) + getSubset)
 FLAG_SEVEN_POINT = 8
 FLAG_FAST_MINIMAL = 16
 FERR_SAMPSON = 0
@@ -118,6 +119,8 @@ SIGNATURES = {
     "mcvGetLastError": (C.c_char_p, []),
     "mcvDeviceCount": (_I, []),
     "mcvVersion": (C.c_char_p, []),
+    "mcvAbiVersion": (_I, []),
+    "mcvCvSubsets": (_I64, [_I, _I, _P, _I, _I64, _P]),
     # device-level API
     "mcvRansacPlanCreate": (_P, [_I, _I, _I64]),
     "mcvRansacPlanDestroy": (None, [_P]),

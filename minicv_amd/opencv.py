@@ -30,11 +30,12 @@ class RansacParams:
     fused_error: bool = False   # opt-in FMA-contracted error (default: OpenCV op-by-op order)
     seven_point: bool = False   # fundamental: OpenCV FM_RANSAC's 7-point minimal sets (<= 3 models each)
     fast_minimal: bool = False  # opt-in: H / 8-point F minimal solve by elimination (default: cv::eigen)
+    cv_sampler: bool = False    # OpenCV's own sample stream (cv::RNG((uint64)-1) + getSubset); seed unused
 
     def to_c(self) -> N.RansacConfig:
         flags = (N.FLAG_FIXED_ITERS if self.fixed_iters else 0) | (0 if self.refine else N.FLAG_NO_REFINE) | \
             (N.FLAG_FUSED_ERROR if self.fused_error else 0) | (N.FLAG_SEVEN_POINT if self.seven_point else 0) | \
-            (N.FLAG_FAST_MINIMAL if self.fast_minimal else 0)
+            (N.FLAG_FAST_MINIMAL if self.fast_minimal else 0) | (N.FLAG_CV_SAMPLER if self.cv_sampler else 0)
         return N.RansacConfig(self.threshold, self.confidence, int(self.max_iters), int(self.method),
                               int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(self.device_count), flags,
                               int(self.error_kind), 0)

@@ -587,6 +587,7 @@ int orc_find_essential(const double* a, const double* b, int N, double focal, do
     }
     int64_t niters = maxIters > 1 ? maxIters : 1;
     int* cnt = (int*)malloc(sizeof(int) * EMAX * (size_t)niters);
+    int* cvt = orc_cv_begin(flags, 0, NULL, N, 5, niters);
     orc_e_counts(pts, N, seed, 0, niters, thr2, kind, cnt, nthreads);
     int bc = 0;
     int64_t best = orc_ransac_replay_slots(cnt, niters, EMAX, N, 5, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0, &bc);
@@ -600,6 +601,7 @@ int orc_find_essential(const double* a, const double* b, int N, double focal, do
             if (bestSlotOut) *bestSlotOut = best;
         }
     }
+    orc_cv_end(cvt);
     free(pts);
     return result;
 }

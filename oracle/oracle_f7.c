@@ -153,6 +153,7 @@ int orc_find_fundamental7(const double* a, const double* b, int N, double thr, d
         const int kind = (errorKind == 1 ? 2 : 0) + ((flags & ORC_FLAG_FUSED_ERROR) ? 0 : 1);
         int64_t niters = maxIters > 1 ? maxIters : 1;
         int* cnts = (int*)malloc(sizeof(int) * F7_SLOTS * (size_t)niters);
+        int* cvt = orc_cv_begin(flags, 2, pts, N, 7, niters);
         orc_f7_counts(pts, N, seed, 0, niters, thr2, kind, cnts, nthreads);
         int bc = 0;
         int64_t best = orc_ransac_replay_slots(cnts, niters, F7_SLOTS, N, 7, conf, maxIters,
@@ -165,6 +166,7 @@ int orc_find_fundamental7(const double* a, const double* b, int N, double thr, d
             count = orc_f_count(pts, N, F, thr2, kind, mask);
             if (bestSlotOut) *bestSlotOut = best;
         }
+        orc_cv_end(cvt);
     }
     free(pts);
     return count;

@@ -10,7 +10,8 @@
 
 #define ORC_FLAG_FIXED_ITERS 1
 #define ORC_FLAG_NO_REFINE 2
-#define ORC_FLAG_FUSED_ERROR 4
+#define ORC_FLAG_FUSED_ERROR 64   /* MCV_FLAG_FUSED_ERROR (bit 4 is retired) */
+#define ORC_FLAG_CV_SAMPLER 32    /* MCV_FLAG_CV_SAMPLER */
 
 /* Per-hypothesis word stream: word s = philox({s/4, hyp_lo, hyp_hi, "MCV1"}, {seed_lo, seed_hi})[s%4] */
 typedef struct { uint64_t seed, hyp; uint64_t pos; uint32_t buf[4]; } Stream;
@@ -18,6 +19,9 @@ typedef struct { uint64_t seed, hyp; uint64_t pos; uint32_t buf[4]; } Stream;
 uint32_t stream_next(Stream* st);
 int stream_uniform(Stream* st, int n);
 int draw_distinct(Stream* st, int N, int m, int* idx);
+int64_t orc_cv_subsets(int check, const float* pts4, int N, int m, int64_t rows, int* out);
+int* orc_cv_begin(int flags, int check, const float* pts4, int N, int m, int64_t rows);
+void orc_cv_end(int* t);
 void jacobi3_orc(double* A, double* V);
 float f_err_orc(int kind, const double* F, double x1, double y1, double x2, double y2);
 int orc_update_num_iters(double p, double ep, int modelPoints, int maxIters);

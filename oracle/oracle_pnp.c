@@ -572,6 +572,7 @@ int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const 
     }
     int64_t niters = maxIters > 1 ? maxIters : 1;
     int* cnt = (int*)malloc(sizeof(int) * (size_t)niters);
+    int* cvt = orc_cv_begin(flags, 0, NULL, N, ep ? 5 : 4, niters);
     orc_pnp_counts_k(pts, N, cam8, seed, 0, niters, thr2, fused, kind, cnt, nthreads);
     int bc = 0;
     int64_t best = orc_ransac_replay(cnt, niters, N, ep ? 5 : 4, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0,
@@ -580,6 +581,7 @@ int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const 
     int st = best < 0 ? 0
              : ep     ? orc_pnp_hypothesis_epnp(pts, N, cam8, seed, best, R, t, NULL)
                       : orc_pnp_hypothesis(pts, N, cam8, seed, best, R, t, NULL);
+    orc_cv_end(cvt);
     if (st == 1) {
         uint8_t* m = (uint8_t*)malloc((size_t)N);
         result = orc_pnp_count(pts, N, cam8, R, t, thr2, fused, m);

@@ -16,6 +16,9 @@ _P, _I, _I64, _U64, _D, _F = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_dou
 _SIGS = {
     "orc_philox": (None, [_P, _P, _P]),
     "orc_set_fast_minimal": (None, [_I]),
+    "orc_cv_subsets": (_I64, [_I, _P, _I, _I, _I64, _P]),
+    "orc_cv_begin": (_P, [_I, _I, _P, _I, _I, _I64]),
+    "orc_cv_end": (None, [_P]),
     "orc_h_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P, _P]),
     "orc_h_count": (_I, [_P, _I, _P, _F, _P, _I]),
     "orc_h_counts": (None, [_P, _I, _U64, _I64, _I64, _F, _I, _P, _I]),
@@ -72,7 +75,8 @@ _lib = None
 def load() -> C.CDLL:
     global _lib
     if _lib is None:
-        srcs = [ORACLE_DIR / n for n in ("oracle.c", "oracle_e.c", "oracle_pnp.c", "oracle_scaled.c", "oracle_int.h")]
+        srcs = [ORACLE_DIR / n for n in ("oracle.c", "oracle_e.c", "oracle_pnp.c", "oracle_epnp.c", "oracle_f7.c",
+                                          "oracle_scaled.c", "oracle_int.h")]
         if not ORACLE_SO.exists() or ORACLE_SO.stat().st_mtime < max(p.stat().st_mtime for p in srcs):
             subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
         L = C.CDLL(str(ORACLE_SO))
@@ -95,6 +99,32 @@ class fast_minimal:
 
     def __exit__(self, *exc):
         load().orc_set_fast_minimal(0)
+
+
+def cv_subsets(check: int, pts4, n: int, m: int, rows: int):
+    """OpenCV's getSubset stream (check 0 none, 1 homography, 2 fundamental) -> (accepted rows, int32[rows, m])."""
+    out = np.zeros((max(rows, 1), m), dtype=np.int32)
+    p = 0 if pts4 is None else ptr(np.ascontiguousarray(pts4, dtype=np.float32))
+    k = load().orc_cv_subsets(check, p, n, m, rows, ptr(out))
+    return int(k), out[:rows]
+
+
+class cv_stream:
+    """Context: the oracle's hypothesis functions take OpenCV's sample stream (check 0 / 1 / 2 as in
+    cv_subsets) instead of Philox, for `rows` hypotheses."""
+
+    def __init__(self, check: int, pts4, n: int, m: int, rows: int):
+        self.args = (check, pts4, n, m, rows)
+        self.h = None
+
+    def __enter__(self):
+        check, pts4, n, m, rows = self.args
+        self.keep = None if pts4 is None else np.ascontiguousarray(pts4, dtype=np.float32)
+        self.h = load().orc_cv_begin(32, check, 0 if self.keep is None else ptr(self.keep), n, m, rows)
+        return self
+
+    def __exit__(self, *exc):
+        load().orc_cv_end(self.h)
 
 
 def ptr(a: np.ndarray) -> int:

@@ -84,7 +84,7 @@ int main() {
             std::memset(&m1, 0, sizeof(m1));
             int i1[4] = {-1, -1, -1, -1}, i2[4] = {-1, -1, -1, -1};
             mcv::EigWsLocal ws;
-            const int s1 = mcv::h_hypothesis(pts.data(), N, 7, (uint64_t)h, H1, &m1, i1, ws);
+            const int s1 = mcv::h_hypothesis(pts.data(), N, mcv::Sampler{7, nullptr}, (uint64_t)h, H1, &m1, i1, ws);
             const int s2 = orc_h_hypothesis(pts.data(), N, 7, h, H2, hf2, i2);
             expect(s1 == s2, "h status", s1, s2);
             if (s1 == 1 && s2 == 1) {
@@ -94,7 +94,7 @@ int main() {
             if (N >= 8) {
                 double F1[9] = {0}, F2[9] = {0};
                 int j1[8], j2[8];
-                const int t1 = mcv::f_hypothesis(pts.data(), N, 9, (uint64_t)h, F1, j1, ws);
+                const int t1 = mcv::f_hypothesis(pts.data(), N, mcv::Sampler{9, nullptr}, (uint64_t)h, F1, j1, ws);
                 const int t2 = orc_f_hypothesis(pts.data(), N, 9, h, F2, j2);
                 expect(t1 == t2, "f status", t1, t2);
                 if (t1 == 1 && t2 == 1) expect(same_bits(F1, F2, 9), "f model", h, N);
@@ -119,7 +119,7 @@ int main() {
             std::memset(E1, 0, sizeof(E1));
             std::memset(E2, 0, sizeof(E2));
             int i1[5], i2[5];
-            const int n1 = mcv::e_hypothesis(pts.data(), N, 11, (uint64_t)h, E1, i1);
+            const int n1 = mcv::e_hypothesis(pts.data(), N, mcv::Sampler{11, nullptr}, (uint64_t)h, E1, i1);
             const int n2 = orc_e_hypothesis(pts.data(), N, 11, h, E2, i2);
             expect(n1 == n2, "e count", n1, n2);
             if (n1 > 0 && n1 == n2) expect(same_bits(&E1[0][0], E2, 9 * n1), "e models", h, N);
@@ -156,7 +156,7 @@ int main() {
             std::memset(&p1, 0, sizeof(p1));
             double R2[9] = {0}, t2[3] = {0};
             int i1[4], i2[4];
-            const int s1 = mcv::pnp_hypothesis(pts.data(), N, cam, 5, (uint64_t)h, p1, i1);
+            const int s1 = mcv::pnp_hypothesis(pts.data(), N, cam, mcv::Sampler{5, nullptr}, (uint64_t)h, p1, i1);
             const int s2 = orc_pnp_hypothesis(reinterpret_cast<const float*>(pts.data()), N, cam8, 5, h, R2, t2, i2);
             expect(s1 == s2, "pnp status", s1, s2);
             if (s1 == 1 && s2 == 1) expect(same_bits(p1.R, R2, 9) && same_bits(p1.t, t2, 3), "pnp pose", h, N);
@@ -168,7 +168,7 @@ int main() {
             std::memset(&e1, 0, sizeof(e1));
             double R3[9] = {0}, t3[3] = {0};
             int j1[5], j2[5];
-            const int u1 = mcv::pnp_hypothesis_epnp(q.data(), N, cam, 6, (uint64_t)h, e1, j1);
+            const int u1 = mcv::pnp_hypothesis_epnp(q.data(), N, cam, mcv::Sampler{6, nullptr}, (uint64_t)h, e1, j1);
             const int u2 = orc_pnp_hypothesis_epnp(reinterpret_cast<const float*>(q.data()), N, cam8, 6, h, R3, t3, j2);
             expect(u1 == u2, "epnp status", u1, u2);
             if (u1 == 1 && u2 == 1) expect(same_bits(e1.R, R3, 9) && same_bits(e1.t, t3, 3), "epnp pose", h, N);

@@ -1,0 +1,160 @@
+"""GPU parity with OpenCV's own sample stream (MCV_FLAG_CV_SAMPLER): the kernels read getSubset's
+subsets (cv::RNG((uint64)-1), duplicate rejection, checkSubset; generated on the host) and every
+per-hypothesis count, mask and model must equal the oracle consuming its own, independently generated
+stream (oracle/oracle.c orc_cv_subsets; the two streams are pinned to each other and to a pure-Python
+cv::RNG in tests/test_cv_sampler.py). cvRecoverPose(s) and cvSolvePnPRansac use this stream by
+default — the reference's signatures carry no seed (MiniCVNative.cpp:93-139,165-215)."""
+import numpy as np
+import pytest
+
+from minicv_amd import native as N
+from minicv_amd import opencv, synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+CV = N.FLAG_CV_SAMPLER
+
+
+@pytest.fixture(scope="module")
+def torch_dev(gpu):
+    import torch
+    return torch, torch.device("cuda:0")
+
+
+def _device_counts(torch_dev, model, pts, n, cfg, begin, count, slots=1):
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    plan = D.RansacPlan(model, n, count * slots)
+    key = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(count * slots, dtype=torch.int32, device=dev)
+    plan.evaluate(pts, n, cfg, begin, count, key, counts)
+    torch.cuda.synchronize()
+    out = counts.cpu().numpy()
+    plan.close()
+    return out
+
+
+@pytest.mark.parametrize("n,outl,seed,count", [(200, 0.5, 1, 2000), (3000, 0.6, 2, 4096), (20000, 0.5, 3, 1000)])
+def test_homography_counts_on_cv_stream(torch_dev, oracle, n, outl, seed, count):
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    src, dst, _ = S.homography_problem(n, seed, outlier_frac=outl)
+    thr = 5e-3
+    cfg = opencv.RansacParams(threshold=thr, seed=12345, cv_sampler=True).to_c()
+    got = _device_counts(torch_dev, N.MODEL_HOMOGRAPHY, D.pack_points_tensor(src, dst, dev), n, cfg, 0, count)
+    p4 = oracle.pack4(src, dst)
+    with oracle.cv_stream(1, p4, n, 4, count):
+        ref = oracle.h_counts(p4, 0, 0, count, float(np.float32(thr * thr)), fused=False)
+    np.testing.assert_array_equal(got, ref)
+    # a later chunk of the same search reads the same rows
+    got2 = _device_counts(torch_dev, N.MODEL_HOMOGRAPHY, D.pack_points_tensor(src, dst, dev), n, cfg, 0, count // 2)
+    np.testing.assert_array_equal(got2, ref[:count // 2])
+
+
+@pytest.mark.parametrize("seven", [False, True])
+def test_fundamental_counts_on_cv_stream(torch_dev, oracle, seven):
+    torch, dev = torch_dev
+    from minicv_amd import device as D
+    a, b, *_ = S.fundamental_problem(3000, seed=5, outlier_frac=0.5)
+    thr, count = 5e-3, 1024
+    cfg = opencv.RansacParams(threshold=thr, seed=7, cv_sampler=True, seven_point=seven,
+                              error_kind=N.FERR_EPIPOLAR if seven else N.FERR_SAMPSON).to_c()
+    slots = 3 if seven else 1
+    got = _device_counts(torch_dev, N.MODEL_FUNDAMENTAL, D.pack_points_tensor(a, b, dev), 3000, cfg, 0, count, slots)
+    p4 = oracle.pack4(a, b)
+    with oracle.cv_stream(2, p4, 3000, 7 if seven else 8, count):
+        if seven:
+            ref = oracle.f7_counts(p4, 0, 0, count, float(np.float32(thr * thr)), kind=3)
+        else:
+            ref = oracle.f_counts(p4, 0, 0, count, float(np.float32(thr * thr)), kind=1)
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("n,outl,seed,thr", [(500, 0.5, 1, 1.0), (5000, 0.5, 2, 1.0), (20000, 0.6, 3, 2.0)])
+def test_find_homography_cv_stream_vs_oracle(gpu, oracle, n, outl, seed, thr):
+    src, dst, _ = S.homography_problem(n, seed, outlier_frac=outl)
+    p = opencv.RansacParams(threshold=5e-3, confidence=0.995, max_iters=2000, seed=99, cv_sampler=True)
+    cnt, H, mask = opencv.findHomography(src, dst, p)
+    cnt_o, H_o, mask_o, _ = oracle.find_homography(src, dst, thr=5e-3, conf=0.995, max_iters=2000, flags=CV)
+    assert cnt == cnt_o
+    np.testing.assert_array_equal(mask, mask_o.astype(bool))
+    assert np.linalg.norm(H - H_o) / np.linalg.norm(H_o) < 1e-6
+
+
+def test_find_homography_null_config_is_opencv_default(native, gpu, oracle):
+    """cfg == NULL: cv::findHomography's defaults (thr 3, conf 0.995, 2000 iterations) and its own stream."""
+    src, dst, _ = S.homography_problem(3000, 4, outlier_frac=0.5)
+    src, dst = src * 300, dst * 300
+    a = np.ascontiguousarray(src, dtype=np.float64)
+    b = np.ascontiguousarray(dst, dtype=np.float64)
+    H = N.M33d()
+    ms = np.zeros(3000, dtype=np.uint8)
+    cnt = N.lib().cvFindHomography(a.ctypes.data, b.ctypes.data, 3000, None, N.C.addressof(H), ms.ctypes.data)
+    cnt_o, H_o, mask_o, _ = oracle.find_homography(src, dst, thr=3.0, conf=0.995, max_iters=2000, flags=CV)
+    assert cnt == cnt_o > 0
+    np.testing.assert_array_equal(ms, mask_o)
+
+
+@pytest.mark.parametrize("seven", [False, True])
+def test_find_fundamental_cv_stream_vs_oracle(gpu, oracle, seven):
+    a, b, *_ = S.fundamental_problem(5000, seed=8, outlier_frac=0.5)
+    p = opencv.RansacParams(threshold=5e-3, confidence=0.99, max_iters=1000, cv_sampler=True, seven_point=seven,
+                            error_kind=N.FERR_EPIPOLAR if seven else N.FERR_SAMPSON)
+    cnt, F, mask = opencv.findFundamentalMat(a, b, p)
+    if seven:
+        cnt_o, F_o, mask_o, _ = oracle.find_fundamental7(a, b, thr=5e-3, conf=0.99, max_iters=1000, flags=CV,
+                                                         error_kind=1)
+    else:
+        cnt_o, F_o, mask_o, _ = oracle.find_fundamental(a, b, thr=5e-3, conf=0.99, max_iters=1000, flags=CV)
+    assert cnt == cnt_o
+    np.testing.assert_array_equal(mask, mask_o.astype(bool))
+    np.testing.assert_array_equal(F, F_o)
+
+
+@pytest.mark.parametrize("n,outl,seed", [(300, 0.5, 1), (5000, 0.5, 2), (20000, 0.6, 3)])
+def test_recover_pose_default_stream(gpu, oracle, n, outl, seed):
+    FOCAL, PP = 800.0, (640.0, 360.0)
+    a, b, *_ = S.essential_problem(n, seed=seed, outlier_frac=outl, focal=FOCAL, pp=PP)
+    cfg = opencv.recoverPoseConfig(FOCAL, PP, 0.999, 1.0)
+    res, Rg, tg, ms = opencv.recoverPose(cfg, a, b)
+    rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=0.999, max_iters=1000, flags=CV)
+    np.testing.assert_array_equal(ms, rmask.astype(bool))
+    rres, Rr, tr, g = oracle.recover_pose(a, b, Er, rmask, FOCAL, PP)
+    assert res == g
+    np.testing.assert_array_equal(Rg, Rr)
+    np.testing.assert_array_equal(tg, tr)
+    # the Philox stream (seed 0) is a different hypothesis sequence: same geometry, other samples
+    p = opencv.RansacParams(threshold=1.0, confidence=0.999, max_iters=1000, seed=0)
+    cnt_p, E_p, m_p = opencv.findEssentialMat(a, b, FOCAL, PP, p)
+    assert cnt_p > 0
+
+
+@pytest.mark.parametrize("kind", ["Iterative", "EPNP", "AP3P", "P3P"])
+@pytest.mark.parametrize("n,seed,dist", [(300, 1, None), (5000, 2, True)])
+def test_solve_pnp_ransac_default_stream(gpu, oracle, kind, n, seed, dist):
+    DIST = np.array([0.05, -0.01, 1e-3, -5e-4]) if dist else None
+    img, W, inl, K, d, R, t = S.pnp_problem(n, seed=seed, outlier_frac=0.5, sigma=0.3, dist=DIST)
+    ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, d, kind=kind, iterations=200, reproj_error=2.0,
+                                               confidence=0.99)
+    rc, rr, rt, rmask, _ = oracle.solve_pnp_ransac(img, W, K, d, thr=2.0, conf=0.99, max_iters=200, flags=CV,
+                                                   kind=opencv.SOLVER_KIND[kind])
+    assert ok and rc > 0
+    np.testing.assert_array_equal(inliers, np.nonzero(rmask)[0])
+    if opencv.SOLVER_KIND[kind] != 0:
+        np.testing.assert_allclose(r, rr, rtol=0, atol=1e-14)
+        np.testing.assert_array_equal(tt, rt)
+    else:
+        np.testing.assert_allclose(r, rr, rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(tt, rt, rtol=1e-6, atol=1e-9)
+
+
+def test_multishard_cv_stream_identical(gpu):
+    """deviceCount = 4 splits every chunk over shard workspaces; each gets the same table."""
+    src, dst, _ = S.homography_problem(5000, 6, outlier_frac=0.6)
+    p1 = opencv.RansacParams(threshold=5e-3, max_iters=3000, cv_sampler=True)
+    p4 = opencv.RansacParams(threshold=5e-3, max_iters=3000, cv_sampler=True, device_count=4)
+    c1, H1, m1 = opencv.findHomography(src, dst, p1)
+    c4, H4, m4 = opencv.findHomography(src, dst, p4)
+    assert c1 == c4
+    np.testing.assert_array_equal(m1, m4)
+    np.testing.assert_array_equal(H1, H4)

@@ -110,7 +110,8 @@ def test_recover_pose_vs_oracle(gpu, oracle, n, outl, seed, thr):
     a, b, inl, R, tu, E = S.essential_problem(n, seed=seed, outlier_frac=outl, sigma=0.2)
     cfg = opencv.recoverPoseConfig(FOCAL, PP, 0.999, thr)
     res, Rg, tg, ms = opencv.recoverPose(cfg, a, b)
-    rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=thr, conf=0.999, max_iters=1000, seed=0)
+    rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=thr, conf=0.999, max_iters=1000,
+                                             flags=N.FLAG_CV_SAMPLER)   # OpenCV's own sample stream
     np.testing.assert_array_equal(ms, rmask)                          # ms = RANSAC mask (:206-210)
     rres, Rr, tr, g = oracle.recover_pose(a, b, Er, rmask, FOCAL, PP)
     assert res == rres
@@ -124,7 +125,8 @@ def test_recover_poses_vs_oracle(gpu, oracle):
     a, b, inl, R, tu, E = S.essential_problem(4000, seed=9, outlier_frac=0.5, sigma=0.2)
     cfg = opencv.recoverPoseConfig(FOCAL, PP, 0.999, 1.0)
     R1, R2, t, ms = opencv.recoverPoses(cfg, a, b)
-    rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=0.999, max_iters=1000, seed=0)
+    rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=0.999, max_iters=1000,
+                                             flags=N.FLAG_CV_SAMPLER)
     np.testing.assert_array_equal(ms, rmask)
     oR1, oR2, ot = oracle.e_decompose(Er)
     np.testing.assert_array_equal(R1, oR1)

@@ -155,7 +155,7 @@ def test_solve_pnp_ransac_reference_signature(native, gpu):
 def test_n4_and_solve_pnp(gpu, oracle):
     img, W, inl, K, d, R, t = S.pnp_problem(4, seed=12, outlier_frac=0, sigma=0)
     ok, r, tt, inliers = opencv.solvePnPRansac(img, W, K, None, iterations=100, reproj_error=2.0)
-    rc, rr, rt, rmask, _ = oracle.solve_pnp_ransac(img, W, K, None, thr=2.0)
+    rc, rr, rt, rmask, _ = oracle.solve_pnp_ransac(img, W, K, None, thr=2.0, flags=N.FLAG_CV_SAMPLER)
     assert ok and list(inliers) == [0, 1, 2, 3] and rc == 4
     np.testing.assert_array_equal(r, rr)
     np.testing.assert_array_equal(tt, rt)
