@@ -164,7 +164,10 @@ MCV_API mcvBool cvDetectArucoMarkers(char* data, int width, int height, int chan
                                      OpenCV's computeError produces, e.g. clang on arm64). Default:
                                      op-by-op, every operation rounded as written = OpenCV's x86-64
                                      (SSE baseline) build, the reference's Linux/AMD64 target. */
-#define MCV_FLAG_FAST_MINIMAL 16  /* homography / 8-point fundamental: opt-in minimal solve by 8x8 Gaussian
+#define MCV_FLAG_FAST_MINIMAL 16  /* opt-in replacement minimal solvers. Essential: Gauss-Jordan null space,
+                                     polynomial-product constraints, Illinois real roots (default: the
+                                     reference's fivepoint.cpp solver). Homography / 8-point fundamental:
+                                     minimal solve by 8x8 Gaussian
                                      elimination with h22 = 1 / f22 = 1 (no eigenvalue check for F).
                                      Default: OpenCV's own runKernel / run8Point, the 9x9 cv::eigen
                                      (JacobiImpl_) of LtL / A^T A. The two agree to ~1e-11 relative; the
@@ -401,9 +404,13 @@ MCV_API long long mcvTestDivF64(int mode, unsigned long long seed, long long cou
  * sweep, 3 = op-by-op through the certified division-free sweep (the default path). */
 MCV_API int mcvTestHomographySweep(const float* pts4, int N, const float* models8, int nModels, float thr2, int fused,
                                    int* counts);
-/* Host twins of the essential path: hypothesis (double4 normalised points; E90 = 10 x 9) and the
- * raw five-point solve (x1[5], y1[5], x2[5], y2[5] packed in p20). Return the model count / status. */
+/* Host twins of the essential path: hypothesis (double4 normalised points; E90 = 10 x 9; the reference's
+ * solver, as the default GPU path) and the raw five-point solves (x1[5], y1[5], x2[5], y2[5] packed in
+ * p20): mcvHostFivePoint = the opt-in replacement solver, mcvHostFivePointRef = the reference's.
+ * Return the model count / status. */
 MCV_API int mcvHostEssential(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90, int* sampleIdx);
+/* mcvHostEssential with the opt-in replacement solver (MCV_FLAG_FAST_MINIMAL). */
+MCV_API int mcvHostEssentialFast(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90, int* sampleIdx);
 MCV_API int mcvHostFivePoint(const double* p20, double* E90);
 /* Host build of the cvFivePoint export's own path (e_solve5_ref), same packing as mcvHostFivePoint. */
 MCV_API int mcvHostFivePointRef(const double* p20, double* E90);

@@ -1,5 +1,6 @@
 // hyp_essential.h — per-hypothesis code of the essential-matrix RANSAC path:
-// the five-point minimal solver, the pose decomposition and the two-view cheirality test.
+// the opt-in replacement five-point solver (MCV_FLAG_FAST_MINIMAL; the default is the reference's own,
+// five_point_ref.h), the pose decomposition and the two-view cheirality test.
 // Compiled for gfx950 (ransac_e.hip) and for the host (mcvHostEssential test hook) with
 // -ffp-contract=off, so both sides round every operation identically (fp64 +,-,*,/ and sqrt are
 // IEEE correctly rounded on both; comparisons and integer bisection are exact).
@@ -24,7 +25,6 @@
 
 #include "mcv_common.h"
 #include "hyp_fundamental.h"   // jacobi3
-#include "epnp.h"              // jacobi_svd (the cvFivePoint export's SVDs)
 
 namespace mcv {
 
@@ -522,208 +522,8 @@ MCV_HD int e_solve5(const double* x1, const double* y1, const double* x2, const 
     return count;
 }
 
-// ---- the cvFivePoint export's own path (fivepoint.cpp:233-339) ----------------------------------
-// The RANSAC solver above keeps every step bit-reproducible and cheap; the standalone export
-// restates the reference's steps instead, so that its models come out in the reference's order:
-//  * null space: SVD::compute(Q, FULL_UV) of the 5 x 9 system = JacobiSVD on Q's rows with the four
-//    completion rows drawn by cv::RNG(0x12345678) and orthogonalised (epnp.h jacobi_svd<9, 5, 9>);
-//    EE = Vt rows 5..8 (fivepoint.cpp:252-254);
-//  * coefficient matrix: e_coeffs (the same polynomial entries as getCoeffMat, other operation
-//    order), A(:, 0:10)^-1 A(:, 10:20) by OpenCV's LU (partial pivoting, LUImpl) and a sequential
-//    product, B rows and det B(z) as above (rounding-level differences to the reference);
-//  * roots: cv::solvePoly restated exactly (Durand-Kerner from (1 + i)^k, 300 sweeps of in-place
-//    updates, OpenCV's Complex division by 1 / |b|^2), kept when |Im| <= 1e-10, in that order;
-//  * (x, y): SVD::solveZ of B(z) (last row of Vt of its 3 x 3 JacobiSVD), skipped when
-//    |xy1[2]| < 1e-10; E = x X + y Y + z Z + W scaled by 1 / ||E||.
-
-// OpenCV LUImpl<double> on A (n x n, destroyed) with right-hand sides b (n x nb): b <- A^-1 b.
-template <int N, int NB>
-MCV_HD bool e_lu_solve(double (&A)[N][N], double (&b)[N][NB]) {
-    const double eps = kDblEpsilon * 100;
-    for (int i = 0; i < N; ++i) {
-        int k = i;
-        for (int j = i + 1; j < N; ++j)
-            if (fabs(A[j][i]) > fabs(A[k][i])) k = j;
-        if (fabs(A[k][i]) < eps) return false;
-        if (k != i) {
-            for (int j = i; j < N; ++j) { const double t = A[i][j]; A[i][j] = A[k][j]; A[k][j] = t; }
-            for (int j = 0; j < NB; ++j) { const double t = b[i][j]; b[i][j] = b[k][j]; b[k][j] = t; }
-        }
-        const double d = -1 / A[i][i];
-        for (int j = i + 1; j < N; ++j) {
-            const double alpha = A[j][i] * d;
-            for (int q = i + 1; q < N; ++q) A[j][q] += alpha * A[i][q];
-            for (int q = 0; q < NB; ++q) b[j][q] += alpha * b[i][q];
-        }
-        A[i][i] = -d;
-    }
-    for (int i = N - 1; i >= 0; --i)
-        for (int j = 0; j < NB; ++j) {
-            double s = b[i][j];
-            for (int q = i + 1; q < N; ++q) s -= A[i][q] * b[q][j];
-            b[i][j] = s * A[i][i];
-        }
-    return true;
-}
-
-struct ECplx { double re, im; };
-
-// Durand-Kerner sweeps of cv::solvePoly on a polynomial of fixed degree NN (co[0..NN], roots[0..NN)):
-// the same in-place updates in the same order as the generic loop below, with compile-time indices so
-// the GPU keeps roots and coefficients in registers. solvePoly stops only when a whole sweep leaves
-// every root unchanged (maxDiff <= 0), which in practice never happens: all 300 sweeps run.
-template <int NN>
-MCV_HD void e_dk_sweeps(ECplx (&co)[11], ECplx (&roots)[10]) {
-    ECplx cc[NN + 1], rr[NN];
-#pragma unroll
-    for (int i = 0; i <= NN; ++i) cc[i] = co[i];
-#pragma unroll
-    for (int i = 0; i < NN; ++i) rr[i] = roots[i];
-    for (int iter = 0; iter < 300; ++iter) {
-        double maxDiff = 0;
-#pragma unroll
-        for (int i = 0; i < NN; ++i) {
-            const ECplx p = rr[i];
-            ECplx num = cc[NN], den = cc[NN];
-#pragma unroll
-            for (int j = 0; j < NN; ++j) {
-                num = {num.re * p.re - num.im * p.im + cc[NN - j - 1].re, num.re * p.im + num.im * p.re + cc[NN - j - 1].im};
-                if (j != i) {
-                    const ECplx d = {p.re - rr[j].re, p.im - rr[j].im};
-                    den = {den.re * d.re - den.im * d.im, den.re * d.im + den.im * d.re};
-                }
-            }
-            const double t = 1. / (den.re * den.re + den.im * den.im);
-            num = {(num.re * den.re + num.im * den.im) * t, (-num.re * den.im + num.im * den.re) * t};
-            rr[i] = {p.re - num.re, p.im - num.im};
-            const double a = sqrt(num.re * num.re + num.im * num.im);
-            maxDiff = maxDiff > a ? maxDiff : a;
-        }
-        if (maxDiff <= 0) break;
-    }
-#pragma unroll
-    for (int i = 0; i < NN; ++i) roots[i] = rr[i];
-}
-
-// cv::solvePoly(coeffs, roots, 300) for a degree-10 real polynomial (coeffs ascending).
-MCV_HD void e_solve_poly10(const double* c, ECplx (&roots)[10], ECplx (&co)[11]) {
-    for (int i = 0; i <= 10; ++i) co[i] = {c[i], 0.0};
-    int n = 10;
-    for (; n > 1; --n)
-        if (fabs(co[n].re) + fabs(co[n].im) > kDblEpsilon) break;
-    ECplx p = {1, 0};
-    const ECplx r = {1, 1};
-    for (int i = 0; i < 10; ++i) roots[i] = {0.0, 0.0};
-    for (int i = 0; i < n; ++i) {
-        roots[i] = p;
-        p = {p.re * r.re - p.im * r.im, p.re * r.im + p.im * r.re};
-    }
-    if (n == 10) {   // the full degree (the leading coefficient of det B(z) is not ~0)
-        e_dk_sweeps<10>(co, roots);
-        return;
-    }
-    for (int iter = 0; iter < 300; ++iter) {
-        double maxDiff = 0;
-        for (int i = 0; i < n; ++i) {
-            p = roots[i];
-            ECplx num = co[n], den = co[n];
-            for (int j = 0; j < n; ++j) {
-                num = {num.re * p.re - num.im * p.im + co[n - j - 1].re, num.re * p.im + num.im * p.re + co[n - j - 1].im};
-                if (j != i) {
-                    const ECplx d = {p.re - roots[j].re, p.im - roots[j].im};
-                    den = {den.re * d.re - den.im * d.im, den.re * d.im + den.im * d.re};
-                }
-            }
-            const double t = 1. / (den.re * den.re + den.im * den.im);
-            num = {(num.re * den.re + num.im * den.im) * t, (-num.re * den.im + num.im * den.re) * t};
-            roots[i] = {p.re - num.re, p.im - num.im};
-            const double a = sqrt(num.re * num.re + num.im * num.im);
-            maxDiff = maxDiff > a ? maxDiff : a;
-        }
-        if (maxDiff <= 0) break;
-    }
-    for (; n < 10; ++n) roots[n] = roots[n - 1];
-}
-
-// Working set of the export's five-point solve: a private array on the host; on the GPU one
-// __shared__ copy for the single solving lane (its data-dependent pivoting and root loops otherwise
-// run from 4 KB of scratch).
-struct E5RefWs {
-    double U[9][9];
-    double A[10][20], L[10][10], C[10][10], P[10][10];
-    ECplx co[11], roots[10];
-};
-
-// The export's five-point solve (normalised coordinates as given): E[10][9] row-major, count.
-MCV_HD int e_solve5_ref(const double* x1, const double* y1, const double* x2, const double* y2, double (*E)[9],
-                        E5RefWs& ws) {
-    double nb[4][9];
-    {
-        double (&U)[9][9] = ws.U;
-        double w[5];
-        for (int i = 0; i < 9; ++i)
-            for (int k = 0; k < 9; ++k) U[i][k] = 0.0;
-        for (int i = 0; i < 5; ++i) {
-            U[i][0] = x1[i] * x2[i]; U[i][1] = y1[i] * x2[i]; U[i][2] = x2[i] * 1.0;
-            U[i][3] = x1[i] * y2[i]; U[i][4] = y1[i] * y2[i]; U[i][5] = y2[i] * 1.0;
-            U[i][6] = x1[i] * 1.0; U[i][7] = y1[i] * 1.0; U[i][8] = 1.0;
-        }
-        jacobi_svd<9, 5, 9>(U, w, (double(*)[5])nullptr);
-        for (int b = 0; b < 4; ++b)
-            for (int k = 0; k < 9; ++k) nb[b][k] = U[5 + b][k];
-    }
-    double (&C)[10][10] = ws.C;
-    {
-        double (&A)[10][20] = ws.A;
-        double (&L)[10][10] = ws.L;
-        e_coeffs(nb, A);
-        for (int r = 0; r < 10; ++r)
-            for (int k = 0; k < 10; ++k) { L[r][k] = A[r][k]; C[r][k] = k == r ? 1.0 : 0.0; }
-        if (!e_lu_solve<10, 10>(L, C)) return 0;    // C = A(:, 0:10)^-1
-        double (&P)[10][10] = ws.P;
-        for (int r = 0; r < 10; ++r)
-            for (int k = 0; k < 10; ++k) {
-                double s = 0;
-                for (int q = 0; q < 10; ++q) s += C[r][q] * A[q][10 + k];
-                P[r][k] = s;
-            }
-        for (int r = 0; r < 10; ++r)
-            for (int k = 0; k < 10; ++k) C[r][k] = P[r][k];
-    }
-    double bx[3][4], by[3][4], bc[3][5];
-    e_bz(&C[0][0], 10, bx, by, bc);
-    double det[11];
-    e_detpoly(bx, by, bc, det);
-    ECplx (&roots)[10] = ws.roots;
-    e_solve_poly10(det, roots, ws.co);
-    int count = 0;
-    for (int i = 0; i < 10; ++i) {
-        if (fabs(roots[i].im) > 1e-10) continue;
-        const double z1 = roots[i].re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
-        double Bz[3][3];
-        for (int j = 0; j < 3; ++j) {
-            Bz[j][0] = bx[j][3] * z3 + bx[j][2] * z2 + bx[j][1] * z1 + bx[j][0];
-            Bz[j][1] = by[j][3] * z3 + by[j][2] * z2 + by[j][1] * z1 + by[j][0];
-            Bz[j][2] = bc[j][4] * z4 + bc[j][3] * z3 + bc[j][2] * z2 + bc[j][1] * z1 + bc[j][0];
-        }
-        double At[3][3], w[3], Vt[3][3];
-        for (int a = 0; a < 3; ++a)
-            for (int b = 0; b < 3; ++b) At[a][b] = Bz[b][a];
-        jacobi_svd<3, 3>(At, w, Vt);
-        const double* xy1 = Vt[2];
-        if (fabs(xy1[2]) < 1e-10) continue;
-        const double x = xy1[0] / xy1[2], y = xy1[1] / xy1[2];
-        double e[9], ss = 0;
-        for (int k = 0; k < 9; ++k) {
-            e[k] = nb[0][k] * x + nb[1][k] * y + nb[2][k] * z1 + nb[3][k];
-            ss += e[k] * e[k];
-        }
-        const double sc = 1. / sqrt(ss);
-        for (int k = 0; k < 9; ++k) E[count][k] = e[k] * sc;
-        ++count;
-    }
-    return count;
-}
+// The reference's own five-point solver (the default RANSAC path and the cvFivePoint export) lives in
+// five_point_ref.h; e_solve5 above is the opt-in replacement (MCV_FLAG_FAST_MINIMAL).
 
 // One hypothesis on packed double4 normalised correspondences {x1, y1, x2, y2}: 5 distinct
 // indices from the Philox stream (no subset check: EMEstimatorCallback has none), five-point

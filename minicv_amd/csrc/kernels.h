@@ -105,6 +105,11 @@ void launch_e_generate(const double* d_pts4, int N, Sampler smp, int64_t hypBegi
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
                      int maxModels, int* d_counts, float thr2, int kind, hipStream_t s, const float* d_pts32 = nullptr,
                      const double* d_bb = nullptr);
+// The reference's five-point solver (five_point_ref.h) over a chunk: the default RANSAC generate.
+size_t e5_stage_bytes(int hypCount);
+void launch_e5_generate(const double* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_dense,
+                        int* d_denseSlot, int* d_nDense, int* d_counts, void* d_stage, hipStream_t s);
+void launch_e5_one(const double* d_pts4, int N, Sampler smp, int64_t hyp, EOneOut* d_out, hipStream_t s);
 void launch_e_fetch(const void* d_dense, const int* d_denseSlot, const int* d_nDense, int maxModels, int slot,
                     void* d_out, int* d_found, hipStream_t s);
 void launch_e_one(const double* d_pts4, int N, Sampler smp, int64_t hyp, EOneOut* d_out, hipStream_t s);

@@ -18,7 +18,7 @@
 //   mcv_e_one           recompute one hypothesis (winner) -> all its models (one wave).
 //   mcv_e_mask          inlier mask of the winner.
 //   mcv_e_cheirality    recoverPose: one lane per (RANSAC inlier, (R, t) candidate) cheirality test.
-//   mcv_e_fivepoint     cvFivePoint: the reference's own five-point path on raw coordinates (one lane).
+// The reference's five-point solver (the default RANSAC generate, cvFivePoint): ransac_e5.hip.
 #include "mcv_common.h"
 #include "hyp_essential.h"
 #include "five_point_wave.h"
@@ -386,17 +386,6 @@ __global__ __launch_bounds__(256) void mcv_e_cheirality(const double4* __restric
     }
 }
 
-// cvFivePoint: the export's own path (e_solve5_ref: JacobiSVD null space, LU elimination,
-// solvePoly roots with |Im| <= 1e-10 in its order, solveZ), one lane.
-__global__ __launch_bounds__(64) void mcv_e_fivepoint(EFiveIn in, EOneOut* __restrict__ out) {
-    __shared__ E5RefWs ws;
-    if (threadIdx.x != 0) return;
-    const int n = e_solve5_ref(in.x1, in.y1, in.x2, in.y2, out->E, ws);   // models straight to the record
-    out->status = n;
-    for (int s = n > 0 ? n : 0; s < kEMaxModels; ++s)
-        for (int k = 0; k < 9; ++k) out->E[s][k] = 0.0;
-}
-
 // ---- launchers ---------------------------------------------------------------------------------
 void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, double* d_pts4, hipStream_t s) {
     if (N <= 0) return;
@@ -555,8 +544,5 @@ void launch_e_cheirality(const double* d_pts4, int N, const uint8_t* d_mask, con
                        N, d_mask, c, dist, d_good4);
 }
 
-void launch_e_fivepoint(const EFiveIn& in, EOneOut* d_out, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_e_fivepoint, dim3(1), dim3(64), 0, s, in, d_out);
-}
 
 }  // namespace mcv

@@ -26,18 +26,28 @@ namespace mcv {
 static const double kCheiralityDist = 50.0;   // recoverPose's distanceThresh for the focal/pp overload
 
 static int e_kind(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_ERROR) ? 0 : 1; }
+// MCV_FLAG_FAST_MINIMAL: the replacement five-point solver (Gauss-Jordan null space, polynomial-product
+// constraints, Illinois real roots) instead of the reference's (fivepoint.cpp / five_point_ref.h).
+static bool e_fast(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0; }
 
 void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
                       int* d_counts, hipStream_t s) {
     const float thr2 = (float)(cfg.threshold * cfg.threshold);
     const Sampler smp = P.sampler(cfg);
+    const bool fast = e_fast(cfg);
     {
         ProfScope pg("e_generate", s);
-        if (hypCount >= kEStageMinHyps) P.estage.ensure((size_t)hypCount * sizeof(EStage));
-        launch_e_generate(d_pts, N, smp, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts,
-                          hypCount >= kEStageMinHyps ? P.estage.p : nullptr, s);
+        if (fast) {   // opt-in: the Illinois replacement solver (hyp_essential.h / five_point_wave.h)
+            if (hypCount >= kEStageMinHyps) P.estage.ensure((size_t)hypCount * sizeof(EStage));
+            launch_e_generate(d_pts, N, smp, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts,
+                              hypCount >= kEStageMinHyps ? P.estage.p : nullptr, s);
+        } else {      // default: the reference's own five-point solver (five_point_ref.h)
+            P.estage.ensure(e5_stage_bytes(hypCount));
+            launch_e5_generate(d_pts, N, smp, hypBegin, hypCount, P.models.p, P.dslot.p, P.ndense.p, d_counts,
+                               P.estage.p, s);
+        }
     }
-    P.last.set(hypBegin, hypCount, smp, d_pts, N, 30);
+    P.last.set(hypBegin, hypCount, smp, d_pts, N, fast ? 31 : 30);
     P.bb4.ensure(4);
     P.pts.ensure((size_t)N * 4);
     launch_abs_bound4(d_pts, true, N, P.bb4.p, P.pts.p, s);   // fp32 copy + bounds for the prefilter
@@ -46,9 +56,11 @@ void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& c
                     s, P.pts.p, P.bb4.p);
 }
 
-static EOneOut e_one(Plan& P, const double* d_pts, int N, const Sampler& smp, int64_t hyp, hipStream_t s) {
+static EOneOut e_one(Plan& P, const double* d_pts, int N, const Sampler& smp, int64_t hyp, bool fast,
+                     hipStream_t s) {
     EOneOut* d_one = (EOneOut*)P.one.p;
-    launch_e_one(d_pts, N, smp, hyp, d_one, s);
+    if (fast) launch_e_one(d_pts, N, smp, hyp, d_one, s);
+    else launch_e5_one(d_pts, N, smp, hyp, d_one, s);
     MCV_HIP(hipGetLastError());
     EOneOut one;
     MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(EOneOut), hipMemcpyDeviceToHost, s));
@@ -75,7 +87,7 @@ int e_finalize(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int
     const int k = (int)(slot % kEModelSlots);
     bool have = false;
     const Sampler smp = P.sampler(cfg);
-    if (P.last.covers(hyp, smp, d_pts, N, 30)) {
+    if (P.last.covers(hyp, smp, d_pts, N, e_fast(cfg) ? 31 : 30)) {
         const int local = (int)((hyp - P.last.begin) * kEModelSlots + k);
         int* d_found = P.ndense.p + 7;
         uint8_t* d_out = P.one.p;
@@ -90,7 +102,7 @@ int e_finalize(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int
         }
     }
     if (!have) {
-        const EOneOut one = e_one(P, d_pts, N, smp, hyp, s);
+        const EOneOut one = e_one(P, d_pts, N, smp, hyp, e_fast(cfg), s);
         if (one.status <= k) fail("winning slot %lld has no model (status %d)", (long long)slot, one.status);
         for (int j = 0; j < 9; ++j) E[j] = one.E[k][j];
     }
@@ -321,10 +333,11 @@ extern "C" MCV_API int mcvPackEssential(const mcvV2d* a, const mcvV2d* b, int N,
 }
 
 // ---- host twins (test hooks) -------------------------------------------------------------------
-extern "C" MCV_API int mcvHostEssential(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90,
-                                        int* sampleIdx) {
+// Host twin with the opt-in replacement solver (MCV_FLAG_FAST_MINIMAL).
+extern "C" MCV_API int mcvHostEssentialFast(const double* pts4, int N, uint64_t seed, int64_t hyp, double* E90,
+                                            int* sampleIdx) {
     MCV_GUARD(kStatusNoSample - 1, {
-        if (!pts4 || !E90 || N < 5) fail("mcvHostEssential: bad argument");
+        if (!pts4 || !E90 || N < 5) fail("mcvHostEssentialFast: bad argument");
         double E[kEMaxModels][9];
         const int n = e_hypothesis(pts4, N, Sampler{seed, nullptr}, (uint64_t)hyp, E, sampleIdx);
         for (int s = 0; s < kEMaxModels; ++s)
@@ -338,18 +351,6 @@ extern "C" MCV_API int mcvHostFivePoint(const double* p20, double* E90) {
         if (!p20 || !E90) fail("mcvHostFivePoint: null argument");
         double E[kEMaxModels][9];
         const int n = e_solve5(p20, p20 + 5, p20 + 10, p20 + 15, E);
-        for (int s = 0; s < kEMaxModels; ++s)
-            for (int k = 0; k < 9; ++k) E90[9 * s + k] = s < n ? E[s][k] : 0.0;
-        return n;
-    })
-}
-
-extern "C" MCV_API int mcvHostFivePointRef(const double* p20, double* E90) {
-    MCV_GUARD(-1, {
-        if (!p20 || !E90) fail("mcvHostFivePointRef: null argument");
-        double E[kEMaxModels][9];
-        E5RefWs ws;
-        const int n = e_solve5_ref(p20, p20 + 5, p20 + 10, p20 + 15, E, ws);
         for (int s = 0; s < kEMaxModels; ++s)
             for (int k = 0; k < 9; ++k) E90[9 * s + k] = s < n ? E[s][k] : 0.0;
         return n;

@@ -144,6 +144,7 @@ SIGNATURES = {
     "mcvHostHypothesis": (_I, [_I, _P, _I, _U64, _I64, _P, _P, _P]),
     "mcvHostPhilox": (None, [C.c_uint32] * 6 + [_P]),
     "mcvHostEssential": (_I, [_P, _I, _U64, _I64, _P, _P]),
+    "mcvHostEssentialFast": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostFivePoint": (_I, [_P, _P]),
     "mcvHostFivePointRef": (_I, [_P, _P]),
     "mcvHostF7": (_I, [_P, _I, _U64, _I64, _P, _P]),

@@ -192,6 +192,7 @@ static void mul33(const double* A, const double* B, double* C) {
  * MCV_FLAG_FAST_MINIMAL elimination. Test infrastructure: set before the (OpenMP) calls. */
 static int g_fast_minimal = 0;
 void orc_set_fast_minimal(int v) { g_fast_minimal = v; }
+int orc_get_fast_minimal(void) { return g_fast_minimal; }
 
 /* MCV_FLAG_FAST_MINIMAL (opt-in): runKernel's normalisation, then the 8x8 system (h22 = 1) by Gaussian
  * elimination with partial pivoting (first maximum), back substitution, de-normalisation,

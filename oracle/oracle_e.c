@@ -339,12 +339,63 @@ int orc_e_solve5(const double* x1, const double* y1, const double* x2, const dou
     return count;
 }
 
-/* cvFivePoint's own path (fivepoint.cpp:233-339) as the export restates it: null space from
- * SVD::compute(Q, FULL_UV) (JacobiSVD with the cv::RNG completion rows), A(:, :10)^-1 A(:, 10:) by
- * OpenCV's LUImpl and a sequential product, det B(z), cv::solvePoly (Durand-Kerner, 300 sweeps,
- * OpenCV Complex arithmetic), roots with |Im| <= 1e-10 in solvePoly's order, SVD::solveZ of B(z),
- * E scaled by 1 / ||E||. Deviations from the reference: the coefficient matrix and det B(z) use
- * the generic products of constraint_matrix / pmul (the same polynomials, other rounding). */
+/* ---- the reference's own five-point path (fivepoint.cpp:233-339, runFivepoint) ----------------
+ * Default minimal solver of the RANSAC path and the cvFivePoint export. Every step restated in the
+ * reference's (and OpenCV 4.x's [ext]) operation order:
+ *  - null space: SVD::compute(Q, W, U, Vt, MODIFY_A | FULL_UV) of the 5 x 9 system (:252) = JacobiSVD on
+ *    Q's rows with the four completion rows drawn by cv::RNG(0x12345678) (orc_jsvd); EE = Vt rows 5..8;
+ *  - the 10 x 20 constraint matrix: getCoeffMat (:10-231), every entry's expression evaluated term by
+ *    term in the source's order from fivepoint_terms.inc (generated from the reference's text by
+ *    scripts/gen/gen_fivepoint_terms.py), then its column permutation perm[20] (:220-225);
+ *  - A = A.colRange(0, 10).inv() * A.colRange(10, 20) (:260): OpenCV evaluates inv(X) * Y as
+ *    cv::solve(X, Y, DECOMP_LU) [ext: matop.cpp MatOp_Invert::matmul -> MatOp_Solve] = LUImpl on X with
+ *    the ten right-hand sides (eps 100 DBL_EPSILON), not an explicit inverse;
+ *  - B (3 x 13) = row1 - row2 from rows 4..9 (:262-277), the degree-10 coefficients c[] (:299-309)
+ *    term by term from fivepoint_terms.inc;
+ *  - cv::solvePoly (Durand-Kerner, 300 sweeps, OpenCV Complex arithmetic), roots with |Im| <= 1e-10 in
+ *    solvePoly's order; Bz rows (:318-323); SVD::solveZ (last row of Vt of the 3 x 3 JacobiSVD);
+ *    |xy1[2]| < 1e-10 skips; Evec = ((X x + Y y) + 0) + Z z + W (addWeighted, scaleAdd, add), Evec /= norm
+ *    (normL2Sqr's 4-way unrolled sum; convertTo by 1 / norm).
+ * Divergences (degenerate samples only): a singular 10 x 10 block (|pivot| < 100 DBL_EPSILON) gives no
+ * model here, where cv::solve returns zeros and the reference goes on to NaN / arbitrary models; a
+ * leading coefficient |c[10]| <= DBL_EPSILON repeats the last root where solvePoly copies uninitialised
+ * buffer entries. */
+#include "fivepoint_terms.inc"
+
+static double fp_factor(unsigned char f, const double* v) {
+    const int k = f >> 6, i = f & 63;
+    if (k == 0) return orc_fp_literals[i];
+    if (k == 1) return v[i];
+    const double p2 = v[i] * v[i];
+    return k == 2 ? p2 : p2 * v[i];
+}
+
+static double fp_sum(const OrcFpTerm* t, int n, const double* v) {
+    double acc = 0;
+    for (int j = 0; j < n; ++j) {
+        double p = fp_factor(t[j].f[0], v);
+        for (int q = 1; q < 4 && t[j].f[q] != 0xFF; ++q) p = p * fp_factor(t[j].f[q], v);
+        if (t[j].neg) p = -p;
+        acc = j == 0 ? p : acc + p;
+    }
+    return acc;
+}
+
+/* getCoeffMat(e, A): e = EE^T (4 x 9 row-major), A row-major 10 x 20 after the column permutation */
+void orc_fp_coeff_matrix(const double* e, double* A) {
+    double Araw[200];
+    for (int k = 0; k < 200; ++k)
+        Araw[k] = fp_sum(orc_fp_a_terms + orc_fp_a_start[k], orc_fp_a_start[k + 1] - orc_fp_a_start[k], e);
+    for (int i = 0; i < 20; ++i)
+        for (int j = 0; j < 10; ++j) A[i + 20 * j] = Araw[orc_fp_perm[i] + 20 * j];
+}
+
+void orc_fp_det_coeffs(const double* b, double* c) {
+    for (int k = 0; k < 11; ++k)
+        c[k] = fp_sum(orc_fp_c_terms + orc_fp_c_start[k], orc_fp_c_start[k + 1] - orc_fp_c_start[k], b);
+}
+
+/* LUImpl<double>(A, 10, b, 10 right-hand sides), eps = 100 DBL_EPSILON; b <- A^-1 b. */
 static int lu_solve10(double A[10][10], double b[10][10]) {
     const double eps = DBL_EPSILON * 100;
     for (int i = 0; i < 10; ++i) {
@@ -408,15 +459,36 @@ void orc_solve_poly10(const double* c, double* rre, double* rim) {
             rre[i] = pre - qre;
             rim[i] = pim - qim;
             double a = sqrt(qre * qre + qim * qim);
-            maxDiff = maxDiff > a ? maxDiff : a;
+            maxDiff = maxDiff < a ? a : maxDiff;   /* std::max(maxDiff, cv::abs(num)) */
         }
         if (maxDiff <= 0) break;
     }
     for (; n < 10; ++n) { rre[n] = rre[n - 1]; rim[n] = rim[n - 1]; }
 }
 
+/* B (3 x 13, row-major as fivepoint.cpp's b[39]) from the solved 10 x 10 block C */
+static void fp_b_matrix(double C[10][10], double* b) {
+    for (int i = 0; i < 3; ++i) {
+        const double* r1 = C[2 * i + 4];
+        const double* r2 = C[2 * i + 5];
+        double row1[13] = {0}, row2[13] = {0};
+        for (int k = 0; k < 3; ++k) { row1[1 + k] = r1[k] * 1.0; row1[5 + k] = r1[3 + k] * 1.0; row2[k] = r2[k] * 1.0; row2[4 + k] = r2[3 + k] * 1.0; }
+        for (int k = 0; k < 4; ++k) { row1[9 + k] = r1[6 + k] * 1.0; row2[8 + k] = r2[6 + k] * 1.0; }
+        for (int k = 0; k < 13; ++k) b[13 * i + k] = row1[k] - row2[k];
+    }
+}
+
+/* normL2Sqr<double, double>(a, 9) with CV_ENABLE_UNROLLED [ext: OpenCV core/base.hpp] */
+static double norm_l2sqr9(const double* a) {
+    double s = 0;
+    int i = 0;
+    for (; i <= 9 - 4; i += 4) s += a[i] * a[i] + a[i + 1] * a[i + 1] + a[i + 2] * a[i + 2] + a[i + 3] * a[i + 3];
+    for (; i < 9; ++i) s += a[i] * a[i];
+    return s;
+}
+
 int orc_e_solve5_ref(const double* x1, const double* y1, const double* x2, const double* y2, double* Eout) {
-    double nb[4][9], A[10][20], C[10][10];
+    double nb[4][9], A[200], C[10][10];
     {
         double U[81], w[5];
         memset(U, 0, sizeof(U));
@@ -429,62 +501,36 @@ int orc_e_solve5_ref(const double* x1, const double* y1, const double* x2, const
         orc_jsvd(U, w, NULL, 9, 5, 9);
         for (int b = 0; b < 4; ++b) memcpy(nb[b], U + 9 * (5 + b), sizeof(double) * 9);
     }
-    constraint_matrix(nb, A);
+    orc_fp_coeff_matrix(&nb[0][0], A);
     {
-        double L[10][10], P[10][10];
+        double L[10][10];
         for (int r = 0; r < 10; ++r)
-            for (int k = 0; k < 10; ++k) { L[r][k] = A[r][k]; C[r][k] = k == r ? 1.0 : 0.0; }
+            for (int k = 0; k < 10; ++k) { L[r][k] = A[20 * r + k]; C[r][k] = A[20 * r + 10 + k]; }
         if (!lu_solve10(L, C)) return 0;
-        for (int r = 0; r < 10; ++r)
-            for (int k = 0; k < 10; ++k) {
-                double s = 0;
-                for (int q = 0; q < 10; ++q) s += C[r][q] * A[q][10 + k];
-                P[r][k] = s;
-            }
-        memcpy(C, P, sizeof(P));
     }
-    double X[3][4], Y[3][4], K[3][5];
-    for (int i = 0; i < 3; ++i) {
-        const double* e = C[4 + 2 * i];
-        const double* f = C[5 + 2 * i];
-        X[i][3] = 0.0 - f[0]; X[i][2] = e[0] - f[1]; X[i][1] = e[1] - f[2]; X[i][0] = e[2] - 0.0;
-        Y[i][3] = 0.0 - f[3]; Y[i][2] = e[3] - f[4]; Y[i][1] = e[4] - f[5]; Y[i][0] = e[5] - 0.0;
-        K[i][4] = 0.0 - f[6]; K[i][3] = e[6] - f[7]; K[i][2] = e[7] - f[8]; K[i][1] = e[8] - f[9];
-        K[i][0] = e[9] - 0.0;
-    }
-    double u[8], v[8], w7[8], P1[11], P2[11], P3[11], a6[7], b6[7], w6[7], det[11];
-    pmul(Y[1], 3, K[2], 4, u); pmul(Y[2], 3, K[1], 4, v);
-    for (int k = 0; k < 8; ++k) w7[k] = u[k] - v[k];
-    pmul(X[0], 3, w7, 7, P1);
-    pmul(X[1], 3, K[2], 4, u); pmul(X[2], 3, K[1], 4, v);
-    for (int k = 0; k < 8; ++k) w7[k] = u[k] - v[k];
-    pmul(Y[0], 3, w7, 7, P2);
-    pmul(X[1], 3, Y[2], 3, a6); pmul(X[2], 3, Y[1], 3, b6);
-    for (int k = 0; k < 7; ++k) w6[k] = a6[k] - b6[k];
-    pmul(K[0], 4, w6, 6, P3);
-    for (int k = 0; k < 11; ++k) det[k] = P1[k] - P2[k] + P3[k];
+    double b[39], c[11];
+    fp_b_matrix(C, b);
+    orc_fp_det_coeffs(b, c);
     double rre[10], rim[10];
-    orc_solve_poly10(det, rre, rim);
+    orc_solve_poly10(c, rre, rim);
     int count = 0;
     for (int i = 0; i < 10; ++i) {
         if (fabs(rim[i]) > 1e-10) continue;
         double z1 = rre[i], z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
         double At[9], w[3], Vt[9];
         for (int j = 0; j < 3; ++j) {
-            At[j] = X[j][3] * z3 + X[j][2] * z2 + X[j][1] * z1 + X[j][0];
-            At[3 + j] = Y[j][3] * z3 + Y[j][2] * z2 + Y[j][1] * z1 + Y[j][0];
-            At[6 + j] = K[j][4] * z4 + K[j][3] * z3 + K[j][2] * z2 + K[j][1] * z1 + K[j][0];
+            const double* br = b + 13 * j;
+            At[j] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
+            At[3 + j] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
+            At[6 + j] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
         }
         orc_jsvd(At, w, Vt, 3, 3, 3);
         const double* xy1 = Vt + 6;
         if (fabs(xy1[2]) < 1e-10) continue;
-        double x = xy1[0] / xy1[2], y = xy1[1] / xy1[2], e[9], ss = 0;
-        for (int k = 0; k < 9; ++k) {
-            e[k] = nb[0][k] * x + nb[1][k] * y + nb[2][k] * z1 + nb[3][k];
-            ss += e[k] * e[k];
-        }
-        double sc = 1. / sqrt(ss);
-        for (int k = 0; k < 9; ++k) Eout[9 * count + k] = e[k] * sc;
+        double x = xy1[0] / xy1[2], y = xy1[1] / xy1[2], e[9];
+        for (int k = 0; k < 9; ++k) e[k] = ((nb[0][k] * x + nb[1][k] * y) + 0.0 + nb[2][k] * z1) + nb[3][k];
+        double sc = 1. / sqrt(norm_l2sqr9(e));
+        for (int k = 0; k < 9; ++k) Eout[9 * count + k] = e[k] * sc + 0.0;
         ++count;
     }
     return count;
@@ -503,7 +549,8 @@ int orc_e_hypothesis(const double* pts4, int N, uint64_t seed, int64_t hyp, doub
             x1[i] = p[0]; y1[i] = p[1]; x2[i] = p[2]; y2[i] = p[3];
         }
         if (idx_out) memcpy(idx_out, idx, sizeof(idx));
-        return orc_e_solve5(x1, y1, x2, y2, E90);
+        /* default: the reference's own solver; MCV_FLAG_FAST_MINIMAL: the Illinois replacement */
+        return orc_get_fast_minimal() ? orc_e_solve5(x1, y1, x2, y2, E90) : orc_e_solve5_ref(x1, y1, x2, y2, E90);
     }
     return ORC_NO_SAMPLE;
 }
@@ -576,7 +623,7 @@ int orc_find_essential(const double* a, const double* b, int N, double focal, do
     if (N == 5) {
         double x1[5], y1[5], x2[5], y2[5], Es[EMAX * 9];
         for (int i = 0; i < 5; ++i) { x1[i] = pts[4 * i]; y1[i] = pts[4 * i + 1]; x2[i] = pts[4 * i + 2]; y2[i] = pts[4 * i + 3]; }
-        int n = orc_e_solve5(x1, y1, x2, y2, Es);
+        int n = orc_e_solve5_ref(x1, y1, x2, y2, Es);   /* count == modelPoints: runKernel once */
         if (n == 1) {
             memcpy(E, Es, sizeof(double) * 9);
             if (mask) memset(mask, 1, 5);
@@ -588,6 +635,8 @@ int orc_find_essential(const double* a, const double* b, int N, double focal, do
     int64_t niters = maxIters > 1 ? maxIters : 1;
     int* cnt = (int*)malloc(sizeof(int) * EMAX * (size_t)niters);
     int* cvt = orc_cv_begin(flags, 0, NULL, N, 5, niters);
+    const int fast0 = orc_get_fast_minimal();
+    if (flags & ORC_FLAG_FAST_MINIMAL) orc_set_fast_minimal(1);
     orc_e_counts(pts, N, seed, 0, niters, thr2, kind, cnt, nthreads);
     int bc = 0;
     int64_t best = orc_ransac_replay_slots(cnt, niters, EMAX, N, 5, conf, maxIters, (flags & ORC_FLAG_FIXED_ITERS) != 0, &bc);
@@ -602,6 +651,7 @@ int orc_find_essential(const double* a, const double* b, int N, double focal, do
         }
     }
     orc_cv_end(cvt);
+    orc_set_fast_minimal(fast0);
     free(pts);
     return result;
 }

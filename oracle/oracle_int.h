@@ -12,6 +12,9 @@
 #define ORC_FLAG_NO_REFINE 2
 #define ORC_FLAG_FUSED_ERROR 64   /* MCV_FLAG_FUSED_ERROR (bit 4 is retired) */
 #define ORC_FLAG_CV_SAMPLER 32    /* MCV_FLAG_CV_SAMPLER */
+#define ORC_FLAG_FAST_MINIMAL 16  /* MCV_FLAG_FAST_MINIMAL: the non-reference minimal solvers */
+int orc_get_fast_minimal(void);
+void orc_set_fast_minimal(int v);
 
 /* Per-hypothesis word stream: word s = philox({s/4, hyp_lo, hyp_hi, "MCV1"}, {seed_lo, seed_hi})[s%4] */
 typedef struct { uint64_t seed, hyp; uint64_t pos; uint32_t buf[4]; } Stream;

@@ -17,6 +17,8 @@ _SIGS = {
     "orc_philox": (None, [_P, _P, _P]),
     "orc_set_fast_minimal": (None, [_I]),
     "orc_cv_subsets": (_I64, [_I, _P, _I, _I, _I64, _P]),
+    "orc_fp_coeff_matrix": (None, [_P, _P]),
+    "orc_fp_det_coeffs": (None, [_P, _P]),
     "orc_cv_begin": (_P, [_I, _I, _P, _I, _I, _I64]),
     "orc_cv_end": (None, [_P]),
     "orc_h_hypothesis": (_I, [_P, _I, _U64, _I64, _P, _P, _P]),
@@ -76,7 +78,7 @@ def load() -> C.CDLL:
     global _lib
     if _lib is None:
         srcs = [ORACLE_DIR / n for n in ("oracle.c", "oracle_e.c", "oracle_pnp.c", "oracle_epnp.c", "oracle_f7.c",
-                                          "oracle_scaled.c", "oracle_int.h")]
+                                          "oracle_scaled.c", "oracle_int.h", "fivepoint_terms.inc")]
         if not ORACLE_SO.exists() or ORACLE_SO.stat().st_mtime < max(p.stat().st_mtime for p in srcs):
             subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
         L = C.CDLL(str(ORACLE_SO))

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "hyp_essential.h"
+#include "five_point_ref.h"
 #include "hyp_fundamental.h"
 #include "hyp_homography.h"
 #include "hyp_pnp.h"
@@ -36,6 +37,7 @@ int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const 
 int orc_solve_pnp(const double* img, const double* world, int N, const double* K9, const double* dist4, int kind,
                   double* rvec, double* tvec);
 int orc_e_solve5_ref(const double* x1, const double* y1, const double* x2, const double* y2, double* Eout);
+void orc_set_fast_minimal(int v);
 int orc_find_homography(const double* src, const double* dst, int N, double thr, double conf, int maxIters, int method,
                         uint64_t seed, int flags, double* H, uint8_t* mask, int64_t* bestHypOut, int nthreads);
 int orc_find_fundamental(const double* a, const double* b, int N, double thr, double conf, int maxIters, int method,
@@ -119,8 +121,10 @@ int main() {
             std::memset(E1, 0, sizeof(E1));
             std::memset(E2, 0, sizeof(E2));
             int i1[5], i2[5];
+            orc_set_fast_minimal(1);   // e_hypothesis = the opt-in replacement solver
             const int n1 = mcv::e_hypothesis(pts.data(), N, mcv::Sampler{11, nullptr}, (uint64_t)h, E1, i1);
             const int n2 = orc_e_hypothesis(pts.data(), N, 11, h, E2, i2);
+            orc_set_fast_minimal(0);
             expect(n1 == n2, "e count", n1, n2);
             if (n1 > 0 && n1 == n2) expect(same_bits(&E1[0][0], E2, 9 * n1), "e models", h, N);
             if (h < 6) {   // the cvFivePoint export path on the first five points
@@ -130,8 +134,7 @@ int main() {
                 }
                 std::memset(E1, 0, sizeof(E1));
                 std::memset(E2, 0, sizeof(E2));
-                mcv::E5RefWs ws5;
-                const int r1 = mcv::e_solve5_ref(x1, y1, x2, y2, E1, ws5);
+                const int r1 = mcv::fpr_solve5(x1, y1, x2, y2, E1);
                 const int r2 = orc_e_solve5_ref(x1, y1, x2, y2, E2);
                 expect(r1 == r2, "e ref count", r1, r2);
                 if (r1 > 0 && r1 == r2) expect(same_bits(&E1[0][0], E2, 9 * r1), "e ref models", h, N);

@@ -120,7 +120,7 @@ def test_recover_pose_default_stream(gpu, oracle, n, outl, seed):
     rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=0.999, max_iters=1000, flags=CV)
     np.testing.assert_array_equal(ms, rmask.astype(bool))
     rres, Rr, tr, g = oracle.recover_pose(a, b, Er, rmask, FOCAL, PP)
-    assert res == g
+    assert res == rres
     np.testing.assert_array_equal(Rg, Rr)
     np.testing.assert_array_equal(tg, tr)
     # the Philox stream (seed 0) is a different hypothesis sequence: same geometry, other samples

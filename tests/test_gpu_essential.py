@@ -43,14 +43,15 @@ def test_five_point_exact_geometry(gpu):
     assert min(min(np.abs(e - E).max(), np.abs(e + E).max()) for e in Es) < 1e-8
 
 
-@pytest.mark.parametrize("n,outl,seed,begin,count,unfused", [
-    (5, 0.0, 1, 0, 64, False), (6, 0.3, 2, 0, 100, False), (300, 0.5, 3, 0, 512, False),
-    (2000, 0.5, 4, 123457, 512, False), (1999, 0.6, 5, 0, 256, True), (64, 0.2, 6, 2**28, 300, False),
-    (1000, 0.5, 11, 5, 20000, True),
-    # >= kEStageMinHyps hypotheses per chunk: the split path (matrix phases per 16-lane group, roots
-    # per 4-lane group)
-    (1000, 0.5, 12, 5, 33000, True), (300, 0.5, 8, 77, 50000, False), (5, 0.0, 10, 0, 32768, False)])
-def test_e_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, unfused):
+@pytest.mark.parametrize("n,outl,seed,begin,count,unfused,fast", [
+    (5, 0.0, 1, 0, 64, False, False), (6, 0.3, 2, 0, 100, False, False), (300, 0.5, 3, 0, 512, False, False),
+    (2000, 0.5, 4, 123457, 512, False, False), (1999, 0.6, 5, 0, 256, True, False),
+    (64, 0.2, 6, 2**28, 300, False, False), (1000, 0.5, 11, 5, 20000, True, False),
+    (300, 0.5, 8, 77, 50000, False, False), (5, 0.0, 10, 0, 32768, False, False),
+    # MCV_FLAG_FAST_MINIMAL (the replacement solver); >= kEStageMinHyps hypotheses per chunk take its
+    # split path (matrix phases per 16-lane group, roots per 4-lane group)
+    (300, 0.5, 3, 0, 512, False, True), (1000, 0.5, 12, 5, 33000, True, True), (5, 0.0, 10, 0, 32768, False, True)])
+def test_e_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count, unfused, fast):
     torch, dev = torch_dev
     from minicv_amd import device as D
     a, b, *_ = S.essential_problem(n, seed=seed, outlier_frac=outl)
@@ -59,12 +60,13 @@ def test_e_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count,
     np.testing.assert_array_equal(pts.cpu().numpy(), ref_pts)          # normalisation on the GPU
     plan = D.RansacPlan(N.MODEL_ESSENTIAL, n, count)
     thr = 1.0 / FOCAL                                                  # device API: normalised units
-    cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused).to_c()
+    cfg = opencv.RansacParams(threshold=thr, seed=seed, fused_error=not unfused, fast_minimal=fast).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     counts = torch.zeros(count * N.E_SLOTS, dtype=torch.int32, device=dev)
     plan.evaluate(pts, n, cfg, begin, count, key, counts)
     got = counts.cpu().numpy()
-    ref = oracle.e_counts(ref_pts, seed, begin, count, float(np.float32(thr * thr)), 1 if unfused else 0)
+    with oracle.fast_minimal(fast):
+        ref = oracle.e_counts(ref_pts, seed, begin, count, float(np.float32(thr * thr)), 1 if unfused else 0)
     np.testing.assert_array_equal(got, ref)
     if (ref >= 5).any() and not (ref == -2).any():
         c = ref.max()
@@ -76,12 +78,14 @@ def test_e_slot_counts_bit_exact(torch_dev, oracle, n, outl, seed, begin, count,
 @pytest.mark.parametrize("n,outl,seed,iters,conf,flags", [
     (6, 0.0, 1, 1000, 0.999, 0), (50, 0.3, 2, 1000, 0.999, 0), (500, 0.5, 3, 1000, 0.999, 0),
     (3000, 0.5, 4, 1000, 0.999, 0), (3000, 0.6, 5, 300, 0.999, N.FLAG_FIXED_ITERS),
-    (2000, 0.5, 6, 1000, 0.99, N.FLAG_FUSED_ERROR), (20000, 0.5, 7, 1000, 0.999, 0)])
+    (2000, 0.5, 6, 1000, 0.99, N.FLAG_FUSED_ERROR), (20000, 0.5, 7, 1000, 0.999, 0),
+    (3000, 0.5, 4, 1000, 0.999, N.FLAG_FAST_MINIMAL), (3000, 0.5, 8, 1000, 0.999, N.FLAG_CV_SAMPLER)])
 def test_find_essential_vs_oracle(gpu, oracle, n, outl, seed, iters, conf, flags):
     a, b, inl, R, tu, E = S.essential_problem(n, seed=seed, outlier_frac=outl)
     p = opencv.RansacParams(threshold=1.0, confidence=conf, max_iters=iters, seed=seed,
                             fixed_iters=bool(flags & N.FLAG_FIXED_ITERS),
-                            fused_error=bool(flags & N.FLAG_FUSED_ERROR))
+                            fused_error=bool(flags & N.FLAG_FUSED_ERROR),
+                            fast_minimal=bool(flags & N.FLAG_FAST_MINIMAL), cv_sampler=bool(flags & N.FLAG_CV_SAMPLER))
     cnt, Eg, mask = opencv.findEssentialMat(a, b, FOCAL, PP, p)
     rc, Er, rmask, best = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=conf, max_iters=iters, seed=seed,
                                                 flags=flags)
