@@ -107,7 +107,8 @@ MCV_API int  cvFivePoint(const mcvV2d* pa, const mcvV2d* pb, mcvM33d* Es);
  * final pose on the inliers: LM from the RANSAC pose (kind 0), EPnP (every other kind).
  * outInliers (caller: N ints) = RANSAC inlier indices.
  * cvSolvePnP: kinds 2 / 5 need N == 4 (AP3P, the 4th point picks the solution); 1 / 3 / 4:
- * EPnP on all points; 0 / 6 (ITERATIVE / SQPNP) and others: EPnP, then LM over all points. */
+ * EPnP on all points; 0 (ITERATIVE) and values outside 0..6: EPnP, then LM over all points;
+ * 6 (SQPNP) fails (false, mcvGetLastError says so): SQPnP's estimator is not provided. */
 MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                         const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec);
 MCV_API mcvBool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,

@@ -82,6 +82,7 @@ struct Plan {
     PinnedBuf<float> h_pack;
     PinnedBuf<uint8_t> h_one;
     PinnedBuf<int> h_i;
+    PinnedBuf<uint64_t> h_keys;   // per-shard best key + first failure (fixed-iteration searches)
 
     void reserve(int n, int64_t hyps);
     hipStream_t own_stream();

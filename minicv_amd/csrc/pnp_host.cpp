@@ -487,6 +487,11 @@ extern "C" MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* wor
         if (N < 4) fail("cvSolvePnP: need at least 4 correspondences (N=%d)", N);
         // solverKind as MiniCVNative.cpp:54-75 maps it (6 = SQPNP, unknown = ITERATIVE)
         const int kind = solverKind >= 0 && solverKind <= 6 ? solverKind : 0;
+        if (kind == 6)
+            // SOLVEPNP_SQPNP (MiniCVNative.cpp:72-74) is a different estimator (the global minimum of the
+            // object-space error by SQP over the null space of Omega); it is not restated here, and this
+            // export fails rather than answer with another estimator's pose
+            fail("cvSolvePnP: solverKind 6 (SOLVEPNP_SQPNP) is not provided by this library");
         const bool p3p = kind == 2 || kind == 5;
         if (p3p && N != 4) fail("cvSolvePnP: P3P / AP3P need exactly 4 points (N=%d)", N);
         require_device();
@@ -497,8 +502,8 @@ extern "C" MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* wor
             r = pnp_ransac(P, imgPoints, worldPoints, N, K.M, distortionCoeffs, pnp_config(1, 1.f, 0.99, kind), s);
         } else {
             // EPnP on all points in double (solvePnPGeneric keeps the caller's CV_64F points);
-            // ITERATIVE / SQPNP: then LM over all points from that pose (the reference's DLT or
-            // homography initialisation and SQPnP's global search are not restated)
+            // ITERATIVE: then LM over all points from that pose (the reference's DLT or homography
+            // initialisation is not restated: DESIGN.md §3)
             set_camera(P, K.M, distortionCoeffs);
             P.reserve(N, 1);
             pnp_pack(P, imgPoints, worldPoints, N, P.ptsd.p, s);
@@ -511,7 +516,7 @@ extern "C" MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* wor
             rodrigues_inv(R9, r.r);
             r.ok = std::isfinite(r.r[0]) && std::isfinite(r.r[1]) && std::isfinite(r.r[2]) && std::isfinite(r.t[0]) &&
                    std::isfinite(r.t[1]) && std::isfinite(r.t[2]);
-            if (r.ok && (kind == 0 || kind == 6)) pnp_lm(P, P.ptsd.p, N, nullptr, r.r, r.t, 20, s);
+            if (r.ok && kind == 0) pnp_lm(P, P.ptsd.p, N, nullptr, r.r, r.t, 20, s);
         }
         if (!r.ok) {
             set_last_error("cvSolvePnP: no pose");

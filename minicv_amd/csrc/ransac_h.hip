@@ -703,8 +703,10 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
     int nev = 0;
+    // an event records the trip index (base / TRIP: < 2^24 for any N < 2^31, pairs = N / 2) and the
+    // undecided-model mask in its low 8 bits
+    constexpr int TRIP = 64 * NP;
     if (fast) {
-        constexpr int TRIP = 64 * NP;
         const int nFull = nComplete / TRIP * TRIP;
         uint64_t all[NP];
 #pragma unroll
@@ -721,7 +723,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
                     h_cert_fix<K, NP, false>(und, models, h0, hypCount, offsets[wib], slopes.a, q, all, all, thr2,
                                              one, cnt);
                 } else {
-                    if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)base << 8) | und;
+                    if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)(base / TRIP) << 8) | und;
                     ++nev;
                 }
             }
@@ -738,7 +740,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
             }
             const uint32_t und = h_cert_trip<K, NP, true>(hp, hc, slopes.a, cb, q, vx, vy, one, cnt);
             if (und != 0) {
-                if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)base << 8) | und;
+                if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)(base / TRIP) << 8) | und;
                 ++nev;
             }
         }
@@ -748,7 +750,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
             __builtin_amdgcn_wave_barrier();
             for (int e = 0; e < nev; ++e) {
                 const uint32_t ev = __builtin_amdgcn_readfirstlane(events[wib][e]);
-                const int base = (int)(ev >> 8);
+                const int base = (int)(ev >> 8) * TRIP;
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     if (!(ev & (1u << k))) continue;

@@ -506,13 +506,21 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
         MCV_HIP(hipSetDevice(home));
     }
     int64_t begin = 0;
-    int64_t chunk = std::min<int64_t>(std::max<int64_t>(st.niters, 1), kChunkFirst);
+    // adaptive calls start small (niters shrinks with the first good model); a fixed budget is
+    // evaluated in chunks of kChunkMax from the start
+    int64_t chunk = std::min<int64_t>(std::max<int64_t>(st.niters, 1), fixed ? kChunkMax : kChunkFirst);
+    P.h_keys.ensure(2 * kMaxShards);
     while (!st.stopped) {
         const int64_t remaining = st.niters - begin;
         if (remaining <= 0) break;
         const int cnt = (int)std::min<int64_t>(remaining, chunk);
         P.reserve(N, cnt * slotScale);
         const int nsh = std::min<int>((int)sh.size(), cnt);
+        // fixed iterations: the sequential replay's answer is the first maximum over the counts >= m
+        // before the first sampler failure, so each shard reduces its range on its own device to the
+        // packed key (count << 32 | ~slot) + its first failure and sends 16 B; only a chunk with a
+        // sampler failure (degenerate data) falls back to gathering the counts. Adaptive calls gather
+        // the counts (4 B per model slot) and replay them in order.
         int64_t off = 0;
         for (int k = 0; k < nsh; ++k) {
             const int ck = (int)(cnt / nsh + (k < cnt % nsh ? 1 : 0));
@@ -521,18 +529,49 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
                 MCV_HIP(hipSetDevice(x.dev));
                 x.P->reserve(N, ck * slotScale);
             }
-            evaluate_chunk(*x.P, x.pts, N, cfg, begin + off, ck, x.P->counts.p, nullptr, x.s);
-            MCV_HIP(hipMemcpyAsync(P.h_counts.p + off * slots, x.P->counts.p, (size_t)ck * slots * sizeof(int),
-                                   hipMemcpyDeviceToHost, x.s));
+            evaluate_chunk(*x.P, x.pts, N, cfg, begin + off, ck, x.P->counts.p, fixed ? x.P->key.p : nullptr, x.s);
+            if (fixed)
+                MCV_HIP(hipMemcpyAsync(P.h_keys.p + 2 * k, x.P->key.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                       x.s));
+            else
+                MCV_HIP(hipMemcpyAsync(P.h_counts.p + off * slots, x.P->counts.p, (size_t)ck * slots * sizeof(int),
+                                       hipMemcpyDeviceToHost, x.s));
             off += ck;
         }
         for (int k = 0; k < nsh; ++k) {
             if (k > 0) MCV_HIP(hipSetDevice(sh[k].dev));
             MCV_HIP(hipStreamSynchronize(sh[k].s));
         }
+        bool replayed = false;
+        if (fixed) {
+            uint64_t best = 0;
+            bool failed = false;
+            for (int k = 0; k < nsh; ++k) {
+                best = std::max(best, P.h_keys.p[2 * k]);
+                failed = failed || (int64_t)P.h_keys.p[2 * k + 1] != INT64_MAX;
+            }
+            if (!failed) {
+                const int c = (int)(best >> 32);
+                if (best != 0 && c > std::max(st.bestCount, m - 1)) {
+                    st.bestCount = c;
+                    st.bestIndex = (int64_t)(0xFFFFFFFFull - (best & 0xFFFFFFFFull));
+                }
+                replayed = true;
+            } else {   // a sampler failure inside the chunk: the counts, in order
+                off = 0;
+                for (int k = 0; k < nsh; ++k) {
+                    const int ck = (int)(cnt / nsh + (k < cnt % nsh ? 1 : 0));
+                    if (k > 0) MCV_HIP(hipSetDevice(sh[k].dev));
+                    MCV_HIP(hipMemcpy(P.h_counts.p + off * slots, sh[k].P->counts.p, (size_t)ck * slots * sizeof(int),
+                                      hipMemcpyDeviceToHost));
+                    off += ck;
+                }
+            }
+        }
         if (nsh > 1) MCV_HIP(hipSetDevice(home));
-        replay_chunk(&st, P.h_counts.p, begin, cnt, slots, N, m, cfg.confidence, fixed ? 1 : 0);
+        if (!replayed) replay_chunk(&st, P.h_counts.p, begin, cnt, slots, N, m, cfg.confidence, fixed ? 1 : 0);
         begin += cnt;
+        if (begin >= st.niters) st.stopped = 1;
         chunk = std::min<int64_t>(chunk * 2, kChunkMax);
     }
     return st.bestIndex;

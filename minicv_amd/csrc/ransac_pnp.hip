@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void mcv_pnp_extent(const PnpPoint* __restrict
 
 // Exact inlier count of one pose over the 128 points [base, base + 128) n [p0, p1) (two per lane):
 // the reference's fp64 projection + fp32 error (pnp_error). The prefilter's undecided trips.
-__device__ __noinline__ uint32_t pnp_exact_trip(const PnpPoint* __restrict__ pts, int base, int p0, int p1,
+__device__ __forceinline__ uint32_t pnp_exact_trip(const PnpPoint* __restrict__ pts, int base, int p0, int p1,
                                                 PnpCamera cam, const PnpPose* __restrict__ models, int hk,
                                                 float thr2, bool fused) {
     const int lane = threadIdx.x & 63;
@@ -260,25 +260,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             ++nev;
         }
     }
-    if (nev > kPnpEvents) {
-        // too many undecided trips (a pose outside the bound's domain): exact recount of the chunk
-#pragma unroll 1
-        for (int k = 0; k < K; ++k) {
-            if (!valid[k]) continue;
-            uint32_t c = 0;
-            for (int base = p0; base < p1; base += 128) c += pnp_exact_trip(pts, base, p0, p1, cam, models, h0 + k, thr2, fused);
+    // exact recount of the logged (trip, pose) events; too many undecided trips (a pose outside the
+    // bound's domain) recount every trip of the chunk for every pose. One inlined copy of the fp64 trip
+    // serves both (a called function would put its frame and the caller's saved registers in scratch).
+    const bool overflow = nev > kPnpEvents;
+    if (overflow) {
 #pragma unroll
-            for (int kk = 0; kk < K; ++kk) cnt[kk] = kk == k ? c : cnt[kk];
-        }
-    } else if (nev > 0) {
+        for (int k = 0; k < K; ++k) cnt[k] = 0;
+    }
+    const int nres = overflow ? (p1 - p0 + 127) / 128 : nev;
+    if (nres > 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        for (int e = 0; e < nev; ++e) {
-            const uint32_t ev = __builtin_amdgcn_readfirstlane(events[wib][e]);
-            const int base = p0 + (int)(ev >> 8) * 128;
+    }
+    for (int e = 0; e < nres; ++e) {
+        const uint32_t ev = overflow ? (((uint32_t)e << 8) | validMask)
+                                     : (uint32_t)__builtin_amdgcn_readfirstlane(events[wib][e]);
+        const int base = p0 + (int)(ev >> 8) * 128;
+        uint32_t m = ev & 0xFFu;
+        while (m != 0) {   // wave-uniform
+            const int k = __builtin_ctz(m);
+            m &= m - 1;
+            const uint32_t c = pnp_exact_trip(pts, base, p0, p1, cam, models, h0 + k, thr2, fused);
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (ev & (1u << k)) cnt[k] += pnp_exact_trip(pts, base, p0, p1, cam, models, h0 + k, thr2, fused);
+            for (int kk = 0; kk < K; ++kk) cnt[kk] += kk == k ? c : 0u;
         }
     }
     if (lane == 0) {

@@ -171,6 +171,9 @@ def test_n4_and_solve_pnp(gpu, oracle):
     ok4, r4, t4 = oracle.solve_pnp(img, W, K, d, kind=0)
     np.testing.assert_allclose(r3, r4, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(t3, t4, rtol=1e-6, atol=1e-9)
+    # kind 6 (SOLVEPNP_SQPNP) is not provided: an explicit failure, not another estimator's pose
+    with pytest.raises(N.NativeError, match="SQPNP"):
+        opencv.solvePnP(img, W, K, d, kind="SQPNP")
 
 
 @pytest.mark.parametrize("n,kind", [(6, "EPNP"), (500, "EPNP"), (3000, "UPNP"), (20000, "DLS"), (4, "EPNP")])
