@@ -427,13 +427,17 @@ MCV_API int mcvHostRealRoots(const double* c, int deg, int fixed, double* roots)
  * p1, p2), and the Rodrigues maps used by the LM refit. */
 MCV_API int mcvHostPnP(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9, double* t3,
                        int* idx4);
+/* mcvHostPnP with the opt-in real-root-finder AP3P quartic (MCV_FLAG_FAST_MINIMAL). */
+MCV_API int mcvHostPnPFast(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9,
+                           double* t3, int* idx4);
 /* EPnP twins: a 5-point EPnP hypothesis (idx5: the sample), and epnp_solve_small<5> on given world
  * points pw15 (5 x 3) and pixel observations us10 (5 x 2), cam4 = fu, fv, uc, vc. */
 MCV_API int mcvHostPnPEpnp(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9,
                            double* t3, int* idx5);
 MCV_API void mcvHostEpnp5(const double* pw15, const double* us10, const double* cam4, double* R9, double* t3);
 /* Device self-test: the PnP generate kernel's poses for hypotheses [hypBegin, hypBegin + hypCount) on
- * host PnpPoint[N] (kind: solverKind, EPnP kernel unless 2 / 5). poses12[h] = {R (9), t (3)},
+ * host PnpPoint[N] (kind: solverKind, EPnP kernel unless 2 / 5; | MCV_HOST_FAST_MINIMAL: the opt-in
+ * real-root-finder AP3P quartic). poses12[h] = {R (9), t (3)},
  * status[h] = 1 or -1 / -2. Returns hypCount, -1 on failure. */
 MCV_API int mcvTestPnpHypotheses(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hypBegin,
                                  int hypCount, int kind, double* poses12, int* status);

@@ -6,11 +6,12 @@
 // Restated behaviour:
 //  * AP3P (Ke & Roumeliotis, CVPR 2017) exactly as the reference's computePoses
 //    (ap3p.cpp:123-255): bearing vectors, the f1i / f2i / g1..g7 terms, the quartic in
-//    cos(theta1'), C13, R = Ck1nl C13 Cb1k3tz^T, t = sin(theta1') b3' - R^T w3. The quartic's real
-//    roots come from e_poly_real_roots (derivative-interval bisection, hyp_essential.h) instead
-//    of solveQuartic's complex Ferrari formulas + polishQuarticRoots (ap3p.cpp:10-74): those use
-//    complex sqrt / cbrt / pow, whose last bits differ between libm and the GPU's ocml, and they
-//    return the real parts of complex roots as spurious candidates.
+//    cos(theta1'), C13, R = Ck1nl C13 Cb1k3tz^T, t = sin(theta1') b3' - R^T w3. The quartic by the
+//    reference's own solveQuartic (Ferrari through complex arithmetic) + polishQuarticRoots
+//    (ap3p.cpp:10-77), real parts of complex roots kept as candidates — the RANSAC default; its
+//    transcendentals are the device's (ocml) on the GPU and glibc's on the host, so a root can
+//    differ in its last bits between the two. MCV_FLAG_FAST_MINIMAL: the real roots
+//    from e_poly_real_roots (derivative-interval bisection, bit-identical host / GPU).
 //  * Camera-from-world rotation of a solution is R^T (OpenCV's ap3p stores the transpose;
 //    the reference's solveAp3p export returns R itself, ap3p.cpp:245-250 — kept for that export).
 //  * OpenCV 4.x solvePnPRansac / PnPRansacCallback [ext]: 4-point minimal sets for P3P / AP3P
@@ -344,6 +345,38 @@ MCV_HD int ap3p_compute_poses_ref(const double (*b)[3], const double (*w)[3], do
     return n;
 }
 
+// computePoses with the reference's own quartic path (solveQuartic + polishQuarticRoots, ap3p.cpp:203-204):
+// the four polished Ferrari roots in order, |cos| > 1 skipped (a NaN root is not: as in the reference,
+// it yields a NaN pose, which counts no inliers), poses appended through selects (register-resident).
+// The RANSAC kernel's default; its transcendentals (cbrt, log, atan2, exp, cos, hypot) are the device's
+// own on the GPU and glibc's on the host.
+MCV_HD int ap3p_compute_poses_ferrari(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3]) {
+    Ap3pSetup S;
+    ap3p_setup(b, w, S);
+    const double f[5] = {S.c[4], S.c[3], S.c[2], S.c[1], S.c[0]};
+    double s[4];
+    ap3p_solve_quartic(f, s);
+    ap3p_polish(f, s);
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const double ct1 = s[i];
+        if (fabs(ct1) > 1) continue;
+        double R[9], tv[3];
+        (void)ap3p_pose(S, ct1, R, tv);
+#pragma unroll
+        for (int slot = 0; slot < kPnpMaxSolutions; ++slot) {
+            const bool wr = slot == n;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Rr[slot][k] = wr ? R[k] : Rr[slot][k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) tr[slot][k] = wr ? tv[k] : tr[slot][k];
+        }
+        ++n;
+    }
+    return n;
+}
+
 // Bearing vector of a normalised image point (x, y): (x, y, 1) / |(x, y, 1)| as the reference
 // builds it (ap3p.cpp:285-301: mk = 1 / norm, then mu *= mk, mv *= mk).
 MCV_HD void pnp_bearing(double x, double y, double* b) {
@@ -397,10 +430,67 @@ MCV_HD int pnp_ap3p4(const PnpCamera& c, const double* x, const double* y, const
 // fp32 as solvePnPRansac's convertTo(CV_32F).
 struct PnpPoint { float X, Y, Z, u, v, pad0, pad1, pad2; };
 
-// One hypothesis: 4 distinct indices (Philox stream), undistort, AP3P + 4th-point selection.
+// OpenCV 4.x's AP3P minimal solve as PnPRansacCallback runs it on a 4-point subset [ext: calib3d
+// solvePnP -> solveP3P -> ap3p::solve(Rs, ts, opoints, undistortedPoints)]: undistortPoints writes the
+// normalised points into a CV_32F result (xf = (float)x), extract_points maps them back to pixels
+// (mu = xf fx + cx in double), ap3p::solve normalises again (inv_fx mu - cx_fx, inv_fx = 1 / fx,
+// cx_fx = cx / fx) and builds the bearings (ap3p.cpp:285-301's form), computePoses with the Ferrari
+// quartic, and the fourth point picks the solution of least pixel reprojection error
+// ((cx + fx X3p / Z3p - mu3)^2 + ..., first minimum). Returns 1 and the camera-from-world pose, or 0.
+MCV_HD int pnp_ap3p4_cv(const PnpCamera& c, const double* x, const double* y, const double (*W)[3], PnpPose& pose) {
+    const double inv_fx = 1. / c.fx, inv_fy = 1. / c.fy, cx_fx = c.cx / c.fx, cy_fy = c.cy / c.fy;
+    double mu[4], mv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        mu[i] = (double)(float)x[i] * c.fx + c.cx;
+        mv[i] = (double)(float)y[i] * c.fy + c.cy;
+    }
+    double b[3][3], w[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        pnp_bearing(inv_fx * mu[i] - cx_fx, inv_fy * mv[i] - cy_fy, b[i]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) w[i][k] = W[i][k];
+    }
+    double Rr[kPnpMaxSolutions][9], tr[kPnpMaxSolutions][3];
+#pragma unroll
+    for (int i = 0; i < kPnpMaxSolutions; ++i) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Rr[i][k] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) tr[i][k] = 0.0;
+    }
+    const int n = ap3p_compute_poses_ferrari(b, w, Rr, tr);
+    if (n == 0) return 0;
+    double bestErr = 0, bR[9], bt[3];
+#pragma unroll
+    for (int i = 0; i < kPnpMaxSolutions; ++i) {
+        if (i >= n) break;
+        const double* R = Rr[i];   // camera-from-world rotation = Rr^T
+        const double X = R[0] * W[3][0] + R[3] * W[3][1] + R[6] * W[3][2] + tr[i][0];
+        const double Y = R[1] * W[3][0] + R[4] * W[3][1] + R[7] * W[3][2] + tr[i][1];
+        const double Z = R[2] * W[3][0] + R[5] * W[3][1] + R[8] * W[3][2] + tr[i][2];
+        const double mu3p = c.cx + c.fx * X / Z;
+        const double mv3p = c.cy + c.fy * Y / Z;
+        const double e = (mu3p - mu[3]) * (mu3p - mu[3]) + (mv3p - mv[3]) * (mv3p - mv[3]);
+        const bool take = i == 0 || bestErr > e;   // first minimum
+        bestErr = take ? e : bestErr;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) bR[k] = take ? R[k] : bR[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) bt[k] = take ? tr[i][k] : bt[k];
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q) pose.R[3 * r + q] = bR[3 * q + r];
+    for (int k = 0; k < 3; ++k) pose.t[k] = bt[k];
+    return 1;
+}
+
+// One hypothesis: 4 distinct indices, undistort, AP3P + 4th-point selection: OpenCV's chain
+// (pnp_ap3p4_cv, default) or, with fast (MCV_FLAG_FAST_MINIMAL), the real-root-finder form (pnp_ap3p4).
 // Returns 1 (model), kStatusNoModel or kStatusNoSample.
 MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
-                          PnpPose& pose, int* idx_out) {
+                          PnpPose& pose, int* idx_out, bool fast = false) {
     SubsetSrc<4> src(smp, hyp);
     int idx[4];
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
@@ -414,7 +504,7 @@ MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, const 
             W[i][0] = p.X; W[i][1] = p.Y; W[i][2] = p.Z;
         }
         if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
-        return pnp_ap3p4(c, x, y, W, pose) ? 1 : kStatusNoModel;
+        return (fast ? pnp_ap3p4(c, x, y, W, pose) : pnp_ap3p4_cv(c, x, y, W, pose)) ? 1 : kStatusNoModel;
     }
     return kStatusNoSample;
 }

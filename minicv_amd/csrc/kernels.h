@@ -134,14 +134,15 @@ struct Ap3pOut {
     int count;
 };
 void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_pts, hipStream_t s);
+// fast (MCV_FLAG_FAST_MINIMAL): the AP3P kernel's real-root-finder quartic instead of the reference's Ferrari
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
-                         bool epnp, void* d_models, int* d_counts, hipStream_t s);
+                         bool epnp, void* d_models, int* d_counts, hipStream_t s, bool fast = false);
 // d_ext: 3 doubles of device scratch filled by launch_pnp_extent (the certified sweep's bound).
 void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s);
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
                        float thr2, bool fused, const double* d_ext, hipStream_t s);
 void launch_pnp_one(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hyp, bool epnp,
-                    PnpOneOut* d_out, hipStream_t s);
+                    PnpOneOut* d_out, hipStream_t s, bool fast = false);
 void launch_pnp_solve5(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s);
 void launch_mask_compact(const uint8_t* d_mask, int N, int* d_idx, int* d_count, hipStream_t s);
 // EPnP over n points: d_pts (+ optional index list d_idx) fp32 PnpPoints, or d_img / d_world fp64.
@@ -160,7 +161,7 @@ struct EpnpPassArgs {
 };
 void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, const EpnpPassArgs& a, int nacc,
                       double* d_part, hipStream_t s);
-void launch_pnp_solve4(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s);
+void launch_pnp_solve4(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s, bool fast = false);
 void launch_pnp_mask(const void* d_pts, int N, const double* cam8, const double* R9, const double* t3, float thr2,
                      bool fused, uint8_t* d_mask, int* d_count, hipStream_t s);
 void launch_pnp_ap3p(const Ap3pIn& in, Ap3pOut* d_out, hipStream_t s);

@@ -115,6 +115,8 @@ static void pnp_pack(Plan& P, const mcvV2d* img, const mcvV3d* world, int N, voi
 }
 
 static bool fused_pnp(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_ERROR) != 0; }
+// MCV_FLAG_FAST_MINIMAL: AP3P hypotheses from the real-root finder instead of the reference's Ferrari quartic
+static bool fast_ap3p(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0; }
 bool pnp_cfg_epnp(const RansacConfig& cfg) { return pnp_kind_epnp(pnp_kind(cfg.pnpKind)); }
 
 void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
@@ -122,8 +124,8 @@ void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
     const float thr2 = (float)(cfg.threshold * cfg.threshold);
     const bool epnp = pnp_cfg_epnp(cfg);
     const Sampler smp = P.sampler(cfg);
-    launch_pnp_generate(d_pts, N, P.pnpCam, smp, hypBegin, hypCount, epnp, P.models.p, d_counts, s);
-    P.last.set(hypBegin, hypCount, smp, d_pts, N, epnp ? 1 : 0);
+    launch_pnp_generate(d_pts, N, P.pnpCam, smp, hypBegin, hypCount, epnp, P.models.p, d_counts, s, fast_ap3p(cfg));
+    P.last.set(hypBegin, hypCount, smp, d_pts, N, epnp ? 1 : (fast_ap3p(cfg) ? 2 : 0));
     P.bb4.ensure(4);
     launch_pnp_extent(d_pts, N, P.bb4.p, s);
     ProfScope ps("pnp_verify", s);
@@ -340,7 +342,7 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
     PnpOneOut one;
     const bool epnp = pnp_cfg_epnp(cfg);
     const Sampler smp = P.sampler(cfg);
-    if (P.last.covers(hyp, smp, d_pts, N, epnp ? 1 : 0)) {
+    if (P.last.covers(hyp, smp, d_pts, N, epnp ? 1 : (fast_ap3p(cfg) ? 2 : 0))) {
         // the winner's pose straight from the last chunk's model buffer (the same code produced it)
         // instead of a single-lane re-solve
         const PnpPose* d_m = (const PnpPose*)P.models.p + (hyp - P.last.begin);
@@ -352,7 +354,7 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
         std::memcpy(one.t, pose.t, sizeof(one.t));
         one.status = 1;
     } else {
-        launch_pnp_one(d_pts, N, P.pnpCam, smp, hyp, epnp, (PnpOneOut*)P.one.p, s);
+        launch_pnp_one(d_pts, N, P.pnpCam, smp, hyp, epnp, (PnpOneOut*)P.one.p, s, fast_ap3p(cfg));
         MCV_HIP(hipGetLastError());
         one = pnp_fetch_one(P, s);
     }
@@ -389,7 +391,7 @@ static PnpResult pnp_ransac(Plan& P, const mcvV2d* img, const mcvV3d* world, int
     const bool epnp = pnp_cfg_epnp(cfg);
     if (N == 4 || (epnp && N == 5)) {
         // npoints == model_points: one solvePnP on all points (P3P for 4, here AP3P; EPnP for 5)
-        if (N == 4) launch_pnp_solve4(P.ptsd.p, P.pnpCam, (PnpOneOut*)P.one.p, s);
+        if (N == 4) launch_pnp_solve4(P.ptsd.p, P.pnpCam, (PnpOneOut*)P.one.p, s, fast_ap3p(cfg));
         else launch_pnp_solve5(P.ptsd.p, P.pnpCam, (PnpOneOut*)P.one.p, s);
         MCV_HIP(hipGetLastError());
         const PnpOneOut one = pnp_fetch_one(P, s);
@@ -647,19 +649,27 @@ extern "C" MCV_API int mcvRansacPlanSetCamera(mcvRansacPlan* plan, const double*
 extern "C" MCV_API void mcvHostRodrigues(const double* r, double* R, double* dR27) { rodrigues(r, R, dR27); }
 extern "C" MCV_API void mcvHostRodriguesInv(const double* R, double* r) { rodrigues_inv(R, r); }
 
+static int host_pnp(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9, double* t3,
+                    int* idx4, bool fast) {
+    if (!pts || !cam8 || !R9 || !t3 || N < 4) fail("mcvHostPnP: bad argument");
+    PnpCamera c{cam8[0], cam8[1], cam8[2], cam8[3], cam8[4], cam8[5], cam8[6], cam8[7]};
+    PnpPose p;
+    for (int k = 0; k < 9; ++k) p.R[k] = 0;
+    for (int k = 0; k < 3; ++k) p.t[k] = 0;
+    const int st = pnp_hypothesis((const PnpPoint*)pts, N, c, Sampler{seed, nullptr}, (uint64_t)hyp, p, idx4, fast);
+    for (int k = 0; k < 9; ++k) R9[k] = p.R[k];
+    for (int k = 0; k < 3; ++k) t3[k] = p.t[k];
+    return st;
+}
+
 extern "C" MCV_API int mcvHostPnP(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R9,
                                   double* t3, int* idx4) {
-    MCV_GUARD(kStatusNoSample - 1, {
-        if (!pts || !cam8 || !R9 || !t3 || N < 4) fail("mcvHostPnP: bad argument");
-        PnpCamera c{cam8[0], cam8[1], cam8[2], cam8[3], cam8[4], cam8[5], cam8[6], cam8[7]};
-        PnpPose p;
-        for (int k = 0; k < 9; ++k) p.R[k] = 0;
-        for (int k = 0; k < 3; ++k) p.t[k] = 0;
-        const int st = pnp_hypothesis((const PnpPoint*)pts, N, c, Sampler{seed, nullptr}, (uint64_t)hyp, p, idx4);
-        for (int k = 0; k < 9; ++k) R9[k] = p.R[k];
-        for (int k = 0; k < 3; ++k) t3[k] = p.t[k];
-        return st;
-    })
+    MCV_GUARD(kStatusNoSample - 1, { return host_pnp(pts, N, cam8, seed, hyp, R9, t3, idx4, false); })
+}
+
+extern "C" MCV_API int mcvHostPnPFast(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp,
+                                      double* R9, double* t3, int* idx4) {
+    MCV_GUARD(kStatusNoSample - 1, { return host_pnp(pts, N, cam8, seed, hyp, R9, t3, idx4, true); })
 }
 
 extern "C" MCV_API int mcvHostPnPEpnp(const void* pts, int N, const double* cam8, uint64_t seed, int64_t hyp,
@@ -706,9 +716,10 @@ extern "C" MCV_API int mcvTestPnpHypotheses(const float* pts, int N, const doubl
         P.reserve(N, hypCount);
         for (int k = 0; k < 8; ++k) P.pnpCam[k] = cam8[k];
         MCV_HIP(hipMemcpyAsync(P.ptsd.p, pts, (size_t)N * sizeof(PnpPoint), hipMemcpyHostToDevice, s));
+        const bool fast = (kind & MCV_HOST_FAST_MINIMAL) != 0;
+        kind &= ~MCV_HOST_FAST_MINIMAL;
         launch_pnp_generate(P.ptsd.p, N, P.pnpCam, Sampler{seed, nullptr}, hypBegin, hypCount,
-                            pnp_kind_epnp(pnp_kind(kind)), P.models.p,
-                            P.counts.p, s);
+                            pnp_kind_epnp(pnp_kind(kind)), P.models.p, P.counts.p, s, fast);
         MCV_HIP(hipGetLastError());
         std::vector<PnpPose> m((size_t)hypCount);
         MCV_HIP(hipMemcpyAsync(m.data(), P.models.p, m.size() * sizeof(PnpPose), hipMemcpyDeviceToHost, s));

@@ -45,7 +45,8 @@ static constexpr int kEpnpWsStride = 145;   // doubles per lane (12 x 12 + 1: ba
 template <bool EPNP>
 __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
                                                        Sampler smp, int64_t hypBegin, int hypCount,
-                                                       PnpPose* __restrict__ models, int* __restrict__ counts) {
+                                                       PnpPose* __restrict__ models, int* __restrict__ counts,
+                                                       bool fast) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     PnpPose p;
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restric
         EpnpWs& A = *reinterpret_cast<EpnpWs*>(ws + (size_t)threadIdx.x * kEpnpWsStride);
         st = pnp_hypothesis_epnp(pts, N, cam, smp, (uint64_t)(hypBegin + i), p, nullptr, A);
     } else {
-        st = pnp_hypothesis(pts, N, cam, smp, (uint64_t)(hypBegin + i), p, nullptr);
+        st = pnp_hypothesis(pts, N, cam, smp, (uint64_t)(hypBegin + i), p, nullptr, fast);
     }
     if (st == 1) {
         models[i] = p;
@@ -294,14 +295,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 __global__ void mcv_pnp_one(const PnpPoint* __restrict__ pts, int N, PnpCamera cam, Sampler smp, int64_t hyp,
-                            bool epnp, PnpOneOut* __restrict__ out) {
+                            bool epnp, bool fast, PnpOneOut* __restrict__ out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     PnpPose p;
     for (int k = 0; k < 9; ++k) p.R[k] = 0;
     for (int k = 0; k < 3; ++k) p.t[k] = 0;
     int idx[5] = {-1, -1, -1, -1, -1};
     out->status = epnp ? pnp_hypothesis_epnp(pts, N, cam, smp, (uint64_t)hyp, p, idx)
-                       : pnp_hypothesis(pts, N, cam, smp, (uint64_t)hyp, p, idx);
+                       : pnp_hypothesis(pts, N, cam, smp, (uint64_t)hyp, p, idx, fast);
     for (int k = 0; k < 9; ++k) out->R[k] = p.R[k];
     for (int k = 0; k < 3; ++k) out->t[k] = p.t[k];
     for (int k = 0; k < 5; ++k) out->idx[k] = idx[k];
@@ -321,7 +322,7 @@ __global__ void mcv_pnp_solve5(const PnpPoint* __restrict__ pts, PnpCamera cam, 
 }
 
 // Direct four-point solve on given normalised points (N == 4 path of solvePnPRansac / solvePnP).
-__global__ void mcv_pnp_solve4(const PnpPoint* __restrict__ pts, PnpCamera cam, PnpOneOut* __restrict__ out) {
+__global__ void mcv_pnp_solve4(const PnpPoint* __restrict__ pts, PnpCamera cam, bool fast, PnpOneOut* __restrict__ out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     double x[4], y[4], W[4][3];
     for (int i = 0; i < 4; ++i) {
@@ -332,7 +333,7 @@ __global__ void mcv_pnp_solve4(const PnpPoint* __restrict__ pts, PnpCamera cam, 
     PnpPose p;
     for (int k = 0; k < 9; ++k) p.R[k] = 0;
     for (int k = 0; k < 3; ++k) p.t[k] = 0;
-    out->status = pnp_ap3p4(cam, x, y, W, p) ? 1 : kStatusNoModel;
+    out->status = (fast ? pnp_ap3p4(cam, x, y, W, p) : pnp_ap3p4_cv(cam, x, y, W, p)) ? 1 : kStatusNoModel;
     for (int k = 0; k < 9; ++k) out->R[k] = p.R[k];
     for (int k = 0; k < 3; ++k) out->t[k] = p.t[k];
     for (int k = 0; k < 4; ++k) out->idx[k] = k;
@@ -623,13 +624,13 @@ void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_
 }
 
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
-                         bool epnp, void* d_models, int* d_counts, hipStream_t s) {
+                         bool epnp, void* d_models, int* d_counts, hipStream_t s, bool fast) {
     if (epnp)
         hipLaunchKernelGGL(mcv_pnp_generate<true>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
-                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
+                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast);
     else
         hipLaunchKernelGGL(mcv_pnp_generate<false>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
-                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts);
+                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast);
 }
 
 // Grid of a pose-wave x point-chunk sweep: waves x chunks >= ~8 waves per SIMD, chunks >= 2048
@@ -729,9 +730,9 @@ void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void*
 }
 
 void launch_pnp_one(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hyp, bool epnp,
-                    PnpOneOut* d_out, hipStream_t s) {
+                    PnpOneOut* d_out, hipStream_t s, bool fast) {
     hipLaunchKernelGGL(mcv_pnp_one, dim3(1), dim3(64), 0, s, (const PnpPoint*)d_pts, N, to_cam(cam8), smp, hyp, epnp,
-                       d_out);
+                       fast, d_out);
 }
 
 void launch_pnp_solve5(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s) {
@@ -767,8 +768,8 @@ void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, c
     }
 }
 
-void launch_pnp_solve4(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s) {
-    hipLaunchKernelGGL(mcv_pnp_solve4, dim3(1), dim3(64), 0, s, (const PnpPoint*)d_pts, to_cam(cam8), d_out);
+void launch_pnp_solve4(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s, bool fast) {
+    hipLaunchKernelGGL(mcv_pnp_solve4, dim3(1), dim3(64), 0, s, (const PnpPoint*)d_pts, to_cam(cam8), fast, d_out);
 }
 
 void launch_pnp_mask(const void* d_pts, int N, const double* cam8, const double* R9, const double* t3, float thr2,

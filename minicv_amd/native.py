@@ -151,6 +151,7 @@ SIGNATURES = {
     "mcvHostDecomposeEssential": (None, [_P, _P, _P, _P]),
     "mcvHostRealRoots": (_I, [_P, _I, _I, _P]),
     "mcvHostPnP": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
+    "mcvHostPnPFast": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
     "mcvHostPnPEpnp": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
     "mcvHostPnpCert": (_I, [_P, _I, _P, _P, _P, C.c_float, _I, _P, _P]),
     "mcvTestPnpSweep": (_I, [_P, _I, _P, _P, _I, C.c_float, _I, _I, _P]),

@@ -265,6 +265,43 @@ static int ap3p4(const Cam* c, const double* x, const double* y, const double* W
     return 1;
 }
 
+/* OpenCV 4.x's AP3P on a 4-point subset (solvePnP -> solveP3P -> ap3p::solve [ext]): undistortPoints into
+ * a CV_32F result, extract_points' pixels (xf fx + cx), ap3p's normalisation (inv_fx mu - cx_fx), the
+ * reference's computePoses with its Ferrari quartic + polish (glibc's transcendentals: the reference's own
+ * arithmetic on Linux), the fourth point's pixel reprojection error picks (first minimum). */
+static int ap3p4_cv(const Cam* c, const double* x, const double* y, const double* W /*4x3*/, double* R, double* t) {
+    const double inv_fx = 1. / c->fx, inv_fy = 1. / c->fy, cx_fx = c->cx / c->fx, cy_fy = c->cy / c->fy;
+    double mu[4], mv[4], b[9], Rr[36], tr[12];
+    for (int i = 0; i < 4; ++i) {
+        mu[i] = (double)(float)x[i] * c->fx + c->cx;
+        mv[i] = (double)(float)y[i] * c->fy + c->cy;
+    }
+    for (int i = 0; i < 3; ++i) bearing(inv_fx * mu[i] - cx_fx, inv_fy * mv[i] - cy_fy, b + 3 * i);
+    int n = ap3p_poses_impl(b, W, Rr, tr, 1);
+    if (n == 0) return 0;
+    int best = 0;
+    double be = 0;
+    for (int i = 0; i < n; ++i) {
+        const double* Q = Rr + 9 * i;
+        const double* w4 = W + 9;
+        double X = Q[0] * w4[0] + Q[3] * w4[1] + Q[6] * w4[2] + tr[3 * i];
+        double Y = Q[1] * w4[0] + Q[4] * w4[1] + Q[7] * w4[2] + tr[3 * i + 1];
+        double Z = Q[2] * w4[0] + Q[5] * w4[1] + Q[8] * w4[2] + tr[3 * i + 2];
+        double mu3p = c->cx + c->fx * X / Z, mv3p = c->cy + c->fy * Y / Z;
+        double e = (mu3p - mu[3]) * (mu3p - mu[3]) + (mv3p - mv[3]) * (mv3p - mv[3]);
+        if (i == 0 || be > e) { best = i; be = e; }
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q) R[3 * r + q] = Rr[9 * best + 3 * q + r];
+    memcpy(t, tr + 3 * best, sizeof(double) * 3);
+    return 1;
+}
+
+/* the RANSAC form of the 4-point solve: OpenCV's chain (default) or the real-root-finder form */
+static int ap3p4_sel(const Cam* c, const double* x, const double* y, const double* W, double* R, double* t) {
+    return orc_get_fast_minimal() ? ap3p4(c, x, y, W, R, t) : ap3p4_cv(c, x, y, W, R, t);
+}
+
 /* pts: N x 8 floats {X, Y, Z, u, v, 0, 0, 0} (the device PnpPoint layout). */
 int orc_pnp_hypothesis(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R, double* t,
                        int* idx_out) {
@@ -281,7 +318,7 @@ int orc_pnp_hypothesis(const float* pts, int N, const double* cam8, uint64_t see
             W[3 * i] = p[0]; W[3 * i + 1] = p[1]; W[3 * i + 2] = p[2];
         }
         if (idx_out) memcpy(idx_out, idx, sizeof(idx));
-        return ap3p4(&c, x, y, W, R, t) ? 1 : ORC_NO_MODEL;
+        return ap3p4_sel(&c, x, y, W, R, t) ? 1 : ORC_NO_MODEL;
     }
     return ORC_NO_SAMPLE;
 }
@@ -530,9 +567,25 @@ void orc_pnp_vvs(const float* pts, int N, const double* cam8, double* rvec, doub
  * model_points: one solve on all points; final pose: LM from the RANSAC pose for ITERATIVE (0),
  * EPnP on the inliers (float points as doubles) for the others.
  * Returns the inlier count (0 on failure); mask, rvec, tvec out. */
+static int solve_pnp_ransac_impl(const double* img, const double* world, int N, const double* K9, const double* dist4,
+                                 double thr, double conf, int maxIters, uint64_t seed, int flags, int kind,
+                                 double* rvec, double* tvec, uint8_t* mask, int64_t* bestOut, int nthreads);
+
+/* flags & ORC_FLAG_FAST_MINIMAL: the AP3P kinds take the real-root-finder quartic for the call */
 int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const double* K9, const double* dist4,
                            double thr, double conf, int maxIters, uint64_t seed, int flags, int kind, double* rvec,
                            double* tvec, uint8_t* mask, int64_t* bestOut, int nthreads) {
+    const int fast0 = orc_get_fast_minimal();
+    if (flags & ORC_FLAG_FAST_MINIMAL) orc_set_fast_minimal(1);
+    int r = solve_pnp_ransac_impl(img, world, N, K9, dist4, thr, conf, maxIters, seed, flags, kind, rvec, tvec, mask,
+                                  bestOut, nthreads);
+    orc_set_fast_minimal(fast0);
+    return r;
+}
+
+static int solve_pnp_ransac_impl(const double* img, const double* world, int N, const double* K9, const double* dist4,
+                                 double thr, double conf, int maxIters, uint64_t seed, int flags, int kind,
+                                 double* rvec, double* tvec, uint8_t* mask, int64_t* bestOut, int nthreads) {
     if (bestOut) *bestOut = -1;
     if (N < 4) return 0;
     if (kind < 0 || kind > 5) kind = 0;
@@ -557,7 +610,7 @@ int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const 
                 undistort(&c, (double)pts[8 * i + 3], (double)pts[8 * i + 4], &x[i], &y[i]);
                 W[3 * i] = pts[8 * i]; W[3 * i + 1] = pts[8 * i + 1]; W[3 * i + 2] = pts[8 * i + 2];
             }
-            ok = ap3p4(&c, x, y, W, R, t);
+            ok = ap3p4_sel(&c, x, y, W, R, t);
         } else {
             orc_epnp5_f32(pts, cam8, R, t);
         }

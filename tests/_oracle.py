@@ -90,7 +90,8 @@ def load() -> C.CDLL:
 
 
 class fast_minimal:
-    """Context: the H / 8-point F hypotheses use the MCV_FLAG_FAST_MINIMAL elimination solver."""
+    """Context: the MCV_FLAG_FAST_MINIMAL replacement minimal solvers (H / 8-point F elimination, E Illinois,
+    AP3P real-root finder)."""
 
     def __init__(self, on: bool = True):
         self.on = on

@@ -85,21 +85,38 @@ def test_epnp_hypotheses_bit_exact(native, gpu, oracle, n, seed, dist, planar):
         np.testing.assert_array_equal(poses[h, 9:], to, err_msg=f"hyp {h}")
 
 
-def test_ap3p_hypotheses_bit_exact(native, gpu, oracle):
+@pytest.mark.parametrize("fast", [False, True])
+def test_ap3p_hypotheses_vs_oracle(native, gpu, oracle, fast):
+    """AP3P kernel poses against the oracle. fast (MCV_FLAG_FAST_MINIMAL, the real-root finder): bit-exact.
+    Default (the reference's Ferrari quartic + polish, OpenCV's float / pixel input chain): the device's
+    transcendentals (ocml) meet glibc's in the oracle, so a pose may differ in its last bits; every status
+    must agree and every pose within 1e-9 relative, and the share of bit-identical poses is reported."""
     img, W, inl, K, d, R, t = S.pnp_problem(800, seed=5, outlier_frac=0.5, dist=DIST)
     pts8 = oracle.pack_pnp(img, W)
     c8 = oracle.cam8(K, d)
-    count = 512
+    count = 2048
     poses = np.zeros((count, 12))
     status = np.zeros(count, np.int32)
-    assert native.lib().mcvTestPnpHypotheses(pts8.ctypes.data, 800, c8.ctypes.data, 3, 0, count, 5,
+    kind = 5 | (0x100 if fast else 0)
+    assert native.lib().mcvTestPnpHypotheses(pts8.ctypes.data, 800, c8.ctypes.data, 3, 0, count, kind,
                                              poses.ctypes.data, status.ctypes.data) == count
-    for h in range(count):
-        st, Ro, to, _ = oracle.pnp_hypothesis(pts8, c8, 3, h)
-        assert status[h] == st
-        if st == 1:
-            np.testing.assert_array_equal(poses[h, :9], Ro.ravel())
-            np.testing.assert_array_equal(poses[h, 9:], to)
+    same = finite = 0
+    with oracle.fast_minimal(fast):
+        for h in range(count):
+            st, Ro, to, _ = oracle.pnp_hypothesis(pts8, c8, 3, h)
+            assert status[h] == st
+            if st != 1:
+                continue
+            ref = np.concatenate([Ro.ravel(), to])
+            if fast:
+                np.testing.assert_array_equal(poses[h], ref)
+            elif np.isfinite(ref).all():
+                finite += 1
+                same += bool(np.array_equal(poses[h], ref))
+                np.testing.assert_allclose(poses[h], ref, rtol=1e-9, atol=1e-12)
+    if not fast:
+        print(f"AP3P Ferrari: {same} of {finite} finite poses bit-identical to the glibc oracle")
+        assert same >= 0.9 * finite
 
 
 @pytest.mark.parametrize("kind", [5, 1, 0])
