@@ -254,7 +254,7 @@ MCV_API int cvMatchL2(const float* q, const int nq, const float* t, const int nt
                       int* idx, float* dist, int* idx2, float* dist2);
 
 /* Diagnostics of the exact L2 re-rank: queries the calling thread's last L2 match sent to the exact
- * full scan (near-ties the GEMM form cannot separate); synchronises the device. */
+ * full scan (near-ties the GEMM form cannot separate); synchronises that match's stream. */
 MCV_API int mcvL2LastExactScans(void);
 
 /* Last error message of the calling thread ("" if none). */

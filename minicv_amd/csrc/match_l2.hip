@@ -459,6 +459,7 @@ struct L2Work {
     DevBuf<unsigned> tmax;
     DevBuf<int> amb;   // [0] = count, [1..] = queued queries
     DevBuf<L2Top2d> scanPart;   // exact-scan partials: < kL2ScanBlocks x kL2ScanQ records
+    hipStream_t last = nullptr; // stream of the last match (the diagnostics read the queue length there)
 };
 
 static L2Work& l2_work() {
@@ -524,17 +525,18 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
                            d_dist, d_idx2, d_dist2);
     }
     MCV_HIP(hipGetLastError());
+    wk.last = s;
     return nq;
 }
 
 // Queries the last launch_match_l2 of this thread sent to the exact scan (diagnostics; synchronises
-// the device).
+// that launch's stream only).
 int l2_last_exact_scans() {
     L2Work& wk = l2_work();
     if (!wk.amb.p) return 0;
     int n = 0;
-    MCV_HIP(hipDeviceSynchronize());
-    MCV_HIP(hipMemcpy(&n, wk.amb.p, sizeof(int), hipMemcpyDeviceToHost));
+    MCV_HIP(hipMemcpyAsync(&n, wk.amb.p, sizeof(int), hipMemcpyDeviceToHost, wk.last));
+    MCV_HIP(hipStreamSynchronize(wk.last));
     return n;
 }
 

@@ -6,7 +6,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from minicv_amd import opencv, synthetic as S
+from minicv_amd import native as N, opencv, synthetic as S
 
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
@@ -104,6 +104,24 @@ def test_l2_near_ties_take_the_exact_scan(gpu, oracle):
 def test_l2_shapes(gpu, oracle, nq, nt, dim):
     q, t, _ = S.l2_problem(nq, nt, dim=dim, seed=nq + nt + dim)
     check_l2(oracle, q, t)
+
+
+def test_l2_duplicated_train_exact_scan_cost(gpu, oracle):
+    """Repeated-texture train sets: every query's best and second best are exact duplicates, so the GEMM
+    form cannot separate them and every query takes the exact scan (O(nq nt dim) fp64). The answer is still
+    the oracle's, and the queue length and the call's time are reported (the ADVICE r02 worst case)."""
+    import time
+    rng = np.random.default_rng(17)
+    base = S.sift_like(500, 128, rng)
+    t = np.concatenate([base] * 8).astype(np.float32)                       # 4000 rows, 500 distinct
+    q = (base[rng.integers(0, 500, size=2000)] + rng.normal(scale=0.3, size=(2000, 128))).astype(np.float32)
+    opencv.matchL2(q, t)                                                    # warm-up
+    t0 = time.perf_counter()
+    check_l2(oracle, q, t)
+    scans = N.lib().mcvL2LastExactScans()
+    print(f"duplicated train: {scans} of {len(q)} queries took the exact scan; "
+          f"match + oracle check {time.perf_counter() - t0:.3f} s")
+    assert scans >= 0.9 * len(q)
 
 
 def test_l2_ties_lowest_index(gpu):
