@@ -65,7 +65,7 @@ HAM_OPS_PER_PAIR = 24
 # Issue models (secondary: what the kernels' instruction streams allow at 2.4 GHz, SIMD cycles per
 # 64 evaluations; measured issue costs: VOP3/VOP3P 4 cycles, VOP2/VOPC e32 2, transcendental 8):
 #   Sampson prefilter (F, E): 56 per (model, correspondence); Hamming 58 per pair. The homography
-#   sweeps use the measured VALU instruction count instead (h_issue, from the PMC pass).
+#   sweeps use the measured VALU instruction count instead (measured_issue, from the SQ pass).
 SPK_CYC_PER_WAVE_EVAL = 56
 # Certified PnP prefilter (pnp_pk.h): per point pair (two lanes' worth of evaluations) 40 packed
 # ops at 4 cycles, 2 v_rcp_f32 at 8, 2 v_max_f32 + 2 v_mul_f32 + 6 v_cmp (VOP3) at 4 = 216 cycles
@@ -296,22 +296,27 @@ def bench_matcher(args):
         dist.destroy_process_group()
 
 
-def h_issue(kernel: str, config: str, evals_per_s: float):
-    """Secondary issue-rate model of the homography sweep from the committed PMC pass
-    (profiles/pmc_traffic.json: SQ_INSTS_VALU per evaluation): every SIMD issuing one wave64 VALU
-    instruction per 4 cycles at 2.4 GHz."""
+def measured_issue(kernel: str, config: str, evals_per_s: float):
+    """Issue rate of a sweep from its committed SQ counter pass (profiles/pmc_traffic.json:
+    SQ_INSTS_VALU per evaluation): every SIMD issuing one wave64 VALU instruction per 4 cycles at
+    2.4 GHz. None when no pass was taken on this workload config."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     try:
         d = json.loads(p.read_text()).get(kernel) if p.exists() else None
-        per = d["counters"]["derived"]["valu_instr_per_eval"] if d and d.get("config") == config else None
+        der = d["counters"]["derived"] if d and d.get("config") == config else None
+        per = der["valu_instr_per_eval"] if der else None
     except Exception:
-        per = None
+        der, per = None, None
     if not per:
         return None
     peak = SIMD_CYC_PER_S * 16 / per
-    return {"achieved": evals_per_s, "peak": peak, "unit": "evaluations/s", "frac": evals_per_s / peak,
-            "model": f"{per:.2f} VALU lane-instructions per evaluation (rocprofv3 SQ_INSTS_VALU, profiles/"
-                     "pmc_traffic.json), one wave64 VALU instruction per SIMD per 4 cycles at 2.4 GHz"}
+    out = {"achieved": evals_per_s, "peak": peak, "unit": "evaluations/s", "frac": evals_per_s / peak,
+           "model": f"{per:.2f} VALU lane-instructions per evaluation (rocprofv3 SQ_INSTS_VALU, profiles/"
+                    "pmc_traffic.json), one wave64 VALU instruction per SIMD per 4 cycles at 2.4 GHz"}
+    if der.get("valu_busy"):   # the counter pass's own share of SIMD cycles with a VALU instruction issuing
+        out["valu_busy_measured"] = der["valu_busy"]
+        out["clock_GHz_measured"] = der.get("clock_GHz")
+    return out
 
 
 def load_traffic(kernel: str, config: str):
@@ -465,7 +470,7 @@ def bench_ransac(args):
                                      "algorithmic_bytes_per_launch": alg_bytes, "peak": HBM_PEAK_GBPS,
                                      "note": "16 B x N per hypothesis as if streamed from HBM; the 1.6 MB point "
                                              "set is L2-resident, measured HBM bytes per launch are `traffic`"},
-                             "issue": h_issue(hkern, f"{n}x{hyps}", evals_per_s)},
+                             "issue": measured_issue(hkern, f"{n}x{hyps}", evals_per_s)},
                 "result": {"best_count": result["count"], "best_hyp": result["idx"],
                            "refined_count": result["final_count"]},
             }
@@ -498,7 +503,8 @@ def bench_ransac(args):
                                       "vector roof binds",
                              "hbm": {"effective_GBps": alg_bytes / (avg_ms * 1e-3) / 1e9,
                                      "algorithmic_bytes_per_launch": alg_bytes, "peak": HBM_PEAK_GBPS},
-                             "issue": {"achieved": evals_per_s, "peak": issue_peak(SPK_CYC_PER_WAVE_EVAL),
+                             "issue": measured_issue("mcv_f_verify", f"{n}x{hyps}", evals_per_s) or
+                                      {"achieved": evals_per_s, "peak": issue_peak(SPK_CYC_PER_WAVE_EVAL),
                                        "unit": "evaluations/s",
                                        "frac": evals_per_s / issue_peak(SPK_CYC_PER_WAVE_EVAL),
                                        "model": f"certified packed-fp32 Sampson prefilter: {SPK_CYC_PER_WAVE_EVAL} "
@@ -570,7 +576,7 @@ def bench_essential(args, world, rank, dev):
     pts = D.pack_essential_tensor(a, b, E_FOCAL, E_PP, dev)
     plan = D.RansacPlan(NL.MODEL_ESSENTIAL, n, hyps)
     cfg = opencv.RansacParams(threshold=E_THR_PX / E_FOCAL, confidence=0.999, max_iters=total, seed=E_SEED,
-                              fixed_iters=True, fused_error=args.fused).to_c()
+                              fixed_iters=True, fused_error=args.fused, fast_minimal=args.fast_minimal).to_c()
     key = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = torch.zeros(n, dtype=torch.uint8, device=dev)
     red = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -636,6 +642,8 @@ def bench_essential(args, world, rank, dev):
             "config": {"workload": f"findEssentialMat five-point RANSAC, {n} correspondences x {total} hypotheses "
                                    f"(<= 10 models each) per call sharded over {world} GPU(s)",
                        "correspondences": n, "hypotheses_total": total, "threshold_px": E_THR_PX,
+                       "minimal_solver": "Illinois real roots (opt-in MCV_FLAG_FAST_MINIMAL)" if args.fast_minimal
+                       else "fivepoint.cpp (getCoeffMat terms, cv::solve LU, solvePoly Durand-Kerner)",
                        "parallelism": f"hypothesis-sharded dp{world}"},
             "kernels": {"mcv_e_generate": {"avg_launch_ms": g_ms, "launches": gl},
                         "mcv_e_verify": {"avg_launch_ms": v_ms, "launches": vl}},
@@ -647,7 +655,8 @@ def bench_essential(args, world, rank, dev):
                                   "certified packed-fp32 prefilter, fp64 only for undecided lanes",
                          "hbm": {"effective_GBps": alg_bytes / (v_ms * 1e-3) / 1e9,
                                  "algorithmic_bytes_per_launch": alg_bytes, "peak": HBM_PEAK_GBPS},
-                         "issue": {"achieved": n * models / (v_ms * 1e-3), "peak": issue_peak(SPK_CYC_PER_WAVE_EVAL),
+                         "issue": measured_issue("mcv_e_verify", f"{n}x{hyps}", n * models / (v_ms * 1e-3)) or
+                                  {"achieved": n * models / (v_ms * 1e-3), "peak": issue_peak(SPK_CYC_PER_WAVE_EVAL),
                                    "unit": "evaluations/s",
                                    "frac": n * models / (v_ms * 1e-3) / issue_peak(SPK_CYC_PER_WAVE_EVAL),
                                    "model": f"certified packed-fp32 Sampson prefilter: {SPK_CYC_PER_WAVE_EVAL} SIMD "
@@ -706,7 +715,7 @@ def bench_pnp(args, world, rank, dev):
     plan = D.RansacPlan(NL.MODEL_PNP, n, hyps)
     plan.set_camera(K, d)
     cfg = opencv.RansacParams(threshold=P_THR_PX, confidence=0.99, max_iters=total, seed=P_SEED,
-                              fixed_iters=True, fused_error=args.fused).to_c()
+                              fixed_iters=True, fused_error=args.fused, fast_minimal=args.fast_minimal).to_c()
     kind = opencv.SOLVER_KIND[args.pnp_kind]
     cfg.pnpKind = kind
     key = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -773,7 +782,8 @@ def bench_pnp(args, world, rank, dev):
                    "frac": p_fl / FP32_PEAK_TF, **common,
                    "model": f"{P_FLOPS_PER_EVAL} (fp64-definition) flops per (hypothesis, correspondence), a "
                             "division counted as one; decided by the certified packed-fp32 prefilter (pnp_pk.h)",
-                   "issue": {"achieved": evals_s, "peak": issue_peak(PPK_CYC_PER_WAVE_EVAL), "unit": "evaluations/s",
+                   "issue": measured_issue("mcv_pnp_verify", f"{n}x{hyps}", evals_s) or
+                            {"achieved": evals_s, "peak": issue_peak(PPK_CYC_PER_WAVE_EVAL), "unit": "evaluations/s",
                              "frac": evals_s / issue_peak(PPK_CYC_PER_WAVE_EVAL),
                              "model": f"certified packed-fp32 projection + bound: {PPK_CYC_PER_WAVE_EVAL} SIMD "
                                       "cycles per 64 (pose, point) at 2.4 GHz"}}
@@ -792,6 +802,8 @@ def bench_pnp(args, world, rank, dev):
                                    f" minimal sets), {n} correspondences x {total} hypotheses per call sharded over "
                                    f"{world} GPU(s) + {'LM' if kind == 0 else 'EPnP'} inlier solve",
                        "correspondences": n, "solver_kind": kind,
+                       "minimal_solver": ("AP3P Rolle-bracket real roots (opt-in MCV_FLAG_FAST_MINIMAL)" if args.fast_minimal
+                                          else "AP3P ap3p.cpp Ferrari + polish") if kind in (2, 5) else "EPnP-5",
                        "hypotheses_total": total, "threshold_px": P_THR_PX,
                        "parallelism": f"hypothesis-sharded dp{world}"},
             "kernels": {"mcv_pnp_verify": {"avg_launch_ms": v_ms, "launches": vl,

@@ -342,6 +342,38 @@ MCV_HD double fpr_dk_sweep(const FprCplx (&cc)[11], FprCplx (&rr)[10]) {
     return md2;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// The same sweep with every 1. / q as the refined reciprocal and no branch: the whole sweep is one basic
+// block, so the scheduler overlaps root i + 1's Horner evaluation (independent of this sweep's updates)
+// with root i's dependent denominator / division chain. `bad` reports a q outside the refined domain; the
+// caller then discards the sweep and reruns it with IEEE = true (the division's own branch-free expansion).
+template <int NN, bool IEEE>
+__device__ double fpr_dk_sweep_nb(const FprCplx (&cc)[11], FprCplx (&rr)[10], bool& bad) {
+    double md2 = 0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+        const FprCplx p = rr[i];
+        FprCplx num = cc[NN], den = cc[NN];
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {
+            num = {num.re * p.re - num.im * p.im + cc[NN - j - 1].re, num.re * p.im + num.im * p.re + cc[NN - j - 1].im};
+            if (j != i) {
+                const FprCplx d = {p.re - rr[j].re, p.im - rr[j].im};
+                den = {den.re * d.re - den.im * d.im, den.re * d.im + den.im * d.re};
+            }
+        }
+        const double q = den.re * den.re + den.im * den.im;
+        bad |= !div_f64_refined_domain(q);
+        const double t = IEEE ? 1. / q : div_f64_refined(1.0, q, rcp_f64_refined(q));
+        num = {(num.re * den.re + num.im * den.im) * t, (-num.re * den.im + num.im * den.re) * t};
+        rr[i] = {p.re - num.re, p.im - num.im};
+        const double a2 = num.re * num.re + num.im * num.im;
+        md2 = md2 < a2 ? a2 : md2;
+    }
+    return md2;
+}
+#endif
+
 // cv::solvePoly(c (ascending, degree 10), roots, 300).
 MCV_HD void fpr_solve_poly(const double (&c)[11], FprCplx (&roots)[10]) {
     FprCplx co[11];
@@ -357,32 +389,56 @@ MCV_HD void fpr_solve_poly(const double (&c)[11], FprCplx (&roots)[10]) {
         if (i < n) p = {p.re * 1.0 - p.im * 1.0, p.re * 1.0 + p.im * 1.0};
     }
     if (n == 10) {
-        for (int iter = 0; iter < 300; ++iter)
+        for (int iter = 0; iter < 300; ++iter) {
+#if defined(__HIP_DEVICE_COMPILE__)
+            FprCplx keep[10];
+#pragma unroll
+            for (int i = 0; i < 10; ++i) keep[i] = roots[i];
+            bool bad = false;
+            double md2 = fpr_dk_sweep_nb<10, false>(co, roots, bad);
+            if (bad) {   // rare: redo the sweep with the IEEE divisions
+#pragma unroll
+                for (int i = 0; i < 10; ++i) roots[i] = keep[i];
+                md2 = fpr_dk_sweep_nb<10, true>(co, roots, bad);
+            }
+            if (md2 <= 0) break;
+#else
             if (fpr_dk_sweep<10>(co, roots) <= 0) break;
+#endif
+        }
         return;
     }
-    // lower degree (a vanishing leading coefficient): the generic loop, rare
+    // lower degree (a vanishing leading coefficient): the generic loop, rare. It works on its own copy
+    // (dynamically indexed, so in scratch) and hands the roots back by constant indices: `roots` itself
+    // is never indexed dynamically and stays in registers on the degree-10 path.
+    FprCplx rr[10], cl[11];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) rr[i] = roots[i];
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) cl[i] = co[i];
     for (int iter = 0; iter < 300; ++iter) {
         double md2 = 0;
         for (int i = 0; i < n; ++i) {
-            const FprCplx pp = roots[i];
-            FprCplx num = co[n], den = co[n];
+            const FprCplx pp = rr[i];
+            FprCplx num = cl[n], den = cl[n];
             for (int j = 0; j < n; ++j) {
-                num = {num.re * pp.re - num.im * pp.im + co[n - j - 1].re, num.re * pp.im + num.im * pp.re + co[n - j - 1].im};
+                num = {num.re * pp.re - num.im * pp.im + cl[n - j - 1].re, num.re * pp.im + num.im * pp.re + cl[n - j - 1].im};
                 if (j != i) {
-                    const FprCplx d = {pp.re - roots[j].re, pp.im - roots[j].im};
+                    const FprCplx d = {pp.re - rr[j].re, pp.im - rr[j].im};
                     den = {den.re * d.re - den.im * d.im, den.re * d.im + den.im * d.re};
                 }
             }
             const double t = 1. / (den.re * den.re + den.im * den.im);
             num = {(num.re * den.re + num.im * den.im) * t, (-num.re * den.im + num.im * den.re) * t};
-            roots[i] = {pp.re - num.re, pp.im - num.im};
+            rr[i] = {pp.re - num.re, pp.im - num.im};
             const double a2 = num.re * num.re + num.im * num.im;
             md2 = md2 < a2 ? a2 : md2;
         }
         if (md2 <= 0) break;
     }
-    for (; n < 10; ++n) roots[n] = roots[n - 1];
+    for (int k = n; k < 10; ++k) rr[k] = rr[k - 1];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) roots[i] = rr[i];
 }
 
 // normL2Sqr<double, double>(a, 9) with CV_ENABLE_UNROLLED [ext: OpenCV core/base.hpp].

@@ -45,6 +45,15 @@ inline int eig_lanes() {   // host: the launchers' screen knob
     return v;
 }
 
+// Workspace layout knob (host): MCV_EIG_SOA = 1 selects the element-major EigWsSoA slices (screen).
+inline bool eig_soa() {
+    static const bool v = [] {
+        const char* e = getenv("MCV_EIG_SOA");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
 // Packed index of A(r, c), r < c < 9: row r starts at 7r - r(r-1)/2 - 1 + (r + 1); the base is
 // r(15 - r)/2 - 1 (r(15 - r) is even), one 24-bit multiply for a dynamic r.
 MCV_HD int eig_row_base(int r) {
@@ -69,6 +78,25 @@ struct EigWsLane {
     double* p;
     MCV_HD double& operator[](int e) { return p[e]; }
 };
+
+// Bank-conflict-free slices (element-major): a block of L lanes keeps its first 32 lanes' working sets
+// as [e][32] (element e of lane t at double 32 e + t) and the other L - 32 lanes' as [e][L - 32] behind
+// them. A ds_read/write_b64 serves a half-wave of 32 lanes over 64 four-byte banks; with the lane in
+// the low bits of the double index every lane of a half-wave owns its own bank pair (the first group)
+// or one of L - 32 <= 32 pairs spaced by the group's stride (the second: 8 e + t' never collides for
+// |t - t'| < 8), whatever element each lane touches — the pivot-dependent (k, l) accesses included.
+// The second group's size must be a power of two (L = 40 / 48 / 64).
+struct EigWsSoA {
+    char* p;    // lane base
+    int sh;     // log2 of the element stride in bytes
+    MCV_HD double& operator[](int e) { return *(double*)(p + ((unsigned)e << sh)); }
+};
+template <int L>
+MCV_HD EigWsSoA eig_ws_soa(double* block, int t) {
+    static_assert(L > 32 && L <= 64 && ((L - 32) & (L - 33)) == 0, "second lane group must be a power of two");
+    constexpr int sh2 = __builtin_ctz(L - 32) + 3;
+    return t < 32 ? EigWsSoA{(char*)(block + t), 8} : EigWsSoA{(char*)(block + 32 * kEigWs + (t - 32)), sh2};
+}
 
 // 4-bit fields: indR[i] at field i (i = 0..7), indC[i] at field i - 1 (i = 1..8).
 MCV_HD int eig_nib(uint32_t x, int i) { return (int)((x >> (4 * i)) & 15u); }

@@ -26,7 +26,7 @@ namespace mcv {
 
 // One lane per hypothesis; run8Point's eigen-solve working set in LDS, one column per lane.
 // FAST = MCV_FLAG_FAST_MINIMAL (no workspace).
-template <bool FAST, int L = kEigLanes>
+template <bool FAST, int L = kEigLanes, bool SOA = false>
 __global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __restrict__ pts4, int N, Sampler smp,
                                                      int64_t hypBegin, int hypCount, FModelD* __restrict__ models,
                                                      int* __restrict__ counts) {
@@ -39,8 +39,13 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __
         st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
-        EigWsLane ws{lds + threadIdx.x * kEigWs};
-        st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
+        if constexpr (SOA) {
+            EigWsSoA ws = eig_ws_soa<L>(lds, threadIdx.x);
+            st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
+        } else {
+            EigWsLane ws{lds + threadIdx.x * kEigWs};
+            st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
+        }
     }
     if (st == 1) {
         models[i] = m;
@@ -319,29 +324,26 @@ void launch_f_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin
     if (fast)
         hipLaunchKernelGGL(mcv_f_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, smp, hypBegin,
                            hypCount, (FModelD*)d_models, d_counts);
-    else
-        switch (eig_lanes()) {
-            case 64:
-                hipLaunchKernelGGL((mcv_f_generate<false, 64>), dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N,
-                                   smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
-                break;
-            case 48:
-                hipLaunchKernelGGL((mcv_f_generate<false, 48>), dim3((hypCount + 47) / 48), dim3(48), 0, s, d_pts4, N,
-                                   smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
-                break;
-            case 32:
-                hipLaunchKernelGGL((mcv_f_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
-                                   smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
-                break;
-            case 39:
-                hipLaunchKernelGGL((mcv_f_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
-                                   smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
-                break;
-            default:
-                hipLaunchKernelGGL((mcv_f_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
-                                   dim3(kEigLanes), 0, s, d_pts4, N, smp, hypBegin, hypCount, (FModelD*)d_models,
-                                   d_counts);
+    else {
+        // lanes per block and workspace layout: MCV_EIG_LANES / MCV_EIG_SOA screens (jacobi_eig.h)
+#define MCV_F_GENERATE(LL, SO)                                                                                    \
+    hipLaunchKernelGGL((mcv_f_generate<false, LL, SO>), dim3((hypCount + LL - 1) / LL), dim3(LL), 0, s, d_pts4, N, smp, hypBegin, hypCount, (FModelD*)d_models, d_counts)
+        const int L = eig_lanes();
+        if (eig_soa()) {
+            if (L == 48) MCV_F_GENERATE(48, true);
+            else if (L == 64) MCV_F_GENERATE(64, true);
+            else MCV_F_GENERATE(40, true);
+        } else {
+            switch (L) {
+                case 64: MCV_F_GENERATE(64, false); break;
+                case 48: MCV_F_GENERATE(48, false); break;
+                case 32: MCV_F_GENERATE(32, false); break;
+                case 39: MCV_F_GENERATE(39, false); break;
+                default: MCV_F_GENERATE(kEigLanes, false);
+            }
         }
+#undef MCV_F_GENERATE
+    }
 }
 
 void launch_f_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, FOneOut* d_out, hipStream_t s, bool fast) {

@@ -29,7 +29,7 @@ namespace mcv {
 // One lane per hypothesis; the runKernel eigen-solve's working set (127 doubles) in LDS, one slice
 // per lane (jacobi_eig.h): 40.6 KB per 40-lane block, 4 blocks per CU. FAST = MCV_FLAG_FAST_MINIMAL
 // (no workspace).
-template <bool FAST, int L = kEigLanes>
+template <bool FAST, int L = kEigLanes, bool SOA = false>
 __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __restrict__ pts4, int N, Sampler smp,
                                                      int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
                                                      double* __restrict__ h64, int* __restrict__ counts) {
@@ -43,8 +43,13 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
         st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
-        EigWsLane ws{lds + threadIdx.x * kEigWs};
-        st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
+        if constexpr (SOA) {
+            EigWsSoA ws = eig_ws_soa<L>(lds, threadIdx.x);
+            st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
+        } else {
+            EigWsLane ws{lds + threadIdx.x * kEigWs};
+            st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
+        }
     }
     if (st == 1) {
         models[i] = mf;
@@ -1019,30 +1024,26 @@ void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin
     if (fast)
         hipLaunchKernelGGL(mcv_h_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, smp, hypBegin,
                            hypCount, (HModelF*)d_models, d_h64, d_counts);
-    else
-        switch (eig_lanes()) {
-            case 64:
-                hipLaunchKernelGGL((mcv_h_generate<false, 64>), dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N,
-                                   smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
-                break;
-            case 48:
-                hipLaunchKernelGGL((mcv_h_generate<false, 48>), dim3((hypCount + 47) / 48), dim3(48), 0, s, d_pts4, N,
-                                   smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
-                break;
-
-            case 32:
-                hipLaunchKernelGGL((mcv_h_generate<false, 32>), dim3((hypCount + 31) / 32), dim3(32), 0, s, d_pts4, N,
-                                   smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
-                break;
-            case 39:
-                hipLaunchKernelGGL((mcv_h_generate<false, 39>), dim3((hypCount + 38) / 39), dim3(39), 0, s, d_pts4, N,
-                                   smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
-                break;
-            default:
-                hipLaunchKernelGGL((mcv_h_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
-                                   dim3(kEigLanes), 0, s, d_pts4, N, smp, hypBegin, hypCount, (HModelF*)d_models, d_h64,
-                                   d_counts);
+    else {
+        // lanes per block and workspace layout: MCV_EIG_LANES / MCV_EIG_SOA screens (jacobi_eig.h)
+#define MCV_H_GENERATE(LL, SO)                                                                                    \
+    hipLaunchKernelGGL((mcv_h_generate<false, LL, SO>), dim3((hypCount + LL - 1) / LL), dim3(LL), 0, s, d_pts4, N, smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts)
+        const int L = eig_lanes();
+        if (eig_soa()) {
+            if (L == 48) MCV_H_GENERATE(48, true);
+            else if (L == 64) MCV_H_GENERATE(64, true);
+            else MCV_H_GENERATE(40, true);
+        } else {
+            switch (L) {
+                case 64: MCV_H_GENERATE(64, false); break;
+                case 48: MCV_H_GENERATE(48, false); break;
+                case 32: MCV_H_GENERATE(32, false); break;
+                case 39: MCV_H_GENERATE(39, false); break;
+                default: MCV_H_GENERATE(kEigLanes, false);
+            }
         }
+#undef MCV_H_GENERATE
+    }
 }
 
 void launch_h_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast) {

@@ -3,11 +3,11 @@
   gpurun_out/bench_<w>.log           -> profiles/<round>_bench_<w>.json   (the bench JSON line)
   gpurun_out/prof_<w>/run_kernel_stats.csv -> profiles/<round>/kernel_stats_<w>.csv
   gpurun_out/pmc_{fetch,write}_<w>/run_counter_collection.csv -> profiles/<round>/pmc_{fetch,write}_<w>.csv
-  gpurun_out/pmc_sq/run_counter_collection.csv -> profiles/<round>/pmc_sq_homography.csv
+  gpurun_out/pmc_sq_<w>/run_counter_collection.csv -> profiles/<round>/pmc_sq_<w>.csv
 and derive profiles/pmc_traffic.json: HBM bytes per launch of each workload's dominant kernel
 (FETCH_SIZE x2 + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), keyed by kernel with
-the workload config it was measured on (bench.py reads it for `roofline.traffic`), plus the SQ
-counters of the homography sweep. Usage: collect_profiles.py r01
+the workload config it was measured on (bench.py reads it for `roofline.traffic`), plus each sweep's
+SQ counters and the VALU instructions per evaluation derived from them (bench.py's `roofline.issue`). Usage: collect_profiles.py r01
 """
 import csv
 import json
@@ -63,18 +63,10 @@ def main():
     traffic = {}
     mean = lambda xs: sum(xs) / len(xs)
     for w, kernel in KERNELS.items():
-        fetch = OUT / f"pmc_fetch_{w}" / "run_counter_collection.csv"
-        write = OUT / f"pmc_write_{w}" / "run_counter_collection.csv"
-        if not (fetch.exists() and write.exists()):
-            continue
-        shutil.copy(fetch, PROF / rnd / f"pmc_fetch_{w}.csv")
-        shutil.copy(write, PROF / rnd / f"pmc_write_{w}.csv")
-        f = pmc_sums(fetch, kernel).get("FETCH_SIZE")
-        wr = pmc_sums(write, kernel).get("WRITE_SIZE")
-        if not f or not wr:
-            continue
         j = last_json(PROF / f"{rnd}_bench_{w}.json") if (PROF / f"{rnd}_bench_{w}.json").exists() else None
-        c = j["config"] if j else {}
+        if not j:
+            continue
+        c = j["config"]
         if w == "homography":
             config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_per_gpu')}", \
                 16.0 * c.get("correspondences", 0) * c.get("hypotheses_per_gpu", 0)
@@ -82,7 +74,7 @@ def main():
             config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
                 16.0 * c.get("correspondences", 0) * c.get("hypotheses_total", 0)
         elif w == "essential":
-            models = (j or {}).get("roofline", {}).get("models_per_launch", 0)
+            models = j.get("roofline", {}).get("models_per_launch", 0)
             config, alg = f"{c.get('correspondences')}x{c.get('hypotheses_total')}", \
                 16.0 * c.get("correspondences", 0) * models
         elif w == "pnp":
@@ -94,28 +86,38 @@ def main():
             config = f"{c.get('queries')}x{c.get('train')}"
             dim_bytes = 32.0 if w == "hamming" else 512.0
             alg = dim_bytes * c.get("queries", 0) * c.get("train", 0)
-        traffic[kernel] = {
-            "workload": w, "config": config,
-            "FETCH_SIZE_KB": mean(f), "WRITE_SIZE_KB": mean(wr), "dispatches": len(f),
-            "hbm_bytes_per_launch": (2 * mean(f) + mean(wr)) * 1024.0,
-            "algorithmic_bytes_per_launch": alg,
-        }
-        print("traffic", kernel, traffic[kernel]["hbm_bytes_per_launch"])
-    sq_src = OUT / "pmc_sq" / "run_counter_collection.csv"
-    if sq_src.exists():
-        shutil.copy(sq_src, PROF / rnd / "pmc_sq_homography.csv")
-        sq = {k: mean(v) for k, v in sorted(pmc_sums(sq_src, KERNELS["homography"]).items())}
-        if KERNELS["homography"] in traffic:
-            t = traffic[KERNELS["homography"]]
+        t = {"workload": w, "config": config, "algorithmic_bytes_per_launch": alg}
+        fetch = OUT / f"pmc_fetch_{w}" / "run_counter_collection.csv"
+        write = OUT / f"pmc_write_{w}" / "run_counter_collection.csv"
+        if fetch.exists() and write.exists():
+            shutil.copy(fetch, PROF / rnd / f"pmc_fetch_{w}.csv")
+            shutil.copy(write, PROF / rnd / f"pmc_write_{w}.csv")
+            f = pmc_sums(fetch, kernel).get("FETCH_SIZE")
+            wr = pmc_sums(write, kernel).get("WRITE_SIZE")
+            if f and wr:
+                t.update({"FETCH_SIZE_KB": mean(f), "WRITE_SIZE_KB": mean(wr), "dispatches": len(f),
+                          "hbm_bytes_per_launch": (2 * mean(f) + mean(wr)) * 1024.0})
+                print("traffic", kernel, t["hbm_bytes_per_launch"])
+        # SQ pass (SQ_INSTS_VALU & co.): measured VALU instructions per evaluation and VALU busy share
+        sq_src = OUT / f"pmc_sq_{w}" / "run_counter_collection.csv"
+        if not sq_src.exists() and w == "homography":
+            sq_src = OUT / "pmc_sq" / "run_counter_collection.csv"
+        if sq_src.exists():
+            shutil.copy(sq_src, PROF / rnd / f"pmc_sq_{w}.csv")
+            sq = {k: mean(v) for k, v in sorted(pmc_sums(sq_src, kernel).items())}
             d = {"sq": sq}
-            hb = last_json(PROF / f"{rnd}_bench_homography.json")
-            if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_INSTS_VALU") and hb:
-                ms = hb["roofline"]["avg_launch_ms"]
-                evals = t["algorithmic_bytes_per_launch"] / 16.0
-                # GRBM_GUI_ACTIVE is summed over the 8 XCDs' GRBM instances
-                d["derived"] = {"clock_GHz": sq["GRBM_GUI_ACTIVE"] / 8 / (ms * 1e-3) / 1e9,
-                                "valu_instr_per_eval": sq["SQ_INSTS_VALU"] * 64 / evals}
+            ms = j.get("roofline", {}).get("avg_launch_ms")
+            if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_INSTS_VALU") and ms:
+                evals = alg / (20.0 if w == "pnp" else 16.0)
+                cyc = sq["GRBM_GUI_ACTIVE"] / 8          # summed over the 8 XCDs' GRBM instances
+                d["derived"] = {"clock_GHz": cyc / (ms * 1e-3) / 1e9,
+                                "valu_instr_per_eval": sq["SQ_INSTS_VALU"] * 64 / evals,
+                                # one wave64 VALU instruction occupies a SIMD for 4 cycles; 1024 SIMDs
+                                "valu_busy": sq["SQ_INSTS_VALU"] * 4 / (1024 * cyc)}
+                print("sq", kernel, d["derived"])
             t["counters"] = d
+        if "hbm_bytes_per_launch" in t or "counters" in t:
+            traffic[kernel] = t
     if traffic:
         for v in traffic.values():
             v["correction"] = ("FETCH_SIZE x2 (gfx950 counts half of a wide streaming read, MI355X_MICROARCH.md "

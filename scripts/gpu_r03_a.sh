@@ -9,11 +9,12 @@ step() {   # name timeout cmd...
     timeout -k 10 "$tmo" "$@" > "$R/gpurun_out/$name.log" 2>&1
     local rc=$?
     echo "$name rc=$rc"; tail -3 "$R/gpurun_out/$name.log"
-    if [ $rc -ne 0 ]; then exit $rc; fi
+    # a plain test failure (1) lets the benches run; faults, aborts and time limits end the script
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-step tests 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+step tests 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu \
     tests/test_gpu_essential.py tests/test_gpu_cv_sampler.py tests/test_gpu_pnp.py tests/test_gpu_multishard.py \
-    tests/test_gpu_homography.py
+    tests/test_gpu_homography.py tests/test_gpu_matchers.py
 step bench_e 300 python bench.py --workload essential --steps 5 --warmup 2 --no-cpu-baseline
 step bench_pnp 300 python bench.py --workload pnp --steps 5 --warmup 2 --no-cpu-baseline
 cd /tmp && export TMPDIR=/tmp

@@ -147,7 +147,7 @@ def test_recover_poses2_convention(gpu):
     assert 1 <= len(poses) <= 2 and mask.sum() > 0.8 * inl.sum()
 
 
-def test_recover_edge_cases(gpu):
+def test_recover_edge_cases(gpu, oracle):
     cfg = opencv.recoverPoseConfig(FOCAL, PP, 0.999, 1.0)
     a, b, *_ = S.essential_problem(4, seed=1, outlier_frac=0)
     R1, R2, t, ms = opencv.recoverPoses(cfg, a, b)                     # N < 5: false, outputs untouched
@@ -155,13 +155,26 @@ def test_recover_edge_cases(gpu):
     assert list(t) == [100, 123, 432] and not ms.any()
     with pytest.raises(N.NativeError, match="at least 5"):
         opencv.recoverPose(cfg, a, b)
-    # all points identical: every sample is degenerate -> no model
+    # all points identical: every sample is degenerate. fivepoint.cpp's arithmetic still returns
+    # models there (the SVD null space of a rank-1 system is some 4-dimensional basis, and the
+    # polynomial has real roots), every point is an inlier of them, and the pose follows — the
+    # product must return what the restated reference returns
     a = np.tile([[100.0, 200.0]], (50, 1))
     b = np.tile([[110.0, 190.0]], (50, 1))
     R1, R2, t, ms = opencv.recoverPoses(cfg, a, b)
-    assert list(t) == [100, 123, 432] and not ms.any()
-    with pytest.raises(N.NativeError):
-        opencv.recoverPose(cfg, a, b)
+    rc, Er, rmask, _ = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=0.999, max_iters=1000,
+                                             flags=N.FLAG_CV_SAMPLER)
+    assert rc == 50
+    np.testing.assert_array_equal(ms, rmask)
+    oR1, oR2, ot = oracle.e_decompose(Er)
+    np.testing.assert_array_equal(t, ot)
+    # the replacement solver (opt-in) finds no model on the degenerate set, on both sides
+    rc_f, *_ = oracle.find_essential(a, b, FOCAL, PP, thr=1.0, conf=0.999, max_iters=1000,
+                                     flags=N.FLAG_CV_SAMPLER | N.FLAG_FAST_MINIMAL)
+    assert rc_f == 0
+    fp = opencv.RansacParams(threshold=1.0, confidence=0.999, max_iters=1000, cv_sampler=True, fast_minimal=True)
+    with pytest.raises(N.NativeError, match="no model"):
+        opencv.findEssentialMat(a, b, FOCAL, PP, fp)
     with pytest.raises(N.NativeError, match="confidence"):
         opencv.recoverPose(opencv.recoverPoseConfig(FOCAL, PP, 1.5, 1.0), *S.essential_problem(50, seed=2)[:2])
 
