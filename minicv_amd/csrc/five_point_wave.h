@@ -486,23 +486,26 @@ __device__ __forceinline__ int ew_hypothesis(EWave& S, const EGroup<G>& g, const
                                              const Sampler& smp, uint64_t hyp, double (&E)[9], int* idx_out) {
     SubsetSrc<5> src(smp, hyp);
     int idx[5];
+    bool found = false;   // search and solve apart (h_hypothesis): one solve pass per wave
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
         const int got = src.next(N, idx);
         if (got < 0) break;
         if (got == 0) continue;
-        if (idx_out)
-            for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
-        for (int e = g.sub; e < 20; e += G) {
-            const int c = e / 5, i = e - 5 * (e / 5);
-            int id = idx[0];
-#pragma unroll
-            for (int k = 1; k < 5; ++k) id = i == k ? idx[k] : id;
-            S.pt[c][i] = pts4[4 * (int64_t)id + c];
-        }
-        ew_sync();
-        return ew_solve5(S, g, E);
+        found = true;
+        break;
     }
-    return kStatusNoSample;
+    if (!found) return kStatusNoSample;
+    if (idx_out)
+        for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
+    for (int e = g.sub; e < 20; e += G) {
+        const int c = e / 5, i = e - 5 * (e / 5);
+        int id = idx[0];
+#pragma unroll
+        for (int k = 1; k < 5; ++k) id = i == k ? idx[k] : id;
+        S.pt[c][i] = pts4[4 * (int64_t)id + c];
+    }
+    ew_sync();
+    return ew_solve5(S, g, E);
 }
 
 // ---- split path: the matrix phases per 16-lane group, the root finder on fewer lanes -------------
@@ -518,10 +521,15 @@ __device__ __forceinline__ void ew_stage_hypothesis(EWave& S, const EGroup<G>& g
     SubsetSrc<5> src(smp, hyp);
     int idx[5];
     int status = kStatusNoSample;
+    bool found = false;   // search and solve apart (h_hypothesis): one solve pass per wave
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
         const int got = src.next(N, idx);
         if (got < 0) break;
         if (got == 0) continue;
+        found = true;
+        break;
+    }
+    if (found) {
         for (int e = g.sub; e < 20; e += G) {
             const int c = e / 5, i = e - 5 * (e / 5);
             int id = idx[0];
@@ -531,11 +539,10 @@ __device__ __forceinline__ void ew_stage_hypothesis(EWave& S, const EGroup<G>& g
         }
         ew_sync();
         status = 0;
-        if (!ew_null_basis(S, g)) break;
-        ew_coeffs(S, g);
-        if (!ew_eliminate(S, g)) break;
-        status = 1;
-        break;
+        if (ew_null_basis(S, g)) {
+            ew_coeffs(S, g);
+            if (ew_eliminate(S, g)) status = 1;
+        }
     }
     if (status == 1) {
         for (int e = g.sub; e < 36; e += G) out->nb[e / 9][e - 9 * (e / 9)] = S.nb[e / 9][e - 9 * (e / 9)];

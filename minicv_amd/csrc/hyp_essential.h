@@ -531,19 +531,22 @@ MCV_HD int e_solve5(const double* x1, const double* y1, const double* x2, const 
 MCV_HD int e_hypothesis(const double* pts4, int N, const Sampler& smp, uint64_t hyp, double (*E)[9], int* idx_out) {
     SubsetSrc<5> src(smp, hyp);
     int idx[5];
+    bool found = false;   // search and solve apart (h_hypothesis): one solve pass per wave
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
         const int got = src.next(N, idx);
         if (got < 0) break;
         if (got == 0) continue;
-        double x1[5], y1[5], x2[5], y2[5];
-        for (int i = 0; i < 5; ++i) {
-            const double* p = pts4 + 4 * (int64_t)idx[i];
-            x1[i] = p[0]; y1[i] = p[1]; x2[i] = p[2]; y2[i] = p[3];
-        }
-        if (idx_out) for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
-        return e_solve5(x1, y1, x2, y2, E);
+        found = true;
+        break;
     }
-    return kStatusNoSample;
+    if (!found) return kStatusNoSample;
+    double x1[5], y1[5], x2[5], y2[5];
+    for (int i = 0; i < 5; ++i) {
+        const double* p = pts4 + 4 * (int64_t)idx[i];
+        x1[i] = p[0]; y1[i] = p[1]; x2[i] = p[2]; y2[i] = p[3];
+    }
+    if (idx_out) for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
+    return e_solve5(x1, y1, x2, y2, E);
 }
 
 // ---- pose ----------------------------------------------------------------------------------

@@ -83,6 +83,7 @@ MCV_HD int f7_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t 
     SubsetSrc<7> src(smp, hyp);
     float x1[7], y1[7], x2[7], y2[7];
     int idx[7];
+    bool found = false;
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
         const int got = src.next(N, idx);
         if (got < 0) break;
@@ -92,10 +93,12 @@ MCV_HD int f7_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t 
             x1[i] = p[0]; y1[i] = p[1]; x2[i] = p[2]; y2[i] = p[3];
         }
         if (!src.tabled() && (have_collinear_last<7>(x1, y1) || have_collinear_last<7>(x2, y2))) continue;
-        if (idx_out) for (int i = 0; i < 7; ++i) idx_out[i] = idx[i];
-        return f_solve7(x1, y1, x2, y2, F);
+        found = true;   // search and solve apart (h_hypothesis): one solve pass per wave
+        break;
     }
-    return kStatusNoSample;
+    if (!found) return kStatusNoSample;
+    if (idx_out) for (int i = 0; i < 7; ++i) idx_out[i] = idx[i];
+    return f_solve7(x1, y1, x2, y2, F);
 }
 
 }  // namespace mcv

@@ -278,6 +278,7 @@ MCV_HD int f_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t h
     SubsetSrc<8> src(smp, hyp);
     float x1[8], y1[8], x2[8], y2[8];
     int idx[8];
+    bool found = false;
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
         const int got = src.next(N, idx);
         if (got < 0) break;
@@ -288,10 +289,12 @@ MCV_HD int f_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t h
             x1[i] = p[0]; y1[i] = p[1]; x2[i] = p[2]; y2[i] = p[3];
         }
         if (!src.tabled() && (have_collinear_last<8>(x1, y1) || have_collinear_last<8>(x2, y2))) continue;
-        if (idx_out) for (int i = 0; i < 8; ++i) idx_out[i] = idx[i];
-        return f_solve8(x1, y1, x2, y2, F, ws, fast) ? 1 : kStatusNoModel;
+        found = true;   // search and solve apart (h_hypothesis): one solve pass per wave
+        break;
     }
-    return kStatusNoSample;
+    if (!found) return kStatusNoSample;
+    if (idx_out) for (int i = 0; i < 8; ++i) idx_out[i] = idx[i];
+    return f_solve8(x1, y1, x2, y2, F, ws, fast) ? 1 : kStatusNoModel;
 }
 
 // ---- errors (fp64, cast to float) ----------------------------------------------------------

@@ -301,6 +301,10 @@ MCV_HD int h_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t h
     SubsetSrc<4> src(smp, hyp);
     float sx[4], sy[4], dx[4], dy[4];
     int idx[4];
+    // The sample search and the solve are kept apart: with the solve inside the attempt loop, lanes of
+    // one wave that accept their sample at different attempts would each run the eigen-solve in a
+    // separate pass of the loop (one pass per distinct attempt count).
+    bool found = false;
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
         const int got = src.next(N, idx);
         if (got < 0) break;
@@ -313,16 +317,18 @@ MCV_HD int h_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t h
             sx[i] = p[0]; sy[i] = p[1]; dx[i] = p[2]; dy[i] = p[3];
         }
         if (!src.tabled() && !h_check_subset(sx, sy, dx, dy)) continue;
-        if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
-        if (!h_solve4(sx, sy, dx, dy, H, ws, fast)) return kStatusNoModel;
-        bool ok = true;
-        for (int i = 0; i < 8; ++i) {
-            mf->h[i] = (float)H[i];
-            ok = ok && isfinite(mf->h[i]);
-        }
-        return ok ? 1 : kStatusNoModel;
+        found = true;
+        break;
     }
-    return kStatusNoSample;
+    if (!found) return kStatusNoSample;
+    if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
+    if (!h_solve4(sx, sy, dx, dy, H, ws, fast)) return kStatusNoModel;
+    bool ok = true;
+    for (int i = 0; i < 8; ++i) {
+        mf->h[i] = (float)H[i];
+        ok = ok && isfinite(mf->h[i]);
+    }
+    return ok ? 1 : kStatusNoModel;
 }
 
 // HomographyEstimatorCallback::computeError for one correspondence, two bit-level definitions

@@ -493,20 +493,23 @@ MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, const 
                           PnpPose& pose, int* idx_out, bool fast = false) {
     SubsetSrc<4> src(smp, hyp);
     int idx[4];
+    bool found = false;   // search and solve apart (h_hypothesis): one solve pass per wave
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
         const int got = src.next(N, idx);
         if (got < 0) break;
         if (got == 0) continue;
-        double x[4], y[4], W[4][3];
-        for (int i = 0; i < 4; ++i) {
-            const PnpPoint p = pts[idx[i]];
-            pnp_undistort(c, (double)p.u, (double)p.v, x[i], y[i]);
-            W[i][0] = p.X; W[i][1] = p.Y; W[i][2] = p.Z;
-        }
-        if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
-        return (fast ? pnp_ap3p4(c, x, y, W, pose) : pnp_ap3p4_cv(c, x, y, W, pose)) ? 1 : kStatusNoModel;
+        found = true;
+        break;
     }
-    return kStatusNoSample;
+    if (!found) return kStatusNoSample;
+    double x[4], y[4], W[4][3];
+    for (int i = 0; i < 4; ++i) {
+        const PnpPoint p = pts[idx[i]];
+        pnp_undistort(c, (double)p.u, (double)p.v, x[i], y[i]);
+        W[i][0] = p.X; W[i][1] = p.Y; W[i][2] = p.Z;
+    }
+    if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
+    return (fast ? pnp_ap3p4(c, x, y, W, pose) : pnp_ap3p4_cv(c, x, y, W, pose)) ? 1 : kStatusNoModel;
 }
 
 // PnP solver kinds (the reference's solverKind, MiniCVNative.cpp:99-116): 0 ITERATIVE, 1 EPNP,
@@ -549,17 +552,20 @@ MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, c
                                PnpPose& pose, int* idx_out, EpnpWs& ws) {
     SubsetSrc<5> src(smp, hyp);
     int idx[5];
+    bool found = false;   // search and solve apart (h_hypothesis): one solve pass per wave
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
         const int got = src.next(N, idx);
         if (got < 0) break;
         if (got == 0) continue;
-        PnpPoint p5[5];
-        for (int i = 0; i < 5; ++i) p5[i] = pts[idx[i]];
-        if (idx_out) for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
-        pnp_epnp5(c, p5, pose, ws);
-        return 1;
+        found = true;
+        break;
     }
-    return kStatusNoSample;
+    if (!found) return kStatusNoSample;
+    PnpPoint p5[5];
+    for (int i = 0; i < 5; ++i) p5[i] = pts[idx[i]];
+    if (idx_out) for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
+    pnp_epnp5(c, p5, pose, ws);
+    return 1;
 }
 MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
                                PnpPose& pose, int* idx_out) {

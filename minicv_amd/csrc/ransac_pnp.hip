@@ -714,6 +714,8 @@ void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void*
     if (!fp64 && pc.ok && d_ext) {
         switch (k) {
             case 2: launch_pnp_verify_pk_k<2>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
+            case 3: launch_pnp_verify_pk_k<3>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
+            case 5: launch_pnp_verify_pk_k<5>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
             case 6: launch_pnp_verify_pk_k<6>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
             case 8: launch_pnp_verify_pk_k<8>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
             default: launch_pnp_verify_pk_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2,

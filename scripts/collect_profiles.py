@@ -24,7 +24,7 @@ WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2", "
 KERNELS = {"homography": "mcv_h_verify_cert", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
            "l2": "mcv_l2_mfma", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify",
            "scaled": "mcv_scaled_costs"}
-EXTRA_BENCH = ["homography_fused", "homography_fast", "pnp_ap3p"]   # second bench lines (bench_<name>.log)
+EXTRA_BENCH = ["homography_fused", "homography_fast", "pnp_ap3p", "essential_fast"]   # second bench lines (bench_<name>.log)
 
 
 def last_json(path: Path):
@@ -118,6 +118,9 @@ def main():
             t["counters"] = d
         if "hbm_bytes_per_launch" in t or "counters" in t:
             traffic[kernel] = t
+    lds = OUT / "pmc_lds_homography" / "run_counter_collection.csv"
+    if lds.exists():
+        shutil.copy(lds, PROF / rnd / "pmc_lds_homography.csv")
     if traffic:
         for v in traffic.values():
             v["correction"] = ("FETCH_SIZE x2 (gfx950 counts half of a wide streaming read, MI355X_MICROARCH.md "
