@@ -275,9 +275,10 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
         spk_make_pair(pr[kp], Fa, Fb, B, cut);
 #pragma unroll
         for (int j = 0; j < 9; ++j) asm volatile("" : "+v"(pr[kp].f[j]));
-        asm volatile("" : "+v"(pr[kp].ec));
-        asm volatile("" : "+v"(pr[kp].nedl));
-        asm volatile("" : "+v"(pr[kp].edh));
+        asm volatile("" : "+v"(pr[kp].ain));
+        asm volatile("" : "+v"(pr[kp].bin));
+        asm volatile("" : "+v"(pr[kp].aout));
+        asm volatile("" : "+v"(pr[kp].bout));
     }
     auto f64 = [&](int k, double (&F)[9]) {
         const int mk = valid[k] ? m0 + k : -1;

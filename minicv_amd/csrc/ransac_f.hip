@@ -180,9 +180,10 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
         // VGPR operands (the pairs are wave-uniform): no constant-bus moves inside the packed ops
 #pragma unroll
         for (int j = 0; j < 9; ++j) asm volatile("" : "+v"(pr[kp].f[j]));
-        asm volatile("" : "+v"(pr[kp].ec));
-        asm volatile("" : "+v"(pr[kp].nedl));
-        asm volatile("" : "+v"(pr[kp].edh));
+        asm volatile("" : "+v"(pr[kp].ain));
+        asm volatile("" : "+v"(pr[kp].bin));
+        asm volatile("" : "+v"(pr[kp].aout));
+        asm volatile("" : "+v"(pr[kp].bout));
     }
     auto f64 = [&](int k, double (&F)[9]) {
         const int hk = valid[k] ? h0 + k : -1;

@@ -2,9 +2,11 @@
 //
 // The reference decides inlier <=> (float)(c * c / den) <= thr2 with c, den evaluated in fp64
 // (f_err_sampson[_fused]). The sweep evaluates c and den in fp32 instead — two models per
-// v_pk_fma_f32, so 14 issue slots per (model, correspondence) against 22 for the fp64 test — and
-// decides every lane whose fp32 values are far enough from the threshold to make the fp64 answer
-// certain; the rest (a fraction ~1e-4 of evaluations) take the exact fp64 test.
+// v_pk_fma_f32: 15 packed FMAs + 1 packed multiply for c and den, then c^2 and two linear cuts in den
+// (1 packed multiply + 2 packed FMAs, spk_cut1) and 4 compares per model pair, i.e. 11.75 VALU issue
+// slots per (model, correspondence) against 22 for the fp64 test — and decides every lane whose fp32
+// values are far enough from the threshold to make the fp64 answer certain; the rest (a fraction
+// ~1e-4 of evaluations) take the exact fp64 test.
 //
 // Error bound (u = 2^-24; inputs |x1| <= X1, |y1| <= Y1, |x2| <= X2, |y2| <= Y2 over the point set):
 //   Ax = |F0| X1 + |F1| Y1 + |F2|, Ay, Az likewise, Bx = |F0| X2 + |F3| Y2 + |F6|, By = |F1| X2 + ...,
@@ -30,7 +32,8 @@ namespace mcv {
 
 struct SampsonPkBound { double Ec, Ed; };
 
-MCV_HD SampsonPkBound sampson_pk_bound(const double* F, double X1, double Y1, double X2, double Y2) {
+MCV_HD SampsonPkBound sampson_pk_bound(const double* F, double X1, double Y1, double X2, double Y2,
+                                       double* DmOut = nullptr) {
     const double a0 = fabs(F[0]), a1 = fabs(F[1]), a2 = fabs(F[2]), a3 = fabs(F[3]), a4 = fabs(F[4]);
     const double a5 = fabs(F[5]), a6 = fabs(F[6]), a7 = fabs(F[7]), a8 = fabs(F[8]);
     const double Ax = a0 * X1 + a1 * Y1 + a2, Ay = a3 * X1 + a4 * Y1 + a5, Az = a6 * X1 + a7 * Y1 + a8;
@@ -44,6 +47,7 @@ MCV_HD SampsonPkBound sampson_pk_bound(const double* F, double X1, double Y1, do
     const bool ok = Mc >= 0x1p-90 && Mc <= 0x1p60 && Dm >= 0x1p-90 && Dm <= 0x1p60 && Ax <= 0x1p60 &&
                     Ay <= 0x1p60 && Bx <= 0x1p60 && By <= 0x1p60;   // false for NaN too
     if (!ok) b.Ec = b.Ed = __builtin_inf();
+    if (DmOut) *DmOut = Dm;
     return b;
 }
 
@@ -73,26 +77,84 @@ inline SampsonPkCut sampson_pk_cut_host(const SampsonCut& c) {
     return k;
 }
 
-// Two models (one pair) in packed fp32, plus their bound terms: Ec, -Ed L32, Ed H32 (rounded up in
-// magnitude, so that the tests stay conservative).
+MCV_HD float spk_f32_up(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __double2float_ru(v);
+#else
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, __builtin_inff());
+    return f;
+#endif
+}
+MCV_HD float spk_f32_dn(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __double2float_rd(v);
+#else
+    float f = (float)v;
+    if ((double)f > v) f = std::nextafter(f, -__builtin_inff());
+    return f;
+#endif
+}
+
+// Two models (one pair) in packed fp32, plus the linear cuts of the decision (below): c^2 against
+// den ain + bin (inlier) and den aout + bout (outlier).
 struct SampsonPkPair {
     sf2 f[9];
-    sf2 ec, nedl, edh;
+    sf2 ain, bin, aout, bout;
 };
 
-__device__ __forceinline__ float spk_f32_up(double v) { return __double2float_ru(v); }
+// The cuts in the form the sweep evaluates: one square and two FMAs per (model, correspondence).
+// The certificate above needs, in exact arithmetic on the fp32 values c, den,
+//   inlier:  (|c| + Ec)^2 < L (den - Ed),   outlier: max(|c| - Ec, 0)^2 > H (den + Ed).
+// With 2 |c| Ec <= Ec (c^2 / K + K) for any K > 0 (AM-GM; equality at |c| = K) both follow from
+//   c^2 (1 + Ec/K) + Ec K + Ec^2 < L (den - Ed)   <=>  c^2 < den ain + bin,
+//     ain = L / (1 + e), bin = -(L Ed + Ec K + Ec^2) / (1 + e), e = Ec / K,
+//   c^2 (1 - Ec/K) - Ec K + Ec^2 > H (den + Ed)   <=>  c^2 > den aout + bout   (K > Ec),
+//     aout = H / (1 - e), bout = (H Ed + Ec K - Ec^2) / (1 - e)
+// (for |c| < Ec the outlier left side is <= -Ec (K - Ec)^2 / K <= 0, so no such lane is certified).
+// The cross term's slack Ec (|c| - K)^2 / K is smallest where the decision is close: K is the |c| of
+// a point on the threshold with den = Dm / 4 (the typical den of the bench models lies in
+// [0.01, 0.7] Dm). fp32 evaluation of c^2 and of the FMA (relative u each) sits inside the 2^-21
+// margins on ain / aout; bin / bout are rounded outward.
+struct SpkCut1 { float ain, bin, aout, bout; };
+MCV_HD SpkCut1 spk_cut1(const SampsonPkBound& b, double Dm, float L32, float H32) {
+    SpkCut1 r;
+    if (!(b.Ec < __builtin_inf()) || !(b.Ed < __builtin_inf())) {   // outside the bound's domain: undecided
+        r.ain = 0.0f; r.bin = -1.0f; r.aout = __builtin_inff(); r.bout = __builtin_inff();
+        return r;
+    }
+    const double H = (double)H32;
+    double K = sqrt(H * Dm * 0.25);
+    if (!(K > 2 * b.Ec)) K = 2 * b.Ec + 0x1p-120;
+    const double e = b.Ec / K;
+    const double ec2 = b.Ec * b.Ec, eck = b.Ec * K;
+    if (L32 > 0) {
+        const double L = (double)L32;
+        r.ain = spk_f32_dn(L / (1.0 + e) * (1.0 - 0x1p-21));
+        r.bin = -spk_f32_up((L * b.Ed + eck + ec2) / (1.0 + e) * (1.0 + 0x1p-40));
+    } else {   // lo <= 0: nothing certified inside
+        r.ain = 0.0f; r.bin = -1.0f;
+    }
+    r.aout = spk_f32_up(H / (1.0 - e) * (1.0 + 0x1p-21));
+    r.bout = spk_f32_up((H * b.Ed + eck - ec2) / (1.0 - e) * (1.0 + 0x1p-40));
+    return r;
+}
+
+
 
 // Build one pair from two fp64 models (F row-major) and the point-set bounds bb = {X1, Y1, X2, Y2}.
 __device__ __forceinline__ void spk_make_pair(SampsonPkPair& P, const double* Fa, const double* Fb, const double* bb,
                                               const SampsonPkCut& k) {
 #pragma unroll
     for (int j = 0; j < 9; ++j) P.f[j] = sf2{(float)Fa[j], (float)Fb[j]};
-    const SampsonPkBound ba = sampson_pk_bound(Fa, bb[0], bb[1], bb[2], bb[3]);
-    const SampsonPkBound bbn = sampson_pk_bound(Fb, bb[0], bb[1], bb[2], bb[3]);
-    const double L = k.L32 > 0 ? (double)k.L32 : 0.0;
-    P.ec = sf2{spk_f32_up(ba.Ec), spk_f32_up(bbn.Ec)};
-    P.nedl = sf2{-spk_f32_up(ba.Ed * L), -spk_f32_up(bbn.Ed * L)};
-    P.edh = sf2{spk_f32_up(ba.Ed * (double)k.H32), spk_f32_up(bbn.Ed * (double)k.H32)};
+    double Dma, Dmb;
+    const SampsonPkBound ba = sampson_pk_bound(Fa, bb[0], bb[1], bb[2], bb[3], &Dma);
+    const SampsonPkBound bbn = sampson_pk_bound(Fb, bb[0], bb[1], bb[2], bb[3], &Dmb);
+    const SpkCut1 ca = spk_cut1(ba, Dma, k.L32, k.H32), cb = spk_cut1(bbn, Dmb, k.L32, k.H32);
+    P.ain = sf2{ca.ain, cb.ain};
+    P.bin = sf2{ca.bin, cb.bin};
+    P.aout = sf2{ca.aout, cb.aout};
+    P.bout = sf2{ca.bout, cb.bout};
 }
 
 // One correspondence (p01 = {x1, y1}, p23 = {x2, y2}) against one model pair: lane masks of the
@@ -107,17 +169,13 @@ __device__ __forceinline__ void spk_test(const SampsonPkPair& P, sf2 p01, sf2 p2
     const sf2 by = spk_fma(P.f[1], x2, spk_fma(P.f[4], y2, P.f[7]));
     const sf2 c = spk_fma(x2, ax, spk_fma(y2, ay, az));
     const sf2 den = spk_fma(ax, ax, spk_fma(ay, ay, spk_fma(bx, bx, by * by)));
-    const sf2 ac = __builtin_elementwise_max(c, -c);
-    const sf2 b = ac + P.ec;
-    const sf2 b2 = b * b;
-    const sf2 r = spk_fma(den, sf2{L32, L32}, P.nedl);
-    const sf2 a = __builtin_elementwise_max(ac - P.ec, sf2{0.0f, 0.0f});
-    const sf2 a2 = a * a;
-    const sf2 q = spk_fma(den, sf2{H32, H32}, P.edh);
-    const uint64_t i0 = __builtin_amdgcn_ballot_w64(b2.x < r.x);
-    const uint64_t i1 = __builtin_amdgcn_ballot_w64(b2.y < r.y);
-    const uint64_t o0 = __builtin_amdgcn_ballot_w64(a2.x > q.x);
-    const uint64_t o1 = __builtin_amdgcn_ballot_w64(a2.y > q.y);
+    const sf2 c2 = c * c;
+    const sf2 r = spk_fma(den, P.ain, P.bin);
+    const sf2 q = spk_fma(den, P.aout, P.bout);
+    const uint64_t i0 = __builtin_amdgcn_ballot_w64(c2.x < r.x);
+    const uint64_t i1 = __builtin_amdgcn_ballot_w64(c2.y < r.y);
+    const uint64_t o0 = __builtin_amdgcn_ballot_w64(c2.x > q.x);
+    const uint64_t o1 = __builtin_amdgcn_ballot_w64(c2.y > q.y);
     in0 = i0;
     in1 = i1;
     amb0 = ~(i0 | o0);
@@ -135,31 +193,37 @@ __device__ __forceinline__ void spk_sweep_point(const SampsonPkPair (&pr)[KP], f
                                                 uint32_t (&cnt)[2 * KP]) {
     const uint64_t vm = __builtin_amdgcn_ballot_w64(v);
     const sf2 p01 = sf2{q.x, q.y}, p23 = sf2{q.z, q.w};
-    uint64_t inm[2 * KP], amb[2 * KP], anyAmb = 0;
+    // certified inliers are counted at once and only the union of the undecided lanes stays live (few
+    // scalar registers in the hot loop); the rare fallback recomputes a model's masks
+    uint64_t anyAmb = 0;
 #pragma unroll
     for (int kp = 0; kp < KP; ++kp) {
         uint64_t i0, i1, a0, a1;
         spk_test(pr[kp], p01, p23, L32, H32, i0, i1, a0, a1);
-        inm[2 * kp] = vm & i0;
-        inm[2 * kp + 1] = vm & i1;
-        amb[2 * kp] = vm & a0;
-        amb[2 * kp + 1] = vm & a1;
-        anyAmb |= amb[2 * kp] | amb[2 * kp + 1];
+        cnt[2 * kp] += (uint32_t)__popcll(vm & i0);
+        cnt[2 * kp + 1] += (uint32_t)__popcll(vm & i1);
+        anyAmb |= vm & (a0 | a1);
     }
     if (__builtin_expect(anyAmb != 0, 0)) {
         const uint64_t me = 1ull << (__lane_id() & 63);
         double x1, y1, x2, y2;
         x64(x1, y1, x2, y2);
 #pragma unroll
-        for (int k = 0; k < 2 * KP; ++k) {
-            if (amb[k] == 0) continue;
-            double F[9];
-            f64(k, F);
-            inm[k] |= __builtin_amdgcn_ballot_w64((amb[k] & me) != 0 && f_error(kind, F, x1, y1, x2, y2) <= thr2);
+        for (int kp = 0; kp < KP; ++kp) {
+            uint64_t i0, i1, a0, a1;
+            spk_test(pr[kp], p01, p23, L32, H32, i0, i1, a0, a1);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint64_t amb = vm & (h ? a1 : a0);
+                if (amb == 0) continue;
+                const int k = 2 * kp + h;
+                double F[9];
+                f64(k, F);
+                cnt[k] += (uint32_t)__popcll(
+                    __builtin_amdgcn_ballot_w64((amb & me) != 0 && f_error(kind, F, x1, y1, x2, y2) <= thr2));
+            }
         }
     }
-#pragma unroll
-    for (int k = 0; k < 2 * KP; ++k) cnt[k] += (uint32_t)__popcll(inm[k]);
 }
 #endif
 
