@@ -120,7 +120,7 @@ void launch_e_cheirality(const double* d_pts4, int N, const uint8_t* d_mask, con
 void launch_e_fivepoint(const EFiveIn& in, EOneOut* d_out, hipStream_t s);
 
 // ---- PnP (ransac_pnp.hip); cam8 = {fx, fy, cx, cy, k1, k2, p1, p2}
-static const int kVerifyPnpPosesPerWave = 4;
+static const int kVerifyPnpPosesPerWave = 3;
 struct PnpOneOut {
     double R[9];
     double t[3];

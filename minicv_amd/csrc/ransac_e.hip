@@ -24,6 +24,7 @@
 #include "five_point_wave.h"
 #include "sampson_pk.h"
 #include "kernels.h"
+#include <algorithm>
 #include <cstdlib>
 
 namespace mcv {
@@ -243,9 +244,12 @@ __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ 
     }
 }
 
+// Grid = (model waves over the dense list) x (point chunks of `chunk` points, a multiple of 64 P): the
+// partial counts of a model's chunks are added atomically (mcv_e5_roots / the fast roots kernel zeroed
+// every model slot), and the extra rounds of shorter waves shrink the idle tail of the last round.
 template <int KP, int P>
 __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict__ pts32,
-                                                       const double4* __restrict__ pts, int N,
+                                                       const double4* __restrict__ pts, int N, int chunk,
                                                        const EModel* __restrict__ dense,
                                                        const int* __restrict__ denseSlot,
                                                        const int* __restrict__ nDense, int* __restrict__ counts,
@@ -289,8 +293,10 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
     const int step = 64 * P;
-    const int nFull = N - N % step;
-    for (int base = 0; base < nFull; base += step) {
+    const int p0 = blockIdx.y * chunk;
+    const int p1 = min(N, p0 + chunk);
+    const int nFull = p0 + (p1 - p0) / step * step;
+    for (int base = p0; base < nFull; base += step) {
         float4 q[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) q[p] = pts32[base + 64 * p + lane];
@@ -304,10 +310,10 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
             spk_sweep_point<KP>(pr, q[p], true, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
         }
     }
-    for (int base = nFull; base < N; base += 64) {
+    for (int base = nFull; base < p1; base += 64) {
         const int p = base + lane;
-        const bool v = p < N;
-        const int idx = v ? p : 0;
+        const bool v = p < p1;
+        const int idx = v ? p : p0;
         const float4 q = pts32[idx];
         auto x64 = [&](double& x1, double& y1, double& x2, double& y2) {
             const double4 d = pts[idx];
@@ -317,8 +323,11 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
     }
     if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (valid[k]) counts[denseSlot[m0 + k]] = (int)cnt[k];
+        for (int k = 0; k < K; ++k) {
+            if (!valid[k]) continue;
+            if (gridDim.y == 1) counts[denseSlot[m0 + k]] = (int)cnt[k];
+            else if (cnt[k]) atomicAdd(counts + denseSlot[m0 + k], (int)cnt[k]);
+        }
     }
 }
 
@@ -474,8 +483,19 @@ static void launch_e_verify_pk_kp(const float4* p32, const double4* p, int N, co
                                   const int* d_nDense, int maxModels, int* d_counts, float thr2, int kind,
                                   const SampsonPkCut& cut, const double* d_bb, hipStream_t s) {
     const int blocks = ((maxModels + 2 * KP - 1) / (2 * KP) + 3) / 4;
-    hipLaunchKernelGGL((mcv_e_verify_pk<KP, P>), dim3(blocks), dim3(256), 0, s, p32, p, N, m, d_denseSlot, d_nDense,
-                       d_counts, thr2, kind, cut, d_bb);
+    // point chunks of at least MCV_E_CHUNK (default 32768) correspondences
+    static const int minChunk = [] {
+        const char* e = getenv("MCV_E_CHUNK");
+        const int v = e ? atoi(e) : 32768;
+        return v > 0 ? v : (1 << 30);
+    }();
+    const int step = 64 * P;
+    int chunks = std::max(1, N / minChunk);
+    int chunk = (N + chunks - 1) / chunks;
+    chunk = (chunk + step - 1) / step * step;
+    chunks = std::max(1, (N + chunk - 1) / chunk);
+    hipLaunchKernelGGL((mcv_e_verify_pk<KP, P>), dim3(blocks, chunks), dim3(256), 0, s, p32, p, N, chunk, m,
+                       d_denseSlot, d_nDense, d_counts, thr2, kind, cut, d_bb);
 }
 
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,

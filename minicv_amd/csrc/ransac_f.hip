@@ -151,8 +151,12 @@ __global__ __launch_bounds__(256) void mcv_abs_bound4(const T4* __restrict__ pts
     }
 }
 
+// Grid = (model waves) x (point chunks of `chunk` points, a multiple of 64 P): with one chunk a wave sweeps
+// all N points and the last round of waves leaves SIMDs idle (8192 waves of 8 models at 65536
+// hypotheses = 2.7 rounds of 3 waves per SIMD); chunks even the rounds out, their partial counts are
+// added atomically (the generate kernel zeroed every valid slot).
 template <int KP, int P>
-__global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict__ pts, int N,
+__global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict__ pts, int N, int chunk,
                                                        const FModelD* __restrict__ models, int* __restrict__ counts,
                                                        int hypCount, float thr2, int kind, SampsonPkCut cut,
                                                        const double* __restrict__ bb) {
@@ -194,8 +198,10 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
     const int step = 64 * P;
-    const int nFull = N - N % step;
-    for (int base = 0; base < nFull; base += step) {
+    const int p0 = blockIdx.y * chunk;
+    const int p1 = min(N, p0 + chunk);
+    const int nFull = p0 + (p1 - p0) / step * step;
+    for (int base = p0; base < nFull; base += step) {
         float4 q[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) q[p] = pts[base + 64 * p + lane];
@@ -206,17 +212,20 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
             spk_sweep_point<KP>(pr, qp, true, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
         }
     }
-    for (int base = nFull; base < N; base += 64) {
+    for (int base = nFull; base < p1; base += 64) {
         const int p = base + lane;
-        const bool v = p < N;
-        const float4 q = pts[v ? p : 0];
+        const bool v = p < p1;
+        const float4 q = pts[v ? p : p0];
         auto x64 = [&](double& x1, double& y1, double& x2, double& y2) { x1 = q.x; y1 = q.y; x2 = q.z; y2 = q.w; };
         spk_sweep_point<KP>(pr, q, v, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
     }
     if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (valid[k]) counts[h0 + k] = (int)cnt[k];
+        for (int k = 0; k < K; ++k) {
+            if (!valid[k]) continue;
+            if (gridDim.y == 1) counts[h0 + k] = (int)cnt[k];
+            else if (cnt[k]) atomicAdd(counts + h0 + k, (int)cnt[k]);
+        }
     }
 }
 
@@ -387,9 +396,23 @@ void launch_abs_bound4(const void* d_pts4, bool fp64, int N, double* d_bb, float
 template <int KP, int P>
 static void launch_f_verify_pk_kp(const float4* p, int N, const FModelD* m, int* d_counts, int hypCount, float thr2,
                                   int kind, const SampsonPkCut& cut, const double* d_bb, hipStream_t s) {
-    const int blocks = ((hypCount + 2 * KP - 1) / (2 * KP) + 3) / 4;
-    hipLaunchKernelGGL((mcv_f_verify_pk<KP, P>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, kind,
-                       cut, d_bb);
+    const int waves = (hypCount + 2 * KP - 1) / (2 * KP);
+    const int blocks = (waves + 3) / 4;
+    // point chunks: about 64 waves per SIMD in total (the last round is a small share), chunks
+    // of at least 8192 points (the per-wave model setup stays small against the sweep)
+    static const int target = [] {
+        const char* e = getenv("MCV_F_WAVES");
+        return e ? atoi(e) : 65536;
+    }();
+    const int step = 64 * P;
+    int chunks = (target + waves - 1) / waves;
+    const int maxChunks = std::max(1, N / 8192);
+    chunks = std::max(1, std::min(chunks, maxChunks));
+    int chunk = (N + chunks - 1) / chunks;
+    chunk = (chunk + step - 1) / step * step;
+    chunks = std::max(1, (N + chunk - 1) / chunk);
+    hipLaunchKernelGGL((mcv_f_verify_pk<KP, P>), dim3(blocks, chunks), dim3(256), 0, s, p, N, chunk, m, d_counts,
+                       hypCount, thr2, kind, cut, d_bb);
 }
 
 void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,

@@ -213,7 +213,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         asm volatile("" : "+v"(pp[k].t0), "+v"(pp[k].t1), "+v"(pp[k].t2), "+v"(pp[k].c1));
         // pose coefficient pairs in SGPRs, read through op_sel. (K = 4 poses' pairs plus the ballot masks
         // of their interleaved tests overflow the SGPR file by ~15 spilled dwords per trip; the VGPR-pair
-        // placement that avoids it measured slower: 1.92 vs 1.79 ms at the PnP bench)
+        // placement that avoids it measured slower: 1.92 vs 1.79 ms at the PnP bench. K = 3, the
+        // default since round 3, spills less: 1.62 vs 1.72 ms at K = 4, 1.78 ms at K = 5)
         pp[k].r01 = pk_uniform(pp[k].r01); pp[k].r23 = pk_uniform(pp[k].r23); pp[k].r45 = pk_uniform(pp[k].r45);
         pp[k].r67 = pk_uniform(pp[k].r67); pp[k].r8c2 = pk_uniform(pp[k].r8c2);
     }
@@ -714,7 +715,7 @@ void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void*
     if (!fp64 && pc.ok && d_ext) {
         switch (k) {
             case 2: launch_pnp_verify_pk_k<2>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
-            case 3: launch_pnp_verify_pk_k<3>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
+            case 4: launch_pnp_verify_pk_k<4>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
             case 5: launch_pnp_verify_pk_k<5>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
             case 6: launch_pnp_verify_pk_k<6>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
             case 8: launch_pnp_verify_pk_k<8>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
