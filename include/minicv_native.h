@@ -451,6 +451,12 @@ MCV_API int mcvTestPnpSweep(const float* pts, int N, const double* cam8, const d
  * Returns the number of decided points whose decision differs from the exact test (must be 0). */
 MCV_API int mcvHostPnpCert(const float* pts, int N, const double* cam8, const double* R9, const double* t3,
                            float thr2, int fused, int* decision, int* exact);
+/* Host twin of the certified Sampson prefilter (sampson_pk.h) for one fp64 model F9 over host float4
+ * points {x1, y1, x2, y2}: decision[i] = 1 certified inlier, 0 certified outlier, -1 undecided; exact[i]
+ * = the fp64 Sampson test (kind 0 fused, 1 op-by-op). Returns the number of decided points whose decision
+ * differs from the exact test (must be 0). */
+MCV_API int mcvHostSampsonCert(const float* pts4, int N, const double* F9, float thr2, int kind, int* decision,
+                               int* exact);
 /* Host build of solveAp3p's computation (mu3 / mv3 pixels, W9 = 3 world points), R36 / t12 out. */
 MCV_API int mcvHostSolveAp3p(const double* mu3, const double* mv3, const double* W9, double inv_fx, double inv_fy,
                              double cx_fx, double cy_fy, double* R36, double* t12);

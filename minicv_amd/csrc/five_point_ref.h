@@ -350,13 +350,25 @@ MCV_HD double fpr_dk_sweep(const FprCplx (&cc)[11], FprCplx (&rr)[10]) {
 template <int NN, bool IEEE>
 __device__ double fpr_dk_sweep_nb(const FprCplx (&cc)[11], FprCplx (&rr)[10], bool& bad) {
     double md2 = 0;
+    // root i's numerator depends only on rr[i] as the sweep found it (no earlier step of the sweep
+    // writes rr[i]): all ten Horner evaluations are formed first, as independent chains, and only the
+    // denominators and updates run in the sweep's order
+    FprCplx nums[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
         const FprCplx p = rr[i];
-        FprCplx num = cc[NN], den = cc[NN];
+        FprCplx num = cc[NN];
+#pragma unroll
+        for (int j = 0; j < NN; ++j)
+            num = {num.re * p.re - num.im * p.im + cc[NN - j - 1].re, num.re * p.im + num.im * p.re + cc[NN - j - 1].im};
+        nums[i] = num;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+        const FprCplx p = rr[i];
+        FprCplx num = nums[i], den = cc[NN];
 #pragma unroll
         for (int j = 0; j < NN; ++j) {
-            num = {num.re * p.re - num.im * p.im + cc[NN - j - 1].re, num.re * p.im + num.im * p.re + cc[NN - j - 1].im};
             if (j != i) {
                 const FprCplx d = {p.re - rr[j].re, p.im - rr[j].im};
                 den = {den.re * d.re - den.im * d.im, den.re * d.im + den.im * d.re};

@@ -8,6 +8,7 @@
 #include "linalg.h"
 #include "hyp_fundamental.h"
 #include "hyp_f7.h"
+#include "sampson_pk.h"
 #include "plan.h"
 
 #include <cmath>
@@ -116,4 +117,35 @@ extern "C" MCV_API int mcvHostF7(const float* pts4, int N, uint64_t seed, int64_
             for (int k = 0; k < 9; ++k) F27[9 * s + k] = F[s][k];
         return n;
     })
+}
+
+// Host twin of the certified Sampson prefilter (sampson_pk.h) for one fp64 model over host float4 points
+// {x1, y1, x2, y2}: decision[i] = 1 certified inlier, 0 certified outlier, -1 undecided; exact[i] = the
+// fp64 test f_error(kind, ...) <= thr2 (kind 0 fused / 1 op-by-op Sampson). The point-set bound is the
+// sweep's (max |coordinate| per column). Returns the number of decided points that differ from the
+// exact test (must be 0).
+extern "C" MCV_API int mcvHostSampsonCert(const float* pts4, int N, const double* F9, float thr2, int kind,
+                                          int* decision, int* exact) {
+    double bb[4] = {0, 0, 0, 0};
+    for (int i = 0; i < N; ++i)
+        for (int c = 0; c < 4; ++c) {
+            const double v = pts4[4 * i + c];
+            bb[c] = std::isfinite(v) ? std::fmax(bb[c], std::fabs(v)) : INFINITY;
+        }
+    const SampsonPkCut cut = sampson_pk_cut_host(sampson_cut(thr2));
+    double Dm;
+    const SampsonPkBound b = sampson_pk_bound(F9, bb[0], bb[1], bb[2], bb[3], &Dm);
+    const SpkCut1 k = spk_cut1(b, Dm, cut.L32, cut.H32);
+    float f[9];
+    for (int j = 0; j < 9; ++j) f[j] = (float)F9[j];
+    int bad = 0;
+    for (int i = 0; i < N; ++i) {
+        const float* q = pts4 + 4 * (size_t)i;
+        const int d = spk_decide_host(f, k, q[0], q[1], q[2], q[3]);
+        const int e = f_error(kind, F9, q[0], q[1], q[2], q[3]) <= thr2 ? 1 : 0;
+        decision[i] = d;
+        exact[i] = e;
+        if (d >= 0 && d != e) ++bad;
+    }
+    return bad;
 }

@@ -183,6 +183,25 @@ __device__ __forceinline__ void spk_test(const SampsonPkPair& P, sf2 p01, sf2 p2
 }
 
 
+// Host twin of one model's decision at one correspondence (the same fp32 operations as spk_test on one
+// half of the packed pair): 1 certified inlier, 0 certified outlier, -1 undecided.
+inline int spk_decide_host(const float (&f)[9], const SpkCut1& k, float x1, float y1, float x2, float y2) {
+    const float ax = std::fmaf(f[0], x1, std::fmaf(f[1], y1, f[2]));
+    const float ay = std::fmaf(f[3], x1, std::fmaf(f[4], y1, f[5]));
+    const float az = std::fmaf(f[6], x1, std::fmaf(f[7], y1, f[8]));
+    const float bx = std::fmaf(f[0], x2, std::fmaf(f[3], y2, f[6]));
+    const float by = std::fmaf(f[1], x2, std::fmaf(f[4], y2, f[7]));
+    const float c = std::fmaf(x2, ax, std::fmaf(y2, ay, az));
+    const float by2 = by * by;
+    const float den = std::fmaf(ax, ax, std::fmaf(ay, ay, std::fmaf(bx, bx, by2)));
+    const float c2 = c * c;
+    const float r = std::fmaf(den, k.ain, k.bin);
+    const float q = std::fmaf(den, k.aout, k.bout);
+    if (c2 < r) return 1;
+    if (c2 > q) return 0;
+    return -1;
+}
+
 // One sweep step of KP model pairs at one correspondence per lane (v: lane holds a point):
 // certified inliers counted, undecided lanes re-tested in fp64 (f_error, kind 0/1) in one
 // wave-uniform branch. F64 fetches model k's fp64 coefficients (global memory; the fallback is
