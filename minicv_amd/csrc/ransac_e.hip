@@ -249,14 +249,17 @@ __global__ __launch_bounds__(256) void mcv_e_verify(const double4* __restrict__ 
 // every model slot), and the extra rounds of shorter waves shrink the idle tail of the last round.
 template <int KP, int P>
 __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict__ pts32,
-                                                       const double4* __restrict__ pts, int N, int chunk,
+                                                       const double4* __restrict__ pts, int N, int chunk, bool xcdMap,
                                                        const EModel* __restrict__ dense,
                                                        const int* __restrict__ denseSlot,
                                                        const int* __restrict__ nDense, int* __restrict__ counts,
                                                        float thr2, int kind, SampsonPkCut cut,
                                                        const double* __restrict__ bb) {
     constexpr int K = 2 * KP;
-    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    // XCD-aware (block, chunk) order as in mcv_f_verify_pk: chunk = linear block id mod C (C | 8)
+    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
+    const int wave = __builtin_amdgcn_readfirstlane((int)((bx * 256u + threadIdx.x) >> 6));
     const int lane = threadIdx.x & 63;
     const int total = __builtin_amdgcn_readfirstlane(*nDense);
     const int m0 = wave * K;
@@ -293,7 +296,7 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
     const int step = 64 * P;
-    const int p0 = blockIdx.y * chunk;
+    const int p0 = (int)by * chunk;
     const int p1 = min(N, p0 + chunk);
     const int nFull = p0 + (p1 - p0) / step * step;
     for (int base = p0; base < nFull; base += step) {
@@ -483,10 +486,11 @@ static void launch_e_verify_pk_kp(const float4* p32, const double4* p, int N, co
                                   const int* d_nDense, int maxModels, int* d_counts, float thr2, int kind,
                                   const SampsonPkCut& cut, const double* d_bb, hipStream_t s) {
     const int blocks = ((maxModels + 2 * KP - 1) / (2 * KP) + 3) / 4;
-    // point chunks of at least MCV_E_CHUNK (default 32768) correspondences
+    // point chunks of at least MCV_E_CHUNK (default 50000) correspondences (screen at N = 100k: one chunk
+    // 12.16 ms, 16384-point chunks 12.25, 32768 12.04, 50000 11.92)
     static const int minChunk = [] {
         const char* e = getenv("MCV_E_CHUNK");
-        const int v = e ? atoi(e) : 32768;
+        const int v = e ? atoi(e) : 50000;
         return v > 0 ? v : (1 << 30);
     }();
     const int step = 64 * P;
@@ -494,8 +498,12 @@ static void launch_e_verify_pk_kp(const float4* p32, const double4* p, int N, co
     int chunk = (N + chunks - 1) / chunks;
     chunk = (chunk + step - 1) / step * step;
     chunks = std::max(1, (N + chunk - 1) / chunk);
-    hipLaunchKernelGGL((mcv_e_verify_pk<KP, P>), dim3(blocks, chunks), dim3(256), 0, s, p32, p, N, chunk, m,
-                       d_denseSlot, d_nDense, d_counts, thr2, kind, cut, d_bb);
+    static const bool xcd = [] {
+        const char* e = getenv("MCV_XCD_MAP");
+        return e ? atoi(e) != 0 : true;
+    }();
+    hipLaunchKernelGGL((mcv_e_verify_pk<KP, P>), dim3(blocks, chunks), dim3(256), 0, s, p32, p, N, chunk,
+                       xcd && (8 % chunks) == 0, m, d_denseSlot, d_nDense, d_counts, thr2, kind, cut, d_bb);
 }
 
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,

@@ -156,12 +156,17 @@ __global__ __launch_bounds__(256) void mcv_abs_bound4(const T4* __restrict__ pts
 // hypotheses = 2.7 rounds of 3 waves per SIMD); chunks even the rounds out, their partial counts are
 // added atomically (the generate kernel zeroed every valid slot).
 template <int KP, int P>
-__global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict__ pts, int N, int chunk,
+__global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict__ pts, int N, int chunk, bool xcdMap,
                                                        const FModelD* __restrict__ models, int* __restrict__ counts,
                                                        int hypCount, float thr2, int kind, SampsonPkCut cut,
                                                        const double* __restrict__ bb) {
     constexpr int K = 2 * KP;
-    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
+    // XCD-aware (block, chunk) order: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+    // speed only), so with the chunk = linear block id mod C (C | 8) every XCD streams one chunk of the
+    // points through its own L2 (500k correspondences = 8 MB, 1 MB per chunk at C = 8)
+    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
+    const int wave = __builtin_amdgcn_readfirstlane((int)((bx * 256u + threadIdx.x) >> 6));
     const int lane = threadIdx.x & 63;
     const int h0 = wave * K;
     if (h0 >= hypCount) return;
@@ -198,7 +203,7 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
     const int step = 64 * P;
-    const int p0 = blockIdx.y * chunk;
+    const int p0 = (int)by * chunk;
     const int p1 = min(N, p0 + chunk);
     const int nFull = p0 + (p1 - p0) / step * step;
     for (int base = p0; base < nFull; base += step) {
@@ -411,8 +416,12 @@ static void launch_f_verify_pk_kp(const float4* p, int N, const FModelD* m, int*
     int chunk = (N + chunks - 1) / chunks;
     chunk = (chunk + step - 1) / step * step;
     chunks = std::max(1, (N + chunk - 1) / chunk);
-    hipLaunchKernelGGL((mcv_f_verify_pk<KP, P>), dim3(blocks, chunks), dim3(256), 0, s, p, N, chunk, m, d_counts,
-                       hypCount, thr2, kind, cut, d_bb);
+    static const bool xcd = [] {
+        const char* e = getenv("MCV_XCD_MAP");
+        return e ? atoi(e) != 0 : true;
+    }();
+    hipLaunchKernelGGL((mcv_f_verify_pk<KP, P>), dim3(blocks, chunks), dim3(256), 0, s, p, N, chunk,
+                       xcd && (8 % chunks) == 0, m, d_counts, hypCount, thr2, kind, cut, d_bb);
 }
 
 void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
