@@ -52,23 +52,41 @@ MCV_HD double cv_hypot(double a, double b) {
 // Vt (if non-null) the right singular vectors as rows. The A result does not depend on Vt.
 // N1 > N (SVD::FULL_UV with more columns than rows): rows N .. N1-1 of A start at zero and are
 // completed to an orthonormal basis by the cv::RNG branch.
-template <int M, int N, int N1 = N>
-MCV_HD void jacobi_svd(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
+// Device: the small decompositions (N <= 6: the 3 x 3 control-point / ABt SVDs, cv::solve's 6 x K)
+// unroll their pair and element loops, so A, W and Vt stay in registers (rolled, their data-dependent
+// row indices put them in scratch); the 12 x 12 keeps its rolled loops over the caller's LDS slice.
+// Unrolling changes no operation or its order.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MCV_SVD_UNROLL _Pragma("unroll SU")
+#define MCV_SMALL_UNROLL _Pragma("unroll")
+#else
+#define MCV_SVD_UNROLL
+#define MCV_SMALL_UNROLL
+#endif
+template <int M, int N, int N1, bool HASV>
+MCV_HD void jacobi_svd_core(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
+    constexpr int SU = N <= 6 ? 16 : 1;
     const double eps = kDblEpsilon * 10, minval = kDblMin;
     double W[N];
+    MCV_SVD_UNROLL
     for (int i = 0; i < N; ++i) {
         double sd = 0;
+        MCV_SMALL_UNROLL
         for (int k = 0; k < M; ++k) sd += A[i][k] * A[i][k];
         W[i] = sd;
-        if (Vt)
+        if constexpr (HASV)
+            MCV_SMALL_UNROLL
             for (int k = 0; k < N; ++k) Vt[i][k] = k == i ? 1.0 : 0.0;
     }
     const int maxIter = M > 30 ? M : 30;
     for (int iter = 0; iter < maxIter; ++iter) {
         bool changed = false;
+        MCV_SVD_UNROLL
         for (int i = 0; i < N - 1; ++i)
+            MCV_SVD_UNROLL
             for (int j = i + 1; j < N; ++j) {
                 double a = W[i], b = W[j], p = 0;
+                MCV_SMALL_UNROLL
                 for (int k = 0; k < M; ++k) p += A[i][k] * A[j][k];
                 if (__builtin_fabs(p) <= eps * __builtin_sqrt(a * b)) continue;
                 p *= 2;
@@ -83,6 +101,7 @@ MCV_HD void jacobi_svd(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
                     s = p / (gamma * c * 2);
                 }
                 a = b = 0;
+                MCV_SMALL_UNROLL
                 for (int k = 0; k < M; ++k) {
                     const double t0 = c * A[i][k] + s * A[j][k];
                     const double t1 = -s * A[i][k] + c * A[j][k];
@@ -94,7 +113,8 @@ MCV_HD void jacobi_svd(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
                 W[i] = a;
                 W[j] = b;
                 changed = true;
-                if (Vt)
+                if constexpr (HASV)
+                    MCV_SMALL_UNROLL
                     for (int k = 0; k < N; ++k) {
                         const double t0 = c * Vt[i][k] + s * Vt[j][k];
                         const double t1 = -s * Vt[i][k] + c * Vt[j][k];
@@ -104,50 +124,80 @@ MCV_HD void jacobi_svd(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
             }
         if (!changed) break;
     }
+    MCV_SVD_UNROLL
     for (int i = 0; i < N; ++i) {
         double sd = 0;
+        MCV_SMALL_UNROLL
         for (int k = 0; k < M; ++k) sd += A[i][k] * A[i][k];
         W[i] = __builtin_sqrt(sd);
     }
+    MCV_SVD_UNROLL
     for (int i = 0; i < N - 1; ++i) {
         int j = i;
+        double wj = W[i];
+        MCV_SMALL_UNROLL
         for (int k = i + 1; k < N; ++k)
-            if (W[j] < W[k]) j = k;
-        if (i != j) {
-            const double tw = W[i]; W[i] = W[j]; W[j] = tw;
-            for (int k = 0; k < M; ++k) { const double t = A[i][k]; A[i][k] = A[j][k]; A[j][k] = t; }
-            if (Vt)
-                for (int k = 0; k < N; ++k) { const double t = Vt[i][k]; Vt[i][k] = Vt[j][k]; Vt[j][k] = t; }
+            if (wj < W[k]) j = k, wj = W[k];
+        // the swap with row j, as a compile-time row index per candidate (no dynamic indexing)
+        MCV_SVD_UNROLL
+        for (int jj = i + 1; jj < N; ++jj) {
+            if (jj != j) continue;
+            const double tw = W[i]; W[i] = W[jj]; W[jj] = tw;
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < M; ++k) { const double t = A[i][k]; A[i][k] = A[jj][k]; A[jj][k] = t; }
+            if constexpr (HASV)
+                MCV_SMALL_UNROLL
+                for (int k = 0; k < N; ++k) { const double t = Vt[i][k]; Vt[i][k] = Vt[jj][k]; Vt[jj][k] = t; }
         }
     }
+    MCV_SVD_UNROLL
     for (int i = 0; i < N; ++i) Wo[i] = W[i];
     CvRng rng{0x12345678u};
+    MCV_SVD_UNROLL
     for (int i = 0; i < N1; ++i) {
         double sd = i < N ? W[i] : 0;
         for (int ii = 0; ii < 100 && sd <= minval; ++ii) {
             // null singular value: random +-1/M vector orthogonalised against the previous rows
             const double val0 = 1. / M;
+            MCV_SMALL_UNROLL
             for (int k = 0; k < M; ++k) A[i][k] = (rng.next() & 256) != 0 ? val0 : -val0;
             for (int it = 0; it < 2; ++it)
+                MCV_SVD_UNROLL
                 for (int j = 0; j < i; ++j) {
                     sd = 0;
+                    MCV_SMALL_UNROLL
                     for (int k = 0; k < M; ++k) sd += A[i][k] * A[j][k];
                     double asum = 0;
+                    MCV_SMALL_UNROLL
                     for (int k = 0; k < M; ++k) {
                         const double t = A[i][k] - sd * A[j][k];
                         A[i][k] = t;
                         asum += __builtin_fabs(t);
                     }
                     asum = asum > eps * 100 ? 1 / asum : 0;
+                    MCV_SMALL_UNROLL
                     for (int k = 0; k < M; ++k) A[i][k] *= asum;
                 }
             sd = 0;
+            MCV_SMALL_UNROLL
             for (int k = 0; k < M; ++k) sd += A[i][k] * A[i][k];
             sd = __builtin_sqrt(sd);
         }
         const double s = sd > minval ? 1 / sd : 0.;
+        MCV_SMALL_UNROLL
         for (int k = 0; k < M; ++k) A[i][k] *= s;
     }
+}
+
+// With Vt (rows: the right singular vectors) / without (a compile-time choice: a runtime null test of
+// a private array's address kept that array out of registers on the GPU).
+template <int M, int N, int N1 = N>
+MCV_HD void jacobi_svd(double (&A)[N1][M], double (&Wo)[N], double (&Vt)[N][N]) {
+    jacobi_svd_core<M, N, N1, true>(A, Wo, Vt);
+}
+template <int M, int N, int N1 = N>
+MCV_HD void jacobi_svd(double (&A)[N1][M], double (&Wo)[N], decltype(nullptr)) {
+    jacobi_svd_core<M, N, N1, false>(A, Wo, nullptr);
 }
 
 // SVBkSb for one right-hand side: x = sum_i [|w_i| > 2 eps sum w] (u_i . b / w_i) v_i, with
@@ -156,16 +206,21 @@ template <int M, int N>
 MCV_HD void svd_backsubst(const double (&U)[N][M], const double (&w)[N], const double (&Vt)[N][N],
                           const double (&b)[M], double (&x)[N]) {
     double thr = 0;
+    MCV_SMALL_UNROLL
     for (int i = 0; i < N; ++i) thr += w[i];
     thr *= kDblEpsilon * 2;
+    MCV_SMALL_UNROLL
     for (int j = 0; j < N; ++j) x[j] = 0;
+    MCV_SMALL_UNROLL
     for (int i = 0; i < N; ++i) {
         double wi = w[i];
         if (__builtin_fabs(wi) <= thr) continue;
         wi = 1 / wi;
         double s = 0;
+        MCV_SMALL_UNROLL
         for (int j = 0; j < M; ++j) s += U[i][j] * b[j];
         s *= wi;
+        MCV_SMALL_UNROLL
         for (int j = 0; j < N; ++j) x[j] = x[j] + s * Vt[i][j];
     }
 }
@@ -174,18 +229,25 @@ MCV_HD void svd_backsubst(const double (&U)[N][M], const double (&w)[N], const d
 template <int N>
 MCV_HD void svd_pinv(const double (&U)[N][N], const double (&w)[N], const double (&Vt)[N][N], double (&X)[N][N]) {
     double thr = 0;
+    MCV_SMALL_UNROLL
     for (int i = 0; i < N; ++i) thr += w[i];
     thr *= kDblEpsilon * 2;
+    MCV_SMALL_UNROLL
     for (int r = 0; r < N; ++r)
+        MCV_SMALL_UNROLL
         for (int c = 0; c < N; ++c) X[r][c] = 0;
+    MCV_SMALL_UNROLL
     for (int i = 0; i < N; ++i) {
         double wi = w[i];
         if (__builtin_fabs(wi) <= thr) continue;
         wi = 1 / wi;
         double buf[N];
+        MCV_SMALL_UNROLL
         for (int c = 0; c < N; ++c) buf[c] = U[i][c] * wi;
+        MCV_SMALL_UNROLL
         for (int r = 0; r < N; ++r) {
             const double s = Vt[i][r];
+            MCV_SMALL_UNROLL
             for (int c = 0; c < N; ++c) X[r][c] = X[r][c] + s * buf[c];
         }
     }
@@ -195,7 +257,9 @@ MCV_HD void svd_pinv(const double (&U)[N][N], const double (&w)[N], const double
 template <int K>
 MCV_HD void svd_solve6(const double (&L)[6][K], const double (&rho)[6], double (&x)[K]) {
     double A[K][6], w[K], Vt[K][K];
+    MCV_SMALL_UNROLL
     for (int i = 0; i < K; ++i)
+        MCV_SMALL_UNROLL
         for (int r = 0; r < 6; ++r) A[i][r] = L[r][i];
     jacobi_svd<6, K>(A, w, Vt);
     svd_backsubst<6, K>(A, w, Vt, rho, x);
@@ -218,7 +282,7 @@ MCV_HD void epnp_control(const double (&sum)[3], const double (&pw0tpw0)[3][3], 
     double A[3][3], dc[3];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) A[i][j] = pw0tpw0[j][i];
-    jacobi_svd<3, 3>(A, dc, (double(*)[3])nullptr);   // A = U^T (uct)
+    jacobi_svd<3, 3>(A, dc, nullptr);   // A = U^T (uct)
     for (int i = 1; i < 4; ++i) {
         const double k = __builtin_sqrt(dc[i - 1] / n);
         for (int j = 0; j < 3; ++j) C.cws[i][j] = C.cws[0][j] + k * A[i - 1][j];
@@ -305,22 +369,29 @@ MCV_HD void epnp_qr_solve(double (&A)[6][4], double (&b)[6], double (&X)[4]) {
     }
 }
 
-MCV_HD void epnp_gauss_newton(const double (&L)[6][10], const double (&rho)[6], double (&be)[4]) {
+// L_6x10 row r at Lr[r * 12 .. + 9], rho[r] at Lr[r * 12 + 10] (rows of the SVD workspace).
+MCV_HD void epnp_gauss_newton(const double* Lr, double (&be)[4]) {
     double X[4] = {0, 0, 0, 0};   // kept across iterations, as epnp::gauss_newton's x
     for (int it = 0; it < 5; ++it) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        // re-read L and rho from the workspace every iteration (hoisted, they would hold 132 registers)
+        asm volatile("" ::: "memory");
+#endif
         double A[6][4], b[6];
+        MCV_SMALL_UNROLL
         for (int i = 0; i < 6; ++i) {
-            const double* l = L[i];
+            const double* l = Lr + 12 * i;
             A[i][0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
             A[i][1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
             A[i][2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
             A[i][3] = l[6] * be[0] + l[7] * be[1] + l[8] * be[2] + 2 * l[9] * be[3];
-            b[i] = rho[i] - (l[0] * be[0] * be[0] + l[1] * be[0] * be[1] + l[2] * be[1] * be[1] +
-                             l[3] * be[0] * be[2] + l[4] * be[1] * be[2] + l[5] * be[2] * be[2] +
-                             l[6] * be[0] * be[3] + l[7] * be[1] * be[3] + l[8] * be[2] * be[3] +
-                             l[9] * be[3] * be[3]);
+            b[i] = l[10] - (l[0] * be[0] * be[0] + l[1] * be[0] * be[1] + l[2] * be[1] * be[1] +
+                            l[3] * be[0] * be[2] + l[4] * be[1] * be[2] + l[5] * be[2] * be[2] +
+                            l[6] * be[0] * be[3] + l[7] * be[1] * be[3] + l[8] * be[2] * be[3] +
+                            l[9] * be[3] * be[3]);
         }
         epnp_qr_solve(A, b, X);
+        MCV_SMALL_UNROLL
         for (int i = 0; i < 4; ++i) be[i] += X[i];
     }
 }
@@ -328,53 +399,55 @@ MCV_HD void epnp_gauss_newton(const double (&L)[6][10], const double (&rho)[6], 
 // A: the 12 x 12 working matrix of the SVD (caller storage: a register / scratch array on the host,
 // a per-lane LDS slice in the GPU hypothesis kernel).
 typedef double EpnpWs[12][12];
-MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBetas& B, EpnpWs& A) {
+
+// compute_pose from M^T M to the betas of the three approximations, in place: on entry A holds the
+// full symmetric M^T M; on return its rows 11, 10, 9, 8 are the four null-space vectors v_0..v_3
+// (rows of U^T), rows 0..5 hold L_6x10 (columns 0..9) and rho (column 10) — the working matrix keeps
+// what the GPU lane would otherwise hold in registers (v, L, rho: 114 doubles).
+MCV_HD void epnp_betas_ws(const EpnpCtrl& C, double (&betas)[4][4], EpnpWs& A) {
     {
         // cvSVD(MtM, D, Ut, 0, MODIFY_A | U_T): Jacobi on transpose(MtM) (= MtM after completeSymm)
         double w[12];
-        for (int a = 0; a < 12; ++a)
-            for (int b = a; b < 12; ++b) A[a][b] = A[b][a] = mtm[mtm_index(a, b)];
-        jacobi_svd<12, 12>(A, w, (double(*)[12])nullptr);
-        for (int i = 0; i < 4; ++i)
-            for (int k = 0; k < 12; ++k) B.v[i][k] = A[11 - i][k];
+        jacobi_svd<12, 12>(A, w, nullptr);
     }
-    double L[6][10], rho[6];
     {
-        double dv[4][6][3];
-        for (int i = 0; i < 4; ++i) {
-            int a = 0, b = 1;
-            for (int j = 0; j < 6; ++j) {
-                for (int k = 0; k < 3; ++k) dv[i][j][k] = B.v[i][3 * a + k] - B.v[i][3 * b + k];
-                ++b;
-                if (b > 3) { ++a; b = a + 1; }
-            }
-        }
-        for (int i = 0; i < 6; ++i) {
-            L[i][0] = dot3(dv[0][i], dv[0][i]);
-            L[i][1] = 2.0 * dot3(dv[0][i], dv[1][i]);
-            L[i][2] = dot3(dv[1][i], dv[1][i]);
-            L[i][3] = 2.0 * dot3(dv[0][i], dv[2][i]);
-            L[i][4] = 2.0 * dot3(dv[1][i], dv[2][i]);
-            L[i][5] = dot3(dv[2][i], dv[2][i]);
-            L[i][6] = 2.0 * dot3(dv[0][i], dv[3][i]);
-            L[i][7] = 2.0 * dot3(dv[1][i], dv[3][i]);
-            L[i][8] = 2.0 * dot3(dv[2][i], dv[3][i]);
-            L[i][9] = dot3(dv[3][i], dv[3][i]);
-        }
         const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
-        for (int i = 0; i < 6; ++i) {
-            const double* p1 = C.cws[pa[i]];
-            const double* p2 = C.cws[pb[i]];
-            rho[i] = (p1[0] - p2[0]) * (p1[0] - p2[0]) + (p1[1] - p2[1]) * (p1[1] - p2[1]) +
-                     (p1[2] - p2[2]) * (p1[2] - p2[2]);
+        MCV_SMALL_UNROLL
+        for (int r = 0; r < 6; ++r) {
+            // edge r = (a, b) of compute_L_6x10's dv loop (a = 0, b = 1, 2, 3, then 1-2, 1-3, 2-3)
+            double dv[4][3];
+            MCV_SMALL_UNROLL
+            for (int i = 0; i < 4; ++i)
+                MCV_SMALL_UNROLL
+                for (int k = 0; k < 3; ++k) dv[i][k] = A[11 - i][3 * pa[r] + k] - A[11 - i][3 * pb[r] + k];
+            double* L = A[r];
+            L[0] = dot3(dv[0], dv[0]);
+            L[1] = 2.0 * dot3(dv[0], dv[1]);
+            L[2] = dot3(dv[1], dv[1]);
+            L[3] = 2.0 * dot3(dv[0], dv[2]);
+            L[4] = 2.0 * dot3(dv[1], dv[2]);
+            L[5] = dot3(dv[2], dv[2]);
+            L[6] = 2.0 * dot3(dv[0], dv[3]);
+            L[7] = 2.0 * dot3(dv[1], dv[3]);
+            L[8] = 2.0 * dot3(dv[2], dv[3]);
+            L[9] = dot3(dv[3], dv[3]);
+            const double* p1 = C.cws[pa[r]];
+            const double* p2 = C.cws[pb[r]];
+            L[10] = (p1[0] - p2[0]) * (p1[0] - p2[0]) + (p1[1] - p2[1]) * (p1[1] - p2[1]) +
+                    (p1[2] - p2[2]) * (p1[2] - p2[2]);
         }
     }
-    for (int k = 0; k < 4; ++k) B.betas[0][k] = 0;
+    const double* Lr = A[0];
+    double rho[6];
+    MCV_SMALL_UNROLL
+    for (int i = 0; i < 6; ++i) rho[i] = A[i][10];
+    for (int k = 0; k < 4; ++k) betas[0][k] = 0;
     {   // approximation 1: [B11 B12 B13 B14]
         double L4[6][4], b4[4];
-        for (int i = 0; i < 6; ++i) { L4[i][0] = L[i][0]; L4[i][1] = L[i][1]; L4[i][2] = L[i][3]; L4[i][3] = L[i][6]; }
+        MCV_SMALL_UNROLL
+        for (int i = 0; i < 6; ++i) { L4[i][0] = A[i][0]; L4[i][1] = A[i][1]; L4[i][2] = A[i][3]; L4[i][3] = A[i][6]; }
         svd_solve6<4>(L4, rho, b4);
-        double* be = B.betas[1];
+        double* be = betas[1];
         if (b4[0] < 0) {
             be[0] = __builtin_sqrt(-b4[0]);
             be[1] = -b4[1] / be[0];
@@ -386,13 +459,14 @@ MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBet
             be[2] = b4[2] / be[0];
             be[3] = b4[3] / be[0];
         }
-        epnp_gauss_newton(L, rho, B.betas[1]);
+        epnp_gauss_newton(Lr, betas[1]);
     }
     {   // approximation 2: [B11 B12 B22]
         double L3[6][3], b3[3];
-        for (int i = 0; i < 6; ++i) { L3[i][0] = L[i][0]; L3[i][1] = L[i][1]; L3[i][2] = L[i][2]; }
+        MCV_SMALL_UNROLL
+        for (int i = 0; i < 6; ++i) { L3[i][0] = A[i][0]; L3[i][1] = A[i][1]; L3[i][2] = A[i][2]; }
         svd_solve6<3>(L3, rho, b3);
-        double* be = B.betas[2];
+        double* be = betas[2];
         if (b3[0] < 0) {
             be[0] = __builtin_sqrt(-b3[0]);
             be[1] = (b3[2] < 0) ? __builtin_sqrt(-b3[2]) : 0.0;
@@ -403,14 +477,16 @@ MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBet
         if (b3[1] < 0) be[0] = -be[0];
         be[2] = 0.0;
         be[3] = 0.0;
-        epnp_gauss_newton(L, rho, B.betas[2]);
+        epnp_gauss_newton(Lr, betas[2]);
     }
     {   // approximation 3: [B11 B12 B22 B13 B23]
         double L5[6][5], b5[5];
+        MCV_SMALL_UNROLL
         for (int i = 0; i < 6; ++i)
-            for (int k = 0; k < 5; ++k) L5[i][k] = L[i][k];
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 5; ++k) L5[i][k] = A[i][k];
         svd_solve6<5>(L5, rho, b5);
-        double* be = B.betas[3];
+        double* be = betas[3];
         if (b5[0] < 0) {
             be[0] = __builtin_sqrt(-b5[0]);
             be[1] = (b5[2] < 0) ? __builtin_sqrt(-b5[2]) : 0.0;
@@ -421,8 +497,18 @@ MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBet
         if (b5[1] < 0) be[0] = -be[0];
         be[2] = b5[3] / be[0];
         be[3] = 0.0;
-        epnp_gauss_newton(L, rho, B.betas[3]);
+        epnp_gauss_newton(Lr, betas[3]);
     }
+}
+
+// The same from the packed upper triangle of M^T M (the host inlier solve), with the null-space
+// vectors copied out.
+MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBetas& B, EpnpWs& A) {
+    for (int a = 0; a < 12; ++a)
+        for (int b = a; b < 12; ++b) A[a][b] = A[b][a] = mtm[mtm_index(a, b)];
+    epnp_betas_ws(C, B.betas, A);
+    for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 12; ++k) B.v[i][k] = A[11 - i][k];
 }
 
 MCV_HD void epnp_betas(const double (&mtm)[kMtmSums], const EpnpCtrl& C, EpnpBetas& B) {
@@ -437,6 +523,20 @@ MCV_HD void epnp_ccs(const EpnpBetas& B, const double (&be)[4], double (&ccs)[4]
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j)
             for (int k = 0; k < 3; ++k) ccs[j][k] += be[i] * B.v[i][3 * j + k];
+}
+
+// The same with the null-space vectors in the workspace (v_i = A[11 - i], epnp_betas_ws).
+MCV_HD void epnp_ccs_ws(const EpnpWs& A, const double (&be)[4], double (&ccs)[4][3]) {
+    MCV_SMALL_UNROLL
+    for (int j = 0; j < 4; ++j)
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 3; ++k) ccs[j][k] = 0.0;
+    MCV_SMALL_UNROLL
+    for (int i = 0; i < 4; ++i)
+        MCV_SMALL_UNROLL
+        for (int j = 0; j < 4; ++j)
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 3; ++k) ccs[j][k] += be[i] * A[11 - i][3 * j + k];
 }
 
 MCV_HD void epnp_pc(const double (&a)[4], const double (&ccs)[4][3], double (&pc)[3]) {
@@ -504,28 +604,33 @@ MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2
     }
     double al[NP][4];
     for (int i = 0; i < NP; ++i) epnp_alphas(C, pw[i], al[i]);
-    double mtm[kMtmSums];
-    for (int k = 0; k < kMtmSums; ++k) mtm[k] = 0;
-    for (int i = 0; i < NP; ++i) {
-        double r1[12], r2[12];
-        epnp_m_rows(al[i], us[i][0], us[i][1], cam, r1, r2);
-        int o = 0;
+    {
+        double mtm[kMtmSums];
+        for (int k = 0; k < kMtmSums; ++k) mtm[k] = 0;
+        for (int i = 0; i < NP; ++i) {
+            double r1[12], r2[12];
+            epnp_m_rows(al[i], us[i][0], us[i][1], cam, r1, r2);
+            int o = 0;
+            for (int a = 0; a < 12; ++a)
+                for (int b = a; b < 12; ++b, ++o) {
+                    mtm[o] += r1[a] * r1[b];
+                    mtm[o] += r2[a] * r2[b];
+                }
+        }
         for (int a = 0; a < 12; ++a)
-            for (int b = a; b < 12; ++b, ++o) {
-                mtm[o] += r1[a] * r1[b];
-                mtm[o] += r2[a] * r2[b];
-            }
+            for (int b = a; b < 12; ++b) ws[a][b] = ws[b][a] = mtm[mtm_index(a, b)];
     }
-    EpnpBetas B;
-    epnp_betas(mtm, C, B, ws);
+    double betas[4][4];
+    epnp_betas_ws(C, betas, ws);   // v, L and rho stay in ws
     double pw0[3] = {0, 0, 0};
     for (int i = 0; i < NP; ++i)
         for (int j = 0; j < 3; ++j) pw0[j] += pw[i][j];
     for (int j = 0; j < 3; ++j) pw0[j] /= NP;
-    double rep[4] = {0, 0, 0, 0}, Rs[4][3][3], ts[4][3];
+    // compute_pose's choice (epnp_pick: N = 1, then 2 / 3 if strictly smaller) as a running best
+    double bestRep = 0;
     for (int N = 1; N <= 3; ++N) {
         double ccs[4][3], pc[NP][3];
-        epnp_ccs(B, B.betas[N], ccs);
+        epnp_ccs_ws(ws, betas[N], ccs);
         for (int i = 0; i < NP; ++i) epnp_pc(al[i], ccs, pc[i]);
         if (pc[0][2] < 0.0)   // solve_for_sign
             for (int i = 0; i < NP; ++i)
@@ -540,15 +645,18 @@ MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2
         for (int i = 0; i < NP; ++i)
             for (int j = 0; j < 3; ++j)
                 for (int k = 0; k < 3; ++k) abt[j][k] += (pc[i][j] - pc0[j]) * (pw[i][k] - pw0[k]);
-        epnp_rt(abt, pc0, pw0, Rs[N], ts[N]);
+        double R[3][3], t[3];
+        epnp_rt(abt, pc0, pw0, R, t);
         double s = 0.0;
-        for (int i = 0; i < NP; ++i) s += epnp_reproj_term(Rs[N], ts[N], cam, pw[i], us[i][0], us[i][1]);
-        rep[N] = s / NP;
-    }
-    const int N = epnp_pick(rep);
-    for (int i = 0; i < 3; ++i) {
-        for (int j = 0; j < 3; ++j) Rout[i][j] = Rs[N][i][j];
-        tout[i] = ts[N][i];
+        for (int i = 0; i < NP; ++i) s += epnp_reproj_term(R, t, cam, pw[i], us[i][0], us[i][1]);
+        const double rep = s / NP;
+        if (N == 1 || rep < bestRep) {
+            bestRep = rep;
+            for (int i = 0; i < 3; ++i) {
+                for (int j = 0; j < 3; ++j) Rout[i][j] = R[i][j];
+                tout[i] = t[i];
+            }
+        }
     }
 }
 

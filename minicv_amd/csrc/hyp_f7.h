@@ -31,7 +31,7 @@ MCV_HD int f_solve7(const float* x1, const float* y1, const float* x2, const flo
         A[i][6] = X0; A[i][7] = Y0; A[i][8] = 1;
     }
     double w[7];
-    jacobi_svd<9, 7, 9>(A, w, (double(*)[7])nullptr);
+    jacobi_svd<9, 7, 9>(A, w, nullptr);
     double f1[9], f2[9];
     for (int i = 0; i < 9; ++i) {
         f2[i] = A[8][i];
