@@ -24,6 +24,7 @@
 #pragma once
 
 #include <cstdlib>
+#include <type_traits>
 #include "mcv_common.h"
 #include "epnp.h"   // cv_hypot (lapack.cpp's hypot)
 
@@ -97,6 +98,33 @@ MCV_HD EigWsSoA eig_ws_soa(double* block, int t) {
     constexpr int sh2 = __builtin_ctz(L - 32) + 3;
     return t < 32 ? EigWsSoA{(char*)(block + t), 8} : EigWsSoA{(char*)(block + 32 * kEigWs + (t - 32)), sh2};
 }
+
+// Byte offsets of the rotated pairs per pivot: row tri(k, l) holds, for i = 0..8, the elements
+// (A(i|k), A(i|l)) of the packed upper triangle as 8 e (the junk slot for i = k, l) in the low / high
+// 16 bits of word i. The GPU lane-slice solver reads one 48-byte row per rotation (constant memory,
+// L1-resident: 1.7 KB) instead of selecting the 18 elements with ~100 integer ops.
+struct EigPairLut {
+    uint32_t w[36][12];
+};
+constexpr EigPairLut eig_make_pair_lut() {
+    EigPairLut t{};
+    for (int k = 0; k < 9; ++k)
+        for (int l = k + 1; l < 9; ++l) {
+            const int row = ((k * (15 - k)) >> 1) - 1 + l;
+            for (int i = 0; i < 9; ++i) {
+                int e0 = kEigJunk, e1 = kEigJunk;
+                if (i != k && i != l) {
+                    e0 = i < k ? ((i * (15 - i)) >> 1) - 1 + k : ((k * (15 - k)) >> 1) - 1 + i;
+                    e1 = i < l ? ((i * (15 - i)) >> 1) - 1 + l : ((l * (15 - l)) >> 1) - 1 + i;
+                }
+                t.w[row][i] = (uint32_t)(8 * e0) | ((uint32_t)(8 * e1) << 16);
+            }
+        }
+    return t;
+}
+#if defined(__HIP__)
+static __constant__ EigPairLut kEigPairLut = eig_make_pair_lut();
+#endif
 
 // 4-bit fields: indR[i] at field i (i = 0..7), indC[i] at field i - 1 (i = 1..8).
 MCV_HD int eig_nib(uint32_t x, int i) { return (int)((x >> (4 * i)) & 15u); }
@@ -240,18 +268,37 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
         int e0[n], e1[n];
         double a0[n], b0[n], va[n], vb[n];
 #if defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (std::is_same<WS, EigWsLane>::value) {
+            // the pair table's row for this pivot (3 vector loads from L1) -> byte offsets
+            const uint4* lr = reinterpret_cast<const uint4*>(kEigPairLut.w[ekl]);
+            const uint4 q0 = lr[0], q1 = lr[1];
+            const uint32_t q8 = kEigPairLut.w[ekl][8];
+            const uint32_t qw[n] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q8};
+            char* const b = reinterpret_cast<char*>(ws.p);
+#pragma unroll
+            for (int i = 0; i < n; ++i) {
+                e0[i] = (int)(qw[i] & 0xffffu);
+                e1[i] = (int)(qw[i] >> 16);
+                a0[i] = *reinterpret_cast<const double*>(b + e0[i]);
+                b0[i] = *reinterpret_cast<const double*>(b + e1[i]);
+            }
+        } else
+#endif
+        {
+#if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-        for (int i = 0; i < n; ++i) {
-            // branch-free index selection (a select of LDS addresses feeding a load is otherwise
-            // turned into control flow around each load)
-            const int mk = -(int)(i < k), ml = -(int)(i < l), ms = -(int)(i == k || i == l);
-            const int x0 = ((eig_row_base(i) + k) & mk) | ((rk + i) & ~mk);
-            const int x1 = ((eig_row_base(i) + l) & ml) | ((rl + i) & ~ml);
-            e0[i] = (kEigJunk & ms) | (x0 & ~ms);
-            e1[i] = (kEigJunk & ms) | (x1 & ~ms);
-            a0[i] = ws[e0[i]];
-            b0[i] = ws[e1[i]];
+            for (int i = 0; i < n; ++i) {
+                // branch-free index selection (a select of LDS addresses feeding a load is otherwise
+                // turned into control flow around each load)
+                const int mk = -(int)(i < k), ml = -(int)(i < l), ms = -(int)(i == k || i == l);
+                const int x0 = ((eig_row_base(i) + k) & mk) | ((rk + i) & ~mk);
+                const int x1 = ((eig_row_base(i) + l) & ml) | ((rl + i) & ~ml);
+                e0[i] = (kEigJunk & ms) | (x0 & ~ms);
+                e1[i] = (kEigJunk & ms) | (x1 & ~ms);
+                a0[i] = ws[e0[i]];
+                b0[i] = ws[e1[i]];
+            }
         }
         const int vk = kEigV + (k << 3) + k, vl = kEigV + (l << 3) + l;   // + 9 k, + 9 l
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -276,6 +323,13 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
         for (int i = 0; i < n; ++i) {
             nk[i] = a0[i] * c - b0[i] * s;
             nl[i] = a0[i] * s + b0[i] * c;
+#if defined(__HIP_DEVICE_COMPILE__)
+            if constexpr (std::is_same<WS, EigWsLane>::value) {   // e0 / e1 are byte offsets here
+                *reinterpret_cast<double*>(reinterpret_cast<char*>(ws.p) + e0[i]) = nk[i];
+                *reinterpret_cast<double*>(reinterpret_cast<char*>(ws.p) + e1[i]) = nl[i];
+                continue;
+            }
+#endif
             ws[e0[i]] = nk[i];
             ws[e1[i]] = nl[i];
         }
