@@ -53,6 +53,7 @@ FP64_PEAK_TF = 78.6
 # attainable flop rate of that arithmetic is half the FMA-counted fp64 peak.
 FP64_NOFMA_PEAK_TF = FP64_PEAK_TF / 2
 FP32_MFMA_PEAK_TF = 157.3
+F16_MFMA_PEAK_TF = 2516.6      # dense f16 MFMA: 32x32x16 = 16384 MAC per 32 cycles per SIMD, 1024 SIMDs, 2.4 GHz
 INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # Algorithmic work per unit: homography computeError = 25 flops per (hypothesis,
 # correspondence) (3 dot products, 1 reciprocal, 2 sub, 2 mul, 1 add, 1 compare); Sampson error =
@@ -261,14 +262,24 @@ def bench_matcher(args):
                     "dtype": "u32", "scaling": "strong"}
         else:
             exact_scans = NL.lib().mcvL2LastExactScans()
+            form = NL.lib().mcvL2LastGemmForm()
             flops = 2.0 * cnt * nt * 128
             tf = flops / (avg_ms * 1e-3) / 1e12
+            if form == 16:   # f16-split GEMM form: three f16 MFMA products per (query, train, dim)
+                roof = {"bound": "mfma-f16", "achieved": 3.0 * tf, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                        "frac": 3.0 * tf / F16_MFMA_PEAK_TF, "kernel": "mcv_l2_mfma16",
+                        "model": "fp32 operands split into f16 hi + lo; hi.hi + hi.lo + lo.hi on "
+                                 "v_mfma_f32_32x32x16_f16 = 3 x 2 Nq Nt D MFMA flops per launch; "
+                                 f"algorithmic rate {tf:.1f} TFLOP/s (2 Nq Nt D)"}
+            else:
+                roof = {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                        "frac": tf / FP32_MFMA_PEAK_TF, "kernel": "mcv_l2_mfma"}
+            roof.update({"traffic": load_traffic(roof["kernel"], f"{nq}x{nt}"), "avg_launch_ms": avg_ms})
             line = {"metric": "BF L2 knn-2 TFLOP/s, SIFT-128 50k x 50k fp32 GEMM on MFMA (BASELINE config[4])",
                     "value": 2.0 * nq * nt * 128 * args.steps / el / 1e12, "unit": "TFLOP/s",
-                    "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                                 "frac": tf / FP32_MFMA_PEAK_TF,
-                                 "traffic": load_traffic("mcv_l2_mfma", f"{nq}x{nt}"), "kernel": "mcv_l2_mfma",
-                                 "avg_launch_ms": avg_ms},
+                    "roofline": roof,
+                    "gemm_form": {16: "f16 split (hi.hi + hi.lo + lo.hi), exact re-rank",
+                                  32: "f32, exact re-rank"}.get(form, str(form)),
                     "exact_rerank": {"queries_to_exact_scan": exact_scans,
                                      "note": "idx / dist are the exact direct-sum answer (fp64, ties -> lowest "
                                              "index); the GEMM form only nominates candidates"},

@@ -256,6 +256,9 @@ MCV_API int cvMatchL2(const float* q, const int nq, const float* t, const int nt
 /* Diagnostics of the exact L2 re-rank: queries the calling thread's last L2 match sent to the exact
  * full scan (near-ties the GEMM form cannot separate); synchronises that match's stream. */
 MCV_API int mcvL2LastExactScans(void);
+/* GEMM form of the calling thread's last L2 match: 16 = f16 split (every |x| < 2^15, dim <= 128),
+ * 32 = f32; synchronises that match's stream. */
+MCV_API int mcvL2LastGemmForm(void);
 
 /* Last error message of the calling thread ("" if none). */
 MCV_API const char* mcvGetLastError(void);

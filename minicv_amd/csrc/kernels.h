@@ -187,6 +187,7 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
 int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim, int* d_idx, float* d_dist,
                     int* d_idx2, float* d_dist2, hipStream_t s);
 int l2_last_exact_scans();
+int l2_last_gemm_form();
 
 // ---- CameraPose.findScaled (scaled_pose.hip)
 struct ScaledSetup;

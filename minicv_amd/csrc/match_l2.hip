@@ -17,6 +17,14 @@
 //   and inserts each score with 2 v_cmp + 6 v_cndmask (no divergent branch per score: the branchy
 //   form the compiler chose cost 7 % of the kernel, 5.80 -> 5.38 ms at cfg5).
 //   Grid = (query blocks of 128) x (train chunks); each lane keeps its top-3 GEMM-form scores.
+// mcv_l2_mfma16<DP, TR>: the same GEMM form on the f16 matrix pipe (16x the f32 MFMA rate) with every
+//   fp32 operand split into f16 hi + lo (x = hi + lo + r, |r| <= 2^-22 |x| + 2^-13): q.t ~ qh.th +
+//   qh.tl + ql.th in two 32x32x16 accumulator chains (hi.hi; hi.lo then lo.hi) — 24 MFMAs of 32
+//   cycles per 32 x 32 x 128 tile against 64 of 64 cycles in f32. f16 x f16 products are exact in f32; the dropped ql.tl and the
+//   split residuals add 2^-21 |q| |t| + 2^-12.9 sqrt(dim) (|q| + |t|) to the nomination's error
+//   bound (mcv_l2_refine's tol16), so the exact answer is unchanged. Used when every coordinate of
+//   both sets is finite with |x| < 2^15 (fp16 range); mcv_l2_prep16 records max |x| and each kernel
+//   runs or returns on that device-side flag (no host round trip).
 // mcv_l2_refine folds the per-chunk top-3s and makes the result exact: the three candidates' exact
 //   squared distances (fp64 direct sum in dim order, the oracle's definition) give the top-2 unless a
 //   bound on the GEMM form's rounding leaves room for another train (near-ties), in which case the
@@ -31,6 +39,11 @@
 namespace mcv {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+static constexpr unsigned kL2F16MaxBits = 0x47000000u;   // 32768.0f: |x| below it fits fp16 (max 65504)
+
+// The f16-split path's domain flag (max |x| over both sets as float bits; null: f32 path only).
+__device__ __forceinline__ bool l2_f16_domain(const unsigned* dom) { return dom && *dom < kL2F16MaxBits; }
 
 struct L2Part { float b1, b2, b3; int i1, i2, i3; };
 
@@ -86,7 +99,8 @@ __device__ __forceinline__ void third_fold(float& c1, float& c2, float& c3, floa
 // Parity-split, zero-padded copy [nPad][DP] + squared norms (fp32, wave tree sum: the order only
 // affects the GEMM form, whose rounding the exact re-rank bounds whatever the order).
 __global__ void mcv_l2_prep(const float* __restrict__ src, int n, int dim, int DP, int nPad, float* __restrict__ dst,
-                            float* __restrict__ norms, float padNorm, unsigned* __restrict__ unused) {
+                            float* __restrict__ norms, float padNorm, const unsigned* __restrict__ dom) {
+    if (l2_f16_domain(dom)) return;   // the f16-split path runs (mcv_l2_prep16 wrote the norms)
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (r >= nPad) return;
@@ -150,7 +164,9 @@ __device__ __forceinline__ void l2_lstore(float* __restrict__ lds, float* __rest
 template <int DP, int TR>
 __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ qp, const float* __restrict__ tp,
                                                      const float* __restrict__ tnorm, int ntTiles,
-                                                     int tilesPerChunk, int nqPad, L2Part* __restrict__ part) {
+                                                     int tilesPerChunk, int nqPad, L2Part* __restrict__ part,
+                                                     const unsigned* __restrict__ dom) {
+    if (l2_f16_domain(dom)) return;   // grid-uniform: mcv_l2_mfma16 takes this launch
     constexpr int KS = DP / 2;          // MFMA k-steps (2 dims each)
     constexpr int ROWF = DP + 4;        // padded LDS row, floats
     constexpr int PER = TR * DP / 1024; // float4 staging loads per thread per tile (TR rows x DP)
@@ -251,6 +267,256 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
     }
 }
 
+// ---- f16-split GEMM form ---------------------------------------------------------------------
+
+// Row-major split copies [nPad][DP] (hi = RN f16 of x, lo = RN f16 of the exact fp32 residual x - hi),
+// zero padding, the fp32 squared norm (as mcv_l2_prep) and the row's max |x| (float bits; a
+// non-finite coordinate records +inf: out of the f16 domain; 0 for padding rows). mcv_l2_dommax folds
+// the rows' maxima (one atomic per row on one address serialised to ~0.5 ms per call).
+__global__ void mcv_l2_prep16(const float* __restrict__ src, int n, int dim, int DP, int nPad, _Float16* __restrict__ hi,
+                              _Float16* __restrict__ lo, float* __restrict__ norms, float padNorm,
+                              unsigned* __restrict__ rowmax) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nPad) return;
+    float acc = 0.f;
+    unsigned m = 0;
+    for (int k = lane; k < DP; k += 64) {
+        const float v = (r < n && k < dim) ? src[(size_t)r * dim + k] : 0.f;
+        const _Float16 h = (_Float16)v;
+        hi[(size_t)r * DP + k] = h;
+        lo[(size_t)r * DP + k] = (_Float16)(v - (float)h);
+        acc = fmaf(v, v, acc);
+        const float a = fabsf(v);
+        const unsigned b = a == a && a < __builtin_inff() ? __float_as_uint(a) : 0x7f800000u;
+        m = b > m ? b : m;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        acc += __shfl_xor(acc, off, 64);
+        const unsigned o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    if (lane == 0) {
+        norms[r] = r < n ? acc : padNorm;
+        rowmax[r] = r < n ? m : 0u;
+    }
+}
+
+// dom = max over both sets' row maxima (bit order = float order for non-negative floats).
+__global__ __launch_bounds__(1024) void mcv_l2_dommax(const unsigned* __restrict__ a, int na, const unsigned* __restrict__ b,
+                                                      int nb, unsigned* __restrict__ dom) {
+    __shared__ unsigned sm[16];
+    unsigned m = 0;
+    for (int i = threadIdx.x; i < na; i += 1024) m = a[i] > m ? a[i] : m;
+    for (int i = threadIdx.x; i < nb; i += 1024) m = b[i] > m ? b[i] : m;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) m = sm[w] > m ? sm[w] : m;
+        *dom = m;
+    }
+}
+
+template <int DP, int TR, int NT>
+__device__ __forceinline__ void l2_gload16(const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
+                                           const float* __restrict__ tnorm, int tile,
+                                           f16x8 (&sh)[(TR * DP / 8 + NT - 1) / NT], f16x8 (&sl)[(TR * DP / 8 + NT - 1) / NT],
+                                           float& nstg) {
+    constexpr int CH = TR * DP / 8, PER = (CH + NT - 1) / NT;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x + NT * j;
+        if (CH % NT == 0 || c < CH) {
+            sh[j] = reinterpret_cast<const f16x8*>(th + (size_t)tile * TR * DP)[c];
+            sl[j] = reinterpret_cast<const f16x8*>(tl + (size_t)tile * TR * DP)[c];
+        }
+    }
+    if (threadIdx.x < TR) nstg = tnorm[tile * TR + threadIdx.x];
+}
+
+template <int DP, int TR, int NT>
+__device__ __forceinline__ void l2_lstore16(_Float16* __restrict__ lh, _Float16* __restrict__ ll, float* __restrict__ lnorm,
+                                            const f16x8 (&sh)[(TR * DP / 8 + NT - 1) / NT],
+                                            const f16x8 (&sl)[(TR * DP / 8 + NT - 1) / NT], float nstg) {
+    constexpr int CH = TR * DP / 8, PER = (CH + NT - 1) / NT, ROWH = DP + 8;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x + NT * j;
+        if (CH % NT == 0 || c < CH) {
+            const int row = c / (DP / 8), c8 = c % (DP / 8);
+            *reinterpret_cast<f16x8*>(&lh[row * ROWH + 8 * c8]) = sh[j];
+            *reinterpret_cast<f16x8*>(&ll[row * ROWH + 8 * c8]) = sl[j];
+        }
+    }
+    if (threadIdx.x < TR) lnorm[threadIdx.x] = nstg;
+}
+
+// Registers [r0, r0 + RN) of a tile's scores -> the lane's running top-2 / third place (train rows in
+// ascending index order across calls with increasing ranges). The index carried is the tile-row
+// index without the lane half's 4 h (wave-uniform, an SGPR operand of the selects); the caller adds
+// 4 h to i1 / i2 at the end (ties never compare indices here: the rows arrive in ascending order).
+template <int NC, int RN = 16>
+__device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const floatx16 (&as)[NC], const float4 (&nv)[NC][4],
+                                              int base, float& b1, int& i1, float& b2, int& i2, float& b3, int r0 = 0) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = r0; r < r0 + RN; ++r) {
+            const int row = 32 * c + (r & 3) + 8 * (r >> 2);
+            const float4 n4 = nv[c][r >> 2];
+            const float nrm = (r & 3) == 0 ? n4.x : (r & 3) == 1 ? n4.y : (r & 3) == 2 ? n4.z : n4.w;
+            const float dot = am[c][r] + as[c][r];
+            const float s = fmaf(-2.f, dot, nrm);
+            top2b3_push_asc(b1, i1, b2, i2, b3, s, __builtin_amdgcn_readfirstlane(base + row));
+        }
+}
+
+// Block = WPB waves x 32 queries (WPB = 8: each staged train tile serves 256 queries, halving the
+// train stream from MALL against 4); per train tile of TR rows and each 16-dim k block: A = the tile's hi /
+// lo rows from LDS (one ds_read_b128 each: lane l holds row l & 31, dims 16 kb + 8 (l >> 5) + j),
+// B = the wave's queries hi / lo (VGPR-resident, the same dims), three accumulator chains
+// (hi.hi, hi.lo, lo.hi) interleaved. Scores, epilogue and output as mcv_l2_mfma.
+template <int DP, int TR, int WPB>
+__global__ __launch_bounds__(64 * WPB) void mcv_l2_mfma16(const _Float16* __restrict__ qh, const _Float16* __restrict__ ql,
+                                                       const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
+                                                       const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk,
+                                                       int nqPad, L2Part* __restrict__ part,
+                                                       const unsigned* __restrict__ dom, bool xcdMap) {
+    if (!l2_f16_domain(dom)) return;   // grid-uniform: the f32 kernel takes this launch
+    // XCD-aware (query block, train chunk) order: blocks are dealt round-robin over the 8 XCDs, so with
+    // chunk = linear block id mod C (C | 8) every XCD streams one chunk of the train set (3.2 MB of f16
+    // hi / lo at cfg5) through its own L2 instead of the whole set through the MALL
+    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
+    constexpr int KB = DP / 16;
+    constexpr int ROWH = DP + 8;              // halves per LDS row (16 B pad: conflict-free b128 reads)
+    constexpr int NC = TR / 32;
+    constexpr int NT = 64 * WPB;
+    constexpr int PER = (TR * DP / 8 + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) _Float16 lh[2][TR * ROWH];
+    __shared__ __attribute__((aligned(16))) _Float16 ll[2][TR * ROWH];
+    __shared__ __attribute__((aligned(16))) float lnorm[2][TR];
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int q0 = (bx * WPB + wave) * 32;
+    f16x8 bh[KB], bl[KB];
+    {
+        const f16x8* rh = reinterpret_cast<const f16x8*>(qh + (size_t)(q0 + col) * DP + 8 * h);
+        const f16x8* rl = reinterpret_cast<const f16x8*>(ql + (size_t)(q0 + col) * DP + 8 * h);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            bh[kb] = rh[2 * kb];
+            bl[kb] = rl[2 * kb];
+        }
+    }
+    const int tBegin = by * tilesPerChunk;
+    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
+    float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
+    int i1 = -1, i2 = -1;
+    // Train tiles: LDS double buffer, fed from two register staging sets, so a tile's global loads
+    // are issued two tiles before it is computed on (one tile of compute hides less than a MALL load)
+    f16x8 sh0[PER], sl0[PER], sh1[PER], sl1[PER];
+    float ns0 = 0.f, ns1 = 0.f;
+    if (tBegin < tEnd) {
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, tBegin, sh0, sl0, ns0);
+        l2_lstore16<DP, TR, NT>(lh[0], ll[0], lnorm[0], sh0, sl0, ns0);
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(tBegin + 1, tEnd - 1), sh1, sl1, ns1);
+    }
+    __syncthreads();
+    // Two accumulator sets (hi.hi and hi.lo + lo.hi chains, norms, tile index) in turn: a tile's MFMAs
+    // fill one set while the previous tile's epilogue (VALU) drains the other, with no copies. The
+    // first trip drains a dummy set: +inf norms score +inf, which changes no top-2 and no third place.
+    floatx16 xm[NC], xs[NC], ym[NC], ys[NC];
+    float4 xn[NC][4], yn[NC][4];
+    int xt = tBegin, yt = tBegin;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yn[c][j] = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ym[c][r] = ys[c][r] = 0.f;
+    // one tile t: loads of tile t + 2 into staging set (ldh, ldl), MFMAs on LDS buffer buf into (cm, cs),
+    // the epilogue of (em, es), then tile t + 1 (staging set sth / stl, loaded a tile ago) into the other
+    // LDS buffer
+    auto tile = [&](int t, f16x8 (&ldh)[PER], f16x8 (&ldl)[PER], float& ldn, const f16x8 (&sth)[PER],
+                    const f16x8 (&stl)[PER], const float& stn, floatx16 (&cm)[NC], floatx16 (&cs)[NC],
+                    float4 (&cn)[NC][4], int& ct, const floatx16 (&em)[NC], const floatx16 (&es)[NC],
+                    const float4 (&en)[NC][4], int et) {
+        const int buf = (t - tBegin) & 1;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cn[c][j] = *reinterpret_cast<const float4*>(&lnorm[buf][32 * c + 8 * j + 4 * h]);
+        ct = t;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cm[c][r] = cs[c][r] = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            f16x8 ah[NC], al[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                ah[c] = *reinterpret_cast<const f16x8*>(&lh[buf][(32 * c + col) * ROWH + 16 * kb + 8 * h]);
+                al[c] = *reinterpret_cast<const f16x8*>(&ll[buf][(32 * c + col) * ROWH + 16 * kb + 8 * h]);
+            }
+#pragma unroll
+            for (int c = 0; c < NC; ++c) cm[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], bh[kb], cm[c], 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) cs[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], bl[kb], cs[c], 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) cs[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], bh[kb], cs[c], 0, 0, 0);
+            // a share of the previous tile's epilogue (VALU) after each k block's three MFMAs
+            if constexpr (NC == 1 && KB == 8) l2_epilogue16<NC, 2>(em, es, en, et * TR, b1, i1, b2, i2, b3, 2 * kb);
+        }
+        if constexpr (!(NC == 1 && KB == 8)) l2_epilogue16<NC>(em, es, en, et * TR, b1, i1, b2, i2, b3);
+        // tile t + 2's loads issued after the MFMAs (issued ahead of them, the in-order vmcnt made the
+        // k loop wait for them); they land during the next tile
+        // unconditional (past the chunk's end: a re-read of its last tile, stored into the idle buffer),
+        // so the vmcnt waits count exact numbers of loads instead of draining the queue
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), ldh, ldl, ldn);
+        l2_lstore16<DP, TR, NT>(lh[buf ^ 1], ll[buf ^ 1], lnorm[buf ^ 1], sth, stl, stn);
+        __syncthreads();
+    };
+    // the query fragments' loads complete here, once: left pending, their first uses inside the k loop
+    // become vmcnt waits that, in steady state, drain the staging loads in flight (in-order counter)
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    for (int t = tBegin; t < tEnd; t += 2) {
+        tile(t, sh0, sl0, ns0, sh1, sl1, ns1, xm, xs, xn, xt, ym, ys, yn, yt);
+        if (t + 1 < tEnd) tile(t + 1, sh1, sl1, ns1, sh0, sl0, ns0, ym, ys, yn, yt, xm, xs, xn, xt);
+    }
+    // the last tile's set: x after an odd count of tiles, y after an even one
+    if (tBegin < tEnd) {
+        if (((tEnd - tBegin) & 1) != 0) l2_epilogue16<NC>(xm, xs, xn, xt * TR, b1, i1, b2, i2, b3);
+        else l2_epilogue16<NC>(ym, ys, yn, yt * TR, b1, i1, b2, i2, b3);
+    }
+    // the lane half's row offset (the epilogue carried wave-uniform tile-row indices)
+    if (i1 >= 0) i1 += 4 * h;
+    if (i2 >= 0) i2 += 4 * h;
+    const float ob1 = __shfl_xor(b1, 32, 64), ob2 = __shfl_xor(b2, 32, 64), ob3 = __shfl_xor(b3, 32, 64);
+    const int oi1 = __shfl_xor(i1, 32, 64), oi2 = __shfl_xor(i2, 32, 64);
+    if (h == 0) {
+        float c1 = b1, c2 = b2, c3 = b3;
+        third_fold(c1, c2, c3, ob1);
+        third_fold(c1, c2, c3, ob2);
+        third_fold(c1, c2, c3, ob3);
+        top2_push(b1, i1, b2, i2, ob1, oi1);
+        top2_push(b1, i1, b2, i2, ob2, oi2);
+        L2Part p;
+        p.b1 = b1; p.b2 = b2; p.b3 = c3; p.i1 = i1; p.i2 = i2; p.i3 = -1;
+        part[(size_t)by * nqPad + q0 + col] = p;
+    }
+}
+
 // Exact squared distance (the oracle's definition: fp64 differences, sequential sum in dim order,
 // every operation rounded as written).
 __device__ __forceinline__ double l2_exact(const float* __restrict__ q, const float* __restrict__ t, int dim) {
@@ -260,6 +526,38 @@ __device__ __forceinline__ double l2_exact(const float* __restrict__ q, const fl
         d = d + e * e;
     }
     return d;
+}
+
+// Both candidates' exact squared distances in one pass (two independent sequential chains; float4
+// loads when the rows are 16-byte aligned). Each sum is l2_exact's, operation for operation.
+__device__ __forceinline__ void l2_exact2(const float* __restrict__ q, const float* __restrict__ ta,
+                                          const float* __restrict__ tb, int dim, double& da, double& db) {
+    double a = 0, b = 0;
+    const bool v4 = (dim & 3) == 0 && (((uintptr_t)q | (uintptr_t)ta | (uintptr_t)tb) & 15) == 0;
+    if (v4) {
+        const float4 *q4 = reinterpret_cast<const float4*>(q), *a4 = reinterpret_cast<const float4*>(ta),
+                     *b4 = reinterpret_cast<const float4*>(tb);
+        for (int k = 0; k < dim / 4; ++k) {
+            const float4 x = q4[k], y = a4[k], z = b4[k];
+            const double xs[4] = {(double)x.x, (double)x.y, (double)x.z, (double)x.w};
+            const double ys[4] = {(double)y.x, (double)y.y, (double)y.z, (double)y.w};
+            const double zs[4] = {(double)z.x, (double)z.y, (double)z.z, (double)z.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const double e = xs[j] - ys[j], f = xs[j] - zs[j];
+                a = a + e * e;
+                b = b + f * f;
+            }
+        }
+    } else {
+        for (int k = 0; k < dim; ++k) {
+            const double x = (double)q[k], e = x - (double)ta[k], f = x - (double)tb[k];
+            a = a + e * e;
+            b = b + f * f;
+        }
+    }
+    da = a;
+    db = b;
 }
 
 __device__ __forceinline__ bool lex_less_d(double a, int ia, double b, int ib) {
@@ -278,7 +576,7 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
                               const float* __restrict__ qnorm, const unsigned* __restrict__ tmaxBits,
                               const float* __restrict__ qraw, const float* __restrict__ traw, int* __restrict__ idx,
                               float* __restrict__ dist, int* __restrict__ idx2, float* __restrict__ dist2,
-                              int* __restrict__ ambCount, int* __restrict__ ambList) {
+                              int* __restrict__ ambCount, int* __restrict__ ambList, const unsigned* __restrict__ dom) {
     const int q = blockIdx.x * 256 + threadIdx.x;
     if (q >= nq) return;
     float b1 = INFINITY, b2 = INFINITY, c1 = INFINITY, c2 = INFINITY, c3 = INFINITY;
@@ -295,11 +593,16 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
     double e1 = INFINITY, e2 = INFINITY;
     int j1 = -1, j2 = -1;
     const int cand[2] = {i1, i2};
+    double ec[2] = {INFINITY, INFINITY};
+    // both candidates' sums together (a missing second candidate re-reads the first's row and is
+    // skipped below; no candidate at all only when the train set is empty)
+    if (i1 >= 0)
+        l2_exact2(qr, traw + (size_t)i1 * dim, traw + (size_t)(i2 < 0 ? i1 : i2) * dim, dim, ec[0], ec[1]);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const int j = cand[c];
         if (j < 0) continue;
-        const double e = l2_exact(qr, traw + (size_t)j * dim, dim);
+        const double e = ec[c];
         if (lex_less_d(e, j, e1, j1)) { e2 = e1; j2 = j1; e1 = e; j1 = j; }
         else if (lex_less_d(e, j, e2, j2)) { e2 = e; j2 = j; }
     }
@@ -308,7 +611,22 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
     if (!certain && i2 >= 0) {
         const double qn = (double)qnorm[q], T2 = (double)__uint_as_float(*tmaxBits);
         const double u = 0x1p-24;
-        const double tol = 1.01 * (dim + 4) * u * (T2 + 2.0 * sqrt(qn * (1.0 + 1e-6)) * sqrt(T2) + qn) + 1e-30;
+        const double qa = sqrt(qn * (1.0 + 1e-6)), T = sqrt(T2);
+        double tol;
+        if (l2_f16_domain(dom)) {
+            // f16 split, x = hi + lo + r with |lo| <= 2^-11 |x| + 2^-14, |r| <= 2^-22 |x| + 2^-13 (RN;
+            // f16 subnormals flushed or not): q_i t_i - (qh th + qh tl + ql th) <= 3.01 2^-22 |q_i t_i|
+            // + 1.0012 2^-13 (|q_i| + |t_i|) + 2^-25 per dim, so with Cauchy-Schwarz the dot's error is
+            // E <= |q| T (2.2 dim u (1 + 2^-9) + 2^-20 + 3.02 u) (the f32-accumulated hi.hi chain and the
+            // 2 dim-term hi.lo / lo.hi chain, whose terms are below 2^-10 of hi.hi's, at <= 2 u per step;
+            // the split; the final add and the score's fma) + 1.25e-4 sqrt(dim) (|q| + T)
+            // + dim 2^-25
+            const double E = qa * T * (2.2 * dim * u * (1.0 + 0x1p-9) + 0x1p-20 + 3.02 * u) +
+                             1.25e-4 * sqrt((double)dim) * (qa + T) + dim * 0x1p-25;
+            tol = 1.01 * ((dim + 4) * u * (T2 + qn) + 2.0 * E) + 1e-30;
+        } else {
+            tol = 1.01 * (dim + 4) * u * (T2 + 2.0 * qa * T + qn) + 1e-30;
+        }
         const double approx3 = (double)qnorm[q] + (double)c3;
         certain = approx3 - tol > e2 * (1.0 + 1e-12);   // every other train is strictly farther
     }
@@ -351,12 +669,26 @@ __device__ __forceinline__ void l2_write_final(int q, const L2Top2d& r, int* idx
     if (dist2) dist2[q] = r.j2 >= 0 ? (float)sqrt(r.d2) : INFINITY;
 }
 
-__global__ __launch_bounds__(256) void mcv_l2_exact_scan(const float* __restrict__ qraw, const float* __restrict__ traw,
+// The queued queries in fp64, batch-interleaved [a / 8][dim][8]: the 8 values of one dimension of a
+// batch are 64 contiguous bytes, so the exact scan reads a batch's k .. k + 3 with four scalar
+// dwordx16 loads off one pointer that advances by 256 B (per-query row addresses cost ~100 scalar
+// ops per step, and one CU's scalar unit serves its four SIMDs).
+__global__ void mcv_l2_amb_convert(const float* __restrict__ qraw, int dim, const int* __restrict__ ambCount,
+                                   const int* __restrict__ ambList, double* __restrict__ qd) {
+    const int n = *ambCount;
+    const int nPad = (n + kL2ScanQ - 1) / kL2ScanQ * kL2ScanQ;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nPad * dim; e += gridDim.x * blockDim.x) {
+        const int a = e / dim, k = e - a * dim;
+        const double v = a < n ? (double)qraw[(size_t)ambList[a] * dim + k] : 0.0;
+        qd[((size_t)(a / kL2ScanQ) * dim + k) * kL2ScanQ + (a % kL2ScanQ)] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void mcv_l2_exact_scan(const double* __restrict__ qd, const float* __restrict__ traw,
                                                          int nt, int dim, const int* __restrict__ ambCount,
                                                          const int* __restrict__ ambList, L2Top2d* __restrict__ part,
                                                          int* __restrict__ idx, float* __restrict__ dist,
                                                          int* __restrict__ idx2, float* __restrict__ dist2) {
-    __shared__ double qs[kL2ScanQ][256];
     __shared__ double sd1[256], sd2[256];
     __shared__ int sj1[256], sj2[256];
     const int n = *ambCount;
@@ -368,11 +700,9 @@ __global__ __launch_bounds__(256) void mcv_l2_exact_scan(const float* __restrict
         const int a0 = batch * kL2ScanQ;
         const int nb = min(kL2ScanQ, n - a0);
         const int jb = (int)((int64_t)chunk * nt / T), je = (int)((int64_t)(chunk + 1) * nt / T);
-        for (int e = threadIdx.x; e < kL2ScanQ * dim; e += 256) {
-            const int b = e / dim, k = e % dim;
-            qs[b][k] = b < nb ? (double)qraw[(size_t)ambList[a0 + b] * dim + k] : 0.0;
-        }
-        __syncthreads();
+        // the batch's block of qd (wave-uniform addresses: scalar loads, SGPR operands; the padding
+        // members of the last batch are zeros and never reported)
+        const double* qb = qd + (size_t)batch * dim * kL2ScanQ;
         double e1[kL2ScanQ], e2[kL2ScanQ];
         int j1[kL2ScanQ], j2[kL2ScanQ];
 #pragma unroll
@@ -391,7 +721,7 @@ __global__ __launch_bounds__(256) void mcv_l2_exact_scan(const float* __restrict
                     for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
                         for (int b = 0; b < kL2ScanQ; ++b) {
-                            const double df = qs[b][k + kk] - tv[kk];
+                            const double df = qb[(k + kk) * kL2ScanQ + b] - tv[kk];
                             d[b] = d[b] + df * df;
                         }
                 }
@@ -400,7 +730,7 @@ __global__ __launch_bounds__(256) void mcv_l2_exact_scan(const float* __restrict
                     const double tv = (double)tr[k];
 #pragma unroll
                     for (int b = 0; b < kL2ScanQ; ++b) {
-                        const double df = qs[b][k] - tv;
+                        const double df = qb[k * kL2ScanQ + b] - tv;
                         d[b] = d[b] + df * df;
                     }
                 }
@@ -459,7 +789,13 @@ struct L2Work {
     DevBuf<unsigned> tmax;
     DevBuf<int> amb;   // [0] = count, [1..] = queued queries
     DevBuf<L2Top2d> scanPart;   // exact-scan partials: < kL2ScanBlocks x kL2ScanQ records
+    DevBuf<_Float16> qh, ql, th, tl;   // f16-split copies (DP <= 128)
+    DevBuf<unsigned> dom;              // max |x| over both sets (float bits): the f16 path's domain
+    DevBuf<unsigned> qmax, tmaxr;      // per-row max |x|
+    DevBuf<double> qd;                 // queued queries in fp64 (+ one batch of slack)
     hipStream_t last = nullptr; // stream of the last match (the diagnostics read the queue length there)
+    bool lastF16 = false;       // the last match launched the f16-split form (its flag decided on device)
+    bool ran = false;           // a match ran on this thread (its stream may be the null stream)
 };
 
 static L2Work& l2_work() {
@@ -473,12 +809,17 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     if (nq <= 0) return 0;
     L2Work& wk = l2_work();
     const int DP = dim <= 32 ? 32 : dim <= 64 ? 64 : dim <= 128 ? 128 : 256;
-    const int nqPad = (nq + 127) / 128 * 128;
+    const int nqPad = (nq + 255) / 256 * 256;   // whole 128-query (f32) and 128 / 256-query (f16) blocks
     static const int TRsel = [] {   // train rows per tile (variant screen: 32 or 64)
         const char* e = getenv("MCV_L2_TR");
         return e && atoi(e) == 64 ? 64 : 32;   // screened equal (scripts/sweep_l2.sh): keep one chain
     }();
-    const int TR = DP <= 128 ? TRsel : 32;
+    static const bool f16ok = [] {   // MCV_L2_F16 = 0: the f32 GEMM form only (screen)
+        const char* e = getenv("MCV_L2_F16");
+        return !(e && atoi(e) == 0);
+    }();
+    const bool f16 = f16ok && DP <= 128;   // the f16-split kernel tiles 32 train rows
+    const int TR = DP <= 128 && !f16 ? TRsel : 32;
     const int ntPad = nt > 0 ? (nt + TR - 1) / TR * TR : TR;
     const int ntTiles = ntPad / TR;
     wk.qp.ensure((size_t)nqPad * DP);
@@ -488,24 +829,66 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     wk.tmax.ensure(1);
     wk.amb.ensure((size_t)nq + 1);
     MCV_HIP(hipMemsetAsync(wk.amb.p, 0, sizeof(int), s));
+    // f16-split GEMM form for DP <= 128: the split preps record max |x|, and the f32 prep / GEMM
+    // return on the device when it is inside the f16 domain (no host round trip)
+    const unsigned* dom = nullptr;
+    if (f16) {
+        wk.qh.ensure((size_t)nqPad * DP);
+        wk.ql.ensure((size_t)nqPad * DP);
+        wk.th.ensure((size_t)ntPad * DP);
+        wk.tl.ensure((size_t)ntPad * DP);
+        wk.dom.ensure(1);
+        wk.qmax.ensure(nqPad);
+        wk.tmaxr.ensure(ntPad);
+        hipLaunchKernelGGL(mcv_l2_prep16, dim3((nqPad + 3) / 4), dim3(256), 0, s, d_q, nq, dim, DP, nqPad, wk.qh.p,
+                           wk.ql.p, wk.qn.p, 0.f, wk.qmax.p);
+        hipLaunchKernelGGL(mcv_l2_prep16, dim3((ntPad + 3) / 4), dim3(256), 0, s, d_t, nt, dim, DP, ntPad, wk.th.p,
+                           wk.tl.p, wk.tn.p, __builtin_inff(), wk.tmaxr.p);
+        hipLaunchKernelGGL(mcv_l2_dommax, dim3(1), dim3(1024), 0, s, wk.qmax.p, nq, wk.tmaxr.p, nt, wk.dom.p);
+        dom = wk.dom.p;
+    }
     hipLaunchKernelGGL(mcv_l2_prep, dim3((nqPad + 3) / 4), dim3(256), 0, s, d_q, nq, dim, DP, nqPad, wk.qp.p, wk.qn.p,
-                       0.f, (unsigned*)nullptr);
+                       0.f, dom);
     // padding rows get a +inf norm: their scores are +inf and never enter a top-2 or the third place
     hipLaunchKernelGGL(mcv_l2_prep, dim3((ntPad + 3) / 4), dim3(256), 0, s, d_t, nt, dim, DP, ntPad, wk.tp.p, wk.tn.p,
-                       __builtin_inff(), (unsigned*)nullptr);
+                       __builtin_inff(), dom);
     hipLaunchKernelGGL(mcv_l2_maxnorm, dim3(1), dim3(1024), 0, s, wk.tn.p, nt, wk.tmax.p);
     const int qblocks = nqPad / 128;
     int nchunks = (2048 + qblocks - 1) / qblocks;
+    if (f16) nchunks = 8;   // one train chunk per XCD (mcv_l2_mfma16's block order)
     if (nchunks > ntTiles) nchunks = ntTiles;
     if (nchunks < 1) nchunks = 1;
     const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
     nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
+    static const bool xcdOk = [] {   // MCV_XCD_MAP = 0: plain (query block, chunk) order (screen)
+        const char* e = getenv("MCV_XCD_MAP");
+        return e ? atoi(e) != 0 : true;
+    }();
+    const bool xcdMap = xcdOk && (8 % nchunks) == 0;
     wk.part.ensure((size_t)nchunks * nqPad);
     dim3 grid(qblocks, nchunks);
     {
         ProfScope ps("l2_mfma", s);
 #define MCV_L2_LAUNCH(D, T) hipLaunchKernelGGL((mcv_l2_mfma<D, T>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, \
-                                               ntTiles, tilesPerChunk, nqPad, wk.part.p)
+                                               ntTiles, tilesPerChunk, nqPad, wk.part.p, dom)
+        static const int wpb = [] {   // waves (32 queries each) per f16 block: 8, or 4 (screen)
+            const char* e = getenv("MCV_L2_WPB");
+            return e && atoi(e) == 4 ? 4 : 8;
+        }();
+#define MCV_L2_LAUNCH16(D, W) hipLaunchKernelGGL((mcv_l2_mfma16<D, 32, W>), dim3(nqPad / (32 * W), nchunks), \
+                                                 dim3(64 * W), 0, s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, \
+                                                 tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
+        if (f16) {
+            switch (DP * 10 + wpb) {
+                case 324: MCV_L2_LAUNCH16(32, 4); break;
+                case 328: MCV_L2_LAUNCH16(32, 8); break;
+                case 644: MCV_L2_LAUNCH16(64, 4); break;
+                case 648: MCV_L2_LAUNCH16(64, 8); break;
+                case 1284: MCV_L2_LAUNCH16(128, 4); break;
+                default: MCV_L2_LAUNCH16(128, 8); break;
+            }
+        }
+#undef MCV_L2_LAUNCH16
         switch (DP) {
             case 32: if (TR == 64) MCV_L2_LAUNCH(32, 64); else MCV_L2_LAUNCH(32, 32); break;
             case 64: if (TR == 64) MCV_L2_LAUNCH(64, 64); else MCV_L2_LAUNCH(64, 32); break;
@@ -515,17 +898,21 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
 #undef MCV_L2_LAUNCH
     }
     hipLaunchKernelGGL(mcv_l2_refine, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nqPad, nchunks, nt, dim,
-                       wk.qn.p, wk.tmax.p, d_q, d_t, d_idx, d_dist, d_idx2, d_dist2, wk.amb.p, wk.amb.p + 1);
+                       wk.qn.p, wk.tmax.p, d_q, d_t, d_idx, d_dist, d_idx2, d_dist2, wk.amb.p, wk.amb.p + 1, dom);
     {
         ProfScope ps("l2_exact", s);
         wk.scanPart.ensure((size_t)kL2ScanBlocks * kL2ScanQ);
-        hipLaunchKernelGGL(mcv_l2_exact_scan, dim3(kL2ScanBlocks), dim3(256), 0, s, d_q, d_t, nt, dim, wk.amb.p,
+        wk.qd.ensure((size_t)(nq + kL2ScanQ) * dim);
+        hipLaunchKernelGGL(mcv_l2_amb_convert, dim3(256), dim3(256), 0, s, d_q, dim, wk.amb.p, wk.amb.p + 1, wk.qd.p);
+        hipLaunchKernelGGL(mcv_l2_exact_scan, dim3(kL2ScanBlocks), dim3(256), 0, s, wk.qd.p, d_t, nt, dim, wk.amb.p,
                            wk.amb.p + 1, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2);
         hipLaunchKernelGGL(mcv_l2_exact_merge, dim3(8), dim3(256), 0, s, wk.amb.p, wk.amb.p + 1, wk.scanPart.p, d_idx,
                            d_dist, d_idx2, d_dist2);
     }
     MCV_HIP(hipGetLastError());
     wk.last = s;
+    wk.lastF16 = f16;
+    wk.ran = true;
     return nq;
 }
 
@@ -538,6 +925,16 @@ int l2_last_exact_scans() {
     MCV_HIP(hipMemcpyAsync(&n, wk.amb.p, sizeof(int), hipMemcpyDeviceToHost, wk.last));
     MCV_HIP(hipStreamSynchronize(wk.last));
     return n;
+}
+
+int l2_last_gemm_form() {
+    L2Work& wk = l2_work();
+    if (!wk.ran) return 0;
+    if (!wk.lastF16) return 32;
+    unsigned d = 0;
+    MCV_HIP(hipMemcpyAsync(&d, wk.dom.p, sizeof(unsigned), hipMemcpyDeviceToHost, wk.last));
+    MCV_HIP(hipStreamSynchronize(wk.last));
+    return d < kL2F16MaxBits ? 16 : 32;
 }
 
 }  // namespace mcv

@@ -99,3 +99,7 @@ extern "C" MCV_API int mcvMatchL2Device(const float* d_q, int nq, const float* d
 extern "C" MCV_API int mcvL2LastExactScans(void) {
     MCV_GUARD(-1, { return l2_last_exact_scans(); })
 }
+
+extern "C" MCV_API int mcvL2LastGemmForm(void) {
+    MCV_GUARD(-1, { return l2_last_gemm_form(); })
+}

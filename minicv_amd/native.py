@@ -132,6 +132,7 @@ SIGNATURES = {
     "mcvRansacFinalize": (_I, [_P, _P, _I, _P, _I64, _P, _P, _P]),
     "mcvReplayInit": (None, [_P, _I]),
     "mcvL2LastExactScans": (_I, []),
+    "mcvL2LastGemmForm": (_I, []),
     "mcvReplayChunk": (_I, [_P, _P, _I64, _I64, _I, _I, _D, _I]),
     "mcvReplayChunkModels": (_I, [_P, _P, _I64, _I64, _I, _I, _I, _D, _I]),
     "mcvMatchHammingDevice": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),

@@ -124,6 +124,20 @@ def test_l2_duplicated_train_exact_scan_cost(gpu, oracle):
     assert scans >= 0.9 * len(q)
 
 
+@pytest.mark.parametrize("scale,shift", [(1.0, 0.0), (32767.0 / 255.0, 0.0), (32768.0 / 255.0, 0.0), (1e4, 0.0),
+                                         (1e-6, 0.0), (3e-9, 0.0), (1.0, -127.5), (2.0 ** -20, 2.0 ** -20)])
+def test_l2_f16_split_domain(gpu, oracle, scale, shift):
+    """The f16-split GEMM form runs while every |x| < 2^15 (the first two scales, the tiny ones whose
+    split parts are f16 subnormals, signed data); at max |x| = 2^15 and above the f32 form takes the
+    launch (device-side flag). Either way the answer is the oracle's, bit for bit."""
+    q, t, _ = S.l2_problem(300, 1200, dim=128, seed=23)
+    q = (q.astype(np.float64) * scale + shift).astype(np.float32)
+    t = (t.astype(np.float64) * scale + shift).astype(np.float32)
+    if scale == 32768.0 / 255.0:
+        t[0, 0] = np.float32(32768.0)   # exactly at the bound: out of the f16 domain
+    check_l2(oracle, q, t)
+
+
 def test_l2_ties_lowest_index(gpu):
     rng = np.random.default_rng(3)
     base = S.sift_like(40, 128, rng)
