@@ -108,7 +108,9 @@ MCV_API int  cvFivePoint(const mcvV2d* pa, const mcvV2d* pb, mcvM33d* Es);
  * outInliers (caller: N ints) = RANSAC inlier indices.
  * cvSolvePnP: kinds 2 / 5 need N == 4 (AP3P, the 4th point picks the solution); 1 / 3 / 4:
  * EPnP on all points; 0 (ITERATIVE) and values outside 0..6: EPnP, then LM over all points;
- * 6 (SQPNP) fails (false, mcvGetLastError says so): SQPnP's estimator is not provided. */
+ * 6 (SQPNP, N >= 3): OpenCV's sqpnp::PoseSolver on the undistorted normalised points (computeOmega's
+ * sums on the GPU, the SQP search on the host; its assertion failures return false with the reason,
+ * no solution in front of the camera returns false). */
 MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
                         const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec);
 MCV_API mcvBool cvSolvePnPRansac(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,
@@ -463,6 +465,10 @@ MCV_API int mcvHostSampsonCert(const float* pts4, int N, const double* F9, float
 /* Host build of solveAp3p's computation (mu3 / mv3 pixels, W9 = 3 world points), R36 / t12 out. */
 MCV_API int mcvHostSolveAp3p(const double* mu3, const double* mv3, const double* W9, double inv_fx, double inv_fy,
                              double cx_fx, double cy_fy, double* R36, double* t12);
+/* Host twin of cvSolvePnP kind 6 (SQPnP) on double img (N x 2) / world (N x 3), cam8 as above: the
+ * computeOmega sums in the device passes' block order, then the same host solve. R9 / t3 = the first
+ * solution; returns the solution count, 0 (none), or -1 / -2 / -3 (computeOmega's assertions). */
+MCV_API int mcvHostSqpnp(const double* img, const double* world, int N, const double* cam8, double* R9, double* t3);
 MCV_API void mcvHostRodrigues(const double* r, double* R, double* dR27);
 MCV_API void mcvHostRodriguesInv(const double* R, double* r);
 /* OpenCV's sample stream (MCV_FLAG_CV_SAMPLER) on the host: rows [0, rows) of m indices each for the

@@ -146,9 +146,12 @@ void launch_pnp_one(const void* d_pts, int N, const double* cam8, Sampler smp, i
 void launch_pnp_solve5(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s);
 void launch_mask_compact(const uint8_t* d_mask, int N, int* d_idx, int* d_count, hipStream_t s);
 // EPnP over n points: d_pts (+ optional index list d_idx) fp32 PnpPoints, or d_img / d_world fp64.
+// normalized: d_us = undistortPoints' normalised coordinates (SQPnP) instead of x f + c (EPnP).
 void launch_epnp_prep(const void* d_pts, const int* d_idx, const double* d_img, const double* d_world, int n,
-                      const double* cam8, double* d_pw, double* d_us, hipStream_t s);
-enum { kEpnpPassSumPw = 0, kEpnpPassPw0 = 1, kEpnpPassMtm = 2, kEpnpPassPc = 3, kEpnpPassAbt = 4, kEpnpPassReproj = 5 };
+                      const double* cam8, double* d_pw, double* d_us, hipStream_t s, bool normalized = false);
+// SQPnP passes (sqpnp.h): the 39 computeOmega sums; the positive-depth count of the pose R[0] / t[0].
+enum { kEpnpPassSumPw = 0, kEpnpPassPw0 = 1, kEpnpPassMtm = 2, kEpnpPassPc = 3, kEpnpPassAbt = 4, kEpnpPassReproj = 5,
+       kEpnpPassSqp = 6, kEpnpPassSqpDepth = 7 };
 struct EpnpPassArgs {
     EpnpCtrl C;
     EpnpCam cam;

@@ -684,7 +684,26 @@ __global__ void mcv_l2_amb_convert(const float* __restrict__ qraw, int dim, cons
     }
 }
 
-__global__ __launch_bounds__(256) void mcv_l2_exact_scan(const double* __restrict__ qd, const float* __restrict__ traw,
+// The train set transposed ([dim][nt]) for the exact scan's coalesced reads; skipped on the device
+// when nothing is queued.
+__global__ __launch_bounds__(256) void mcv_l2_transpose_train(const float* __restrict__ traw, int nt, int dim,
+                                                              const int* __restrict__ ambCount, float* __restrict__ tT) {
+    if (*ambCount == 0) return;
+    __shared__ float tile[64][65];
+    const int j0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int j = j0 + r, k = k0 + tx;
+        tile[r][tx] = j < nt && k < dim ? traw[(size_t)j * dim + k] : 0.f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int k = k0 + r, j = j0 + tx;
+        if (k < dim && j < nt) tT[(size_t)k * nt + j] = tile[tx][r];
+    }
+}
+
+__global__ __launch_bounds__(256) void mcv_l2_exact_scan(const double* __restrict__ qd, const float* __restrict__ tT,
                                                          int nt, int dim, const int* __restrict__ ambCount,
                                                          const int* __restrict__ ambList, L2Top2d* __restrict__ part,
                                                          int* __restrict__ idx, float* __restrict__ dist,
@@ -707,30 +726,31 @@ __global__ __launch_bounds__(256) void mcv_l2_exact_scan(const double* __restric
         int j1[kL2ScanQ], j2[kL2ScanQ];
 #pragma unroll
         for (int b = 0; b < kL2ScanQ; ++b) { e1[b] = e2[b] = INFINITY; j1[b] = j2[b] = -1; }
-        const bool vec4 = (dim & 3) == 0 && ((uintptr_t)traw & 15) == 0;   // 16-byte aligned rows: float4 loads
         for (int j = jb + threadIdx.x; j < je; j += 256) {
-            const float* tr = traw + (size_t)j * dim;
+            // lane = train row: dimension k of 64 consecutive rows is one coalesced 256-byte load of
+            // the transposed copy (row-per-lane reads of the row-major set touched 64 cache lines per
+            // load and re-fetched each line once per 16 bytes used); four dims loaded one step ahead
+            const float* tc = tT + j;
             double d[kL2ScanQ];
 #pragma unroll
             for (int b = 0; b < kL2ScanQ; ++b) d[b] = 0.0;
-            if (vec4) {
-                for (int k = 0; k < dim; k += 4) {
-                    const float4 t4 = *reinterpret_cast<const float4*>(tr + k);
-                    const double tv[4] = {(double)t4.x, (double)t4.y, (double)t4.z, (double)t4.w};
+            float nx[4];
 #pragma unroll
-                    for (int kk = 0; kk < 4; ++kk)
+            for (int kk = 0; kk < 4; ++kk) nx[kk] = kk < dim ? tc[(size_t)kk * nt] : 0.f;
+            for (int k = 0; k < dim; k += 4) {
+                float cur[4];
 #pragma unroll
-                        for (int b = 0; b < kL2ScanQ; ++b) {
-                            const double df = qb[(k + kk) * kL2ScanQ + b] - tv[kk];
-                            d[b] = d[b] + df * df;
-                        }
+                for (int kk = 0; kk < 4; ++kk) {
+                    cur[kk] = nx[kk];
+                    nx[kk] = k + 4 + kk < dim ? tc[(size_t)(k + 4 + kk) * nt] : 0.f;
                 }
-            } else {
-                for (int k = 0; k < dim; ++k) {
-                    const double tv = (double)tr[k];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    if (k + kk >= dim) break;   // wave-uniform
+                    const double tv = (double)cur[kk];
 #pragma unroll
                     for (int b = 0; b < kL2ScanQ; ++b) {
-                        const double df = qb[k * kL2ScanQ + b] - tv;
+                        const double df = qb[(k + kk) * kL2ScanQ + b] - tv;
                         d[b] = d[b] + df * df;
                     }
                 }
@@ -793,6 +813,7 @@ struct L2Work {
     DevBuf<unsigned> dom;              // max |x| over both sets (float bits): the f16 path's domain
     DevBuf<unsigned> qmax, tmaxr;      // per-row max |x|
     DevBuf<double> qd;                 // queued queries in fp64 (+ one batch of slack)
+    DevBuf<float> tT;                  // the train set transposed (exact scan)
     hipStream_t last = nullptr; // stream of the last match (the diagnostics read the queue length there)
     bool lastF16 = false;       // the last match launched the f16-split form (its flag decided on device)
     bool ran = false;           // a match ran on this thread (its stream may be the null stream)
@@ -904,7 +925,11 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         wk.scanPart.ensure((size_t)kL2ScanBlocks * kL2ScanQ);
         wk.qd.ensure((size_t)(nq + kL2ScanQ) * dim);
         hipLaunchKernelGGL(mcv_l2_amb_convert, dim3(256), dim3(256), 0, s, d_q, dim, wk.amb.p, wk.amb.p + 1, wk.qd.p);
-        hipLaunchKernelGGL(mcv_l2_exact_scan, dim3(kL2ScanBlocks), dim3(256), 0, s, wk.qd.p, d_t, nt, dim, wk.amb.p,
+        wk.tT.ensure((size_t)(nt > 0 ? nt : 1) * dim);
+        if (nt > 0)
+            hipLaunchKernelGGL(mcv_l2_transpose_train, dim3((nt + 63) / 64, (dim + 63) / 64), dim3(256), 0, s, d_t, nt,
+                               dim, wk.amb.p, wk.tT.p);
+        hipLaunchKernelGGL(mcv_l2_exact_scan, dim3(kL2ScanBlocks), dim3(256), 0, s, wk.qd.p, wk.tT.p, nt, dim, wk.amb.p,
                            wk.amb.p + 1, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2);
         hipLaunchKernelGGL(mcv_l2_exact_merge, dim3(8), dim3(256), 0, s, wk.amb.p, wk.amb.p + 1, wk.scanPart.p, d_idx,
                            d_dist, d_idx2, d_dist2);

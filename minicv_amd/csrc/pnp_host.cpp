@@ -15,6 +15,7 @@
 #include "plan.h"
 #include "hyp_pnp.h"
 #include "pnp_pk.h"
+#include "sqpnp.h"
 
 #include <cmath>
 #include <cfloat>
@@ -317,6 +318,47 @@ static void epnp_device(Plan& P, const double* d_pw, const double* d_us, int n, 
     }
 }
 
+// solvePnP(SOLVEPNP_SQPNP) (reference MiniCVNative.cpp:72-74, :82): undistortPoints' normalised
+// coordinates and the computeOmega sums as one device pass, the SQPnP algebra on the host (sqpnp.h),
+// the positive-depth count of positiveMajorityDepths as a device pass when the centroid check fails.
+// Returns sqpnp_from_sums' code; R9 / t3: the first solution.
+static int sqpnp_device(Plan& P, const double* d_pw, const double* d_us, int n, double* R9, double* t3,
+                        hipStream_t s) {
+    EpnpPassArgs A;
+    std::memset(&A, 0, sizeof(A));
+    const int nblk = (n + kEpnpBlock - 1) / kEpnpBlock;
+    std::vector<double> part;
+    auto pass = [&](int mode, int nacc, double* out) {
+        P.part.ensure((size_t)nacc * nblk);
+        launch_epnp_pass(mode, d_pw, d_us, n, A, nacc, P.part.p, s);
+        MCV_HIP(hipGetLastError());
+        part.resize((size_t)nacc * nblk);
+        MCV_HIP(hipMemcpyAsync(part.data(), P.part.p, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+        for (int a = 0; a < nacc; ++a) {
+            double t = 0;
+            for (int b = 0; b < nblk; ++b) t += part[(size_t)a * nblk + b];
+            out[a] = t;
+        }
+    };
+    double sums[kSqpSums];
+    pass(kEpnpPassSqp, kSqpSums, sums);
+    auto npos = [&](const double* rh, const double* t) {
+        for (int k = 0; k < 3; ++k) A.R[0][2][k] = rh[6 + k];
+        A.t[0][2] = t[2];
+        double c;
+        pass(kEpnpPassSqpDepth, 1, &c);
+        return (int)c;
+    };
+    double rh[9], t[3];
+    const int r = sqpnp_from_sums(sums, n, npos, rh, t);
+    if (r > 0) {
+        std::memcpy(R9, rh, sizeof(rh));
+        std::memcpy(t3, t, sizeof(t));
+    }
+    return r;
+}
+
 // solvePnPRansac's final EPnP: the inliers (compressElems order) of the float points as doubles,
 // image points through undistortPoints with a double result.
 static void epnp_inliers(Plan& P, const void* d_pts, int N, const uint8_t* d_mask, double* R9, double* t3,
@@ -486,14 +528,10 @@ extern "C" MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* wor
                                    const double* distortionCoeffs, const int solverKind, mcvV3d* tVec, mcvV3d* rVec) {
     MCV_GUARD(false, {
         if (!imgPoints || !worldPoints || !tVec || !rVec) fail("cvSolvePnP: null argument");
-        if (N < 4) fail("cvSolvePnP: need at least 4 correspondences (N=%d)", N);
         // solverKind as MiniCVNative.cpp:54-75 maps it (6 = SQPNP, unknown = ITERATIVE)
         const int kind = solverKind >= 0 && solverKind <= 6 ? solverKind : 0;
-        if (kind == 6)
-            // SOLVEPNP_SQPNP (MiniCVNative.cpp:72-74) is a different estimator (the global minimum of the
-            // object-space error by SQP over the null space of Omega); it is not restated here, and this
-            // export fails rather than answer with another estimator's pose
-            fail("cvSolvePnP: solverKind 6 (SOLVEPNP_SQPNP) is not provided by this library");
+        // solvePnPGeneric's point-count assertion: SQPnP from 3 points, the others from 4
+        if (N < (kind == 6 ? 3 : 4)) fail("cvSolvePnP: need at least %d correspondences (N=%d)", kind == 6 ? 3 : 4, N);
         const bool p3p = kind == 2 || kind == 5;
         if (p3p && N != 4) fail("cvSolvePnP: P3P / AP3P need exactly 4 points (N=%d)", N);
         require_device();
@@ -502,6 +540,27 @@ extern "C" MCV_API mcvBool cvSolvePnP(const mcvV2d* imgPoints, const mcvV3d* wor
         PnpResult r;
         if (p3p) {
             r = pnp_ransac(P, imgPoints, worldPoints, N, K.M, distortionCoeffs, pnp_config(1, 1.f, 0.99, kind), s);
+        } else if (kind == 6) {
+            set_camera(P, K.M, distortionCoeffs);
+            P.raw.ensure((size_t)N * 5);
+            MCV_HIP(hipMemcpyAsync(P.raw.p, imgPoints, (size_t)N * sizeof(mcvV2d), hipMemcpyHostToDevice, s));
+            MCV_HIP(hipMemcpyAsync(P.raw.p + 2 * (size_t)N, worldPoints, (size_t)N * sizeof(mcvV3d),
+                                   hipMemcpyHostToDevice, s));
+            P.epw.ensure((size_t)3 * N);
+            P.eus.ensure((size_t)2 * N);
+            launch_epnp_prep(nullptr, nullptr, P.raw.p, P.raw.p + 2 * (size_t)N, N, P.pnpCam, P.epw.p, P.eus.p, s,
+                             true);
+            MCV_HIP(hipGetLastError());
+            double R9[9];
+            const int code = sqpnp_device(P, P.epw.p, P.eus.p, N, R9, r.t, s);
+            // computeOmega's CV_Asserts (an exception in OpenCV): a failure with the reason
+            if (code == -1) fail("cvSolvePnP(SQPNP): point coordinate variance below 1e-5 (degenerate image points)");
+            if (code == -2) fail("cvSolvePnP(SQPNP): Omega's largest singular value below 1e-7");
+            if (code == -3) fail("cvSolvePnP(SQPNP): Omega's null space has more than 6 dimensions");
+            if (code > 0) {
+                rodrigues_inv(R9, r.r);
+                r.ok = true;
+            }
         } else {
             // EPnP on all points in double (solvePnPGeneric keeps the caller's CV_64F points);
             // ITERATIVE: then LM over all points from that pose (the reference's DLT or homography
@@ -545,6 +604,45 @@ static void refine_common(const mcvV2d* img, const mcvV3d* world, int N, const m
     else pnp_lm(P, P.ptsd.p, N, nullptr, r, t, 20, s);
     rVec->X = r[0]; rVec->Y = r[1]; rVec->Z = r[2];
     tVec->X = t[0]; tVec->Y = t[1]; tVec->Z = t[2];
+}
+
+extern "C" MCV_API int mcvHostSqpnp(const double* img, const double* world, int N, const double* cam8, double* R9,
+                                    double* t3) {
+    MCV_GUARD(-4, {
+        if (!img || !world || !cam8 || !R9 || !t3 || N < 3) fail("mcvHostSqpnp: bad argument");
+        PnpCamera c;
+        c.fx = cam8[0]; c.fy = cam8[1]; c.cx = cam8[2]; c.cy = cam8[3];
+        c.k1 = cam8[4]; c.k2 = cam8[5]; c.p1 = cam8[6]; c.p2 = cam8[7];
+        double sums[kSqpSums];
+        for (int a = 0; a < kSqpSums; ++a) sums[a] = 0;
+        for (int b0 = 0; b0 < N; b0 += kEpnpBlock) {   // mcv_epnp_pass's order: blocks, each from 0
+            const int b1 = std::min(N, b0 + kEpnpBlock);
+            double part[kSqpSums];
+            for (int a = 0; a < kSqpSums; ++a) part[a] = 0;
+            for (int i = b0; i < b1; ++i) {
+                double x, y;
+                pnp_undistort(c, img[2 * (size_t)i], img[2 * (size_t)i + 1], x, y);
+                const double* P = world + 3 * (size_t)i;
+                for (int a = 0; a < kSqpSums; ++a) part[a] += sqpnp_term(x, y, P[0], P[1], P[2], a);
+            }
+            for (int a = 0; a < kSqpSums; ++a) sums[a] += part[a];
+        }
+        auto npos = [&](const double* rh, const double* t) {
+            int k = 0;
+            for (int i = 0; i < N; ++i) {
+                const double* P = world + 3 * (size_t)i;
+                k += rh[6] * P[0] + rh[7] * P[1] + rh[8] * P[2] + t[2] > 0;
+            }
+            return k;
+        };
+        double rh[9], t[3];
+        const int r = sqpnp_from_sums(sums, N, npos, rh, t);
+        if (r > 0) {
+            std::memcpy(R9, rh, sizeof(rh));
+            std::memcpy(t3, t, sizeof(t));
+        }
+        return r;
+    })
 }
 
 extern "C" MCV_API void cvRefinePnPLM(const mcvV2d* imgPoints, const mcvV3d* worldPoints, const int N, const mcvM33d K,

@@ -18,6 +18,7 @@
 #include "mcv_common.h"
 #include "hyp_pnp.h"
 #include "pnp_pk.h"
+#include "sqpnp.h"
 #include "reduce.h"
 #include "kernels.h"
 #include <cstdlib>
@@ -506,13 +507,13 @@ __global__ __launch_bounds__(256) void mcv_epnp_prep_f32(const PnpPoint* __restr
 
 __global__ __launch_bounds__(256) void mcv_epnp_prep_f64(const double* __restrict__ img, const double* __restrict__ world,
                                                          int n, PnpCamera c, double* __restrict__ pw,
-                                                         double* __restrict__ us) {
+                                                         double* __restrict__ us, bool normalized) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     double x, y;
     pnp_undistort(c, img[2 * (size_t)i], img[2 * (size_t)i + 1], x, y);
-    us[2 * (size_t)i] = x * c.fx + c.cx;
-    us[2 * (size_t)i + 1] = y * c.fy + c.cy;
+    us[2 * (size_t)i] = normalized ? x : x * c.fx + c.cx;
+    us[2 * (size_t)i + 1] = normalized ? y : y * c.fy + c.cy;
     for (int k = 0; k < 3; ++k) pw[3 * (size_t)i + k] = world[3 * (size_t)i + k];
 }
 
@@ -550,6 +551,10 @@ __device__ __forceinline__ void epnp_pass_term(const double* __restrict__ pw, co
         epnp_alphas(A.C, p, al);
         epnp_pc(al, A.ccs[N], pc);
         t[0] = (pc[j] - A.pc0[N][j]) * (p[k] - A.pw0[k]);
+    } else if (MODE == kEpnpPassSqp) {
+        t[0] = sqpnp_term(us[2 * (size_t)i], us[2 * (size_t)i + 1], p[0], p[1], p[2], acc);
+    } else if (MODE == kEpnpPassSqpDepth) {
+        t[0] = A.R[0][2][0] * p[0] + A.R[0][2][1] * p[1] + A.R[0][2][2] * p[2] + A.t[0][2] > 0 ? 1.0 : 0.0;
     } else {
         t[0] = epnp_reproj_term(A.R[acc], A.t[acc], A.cam, p, us[2 * (size_t)i], us[2 * (size_t)i + 1]);
     }
@@ -747,14 +752,14 @@ void launch_mask_compact(const uint8_t* d_mask, int N, int* d_idx, int* d_count,
 }
 
 void launch_epnp_prep(const void* d_pts, const int* d_idx, const double* d_img, const double* d_world, int n,
-                      const double* cam8, double* d_pw, double* d_us, hipStream_t s) {
+                      const double* cam8, double* d_pw, double* d_us, hipStream_t s, bool normalized) {
     if (n <= 0) return;
     if (d_pts)
         hipLaunchKernelGGL(mcv_epnp_prep_f32, dim3((n + 255) / 256), dim3(256), 0, s, (const PnpPoint*)d_pts, d_idx, n,
                            to_cam(cam8), d_pw, d_us);
     else
         hipLaunchKernelGGL(mcv_epnp_prep_f64, dim3((n + 255) / 256), dim3(256), 0, s, d_img, d_world, n, to_cam(cam8),
-                           d_pw, d_us);
+                           d_pw, d_us, normalized);
 }
 
 void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, const EpnpPassArgs& a, int nacc,
@@ -767,6 +772,8 @@ void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, c
         case kEpnpPassMtm: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassMtm>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
         case kEpnpPassPc: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassPc>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
         case kEpnpPassAbt: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassAbt>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
+        case kEpnpPassSqp: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSqp>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
+        case kEpnpPassSqpDepth: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSqpDepth>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
         default: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassReproj>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part);
     }
 }

@@ -156,6 +156,7 @@ SIGNATURES = {
     "mcvHostPnPEpnp": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
     "mcvHostPnpCert": (_I, [_P, _I, _P, _P, _P, C.c_float, _I, _P, _P]),
     "mcvHostSampsonCert": (_I, [_P, _I, _P, C.c_float, _I, _P, _P]),
+    "mcvHostSqpnp": (_I, [_P, _P, _I, _P, _P, _P]),
     "mcvTestPnpSweep": (_I, [_P, _I, _P, _P, _I, C.c_float, _I, _I, _P]),
     "mcvHostEpnp5": (None, [_P, _P, _P, _P, _P]),
     "mcvHostSolveAp3p": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _P]),

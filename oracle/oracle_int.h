@@ -50,5 +50,6 @@ void orc_epnp5_f32(const float* p5, const double* cam8, double* R, double* t);
 int orc_pnp_hypothesis_epnp(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R,
                             double* t, int* idx_out);
 void orc_epnp_points(const double* img, const double* world, int n, const double* cam8, double* R, double* t);
+int orc_sqpnp(const double* img, const double* world, int n, const double* cam8, double* rvec, double* tvec);
 
 #endif

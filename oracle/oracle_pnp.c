@@ -676,18 +676,20 @@ int orc_solve_pnp_ransac(const double* img, const double* world, int N, const do
                                   bestOut, nthreads);
 }
 
-/* cvSolvePnP for the EPnP family (1, 3, 4: EPnP on all double points) and ITERATIVE / SQPNP (0, 6:
- * that pose, then LM over all points as float PnpPoints). Returns 1, or 0 for a non-finite pose. */
+/* cvSolvePnP for the EPnP family (1, 3, 4: EPnP on all double points), ITERATIVE (0 and unknown
+ * kinds: that pose, then LM over all points as float PnpPoints) and SQPNP (6: oracle_sqpnp.c).
+ * Returns 1, or 0 for a non-finite pose / no SQPnP solution. */
 int orc_solve_pnp(const double* img, const double* world, int N, const double* K9, const double* dist4, int kind,
                   double* rvec, double* tvec) {
     double cam8[8] = {K9[0], K9[4], K9[2], K9[5], dist4 ? dist4[0] : 0, dist4 ? dist4[1] : 0, dist4 ? dist4[2] : 0,
                       dist4 ? dist4[3] : 0};
+    if (kind == 6) return orc_sqpnp(img, world, N, cam8, rvec, tvec) > 0;
     double R[9];
     orc_epnp_points(img, world, N, cam8, R, tvec);
     orc_rodrigues_inv(R, rvec);
     for (int k = 0; k < 3; ++k)
         if (!isfinite(rvec[k]) || !isfinite(tvec[k])) return 0;
-    if (kind == 0 || kind == 6 || kind < 0 || kind > 6) {
+    if (kind == 0 || kind < 0 || kind > 6) {
         float* pts = (float*)calloc((size_t)N * 8, sizeof(float));
         for (int i = 0; i < N; ++i) {
             float* p = pts + 8 * (size_t)i;

@@ -60,6 +60,7 @@ _SIGS = {
     "orc_pnp_counts_k": (None, [_P, _I, _P, _U64, _I64, _I64, _F, _I, _I, _P, _I]),
     "orc_solve_pnp_ransac_k": (_I, [_P, _P, _I, _P, _P, _D, _D, _I, _U64, _I, _I, _P, _P, _P, _P, _I]),
     "orc_solve_pnp": (_I, [_P, _P, _I, _P, _P, _I, _P, _P]),
+    "orc_sqpnp_pose": (_I, [_P, _P, _I, _P, _P, _P]),
     "orc_epnp": (None, [_P, _P, _I, _P, _P, _P]),
     "orc_epnp5_f32": (None, [_P, _P, _P, _P]),
     "orc_pnp_hypothesis_epnp": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
@@ -450,6 +451,16 @@ def solve_pnp(img, world, K, dist=None, kind=1):
     r, t = np.zeros(3), np.zeros(3)
     ok = load().orc_solve_pnp(ptr(img), ptr(world), img.shape[0], ptr(K9), ptr(d), int(kind), ptr(r), ptr(t))
     return bool(ok), r, t
+
+
+def sqpnp_pose(img, world, cam8):
+    """oracle_sqpnp.c's solve -> (code, R (3 x 3), t): code > 0 = solution count."""
+    img = np.ascontiguousarray(img, dtype=np.float64)
+    world = np.ascontiguousarray(world, dtype=np.float64)
+    c8 = np.ascontiguousarray(cam8, dtype=np.float64)
+    R, t = np.zeros(9), np.zeros(3)
+    code = load().orc_sqpnp_pose(ptr(img), ptr(world), img.shape[0], ptr(c8), ptr(R), ptr(t))
+    return code, R.reshape(3, 3), t
 
 
 def pnp_count(pts8, c8, R, t, thr2, fused=False):

@@ -22,6 +22,7 @@
 #include "hyp_homography.h"
 #include "hyp_pnp.h"
 #include "hyp_scaled.h"
+#include "sqpnp.h"
 
 extern "C" {
 int orc_h_hypothesis(const float* pts4, int N, uint64_t seed, int64_t hyp, double* H, float* hf, int* idx_out);
@@ -36,6 +37,7 @@ int orc_solve_pnp_ransac_k(const double* img, const double* world, int N, const 
                            double* tvec, uint8_t* mask, int64_t* bestOut, int nthreads);
 int orc_solve_pnp(const double* img, const double* world, int N, const double* K9, const double* dist4, int kind,
                   double* rvec, double* tvec);
+int orc_sqpnp_pose(const double* img, const double* world, int n, const double* cam8, double* rh9, double* t3);
 int orc_e_solve5_ref(const double* x1, const double* y1, const double* x2, const double* y2, double* Eout);
 void orc_set_fast_minimal(int v);
 int orc_find_homography(const double* src, const double* dst, int N, double thr, double conf, int maxIters, int method,
@@ -218,6 +220,30 @@ int main() {
         }
         k = orc_solve_pnp(img.data(), w3.data(), N, K9, d4, 1, rv, tv);
         expect(k >= 0, "solve_pnp", k, 0);
+        // SQPnP: sqpnp.h's host solve over the same sums (sequential: N <= 1024) equals oracle_sqpnp.c
+        for (int n : {3, 4, 7, N}) {
+            const double cam8[8] = {800, 820, 640, 360, 0, 0, 0, 0};
+            double sums[mcv::kSqpSums] = {0};
+            for (int i = 0; i < n; ++i) {
+                mcv::PnpCamera pc;
+                pc.fx = 800; pc.fy = 820; pc.cx = 640; pc.cy = 360; pc.k1 = pc.k2 = pc.p1 = pc.p2 = 0;
+                double x, y;
+                mcv::pnp_undistort(pc, img[2 * i], img[2 * i + 1], x, y);
+                for (int a = 0; a < mcv::kSqpSums; ++a)
+                    sums[a] += mcv::sqpnp_term(x, y, w3[3 * i], w3[3 * i + 1], w3[3 * i + 2], a);
+            }
+            auto npos = [&](const double* rh, const double* t) {
+                int c = 0;
+                for (int i = 0; i < n; ++i)
+                    c += rh[6] * w3[3 * i] + rh[7] * w3[3 * i + 1] + rh[8] * w3[3 * i + 2] + t[2] > 0;
+                return c;
+            };
+            double rh[9], t[3], ro[9], to[3];
+            const int c1 = mcv::sqpnp_from_sums(sums, n, npos, rh, t);
+            const int c2 = orc_sqpnp_pose(img.data(), w3.data(), n, cam8, ro, to);
+            expect(c1 == c2, "sqpnp code", c1, c2);
+            if (c1 > 0 && c1 == c2) expect(same_bits(rh, ro, 9) && same_bits(t, to, 3), "sqpnp pose", n, 0);
+        }
         // matchers
         std::vector<uint8_t> qb(64 * 32), tb(80 * 32);
         for (auto& v : qb) v = (uint8_t)(rng() & 0xFF);

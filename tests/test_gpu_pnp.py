@@ -188,9 +188,50 @@ def test_n4_and_solve_pnp(gpu, oracle):
     ok4, r4, t4 = oracle.solve_pnp(img, W, K, d, kind=0)
     np.testing.assert_allclose(r3, r4, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(t3, t4, rtol=1e-6, atol=1e-9)
-    # kind 6 (SOLVEPNP_SQPNP) is not provided: an explicit failure, not another estimator's pose
-    with pytest.raises(N.NativeError, match="SQPNP"):
-        opencv.solvePnP(img, W, K, d, kind="SQPNP")
+    # kind 6 (SOLVEPNP_SQPNP): the SQPnP pose, the oracle's to the last bit of t
+    ok5, r5, t5 = opencv.solvePnP(img, W, K, d, kind="SQPNP")
+    ok6, r6, t6 = oracle.solve_pnp(img, W, K, d, kind=6)
+    assert ok5 and ok6
+    np.testing.assert_array_equal(t5, t6)
+    np.testing.assert_allclose(r5, r6, rtol=0, atol=1e-14)
+
+
+@pytest.mark.parametrize("n,planar,sigma", [(3, False, 0.0), (4, True, 0.0), (6, False, 0.3), (50, False, 1.0),
+                                            (500, True, 0.5), (1024, False, 0.5), (1025, False, 0.5),
+                                            (20000, False, 1.0)])
+def test_solve_pnp_sqpnp_vs_oracle(gpu, oracle, n, planar, sigma):
+    """cvSolvePnP kind 6 (SOLVEPNP_SQPNP, MiniCVNative.cpp:72-74): computeOmega's sums as device passes
+    (blocked beyond 1024 points), the SQPnP search on the host; t bit-exact against oracle_sqpnp.c, r
+    through the two Rodrigues restatements; noise-free scenes give the pose back."""
+    rng = np.random.default_rng(500 + n + planar)
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    R = S.rotation(rng.normal(size=3), rng.uniform(0.0, 1.0))
+    t = np.array([rng.normal() * 0.3, rng.normal() * 0.3, rng.uniform(6, 12)])
+    W = rng.uniform(-2, 2, size=(n, 3))
+    if planar:
+        W[:, 2] = 0.0
+    Pc = W @ R.T + t
+    img = np.c_[Pc[:, 0] / Pc[:, 2] * K[0, 0] + K[0, 2], Pc[:, 1] / Pc[:, 2] * K[1, 1] + K[1, 2]]
+    img = img + rng.normal(scale=sigma, size=img.shape)
+    d = [-0.05, 0.01, 0.0, 0.001] if n >= 1000 else None
+    ok, r, tt = opencv.solvePnP(img, W, K, d, kind="SQPNP")
+    ok2, rr, rt = oracle.solve_pnp(img, W, K, d, kind=6)
+    assert ok and ok2
+    np.testing.assert_array_equal(tt, rt)
+    np.testing.assert_allclose(r, rr, rtol=0, atol=1e-14)
+    if sigma == 0 and n >= 4:
+        assert np.abs(rot(r) - R).max() < 1e-8
+
+
+def test_solve_pnp_sqpnp_failures(gpu):
+    """computeOmega's assertion (coincident image points) and solvePnPGeneric's point count fail with
+    the reason; the reference's P/Invoke sees false."""
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    W = np.random.default_rng(0).uniform(-1, 1, size=(10, 3)) + [0, 0, 5]
+    with pytest.raises(N.NativeError, match="variance"):
+        opencv.solvePnP(np.tile([[600.0, 300.0]], (10, 1)), W, K, None, kind="SQPNP")
+    with pytest.raises(N.NativeError, match="at least 3"):
+        opencv.solvePnP(np.zeros((2, 2)) + 300.0, W[:2], K, None, kind="SQPNP")
 
 
 @pytest.mark.parametrize("n,kind", [(6, "EPNP"), (500, "EPNP"), (3000, "UPNP"), (20000, "DLS"), (4, "EPNP")])

@@ -206,6 +206,102 @@ def test_solve_pnp_all_points(oracle, kind):
     assert ok and np.abs(Rr - R).max() < 1e-6 and np.abs(tt - t).max() < 1e-5
 
 
+def _object_space_cost(R, W, xy):
+    """SQPnP's objective restated independently: min over t of sum ||[I2 | -x_i] (R P_i + t)||^2 (the
+    quadratic form r^T Omega r of computeOmega), t by linear least squares."""
+    n = len(W)
+    A = np.zeros((2 * n, 3))
+    b = np.zeros(2 * n)
+    for i, ((x, y), P) in enumerate(zip(xy, W)):
+        M = np.array([[1.0, 0.0, -x], [0.0, 1.0, -y]])
+        A[2 * i:2 * i + 2] = M
+        b[2 * i:2 * i + 2] = -M @ (R @ P)
+    t, *_ = np.linalg.lstsq(A, b, rcond=None)
+    res = A @ t - b
+    return float(res @ res), t
+
+
+def _normalised(img, K):
+    return np.c_[(img[:, 0] - K[0, 2]) / K[0, 0], (img[:, 1] - K[1, 2]) / K[1, 1]]
+
+
+@pytest.mark.parametrize("n,planar", [(3, False), (4, False), (6, False), (50, False), (500, False), (3000, False),
+                                      (4, True), (20, True), (1000, True)])
+def test_sqpnp_exact_recovery(oracle, n, planar):
+    """SQPnP (cvSolvePnP kind 6) on noise-free correspondences returns the pose: general and planar
+    scenes (Omega with a larger null space), 3 points (the minimum solvePnPGeneric admits for SQPnP)
+    and more than one 1024-point block of sums."""
+    rng = np.random.default_rng(100 + n + planar)
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    R, t = _pose(rng)
+    W = rng.uniform(-2, 2, size=(n, 3))
+    if planar:
+        W[:, 2] = 0.0
+    Pc = W @ R.T + t
+    img = np.c_[Pc[:, 0] / Pc[:, 2] * K[0, 0] + K[0, 2], Pc[:, 1] / Pc[:, 2] * K[1, 1] + K[1, 2]]
+    ok, r, tt = oracle.solve_pnp(img, W, K, None, kind=6)
+    Rr, _ = oracle.rodrigues(r)
+    assert ok
+    if n >= 4:
+        assert np.abs(Rr - R).max() < 1e-8 and np.abs(tt - t).max() < 1e-7
+    else:   # P3P has up to four exact poses: SQPnP returns one of zero cost
+        assert _object_space_cost(Rr, W, _normalised(img, K))[0] < 1e-18
+
+
+def test_sqpnp_global_minimum_with_noise(oracle):
+    """With pixel noise the answer minimises the object-space cost: its cost is below that of the true
+    pose, of EPnP's pose and of small rotations around it; t is the cost's minimiser for that R."""
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        img, W, inl, K, d, R, t = S.pnp_problem(300, seed=70 + trial, outlier_frac=0.0, sigma=1.0)
+        ok, r, tt = oracle.solve_pnp(img, W, K, None, kind=6)
+        assert ok
+        Rr, _ = oracle.rodrigues(r)
+        xy = _normalised(img, K)
+        c0, t_ls = _object_space_cost(Rr, W, xy)
+        np.testing.assert_allclose(tt, t_ls, rtol=1e-6, atol=1e-9)
+        assert c0 <= _object_space_cost(R, W, xy)[0] * (1 + 1e-9)
+        ok1, r1, _ = oracle.solve_pnp(img, W, K, None, kind=1)
+        assert c0 <= _object_space_cost(oracle.rodrigues(r1)[0], W, xy)[0] * (1 + 1e-9)
+        for _ in range(20):
+            dR, _ = oracle.rodrigues(rng.normal(size=3) * 1e-4)
+            assert c0 <= _object_space_cost(dR @ Rr, W, xy)[0] * (1 + 1e-12)
+
+
+def test_sqpnp_degenerate_inputs(oracle):
+    """computeOmega's assertions: image points that all coincide (coordinate variance 0) fail."""
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    W = np.random.default_rng(0).uniform(-1, 1, size=(10, 3)) + [0, 0, 5]
+    img = np.tile([[600.0, 300.0]], (10, 1))
+    ok, _, _ = oracle.solve_pnp(img, W, K, None, kind=6)
+    assert not ok
+
+
+@pytest.mark.parametrize("n,planar,sigma", [(3, False, 0.0), (6, False, 0.5), (200, False, 1.0), (200, True, 1.0),
+                                            (2500, False, 0.5)])
+def test_host_sqpnp_bit_exact(native, oracle, n, planar, sigma):
+    """The product's SQPnP algebra (sqpnp.h, host build, over sums in the device passes' block order)
+    equals oracle_sqpnp.c bit for bit, distortion included."""
+    rng = np.random.default_rng(300 + n)
+    K = np.array([[800.0, 0, 640], [0, 820.0, 360], [0, 0, 1]])
+    dist = np.array([-0.08, 0.01, 0.001, -0.0005])
+    R, t = _pose(rng)
+    W = rng.uniform(-2, 2, size=(n, 3))
+    if planar:
+        W[:, 2] = 0.0
+    Pc = W @ R.T + t
+    img = np.c_[Pc[:, 0] / Pc[:, 2] * K[0, 0] + K[0, 2], Pc[:, 1] / Pc[:, 2] * K[1, 1] + K[1, 2]]
+    img = img + rng.normal(scale=sigma, size=img.shape)
+    cam8 = np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2], *dist])
+    code, Ro, to = oracle.sqpnp_pose(img, W, cam8)
+    R9, t3 = np.zeros(9), np.zeros(3)
+    img_c, W_c = np.ascontiguousarray(img), np.ascontiguousarray(W)
+    got = native.lib().mcvHostSqpnp(img_c.ctypes.data, W_c.ctypes.data, n, cam8.ctypes.data, R9.ctypes.data, t3.ctypes.data)
+    assert got == code and code > 0
+    np.testing.assert_array_equal(R9, Ro.ravel())
+    np.testing.assert_array_equal(t3, to)
+
+
 def _ap3p_triples(count, seed):
     """Random 3-point problems: pixel observations of a random pose, a few of them perturbed so that
     the quartic has complex roots (whose real parts the reference keeps) or nearly double roots."""

@@ -17,7 +17,7 @@ SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-f
 @pytest.mark.skipif(shutil.which("gcc") is None or shutil.which("g++") is None, reason="needs gcc / g++")
 def test_host_code_under_asan_ubsan(tmp_path):
     objs = []
-    for c in ("oracle.c", "oracle_e.c", "oracle_pnp.c", "oracle_epnp.c", "oracle_f7.c", "oracle_scaled.c"):
+    for c in ("oracle.c", "oracle_e.c", "oracle_pnp.c", "oracle_epnp.c", "oracle_f7.c", "oracle_scaled.c", "oracle_sqpnp.c"):
         o = tmp_path / (c + ".o")
         subprocess.run(["gcc", "-std=c11", *SAN, "-c", str(ROOT / "oracle" / c), "-o", str(o)], check=True,
                        capture_output=True, text=True)
