@@ -576,7 +576,8 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
                               const float* __restrict__ qnorm, const unsigned* __restrict__ tmaxBits,
                               const float* __restrict__ qraw, const float* __restrict__ traw, int* __restrict__ idx,
                               float* __restrict__ dist, int* __restrict__ idx2, float* __restrict__ dist2,
-                              int* __restrict__ ambCount, int* __restrict__ ambList, const unsigned* __restrict__ dom) {
+                              int* __restrict__ ambCount, int* __restrict__ ambList, double* __restrict__ ambE2,
+                              const unsigned* __restrict__ dom) {
     const int q = blockIdx.x * 256 + threadIdx.x;
     if (q >= nq) return;
     float b1 = INFINITY, b2 = INFINITY, c1 = INFINITY, c2 = INFINITY, c3 = INFINITY;
@@ -631,7 +632,9 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
         certain = approx3 - tol > e2 * (1.0 + 1e-12);   // every other train is strictly farther
     }
     if (!certain) {
-        ambList[atomicAdd(ambCount, 1)] = q;
+        const int pos = atomicAdd(ambCount, 1);
+        ambList[pos] = q;
+        ambE2[pos] = j2 >= 0 ? e2 : INFINITY;   // the exact scan's filter bound (>= the true second best)
         return;
     }
     idx[q] = j1;
@@ -643,12 +646,21 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
 // Exact scan of the queued queries. Work items = (batch of kL2ScanQ queued queries) x (train chunk),
 // sized from the queue length on the device so that the fixed grid of kL2ScanBlocks workgroups is
 // filled however few queries are queued (no host round trip): T = kL2ScanBlocks / batches chunks
-// per batch (1 when batches >= kL2ScanBlocks). The queries sit in LDS as fp64 (broadcast reads);
-// each thread streams train rows of its chunk and keeps, per query, the lexicographic (d^2, index)
-// top-2 of the exact sums; an LDS tree merges the block, and mcv_l2_exact_merge folds the chunks in
-// order. Every sum runs in dim order in one lane: the oracle's summation, bit for bit.
+// per batch (1 when batches >= kL2ScanBlocks). Each lane streams train rows of its chunk and keeps, per
+// query, the lexicographic (d^2, index) top-2 of exact sums; an LDS tree merges the block, and
+// mcv_l2_exact_merge folds the chunks in order.
+// A certified fp32 filter decides which rows need the exact sum: refine's exact second best of the
+// two GEMM candidates, e2c, bounds the true second best, and a row whose fp32 sum s (packed fp32,
+// sub + fma per dimension) satisfies s > e2c (1 + (dim + 3) u 1.01) + 1e-30 has exact d^2 > e2c
+// (|s - d^2| <= ((1 + gamma_dim)(1 + u)^2 - 1) d^2), so it can enter no top-2; every other row
+// (a handful per query, NaN sums included) gets the exact fp64 sum in dim order in one lane — the
+// oracle's summation, bit for bit.
 static constexpr int kL2ScanQ = 8;
-static constexpr int kL2ScanBlocks = 1024;
+static constexpr int kL2ScanBlocks = 256;     // one 16-wave workgroup per CU: the CU's waves share one
+static constexpr int kL2ScanThreads = 1024;   // batch, so its queries stay in the scalar cache
+static constexpr int kL2ScanPF = 8;           // dims per prefetch group
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct L2Top2d { double d1, d2; int j1, j2; };
 
@@ -657,8 +669,8 @@ __device__ __forceinline__ void top2d_push(double& a1, int& k1, double& a2, int&
     else if (lex_less_d(e, j, a2, k2)) { a2 = e; k2 = j; }
 }
 
-__device__ __forceinline__ int l2_scan_chunks(int nbatch) {
-    return nbatch >= kL2ScanBlocks ? 1 : kL2ScanBlocks / nbatch;
+__device__ __forceinline__ int l2_scan_chunks(int nbatch, int blocks) {
+    return nbatch >= blocks ? 1 : blocks / nbatch;
 }
 
 __device__ __forceinline__ void l2_write_final(int q, const L2Top2d& r, int* idx, float* dist, int* idx2,
@@ -669,25 +681,30 @@ __device__ __forceinline__ void l2_write_final(int q, const L2Top2d& r, int* idx
     if (dist2) dist2[q] = r.j2 >= 0 ? (float)sqrt(r.d2) : INFINITY;
 }
 
-// The queued queries in fp64, batch-interleaved [a / 8][dim][8]: the 8 values of one dimension of a
-// batch are 64 contiguous bytes, so the exact scan reads a batch's k .. k + 3 with four scalar
-// dwordx16 loads off one pointer that advances by 256 B (per-query row addresses cost ~100 scalar
-// ops per step, and one CU's scalar unit serves its four SIMDs).
-__global__ void mcv_l2_amb_convert(const float* __restrict__ qraw, int dim, const int* __restrict__ ambCount,
-                                   const int* __restrict__ ambList, double* __restrict__ qd) {
+// The queued queries batch-interleaved [a / 8][dimPad][8], in fp64 (qd, the exact sums) and fp32 (qf,
+// the filter): one dimension of a batch is 64 (32) contiguous bytes, so the scan reads it with one
+// scalar load off a pointer that advances per dimension. Dimensions dim .. dimPad - 1 are zeros here
+// and in the transposed train copy (an exact +0 in every filter sum), so the filter loop needs no
+// per-dimension guard.
+__global__ void mcv_l2_amb_convert(const float* __restrict__ qraw, int dim, int dimPad,
+                                   const int* __restrict__ ambCount, const int* __restrict__ ambList,
+                                   double* __restrict__ qd, float* __restrict__ qf) {
     const int n = *ambCount;
     const int nPad = (n + kL2ScanQ - 1) / kL2ScanQ * kL2ScanQ;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nPad * dim; e += gridDim.x * blockDim.x) {
-        const int a = e / dim, k = e - a * dim;
-        const double v = a < n ? (double)qraw[(size_t)ambList[a] * dim + k] : 0.0;
-        qd[((size_t)(a / kL2ScanQ) * dim + k) * kL2ScanQ + (a % kL2ScanQ)] = v;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nPad * dimPad; e += gridDim.x * blockDim.x) {
+        const int a = e / dimPad, k = e - a * dimPad;
+        const float v = a < n && k < dim ? qraw[(size_t)ambList[a] * dim + k] : 0.f;
+        const size_t o = ((size_t)(a / kL2ScanQ) * dimPad + k) * kL2ScanQ + (a % kL2ScanQ);
+        qd[o] = (double)v;
+        qf[o] = v;
     }
 }
 
 // The train set transposed ([dim][nt]) for the exact scan's coalesced reads; skipped on the device
 // when nothing is queued.
 __global__ __launch_bounds__(256) void mcv_l2_transpose_train(const float* __restrict__ traw, int nt, int dim,
-                                                              const int* __restrict__ ambCount, float* __restrict__ tT) {
+                                                              int dimPad, const int* __restrict__ ambCount,
+                                                              float* __restrict__ tT) {
     if (*ambCount == 0) return;
     __shared__ float tile[64][65];
     const int j0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
@@ -699,71 +716,96 @@ __global__ __launch_bounds__(256) void mcv_l2_transpose_train(const float* __res
     __syncthreads();
     for (int r = ty; r < 64; r += 4) {
         const int k = k0 + r, j = j0 + tx;
-        if (k < dim && j < nt) tT[(size_t)k * nt + j] = tile[tx][r];
+        if (k < dimPad && j < nt) tT[(size_t)k * nt + j] = tile[tx][r];
     }
 }
 
-__global__ __launch_bounds__(256) void mcv_l2_exact_scan(const double* __restrict__ qd, const float* __restrict__ tT,
-                                                         int nt, int dim, const int* __restrict__ ambCount,
-                                                         const int* __restrict__ ambList, L2Top2d* __restrict__ part,
-                                                         int* __restrict__ idx, float* __restrict__ dist,
-                                                         int* __restrict__ idx2, float* __restrict__ dist2) {
-    __shared__ double sd1[256], sd2[256];
-    __shared__ int sj1[256], sj2[256];
+__global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
+    const double* __restrict__ qd, const float* __restrict__ qf, const float* __restrict__ tT,
+    const float* __restrict__ traw, int nt, int dim, int dimPad, const int* __restrict__ ambCount,
+    const int* __restrict__ ambList, const double* __restrict__ ambE2, L2Top2d* __restrict__ part,
+    int* __restrict__ idx, float* __restrict__ dist, int* __restrict__ idx2, float* __restrict__ dist2) {
+    const int blocks = gridDim.x;
+    __shared__ double sd1[kL2ScanThreads], sd2[kL2ScanThreads];
+    __shared__ int sj1[kL2ScanThreads], sj2[kL2ScanThreads];
     const int n = *ambCount;
     const int nbatch = (n + kL2ScanQ - 1) / kL2ScanQ;
     if (nbatch == 0) return;
-    const int T = l2_scan_chunks(nbatch);
+    const int T = l2_scan_chunks(nbatch, blocks);
+    const double F = 1.0 + 1.01 * (dim + 3) * 0x1p-24;
     for (int item = blockIdx.x; item < nbatch * T; item += gridDim.x) {
         const int batch = item / T, chunk = item % T;
         const int a0 = batch * kL2ScanQ;
         const int nb = min(kL2ScanQ, n - a0);
         const int jb = (int)((int64_t)chunk * nt / T), je = (int)((int64_t)(chunk + 1) * nt / T);
-        // the batch's block of qd (wave-uniform addresses: scalar loads, SGPR operands; the padding
-        // members of the last batch are zeros and never reported)
-        const double* qb = qd + (size_t)batch * dim * kL2ScanQ;
+        // the batch's blocks of qd / qf (wave-uniform addresses: scalar loads, SGPR operands; the
+        // padding members of the last batch are zeros and never reported)
+        const double* qb = qd + (size_t)batch * dimPad * kL2ScanQ;
+        const f32x2* qb2 = reinterpret_cast<const f32x2*>(qf + (size_t)batch * dimPad * kL2ScanQ);
+        double thr[kL2ScanQ];
+#pragma unroll
+        for (int b = 0; b < kL2ScanQ; ++b) {
+            const double t = ambE2[a0 + min(b, nb - 1)] * F + 1e-30;
+            // near fp32 overflow the filter decides nothing; the last batch's padding members skip all
+            thr[b] = b >= nb ? -INFINITY : t < 1e38 ? t : INFINITY;
+        }
         double e1[kL2ScanQ], e2[kL2ScanQ];
         int j1[kL2ScanQ], j2[kL2ScanQ];
 #pragma unroll
         for (int b = 0; b < kL2ScanQ; ++b) { e1[b] = e2[b] = INFINITY; j1[b] = j2[b] = -1; }
-        for (int j = jb + threadIdx.x; j < je; j += 256) {
-            // lane = train row: dimension k of 64 consecutive rows is one coalesced 256-byte load of
-            // the transposed copy (row-per-lane reads of the row-major set touched 64 cache lines per
-            // load and re-fetched each line once per 16 bytes used); four dims loaded one step ahead
-            const float* tc = tT + j;
-            double d[kL2ScanQ];
+        // lane = train row: dimension k of 64 consecutive rows is one coalesced 256-byte load of the
+        // transposed copy, loaded one group of kL2ScanPF dims ahead across row boundaries
+        const int G = dimPad / kL2ScanPF;
+        int j = jb + threadIdx.x;
+        float nx[kL2ScanPF];
 #pragma unroll
-            for (int b = 0; b < kL2ScanQ; ++b) d[b] = 0.0;
-            float nx[4];
+        for (int kk = 0; kk < kL2ScanPF; ++kk) nx[kk] = j < je ? tT[(size_t)kk * nt + j] : 0.f;
+        while (j < je) {
+            f32x2 sacc[kL2ScanQ / 2];
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) nx[kk] = kk < dim ? tc[(size_t)kk * nt] : 0.f;
-            for (int k = 0; k < dim; k += 4) {
-                float cur[4];
+            for (int p = 0; p < kL2ScanQ / 2; ++p) sacc[p] = (f32x2)(0.f);
+            for (int g = 0; g < G; ++g) {
+                float cur[kL2ScanPF];
+                const int jn = g + 1 < G ? j : j + kL2ScanThreads, kn = g + 1 < G ? (g + 1) * kL2ScanPF : 0;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
+                for (int kk = 0; kk < kL2ScanPF; ++kk) {
                     cur[kk] = nx[kk];
-                    nx[kk] = k + 4 + kk < dim ? tc[(size_t)(k + 4 + kk) * nt] : 0.f;
+                    nx[kk] = jn < je ? tT[(size_t)(kn + kk) * nt + jn] : 0.f;
                 }
+                const int k = g * kL2ScanPF;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    if (k + kk >= dim) break;   // wave-uniform
-                    const double tv = (double)cur[kk];
+                for (int kk = 0; kk < kL2ScanPF; ++kk) {
+                    const f32x2 tv = (f32x2)(cur[kk]);
 #pragma unroll
-                    for (int b = 0; b < kL2ScanQ; ++b) {
-                        const double df = qb[(k + kk) * kL2ScanQ + b] - tv;
-                        d[b] = d[b] + df * df;
+                    for (int p = 0; p < kL2ScanQ / 2; ++p) {
+                        const f32x2 df = qb2[(k + kk) * (kL2ScanQ / 2) + p] - tv;
+                        sacc[p] = __builtin_elementwise_fma(df, df, sacc[p]);
                     }
                 }
             }
+            // rows the filter cannot exclude: the exact fp64 sum, dimension order, one lane
+            const float* tr = traw + (size_t)j * dim;
 #pragma unroll
-            for (int b = 0; b < kL2ScanQ; ++b) top2d_push(e1[b], j1[b], e2[b], j2[b], d[b], j);
+            for (int b = 0; b < kL2ScanQ; ++b) {
+                const float sf = (b & 1) ? sacc[b >> 1].y : sacc[b >> 1].x;
+                if (!((double)sf > thr[b])) {
+                    double d = 0.0;
+#pragma unroll 8
+                    for (int k = 0; k < dim; ++k) {
+                        const double df = qb[k * kL2ScanQ + b] - (double)tr[k];
+                        d = d + df * df;
+                    }
+                    top2d_push(e1[b], j1[b], e2[b], j2[b], d, j);
+                }
+            }
+            j += kL2ScanThreads;
         }
 #pragma unroll
         for (int b = 0; b < kL2ScanQ; ++b) {
             if (b >= nb) break;   // block-uniform
             sd1[threadIdx.x] = e1[b]; sd2[threadIdx.x] = e2[b]; sj1[threadIdx.x] = j1[b]; sj2[threadIdx.x] = j2[b];
             __syncthreads();
-            for (int off = 128; off >= 1; off >>= 1) {
+            for (int off = kL2ScanThreads / 2; off >= 1; off >>= 1) {
                 if (threadIdx.x < off) {
                     double a1 = sd1[threadIdx.x], a2 = sd2[threadIdx.x];
                     int k1 = sj1[threadIdx.x], k2 = sj2[threadIdx.x];
@@ -786,11 +828,11 @@ __global__ __launch_bounds__(256) void mcv_l2_exact_scan(const double* __restric
 // Fold the per-chunk top-2s of each queued query in chunk order (T > 1 only).
 __global__ void mcv_l2_exact_merge(const int* __restrict__ ambCount, const int* __restrict__ ambList,
                                    const L2Top2d* __restrict__ part, int* __restrict__ idx, float* __restrict__ dist,
-                                   int* __restrict__ idx2, float* __restrict__ dist2) {
+                                   int* __restrict__ idx2, float* __restrict__ dist2, int blocks) {
     const int n = *ambCount;
     const int nbatch = (n + kL2ScanQ - 1) / kL2ScanQ;
     if (nbatch == 0) return;
-    const int T = l2_scan_chunks(nbatch);
+    const int T = l2_scan_chunks(nbatch, blocks);
     if (T == 1) return;
     for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < n; a += gridDim.x * blockDim.x) {
         L2Top2d r{INFINITY, INFINITY, -1, -1};
@@ -813,6 +855,8 @@ struct L2Work {
     DevBuf<unsigned> dom;              // max |x| over both sets (float bits): the f16 path's domain
     DevBuf<unsigned> qmax, tmaxr;      // per-row max |x|
     DevBuf<double> qd;                 // queued queries in fp64 (+ one batch of slack)
+    DevBuf<float> qf;                  // ... and in fp32 (the exact scan's filter)
+    DevBuf<double> ambE2;              // per queued query: the filter bound (refine's exact second best)
     DevBuf<float> tT;                  // the train set transposed (exact scan)
     hipStream_t last = nullptr; // stream of the last match (the diagnostics read the queue length there)
     bool lastF16 = false;       // the last match launched the f16-split form (its flag decided on device)
@@ -849,6 +893,7 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     wk.tn.ensure(ntPad);
     wk.tmax.ensure(1);
     wk.amb.ensure((size_t)nq + 1);
+    wk.ambE2.ensure((size_t)nq);
     MCV_HIP(hipMemsetAsync(wk.amb.p, 0, sizeof(int), s));
     // f16-split GEMM form for DP <= 128: the split preps record max |x|, and the f32 prep / GEMM
     // return on the device when it is inside the f16 domain (no host round trip)
@@ -919,20 +964,30 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
 #undef MCV_L2_LAUNCH
     }
     hipLaunchKernelGGL(mcv_l2_refine, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nqPad, nchunks, nt, dim,
-                       wk.qn.p, wk.tmax.p, d_q, d_t, d_idx, d_dist, d_idx2, d_dist2, wk.amb.p, wk.amb.p + 1, dom);
+                       wk.qn.p, wk.tmax.p, d_q, d_t, d_idx, d_dist, d_idx2, d_dist2, wk.amb.p, wk.amb.p + 1,
+                       wk.ambE2.p, dom);
     {
         ProfScope ps("l2_exact", s);
-        wk.scanPart.ensure((size_t)kL2ScanBlocks * kL2ScanQ);
-        wk.qd.ensure((size_t)(nq + kL2ScanQ) * dim);
-        hipLaunchKernelGGL(mcv_l2_amb_convert, dim3(256), dim3(256), 0, s, d_q, dim, wk.amb.p, wk.amb.p + 1, wk.qd.p);
-        wk.tT.ensure((size_t)(nt > 0 ? nt : 1) * dim);
+        static const int scanBlocks = [] {   // exact-scan grid (screen: MCV_L2_SCAN_BLOCKS)
+            const char* e = getenv("MCV_L2_SCAN_BLOCKS");
+            const int v = e ? atoi(e) : kL2ScanBlocks;
+            return v >= 64 && v <= 8192 ? v : kL2ScanBlocks;
+        }();
+        wk.scanPart.ensure((size_t)scanBlocks * kL2ScanQ);
+        const int dimPad = (dim + kL2ScanPF - 1) / kL2ScanPF * kL2ScanPF;
+        wk.qd.ensure((size_t)(nq + kL2ScanQ) * dimPad);
+        wk.qf.ensure((size_t)(nq + kL2ScanQ) * dimPad);
+        hipLaunchKernelGGL(mcv_l2_amb_convert, dim3(256), dim3(256), 0, s, d_q, dim, dimPad, wk.amb.p, wk.amb.p + 1,
+                           wk.qd.p, wk.qf.p);
+        wk.tT.ensure((size_t)(nt > 0 ? nt : 1) * dimPad);
         if (nt > 0)
-            hipLaunchKernelGGL(mcv_l2_transpose_train, dim3((nt + 63) / 64, (dim + 63) / 64), dim3(256), 0, s, d_t, nt,
-                               dim, wk.amb.p, wk.tT.p);
-        hipLaunchKernelGGL(mcv_l2_exact_scan, dim3(kL2ScanBlocks), dim3(256), 0, s, wk.qd.p, wk.tT.p, nt, dim, wk.amb.p,
-                           wk.amb.p + 1, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2);
+            hipLaunchKernelGGL(mcv_l2_transpose_train, dim3((nt + 63) / 64, (dimPad + 63) / 64), dim3(256), 0, s,
+                               d_t, nt, dim, dimPad, wk.amb.p, wk.tT.p);
+        hipLaunchKernelGGL(mcv_l2_exact_scan, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, wk.qd.p, wk.qf.p, wk.tT.p,
+                           d_t, nt, dim, dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist,
+                           d_idx2, d_dist2);
         hipLaunchKernelGGL(mcv_l2_exact_merge, dim3(8), dim3(256), 0, s, wk.amb.p, wk.amb.p + 1, wk.scanPart.p, d_idx,
-                           d_dist, d_idx2, d_dist2);
+                           d_dist, d_idx2, d_dist2, scanBlocks);
     }
     MCV_HIP(hipGetLastError());
     wk.last = s;

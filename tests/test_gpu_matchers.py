@@ -98,6 +98,19 @@ def test_l2_near_ties_take_the_exact_scan(gpu, oracle):
     check_l2(oracle, q, t)
 
 
+@pytest.mark.parametrize("offset", [0.0, 1000.0])
+def test_l2_exact_scan_filter_near_threshold(gpu, oracle, offset):
+    """The exact scan's fp32 filter against rows whose distances sit within fp32 rounding of the
+    filter bound: clusters of near-duplicates (perturbations of 1e-3 on values up to 1000 + 255) around
+    each query's true neighbours; every decision still equals the oracle's exact answer."""
+    rng = np.random.default_rng(29)
+    base = S.sift_like(200, 128, rng).astype(np.float64) + offset
+    t = np.concatenate([base + rng.normal(scale=1e-3, size=base.shape) for _ in range(6)]).astype(np.float32)
+    q = (base[rng.integers(0, 200, size=700)] + rng.normal(scale=2e-3, size=(700, 128))).astype(np.float32)
+    check_l2(oracle, q, t)
+    assert N.lib().mcvL2LastExactScans() > 0
+
+
 @pytest.mark.parametrize("nq,nt,dim", [(1, 1, 128), (1, 2, 128), (33, 31, 128), (200, 777, 128), (129, 4099, 128),
                                        (300, 500, 64), (100, 300, 32), (100, 300, 17), (64, 200, 256),
                                        (250, 333, 61)])
