@@ -656,8 +656,11 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
 // (a handful per query, NaN sums included) gets the exact fp64 sum in dim order in one lane — the
 // oracle's summation, bit for bit.
 static constexpr int kL2ScanQ = 8;
-static constexpr int kL2ScanBlocks = 256;     // one 16-wave workgroup per CU: the CU's waves share one
-static constexpr int kL2ScanThreads = 1024;   // batch, so its queries stay in the scalar cache
+#ifndef MCV_L2_SCAN_THREADS
+#define MCV_L2_SCAN_THREADS 1024
+#endif
+static constexpr int kL2ScanThreads = MCV_L2_SCAN_THREADS;   // 1024: one 16-wave workgroup per CU, whose
+static constexpr int kL2ScanBlocks = 256 * 1024 / kL2ScanThreads;   // waves share one batch in the scalar cache
 static constexpr int kL2ScanPF = 8;           // dims per prefetch group
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -755,50 +758,64 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
         for (int b = 0; b < kL2ScanQ; ++b) { e1[b] = e2[b] = INFINITY; j1[b] = j2[b] = -1; }
         // lane = train row: dimension k of 64 consecutive rows is one coalesced 256-byte load of the
         // transposed copy, loaded one group of kL2ScanPF dims ahead across row boundaries
+        // One linear sequence of (row, group of kL2ScanPF dims) steps per lane, the same for every lane
+        // (lanes with fewer rows stop early): group L + 2's loads are issued while group L is summed,
+        // so two groups of VALU work cover each load, across row boundaries.
         const int G = dimPad / kL2ScanPF;
-        int j = jb + threadIdx.x;
-        float nx[kL2ScanPF];
+        const int jl = jb + threadIdx.x;
+        const int rows = jl < je ? (je - 1 - jl) / kL2ScanThreads + 1 : 0;
+        const int Ltot = rows * G;
+        // unconditional loads (a step past the lane's rows re-reads row jb, unused): the in-order
+        // vmcnt waits then count exact numbers of loads
+        auto gload = [&](float (&buf)[kL2ScanPF], int L) {
+            const int rr = L / G, k0 = (L - rr * G) * kL2ScanPF;
+            const int jj = L < Ltot ? jl + rr * kL2ScanThreads : jb;
 #pragma unroll
-        for (int kk = 0; kk < kL2ScanPF; ++kk) nx[kk] = j < je ? tT[(size_t)kk * nt + j] : 0.f;
-        while (j < je) {
-            f32x2 sacc[kL2ScanQ / 2];
+            for (int kk = 0; kk < kL2ScanPF; ++kk) buf[kk] = tT[(size_t)(k0 + kk) * nt + jj];
+        };
+        f32x2 sacc[kL2ScanQ / 2];
+        auto step = [&](const float (&buf)[kL2ScanPF], int L) {
+            const int rr = L / G, g = L - rr * G;
+            if (g == 0)
 #pragma unroll
-            for (int p = 0; p < kL2ScanQ / 2; ++p) sacc[p] = (f32x2)(0.f);
-            for (int g = 0; g < G; ++g) {
-                float cur[kL2ScanPF];
-                const int jn = g + 1 < G ? j : j + kL2ScanThreads, kn = g + 1 < G ? (g + 1) * kL2ScanPF : 0;
+                for (int p = 0; p < kL2ScanQ / 2; ++p) sacc[p] = (f32x2)(0.f);
+            const int k = g * kL2ScanPF;
 #pragma unroll
-                for (int kk = 0; kk < kL2ScanPF; ++kk) {
-                    cur[kk] = nx[kk];
-                    nx[kk] = jn < je ? tT[(size_t)(kn + kk) * nt + jn] : 0.f;
-                }
-                const int k = g * kL2ScanPF;
+            for (int kk = 0; kk < kL2ScanPF; ++kk) {
+                const f32x2 tv = (f32x2)(buf[kk]);
 #pragma unroll
-                for (int kk = 0; kk < kL2ScanPF; ++kk) {
-                    const f32x2 tv = (f32x2)(cur[kk]);
-#pragma unroll
-                    for (int p = 0; p < kL2ScanQ / 2; ++p) {
-                        const f32x2 df = qb2[(k + kk) * (kL2ScanQ / 2) + p] - tv;
-                        sacc[p] = __builtin_elementwise_fma(df, df, sacc[p]);
-                    }
+                for (int p = 0; p < kL2ScanQ / 2; ++p) {
+                    const f32x2 df = qb2[(k + kk) * (kL2ScanQ / 2) + p] - tv;
+                    sacc[p] = __builtin_elementwise_fma(df, df, sacc[p]);
                 }
             }
-            // rows the filter cannot exclude: the exact fp64 sum, dimension order, one lane
-            const float* tr = traw + (size_t)j * dim;
+            if (g == G - 1) {
+                // rows the filter cannot exclude: the exact fp64 sum, dimension order, one lane
+                const int jr = jl + rr * kL2ScanThreads;
+                const float* tr = traw + (size_t)jr * dim;
 #pragma unroll
-            for (int b = 0; b < kL2ScanQ; ++b) {
-                const float sf = (b & 1) ? sacc[b >> 1].y : sacc[b >> 1].x;
-                if (!((double)sf > thr[b])) {
-                    double d = 0.0;
+                for (int b = 0; b < kL2ScanQ; ++b) {
+                    const float sf = (b & 1) ? sacc[b >> 1].y : sacc[b >> 1].x;
+                    if (!((double)sf > thr[b])) {
+                        double d = 0.0;
 #pragma unroll 8
-                    for (int k = 0; k < dim; ++k) {
-                        const double df = qb[k * kL2ScanQ + b] - (double)tr[k];
-                        d = d + df * df;
+                        for (int kx = 0; kx < dim; ++kx) {
+                            const double df = qb[kx * kL2ScanQ + b] - (double)tr[kx];
+                            d = d + df * df;
+                        }
+                        top2d_push(e1[b], j1[b], e2[b], j2[b], d, jr);
                     }
-                    top2d_push(e1[b], j1[b], e2[b], j2[b], d, j);
                 }
             }
-            j += kL2ScanThreads;
+        };
+        float bufA[kL2ScanPF], bufB[kL2ScanPF];
+        gload(bufA, 0);
+        gload(bufB, 1);
+        for (int L = 0; L < Ltot; L += 2) {   // G is even (dimPad: a multiple of 2 groups)
+            step(bufA, L);
+            gload(bufA, L + 2);
+            step(bufB, L + 1);
+            gload(bufB, L + 3);
         }
 #pragma unroll
         for (int b = 0; b < kL2ScanQ; ++b) {
@@ -974,7 +991,7 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
             return v >= 64 && v <= 8192 ? v : kL2ScanBlocks;
         }();
         wk.scanPart.ensure((size_t)scanBlocks * kL2ScanQ);
-        const int dimPad = (dim + kL2ScanPF - 1) / kL2ScanPF * kL2ScanPF;
+        const int dimPad = (dim + 2 * kL2ScanPF - 1) / (2 * kL2ScanPF) * (2 * kL2ScanPF);
         wk.qd.ensure((size_t)(nq + kL2ScanQ) * dimPad);
         wk.qf.ensure((size_t)(nq + kL2ScanQ) * dimPad);
         hipLaunchKernelGGL(mcv_l2_amb_convert, dim3(256), dim3(256), 0, s, d_q, dim, dimPad, wk.amb.p, wk.amb.p + 1,
