@@ -655,7 +655,7 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
 // (|s - d^2| <= ((1 + gamma_dim)(1 + u)^2 - 1) d^2), so it can enter no top-2; every other row
 // (a handful per query, NaN sums included) gets the exact fp64 sum in dim order in one lane — the
 // oracle's summation, bit for bit.
-static constexpr int kL2ScanQ = 8;
+static constexpr int kL2ScanQ = 32;
 #ifndef MCV_L2_SCAN_THREADS
 #define MCV_L2_SCAN_THREADS 1024
 #endif
@@ -728,14 +728,18 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
     const float* __restrict__ traw, int nt, int dim, int dimPad, const int* __restrict__ ambCount,
     const int* __restrict__ ambList, const double* __restrict__ ambE2, L2Top2d* __restrict__ part,
     int* __restrict__ idx, float* __restrict__ dist, int* __restrict__ idx2, float* __restrict__ dist2) {
+    constexpr int NW = kL2ScanThreads / 64;
     const int blocks = gridDim.x;
-    __shared__ double sd1[kL2ScanThreads], sd2[kL2ScanThreads];
-    __shared__ int sj1[kL2ScanThreads], sj2[kL2ScanThreads];
+    // per wave and query: the lexicographic top-2 of the exact sums the wave computed (rare updates,
+    // wave-uniform, so no atomics); the filter bounds
+    __shared__ L2Top2d wtop[NW][kL2ScanQ];
+    __shared__ double sthr[kL2ScanQ];
     const int n = *ambCount;
     const int nbatch = (n + kL2ScanQ - 1) / kL2ScanQ;
     if (nbatch == 0) return;
     const int T = l2_scan_chunks(nbatch, blocks);
     const double F = 1.0 + 1.01 * (dim + 3) * 0x1p-24;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int item = blockIdx.x; item < nbatch * T; item += gridDim.x) {
         const int batch = item / T, chunk = item % T;
         const int a0 = batch * kL2ScanQ;
@@ -745,22 +749,18 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
         // padding members of the last batch are zeros and never reported)
         const double* qb = qd + (size_t)batch * dimPad * kL2ScanQ;
         const f32x2* qb2 = reinterpret_cast<const f32x2*>(qf + (size_t)batch * dimPad * kL2ScanQ);
-        double thr[kL2ScanQ];
-#pragma unroll
-        for (int b = 0; b < kL2ScanQ; ++b) {
+        if (threadIdx.x < kL2ScanQ) {
+            const int b = threadIdx.x;
             const double t = ambE2[a0 + min(b, nb - 1)] * F + 1e-30;
             // near fp32 overflow the filter decides nothing; the last batch's padding members skip all
-            thr[b] = b >= nb ? -INFINITY : t < 1e38 ? t : INFINITY;
+            sthr[b] = b >= nb ? -INFINITY : t < 1e38 ? t : INFINITY;
         }
-        double e1[kL2ScanQ], e2[kL2ScanQ];
-        int j1[kL2ScanQ], j2[kL2ScanQ];
-#pragma unroll
-        for (int b = 0; b < kL2ScanQ; ++b) { e1[b] = e2[b] = INFINITY; j1[b] = j2[b] = -1; }
+        if (lane < kL2ScanQ) wtop[wv][lane] = L2Top2d{INFINITY, INFINITY, -1, -1};
+        __syncthreads();
         // lane = train row: dimension k of 64 consecutive rows is one coalesced 256-byte load of the
-        // transposed copy, loaded one group of kL2ScanPF dims ahead across row boundaries
-        // One linear sequence of (row, group of kL2ScanPF dims) steps per lane, the same for every lane
-        // (lanes with fewer rows stop early): group L + 2's loads are issued while group L is summed,
-        // so two groups of VALU work cover each load, across row boundaries.
+        // transposed copy. One linear sequence of (row, group of kL2ScanPF dims) steps per lane, the
+        // same for every lane (lanes with fewer rows stop early): group L + 2's loads are issued while
+        // group L is summed, across row boundaries.
         const int G = dimPad / kL2ScanPF;
         const int jl = jb + threadIdx.x;
         const int rows = jl < je ? (je - 1 - jl) / kL2ScanThreads + 1 : 0;
@@ -774,6 +774,26 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
             for (int kk = 0; kk < kL2ScanPF; ++kk) buf[kk] = tT[(size_t)(k0 + kk) * nt + jj];
         };
         f32x2 sacc[kL2ScanQ / 2];
+        // a row the filter cannot exclude for query b: the exact fp64 sum in dimension order, computed
+        // by the whole wave on the row's wave-uniform address, one candidate lane at a time
+        auto exact_rows = [&](int b, bool pass, int jr) {
+            uint64_t m = __ballot(pass);
+            while (m) {
+                const int l = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const int jc = __builtin_amdgcn_readlane(jr, l);
+                const float* tr = traw + (size_t)jc * dim;
+                double d = 0.0;
+#pragma unroll 8
+                for (int kx = 0; kx < dim; ++kx) {
+                    const double df = qb[kx * kL2ScanQ + b] - (double)tr[kx];
+                    d = d + df * df;
+                }
+                L2Top2d w = wtop[wv][b];
+                top2d_push(w.d1, w.j1, w.d2, w.j2, d, jc);
+                if (lane == 0) wtop[wv][b] = w;
+            }
+        };
         auto step = [&](const float (&buf)[kL2ScanPF], int L) {
             const int rr = L / G, g = L - rr * G;
             if (g == 0)
@@ -790,21 +810,11 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
                 }
             }
             if (g == G - 1) {
-                // rows the filter cannot exclude: the exact fp64 sum, dimension order, one lane
                 const int jr = jl + rr * kL2ScanThreads;
-                const float* tr = traw + (size_t)jr * dim;
 #pragma unroll
-                for (int b = 0; b < kL2ScanQ; ++b) {
-                    const float sf = (b & 1) ? sacc[b >> 1].y : sacc[b >> 1].x;
-                    if (!((double)sf > thr[b])) {
-                        double d = 0.0;
-#pragma unroll 8
-                        for (int kx = 0; kx < dim; ++kx) {
-                            const double df = qb[kx * kL2ScanQ + b] - (double)tr[kx];
-                            d = d + df * df;
-                        }
-                        top2d_push(e1[b], j1[b], e2[b], j2[b], d, jr);
-                    }
+                for (int p = 0; p < kL2ScanQ / 2; ++p) {
+                    exact_rows(2 * p, !((double)sacc[p].x > sthr[2 * p]), jr);
+                    exact_rows(2 * p + 1, !((double)sacc[p].y > sthr[2 * p + 1]), jr);
                 }
             }
         };
@@ -817,48 +827,51 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
             step(bufB, L + 1);
             gload(bufB, L + 3);
         }
-#pragma unroll
-        for (int b = 0; b < kL2ScanQ; ++b) {
-            if (b >= nb) break;   // block-uniform
-            sd1[threadIdx.x] = e1[b]; sd2[threadIdx.x] = e2[b]; sj1[threadIdx.x] = j1[b]; sj2[threadIdx.x] = j2[b];
-            __syncthreads();
-            for (int off = kL2ScanThreads / 2; off >= 1; off >>= 1) {
-                if (threadIdx.x < off) {
-                    double a1 = sd1[threadIdx.x], a2 = sd2[threadIdx.x];
-                    int k1 = sj1[threadIdx.x], k2 = sj2[threadIdx.x];
-                    top2d_push(a1, k1, a2, k2, sd1[threadIdx.x + off], sj1[threadIdx.x + off]);
-                    top2d_push(a1, k1, a2, k2, sd2[threadIdx.x + off], sj2[threadIdx.x + off]);
-                    sd1[threadIdx.x] = a1; sd2[threadIdx.x] = a2; sj1[threadIdx.x] = k1; sj2[threadIdx.x] = k2;
-                }
-                __syncthreads();
+        __syncthreads();
+        // fold the waves' top-2s (lexicographic: the order of candidates does not matter)
+        if (threadIdx.x < nb) {
+            const int b = threadIdx.x;
+            L2Top2d r{INFINITY, INFINITY, -1, -1};
+            for (int w = 0; w < NW; ++w) {
+                const L2Top2d x = wtop[w][b];
+                top2d_push(r.d1, r.j1, r.d2, r.j2, x.d1, x.j1);
+                top2d_push(r.d1, r.j1, r.d2, r.j2, x.d2, x.j2);
             }
-            if (threadIdx.x == 0) {
-                const L2Top2d r{sd1[0], sd2[0], sj1[0], sj2[0]};
-                if (T == 1) l2_write_final(ambList[a0 + b], r, idx, dist, idx2, dist2);
-                else part[(size_t)(a0 + b) * T + chunk] = r;
-            }
-            __syncthreads();
+            if (T == 1) l2_write_final(ambList[a0 + b], r, idx, dist, idx2, dist2);
+            else part[(size_t)(a0 + b) * T + chunk] = r;
         }
+        __syncthreads();
     }
 }
 
-// Fold the per-chunk top-2s of each queued query in chunk order (T > 1 only).
-__global__ void mcv_l2_exact_merge(const int* __restrict__ ambCount, const int* __restrict__ ambList,
-                                   const L2Top2d* __restrict__ part, int* __restrict__ idx, float* __restrict__ dist,
-                                   int* __restrict__ idx2, float* __restrict__ dist2, int blocks) {
+// Fold the per-chunk top-2s of each queued query (T > 1 only): one wave per query, lanes over the
+// chunks, then a lexicographic butterfly (the top-2 of a set does not depend on the fold order).
+__global__ __launch_bounds__(256) void mcv_l2_exact_merge(const int* __restrict__ ambCount,
+                                                          const int* __restrict__ ambList,
+                                                          const L2Top2d* __restrict__ part, int* __restrict__ idx,
+                                                          float* __restrict__ dist, int* __restrict__ idx2,
+                                                          float* __restrict__ dist2, int blocks) {
     const int n = *ambCount;
     const int nbatch = (n + kL2ScanQ - 1) / kL2ScanQ;
     if (nbatch == 0) return;
     const int T = l2_scan_chunks(nbatch, blocks);
     if (T == 1) return;
-    for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < n; a += gridDim.x * blockDim.x) {
+    const int lane = threadIdx.x & 63;
+    for (int a = blockIdx.x * 4 + (threadIdx.x >> 6); a < n; a += gridDim.x * 4) {
         L2Top2d r{INFINITY, INFINITY, -1, -1};
-        for (int c = 0; c < T; ++c) {
+        for (int c = lane; c < T; c += 64) {
             const L2Top2d p = part[(size_t)a * T + c];
             top2d_push(r.d1, r.j1, r.d2, r.j2, p.d1, p.j1);
             top2d_push(r.d1, r.j1, r.d2, r.j2, p.d2, p.j2);
         }
-        l2_write_final(ambList[a], r, idx, dist, idx2, dist2);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double o1 = __shfl_xor(r.d1, off, 64), o2 = __shfl_xor(r.d2, off, 64);
+            const int k1 = __shfl_xor(r.j1, off, 64), k2 = __shfl_xor(r.j2, off, 64);
+            top2d_push(r.d1, r.j1, r.d2, r.j2, o1, k1);
+            top2d_push(r.d1, r.j1, r.d2, r.j2, o2, k2);
+        }
+        if (lane == 0) l2_write_final(ambList[a], r, idx, dist, idx2, dist2);
     }
 }
 
@@ -1003,7 +1016,7 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         hipLaunchKernelGGL(mcv_l2_exact_scan, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, wk.qd.p, wk.qf.p, wk.tT.p,
                            d_t, nt, dim, dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist,
                            d_idx2, d_dist2);
-        hipLaunchKernelGGL(mcv_l2_exact_merge, dim3(8), dim3(256), 0, s, wk.amb.p, wk.amb.p + 1, wk.scanPart.p, d_idx,
+        hipLaunchKernelGGL(mcv_l2_exact_merge, dim3(64), dim3(256), 0, s, wk.amb.p, wk.amb.p + 1, wk.scanPart.p, d_idx,
                            d_dist, d_idx2, d_dist2, scanBlocks);
     }
     MCV_HIP(hipGetLastError());
