@@ -115,22 +115,53 @@ __global__ void mcv_l2_prep(const float* __restrict__ src, int n, int dim, int D
     if (lane == 0) norms[r] = r < n ? acc : padNorm;
 }
 
-// max over the real rows' norms (non-negative: float order = bit order); NaN -> +inf.
-__global__ __launch_bounds__(1024) void mcv_l2_maxnorm(const float* __restrict__ norms, int n,
-                                                      unsigned* __restrict__ out) {
-    __shared__ float sm[16];
-    float m = 0.f;
-    for (int i = threadIdx.x; i < n; i += 1024) {
-        const float v = norms[i];
-        m = v == v ? fmaxf(m, v) : __builtin_inff();
-    }
+// Max of non-negative float bit patterns over a[0, na) and b[0, nb) (bit order = float order; NaN ->
+// +inf): per-block maxima, the last block to finish folds them, writes *out and re-arms its counter
+// (grid-wide, one launch, no host round trip). The row norms' maximum and the f16 domain use it.
+static constexpr int kL2MaxBlocks = 64;
+__global__ __launch_bounds__(256) void mcv_l2_umax(const unsigned* __restrict__ a, int na,
+                                                   const unsigned* __restrict__ b, int nb,
+                                                   unsigned* __restrict__ part, unsigned* __restrict__ count,
+                                                   unsigned* __restrict__ out) {
+    __shared__ unsigned sm[4];
+    __shared__ bool last;
+    auto fold = [&](unsigned m) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
-    __syncthreads();
+        for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned o = __shfl_xor(m, off, 64);
+            m = o > m ? o : m;
+        }
+        if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+        __syncthreads();
+        m = sm[0];
+        for (int w = 1; w < 4; ++w) m = sm[w] > m ? sm[w] : m;
+        return m;
+    };
+    unsigned m = 0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < na + nb; i += gridDim.x * 256) {
+        unsigned v = i < na ? a[i] : b[i - na];
+        v = v > 0x7f800000u ? 0x7f800000u : v;   // NaN (and any sign-bit pattern) -> +inf
+        m = v > m ? v : m;
+    }
+    m = fold(m);
     if (threadIdx.x == 0) {
-        for (int w = 1; w < 16; ++w) m = fmaxf(m, sm[w]);
-        *out = __float_as_uint(m);
+        part[blockIdx.x] = m;
+        __threadfence();
+        last = atomicAdd(count, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    unsigned r = 0;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) {
+        const unsigned v = __atomic_load_n(&part[i], __ATOMIC_RELAXED);
+        r = v > r ? v : r;
+    }
+    __syncthreads();
+    r = fold(r);
+    if (threadIdx.x == 0) {
+        *out = r;
+        *count = 0u;
     }
 }
 
@@ -271,7 +302,7 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
 
 // Row-major split copies [nPad][DP] (hi = RN f16 of x, lo = RN f16 of the exact fp32 residual x - hi),
 // zero padding, the fp32 squared norm (as mcv_l2_prep) and the row's max |x| (float bits; a
-// non-finite coordinate records +inf: out of the f16 domain; 0 for padding rows). mcv_l2_dommax folds
+// non-finite coordinate records +inf: out of the f16 domain; 0 for padding rows). mcv_l2_umax folds
 // the rows' maxima (one atomic per row on one address serialised to ~0.5 ms per call).
 __global__ void mcv_l2_prep16(const float* __restrict__ src, int n, int dim, int DP, int nPad, _Float16* __restrict__ hi,
                               _Float16* __restrict__ lo, float* __restrict__ norms, float padNorm,
@@ -303,25 +334,6 @@ __global__ void mcv_l2_prep16(const float* __restrict__ src, int n, int dim, int
     }
 }
 
-// dom = max over both sets' row maxima (bit order = float order for non-negative floats).
-__global__ __launch_bounds__(1024) void mcv_l2_dommax(const unsigned* __restrict__ a, int na, const unsigned* __restrict__ b,
-                                                      int nb, unsigned* __restrict__ dom) {
-    __shared__ unsigned sm[16];
-    unsigned m = 0;
-    for (int i = threadIdx.x; i < na; i += 1024) m = a[i] > m ? a[i] : m;
-    for (int i = threadIdx.x; i < nb; i += 1024) m = b[i] > m ? b[i] : m;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const unsigned o = __shfl_xor(m, off, 64);
-        m = o > m ? o : m;
-    }
-    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < 16; ++w) m = sm[w] > m ? sm[w] : m;
-        *dom = m;
-    }
-}
 
 template <int DP, int TR, int NT>
 __device__ __forceinline__ void l2_gload16(const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
@@ -883,6 +895,8 @@ struct L2Work {
     DevBuf<L2Top2d> scanPart;   // exact-scan partials: < kL2ScanBlocks x kL2ScanQ records
     DevBuf<_Float16> qh, ql, th, tl;   // f16-split copies (DP <= 128)
     DevBuf<unsigned> dom;              // max |x| over both sets (float bits): the f16 path's domain
+    DevBuf<unsigned> maxPart;          // mcv_l2_umax: per-block maxima (2 x kL2MaxBlocks)
+    DevBuf<unsigned> maxCount;         // ... and its two finish counters (zeroed once, re-armed by each launch)
     DevBuf<unsigned> qmax, tmaxr;      // per-row max |x|
     DevBuf<double> qd;                 // queued queries in fp64 (+ one batch of slack)
     DevBuf<float> qf;                  // ... and in fp32 (the exact scan's filter)
@@ -922,6 +936,11 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     wk.qn.ensure(nqPad);
     wk.tn.ensure(ntPad);
     wk.tmax.ensure(1);
+    if (!wk.maxCount.p) {
+        wk.maxCount.ensure(2);
+        MCV_HIP(hipMemsetAsync(wk.maxCount.p, 0, 2 * sizeof(unsigned), s));
+    }
+    wk.maxPart.ensure(2 * kL2MaxBlocks);
     wk.amb.ensure((size_t)nq + 1);
     wk.ambE2.ensure((size_t)nq);
     MCV_HIP(hipMemsetAsync(wk.amb.p, 0, sizeof(int), s));
@@ -940,7 +959,8 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
                            wk.ql.p, wk.qn.p, 0.f, wk.qmax.p);
         hipLaunchKernelGGL(mcv_l2_prep16, dim3((ntPad + 3) / 4), dim3(256), 0, s, d_t, nt, dim, DP, ntPad, wk.th.p,
                            wk.tl.p, wk.tn.p, __builtin_inff(), wk.tmaxr.p);
-        hipLaunchKernelGGL(mcv_l2_dommax, dim3(1), dim3(1024), 0, s, wk.qmax.p, nq, wk.tmaxr.p, nt, wk.dom.p);
+        hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s, wk.qmax.p, nq, wk.tmaxr.p, nt, wk.maxPart.p,
+                           wk.maxCount.p, wk.dom.p);
         dom = wk.dom.p;
     }
     hipLaunchKernelGGL(mcv_l2_prep, dim3((nqPad + 3) / 4), dim3(256), 0, s, d_q, nq, dim, DP, nqPad, wk.qp.p, wk.qn.p,
@@ -948,7 +968,8 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     // padding rows get a +inf norm: their scores are +inf and never enter a top-2 or the third place
     hipLaunchKernelGGL(mcv_l2_prep, dim3((ntPad + 3) / 4), dim3(256), 0, s, d_t, nt, dim, DP, ntPad, wk.tp.p, wk.tn.p,
                        __builtin_inff(), dom);
-    hipLaunchKernelGGL(mcv_l2_maxnorm, dim3(1), dim3(1024), 0, s, wk.tn.p, nt, wk.tmax.p);
+    hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s, reinterpret_cast<const unsigned*>(wk.tn.p), nt,
+                       nullptr, 0, wk.maxPart.p + kL2MaxBlocks, wk.maxCount.p + 1, wk.tmax.p);
     const int qblocks = nqPad / 128;
     int nchunks = (2048 + qblocks - 1) / qblocks;
     if (f16) nchunks = 8;   // one train chunk per XCD (mcv_l2_mfma16's block order)
