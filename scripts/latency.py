@@ -34,10 +34,15 @@ def main():
         out.append(("cvRecoverPose", n, timed(lambda: opencv.recoverPose(cfg, a, b))))
         img, W, _, K, d, _, _ = S.pnp_problem(n, seed=3)
         out.append(("cvSolvePnPRansac", n, timed(lambda: opencv.solvePnPRansac(img, W, K, d, reproj_error=2.0))))
+        img0, W0, _, K0, d0, _, _ = S.pnp_problem(n, seed=8, outlier_frac=0.0, sigma=0.5)
+        out.append(("cvSolvePnP(SQPNP)", n, timed(lambda: opencv.solvePnP(img0, W0, K0, d0, kind="SQPNP"))))
+        out.append(("cvSolvePnP(EPNP)", n, timed(lambda: opencv.solvePnP(img0, W0, K0, d0, kind="EPNP"))))
         fa, fb, _, _ = S.fundamental_problem(n, 4)
         out.append(("cvFindFundamentalMat", n, timed(lambda: opencv.findFundamentalMat(fa, fb))))
         q, t, _ = S.hamming_problem(n, n, seed=5)
         out.append(("cvMatchHamming", n, timed(lambda: opencv.matchHamming(q, t))))
+        lq, lt, _ = S.l2_problem(n, n, dim=128, seed=9)
+        out.append(("cvMatchL2", n, timed(lambda: opencv.matchL2(lq, lt))))
         cam, pose, W3, O2, _ = S.scaled_problem(n, seed=7)
         out.append(("cvFindScaledPose", n, timed(lambda: CM.findScaled(0.01, cam, (W3, O2), pose))))
     a, b, *_ = S.essential_problem(5, seed=6, outlier_frac=0)

@@ -6,7 +6,7 @@ set -u
 mkdir -p gpurun_out
 export MCV_DIST_BACKEND=gloo
 port=29611
-for w in ${WORKLOADS:-homography fundamental essential pnp hamming}; do
+for w in ${WORKLOADS:-homography fundamental essential pnp hamming l2 scaled}; do
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port $port bench.py --workload $w --gpus 2 --steps 2 --warmup 1 \
         --no-cpu-baseline > gpurun_out/rehearse_$w.log 2>&1
