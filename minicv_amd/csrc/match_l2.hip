@@ -385,7 +385,10 @@ __device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const fl
             const float nrm = (r & 3) == 0 ? n4.x : (r & 3) == 1 ? n4.y : (r & 3) == 2 ? n4.z : n4.w;
             const float dot = am[c][r] + as[c][r];
             const float s = fmaf(-2.f, dot, nrm);
-            top2b3_push_asc(b1, i1, b2, i2, b3, s, __builtin_amdgcn_readfirstlane(base + row));
+            // a score >= b3 changes neither the top-2 nor the third place (med3(s, b2, b3) = b3): past
+            // the first tiles almost no lane of a wave needs the 9-instruction insertion, and a
+            // branch with no lane active is skipped whole
+            if (s < b3) top2b3_push_asc(b1, i1, b2, i2, b3, s, __builtin_amdgcn_readfirstlane(base + row));
         }
 }
 
