@@ -277,7 +277,9 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
                 const float4 n4 = nv[c][r >> 2];
                 const float nrm = (r & 3) == 0 ? n4.x : (r & 3) == 1 ? n4.y : (r & 3) == 2 ? n4.z : n4.w;
                 const float s = fmaf(-2.f, acc[c][r], nrm);
-                top2b3_push_asc(b1, i1, b2, i2, b3, s, t * TR + row);
+                // as in mcv_l2_mfma16: a score >= b3 (or NaN, which the exact definition never ranks)
+                // changes nothing
+                if (s < b3) top2b3_push_asc(b1, i1, b2, i2, b3, s, t * TR + row);
             }
         l2_lstore<DP, TR>(lds[buf ^ 1], lnorm[buf ^ 1], stg, nstg);
         __syncthreads();

@@ -151,6 +151,20 @@ def test_l2_f16_split_domain(gpu, oracle, scale, shift):
     check_l2(oracle, q, t)
 
 
+@pytest.mark.parametrize("dim", [128, 200])
+def test_l2_non_finite_coordinates(gpu, oracle, dim):
+    """NaN / inf coordinates in some queries and train rows (the f32 GEMM form takes the launch): a NaN
+    distance never enters a top-2 (the oracle's strict < in index order), +inf distances rank last."""
+    q, t, _ = S.l2_problem(300, 900, dim=dim, seed=31)
+    q, t = q.copy(), t.copy()
+    q[5, 3] = np.nan
+    q[7, :] = np.nan
+    t[11, 0] = np.nan
+    t[13, 2] = np.inf
+    t[17, :] = np.inf
+    check_l2(oracle, q, t)
+
+
 def test_l2_ties_lowest_index(gpu):
     rng = np.random.default_rng(3)
     base = S.sift_like(40, 128, rng)
