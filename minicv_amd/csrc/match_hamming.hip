@@ -243,7 +243,11 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     if (bytesPerDesc < 1 || bytesPerDesc > 64) fail("cvMatchHamming: bytesPerDesc %d outside [1, 64]", bytesPerDesc);
     if (nt < 0 || nt > (int)kIdxMask) fail("cvMatchHamming: nt %d outside [0, 2^22)", nt);
     if (nq <= 0) return 0;
-    thread_local HammingWork wk;
+    int dev = 0;   // per host thread and device (DevBuf does not follow a device switch)
+    MCV_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 16) fail("cvMatchHamming: device %d outside the 16 per-thread workspaces", dev);
+    thread_local HammingWork works[16];
+    HammingWork& wk = works[dev];
     const int W = bytesPerDesc <= 32 ? 8 : 16;
     const uint32_t* q = (const uint32_t*)d_q;
     const uint32_t* t = (const uint32_t*)d_t;

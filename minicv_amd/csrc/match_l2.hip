@@ -912,9 +912,13 @@ struct L2Work {
     bool ran = false;           // a match ran on this thread (its stream may be the null stream)
 };
 
+// Per host thread and device (DevBuf does not follow a device switch of the calling thread).
 static L2Work& l2_work() {
-    thread_local L2Work wk;
-    return wk;
+    int d = 0;
+    MCV_HIP(hipGetDevice(&d));
+    if (d < 0 || d >= 16) fail("cvMatchL2: device %d outside the 16 per-thread workspaces", d);
+    thread_local L2Work wk[16];
+    return wk[d];
 }
 
 int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim, int* d_idx, float* d_dist,
