@@ -29,14 +29,14 @@ sys.path.insert(0, str(ROOT))
 N_CORR = 100_000
 HYPS_PER_GPU = 1 << 20
 F_N_CORR = 500_000            # BASELINE config[3]: findFundamentalMat 8-pt, 500k correspondences
-F_HYPS_TOTAL = 1 << 16        # hypotheses per call, sharded over the ranks (strong scaling)
+F_HYPS_TOTAL = 1 << 20        # hypotheses per call, sharded over the ranks (strong scaling; SURVEY.md:125,410)
 F_SEED = 4
 E_N_CORR = 100_000            # essential (cvRecoverPose path): not a BASELINE config
-E_HYPS_TOTAL = 1 << 16
+E_HYPS_TOTAL = 1 << 20        # as cfg4: 131072 hypotheses per rank at 8 ranks
 E_SEED = 6
 E_FOCAL, E_PP, E_THR_PX = 800.0, (640.0, 360.0), 1.0
 P_N_CORR = 20_000             # PnP (cvSolvePnPRansac path): reference testPnp size (Program.fs:14)
-P_HYPS_TOTAL = 1 << 16
+P_HYPS_TOTAL = 1 << 20
 P_FLOPS_PER_EVAL = 51         # pnp_project: R X + t (18), 1 / Zc (1), distortion + intrinsics (32)
 P_SEED = 8
 P_THR_PX = 2.0
@@ -113,8 +113,12 @@ def dist_setup(torch, dist):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("MCV_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
     if backend != "nccl":
-        local = local % max(torch.cuda.device_count(), 1)
+        local = local % max(ndev, 1)
+    elif local >= ndev:
+        raise SystemExit(f"rank {rank}: {world} ranks over RCCL need {world} visible GPUs, this box has {ndev} "
+                         "(MCV_DIST_BACKEND=gloo rehearses the ranks on a shared device)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -346,8 +350,59 @@ def load_traffic(kernel: str, config: str):
     return None
 
 
+def launch_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N rank processes of this same command, one per GPU,
+    with the environment torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
+    MASTER_ADDR = 127.0.0.1, a free MASTER_PORT), before this process imports torch or touches a GPU
+    (the ranks are children, never an exec). Waits for all of them; when one fails the others are
+    terminated and its exit code is returned. Rank 0 prints the one JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-u", str(Path(__file__).resolve()), *sys.argv[1:]]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env))
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                stop_all()
+                break
+            time.sleep(0.1)
+        if rc == 0:
+            rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    except KeyboardInterrupt:
+        stop_all()
+        rc = 130
+    return 128 - rc if rc < 0 else rc   # a rank killed by signal s -> 128 + s
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
     if args.workload in ("hamming", "l2"):
         return bench_matcher(args)
     if args.workload == "scaled":
@@ -360,10 +415,6 @@ def bench_ransac(args):
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
     world, rank, dev = dist_setup(torch, dist)
 
     from minicv_amd import native as NL, opencv, synthetic as S

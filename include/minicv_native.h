@@ -23,6 +23,7 @@
 
 #include <stdint.h>
 #include <stdbool.h>
+#include <stddef.h>
 
 #if defined(_WIN32)
 #define MCV_API __declspec(dllexport)
@@ -340,7 +341,11 @@ MCV_API int mcvPackEssential(const mcvV2d* a, const mcvV2d* b, int N, double foc
  *   key = (count << 32) | (0xFFFFFFFF - hypIndex)     (0 when no hypothesis has >= m inliers)
  * written to d_key[0]; d_key[1] = first hypothesis index whose sampler failed (or INT64 max).
  * d_counts (optional, may be NULL): per-hypothesis status/count (int32, -1 no model, -2 no sample).
- * Asynchronous on `stream`. Returns 1 on successful launch, 0 on error. */
+ * Asynchronous on `stream`, except with MCV_FLAG_CV_SAMPLER: OpenCV's subset stream is generated on
+ * the host, so the call synchronises `stream` (to check the plan's table against N and the points'
+ * fingerprint, and to rebuild it when hypBegin == 0 or either differs). The plan fingerprints the
+ * points of every evaluated chunk; mcvRansacFinalize re-solves the winner when the buffer's content
+ * changed since (a rewrite in place, same pointer and N). Returns 1 on successful launch, 0 on error. */
 MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const void* d_pts4, int N, const RansacConfig* cfg,
                               int64_t hypBegin, int64_t hypCount, uint64_t* d_key, int* d_counts, void* stream);
 
@@ -476,6 +481,11 @@ MCV_API void mcvHostRodriguesInv(const double* R, double* r);
  * PnP: no check, pts4 may be NULL). Rows from the first failed getSubset on are -1. Returns the number
  * of accepted rows, -1 on bad arguments. */
 MCV_API int64_t mcvCvSubsets(int model, int m, const float* pts4, int N, int64_t rows, int* out);
+/* The plan guards' fingerprint (mcv_common.h fp_term summed over the 32-bit words) of a host buffer:
+ * the device kernel gives the same value for the same bytes. */
+MCV_API uint64_t mcvHostFingerprint(const void* buf, size_t bytes);
+/* The device kernel's fingerprint of a device buffer into d_out[0] (synchronous). Returns 1, 0 on error. */
+MCV_API int mcvTestFingerprint(const void* d_buf, size_t bytes, uint64_t* d_out);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                            uint32_t* out4);
 /* Host twin of CameraPose.findScaled: the same candidates and costs as cvFindScaledPoseCosts,

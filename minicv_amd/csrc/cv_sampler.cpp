@@ -19,6 +19,7 @@
 #include "hyp_homography.h"
 #include "hyp_fundamental.h"
 #include "plan.h"
+#include "kernels.h"
 
 #include <vector>
 #include <cstring>
@@ -107,12 +108,21 @@ void cv_table_build(int model, const RansacConfig& cfg, const float* h_pts4, int
     cv_subsets_m(m, check, h_pts4, N, rows, out.data());
 }
 
-void cv_table_upload(Plan& P, const std::vector<int>& t, int m, int64_t rows, hipStream_t s) {
+bool cv_table_reads_points(int model) { return check_kind(model) != 0; }
+
+uint64_t cv_table_points_fp(int model, const float* h_pts4, int N) {
+    return cv_table_reads_points(model) && h_pts4 ? host_fingerprint(h_pts4, (size_t)N * 16) : 0;
+}
+
+void cv_table_upload(Plan& P, const std::vector<int>& t, int m, int64_t rows, int N, uint64_t pointsFp,
+                     hipStream_t s) {
     P.subsets.ensure((size_t)m * (size_t)std::max<int64_t>(rows, 1));
     MCV_HIP(hipMemcpyAsync(P.subsets.p, t.data(), (size_t)m * rows * sizeof(int), hipMemcpyHostToDevice, s));
     MCV_HIP(hipStreamSynchronize(s));
     P.subsetRows = rows;
     P.subsetM = m;
+    P.subsetN = N;
+    P.subsetFp = pointsFp;
     P.last.clear();
 }
 
@@ -127,7 +137,7 @@ void cv_table_prepare(Plan& P, const void* d_pts, const float* h_pts4, int N, co
     }
     std::vector<int> t;
     cv_table_build(P.model, cfg, h_pts4, N, rows, t);
-    cv_table_upload(P, t, model_points_cfg(P.model, cfg), rows, s);
+    cv_table_upload(P, t, model_points_cfg(P.model, cfg), rows, N, cv_table_points_fp(P.model, h_pts4, N), s);
 }
 
 Sampler Plan::sampler(const RansacConfig& cfg) const {

@@ -178,6 +178,10 @@ void launch_best(const int* d_counts, int n, int64_t hypBegin, int minCount, uin
                  uint64_t* d_out, hipStream_t s);
 void launch_fill_u8(uint8_t* d, int n, uint8_t v, hipStream_t s);
 
+// ---- point-buffer fingerprints (plan_guard.hip; mcv_common.h fp_term): d_out = the sum, async
+void launch_fingerprint(const void* d_buf, size_t bytes, uint64_t* d_out, hipStream_t s);
+uint64_t host_fingerprint(const void* h_buf, size_t bytes);
+
 // ---- match -> RANSAC hand-off (match_pipeline.hip)
 void launch_match_compact(const int* d_idx, const int* d_di1, const int* d_di2, const float* d_df1,
                           const float* d_df2, const int* d_idxBack, int nq, float ratio, float maxDist,

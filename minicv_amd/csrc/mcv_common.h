@@ -166,10 +166,26 @@ MCV_HD int SubsetSrc<M>::next(int N, int (&idx)[M]) {
     if (row) {
 #pragma unroll
         for (int i = 0; i < M; ++i) idx[i] = row[i];
-        return idx[0] >= 0 ? 1 : -1;
+        // a row is a subset of [0, N) by construction (the table is rebuilt whenever N or the points
+        // change, ransac_host.cpp); an index outside it ends the stream instead of reading past pts
+        bool in = true;
+#pragma unroll
+        for (int i = 0; i < M; ++i) in = in && (unsigned)idx[i] < (unsigned)N;
+        return idx[0] >= 0 && in ? 1 : -1;
     }
     return draw_distinct<M>(rs, N, idx) ? 1 : 0;
 }
+
+// Fingerprint of a point buffer (the plan's stale-buffer guards): the sum mod 2^64 over its 32-bit
+// words w_i of fp_term(i, w_i). Position-keyed, so a rewrite, a permutation or a resize changes it
+// (up to 64-bit collisions); a sum, so the device computes it in any order (plan_guard.hip).
+MCV_HD uint64_t fp_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+MCV_HD uint64_t fp_term(uint64_t i, uint32_t w) { return fp_mix(fp_mix(i) ^ (uint64_t)w); }
 
 // v_rcp_f32 + one FMA Newton step: equals the IEEE 1.f / w for every |w| in [2^-126, 2^126)
 // (exhaustive GPU check, mcvTestRcpExhaustive mode 3); callers guarantee that range.

@@ -21,8 +21,11 @@ int model_slots(int model);      // model slots per hypothesis (essential: 10)
 
 // Key of the last evaluated chunk. A winner inside it takes its model from the chunk's buffers
 // instead of a re-solve; the key names everything that produced those buffers (the hypothesis
-// range, the sample source, the point buffer and N, the minimal solver) plus an evaluation
-// generation, so any other evaluate in between, or a different solver / sampler, invalidates it.
+// range, the sample source, the point buffer and N, the minimal solver), and every evaluate replaces
+// it, so any other evaluate in between, or a different solver / sampler, invalidates it. The points'
+// content is keyed too: the evaluate fingerprints the buffer (Plan::fp[0], mark_chunk), finalize
+// fingerprints it again and re-solves the winner when the two differ (a caller that rewrote the
+// buffer in place, same pointer and N, between evaluate and finalize).
 struct LastChunk {
     int64_t begin = -1, count = 0;
     uint64_t seed = 0;
@@ -76,6 +79,10 @@ struct Plan {
     DevBuf<int> subsets;      // MCV_FLAG_CV_SAMPLER: OpenCV's getSubset stream, subsetM ints per hypothesis
     int64_t subsetRows = 0;   // hypotheses [0, subsetRows) covered by `subsets`
     int subsetM = 0;
+    int subsetN = 0;          // the N the table was drawn for (its rows index [0, subsetN))
+    uint64_t subsetFp = 0;    // H / F: fingerprint of the points whose checkSubset accepted the rows
+    DevBuf<uint64_t> fp;      // [0] the last chunk's points (mark_chunk), [1] the points at finalize / check
+    PinnedBuf<uint64_t> h_fp;
     Sampler sampler(const RansacConfig& cfg) const;
     PinnedBuf<int> h_counts;
     PinnedBuf<double> h_red;
@@ -121,13 +128,27 @@ struct ProfScope {
     }
 };
 void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst, hipStream_t s);
+size_t point_bytes(int model, int N);   // device point buffer: 16 N (H / F float4), 32 N (E double4, PnP)
+// Evaluate side: P.last = this chunk, and the fingerprint of its points -> P.fp[0] (async).
+void mark_chunk(Plan& P, int64_t begin, int64_t count, const Sampler& smp, const void* d_pts, int N, int kind,
+                hipStream_t s);
+// Finalize side, on the cached-model path: the current points' fingerprint -> P.fp[1], both to
+// P.h_fp (async; chunk_fresh reads them after the caller's next stream synchronisation).
+void queue_chunk_check(Plan& P, const void* d_pts, int N, hipStream_t s);
+inline bool chunk_fresh(const Plan& P) { return P.h_fp.p[0] == P.h_fp.p[1]; }
+// The device points' fingerprint, synchronously (CV-sampler table checks).
+uint64_t device_fingerprint(Plan& P, const void* d_pts, int N, hipStream_t s);
 double effective_threshold(const RansacConfig& cfg);
 bool cv_sampler(const RansacConfig& cfg);   // MCV_FLAG_CV_SAMPLER
 void check_flags(const RansacConfig& cfg, const char* who);   // rejects the retired bit 4
 // OpenCV's subset stream (cv_sampler.cpp): rows [0, rows) for P's model / cfg, uploaded to P.subsets.
 // h_pts4: host float4 points for the models with a checkSubset (H, F); nullptr = read from d_pts.
 void cv_table_build(int model, const RansacConfig& cfg, const float* h_pts4, int N, int64_t rows, std::vector<int>& out);
-void cv_table_upload(Plan& P, const std::vector<int>& t, int m, int64_t rows, hipStream_t s);
+void cv_table_upload(Plan& P, const std::vector<int>& t, int m, int64_t rows, int N, uint64_t pointsFp,
+                     hipStream_t s);
+bool cv_table_reads_points(int model);   // the table depends on the points (H / F checkSubset), not only N
+// host float4 points -> the fingerprint a table records (0 for the models whose table ignores them)
+uint64_t cv_table_points_fp(int model, const float* h_pts4, int N);
 void cv_table_prepare(Plan& P, const void* d_pts, const float* h_pts4, int N, const RansacConfig& cfg, int64_t rows,
                       hipStream_t s);
 bool fused_error(const RansacConfig& cfg);

@@ -126,7 +126,7 @@ void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
     const bool epnp = pnp_cfg_epnp(cfg);
     const Sampler smp = P.sampler(cfg);
     launch_pnp_generate(d_pts, N, P.pnpCam, smp, hypBegin, hypCount, epnp, P.models.p, d_counts, s, fast_ap3p(cfg));
-    P.last.set(hypBegin, hypCount, smp, d_pts, N, epnp ? 1 : (fast_ap3p(cfg) ? 2 : 0));
+    mark_chunk(P, hypBegin, hypCount, smp, d_pts, N, epnp ? 1 : (fast_ap3p(cfg) ? 2 : 0), s);
     P.bb4.ensure(4);
     launch_pnp_extent(d_pts, N, P.bb4.p, s);
     ProfScope ps("pnp_verify", s);
@@ -389,7 +389,12 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
         // instead of a single-lane re-solve
         const PnpPose* d_m = (const PnpPose*)P.models.p + (hyp - P.last.begin);
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_m, sizeof(PnpPose), hipMemcpyDeviceToHost, s));
+        queue_chunk_check(P, d_pts, N, s);
         MCV_HIP(hipStreamSynchronize(s));
+        if (!chunk_fresh(P)) {   // the points changed since the chunk was evaluated: re-solve
+            P.last.clear();
+            return p_finalize(P, d_pts, N, cfg, hyp, model9, d_mask, s);
+        }
         PnpPose pose;
         std::memcpy(&pose, P.h_one.p, sizeof(PnpPose));
         std::memcpy(one.R, pose.R, sizeof(one.R));

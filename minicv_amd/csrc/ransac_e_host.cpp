@@ -47,7 +47,7 @@ void e_evaluate_chunk(Plan& P, const double* d_pts, int N, const RansacConfig& c
                                P.estage.p, s);
         }
     }
-    P.last.set(hypBegin, hypCount, smp, d_pts, N, fast ? 31 : 30);
+    mark_chunk(P, hypBegin, hypCount, smp, d_pts, N, fast ? 31 : 30, s);
     P.bb4.ensure(4);
     P.pts.ensure((size_t)N * 4);
     launch_abs_bound4(d_pts, true, N, P.bb4.p, P.pts.p, s);   // fp32 copy + bounds for the prefilter
@@ -95,8 +95,10 @@ int e_finalize(Plan& P, const double* d_pts, int N, const RansacConfig& cfg, int
         MCV_HIP(hipGetLastError());
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_out, 9 * sizeof(double), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipMemcpyAsync(P.h_i.p, d_found, sizeof(int), hipMemcpyDeviceToHost, s));
+        queue_chunk_check(P, d_pts, N, s);
         MCV_HIP(hipStreamSynchronize(s));
-        if (P.h_i.p[0] == 1) {
+        if (!chunk_fresh(P)) P.last.clear();   // the points changed since the chunk was evaluated: re-solve
+        else if (P.h_i.p[0] == 1) {
             std::memcpy(E, P.h_one.p, 9 * sizeof(double));
             have = true;
         }

@@ -35,7 +35,12 @@ int f_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
         // of a single-lane re-solve (the eigen-solve's ~0.5 ms latency)
         const FModelD* d_m = (const FModelD*)P.models.p + (hyp - P.last.begin);
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_m, sizeof(FModelD), hipMemcpyDeviceToHost, s));
+        queue_chunk_check(P, d_pts, N, s);
         MCV_HIP(hipStreamSynchronize(s));
+        if (!chunk_fresh(P)) {   // the points changed since the chunk was evaluated: re-solve
+            P.last.clear();
+            return f_finalize(P, d_pts, N, cfg, hyp, F, d_mask, s);
+        }
         std::memcpy(one.F, P.h_one.p, sizeof(FModelD));
         one.status = 1;
     } else {

@@ -162,14 +162,36 @@ Plan& thread_plan(int model, int shard) {
     return *plans.back();
 }
 
+size_t point_bytes(int model, int N) {
+    return (size_t)N * (model == MCV_MODEL_ESSENTIAL || model == MCV_MODEL_PNP ? 32 : 16);
+}
+
 // Device-resident point buffer of a plan (layout per model) and its size in bytes.
 static void* plan_points(Plan& P, int N, size_t* bytes) {
-    if (P.model == MCV_MODEL_ESSENTIAL || P.model == MCV_MODEL_PNP) {
-        *bytes = (size_t)N * 32;
-        return P.ptsd.p;
-    }
-    *bytes = (size_t)N * 16;
-    return P.pts.p;
+    *bytes = point_bytes(P.model, N);
+    return P.model == MCV_MODEL_ESSENTIAL || P.model == MCV_MODEL_PNP ? (void*)P.ptsd.p : (void*)P.pts.p;
+}
+
+void mark_chunk(Plan& P, int64_t begin, int64_t count, const Sampler& smp, const void* d_pts, int N, int kind,
+                hipStream_t s) {
+    P.fp.ensure(2);
+    P.h_fp.ensure(2);
+    P.last.set(begin, count, smp, d_pts, N, kind);
+    launch_fingerprint(d_pts, point_bytes(P.model, N), P.fp.p, s);
+}
+
+void queue_chunk_check(Plan& P, const void* d_pts, int N, hipStream_t s) {
+    launch_fingerprint(d_pts, point_bytes(P.model, N), P.fp.p + 1, s);
+    MCV_HIP(hipMemcpyAsync(P.h_fp.p, P.fp.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+}
+
+uint64_t device_fingerprint(Plan& P, const void* d_pts, int N, hipStream_t s) {
+    P.fp.ensure(2);
+    P.h_fp.ensure(2);
+    launch_fingerprint(d_pts, point_bytes(P.model, N), P.fp.p + 1, s);
+    MCV_HIP(hipMemcpyAsync(P.h_fp.p + 1, P.fp.p + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipStreamSynchronize(s));
+    return P.h_fp.p[1];
 }
 
 void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst, hipStream_t s) {
@@ -345,7 +367,7 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
                               fast_minimal(cfg));
         }
         // the winner's models can come straight from this chunk's buffers (h_finalize)
-        P.last.set(hypBegin, hypCount, smp, d_pts, N, fast_minimal(cfg) ? 21 : 20);
+        mark_chunk(P, hypBegin, hypCount, smp, d_pts, N, fast_minimal(cfg) ? 21 : 20, s);
         ProfScope ps("h_verify", s);
         if (!fused) {
             // default: OpenCV's op-by-op error, certified division-free packed sweep
@@ -377,7 +399,7 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
             launch_f_generate(d_pts, N, smp, hypBegin, hypCount, P.models.p, d_counts, s, fast_minimal(cfg));
         }
         // the winner's fp64 model can come straight from this chunk's buffer (f_finalize)
-        P.last.set(hypBegin, hypCount, smp, d_pts, N, fast_minimal(cfg) ? 11 : 10);
+        mark_chunk(P, hypBegin, hypCount, smp, d_pts, N, fast_minimal(cfg) ? 11 : 10, s);
         P.bb4.ensure(4);
         launch_abs_bound4(d_pts, false, N, P.bb4.p, nullptr, s);
         ProfScope ps("f_verify", s);
@@ -402,7 +424,8 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     // winner re-solve -> mask from the device-side record -> one read-back of both
     HOneOut* d_one = (HOneOut*)P.one.p;
     const Sampler smp = P.sampler(cfg);
-    if (P.last.covers(hyp, smp, d_pts, N, fast_minimal(cfg) ? 21 : 20)) {
+    const bool cached = P.last.covers(hyp, smp, d_pts, N, fast_minimal(cfg) ? 21 : 20);
+    if (cached) {
         // the winner's fp64 and fp32 models straight from the last chunk's buffers (the same code
         // produced them) instead of a single-lane eigen re-solve (~0.4 ms); a winner has status 1
         const int64_t local = hyp - P.last.begin;
@@ -411,6 +434,7 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
                                hipMemcpyDeviceToDevice, s));
         P.h_i.p[1] = 1;
         MCV_HIP(hipMemcpyAsync(&d_one->status, P.h_i.p + 1, sizeof(int), hipMemcpyHostToDevice, s));
+        queue_chunk_check(P, d_pts, N, s);
     } else {
         launch_h_one(d_pts, N, smp, hyp, d_one, s, fast_minimal(cfg));
     }
@@ -421,6 +445,10 @@ int h_finalize(Plan& P, const float* d_pts, int N, const RansacConfig& cfg, int6
     MCV_HIP(hipMemcpyAsync(P.h_one.p, d_one, sizeof(HOneOut), hipMemcpyDeviceToHost, s));
     MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
     MCV_HIP(hipStreamSynchronize(s));
+    if (cached && !chunk_fresh(P)) {   // the points changed since the chunk was evaluated: re-solve
+        P.last.clear();
+        return h_finalize(P, d_pts, N, cfg, hyp, H, d_mask, s);
+    }
     std::memcpy(&one, P.h_one.p, sizeof(HOneOut));
     if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
     const int count = P.h_i.p[0];
@@ -476,6 +504,7 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
     // OpenCV's sample stream: the whole budget's subsets up front (niters only shrinks), uploaded to
     // every shard's workspace
     std::vector<int> table;
+    uint64_t tableFp = 0;
     const int64_t tableRows = std::max(cfg.maxIters, 1);
     if (cv_sampler(cfg)) {
         std::vector<float> host;
@@ -486,7 +515,8 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
             h_pts4 = host.data();
         }
         cv_table_build(P.model, cfg, h_pts4, N, tableRows, table);
-        cv_table_upload(P, table, m, tableRows, s);
+        tableFp = cv_table_points_fp(P.model, h_pts4, N);
+        cv_table_upload(P, table, m, tableRows, N, tableFp, s);
     }
     if (shards > 1) {
         size_t bytes = 0;
@@ -500,7 +530,7 @@ int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
             void* dst = plan_points(Pk, N, &bytes);
             hipStream_t sk = Pk.own_stream();
             MCV_HIP(hipMemcpyPeerAsync(dst, dev, d_pts, home, bytes, sk));
-            if (cv_sampler(cfg)) cv_table_upload(Pk, table, m, tableRows, sk);
+            if (cv_sampler(cfg)) cv_table_upload(Pk, table, m, tableRows, N, tableFp, sk);
             sh.push_back({&Pk, dst, sk, dev});
         }
         MCV_HIP(hipSetDevice(home));
@@ -670,6 +700,18 @@ extern "C" MCV_API int mcvPackCorrespondences(const mcvV2d* a, const mcvV2d* b, 
     })
 }
 
+namespace mcv {
+// The CV-sampler table of P cannot serve hypotheses [.., rowsNeeded) of a search over these points:
+// a search that starts at 0 (begin == 0), too few rows, another sample size, another N, or (H / F,
+// whose checkSubset reads the points) other point content. The content check synchronises s.
+static bool cv_table_stale(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t begin,
+                           int64_t rowsNeeded, hipStream_t s) {
+    if (begin == 0 || P.subsetRows < rowsNeeded || P.subsetM != model_points_cfg(P.model, cfg) || P.subsetN != N)
+        return true;
+    return cv_table_reads_points(P.model) && device_fingerprint(P, d_pts, N, s) != P.subsetFp;
+}
+}  // namespace mcv
+
 extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const void* d_pts4, int N, const RansacConfig* cfg,
                                          int64_t hypBegin, int64_t hypCount, uint64_t* d_key, int* d_counts,
                                          void* stream) {
@@ -684,9 +726,9 @@ extern "C" MCV_API int mcvRansacEvaluate(mcvRansacPlan* plan, const void* d_pts4
         if (hypBegin < 0 || (hypBegin + hypCount) * model_slots_cfg(P->model, *cfg) > 0xFFFFFFFFll)
             fail("mcvRansacEvaluate: hypothesis (slot) index beyond 2^32");
         check_flags(*cfg, "mcvRansacEvaluate");
-        if (cv_sampler(*cfg) && (hypBegin == 0 || P->subsetRows < hypBegin + hypCount ||
-                                 P->subsetM != model_points_cfg(P->model, *cfg)))
-            // a search starts at hypothesis 0: the stream is rebuilt from the current points
+        if (cv_sampler(*cfg) && cv_table_stale(*P, d_pts4, N, *cfg, hypBegin, hypBegin + hypCount, (hipStream_t)stream))
+            // a search starts at hypothesis 0, and a table drawn for other points is never reused: the
+            // stream is rebuilt from the current points
             cv_table_prepare(*P, d_pts4, nullptr, N, *cfg, std::max<int64_t>(hypBegin + hypCount, cfg->maxIters),
                              (hipStream_t)stream);
         evaluate_chunk(*P, d_pts4, N, *cfg, hypBegin, (int)hypCount, d_counts ? d_counts : P->counts.p, d_key,
@@ -704,7 +746,7 @@ extern "C" MCV_API int mcvRansacFinalize(mcvRansacPlan* plan, const void* d_pts4
         check_flags(*cfg, "mcvRansacFinalize");
         P->reserve(N, 1);
         const int64_t hyp = hypIndex / model_slots_cfg(P->model, *cfg);
-        if (cv_sampler(*cfg) && (P->subsetRows <= hyp || P->subsetM != model_points_cfg(P->model, *cfg)))
+        if (cv_sampler(*cfg) && cv_table_stale(*P, d_pts4, N, *cfg, 1, hyp + 1, (hipStream_t)stream))
             cv_table_prepare(*P, d_pts4, nullptr, N, *cfg, std::max<int64_t>(hyp + 1, cfg->maxIters),
                              (hipStream_t)stream);
         return finalize(*P, d_pts4, N, *cfg, hypIndex, model9, d_mask, (hipStream_t)stream);

@@ -114,8 +114,13 @@ struct SampsonPkPair {
 // (for |c| < Ec the outlier left side is <= -Ec (K - Ec)^2 / K <= 0, so no such lane is certified).
 // The cross term's slack Ec (|c| - K)^2 / K is smallest where the decision is close: K is the |c| of
 // a point on the threshold with den = Dm / 4 (the typical den of the bench models lies in
-// [0.01, 0.7] Dm). fp32 evaluation of c^2 and of the FMA (relative u each) sits inside the 2^-21
-// margins on ain / aout; bin / bout are rounded outward.
+// [0.01, 0.7] Dm). fp32 evaluation: c2 = c^2 (1 + d1) and the FMA's sum (den a + b)(1 + d2), |d| <= u
+// = 2^-24, so a computed decision holds for the exact c^2 against (den a + b)(1 +- 2.0001 u). Inlier:
+// den ain + bin > 0 whenever a lane passes (c2 >= 0); (den ain + bin)(1 + 2.0001 u) <= den ain' + bin'
+// because ain carries a 2^-21 margin and bin < 0 only grows more negative under (1 + 2.0001 u).
+// Outlier: (den aout + bout)(1 - 2.0001 u) >= den aout' + bout' needs the margin on both terms: aout
+// carries 2^-21 and bout > 0 (H Ed + Ec (K - Ec) with K > 2 Ec) carries 2^-20 (with only
+// 2^-40 on bout a lane whose den aout is small next to bout was not covered).
 struct SpkCut1 { float ain, bin, aout, bout; };
 MCV_HD SpkCut1 spk_cut1(const SampsonPkBound& b, double Dm, float L32, float H32) {
     SpkCut1 r;
@@ -136,7 +141,7 @@ MCV_HD SpkCut1 spk_cut1(const SampsonPkBound& b, double Dm, float L32, float H32
         r.ain = 0.0f; r.bin = -1.0f;
     }
     r.aout = spk_f32_up(H / (1.0 - e) * (1.0 + 0x1p-21));
-    r.bout = spk_f32_up((H * b.Ed + eck - ec2) / (1.0 - e) * (1.0 + 0x1p-40));
+    r.bout = spk_f32_up((H * b.Ed + eck - ec2) / (1.0 - e) * (1.0 + 0x1p-20));
     return r;
 }
 

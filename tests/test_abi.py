@@ -172,3 +172,28 @@ def test_host_f_hypothesis_bit_exact_vs_oracle(native, oracle, n, outliers, seed
         if st == 1:
             np.testing.assert_array_equal(F, F2)
             np.testing.assert_array_equal(idx, idx2)
+
+
+def test_host_fingerprint_definition(native):
+    """The plan guards' fingerprint (mcv_common.h fp_term: splitmix64 finalizer keyed by the word's
+    position, summed mod 2^64) restated in Python; a rewrite, a swap of two words and a length change
+    all change it."""
+    import numpy as np
+    M = (1 << 64) - 1
+
+    def mix(z):
+        z = (z + 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    rng = np.random.default_rng(1)
+    w = rng.integers(0, 2**32, size=257, dtype=np.uint32)
+    ref = sum(mix(mix(i) ^ int(x)) for i, x in enumerate(w)) & M
+    fp = native.lib().mcvHostFingerprint
+    assert fp(w.ctypes.data, w.nbytes) == ref
+    w2 = w.copy()
+    w2[[3, 4]] = w2[[4, 3]]
+    assert fp(w2.ctypes.data, w2.nbytes) != ref
+    assert fp(w.ctypes.data, w.nbytes - 4) != ref
+    assert fp(w.ctypes.data, 0) == 0

@@ -91,3 +91,36 @@ def test_sampson_cert_edge_inputs(native):
     pts4 = np.ascontiguousarray(np.c_[src, dst], np.float32)
     bad, dec, ex = _cert(L, pts4, dummy, thr2, 1)
     assert bad == 0 and (dec == 0).all()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_sampson_cert_near_epipoles(native, kind):
+    """the outlier cut c^2 > den aout + bout where den is close to 0 (both points near their
+    epipoles, so F x1 and F^T x2 nearly vanish) and the constant term bout dominates: offsets from the
+    epipoles swept over 12 decades put c^2 on both sides of bout. Every decided lane must equal the exact
+    test."""
+    L = native.lib()
+    rng = np.random.default_rng(11)
+    thr2 = np.float32(5e-3 * 5e-3)
+    decided = 0
+    for trial in range(12):
+        G = rng.normal(size=(3, 3))
+        U, s, Vt = np.linalg.svd(G)
+        s[2] = 0
+        F = U @ np.diag(s) @ Vt
+        F /= np.linalg.norm(F)
+        e1, e2 = Vt[2], U[:, 2]               # F e1 = 0, e2^T F = 0
+        if abs(e1[2]) < 1e-3 or abs(e2[2]) < 1e-3:
+            continue
+        e1, e2 = e1[:2] / e1[2], e2[:2] / e2[2]
+        if np.abs(np.r_[e1, e2]).max() > 50:
+            continue
+        n = 4000
+        scale = 10.0 ** rng.uniform(-10, 1, size=(n, 1))
+        x1 = e1 + scale * rng.normal(size=(n, 2))
+        x2 = e2 + scale * rng.normal(size=(n, 2)) * 10.0 ** rng.uniform(-2, 2, size=(n, 1))
+        pts4 = np.ascontiguousarray(np.c_[x1, x2], np.float32)
+        bad, dec, ex = _cert(L, pts4, F, thr2, kind)
+        assert bad == 0, f"trial {trial}: {bad} decided points differ from the exact fp64 test"
+        decided += int((dec >= 0).sum())
+    assert decided > 0
