@@ -55,6 +55,7 @@ FP64_NOFMA_PEAK_TF = FP64_PEAK_TF / 2
 FP32_MFMA_PEAK_TF = 157.3
 F16_MFMA_PEAK_TF = 2516.6      # dense f16 MFMA: 32x32x16 = 16384 MAC per 32 cycles per SIMD, 1024 SIMDs, 2.4 GHz
 INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+I8_MFMA_PEAK_TOPS = 2 * F16_MFMA_PEAK_TF   # MI355X_MICROARCH.md: i8 32x32x32 at the cycles of bf16 32x32x16
 # Algorithmic work per unit: homography computeError = 25 flops per (hypothesis,
 # correspondence) (3 dot products, 1 reciprocal, 2 sub, 2 mul, 1 add, 1 compare); Sampson error =
 # 34 fp64 flops per (model, correspondence) (F x1 12, F^T x2 8, x2^T F x1 4, denominator 7, c^2,
@@ -246,9 +247,21 @@ def bench_matcher(args):
         if ham:
             pairs = cnt * nt
             ach = pairs / (avg_ms * 1e-3)
+            gemm = os.environ.get("MCV_HAMMING_FORM", "") != "popcount"
+            kp = 256   # 32-byte descriptors: 256 +-1 bytes per expanded row
+            mfma_roof = {"bound": "mfma-i8", "achieved": 2.0 * kp * ach / 1e12, "peak": I8_MFMA_PEAK_TOPS,
+                         "unit": "Tops/s", "frac": 2.0 * kp * ach / 1e12 / I8_MFMA_PEAK_TOPS,
+                         "traffic": load_traffic("mcv_hamming_mfma", f"{nq}x{nt}"), "kernel": "mcv_hamming_mfma",
+                         "avg_launch_ms": avg_ms,
+                         "model": "Hamming as a +-1 int8 GEMM: [nt x 256] x [256 x nq] on v_mfma_i32_32x32x32_i8 "
+                                  "(2 x 256 int8 ops per pair; sum a b = 256 - 2 ham), exact in int32; the "
+                                  f"popcount view: {HAM_OPS_PER_PAIR * ach / 1e12:.1f} of {INT32_PEAK_TOPS:.1f} "
+                                  "int32 Tops/s at 24 ops per pair"}
             line = {"metric": "BF Hamming knn-2 queries/sec, 10k x 10k 256-bit (BASELINE config[1])",
                     "value": nq * args.steps / el, "unit": "queries/s",
-                    "roofline": {"bound": "int-valu", "achieved": HAM_OPS_PER_PAIR * ach / 1e12,
+                    "hamming_form": "int8 GEMM on the matrix cores (default)" if gemm else
+                                    "XOR / popcount sweep (MCV_HAMMING_FORM=popcount)",
+                    "roofline": mfma_roof if gemm else {"bound": "int-valu", "achieved": HAM_OPS_PER_PAIR * ach / 1e12,
                                  "peak": INT32_PEAK_TOPS, "unit": "Tops/s",
                                  "frac": HAM_OPS_PER_PAIR * ach / 1e12 / INT32_PEAK_TOPS,
                                  "traffic": load_traffic("mcv_hamming_partial", f"{nq}x{nt}"),
@@ -263,7 +276,7 @@ def bench_matcher(args):
                                            "unit": "pairs/s", "frac": ach / issue_peak(HAMMING_CYC_PER_WAVE_PAIR),
                                            "model": f"{HAMMING_CYC_PER_WAVE_PAIR} SIMD cycles per 64 (query, "
                                                     "train) pairs at 2.4 GHz"}},
-                    "dtype": "u32", "scaling": "strong"}
+                    "dtype": "i8" if gemm else "u32", "scaling": "strong"}
         else:
             exact_scans = NL.lib().mcvL2LastExactScans()
             form = NL.lib().mcvL2LastGemmForm()

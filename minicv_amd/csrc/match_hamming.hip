@@ -21,8 +21,10 @@
 #include "kernels.h"
 #include "mcv_runtime.h"
 #include "plan.h"
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 
 namespace mcv {
 
@@ -218,6 +220,150 @@ __global__ __launch_bounds__(256) void mcv_hamming_merge(const uint2* __restrict
     if (dist2) dist2[qi] = m2 == 0xFFFFFFFFu ? INT_MAX : (int)(m2 >> kIdxBits);
 }
 
+// ---- The GEMM form (default, round 4): Hamming distance as an int8 dot product on the matrix cores.
+// With every bit b of a descriptor mapped to the byte 1 - 2b (+-1), sum_k a_k b_k = Kp - 2 ham(a, b)
+// over the Kp = 32 W bit positions (the zero pads are equal bits: they add 1 each and no distance), so
+// the all-pairs distances are a dense [nt x Kp] x [Kp x nq] int8 GEMM: v_mfma_i32_32x32x32_i8 (2x the
+// bf16 rate, exact in int32). The queries are stored negated and the accumulator starts at Kp, so it
+// ends at 2 ham; key = (2 ham << 21) + trainIdx = ham << 22 | trainIdx, the popcount form's key (the
+// same top-2 rule, bit for bit). Per 32 x 32 tile and lane: 16 keys, each one v_lshl_add_u32 and the
+// med3 / min top-2 update.
+//
+// Expanded rows are read in a fixed k order by both operands: lane l (row / column l & 31, half
+// h = l >> 5) takes bytes [16 KS h + 16 s, + 16) of its row at k step s, so a lane's bytes are
+// contiguous; any order serves, as long as both operands use the same one.
+__global__ void mcv_hamming_expand(const uint32_t* __restrict__ words, int n, int W, int8_t sign,
+                                   int8_t* __restrict__ out) {
+    // one thread per 32-bit word -> 32 bytes (two 16-byte stores)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n * W) return;
+    const uint32_t v = words[i];
+    uint32_t o[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int bit = (v >> (4 * b + k)) & 1;
+            const int8_t e = (int8_t)(sign * (1 - 2 * bit));
+            r |= (uint32_t)(uint8_t)e << (8 * k);
+        }
+        o[b] = r;
+    }
+    uint4* dst = reinterpret_cast<uint4*>(out + (size_t)i * 32);
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+// Block = WPB waves x QT query tiles of 32 (VGPR-resident B fragments); the block's train tiles (32
+// rows x Kp bytes) are staged in LDS (double buffer, 16-byte row pad: conflict-free ds_read_b128) and
+// each A fragment read from LDS feeds QT MFMAs. Grid = (query blocks) x (train chunks); the chunk's
+// top-2 per query goes to part[chunk][query] (mcv_hamming_merge folds the chunks).
+template <int KS, int QT, int WPB>
+__global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const int8_t* __restrict__ qx, int nq,
+                                                             const int8_t* __restrict__ tx, int nt, int ntTiles,
+                                                             int tilesPerChunk, uint2* __restrict__ part, bool xcdMap) {
+    constexpr int RB = 32 * KS;            // bytes per expanded row (Kp)
+    constexpr int RBP = RB + 16;           // LDS row stride
+    constexpr int NT = 64 * WPB;
+    constexpr int CH = 32 * RB / 16;       // 16-byte pieces per train tile
+    constexpr int PER = (CH + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) int8_t lt[2][32 * RBP];
+    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int q0 = (bx * WPB + wave) * QT * 32;
+    i32x4 bq[QT][KS];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int qi = min(q0 + 32 * qt + col, nq - 1);
+        const i32x4* r = reinterpret_cast<const i32x4*>(qx + (size_t)qi * RB + 16 * KS * h);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) bq[qt][s] = r[s];
+    }
+    const int tBegin = by * tilesPerChunk;
+    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
+    uint32_t m1[QT], m2[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = 0xFFFFFFFFu;
+    auto gload = [&](int t, i32x4 (&st)[PER]) {
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int id = threadIdx.x + NT * p;
+            if (id < CH) {
+                const int row = min(t * 32 + id / (RB / 16), nt - 1);
+                st[p] = *reinterpret_cast<const i32x4*>(tx + (size_t)row * RB + 16 * (id % (RB / 16)));
+            }
+        }
+    };
+    auto lstore = [&](int buf, const i32x4 (&st)[PER]) {
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+            const int id = threadIdx.x + NT * p;
+            if (id < CH) *reinterpret_cast<i32x4*>(&lt[buf][(id / (RB / 16)) * RBP + 16 * (id % (RB / 16))]) = st[p];
+        }
+    };
+    // the row offsets of this lane's 16 accumulator entries (C/D layout: row = (i & 3) + 8 (i >> 2) + 4 h)
+    uint32_t rowoff[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rowoff[i] = (uint32_t)((i & 3) + 8 * (i >> 2) + 4 * h);
+    i32x4 st[PER];
+    if (tBegin < tEnd) {
+        gload(tBegin, st);
+        lstore(0, st);
+        gload(min(tBegin + 1, tEnd - 1), st);
+    }
+    __syncthreads();
+    for (int t = tBegin; t < tEnd; ++t) {
+        const int buf = (t - tBegin) & 1;
+        i32x16 acc[QT];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[qt][i] = RB;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const i32x4 a = *reinterpret_cast<const i32x4*>(&lt[buf][col * RBP + 16 * KS * h + 16 * s]);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][s], acc[qt], 0, 0, 0);
+        }
+        // the next tile: staged registers -> the other buffer, then the loads of the one after
+        lstore(buf ^ 1, st);
+        gload(min(t + 2, tEnd - 1), st);
+        const uint32_t base = (uint32_t)t * 32;
+        if (base + 32 <= (uint32_t)nt) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t j = base + rowoff[i];
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) top2_push(m1[qt], m2[qt], ((uint32_t)acc[qt][i] << 21) + j);
+            }
+        } else {   // the train set's last, partial tile: rows past nt never enter a top-2
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t j = base + rowoff[i];
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+                    top2_push(m1[qt], m2[qt], j < (uint32_t)nt ? ((uint32_t)acc[qt][i] << 21) + j : 0xFFFFFFFFu);
+            }
+        }
+        __syncthreads();
+    }
+    // lanes l and l + 32 hold the same query (other rows): merge, then one record per query and chunk
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const uint32_t o1 = __shfl_xor(m1[qt], 32, 64), o2 = __shfl_xor(m2[qt], 32, 64);
+        top2_push(m1[qt], m2[qt], o1);
+        top2_push(m1[qt], m2[qt], o2);
+        const int qi = q0 + 32 * qt + col;
+        if (h == 0 && qi < nq) part[(size_t)by * nq + qi] = make_uint2(m1[qt], m2[qt]);
+    }
+}
+
 // Re-pack [n][bytes] rows into zero-padded [n][W] 32-bit words (XOR of the zero pads is 0).
 __global__ void mcv_hamming_repack(const uint8_t* __restrict__ src, int n, int bytes, int W,
                                    uint32_t* __restrict__ dst) {
@@ -235,7 +381,9 @@ __global__ void mcv_hamming_repack(const uint8_t* __restrict__ src, int n, int b
 
 struct HammingWork {
     DevBuf<uint32_t> qpack, tpack;
+    DevBuf<int8_t> qx, tx;   // the GEMM form's +-1 expansions (Kp = 32 W bytes per row)
     DevBuf<uint2> part;
+    StreamFence fence;   // calls on different streams take turns on these buffers
 };
 
 int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc, int* d_idx,
@@ -248,6 +396,7 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     if (dev < 0 || dev >= 16) fail("cvMatchHamming: device %d outside the 16 per-thread workspaces", dev);
     thread_local HammingWork works[16];
     HammingWork& wk = works[dev];
+    wk.fence.enter(s);
     const int W = bytesPerDesc <= 32 ? 8 : 16;
     const uint32_t* q = (const uint32_t*)d_q;
     const uint32_t* t = (const uint32_t*)d_t;
@@ -262,6 +411,44 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
                                bytesPerDesc, W, wk.tpack.p);
         q = wk.qpack.p;
         t = wk.tpack.p;
+    }
+    // MCV_HAMMING_FORM=popcount: the XOR / popcount sweep (read per call: tests compare both forms)
+    const char* formEnv = getenv("MCV_HAMMING_FORM");
+    const bool gemm = !(formEnv && std::strcmp(formEnv, "popcount") == 0);
+    if (gemm && nt > 0) {
+        constexpr int QT = 2, WPB = 4;
+        const int Kp = 32 * W;
+        wk.qx.ensure((size_t)nq * Kp);
+        wk.tx.ensure((size_t)nt * Kp);
+        hipLaunchKernelGGL(mcv_hamming_expand, dim3((nq * W + 255) / 256), dim3(256), 0, s, q, nq, W, (int8_t)-1,
+                           wk.qx.p);
+        hipLaunchKernelGGL(mcv_hamming_expand, dim3((nt * W + 255) / 256), dim3(256), 0, s, t, nt, W, (int8_t)1,
+                           wk.tx.p);
+        const int qblocks = (nq + 32 * QT * WPB - 1) / (32 * QT * WPB);
+        const int ntTiles = (nt + 31) / 32;
+        static const int target = [] {   // waves in the grid (screen: MCV_HAMMING_WAVES)
+            const char* e = getenv("MCV_HAMMING_WAVES");
+            return e ? atoi(e) : 4096;
+        }();
+        int nchunks = std::max(1, std::min(ntTiles, (target / WPB + qblocks - 1) / qblocks));
+        if (nchunks > 8) nchunks = nchunks / 8 * 8;   // whole XCD rounds
+        const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
+        nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
+        wk.part.ensure((size_t)nchunks * nq);
+        {
+            ProfScope ps("hamming", s);
+            if (W == 8)
+                hipLaunchKernelGGL((mcv_hamming_mfma<8, QT, WPB>), dim3(qblocks, nchunks), dim3(64 * WPB), 0, s, wk.qx.p, nq,
+                                   wk.tx.p, nt, ntTiles, tilesPerChunk, wk.part.p, (8 % nchunks) == 0 || nchunks % 8 == 0);
+            else
+                hipLaunchKernelGGL((mcv_hamming_mfma<16, QT, WPB>), dim3(qblocks, nchunks), dim3(64 * WPB), 0, s, wk.qx.p,
+                                   nq, wk.tx.p, nt, ntTiles, tilesPerChunk, wk.part.p, (8 % nchunks) == 0 || nchunks % 8 == 0);
+        }
+        hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nchunks, d_idx,
+                           d_dist, d_idx2, d_dist2);
+        MCV_HIP(hipGetLastError());
+        wk.fence.leave(s);
+        return nq;
     }
     static const int targetWaves = [] {
         const char* e = getenv("MCV_HAMMING_WAVES");  // variant screen (scripts/sweep_hamming.sh)
@@ -295,6 +482,7 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nparts, d_idx,
                        d_dist, d_idx2, d_dist2);
     MCV_HIP(hipGetLastError());
+    wk.fence.leave(s);
     return nq;
 }
 

@@ -534,6 +534,136 @@ __global__ __launch_bounds__(64 * WPB) void mcv_l2_mfma16(const _Float16* __rest
     }
 }
 
+// Register-blocked variant (round 4): each wave holds QT sets of 32 queries (VGPR-resident hi / lo B
+// fragments), so every A fragment read from LDS feeds 3 QT MFMAs instead of 3, and a block of WPB
+// waves serves 32 QT WPB queries from one staged train tile. Otherwise as mcv_l2_mfma16: two
+// accumulator sets in turn (a tile's MFMAs fill one while the previous tile's epilogue drains the
+// other), LDS double buffer fed two tiles ahead, XCD-aware chunk order.
+template <int DP, int WPB, int QT>
+__global__ __launch_bounds__(64 * WPB) void mcv_l2_mfma16x(const _Float16* __restrict__ qh, const _Float16* __restrict__ ql,
+                                                        const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
+                                                        const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk,
+                                                        int nqPad, L2Part* __restrict__ part,
+                                                        const unsigned* __restrict__ dom, bool xcdMap) {
+    constexpr int TR = 32;
+    if (!l2_f16_domain(dom)) return;   // grid-uniform: the f32 kernel takes this launch
+    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
+    constexpr int KB = DP / 16;
+    constexpr int ROWH = DP + 8;
+    constexpr int NT = 64 * WPB;
+    constexpr int PER = (TR * DP / 8 + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) _Float16 lh[2][TR * ROWH];
+    __shared__ __attribute__((aligned(16))) _Float16 ll[2][TR * ROWH];
+    __shared__ __attribute__((aligned(16))) float lnorm[2][TR];
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int q0 = (bx * WPB + wave) * 32 * QT;
+    f16x8 bh[QT][KB], bl[QT][KB];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const f16x8* rh = reinterpret_cast<const f16x8*>(qh + (size_t)(q0 + 32 * qt + col) * DP + 8 * h);
+        const f16x8* rl = reinterpret_cast<const f16x8*>(ql + (size_t)(q0 + 32 * qt + col) * DP + 8 * h);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            bh[qt][kb] = rh[2 * kb];
+            bl[qt][kb] = rl[2 * kb];
+        }
+    }
+    const int tBegin = by * tilesPerChunk;
+    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
+    float b1[QT], b2[QT], b3[QT];
+    int i1[QT], i2[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        b1[qt] = b2[qt] = b3[qt] = INFINITY;
+        i1[qt] = i2[qt] = -1;
+    }
+    f16x8 sh0[PER], sl0[PER], sh1[PER], sl1[PER];
+    float ns0 = 0.f, ns1 = 0.f;
+    if (tBegin < tEnd) {
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, tBegin, sh0, sl0, ns0);
+        l2_lstore16<DP, TR, NT>(lh[0], ll[0], lnorm[0], sh0, sl0, ns0);
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(tBegin + 1, tEnd - 1), sh1, sl1, ns1);
+    }
+    __syncthreads();
+    floatx16 xm[QT], xs[QT], ym[QT], ys[QT];
+    float4 xn[1][4], yn[1][4];
+    int xt = tBegin, yt = tBegin;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) yn[0][j] = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ym[qt][r] = ys[qt][r] = 0.f;
+    auto epi = [&](const floatx16 (&em)[QT], const floatx16 (&es)[QT], const float4 (&en)[1][4], int base, int r0,
+                   int rn) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const floatx16 a[1] = {em[qt]}, b[1] = {es[qt]};
+            if (rn == 16) l2_epilogue16<1>(a, b, en, base, b1[qt], i1[qt], b2[qt], i2[qt], b3[qt]);
+            else l2_epilogue16<1, 2>(a, b, en, base, b1[qt], i1[qt], b2[qt], i2[qt], b3[qt], r0);
+        }
+    };
+    auto tile = [&](int t, f16x8 (&ldh)[PER], f16x8 (&ldl)[PER], float& ldn, const f16x8 (&sth)[PER],
+                    const f16x8 (&stl)[PER], const float& stn, floatx16 (&cm)[QT], floatx16 (&cs)[QT],
+                    float4 (&cn)[1][4], int& ct, const floatx16 (&em)[QT], const floatx16 (&es)[QT],
+                    const float4 (&en)[1][4], int et) {
+        const int buf = (t - tBegin) & 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cn[0][j] = *reinterpret_cast<const float4*>(&lnorm[buf][8 * j + 4 * h]);
+        ct = t;
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cm[qt][r] = cs[qt][r] = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(&lh[buf][col * ROWH + 16 * kb + 8 * h]);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(&ll[buf][col * ROWH + 16 * kb + 8 * h]);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) cm[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[qt][kb], cm[qt], 0, 0, 0);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) cs[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[qt][kb], cs[qt], 0, 0, 0);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) cs[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[qt][kb], cs[qt], 0, 0, 0);
+            if constexpr (KB == 8) epi(em, es, en, et * TR, 2 * kb, 2);
+        }
+        if constexpr (KB != 8) epi(em, es, en, et * TR, 0, 16);
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), ldh, ldl, ldn);
+        l2_lstore16<DP, TR, NT>(lh[buf ^ 1], ll[buf ^ 1], lnorm[buf ^ 1], sth, stl, stn);
+        __syncthreads();
+    };
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the query fragments, once
+    for (int t = tBegin; t < tEnd; t += 2) {
+        tile(t, sh0, sl0, ns0, sh1, sl1, ns1, xm, xs, xn, xt, ym, ys, yn, yt);
+        if (t + 1 < tEnd) tile(t + 1, sh1, sl1, ns1, sh0, sl0, ns0, ym, ys, yn, yt, xm, xs, xn, xt);
+    }
+    if (tBegin < tEnd) {
+        if (((tEnd - tBegin) & 1) != 0) epi(xm, xs, xn, xt * TR, 0, 16);
+        else epi(ym, ys, yn, yt * TR, 0, 16);
+    }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        if (i1[qt] >= 0) i1[qt] += 4 * h;
+        if (i2[qt] >= 0) i2[qt] += 4 * h;
+        const float ob1 = __shfl_xor(b1[qt], 32, 64), ob2 = __shfl_xor(b2[qt], 32, 64), ob3 = __shfl_xor(b3[qt], 32, 64);
+        const int oi1 = __shfl_xor(i1[qt], 32, 64), oi2 = __shfl_xor(i2[qt], 32, 64);
+        if (h == 0) {
+            float c1 = b1[qt], c2 = b2[qt], c3 = b3[qt];
+            third_fold(c1, c2, c3, ob1);
+            third_fold(c1, c2, c3, ob2);
+            third_fold(c1, c2, c3, ob3);
+            top2_push(b1[qt], i1[qt], b2[qt], i2[qt], ob1, oi1);
+            top2_push(b1[qt], i1[qt], b2[qt], i2[qt], ob2, oi2);
+            L2Part p;
+            p.b1 = b1[qt]; p.b2 = b2[qt]; p.b3 = c3; p.i1 = i1[qt]; p.i2 = i2[qt]; p.i3 = -1;
+            part[(size_t)by * nqPad + q0 + 32 * qt + col] = p;
+        }
+    }
+}
+
 // Exact squared distance (the oracle's definition: fp64 differences, sequential sum in dim order,
 // every operation rounded as written).
 __device__ __forceinline__ double l2_exact(const float* __restrict__ q, const float* __restrict__ t, int dim) {
@@ -624,9 +754,11 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
         if (lex_less_d(e, j, e1, j1)) { e2 = e1; j2 = j1; e1 = e; j1 = j; }
         else if (lex_less_d(e, j, e2, j2)) { e2 = e; j2 = j; }
     }
-    // c3 = the third-smallest GEMM score: every train other than i1, i2 scores >= c3
-    bool certain = nt <= 2;
-    if (!certain && i2 >= 0) {
+    // c3 = the third-smallest GEMM score: every train other than i1, i2 scores >= c3. With nt <= 2 the
+    // candidates are every train row, unless a score was inf / NaN (fp32 norms overflow for |x| ~ 1e19
+    // while the fp64 sums stay finite): a missing candidate sends the query to the exact scan.
+    bool certain = nt == 0 || (nt <= 2 && i1 >= 0 && (nt < 2 || i2 >= 0));
+    if (!certain && nt > 2 && i2 >= 0) {
         const double qn = (double)qnorm[q], T2 = (double)__uint_as_float(*tmaxBits);
         const double u = 0x1p-24;
         const double qa = sqrt(qn * (1.0 + 1e-6)), T = sqrt(T2);
@@ -910,6 +1042,7 @@ struct L2Work {
     hipStream_t last = nullptr; // stream of the last match (the diagnostics read the queue length there)
     bool lastF16 = false;       // the last match launched the f16-split form (its flag decided on device)
     bool ran = false;           // a match ran on this thread (its stream may be the null stream)
+    StreamFence fence;          // calls on different streams take turns on these buffers
 };
 
 // Per host thread and device (DevBuf does not follow a device switch of the calling thread).
@@ -926,6 +1059,7 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     if (dim <= 0 || dim > 256) fail("cvMatchL2: dim %d outside [1, 256]", dim);
     if (nq <= 0) return 0;
     L2Work& wk = l2_work();
+    wk.fence.enter(s);
     const int DP = dim <= 32 ? 32 : dim <= 64 ? 64 : dim <= 128 ? 128 : 256;
     const int nqPad = (nq + 255) / 256 * 256;   // whole 128-query (f32) and 128 / 256-query (f16) blocks
     static const int TRsel = [] {   // train rows per tile (variant screen: 32 or 64)
@@ -1004,7 +1138,20 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
 #define MCV_L2_LAUNCH16(D, W) hipLaunchKernelGGL((mcv_l2_mfma16<D, 32, W>), dim3(nqPad / (32 * W), nchunks), \
                                                  dim3(64 * W), 0, s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, \
                                                  tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
-        if (f16) {
+        static const int qtSel = [] {   // query sets per wave of the f16 form: 1 (mcv_l2_mfma16) or 2 (screen)
+            const char* e = getenv("MCV_L2_QT");
+            return e && atoi(e) == 2 ? 2 : 1;
+        }();
+#define MCV_L2_LAUNCH16X(D) hipLaunchKernelGGL((mcv_l2_mfma16x<D, 4, 2>), dim3(nqPad / 256, nchunks), dim3(256), 0, s, \
+                                               wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, \
+                                               wk.part.p, dom, xcdMap)
+        if (f16 && qtSel == 2) {
+            switch (DP) {
+                case 32: MCV_L2_LAUNCH16X(32); break;
+                case 64: MCV_L2_LAUNCH16X(64); break;
+                default: MCV_L2_LAUNCH16X(128); break;
+            }
+        } else if (f16) {
             switch (DP * 10 + wpb) {
                 case 324: MCV_L2_LAUNCH16(32, 4); break;
                 case 328: MCV_L2_LAUNCH16(32, 8); break;
@@ -1015,6 +1162,7 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
             }
         }
 #undef MCV_L2_LAUNCH16
+#undef MCV_L2_LAUNCH16X
         switch (DP) {
             case 32: if (TR == 64) MCV_L2_LAUNCH(32, 64); else MCV_L2_LAUNCH(32, 32); break;
             case 64: if (TR == 64) MCV_L2_LAUNCH(64, 64); else MCV_L2_LAUNCH(64, 32); break;
@@ -1050,6 +1198,7 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
                            d_dist, d_idx2, d_dist2, scanBlocks);
     }
     MCV_HIP(hipGetLastError());
+    wk.fence.leave(s);
     wk.last = s;
     wk.lastF16 = f16;
     wk.ran = true;

@@ -84,4 +84,26 @@ struct PinnedBuf {
     }
 };
 
+// Orders the uses of one per-thread workspace across streams: the device-level matchers are
+// asynchronous on the caller's stream, so a call on stream B right after one on stream A would race on
+// the shared buffers (and on their finish counters). enter(s) makes s wait for the previous use when
+// that ran on another stream; leave(s) records this use's completion.
+struct StreamFence {
+    hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;
+    bool used = false;
+    void enter(hipStream_t s) {
+        if (used && last != s) MCV_HIP(hipStreamWaitEvent(s, ev, 0));
+    }
+    void leave(hipStream_t s) {
+        if (!ev) MCV_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        MCV_HIP(hipEventRecord(ev, s));
+        last = s;
+        used = true;
+    }
+    ~StreamFence() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
+
 }  // namespace mcv

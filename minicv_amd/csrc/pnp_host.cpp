@@ -867,8 +867,11 @@ extern "C" MCV_API int mcvTestPnpSweep(const float* pts, int N, const double* ca
     });
 }
 
+// fused bit 1 (value 2): the cheap tier alone (its decided lanes must equal the exact test too).
 extern "C" MCV_API int mcvHostPnpCert(const float* pts, int N, const double* cam8, const double* R9, const double* t3,
                                       float thr2, int fused, int* decision, int* exact) {
+    const int tiers = (fused & 2) ? 1 : 3;
+    fused &= 1;
     const PnpPoint* q = (const PnpPoint*)pts;
     double ext[3] = {0, 0, 0};
     for (int i = 0; i < N; ++i) {
@@ -877,11 +880,11 @@ extern "C" MCV_API int mcvHostPnpCert(const float* pts, int N, const double* cam
     }
     const PnpPkCam pc = pnp_pk_cam_host(cam8, thr2);
     PnpPkPose pp;
-    pnp_pk_pose(R9, t3, ext, pp);
+    pnp_pk_pose(R9, t3, ext, pc, pp);
     PnpCamera cam{cam8[0], cam8[1], cam8[2], cam8[3], cam8[4], cam8[5], cam8[6], cam8[7]};
     int bad = 0;
     for (int i = 0; i < N; ++i) {
-        const int d = pc.ok ? pnp_pk_decide_host(pc, pp, q[i].X, q[i].Y, q[i].Z, q[i].u, q[i].v) : -1;
+        const int d = pc.ok ? pnp_pk_decide_host(pc, pp, q[i].X, q[i].Y, q[i].Z, q[i].u, q[i].v, tiers) : -1;
         const int e = pnp_error(cam, R9, t3, q[i].X, q[i].Y, q[i].Z, q[i].u, q[i].v, fused != 0) <= thr2 ? 1 : 0;
         decision[i] = d;
         exact[i] = e;

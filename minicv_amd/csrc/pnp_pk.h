@@ -53,10 +53,19 @@ struct PnpPkCam {
 };
 
 // Per-pose constants (computed per wave from the fp64 pose and the point extents).
+// Cheap tier (round 4): on the domain r2 <= mc^2, |Zc32| >= zmin the per-lane bound g is at most
+// alpha |iz| + beta, and with |iz| <= (iz^2 / kappa + kappa) / 2 (AM-GM) both cuts become one FMA in
+// iz^2 = fl(iz * iz): S < LI0 - LI1 iz^2 (inlier), S > HO0 + HO1 iz^2 (outlier), decided only where
+// w = fma(iz^2, P, r2) <= W (which implies both domain conditions). pnp_pk_pose derives them; a trip
+// with a lane the cheap tier leaves undecided runs the exact per-lane bound (pnp_pk_bound).
 struct PnpPkPose {
     float R[9], t[3];
     float c1, c2, zmin;
+    float LI0, nLI1, HO0, HO1, W, P;   // the cheap tier's cuts (nLI1 = -LI1) and domain
+    float HO0B, HO1B, WB, PB;          // its wide-domain outlier cut (r2 <= kPnpPkMc2B)
 };
+static constexpr double kPnpPkMc2 = 2.0;     // the cheap tier's domain: max(|x|, |y|)^2 <= r2 <= 2
+static constexpr double kPnpPkMc2B = 64.0;   // ... and its outlier-only wide domain
 
 MCV_HD float pk_f32_ru(double v) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -106,8 +115,35 @@ inline PnpPkCam pnp_pk_cam_host(const double* cam8, float thr2) {
     return c;
 }
 
+// The cheap tier's constants for the domain r2 <= mc2 (derivation in pnp_pk_pose).
+MCV_HD void pnp_pk_cheap(const PnpPkPose& p, const PnpPkCam& c, double tz, bool ok, double mc2, float& LI0, float& nLI1,
+                         float& HO0, float& HO1, float& Wo, float& Po) {
+    const double thrLo = c.thrLo, thrHi = c.thrHi, twoT = c.twoT, gk = c.gk;
+    const double mc = sqrt(mc2), izc = (1.0 / (double)p.zmin) * (1 + 0x1p-22);
+    const double a = ((double)p.c1 + mc * (double)p.c2) * (1 + 0x1p-40);
+    const double rc = (mc + izc * a) * (1 + 0x1p-40), rc2 = rc * rc;
+    const double Lc = (1.0 + rc * ((double)c.cp + rc2 * ((double)c.A2 + (double)c.A4 * rc2))) * (1 + 0x1p-38);
+    const double alpha = (double)c.Fg * Lc * a * (1 + 0x1p-38);
+    const double beta = ((double)c.Fg * Lc * (double)c.u13 * rc + (double)c.Cg) * (1 + 0x1p-38);
+    const double kappa = 1.0 / fmax(fabs(tz), (double)p.zmin);
+    const double uu = 2.0 * 0x1p-24;
+    const double li0 = thrLo - twoT * (beta + alpha * kappa * 0.5) * (1 + 0x1p-38) - uu * thrLo;
+    const double li1 = twoT * alpha * (1 + uu) / (2.0 * kappa) * (1 + 0x1p-20);
+    const double ho0 = (thrHi + 2.0 * gk * beta * beta + twoT * (beta + alpha * kappa * 0.5)) * (1 + 0x1p-20);
+    const double ho1 = (2.0 * gk * alpha * alpha + twoT * alpha / (2.0 * kappa)) * (1 + uu) * (1 + 0x1p-20);
+    const double W = mc2 * (1 - 0x1p-20), P = W * (double)p.zmin * (double)p.zmin * (1 + 0x1p-18);
+    const bool cok = ok && c.ok && li0 == li0 && li1 < 0x1p100 && ho0 < 0x1p100 && ho1 < 0x1p100 && P < 0x1p100 &&
+                     P > 0x1p-100;
+    LI0 = cok ? pk_f32_rd(li0) : -__builtin_inff();
+    nLI1 = cok ? -pk_f32_ru(li1) : 0.0f;
+    HO0 = cok ? pk_f32_ru(ho0) : __builtin_inff();
+    HO1 = cok ? pk_f32_ru(ho1) : 0.0f;
+    Wo = cok ? pk_f32_rd(W) : -1.0f;
+    Po = cok ? pk_f32_ru(P) : 1.0f;
+}
+
 // ext = {Xm, Ym, Zm} (inf when any coordinate is not finite).
-MCV_HD void pnp_pk_pose(const double* R, const double* t, const double* ext, PnpPkPose& p) {
+MCV_HD void pnp_pk_pose(const double* R, const double* t, const double* ext, const PnpPkCam& c, PnpPkPose& p) {
     for (int j = 0; j < 9; ++j) p.R[j] = (float)R[j];
     for (int j = 0; j < 3; ++j) p.t[j] = (float)t[j];
     double M[3];
@@ -120,6 +156,25 @@ MCV_HD void pnp_pk_pose(const double* R, const double* t, const double* ext, Pnp
     p.c1 = ok ? pk_f32_ru(eXY * (1 + 0x1p-10) * (1 + 0x1p-7)) : __builtin_inff();
     p.c2 = ok ? pk_f32_ru(1.6 * eZ * (1 + 0x1p-7)) : __builtin_inff();
     p.zmin = ok ? pk_f32_ru(fmax(eZ * 0x1p10, 0x1p-100)) : __builtin_inff();
+    // Cheap tier. On the domain the exact tier's quantities are bounded by (fp64, every step rounded
+    // outward by the 2^-40 factors): |iz32| <= izc (1 + 2^-22) with izc = 1 / zmin; delta <= |iz| a,
+    // a = c1 + mc c2; rho <= rc = mc + izc (1 + 2^-22) a; L <= Lc = L(rc); q = u13 rho + delta <=
+    // u13 rc + |iz| a; g = Fg L q + Cg <= alpha |iz| + beta, alpha = Fg Lc a, beta = Fg Lc u13 rc + Cg.
+    // iz2 = fl(iz32^2) >= iz32^2 (1 - u): |iz32| <= (iz2 (1 + 2u) / kappa + kappa) / 2 and
+    // iz32^2 <= iz2 (1 + 2u). Inlier: thrLo - twoT g >= LI0 - LI1 iz2 with
+    //   LI0 = thrLo - twoT (beta + alpha kappa / 2),  LI1 = twoT alpha (1 + 2u) / (2 kappa);
+    // outlier (g^2 <= 2 alpha^2 iz32^2 + 2 beta^2): thrHi + gk g^2 + twoT g <= HO0 + HO1 iz2 with
+    //   HO0 = thrHi + 2 gk beta^2 + twoT (beta + alpha kappa / 2),
+    //   HO1 = (2 gk alpha^2 + twoT alpha / (2 kappa)) (1 + 2u).
+    // The FMAs' rounding: LI0 lowered by 2u thrLo, LI1 / HO0 / HO1 raised by 2^-20 (an fp32 result
+    // within u of the FMA's exact value then stays on the safe side). Domain: w = fl(fma(iz2, P, r2))
+    // <= W, W = mc^2 (1 - 2^-20), P = W zmin^2 (1 + 2^-18), gives r2 <= W / (1 - u) (so m^2 <=
+    // r2 / (1 - 2u) < mc^2) and iz2 <= 1 / (zmin^2 (1 + 2^-18) (1 - u)) (so 1 / |Zc32| <=
+    // |iz32| (1 + 2^-22) < 1 / zmin); a NaN lane fails it. kappa = 1 / max(|t_z|, zmin): the cut is
+    // tightest for points near the depth of the world origin.
+    pnp_pk_cheap(p, c, t[2], ok, kPnpPkMc2, p.LI0, p.nLI1, p.HO0, p.HO1, p.W, p.P);
+    float li0, nli1;
+    pnp_pk_cheap(p, c, t[2], ok, kPnpPkMc2B, li0, nli1, p.HO0B, p.HO1B, p.WB, p.PB);
 }
 
 // Elementwise helpers: V = float (host twin, one point) or f2 (device, two points).
@@ -186,12 +241,14 @@ MCV_HD PnpPkCamV<V> pnp_pk_cam_v(const PnpPkCam& c, V z) {
     v.one = pkv_splat(1.0f, z);
     return v;
 }
-// Pose: R and c2 as coefficient pairs, t and c1 splatted (each meets a pose coefficient in an FMA).
+// Pose: R and c2 as coefficient pairs, t and c1 splatted (each meets a pose coefficient in an FMA);
+// the cheap tier's constants as VGPR pairs read through op_sel ({P, -LI1}, {LI0, HO1}, {HO0, W}).
 template <class V>
 struct PnpPkPoseV {
     typedef typename PkPairOf<V>::type P;
     P r01, r23, r45, r67, r8c2;
     V t0, t1, t2, c1;
+    P qPl, qLh, qHW, qB0, qB1;   // ..., {PB, HO1B}, {HO0B, WB}
     float zmin;
 };
 template <class V>
@@ -201,20 +258,27 @@ MCV_HD PnpPkPoseV<V> pnp_pk_pose_v(const PnpPkPose& p, V z) {
     v.r67 = pkp_make(p.R[6], p.R[7], z); v.r8c2 = pkp_make(p.R[8], p.c2, z);
     v.t0 = pkv_splat(p.t[0], z); v.t1 = pkv_splat(p.t[1], z); v.t2 = pkv_splat(p.t[2], z);
     v.c1 = pkv_splat(p.c1, z);
+    v.qPl = pkp_make(p.P, p.nLI1, z); v.qLh = pkp_make(p.LI0, p.HO1, z); v.qHW = pkp_make(p.HO0, p.W, z);
+    v.qB0 = pkp_make(p.PB, p.HO1B, z); v.qB1 = pkp_make(p.HO0B, p.WB, z);
     v.zmin = p.zmin;
     return v;
 }
 
-// The certified quantities of one point (V = float) or two points (V = f2) against one pose:
-// S (squared fp32 pixel distance), lo / hi (the two cuts) and Zc (for the domain test |Zc| >= zmin).
-// Per point pair (packed): 40 packed ops, 2 v_rcp_f32, 2 v_max_f32 and 2 v_mul_f32 with |.|.
+// The projection of one point (V = float) or two points (V = f2) against one pose: S (squared fp32
+// pixel distance), the cheap tier's cuts loC / hiC and domain value w (decided where w <= W), and the
+// per-point values the exact tier needs (x, y, iz, Zc). Per point pair (packed): 33 packed ops and
+// 2 v_rcp_f32.
 template <class V>
-MCV_HD void pnp_pk_eval(const PnpPkCamV<V>& c, const PnpPkPoseV<V>& p, V X, V Y, V Z, V uo, V vo, V& S, V& lo, V& hi,
-                        V& Zc) {
+struct PnpPkProj {
+    V S, loC, hiC, w, x, y, iz, Zc, r2;
+};
+template <class V>
+MCV_HD PnpPkProj<V> pnp_pk_project(const PnpPkCamV<V>& c, const PnpPkPoseV<V>& p, V X, V Y, V Z, V uo, V vo) {
     const V z = X;   // type tag only
+    PnpPkProj<V> o;
     const V Xc = pkv_fma(pkp_lo(p.r01, z), X, pkv_fma(pkp_hi(p.r01, z), Y, pkv_fma(pkp_lo(p.r23, z), Z, p.t0)));
     const V Yc = pkv_fma(pkp_hi(p.r23, z), X, pkv_fma(pkp_lo(p.r45, z), Y, pkv_fma(pkp_hi(p.r45, z), Z, p.t1)));
-    Zc = pkv_fma(pkp_lo(p.r67, z), X, pkv_fma(pkp_hi(p.r67, z), Y, pkv_fma(pkp_lo(p.r8c2, z), Z, p.t2)));
+    const V Zc = pkv_fma(pkp_lo(p.r67, z), X, pkv_fma(pkp_hi(p.r67, z), Y, pkv_fma(pkp_lo(p.r8c2, z), Z, p.t2)));
     const V iz = pkv_rcp(Zc);
     const V x = Xc * iz, y = Yc * iz;
     const V r2 = pkv_fma(x, x, y * y);
@@ -225,10 +289,23 @@ MCV_HD void pnp_pk_eval(const PnpPkCamV<V>& c, const PnpPkPoseV<V>& p, V X, V Y,
     const V u = pkv_fma(pkp_hi(c.p2fx, z), xd, c.cx);
     const V v = pkv_fma(pkp_lo(c.fyA4, z), yd, c.cy);
     const V D = uo - u, E = vo - v;
-    S = pkv_fma(D, D, E * E);
-    // bound
-    const V m = pkv_absmax(x, y);
-    const V delta = pkv_absmul(iz, pkv_fma(m, pkp_hi(p.r8c2, z), p.c1));
+    o.S = pkv_fma(D, D, E * E);
+    // cheap tier
+    const V iz2 = iz * iz;
+    o.w = pkv_fma(iz2, pkp_lo(p.qPl, z), r2);
+    o.loC = pkv_fma(iz2, pkp_hi(p.qPl, z), pkp_lo(p.qLh, z));
+    o.hiC = pkv_fma(iz2, pkp_hi(p.qLh, z), pkp_lo(p.qHW, z));
+    o.x = x; o.y = y; o.iz = iz; o.Zc = Zc; o.r2 = r2;
+    return o;
+}
+
+// The exact tier's cuts for the lanes the cheap tier leaves undecided: the per-lane bound g from m =
+// max(|x|, |y|) and |iz| (decided where |Zc| >= zmin). 12 packed ops, 2 v_max_f32 and 2 v_mul_f32 with |.|.
+template <class V>
+MCV_HD void pnp_pk_bound(const PnpPkCamV<V>& c, const PnpPkPoseV<V>& p, const PnpPkProj<V>& o, V& lo, V& hi) {
+    const V z = o.x;
+    const V m = pkv_absmax(o.x, o.y);
+    const V delta = pkv_absmul(o.iz, pkv_fma(m, pkp_hi(p.r8c2, z), p.c1));
     const V rho = m + delta;
     const V rho2 = rho * rho;
     const V L = pkv_fma(rho, pkv_fma(rho2, pkv_fma(rho2, pkp_hi(c.fyA4, z), c.A2), pkp_lo(c.cpu13, z)), c.one);
@@ -239,12 +316,24 @@ MCV_HD void pnp_pk_eval(const PnpPkCamV<V>& c, const PnpPkPoseV<V>& p, V X, V Y,
 }
 
 // Host twin of the decision for one point: 1 certified inlier, 0 certified outlier, -1 undecided.
-inline int pnp_pk_decide_host(const PnpPkCam& c, const PnpPkPose& p, float X, float Y, float Z, float uo, float vo) {
-    float S, lo, hi, Zc;
-    pnp_pk_eval<float>(pnp_pk_cam_v<float>(c, 0.0f), pnp_pk_pose_v<float>(p, 0.0f), X, Y, Z, uo, vo, S, lo, hi, Zc);
-    if (!(std::fabs(Zc) >= p.zmin)) return -1;
-    if (S < lo) return 1;
-    if (S > hi) return 0;
+// tiers: 1 = the cheap tier only, 3 = the sweep's order (cheap, then the exact tier if undecided).
+inline int pnp_pk_decide_host(const PnpPkCam& c, const PnpPkPose& p, float X, float Y, float Z, float uo, float vo,
+                              int tiers = 3) {
+    const PnpPkCamV<float> cv = pnp_pk_cam_v<float>(c, 0.0f);
+    const PnpPkPoseV<float> pv = pnp_pk_pose_v<float>(p, 0.0f);
+    const PnpPkProj<float> o = pnp_pk_project<float>(cv, pv, X, Y, Z, uo, vo);
+    if (o.w <= p.W) {
+        if (o.S < o.loC) return 1;
+        if (o.S > o.hiC) return 0;
+    }
+    const float iz2 = o.iz * o.iz;   // the wide domain's outlier cut (the sweep's second step)
+    if (fmaf(iz2, p.PB, o.r2) <= p.WB && o.S > fmaf(iz2, p.HO1B, p.HO0B)) return 0;
+    if (!(tiers & 2)) return -1;
+    float lo, hi;
+    pnp_pk_bound<float>(cv, pv, o, lo, hi);
+    if (!(std::fabs(o.Zc) >= p.zmin)) return -1;
+    if (o.S < lo) return 1;
+    if (o.S > hi) return 0;
     return -1;
 }
 

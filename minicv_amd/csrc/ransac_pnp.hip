@@ -181,7 +181,7 @@ __device__ __forceinline__ pkf2 pk_uniform(pkf2 v) {
                 __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y)))};
 }
 
-template <int K, int WPE>
+template <int K, int WPE, bool CHEAP = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void mcv_pnp_verify_pk(const PnpPoint* __restrict__ pts, int N, int chunk,
                                                          PnpCamera cam, PnpPkCam pc, const PnpPose* __restrict__ models,
                                                          int* __restrict__ counts, int hypCount, float thr2, bool fused,
@@ -197,9 +197,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const pkf2 z2 = pkf2{0.0f, 0.0f};
     PnpPkCamV<pkf2> cv = pnp_pk_cam_v<pkf2>(pc, z2);
     asm volatile("" : "+v"(cv.k1), "+v"(cv.cx), "+v"(cv.cy), "+v"(cv.A2), "+v"(cv.Cg), "+v"(cv.thrLo), "+v"(cv.twoT));
+    // the projection's coefficient pairs in SGPRs; the exact tier's (rarely run) in VGPR pairs
     cv.k2tp1 = pk_uniform(cv.k2tp1); cv.tp2p1 = pk_uniform(cv.tp2p1); cv.p2fx = pk_uniform(cv.p2fx);
-    cv.fyA4 = pk_uniform(cv.fyA4); cv.cpu13 = pk_uniform(cv.cpu13); cv.Fgnt = pk_uniform(cv.Fgnt);
-    cv.gkHi = pk_uniform(cv.gkHi);
+    cv.fyA4 = pk_uniform(cv.fyA4);
+    asm volatile("" : "+v"(cv.cpu13), "+v"(cv.Fgnt), "+v"(cv.gkHi));
     PnpPkPoseV<pkf2> pp[K];
     bool valid[K];
 #pragma unroll
@@ -208,10 +209,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         valid[k] = hk < hypCount && counts[hk] >= 0;
         const PnpPose m = models[valid[k] ? hk : h0];
         PnpPkPose p;
-        pnp_pk_pose(m.R, m.t, e3, p);
+        pnp_pk_pose(m.R, m.t, e3, pc, p);
         pp[k] = pnp_pk_pose_v<pkf2>(p, z2);
         pp[k].zmin = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(pp[k].zmin)));
         asm volatile("" : "+v"(pp[k].t0), "+v"(pp[k].t1), "+v"(pp[k].t2), "+v"(pp[k].c1));
+        asm volatile("" : "+v"(pp[k].qPl), "+v"(pp[k].qLh), "+v"(pp[k].qHW), "+v"(pp[k].qB0), "+v"(pp[k].qB1));
         // pose coefficient pairs in SGPRs, read through op_sel. (K = 4 poses' pairs plus the ballot masks
         // of their interleaved tests overflow the SGPR file by ~15 spilled dwords per trip; the VGPR-pair
         // placement that avoids it measured slower: 1.92 vs 1.79 ms at the PnP bench. K = 3, the
@@ -237,20 +239,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const pkf2 X = pkf2{a.X, b.X}, Y = pkf2{a.Y, b.Y}, Z = pkf2{a.Z, b.Z};
         const pkf2 U = pkf2{a.u, b.u}, V = pkf2{a.v, b.v};
         uint32_t und = 0;
-        asm volatile("" : "+s"(cv.k2tp1), "+s"(cv.tp2p1), "+s"(cv.p2fx), "+s"(cv.fyA4), "+s"(cv.cpu13), "+s"(cv.Fgnt),
-                     "+s"(cv.gkHi));
+        asm volatile("" : "+s"(cv.k2tp1), "+s"(cv.tp2p1), "+s"(cv.p2fx), "+s"(cv.fyA4));
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             asm volatile("" : "+s"(pp[k].r01), "+s"(pp[k].r23), "+s"(pp[k].r45), "+s"(pp[k].r67), "+s"(pp[k].r8c2));
-            pkf2 S, lo, hi, Zc;
-            pnp_pk_eval<pkf2>(cv, pp[k], X, Y, Z, U, V, S, lo, hi, Zc);
-            const uint64_t d0 = __builtin_amdgcn_ballot_w64(fabsf(Zc.x) >= pp[k].zmin);
-            const uint64_t d1 = __builtin_amdgcn_ballot_w64(fabsf(Zc.y) >= pp[k].zmin);
-            const uint64_t in0 = __builtin_amdgcn_ballot_w64(S.x < lo.x) & d0;
-            const uint64_t in1 = __builtin_amdgcn_ballot_w64(S.y < lo.y) & d1;
-            const uint64_t out0 = __builtin_amdgcn_ballot_w64(S.x > hi.x) & d0;
-            const uint64_t out1 = __builtin_amdgcn_ballot_w64(S.y > hi.y) & d1;
-            const uint64_t u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
+            const PnpPkProj<pkf2> o = pnp_pk_project<pkf2>(cv, pp[k], X, Y, Z, U, V);
+            uint64_t in0 = 0, in1 = 0, out0 = 0, out1 = 0, u = vm0 | vm1;
+            if constexpr (CHEAP) {
+                // cheap tier: one FMA per cut (pnp_pk_pose), decided inside its domain w <= W
+                const float Wk = pp[k].qHW.y;
+                const uint64_t c0 = __builtin_amdgcn_ballot_w64(o.w.x <= Wk);
+                const uint64_t c1 = __builtin_amdgcn_ballot_w64(o.w.y <= Wk);
+                in0 = __builtin_amdgcn_ballot_w64(o.S.x < o.loC.x) & c0;
+                in1 = __builtin_amdgcn_ballot_w64(o.S.y < o.loC.y) & c1;
+                out0 = __builtin_amdgcn_ballot_w64(o.S.x > o.hiC.x) & c0;
+                out1 = __builtin_amdgcn_ballot_w64(o.S.y > o.hiC.y) & c1;
+                u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
+            }
+            if (CHEAP && u != 0) {   // wave-uniform: the wide domain's outlier cut (points projecting off-image)
+                const pkf2 iz2 = o.iz * o.iz;
+                const pkf2 wB = __builtin_elementwise_fma(iz2, pkp_lo(pp[k].qB0, iz2), o.r2);
+                const pkf2 hB = __builtin_elementwise_fma(iz2, pkp_hi(pp[k].qB0, iz2), pkp_lo(pp[k].qB1, iz2));
+                const float WB = pp[k].qB1.y;
+                out0 |= __builtin_amdgcn_ballot_w64(o.S.x > hB.x) & __builtin_amdgcn_ballot_w64(wB.x <= WB);
+                out1 |= __builtin_amdgcn_ballot_w64(o.S.y > hB.y) & __builtin_amdgcn_ballot_w64(wB.y <= WB);
+                u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
+            }
+            if (u != 0) {   // wave-uniform: the exact tier's per-lane bound for this (pose, trip)
+                pkf2 lo, hi;
+                pnp_pk_bound<pkf2>(cv, pp[k], o, lo, hi);
+                const uint64_t d0 = __builtin_amdgcn_ballot_w64(fabsf(o.Zc.x) >= pp[k].zmin);
+                const uint64_t d1 = __builtin_amdgcn_ballot_w64(fabsf(o.Zc.y) >= pp[k].zmin);
+                in0 |= __builtin_amdgcn_ballot_w64(o.S.x < lo.x) & d0;
+                in1 |= __builtin_amdgcn_ballot_w64(o.S.y < lo.y) & d1;
+                out0 |= __builtin_amdgcn_ballot_w64(o.S.x > hi.x) & d0;
+                out1 |= __builtin_amdgcn_ballot_w64(o.S.y > hi.y) & d1;
+                u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
+            }
             // branch-free: a trip with an undecided lane adds nothing here (recounted exactly later)
             const uint32_t bit = u != 0 ? 1u << k : 0u;
             und |= bit;
@@ -681,7 +706,19 @@ static void launch_pnp_verify_pk_k(const void* d_pts, int N, const double* cam8,
         const char* e = getenv("MCV_PNP_WPE");
         return e ? atoi(e) : 3;
     }();
-    if (wpe >= 5)
+    // MCV_PNP_TIERS=2: the cheap tier first (pnp_pk.h), the exact per-lane bound for the (pose, trip)s it
+    // leaves undecided. Measured slower at the PnP bench (26.9 vs 24.1 ms per 2^20 hypotheses: a third
+    // of the (pose, trip)s of EPnP hypotheses hold points projecting off-image, which the cheap tier's
+    // domain excludes, and its branches cost more than the 37 VALU it saves), so the default is the
+    // exact per-lane bound alone.
+    static const bool exactOnly = [] {
+        const char* e = getenv("MCV_PNP_TIERS");
+        return !(e && atoi(e) == 2);
+    }();
+    if (exactOnly)
+        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3, false>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk,
+                           to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
+    else if (wpe >= 5)
         hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 5>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
                            pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
     else if (wpe == 4)

@@ -15,9 +15,9 @@ step() {   # name timeout cmd...
     echo "$name rc=$rc"; tail -2 "$R/gpurun_out/$name.log"
     if [ $rc -ne 0 ]; then exit $rc; fi
 }
-PARTS=${PARTS:-tlsb}
+PARTS=${PARTS:-tplsb}
 if [[ $PARTS == *t* ]]; then
-step pytest_guard 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests/test_gpu_plan_guard.py tests/test_gpu_cv_sampler.py tests/test_gpu_fundamental.py tests/test_gpu_essential.py}
+step pytest_guard 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests/test_gpu_plan_guard.py tests/test_gpu_cv_sampler.py tests/test_gpu_fundamental.py tests/test_gpu_essential.py tests/test_gpu_matchers.py tests/test_gpu_pnp.py}
 fi
 if [[ $PARTS == *l* ]]; then
 for w in ${WORKLOADS:-homography fundamental essential pnp hamming l2 scaled}; do
@@ -29,4 +29,8 @@ step rank_share 600 python scripts/exp/rank_share_timing.py
 fi
 if [[ $PARTS == *b* ]]; then
 step bench_fundamental 300 python bench.py --workload fundamental --steps 5 --warmup 1 --cpu-seconds 8
+fi
+if [[ $PARTS == *p* ]]; then
+step bench_pnp 300 python bench.py --workload pnp --steps 5 --warmup 2 --no-cpu-baseline
+step bench_pnp_ap3p 300 python bench.py --workload pnp --pnp-kind AP3P --steps 5 --warmup 2 --no-cpu-baseline
 fi

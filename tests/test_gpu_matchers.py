@@ -201,3 +201,85 @@ def test_l2_full_size_cfg5(gpu, oracle):
     again = opencv.matchL2(q, t)
     np.testing.assert_array_equal(again[0], idx)
     np.testing.assert_array_equal(again[1], d)
+
+
+@pytest.mark.parametrize("nt", [1, 2, 3])
+def test_l2_fp32_norm_overflow_few_train(gpu, oracle, nt):
+    """coordinates around 1e20 overflow the fp32 norms (every GEMM score inf) while the fp64
+    distances stay finite; with nt <= 2 the refine step once certified the empty candidate list. A query
+    without both candidates now takes the exact scan: the oracle's finite answer."""
+    rng = np.random.default_rng(40 + nt)
+    q = (rng.normal(size=(70, 128)) * 1e20).astype(np.float32)
+    t = (rng.normal(size=(nt, 128)) * 1e20).astype(np.float32)
+    check_l2(oracle, q, t)
+    idx = opencv.matchL2(q, t)[0]
+    assert (idx >= 0).all()
+
+
+def test_matchers_back_to_back_on_two_streams(gpu, oracle):
+    """the device-level matchers are asynchronous on the caller's stream and share one
+    workspace per thread and device; two calls on different streams, issued back to back without a
+    synchronisation, must not race (StreamFence orders them)."""
+    import torch
+    from minicv_amd import device as D
+    dev = torch.device("cuda:0")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    qa, ta, _ = S.l2_problem(3000, 5000, dim=128, seed=51)
+    qb, tb, _ = S.l2_problem(2000, 7000, dim=128, seed=52)
+    ha, hta, _ = S.hamming_problem(3000, 4000, seed=53)
+    hb, htb, _ = S.hamming_problem(2500, 6000, seed=54)
+    out = {}
+    for name, (q, t, fn, dt) in {"l2a": (qa, ta, D.match_l2, torch.float32), "l2b": (qb, tb, D.match_l2, torch.float32),
+                                 "ha": (ha, hta, D.match_hamming, torch.int32),
+                                 "hb": (hb, htb, D.match_hamming, torch.int32)}.items():
+        qd, td = torch.from_numpy(q).to(dev), torch.from_numpy(t).to(dev)
+        out[name] = (qd, td, fn, torch.empty(len(q), dtype=torch.int32, device=dev),
+                     torch.empty(len(q), dtype=dt, device=dev))
+    torch.cuda.synchronize()
+    for k in range(3):
+        for name, s in (("l2a", s1), ("l2b", s2), ("ha", s1), ("hb", s2)):
+            qd, td, fn, idx, dist = out[name]
+            with torch.cuda.stream(s):
+                fn(qd, td, idx, dist, stream=s)
+    torch.cuda.synchronize()
+    for name, (q, t) in {"l2a": (qa, ta), "l2b": (qb, tb)}.items():
+        ri, rd, _, _ = oracle.match_l2(q[:300], t)
+        np.testing.assert_array_equal(out[name][3].cpu().numpy()[:300], ri)
+    for name, (q, t) in {"ha": (ha, hta), "hb": (hb, htb)}.items():
+        ri, rd, _, _ = oracle.match_hamming(q, t)
+        np.testing.assert_array_equal(out[name][3].cpu().numpy(), ri)
+
+
+@pytest.fixture(params=["gemm", "popcount"])
+def hamming_form(request, monkeypatch):
+    """Both Hamming forms: the int8 GEMM on the matrix cores (default) and the XOR / popcount sweep
+    (MCV_HAMMING_FORM=popcount, read by the library on every call)."""
+    if request.param == "popcount":
+        monkeypatch.setenv("MCV_HAMMING_FORM", "popcount")
+    else:
+        monkeypatch.delenv("MCV_HAMMING_FORM", raising=False)
+    return request.param
+
+
+@pytest.mark.parametrize("nq,nt,nbytes", [(1, 1, 32), (33, 31, 32), (257, 1000, 16), (300, 333, 61), (513, 4099, 64),
+                                          (1000, 70000, 32)])
+def test_hamming_forms_agree(gpu, oracle, hamming_form, nq, nt, nbytes):
+    q, t, _ = S.hamming_problem(nq, nt, nbytes=nbytes, seed=3 * nq + nt)
+    check_hamming(oracle, q, t)
+
+
+@pytest.mark.parametrize("nbytes", [32, 64])
+def test_hamming_extreme_distances(gpu, oracle, hamming_form, nbytes):
+    """All-zero / all-one descriptors: distances 0 and the maximum 8 * nbytes (the GEMM form's accumulator
+    at 2 Kp, its key at 2^31 + index), ties at the maximum broken by the lowest index."""
+    rng = np.random.default_rng(nbytes)
+    t = rng.integers(0, 256, size=(3000, nbytes), dtype=np.uint8)
+    t[:100] = 0
+    t[100:200] = 255
+    q = np.concatenate([np.zeros((40, nbytes), np.uint8), np.full((40, nbytes), 255, np.uint8),
+                        rng.integers(0, 256, size=(50, nbytes), dtype=np.uint8)])
+    t2 = np.full((5, nbytes), 255, np.uint8)          # every query at one distance from all of them
+    check_hamming(oracle, q, t)
+    check_hamming(oracle, q[:40], t2)
+    idx, dist, idx2, dist2 = opencv.matchHamming(q[:40], t2)
+    assert (dist == 8 * nbytes).all() and (idx == 0).all() and (idx2 == 1).all()

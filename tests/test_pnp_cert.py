@@ -59,13 +59,19 @@ def test_cert_decisions_equal_exact(native, oracle, di, fused):
             pts8 = oracle.pack_pnp(obs, W)
             bad, dec, ex = _cert(L, pts8, c8, Rp, tp, np.float32(thr * thr), fused)
             assert bad == 0, f"{bad} decided lanes differ from the exact test"
+            badc, decc, _ = _cert(L, pts8, c8, Rp, tp, np.float32(thr * thr), int(fused) | 2)
+            assert badc == 0, f"cheap tier: {badc} decided lanes differ from the exact test"
+            assert ((decc < 0) | (decc == dec)).all()
             m = np.isfinite(obs).all(axis=1)
             total += int(m.sum())
             und += int((dec[m] < 0).sum())
-    # the true pose on the benchmark-like data: essentially everything decided
+    # the true pose on the benchmark-like data: essentially everything decided, nearly all of it by the
+    # cheap tier
     pts8 = oracle.pack_pnp(img, W)
     _, dec, _ = _cert(L, pts8, c8, R, t, np.float32(thr * thr), fused)
     assert (dec < 0).mean() < 1e-3
+    _, decc, _ = _cert(L, pts8, c8, R, t, np.float32(thr * thr), int(fused) | 2)
+    assert (decc < 0).mean() < 0.02
 
 
 def test_cert_edge_inputs(native, oracle):
@@ -90,6 +96,7 @@ def test_cert_edge_inputs(native, oracle):
             pts8 = oracle.pack_pnp(img, W)
             bad, dec, ex = _cert(L, pts8, c8, R, t, thr2, fused)
             assert bad == 0
+            assert _cert(L, pts8, c8, R, t, thr2, int(fused) | 2)[0] == 0
     # a non-finite extent disables certification for every lane (all undecided)
     pts8 = oracle.pack_pnp(img, W)
     _, dec, _ = _cert(L, pts8, c8, R, t, np.float32(4.0), False)
