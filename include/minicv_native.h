@@ -458,8 +458,9 @@ MCV_API int mcvTestPnpSweep(const float* pts, int N, const double* cam8, const d
                             float thr2, int fused, int mode, int* counts);
 /* Host twin of the certified PnP prefilter (pnp_pk.h) for one pose over host PnpPoint[N]: decision[i]
  * = 1 certified inlier, 0 certified outlier, -1 undecided; exact[i] = the fp64 test (pnp_error).
- * fused: bit 0 = the FMA-contracted error; bit 1 = the cheap tier alone (default: the sweep's order,
- * the cheap tier then the exact per-lane bound for what it leaves undecided).
+ * fused: bit 0 = the FMA-contracted error; bit 1 = the cheap tier alone (default: the cheap tier, then
+ * the exact per-lane bound for what it leaves undecided: MCV_PNP_TIERS=2's order; the default sweep
+ * runs the exact bound alone, whose decisions are a superset of the cheap tier's on its domain).
  * Returns the number of decided points whose decision differs from the exact test (must be 0). */
 MCV_API int mcvHostPnpCert(const float* pts, int N, const double* cam8, const double* R9, const double* t3,
                            float thr2, int fused, int* decision, int* exact);

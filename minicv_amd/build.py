@@ -44,11 +44,17 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
+# Per-source extra flags (none). Tried: `-mllvm -amdgpu-mfma-vgpr-form` on match_hamming.hip (MFMA
+# accumulators in VGPRs, no accvgpr copies) returned wrong Hamming distances for a few pairs with two
+# MFMA row tiles per staged train tile (deterministic per grid shape, gone without the flag): not used.
+EXTRA: dict = {}
+
+
 def _compile(src: Path, hmt: float) -> Path:
     obj = BUILD / (src.name + ".o")
-    if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hmt):
+    if obj.exists() and obj.stat().st_mtime > max(src.stat().st_mtime, hmt, Path(__file__).stat().st_mtime):
         return obj
-    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *EXTRA.get(src.name, []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stderr}")

@@ -221,57 +221,48 @@ __global__ __launch_bounds__(256) void mcv_hamming_merge(const uint2* __restrict
 }
 
 // ---- The GEMM form (default, round 4): Hamming distance as an int8 dot product on the matrix cores.
-// With every bit b of a descriptor mapped to the byte 1 - 2b (+-1), sum_k a_k b_k = Kp - 2 ham(a, b)
-// over the Kp = 32 W bit positions (the zero pads are equal bits: they add 1 each and no distance), so
-// the all-pairs distances are a dense [nt x Kp] x [Kp x nq] int8 GEMM: v_mfma_i32_32x32x32_i8 (2x the
-// bf16 rate, exact in int32). The queries are stored negated and the accumulator starts at Kp, so it
-// ends at 2 ham; key = (2 ham << 21) + trainIdx = ham << 22 | trainIdx, the popcount form's key (the
-// same top-2 rule, bit for bit). Per 32 x 32 tile and lane: 16 keys, each one v_lshl_add_u32 and the
-// med3 / min top-2 update.
+// Every bit b of a descriptor becomes the byte 64 (1 - 2 b) (train) or -64 (1 - 2 b) (query), so the
+// int32 sum over the Kp = 32 W bit positions of train x query is -4096 (Kp - 2 ham) (the zero pad bits
+// are equal in both: they add nothing to ham), and with the accumulator started at C = 4096 Kp + j'
+// (j' = the train row's index inside its chunk, < 4096) the MFMA chain ends exactly at the key
+//   acc = 8192 ham + j',
+// ordered as (distance, lowest index): the top-2 update is one v_med3_u32 and one v_min_u32 per score
+// and no key arithmetic. The all-pairs keys are a dense [nt x Kp] x [Kp x nq] int8 GEMM on
+// v_mfma_i32_32x32x32_i8 (2x the bf16 rate, exact in int32). At the end the chunk-local keys become the
+// popcount form's ham << 22 | trainIdx (the same rule, bit for bit).
 //
-// Expanded rows are read in a fixed k order by both operands: lane l (row / column l & 31, half
-// h = l >> 5) takes bytes [16 KS h + 16 s, + 16) of its row at k step s, so a lane's bytes are
-// contiguous; any order serves, as long as both operands use the same one.
-__global__ void mcv_hamming_expand(const uint32_t* __restrict__ words, int n, int W, int8_t sign,
-                                   int8_t* __restrict__ out) {
-    // one thread per 32-bit word -> 32 bytes (two 16-byte stores)
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n * W) return;
-    const uint32_t v = words[i];
-    uint32_t o[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int bit = (v >> (4 * b + k)) & 1;
-            const int8_t e = (int8_t)(sign * (1 - 2 * bit));
-            r |= (uint32_t)(uint8_t)e << (8 * k);
-        }
-        o[b] = r;
-    }
-    uint4* dst = reinterpret_cast<uint4*>(out + (size_t)i * 32);
-    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
-    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+// The +-64 bytes are never stored: word w of a descriptor expands to the 32 bytes [32 w, 32 w + 32),
+// dword d of them holding bits d, d + 8, d + 16, d + 24 (one shift and one v_and_or_b32 per dword).
+// Queries are expanded once into their VGPR-resident B fragments; the block's train tiles are loaded
+// packed (32 B per 256-bit row) and expanded into the LDS tile. Lane l (row / column l & 31, half
+// h = l >> 5) takes bytes [16 KS h + 16 s, + 16) of its row at k step s (word KS h / 2 + s / 2,
+// dwords 4 (s & 1) .. + 3); both operands use the same map.
+template <bool NEG>
+__device__ __forceinline__ int32_t ham_expand_dword(uint32_t v, int d) {   // v: the word, already ~ for NEG
+    const uint32_t x = d < 7 ? v << (7 - d) : v;
+    return (int32_t)((x & 0x80808080u) | 0x40404040u);
 }
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
+static constexpr int kHamChunkRows = 4096;   // j' < 4096 < 8192: the key's index field
 
 // Block = WPB waves x QT query tiles of 32 (VGPR-resident B fragments); the block's train tiles (32
-// rows x Kp bytes) are staged in LDS (double buffer, 16-byte row pad: conflict-free ds_read_b128) and
-// each A fragment read from LDS feeds QT MFMAs. Grid = (query blocks) x (train chunks); the chunk's
-// top-2 per query goes to part[chunk][query] (mcv_hamming_merge folds the chunks).
-template <int KS, int QT, int WPB>
-__global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const int8_t* __restrict__ qx, int nq,
-                                                             const int8_t* __restrict__ tx, int nt, int ntTiles,
+// rows x Kp bytes, expanded from the packed rows) are staged in LDS (double buffer, 16-byte row pad:
+// conflict-free ds_read_b128) and each A fragment read from LDS feeds QT MFMAs. Grid = (query blocks)
+// x (train chunks of <= 4096 rows); the chunk's top-2 per query goes to part[chunk][query]
+// (mcv_hamming_merge folds the chunks).
+template <int W, int QT, int WPB, int SUB>
+__global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
+                                                             const uint32_t* __restrict__ t, int nt, int ntTiles,
                                                              int tilesPerChunk, uint2* __restrict__ part, bool xcdMap) {
-    constexpr int RB = 32 * KS;            // bytes per expanded row (Kp)
+    constexpr int KS = W;                  // k steps of 32 bytes (Kp = 32 W)
+    constexpr int RB = 32 * KS;            // bytes per expanded row
     constexpr int RBP = RB + 16;           // LDS row stride
     constexpr int NT = 64 * WPB;
-    constexpr int CH = 32 * RB / 16;       // 16-byte pieces per train tile
-    constexpr int PER = (CH + NT - 1) / NT;
-    __shared__ __attribute__((aligned(16))) int8_t lt[2][32 * RBP];
+    constexpr int TRW = 32 * SUB;          // train rows per staged tile (SUB MFMA row tiles)
+    constexpr int PER = (TRW * W + NT - 1) / NT;   // packed words of a tile per thread
+    __shared__ __attribute__((aligned(16))) int8_t lt[2][TRW * RBP];
     const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
     const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -281,86 +272,113 @@ __global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const int8_t* __res
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
         const int qi = min(q0 + 32 * qt + col, nq - 1);
-        const i32x4* r = reinterpret_cast<const i32x4*>(qx + (size_t)qi * RB + 16 * KS * h);
+        const uint32_t* qr = q + (size_t)qi * W + (KS / 2) * h;
 #pragma unroll
-        for (int s = 0; s < KS; ++s) bq[qt][s] = r[s];
+        for (int s2 = 0; s2 < KS / 2; ++s2) {
+            const uint32_t wd = ~qr[s2];
+            bq[qt][2 * s2] = i32x4{ham_expand_dword<true>(wd, 0), ham_expand_dword<true>(wd, 1),
+                                   ham_expand_dword<true>(wd, 2), ham_expand_dword<true>(wd, 3)};
+            bq[qt][2 * s2 + 1] = i32x4{ham_expand_dword<true>(wd, 4), ham_expand_dword<true>(wd, 5),
+                                       ham_expand_dword<true>(wd, 6), ham_expand_dword<true>(wd, 7)};
+        }
     }
     const int tBegin = by * tilesPerChunk;
     const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
-    uint32_t m1[QT], m2[QT];
+    uint32_t m1[QT], m2[QT], n1[QT], n2[QT];
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = 0xFFFFFFFFu;
-    auto gload = [&](int t, i32x4 (&st)[PER]) {
+    for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = n1[qt] = n2[qt] = 0xFFFFFFFFu;
+    auto gload = [&](int tl, uint32_t (&st)[PER]) {
 #pragma unroll
         for (int p = 0; p < PER; ++p) {
             const int id = threadIdx.x + NT * p;
-            if (id < CH) {
-                const int row = min(t * 32 + id / (RB / 16), nt - 1);
-                st[p] = *reinterpret_cast<const i32x4*>(tx + (size_t)row * RB + 16 * (id % (RB / 16)));
+            if (id < TRW * W) {
+                const int row = min(tl * TRW + id / W, nt - 1);
+                st[p] = t[(size_t)row * W + id % W];
             }
         }
     };
-    auto lstore = [&](int buf, const i32x4 (&st)[PER]) {
+    auto lstore = [&](int buf, const uint32_t (&st)[PER]) {
 #pragma unroll
         for (int p = 0; p < PER; ++p) {
             const int id = threadIdx.x + NT * p;
-            if (id < CH) *reinterpret_cast<i32x4*>(&lt[buf][(id / (RB / 16)) * RBP + 16 * (id % (RB / 16))]) = st[p];
+            if (id < TRW * W) {
+                const uint32_t v = st[p];
+                int8_t* dst = &lt[buf][(id / W) * RBP + 32 * (id % W)];
+                *reinterpret_cast<i32x4*>(dst) = i32x4{ham_expand_dword<false>(v, 0), ham_expand_dword<false>(v, 1),
+                                                      ham_expand_dword<false>(v, 2), ham_expand_dword<false>(v, 3)};
+                *reinterpret_cast<i32x4*>(dst + 16) = i32x4{ham_expand_dword<false>(v, 4), ham_expand_dword<false>(v, 5),
+                                                           ham_expand_dword<false>(v, 6), ham_expand_dword<false>(v, 7)};
+            }
         }
     };
-    // the row offsets of this lane's 16 accumulator entries (C/D layout: row = (i & 3) + 8 (i >> 2) + 4 h)
-    uint32_t rowoff[16];
+    // accumulator start values: 4096 Kp + j' (rows past nt: 2^30, which ends above every real key)
+    i32x16 c0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) rowoff[i] = (uint32_t)((i & 3) + 8 * (i >> 2) + 4 * h);
-    i32x4 st[PER];
+    for (int i = 0; i < 16; ++i) c0[i] = 4096 * RB + (i & 3) + 8 * (i >> 2) + 4 * h;
+    uint32_t st[PER];
     if (tBegin < tEnd) {
         gload(tBegin, st);
         lstore(0, st);
         gload(min(tBegin + 1, tEnd - 1), st);
     }
     __syncthreads();
-    for (int t = tBegin; t < tEnd; ++t) {
-        const int buf = (t - tBegin) & 1;
-        i32x16 acc[QT];
+    for (int tl = tBegin; tl < tEnd; ++tl) {
+        const int buf = (tl - tBegin) & 1;
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
+        for (int sb = 0; sb < SUB; ++sb) {
+            i32x16 cs = c0;
+            if (__builtin_expect(tl * TRW + 32 * (sb + 1) > nt, 0)) {   // rows past nt (block-uniform)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) acc[qt][i] = RB;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const i32x4 a = *reinterpret_cast<const i32x4*>(&lt[buf][col * RBP + 16 * KS * h + 16 * s]);
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][s], acc[qt], 0, 0, 0);
-        }
-        // the next tile: staged registers -> the other buffer, then the loads of the one after
-        lstore(buf ^ 1, st);
-        gload(min(t + 2, tEnd - 1), st);
-        const uint32_t base = (uint32_t)t * 32;
-        if (base + 32 <= (uint32_t)nt) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint32_t j = base + rowoff[i];
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) top2_push(m1[qt], m2[qt], ((uint32_t)acc[qt][i] << 21) + j);
+                for (int i = 0; i < 16; ++i)
+                    if (tl * TRW + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * h >= nt) cs[i] = 1 << 30;
+                asm volatile("" : "+v"(cs));   // a branch once per launch, not 32 selects per tile
             }
-        } else {   // the train set's last, partial tile: rows past nt never enter a top-2
+            i32x16 acc[QT];
+            const int8_t* ar = &lt[buf][(32 * sb + col) * RBP + 16 * KS * h];
+            {
+                const i32x4 a = *reinterpret_cast<const i32x4*>(ar);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint32_t j = base + rowoff[i];
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt)
-                    top2_push(m1[qt], m2[qt], j < (uint32_t)nt ? ((uint32_t)acc[qt][i] << 21) + j : 0xFFFFFFFFu);
+                for (int qt = 0; qt < QT; ++qt) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][0], cs, 0, 0, 0);
             }
+#pragma unroll
+            for (int s = 1; s < KS; ++s) {
+                const i32x4 a = *reinterpret_cast<const i32x4*>(ar + 16 * s);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][s], acc[qt], 0, 0, 0);
+            }
+            if (sb == SUB - 1) {
+                lstore(buf ^ 1, st);
+                gload(min(tl + 2, tEnd - 1), st);
+            }
+            // two independent top-2 chains per query tile (rows i < 8 and i >= 8), merged at the end:
+            // the med3 / min updates of one chain depend on each other, two chains overlap
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    top2_push(m1[qt], m2[qt], (uint32_t)acc[qt][i]);
+                    top2_push(n1[qt], n2[qt], (uint32_t)acc[qt][i + 8]);
+                }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) c0[i] += 32;
         }
         __syncthreads();
     }
-    // lanes l and l + 32 hold the same query (other rows): merge, then one record per query and chunk
+    // lanes l and l + 32 hold the same query (other rows): merge, then the popcount form's keys
+    const uint32_t base = (uint32_t)tBegin * TRW;
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
+        top2_push(m1[qt], m2[qt], n1[qt]);   // chunk-local keys: the index field keeps them distinct
+        top2_push(m1[qt], m2[qt], n2[qt]);
         const uint32_t o1 = __shfl_xor(m1[qt], 32, 64), o2 = __shfl_xor(m2[qt], 32, 64);
         top2_push(m1[qt], m2[qt], o1);
         top2_push(m1[qt], m2[qt], o2);
+        auto glob = [&](uint32_t k) {
+            // a masked row ends at 2^30 - 4096 (Kp - 2 ham) >= 2^30 - 2^22; a real key is below 2^23
+            return k >= (1u << 29) ? 0xFFFFFFFFu : ((k >> 13) << kIdxBits) | (base + (k & (kHamChunkRows - 1)));
+        };
         const int qi = q0 + 32 * qt + col;
-        if (h == 0 && qi < nq) part[(size_t)by * nq + qi] = make_uint2(m1[qt], m2[qt]);
+        if (h == 0 && qi < nq) part[(size_t)by * nq + qi] = make_uint2(glob(m1[qt]), glob(m2[qt]));
     }
 }
 
@@ -381,7 +399,6 @@ __global__ void mcv_hamming_repack(const uint8_t* __restrict__ src, int n, int b
 
 struct HammingWork {
     DevBuf<uint32_t> qpack, tpack;
-    DevBuf<int8_t> qx, tx;   // the GEMM form's +-1 expansions (Kp = 32 W bytes per row)
     DevBuf<uint2> part;
     StreamFence fence;   // calls on different streams take turns on these buffers
 };
@@ -416,33 +433,37 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     const char* formEnv = getenv("MCV_HAMMING_FORM");
     const bool gemm = !(formEnv && std::strcmp(formEnv, "popcount") == 0);
     if (gemm && nt > 0) {
-        constexpr int QT = 2, WPB = 4;
-        const int Kp = 32 * W;
-        wk.qx.ensure((size_t)nq * Kp);
-        wk.tx.ensure((size_t)nt * Kp);
-        hipLaunchKernelGGL(mcv_hamming_expand, dim3((nq * W + 255) / 256), dim3(256), 0, s, q, nq, W, (int8_t)-1,
-                           wk.qx.p);
-        hipLaunchKernelGGL(mcv_hamming_expand, dim3((nt * W + 255) / 256), dim3(256), 0, s, t, nt, W, (int8_t)1,
-                           wk.tx.p);
+        constexpr int WPB = 4;
+        static const int QT = [] {   // query tiles per wave: 2, or 1 (screen: MCV_HAMMING_QT)
+            const char* e = getenv("MCV_HAMMING_QT");
+            return e && atoi(e) == 1 ? 1 : 2;
+        }();
+        static const int SUB = [] {   // 32-row MFMA tiles per staged train tile: 1, or 2 (screen: MCV_HAMMING_SUB;
+            const char* e = getenv("MCV_HAMMING_SUB");   // 2 measured 33.6 vs 32.1 us at cfg2)
+            return e && atoi(e) == 2 ? 2 : 1;
+        }();
         const int qblocks = (nq + 32 * QT * WPB - 1) / (32 * QT * WPB);
-        const int ntTiles = (nt + 31) / 32;
-        static const int target = [] {   // waves in the grid (screen: MCV_HAMMING_WAVES)
-            const char* e = getenv("MCV_HAMMING_WAVES");
-            return e ? atoi(e) : 4096;
+        const int ntTiles = (nt + 32 * SUB - 1) / (32 * SUB);
+        static const int target = [] {   // waves in the grid (screen: MCV_HAMMING_WAVES; cfg2: 2048 / 4096 /
+            const char* e = getenv("MCV_HAMMING_WAVES");   // 8192 / 16384 -> 43.2 / 33.3 / 32.1 / 34.8 us)
+            return e ? atoi(e) : 8192;
         }();
         int nchunks = std::max(1, std::min(ntTiles, (target / WPB + qblocks - 1) / qblocks));
         if (nchunks > 8) nchunks = nchunks / 8 * 8;   // whole XCD rounds
+        nchunks = std::max(nchunks, (ntTiles * 32 * SUB + kHamChunkRows - 1) / kHamChunkRows);   // key index field
         const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
         nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
+        const bool xcdMap = (8 % nchunks) == 0 || nchunks % 8 == 0;
         wk.part.ensure((size_t)nchunks * nq);
         {
             ProfScope ps("hamming", s);
-            if (W == 8)
-                hipLaunchKernelGGL((mcv_hamming_mfma<8, QT, WPB>), dim3(qblocks, nchunks), dim3(64 * WPB), 0, s, wk.qx.p, nq,
-                                   wk.tx.p, nt, ntTiles, tilesPerChunk, wk.part.p, (8 % nchunks) == 0 || nchunks % 8 == 0);
-            else
-                hipLaunchKernelGGL((mcv_hamming_mfma<16, QT, WPB>), dim3(qblocks, nchunks), dim3(64 * WPB), 0, s, wk.qx.p,
-                                   nq, wk.tx.p, nt, ntTiles, tilesPerChunk, wk.part.p, (8 % nchunks) == 0 || nchunks % 8 == 0);
+#define MCV_HAM_GEMM(W_, Q_, S_) hipLaunchKernelGGL((mcv_hamming_mfma<W_, Q_, WPB, S_>), dim3(qblocks, nchunks), \
+                                                    dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, tilesPerChunk, wk.part.p, \
+                                                    xcdMap)
+            if (W == 8 && QT == 1) { if (SUB == 2) MCV_HAM_GEMM(8, 1, 2); else MCV_HAM_GEMM(8, 1, 1); }
+            else if (W == 8) { if (SUB == 2) MCV_HAM_GEMM(8, 2, 2); else MCV_HAM_GEMM(8, 2, 1); }
+            else { if (SUB == 2) MCV_HAM_GEMM(16, 2, 2); else MCV_HAM_GEMM(16, 2, 1); }
+#undef MCV_HAM_GEMM
         }
         hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nchunks, d_idx,
                            d_dist, d_idx2, d_dist2);
