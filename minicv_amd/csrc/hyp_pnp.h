@@ -25,6 +25,7 @@
 #include "mcv_common.h"
 #include "hyp_essential.h"   // e_poly_real_roots
 #include "epnp.h"   // EPnP; kDblMin
+#include "glibc_math.h"   // glibc's cbrt / hypot / clog branches (the reference's libm)
 
 namespace mcv {
 
@@ -258,7 +259,7 @@ MCV_HD Cplx cplx_sqrt(double x, double y) {
         const double r = fabs(y) >= 2 * kDblMin ? sqrt(0.5 * fabs(y)) : 0.5 * sqrt(2 * fabs(y));
         return {r, copysign(r, y)};
     }
-    const double d = hypot(x, y);
+    const double d = glibc_hypot(x, y);   // glibc's csqrt calls glibc's hypot (glibc_math.h)
     double r, s;
     if (x > 0) {
         r = sqrt(0.5 * (d + x));
@@ -282,8 +283,11 @@ MCV_HD Cplx cplx_div(Cplx a, Cplx b) {
     return {((a.im * ratio) + a.re) / denom, (a.im - (a.re * ratio)) / denom};
 }
 
-// factors: a4, a3, a2, a1, a0 (descending, as solveQuartic reads them)
-MCV_HD void ap3p_solve_quartic(const double* f, double* roots) {
+// factors: a4, a3, a2, a1, a0 (descending, as solveQuartic reads them). cplx (optional) is set when the
+// resolvent's w is complex: pow(w, 1/3) then runs clog / exp / cos / atan2, glibc's table-driven
+// functions, which the device does not restate (its own ocml ones return other last bits), so the device
+// kernels hand those solves to the host (kStatusHostSolve); every other step is glibc's bit for bit.
+MCV_HD void ap3p_solve_quartic(const double* f, double* roots, bool* cplx = nullptr) {
     const double a4 = f[0], a3 = f[1], a2 = f[2], a1 = f[3], a0 = f[4];
     const double a4_2 = a4 * a4, a3_2 = a3 * a3, a4_3 = a4_2 * a4, a2a4 = a2 * a4;
     const double p4 = (8 * a2a4 - 3 * a3_2) / (8 * a4_2);
@@ -296,12 +300,15 @@ MCV_HD void ap3p_solve_quartic(const double* f, double* roots) {
     if (q3 >= 0) w = {-sd.re - q3, -sd.im};
     else w = {sd.re - q3, sd.im};
     double t;
+    if (cplx) *cplx = w.im != 0.0;
     if (w.im == 0.0) {
-        const double wr = cbrt(w.re);
+        const double wr = glibc_cbrt(w.re);   // glibc's bits (glibc_math.h)
         t = 2.0 * (wr + p3 / wr);
     } else {
+        // pow(w, 1 / 3) = polar(exp(log|w| / 3), arg(w) / 3) (libstdc++), log|w| = clog's real part with
+        // glibc's branches; log / log1p / exp / cos / atan2 are the device's own (see glibc_clog_re)
         const double third = 1.0 / 3;
-        const double lr = log(hypot(w.re, w.im)), li = atan2(w.im, w.re);
+        const double lr = glibc_clog_re(w.re, w.im), li = atan2(w.im, w.re);
         t = 4.0 * (exp(third * lr) * cos(third * li));
     }
     const Cplx sqrt_2m = cplx_sqrt(-2 * p4 / 3 + t, 0.0);
@@ -328,12 +335,13 @@ MCV_HD void ap3p_polish(const double* c, double* roots) {
 
 // computePoses exactly as the export runs it: the four polished Ferrari roots in order, |cos| > 1
 // skipped, nothing else filtered (non-finite poses of degenerate input are returned as they come).
-MCV_HD int ap3p_compute_poses_ref(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3]) {
+MCV_HD int ap3p_compute_poses_ref(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3],
+                                  bool* cplx = nullptr) {
     Ap3pSetup S;
     ap3p_setup(b, w, S);
     const double f[5] = {S.c[4], S.c[3], S.c[2], S.c[1], S.c[0]};
     double s[4];
-    ap3p_solve_quartic(f, s);
+    ap3p_solve_quartic(f, s, cplx);
     ap3p_polish(f, s);
     int n = 0;
     for (int i = 0; i < 4; ++i) {
@@ -350,12 +358,13 @@ MCV_HD int ap3p_compute_poses_ref(const double (*b)[3], const double (*w)[3], do
 // it yields a NaN pose, which counts no inliers), poses appended through selects (register-resident).
 // The RANSAC kernel's default; its transcendentals (cbrt, log, atan2, exp, cos, hypot) are the device's
 // own on the GPU and glibc's on the host.
-MCV_HD int ap3p_compute_poses_ferrari(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3]) {
+MCV_HD int ap3p_compute_poses_ferrari(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3],
+                                      bool* cplx = nullptr) {
     Ap3pSetup S;
     ap3p_setup(b, w, S);
     const double f[5] = {S.c[4], S.c[3], S.c[2], S.c[1], S.c[0]};
     double s[4];
-    ap3p_solve_quartic(f, s);
+    ap3p_solve_quartic(f, s, cplx);
     ap3p_polish(f, s);
     int n = 0;
 #pragma unroll
@@ -437,7 +446,8 @@ struct PnpPoint { float X, Y, Z, u, v, pad0, pad1, pad2; };
 // cx_fx = cx / fx) and builds the bearings (ap3p.cpp:285-301's form), computePoses with the Ferrari
 // quartic, and the fourth point picks the solution of least pixel reprojection error
 // ((cx + fx X3p / Z3p - mu3)^2 + ..., first minimum). Returns 1 and the camera-from-world pose, or 0.
-MCV_HD int pnp_ap3p4_cv(const PnpCamera& c, const double* x, const double* y, const double (*W)[3], PnpPose& pose) {
+MCV_HD int pnp_ap3p4_cv(const PnpCamera& c, const double* x, const double* y, const double (*W)[3], PnpPose& pose,
+                        bool* cplx = nullptr) {
     const double inv_fx = 1. / c.fx, inv_fy = 1. / c.fy, cx_fx = c.cx / c.fx, cy_fy = c.cy / c.fy;
     double mu[4], mv[4];
 #pragma unroll
@@ -460,7 +470,7 @@ MCV_HD int pnp_ap3p4_cv(const PnpCamera& c, const double* x, const double* y, co
 #pragma unroll
         for (int k = 0; k < 3; ++k) tr[i][k] = 0.0;
     }
-    const int n = ap3p_compute_poses_ferrari(b, w, Rr, tr);
+    const int n = ap3p_compute_poses_ferrari(b, w, Rr, tr, cplx);
     if (n == 0) return 0;
     double bestErr = 0, bR[9], bt[3];
 #pragma unroll
@@ -488,7 +498,8 @@ MCV_HD int pnp_ap3p4_cv(const PnpCamera& c, const double* x, const double* y, co
 
 // One hypothesis: 4 distinct indices, undistort, AP3P + 4th-point selection: OpenCV's chain
 // (pnp_ap3p4_cv, default) or, with fast (MCV_FLAG_FAST_MINIMAL), the real-root-finder form (pnp_ap3p4).
-// Returns 1 (model), kStatusNoModel or kStatusNoSample.
+// Returns 1 (model), kStatusNoModel or kStatusNoSample; on the device also kStatusHostSolve (the
+// reference's quartic takes the complex-pow branch: ap3p_solve_quartic).
 MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
                           PnpPose& pose, int* idx_out, bool fast = false) {
     SubsetSrc<4> src(smp, hyp);
@@ -509,7 +520,13 @@ MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, const 
         W[i][0] = p.X; W[i][1] = p.Y; W[i][2] = p.Z;
     }
     if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
-    return (fast ? pnp_ap3p4(c, x, y, W, pose) : pnp_ap3p4_cv(c, x, y, W, pose)) ? 1 : kStatusNoModel;
+    bool cplx = false;
+    const int ok = fast ? pnp_ap3p4(c, x, y, W, pose) : pnp_ap3p4_cv(c, x, y, W, pose, &cplx);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (cplx) return kStatusHostSolve;   // glibc's complex pow: the host solves this hypothesis
+#endif
+    (void)cplx;
+    return ok ? 1 : kStatusNoModel;
 }
 
 // PnP solver kinds (the reference's solverKind, MiniCVNative.cpp:99-116): 0 ITERATIVE, 1 EPNP,

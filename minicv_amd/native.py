@@ -145,6 +145,7 @@ SIGNATURES = {
     "mcvHostHypothesis": (_I, [_I, _P, _I, _U64, _I64, _P, _P, _P]),
     "mcvHostPhilox": (None, [C.c_uint32] * 6 + [_P]),
     "mcvHostFingerprint": (_U64, [_P, C.c_size_t]),
+    "mcvHostGlibcMath": (_I, [_I, _P, _P, _I, _P]),
     "mcvTestFingerprint": (_I, [_P, C.c_size_t, _P]),
     "mcvHostEssential": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostEssentialFast": (_I, [_P, _I, _U64, _I64, _P, _P]),

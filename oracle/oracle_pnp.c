@@ -90,6 +90,17 @@ static double nrm(const double* a) { return sqrt(a[0] * a[0] + a[1] * a[1] + a[2
  * Linux: C99 complex with glibc's csqrt / clog, pow(complex, double) = polar(exp(y log|w|), y arg w)
  * (libstdc++'s non-real branch), real / complex through libgcc's __divdc3; then
  * polishQuarticRoots (ap3p.cpp:61-74). f: descending coefficients a4..a0. */
+static _Thread_local int orc_last_branch = -1;   /* the last ferrari_ref's branch: 0 cbrt, 1 complex pow */
+int orc_ap3p_last_branch(void) { return orc_last_branch; }
+
+/* glibc's own functions over arrays (the reference for glibc_math.h's restatements):
+ * fn 0 cbrt(a), 1 hypot(a, b), 2 creal(clog(a + i b)). */
+int orc_libm(int fn, const double* a, const double* b, int n, double* out) {
+    for (int i = 0; i < n; ++i)
+        out[i] = fn == 0 ? cbrt(a[i]) : fn == 1 ? hypot(a[i], b[i]) : creal(clog(CMPLX(a[i], b[i])));
+    return n;
+}
+
 static void ferrari_ref(const double* f, double* roots) {
     double a4 = f[0], a3 = f[1], a2 = f[2], a1 = f[3], a0 = f[4];
     double a4_2 = a4 * a4, a3_2 = a3 * a3, a4_3 = a4_2 * a4, a2a4 = a2 * a4;
@@ -105,6 +116,7 @@ static void ferrari_ref(const double* f, double* roots) {
         w = -sd - q3;
     else
         w = sd - q3;
+    orc_last_branch = cimag(w) == 0.0 ? 0 : 1;
     if (cimag(w) == 0.0) {
         double wr = cbrt(creal(w));
         t = 2.0 * (wr + p3 / wr);
@@ -306,6 +318,7 @@ static int ap3p4_sel(const Cam* c, const double* x, const double* y, const doubl
 int orc_pnp_hypothesis(const float* pts, int N, const double* cam8, uint64_t seed, int64_t hyp, double* R, double* t,
                        int* idx_out) {
     Cam c = cam_of(cam8);
+    orc_last_branch = -1;
     Stream st;
     st.seed = seed; st.hyp = (uint64_t)hyp; st.pos = 0;
     int idx[4];

@@ -51,6 +51,8 @@ _SIGS = {
     "orc_recover_pose": (_I, [_P, _P, _I, _D, _D, _D, _P, _P, _P, _P, _P]),
     "orc_ap3p_poses": (_I, [_P, _P, _P, _P]),
     "orc_solve_ap3p": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _P]),
+    "orc_libm": (_I, [_I, _P, _P, _I, _P]),
+    "orc_ap3p_last_branch": (_I, []),
     "orc_pnp_hypothesis": (_I, [_P, _I, _P, _U64, _I64, _P, _P, _P]),
     "orc_pnp_count": (_I, [_P, _I, _P, _P, _P, _F, _I, _P]),
     "orc_pnp_counts": (None, [_P, _I, _P, _U64, _I64, _I64, _F, _I, _P, _I]),
@@ -549,3 +551,17 @@ def scaled_costs_sample(cam14, world, obs, R, t, n_cand, nthreads=0):
     load().orc_scaled_costs_sample(ptr(cam), ptr(W), ptr(O), n, ptr(R9), ptr(T3), n_cand, ptr(sc), ptr(co),
                                    ptr(used), nthreads)
     return co[:n_cand]
+
+
+def libm(fn, a, b=None):
+    """glibc's cbrt (fn 0), hypot (1) or creal(clog(a + i b)) (2) over arrays, from the oracle library."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(a if b is None else b, dtype=np.float64)
+    out = np.zeros_like(a)
+    load().orc_libm(fn, ptr(a), ptr(b), a.shape[0], ptr(out))
+    return out
+
+
+def ap3p_last_branch():
+    """The branch the oracle's last Ferrari quartic took: 0 real w (cbrt), 1 complex w (pow), -1 none."""
+    return load().orc_ap3p_last_branch()
