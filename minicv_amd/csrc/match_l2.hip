@@ -33,6 +33,7 @@
 #include "kernels.h"
 #include "mcv_runtime.h"
 #include "plan.h"
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -97,70 +98,98 @@ __device__ __forceinline__ void third_fold(float& c1, float& c2, float& c3, floa
 }
 
 // Parity-split, zero-padded copy [nPad][DP] + squared norms (fp32, wave tree sum: the order only
-// affects the GEMM form, whose rounding the exact re-rank bounds whatever the order).
-__global__ void mcv_l2_prep(const float* __restrict__ src, int n, int dim, int DP, int nPad, float* __restrict__ dst,
-                            float* __restrict__ norms, float padNorm, const unsigned* __restrict__ dom) {
+// affects the GEMM form, whose rounding the exact re-rank bounds whatever the order). One launch
+// covers the query and the train set (rows of q, then rows of t).
+struct L2PrepF32 {
+    const float* src;
+    int n, nPad;
+    float* dst;
+    float* norms;
+    float padNorm;
+};
+__global__ void mcv_l2_prep(L2PrepF32 q, L2PrepF32 t, int dim, int DP, const unsigned* __restrict__ dom) {
     if (l2_f16_domain(dom)) return;   // the f16-split path runs (mcv_l2_prep16 wrote the norms)
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (r >= nPad) return;
-    float acc = 0.f;
-    for (int k = lane; k < DP; k += 64) {
-        const float v = (r < n && k < dim) ? src[(size_t)r * dim + k] : 0.f;
-        dst[(size_t)r * DP + (k & 1) * (DP / 2) + (k >> 1)] = v;
-        acc = fmaf(v, v, acc);
-    }
+    for (int rr = blockIdx.x * 4 + (threadIdx.x >> 6); rr < q.nPad + t.nPad; rr += gridDim.x * 4) {
+        const bool isq = rr < q.nPad;
+        const int r = isq ? rr : rr - q.nPad, n = isq ? q.n : t.n;
+        const float* src = isq ? q.src : t.src;
+        float* dst = isq ? q.dst : t.dst;
+        float acc = 0.f;
+        for (int k = lane; k < DP; k += 64) {
+            const float v = (r < n && k < dim) ? src[(size_t)r * dim + k] : 0.f;
+            dst[(size_t)r * DP + (k & 1) * (DP / 2) + (k >> 1)] = v;
+            acc = fmaf(v, v, acc);
+        }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if (lane == 0) norms[r] = r < n ? acc : padNorm;
+        for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (lane == 0) (isq ? q.norms : t.norms)[r] = r < n ? acc : (isq ? q.padNorm : t.padNorm);
+    }
 }
 
-// Max of non-negative float bit patterns over a[0, na) and b[0, nb) (bit order = float order; NaN ->
-// +inf): per-block maxima, the last block to finish folds them, writes *out and re-arms its counter
-// (grid-wide, one launch, no host round trip). The row norms' maximum and the f16 domain use it.
+// Row-per-wave preps run grid-stride over at most this many 4-wave blocks.
+static constexpr int kL2PrepBlocks = 16384;
+static int l2_prep_blocks(int nPad) { return std::min((nPad + 3) / 4, kL2PrepBlocks); }
+
+// Max of non-negative float bit patterns over a[0, na) and b[0, nb) -> *out, and over c[0, nc) ->
+// *out2 when c is given (bit order = float order; NaN -> +inf): per-block maxima, the last block to
+// finish folds them, writes the results and re-arms its counter (grid-wide, one launch, no host round
+// trip). The f16 domain (row maxima of both sets) and the train norms' maximum use it.
 static constexpr int kL2MaxBlocks = 64;
 __global__ __launch_bounds__(256) void mcv_l2_umax(const unsigned* __restrict__ a, int na,
                                                    const unsigned* __restrict__ b, int nb,
+                                                   const unsigned* __restrict__ c, int nc,
                                                    unsigned* __restrict__ part, unsigned* __restrict__ count,
-                                                   unsigned* __restrict__ out) {
-    __shared__ unsigned sm[4];
+                                                   unsigned* __restrict__ out, unsigned* __restrict__ out2) {
+    __shared__ unsigned sm[2][4];
     __shared__ bool last;
-    auto fold = [&](unsigned m) {
+    auto fold = [&](unsigned m, int j) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             const unsigned o = __shfl_xor(m, off, 64);
             m = o > m ? o : m;
         }
-        if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+        if ((threadIdx.x & 63) == 0) sm[j][threadIdx.x >> 6] = m;
         __syncthreads();
-        m = sm[0];
-        for (int w = 1; w < 4; ++w) m = sm[w] > m ? sm[w] : m;
+        m = sm[j][0];
+        for (int w = 1; w < 4; ++w) m = sm[j][w] > m ? sm[j][w] : m;
         return m;
     };
-    unsigned m = 0;
+    auto clampv = [](unsigned v) { return v > 0x7f800000u ? 0x7f800000u : v; };   // NaN (any sign bit) -> +inf
+    unsigned m = 0, m2 = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < na + nb; i += gridDim.x * 256) {
-        unsigned v = i < na ? a[i] : b[i - na];
-        v = v > 0x7f800000u ? 0x7f800000u : v;   // NaN (and any sign-bit pattern) -> +inf
+        const unsigned v = clampv(i < na ? a[i] : b[i - na]);
         m = v > m ? v : m;
     }
-    m = fold(m);
+    if (c)
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < nc; i += gridDim.x * 256) {
+            const unsigned v = clampv(c[i]);
+            m2 = v > m2 ? v : m2;
+        }
+    m = fold(m, 0);
+    m2 = fold(m2, 1);
     if (threadIdx.x == 0) {
         part[blockIdx.x] = m;
+        part[gridDim.x + blockIdx.x] = m2;
         __threadfence();
         last = atomicAdd(count, 1u) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
     __threadfence();
-    unsigned r = 0;
+    unsigned r = 0, r2 = 0;
     for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) {
         const unsigned v = __atomic_load_n(&part[i], __ATOMIC_RELAXED);
+        const unsigned v2 = __atomic_load_n(&part[gridDim.x + i], __ATOMIC_RELAXED);
         r = v > r ? v : r;
+        r2 = v2 > r2 ? v2 : r2;
     }
     __syncthreads();
-    r = fold(r);
+    r = fold(r, 0);
+    r2 = fold(r2, 1);
     if (threadIdx.x == 0) {
         *out = r;
+        if (c) *out2 = r2;
         *count = 0u;
     }
 }
@@ -305,34 +334,49 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
 // Row-major split copies [nPad][DP] (hi = RN f16 of x, lo = RN f16 of the exact fp32 residual x - hi),
 // zero padding, the fp32 squared norm (as mcv_l2_prep) and the row's max |x| (float bits; a
 // non-finite coordinate records +inf: out of the f16 domain; 0 for padding rows). mcv_l2_umax folds
-// the rows' maxima (one atomic per row on one address serialised to ~0.5 ms per call).
-__global__ void mcv_l2_prep16(const float* __restrict__ src, int n, int dim, int DP, int nPad, _Float16* __restrict__ hi,
-                              _Float16* __restrict__ lo, float* __restrict__ norms, float padNorm,
-                              unsigned* __restrict__ rowmax) {
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+// the rows' maxima (one atomic per row on one address serialised to ~0.5 ms per call). The norms equal
+// mcv_l2_prep's bit for bit (the same fmaf order and tree), so either kernel's train norms give the
+// same maximum. One launch covers both sets and zeroes the call's exact-scan queue.
+struct L2PrepF16 {
+    const float* src;
+    int n, nPad;
+    _Float16* hi;
+    _Float16* lo;
+    float* norms;
+    float padNorm;
+    unsigned* rowmax;
+};
+__global__ void mcv_l2_prep16(L2PrepF16 q, L2PrepF16 t, int dim, int DP, int* __restrict__ ambCount) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ambCount = 0;   // the exact-scan queue of this call
     const int lane = threadIdx.x & 63;
-    if (r >= nPad) return;
-    float acc = 0.f;
-    unsigned m = 0;
-    for (int k = lane; k < DP; k += 64) {
-        const float v = (r < n && k < dim) ? src[(size_t)r * dim + k] : 0.f;
-        const _Float16 h = (_Float16)v;
-        hi[(size_t)r * DP + k] = h;
-        lo[(size_t)r * DP + k] = (_Float16)(v - (float)h);
-        acc = fmaf(v, v, acc);
-        const float a = fabsf(v);
-        const unsigned b = a == a && a < __builtin_inff() ? __float_as_uint(a) : 0x7f800000u;
-        m = b > m ? b : m;
-    }
+    for (int rr = blockIdx.x * 4 + (threadIdx.x >> 6); rr < q.nPad + t.nPad; rr += gridDim.x * 4) {
+        const bool isq = rr < q.nPad;
+        const int r = isq ? rr : rr - q.nPad, n = isq ? q.n : t.n;
+        const float* src = isq ? q.src : t.src;
+        _Float16* hi = isq ? q.hi : t.hi;
+        _Float16* lo = isq ? q.lo : t.lo;
+        float acc = 0.f;
+        unsigned m = 0;
+        for (int k = lane; k < DP; k += 64) {
+            const float v = (r < n && k < dim) ? src[(size_t)r * dim + k] : 0.f;
+            const _Float16 h = (_Float16)v;
+            hi[(size_t)r * DP + k] = h;
+            lo[(size_t)r * DP + k] = (_Float16)(v - (float)h);
+            acc = fmaf(v, v, acc);
+            const float a = fabsf(v);
+            const unsigned b = a == a && a < __builtin_inff() ? __float_as_uint(a) : 0x7f800000u;
+            m = b > m ? b : m;
+        }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        acc += __shfl_xor(acc, off, 64);
-        const unsigned o = __shfl_xor(m, off, 64);
-        m = o > m ? o : m;
-    }
-    if (lane == 0) {
-        norms[r] = r < n ? acc : padNorm;
-        rowmax[r] = r < n ? m : 0u;
+        for (int off = 32; off >= 1; off >>= 1) {
+            acc += __shfl_xor(acc, off, 64);
+            const unsigned o = __shfl_xor(m, off, 64);
+            m = o > m ? o : m;
+        }
+        if (lane == 0) {
+            (isq ? q.norms : t.norms)[r] = r < n ? acc : (isq ? q.padNorm : t.padNorm);
+            (isq ? q.rowmax : t.rowmax)[r] = r < n ? m : 0u;
+        }
     }
 }
 
@@ -725,7 +769,7 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
                               float* __restrict__ dist, int* __restrict__ idx2, float* __restrict__ dist2,
                               int* __restrict__ ambCount, int* __restrict__ ambList, double* __restrict__ ambE2,
                               const unsigned* __restrict__ dom) {
-    const int q = blockIdx.x * 256 + threadIdx.x;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     float b1 = INFINITY, b2 = INFINITY, c1 = INFINITY, c2 = INFINITY, c3 = INFINITY;
     int i1 = -1, i2 = -1;
@@ -795,22 +839,23 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
 // Exact scan of the queued queries. Work items = (batch of kL2ScanQ queued queries) x (train chunk),
 // sized from the queue length on the device so that the fixed grid of kL2ScanBlocks workgroups is
 // filled however few queries are queued (no host round trip): T = kL2ScanBlocks / batches chunks
-// per batch (1 when batches >= kL2ScanBlocks). Each lane streams train rows of its chunk and keeps, per
-// query, the lexicographic (d^2, index) top-2 of exact sums; an LDS tree merges the block, and
-// mcv_l2_exact_merge folds the chunks in order.
+// per batch (1 when batches >= kL2ScanBlocks). A workgroup stages its batch (fp32, from the raw
+// queries through the queue) and then tiles of its chunk's train rows (row-major, straight from the
+// caller's train set: the tile is contiguous memory) in LDS; the next tile's loads are in flight in
+// registers while the current one is filtered. Per query it keeps the lexicographic (d^2, index) top-2
+// of exact sums; an LDS tree merges the block, and mcv_l2_exact_merge folds the chunks in order.
 // A certified fp32 filter decides which rows need the exact sum: refine's exact second best of the
 // two GEMM candidates, e2c, bounds the true second best, and a row whose fp32 sum s (packed fp32,
 // sub + fma per dimension) satisfies s > e2c (1 + (dim + 3) u 1.01) + 1e-30 has exact d^2 > e2c
 // (|s - d^2| <= ((1 + gamma_dim)(1 + u)^2 - 1) d^2), so it can enter no top-2; every other row
-// (a handful per query, NaN sums included) gets the exact fp64 sum in dim order in one lane — the
-// oracle's summation, bit for bit.
+// (a handful per query, NaN sums included) gets the exact fp64 sum in dim order — the oracle's
+// summation, bit for bit (the query's fp64 values are its fp32 ones widened, as the oracle's).
+// The tile replaced a lane-per-row walk over a transposed train copy whose dependent loads left the
+// scan latency-bound (64 us at the 8-rank share, whatever the queue length; 42 us with no exact row).
 static constexpr int kL2ScanQ = 32;
-#ifndef MCV_L2_SCAN_THREADS
-#define MCV_L2_SCAN_THREADS 1024
-#endif
-static constexpr int kL2ScanThreads = MCV_L2_SCAN_THREADS;   // 1024: one 16-wave workgroup per CU, whose
-static constexpr int kL2ScanBlocks = 256 * 1024 / kL2ScanThreads;   // waves share one batch in the scalar cache
-static constexpr int kL2ScanPF = 8;           // dims per prefetch group
+static constexpr int kL2ScanThreads = 1024;   // one 16-wave workgroup per CU
+static constexpr int kL2ScanBlocks = 256;
+static constexpr int kL2TileFloats = 128 * 132;   // train tile: 128 rows of dimPad <= 128 (+4 pad)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -833,148 +878,155 @@ __device__ __forceinline__ void l2_write_final(int q, const L2Top2d& r, int* idx
     if (dist2) dist2[q] = r.j2 >= 0 ? (float)sqrt(r.d2) : INFINITY;
 }
 
-// The queued queries batch-interleaved [a / 8][dimPad][8], in fp64 (qd, the exact sums) and fp32 (qf,
-// the filter): one dimension of a batch is 64 (32) contiguous bytes, so the scan reads it with one
-// scalar load off a pointer that advances per dimension. Dimensions dim .. dimPad - 1 are zeros here
-// and in the transposed train copy (an exact +0 in every filter sum), so the filter loop needs no
-// per-dimension guard.
-__global__ void mcv_l2_amb_convert(const float* __restrict__ qraw, int dim, int dimPad,
-                                   const int* __restrict__ ambCount, const int* __restrict__ ambList,
-                                   double* __restrict__ qd, float* __restrict__ qf) {
-    const int n = *ambCount;
-    const int nPad = (n + kL2ScanQ - 1) / kL2ScanQ * kL2ScanQ;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nPad * dimPad; e += gridDim.x * blockDim.x) {
-        const int a = e / dimPad, k = e - a * dimPad;
-        const float v = a < n && k < dim ? qraw[(size_t)ambList[a] * dim + k] : 0.f;
-        const size_t o = ((size_t)(a / kL2ScanQ) * dimPad + k) * kL2ScanQ + (a % kL2ScanQ);
-        qd[o] = (double)v;
-        qf[o] = v;
+// The exact fp64 distance of one row to one query by a whole wave (every lane active): lane k forms
+// the k-th squared difference (each product rounded on its own, as in the sequential loop), then the
+// products are added in dimension order off the lanes (v_readlane into an SGPR operand): the oracle's
+// sum bit for bit. qcol = the query's fp32 column in LDS (stride kL2ScanQ), row = the tile row.
+__device__ __forceinline__ double l2_exact_row_wave(const float* qcol, const float* row, int dim, int lane) {
+    double p[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int k = c * 64 + lane;
+        const double df = k < dim ? (double)qcol[k * kL2ScanQ] - (double)row[k] : 0.0;
+        p[c] = df * df;
     }
+    double d = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int n = min(64, dim - c * 64);
+        if (n <= 0) break;
+        const unsigned long long bits = __double_as_longlong(p[c]);
+        const int lo = (int)(unsigned)bits, hi = (int)(unsigned)(bits >> 32);
+        for (int l = 0; l < n; ++l) {
+            const unsigned long long v = (unsigned long long)(unsigned)__builtin_amdgcn_readlane(lo, l) |
+                                         ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(hi, l) << 32);
+            d = d + __longlong_as_double((long long)v);
+        }
+    }
+    return d;
 }
 
-// The train set transposed ([dim][nt]) for the exact scan's coalesced reads; skipped on the device
-// when nothing is queued.
-__global__ __launch_bounds__(256) void mcv_l2_transpose_train(const float* __restrict__ traw, int nt, int dim,
-                                                              int dimPad, const int* __restrict__ ambCount,
-                                                              float* __restrict__ tT) {
-    if (*ambCount == 0) return;
-    __shared__ float tile[64][65];
-    const int j0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    for (int r = ty; r < 64; r += 4) {
-        const int j = j0 + r, k = k0 + tx;
-        tile[r][tx] = j < nt && k < dim ? traw[(size_t)j * dim + k] : 0.f;
-    }
-    __syncthreads();
-    for (int r = ty; r < 64; r += 4) {
-        const int k = k0 + r, j = j0 + tx;
-        if (k < dimPad && j < nt) tT[(size_t)k * nt + j] = tile[tx][r];
-    }
-}
-
+// DPMAX = 128: tiles of 128 rows, 4 queries per thread; DPMAX = 256: 64 rows, 2 queries per thread.
+// Thread t filters tile row t % RT against queries (t / RT) * QG .. + QG - 1 (wave-uniform: the
+// query values are LDS broadcasts).
+template <int DPMAX>
 __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
-    const double* __restrict__ qd, const float* __restrict__ qf, const float* __restrict__ tT,
-    const float* __restrict__ traw, int nt, int dim, int dimPad, const int* __restrict__ ambCount,
-    const int* __restrict__ ambList, const double* __restrict__ ambE2, L2Top2d* __restrict__ part,
-    int* __restrict__ idx, float* __restrict__ dist, int* __restrict__ idx2, float* __restrict__ dist2) {
-    constexpr int NW = kL2ScanThreads / 64;
-    const int blocks = gridDim.x;
-    // per wave and query: the lexicographic top-2 of the exact sums the wave computed (rare updates,
-    // wave-uniform, so no atomics); the filter bounds
+    const float* __restrict__ qraw, const float* __restrict__ traw, int nt, int dim, int dimPad,
+    const int* __restrict__ ambCount, const int* __restrict__ ambList, const double* __restrict__ ambE2,
+    L2Top2d* __restrict__ part, int* __restrict__ idx, float* __restrict__ dist, int* __restrict__ idx2,
+    float* __restrict__ dist2) {
+    constexpr int NT = kL2ScanThreads, NW = NT / 64;
+    constexpr int RS = DPMAX + 4;                    // tile row stride (floats; 16-B aligned rows)
+    constexpr int RT = kL2TileFloats / (128 + 4) * 128 / DPMAX;   // 128 or 64 rows
+    constexpr int QG = kL2ScanQ * RT / NT;           // queries per thread: 4 or 2
+    constexpr int RSTEP = NT / DPMAX;                // tile rows one pass of the workgroup loads
+    constexpr int PER = RT / RSTEP;                  // tile elements per thread
+    static_assert(QG == 2 || QG == 4, "tile shape");
     __shared__ L2Top2d wtop[NW][kL2ScanQ];
     __shared__ double sthr[kL2ScanQ];
+    __shared__ __attribute__((aligned(16))) float sq[DPMAX * kL2ScanQ];   // [dimPad][kL2ScanQ]
+    __shared__ __attribute__((aligned(16))) float tile[RT * RS];
     const int n = *ambCount;
     const int nbatch = (n + kL2ScanQ - 1) / kL2ScanQ;
     if (nbatch == 0) return;
-    const int T = l2_scan_chunks(nbatch, blocks);
+    const int T = l2_scan_chunks(nbatch, gridDim.x);
     const double F = 1.0 + 1.01 * (dim + 3) * 0x1p-24;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int trow = threadIdx.x % RT, qg = threadIdx.x / RT;
+    // tile loads: thread t loads dimension t % DPMAX of rows t / DPMAX + i RSTEP (coalesced along each
+    // row; dimensions >= dim load as zeros, an exact +0 in every sum; no division per element)
+    const int ek = threadIdx.x & (DPMAX - 1), erb = threadIdx.x / DPMAX;
+    const bool kin = ek < dim;
+    auto tload = [&](float (&v)[PER], int r0, int re) {
+        const float* src = traw + (size_t)(r0 + erb) * dim + ek;
+        const int lim = re - r0 - erb;   // rows i RSTEP < lim are inside the chunk
+#pragma unroll
+        for (int i = 0; i < PER; ++i) v[i] = kin && i * RSTEP < lim ? src[(size_t)i * RSTEP * dim] : 0.f;
+    };
+    auto tstore = [&](const float (&v)[PER]) {
+        float* dst = tile + erb * RS + ek;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) dst[i * RSTEP * RS] = v[i];
+    };
     for (int item = blockIdx.x; item < nbatch * T; item += gridDim.x) {
         const int batch = item / T, chunk = item % T;
         const int a0 = batch * kL2ScanQ;
         const int nb = min(kL2ScanQ, n - a0);
         const int jb = (int)((int64_t)chunk * nt / T), je = (int)((int64_t)(chunk + 1) * nt / T);
-        // the batch's blocks of qd / qf (wave-uniform addresses: scalar loads, SGPR operands; the
-        // padding members of the last batch are zeros and never reported)
-        const double* qb = qd + (size_t)batch * dimPad * kL2ScanQ;
-        const f32x2* qb2 = reinterpret_cast<const f32x2*>(qf + (size_t)batch * dimPad * kL2ScanQ);
+        float nxt[PER];
+        tload(nxt, jb, je);   // the first tile's loads overlap the batch staging
+        {
+            // thread t stages query t % kL2ScanQ, dimensions t / kL2ScanQ + i NT / kL2ScanQ: one queue
+            // read, then independent loads (the last batch's padding members are zeros, never reported)
+            const int b = threadIdx.x % kL2ScanQ;
+            const float* qr = b < nb ? qraw + (size_t)ambList[a0 + b] * dim : nullptr;
+            for (int k = threadIdx.x / kL2ScanQ; k < dimPad; k += NT / kL2ScanQ)
+                sq[k * kL2ScanQ + b] = qr && k < dim ? qr[k] : 0.f;
+        }
         if (threadIdx.x < kL2ScanQ) {
             const int b = threadIdx.x;
             const double t = ambE2[a0 + min(b, nb - 1)] * F + 1e-30;
-            // near fp32 overflow the filter decides nothing; the last batch's padding members skip all
+            // near fp32 overflow the filter decides nothing; the padding members skip every row
             sthr[b] = b >= nb ? -INFINITY : t < 1e38 ? t : INFINITY;
         }
         if (lane < kL2ScanQ) wtop[wv][lane] = L2Top2d{INFINITY, INFINITY, -1, -1};
-        __syncthreads();
-        // lane = train row: dimension k of 64 consecutive rows is one coalesced 256-byte load of the
-        // transposed copy. One linear sequence of (row, group of kL2ScanPF dims) steps per lane, the
-        // same for every lane (lanes with fewer rows stop early): group L + 2's loads are issued while
-        // group L is summed, across row boundaries.
-        const int G = dimPad / kL2ScanPF;
-        const int jl = jb + threadIdx.x;
-        const int rows = jl < je ? (je - 1 - jl) / kL2ScanThreads + 1 : 0;
-        const int Ltot = rows * G;
-        // unconditional loads (a step past the lane's rows re-reads row jb, unused): the in-order
-        // vmcnt waits then count exact numbers of loads
-        auto gload = [&](float (&buf)[kL2ScanPF], int L) {
-            const int rr = L / G, k0 = (L - rr * G) * kL2ScanPF;
-            const int jj = L < Ltot ? jl + rr * kL2ScanThreads : jb;
+        for (int r0 = jb; r0 < je; r0 += RT) {
+            __syncthreads();   // the previous tile's readers are done (and the batch is staged)
+            tstore(nxt);
+            __syncthreads();
+            if (r0 + RT < je) tload(nxt, r0 + RT, je);   // in flight while this tile is filtered
+            const float* tr = tile + trow * RS;
+            const float* qv = sq + qg * QG;
+            f32x2 acc[QG / 2];
 #pragma unroll
-            for (int kk = 0; kk < kL2ScanPF; ++kk) buf[kk] = tT[(size_t)(k0 + kk) * nt + jj];
-        };
-        f32x2 sacc[kL2ScanQ / 2];
-        // a row the filter cannot exclude for query b: the exact fp64 sum in dimension order, computed
-        // by the whole wave on the row's wave-uniform address, one candidate lane at a time
-        auto exact_rows = [&](int b, bool pass, int jr) {
-            uint64_t m = __ballot(pass);
+            for (int p = 0; p < QG / 2; ++p) acc[p] = (f32x2)(0.f);
+            // 8 dimensions a trip, every LDS read of the trip issued before the first use; a wave whose
+            // queries are all padding members of the last batch skips the trip loop (wave-uniform)
+            const int kEnd = qg * QG < nb ? dimPad : 0;
+            for (int k = 0; k < kEnd; k += 8) {
+                const float4 t4a = *reinterpret_cast<const float4*>(tr + k);
+                const float4 t4b = *reinterpret_cast<const float4*>(tr + k + 4);
+                f32x2 qk[8][QG / 2];
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                    for (int p = 0; p < QG / 2; ++p)
+                        qk[kk][p] = *reinterpret_cast<const f32x2*>(qv + (k + kk) * kL2ScanQ + 2 * p);
+                const float tk[8] = {t4a.x, t4a.y, t4a.z, t4a.w, t4b.x, t4b.y, t4b.z, t4b.w};
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) {
+                    const f32x2 tv = (f32x2)(tk[kk]);
+#pragma unroll
+                    for (int p = 0; p < QG / 2; ++p) {
+                        const f32x2 df = qk[kk][p] - tv;
+                        acc[p] = __builtin_elementwise_fma(df, df, acc[p]);
+                    }
+                }
+            }
+            uint32_t pend = 0;
+            if (r0 + trow < je) {
+#pragma unroll
+                for (int p = 0; p < QG / 2; ++p) {
+                    pend |= (uint32_t)!((double)acc[p].x > sthr[qg * QG + 2 * p]) << (2 * p);
+                    pend |= (uint32_t)!((double)acc[p].y > sthr[qg * QG + 2 * p + 1]) << (2 * p + 1);
+                }
+            }
+            // the rows the filter kept: exact sums by the whole wave, one (row, query) at a time
+            uint64_t m = __ballot(pend != 0);
             while (m) {
                 const int l = __ffsll((unsigned long long)m) - 1;
                 m &= m - 1;
-                const int jc = __builtin_amdgcn_readlane(jr, l);
-                const float* tr = traw + (size_t)jc * dim;
-                double d = 0.0;
-#pragma unroll 8
-                for (int kx = 0; kx < dim; ++kx) {
-                    const double df = qb[kx * kL2ScanQ + b] - (double)tr[kx];
-                    d = d + df * df;
-                }
-                L2Top2d w = wtop[wv][b];
-                top2d_push(w.d1, w.j1, w.d2, w.j2, d, jc);
-                if (lane == 0) wtop[wv][b] = w;
-            }
-        };
-        auto step = [&](const float (&buf)[kL2ScanPF], int L) {
-            const int rr = L / G, g = L - rr * G;
-            if (g == 0)
-#pragma unroll
-                for (int p = 0; p < kL2ScanQ / 2; ++p) sacc[p] = (f32x2)(0.f);
-            const int k = g * kL2ScanPF;
-#pragma unroll
-            for (int kk = 0; kk < kL2ScanPF; ++kk) {
-                const f32x2 tv = (f32x2)(buf[kk]);
-#pragma unroll
-                for (int p = 0; p < kL2ScanQ / 2; ++p) {
-                    const f32x2 df = qb2[(k + kk) * (kL2ScanQ / 2) + p] - tv;
-                    sacc[p] = __builtin_elementwise_fma(df, df, sacc[p]);
+                const int rl = __builtin_amdgcn_readlane(trow, l);
+                uint32_t pb = (uint32_t)__builtin_amdgcn_readlane((int)pend, l);
+                while (pb) {
+                    const int b = qg * QG + __builtin_ctz(pb);
+                    pb &= pb - 1;
+                    const double d = l2_exact_row_wave(sq + b, tile + rl * RS, dim, lane);
+                    L2Top2d w = wtop[wv][b];
+                    top2d_push(w.d1, w.j1, w.d2, w.j2, d, r0 + rl);
+                    if (lane == 0) wtop[wv][b] = w;
                 }
             }
-            if (g == G - 1) {
-                const int jr = jl + rr * kL2ScanThreads;
-#pragma unroll
-                for (int p = 0; p < kL2ScanQ / 2; ++p) {
-                    exact_rows(2 * p, !((double)sacc[p].x > sthr[2 * p]), jr);
-                    exact_rows(2 * p + 1, !((double)sacc[p].y > sthr[2 * p + 1]), jr);
-                }
-            }
-        };
-        float bufA[kL2ScanPF], bufB[kL2ScanPF];
-        gload(bufA, 0);
-        gload(bufB, 1);
-        for (int L = 0; L < Ltot; L += 2) {   // G is even (dimPad: a multiple of 2 groups)
-            step(bufA, L);
-            gload(bufA, L + 2);
-            step(bufB, L + 1);
-            gload(bufB, L + 3);
         }
         __syncthreads();
         // fold the waves' top-2s (lexicographic: the order of candidates does not matter)
@@ -1033,12 +1085,9 @@ struct L2Work {
     DevBuf<_Float16> qh, ql, th, tl;   // f16-split copies (DP <= 128)
     DevBuf<unsigned> dom;              // max |x| over both sets (float bits): the f16 path's domain
     DevBuf<unsigned> maxPart;          // mcv_l2_umax: per-block maxima (2 x kL2MaxBlocks)
-    DevBuf<unsigned> maxCount;         // ... and its two finish counters (zeroed once, re-armed by each launch)
+    DevBuf<unsigned> maxCount;         // ... and its finish counter (zeroed once, re-armed by each launch)
     DevBuf<unsigned> qmax, tmaxr;      // per-row max |x|
-    DevBuf<double> qd;                 // queued queries in fp64 (+ one batch of slack)
-    DevBuf<float> qf;                  // ... and in fp32 (the exact scan's filter)
     DevBuf<double> ambE2;              // per queued query: the filter bound (refine's exact second best)
-    DevBuf<float> tT;                  // the train set transposed (exact scan)
     hipStream_t last = nullptr; // stream of the last match (the diagnostics read the queue length there)
     bool lastF16 = false;       // the last match launched the f16-split form (its flag decided on device)
     bool ran = false;           // a match ran on this thread (its stream may be the null stream)
@@ -1080,16 +1129,16 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     wk.tn.ensure(ntPad);
     wk.tmax.ensure(1);
     if (!wk.maxCount.p) {
-        wk.maxCount.ensure(2);
-        MCV_HIP(hipMemsetAsync(wk.maxCount.p, 0, 2 * sizeof(unsigned), s));
+        wk.maxCount.ensure(1);
+        MCV_HIP(hipMemsetAsync(wk.maxCount.p, 0, sizeof(unsigned), s));
     }
     wk.maxPart.ensure(2 * kL2MaxBlocks);
     wk.amb.ensure((size_t)nq + 1);
     wk.ambE2.ensure((size_t)nq);
-    MCV_HIP(hipMemsetAsync(wk.amb.p, 0, sizeof(int), s));
-    // f16-split GEMM form for DP <= 128: the split preps record max |x|, and the f32 prep / GEMM
+    // f16-split GEMM form for DP <= 128: the split prep records max |x|, and the f32 prep / GEMM
     // return on the device when it is inside the f16 domain (no host round trip)
     const unsigned* dom = nullptr;
+    const unsigned* tnBits = reinterpret_cast<const unsigned*>(wk.tn.p);
     if (f16) {
         wk.qh.ensure((size_t)nqPad * DP);
         wk.ql.ensure((size_t)nqPad * DP);
@@ -1098,24 +1147,31 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         wk.dom.ensure(1);
         wk.qmax.ensure(nqPad);
         wk.tmaxr.ensure(ntPad);
-        hipLaunchKernelGGL(mcv_l2_prep16, dim3((nqPad + 3) / 4), dim3(256), 0, s, d_q, nq, dim, DP, nqPad, wk.qh.p,
-                           wk.ql.p, wk.qn.p, 0.f, wk.qmax.p);
-        hipLaunchKernelGGL(mcv_l2_prep16, dim3((ntPad + 3) / 4), dim3(256), 0, s, d_t, nt, dim, DP, ntPad, wk.th.p,
-                           wk.tl.p, wk.tn.p, __builtin_inff(), wk.tmaxr.p);
-        hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s, wk.qmax.p, nq, wk.tmaxr.p, nt, wk.maxPart.p,
-                           wk.maxCount.p, wk.dom.p);
+        const L2PrepF16 pq{d_q, nq, nqPad, wk.qh.p, wk.ql.p, wk.qn.p, 0.f, wk.qmax.p};
+        // padding rows get a +inf norm: their scores are +inf and never enter a top-2 or the third place
+        const L2PrepF16 pt{d_t, nt, ntPad, wk.th.p, wk.tl.p, wk.tn.p, __builtin_inff(), wk.tmaxr.p};
+        hipLaunchKernelGGL(mcv_l2_prep16, dim3(l2_prep_blocks(nqPad + ntPad)), dim3(256), 0, s, pq, pt, dim, DP,
+                           wk.amb.p);
+        hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s, wk.qmax.p, nq, wk.tmaxr.p, nt, tnBits, nt,
+                           wk.maxPart.p, wk.maxCount.p, wk.dom.p, wk.tmax.p);
         dom = wk.dom.p;
+    } else {
+        MCV_HIP(hipMemsetAsync(wk.amb.p, 0, sizeof(int), s));
     }
-    hipLaunchKernelGGL(mcv_l2_prep, dim3((nqPad + 3) / 4), dim3(256), 0, s, d_q, nq, dim, DP, nqPad, wk.qp.p, wk.qn.p,
-                       0.f, dom);
-    // padding rows get a +inf norm: their scores are +inf and never enter a top-2 or the third place
-    hipLaunchKernelGGL(mcv_l2_prep, dim3((ntPad + 3) / 4), dim3(256), 0, s, d_t, nt, dim, DP, ntPad, wk.tp.p, wk.tn.p,
-                       __builtin_inff(), dom);
-    hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s, reinterpret_cast<const unsigned*>(wk.tn.p), nt,
-                       nullptr, 0, wk.maxPart.p + kL2MaxBlocks, wk.maxCount.p + 1, wk.tmax.p);
+    {
+        const L2PrepF32 pq{d_q, nq, nqPad, wk.qp.p, wk.qn.p, 0.f};
+        const L2PrepF32 pt{d_t, nt, ntPad, wk.tp.p, wk.tn.p, __builtin_inff()};
+        hipLaunchKernelGGL(mcv_l2_prep, dim3(l2_prep_blocks(nqPad + ntPad)), dim3(256), 0, s, pq, pt, dim, DP, dom);
+    }
+    if (!f16)
+        hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s, tnBits, nt, nullptr, 0, nullptr, 0,
+                           wk.maxPart.p, wk.maxCount.p, wk.tmax.p, nullptr);
     const int qblocks = nqPad / 128;
     int nchunks = (2048 + qblocks - 1) / qblocks;
-    if (f16) nchunks = 8;   // one train chunk per XCD (mcv_l2_mfma16's block order)
+    // f16: one train chunk per XCD (mcv_l2_mfma16's block order). More chunks at small query counts
+    // measured slower at the 8-rank share (6250 queries: 0.42 ms with 8 chunks, 0.48 / 0.50 with 16 /
+    // 64; each added chunk re-reads the block's 256 queries)
+    if (f16) nchunks = 8;
     if (nchunks > ntTiles) nchunks = ntTiles;
     if (nchunks < 1) nchunks = 1;
     const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
@@ -1171,7 +1227,9 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         }
 #undef MCV_L2_LAUNCH
     }
-    hipLaunchKernelGGL(mcv_l2_refine, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nqPad, nchunks, nt, dim,
+    // one wave per block: the latency-bound exact sums of a rank's few thousand queries spread over
+    // every CU (6250 queries: 40 -> 14 us)
+    hipLaunchKernelGGL(mcv_l2_refine, dim3((nq + 63) / 64), dim3(64), 0, s, wk.part.p, nq, nqPad, nchunks, nt, dim,
                        wk.qn.p, wk.tmax.p, d_q, d_t, d_idx, d_dist, d_idx2, d_dist2, wk.amb.p, wk.amb.p + 1,
                        wk.ambE2.p, dom);
     {
@@ -1182,18 +1240,15 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
             return v >= 64 && v <= 8192 ? v : kL2ScanBlocks;
         }();
         wk.scanPart.ensure((size_t)scanBlocks * kL2ScanQ);
-        const int dimPad = (dim + 2 * kL2ScanPF - 1) / (2 * kL2ScanPF) * (2 * kL2ScanPF);
-        wk.qd.ensure((size_t)(nq + kL2ScanQ) * dimPad);
-        wk.qf.ensure((size_t)(nq + kL2ScanQ) * dimPad);
-        hipLaunchKernelGGL(mcv_l2_amb_convert, dim3(256), dim3(256), 0, s, d_q, dim, dimPad, wk.amb.p, wk.amb.p + 1,
-                           wk.qd.p, wk.qf.p);
-        wk.tT.ensure((size_t)(nt > 0 ? nt : 1) * dimPad);
-        if (nt > 0)
-            hipLaunchKernelGGL(mcv_l2_transpose_train, dim3((nt + 63) / 64, (dimPad + 63) / 64), dim3(256), 0, s,
-                               d_t, nt, dim, dimPad, wk.amb.p, wk.tT.p);
-        hipLaunchKernelGGL(mcv_l2_exact_scan, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, wk.qd.p, wk.qf.p, wk.tT.p,
-                           d_t, nt, dim, dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist,
-                           d_idx2, d_dist2);
+        const int dimPad = (dim + 7) / 8 * 8;   // the filter's 8-dimension trips over float4 rows
+        if (dimPad <= 128)
+            hipLaunchKernelGGL(mcv_l2_exact_scan<128>, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, d_q, d_t, nt, dim,
+                               dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2);
+        else
+            hipLaunchKernelGGL(mcv_l2_exact_scan<256>, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, d_q, d_t, nt, dim,
+                               dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2);
+        // the chunks' top-2s folded by a launch of their own: in the scan's last workgroup the fold is one
+        // block's serial chain (+23 us at the 8-rank share, +170 us at 241 queued queries x 32 chunks)
         hipLaunchKernelGGL(mcv_l2_exact_merge, dim3(64), dim3(256), 0, s, wk.amb.p, wk.amb.p + 1, wk.scanPart.p, d_idx,
                            d_dist, d_idx2, d_dist2, scanBlocks);
     }

@@ -2,11 +2,14 @@
 N = 1, 2, 4, 8 on one GPU: what each rank of the driver's scaling run computes (device arrays,
 synchronous steps, median of 10)."""
 import json
+import sys
 import time
+from pathlib import Path
 
 import numpy as np
 import torch
 
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from minicv_amd import device as D, synthetic as S
 
 
