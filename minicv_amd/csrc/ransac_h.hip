@@ -63,6 +63,33 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
     }
 }
 
+// Four lanes per hypothesis (jacobi_eig.h's EigWsQuad): HB hypotheses per block, one 127-double slice
+// each; the quad runs the sample search and the DLT redundantly (same values in all four lanes) and
+// splits the eigen-solve's element work; lane 0 of the quad writes the outputs.
+template <int HB>
+__global__ __launch_bounds__(4 * HB) void mcv_h_generate_q4(const float* __restrict__ pts4, int N, Sampler smp,
+                                                          int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
+                                                          double* __restrict__ h64, int* __restrict__ counts) {
+    const int hl = threadIdx.x >> 2;
+    const int i = blockIdx.x * HB + hl;
+    if (i >= hypCount) return;   // whole quads
+    __shared__ double lds[kEigWs * HB];
+    EigWsQuad ws{lds + hl * kEigWs, (int)(threadIdx.x & 3)};
+    double H[9];
+    HModelF mf;
+    const int st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
+    if (ws.sub != 0) return;
+    if (st == 1) {
+        models[i] = mf;
+        for (int j = 0; j < 9; ++j) h64[9 * (int64_t)i + j] = H[j];
+        counts[i] = 0;
+    } else {
+        for (int j = 0; j < 8; ++j) mf.h[j] = 0.f;
+        models[i] = mf;
+        counts[i] = st;
+    }
+}
+
 // One hypothesis in full (finalize path): fp64 model, fp32 model, status, sample.
 __global__ void mcv_h_one(const float* __restrict__ pts4, int N, Sampler smp, int64_t hyp, HOneOut* __restrict__ out,
                           bool fast) {
@@ -1029,7 +1056,20 @@ void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin
 #define MCV_H_GENERATE(LL, SO)                                                                                    \
     hipLaunchKernelGGL((mcv_h_generate<false, LL, SO>), dim3((hypCount + LL - 1) / LL), dim3(LL), 0, s, d_pts4, N, smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts)
         const int L = eig_lanes();
-        if (eig_soa()) {
+        static const int q4 = [] {   // MCV_EIG_Q4 = hypotheses per block of the four-lane form (screen)
+            const char* e = getenv("MCV_EIG_Q4");
+            return e ? atoi(e) : 0;
+        }();
+        if (q4 == 32)
+            hipLaunchKernelGGL(mcv_h_generate_q4<32>, dim3((hypCount + 31) / 32), dim3(128), 0, s, d_pts4, N, smp,
+                               hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
+        else if (q4 == 40)
+            hipLaunchKernelGGL(mcv_h_generate_q4<40>, dim3((hypCount + 39) / 40), dim3(160), 0, s, d_pts4, N, smp,
+                               hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
+        else if (q4 == 64)
+            hipLaunchKernelGGL(mcv_h_generate_q4<64>, dim3((hypCount + 63) / 64), dim3(256), 0, s, d_pts4, N, smp,
+                               hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
+        else if (eig_soa()) {
             if (L == 48) MCV_H_GENERATE(48, true);
             else if (L == 64) MCV_H_GENERATE(64, true);
             else MCV_H_GENERATE(40, true);
