@@ -21,7 +21,7 @@ OUT = ROOT / "gpurun_out"
 PROF = ROOT / "profiles"
 WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2", "scaled"]
 # dominant kernel per BASELINE workload (substring of the demangled rocprofv3 kernel name)
-KERNELS = {"homography": "mcv_h_verify_cert", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_partial",
+KERNELS = {"homography": "mcv_h_verify_cert", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_mfma",
            "l2": "mcv_l2_mfma16", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify",
            "scaled": "mcv_scaled_costs"}
 EXTRA_BENCH = ["homography_fused", "homography_fast", "pnp_ap3p", "essential_fast"]   # second bench lines (bench_<name>.log)
@@ -86,7 +86,8 @@ def main():
             config = f"{c.get('queries')}x{c.get('train')}"
             dim_bytes = 32.0 if w == "hamming" else 512.0
             alg = dim_bytes * c.get("queries", 0) * c.get("train", 0)
-        t = {"workload": w, "config": config, "algorithmic_bytes_per_launch": alg}
+        t = {"workload": w, "config": config, "algorithmic_bytes_per_launch": alg,
+             "source": f"rocprofv3 --kernel-trace --pmc (one counter per pass), bench.py, round {rnd}"}
         fetch = OUT / f"pmc_fetch_{w}" / "run_counter_collection.csv"
         write = OUT / f"pmc_write_{w}" / "run_counter_collection.csv"
         if fetch.exists() and write.exists():
@@ -98,6 +99,18 @@ def main():
                 t.update({"FETCH_SIZE_KB": mean(f), "WRITE_SIZE_KB": mean(wr), "dispatches": len(f),
                           "hbm_bytes_per_launch": (2 * mean(f) + mean(wr)) * 1024.0})
                 print("traffic", kernel, t["hbm_bytes_per_launch"])
+        # MFMA SQ pass (matchers): MFMA instructions, MFMA busy share of the SIMD cycles
+        mf_src = OUT / f"pmc_mfma_{w}" / "run_counter_collection.csv"
+        if mf_src.exists():
+            shutil.copy(mf_src, PROF / rnd / f"pmc_mfma_{w}.csv")
+            sq = {k: mean(v) for k, v in sorted(pmc_sums(mf_src, kernel).items())}
+            d = {"sq": sq}
+            if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+                cyc = sq["GRBM_GUI_ACTIVE"] / 8
+                # SQ_VALU_MFMA_BUSY_CYCLES counts cycles (MI355X_MICROARCH.md), summed over the 1024 SIMDs
+                d["derived"] = {"kernel_cycles": cyc, "mfma_busy": sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc)}
+                print("mfma", kernel, d["derived"])
+            t["counters"] = d
         # SQ pass (SQ_INSTS_VALU & co.): measured VALU instructions per evaluation and VALU busy share
         sq_src = OUT / f"pmc_sq_{w}" / "run_counter_collection.csv"
         if not sq_src.exists() and w == "homography":
@@ -121,11 +134,20 @@ def main():
     lds = OUT / "pmc_lds_homography" / "run_counter_collection.csv"
     if lds.exists():
         shutil.copy(lds, PROF / rnd / "pmc_lds_homography.csv")
+    # extra screens: raw SQ counters of named kernels (e.g. the H generate, lane vs quad form)
+    for src in sorted(OUT.glob("pmc_gen_*")):
+        f = src / "run_counter_collection.csv"
+        if f.exists():
+            shutil.copy(f, PROF / rnd / f"{src.name}.csv")
     if traffic:
+        # merge: entries not re-measured this round stay as they were (their config says what they measured)
+        old = PROF / "pmc_traffic.json"
+        merged = json.loads(old.read_text()) if old.exists() else {}
+        merged.update(traffic)
+        traffic = merged
         for v in traffic.values():
-            v["correction"] = ("FETCH_SIZE x2 (gfx950 counts half of a wide streaming read, MI355X_MICROARCH.md "
-                               "HBM) + WRITE_SIZE; units KB")
-            v["source"] = f"rocprofv3 --kernel-trace --pmc (one counter per pass), bench.py, round {rnd}"
+            v.setdefault("correction", "FETCH_SIZE x2 (gfx950 counts half of a wide streaming read, MI355X_MICROARCH.md "
+                                       "HBM) + WRITE_SIZE; units KB")
         (PROF / "pmc_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
 
 
