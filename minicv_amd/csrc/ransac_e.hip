@@ -486,16 +486,15 @@ static void launch_e_verify_pk_kp(const float4* p32, const double4* p, int N, co
                                   const int* d_nDense, int maxModels, int* d_counts, float thr2, int kind,
                                   const SampsonPkCut& cut, const double* d_bb, hipStream_t s) {
     const int blocks = ((maxModels + 2 * KP - 1) / (2 * KP) + 3) / 4;
-    // point chunks of at least MCV_E_CHUNK (default 50000) correspondences when the models alone leave
-    // the chip short of workgroups (screen at N = 100k, 2^16 hypotheses: one chunk 12.16 ms, 16384-point
-    // chunks 12.25, 32768 12.04, 50000 11.92); one chunk once they fill it (2^20 hypotheses: 186.7 vs
-    // 187.9 ms, and each model's count written once: 62 vs 284 MB of writes per launch)
-    static const int envChunk = [] {
+    // point chunks of at least MCV_E_CHUNK (default 50000) correspondences (screen at N = 100k: one chunk
+    // 12.16 ms, 16384-point chunks 12.25, 32768 12.04, 50000 11.92). At 2^20 hypotheses one chunk writes
+    // 62 instead of 284 MB of partial counts per launch but streams the whole 4.8 MB point set through
+    // each XCD's 4 MB L2 (24.8 GB of fetches per launch against 0.7 GB; the same 223 ms a step): kept at two.
+    static const int minChunk = [] {
         const char* e = getenv("MCV_E_CHUNK");
-        const int v = e ? atoi(e) : 0;
-        return v > 0 ? v : 0;
+        const int v = e ? atoi(e) : 50000;
+        return v > 0 ? v : (1 << 30);
     }();
-    const int minChunk = envChunk ? envChunk : blocks >= 2048 ? (1 << 30) : 50000;
     const int step = 64 * P;
     int chunks = std::max(1, N / minChunk);
     int chunk = (N + chunks - 1) / chunks;
