@@ -284,7 +284,10 @@ def bench_matcher(args):
             tf = flops / (avg_ms * 1e-3) / 1e12
             if form == 16:   # f16-split GEMM form: three f16 MFMA products per (query, train, dim)
                 roof = {"bound": "mfma-f16", "achieved": 3.0 * tf, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                        "frac": 3.0 * tf / F16_MFMA_PEAK_TF, "kernel": "mcv_l2_mfma16",
+                        "frac": 3.0 * tf / F16_MFMA_PEAK_TF,
+                        # MCV_L2_FORM (screen) 1 / 2 select the round-3 kernel / the one-wave two-set form
+                        "kernel": {"1": "mcv_l2_mfma16", "2": "mcv_l2_mfma16x"}.get(os.environ.get("MCV_L2_FORM", "0"),
+                                                                                  "mcv_l2_mfma16q"),
                         "model": "fp32 operands split into f16 hi + lo; hi.hi + hi.lo + lo.hi on "
                                  "v_mfma_f32_32x32x16_f16 = 3 x 2 Nq Nt D MFMA flops per launch; "
                                  f"algorithmic rate {tf:.1f} TFLOP/s (2 Nq Nt D)"}

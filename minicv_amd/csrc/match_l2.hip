@@ -578,6 +578,111 @@ __global__ __launch_bounds__(64 * WPB) void mcv_l2_mfma16(const _Float16* __rest
     }
 }
 
+// The default f16-split GEMM form (round 4): mcv_l2_mfma16's tiles, MFMA chains and epilogue with one
+// accumulator set per query set (QT sets of 32 queries per wave) instead of two sets in turn, and
+// the next tile staged one tile ahead through one register set: 150 VGPRs for QT = 1, so three waves
+// per SIMD (WAVES, amdgpu_waves_per_eu) overlap one wave's epilogue with the others' MFMAs instead of
+// one wave interleaving them. WPB = 4, QT = 1: blocks of 128 queries, 3 blocks per CU. QT = 2 (two
+// query sets per wave: each A fragment read from LDS feeds 6 MFMAs) fits two waves per SIMD (252
+// VGPRs) and measured slower (2.17 vs 1.98 ms at cfg5): the LDS reads were not the limiter.
+template <int DP, int WPB, int QT, int WAVES>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void mcv_l2_mfma16q(
+    const _Float16* __restrict__ qh, const _Float16* __restrict__ ql, const _Float16* __restrict__ th,
+    const _Float16* __restrict__ tl, const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk, int nqPad,
+    L2Part* __restrict__ part, const unsigned* __restrict__ dom, bool xcdMap) {
+    constexpr int TR = 32;
+    if (!l2_f16_domain(dom)) return;   // grid-uniform: the f32 kernel takes this launch
+    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
+    constexpr int KB = DP / 16;
+    constexpr int ROWH = DP + 8;
+    constexpr int NT = 64 * WPB;
+    constexpr int PER = (TR * DP / 8 + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) _Float16 lh[2][TR * ROWH];
+    __shared__ __attribute__((aligned(16))) _Float16 ll[2][TR * ROWH];
+    __shared__ __attribute__((aligned(16))) float lnorm[2][TR];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int q0 = (bx * WPB + wave) * 32 * QT;
+    f16x8 bh[QT][KB], bl[QT][KB];
+#pragma unroll
+    for (int q = 0; q < QT; ++q) {
+        const f16x8* rh = reinterpret_cast<const f16x8*>(qh + (size_t)(q0 + 32 * q + col) * DP + 8 * h);
+        const f16x8* rl = reinterpret_cast<const f16x8*>(ql + (size_t)(q0 + 32 * q + col) * DP + 8 * h);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            bh[q][kb] = rh[2 * kb];
+            bl[q][kb] = rl[2 * kb];
+        }
+    }
+    const int tBegin = by * tilesPerChunk;
+    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
+    float b1[QT], b2[QT], b3[QT];
+    int i1[QT], i2[QT];
+#pragma unroll
+    for (int q = 0; q < QT; ++q) b1[q] = b2[q] = b3[q] = INFINITY, i1[q] = i2[q] = -1;
+    f16x8 sh[PER], sl[PER];
+    float ns = 0.f;
+    if (tBegin < tEnd) {
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, tBegin, sh, sl, ns);
+        l2_lstore16<DP, TR, NT>(lh[0], ll[0], lnorm[0], sh, sl, ns);
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(tBegin + 1, tEnd - 1), sh, sl, ns);
+    }
+    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // the query fragments' loads, once (vmcnt(0))
+    for (int t = tBegin; t < tEnd; ++t) {
+        const int buf = (t - tBegin) & 1;
+        floatx16 m[QT], sm[QT];
+#pragma unroll
+        for (int q = 0; q < QT; ++q)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) m[q][r] = sm[q][r] = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(&lh[buf][col * ROWH + 16 * kb + 8 * h]);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(&ll[buf][col * ROWH + 16 * kb + 8 * h]);
+#pragma unroll
+            for (int q = 0; q < QT; ++q) m[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[q][kb], m[q], 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < QT; ++q) sm[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[q][kb], sm[q], 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < QT; ++q) sm[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[q][kb], sm[q], 0, 0, 0);
+        }
+        // the next tile (staged a tile ago) into the idle LDS buffer, the one after into the staging set
+        l2_lstore16<DP, TR, NT>(lh[buf ^ 1], ll[buf ^ 1], lnorm[buf ^ 1], sh, sl, ns);
+        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), sh, sl, ns);
+        float4 nv[1][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nv[0][j] = *reinterpret_cast<const float4*>(&lnorm[buf][8 * j + 4 * h]);
+#pragma unroll
+        for (int q = 0; q < QT; ++q) {
+            const floatx16 am[1] = {m[q]}, as[1] = {sm[q]};
+            l2_epilogue16<1>(am, as, nv, t * TR, b1[q], i1[q], b2[q], i2[q], b3[q]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < QT; ++q) {
+        if (i1[q] >= 0) i1[q] += 4 * h;
+        if (i2[q] >= 0) i2[q] += 4 * h;
+        const float ob1 = __shfl_xor(b1[q], 32, 64), ob2 = __shfl_xor(b2[q], 32, 64), ob3 = __shfl_xor(b3[q], 32, 64);
+        const int oi1 = __shfl_xor(i1[q], 32, 64), oi2 = __shfl_xor(i2[q], 32, 64);
+        if (h == 0) {
+            float c1 = b1[q], c2 = b2[q], c3 = b3[q];
+            third_fold(c1, c2, c3, ob1);
+            third_fold(c1, c2, c3, ob2);
+            third_fold(c1, c2, c3, ob3);
+            float x1 = b1[q], x2 = b2[q];
+            int j1 = i1[q], j2 = i2[q];
+            top2_push(x1, j1, x2, j2, ob1, oi1);
+            top2_push(x1, j1, x2, j2, ob2, oi2);
+            L2Part p;
+            p.b1 = x1; p.b2 = x2; p.b3 = c3; p.i1 = j1; p.i2 = j2; p.i3 = -1;
+            part[(size_t)by * nqPad + q0 + 32 * q + col] = p;
+        }
+    }
+}
+
 // Register-blocked variant (round 4): each wave holds QT sets of 32 queries (VGPR-resident hi / lo B
 // fragments), so every A fragment read from LDS feeds 3 QT MFMAs instead of 3, and a block of WPB
 // waves serves 32 QT WPB queries from one staged train tile. Otherwise as mcv_l2_mfma16: two
@@ -1168,10 +1273,36 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
                            wk.maxPart.p, wk.maxCount.p, wk.tmax.p, nullptr);
     const int qblocks = nqPad / 128;
     int nchunks = (2048 + qblocks - 1) / qblocks;
-    // f16: one train chunk per XCD (mcv_l2_mfma16's block order). More chunks at small query counts
-    // measured slower at the 8-rank share (6250 queries: 0.42 ms with 8 chunks, 0.48 / 0.50 with 16 /
-    // 64; each added chunk re-reads the block's 256 queries)
+    // f16 forms. The round-3 kernels: one train chunk per XCD (their block order). The default
+    // mcv_l2_mfma16q<D, 4, 1, 3> runs 3 blocks per CU, so a grid runs in "rounds" of 3 x CUs blocks and
+    // a round that is barely begun costs most of a block's time: the chunk count C minimises
+    // ceil(qblocks C / (3 CUs)) (1 / C + 0.01) (the 0.01: a block's fixed cost against a whole-train
+    // sweep) over C = 4 .. 24. Screened at cfg5's rank shares (scripts/gpu_r04_q.sh, 50k / N queries):
+    // C = 15 took N = 1 / 2 / 4 / 8 to 1.98 / 1.12 / 0.58 / 0.35 ms against 2.14 / 1.21 / 0.74 / 0.40
+    // with 8 and 2.01 / 1.16 / 0.65 / 0.44 with 16 (N = 8: 800 blocks, one past a round).
+    static const int form0 = [] {
+        const char* e = getenv("MCV_L2_FORM");
+        return e ? atoi(e) : 0;
+    }();
     if (f16) nchunks = 8;
+    if (f16 && form0 == 0) {
+        static const int cus = [] {
+            int d = 0, n = 0;
+            (void)hipGetDevice(&d);
+            return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
+        }();
+        const int qb = nqPad / 128, slots = 3 * cus;
+        double best = 1e30;
+        for (int c = 4; c <= 24; ++c) {
+            const double cost = (double)((qb * c + slots - 1) / slots) * (1.0 / c + 0.01);
+            if (cost < best - 1e-12) best = cost, nchunks = c;
+        }
+    }
+    static const int chunksEnv = [] {   // screen: MCV_L2_CHUNKS = the f16 form's train chunk count
+        const char* e = getenv("MCV_L2_CHUNKS");
+        return e ? atoi(e) : 0;
+    }();
+    if (f16 && chunksEnv > 0) nchunks = chunksEnv;
     if (nchunks > ntTiles) nchunks = ntTiles;
     if (nchunks < 1) nchunks = 1;
     const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
@@ -1187,21 +1318,43 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         ProfScope ps("l2_mfma", s);
 #define MCV_L2_LAUNCH(D, T) hipLaunchKernelGGL((mcv_l2_mfma<D, T>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, \
                                                ntTiles, tilesPerChunk, nqPad, wk.part.p, dom)
-        static const int wpb = [] {   // waves (32 queries each) per f16 block: 8, or 4 (screen)
+        static const int wpb = [] {   // MCV_L2_FORM = 1: waves (32 queries each) per block, 8 or 4 (screen)
             const char* e = getenv("MCV_L2_WPB");
             return e && atoi(e) == 4 ? 4 : 8;
         }();
 #define MCV_L2_LAUNCH16(D, W) hipLaunchKernelGGL((mcv_l2_mfma16<D, 32, W>), dim3(nqPad / (32 * W), nchunks), \
                                                  dim3(64 * W), 0, s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, \
                                                  tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
-        static const int qtSel = [] {   // query sets per wave of the f16 form: 1 (mcv_l2_mfma16) or 2 (screen)
-            const char* e = getenv("MCV_L2_QT");
-            return e && atoi(e) == 2 ? 2 : 1;
+        // f16 form (MCV_L2_FORM, screen): 0 (default) mcv_l2_mfma16q<D, 4, 1, 3>: 4 waves x 32 queries per
+        // block, one accumulator set, three waves per SIMD (1.98 vs 2.07 ms at cfg5); 1 the round-3
+        // mcv_l2_mfma16 (two accumulator sets in turn, MCV_L2_WPB); 2 mcv_l2_mfma16x (two query sets,
+        // one wave per SIMD: 2.98 ms); 3 mcv_l2_mfma16q<D, 4, 2, 2> (two query sets at two waves per
+        // SIMD: 2.17 ms). 8-wave blocks at three waves per SIMD measured 2.36 ms, four waves per SIMD
+        // (23 spilled VGPRs) 2.55 ms.
+        static const int form = [] {
+            const char* e = getenv("MCV_L2_FORM");
+            const int v = e ? atoi(e) : 0;
+            return v >= 0 && v <= 3 ? v : 0;
         }();
 #define MCV_L2_LAUNCH16X(D) hipLaunchKernelGGL((mcv_l2_mfma16x<D, 4, 2>), dim3(nqPad / 256, nchunks), dim3(256), 0, s, \
                                                wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, \
                                                wk.part.p, dom, xcdMap)
-        if (f16 && qtSel == 2) {
+#define MCV_L2_LAUNCH16Q(D, W, Q, V)                                                                               \
+    hipLaunchKernelGGL((mcv_l2_mfma16q<D, W, Q, V>), dim3(nqPad / (32 * W * Q), nchunks), dim3(64 * W), 0, s, wk.qh.p, \
+                       wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
+        if (f16 && form == 0) {
+            switch (DP) {
+                case 32: MCV_L2_LAUNCH16Q(32, 4, 1, 3); break;
+                case 64: MCV_L2_LAUNCH16Q(64, 4, 1, 3); break;
+                default: MCV_L2_LAUNCH16Q(128, 4, 1, 3); break;
+            }
+        } else if (f16 && form == 3) {
+            switch (DP) {
+                case 32: MCV_L2_LAUNCH16Q(32, 4, 2, 2); break;
+                case 64: MCV_L2_LAUNCH16Q(64, 4, 2, 2); break;
+                default: MCV_L2_LAUNCH16Q(128, 4, 2, 2); break;
+            }
+        } else if (f16 && form == 2) {
             switch (DP) {
                 case 32: MCV_L2_LAUNCH16X(32); break;
                 case 64: MCV_L2_LAUNCH16X(64); break;
@@ -1219,6 +1372,7 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         }
 #undef MCV_L2_LAUNCH16
 #undef MCV_L2_LAUNCH16X
+#undef MCV_L2_LAUNCH16Q
         switch (DP) {
             case 32: if (TR == 64) MCV_L2_LAUNCH(32, 64); else MCV_L2_LAUNCH(32, 32); break;
             case 64: if (TR == 64) MCV_L2_LAUNCH(64, 64); else MCV_L2_LAUNCH(64, 32); break;
