@@ -860,6 +860,26 @@ __device__ __forceinline__ bool lex_less_d(double a, int ia, double b, int ib) {
     return (a < b) | ((a == b) & ((unsigned)ia < (unsigned)ib));
 }
 
+// The GEMM form's error bound on a (query, train) score: every train t's exact d^2 >= qn + score(t)
+// - tol (qn = the query's fp32 norm, T2 = the largest fp32 train norm).
+__device__ __forceinline__ double l2_gemm_tol(double qn, double T2, int dim, bool f16) {
+    const double u = 0x1p-24;
+    const double qa = sqrt(qn * (1.0 + 1e-6)), T = sqrt(T2);
+    if (f16) {
+        // f16 split, x = hi + lo + r with |lo| <= 2^-11 |x| + 2^-14, |r| <= 2^-22 |x| + 2^-13 (RN;
+        // f16 subnormals flushed or not): q_i t_i - (qh th + qh tl + ql th) <= 3.01 2^-22 |q_i t_i|
+        // + 1.0012 2^-13 (|q_i| + |t_i|) + 2^-25 per dim, so with Cauchy-Schwarz the dot's error is
+        // E <= |q| T (2.2 dim u (1 + 2^-9) + 2^-20 + 3.02 u) (the f32-accumulated hi.hi chain and the
+        // 2 dim-term hi.lo / lo.hi chain, whose terms are below 2^-10 of hi.hi's, at <= 2 u per step;
+        // the split; the final add and the score's fma) + 1.25e-4 sqrt(dim) (|q| + T)
+        // + dim 2^-25
+        const double E = qa * T * (2.2 * dim * u * (1.0 + 0x1p-9) + 0x1p-20 + 3.02 * u) +
+                         1.25e-4 * sqrt((double)dim) * (qa + T) + dim * 0x1p-25;
+        return 1.01 * ((dim + 4) * u * (T2 + qn) + 2.0 * E) + 1e-30;
+    }
+    return 1.01 * (dim + 4) * u * (T2 + 2.0 * qa * T + qn) + 1e-30;
+}
+
 // Merge the per-chunk top-3s, then make the answer exact: the exact distances of the three GEMM-form
 // candidates give the exact top-2 among them; every other train t has GEMM score >= the third's, so
 // its exact d^2 >= approx3 - tol (tol bounds the GEMM form's rounding, below); when approx3 - tol
@@ -909,23 +929,7 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
     bool certain = nt == 0 || (nt <= 2 && i1 >= 0 && (nt < 2 || i2 >= 0));
     if (!certain && nt > 2 && i2 >= 0) {
         const double qn = (double)qnorm[q], T2 = (double)__uint_as_float(*tmaxBits);
-        const double u = 0x1p-24;
-        const double qa = sqrt(qn * (1.0 + 1e-6)), T = sqrt(T2);
-        double tol;
-        if (l2_f16_domain(dom)) {
-            // f16 split, x = hi + lo + r with |lo| <= 2^-11 |x| + 2^-14, |r| <= 2^-22 |x| + 2^-13 (RN;
-            // f16 subnormals flushed or not): q_i t_i - (qh th + qh tl + ql th) <= 3.01 2^-22 |q_i t_i|
-            // + 1.0012 2^-13 (|q_i| + |t_i|) + 2^-25 per dim, so with Cauchy-Schwarz the dot's error is
-            // E <= |q| T (2.2 dim u (1 + 2^-9) + 2^-20 + 3.02 u) (the f32-accumulated hi.hi chain and the
-            // 2 dim-term hi.lo / lo.hi chain, whose terms are below 2^-10 of hi.hi's, at <= 2 u per step;
-            // the split; the final add and the score's fma) + 1.25e-4 sqrt(dim) (|q| + T)
-            // + dim 2^-25
-            const double E = qa * T * (2.2 * dim * u * (1.0 + 0x1p-9) + 0x1p-20 + 3.02 * u) +
-                             1.25e-4 * sqrt((double)dim) * (qa + T) + dim * 0x1p-25;
-            tol = 1.01 * ((dim + 4) * u * (T2 + qn) + 2.0 * E) + 1e-30;
-        } else {
-            tol = 1.01 * (dim + 4) * u * (T2 + 2.0 * qa * T + qn) + 1e-30;
-        }
+        const double tol = l2_gemm_tol(qn, T2, dim, l2_f16_domain(dom));
         const double approx3 = (double)qnorm[q] + (double)c3;
         certain = approx3 - tol > e2 * (1.0 + 1e-12);   // every other train is strictly farther
     }
@@ -987,12 +991,13 @@ __device__ __forceinline__ void l2_write_final(int q, const L2Top2d& r, int* idx
 // the k-th squared difference (each product rounded on its own, as in the sequential loop), then the
 // products are added in dimension order off the lanes (v_readlane into an SGPR operand): the oracle's
 // sum bit for bit. qcol = the query's fp32 column in LDS (stride kL2ScanQ), row = the tile row.
+template <int QS = kL2ScanQ>
 __device__ __forceinline__ double l2_exact_row_wave(const float* qcol, const float* row, int dim, int lane) {
     double p[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int k = c * 64 + lane;
-        const double df = k < dim ? (double)qcol[k * kL2ScanQ] - (double)row[k] : 0.0;
+        const double df = k < dim ? (double)qcol[k * QS] - (double)row[k] : 0.0;
         p[c] = df * df;
     }
     double d = 0.0;
@@ -1019,7 +1024,8 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
     const float* __restrict__ qraw, const float* __restrict__ traw, int nt, int dim, int dimPad,
     const int* __restrict__ ambCount, const int* __restrict__ ambList, const double* __restrict__ ambE2,
     L2Top2d* __restrict__ part, int* __restrict__ idx, float* __restrict__ dist, int* __restrict__ idx2,
-    float* __restrict__ dist2) {
+    float* __restrict__ dist2, const unsigned* __restrict__ dom16) {
+    if (l2_f16_domain(dom16)) return;   // grid-uniform: mcv_l2_scan16 took this call
     constexpr int NT = kL2ScanThreads, NW = NT / 64;
     constexpr int RS = DPMAX + 4;                    // tile row stride (floats; 16-B aligned rows)
     constexpr int RT = kL2TileFloats / (128 + 4) * 128 / DPMAX;   // 128 or 64 rows
@@ -1135,6 +1141,125 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
         }
         __syncthreads();
         // fold the waves' top-2s (lexicographic: the order of candidates does not matter)
+        if (threadIdx.x < nb) {
+            const int b = threadIdx.x;
+            L2Top2d r{INFINITY, INFINITY, -1, -1};
+            for (int w = 0; w < NW; ++w) {
+                const L2Top2d x = wtop[w][b];
+                top2d_push(r.d1, r.j1, r.d2, r.j2, x.d1, x.j1);
+                top2d_push(r.d1, r.j1, r.d2, r.j2, x.d2, x.j2);
+            }
+            if (T == 1) l2_write_final(ambList[a0 + b], r, idx, dist, idx2, dist2);
+            else part[(size_t)(a0 + b) * T + chunk] = r;
+        }
+        __syncthreads();
+    }
+}
+
+// Exact scan of the queued queries, f16 domain (round 4): the filter is the GEMM form itself. A
+// (batch of 32 queued queries, train chunk) item runs the f16-split MFMA chains of mcv_l2_mfma16q
+// over the chunk's 32-row tiles (A fragments straight from the split train copy, B = the batch's
+// queries gathered through the queue), 4 waves taking tiles in turn; a (query, row) whose GEMM score
+// is at most thr = e2 (1 + 1e-12) + tol - qn (refine's bound: every row's exact d^2 >= qn + score -
+// tol, so a row above it cannot enter the top-2) gets the exact fp64 sum (the whole wave, lane-
+// parallel, the oracle's order). About as many rows survive as with the fp32 filter (the ambiguous
+// queries' near-ties), for 3 MFMAs per 16 dims instead of 2 packed VALU ops per dimension.
+template <int DP>
+__global__ __launch_bounds__(256) void mcv_l2_scan16(
+    const _Float16* __restrict__ qh, const _Float16* __restrict__ ql, const _Float16* __restrict__ th,
+    const _Float16* __restrict__ tl, const float* __restrict__ tnorm, const float* __restrict__ qnorm,
+    const unsigned* __restrict__ tmaxBits, const float* __restrict__ qraw, const float* __restrict__ traw, int nt,
+    int ntTiles, int dim, const int* __restrict__ ambCount, const int* __restrict__ ambList,
+    const double* __restrict__ ambE2, L2Top2d* __restrict__ part, int* __restrict__ idx, float* __restrict__ dist,
+    int* __restrict__ idx2, float* __restrict__ dist2, const unsigned* __restrict__ dom) {
+    if (!l2_f16_domain(dom)) return;   // grid-uniform: mcv_l2_exact_scan takes this call
+    constexpr int KB = DP / 16, NW = 4;
+    __shared__ L2Top2d wtop[NW][kL2ScanQ];
+    __shared__ float sthr[kL2ScanQ];
+    const int n = *ambCount;
+    const int nbatch = (n + kL2ScanQ - 1) / kL2ScanQ;
+    if (nbatch == 0) return;
+    const int T = l2_scan_chunks(nbatch, gridDim.x);
+    const double T2 = (double)__uint_as_float(*tmaxBits);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    for (int item = blockIdx.x; item < nbatch * T; item += gridDim.x) {
+        const int batch = item / T, chunk = item % T;
+        const int a0 = batch * kL2ScanQ;
+        const int nb = min(kL2ScanQ, n - a0);
+        const int tb = (int)((int64_t)chunk * ntTiles / T), te = (int)((int64_t)(chunk + 1) * ntTiles / T);
+        if (threadIdx.x < kL2ScanQ) {
+            const int b = threadIdx.x;
+            float thr = -INFINITY;   // padding members keep nothing
+            if (b < nb) {
+                const int q = ambList[a0 + b];
+                const double qn = (double)qnorm[q];
+                const double x = ambE2[a0 + b] * (1.0 + 1e-12) + l2_gemm_tol(qn, T2, dim, true) - qn;
+                // rounded up (and a little more) to fp32: the fp32 compare keeps a superset
+                thr = x < 0x1p120 ? __double2float_ru(x + fabs(x) * 0x1p-40) : INFINITY;
+            }
+            sthr[b] = thr;
+        }
+        if (lane < kL2ScanQ) wtop[wv][lane] = L2Top2d{INFINITY, INFINITY, -1, -1};
+        __syncthreads();
+        const int qc = col < nb ? ambList[a0 + col] : -1;
+        const float myThr = sthr[col];
+        f16x8 bh[KB], bl[KB];
+        {
+            const f16x8 z = (f16x8)((_Float16)0);
+            const f16x8* rh = reinterpret_cast<const f16x8*>(qh + (size_t)(qc < 0 ? 0 : qc) * DP + 8 * h);
+            const f16x8* rl = reinterpret_cast<const f16x8*>(ql + (size_t)(qc < 0 ? 0 : qc) * DP + 8 * h);
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                bh[kb] = qc < 0 ? z : rh[2 * kb];
+                bl[kb] = qc < 0 ? z : rl[2 * kb];
+            }
+        }
+        for (int t = tb + wv; t < te; t += NW) {
+            floatx16 m, sm;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) m[r] = sm[r] = 0.f;
+            const f16x8* ah8 = reinterpret_cast<const f16x8*>(th + ((size_t)t * 32 + col) * DP + 8 * h);
+            const f16x8* al8 = reinterpret_cast<const f16x8*>(tl + ((size_t)t * 32 + col) * DP + 8 * h);
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                const f16x8 ah = ah8[2 * kb], al = al8[2 * kb];
+                m = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[kb], m, 0, 0, 0);
+                sm = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[kb], sm, 0, 0, 0);
+                sm = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[kb], sm, 0, 0, 0);
+            }
+            // lane (query col, half h) holds rows (r & 3) + 8 (r >> 2) + 4 h of the tile
+            uint32_t keep = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 n4 = *reinterpret_cast<const float4*>(tnorm + (size_t)t * 32 + 8 * j + 4 * h);
+                const float nn[4] = {n4.x, n4.y, n4.z, n4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 4 * j + i;
+                    const float sc = fmaf(-2.f, m[r] + sm[r], nn[i]);
+                    keep |= (uint32_t)(sc <= myThr) << r;
+                }
+            }
+            uint64_t mk = __ballot(keep != 0);
+            while (mk) {
+                const int l = __ffsll((unsigned long long)mk) - 1;
+                mk &= mk - 1;
+                uint32_t pb = (uint32_t)__builtin_amdgcn_readlane((int)keep, l);
+                const int q = __builtin_amdgcn_readlane(qc, l);
+                const int bq = l & 31, hh = l >> 5;
+                while (pb) {
+                    const int r = __builtin_ctz(pb);
+                    pb &= pb - 1;
+                    const int row = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                    if (row >= nt) continue;   // padding rows (never below a finite threshold anyway)
+                    const double d = l2_exact_row_wave<1>(qraw + (size_t)q * dim, traw + (size_t)row * dim, dim, lane);
+                    L2Top2d w = wtop[wv][bq];
+                    top2d_push(w.d1, w.j1, w.d2, w.j2, d, row);
+                    if (lane == 0) wtop[wv][bq] = w;
+                }
+            }
+        }
+        __syncthreads();
         if (threadIdx.x < nb) {
             const int b = threadIdx.x;
             L2Top2d r{INFINITY, INFINITY, -1, -1};
@@ -1394,13 +1519,34 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
             return v >= 64 && v <= 8192 ? v : kL2ScanBlocks;
         }();
         wk.scanPart.ensure((size_t)scanBlocks * kL2ScanQ);
+        static const bool scan16ok = [] {   // MCV_L2_SCAN16 = 0: the fp32-filter scan only (screen)
+            const char* e = getenv("MCV_L2_SCAN16");
+            return !(e && atoi(e) == 0);
+        }();
+        // f16 domain: the MFMA-filtered scan (the VALU scan returns on the device flag); otherwise the
+        // fp32-filter scan
+        const unsigned* dom16 = f16 && scan16ok ? dom : nullptr;
+        if (dom16) {
+#define MCV_L2_SCAN16(D)                                                                                        \
+    hipLaunchKernelGGL(mcv_l2_scan16<D>, dim3(scanBlocks), dim3(256), 0, s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, \
+                       wk.qn.p, wk.tmax.p, d_q, d_t, nt, ntTiles, dim, wk.amb.p, wk.amb.p + 1, wk.ambE2.p,            \
+                       wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2, dom16)
+            switch (DP) {
+                case 32: MCV_L2_SCAN16(32); break;
+                case 64: MCV_L2_SCAN16(64); break;
+                default: MCV_L2_SCAN16(128); break;
+            }
+#undef MCV_L2_SCAN16
+        }
         const int dimPad = (dim + 7) / 8 * 8;   // the filter's 8-dimension trips over float4 rows
         if (dimPad <= 128)
             hipLaunchKernelGGL(mcv_l2_exact_scan<128>, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, d_q, d_t, nt, dim,
-                               dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2);
+                               dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2,
+                               dom16);
         else
             hipLaunchKernelGGL(mcv_l2_exact_scan<256>, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, d_q, d_t, nt, dim,
-                               dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2);
+                               dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2,
+                               dom16);
         // the chunks' top-2s folded by a launch of their own: in the scan's last workgroup the fold is one
         // block's serial chain (+23 us at the 8-rank share, +170 us at 241 queued queries x 32 chunks)
         hipLaunchKernelGGL(mcv_l2_exact_merge, dim3(64), dim3(256), 0, s, wk.amb.p, wk.amb.p + 1, wk.scanPart.p, d_idx,
