@@ -160,7 +160,11 @@ __global__ __launch_bounds__(64) void mcv_e5_lu(E5StageView st) {
     }
 }
 
-__global__ __launch_bounds__(64) void mcv_e5_roots(E5StageView st, EModel* __restrict__ dense,
+// Two waves per SIMD (amdgpu_waves_per_eu: 324 -> 256 VGPRs, ~50 spilled): the 300-sweep Durand-Kerner
+// chain is latency-bound at one wave, 29.5 -> 25.8 ms per 2^20 hypotheses. Splitting solvePoly into a
+// kernel of its own (roots through the stage) measured 24.0 + 2.3 ms: solvePoly itself holds the
+// registers; three / four waves per SIMD spill 58 / 121 VGPRs and lose.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void mcv_e5_roots(E5StageView st, EModel* __restrict__ dense,
                                                    int* __restrict__ denseSlot, int* __restrict__ nDense,
                                                    int* __restrict__ counts) {
     const int lane = threadIdx.x;
