@@ -190,6 +190,10 @@ __device__ __forceinline__ uint32_t pnp_exact_trip(const PnpPoint* __restrict__ 
 // is recorded (LDS event list: trip << 8 | pose mask) and recounted exactly after the sweep. An
 // event-list overflow recounts the wave's chunk exactly. Partial counts by integer atomics.
 static constexpr int kPnpEvents = 192;   // per wave
+// LANE form (round 4, the default): the log holds undecided (point, pose) lanes instead of (trip, pose
+// mask) events, and the recount takes 64 of them per pass, one per lane: a trip with one undecided
+// lane costs one lane of an fp64 pass instead of a whole fp64 trip. Entry = (point - p0) << 3 | pose.
+static constexpr int kPnpLaneEvents = 512;   // per wave
 
 // A wave-uniform pair into SGPRs (readfirstlane is an int builtin: bit copies).
 __device__ __forceinline__ pkf2 pk_uniform(pkf2 v) {
@@ -197,13 +201,14 @@ __device__ __forceinline__ pkf2 pk_uniform(pkf2 v) {
                 __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y)))};
 }
 
-template <int K, int WPE, bool CHEAP = true>
+template <int K, int WPE, bool CHEAP = true, bool LANE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void mcv_pnp_verify_pk(const PnpPoint* __restrict__ pts, int N, int chunk,
                                                          PnpCamera cam, PnpPkCam pc, const PnpPose* __restrict__ models,
                                                          int* __restrict__ counts, int hypCount, float thr2, bool fused,
                                                          const double* __restrict__ ext) {
     static_assert(K <= 8, "pose mask in 8 bits");
-    __shared__ uint32_t events[4][kPnpEvents];
+    constexpr int kCap = LANE ? kPnpLaneEvents : kPnpEvents;
+    __shared__ uint32_t events[4][kCap];
     const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * 256u + threadIdx.x) >> 6));
     const int wib = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -292,17 +297,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 out1 |= __builtin_amdgcn_ballot_w64(o.S.y > hi.y) & d1;
                 u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
             }
-            // branch-free: a trip with an undecided lane adds nothing here (recounted exactly later)
-            const uint32_t bit = u != 0 ? 1u << k : 0u;
-            und |= bit;
             const uint32_t c = (uint32_t)__popcll(in0 & vm0) + (uint32_t)__popcll(in1 & vm1);
-            cnt[k] += bit ? 0u : c;
+            if constexpr (LANE) {
+                // the decided lanes count now; the undecided ones go to the log, one entry per lane
+                cnt[k] += c;
+                if (u != 0 && ((validMask >> k) & 1u)) {   // wave-uniform, rare
+                    const uint64_t ud0 = vm0 & ~(in0 | out0), ud1 = vm1 & ~(in1 | out1);
+                    const int n0 = __popcll(ud0), n1 = __popcll(ud1);
+                    if (nev + n0 + n1 <= kCap) {
+                        const uint64_t lt = (1ull << lane) - 1ull;
+                        if ((ud0 >> lane) & 1ull)
+                            events[wib][nev + __popcll(ud0 & lt)] = ((uint32_t)(i0 - p0) << 3) | (uint32_t)k;
+                        if ((ud1 >> lane) & 1ull)
+                            events[wib][nev + n0 + __popcll(ud1 & lt)] = ((uint32_t)(i1 - p0) << 3) | (uint32_t)k;
+                    }
+                    nev += n0 + n1;
+                }
+            } else {
+                // branch-free: a trip with an undecided lane adds nothing here (recounted exactly later)
+                const uint32_t bit = u != 0 ? 1u << k : 0u;
+                und |= bit;
+                cnt[k] += bit ? 0u : c;
+            }
         }
-        und &= validMask;
-        if (__builtin_expect(und != 0, 0)) {
-            if (nev < kPnpEvents && lane == 0) events[wib][nev] = ((uint32_t)((base - p0) >> 7) << 8) | und;
-            ++nev;
+        if constexpr (!LANE) {
+            und &= validMask;
+            if (__builtin_expect(und != 0, 0)) {
+                if (nev < kPnpEvents && lane == 0) events[wib][nev] = ((uint32_t)((base - p0) >> 7) << 8) | und;
+                ++nev;
+            }
         }
+    }
+    if constexpr (LANE) {
+        // exact recount, 64 logged lanes per pass; an overflowing log recounts every (point, pose) of
+        // the chunk (same single inlined copy of the fp64 error)
+        const bool overflow = nev > kCap;
+        if (overflow) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) cnt[k] = 0;
+        }
+        const int total = overflow ? (p1 - p0) * K : nev;
+        if (total > 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (int j0 = 0; j0 < total; j0 += 64) {
+            const int j = j0 + lane;
+            bool act = j < total;
+            int k, i;
+            if (overflow) {
+                k = j % K;
+                i = p0 + j / K;
+            } else {
+                const uint32_t ev = events[wib][act ? j : 0];
+                k = (int)(ev & 7u);
+                i = p0 + (int)(ev >> 3);
+            }
+            act = act && ((validMask >> k) & 1u) != 0;
+            const PnpPose m = models[act ? h0 + k : h0];
+            const PnpPoint q = pts[act ? i : p0];
+            double R[9], t[3];
+            for (int r = 0; r < 9; ++r) R[r] = m.R[r];
+            for (int r = 0; r < 3; ++r) t[r] = m.t[r];
+            const bool in = act && pnp_error(cam, R, t, q.X, q.Y, q.Z, q.u, q.v, fused) <= thr2;
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk) cnt[kk] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(in && k == kk));
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (valid[k] && cnt[k]) atomicAdd(counts + h0 + k, (int)cnt[k]);
+        }
+        return;
     }
     // exact recount of the logged (trip, pose) events; too many undecided trips (a pose outside the
     // bound's domain) recount every trip of the chunk for every pose. One inlined copy of the fp64 trip
@@ -742,7 +808,16 @@ static void launch_pnp_verify_pk_k(const void* d_pts, int N, const double* cam8,
         const char* e = getenv("MCV_PNP_TIERS");
         return !(e && atoi(e) == 2);
     }();
-    if (exactOnly)
+    // MCV_PNP_LANE=0: the round-3 recount (a whole fp64 trip per undecided (trip, pose)); the lane log
+    // needs (point - p0) << 3 in 32 bits
+    static const bool laneLog = [] {
+        const char* e = getenv("MCV_PNP_LANE");
+        return !(e && atoi(e) == 0);
+    }();
+    if (exactOnly && laneLog && chunk < (1 << 28))
+        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3, false, true>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N,
+                           chunk, to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
+    else if (exactOnly)
         hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3, false>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk,
                            to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
     else if (wpe >= 5)
