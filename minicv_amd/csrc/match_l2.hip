@@ -438,6 +438,35 @@ __device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const fl
         }
 }
 
+// l2_epilogue16's scores with one wave-level test first: the tile's 16 scores per lane reduced by a
+// min (v_min3), and the insertions (each still behind its own s < b3) only when some lane's minimum
+// beats its third place — past the first tiles one compare and one skipped branch per tile instead of
+// sixteen. Same insertions in the same (ascending row) order.
+template <int NC>
+__device__ __forceinline__ void l2_epilogue16b(const floatx16 (&am)[NC], const floatx16 (&as)[NC], const float4 (&nv)[NC][4],
+                                               int base, float& b1, int& i1, float& b2, int& i2, float& b3) {
+    float sv[NC][16];
+    float mn = __builtin_inff();
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float4 n4 = nv[c][r >> 2];
+            const float nrm = (r & 3) == 0 ? n4.x : (r & 3) == 1 ? n4.y : (r & 3) == 2 ? n4.z : n4.w;
+            sv[c][r] = fmaf(-2.f, am[c][r] + as[c][r], nrm);
+            mn = fminf(mn, sv[c][r]);
+        }
+    if (mn < b3) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = 32 * c + (r & 3) + 8 * (r >> 2);
+                if (sv[c][r] < b3) top2b3_push_asc(b1, i1, b2, i2, b3, sv[c][r], __builtin_amdgcn_readfirstlane(base + row));
+            }
+    }
+}
+
 // Block = WPB waves x 32 queries (WPB = 8: each staged train tile serves 256 queries, halving the
 // train stream from MALL against 4); per train tile of TR rows and each 16-dim k block: A = the tile's hi /
 // lo rows from LDS (one ds_read_b128 each: lane l holds row l & 31, dims 16 kb + 8 (l >> 5) + j),
@@ -585,7 +614,7 @@ __global__ __launch_bounds__(64 * WPB) void mcv_l2_mfma16(const _Float16* __rest
 // one wave interleaving them. WPB = 4, QT = 1: blocks of 128 queries, 3 blocks per CU. QT = 2 (two
 // query sets per wave: each A fragment read from LDS feeds 6 MFMAs) fits two waves per SIMD (252
 // VGPRs) and measured slower (2.17 vs 1.98 ms at cfg5): the LDS reads were not the limiter.
-template <int DP, int WPB, int QT, int WAVES>
+template <int DP, int WPB, int QT, int WAVES, bool EB = false, bool PRIO = false>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void mcv_l2_mfma16q(
     const _Float16* __restrict__ qh, const _Float16* __restrict__ ql, const _Float16* __restrict__ th,
     const _Float16* __restrict__ tl, const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk, int nqPad,
@@ -637,6 +666,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
         for (int q = 0; q < QT; ++q)
 #pragma unroll
             for (int r = 0; r < 16; ++r) m[q][r] = sm[q][r] = 0.f;
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
             const f16x8 ah = *reinterpret_cast<const f16x8*>(&lh[buf][col * ROWH + 16 * kb + 8 * h]);
@@ -648,6 +678,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
             for (int q = 0; q < QT; ++q) sm[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[q][kb], sm[q], 0, 0, 0);
         }
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         // the next tile (staged a tile ago) into the idle LDS buffer, the one after into the staging set
         l2_lstore16<DP, TR, NT>(lh[buf ^ 1], ll[buf ^ 1], lnorm[buf ^ 1], sh, sl, ns);
         l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), sh, sl, ns);
@@ -657,7 +688,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
         for (int q = 0; q < QT; ++q) {
             const floatx16 am[1] = {m[q]}, as[1] = {sm[q]};
-            l2_epilogue16<1>(am, as, nv, t * TR, b1[q], i1[q], b2[q], i2[q], b3[q]);
+            if constexpr (EB) l2_epilogue16b<1>(am, as, nv, t * TR, b1[q], i1[q], b2[q], i2[q], b3[q]);
+            else l2_epilogue16<1>(am, as, nv, t * TR, b1[q], i1[q], b2[q], i2[q], b3[q]);
         }
         __syncthreads();
     }
@@ -1410,7 +1442,7 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         return e ? atoi(e) : 0;
     }();
     if (f16) nchunks = 8;
-    if (f16 && form0 == 0) {
+    if (f16 && (form0 == 0 || form0 >= 4)) {
         static const int cus = [] {
             int d = 0, n = 0;
             (void)hipGetDevice(&d);
@@ -1459,19 +1491,35 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         static const int form = [] {
             const char* e = getenv("MCV_L2_FORM");
             const int v = e ? atoi(e) : 0;
-            return v >= 0 && v <= 3 ? v : 0;
+            return v >= 0 && v <= 5 ? v : 0;
         }();
 #define MCV_L2_LAUNCH16X(D) hipLaunchKernelGGL((mcv_l2_mfma16x<D, 4, 2>), dim3(nqPad / 256, nchunks), dim3(256), 0, s, \
                                                wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, \
                                                wk.part.p, dom, xcdMap)
-#define MCV_L2_LAUNCH16Q(D, W, Q, V)                                                                               \
-    hipLaunchKernelGGL((mcv_l2_mfma16q<D, W, Q, V>), dim3(nqPad / (32 * W * Q), nchunks), dim3(64 * W), 0, s, wk.qh.p, \
-                       wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
-        if (f16 && form == 0) {
+#define MCV_L2_LAUNCH16Q(D, W, Q, V, ...)                                                                          \
+    hipLaunchKernelGGL((mcv_l2_mfma16q<D, W, Q, V, ##__VA_ARGS__>), dim3(nqPad / (32 * W * Q), nchunks), dim3(64 * W), 0, \
+                       s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
+        // 4: form 0 with the per-score epilogue test (l2_epilogue16) instead of the per-tile min test
+        // (l2_epilogue16b, the default: 1.876-1.879 vs 1.886-1.891 ms at cfg5, alternating runs)
+        // 5: form 0 with s_setprio 1 around each tile's MFMA cluster (cdna_hip_programming.md T5): 1.95-1.96
+        // vs 1.88 ms, slower (a prioritised wave's MFMA cluster holds off the other waves' epilogues)
+        if (f16 && form == 5) {
             switch (DP) {
-                case 32: MCV_L2_LAUNCH16Q(32, 4, 1, 3); break;
-                case 64: MCV_L2_LAUNCH16Q(64, 4, 1, 3); break;
-                default: MCV_L2_LAUNCH16Q(128, 4, 1, 3); break;
+                case 32: MCV_L2_LAUNCH16Q(32, 4, 1, 3, true, true); break;
+                case 64: MCV_L2_LAUNCH16Q(64, 4, 1, 3, true, true); break;
+                default: MCV_L2_LAUNCH16Q(128, 4, 1, 3, true, true); break;
+            }
+        } else if (f16 && form == 4) {
+            switch (DP) {
+                case 32: MCV_L2_LAUNCH16Q(32, 4, 1, 3, false); break;
+                case 64: MCV_L2_LAUNCH16Q(64, 4, 1, 3, false); break;
+                default: MCV_L2_LAUNCH16Q(128, 4, 1, 3, false); break;
+            }
+        } else if (f16 && form == 0) {
+            switch (DP) {
+                case 32: MCV_L2_LAUNCH16Q(32, 4, 1, 3, true); break;
+                case 64: MCV_L2_LAUNCH16Q(64, 4, 1, 3, true); break;
+                default: MCV_L2_LAUNCH16Q(128, 4, 1, 3, true); break;
             }
         } else if (f16 && form == 3) {
             switch (DP) {
