@@ -138,6 +138,8 @@ def parse():
     ap.add_argument("--n", type=int, default=N_CORR)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hamming-form", default="gemm", choices=["gemm", "popcount"],
+                    help="Hamming kernel: int8 GEMM on the matrix cores (default) or the XOR / popcount sweep")
     ap.add_argument("--pnp-kind", default="EPNP", choices=["Iterative", "EPNP", "P3P", "DLS", "UPNP", "AP3P"],
                     help="pnp workload: the reference's solverKind (EPNP = its own testPnp, Program.fs:27-32)")
     ap.add_argument("--no-secondary", action="store_true",
@@ -217,7 +219,10 @@ def bench_matcher(args):
     dist2 = torch.empty_like(dist_t)
 
     def step():
-        (D.match_hamming if ham else D.match_l2)(qs, td, idx, dist_t, idx2, dist2)
+        if ham:
+            D.match_hamming(qs, td, idx, dist_t, idx2, dist2, form=args.hamming_form)
+        else:
+            D.match_l2(qs, td, idx, dist_t, idx2, dist2)
 
     for _ in range(args.warmup):
         step()
@@ -247,7 +252,7 @@ def bench_matcher(args):
         if ham:
             pairs = cnt * nt
             ach = pairs / (avg_ms * 1e-3)
-            gemm = os.environ.get("MCV_HAMMING_FORM", "") != "popcount"
+            gemm = args.hamming_form == "gemm"
             kp = 256   # 32-byte descriptors: 256 +-1 bytes per expanded row
             mfma_roof = {"bound": "mfma-i8", "achieved": 2.0 * kp * ach / 1e12, "peak": I8_MFMA_PEAK_TOPS,
                          "unit": "Tops/s", "frac": 2.0 * kp * ach / 1e12 / I8_MFMA_PEAK_TOPS,
@@ -260,7 +265,7 @@ def bench_matcher(args):
             line = {"metric": "BF Hamming knn-2 queries/sec, 10k x 10k 256-bit (BASELINE config[1])",
                     "value": nq * args.steps / el, "unit": "queries/s",
                     "hamming_form": "int8 GEMM on the matrix cores (default)" if gemm else
-                                    "XOR / popcount sweep (MCV_HAMMING_FORM=popcount)",
+                                    "XOR / popcount sweep (--hamming-form popcount)",
                     "roofline": mfma_roof if gemm else {"bound": "int-valu", "achieved": HAM_OPS_PER_PAIR * ach / 1e12,
                                  "peak": INT32_PEAK_TOPS, "unit": "Tops/s",
                                  "frac": HAM_OPS_PER_PAIR * ach / 1e12 / INT32_PEAK_TOPS,
@@ -285,9 +290,7 @@ def bench_matcher(args):
             if form == 16:   # f16-split GEMM form: three f16 MFMA products per (query, train, dim)
                 roof = {"bound": "mfma-f16", "achieved": 3.0 * tf, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s",
                         "frac": 3.0 * tf / F16_MFMA_PEAK_TF,
-                        # MCV_L2_FORM (screen) 1 / 2 select the round-3 kernel / the one-wave two-set form
-                        "kernel": {"1": "mcv_l2_mfma16", "2": "mcv_l2_mfma16x"}.get(os.environ.get("MCV_L2_FORM", "0"),
-                                                                                  "mcv_l2_mfma16q"),
+                        "kernel": "mcv_l2_mfma16q",
                         "model": "fp32 operands split into f16 hi + lo; hi.hi + hi.lo + lo.hi on "
                                  "v_mfma_f32_32x32x16_f16 = 3 x 2 Nq Nt D MFMA flops per launch; "
                                  f"algorithmic rate {tf:.1f} TFLOP/s (2 Nq Nt D)"}
@@ -855,7 +858,7 @@ def bench_pnp(args, world, rank, dev):
                   "hbm": {"effective_GBps": p_bytes / (v_ms * 1e-3) / 1e9,
                           "algorithmic_bytes_per_launch": p_bytes, "peak": HBM_PEAK_GBPS}}
         # default: the certified packed-fp32 sweep (mcv_pnp_verify_pk) decides the fp64 test, so the fp32
-        # vector roof binds; MCV_PNP_FP64=1 runs the all-fp64 sweep (op-by-op: 1 flop per instruction)
+        # vector roof binds
         roof_pk = {"bound": "fp32-valu", "achieved": p_fl, "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
                    "frac": p_fl / FP32_PEAK_TF, **common,
                    "model": f"{P_FLOPS_PER_EVAL} (fp64-definition) flops per (hypothesis, correspondence), a "
@@ -865,11 +868,6 @@ def bench_pnp(args, world, rank, dev):
                              "frac": evals_s / issue_peak(PPK_CYC_PER_WAVE_EVAL),
                              "model": f"certified packed-fp32 projection + bound: {PPK_CYC_PER_WAVE_EVAL} SIMD "
                                       "cycles per 64 (pose, point) at 2.4 GHz"}}
-        roof_fp64 = {"bound": "fp64-valu (unfused: op-by-op projectPoints, 1 flop per instruction)",
-                     "achieved": p_fl, "peak": FP64_NOFMA_PEAK_TF, "unit": "TFLOP/s",
-                     "frac": p_fl / FP64_NOFMA_PEAK_TF, **common,
-                     "model": f"{P_FLOPS_PER_EVAL} fp64 FLOP per (hypothesis, correspondence), a division "
-                              "counted as one"}
         line = {
             "metric": f"RANSAC hypotheses/sec, solvePnPRansac {args.pnp_kind} (cvSolvePnPRansac path) @20k corrs",
             "value": total * args.steps / el, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
@@ -886,7 +884,7 @@ def bench_pnp(args, world, rank, dev):
                        "parallelism": f"hypothesis-sharded dp{world}"},
             "kernels": {"mcv_pnp_verify": {"avg_launch_ms": v_ms, "launches": vl,
                                            "evaluations_per_s": n * hyps / max(v_ms * 1e-3, 1e-12)}},
-            "roofline": (roof_fp64 if os.environ.get("MCV_PNP_FP64", "0") not in ("", "0") else roof_pk),
+            "roofline": roof_pk,
             "result": {"best_count": result["count"], "best_hyp": result["idx"],
                        "final_count": result["final_count"], "true_inliers": int(inl.sum())},
         }

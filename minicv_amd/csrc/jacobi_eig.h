@@ -36,25 +36,8 @@ static constexpr int kEigA = 0, kEigW = 36, kEigV = 45, kEigJunk = 126, kEigWs =
 // Lanes per hypothesis-kernel block: the 1016-byte working set per lane makes LDS the occupancy
 // limit (160 KB per CU). 40 lanes = 4 blocks of 40.6 KB per CU, one wave on every SIMD (cfg3 screen,
 // 2^20 hypotheses: 64 -> 39 lanes took the H generate 13.9 -> 11.4 ms; 39 vs 40 lanes 9.63 vs 9.34 ms
-// in scripts/eig_lanes_screen.sh); MCV_EIG_LANES = 32 / 39 / 48 / 64 re-screens.
+// in scripts/eig_lanes_screen.sh).
 static constexpr int kEigLanes = 40;
-inline int eig_lanes() {   // host: the launchers' screen knob
-    static const int v = [] {
-        const char* e = getenv("MCV_EIG_LANES");
-        return e ? atoi(e) : kEigLanes;
-    }();
-    return v;
-}
-
-// Workspace layout knob (host): MCV_EIG_SOA = 1 selects the element-major EigWsSoA slices (screen).
-inline bool eig_soa() {
-    static const bool v = [] {
-        const char* e = getenv("MCV_EIG_SOA");
-        return e ? atoi(e) != 0 : false;
-    }();
-    return v;
-}
-
 // Packed index of A(r, c), r < c < 9: row r starts at 7r - r(r-1)/2 - 1 + (r + 1); the base is
 // r(15 - r)/2 - 1 (r(15 - r) is even), one 24-bit multiply for a dynamic r.
 MCV_HD int eig_row_base(int r) {
@@ -79,25 +62,6 @@ struct EigWsLane {
     double* p;
     MCV_HD double& operator[](int e) { return p[e]; }
 };
-
-// Bank-conflict-free slices (element-major): a block of L lanes keeps its first 32 lanes' working sets
-// as [e][32] (element e of lane t at double 32 e + t) and the other L - 32 lanes' as [e][L - 32] behind
-// them. A ds_read/write_b64 serves a half-wave of 32 lanes over 64 four-byte banks; with the lane in
-// the low bits of the double index every lane of a half-wave owns its own bank pair (the first group)
-// or one of L - 32 <= 32 pairs spaced by the group's stride (the second: 8 e + t' never collides for
-// |t - t'| < 8), whatever element each lane touches — the pivot-dependent (k, l) accesses included.
-// The second group's size must be a power of two (L = 40 / 48 / 64).
-struct EigWsSoA {
-    char* p;    // lane base
-    int sh;     // log2 of the element stride in bytes
-    MCV_HD double& operator[](int e) { return *(double*)(p + ((unsigned)e << sh)); }
-};
-template <int L>
-MCV_HD EigWsSoA eig_ws_soa(double* block, int t) {
-    static_assert(L > 32 && L <= 64 && ((L - 32) & (L - 33)) == 0, "second lane group must be a power of two");
-    constexpr int sh2 = __builtin_ctz(L - 32) + 3;
-    return t < 32 ? EigWsSoA{(char*)(block + t), 8} : EigWsSoA{(char*)(block + 32 * kEigWs + (t - 32)), sh2};
-}
 
 // Byte offsets of the rotated pairs per pivot: row tri(k, l) holds, for i = 0..8, the elements
 // (A(i|k), A(i|l)) of the packed upper triangle as 8 e (the junk slot for i = k, l) in the low / high
@@ -402,215 +366,5 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
         if (i == pos) r = perm[i];
     return r;
 }
-
-#if defined(__HIP__)
-// ---- four lanes per hypothesis ----------------------------------------------------------------
-// The same JacobiImpl_ run by a quad of lanes sharing one 127-double LDS slice (EigWsQuad): every
-// lane of the quad follows the same control flow on the same values (the pivot, the rotation scalars
-// and indR / indC are computed in all four), and the per-element work is split by element: lane q
-// owns the candidates 4q .. 4q + 3 of the pivot scan and the rotated pairs / V columns i = q, q + 4
-// (and 8 for q = 0). Each element is still produced by one operation sequence of one lane, so the
-// result is bit-identical to eig9_jacobi. The cross-lane steps are quad DPP moves:
-//   pivot: the candidates' pairwise first-maximum tree (h = 1, 2 in a lane, h = 4, 8 across lanes:
-//          the tree of eig9_jacobi, so the same (k, l) on ties);
-//   rescans: lane-local first maxima over increasing indices, then (larger |v|, else smaller index).
-struct EigWsQuad {
-    double* p;   // the hypothesis' slice
-    int sub;     // lane within the quad
-    __device__ double& operator[](int e) { return p[e]; }
-};
-
-template <int CTRL>
-__device__ __forceinline__ int eig_quad_mov(int v) {
-    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL>
-__device__ __forceinline__ double eig_quad_mov(double v) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)eig_quad_mov<CTRL>((int)(unsigned)b);
-    const unsigned hi = (unsigned)eig_quad_mov<CTRL>((int)(unsigned)(b >> 32));
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-static constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E;   // quad_perm [1,0,3,2] / [2,3,0,1]
-
-// LDS ops of one wave complete in order; this keeps the compiler from moving them across.
-__device__ __forceinline__ void eig_quad_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-
-// The pivot tree's cross-lane level: the lower lane group's value comes first.
-template <int CTRL>
-__device__ __forceinline__ void eig_quad_pick(double& v, int& kl, bool upper) {
-    const double ov = eig_quad_mov<CTRL>(v);
-    const int okl = eig_quad_mov<CTRL>(kl);
-    // first = lower group, second = upper group; the second wins only when strictly greater
-    const double f = upper ? ov : v, g = upper ? v : ov;
-    const int fk = upper ? okl : kl, gk = upper ? kl : okl;
-    const bool t = __builtin_fabs(f) < __builtin_fabs(g);
-    v = t ? g : f;
-    kl = t ? gk : fk;
-}
-
-// The rescans' cross-lane level: larger |v| wins, equal magnitudes take the smaller index.
-template <int CTRL>
-__device__ __forceinline__ void eig_quad_first_max(double& v, int& m) {
-    const double ov = eig_quad_mov<CTRL>(v);
-    const int om = eig_quad_mov<CTRL>(m);
-    const double a = __builtin_fabs(v), b = __builtin_fabs(ov);
-    const bool t = a < b || (a == b && om < m);
-    v = t ? ov : v;
-    m = t ? om : m;
-}
-
-__device__ inline int eig9_jacobi(EigWsQuad& ws, double (&w)[9], int pos, int* iters = nullptr) {
-    constexpr int n = 9;
-    const int q = ws.sub;
-    double* const P = ws.p;
-    char* const B = reinterpret_cast<char*>(P);
-    eig_quad_fence();   // the caller's A / W stores (every lane wrote them) precede the reads below
-    for (int e = q; e < n * n; e += 4) P[kEigV + e] = (e / n == e % n) ? 1.0 : 0.0;
-    if (q == 0) P[kEigJunk] = 0.0;
-    uint32_t indR = 0, indC = 0;
-#pragma unroll
-    for (int k = 0; k < n; ++k) {
-        if (k < n - 1) {
-            int m = k + 1;
-            double mv = __builtin_fabs(P[eig_tri(k, k + 1)]);
-#pragma unroll
-            for (int i = k + 2; i < n; ++i) {
-                const double val = __builtin_fabs(P[eig_tri(k, i)]);
-                if (mv < val) mv = val, m = i;
-            }
-            indR = eig_set_nib(indR, k, m);
-        }
-        if (k > 0) {
-            int m = 0;
-            double mv = __builtin_fabs(P[eig_tri(0, k)]);
-#pragma unroll
-            for (int i = 1; i < k; ++i) {
-                const double val = __builtin_fabs(P[eig_tri(i, k)]);
-                if (mv < val) mv = val, m = i;
-            }
-            indC = eig_set_nib(indC, k - 1, m);
-        }
-    }
-    eig_quad_fence();
-    // the lane's elements: i = q, q + 4, and 8 (lane 0 only)
-    const bool has2 = q == 0;
-    int it = 0;
-    for (; it < n * n * 30; ++it) {
-        // candidates 4q .. 4q + 3: c < 8 is row c through indR, c >= 8 column c - 7 through indC
-        double cv[4];
-        int ck[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = 4 * q + j;
-            const bool row = c < 8;
-            const int rr = row ? c : eig_nib(indC, c - 8);
-            const int cc = row ? eig_nib(indR, c) : c - 7;
-            cv[j] = P[eig_row_base(rr) + cc];
-            ck[j] = rr * 16 + cc;
-        }
-        eig_pick(cv[0], ck[0], cv[1], ck[1]);
-        eig_pick(cv[2], ck[2], cv[3], ck[3]);
-        eig_pick(cv[0], ck[0], cv[2], ck[2]);
-        eig_quad_pick<kQuadXor1>(cv[0], ck[0], (q & 1) != 0);
-        eig_quad_pick<kQuadXor2>(cv[0], ck[0], (q & 2) != 0);
-        const int k = ck[0] >> 4, l = ck[0] & 15;
-        const int ekl = eig_tri(k, l);
-        const double p = cv[0];
-        if (__builtin_fabs(p) <= kDblEpsilon) break;
-        const double wk = P[kEigW + k], wl = P[kEigW + l];
-        const uint32_t* lr = kEigPairLut.w[ekl];
-        int e0[3], e1[3];
-        double a0[3], b0[3], va[3], vb[3];
-        const int vk = kEigV + 9 * k, vl = kEigV + 9 * l;
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            const int i = m < 2 ? q + 4 * m : 8;
-            const uint32_t x = lr[i];
-            e0[m] = (int)(x & 0xffffu);
-            e1[m] = (int)(x >> 16);
-            a0[m] = *reinterpret_cast<const double*>(B + e0[m]);
-            b0[m] = *reinterpret_cast<const double*>(B + e1[m]);
-            va[m] = P[vk + i];
-            vb[m] = P[vl + i];
-        }
-        const double y = (wl - wk) * 0.5;
-        double c, s, t;
-        eig_rotation(p, y, c, s, t);
-        if (q == 0) {
-            P[ekl] = 0;
-            P[kEigW + k] = wk - t;
-            P[kEigW + l] = wl + t;
-        }
-        double nk[3], nl[3];
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            nk[m] = a0[m] * c - b0[m] * s;
-            nl[m] = a0[m] * s + b0[m] * c;
-            if (m < 2 || has2) {
-                const int i = m < 2 ? q + 4 * m : 8;
-                *reinterpret_cast<double*>(B + e0[m]) = nk[m];
-                *reinterpret_cast<double*>(B + e1[m]) = nl[m];
-                P[vk + i] = va[m] * c - vb[m] * s;
-                P[vl + i] = va[m] * s + vb[m] * c;
-            }
-        }
-        // rescans of rows / columns k and l: lane-local first maxima, then across the quad
-        int mRk = k + 1, mCk = 0, mRl = l + 1, mCl = 0;
-        double vRk = 0, vCk = 0, vRl = 0, vCl = 0;
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-            const int i = m < 2 ? q + 4 * m : (has2 ? 8 : -1);
-            const double ak = __builtin_fabs(nk[m]), al = __builtin_fabs(nl[m]);
-            const bool tRk = i > k && __builtin_fabs(vRk) < ak, tCk = i >= 0 && i < k && __builtin_fabs(vCk) < ak;
-            const bool tRl = i > l && __builtin_fabs(vRl) < al, tCl = i >= 0 && i < l && __builtin_fabs(vCl) < al;
-            vRk = tRk ? nk[m] : vRk; mRk = tRk ? i : mRk;
-            vCk = tCk ? nk[m] : vCk; mCk = tCk ? i : mCk;
-            vRl = tRl ? nl[m] : vRl; mRl = tRl ? i : mRl;
-            vCl = tCl ? nl[m] : vCl; mCl = tCl ? i : mCl;
-        }
-        eig_quad_first_max<kQuadXor1>(vRk, mRk);
-        eig_quad_first_max<kQuadXor1>(vCk, mCk);
-        eig_quad_first_max<kQuadXor1>(vRl, mRl);
-        eig_quad_first_max<kQuadXor1>(vCl, mCl);
-        eig_quad_first_max<kQuadXor2>(vRk, mRk);
-        eig_quad_first_max<kQuadXor2>(vCk, mCk);
-        eig_quad_first_max<kQuadXor2>(vRl, mRl);
-        eig_quad_first_max<kQuadXor2>(vCl, mCl);
-        if (k < n - 1) indR = eig_set_nib(indR, k, mRk);
-        if (k > 0) indC = eig_set_nib(indC, k - 1, mCk);
-        if (l < n - 1) indR = eig_set_nib(indR, l, mRl);
-        indC = eig_set_nib(indC, l - 1, mCl);
-        eig_quad_fence();
-    }
-    if (iters) *iters = it;
-    eig_quad_fence();
-    int perm[n];
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-        w[i] = P[kEigW + i];
-        perm[i] = i;
-    }
-#pragma unroll
-    for (int k = 0; k < n - 1; ++k) {
-        int m = k;
-        double wm = w[k];
-#pragma unroll
-        for (int i = k + 1; i < n; ++i)
-            if (wm < w[i]) m = i, wm = w[i];
-#pragma unroll
-        for (int i = k + 1; i < n; ++i)
-            if (i == m) {
-                const double tw = w[k]; w[k] = w[i]; w[i] = tw;
-                const int tp = perm[k]; perm[k] = perm[i]; perm[i] = tp;
-            }
-    }
-    int r = 0;
-#pragma unroll
-    for (int i = 0; i < n; ++i)
-        if (i == pos) r = perm[i];
-    return r;
-}
-#endif
 
 }  // namespace mcv

@@ -31,7 +31,7 @@ void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_co
 void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s);
 // Packed-f32 sweep of the fused error over the paired layout (ransac_h.hip, HPair: 32 B per 2).
 void launch_h_pair(const float* d_pts4, int N, void* d_pairs, hipStream_t s);
-bool launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
+void launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
                             int hypCount, float thr2, const float* d_bbox, hipStream_t s);
 // Certified division-free sweep of the op-by-op error (the default) + exact recount of its redo slots;
 // d_bb = launch_abs_bound4 of the float4 points.
@@ -194,8 +194,9 @@ void launch_match_compact(const int* d_idx, const int* d_di1, const int* d_di2, 
                           int* d_off, int* d_pairs, float* d_dist, float* d_pts4, hipStream_t s);
 
 // ---- matchers (match_hamming.hip, match_l2.hip)
+static constexpr int kHammingFormGemm = 0, kHammingFormPopcount = 1;
 int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc, int* d_idx,
-                         int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s);
+                         int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s, int form = kHammingFormGemm);
 int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim, int* d_idx, float* d_dist,
                     int* d_idx2, float* d_dist2, hipStream_t s);
 int l2_last_exact_scans();

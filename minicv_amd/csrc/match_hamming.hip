@@ -404,7 +404,7 @@ struct HammingWork {
 };
 
 int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc, int* d_idx,
-                         int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s) {
+                         int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s, int form) {
     if (bytesPerDesc < 1 || bytesPerDesc > 64) fail("cvMatchHamming: bytesPerDesc %d outside [1, 64]", bytesPerDesc);
     if (nt < 0 || nt > (int)kIdxMask) fail("cvMatchHamming: nt %d outside [0, 2^22)", nt);
     if (nq <= 0) return 0;
@@ -429,25 +429,14 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         q = wk.qpack.p;
         t = wk.tpack.p;
     }
-    // MCV_HAMMING_FORM=popcount: the XOR / popcount sweep (read per call: tests compare both forms)
-    const char* formEnv = getenv("MCV_HAMMING_FORM");
-    const bool gemm = !(formEnv && std::strcmp(formEnv, "popcount") == 0);
-    if (gemm && nt > 0) {
-        constexpr int WPB = 4;
-        static const int QT = [] {   // query tiles per wave: 2, or 1 (screen: MCV_HAMMING_QT)
-            const char* e = getenv("MCV_HAMMING_QT");
-            return e && atoi(e) == 1 ? 1 : 2;
-        }();
-        static const int SUB = [] {   // 32-row MFMA tiles per staged train tile: 1, or 2 (screen: MCV_HAMMING_SUB;
-            const char* e = getenv("MCV_HAMMING_SUB");   // 2 measured 33.6 vs 32.1 us at cfg2)
-            return e && atoi(e) == 2 ? 2 : 1;
-        }();
+    // form 1: the XOR / popcount sweep (mcvMatchHammingDeviceForm); 0: the int8 GEMM (default)
+    if (form == kHammingFormGemm && nt > 0) {
+        // 4 waves per block, 2 query tiles per wave, one 32-row MFMA tile per staged train tile, ~8192
+        // waves in the grid (cfg2 screens: 1 query tile, 2-tile staging 33.6 vs 32.1 us; 2048 / 4096 /
+        // 8192 / 16384 waves 43.2 / 33.3 / 32.1 / 34.8 us)
+        constexpr int WPB = 4, QT = 2, SUB = 1, target = 8192;
         const int qblocks = (nq + 32 * QT * WPB - 1) / (32 * QT * WPB);
         const int ntTiles = (nt + 32 * SUB - 1) / (32 * SUB);
-        static const int target = [] {   // waves in the grid (screen: MCV_HAMMING_WAVES; cfg2: 2048 / 4096 /
-            const char* e = getenv("MCV_HAMMING_WAVES");   // 8192 / 16384 -> 43.2 / 33.3 / 32.1 / 34.8 us)
-            return e ? atoi(e) : 8192;
-        }();
         int nchunks = std::max(1, std::min(ntTiles, (target / WPB + qblocks - 1) / qblocks));
         if (nchunks > 8) nchunks = nchunks / 8 * 8;   // whole XCD rounds
         nchunks = std::max(nchunks, (ntTiles * 32 * SUB + kHamChunkRows - 1) / kHamChunkRows);   // key index field
@@ -460,9 +449,8 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
 #define MCV_HAM_GEMM(W_, Q_, S_) hipLaunchKernelGGL((mcv_hamming_mfma<W_, Q_, WPB, S_>), dim3(qblocks, nchunks), \
                                                     dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, tilesPerChunk, wk.part.p, \
                                                     xcdMap)
-            if (W == 8 && QT == 1) { if (SUB == 2) MCV_HAM_GEMM(8, 1, 2); else MCV_HAM_GEMM(8, 1, 1); }
-            else if (W == 8) { if (SUB == 2) MCV_HAM_GEMM(8, 2, 2); else MCV_HAM_GEMM(8, 2, 1); }
-            else { if (SUB == 2) MCV_HAM_GEMM(16, 2, 2); else MCV_HAM_GEMM(16, 2, 1); }
+            if (W == 8) MCV_HAM_GEMM(8, QT, SUB);
+            else MCV_HAM_GEMM(16, QT, SUB);
 #undef MCV_HAM_GEMM
         }
         hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nchunks, d_idx,
@@ -471,14 +459,9 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         wk.fence.leave(s);
         return nq;
     }
-    static const int targetWaves = [] {
-        const char* e = getenv("MCV_HAMMING_WAVES");  // variant screen (scripts/sweep_hamming.sh)
-        return e ? atoi(e) : 16384;
-    }();
-    static const int Q = [] {
-        const char* e = getenv("MCV_HAMMING_Q");  // queries per lane (1 or 2; 2 screened slower)
-        return e && atoi(e) == 2 ? 2 : 1;
-    }();
+    // popcount form: one query per lane, one SGPR vector per staged group, ~16384 waves
+    // (scripts/sweep_hamming.sh: 2 queries per lane and 2-vector groups screened slower)
+    constexpr int targetWaves = 16384, Q = 1, NB = 1;
     const int qwaves = (nq + 64 * Q - 1) / (64 * Q);
     int nchunks = (targetWaves + qwaves - 1) / qwaves;
     const int maxChunks = nt > 0 ? (nt + 63) / 64 : 1;
@@ -489,16 +472,10 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     wk.part.ensure((size_t)nparts * nq);
     dim3 grid(qwaves, nparts);
     ProfScope ps("hamming", s);
-    static const int NB = [] {
-        const char* e = getenv("MCV_HAMMING_NB");  // SGPR vectors per staged group (1 or 2)
-        return e && atoi(e) == 2 ? 2 : 1;
-    }();
 #define MCV_HAM_LAUNCH(W_, Q_, NB_) \
     hipLaunchKernelGGL((mcv_hamming_partial<W_, Q_, NB_>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p)
-    if (W == 8 && Q == 1) { if (NB == 2) MCV_HAM_LAUNCH(8, 1, 2); else MCV_HAM_LAUNCH(8, 1, 1); }
-    else if (W == 8) { if (NB == 2) MCV_HAM_LAUNCH(8, 2, 2); else MCV_HAM_LAUNCH(8, 2, 1); }
-    else if (Q == 1) { if (NB == 2) MCV_HAM_LAUNCH(16, 1, 2); else MCV_HAM_LAUNCH(16, 1, 1); }
-    else { if (NB == 2) MCV_HAM_LAUNCH(16, 2, 2); else MCV_HAM_LAUNCH(16, 2, 1); }
+    if (W == 8) MCV_HAM_LAUNCH(8, Q, NB);
+    else MCV_HAM_LAUNCH(16, Q, NB);
 #undef MCV_HAM_LAUNCH
     hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nparts, d_idx,
                        d_dist, d_idx2, d_dist2);

@@ -17,7 +17,7 @@
 //   and inserts each score with 2 v_cmp + 6 v_cndmask (no divergent branch per score: the branchy
 //   form the compiler chose cost 7 % of the kernel, 5.80 -> 5.38 ms at cfg5).
 //   Grid = (query blocks of 128) x (train chunks); each lane keeps its top-3 GEMM-form scores.
-// mcv_l2_mfma16<DP, TR>: the same GEMM form on the f16 matrix pipe (16x the f32 MFMA rate) with every
+// mcv_l2_mfma16q<DP, ...>: the same GEMM form on the f16 matrix pipe (16x the f32 MFMA rate) with every
 //   fp32 operand split into f16 hi + lo (x = hi + lo + r, |r| <= 2^-22 |x| + 2^-13): q.t ~ qh.th +
 //   qh.tl + ql.th in two 32x32x16 accumulator chains (hi.hi; hi.lo then lo.hi) — 24 MFMAs of 32
 //   cycles per 32 x 32 x 128 tile against 64 of 64 cycles in f32. f16 x f16 products are exact in f32; the dropped ql.tl and the
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
                                                      const float* __restrict__ tnorm, int ntTiles,
                                                      int tilesPerChunk, int nqPad, L2Part* __restrict__ part,
                                                      const unsigned* __restrict__ dom) {
-    if (l2_f16_domain(dom)) return;   // grid-uniform: mcv_l2_mfma16 takes this launch
+    if (l2_f16_domain(dom)) return;   // grid-uniform: mcv_l2_mfma16q takes this launch
     constexpr int KS = DP / 2;          // MFMA k-steps (2 dims each)
     constexpr int ROWF = DP + 4;        // padded LDS row, floats
     constexpr int PER = TR * DP / 1024; // float4 staging loads per thread per tile (TR rows x DP)
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
                 const float4 n4 = nv[c][r >> 2];
                 const float nrm = (r & 3) == 0 ? n4.x : (r & 3) == 1 ? n4.y : (r & 3) == 2 ? n4.z : n4.w;
                 const float s = fmaf(-2.f, acc[c][r], nrm);
-                // as in mcv_l2_mfma16: a score >= b3 (or NaN, which the exact definition never ranks)
+                // as in mcv_l2_mfma16q: a score >= b3 (or NaN, which the exact definition never ranks)
                 // changes nothing
                 if (s < b3) top2b3_push_asc(b1, i1, b2, i2, b3, s, t * TR + row);
             }
@@ -415,35 +415,16 @@ __device__ __forceinline__ void l2_lstore16(_Float16* __restrict__ lh, _Float16*
     if (threadIdx.x < TR) lnorm[threadIdx.x] = nstg;
 }
 
-// Registers [r0, r0 + RN) of a tile's scores -> the lane's running top-2 / third place (train rows in
-// ascending index order across calls with increasing ranges). The index carried is the tile-row
-// index without the lane half's 4 h (wave-uniform, an SGPR operand of the selects); the caller adds
-// 4 h to i1 / i2 at the end (ties never compare indices here: the rows arrive in ascending order).
-template <int NC, int RN = 16>
-__device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const floatx16 (&as)[NC], const float4 (&nv)[NC][4],
-                                              int base, float& b1, int& i1, float& b2, int& i2, float& b3, int r0 = 0) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int r = r0; r < r0 + RN; ++r) {
-            const int row = 32 * c + (r & 3) + 8 * (r >> 2);
-            const float4 n4 = nv[c][r >> 2];
-            const float nrm = (r & 3) == 0 ? n4.x : (r & 3) == 1 ? n4.y : (r & 3) == 2 ? n4.z : n4.w;
-            const float dot = am[c][r] + as[c][r];
-            const float s = fmaf(-2.f, dot, nrm);
-            // a score >= b3 changes neither the top-2 nor the third place (med3(s, b2, b3) = b3): past
-            // the first tiles almost no lane of a wave needs the 9-instruction insertion, and a
-            // branch with no lane active is skipped whole
-            if (s < b3) top2b3_push_asc(b1, i1, b2, i2, b3, s, __builtin_amdgcn_readfirstlane(base + row));
-        }
-}
-
-// l2_epilogue16's scores with one wave-level test first: the tile's 16 scores per lane reduced by a
-// min (v_min3), and the insertions (each still behind its own s < b3) only when some lane's minimum
-// beats its third place — past the first tiles one compare and one skipped branch per tile instead of
-// sixteen. Same insertions in the same (ascending row) order.
+// A tile's scores (s = |t|^2 - 2 q.t from the two accumulator chains) -> the lane's running top-2 /
+// third place (train rows in ascending index order across calls with increasing ranges). One
+// wave-level test first: the tile's 16 scores per lane reduced by a min (v_min3), and the insertions
+// (each behind its own s < b3: a score >= b3 changes neither the top-2 nor the third place) only when
+// some lane's minimum beats its third place — past the first tiles one compare and one skipped branch
+// per tile (round 4: against a compare-and-branch per score, 1.876-1.879 vs 1.886-1.891 ms at cfg5).
+// The index carried is the tile-row index without the lane half's 4 h (wave-uniform, an SGPR operand
+// of the selects); the caller adds 4 h to i1 / i2 at the end.
 template <int NC>
-__device__ __forceinline__ void l2_epilogue16b(const floatx16 (&am)[NC], const floatx16 (&as)[NC], const float4 (&nv)[NC][4],
+__device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const floatx16 (&as)[NC], const float4 (&nv)[NC][4],
                                                int base, float& b1, int& i1, float& b2, int& i2, float& b3) {
     float sv[NC][16];
     float mn = __builtin_inff();
@@ -467,154 +448,17 @@ __device__ __forceinline__ void l2_epilogue16b(const floatx16 (&am)[NC], const f
     }
 }
 
-// Block = WPB waves x 32 queries (WPB = 8: each staged train tile serves 256 queries, halving the
-// train stream from MALL against 4); per train tile of TR rows and each 16-dim k block: A = the tile's hi /
-// lo rows from LDS (one ds_read_b128 each: lane l holds row l & 31, dims 16 kb + 8 (l >> 5) + j),
-// B = the wave's queries hi / lo (VGPR-resident, the same dims), three accumulator chains
-// (hi.hi, hi.lo, lo.hi) interleaved. Scores, epilogue and output as mcv_l2_mfma.
-template <int DP, int TR, int WPB>
-__global__ __launch_bounds__(64 * WPB) void mcv_l2_mfma16(const _Float16* __restrict__ qh, const _Float16* __restrict__ ql,
-                                                       const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
-                                                       const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk,
-                                                       int nqPad, L2Part* __restrict__ part,
-                                                       const unsigned* __restrict__ dom, bool xcdMap) {
-    if (!l2_f16_domain(dom)) return;   // grid-uniform: the f32 kernel takes this launch
-    // XCD-aware (query block, train chunk) order: blocks are dealt round-robin over the 8 XCDs, so with
-    // chunk = linear block id mod C (C | 8) every XCD streams one chunk of the train set (3.2 MB of f16
-    // hi / lo at cfg5) through its own L2 instead of the whole set through the MALL
-    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
-    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
-    constexpr int KB = DP / 16;
-    constexpr int ROWH = DP + 8;              // halves per LDS row (16 B pad: conflict-free b128 reads)
-    constexpr int NC = TR / 32;
-    constexpr int NT = 64 * WPB;
-    constexpr int PER = (TR * DP / 8 + NT - 1) / NT;
-    __shared__ __attribute__((aligned(16))) _Float16 lh[2][TR * ROWH];
-    __shared__ __attribute__((aligned(16))) _Float16 ll[2][TR * ROWH];
-    __shared__ __attribute__((aligned(16))) float lnorm[2][TR];
-
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int h = lane >> 5, col = lane & 31;
-    const int q0 = (bx * WPB + wave) * 32;
-    f16x8 bh[KB], bl[KB];
-    {
-        const f16x8* rh = reinterpret_cast<const f16x8*>(qh + (size_t)(q0 + col) * DP + 8 * h);
-        const f16x8* rl = reinterpret_cast<const f16x8*>(ql + (size_t)(q0 + col) * DP + 8 * h);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            bh[kb] = rh[2 * kb];
-            bl[kb] = rl[2 * kb];
-        }
-    }
-    const int tBegin = by * tilesPerChunk;
-    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
-    float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
-    int i1 = -1, i2 = -1;
-    // Train tiles: LDS double buffer, fed from two register staging sets, so a tile's global loads
-    // are issued two tiles before it is computed on (one tile of compute hides less than a MALL load)
-    f16x8 sh0[PER], sl0[PER], sh1[PER], sl1[PER];
-    float ns0 = 0.f, ns1 = 0.f;
-    if (tBegin < tEnd) {
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, tBegin, sh0, sl0, ns0);
-        l2_lstore16<DP, TR, NT>(lh[0], ll[0], lnorm[0], sh0, sl0, ns0);
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(tBegin + 1, tEnd - 1), sh1, sl1, ns1);
-    }
-    __syncthreads();
-    // Two accumulator sets (hi.hi and hi.lo + lo.hi chains, norms, tile index) in turn: a tile's MFMAs
-    // fill one set while the previous tile's epilogue (VALU) drains the other, with no copies. The
-    // first trip drains a dummy set: +inf norms score +inf, which changes no top-2 and no third place.
-    floatx16 xm[NC], xs[NC], ym[NC], ys[NC];
-    float4 xn[NC][4], yn[NC][4];
-    int xt = tBegin, yt = tBegin;
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) yn[c][j] = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) ym[c][r] = ys[c][r] = 0.f;
-    // one tile t: loads of tile t + 2 into staging set (ldh, ldl), MFMAs on LDS buffer buf into (cm, cs),
-    // the epilogue of (em, es), then tile t + 1 (staging set sth / stl, loaded a tile ago) into the other
-    // LDS buffer
-    auto tile = [&](int t, f16x8 (&ldh)[PER], f16x8 (&ldl)[PER], float& ldn, const f16x8 (&sth)[PER],
-                    const f16x8 (&stl)[PER], const float& stn, floatx16 (&cm)[NC], floatx16 (&cs)[NC],
-                    float4 (&cn)[NC][4], int& ct, const floatx16 (&em)[NC], const floatx16 (&es)[NC],
-                    const float4 (&en)[NC][4], int et) {
-        const int buf = (t - tBegin) & 1;
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) cn[c][j] = *reinterpret_cast<const float4*>(&lnorm[buf][32 * c + 8 * j + 4 * h]);
-        ct = t;
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cm[c][r] = cs[c][r] = 0.f;
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            f16x8 ah[NC], al[NC];
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                ah[c] = *reinterpret_cast<const f16x8*>(&lh[buf][(32 * c + col) * ROWH + 16 * kb + 8 * h]);
-                al[c] = *reinterpret_cast<const f16x8*>(&ll[buf][(32 * c + col) * ROWH + 16 * kb + 8 * h]);
-            }
-#pragma unroll
-            for (int c = 0; c < NC; ++c) cm[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], bh[kb], cm[c], 0, 0, 0);
-#pragma unroll
-            for (int c = 0; c < NC; ++c) cs[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], bl[kb], cs[c], 0, 0, 0);
-#pragma unroll
-            for (int c = 0; c < NC; ++c) cs[c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], bh[kb], cs[c], 0, 0, 0);
-            // a share of the previous tile's epilogue (VALU) after each k block's three MFMAs
-            if constexpr (NC == 1 && KB == 8) l2_epilogue16<NC, 2>(em, es, en, et * TR, b1, i1, b2, i2, b3, 2 * kb);
-        }
-        if constexpr (!(NC == 1 && KB == 8)) l2_epilogue16<NC>(em, es, en, et * TR, b1, i1, b2, i2, b3);
-        // tile t + 2's loads issued after the MFMAs (issued ahead of them, the in-order vmcnt made the
-        // k loop wait for them); they land during the next tile
-        // unconditional (past the chunk's end: a re-read of its last tile, stored into the idle buffer),
-        // so the vmcnt waits count exact numbers of loads instead of draining the queue
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), ldh, ldl, ldn);
-        l2_lstore16<DP, TR, NT>(lh[buf ^ 1], ll[buf ^ 1], lnorm[buf ^ 1], sth, stl, stn);
-        __syncthreads();
-    };
-    // the query fragments' loads complete here, once: left pending, their first uses inside the k loop
-    // become vmcnt waits that, in steady state, drain the staging loads in flight (in-order counter)
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-    for (int t = tBegin; t < tEnd; t += 2) {
-        tile(t, sh0, sl0, ns0, sh1, sl1, ns1, xm, xs, xn, xt, ym, ys, yn, yt);
-        if (t + 1 < tEnd) tile(t + 1, sh1, sl1, ns1, sh0, sl0, ns0, ym, ys, yn, yt, xm, xs, xn, xt);
-    }
-    // the last tile's set: x after an odd count of tiles, y after an even one
-    if (tBegin < tEnd) {
-        if (((tEnd - tBegin) & 1) != 0) l2_epilogue16<NC>(xm, xs, xn, xt * TR, b1, i1, b2, i2, b3);
-        else l2_epilogue16<NC>(ym, ys, yn, yt * TR, b1, i1, b2, i2, b3);
-    }
-    // the lane half's row offset (the epilogue carried wave-uniform tile-row indices)
-    if (i1 >= 0) i1 += 4 * h;
-    if (i2 >= 0) i2 += 4 * h;
-    const float ob1 = __shfl_xor(b1, 32, 64), ob2 = __shfl_xor(b2, 32, 64), ob3 = __shfl_xor(b3, 32, 64);
-    const int oi1 = __shfl_xor(i1, 32, 64), oi2 = __shfl_xor(i2, 32, 64);
-    if (h == 0) {
-        float c1 = b1, c2 = b2, c3 = b3;
-        third_fold(c1, c2, c3, ob1);
-        third_fold(c1, c2, c3, ob2);
-        third_fold(c1, c2, c3, ob3);
-        top2_push(b1, i1, b2, i2, ob1, oi1);
-        top2_push(b1, i1, b2, i2, ob2, oi2);
-        L2Part p;
-        p.b1 = b1; p.b2 = b2; p.b3 = c3; p.i1 = i1; p.i2 = i2; p.i3 = -1;
-        part[(size_t)by * nqPad + q0 + col] = p;
-    }
-}
-
-// The default f16-split GEMM form (round 4): mcv_l2_mfma16's tiles, MFMA chains and epilogue with one
-// accumulator set per query set (QT sets of 32 queries per wave) instead of two sets in turn, and
-// the next tile staged one tile ahead through one register set: 150 VGPRs for QT = 1, so three waves
-// per SIMD (WAVES, amdgpu_waves_per_eu) overlap one wave's epilogue with the others' MFMAs instead of
-// one wave interleaving them. WPB = 4, QT = 1: blocks of 128 queries, 3 blocks per CU. QT = 2 (two
-// query sets per wave: each A fragment read from LDS feeds 6 MFMAs) fits two waves per SIMD (252
-// VGPRs) and measured slower (2.17 vs 1.98 ms at cfg5): the LDS reads were not the limiter.
-template <int DP, int WPB, int QT, int WAVES, bool EB = false, bool PRIO = false>
+// The f16-split GEMM form. Block = WPB waves x 32 QT queries; per train tile of 32 rows and each
+// 16-dim k block: A = the tile's hi / lo rows from LDS (one ds_read_b128 each: lane l holds row l & 31,
+// dims 16 kb + 8 (l >> 5) + j), B = the wave's queries hi / lo (VGPR-resident, the same dims), three
+// accumulator chains (hi.hi, then hi.lo and lo.hi into one) on v_mfma_f32_32x32x16_f16. One
+// accumulator set per query set, the next tile staged one tile ahead through one register set: 150
+// VGPRs for QT = 1, so three waves per SIMD (WAVES, amdgpu_waves_per_eu) overlap one wave's epilogue
+// with the others' MFMAs. WPB = 4, QT = 1: blocks of 128 queries, 3 blocks per CU. Screened in round
+// 4 (cfg5): the round-3 form with two accumulator sets in turn 2.07 ms; QT = 2 at two waves per SIMD
+// (252 VGPRs) 2.17 ms, at one wave per SIMD 2.98 ms; s_setprio 1 around the MFMA cluster 1.95 ms;
+// 8-wave blocks 2.36 ms; four waves per SIMD (23 spilled VGPRs) 2.55 ms; this form 1.88 ms.
+template <int DP, int WPB, int QT, int WAVES>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void mcv_l2_mfma16q(
     const _Float16* __restrict__ qh, const _Float16* __restrict__ ql, const _Float16* __restrict__ th,
     const _Float16* __restrict__ tl, const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk, int nqPad,
@@ -666,7 +510,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
         for (int q = 0; q < QT; ++q)
 #pragma unroll
             for (int r = 0; r < 16; ++r) m[q][r] = sm[q][r] = 0.f;
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
             const f16x8 ah = *reinterpret_cast<const f16x8*>(&lh[buf][col * ROWH + 16 * kb + 8 * h]);
@@ -678,7 +521,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
             for (int q = 0; q < QT; ++q) sm[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[q][kb], sm[q], 0, 0, 0);
         }
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         // the next tile (staged a tile ago) into the idle LDS buffer, the one after into the staging set
         l2_lstore16<DP, TR, NT>(lh[buf ^ 1], ll[buf ^ 1], lnorm[buf ^ 1], sh, sl, ns);
         l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), sh, sl, ns);
@@ -688,8 +530,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
         for (int q = 0; q < QT; ++q) {
             const floatx16 am[1] = {m[q]}, as[1] = {sm[q]};
-            if constexpr (EB) l2_epilogue16b<1>(am, as, nv, t * TR, b1[q], i1[q], b2[q], i2[q], b3[q]);
-            else l2_epilogue16<1>(am, as, nv, t * TR, b1[q], i1[q], b2[q], i2[q], b3[q]);
+            l2_epilogue16<1>(am, as, nv, t * TR, b1[q], i1[q], b2[q], i2[q], b3[q]);
         }
         __syncthreads();
     }
@@ -715,138 +556,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
     }
 }
 
-// Register-blocked variant (round 4): each wave holds QT sets of 32 queries (VGPR-resident hi / lo B
-// fragments), so every A fragment read from LDS feeds 3 QT MFMAs instead of 3, and a block of WPB
-// waves serves 32 QT WPB queries from one staged train tile. Otherwise as mcv_l2_mfma16: two
-// accumulator sets in turn (a tile's MFMAs fill one while the previous tile's epilogue drains the
-// other), LDS double buffer fed two tiles ahead, XCD-aware chunk order.
-template <int DP, int WPB, int QT>
-__global__ __launch_bounds__(64 * WPB) void mcv_l2_mfma16x(const _Float16* __restrict__ qh, const _Float16* __restrict__ ql,
-                                                        const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
-                                                        const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk,
-                                                        int nqPad, L2Part* __restrict__ part,
-                                                        const unsigned* __restrict__ dom, bool xcdMap) {
-    constexpr int TR = 32;
-    if (!l2_f16_domain(dom)) return;   // grid-uniform: the f32 kernel takes this launch
-    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
-    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
-    constexpr int KB = DP / 16;
-    constexpr int ROWH = DP + 8;
-    constexpr int NT = 64 * WPB;
-    constexpr int PER = (TR * DP / 8 + NT - 1) / NT;
-    __shared__ __attribute__((aligned(16))) _Float16 lh[2][TR * ROWH];
-    __shared__ __attribute__((aligned(16))) _Float16 ll[2][TR * ROWH];
-    __shared__ __attribute__((aligned(16))) float lnorm[2][TR];
-
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int h = lane >> 5, col = lane & 31;
-    const int q0 = (bx * WPB + wave) * 32 * QT;
-    f16x8 bh[QT][KB], bl[QT][KB];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        const f16x8* rh = reinterpret_cast<const f16x8*>(qh + (size_t)(q0 + 32 * qt + col) * DP + 8 * h);
-        const f16x8* rl = reinterpret_cast<const f16x8*>(ql + (size_t)(q0 + 32 * qt + col) * DP + 8 * h);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            bh[qt][kb] = rh[2 * kb];
-            bl[qt][kb] = rl[2 * kb];
-        }
-    }
-    const int tBegin = by * tilesPerChunk;
-    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
-    float b1[QT], b2[QT], b3[QT];
-    int i1[QT], i2[QT];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        b1[qt] = b2[qt] = b3[qt] = INFINITY;
-        i1[qt] = i2[qt] = -1;
-    }
-    f16x8 sh0[PER], sl0[PER], sh1[PER], sl1[PER];
-    float ns0 = 0.f, ns1 = 0.f;
-    if (tBegin < tEnd) {
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, tBegin, sh0, sl0, ns0);
-        l2_lstore16<DP, TR, NT>(lh[0], ll[0], lnorm[0], sh0, sl0, ns0);
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(tBegin + 1, tEnd - 1), sh1, sl1, ns1);
-    }
-    __syncthreads();
-    floatx16 xm[QT], xs[QT], ym[QT], ys[QT];
-    float4 xn[1][4], yn[1][4];
-    int xt = tBegin, yt = tBegin;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) yn[0][j] = make_float4(INFINITY, INFINITY, INFINITY, INFINITY);
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) ym[qt][r] = ys[qt][r] = 0.f;
-    auto epi = [&](const floatx16 (&em)[QT], const floatx16 (&es)[QT], const float4 (&en)[1][4], int base, int r0,
-                   int rn) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const floatx16 a[1] = {em[qt]}, b[1] = {es[qt]};
-            if (rn == 16) l2_epilogue16<1>(a, b, en, base, b1[qt], i1[qt], b2[qt], i2[qt], b3[qt]);
-            else l2_epilogue16<1, 2>(a, b, en, base, b1[qt], i1[qt], b2[qt], i2[qt], b3[qt], r0);
-        }
-    };
-    auto tile = [&](int t, f16x8 (&ldh)[PER], f16x8 (&ldl)[PER], float& ldn, const f16x8 (&sth)[PER],
-                    const f16x8 (&stl)[PER], const float& stn, floatx16 (&cm)[QT], floatx16 (&cs)[QT],
-                    float4 (&cn)[1][4], int& ct, const floatx16 (&em)[QT], const floatx16 (&es)[QT],
-                    const float4 (&en)[1][4], int et) {
-        const int buf = (t - tBegin) & 1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cn[0][j] = *reinterpret_cast<const float4*>(&lnorm[buf][8 * j + 4 * h]);
-        ct = t;
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cm[qt][r] = cs[qt][r] = 0.f;
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(&lh[buf][col * ROWH + 16 * kb + 8 * h]);
-            const f16x8 al = *reinterpret_cast<const f16x8*>(&ll[buf][col * ROWH + 16 * kb + 8 * h]);
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) cm[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[qt][kb], cm[qt], 0, 0, 0);
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) cs[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[qt][kb], cs[qt], 0, 0, 0);
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt) cs[qt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[qt][kb], cs[qt], 0, 0, 0);
-            if constexpr (KB == 8) epi(em, es, en, et * TR, 2 * kb, 2);
-        }
-        if constexpr (KB != 8) epi(em, es, en, et * TR, 0, 16);
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), ldh, ldl, ldn);
-        l2_lstore16<DP, TR, NT>(lh[buf ^ 1], ll[buf ^ 1], lnorm[buf ^ 1], sth, stl, stn);
-        __syncthreads();
-    };
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the query fragments, once
-    for (int t = tBegin; t < tEnd; t += 2) {
-        tile(t, sh0, sl0, ns0, sh1, sl1, ns1, xm, xs, xn, xt, ym, ys, yn, yt);
-        if (t + 1 < tEnd) tile(t + 1, sh1, sl1, ns1, sh0, sl0, ns0, ym, ys, yn, yt, xm, xs, xn, xt);
-    }
-    if (tBegin < tEnd) {
-        if (((tEnd - tBegin) & 1) != 0) epi(xm, xs, xn, xt * TR, 0, 16);
-        else epi(ym, ys, yn, yt * TR, 0, 16);
-    }
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        if (i1[qt] >= 0) i1[qt] += 4 * h;
-        if (i2[qt] >= 0) i2[qt] += 4 * h;
-        const float ob1 = __shfl_xor(b1[qt], 32, 64), ob2 = __shfl_xor(b2[qt], 32, 64), ob3 = __shfl_xor(b3[qt], 32, 64);
-        const int oi1 = __shfl_xor(i1[qt], 32, 64), oi2 = __shfl_xor(i2[qt], 32, 64);
-        if (h == 0) {
-            float c1 = b1[qt], c2 = b2[qt], c3 = b3[qt];
-            third_fold(c1, c2, c3, ob1);
-            third_fold(c1, c2, c3, ob2);
-            third_fold(c1, c2, c3, ob3);
-            top2_push(b1[qt], i1[qt], b2[qt], i2[qt], ob1, oi1);
-            top2_push(b1[qt], i1[qt], b2[qt], i2[qt], ob2, oi2);
-            L2Part p;
-            p.b1 = b1[qt]; p.b2 = b2[qt]; p.b3 = c3; p.i1 = i1[qt]; p.i2 = i2[qt]; p.i3 = -1;
-            part[(size_t)by * nqPad + q0 + 32 * qt + col] = p;
-        }
-    }
-}
-
-// Exact squared distance (the oracle's definition: fp64 differences, sequential sum in dim order,
-// every operation rounded as written).
 __device__ __forceinline__ double l2_exact(const float* __restrict__ q, const float* __restrict__ t, int dim) {
     double d = 0;
     for (int k = 0; k < dim; ++k) {
@@ -1373,16 +1082,8 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     wk.fence.enter(s);
     const int DP = dim <= 32 ? 32 : dim <= 64 ? 64 : dim <= 128 ? 128 : 256;
     const int nqPad = (nq + 255) / 256 * 256;   // whole 128-query (f32) and 128 / 256-query (f16) blocks
-    static const int TRsel = [] {   // train rows per tile (variant screen: 32 or 64)
-        const char* e = getenv("MCV_L2_TR");
-        return e && atoi(e) == 64 ? 64 : 32;   // screened equal (scripts/sweep_l2.sh): keep one chain
-    }();
-    static const bool f16ok = [] {   // MCV_L2_F16 = 0: the f32 GEMM form only (screen)
-        const char* e = getenv("MCV_L2_F16");
-        return !(e && atoi(e) == 0);
-    }();
-    const bool f16 = f16ok && DP <= 128;   // the f16-split kernel tiles 32 train rows
-    const int TR = DP <= 128 && !f16 ? TRsel : 32;
+    const bool f16 = DP <= 128;   // the f16-split form (inside its domain: a device-side flag below)
+    constexpr int TR = 32;        // train rows per tile (f32 form: 32 / 64 screened equal, scripts/sweep_l2.sh)
     const int ntPad = nt > 0 ? (nt + TR - 1) / TR * TR : TR;
     const int ntTiles = ntPad / TR;
     wk.qp.ensure((size_t)nqPad * DP);
@@ -1430,19 +1131,13 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
                            wk.maxPart.p, wk.maxCount.p, wk.tmax.p, nullptr);
     const int qblocks = nqPad / 128;
     int nchunks = (2048 + qblocks - 1) / qblocks;
-    // f16 forms. The round-3 kernels: one train chunk per XCD (their block order). The default
-    // mcv_l2_mfma16q<D, 4, 1, 3> runs 3 blocks per CU, so a grid runs in "rounds" of 3 x CUs blocks and
+    // f16 form: mcv_l2_mfma16q<D, 4, 1, 3> runs 3 blocks per CU, so a grid runs in "rounds" of 3 x CUs blocks and
     // a round that is barely begun costs most of a block's time: the chunk count C minimises
     // ceil(qblocks C / (3 CUs)) (1 / C + 0.01) (the 0.01: a block's fixed cost against a whole-train
     // sweep) over C = 4 .. 24. Screened at cfg5's rank shares (scripts/gpu_r04_q.sh, 50k / N queries):
     // C = 15 took N = 1 / 2 / 4 / 8 to 1.98 / 1.12 / 0.58 / 0.35 ms against 2.14 / 1.21 / 0.74 / 0.40
     // with 8 and 2.01 / 1.16 / 0.65 / 0.44 with 16 (N = 8: 800 blocks, one past a round).
-    static const int form0 = [] {
-        const char* e = getenv("MCV_L2_FORM");
-        return e ? atoi(e) : 0;
-    }();
-    if (f16) nchunks = 8;
-    if (f16 && (form0 == 0 || form0 >= 4)) {
+    if (f16) {
         static const int cus = [] {
             int d = 0, n = 0;
             (void)hipGetDevice(&d);
@@ -1455,102 +1150,33 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
             if (cost < best - 1e-12) best = cost, nchunks = c;
         }
     }
-    static const int chunksEnv = [] {   // screen: MCV_L2_CHUNKS = the f16 form's train chunk count
-        const char* e = getenv("MCV_L2_CHUNKS");
-        return e ? atoi(e) : 0;
-    }();
-    if (f16 && chunksEnv > 0) nchunks = chunksEnv;
     if (nchunks > ntTiles) nchunks = ntTiles;
     if (nchunks < 1) nchunks = 1;
     const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
     nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
-    static const bool xcdOk = [] {   // MCV_XCD_MAP = 0: plain (query block, chunk) order (screen)
-        const char* e = getenv("MCV_XCD_MAP");
-        return e ? atoi(e) != 0 : true;
-    }();
-    const bool xcdMap = xcdOk && (8 % nchunks) == 0;
+    const bool xcdMap = (8 % nchunks) == 0;
     wk.part.ensure((size_t)nchunks * nqPad);
     dim3 grid(qblocks, nchunks);
     {
         ProfScope ps("l2_mfma", s);
 #define MCV_L2_LAUNCH(D, T) hipLaunchKernelGGL((mcv_l2_mfma<D, T>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, \
                                                ntTiles, tilesPerChunk, nqPad, wk.part.p, dom)
-        static const int wpb = [] {   // MCV_L2_FORM = 1: waves (32 queries each) per block, 8 or 4 (screen)
-            const char* e = getenv("MCV_L2_WPB");
-            return e && atoi(e) == 4 ? 4 : 8;
-        }();
-#define MCV_L2_LAUNCH16(D, W) hipLaunchKernelGGL((mcv_l2_mfma16<D, 32, W>), dim3(nqPad / (32 * W), nchunks), \
-                                                 dim3(64 * W), 0, s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, \
-                                                 tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
-        // f16 form (MCV_L2_FORM, screen): 0 (default) mcv_l2_mfma16q<D, 4, 1, 3>: 4 waves x 32 queries per
-        // block, one accumulator set, three waves per SIMD (1.98 vs 2.07 ms at cfg5); 1 the round-3
-        // mcv_l2_mfma16 (two accumulator sets in turn, MCV_L2_WPB); 2 mcv_l2_mfma16x (two query sets,
-        // one wave per SIMD: 2.98 ms); 3 mcv_l2_mfma16q<D, 4, 2, 2> (two query sets at two waves per
-        // SIMD: 2.17 ms). 8-wave blocks at three waves per SIMD measured 2.36 ms, four waves per SIMD
-        // (23 spilled VGPRs) 2.55 ms.
-        static const int form = [] {
-            const char* e = getenv("MCV_L2_FORM");
-            const int v = e ? atoi(e) : 0;
-            return v >= 0 && v <= 5 ? v : 0;
-        }();
-#define MCV_L2_LAUNCH16X(D) hipLaunchKernelGGL((mcv_l2_mfma16x<D, 4, 2>), dim3(nqPad / 256, nchunks), dim3(256), 0, s, \
-                                               wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, \
-                                               wk.part.p, dom, xcdMap)
-#define MCV_L2_LAUNCH16Q(D, W, Q, V, ...)                                                                          \
-    hipLaunchKernelGGL((mcv_l2_mfma16q<D, W, Q, V, ##__VA_ARGS__>), dim3(nqPad / (32 * W * Q), nchunks), dim3(64 * W), 0, \
-                       s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
-        // 4: form 0 with the per-score epilogue test (l2_epilogue16) instead of the per-tile min test
-        // (l2_epilogue16b, the default: 1.876-1.879 vs 1.886-1.891 ms at cfg5, alternating runs)
-        // 5: form 0 with s_setprio 1 around each tile's MFMA cluster (cdna_hip_programming.md T5): 1.95-1.96
-        // vs 1.88 ms, slower (a prioritised wave's MFMA cluster holds off the other waves' epilogues)
-        if (f16 && form == 5) {
+#define MCV_L2_LAUNCH16Q(D)                                                                                 \
+    hipLaunchKernelGGL((mcv_l2_mfma16q<D, 4, 1, 3>), dim3(nqPad / 128, nchunks), dim3(256), 0, s, wk.qh.p, wk.ql.p,   \
+                       wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
+        if (f16) {
             switch (DP) {
-                case 32: MCV_L2_LAUNCH16Q(32, 4, 1, 3, true, true); break;
-                case 64: MCV_L2_LAUNCH16Q(64, 4, 1, 3, true, true); break;
-                default: MCV_L2_LAUNCH16Q(128, 4, 1, 3, true, true); break;
-            }
-        } else if (f16 && form == 4) {
-            switch (DP) {
-                case 32: MCV_L2_LAUNCH16Q(32, 4, 1, 3, false); break;
-                case 64: MCV_L2_LAUNCH16Q(64, 4, 1, 3, false); break;
-                default: MCV_L2_LAUNCH16Q(128, 4, 1, 3, false); break;
-            }
-        } else if (f16 && form == 0) {
-            switch (DP) {
-                case 32: MCV_L2_LAUNCH16Q(32, 4, 1, 3, true); break;
-                case 64: MCV_L2_LAUNCH16Q(64, 4, 1, 3, true); break;
-                default: MCV_L2_LAUNCH16Q(128, 4, 1, 3, true); break;
-            }
-        } else if (f16 && form == 3) {
-            switch (DP) {
-                case 32: MCV_L2_LAUNCH16Q(32, 4, 2, 2); break;
-                case 64: MCV_L2_LAUNCH16Q(64, 4, 2, 2); break;
-                default: MCV_L2_LAUNCH16Q(128, 4, 2, 2); break;
-            }
-        } else if (f16 && form == 2) {
-            switch (DP) {
-                case 32: MCV_L2_LAUNCH16X(32); break;
-                case 64: MCV_L2_LAUNCH16X(64); break;
-                default: MCV_L2_LAUNCH16X(128); break;
-            }
-        } else if (f16) {
-            switch (DP * 10 + wpb) {
-                case 324: MCV_L2_LAUNCH16(32, 4); break;
-                case 328: MCV_L2_LAUNCH16(32, 8); break;
-                case 644: MCV_L2_LAUNCH16(64, 4); break;
-                case 648: MCV_L2_LAUNCH16(64, 8); break;
-                case 1284: MCV_L2_LAUNCH16(128, 4); break;
-                default: MCV_L2_LAUNCH16(128, 8); break;
+                case 32: MCV_L2_LAUNCH16Q(32); break;
+                case 64: MCV_L2_LAUNCH16Q(64); break;
+                default: MCV_L2_LAUNCH16Q(128); break;
             }
         }
-#undef MCV_L2_LAUNCH16
-#undef MCV_L2_LAUNCH16X
 #undef MCV_L2_LAUNCH16Q
         switch (DP) {
-            case 32: if (TR == 64) MCV_L2_LAUNCH(32, 64); else MCV_L2_LAUNCH(32, 32); break;
-            case 64: if (TR == 64) MCV_L2_LAUNCH(64, 64); else MCV_L2_LAUNCH(64, 32); break;
-            case 128: if (TR == 64) MCV_L2_LAUNCH(128, 64); else MCV_L2_LAUNCH(128, 32); break;
-            default: MCV_L2_LAUNCH(256, 32); break;
+            case 32: MCV_L2_LAUNCH(32, TR); break;
+            case 64: MCV_L2_LAUNCH(64, TR); break;
+            case 128: MCV_L2_LAUNCH(128, TR); break;
+            default: MCV_L2_LAUNCH(256, TR); break;
         }
 #undef MCV_L2_LAUNCH
     }
@@ -1561,19 +1187,11 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
                        wk.ambE2.p, dom);
     {
         ProfScope ps("l2_exact", s);
-        static const int scanBlocks = [] {   // exact-scan grid (screen: MCV_L2_SCAN_BLOCKS)
-            const char* e = getenv("MCV_L2_SCAN_BLOCKS");
-            const int v = e ? atoi(e) : kL2ScanBlocks;
-            return v >= 64 && v <= 8192 ? v : kL2ScanBlocks;
-        }();
+        constexpr int scanBlocks = kL2ScanBlocks;
         wk.scanPart.ensure((size_t)scanBlocks * kL2ScanQ);
-        static const bool scan16ok = [] {   // MCV_L2_SCAN16 = 0: the fp32-filter scan only (screen)
-            const char* e = getenv("MCV_L2_SCAN16");
-            return !(e && atoi(e) == 0);
-        }();
         // f16 domain: the MFMA-filtered scan (the VALU scan returns on the device flag); otherwise the
         // fp32-filter scan
-        const unsigned* dom16 = f16 && scan16ok ? dom : nullptr;
+        const unsigned* dom16 = f16 ? dom : nullptr;
         if (dom16) {
 #define MCV_L2_SCAN16(D)                                                                                        \
     hipLaunchKernelGGL(mcv_l2_scan16<D>, dim3(scanBlocks), dim3(256), 0, s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, \

@@ -78,13 +78,22 @@ extern "C" MCV_API int cvMatchL2(const float* q, const int nq, const float* t, c
     })
 }
 
-extern "C" MCV_API int mcvMatchHammingDevice(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc,
-                                             int* d_idx, int* d_dist, int* d_idx2, int* d_dist2, void* stream) {
+extern "C" MCV_API int mcvMatchHammingDeviceForm(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
+                                                 int bytesPerDesc, int* d_idx, int* d_dist, int* d_idx2, int* d_dist2,
+                                                 int form, void* stream) {
     MCV_GUARD(-1, {
         if (nq < 0 || nt < 0 || (nq > 0 && (!d_q || !d_idx || !d_dist))) fail("mcvMatchHammingDevice: bad argument");
+        if (form != kHammingFormGemm && form != kHammingFormPopcount)
+            fail("mcvMatchHammingDeviceForm: form %d is neither 0 (int8 GEMM) nor 1 (popcount)", form);
         return launch_match_hamming(d_q, nq, d_t, nt, bytesPerDesc, d_idx, d_dist, d_idx2, d_dist2,
-                                    (hipStream_t)stream);
+                                    (hipStream_t)stream, form);
     })
+}
+
+extern "C" MCV_API int mcvMatchHammingDevice(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc,
+                                             int* d_idx, int* d_dist, int* d_idx2, int* d_dist2, void* stream) {
+    return mcvMatchHammingDeviceForm(d_q, nq, d_t, nt, bytesPerDesc, d_idx, d_dist, d_idx2, d_dist2,
+                                     kHammingFormGemm, stream);
 }
 
 extern "C" MCV_API int mcvMatchL2Device(const float* d_q, int nq, const float* d_t, int nt, int dim, int* d_idx,

@@ -160,7 +160,6 @@ uint64_t cv_table_points_fp(int model, const float* h_pts4, int N);
 void cv_table_prepare(Plan& P, const void* d_pts, const float* h_pts4, int N, const RansacConfig& cfg, int64_t rows,
                       hipStream_t s);
 bool fused_error(const RansacConfig& cfg);
-bool h_sweep_scalar_only();
 RansacConfig config_or_default(const RansacConfig* cfg);
 int64_t ransac_search(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, hipStream_t s,
                       const float* h_pts4 = nullptr);

@@ -7,9 +7,7 @@
 //                       step over the group's lanes with the working matrices in LDS) -> all 10
 //                       slot statuses + models appended to a dense list (atomic slot allocation;
 //                       results are keyed by slot, so the order of the dense list never reaches an
-//                       output). mcv_e_stage + mcv_e_roots: the split form for large chunks.
-//   mcv_e_generate      the same, one lane per hypothesis running e_solve5 (MCV_E_GEN=1; kept for
-//                       the A/B screen).
+//                       output). mcv_e_stage + mcv_e_roots_g: the split form for large chunks.
 //   mcv_e_verify<K,P,E> inlier sweep over the dense model list: wave = K models in VGPRs, 64
 //                       lanes stream the double4 correspondences, fp64 Sampson error cast to
 //                       float, ballot + popcount; the count lands in the model's slot.
@@ -40,27 +38,6 @@ __global__ __launch_bounds__(256) void mcv_e_pack(const double2* __restrict__ a,
     o.z = (q.x - cx) / f;
     o.w = (q.y - cy) / f;
     out[i] = o;
-}
-
-__global__ __launch_bounds__(64) void mcv_e_generate(const double* __restrict__ pts4, int N, Sampler smp,
-                                                     int64_t hypBegin, int hypCount, EModel* __restrict__ dense,
-                                                     int* __restrict__ denseSlot, int* __restrict__ nDense,
-                                                     int* __restrict__ counts) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= hypCount) return;
-    double E[kEMaxModels][9];
-    const int n = e_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), E, nullptr);
-    const int m = n > 0 ? n : 0;
-    for (int s = 0; s < kEMaxModels; ++s)
-        counts[(int64_t)i * kEMaxModels + s] = s < m ? 0 : (s == 0 && n == kStatusNoSample ? kStatusNoSample : kStatusNoModel);
-    if (m == 0) return;
-    const int base = atomicAdd(nDense, m);
-    for (int s = 0; s < m; ++s) {
-        EModel em;
-        for (int k = 0; k < 9; ++k) em.e[k] = E[s][k];
-        dense[base + s] = em;
-        denseSlot[base + s] = i * kEMaxModels + s;
-    }
 }
 
 template <int G>
@@ -101,56 +78,7 @@ __global__ __launch_bounds__(64) void mcv_e_stage(const double* __restrict__ pts
     ew_stage_hypothesis(S[g.base / G], g, pts4, N, smp, (uint64_t)(hypBegin + i), st + i);
 }
 
-// Split path, part 2: one lane per hypothesis — real roots of det B(z) (e_poly_real_roots, root
-// lists in LDS columns), one model per root, statuses + dense append (one atomic per wave).
-__global__ __launch_bounds__(64) void mcv_e_roots(const EStage* __restrict__ st, int hypCount,
-                                                  EModel* __restrict__ dense, int* __restrict__ denseSlot,
-                                                  int* __restrict__ nDense, int* __restrict__ counts) {
-    __shared__ double Lc[11][64];
-    __shared__ double Lr[2][10][64];
-    const int lane = threadIdx.x;
-    const int i = blockIdx.x * 64 + lane;
-    const bool act = i < hypCount;
-    const EStage* h = st + (act ? i : 0);
-    const int status = act ? h->status : 0;
-    int nr = 0, which = 0;
-    if (status == 1) nr = ew_lane_roots(h->det, Lc, Lr, lane, &which);
-    uint32_t okm = 0;
-    int m = 0;
-    for (int r = 0; r < nr; ++r) {
-        double E[9];
-        if (e_model_at(h->bx, h->by, h->bc, h->nb[0], h->nb[1], h->nb[2], h->nb[3], Lr[which][r][lane], E)) {
-            okm |= 1u << r;
-            ++m;
-        }
-    }
-    if (act)
-        for (int s = 0; s < kEMaxModels; ++s)
-            counts[(int64_t)i * kEMaxModels + s] =
-                s < m ? 0 : (s == 0 && status == kStatusNoSample ? kStatusNoSample : kStatusNoModel);
-    // wave-exclusive scan of m -> one atomic per wave
-    int incl = m;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
-        incl += lane >= o ? y : 0;
-    }
-    const int total = __shfl(incl, 63);
-    int base = 0;
-    if (lane == 63 && total > 0) base = atomicAdd(nDense, total);
-    base = __shfl(base, 63) + incl - m;
-    int t = 0;
-    for (int r = 0; r < nr; ++r) {
-        if (!((okm >> r) & 1u)) continue;
-        EModel em;
-        (void)e_model_at(h->bx, h->by, h->bc, h->nb[0], h->nb[1], h->nb[2], h->nb[3], Lr[which][r][lane], em.e);
-        dense[base + t] = em;
-        denseSlot[base + t] = i * kEMaxModels + t;
-        ++t;
-    }
-}
-
-// Split path, part 2 (default): GR lanes per hypothesis — the derivative levels' intervals dealt
+// Split path, part 2: GR lanes per hypothesis — the derivative levels' intervals dealt
 // over the group (ew_group_roots), models by root over the group's lanes, statuses + dense append.
 template <int GR>
 __global__ __launch_bounds__(64) void mcv_e_roots_g(const EStage* __restrict__ st, int hypCount,
@@ -409,61 +337,19 @@ void launch_e_pack(const double* d_ab, int N, double f, double cx, double cy, do
 
 void launch_e_generate(const double* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_dense,
                        int* d_denseSlot, int* d_nDense, int* d_counts, void* d_stage, hipStream_t s) {
-    // MCV_E_GEN: lanes per hypothesis of the five-point solve (16 / 32 / 64; 1 = the one-lane
-    // e_solve5 kernel), for the A/B screen only
-    static const int group = [] {
-        const char* e = getenv("MCV_E_GEN");
-        return e ? atoi(e) : kEGenLanes;
-    }();
     (void)hipMemsetAsync(d_nDense, 0, sizeof(int), s);
     if (hypCount <= 0) return;
-    if (d_stage && group == kEGenLanes) {   // many hypotheses: matrix phases per group, roots per lane
+    static_assert(kEGenLanes == 16 && kEStageLanes == 16 && kERootLanes == 4, "launch shapes below");
+    if (d_stage) {   // many hypotheses: matrix phases per 16-lane group, roots per 4-lane group
         EStage* st = (EStage*)d_stage;
-        static const int stageLanes = [] {
-            const char* e = getenv("MCV_E_STAGE");   // 8 / 16 / 32 lanes per hypothesis (screen)
-            return e ? atoi(e) : kEStageLanes;
-        }();
-        if (stageLanes == 8)
-            hipLaunchKernelGGL(mcv_e_stage<8>, dim3((hypCount + 7) / 8), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
-                               hypCount, st);
-        else if (stageLanes == 32)
-            hipLaunchKernelGGL(mcv_e_stage<32>, dim3((hypCount + 1) / 2), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
-                               hypCount, st);
-        else
-            hipLaunchKernelGGL(mcv_e_stage<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
-                               hypCount, st);
-        static const int rootLanes = [] {
-            const char* e = getenv("MCV_E_ROOTS");
-            return e ? atoi(e) : kERootLanes;
-        }();
-        if (rootLanes == 1)
-            hipLaunchKernelGGL(mcv_e_roots, dim3((hypCount + 63) / 64), dim3(64), 0, s, st, hypCount,
-                               (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
-        else if (rootLanes == 8)
-            hipLaunchKernelGGL(mcv_e_roots_g<8>, dim3((hypCount + 7) / 8), dim3(64), 0, s, st, hypCount,
-                               (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
-        else
-            hipLaunchKernelGGL(mcv_e_roots_g<4>, dim3((hypCount + 15) / 16), dim3(64), 0, s, st, hypCount,
-                               (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
+        hipLaunchKernelGGL(mcv_e_stage<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
+                           hypCount, st);
+        hipLaunchKernelGGL(mcv_e_roots_g<4>, dim3((hypCount + 15) / 16), dim3(64), 0, s, st, hypCount,
+                           (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
         return;
     }
-    switch (group) {
-        case 1:
-            hipLaunchKernelGGL(mcv_e_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
-                               hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
-            break;
-        case 64:
-            hipLaunchKernelGGL(mcv_e_generate_wave<64>, dim3(hypCount), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
-                               hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
-            break;
-        case 32:
-            hipLaunchKernelGGL(mcv_e_generate_wave<32>, dim3((hypCount + 1) / 2), dim3(64), 0, s, d_pts4, N, smp,
-                               hypBegin, hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
-            break;
-        default:
-            hipLaunchKernelGGL(mcv_e_generate_wave<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, smp,
-                               hypBegin, hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
-    }
+    hipLaunchKernelGGL(mcv_e_generate_wave<16>, dim3((hypCount + 3) / 4), dim3(64), 0, s, d_pts4, N, smp, hypBegin,
+                       hypCount, (EModel*)d_dense, d_denseSlot, d_nDense, d_counts);
 }
 
 template <int K, int P>
@@ -479,71 +365,39 @@ static void launch_e_verify_kp(const double4* p, int N, const EModel* m, const i
                            d_counts, thr2, lo, hi);
 }
 
-// Sweep shape (models per wave K, correspondences per lane per trip P); MCV_E_VARIANT selects
-// alternatives for the variant screen (scripts/sweep_e_variants.sh) only.
+// Certified sweep shape: KP model pairs per wave, P correspondences per lane per trip.
 template <int KP, int P>
 static void launch_e_verify_pk_kp(const float4* p32, const double4* p, int N, const EModel* m, const int* d_denseSlot,
                                   const int* d_nDense, int maxModels, int* d_counts, float thr2, int kind,
                                   const SampsonPkCut& cut, const double* d_bb, hipStream_t s) {
     const int blocks = ((maxModels + 2 * KP - 1) / (2 * KP) + 3) / 4;
-    // point chunks of at least MCV_E_CHUNK (default 50000) correspondences (screen at N = 100k: one chunk
+    // point chunks of at least 50000 correspondences (screen at N = 100k: one chunk
     // 12.16 ms, 16384-point chunks 12.25, 32768 12.04, 50000 11.92). At 2^20 hypotheses one chunk writes
     // 62 instead of 284 MB of partial counts per launch but streams the whole 4.8 MB point set through
     // each XCD's 4 MB L2 (24.8 GB of fetches per launch against 0.7 GB; the same 223 ms a step): kept at two.
-    static const int minChunk = [] {
-        const char* e = getenv("MCV_E_CHUNK");
-        const int v = e ? atoi(e) : 50000;
-        return v > 0 ? v : (1 << 30);
-    }();
+    constexpr int minChunk = 50000;
     const int step = 64 * P;
     int chunks = std::max(1, N / minChunk);
     int chunk = (N + chunks - 1) / chunks;
     chunk = (chunk + step - 1) / step * step;
     chunks = std::max(1, (N + chunk - 1) / chunk);
-    static const bool xcd = [] {
-        const char* e = getenv("MCV_XCD_MAP");
-        return e ? atoi(e) != 0 : true;
-    }();
     hipLaunchKernelGGL((mcv_e_verify_pk<KP, P>), dim3(blocks, chunks), dim3(256), 0, s, p32, p, N, chunk,
-                       xcd && (8 % chunks) == 0, m, d_denseSlot, d_nDense, d_counts, thr2, kind, cut, d_bb);
+                       (8 % chunks) == 0, m, d_denseSlot, d_nDense, d_counts, thr2, kind, cut, d_bb);
 }
 
 void launch_e_verify(const double* d_pts4, int N, const void* d_dense, const int* d_denseSlot, const int* d_nDense,
                      int maxModels, int* d_counts, float thr2, int kind, hipStream_t s, const float* d_pts32,
                      const double* d_bb) {
-    static const int pkv = [] {
-        const char* e = getenv("MCV_E_PK");
-        return e ? atoi(e) : 0;
-    }();
-    if (d_pts32 && d_bb && pkv != 9) {   // certified packed-fp32 prefilter
-        const SampsonPkCut cut = sampson_pk_cut_host(sampson_cut(thr2));
-        const float4* p32 = (const float4*)d_pts32;
-        const double4* p = (const double4*)d_pts4;
-        const EModel* m = (const EModel*)d_dense;
-        switch (pkv) {
-            case 1: launch_e_verify_pk_kp<2, 2>(p32, p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, cut, d_bb, s); return;
-            case 2: launch_e_verify_pk_kp<4, 1>(p32, p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, cut, d_bb, s); return;
-            case 3: launch_e_verify_pk_kp<2, 1>(p32, p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, cut, d_bb, s); return;
-            default: launch_e_verify_pk_kp<3, 2>(p32, p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, cut, d_bb, s); return;
-        }
+    if (d_pts32 && d_bb) {   // certified packed-fp32 prefilter, 3 model pairs per wave
+        launch_e_verify_pk_kp<3, 2>((const float4*)d_pts32, (const double4*)d_pts4, N, (const EModel*)d_dense,
+                                    d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind,
+                                    sampson_pk_cut_host(sampson_cut(thr2)), d_bb, s);
+        return;
     }
-    static const int variant = [] {
-        const char* e = getenv("MCV_E_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    const double4* p = (const double4*)d_pts4;
-    const EModel* m = (const EModel*)d_dense;
     const SampsonCut c = sampson_cut(thr2);
-    switch (variant) {
-        case 1: launch_e_verify_kp<4, 1>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
-        case 2: launch_e_verify_kp<6, 1>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
-        case 3: launch_e_verify_kp<2, 2>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
-        case 4: launch_e_verify_kp<6, 2>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
-        case 5: launch_e_verify_kp<8, 1>(p, N, m, d_denseSlot, d_nDense, maxModels, d_counts, thr2, kind, c.lo, c.hi, s); break;
-        default:
-            launch_e_verify_kp<kVerifyEModelsPerWave, kVerifyEPtsPerLane>(p, N, m, d_denseSlot, d_nDense, maxModels,
-                                                                          d_counts, thr2, kind, c.lo, c.hi, s);
-    }
+    launch_e_verify_kp<kVerifyEModelsPerWave, kVerifyEPtsPerLane>((const double4*)d_pts4, N, (const EModel*)d_dense,
+                                                                  d_denseSlot, d_nDense, maxModels, d_counts, thr2,
+                                                                  kind, c.lo, c.hi, s);
 }
 
 void launch_e_fetch(const void* d_dense, const int* d_denseSlot, const int* d_nDense, int maxModels, int slot,

@@ -26,7 +26,7 @@ namespace mcv {
 
 // One lane per hypothesis; run8Point's eigen-solve working set in LDS, one column per lane.
 // FAST = MCV_FLAG_FAST_MINIMAL (no workspace).
-template <bool FAST, int L = kEigLanes, bool SOA = false>
+template <bool FAST, int L = kEigLanes>
 __global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __restrict__ pts4, int N, Sampler smp,
                                                      int64_t hypBegin, int hypCount, FModelD* __restrict__ models,
                                                      int* __restrict__ counts) {
@@ -39,13 +39,8 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_f_generate(const float* __
         st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
-        if constexpr (SOA) {
-            EigWsSoA ws = eig_ws_soa<L>(lds, threadIdx.x);
-            st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
-        } else {
-            EigWsLane ws{lds + threadIdx.x * kEigWs};
-            st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
-        }
+        EigWsLane ws{lds + threadIdx.x * kEigWs};
+        st = f_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), m.f, nullptr, ws);
     }
     if (st == 1) {
         models[i] = m;
@@ -339,26 +334,9 @@ void launch_f_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin
     if (fast)
         hipLaunchKernelGGL(mcv_f_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, smp, hypBegin,
                            hypCount, (FModelD*)d_models, d_counts);
-    else {
-        // lanes per block and workspace layout: MCV_EIG_LANES / MCV_EIG_SOA screens (jacobi_eig.h)
-#define MCV_F_GENERATE(LL, SO)                                                                                    \
-    hipLaunchKernelGGL((mcv_f_generate<false, LL, SO>), dim3((hypCount + LL - 1) / LL), dim3(LL), 0, s, d_pts4, N, smp, hypBegin, hypCount, (FModelD*)d_models, d_counts)
-        const int L = eig_lanes();
-        if (eig_soa()) {
-            if (L == 48) MCV_F_GENERATE(48, true);
-            else if (L == 64) MCV_F_GENERATE(64, true);
-            else MCV_F_GENERATE(40, true);
-        } else {
-            switch (L) {
-                case 64: MCV_F_GENERATE(64, false); break;
-                case 48: MCV_F_GENERATE(48, false); break;
-                case 32: MCV_F_GENERATE(32, false); break;
-                case 39: MCV_F_GENERATE(39, false); break;
-                default: MCV_F_GENERATE(kEigLanes, false);
-            }
-        }
-#undef MCV_F_GENERATE
-    }
+    else   // kEigLanes per block: LDS-bound occupancy, one wave per SIMD (jacobi_eig.h)
+        hipLaunchKernelGGL((mcv_f_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
+                           dim3(kEigLanes), 0, s, d_pts4, N, smp, hypBegin, hypCount, (FModelD*)d_models, d_counts);
 }
 
 void launch_f_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, FOneOut* d_out, hipStream_t s, bool fast) {
@@ -375,15 +353,6 @@ static void launch_f_verify_kp(const float4* p, int N, const FModelD* m, int* d_
         case 2: hipLaunchKernelGGL((mcv_f_verify<K, P, 2>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, lo, hi); break;
         default: hipLaunchKernelGGL((mcv_f_verify<K, P, 3>), dim3(blocks), dim3(256), 0, s, p, N, m, d_counts, hypCount, thr2, lo, hi); break;
     }
-}
-
-// Sweep shape; MCV_F_VARIANT selects alternatives for tuning experiments only.
-static int f_variant() {
-    static int v = [] {
-        const char* e = getenv("MCV_F_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
 }
 
 void launch_abs_bound4(const void* d_pts4, bool fp64, int N, double* d_bb, float* d_out32, hipStream_t s) {
@@ -405,10 +374,7 @@ static void launch_f_verify_pk_kp(const float4* p, int N, const FModelD* m, int*
     const int blocks = (waves + 3) / 4;
     // point chunks: about 64 waves per SIMD in total (the last round is a small share), chunks
     // of at least 8192 points (the per-wave model setup stays small against the sweep)
-    static const int target = [] {
-        const char* e = getenv("MCV_F_WAVES");
-        return e ? atoi(e) : 65536;
-    }();
+    constexpr int target = 65536;
     const int step = 64 * P;
     int chunks = (target + waves - 1) / waves;
     // and at least enough chunks (a power of two <= 8, one per XCD group) that an XCD's slice of the
@@ -422,12 +388,8 @@ static void launch_f_verify_pk_kp(const float4* p, int N, const FModelD* m, int*
     int chunk = (N + chunks - 1) / chunks;
     chunk = (chunk + step - 1) / step * step;
     chunks = std::max(1, (N + chunk - 1) / chunk);
-    static const bool xcd = [] {
-        const char* e = getenv("MCV_XCD_MAP");
-        return e ? atoi(e) != 0 : true;
-    }();
     hipLaunchKernelGGL((mcv_f_verify_pk<KP, P>), dim3(blocks, chunks), dim3(256), 0, s, p, N, chunk,
-                       xcd && (8 % chunks) == 0, m, d_counts, hypCount, thr2, kind, cut, d_bb);
+                       (8 % chunks) == 0, m, d_counts, hypCount, thr2, kind, cut, d_bb);
 }
 
 void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
@@ -435,33 +397,11 @@ void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_co
     const float4* p = (const float4*)d_pts4;
     const FModelD* m = (const FModelD*)d_models;
     const SampsonCut c = sampson_cut(thr2);
-    if (d_bb && kind <= 1 && f_variant() == 0) {   // Sampson: certified packed-fp32 prefilter
-        const SampsonPkCut cut = sampson_pk_cut_host(c);
-        static const int pkv = [] {
-            const char* e = getenv("MCV_F_PK");
-            return e ? atoi(e) : 0;
-        }();
-        switch (pkv) {
-            case 1: launch_f_verify_pk_kp<2, 2>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
-            case 2: launch_f_verify_pk_kp<3, 2>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
-            case 3: launch_f_verify_pk_kp<4, 2>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
-            case 4: launch_f_verify_pk_kp<3, 1>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
-            case 9: break;   // fp64 sweep
-            default: launch_f_verify_pk_kp<4, 1>(p, N, m, d_counts, hypCount, thr2, kind, cut, d_bb, s); return;
-        }
+    if (d_bb && kind <= 1) {   // Sampson: certified packed-fp32 prefilter, 4 model pairs per wave
+        launch_f_verify_pk_kp<4, 1>(p, N, m, d_counts, hypCount, thr2, kind, sampson_pk_cut_host(c), d_bb, s);
+        return;
     }
-    switch (f_variant()) {
-        case 1: launch_f_verify_kp<4, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
-        case 2: launch_f_verify_kp<6, 1>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
-        case 3: launch_f_verify_kp<6, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
-        case 4: launch_f_verify_kp<8, 1>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
-        case 5: launch_f_verify_kp<2, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
-        case 6: launch_f_verify_kp<3, 2>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
-        case 7: launch_f_verify_kp<2, 4>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s); break;
-        default:
-            launch_f_verify_kp<kVerifyFHypPerWave, kVerifyFPtsPerLane>(p, N, m, d_counts, hypCount, thr2, kind, c.lo,
-                                                                       c.hi, s);
-    }
+    launch_f_verify_kp<kVerifyFHypPerWave, kVerifyFPtsPerLane>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s);
 }
 
 void launch_f_mask(const float* d_pts4, int N, const double* F9, float thr2, int kind, uint8_t* d_mask, int* d_count,

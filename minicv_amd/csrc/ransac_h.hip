@@ -29,7 +29,7 @@ namespace mcv {
 // One lane per hypothesis; the runKernel eigen-solve's working set (127 doubles) in LDS, one slice
 // per lane (jacobi_eig.h): 40.6 KB per 40-lane block, 4 blocks per CU. FAST = MCV_FLAG_FAST_MINIMAL
 // (no workspace).
-template <bool FAST, int L = kEigLanes, bool SOA = false>
+template <bool FAST, int L = kEigLanes>
 __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __restrict__ pts4, int N, Sampler smp,
                                                      int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
                                                      double* __restrict__ h64, int* __restrict__ counts) {
@@ -43,13 +43,8 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
         st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, unused, true);
     } else {
         __shared__ double lds[kEigWs * L];
-        if constexpr (SOA) {
-            EigWsSoA ws = eig_ws_soa<L>(lds, threadIdx.x);
-            st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
-        } else {
-            EigWsLane ws{lds + threadIdx.x * kEigWs};
-            st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
-        }
+        EigWsLane ws{lds + threadIdx.x * kEigWs};
+        st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
     }
     if (st == 1) {
         models[i] = mf;
@@ -57,33 +52,6 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
         counts[i] = 0;
     } else {
         // the zero model (w = 1 everywhere) keeps the packed sweep's slot well-defined
-        for (int j = 0; j < 8; ++j) mf.h[j] = 0.f;
-        models[i] = mf;
-        counts[i] = st;
-    }
-}
-
-// Four lanes per hypothesis (jacobi_eig.h's EigWsQuad): HB hypotheses per block, one 127-double slice
-// each; the quad runs the sample search and the DLT redundantly (same values in all four lanes) and
-// splits the eigen-solve's element work; lane 0 of the quad writes the outputs.
-template <int HB>
-__global__ __launch_bounds__(4 * HB) void mcv_h_generate_q4(const float* __restrict__ pts4, int N, Sampler smp,
-                                                          int64_t hypBegin, int hypCount, HModelF* __restrict__ models,
-                                                          double* __restrict__ h64, int* __restrict__ counts) {
-    const int hl = threadIdx.x >> 2;
-    const int i = blockIdx.x * HB + hl;
-    if (i >= hypCount) return;   // whole quads
-    __shared__ double lds[kEigWs * HB];
-    EigWsQuad ws{lds + hl * kEigWs, (int)(threadIdx.x & 3)};
-    double H[9];
-    HModelF mf;
-    const int st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
-    if (ws.sub != 0) return;
-    if (st == 1) {
-        models[i] = mf;
-        for (int j = 0; j < 9; ++j) h64[9 * (int64_t)i + j] = H[j];
-        counts[i] = 0;
-    } else {
         for (int j = 0; j < 8; ++j) mf.h[j] = 0.f;
         models[i] = mf;
         counts[i] = st;
@@ -427,7 +395,7 @@ __global__ __launch_bounds__(256) void mcv_h_verify_pk(const HPair* __restrict__
 // ------------------------------------------------------------------------------------------
 // Band parameter: relative half-width ~ t + O(u) around thr2 w^2, absolute part ~ (7.5 u G)^2 / t.
 // One t for every model keeps the slopes launch constants.
-static constexpr double kCertT = 0x1p-11;   // default band parameter (MCV_HCERT_T overrides: screens)
+static constexpr double kCertT = 0x1p-11;   // band parameter (screened 2^-12 / 2^-11 / 2^-10: DESIGN.md §7)
 static constexpr double kCertSlop = 0x1p-18;   // covers the O(u) factors (< 16 u = 2^-20 in total)
 
 struct HCertSlopes {
@@ -435,17 +403,8 @@ struct HCertSlopes {
     double t;   // band parameter the per-model offsets use
 };
 
-static double cert_t() {
-    static const double t = [] {
-        const char* e = getenv("MCV_HCERT_T");
-        const double v = e ? atof(e) : 0.0;
-        return v > 0x1p-20 && v < 0x1p-4 ? v : kCertT;
-    }();
-    return t;
-}
-
 HCertSlopes h_cert_slopes_host(float thr2) {
-    const double T = (double)thr2, t = cert_t(), u = 0x1p-24;
+    const double T = (double)thr2, t = kCertT, u = 0x1p-24;
     // inlier cut: |a_in| <= T (1-t)/(1+t) (1 - slop), rounded towards zero
     const double ain = -T * (1.0 - t) / (1.0 + t) * (1.0 - kCertSlop);
     float fi = (float)ain;
@@ -510,35 +469,14 @@ __device__ __forceinline__ void h_cert_values(f2 p0, f2 p1, f2 p2, f2 p3, f2 c, 
     X = pk_fma(W2, hi(a), hi(b));
 }
 
-// Lane masks from the certified values, C++ form (tail trips and the resolve pass): inliers and
-// undecided lanes per half. The sweep's asm form (h_cert_masks_asm) computes the same predicates.
+// Lane masks from the certified values: inliers and
+// undecided lanes per half.
 __device__ __forceinline__ void h_cert_masks(f2 I, f2 X, uint64_t& inx, uint64_t& iny, uint64_t& ux,
                                              uint64_t& uy) {
     inx = __builtin_amdgcn_ballot_w64(I.x < 0.0f);
     iny = __builtin_amdgcn_ballot_w64(I.y < 0.0f);
     ux = __builtin_amdgcn_ballot_w64(__float_as_uint(I.x) <= __float_as_uint(X.x));
     uy = __builtin_amdgcn_ballot_w64(__float_as_uint(I.y) <= __float_as_uint(X.y));
-}
-
-// The same four compares as VOPC e32 (2-cycle issue; the compiler picks the 4-cycle VOP3 form when
-// several lane masks are live at once). Wait states: the leading s_nop 0 covers a packed-op result
-// read right at the statement's start (the compiler places 1 state between dependent packed ops);
-// SALU reads of VCC after a VALU write need none.
-__device__ __forceinline__ void h_cert_masks_asm(f2 I, f2 X, uint64_t& inx, uint64_t& iny, uint64_t& ux,
-                                                 uint64_t& uy) {
-    asm volatile(
-        "s_nop 0\n\t"
-        "v_cmp_gt_f32_e32 vcc, 0, %4\n\t"
-        "s_mov_b64 %0, vcc\n\t"
-        "v_cmp_gt_f32_e32 vcc, 0, %5\n\t"
-        "s_mov_b64 %1, vcc\n\t"
-        "v_cmp_le_u32_e32 vcc, %4, %6\n\t"
-        "s_mov_b64 %2, vcc\n\t"
-        "v_cmp_le_u32_e32 vcc, %5, %7\n\t"
-        "s_mov_b64 %3, vcc"
-        : "=&s"(inx), "=&s"(iny), "=&s"(ux), "=&s"(uy)
-        : "v"(I.x), "v"(I.y), "v"(X.x), "v"(X.y)
-        : "vcc");
 }
 
 // h_error of both correspondences of a pair, packed, operation for operation (every product and sum
@@ -556,7 +494,7 @@ __device__ __forceinline__ f2 h_error_pk(f2 p0, f2 p1, f2 p2, f2 p3, const HPair
 // One trip: NP pairs per lane against the wave's K models. vx / vy: lanes whose first / second
 // correspondence of pair slot j exists (tail trip only). Returns the mask of models with an
 // undecided lane in this trip (bit k); their certified counts are already in cnt.
-template <int K, int NP, bool PRED, bool ASMCMP = false>
+template <int K, int NP, bool PRED>
 __device__ __forceinline__ uint32_t h_cert_trip(f2 (&hp)[K][4], const f2 (&hc)[K], f2 a, const f2 (&cb)[K],
                                                 const HPair (&q)[NP], const uint64_t (&vx)[NP],
                                                 const uint64_t (&vy)[NP], f2 one, uint32_t (&cnt)[K]) {
@@ -578,8 +516,7 @@ __device__ __forceinline__ uint32_t h_cert_trip(f2 (&hp)[K][4], const f2 (&hc)[K
                 iny &= vy[j];
                 und |= (ux & vx[j]) | (uy & vy[j]);
             } else {
-                if constexpr (ASMCMP) h_cert_masks_asm(I, X, inx, iny, ux, uy);
-                else h_cert_masks(I, X, inx, iny, ux, uy);
+                h_cert_masks(I, X, inx, iny, ux, uy);
                 und |= ux | uy;
             }
             cnt[k] += (uint32_t)__popcll(inx) + (uint32_t)__popcll(iny);
@@ -589,44 +526,8 @@ __device__ __forceinline__ uint32_t h_cert_trip(f2 (&hp)[K][4], const f2 (&hc)[K
     return undecided;
 }
 
-// The exact op-by-op error for the undecided lanes of the models in `und`, on the trip's pairs still
-// in registers: a rolled loop over the models, each re-read through the scalar cache with its
-// offsets from LDS, so that this rare path adds little register pressure to the sweep.
-template <int K, int NP, bool PRED>
-__device__ __forceinline__ void h_cert_fix(uint32_t und, const HModelF* __restrict__ models, int h0, int hypCount,
-                                           const f2* __restrict__ offs, f2 a, const HPair (&q)[NP],
-                                           const uint64_t (&vx)[NP], const uint64_t (&vy)[NP], float thr2, f2 one,
-                                           uint32_t (&cnt)[K]) {
-#pragma unroll 1
-    for (int k = 0; k < K; ++k) {
-        if (!(und & (1u << k))) continue;
-        const int hk = h0 + k < hypCount ? h0 + k : hypCount - 1;
-        const f2* mp = (const f2*)&models[hk];
-        const f2 m0 = mp[0], m1 = mp[1], m2 = mp[2], m3 = mp[3];
-        const f2 b = offs[k];
-        uint32_t add = 0;
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            f2 I, X;
-            h_cert_values(m0, m1, m2, m3, f2{m1.x, m2.y}, a, b, q[j], one, I, X);
-            uint64_t inx, iny, ux, uy;
-            h_cert_masks(I, X, inx, iny, ux, uy);
-            if constexpr (PRED) {
-                ux &= vx[j];
-                uy &= vy[j];
-            }
-            if ((ux | uy) == 0) continue;
-            const f2 e = h_error_pk(m0, m1, m2, m3, q[j]);
-            const uint64_t me = 1ull << (__lane_id() & 63);
-            add += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64((ux & me) != 0 && e.x <= thr2)) +
-                   (uint32_t)__popcll(__builtin_amdgcn_ballot_w64((uy & me) != 0 && e.y <= thr2));
-        }
-#pragma unroll
-        for (int kk = 0; kk < K; ++kk) cnt[kk] += (kk == k) ? add : 0u;   // no dynamic register indexing
-    }
-}
-
-// The same with the models still in registers (compile-time model index; the branch per model is
+// The exact op-by-op error for the undecided lanes of the models in `und`, with the models still in
+// registers (compile-time model index; the branch per model is
 // wave-uniform and rarely taken).
 template <int K, int NP, bool PRED>
 __device__ __forceinline__ void h_cert_fix_regs(uint32_t und, const f2 (&hp)[K][4], const f2 (&hc)[K], f2 a,
@@ -692,7 +593,7 @@ __device__ __noinline__ uint32_t h_cert_resolve(const HPair* __restrict__ pairs,
 // nComplete = N / 2 pairs hold two correspondences; pair nComplete (odd N) holds one.
 static constexpr int kCertEvents = 256;   // per wave
 
-template <int K, int NP, int FIX, bool ASMCMP>
+template <int K, int NP>
 __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict__ pairs, int nPairs, int nComplete,
                                                          const HModelF* __restrict__ models, int* __restrict__ counts,
                                                          int hypCount, float thr2, HCertSlopes slopes,
@@ -747,18 +648,9 @@ __global__ __launch_bounds__(256) void mcv_h_verify_cert(const HPair* __restrict
             HPair q[NP];
 #pragma unroll
             for (int j = 0; j < NP; ++j) q[j] = pairs[base + 64 * j + lane];
-            const uint32_t und = h_cert_trip<K, NP, false, ASMCMP>(hp, hc, slopes.a, cb, q, all, all, one, cnt);
-            if (FIX >= 0 && __builtin_expect(und != 0, 0)) {   // FIX < 0: timing diagnostics only
-                if constexpr (FIX == 2) {
-                    h_cert_fix_regs<K, NP, false>(und, hp, hc, slopes.a, cb, q, all, all, thr2, one, cnt);
-                } else if constexpr (FIX == 1) {
-                    h_cert_fix<K, NP, false>(und, models, h0, hypCount, offsets[wib], slopes.a, q, all, all, thr2,
-                                             one, cnt);
-                } else {
-                    if (nev < kCertEvents && lane == 0) events[wib][nev] = ((uint32_t)(base / TRIP) << 8) | und;
-                    ++nev;
-                }
-            }
+            const uint32_t und = h_cert_trip<K, NP, false>(hp, hc, slopes.a, cb, q, all, all, one, cnt);
+            if (__builtin_expect(und != 0, 0))
+                h_cert_fix_regs<K, NP, false>(und, hp, hc, slopes.a, cb, q, all, all, thr2, one, cnt);
         }
         for (int base = nFull; base < nPairs; base += TRIP) {
             HPair q[NP];
@@ -1051,39 +943,10 @@ void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin
     if (fast)
         hipLaunchKernelGGL(mcv_h_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, smp, hypBegin,
                            hypCount, (HModelF*)d_models, d_h64, d_counts);
-    else {
-        // lanes per block and workspace layout: MCV_EIG_LANES / MCV_EIG_SOA screens (jacobi_eig.h)
-#define MCV_H_GENERATE(LL, SO)                                                                                    \
-    hipLaunchKernelGGL((mcv_h_generate<false, LL, SO>), dim3((hypCount + LL - 1) / LL), dim3(LL), 0, s, d_pts4, N, smp, hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts)
-        const int L = eig_lanes();
-        static const int q4 = [] {   // MCV_EIG_Q4 = hypotheses per block of the four-lane form (screen)
-            const char* e = getenv("MCV_EIG_Q4");
-            return e ? atoi(e) : 0;
-        }();
-        if (q4 == 32)
-            hipLaunchKernelGGL(mcv_h_generate_q4<32>, dim3((hypCount + 31) / 32), dim3(128), 0, s, d_pts4, N, smp,
-                               hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
-        else if (q4 == 40)
-            hipLaunchKernelGGL(mcv_h_generate_q4<40>, dim3((hypCount + 39) / 40), dim3(160), 0, s, d_pts4, N, smp,
-                               hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
-        else if (q4 == 64)
-            hipLaunchKernelGGL(mcv_h_generate_q4<64>, dim3((hypCount + 63) / 64), dim3(256), 0, s, d_pts4, N, smp,
-                               hypBegin, hypCount, (HModelF*)d_models, d_h64, d_counts);
-        else if (eig_soa()) {
-            if (L == 48) MCV_H_GENERATE(48, true);
-            else if (L == 64) MCV_H_GENERATE(64, true);
-            else MCV_H_GENERATE(40, true);
-        } else {
-            switch (L) {
-                case 64: MCV_H_GENERATE(64, false); break;
-                case 48: MCV_H_GENERATE(48, false); break;
-                case 32: MCV_H_GENERATE(32, false); break;
-                case 39: MCV_H_GENERATE(39, false); break;
-                default: MCV_H_GENERATE(kEigLanes, false);
-            }
-        }
-#undef MCV_H_GENERATE
-    }
+    else   // kEigLanes per block: LDS-bound occupancy, one wave per SIMD (jacobi_eig.h)
+        hipLaunchKernelGGL((mcv_h_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
+                           dim3(kEigLanes), 0, s, d_pts4, N, smp, hypBegin, hypCount, (HModelF*)d_models, d_h64,
+                           d_counts);
 }
 
 void launch_h_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast) {
@@ -1107,35 +970,10 @@ static void launch_h_verify_kp(const float* d_pts4, int N, const void* d_models,
                            (const HModelF*)d_models, d_counts, hypCount, thr2, d_bbox, redo);
 }
 
-// Sweep shape (hypotheses per wave K, correspondences per lane per trip P). MCV_SWEEP_VARIANT
-// selects an alternative for tuning experiments (tests/bench only); the default is kVerify*.
-static int sweep_variant() {
-    static int v = [] {
-        const char* e = getenv("MCV_SWEEP_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
                      bool fused, const float* d_bbox, hipStream_t s) {
-    switch (sweep_variant()) {
-        case 1: launch_h_verify_kp<8, 4>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 2: launch_h_verify_kp<4, 4>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 3: launch_h_verify_kp<8, 1>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 4: launch_h_verify_kp<6, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 5: launch_h_verify_kp<4, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 6: launch_h_verify_kp<6, 3>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 7: launch_h_verify_kp<5, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 8: launch_h_verify_kp<6, 1>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 9: launch_h_verify_kp<4, 3>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 10: launch_h_verify_kp<3, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 11: launch_h_verify_kp<7, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        case 19: launch_h_verify_kp<6, 2>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused, d_bbox, s); break;
-        default:
-            launch_h_verify_kp<kVerifyHypPerWave, kVerifyPtsPerLane>(d_pts4, N, d_models, d_counts, hypCount, thr2,
-                                                                     fused, d_bbox, s);
-    }
+    launch_h_verify_kp<kVerifyHypPerWave, kVerifyPtsPerLane>(d_pts4, N, d_models, d_counts, hypCount, thr2, fused,
+                                                             d_bbox, s);
 }
 
 template <int K, int NP>
@@ -1153,75 +991,30 @@ void launch_h_pair(const float* d_pts4, int N, void* d_pairs, hipStream_t s) {
                        (HPair*)d_pairs);
 }
 
-static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d_models, int* d_counts,
-                                       int hypCount, float thr2, const float* d_bbox, hipStream_t s);
-
-// Packed sweep (fused error) + the exact recount of the slots it marked kStatusRedo. Returns false
-// when the variant screen selects the scalar sweep.
-bool launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
+// Packed sweep (fused error, <8, 2>: DESIGN.md §7's screen) + the exact recount of the slots it
+// marked kStatusRedo.
+void launch_h_verify_packed(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
                             int hypCount, float thr2, const float* d_bbox, hipStream_t s) {
-    if (!launch_h_verify_pk_variant(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s)) return false;
+    launch_h_verify_pk_k<8, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s);
     launch_h_verify_kp<kVerifyHypPerWave, kVerifyPtsPerLane>(d_pts4, N, d_models, d_counts, hypCount, thr2, true,
                                                              d_bbox, s, 1);
-    return true;
 }
 
-static bool launch_h_verify_pk_variant(const void* d_pairs, int N, const void* d_models, int* d_counts,
-                                       int hypCount, float thr2, const float* d_bbox, hipStream_t s) {
-    switch (sweep_variant()) {
-        case 0: launch_h_verify_pk_k<8, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 26: launch_h_verify_pk_k<6, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 20: launch_h_verify_pk_k<4, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 21: launch_h_verify_pk_k<8, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 22: launch_h_verify_pk_k<4, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 24: launch_h_verify_pk_k<3, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 25: launch_h_verify_pk_k<5, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 27: launch_h_verify_pk_k<5, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 28: launch_h_verify_pk_k<7, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 29: launch_h_verify_pk_k<6, 3>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        case 30: launch_h_verify_pk_k<6, 2>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bbox, s); return true;
-        default: return false;
-    }
-}
-
-template <int K, int NP, int FIX = 1, bool ASMCMP = false>
+template <int K, int NP>
 static void launch_h_verify_cert_k(const void* d_pairs, int N, const void* d_models, int* d_counts, int hypCount,
                                    float thr2, const double* d_bb, hipStream_t s) {
     const int waves = (hypCount + K - 1) / K;
     const int blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL((mcv_h_verify_cert<K, NP, FIX, ASMCMP>), dim3(blocks), dim3(256), 0, s, (const HPair*)d_pairs, (N + 1) / 2,
+    hipLaunchKernelGGL((mcv_h_verify_cert<K, NP>), dim3(blocks), dim3(256), 0, s, (const HPair*)d_pairs, (N + 1) / 2,
                        N / 2, (const HModelF*)d_models, d_counts, hypCount, thr2, h_cert_slopes_host(thr2), d_bb);
 }
 
-// Certified sweep shape (models per wave K, pairs per lane per trip NP); MCV_HCERT_VARIANT selects
-// an alternative for the variant screen (tests / bench only).
-static int cert_variant() {
-    static int v = [] {
-        const char* e = getenv("MCV_HCERT_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 // Certified sweep of the op-by-op error + the exact recount of the slots it marks kStatusRedo.
+// <6, 1>: screened against <4, 2>, <4, 1>, <5, 1>, <3, 2>, <8, 2> and t = 2^-12 / 2^-11 / 2^-10
+// (28.8 ms vs 29.6-33 ms at cfg3; scripts/gpu_r02_cert.sh).
 void launch_h_verify_certified(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
                                int hypCount, float thr2, const double* d_bb, hipStream_t s) {
-    switch (cert_variant()) {
-        case 1: launch_h_verify_cert_k<4, 2, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 2: launch_h_verify_cert_k<4, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 4: launch_h_verify_cert_k<3, 2, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 5: launch_h_verify_cert_k<4, 2, 1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 6: launch_h_verify_cert_k<4, 2, 2, true>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 7: launch_h_verify_cert_k<6, 1, 2, true>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 8: launch_h_verify_cert_k<5, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 90: launch_h_verify_cert_k<4, 2, -1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        case 91: launch_h_verify_cert_k<6, 1, -1, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s); break;
-        // default <6, 1>: screened against <4, 2>, <4, 1>, <5, 1>, <3, 2>, <8, 2> and t = 2^-12 / 2^-11 / 2^-10
-        // (28.8 ms vs 29.6-33 ms at cfg3; scripts/gpu_r02_cert.sh)
-        default: launch_h_verify_cert_k<6, 1, 2, false>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s);
-    }
-    static const bool noredo = getenv("MCV_HCERT_NOREDO") != nullptr;   // diagnostics only
-    if (noredo) return;
+    launch_h_verify_cert_k<6, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s);
     launch_h_verify_kp<kVerifyHypPerWave, kVerifyPtsPerLane>(d_pts4, N, d_models, d_counts, hypCount, thr2, false,
                                                              nullptr, s, 1);
 }

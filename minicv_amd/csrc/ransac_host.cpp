@@ -210,14 +210,6 @@ void pack_points(Plan& P, const mcvV2d* a, const mcvV2d* b, int N, float* d_dst,
 double effective_threshold(const RansacConfig& cfg) { return cfg.threshold > 0 ? cfg.threshold : 3.0; }
 bool fused_error(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FUSED_ERROR) != 0; }
 bool fast_minimal(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0; }
-// MCV_HCERT_VARIANT=-1: run the scalar op-by-op sweep instead of the certified one (screen / A-B only)
-bool h_sweep_scalar_only() {
-    static const bool v = [] {
-        const char* e = getenv("MCV_HCERT_VARIANT");
-        return e && atoi(e) < 0;
-    }();
-    return v;
-}
 
 // HomographyEstimatorCallback::runKernel over the masked correspondences (mask == NULL: all).
 bool h_refit(Plan& P, const float* d_pts, int N, const uint8_t* d_mask, hipStream_t s, double* H) {
@@ -371,12 +363,9 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         ProfScope ps("h_verify", s);
         if (!fused) {
             // default: OpenCV's op-by-op error, certified division-free packed sweep
-            if (h_sweep_scalar_only())
-                launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, false, nullptr, s);
-            else
-                launch_h_verify_certified(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bb4.p, s);
-        } else if (!launch_h_verify_packed(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bbox.p, s)) {
-            launch_h_verify(d_pts, N, P.models.p, d_counts, hypCount, thr2, true, P.bbox.p, s);
+            launch_h_verify_certified(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bb4.p, s);
+        } else {
+            launch_h_verify_packed(d_pts, P.pairs.p, N, P.models.p, d_counts, hypCount, thr2, P.bbox.p, s);
         }
     } else if (f_seven(P.model, cfg)) {
         // OpenCV FM_RANSAC: 7-point samples, 3 model slots per hypothesis (slot keys like essential)

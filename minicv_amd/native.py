@@ -136,6 +136,7 @@ SIGNATURES = {
     "mcvReplayChunk": (_I, [_P, _P, _I64, _I64, _I, _I, _D, _I]),
     "mcvReplayChunkModels": (_I, [_P, _P, _I64, _I64, _I, _I, _I, _D, _I]),
     "mcvMatchHammingDevice": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "mcvMatchHammingDeviceForm": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I, _P]),
     "mcvMatchL2Device": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P]),
     "mcvFindScaledPoseDevice": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P]),
     "mcvProfileEnable": (None, [_I]),

@@ -251,21 +251,32 @@ def test_matchers_back_to_back_on_two_streams(gpu, oracle):
 
 
 @pytest.fixture(params=["gemm", "popcount"])
-def hamming_form(request, monkeypatch):
-    """Both Hamming forms: the int8 GEMM on the matrix cores (default) and the XOR / popcount sweep
-    (MCV_HAMMING_FORM=popcount, read by the library on every call)."""
-    if request.param == "popcount":
-        monkeypatch.setenv("MCV_HAMMING_FORM", "popcount")
-    else:
-        monkeypatch.delenv("MCV_HAMMING_FORM", raising=False)
+def hamming_form(request):
+    """Both Hamming kernel forms: the int8 GEMM on the matrix cores (the default of every entry point)
+    and the XOR / popcount sweep, chosen through mcvMatchHammingDeviceForm."""
     return request.param
+
+
+def check_hamming_form(oracle, form, q, t):
+    """The device entry point with an explicit kernel form against the oracle (all four outputs)."""
+    import torch
+    from minicv_amd import device as D
+    dev = torch.device("cuda:0")
+    nq = q.shape[0]
+    tq, tt = torch.from_numpy(np.ascontiguousarray(q)).to(dev), torch.from_numpy(np.ascontiguousarray(t)).to(dev)
+    idx, dist, idx2, dist2 = (torch.empty(nq, dtype=torch.int32, device=dev) for _ in range(4))
+    D.match_hamming(tq, tt, idx, dist, idx2, dist2, form=form)
+    torch.cuda.synchronize()
+    for g, r in zip((idx, dist, idx2, dist2), oracle.match_hamming(q, t)):
+        np.testing.assert_array_equal(g.cpu().numpy(), r)
+    return idx.cpu().numpy(), dist.cpu().numpy(), idx2.cpu().numpy(), dist2.cpu().numpy()
 
 
 @pytest.mark.parametrize("nq,nt,nbytes", [(1, 1, 32), (33, 31, 32), (257, 1000, 16), (300, 333, 61), (513, 4099, 64),
                                           (1000, 70000, 32)])
 def test_hamming_forms_agree(gpu, oracle, hamming_form, nq, nt, nbytes):
     q, t, _ = S.hamming_problem(nq, nt, nbytes=nbytes, seed=3 * nq + nt)
-    check_hamming(oracle, q, t)
+    check_hamming_form(oracle, hamming_form, q, t)
 
 
 @pytest.mark.parametrize("nbytes", [32, 64])
@@ -279,7 +290,6 @@ def test_hamming_extreme_distances(gpu, oracle, hamming_form, nbytes):
     q = np.concatenate([np.zeros((40, nbytes), np.uint8), np.full((40, nbytes), 255, np.uint8),
                         rng.integers(0, 256, size=(50, nbytes), dtype=np.uint8)])
     t2 = np.full((5, nbytes), 255, np.uint8)          # every query at one distance from all of them
-    check_hamming(oracle, q, t)
-    check_hamming(oracle, q[:40], t2)
-    idx, dist, idx2, dist2 = opencv.matchHamming(q[:40], t2)
+    check_hamming_form(oracle, hamming_form, q, t)
+    idx, dist, idx2, dist2 = check_hamming_form(oracle, hamming_form, q[:40], t2)
     assert (dist == 8 * nbytes).all() and (idx == 0).all() and (idx2 == 1).all()
