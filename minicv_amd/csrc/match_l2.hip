@@ -17,14 +17,14 @@
 //   and inserts each score with 2 v_cmp + 6 v_cndmask (no divergent branch per score: the branchy
 //   form the compiler chose cost 7 % of the kernel, 5.80 -> 5.38 ms at cfg5).
 //   Grid = (query blocks of 128) x (train chunks); each lane keeps its top-3 GEMM-form scores.
-// mcv_l2_mfma16q<DP, ...>: the same GEMM form on the f16 matrix pipe (16x the f32 MFMA rate) with every
+// mcv_l2_gemm<DP> (f16 domain): the same GEMM form on the f16 matrix pipe (16x the f32 MFMA rate) with every
 //   fp32 operand split into f16 hi + lo (x = hi + lo + r, |r| <= 2^-22 |x| + 2^-13): q.t ~ qh.th +
 //   qh.tl + ql.th in two 32x32x16 accumulator chains (hi.hi; hi.lo then lo.hi) — 24 MFMAs of 32
 //   cycles per 32 x 32 x 128 tile against 64 of 64 cycles in f32. f16 x f16 products are exact in f32; the dropped ql.tl and the
 //   split residuals add 2^-21 |q| |t| + 2^-12.9 sqrt(dim) (|q| + |t|) to the nomination's error
 //   bound (mcv_l2_refine's tol16), so the exact answer is unchanged. Used when every coordinate of
-//   both sets is finite with |x| < 2^15 (fp16 range); mcv_l2_prep16 records max |x| and each kernel
-//   runs or returns on that device-side flag (no host round trip).
+//   both sets is finite with |x| < 2^15 (fp16 range); mcv_l2_prep16 records max |x| per block and each
+//   launch picks its form from those maxima on the device (no host round trip, no empty launch).
 // mcv_l2_refine folds the per-chunk top-3s and makes the result exact: the three candidates' exact
 //   squared distances (fp64 direct sum in dim order, the oracle's definition) give the top-2 unless a
 //   bound on the GEMM form's rounding leaves room for another train (near-ties), in which case the
@@ -43,8 +43,30 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 static constexpr unsigned kL2F16MaxBits = 0x47000000u;   // 32768.0f: |x| below it fits fp16 (max 65504)
 
-// The f16-split path's domain flag (max |x| over both sets as float bits; null: f32 path only).
-__device__ __forceinline__ bool l2_f16_domain(const unsigned* dom) { return dom && *dom < kL2F16MaxBits; }
+// Maxima as float bits (non-negative floats; their writers clamp NaN to +inf): n words at p, folded
+// by the calling wave (collective: every lane of the wave calls it and gets the wave-uniform result).
+// mcv_l2_prep16 leaves kL2MaxSlots atomic maxima of max |x| (both sets) and of the train norms, so no
+// launch of its own folds them; the DP > 128 path's mcv_l2_umax leaves one word.
+struct L2Max {
+    const unsigned* p;
+    int n;
+    int stride;   // words between consecutive maxima
+};
+__device__ __forceinline__ unsigned l2_max_bits(L2Max m) {
+    unsigned v = 0;
+    for (int i = (int)(threadIdx.x & 63); i < m.n; i += 64) {
+        const unsigned x = m.p[i * m.stride];
+        v = x > v ? x : v;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned o = __shfl_xor(v, off, 64);
+        v = o > v ? o : v;
+    }
+    return (unsigned)__builtin_amdgcn_readfirstlane((int)v);
+}
+// The f16-split path's domain: max |x| over both sets below 2^15 (p null: the f32 path only).
+__device__ __forceinline__ bool l2_f16_domain(L2Max dom) { return dom.p && l2_max_bits(dom) < kL2F16MaxBits; }
 
 struct L2Part { float b1, b2, b3; int i1, i2, i3; };
 
@@ -99,7 +121,9 @@ __device__ __forceinline__ void third_fold(float& c1, float& c2, float& c3, floa
 
 // Parity-split, zero-padded copy [nPad][DP] + squared norms (fp32, wave tree sum: the order only
 // affects the GEMM form, whose rounding the exact re-rank bounds whatever the order). One launch
-// covers the query and the train set (rows of q, then rows of t).
+// covers the query and the train set (rows of q, then rows of t). dim > 128 only (DP = 256: the f32
+// GEMM form reads these copies); for dim <= 128 mcv_l2_prep16 writes the norms and the f32 form
+// (outside the f16 domain) reads the caller's rows.
 struct L2PrepF32 {
     const float* src;
     int n, nPad;
@@ -107,8 +131,7 @@ struct L2PrepF32 {
     float* norms;
     float padNorm;
 };
-__global__ void mcv_l2_prep(L2PrepF32 q, L2PrepF32 t, int dim, int DP, const unsigned* __restrict__ dom) {
-    if (l2_f16_domain(dom)) return;   // the f16-split path runs (mcv_l2_prep16 wrote the norms)
+__global__ void mcv_l2_prep(L2PrepF32 q, L2PrepF32 t, int dim, int DP) {
     const int lane = threadIdx.x & 63;
     for (int rr = blockIdx.x * 4 + (threadIdx.x >> 6); rr < q.nPad + t.nPad; rr += gridDim.x * 4) {
         const bool isq = rr < q.nPad;
@@ -134,7 +157,8 @@ static int l2_prep_blocks(int nPad) { return std::min((nPad + 3) / 4, kL2PrepBlo
 // Max of non-negative float bit patterns over a[0, na) and b[0, nb) -> *out, and over c[0, nc) ->
 // *out2 when c is given (bit order = float order; NaN -> +inf): per-block maxima, the last block to
 // finish folds them, writes the results and re-arms its counter (grid-wide, one launch, no host round
-// trip). The f16 domain (row maxima of both sets) and the train norms' maximum use it.
+// trip). The DP > 128 path's train-norm maximum (the f16-capable path folds mcv_l2_prep16's per-block
+// maxima where they are read).
 static constexpr int kL2MaxBlocks = 64;
 __global__ __launch_bounds__(256) void mcv_l2_umax(const unsigned* __restrict__ a, int na,
                                                    const unsigned* __restrict__ b, int nb,
@@ -218,30 +242,59 @@ __device__ __forceinline__ void l2_lstore(float* __restrict__ lds, float* __rest
     if (threadIdx.x < TR) lnorm[threadIdx.x] = nstg;
 }
 
-// TR train rows per tile = TR / 32 independent 32x32 accumulator chains per wave, interleaved
-// k-step by k-step (they share the query operands b[]): the matrix pipe never waits on one
-// chain's dependent-accumulator latency.
+// Stage a tile from the caller's row-major train set instead (the f32 form inside the f16-capable
+// launch, DP <= 128): element e = thread + 256 j of the tile (row e / DP, dim e % DP; zero outside
+// [0, nt) x [0, dim)), stored at its parity-split LDS position.
 template <int DP, int TR>
-__global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ qp, const float* __restrict__ tp,
-                                                     const float* __restrict__ tnorm, int ntTiles,
-                                                     int tilesPerChunk, int nqPad, L2Part* __restrict__ part,
-                                                     const unsigned* __restrict__ dom) {
-    if (l2_f16_domain(dom)) return;   // grid-uniform: mcv_l2_mfma16q takes this launch
+__device__ __forceinline__ void l2_gload_raw(const float* __restrict__ traw, int nt, int dim,
+                                             const float* __restrict__ tnorm, int tile, float (&stg)[TR * DP / 256],
+                                             float& nstg) {
+#pragma unroll
+    for (int j = 0; j < TR * DP / 256; ++j) {
+        const int e = threadIdx.x + 256 * j, r = tile * TR + e / DP, k = e % DP;
+        stg[j] = r < nt && k < dim ? traw[(size_t)r * dim + k] : 0.f;
+    }
+    if (threadIdx.x < TR) nstg = tnorm[tile * TR + threadIdx.x];
+}
+
+template <int DP, int TR>
+__device__ __forceinline__ void l2_lstore_raw(float* __restrict__ lds, float* __restrict__ lnorm,
+                                              const float (&stg)[TR * DP / 256], float nstg) {
+    constexpr int ROWF = DP + 4;
+#pragma unroll
+    for (int j = 0; j < TR * DP / 256; ++j) {
+        const int e = threadIdx.x + 256 * j, r = e / DP, k = e % DP;
+        lds[r * ROWF + (k & 1) * (DP / 2) + (k >> 1)] = stg[j];
+    }
+    if (threadIdx.x < TR) lnorm[threadIdx.x] = nstg;
+}
+
+// The f32 GEMM form (one block = 4 waves x 32 queries, a tile = TR train rows = TR / 32 independent
+// 32x32 accumulator chains per wave, interleaved k-step by k-step: they share the query operands b[],
+// so the matrix pipe never waits on one chain's dependent-accumulator latency). RAW: queries and train
+// rows straight from the caller's arrays (raw, nq / nt / dim); otherwise the padded parity-split
+// copies of mcv_l2_prep. lds: 2 TR (DP + 4) floats, lnorm: 2 TR floats.
+template <int DP, int TR, bool RAW>
+__device__ __forceinline__ void l2_gemm32_body(const float* __restrict__ qsrc, const float* __restrict__ tsrc, int nq,
+                                               int nt, int dim, const float* __restrict__ tnorm, int ntTiles,
+                                               int tilesPerChunk, int nqPad, L2Part* __restrict__ part, int bx,
+                                               int by, float* __restrict__ lds, float* __restrict__ lnorm) {
     constexpr int KS = DP / 2;          // MFMA k-steps (2 dims each)
     constexpr int ROWF = DP + 4;        // padded LDS row, floats
-    constexpr int PER = TR * DP / 1024; // float4 staging loads per thread per tile (TR rows x DP)
+    constexpr int PER = RAW ? TR * DP / 256 : TR * DP / 1024;   // staging registers per thread per tile
     constexpr int NC = TR / 32;         // accumulator chains
-    __shared__ __attribute__((aligned(16))) float lds[2][TR * ROWF];
-    __shared__ __attribute__((aligned(16))) float lnorm[2][TR];
-
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
-    const int q0 = (blockIdx.x * 4 + wave) * 32;
+    const int q0 = (bx * 4 + wave) * 32;
 
     // B fragments: query q0 + col, dims 2s + h  (parity-split row: offset h * KS + s)
     float b[KS];
-    {
-        const float4* qrow = reinterpret_cast<const float4*>(qp + (size_t)(q0 + col) * DP + h * KS);
+    if constexpr (RAW) {
+        const int qq = q0 + col;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) b[s] = qq < nq && 2 * s + h < dim ? qsrc[(size_t)qq * dim + 2 * s + h] : 0.f;
+    } else {
+        const float4* qrow = reinterpret_cast<const float4*>(qsrc + (size_t)(q0 + col) * DP + h * KS);
 #pragma unroll
         for (int s4 = 0; s4 < KS / 4; ++s4) {
             const float4 v = qrow[s4];
@@ -249,18 +302,27 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
         }
     }
 
-    const int tBegin = blockIdx.y * tilesPerChunk;
+    const int tBegin = by * tilesPerChunk;
     const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
     float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
     int i1 = -1, i2 = -1;
 
     // Register staging of the next train tile.
-    float4 stg[PER];
+    using Stg = std::conditional_t<RAW, float, float4>;
+    Stg stg[PER];
     float nstg = 0.f;
+    auto gload = [&](int tile) {
+        if constexpr (RAW) l2_gload_raw<DP, TR>(tsrc, nt, dim, tnorm, tile, stg, nstg);
+        else l2_gload<DP, TR>(tsrc, tnorm, tile, stg, nstg);
+    };
+    auto lstore = [&](int buf) {
+        if constexpr (RAW) l2_lstore_raw<DP, TR>(lds + buf * TR * ROWF, lnorm + buf * TR, stg, nstg);
+        else l2_lstore<DP, TR>(lds + buf * TR * ROWF, lnorm + buf * TR, stg, nstg);
+    };
 
     if (tBegin < tEnd) {
-        l2_gload<DP, TR>(tp, tnorm, tBegin, stg, nstg);
-        l2_lstore<DP, TR>(lds[0], lnorm[0], stg, nstg);
+        gload(tBegin);
+        lstore(0);
     }
     __syncthreads();
     for (int t = tBegin; t < tEnd; ++t) {
@@ -268,14 +330,15 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
         const bool more = t + 1 < tEnd;
         // next tile's loads in flight under this tile's MFMAs (the last trip reloads its own tile
         // into the idle buffer: no branch around the staging registers)
-        l2_gload<DP, TR>(tp, tnorm, more ? t + 1 : t, stg, nstg);
+        gload(more ? t + 1 : t);
         // the tile's norms for this lane's rows (8j + 4h .. 8j + 4h + 3 of each chain: 4 b128 reads),
         // fetched ahead of the MFMA chain so the epilogue never waits on LDS
         float4 nv[NC][4];
 #pragma unroll
         for (int c = 0; c < NC; ++c)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) nv[c][j] = *reinterpret_cast<const float4*>(&lnorm[buf][32 * c + 8 * j + 4 * h]);
+            for (int j = 0; j < 4; ++j)
+                nv[c][j] = *reinterpret_cast<const float4*>(&lnorm[buf * TR + 32 * c + 8 * j + 4 * h]);
         floatx16 acc[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c)
@@ -286,7 +349,7 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
             float4 a[NC];
 #pragma unroll
             for (int c = 0; c < NC; ++c)
-                a[c] = *reinterpret_cast<const float4*>(&lds[buf][(32 * c + col) * ROWF + h * KS + 4 * s4]);
+                a[c] = *reinterpret_cast<const float4*>(&lds[buf * TR * ROWF + (32 * c + col) * ROWF + h * KS + 4 * s4]);
 #pragma unroll
             for (int c = 0; c < NC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c].x, b[4 * s4 + 0], acc[c], 0, 0, 0);
 #pragma unroll
@@ -306,11 +369,10 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
                 const float4 n4 = nv[c][r >> 2];
                 const float nrm = (r & 3) == 0 ? n4.x : (r & 3) == 1 ? n4.y : (r & 3) == 2 ? n4.z : n4.w;
                 const float s = fmaf(-2.f, acc[c][r], nrm);
-                // as in mcv_l2_mfma16q: a score >= b3 (or NaN, which the exact definition never ranks)
-                // changes nothing
+                // a score >= b3 (or NaN, which the exact definition never ranks) changes nothing
                 if (s < b3) top2b3_push_asc(b1, i1, b2, i2, b3, s, t * TR + row);
             }
-        l2_lstore<DP, TR>(lds[buf ^ 1], lnorm[buf ^ 1], stg, nstg);
+        lstore(buf ^ 1);
         __syncthreads();
     }
     // merge the two lane halves that hold the same query
@@ -325,18 +387,41 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
         top2_push(b1, i1, b2, i2, ob2, oi2);
         L2Part p;
         p.b1 = b1; p.b2 = b2; p.b3 = c3; p.i1 = i1; p.i2 = i2; p.i3 = -1;
-        part[(size_t)blockIdx.y * nqPad + q0 + col] = p;
+        part[(size_t)by * nqPad + q0 + col] = p;
     }
+}
+
+// The f32 GEMM form over mcv_l2_prep's padded copies (dim > 128).
+template <int DP, int TR>
+__global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ qp, const float* __restrict__ tp,
+                                                     const float* __restrict__ tnorm, int ntTiles,
+                                                     int tilesPerChunk, int nqPad, L2Part* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float lds[2 * TR * (DP + 4)];
+    __shared__ __attribute__((aligned(16))) float lnorm[2 * TR];
+    l2_gemm32_body<DP, TR, false>(qp, tp, 0, 0, 0, tnorm, ntTiles, tilesPerChunk, nqPad, part, blockIdx.x, blockIdx.y,
+                                  lds, lnorm);
 }
 
 // ---- f16-split GEMM form ---------------------------------------------------------------------
 
 // Row-major split copies [nPad][DP] (hi = RN f16 of x, lo = RN f16 of the exact fp32 residual x - hi),
-// zero padding, the fp32 squared norm (as mcv_l2_prep) and the row's max |x| (float bits; a
-// non-finite coordinate records +inf: out of the f16 domain; 0 for padding rows). mcv_l2_umax folds
-// the rows' maxima (one atomic per row on one address serialised to ~0.5 ms per call). The norms equal
-// mcv_l2_prep's bit for bit (the same fmaf order and tree), so either kernel's train norms give the
-// same maximum. One launch covers both sets and zeroes the call's exact-scan queue.
+// zero padding, the fp32 squared norms, and the maxima the later launches fold: slot[blockIdx % S] =
+// max |x| over the block's rows of both sets (float bits; a non-finite coordinate records +inf, out of
+// the f16 domain) and slot[S + blockIdx % S] = max train norm (NaN -> +inf), S = kL2MaxSlots, by one
+// atomicMax per block and quantity. The slots sit kL2SlotStride words apart: device atomics on one
+// 256-byte span serialise (~12 ns each: 3500 blocks' atomics on 16 adjacent words took the cfg5 share's
+// prep from 9.3 to 45 us, scripts/exp/prep_bench.hip; 256-byte spacing 9.9 us). The slots
+// come in two sets used by alternate calls: this launch accumulates into `slot` (zeroed by the
+// previous call) and zeroes `next` for the call after (stream order separates both from every
+// reader). One launch covers both sets (rows of q, then rows of t; grid-stride) and zeroes the
+// call's exact-scan queue.
+// VEC (dim % 4 == 0, 16-B aligned rows): a lane converts one float4, G = DP / 4 lanes a row, 256 / DP
+// rows per wave-trip, two trips' loads in flight; the norm adds the lane's four squares (fmaf chain)
+// and then the G lanes' partial sums by an xor tree. Otherwise a wave per row, lane-strided dims.
+// Both norm orders are sums of dim fmaf-rounded terms, which the GEMM form's error bound
+// (l2_gemm_tol: gamma_dim) covers in any order.
+static constexpr int kL2MaxSlots = 16, kL2SlotStride = 64;
+static constexpr int kL2PrepBlocksMax = 4096;
 struct L2PrepF16 {
     const float* src;
     int n, nPad;
@@ -344,42 +429,125 @@ struct L2PrepF16 {
     _Float16* lo;
     float* norms;
     float padNorm;
-    unsigned* rowmax;
 };
-__global__ void mcv_l2_prep16(L2PrepF16 q, L2PrepF16 t, int dim, int DP, int* __restrict__ ambCount) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *ambCount = 0;   // the exact-scan queue of this call
+__device__ __forceinline__ unsigned l2_abs_bits(float v) {
+    const float a = fabsf(v);
+    return a == a && a < __builtin_inff() ? __float_as_uint(a) : 0x7f800000u;
+}
+__device__ __forceinline__ unsigned l2_norm_bits(float v) {
+    return __float_as_uint(v) > 0x7f800000u ? 0x7f800000u : __float_as_uint(v);   // NaN (any sign) -> +inf
+}
+template <bool VEC>
+__global__ __launch_bounds__(256) void mcv_l2_prep16(L2PrepF16 q, L2PrepF16 t, int dim, int DP, int* __restrict__ ambCount,
+                                                     unsigned* __restrict__ slot, unsigned* __restrict__ next) {
+    __shared__ unsigned red[2][4];
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) *ambCount = 0;   // the exact-scan queue of this call
+        if (threadIdx.x < 2 * kL2MaxSlots) next[threadIdx.x * kL2SlotStride] = 0u;
+    }
     const int lane = threadIdx.x & 63;
-    for (int rr = blockIdx.x * 4 + (threadIdx.x >> 6); rr < q.nPad + t.nPad; rr += gridDim.x * 4) {
-        const bool isq = rr < q.nPad;
-        const int r = isq ? rr : rr - q.nPad, n = isq ? q.n : t.n;
-        const float* src = isq ? q.src : t.src;
-        _Float16* hi = isq ? q.hi : t.hi;
-        _Float16* lo = isq ? q.lo : t.lo;
-        float acc = 0.f;
-        unsigned m = 0;
-        for (int k = lane; k < DP; k += 64) {
-            const float v = (r < n && k < dim) ? src[(size_t)r * dim + k] : 0.f;
-            const _Float16 h = (_Float16)v;
-            hi[(size_t)r * DP + k] = h;
-            lo[(size_t)r * DP + k] = (_Float16)(v - (float)h);
-            acc = fmaf(v, v, acc);
-            const float a = fabsf(v);
-            const unsigned b = a == a && a < __builtin_inff() ? __float_as_uint(a) : 0x7f800000u;
-            m = b > m ? b : m;
-        }
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    const int nrows = q.nPad + t.nPad;
+    unsigned m = 0, mt = 0;
+    if constexpr (VEC) {
+        const int G = DP / 4, RW = 64 / G;   // lanes per row, rows per wave-trip (q.nPad % RW == 0)
+        const int sub = lane / G, c = lane % G;
+        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+        auto row_of = [&](int rr, bool& isq, int& r) {
+            isq = rr < q.nPad;
+            r = isq ? rr : rr - q.nPad;
+        };
+        for (int r0 = wave * RW; r0 < nrows; r0 += 2 * nw * RW) {
+            // two wave-trips: rows r0 + sub and r0 + nw RW + sub, both loads issued first
+            float4 v[2];
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            acc += __shfl_xor(acc, off, 64);
-            const unsigned o = __shfl_xor(m, off, 64);
-            m = o > m ? o : m;
+            for (int u = 0; u < 2; ++u) {
+                const int rr = r0 + u * nw * RW + sub;
+                bool isq;
+                int r;
+                row_of(rr, isq, r);
+                const int n = isq ? q.n : t.n;
+                const float* src = isq ? q.src : t.src;
+                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (rr < nrows && r < n && 4 * c < dim) v[u] = *reinterpret_cast<const float4*>(src + (size_t)r * dim + 4 * c);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int rr = r0 + u * nw * RW + sub;
+                if (r0 + u * nw * RW >= nrows) break;   // wave-uniform
+                bool isq;
+                int r;
+                row_of(rr, isq, r);
+                const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                _Float16 hx[4], lx[4];
+                float acc = 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    hx[e] = (_Float16)x[e];
+                    lx[e] = (_Float16)(x[e] - (float)hx[e]);
+                    acc = fmaf(x[e], x[e], acc);
+                    const unsigned b = l2_abs_bits(x[e]);
+                    m = b > m ? b : m;
+                }
+                for (int off = G / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+                if (rr < nrows) {
+                    _Float16* hi = isq ? q.hi : t.hi;
+                    _Float16* lo = isq ? q.lo : t.lo;
+                    *reinterpret_cast<f16x4*>(hi + (size_t)r * DP + 4 * c) = f16x4{hx[0], hx[1], hx[2], hx[3]};
+                    *reinterpret_cast<f16x4*>(lo + (size_t)r * DP + 4 * c) = f16x4{lx[0], lx[1], lx[2], lx[3]};
+                    if (c == 0) {
+                        const int n = isq ? q.n : t.n;
+                        (isq ? q.norms : t.norms)[r] = r < n ? acc : (isq ? q.padNorm : t.padNorm);
+                        if (!isq && r < n) {
+                            const unsigned b = l2_norm_bits(acc);
+                            mt = b > mt ? b : mt;
+                        }
+                    }
+                }
+            }
         }
-        if (lane == 0) {
-            (isq ? q.norms : t.norms)[r] = r < n ? acc : (isq ? q.padNorm : t.padNorm);
-            (isq ? q.rowmax : t.rowmax)[r] = r < n ? m : 0u;
+    } else {
+        for (int rr = wave; rr < nrows; rr += nw) {
+            const bool isq = rr < q.nPad;
+            const int r = isq ? rr : rr - q.nPad, n = isq ? q.n : t.n;
+            const float* src = isq ? q.src : t.src;
+            _Float16* hi = isq ? q.hi : t.hi;
+            _Float16* lo = isq ? q.lo : t.lo;
+            float acc = 0.f;
+            for (int k = lane; k < DP; k += 64) {
+                const float v = (r < n && k < dim) ? src[(size_t)r * dim + k] : 0.f;
+                const _Float16 hv = (_Float16)v;
+                hi[(size_t)r * DP + k] = hv;
+                lo[(size_t)r * DP + k] = (_Float16)(v - (float)hv);
+                acc = fmaf(v, v, acc);
+                const unsigned b = l2_abs_bits(v);
+                m = b > m ? b : m;
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+            if (lane == 0) {
+                (isq ? q.norms : t.norms)[r] = r < n ? acc : (isq ? q.padNorm : t.padNorm);
+                if (!isq && r < n) {
+                    const unsigned b = l2_norm_bits(acc);
+                    mt = b > mt ? b : mt;
+                }
+            }
         }
     }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned o = __shfl_xor(m, off, 64), ot = __shfl_xor(mt, off, 64);
+        m = o > m ? o : m;
+        mt = ot > mt ? ot : mt;
+    }
+    if (lane == 0) red[0][threadIdx.x >> 6] = m, red[1][threadIdx.x >> 6] = mt;
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        unsigned r = 0;
+        for (int w = 0; w < 4; ++w) r = red[threadIdx.x][w] > r ? red[threadIdx.x][w] : r;
+        if (r) atomicMax(slot + (threadIdx.x * kL2MaxSlots + blockIdx.x % kL2MaxSlots) * kL2SlotStride, r);
+    }
 }
-
 
 template <int DP, int TR, int NT>
 __device__ __forceinline__ void l2_gload16(const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
@@ -448,7 +616,7 @@ __device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const fl
     }
 }
 
-// The f16-split GEMM form. Block = WPB waves x 32 QT queries; per train tile of 32 rows and each
+// The f16-split GEMM form (body of mcv_l2_gemm). Block = WPB waves x 32 QT queries; per train tile of 32 rows and each
 // 16-dim k block: A = the tile's hi / lo rows from LDS (one ds_read_b128 each: lane l holds row l & 31,
 // dims 16 kb + 8 (l >> 5) + j), B = the wave's queries hi / lo (VGPR-resident, the same dims), three
 // accumulator chains (hi.hi, then hi.lo and lo.hi into one) on v_mfma_f32_32x32x16_f16. One
@@ -458,22 +626,22 @@ __device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const fl
 // 4 (cfg5): the round-3 form with two accumulator sets in turn 2.07 ms; QT = 2 at two waves per SIMD
 // (252 VGPRs) 2.17 ms, at one wave per SIMD 2.98 ms; s_setprio 1 around the MFMA cluster 1.95 ms;
 // 8-wave blocks 2.36 ms; four waves per SIMD (23 spilled VGPRs) 2.55 ms; this form 1.88 ms.
-template <int DP, int WPB, int QT, int WAVES>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void mcv_l2_mfma16q(
-    const _Float16* __restrict__ qh, const _Float16* __restrict__ ql, const _Float16* __restrict__ th,
-    const _Float16* __restrict__ tl, const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk, int nqPad,
-    L2Part* __restrict__ part, const unsigned* __restrict__ dom, bool xcdMap) {
+template <int DP, int WPB, int QT>
+__device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, const _Float16* __restrict__ ql,
+                                               const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
+                                               const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk,
+                                               int nqPad, L2Part* __restrict__ part, int bx, int by,
+                                               _Float16* __restrict__ lhb, _Float16* __restrict__ llb,
+                                               float* __restrict__ lnb) {
     constexpr int TR = 32;
-    if (!l2_f16_domain(dom)) return;   // grid-uniform: the f32 kernel takes this launch
-    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
-    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
     constexpr int KB = DP / 16;
     constexpr int ROWH = DP + 8;
     constexpr int NT = 64 * WPB;
     constexpr int PER = (TR * DP / 8 + NT - 1) / NT;
-    __shared__ __attribute__((aligned(16))) _Float16 lh[2][TR * ROWH];
-    __shared__ __attribute__((aligned(16))) _Float16 ll[2][TR * ROWH];
-    __shared__ __attribute__((aligned(16))) float lnorm[2][TR];
+    // LDS double buffers: lh / ll [2][TR * ROWH] halves, lnorm [2][TR]
+    auto lh = [&](int buf) { return lhb + buf * TR * ROWH; };
+    auto ll = [&](int buf) { return llb + buf * TR * ROWH; };
+    auto lnorm = [&](int buf) { return lnb + buf * TR; };
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
     const int q0 = (bx * WPB + wave) * 32 * QT;
@@ -498,7 +666,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
     float ns = 0.f;
     if (tBegin < tEnd) {
         l2_gload16<DP, TR, NT>(th, tl, tnorm, tBegin, sh, sl, ns);
-        l2_lstore16<DP, TR, NT>(lh[0], ll[0], lnorm[0], sh, sl, ns);
+        l2_lstore16<DP, TR, NT>(lh(0), ll(0), lnorm(0), sh, sl, ns);
         l2_gload16<DP, TR, NT>(th, tl, tnorm, min(tBegin + 1, tEnd - 1), sh, sl, ns);
     }
     __syncthreads();
@@ -512,8 +680,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
             for (int r = 0; r < 16; ++r) m[q][r] = sm[q][r] = 0.f;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(&lh[buf][col * ROWH + 16 * kb + 8 * h]);
-            const f16x8 al = *reinterpret_cast<const f16x8*>(&ll[buf][col * ROWH + 16 * kb + 8 * h]);
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(lh(buf) + col * ROWH + 16 * kb + 8 * h);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(ll(buf) + col * ROWH + 16 * kb + 8 * h);
 #pragma unroll
             for (int q = 0; q < QT; ++q) m[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[q][kb], m[q], 0, 0, 0);
 #pragma unroll
@@ -522,11 +690,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
             for (int q = 0; q < QT; ++q) sm[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[q][kb], sm[q], 0, 0, 0);
         }
         // the next tile (staged a tile ago) into the idle LDS buffer, the one after into the staging set
-        l2_lstore16<DP, TR, NT>(lh[buf ^ 1], ll[buf ^ 1], lnorm[buf ^ 1], sh, sl, ns);
+        l2_lstore16<DP, TR, NT>(lh(buf ^ 1), ll(buf ^ 1), lnorm(buf ^ 1), sh, sl, ns);
         l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), sh, sl, ns);
         float4 nv[1][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) nv[0][j] = *reinterpret_cast<const float4*>(&lnorm[buf][8 * j + 4 * h]);
+        for (int j = 0; j < 4; ++j) nv[0][j] = *reinterpret_cast<const float4*>(lnorm(buf) + 8 * j + 4 * h);
 #pragma unroll
         for (int q = 0; q < QT; ++q) {
             const floatx16 am[1] = {m[q]}, as[1] = {sm[q]};
@@ -556,6 +724,40 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(WAVES,
     }
 }
 
+// One GEMM launch for dim <= 128 whatever the data: the f16-split form inside its domain, else the f32
+// form on the caller's rows (l2_gemm32_body<.., RAW>), chosen per wave from mcv_l2_prep16's maxima —
+// no host round trip and no second (empty) launch. The two bodies share the LDS (the larger: the f16
+// form's 2 x 2 x 32 x (DP + 8) halves) and the f32 body fits the f16 form's register budget (three
+// waves per SIMD). XCD-aware (query block, train chunk) order when the chunk count divides 8: blocks
+// are dealt round-robin over the 8 XCDs, so chunk = linear block id mod C puts one chunk's train rows
+// on each XCD's L2.
+struct L2GemmArgs {
+    const _Float16 *qh, *ql, *th, *tl;
+    const float *qraw, *traw, *tnorm;
+    int nq, nt, dim, ntTiles, tilesPerChunk, nqPad;
+    L2Part* part;
+    L2Max dom;
+    bool xcdMap;
+};
+template <int DP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void mcv_l2_gemm(L2GemmArgs a) {
+    constexpr int TR = 32, ROWH = DP + 8, ROWF = DP + 4;
+    constexpr int HALVES = 2 * 2 * TR * ROWH, FLOATS = 2 * TR * ROWF;
+    constexpr int BYTES = (HALVES * 2 > FLOATS * 4 ? HALVES * 2 : FLOATS * 4) + 2 * TR * 4;
+    __shared__ __attribute__((aligned(16))) char smem[BYTES];
+    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
+    const int bx = a.xcdMap ? lin / gridDim.y : blockIdx.x, by = a.xcdMap ? lin % gridDim.y : blockIdx.y;
+    float* lnorm = reinterpret_cast<float*>(smem + BYTES - 2 * TR * 4);
+    if (l2_f16_domain(a.dom)) {
+        _Float16* lh = reinterpret_cast<_Float16*>(smem);
+        l2_gemm16_body<DP, 4, 1>(a.qh, a.ql, a.th, a.tl, a.tnorm, a.ntTiles, a.tilesPerChunk, a.nqPad, a.part, bx, by,
+                                 lh, lh + 2 * TR * ROWH, lnorm);
+    } else {
+        l2_gemm32_body<DP, TR, true>(a.qraw, a.traw, a.nq, a.nt, a.dim, a.tnorm, a.ntTiles, a.tilesPerChunk, a.nqPad,
+                                     a.part, bx, by, reinterpret_cast<float*>(smem), lnorm);
+    }
+}
+
 __device__ __forceinline__ double l2_exact(const float* __restrict__ q, const float* __restrict__ t, int dim) {
     double d = 0;
     for (int k = 0; k < dim; ++k) {
@@ -566,7 +768,8 @@ __device__ __forceinline__ double l2_exact(const float* __restrict__ q, const fl
 }
 
 // Both candidates' exact squared distances in one pass (two independent sequential chains; float4
-// loads when the rows are 16-byte aligned). Each sum is l2_exact's, operation for operation.
+// loads when the rows are 16-byte aligned, issued P float4s ahead of their use: the sums are
+// dependent chains, the loads are not). Each sum is l2_exact's, operation for operation.
 __device__ __forceinline__ void l2_exact2(const float* __restrict__ q, const float* __restrict__ ta,
                                           const float* __restrict__ tb, int dim, double& da, double& db) {
     double a = 0, b = 0;
@@ -574,16 +777,26 @@ __device__ __forceinline__ void l2_exact2(const float* __restrict__ q, const flo
     if (v4) {
         const float4 *q4 = reinterpret_cast<const float4*>(q), *a4 = reinterpret_cast<const float4*>(ta),
                      *b4 = reinterpret_cast<const float4*>(tb);
-        for (int k = 0; k < dim / 4; ++k) {
-            const float4 x = q4[k], y = a4[k], z = b4[k];
-            const double xs[4] = {(double)x.x, (double)x.y, (double)x.z, (double)x.w};
-            const double ys[4] = {(double)y.x, (double)y.y, (double)y.z, (double)y.w};
-            const double zs[4] = {(double)z.x, (double)z.y, (double)z.z, (double)z.w};
+        constexpr int P = 8;
+        const int n4 = dim / 4;
+        float4 x[P], y[P], z[P];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const double e = xs[j] - ys[j], f = xs[j] - zs[j];
-                a = a + e * e;
-                b = b + f * f;
+        for (int j = 0; j < P; ++j)
+            if (j < n4) x[j] = q4[j], y[j] = a4[j], z[j] = b4[j];
+        for (int k = 0; k < n4; k += P) {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                if (k + j >= n4) break;
+                const double xs[4] = {(double)x[j].x, (double)x[j].y, (double)x[j].z, (double)x[j].w};
+                const double ys[4] = {(double)y[j].x, (double)y[j].y, (double)y[j].z, (double)y[j].w};
+                const double zs[4] = {(double)z[j].x, (double)z[j].y, (double)z[j].z, (double)z[j].w};
+                if (k + P + j < n4) x[j] = q4[k + P + j], y[j] = a4[k + P + j], z[j] = b4[k + P + j];
+#pragma unroll
+                for (int e4 = 0; e4 < 4; ++e4) {
+                    const double e = xs[e4] - ys[e4], f = xs[e4] - zs[e4];
+                    a = a + e * e;
+                    b = b + f * f;
+                }
             }
         }
     } else {
@@ -629,12 +842,14 @@ __device__ __forceinline__ double l2_gemm_tol(double qn, double T2, int dim, boo
 //   tol = 1.01 (dim + 4) u (T2max + 2 |q| sqrt(T2max) + |q|^2)
 // covers the fp32 FMA chains of q.t and |t|^2 (gamma_dim each), the fma(-2, q.t, |t|^2), the fp32
 // |q|^2 and the sum |q|^2 + s.
-__global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad, int nchunks, int nt, int dim,
-                              const float* __restrict__ qnorm, const unsigned* __restrict__ tmaxBits,
+__global__ __launch_bounds__(64) void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad, int nchunks, int nt, int dim,
+                              const float* __restrict__ qnorm, L2Max tmax,
                               const float* __restrict__ qraw, const float* __restrict__ traw, int* __restrict__ idx,
                               float* __restrict__ dist, int* __restrict__ idx2, float* __restrict__ dist2,
                               int* __restrict__ ambCount, int* __restrict__ ambList, double* __restrict__ ambE2,
-                              const unsigned* __restrict__ dom) {
+                              L2Max dom) {
+    const bool f16 = l2_f16_domain(dom);
+    const unsigned T2bits = l2_max_bits(tmax);
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     float b1 = INFINITY, b2 = INFINITY, c1 = INFINITY, c2 = INFINITY, c3 = INFINITY;
@@ -669,8 +884,8 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
     // while the fp64 sums stay finite): a missing candidate sends the query to the exact scan.
     bool certain = nt == 0 || (nt <= 2 && i1 >= 0 && (nt < 2 || i2 >= 0));
     if (!certain && nt > 2 && i2 >= 0) {
-        const double qn = (double)qnorm[q], T2 = (double)__uint_as_float(*tmaxBits);
-        const double tol = l2_gemm_tol(qn, T2, dim, l2_f16_domain(dom));
+        const double qn = (double)qnorm[q], T2 = (double)__uint_as_float(T2bits);
+        const double tol = l2_gemm_tol(qn, T2, dim, f16);
         const double approx3 = (double)qnorm[q] + (double)c3;
         certain = approx3 - tol > e2 * (1.0 + 1e-12);   // every other train is strictly farther
     }
@@ -703,7 +918,8 @@ __global__ void mcv_l2_refine(const L2Part* __restrict__ part, int nq, int nqPad
 // The tile replaced a lane-per-row walk over a transposed train copy whose dependent loads left the
 // scan latency-bound (64 us at the 8-rank share, whatever the queue length; 42 us with no exact row).
 static constexpr int kL2ScanQ = 32;
-static constexpr int kL2ScanThreads = 1024;   // one 16-wave workgroup per CU
+static constexpr int kL2ScanThreads = 1024;   // dim > 128: one 16-wave workgroup per CU
+static constexpr int kL2ScanThreadsU = 512;   // dim <= 128 (mcv_l2_scan): 8 waves, 256 VGPRs each
 static constexpr int kL2ScanBlocks = 256;
 static constexpr int kL2TileFloats = 128 * 132;   // train tile: 128 rows of dimPad <= 128 (+4 pad)
 
@@ -757,23 +973,23 @@ __device__ __forceinline__ double l2_exact_row_wave(const float* qcol, const flo
     return d;
 }
 
-// DPMAX = 128: tiles of 128 rows, 4 queries per thread; DPMAX = 256: 64 rows, 2 queries per thread.
+// DPMAX = 128: tiles of 128 rows, 4 (NT = 1024) or 8 (NT = 512) queries per thread; DPMAX = 256: 64
+// rows, 2 queries per thread (NT = 1024).
 // Thread t filters tile row t % RT against queries (t / RT) * QG .. + QG - 1 (wave-uniform: the
-// query values are LDS broadcasts).
-template <int DPMAX>
-__global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
+// query values are LDS broadcasts). Work units = the grid's blocks.
+template <int DPMAX, int NT>
+__device__ __forceinline__ void l2_exact_scan_body(
     const float* __restrict__ qraw, const float* __restrict__ traw, int nt, int dim, int dimPad,
     const int* __restrict__ ambCount, const int* __restrict__ ambList, const double* __restrict__ ambE2,
     L2Top2d* __restrict__ part, int* __restrict__ idx, float* __restrict__ dist, int* __restrict__ idx2,
-    float* __restrict__ dist2, const unsigned* __restrict__ dom16) {
-    if (l2_f16_domain(dom16)) return;   // grid-uniform: mcv_l2_scan16 took this call
-    constexpr int NT = kL2ScanThreads, NW = NT / 64;
+    float* __restrict__ dist2) {
+    constexpr int NW = NT / 64;
     constexpr int RS = DPMAX + 4;                    // tile row stride (floats; 16-B aligned rows)
     constexpr int RT = kL2TileFloats / (128 + 4) * 128 / DPMAX;   // 128 or 64 rows
     constexpr int QG = kL2ScanQ * RT / NT;           // queries per thread: 4 or 2
     constexpr int RSTEP = NT / DPMAX;                // tile rows one pass of the workgroup loads
     constexpr int PER = RT / RSTEP;                  // tile elements per thread
-    static_assert(QG == 2 || QG == 4, "tile shape");
+    static_assert(QG == 2 || QG == 4 || QG == 8, "tile shape");
     __shared__ L2Top2d wtop[NW][kL2ScanQ];
     __shared__ double sthr[kL2ScanQ];
     __shared__ __attribute__((aligned(16))) float sq[DPMAX * kL2ScanQ];   // [dimPad][kL2ScanQ]
@@ -898,7 +1114,7 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
 }
 
 // Exact scan of the queued queries, f16 domain (round 4): the filter is the GEMM form itself. A
-// (batch of 32 queued queries, train chunk) item runs the f16-split MFMA chains of mcv_l2_mfma16q
+// (batch of 32 queued queries, train chunk) item runs the f16-split MFMA chains of mcv_l2_gemm
 // over the chunk's 32-row tiles (A fragments straight from the split train copy, B = the batch's
 // queries gathered through the queue), 4 waves taking tiles in turn; a (query, row) whose GEMM score
 // is at most thr = e2 (1 + 1e-12) + tol - qn (refine's bound: every row's exact d^2 >= qn + score -
@@ -906,30 +1122,35 @@ __global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(
 // parallel, the oracle's order). About as many rows survive as with the fp32 filter (the ambiguous
 // queries' near-ties), for 3 MFMAs per 16 dims instead of 2 packed VALU ops per dimension.
 template <int DP>
-__global__ __launch_bounds__(256) void mcv_l2_scan16(
+__device__ __forceinline__ void l2_scan16_body(
     const _Float16* __restrict__ qh, const _Float16* __restrict__ ql, const _Float16* __restrict__ th,
     const _Float16* __restrict__ tl, const float* __restrict__ tnorm, const float* __restrict__ qnorm,
-    const unsigned* __restrict__ tmaxBits, const float* __restrict__ qraw, const float* __restrict__ traw, int nt,
+    unsigned tmaxBits, const float* __restrict__ qraw, const float* __restrict__ traw, int nt,
     int ntTiles, int dim, const int* __restrict__ ambCount, const int* __restrict__ ambList,
     const double* __restrict__ ambE2, L2Top2d* __restrict__ part, int* __restrict__ idx, float* __restrict__ dist,
-    int* __restrict__ idx2, float* __restrict__ dist2, const unsigned* __restrict__ dom) {
-    if (!l2_f16_domain(dom)) return;   // grid-uniform: mcv_l2_exact_scan takes this call
-    constexpr int KB = DP / 16, NW = 4;
-    __shared__ L2Top2d wtop[NW][kL2ScanQ];
-    __shared__ float sthr[kL2ScanQ];
+    int* __restrict__ idx2, float* __restrict__ dist2) {
+    // the block runs SB = NT / 256 independent 256-thread units (work units = SB x blocks); every
+    // unit takes the same number of item rounds, so the block-wide barriers stay matched
+    constexpr int KB = DP / 16, NW = 4, SB = kL2ScanThreadsU / 256;
+    __shared__ L2Top2d wtop[SB][NW][kL2ScanQ];
+    __shared__ float sthr[SB][kL2ScanQ];
     const int n = *ambCount;
     const int nbatch = (n + kL2ScanQ - 1) / kL2ScanQ;
     if (nbatch == 0) return;
-    const int T = l2_scan_chunks(nbatch, gridDim.x);
-    const double T2 = (double)__uint_as_float(*tmaxBits);
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
-    for (int item = blockIdx.x; item < nbatch * T; item += gridDim.x) {
-        const int batch = item / T, chunk = item % T;
+    const int units = gridDim.x * SB;
+    const int T = l2_scan_chunks(nbatch, units);
+    const double T2 = (double)__uint_as_float(tmaxBits);
+    const int sb = threadIdx.x >> 8, tid = threadIdx.x & 255;
+    const int wv = tid >> 6, lane = tid & 63, h = lane >> 5, col = lane & 31;
+    for (int base = blockIdx.x * SB; base < nbatch * T; base += units) {
+        const int item = base + sb;
+        const bool act = item < nbatch * T;
+        const int batch = act ? item / T : 0, chunk = act ? item % T : 0;
         const int a0 = batch * kL2ScanQ;
-        const int nb = min(kL2ScanQ, n - a0);
-        const int tb = (int)((int64_t)chunk * ntTiles / T), te = (int)((int64_t)(chunk + 1) * ntTiles / T);
-        if (threadIdx.x < kL2ScanQ) {
-            const int b = threadIdx.x;
+        const int nb = act ? min(kL2ScanQ, n - a0) : 0;
+        const int tb = (int)((int64_t)chunk * ntTiles / T), te = act ? (int)((int64_t)(chunk + 1) * ntTiles / T) : tb;
+        if (tid < kL2ScanQ) {
+            const int b = tid;
             float thr = -INFINITY;   // padding members keep nothing
             if (b < nb) {
                 const int q = ambList[a0 + b];
@@ -938,12 +1159,12 @@ __global__ __launch_bounds__(256) void mcv_l2_scan16(
                 // rounded up (and a little more) to fp32: the fp32 compare keeps a superset
                 thr = x < 0x1p120 ? __double2float_ru(x + fabs(x) * 0x1p-40) : INFINITY;
             }
-            sthr[b] = thr;
+            sthr[sb][b] = thr;
         }
-        if (lane < kL2ScanQ) wtop[wv][lane] = L2Top2d{INFINITY, INFINITY, -1, -1};
+        if (lane < kL2ScanQ) wtop[sb][wv][lane] = L2Top2d{INFINITY, INFINITY, -1, -1};
         __syncthreads();
         const int qc = col < nb ? ambList[a0 + col] : -1;
-        const float myThr = sthr[col];
+        const float myThr = sthr[sb][col];
         f16x8 bh[KB], bl[KB];
         {
             const f16x8 z = (f16x8)((_Float16)0);
@@ -994,18 +1215,18 @@ __global__ __launch_bounds__(256) void mcv_l2_scan16(
                     const int row = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
                     if (row >= nt) continue;   // padding rows (never below a finite threshold anyway)
                     const double d = l2_exact_row_wave<1>(qraw + (size_t)q * dim, traw + (size_t)row * dim, dim, lane);
-                    L2Top2d w = wtop[wv][bq];
+                    L2Top2d w = wtop[sb][wv][bq];
                     top2d_push(w.d1, w.j1, w.d2, w.j2, d, row);
-                    if (lane == 0) wtop[wv][bq] = w;
+                    if (lane == 0) wtop[sb][wv][bq] = w;
                 }
             }
         }
         __syncthreads();
-        if (threadIdx.x < nb) {
-            const int b = threadIdx.x;
+        if (tid < nb) {
+            const int b = tid;
             L2Top2d r{INFINITY, INFINITY, -1, -1};
             for (int w = 0; w < NW; ++w) {
-                const L2Top2d x = wtop[w][b];
+                const L2Top2d x = wtop[sb][w][b];
                 top2d_push(r.d1, r.j1, r.d2, r.j2, x.d1, x.j1);
                 top2d_push(r.d1, r.j1, r.d2, r.j2, x.d2, x.j2);
             }
@@ -1016,17 +1237,52 @@ __global__ __launch_bounds__(256) void mcv_l2_scan16(
     }
 }
 
+// The exact scan of the queued queries, one launch for dim <= 128: the MFMA-filtered form in the f16
+// domain (2 x kL2ScanBlocks units of 256 threads), else the fp32-filter form (kL2ScanBlocks units; at
+// 512 threads the rare out-of-domain scan runs half the waves of the dim > 128 one).
+struct L2ScanArgs {
+    const _Float16 *qh, *ql, *th, *tl;
+    const float *tnorm, *qnorm, *qraw, *traw;
+    int nt, ntTiles, dim, dimPad;
+    const int *ambCount, *ambList;
+    const double* ambE2;
+    L2Top2d* part;
+    int* idx;
+    float* dist;
+    int* idx2;
+    float* dist2;
+    L2Max dom, tmax;
+};
+template <int DP>
+__global__ __launch_bounds__(kL2ScanThreadsU) void mcv_l2_scan(L2ScanArgs a) {
+    if (l2_f16_domain(a.dom))
+        l2_scan16_body<DP>(a.qh, a.ql, a.th, a.tl, a.tnorm, a.qnorm, l2_max_bits(a.tmax), a.qraw, a.traw, a.nt,
+                           a.ntTiles, a.dim, a.ambCount, a.ambList, a.ambE2, a.part, a.idx, a.dist, a.idx2, a.dist2);
+    else
+        l2_exact_scan_body<128, kL2ScanThreadsU>(a.qraw, a.traw, a.nt, a.dim, a.dimPad, a.ambCount, a.ambList, a.ambE2,
+                                                 a.part, a.idx, a.dist, a.idx2, a.dist2);
+}
+
+// dim > 128: the fp32-filter form alone.
+template <int DPMAX>
+__global__ __launch_bounds__(kL2ScanThreads) void mcv_l2_exact_scan(L2ScanArgs a) {
+    l2_exact_scan_body<DPMAX, kL2ScanThreads>(a.qraw, a.traw, a.nt, a.dim, a.dimPad, a.ambCount, a.ambList, a.ambE2,
+                                              a.part, a.idx, a.dist, a.idx2, a.dist2);
+}
+
 // Fold the per-chunk top-2s of each queued query (T > 1 only): one wave per query, lanes over the
 // chunks, then a lexicographic butterfly (the top-2 of a set does not depend on the fold order).
 __global__ __launch_bounds__(256) void mcv_l2_exact_merge(const int* __restrict__ ambCount,
                                                           const int* __restrict__ ambList,
                                                           const L2Top2d* __restrict__ part, int* __restrict__ idx,
                                                           float* __restrict__ dist, int* __restrict__ idx2,
-                                                          float* __restrict__ dist2, int blocks) {
+                                                          float* __restrict__ dist2, int blocks, L2Max dom) {
+    // the scan's work units: NT / 256 per block in the f16 domain (l2_scan16_body), one otherwise
+    const int units = l2_f16_domain(dom) ? blocks * (kL2ScanThreadsU / 256) : blocks;
     const int n = *ambCount;
     const int nbatch = (n + kL2ScanQ - 1) / kL2ScanQ;
     if (nbatch == 0) return;
-    const int T = l2_scan_chunks(nbatch, blocks);
+    const int T = l2_scan_chunks(nbatch, units);
     if (T == 1) return;
     const int lane = threadIdx.x & 63;
     for (int a = blockIdx.x * 4 + (threadIdx.x >> 6); a < n; a += gridDim.x * 4) {
@@ -1048,19 +1304,20 @@ __global__ __launch_bounds__(256) void mcv_l2_exact_merge(const int* __restrict_
 }
 
 struct L2Work {
-    DevBuf<float> qp, tp, qn, tn;
+    DevBuf<float> qp, tp, qn, tn;      // f32 padded copies (dim > 128), squared norms
     DevBuf<L2Part> part;
-    DevBuf<unsigned> tmax;
+    DevBuf<unsigned> tmax;             // dim > 128: the train norms' maximum (mcv_l2_umax)
     DevBuf<int> amb;   // [0] = count, [1..] = queued queries
-    DevBuf<L2Top2d> scanPart;   // exact-scan partials: < kL2ScanBlocks x kL2ScanQ records
-    DevBuf<_Float16> qh, ql, th, tl;   // f16-split copies (DP <= 128)
-    DevBuf<unsigned> dom;              // max |x| over both sets (float bits): the f16 path's domain
-    DevBuf<unsigned> maxPart;          // mcv_l2_umax: per-block maxima (2 x kL2MaxBlocks)
-    DevBuf<unsigned> maxCount;         // ... and its finish counter (zeroed once, re-armed by each launch)
-    DevBuf<unsigned> qmax, tmaxr;      // per-row max |x|
+    DevBuf<L2Top2d> scanPart;   // exact-scan partials: < 4 kL2ScanBlocks x kL2ScanQ records
+    DevBuf<_Float16> qh, ql, th, tl;   // f16-split copies (dim <= 128)
+    DevBuf<unsigned> maxPart;          // dim > 128: mcv_l2_umax's per-block maxima (2 x kL2MaxBlocks)
+    DevBuf<unsigned> slots;            // mcv_l2_prep16's maxima: two sets of 2 x kL2MaxSlots (strided; zeroed once)
+    int slotSet = 0;                   // the set the next call accumulates into
+    DevBuf<unsigned> maxCount;         // mcv_l2_umax's finish counter (zeroed once, re-armed by each launch)
     DevBuf<double> ambE2;              // per queued query: the filter bound (refine's exact second best)
     hipStream_t last = nullptr; // stream of the last match (the diagnostics read the queue length there)
-    bool lastF16 = false;       // the last match launched the f16-split form (its flag decided on device)
+    bool lastF16 = false;       // the last match launched the f16-capable path (its form decided on device)
+    const unsigned* lastDom = nullptr;   // ... and its domain slots
     bool ran = false;           // a match ran on this thread (its stream may be the null stream)
     StreamFence fence;          // calls on different streams take turns on these buffers
 };
@@ -1074,6 +1331,12 @@ static L2Work& l2_work() {
     return wk[d];
 }
 
+// dim <= 128 (the f16-capable path) is five launches, with no host round trip and no empty launch:
+//   mcv_l2_prep16 (split copies, norms, per-block maxima) -> mcv_l2_gemm (f16 form or f32 form, decided
+//   per wave from the maxima) -> mcv_l2_refine -> mcv_l2_scan (MFMA-filtered or fp32-filter exact scan)
+//   -> mcv_l2_exact_merge.
+// dim > 128: mcv_l2_prep (padded f32 copies) -> mcv_l2_umax (train-norm maximum) -> mcv_l2_mfma ->
+//   mcv_l2_refine -> mcv_l2_exact_scan -> mcv_l2_exact_merge.
 int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim, int* d_idx, float* d_dist,
                     int* d_idx2, float* d_dist2, hipStream_t s) {
     if (dim <= 0 || dim > 256) fail("cvMatchL2: dim %d outside [1, 256]", dim);
@@ -1081,72 +1344,80 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     L2Work& wk = l2_work();
     wk.fence.enter(s);
     const int DP = dim <= 32 ? 32 : dim <= 64 ? 64 : dim <= 128 ? 128 : 256;
-    const int nqPad = (nq + 255) / 256 * 256;   // whole 128-query (f32) and 128 / 256-query (f16) blocks
-    const bool f16 = DP <= 128;   // the f16-split form (inside its domain: a device-side flag below)
+    const int nqPad = (nq + 255) / 256 * 256;   // whole 128-query blocks
+    const bool f16 = DP <= 128;   // the f16-capable path (inside its domain: decided on the device)
     constexpr int TR = 32;        // train rows per tile (f32 form: 32 / 64 screened equal, scripts/sweep_l2.sh)
     const int ntPad = nt > 0 ? (nt + TR - 1) / TR * TR : TR;
     const int ntTiles = ntPad / TR;
-    wk.qp.ensure((size_t)nqPad * DP);
-    wk.tp.ensure((size_t)ntPad * DP);
     wk.qn.ensure(nqPad);
     wk.tn.ensure(ntPad);
-    wk.tmax.ensure(1);
-    if (!wk.maxCount.p) {
-        wk.maxCount.ensure(1);
-        MCV_HIP(hipMemsetAsync(wk.maxCount.p, 0, sizeof(unsigned), s));
-    }
-    wk.maxPart.ensure(2 * kL2MaxBlocks);
     wk.amb.ensure((size_t)nq + 1);
     wk.ambE2.ensure((size_t)nq);
-    // f16-split GEMM form for DP <= 128: the split prep records max |x|, and the f32 prep / GEMM
-    // return on the device when it is inside the f16 domain (no host round trip)
-    const unsigned* dom = nullptr;
-    const unsigned* tnBits = reinterpret_cast<const unsigned*>(wk.tn.p);
+    L2Max dom{nullptr, 0, 1}, tmax{nullptr, 0, 1};
     if (f16) {
         wk.qh.ensure((size_t)nqPad * DP);
         wk.ql.ensure((size_t)nqPad * DP);
         wk.th.ensure((size_t)ntPad * DP);
         wk.tl.ensure((size_t)ntPad * DP);
-        wk.dom.ensure(1);
-        wk.qmax.ensure(nqPad);
-        wk.tmaxr.ensure(ntPad);
-        const L2PrepF16 pq{d_q, nq, nqPad, wk.qh.p, wk.ql.p, wk.qn.p, 0.f, wk.qmax.p};
+        constexpr int setWords = 2 * kL2MaxSlots * kL2SlotStride;
+        if (!wk.slots.p) {
+            wk.slots.ensure(2 * setWords);
+            MCV_HIP(hipMemsetAsync(wk.slots.p, 0, 2 * setWords * sizeof(unsigned), s));
+        }
+        unsigned* slot = wk.slots.p + setWords * wk.slotSet;
+        unsigned* next = wk.slots.p + setWords * (wk.slotSet ^ 1);
+        wk.slotSet ^= 1;
+        const L2PrepF16 pq{d_q, nq, nqPad, wk.qh.p, wk.ql.p, wk.qn.p, 0.f};
         // padding rows get a +inf norm: their scores are +inf and never enter a top-2 or the third place
-        const L2PrepF16 pt{d_t, nt, ntPad, wk.th.p, wk.tl.p, wk.tn.p, __builtin_inff(), wk.tmaxr.p};
-        hipLaunchKernelGGL(mcv_l2_prep16, dim3(l2_prep_blocks(nqPad + ntPad)), dim3(256), 0, s, pq, pt, dim, DP,
-                           wk.amb.p);
-        hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s, wk.qmax.p, nq, wk.tmaxr.p, nt, tnBits, nt,
-                           wk.maxPart.p, wk.maxCount.p, wk.dom.p, wk.tmax.p);
-        dom = wk.dom.p;
+        const L2PrepF16 pt{d_t, nt, ntPad, wk.th.p, wk.tl.p, wk.tn.p, __builtin_inff()};
+        const bool vec = dim % 4 == 0 && (((uintptr_t)d_q | (uintptr_t)d_t) & 15) == 0;
+        // about two rows per lane group in flight per wave: 4096 blocks cover cfg5's 100k rows in ~3 trips
+        const int rowsPerBlock = vec ? 4 * (256 / DP) * 2 : 4;
+        const int blocks = std::max(1, std::min(kL2PrepBlocksMax, (nqPad + ntPad + rowsPerBlock - 1) / rowsPerBlock));
+        if (vec)
+            hipLaunchKernelGGL(mcv_l2_prep16<true>, dim3(blocks), dim3(256), 0, s, pq, pt, dim, DP, wk.amb.p, slot, next);
+        else
+            hipLaunchKernelGGL(mcv_l2_prep16<false>, dim3(blocks), dim3(256), 0, s, pq, pt, dim, DP, wk.amb.p, slot, next);
+        dom = L2Max{slot, kL2MaxSlots, kL2SlotStride};
+        tmax = L2Max{slot + kL2MaxSlots * kL2SlotStride, kL2MaxSlots, kL2SlotStride};
+        wk.lastDom = slot;
     } else {
+        wk.qp.ensure((size_t)nqPad * DP);
+        wk.tp.ensure((size_t)ntPad * DP);
+        wk.tmax.ensure(1);
+        if (!wk.maxCount.p) {
+            wk.maxCount.ensure(1);
+            MCV_HIP(hipMemsetAsync(wk.maxCount.p, 0, sizeof(unsigned), s));
+        }
+        wk.maxPart.ensure(2 * kL2MaxBlocks);
         MCV_HIP(hipMemsetAsync(wk.amb.p, 0, sizeof(int), s));
-    }
-    {
         const L2PrepF32 pq{d_q, nq, nqPad, wk.qp.p, wk.qn.p, 0.f};
         const L2PrepF32 pt{d_t, nt, ntPad, wk.tp.p, wk.tn.p, __builtin_inff()};
-        hipLaunchKernelGGL(mcv_l2_prep, dim3(l2_prep_blocks(nqPad + ntPad)), dim3(256), 0, s, pq, pt, dim, DP, dom);
+        hipLaunchKernelGGL(mcv_l2_prep, dim3(l2_prep_blocks(nqPad + ntPad)), dim3(256), 0, s, pq, pt, dim, DP);
+        hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s,
+                           reinterpret_cast<const unsigned*>(wk.tn.p), nt, nullptr, 0, nullptr, 0, wk.maxPart.p,
+                           wk.maxCount.p, wk.tmax.p, nullptr);
+        tmax = L2Max{wk.tmax.p, 1, 1};
     }
-    if (!f16)
-        hipLaunchKernelGGL(mcv_l2_umax, dim3(kL2MaxBlocks), dim3(256), 0, s, tnBits, nt, nullptr, 0, nullptr, 0,
-                           wk.maxPart.p, wk.maxCount.p, wk.tmax.p, nullptr);
     const int qblocks = nqPad / 128;
     int nchunks = (2048 + qblocks - 1) / qblocks;
-    // f16 form: mcv_l2_mfma16q<D, 4, 1, 3> runs 3 blocks per CU, so a grid runs in "rounds" of 3 x CUs blocks and
-    // a round that is barely begun costs most of a block's time: the chunk count C minimises
-    // ceil(qblocks C / (3 CUs)) (1 / C + 0.01) (the 0.01: a block's fixed cost against a whole-train
-    // sweep) over C = 4 .. 24. Screened at cfg5's rank shares (scripts/gpu_r04_q.sh, 50k / N queries):
-    // C = 15 took N = 1 / 2 / 4 / 8 to 1.98 / 1.12 / 0.58 / 0.35 ms against 2.14 / 1.21 / 0.74 / 0.40
-    // with 8 and 2.01 / 1.16 / 0.65 / 0.44 with 16 (N = 8: 800 blocks, one past a round).
+    // f16-capable launch: 3 blocks per CU (the f16 form's budget), so a grid runs in "rounds" of
+    // 3 x CUs blocks and a round that is barely begun costs most of a block's time: the chunk count C
+    // minimises ceil(qblocks C / (3 CUs)) (1 / C + 0.01) (the 0.01: a block's fixed cost against a
+    // whole-train sweep) over C = 4 .. 24. Screened at cfg5's rank shares (scripts/gpu_r04_q.sh,
+    // 50k / N queries): C = 15 took N = 1 / 2 / 4 / 8 to 1.98 / 1.12 / 0.58 / 0.35 ms against
+    // 2.14 / 1.21 / 0.74 / 0.40 with 8 and 2.01 / 1.16 / 0.65 / 0.44 with 16 (N = 8: 800 blocks, one
+    // past a round).
     if (f16) {
         static const int cus = [] {
             int d = 0, n = 0;
             (void)hipGetDevice(&d);
             return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
         }();
-        const int qb = nqPad / 128, slots = 3 * cus;
+        const int slots = 3 * cus;
         double best = 1e30;
         for (int c = 4; c <= 24; ++c) {
-            const double cost = (double)((qb * c + slots - 1) / slots) * (1.0 / c + 0.01);
+            const double cost = (double)((qblocks * c + slots - 1) / slots) * (1.0 / c + 0.01);
             if (cost < best - 1e-12) best = cost, nchunks = c;
         }
     }
@@ -1154,69 +1425,49 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     if (nchunks < 1) nchunks = 1;
     const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
     nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
-    const bool xcdMap = (8 % nchunks) == 0;
     wk.part.ensure((size_t)nchunks * nqPad);
-    dim3 grid(qblocks, nchunks);
     {
         ProfScope ps("l2_mfma", s);
-#define MCV_L2_LAUNCH(D, T) hipLaunchKernelGGL((mcv_l2_mfma<D, T>), grid, dim3(256), 0, s, wk.qp.p, wk.tp.p, wk.tn.p, \
-                                               ntTiles, tilesPerChunk, nqPad, wk.part.p, dom)
-#define MCV_L2_LAUNCH16Q(D)                                                                                 \
-    hipLaunchKernelGGL((mcv_l2_mfma16q<D, 4, 1, 3>), dim3(nqPad / 128, nchunks), dim3(256), 0, s, wk.qh.p, wk.ql.p,   \
-                       wk.th.p, wk.tl.p, wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p, dom, xcdMap)
         if (f16) {
+            const L2GemmArgs ga{wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, d_q, d_t, wk.tn.p, nq, nt, dim, ntTiles,
+                                tilesPerChunk, nqPad, wk.part.p, dom, (8 % nchunks) == 0};
+            const dim3 grid(qblocks, nchunks);
             switch (DP) {
-                case 32: MCV_L2_LAUNCH16Q(32); break;
-                case 64: MCV_L2_LAUNCH16Q(64); break;
-                default: MCV_L2_LAUNCH16Q(128); break;
+                case 32: hipLaunchKernelGGL(mcv_l2_gemm<32>, grid, dim3(256), 0, s, ga); break;
+                case 64: hipLaunchKernelGGL(mcv_l2_gemm<64>, grid, dim3(256), 0, s, ga); break;
+                default: hipLaunchKernelGGL(mcv_l2_gemm<128>, grid, dim3(256), 0, s, ga); break;
             }
+        } else {
+            hipLaunchKernelGGL((mcv_l2_mfma<256, TR>), dim3(qblocks, nchunks), dim3(256), 0, s, wk.qp.p, wk.tp.p,
+                               wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p);
         }
-#undef MCV_L2_LAUNCH16Q
-        switch (DP) {
-            case 32: MCV_L2_LAUNCH(32, TR); break;
-            case 64: MCV_L2_LAUNCH(64, TR); break;
-            case 128: MCV_L2_LAUNCH(128, TR); break;
-            default: MCV_L2_LAUNCH(256, TR); break;
-        }
-#undef MCV_L2_LAUNCH
     }
     // one wave per block: the latency-bound exact sums of a rank's few thousand queries spread over
     // every CU (6250 queries: 40 -> 14 us)
     hipLaunchKernelGGL(mcv_l2_refine, dim3((nq + 63) / 64), dim3(64), 0, s, wk.part.p, nq, nqPad, nchunks, nt, dim,
-                       wk.qn.p, wk.tmax.p, d_q, d_t, d_idx, d_dist, d_idx2, d_dist2, wk.amb.p, wk.amb.p + 1,
+                       wk.qn.p, tmax, d_q, d_t, d_idx, d_dist, d_idx2, d_dist2, wk.amb.p, wk.amb.p + 1,
                        wk.ambE2.p, dom);
     {
         ProfScope ps("l2_exact", s);
         constexpr int scanBlocks = kL2ScanBlocks;
-        wk.scanPart.ensure((size_t)scanBlocks * kL2ScanQ);
-        // f16 domain: the MFMA-filtered scan (the VALU scan returns on the device flag); otherwise the
-        // fp32-filter scan
-        const unsigned* dom16 = f16 ? dom : nullptr;
-        if (dom16) {
-#define MCV_L2_SCAN16(D)                                                                                        \
-    hipLaunchKernelGGL(mcv_l2_scan16<D>, dim3(scanBlocks), dim3(256), 0, s, wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, \
-                       wk.qn.p, wk.tmax.p, d_q, d_t, nt, ntTiles, dim, wk.amb.p, wk.amb.p + 1, wk.ambE2.p,            \
-                       wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2, dom16)
+        wk.scanPart.ensure((size_t)scanBlocks * (kL2ScanThreadsU / 256) * kL2ScanQ);
+        const int dimPad = (dim + 7) / 8 * 8;   // the fp32 filter's 8-dimension trips over float4 rows
+        const L2ScanArgs sa{wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, wk.tn.p, wk.qn.p, d_q, d_t, nt, ntTiles, dim, dimPad,
+                            wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2, dom,
+                            tmax};
+        if (f16) {
             switch (DP) {
-                case 32: MCV_L2_SCAN16(32); break;
-                case 64: MCV_L2_SCAN16(64); break;
-                default: MCV_L2_SCAN16(128); break;
+                case 32: hipLaunchKernelGGL(mcv_l2_scan<32>, dim3(scanBlocks), dim3(kL2ScanThreadsU), 0, s, sa); break;
+                case 64: hipLaunchKernelGGL(mcv_l2_scan<64>, dim3(scanBlocks), dim3(kL2ScanThreadsU), 0, s, sa); break;
+                default: hipLaunchKernelGGL(mcv_l2_scan<128>, dim3(scanBlocks), dim3(kL2ScanThreadsU), 0, s, sa); break;
             }
-#undef MCV_L2_SCAN16
+        } else {
+            hipLaunchKernelGGL(mcv_l2_exact_scan<256>, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, sa);
         }
-        const int dimPad = (dim + 7) / 8 * 8;   // the filter's 8-dimension trips over float4 rows
-        if (dimPad <= 128)
-            hipLaunchKernelGGL(mcv_l2_exact_scan<128>, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, d_q, d_t, nt, dim,
-                               dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2,
-                               dom16);
-        else
-            hipLaunchKernelGGL(mcv_l2_exact_scan<256>, dim3(scanBlocks), dim3(kL2ScanThreads), 0, s, d_q, d_t, nt, dim,
-                               dimPad, wk.amb.p, wk.amb.p + 1, wk.ambE2.p, wk.scanPart.p, d_idx, d_dist, d_idx2, d_dist2,
-                               dom16);
         // the chunks' top-2s folded by a launch of their own: in the scan's last workgroup the fold is one
         // block's serial chain (+23 us at the 8-rank share, +170 us at 241 queued queries x 32 chunks)
         hipLaunchKernelGGL(mcv_l2_exact_merge, dim3(64), dim3(256), 0, s, wk.amb.p, wk.amb.p + 1, wk.scanPart.p, d_idx,
-                           d_dist, d_idx2, d_dist2, scanBlocks);
+                           d_dist, d_idx2, d_dist2, scanBlocks, dom);
     }
     MCV_HIP(hipGetLastError());
     wk.fence.leave(s);
@@ -1241,9 +1492,11 @@ int l2_last_gemm_form() {
     L2Work& wk = l2_work();
     if (!wk.ran) return 0;
     if (!wk.lastF16) return 32;
-    unsigned d = 0;
-    MCV_HIP(hipMemcpyAsync(&d, wk.dom.p, sizeof(unsigned), hipMemcpyDeviceToHost, wk.last));
+    unsigned m[kL2MaxSlots * kL2SlotStride];
+    MCV_HIP(hipMemcpyAsync(m, wk.lastDom, sizeof(m), hipMemcpyDeviceToHost, wk.last));
     MCV_HIP(hipStreamSynchronize(wk.last));
+    unsigned d = 0;
+    for (int i = 0; i < kL2MaxSlots; ++i) d = m[i * kL2SlotStride] > d ? m[i * kL2SlotStride] : d;
     return d < kL2F16MaxBits ? 16 : 32;
 }
 

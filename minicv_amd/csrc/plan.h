@@ -120,13 +120,13 @@ inline void reduce_to_host(Plan& P, hipStream_t s, int V, double* out, F launch)
 // Opt-in kernel timing with HIP events recorded on the launch stream (bench.py's live roofline).
 bool prof_enabled();
 void prof_record(const char* name, hipEvent_t a, hipEvent_t b);
+hipEvent_t prof_event();   // a timing event (reused across mcvProfileReset)
 struct ProfScope {
     const char* name;
     hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
     ProfScope(const char* n, hipStream_t st) : name(n), s(st) {
-        if (prof_enabled() && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
-            (void)hipEventRecord(a, s);
+        if (prof_enabled() && (a = prof_event()) && (b = prof_event())) (void)hipEventRecord(a, s);
     }
     ~ProfScope() {
         if (a && b) {

@@ -252,13 +252,16 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
         };
         spk_sweep_point<KP>(pr, q, v, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
     }
-    if (lane == 0) {
+    // lane k writes model k's count (one store / one atomic instruction per wave)
+    int mine = 0;
+    bool mv = false;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (!valid[k]) continue;
-            if (gridDim.y == 1) counts[denseSlot[m0 + k]] = (int)cnt[k];
-            else if (cnt[k]) atomicAdd(counts + denseSlot[m0 + k], (int)cnt[k]);
-        }
+    for (int k = 0; k < K; ++k)
+        if (lane == k) mine = (int)cnt[k], mv = valid[k];
+    if (lane < K && mv) {
+        const int slot = denseSlot[m0 + lane];
+        if (gridDim.y == 1) counts[slot] = mine;
+        else if (mine) atomicAdd(counts + slot, mine);
     }
 }
 

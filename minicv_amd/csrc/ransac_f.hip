@@ -219,13 +219,15 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
         auto x64 = [&](double& x1, double& y1, double& x2, double& y2) { x1 = q.x; y1 = q.y; x2 = q.z; y2 = q.w; };
         spk_sweep_point<KP>(pr, q, v, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
     }
-    if (lane == 0) {
+    // lane k writes model k's count: one store / one atomic instruction per wave over K contiguous slots
+    int mine = 0;
+    bool mv = false;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (!valid[k]) continue;
-            if (gridDim.y == 1) counts[h0 + k] = (int)cnt[k];
-            else if (cnt[k]) atomicAdd(counts + h0 + k, (int)cnt[k]);
-        }
+    for (int k = 0; k < K; ++k)
+        if (lane == k) mine = (int)cnt[k], mv = valid[k];
+    if (lane < K && mv) {
+        if (gridDim.y == 1) counts[h0 + lane] = mine;
+        else if (mine) atomicAdd(counts + h0 + lane, mine);
     }
 }
 

@@ -24,10 +24,24 @@ namespace {
 struct ProfRec { std::string name; hipEvent_t a, b; };
 std::mutex g_prof_mu;
 std::vector<ProfRec> g_prof;
+std::vector<hipEvent_t> g_prof_free;   // events of earlier records, reused (hipEventCreate per launch
+                                       // costs microseconds of host time inside a timed loop)
 bool g_prof_on = false;
 }  // namespace
 namespace mcv {
 bool prof_enabled() { return g_prof_on; }
+hipEvent_t prof_event() {
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        if (!g_prof_free.empty()) {
+            hipEvent_t e = g_prof_free.back();
+            g_prof_free.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
 void prof_record(const char* name, hipEvent_t a, hipEvent_t b) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof.push_back({name, a, b});
@@ -39,8 +53,9 @@ extern "C" MCV_API void mcvProfileEnable(int on) { g_prof_on = on != 0; }
 extern "C" MCV_API void mcvProfileReset(void) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     for (auto& r : g_prof) {
-        (void)hipEventDestroy(r.a);
-        (void)hipEventDestroy(r.b);
+        (void)hipEventSynchronize(r.b);
+        g_prof_free.push_back(r.a);
+        g_prof_free.push_back(r.b);
     }
     g_prof.clear();
 }

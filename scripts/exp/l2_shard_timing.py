@@ -1,6 +1,7 @@
 """Per-rank L2 step time of bench.py's query-sharded cfg5 (nq / N queries x 50k train x 128) for
-N = 1, 2, 4, 8 on one GPU: what each rank of the driver's scaling run computes (device arrays,
-synchronous steps, median of 10)."""
+N = 1, 2, 4, 8 on one GPU: what each rank of the driver's scaling run computes (device arrays;
+`ms` = median of 10 synchronous calls, `async_ms` = 30 calls back to back / 30, as bench.py's timed
+loop runs them)."""
 import json
 import sys
 import time
@@ -33,7 +34,15 @@ def main():
             if k >= 3:
                 ts.append(time.perf_counter() - t0)
         ms = float(np.median(ts)) * 1e3
-        print(json.dumps({"ranks": n, "queries_per_rank": cnt, "ms": round(ms, 3),
+        # back to back, as bench.py's timed loop runs a rank's steps (no synchronisation per step)
+        steps = 30
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            D.match_l2(qs, td, idx, d1, idx2, d2)
+        torch.cuda.synchronize()
+        ams = (time.perf_counter() - t0) / steps * 1e3
+        print(json.dumps({"ranks": n, "queries_per_rank": cnt, "ms": round(ms, 3), "async_ms": round(ams, 3),
                           "tflops_per_rank": round(2 * cnt * 50_000 * 128 / (ms * 1e-3) / 1e12, 1)}), flush=True)
 
 
