@@ -64,6 +64,7 @@ I8_MFMA_PEAK_TOPS = 2 * F16_MFMA_PEAK_TF   # MI355X_MICROARCH.md: i8 32x32x32 at
 H_FLOPS_PER_EVAL = 25
 SAMPSON_FLOPS_PER_EVAL = 34
 HAM_OPS_PER_PAIR = 24
+MATCHER_PROF_STRIDE = 5       # matchers: HIP events around every 5th GEMM launch of the timed loop
 # Issue models (secondary: what the kernels' instruction streams allow at 2.4 GHz, SIMD cycles per
 # 64 evaluations; measured issue costs: VOP3/VOP3P 4 cycles, VOP2/VOPC e32 2, transcendental 8):
 #   Sampson prefilter (F, E): 56 per (model, correspondence); Hamming 58 per pair. The homography
@@ -228,7 +229,9 @@ def bench_matcher(args):
         step()
     torch.cuda.synchronize()
     NL.lib().mcvProfileReset()
-    NL.lib().mcvProfileEnable(1)
+    # every MATCHER_PROF_STRIDE-th GEMM launch is timed: an event pair costs the stream ~3 us each way,
+    # which a 36 us Hamming step would otherwise carry on every step (scripts/exp/ham_gap.py)
+    NL.lib().mcvProfileEnable(MATCHER_PROF_STRIDE)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -257,7 +260,8 @@ def bench_matcher(args):
             mfma_roof = {"bound": "mfma-i8", "achieved": 2.0 * kp * ach / 1e12, "peak": I8_MFMA_PEAK_TOPS,
                          "unit": "Tops/s", "frac": 2.0 * kp * ach / 1e12 / I8_MFMA_PEAK_TOPS,
                          "traffic": load_traffic("mcv_hamming_mfma", f"{nq}x{nt}"), "kernel": "mcv_hamming_mfma",
-                         "avg_launch_ms": avg_ms,
+                         "avg_launch_ms": avg_ms, "timed_launches": launches,
+                         "timed_every": MATCHER_PROF_STRIDE,
                          "model": "Hamming as a +-1 int8 GEMM: [nt x 256] x [256 x nq] on v_mfma_i32_32x32x32_i8 "
                                   "(2 x 256 int8 ops per pair; sum a b = 256 - 2 ham), exact in int32; the "
                                   f"popcount view: {HAM_OPS_PER_PAIR * ach / 1e12:.1f} of {INT32_PEAK_TOPS:.1f} "
@@ -297,7 +301,8 @@ def bench_matcher(args):
             else:
                 roof = {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                         "frac": tf / FP32_MFMA_PEAK_TF, "kernel": "mcv_l2_mfma"}
-            roof.update({"traffic": load_traffic(roof["kernel"], f"{nq}x{nt}"), "avg_launch_ms": avg_ms})
+            roof.update({"traffic": load_traffic(roof["kernel"], f"{nq}x{nt}"), "avg_launch_ms": avg_ms,
+                         "timed_launches": launches, "timed_every": MATCHER_PROF_STRIDE})
             line = {"metric": "BF L2 knn-2 TFLOP/s, SIFT-128 50k x 50k fp32 GEMM on MFMA (BASELINE config[4])",
                     "value": 2.0 * nq * nt * 128 * args.steps / el / 1e12, "unit": "TFLOP/s",
                     "roofline": roof,

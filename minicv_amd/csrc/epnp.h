@@ -63,6 +63,74 @@ MCV_HD double cv_hypot(double a, double b) {
 #define MCV_SVD_UNROLL
 #define MCV_SMALL_UNROLL
 #endif
+// JacobiImpl_'s sweeps for a 12 x 12 working matrix kept in the caller's storage (the EPnP generate's
+// per-lane LDS slice): row i stays in registers for its whole j loop (read once, written back once if
+// it rotated) and row j + 1's loads are issued before row j's rotation, so a pair costs one row read and
+// at most one row write of the slice and its read latency overlaps the previous pair's arithmetic.
+// The operations and their order are jacobi_svd_core's: p, the rotation and the two sums run over k in
+// order, W[i] / W[j] are read and written at the same points, and a row is stored only where the
+// generic loop would have changed it.
+MCV_HD void jacobi_sweeps_rowreg(double (&A)[12][12], double (&W)[12]) {
+    const double eps = kDblEpsilon * 10;
+    for (int iter = 0; iter < 30; ++iter) {
+        bool changed = false;
+        for (int i = 0; i < 11; ++i) {
+            double ri[12], rj[12];
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 12; ++k) ri[k] = A[i][k];
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 12; ++k) rj[k] = A[i + 1][k];
+            double wi = W[i];
+            bool iRot = false;
+            for (int j = i + 1; j < 12; ++j) {
+                double rn[12];
+                const int jn = j + 1 < 12 ? j + 1 : j;   // the last pair re-reads its own row (unused)
+                MCV_SMALL_UNROLL
+                for (int k = 0; k < 12; ++k) rn[k] = A[jn][k];
+                double a = wi, b = W[j], p = 0;
+                MCV_SMALL_UNROLL
+                for (int k = 0; k < 12; ++k) p += ri[k] * rj[k];
+                if (!(__builtin_fabs(p) <= eps * __builtin_sqrt(a * b))) {
+                    p *= 2;
+                    const double beta = a - b, gamma = cv_hypot(p, beta);
+                    double c, s;
+                    if (beta < 0) {
+                        const double delta = (gamma - beta) * 0.5;
+                        s = __builtin_sqrt(delta / gamma);
+                        c = p / (gamma * s * 2);
+                    } else {
+                        c = __builtin_sqrt((gamma + beta) / (gamma * 2));
+                        s = p / (gamma * c * 2);
+                    }
+                    a = b = 0;
+                    MCV_SMALL_UNROLL
+                    for (int k = 0; k < 12; ++k) {
+                        const double t0 = c * ri[k] + s * rj[k];
+                        const double t1 = -s * ri[k] + c * rj[k];
+                        ri[k] = t0;
+                        rj[k] = t1;
+                        a += t0 * t0;
+                        b += t1 * t1;
+                    }
+                    wi = a;
+                    W[j] = b;
+                    changed = true;
+                    iRot = true;
+                    MCV_SMALL_UNROLL
+                    for (int k = 0; k < 12; ++k) A[j][k] = rj[k];
+                }
+                MCV_SMALL_UNROLL
+                for (int k = 0; k < 12; ++k) rj[k] = rn[k];
+            }
+            W[i] = wi;
+            if (iRot)
+                MCV_SMALL_UNROLL
+                for (int k = 0; k < 12; ++k) A[i][k] = ri[k];
+        }
+        if (!changed) break;
+    }
+}
+
 template <int M, int N, int N1, bool HASV>
 MCV_HD void jacobi_svd_core(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
     constexpr int SU = N <= 6 ? 16 : 1;
@@ -78,51 +146,55 @@ MCV_HD void jacobi_svd_core(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]
             MCV_SMALL_UNROLL
             for (int k = 0; k < N; ++k) Vt[i][k] = k == i ? 1.0 : 0.0;
     }
-    const int maxIter = M > 30 ? M : 30;
-    for (int iter = 0; iter < maxIter; ++iter) {
-        bool changed = false;
-        MCV_SVD_UNROLL
-        for (int i = 0; i < N - 1; ++i)
+    if constexpr (M == 12 && N == 12 && N1 == 12 && !HASV) {
+        jacobi_sweeps_rowreg(A, W);   // EPnP's M^T M: the working matrix in the caller's (LDS) storage
+    } else {
+        const int maxIter = M > 30 ? M : 30;
+        for (int iter = 0; iter < maxIter; ++iter) {
+            bool changed = false;
             MCV_SVD_UNROLL
-            for (int j = i + 1; j < N; ++j) {
-                double a = W[i], b = W[j], p = 0;
-                MCV_SMALL_UNROLL
-                for (int k = 0; k < M; ++k) p += A[i][k] * A[j][k];
-                if (__builtin_fabs(p) <= eps * __builtin_sqrt(a * b)) continue;
-                p *= 2;
-                const double beta = a - b, gamma = cv_hypot(p, beta);
-                double c, s;
-                if (beta < 0) {
-                    const double delta = (gamma - beta) * 0.5;
-                    s = __builtin_sqrt(delta / gamma);
-                    c = p / (gamma * s * 2);
-                } else {
-                    c = __builtin_sqrt((gamma + beta) / (gamma * 2));
-                    s = p / (gamma * c * 2);
-                }
-                a = b = 0;
-                MCV_SMALL_UNROLL
-                for (int k = 0; k < M; ++k) {
-                    const double t0 = c * A[i][k] + s * A[j][k];
-                    const double t1 = -s * A[i][k] + c * A[j][k];
-                    A[i][k] = t0;
-                    A[j][k] = t1;
-                    a += t0 * t0;
-                    b += t1 * t1;
-                }
-                W[i] = a;
-                W[j] = b;
-                changed = true;
-                if constexpr (HASV)
+            for (int i = 0; i < N - 1; ++i)
+                MCV_SVD_UNROLL
+                for (int j = i + 1; j < N; ++j) {
+                    double a = W[i], b = W[j], p = 0;
                     MCV_SMALL_UNROLL
-                    for (int k = 0; k < N; ++k) {
-                        const double t0 = c * Vt[i][k] + s * Vt[j][k];
-                        const double t1 = -s * Vt[i][k] + c * Vt[j][k];
-                        Vt[i][k] = t0;
-                        Vt[j][k] = t1;
+                    for (int k = 0; k < M; ++k) p += A[i][k] * A[j][k];
+                    if (__builtin_fabs(p) <= eps * __builtin_sqrt(a * b)) continue;
+                    p *= 2;
+                    const double beta = a - b, gamma = cv_hypot(p, beta);
+                    double c, s;
+                    if (beta < 0) {
+                        const double delta = (gamma - beta) * 0.5;
+                        s = __builtin_sqrt(delta / gamma);
+                        c = p / (gamma * s * 2);
+                    } else {
+                        c = __builtin_sqrt((gamma + beta) / (gamma * 2));
+                        s = p / (gamma * c * 2);
                     }
-            }
-        if (!changed) break;
+                    a = b = 0;
+                    MCV_SMALL_UNROLL
+                    for (int k = 0; k < M; ++k) {
+                        const double t0 = c * A[i][k] + s * A[j][k];
+                        const double t1 = -s * A[i][k] + c * A[j][k];
+                        A[i][k] = t0;
+                        A[j][k] = t1;
+                        a += t0 * t0;
+                        b += t1 * t1;
+                    }
+                    W[i] = a;
+                    W[j] = b;
+                    changed = true;
+                    if constexpr (HASV)
+                        MCV_SMALL_UNROLL
+                        for (int k = 0; k < N; ++k) {
+                            const double t0 = c * Vt[i][k] + s * Vt[j][k];
+                            const double t1 = -s * Vt[i][k] + c * Vt[j][k];
+                            Vt[i][k] = t0;
+                            Vt[j][k] = t1;
+                        }
+                }
+            if (!changed) break;
+        }
     }
     MCV_SVD_UNROLL
     for (int i = 0; i < N; ++i) {

@@ -446,12 +446,9 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         wk.part.ensure((size_t)nchunks * nq);
         {
             ProfScope ps("hamming", s);
-#define MCV_HAM_GEMM(W_, Q_, S_) hipLaunchKernelGGL((mcv_hamming_mfma<W_, Q_, WPB, S_>), dim3(qblocks, nchunks), \
-                                                    dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, tilesPerChunk, wk.part.p, \
-                                                    xcdMap)
-            if (W == 8) MCV_HAM_GEMM(8, QT, SUB);
-            else MCV_HAM_GEMM(16, QT, SUB);
-#undef MCV_HAM_GEMM
+            hipLaunchKernelGGL((W == 8 ? mcv_hamming_mfma<8, QT, WPB, SUB> : mcv_hamming_mfma<16, QT, WPB, SUB>),
+                               dim3(qblocks, nchunks), dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, tilesPerChunk,
+                               wk.part.p, xcdMap);
         }
         hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nchunks, d_idx,
                            d_dist, d_idx2, d_dist2);
@@ -471,12 +468,11 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     const int nparts = (nchunks + 3) / 4;
     wk.part.ensure((size_t)nparts * nq);
     dim3 grid(qwaves, nparts);
-    ProfScope ps("hamming", s);
-#define MCV_HAM_LAUNCH(W_, Q_, NB_) \
-    hipLaunchKernelGGL((mcv_hamming_partial<W_, Q_, NB_>), grid, dim3(256), 0, s, q, nq, t, nt, chunkLen, wk.part.p)
-    if (W == 8) MCV_HAM_LAUNCH(8, Q, NB);
-    else MCV_HAM_LAUNCH(16, Q, NB);
-#undef MCV_HAM_LAUNCH
+    {
+        ProfScope ps("hamming", s);
+        hipLaunchKernelGGL((W == 8 ? mcv_hamming_partial<8, Q, NB> : mcv_hamming_partial<16, Q, NB>), grid, dim3(256),
+                           0, s, q, nq, t, nt, chunkLen, wk.part.p);
+    }
     hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nparts, d_idx,
                        d_dist, d_idx2, d_dist2);
     MCV_HIP(hipGetLastError());

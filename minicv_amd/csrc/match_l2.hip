@@ -1431,12 +1431,8 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
         if (f16) {
             const L2GemmArgs ga{wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, d_q, d_t, wk.tn.p, nq, nt, dim, ntTiles,
                                 tilesPerChunk, nqPad, wk.part.p, dom, (8 % nchunks) == 0};
-            const dim3 grid(qblocks, nchunks);
-            switch (DP) {
-                case 32: hipLaunchKernelGGL(mcv_l2_gemm<32>, grid, dim3(256), 0, s, ga); break;
-                case 64: hipLaunchKernelGGL(mcv_l2_gemm<64>, grid, dim3(256), 0, s, ga); break;
-                default: hipLaunchKernelGGL(mcv_l2_gemm<128>, grid, dim3(256), 0, s, ga); break;
-            }
+            hipLaunchKernelGGL((DP == 32 ? mcv_l2_gemm<32> : DP == 64 ? mcv_l2_gemm<64> : mcv_l2_gemm<128>),
+                               dim3(qblocks, nchunks), dim3(256), 0, s, ga);
         } else {
             hipLaunchKernelGGL((mcv_l2_mfma<256, TR>), dim3(qblocks, nchunks), dim3(256), 0, s, wk.qp.p, wk.tp.p,
                                wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p);

@@ -118,7 +118,11 @@ inline void reduce_to_host(Plan& P, hipStream_t s, int V, double* out, F launch)
 }
 
 // Opt-in kernel timing with HIP events recorded on the launch stream (bench.py's live roofline).
+// mcvProfileEnable(n): every n-th launch of each named scope is timed (n = 1: all of them). An event
+// pair costs the stream ~3 us each way, 17 % of the 36 us cfg2 Hamming step when every launch is
+// timed (scripts/exp/ham_gap.py); a sample keeps the average launch duration and not that cost.
 bool prof_enabled();
+bool prof_sample(const char* name);   // prof_enabled() and this launch is one of the sampled ones
 void prof_record(const char* name, hipEvent_t a, hipEvent_t b);
 hipEvent_t prof_event();   // a timing event (reused across mcvProfileReset)
 struct ProfScope {
@@ -126,7 +130,7 @@ struct ProfScope {
     hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
     ProfScope(const char* n, hipStream_t st) : name(n), s(st) {
-        if (prof_enabled() && (a = prof_event()) && (b = prof_event())) (void)hipEventRecord(a, s);
+        if (prof_sample(n) && (a = prof_event()) && (b = prof_event())) (void)hipEventRecord(a, s);
     }
     ~ProfScope() {
         if (a && b) {

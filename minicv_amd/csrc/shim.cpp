@@ -26,10 +26,19 @@ std::mutex g_prof_mu;
 std::vector<ProfRec> g_prof;
 std::vector<hipEvent_t> g_prof_free;   // events of earlier records, reused (hipEventCreate per launch
                                        // costs microseconds of host time inside a timed loop)
-bool g_prof_on = false;
+int g_prof_on = 0;   // 0 off, else the sampling stride
+std::vector<std::pair<std::string, long>> g_prof_ticks;   // launches seen per scope name
 }  // namespace
 namespace mcv {
-bool prof_enabled() { return g_prof_on; }
+bool prof_enabled() { return g_prof_on != 0; }
+bool prof_sample(const char* name) {
+    if (!g_prof_on) return false;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (auto& t : g_prof_ticks)
+        if (t.first == name) return t.second++ % g_prof_on == 0;
+    g_prof_ticks.push_back({name, 1});
+    return true;
+}
 hipEvent_t prof_event() {
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -48,7 +57,7 @@ void prof_record(const char* name, hipEvent_t a, hipEvent_t b) {
 }
 }  // namespace mcv
 
-extern "C" MCV_API void mcvProfileEnable(int on) { g_prof_on = on != 0; }
+extern "C" MCV_API void mcvProfileEnable(int on) { g_prof_on = on > 0 ? on : 0; }
 
 extern "C" MCV_API void mcvProfileReset(void) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -58,6 +67,7 @@ extern "C" MCV_API void mcvProfileReset(void) {
         g_prof_free.push_back(r.b);
     }
     g_prof.clear();
+    g_prof_ticks.clear();
 }
 
 extern "C" MCV_API int mcvProfileRead(const char* name, double* total_ms) {
