@@ -488,9 +488,10 @@ MCV_API void mcvHostRodriguesInv(const double* R, double* r);
  * PnP: no check, pts4 may be NULL). Rows from the first failed getSubset on are -1. Returns the number
  * of accepted rows, -1 on bad arguments. */
 MCV_API int64_t mcvCvSubsets(int model, int m, const float* pts4, int N, int64_t rows, int* out);
-/* glibc_math.h's restatements over arrays: fn 0 cbrt(a), 1 hypot(a, b), 2 the real part of clog(a + i b)
- * (glibc's branch structure; log / log1p of the host libm), 3 a^2 + b^2 - 1 (glibc's __x2y2m1).
- * Returns n, -1 on bad arguments. */
+/* glibc_math.h's restatements over arrays: fn 0 cbrt(a), 1 hypot(a, b), 2 the real part of clog(a + i b),
+ * 3 a^2 + b^2 - 1 (glibc's __x2y2m1), 4 exp(a), 5 log(a), 6 log1p(a), 7 cos(a), 8 atan2(a, b) — glibc
+ * 2.35's x86_64 (FMA multiarch) code paths, restated so the device computes AP3P's complex cube root
+ * bit-identically to the reference's std::pow. Returns n, -1 on bad arguments. */
 MCV_API int mcvHostGlibcMath(int fn, const double* a, const double* b, int n, double* out);
 /* The plan guards' fingerprint (mcv_common.h fp_term summed over the 32-bit words) of a host buffer:
  * the device kernel gives the same value for the same bytes. */

@@ -122,7 +122,6 @@ void cv_table_upload(Plan& P, const std::vector<int>& t, int m, int64_t rows, in
     P.subsetRows = rows;
     P.subsetM = m;
     P.subsetN = N;
-    if (P.model == MCV_MODEL_PNP) P.h_subsets.assign(t.begin(), t.begin() + (size_t)m * rows);
     P.subsetFp = pointsFp;
     P.last.clear();
 }

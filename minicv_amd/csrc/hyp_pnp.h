@@ -284,9 +284,9 @@ MCV_HD Cplx cplx_div(Cplx a, Cplx b) {
 }
 
 // factors: a4, a3, a2, a1, a0 (descending, as solveQuartic reads them). cplx (optional) is set when the
-// resolvent's w is complex: pow(w, 1/3) then runs clog / exp / cos / atan2, glibc's table-driven
-// functions, which the device does not restate (its own ocml ones return other last bits), so the device
-// kernels hand those solves to the host (kStatusHostSolve); every other step is glibc's bit for bit.
+// resolvent's w is complex: pow(w, 1/3) then runs glibc's clog / exp / cos / atan2 through libstdc++,
+// restated with glibc's tables and its FMA build's operation order in glibc_math.h (as are cbrt and
+// csqrt's hypot on the real branch), so every step is glibc's bit for bit on the device too.
 MCV_HD void ap3p_solve_quartic(const double* f, double* roots, bool* cplx = nullptr) {
     const double a4 = f[0], a3 = f[1], a2 = f[2], a1 = f[3], a0 = f[4];
     const double a4_2 = a4 * a4, a3_2 = a3 * a3, a4_3 = a4_2 * a4, a2a4 = a2 * a4;
@@ -305,11 +305,11 @@ MCV_HD void ap3p_solve_quartic(const double* f, double* roots, bool* cplx = null
         const double wr = glibc_cbrt(w.re);   // glibc's bits (glibc_math.h)
         t = 2.0 * (wr + p3 / wr);
     } else {
-        // pow(w, 1 / 3) = polar(exp(log|w| / 3), arg(w) / 3) (libstdc++), log|w| = clog's real part with
-        // glibc's branches; log / log1p / exp / cos / atan2 are the device's own (see glibc_clog_re)
+        // pow(w, 1 / 3) = polar(exp(log|w| / 3), arg(w) / 3) (libstdc++): clog's real part (glibc's
+        // branches, log / log1p / hypot), its imaginary part atan2, then exp and cos (glibc_math.h)
         const double third = 1.0 / 3;
-        const double lr = glibc_clog_re(w.re, w.im), li = atan2(w.im, w.re);
-        t = 4.0 * (exp(third * lr) * cos(third * li));
+        const double lr = glibc_clog_re(w.re, w.im), li = glibc_atan2(w.im, w.re);
+        t = 4.0 * (glibc_exp(third * lr) * glibc_cos(third * li));
     }
     const Cplx sqrt_2m = cplx_sqrt(-2 * p4 / 3 + t, 0.0);
     const double B_4A = -a3 / (4 * a4);
@@ -356,8 +356,8 @@ MCV_HD int ap3p_compute_poses_ref(const double (*b)[3], const double (*w)[3], do
 // computePoses with the reference's own quartic path (solveQuartic + polishQuarticRoots, ap3p.cpp:203-204):
 // the four polished Ferrari roots in order, |cos| > 1 skipped (a NaN root is not: as in the reference,
 // it yields a NaN pose, which counts no inliers), poses appended through selects (register-resident).
-// The RANSAC kernel's default; its transcendentals (cbrt, log, atan2, exp, cos, hypot) are the device's
-// own on the GPU and glibc's on the host.
+// The RANSAC kernel's default; its transcendentals (cbrt, log, log1p, atan2, exp, cos, hypot) are glibc's
+// restated (glibc_math.h), on the GPU and in the host twin alike.
 MCV_HD int ap3p_compute_poses_ferrari(const double (*b)[3], const double (*w)[3], double (*Rr)[9], double (*tr)[3],
                                       bool* cplx = nullptr) {
     Ap3pSetup S;
@@ -498,8 +498,7 @@ MCV_HD int pnp_ap3p4_cv(const PnpCamera& c, const double* x, const double* y, co
 
 // One hypothesis: 4 distinct indices, undistort, AP3P + 4th-point selection: OpenCV's chain
 // (pnp_ap3p4_cv, default) or, with fast (MCV_FLAG_FAST_MINIMAL), the real-root-finder form (pnp_ap3p4).
-// Returns 1 (model), kStatusNoModel or kStatusNoSample; on the device also kStatusHostSolve (the
-// reference's quartic takes the complex-pow branch: ap3p_solve_quartic).
+// Returns 1 (model), kStatusNoModel or kStatusNoSample.
 MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
                           PnpPose& pose, int* idx_out, bool fast = false) {
     SubsetSrc<4> src(smp, hyp);
@@ -520,12 +519,7 @@ MCV_HD int pnp_hypothesis(const PnpPoint* pts, int N, const PnpCamera& c, const 
         W[i][0] = p.X; W[i][1] = p.Y; W[i][2] = p.Z;
     }
     if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
-    bool cplx = false;
-    const int ok = fast ? pnp_ap3p4(c, x, y, W, pose) : pnp_ap3p4_cv(c, x, y, W, pose, &cplx);
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (cplx) return kStatusHostSolve;   // glibc's complex pow: the host solves this hypothesis
-#endif
-    (void)cplx;
+    const int ok = fast ? pnp_ap3p4(c, x, y, W, pose) : pnp_ap3p4_cv(c, x, y, W, pose);
     return ok ? 1 : kStatusNoModel;
 }
 

@@ -132,16 +132,12 @@ struct Ap3pOut {
     double R[4][9];
     double t[4][3];
     int count;
-    int cplx;   // the quartic took the complex-pow branch: the host recomputes (glibc)
+    int cplx;   // the quartic took the complex-pow branch (glibc's clog / exp / cos / atan2, restated)
 };
 void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_pts, hipStream_t s);
 // fast (MCV_FLAG_FAST_MINIMAL): the AP3P kernel's real-root-finder quartic instead of the reference's Ferrari
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
-                         bool epnp, void* d_models, int* d_counts, hipStream_t s, bool fast = false,
-                         int* d_hsolve = nullptr);
-// host-solved hypotheses (poses12: 12 doubles each) into the chunk's model / count buffers
-void launch_pnp_scatter(const int* d_list, int n, const double* d_poses12, const int* d_status, void* d_models,
-                        int* d_counts, hipStream_t s);
+                         bool epnp, void* d_models, int* d_counts, hipStream_t s, bool fast = false);
 // d_ext: 3 doubles of device scratch filled by launch_pnp_extent (the certified sweep's bound).
 void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s);
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,

@@ -135,7 +135,6 @@ struct SubsetSrc {
 static const int kStatusNoModel = -1;   // minimal solver degenerate -> OpenCV `continue`
 static const int kStatusNoSample = -2;  // sampler exhausted attempts -> OpenCV `break`
 static const int kStatusRedo = -3;      // packed H sweep: count this slot again with the exact sweep
-static const int kStatusHostSolve = -4; // AP3P: the Ferrari resolvent took the complex branch; the host solves it
 static const int kF7Slots = 3;          // 7-point fundamental (run7Point): model slots per hypothesis
 
 static const double kDblEpsilon = 2.2204460492503131e-16;

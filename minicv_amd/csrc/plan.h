@@ -83,14 +83,6 @@ struct Plan {
     uint64_t subsetFp = 0;    // H / F: fingerprint of the points whose checkSubset accepted the rows
     DevBuf<uint64_t> fp;      // [0] the last chunk's points (mark_chunk), [1] the points at finalize / check
     PinnedBuf<uint64_t> h_fp;
-    std::vector<int> h_subsets;   // host copy of `subsets` (the host's AP3P solves read their rows)
-    DevBuf<int> hsolve;           // PnP: [0] count, then the hypotheses handed to the host (kStatusHostSolve)
-    PinnedBuf<int> h_hsolve;
-    DevBuf<double> hposes;        // ... their host-solved poses (12 doubles) and statuses
-    PinnedBuf<double> h_hposes;
-    DevBuf<int> hstatus;
-    PinnedBuf<int> h_hstatus;
-    PinnedBuf<float> h_pnp;       // host copy of the PnP points for those solves
     Sampler sampler(const RansacConfig& cfg) const;
     PinnedBuf<int> h_counts;
     PinnedBuf<double> h_red;

@@ -20,7 +20,6 @@
 #include <cmath>
 #include <cfloat>
 #include <cstring>
-#include <thread>
 #include <algorithm>
 #include <vector>
 #include <algorithm>
@@ -122,93 +121,12 @@ static bool fused_pnp(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FU
 static bool fast_ap3p(const RansacConfig& cfg) { return (cfg.flags & MCV_FLAG_FAST_MINIMAL) != 0; }
 bool pnp_cfg_epnp(const RansacConfig& cfg) { return pnp_kind_epnp(pnp_kind(cfg.pnpKind)); }
 
-// ---- AP3P hypotheses whose Ferrari resolvent takes the complex-pow branch --------------------------
-// The reference's pow(w, 1/3) runs glibc's clog / exp / cos / atan2 (ap3p.cpp:35-41 through libstdc++).
-// glibc implements those with tables and argument-dependent paths that the device does not restate, so
-// the device kernels hand these solves (1-2 % of AP3P hypotheses on the benchmark data; every other
-// step of the quartic is restated, glibc_math.h) to the host, where the same hypothesis code
-// (pnp_hypothesis, host-compiled) calls the host's glibc: the reference's bits. The host threads
-// split the list; the poses go back to the device before the sweep.
-static PnpCamera host_cam(const Plan& P) {
-    return PnpCamera{P.pnpCam[0], P.pnpCam[1], P.pnpCam[2], P.pnpCam[3],
-                     P.pnpCam[4], P.pnpCam[5], P.pnpCam[6], P.pnpCam[7]};
-}
-
-template <class F>
-static void host_parallel(int n, F body) {
-    static const int hw = [] {
-        const char* e = getenv("MCV_HOST_THREADS");
-        const int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
-        return std::max(1, std::min(v, 32));
-    }();
-    const int nt = std::max(1, std::min(hw, (n + 31) / 32));
-    if (nt == 1) {
-        for (int k = 0; k < n; ++k) body(k);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t)
-        th.emplace_back([&, t] {
-            for (int k = t; k < n; k += nt) body(k);
-        });
-    for (auto& x : th) x.join();
-}
-
-// Solve hypotheses hypBegin + list[k] (k < n) on the host: poses12 / status per k.
-static void pnp_host_solve(Plan& P, const void* d_pts, int N, const Sampler& smp, int64_t hypBegin, const int* list,
-                           int n, double* poses12, int* status, hipStream_t s) {
-    P.h_pnp.ensure((size_t)N * 8);
-    MCV_HIP(hipMemcpyAsync(P.h_pnp.p, d_pts, (size_t)N * sizeof(PnpPoint), hipMemcpyDeviceToHost, s));
-    MCV_HIP(hipStreamSynchronize(s));
-    if (smp.table && P.h_subsets.size() < (size_t)4 * (size_t)P.subsetRows) fail("AP3P host solve: no host subset table");
-    const Sampler hs{smp.seed, smp.table ? P.h_subsets.data() : nullptr};
-    const PnpCamera cam = host_cam(P);
-    const PnpPoint* pts = reinterpret_cast<const PnpPoint*>(P.h_pnp.p);
-    host_parallel(n, [&](int k) {
-        PnpPose pose;
-        for (int j = 0; j < 9; ++j) pose.R[j] = 0;
-        for (int j = 0; j < 3; ++j) pose.t[j] = 0;
-        status[k] = pnp_hypothesis(pts, N, cam, hs, (uint64_t)(hypBegin + list[k]), pose, nullptr, false);
-        for (int j = 0; j < 9; ++j) poses12[12 * (size_t)k + j] = pose.R[j];
-        for (int j = 0; j < 3; ++j) poses12[12 * (size_t)k + 9 + j] = pose.t[j];
-    });
-}
-
-// After an AP3P generate with the hsolve list: solve the listed hypotheses on the host and scatter them
-// into the chunk's buffers (synchronises s; a no-op round trip of 4 bytes when the list is empty).
-static void pnp_resolve_host(Plan& P, const void* d_pts, int N, const Sampler& smp, int64_t hypBegin, void* d_models,
-                             int* d_counts, hipStream_t s) {
-    P.h_hsolve.ensure(1);
-    MCV_HIP(hipMemcpyAsync(P.h_hsolve.p, P.hsolve.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    MCV_HIP(hipStreamSynchronize(s));
-    const int n = P.h_hsolve.p[0];
-    if (n <= 0) return;
-    P.h_hsolve.ensure((size_t)n + 1);
-    MCV_HIP(hipMemcpyAsync(P.h_hsolve.p + 1, P.hsolve.p + 1, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, s));
-    P.h_hposes.ensure((size_t)n * 12);
-    P.h_hstatus.ensure((size_t)n);
-    pnp_host_solve(P, d_pts, N, smp, hypBegin, P.h_hsolve.p + 1, n, P.h_hposes.p, P.h_hstatus.p, s);
-    P.hposes.ensure((size_t)n * 12);
-    P.hstatus.ensure((size_t)n);
-    MCV_HIP(hipMemcpyAsync(P.hposes.p, P.h_hposes.p, (size_t)n * 12 * sizeof(double), hipMemcpyHostToDevice, s));
-    MCV_HIP(hipMemcpyAsync(P.hstatus.p, P.h_hstatus.p, (size_t)n * sizeof(int), hipMemcpyHostToDevice, s));
-    launch_pnp_scatter(P.hsolve.p + 1, n, P.hposes.p, P.hstatus.p, d_models, d_counts, s);
-    MCV_HIP(hipGetLastError());
-}
-
-// AP3P generate with the host hand-off (the default, reference-arithmetic path; the opt-in fast solver and
-// EPnP never take it).
+// AP3P / EPnP generate: every hypothesis on the device, the reference's arithmetic included (AP3P's
+// complex-pow branch runs glibc's clog / exp / cos / atan2 as restated in glibc_math.h).
 static void pnp_generate_exact(Plan& P, const void* d_pts, int N, const Sampler& smp, int64_t hypBegin, int hypCount,
                                bool epnp, bool fast, void* d_models, int* d_counts, hipStream_t s) {
-    const bool hand = !epnp && !fast;
-    if (hand) {
-        P.hsolve.ensure((size_t)hypCount + 1);
-        MCV_HIP(hipMemsetAsync(P.hsolve.p, 0, sizeof(int), s));
-    }
-    launch_pnp_generate(d_pts, N, P.pnpCam, smp, hypBegin, hypCount, epnp, d_models, d_counts, s, fast,
-                        hand ? P.hsolve.p : nullptr);
+    launch_pnp_generate(d_pts, N, P.pnpCam, smp, hypBegin, hypCount, epnp, d_models, d_counts, s, fast);
     MCV_HIP(hipGetLastError());
-    if (hand) pnp_resolve_host(P, d_pts, N, smp, hypBegin, d_models, d_counts, s);
 }
 
 void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64_t hypBegin, int hypCount,
@@ -498,13 +416,6 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
         launch_pnp_one(d_pts, N, P.pnpCam, smp, hyp, epnp, (PnpOneOut*)P.one.p, s, fast_ap3p(cfg));
         MCV_HIP(hipGetLastError());
         one = pnp_fetch_one(P, s);
-        if (one.status == kStatusHostSolve) {   // the complex-pow branch: glibc's bits from the host
-            const int zero = 0;
-            double p12[12];
-            pnp_host_solve(P, d_pts, N, smp, hyp, &zero, 1, p12, &one.status, s);
-            for (int k = 0; k < 9; ++k) one.R[k] = p12[k];
-            for (int k = 0; k < 3; ++k) one.t[k] = p12[9 + k];
-        }
     }
     if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
     const int count = pnp_mask_count(P, d_pts, N, cfg, one.R, one.t, d_mask, s);
@@ -521,30 +432,6 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
     }
     for (int k = 0; k < 3; ++k) { model9[k] = r[k]; model9[3 + k] = t[k]; model9[6 + k] = 0; }
     return count;
-}
-
-// The N == 4 solve (mcv_pnp_solve4) on the host, for the complex-pow branch of its quartic.
-static PnpOneOut pnp_solve4_host(Plan& P, hipStream_t s) {
-    PnpPoint q[4];
-    MCV_HIP(hipMemcpyAsync(P.h_one.p, P.ptsd.p, sizeof(q), hipMemcpyDeviceToHost, s));
-    MCV_HIP(hipStreamSynchronize(s));
-    std::memcpy(q, P.h_one.p, sizeof(q));
-    const PnpCamera cam = host_cam(P);
-    double x[4], y[4], W[4][3];
-    for (int i = 0; i < 4; ++i) {
-        pnp_undistort(cam, (double)q[i].u, (double)q[i].v, x[i], y[i]);
-        W[i][0] = q[i].X; W[i][1] = q[i].Y; W[i][2] = q[i].Z;
-    }
-    PnpPose p;
-    for (int k = 0; k < 9; ++k) p.R[k] = 0;
-    for (int k = 0; k < 3; ++k) p.t[k] = 0;
-    PnpOneOut one;
-    one.status = pnp_ap3p4_cv(cam, x, y, W, p) ? 1 : kStatusNoModel;
-    for (int k = 0; k < 9; ++k) one.R[k] = p.R[k];
-    for (int k = 0; k < 3; ++k) one.t[k] = p.t[k];
-    for (int k = 0; k < 4; ++k) one.idx[k] = k;
-    one.idx[4] = -1;
-    return one;
 }
 
 struct PnpResult {
@@ -567,7 +454,6 @@ static PnpResult pnp_ransac(Plan& P, const mcvV2d* img, const mcvV3d* world, int
         else launch_pnp_solve5(P.ptsd.p, P.pnpCam, (PnpOneOut*)P.one.p, s);
         MCV_HIP(hipGetLastError());
         PnpOneOut one = pnp_fetch_one(P, s);
-        if (one.status == kStatusHostSolve) one = pnp_solve4_host(P, s);   // complex-pow branch: glibc's bits
         if (one.status != 1) return res;
         rodrigues_inv(one.R, res.r);
         for (int k = 0; k < 3; ++k) res.t[k] = one.t[k];
@@ -823,14 +709,6 @@ extern "C" MCV_API int solveAp3p(mcvM33d* Rs, mcvV3d* ts, double mu0, double mv0
         MCV_HIP(hipMemcpyAsync(P.h_one.p, P.one.p, sizeof(Ap3pOut), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
         std::memcpy(&out, P.h_one.p, sizeof(Ap3pOut));
-        if (out.cplx) {   // the complex-pow branch: the same computation with the host's glibc
-            double R36[36], t12[12];
-            out.count = mcvHostSolveAp3p(in.mu, in.mv, &in.W[0][0], inv_fx, inv_fy, cx_fx, cy_fy, R36, t12);
-            for (int k = 0; k < out.count; ++k) {
-                for (int j = 0; j < 9; ++j) out.R[k][j] = R36[9 * k + j];
-                for (int j = 0; j < 3; ++j) out.t[k][j] = t12[3 * k + j];
-            }
-        }
         for (int k = 0; k < out.count; ++k) {
             for (int j = 0; j < 9; ++j) Rs[k].M[j] = out.R[k][j];
             ts[k].X = out.t[k][0]; ts[k].Y = out.t[k][1]; ts[k].Z = out.t[k][2];
@@ -1028,11 +906,22 @@ extern "C" MCV_API int mcvHostPnpCert(const float* pts, int N, const double* cam
 
 
 // Test hook: the glibc restatements of glibc_math.h over arrays (fn 0 cbrt(a), 1 hypot(a, b),
-// 2 clog's real part of a + i b, 3 x^2 + y^2 - 1). Returns n, -1 on a bad fn.
+// 2 clog's real part of a + i b, 3 x^2 + y^2 - 1, 4 exp(a), 5 log(a), 6 log1p(a), 7 cos(a),
+// 8 atan2(a, b)). Returns n, -1 on a bad fn.
 extern "C" MCV_API int mcvHostGlibcMath(int fn, const double* a, const double* b, int n, double* out) {
-    if (fn < 0 || fn > 3 || n < 0 || !a || !out || (fn > 0 && !b)) return -1;
-    for (int i = 0; i < n; ++i)
-        out[i] = fn == 0 ? glibc_cbrt(a[i]) : fn == 1 ? glibc_hypot(a[i], b[i]) : fn == 2 ? glibc_clog_re(a[i], b[i])
-                                                                                    : glibc_x2y2m1(a[i], b[i]);
+    if (fn < 0 || fn > 8 || n < 0 || !a || !out || ((fn == 1 || fn == 2 || fn == 3 || fn == 8) && !b)) return -1;
+    for (int i = 0; i < n; ++i) {
+        switch (fn) {
+            case 0: out[i] = glibc_cbrt(a[i]); break;
+            case 1: out[i] = glibc_hypot(a[i], b[i]); break;
+            case 2: out[i] = glibc_clog_re(a[i], b[i]); break;
+            case 3: out[i] = glibc_x2y2m1(a[i], b[i]); break;
+            case 4: out[i] = glibc_exp(a[i]); break;
+            case 5: out[i] = glibc_log(a[i]); break;
+            case 6: out[i] = glibc_log1p(a[i]); break;
+            case 7: out[i] = glibc_cos(a[i]); break;
+            default: out[i] = glibc_atan2(a[i], b[i]); break;
+        }
+    }
     return n;
 }

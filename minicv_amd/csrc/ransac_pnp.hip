@@ -43,13 +43,11 @@ __global__ __launch_bounds__(256) void mcv_pnp_pack(const double* __restrict__ i
 // the SVD's data-dependent row pairs went to scratch: 2.4 KB per lane at one wave per SIMD).
 static constexpr int kEpnpWsStride = 145;   // doubles per lane (12 x 12 + 1: bank spread)
 
-// hsolve (AP3P, may be null): [0] = count, then the chunk-local indices of the hypotheses whose quartic
-// went to the complex-pow branch (kStatusHostSolve: pnp_host.cpp solves them with glibc on the host).
 template <bool EPNP>
 __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
                                                        Sampler smp, int64_t hypBegin, int hypCount,
                                                        PnpPose* __restrict__ models, int* __restrict__ counts,
-                                                       bool fast, int* __restrict__ hsolve) {
+                                                       bool fast) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     PnpPose p;
@@ -66,21 +64,7 @@ __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restric
         counts[i] = 0;
     } else {
         counts[i] = st;
-        if (st == kStatusHostSolve && hsolve) hsolve[1 + atomicAdd(hsolve, 1)] = i;
     }
-}
-
-// The host's solves of listed hypotheses -> their poses and statuses (status 1 -> count slot 0).
-__global__ void mcv_pnp_scatter(const int* __restrict__ list, int n, const double* __restrict__ poses12,
-                                const int* __restrict__ status, PnpPose* __restrict__ models, int* __restrict__ counts) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= n) return;
-    const int i = list[k];
-    PnpPose p;
-    for (int j = 0; j < 9; ++j) p.R[j] = poses12[12 * (size_t)k + j];
-    for (int j = 0; j < 3; ++j) p.t[j] = poses12[12 * (size_t)k + 9 + j];
-    if (status[k] == 1) models[i] = p;
-    counts[i] = status[k] == 1 ? 0 : status[k];
 }
 
 template <int K, bool FUSED>
@@ -422,9 +406,7 @@ __global__ void mcv_pnp_solve4(const PnpPoint* __restrict__ pts, PnpCamera cam, 
     PnpPose p;
     for (int k = 0; k < 9; ++k) p.R[k] = 0;
     for (int k = 0; k < 3; ++k) p.t[k] = 0;
-    bool cplx = false;
-    out->status = (fast ? pnp_ap3p4(cam, x, y, W, p) : pnp_ap3p4_cv(cam, x, y, W, p, &cplx)) ? 1 : kStatusNoModel;
-    if (cplx) out->status = kStatusHostSolve;
+    out->status = (fast ? pnp_ap3p4(cam, x, y, W, p) : pnp_ap3p4_cv(cam, x, y, W, p)) ? 1 : kStatusNoModel;
     for (int k = 0; k < 9; ++k) out->R[k] = p.R[k];
     for (int k = 0; k < 3; ++k) out->t[k] = p.t[k];
     for (int k = 0; k < 4; ++k) out->idx[k] = k;
@@ -721,20 +703,13 @@ void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_
 }
 
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
-                         bool epnp, void* d_models, int* d_counts, hipStream_t s, bool fast, int* d_hsolve) {
+                         bool epnp, void* d_models, int* d_counts, hipStream_t s, bool fast) {
     if (epnp)
         hipLaunchKernelGGL(mcv_pnp_generate<true>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
-                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast, nullptr);
+                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast);
     else
         hipLaunchKernelGGL(mcv_pnp_generate<false>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
-                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast, d_hsolve);
-}
-
-void launch_pnp_scatter(const int* d_list, int n, const double* d_poses12, const int* d_status, void* d_models,
-                        int* d_counts, hipStream_t s) {
-    if (n <= 0) return;
-    hipLaunchKernelGGL(mcv_pnp_scatter, dim3((n + 255) / 256), dim3(256), 0, s, d_list, n, d_poses12, d_status,
-                       (PnpPose*)d_models, d_counts);
+                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast);
 }
 
 // Grid of a pose-wave x point-chunk sweep: waves x chunks >= ~8 waves per SIMD, chunks >= 2048

@@ -94,10 +94,22 @@ static _Thread_local int orc_last_branch = -1;   /* the last ferrari_ref's branc
 int orc_ap3p_last_branch(void) { return orc_last_branch; }
 
 /* glibc's own functions over arrays (the reference for glibc_math.h's restatements):
- * fn 0 cbrt(a), 1 hypot(a, b), 2 creal(clog(a + i b)). */
+ * fn 0 cbrt(a), 1 hypot(a, b), 2 creal(clog(a + i b)), 4 exp(a), 5 log(a), 6 log1p(a), 7 cos(a),
+ * 8 atan2(a, b). */
 int orc_libm(int fn, const double* a, const double* b, int n, double* out) {
-    for (int i = 0; i < n; ++i)
-        out[i] = fn == 0 ? cbrt(a[i]) : fn == 1 ? hypot(a[i], b[i]) : creal(clog(CMPLX(a[i], b[i])));
+    for (int i = 0; i < n; ++i) {
+        switch (fn) {
+            case 0: out[i] = cbrt(a[i]); break;
+            case 1: out[i] = hypot(a[i], b[i]); break;
+            case 2: out[i] = creal(clog(CMPLX(a[i], b[i]))); break;
+            case 4: out[i] = exp(a[i]); break;
+            case 5: out[i] = log(a[i]); break;
+            case 6: out[i] = log1p(a[i]); break;
+            case 7: out[i] = cos(a[i]); break;
+            case 8: out[i] = atan2(a[i], b[i]); break;
+            default: return -1;
+        }
+    }
     return n;
 }
 

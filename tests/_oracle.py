@@ -554,11 +554,12 @@ def scaled_costs_sample(cam14, world, obs, R, t, n_cand, nthreads=0):
 
 
 def libm(fn, a, b=None):
-    """glibc's cbrt (fn 0), hypot (1) or creal(clog(a + i b)) (2) over arrays, from the oracle library."""
+    """glibc's cbrt (fn 0), hypot (1), creal(clog(a + i b)) (2), exp (4), log (5), log1p (6), cos (7) or
+    atan2(a, b) (8) over arrays, from the oracle library."""
     a = np.ascontiguousarray(a, dtype=np.float64)
     b = np.ascontiguousarray(a if b is None else b, dtype=np.float64)
     out = np.zeros_like(a)
-    load().orc_libm(fn, ptr(a), ptr(b), a.shape[0], ptr(out))
+    assert load().orc_libm(fn, ptr(a), ptr(b), a.shape[0], ptr(out)) == a.shape[0]
     return out
 
 

@@ -1,6 +1,7 @@
-"""glibc_math.h's restatements of glibc 2.35 (cbrt, hypot, clog's real part) against the host's glibc,
-bit for bit. The reference's AP3P quartic (ap3p.cpp:10-59) calls these through libstdc++; the GPU kernel
-runs the restatements, so these tests pin the device's cbrt / hypot bits to glibc's. CPU only."""
+"""glibc_math.h's restatements of glibc 2.35 (cbrt, hypot, clog's real part, exp, log, log1p, cos,
+atan2) against the host's glibc, bit for bit. The reference's AP3P quartic (ap3p.cpp:10-59) calls these
+through libstdc++ (std::cbrt, the complex sqrt and pow); the GPU kernel runs the restatements, so these
+tests pin the device's bits to glibc's. CPU only."""
 import numpy as np
 import pytest
 
@@ -82,3 +83,95 @@ def test_clog_real_part_equals_glibc(native, oracle):
     got = _ours(2, A, B)
     bad = np.nonzero(got.view(np.uint64) != ref.view(np.uint64))[0]
     assert len(bad) == 0, f"{len(bad)} mismatches, e.g. clog({A[bad[0]]!r} + i {B[bad[0]]!r}).real"
+
+
+def _check(oracle, fn, a, b=None, name=""):
+    ref = oracle.libm(fn, a, a if b is None else b)
+    got = _ours(fn, a, b)
+    bad = np.nonzero(got.view(np.uint64) != ref.view(np.uint64))[0]
+    assert len(bad) == 0, (f"{len(bad)} mismatches of {len(a)}, e.g. {name}({a[bad[0]]!r}"
+                           + ("" if b is None else f", {b[bad[0]]!r}") + f") = {got[bad[0]]!r} vs {ref[bad[0]]!r}")
+
+
+def test_exp_equals_glibc(native, oracle):
+    """exp over |x| < 512 (glibc_exp's domain; AP3P feeds it log|w| / 3): uniform, small |x| near the
+    2^-54 cut, multiples of ln2 / 128 (the table's nodes) and their neighbours."""
+    rng = np.random.default_rng(4)
+    n = 400_000
+    x = np.concatenate([
+        rng.uniform(-511, 511, n),
+        rng.uniform(-1, 1, n) * 10.0 ** rng.uniform(-20, 0, n),
+        (rng.integers(-20000, 20000, n) * (np.log(2) / 128)) * (1 + rng.choice([-1, 0, 1], n) * 2.0 ** -52),
+        np.array([0.0, -0.0, 2.0 ** -54, -2.0 ** -54, 2.0 ** -55, 1.0, -1.0, 511.0, -511.0]),
+    ])
+    _check(oracle, 4, x, name="exp")
+
+
+def test_log_equals_glibc(native, oracle):
+    """log over positive normal and subnormal x outside glibc's close-to-1 band [1 - 2^-4, 1 + 0x1.09p-4)
+    (the band clog never sends to log)."""
+    rng = np.random.default_rng(5)
+    n = 400_000
+    x = np.concatenate([
+        10.0 ** rng.uniform(-307, 308, n),
+        np.abs(_random_doubles(rng, n)),
+        rng.uniform(0.5, 2.0, n),
+        2.0 ** rng.integers(-1074, 1024, n // 10).astype(np.float64),
+        np.array([np.inf]),
+    ])
+    lo, hi = 1 - 2.0 ** -4, 1 + float.fromhex("0x1.09p-4")
+    x = x[(x > 0) & ~((x >= lo) & (x < hi))]
+    _check(oracle, 5, x, name="log")
+
+
+def test_log1p_equals_glibc(native, oracle):
+    """log1p over x > -1: every magnitude, the branch cuts of s_log1p.c (|x| < 2^-29, 2^-54, the
+    sqrt(2) / 2 - 1 and sqrt(2) - 1 boundaries, 2^53) and clog's x^2 + y^2 - 1 range [-0.5, 3)."""
+    rng = np.random.default_rng(6)
+    n = 400_000
+    x = np.concatenate([
+        _random_doubles(rng, n),
+        rng.uniform(-0.5, 3.0, n),
+        rng.uniform(-1, 1, n) * 10.0 ** rng.uniform(-20, 0, n),
+        np.array([-0.2928932188134524, -0.29289321881345254, 0.41421356237309503, 0.41421356237309515,
+                  2.0 ** -29, 2.0 ** -54, 2.0 ** 53, -0.9999999999999999]),
+    ])
+    cuts = np.array([-0.2928932188134524, 0.41421356237309503, 2.0 ** -29, 2.0 ** -54, 2.0 ** 53])
+    x = np.concatenate([x, (cuts[:, None] * (1 + np.arange(-64, 65) * 2.0 ** -52)).ravel()])
+    x = x[x > -1]
+    _check(oracle, 6, x, name="log1p")
+
+
+def test_cos_equals_glibc(native, oracle):
+    """cos over |x| <= pi / 2 - 0.126 (glibc_cos's domain; AP3P feeds it arg(w) / 3, |.| <= pi / 3):
+    uniform, the 0.855469 switch to sin(pi / 2 - |x|), tiny |x| and the table nodes i / 128."""
+    rng = np.random.default_rng(7)
+    n = 400_000
+    x = np.concatenate([
+        rng.uniform(-1.4447, 1.4447, n),
+        rng.uniform(-1, 1, n) * 10.0 ** rng.uniform(-12, 0, n),
+        0.855469 * (1 + rng.integers(-1000, 1000, n // 10) * 2.0 ** -52),
+        rng.integers(-184, 185, n // 10) / 128.0 * (1 + rng.choice([-1, 0, 1], n // 10) * 2.0 ** -52),
+        np.array([0.0, -0.0, np.pi / 3, -np.pi / 3, 2.0 ** -27, 2.0 ** -28]),
+    ])
+    _check(oracle, 7, x, name="cos")
+
+
+def test_atan2_equals_glibc(native, oracle):
+    """atan2 over every quadrant with |x|, |y| in [2^-500, 2^500]: ratios from 2^-60 to 2^60 (the small-u
+    polynomial, the table branches, the pi / 2 and pi folds), equal magnitudes and AP3P-like arguments."""
+    rng = np.random.default_rng(8)
+    n = 400_000
+    y = rng.choice([1, -1], n) * 10.0 ** rng.uniform(-100, 100, n)
+    x = y * rng.choice([1, -1], n) * 2.0 ** rng.uniform(-60, 60, n)
+    y2 = rng.normal(size=n)
+    x2 = rng.normal(size=n)
+    t = rng.uniform(0, 1, n)
+    y3 = t * rng.choice([1, -1], n)
+    x3 = np.ones(n) * rng.choice([1, -1], n)
+    s = rng.choice([1.0, -1.0], n // 10)
+    A = np.concatenate([y, y2, y3, x3 * s[0], s])
+    B = np.concatenate([x, x2, x3, y3, s * rng.choice([1, -1], n // 10)])
+    keep = (A != 0) & (B != 0) & (np.abs(A) >= 2.0 ** -500) & (np.abs(A) <= 2.0 ** 500) \
+        & (np.abs(B) >= 2.0 ** -500) & (np.abs(B) <= 2.0 ** 500)
+    _check(oracle, 8, A[keep], B[keep], name="atan2")
