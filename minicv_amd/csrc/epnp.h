@@ -63,74 +63,6 @@ MCV_HD double cv_hypot(double a, double b) {
 #define MCV_SVD_UNROLL
 #define MCV_SMALL_UNROLL
 #endif
-// JacobiImpl_'s sweeps for a 12 x 12 working matrix kept in the caller's storage (the EPnP generate's
-// per-lane LDS slice): row i stays in registers for its whole j loop (read once, written back once if
-// it rotated) and row j + 1's loads are issued before row j's rotation, so a pair costs one row read and
-// at most one row write of the slice and its read latency overlaps the previous pair's arithmetic.
-// The operations and their order are jacobi_svd_core's: p, the rotation and the two sums run over k in
-// order, W[i] / W[j] are read and written at the same points, and a row is stored only where the
-// generic loop would have changed it.
-MCV_HD void jacobi_sweeps_rowreg(double (&A)[12][12], double (&W)[12]) {
-    const double eps = kDblEpsilon * 10;
-    for (int iter = 0; iter < 30; ++iter) {
-        bool changed = false;
-        for (int i = 0; i < 11; ++i) {
-            double ri[12], rj[12];
-            MCV_SMALL_UNROLL
-            for (int k = 0; k < 12; ++k) ri[k] = A[i][k];
-            MCV_SMALL_UNROLL
-            for (int k = 0; k < 12; ++k) rj[k] = A[i + 1][k];
-            double wi = W[i];
-            bool iRot = false;
-            for (int j = i + 1; j < 12; ++j) {
-                double rn[12];
-                const int jn = j + 1 < 12 ? j + 1 : j;   // the last pair re-reads its own row (unused)
-                MCV_SMALL_UNROLL
-                for (int k = 0; k < 12; ++k) rn[k] = A[jn][k];
-                double a = wi, b = W[j], p = 0;
-                MCV_SMALL_UNROLL
-                for (int k = 0; k < 12; ++k) p += ri[k] * rj[k];
-                if (!(__builtin_fabs(p) <= eps * __builtin_sqrt(a * b))) {
-                    p *= 2;
-                    const double beta = a - b, gamma = cv_hypot(p, beta);
-                    double c, s;
-                    if (beta < 0) {
-                        const double delta = (gamma - beta) * 0.5;
-                        s = __builtin_sqrt(delta / gamma);
-                        c = p / (gamma * s * 2);
-                    } else {
-                        c = __builtin_sqrt((gamma + beta) / (gamma * 2));
-                        s = p / (gamma * c * 2);
-                    }
-                    a = b = 0;
-                    MCV_SMALL_UNROLL
-                    for (int k = 0; k < 12; ++k) {
-                        const double t0 = c * ri[k] + s * rj[k];
-                        const double t1 = -s * ri[k] + c * rj[k];
-                        ri[k] = t0;
-                        rj[k] = t1;
-                        a += t0 * t0;
-                        b += t1 * t1;
-                    }
-                    wi = a;
-                    W[j] = b;
-                    changed = true;
-                    iRot = true;
-                    MCV_SMALL_UNROLL
-                    for (int k = 0; k < 12; ++k) A[j][k] = rj[k];
-                }
-                MCV_SMALL_UNROLL
-                for (int k = 0; k < 12; ++k) rj[k] = rn[k];
-            }
-            W[i] = wi;
-            if (iRot)
-                MCV_SMALL_UNROLL
-                for (int k = 0; k < 12; ++k) A[i][k] = ri[k];
-        }
-        if (!changed) break;
-    }
-}
-
 template <int M, int N, int N1, bool HASV>
 MCV_HD void jacobi_svd_core(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]) {
     constexpr int SU = N <= 6 ? 16 : 1;
@@ -146,9 +78,7 @@ MCV_HD void jacobi_svd_core(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]
             MCV_SMALL_UNROLL
             for (int k = 0; k < N; ++k) Vt[i][k] = k == i ? 1.0 : 0.0;
     }
-    if constexpr (M == 12 && N == 12 && N1 == 12 && !HASV) {
-        jacobi_sweeps_rowreg(A, W);   // EPnP's M^T M: the working matrix in the caller's (LDS) storage
-    } else {
+    {
         const int maxIter = M > 30 ? M : 30;
         for (int iter = 0; iter < maxIter; ++iter) {
             bool changed = false;
@@ -441,8 +371,199 @@ MCV_HD void epnp_qr_solve(double (&A)[6][4], double (&b)[6], double (&X)[4]) {
     }
 }
 
-// L_6x10 row r at Lr[r * 12 .. + 9], rho[r] at Lr[r * 12 + 10] (rows of the SVD workspace).
-MCV_HD void epnp_gauss_newton(const double* Lr, double (&be)[4]) {
+// Views of the 12 x 12 working matrix: ws(r, c). After the SVD and compute_L_6x10 its rows 0..5 hold
+// L_6x10 (columns 0..9) and rho (column 10), rows 8..11 the null-space vectors. EpnpWsRef: a plain
+// 12 x 12 array (host); EpnpWsSoA: element (r, c) of one hypothesis at p[(12 r + c) s] (structure of
+// arrays over a launch's hypotheses: the split device generate's global scratch).
+struct EpnpWsRef {
+    double (&A)[12][12];
+    MCV_HD double& operator()(int r, int c) const { return A[r][c]; }
+};
+struct EpnpWsSoA {
+    double* p;
+    int64_t s;
+    MCV_HD double& operator()(int r, int c) const { return p[(int64_t)(12 * r + c) * s]; }
+};
+
+// jacobi_svd_core's tail for the 12 x 12 without V (EPnP's cvSVD of M^T M) on a view: the row norms,
+// the descending selection sort (row swaps) and the cv::RNG completion of null rows, in the generic
+// loop's order. W: the squared norms the sweeps left (in), nothing useful (out).
+template <class WS>
+MCV_HD void jacobi12_tail(const WS& A, double (&W)[12]) {
+    const double eps = kDblEpsilon * 10, minval = kDblMin;
+    for (int i = 0; i < 12; ++i) {
+        double sd = 0;
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 12; ++k) sd += A(i, k) * A(i, k);
+        W[i] = __builtin_sqrt(sd);
+    }
+    for (int i = 0; i < 11; ++i) {
+        int j = i;
+        double wj = W[i];
+        for (int k = i + 1; k < 12; ++k)
+            if (wj < W[k]) j = k, wj = W[k];
+        if (j != i) {
+            const double tw = W[i]; W[i] = W[j]; W[j] = tw;
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 12; ++k) { const double t = A(i, k); A(i, k) = A(j, k); A(j, k) = t; }
+        }
+    }
+    CvRng rng{0x12345678u};
+    for (int i = 0; i < 12; ++i) {
+        double sd = W[i];
+        for (int ii = 0; ii < 100 && sd <= minval; ++ii) {
+            const double val0 = 1. / 12;
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 12; ++k) A(i, k) = (rng.next() & 256) != 0 ? val0 : -val0;
+            for (int it = 0; it < 2; ++it)
+                for (int j = 0; j < i; ++j) {
+                    sd = 0;
+                    MCV_SMALL_UNROLL
+                    for (int k = 0; k < 12; ++k) sd += A(i, k) * A(j, k);
+                    double asum = 0;
+                    MCV_SMALL_UNROLL
+                    for (int k = 0; k < 12; ++k) {
+                        const double t = A(i, k) - sd * A(j, k);
+                        A(i, k) = t;
+                        asum += __builtin_fabs(t);
+                    }
+                    asum = asum > eps * 100 ? 1 / asum : 0;
+                    MCV_SMALL_UNROLL
+                    for (int k = 0; k < 12; ++k) A(i, k) *= asum;
+                }
+            sd = 0;
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 12; ++k) sd += A(i, k) * A(i, k);
+            sd = __builtin_sqrt(sd);
+        }
+        const double s = sd > minval ? 1 / sd : 0.;
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 12; ++k) A(i, k) *= s;
+    }
+}
+
+// jacobi_svd_core's sweeps for the 12 x 12 without V (the device's EPnP SVD kernel) with the working
+// matrix split by columns: columns 0..5 of row r at lo[6 r ..] (the caller's per-lane LDS slice,
+// 37 KB per wave: four waves per CU), columns 6..11 in registers (hi[r]). The pair loop keeps i
+// rolled and expands j at compile time (j12_pairs<J>), so row j's register half and W[j] are fixed
+// registers and its LDS half sits at a constant offset; row i's register half and W[i] are read and
+// written once per i through a wave-uniform branch chain (j12_get / j12_set; each case is pinned as a
+// branch, so a read costs the matched case's moves, not a select over all rows), and row j + 1's LDS
+// half is loaded before row j's rotation. The operations and their order are the generic loop's: p,
+// the rotation and the two sums run over k = 0..11 in order, and W[i] / W[j] / the rows change where
+// it changes them.
+// A value moved through an empty asm tagged with the case number: the copies of one case cannot be
+// merged with another case's into a load or store through a phi of addresses (which would keep the
+// register rows in scratch).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MCV_PIN_CASE(x, q) asm volatile("; j12 case %1" : "+v"(x) : "i"(q))
+#else
+#define MCV_PIN_CASE(x, q) ((void)0)
+#endif
+template <int Q>
+MCV_HD void j12_get(const double (&hi)[12][6], const double (&W)[12], int r, double* o, double& w) {
+    if (Q == r) {
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 6; ++k) {
+            double x = hi[Q][k];
+            MCV_PIN_CASE(x, Q);
+            o[k] = x;
+        }
+        double x = W[Q];
+        MCV_PIN_CASE(x, Q);
+        w = x;
+    }
+    if constexpr (Q < 10) j12_get<Q + 1>(hi, W, r, o, w);
+}
+template <int Q>
+MCV_HD void j12_set(double (&hi)[12][6], double (&W)[12], int r, const double* o, double w, bool rot) {
+    if (Q == r) {
+        double x = w;
+        MCV_PIN_CASE(x, Q);
+        W[Q] = x;
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 6; ++k) {
+            double y = rot ? o[k] : hi[Q][k];
+            MCV_PIN_CASE(y, Q);
+            hi[Q][k] = y;
+        }
+    }
+    if constexpr (Q < 10) j12_set<Q + 1>(hi, W, r, o, w, rot);
+}
+template <int J>
+MCV_HD void j12_pairs(double* lo, double (&hi)[12][6], double (&W)[12], int i, double (&ri)[12], double& wi,
+                      double (&nx)[6], bool& changed, bool& iRot) {
+    if (J > i) {
+        const double eps = kDblEpsilon * 10;
+        double rj[12];
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 6; ++k) rj[k] = nx[k];
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 6; ++k) rj[6 + k] = hi[J][k];
+        if constexpr (J < 11)
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 6; ++k) nx[k] = lo[6 * (J + 1) + k];
+        double a = wi, b = W[J], p = 0;
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 12; ++k) p += ri[k] * rj[k];
+        if (!(__builtin_fabs(p) <= eps * __builtin_sqrt(a * b))) {
+            p *= 2;
+            const double beta = a - b, gamma = cv_hypot(p, beta);
+            double c, s;
+            if (beta < 0) {
+                const double delta = (gamma - beta) * 0.5;
+                s = __builtin_sqrt(delta / gamma);
+                c = p / (gamma * s * 2);
+            } else {
+                c = __builtin_sqrt((gamma + beta) / (gamma * 2));
+                s = p / (gamma * c * 2);
+            }
+            a = b = 0;
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 12; ++k) {
+                const double t0 = c * ri[k] + s * rj[k];
+                const double t1 = -s * ri[k] + c * rj[k];
+                ri[k] = t0;
+                rj[k] = t1;
+                a += t0 * t0;
+                b += t1 * t1;
+            }
+            wi = a;
+            W[J] = b;
+            changed = true;
+            iRot = true;
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 6; ++k) lo[6 * J + k] = rj[k];
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 6; ++k) hi[J][k] = rj[6 + k];
+        }
+    }
+    if constexpr (J < 11) j12_pairs<J + 1>(lo, hi, W, i, ri, wi, nx, changed, iRot);
+}
+MCV_HD void jacobi12_sweeps_split(double* lo, double (&hi)[12][6], double (&W)[12]) {
+    for (int iter = 0; iter < 30; ++iter) {
+        bool changed = false;
+        for (int i = 0; i < 11; ++i) {
+            double ri[12], wi = 0, nx[6];
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 6; ++k) ri[k] = lo[6 * i + k];
+            j12_get<0>(hi, W, i, ri + 6, wi);
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 6; ++k) nx[k] = lo[6 * (i + 1) + k];
+            bool iRot = false;
+            j12_pairs<1>(lo, hi, W, i, ri, wi, nx, changed, iRot);
+            j12_set<0>(hi, W, i, ri + 6, wi, iRot);
+            if (iRot)
+                MCV_SMALL_UNROLL
+                for (int k = 0; k < 6; ++k) lo[6 * i + k] = ri[k];
+        }
+        if (!changed) break;
+    }
+}
+
+// L_6x10 row r at ws(r, 0 .. 9), rho[r] at ws(r, 10).
+template <class WS>
+MCV_HD void epnp_gauss_newton(const WS& ws, double (&be)[4]) {
     double X[4] = {0, 0, 0, 0};   // kept across iterations, as epnp::gauss_newton's x
     for (int it = 0; it < 5; ++it) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -452,7 +573,9 @@ MCV_HD void epnp_gauss_newton(const double* Lr, double (&be)[4]) {
         double A[6][4], b[6];
         MCV_SMALL_UNROLL
         for (int i = 0; i < 6; ++i) {
-            const double* l = Lr + 12 * i;
+            double l[11];
+            MCV_SMALL_UNROLL
+            for (int k = 0; k < 11; ++k) l[k] = ws(i, k);
             A[i][0] = 2 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
             A[i][1] = l[1] * be[0] + 2 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
             A[i][2] = l[3] * be[0] + l[4] * be[1] + 2 * l[5] * be[2] + l[8] * be[3];
@@ -476,12 +599,9 @@ typedef double EpnpWs[12][12];
 // full symmetric M^T M; on return its rows 11, 10, 9, 8 are the four null-space vectors v_0..v_3
 // (rows of U^T), rows 0..5 hold L_6x10 (columns 0..9) and rho (column 10) — the working matrix keeps
 // what the GPU lane would otherwise hold in registers (v, L, rho: 114 doubles).
-MCV_HD void epnp_betas_ws(const EpnpCtrl& C, double (&betas)[4][4], EpnpWs& A) {
-    {
-        // cvSVD(MtM, D, Ut, 0, MODIFY_A | U_T): Jacobi on transpose(MtM) (= MtM after completeSymm)
-        double w[12];
-        jacobi_svd<12, 12>(A, w, nullptr);
-    }
+// compute_L_6x10 and rho from the null-space vectors (rows 11, 10, 9, 8) into rows 0..5.
+template <class WS>
+MCV_HD void epnp_l_rows(const double (&cws)[4][3], const WS& A) {
     {
         const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
         MCV_SMALL_UNROLL
@@ -491,33 +611,46 @@ MCV_HD void epnp_betas_ws(const EpnpCtrl& C, double (&betas)[4][4], EpnpWs& A) {
             MCV_SMALL_UNROLL
             for (int i = 0; i < 4; ++i)
                 MCV_SMALL_UNROLL
-                for (int k = 0; k < 3; ++k) dv[i][k] = A[11 - i][3 * pa[r] + k] - A[11 - i][3 * pb[r] + k];
-            double* L = A[r];
-            L[0] = dot3(dv[0], dv[0]);
-            L[1] = 2.0 * dot3(dv[0], dv[1]);
-            L[2] = dot3(dv[1], dv[1]);
-            L[3] = 2.0 * dot3(dv[0], dv[2]);
-            L[4] = 2.0 * dot3(dv[1], dv[2]);
-            L[5] = dot3(dv[2], dv[2]);
-            L[6] = 2.0 * dot3(dv[0], dv[3]);
-            L[7] = 2.0 * dot3(dv[1], dv[3]);
-            L[8] = 2.0 * dot3(dv[2], dv[3]);
-            L[9] = dot3(dv[3], dv[3]);
-            const double* p1 = C.cws[pa[r]];
-            const double* p2 = C.cws[pb[r]];
-            L[10] = (p1[0] - p2[0]) * (p1[0] - p2[0]) + (p1[1] - p2[1]) * (p1[1] - p2[1]) +
-                    (p1[2] - p2[2]) * (p1[2] - p2[2]);
+                for (int k = 0; k < 3; ++k) dv[i][k] = A(11 - i, 3 * pa[r] + k) - A(11 - i, 3 * pb[r] + k);
+            A(r, 0) = dot3(dv[0], dv[0]);
+            A(r, 1) = 2.0 * dot3(dv[0], dv[1]);
+            A(r, 2) = dot3(dv[1], dv[1]);
+            A(r, 3) = 2.0 * dot3(dv[0], dv[2]);
+            A(r, 4) = 2.0 * dot3(dv[1], dv[2]);
+            A(r, 5) = dot3(dv[2], dv[2]);
+            A(r, 6) = 2.0 * dot3(dv[0], dv[3]);
+            A(r, 7) = 2.0 * dot3(dv[1], dv[3]);
+            A(r, 8) = 2.0 * dot3(dv[2], dv[3]);
+            A(r, 9) = dot3(dv[3], dv[3]);
+            const double* p1 = cws[pa[r]];
+            const double* p2 = cws[pb[r]];
+            A(r, 10) = (p1[0] - p2[0]) * (p1[0] - p2[0]) + (p1[1] - p2[1]) * (p1[1] - p2[1]) +
+                       (p1[2] - p2[2]) * (p1[2] - p2[2]);
         }
     }
-    const double* Lr = A[0];
+}
+
+// The SVD of M^T M (in A on entry) and L_6x10 / rho.
+MCV_HD void epnp_null_and_l(const double (&cws)[4][3], EpnpWs& A) {
+    {
+        // cvSVD(MtM, D, Ut, 0, MODIFY_A | U_T): Jacobi on transpose(MtM) (= MtM after completeSymm)
+        double w[12];
+        jacobi_svd<12, 12>(A, w, nullptr);
+    }
+    epnp_l_rows(cws, EpnpWsRef{A});
+}
+
+// Second half: the betas of the three approximations from L_6x10 / rho (ws rows 0..5).
+template <class WS>
+MCV_HD void epnp_betas_from_l(double (&betas)[4][4], const WS& A) {
     double rho[6];
     MCV_SMALL_UNROLL
-    for (int i = 0; i < 6; ++i) rho[i] = A[i][10];
+    for (int i = 0; i < 6; ++i) rho[i] = A(i, 10);
     for (int k = 0; k < 4; ++k) betas[0][k] = 0;
     {   // approximation 1: [B11 B12 B13 B14]
         double L4[6][4], b4[4];
         MCV_SMALL_UNROLL
-        for (int i = 0; i < 6; ++i) { L4[i][0] = A[i][0]; L4[i][1] = A[i][1]; L4[i][2] = A[i][3]; L4[i][3] = A[i][6]; }
+        for (int i = 0; i < 6; ++i) { L4[i][0] = A(i, 0); L4[i][1] = A(i, 1); L4[i][2] = A(i, 3); L4[i][3] = A(i, 6); }
         svd_solve6<4>(L4, rho, b4);
         double* be = betas[1];
         if (b4[0] < 0) {
@@ -531,12 +664,12 @@ MCV_HD void epnp_betas_ws(const EpnpCtrl& C, double (&betas)[4][4], EpnpWs& A) {
             be[2] = b4[2] / be[0];
             be[3] = b4[3] / be[0];
         }
-        epnp_gauss_newton(Lr, betas[1]);
+        epnp_gauss_newton(A, betas[1]);
     }
     {   // approximation 2: [B11 B12 B22]
         double L3[6][3], b3[3];
         MCV_SMALL_UNROLL
-        for (int i = 0; i < 6; ++i) { L3[i][0] = A[i][0]; L3[i][1] = A[i][1]; L3[i][2] = A[i][2]; }
+        for (int i = 0; i < 6; ++i) { L3[i][0] = A(i, 0); L3[i][1] = A(i, 1); L3[i][2] = A(i, 2); }
         svd_solve6<3>(L3, rho, b3);
         double* be = betas[2];
         if (b3[0] < 0) {
@@ -549,14 +682,14 @@ MCV_HD void epnp_betas_ws(const EpnpCtrl& C, double (&betas)[4][4], EpnpWs& A) {
         if (b3[1] < 0) be[0] = -be[0];
         be[2] = 0.0;
         be[3] = 0.0;
-        epnp_gauss_newton(Lr, betas[2]);
+        epnp_gauss_newton(A, betas[2]);
     }
     {   // approximation 3: [B11 B12 B22 B13 B23]
         double L5[6][5], b5[5];
         MCV_SMALL_UNROLL
         for (int i = 0; i < 6; ++i)
             MCV_SMALL_UNROLL
-            for (int k = 0; k < 5; ++k) L5[i][k] = A[i][k];
+            for (int k = 0; k < 5; ++k) L5[i][k] = A(i, k);
         svd_solve6<5>(L5, rho, b5);
         double* be = betas[3];
         if (b5[0] < 0) {
@@ -569,8 +702,13 @@ MCV_HD void epnp_betas_ws(const EpnpCtrl& C, double (&betas)[4][4], EpnpWs& A) {
         if (b5[1] < 0) be[0] = -be[0];
         be[2] = b5[3] / be[0];
         be[3] = 0.0;
-        epnp_gauss_newton(Lr, betas[3]);
+        epnp_gauss_newton(A, betas[3]);
     }
+}
+
+MCV_HD void epnp_betas_ws(const EpnpCtrl& C, double (&betas)[4][4], EpnpWs& A) {
+    epnp_null_and_l(C.cws, A);
+    epnp_betas_from_l(betas, EpnpWsRef{A});
 }
 
 // The same from the packed upper triangle of M^T M (the host inlier solve), with the null-space
@@ -597,8 +735,9 @@ MCV_HD void epnp_ccs(const EpnpBetas& B, const double (&be)[4], double (&ccs)[4]
             for (int k = 0; k < 3; ++k) ccs[j][k] += be[i] * B.v[i][3 * j + k];
 }
 
-// The same with the null-space vectors in the workspace (v_i = A[11 - i], epnp_betas_ws).
-MCV_HD void epnp_ccs_ws(const EpnpWs& A, const double (&be)[4], double (&ccs)[4][3]) {
+// The same with the null-space vectors in the workspace (v_i = ws(11 - i, .), epnp_betas_ws).
+template <class WS>
+MCV_HD void epnp_ccs_ws(const WS& A, const double (&be)[4], double (&ccs)[4][3]) {
     MCV_SMALL_UNROLL
     for (int j = 0; j < 4; ++j)
         MCV_SMALL_UNROLL
@@ -608,7 +747,7 @@ MCV_HD void epnp_ccs_ws(const EpnpWs& A, const double (&be)[4], double (&ccs)[4]
         MCV_SMALL_UNROLL
         for (int j = 0; j < 4; ++j)
             MCV_SMALL_UNROLL
-            for (int k = 0; k < 3; ++k) ccs[j][k] += be[i] * A[11 - i][3 * j + k];
+            for (int k = 0; k < 3; ++k) ccs[j][k] += be[i] * A(11 - i, 3 * j + k);
 }
 
 MCV_HD void epnp_pc(const double (&a)[4], const double (&ccs)[4][3], double (&pc)[3]) {
@@ -654,11 +793,13 @@ MCV_HD int epnp_pick(const double (&rep)[4]) {
 }
 
 // Whole EPnP for a small point set held by the caller (RANSAC minimal sets, n = NP):
-// pw[i] world points, us[i] pixel coordinates (undistorted normalised * f + c).
+// pw[i] world points, us[i] pixel coordinates (undistorted normalised * f + c). Three parts, which the
+// split device generate runs as three kernels: epnp_small_mtm (control points, alphas, M^T M into ws),
+// epnp_null_and_l (the 12 x 12 SVD and L_6x10 in ws) and epnp_small_pose (betas, Gauss-Newton, the
+// three poses and the pick).
 template <int NP>
-MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
-                             double (&Rout)[3][3], double (&tout)[3], EpnpWs& ws) {
-    EpnpCtrl C;
+MCV_HD void epnp_small_mtm(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam, EpnpCtrl& C,
+                           double (&al)[NP][4], double (&mtm)[kMtmSums]) {
     {
         double sum[3] = {0, 0, 0};
         for (int i = 0; i < NP; ++i)
@@ -674,10 +815,8 @@ MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2
             }
         epnp_control(sum, P, NP, C);
     }
-    double al[NP][4];
     for (int i = 0; i < NP; ++i) epnp_alphas(C, pw[i], al[i]);
     {
-        double mtm[kMtmSums];
         for (int k = 0; k < kMtmSums; ++k) mtm[k] = 0;
         for (int i = 0; i < NP; ++i) {
             double r1[12], r2[12];
@@ -689,11 +828,14 @@ MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2
                     mtm[o] += r2[a] * r2[b];
                 }
         }
-        for (int a = 0; a < 12; ++a)
-            for (int b = a; b < 12; ++b) ws[a][b] = ws[b][a] = mtm[mtm_index(a, b)];
     }
+}
+
+template <int NP, class WS>
+MCV_HD void epnp_small_pose(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
+                            const double (&al)[NP][4], const WS& ws, double (&Rout)[3][3], double (&tout)[3]) {
     double betas[4][4];
-    epnp_betas_ws(C, betas, ws);   // v, L and rho stay in ws
+    epnp_betas_from_l(betas, ws);   // v, L and rho in ws
     double pw0[3] = {0, 0, 0};
     for (int i = 0; i < NP; ++i)
         for (int j = 0; j < 3; ++j) pw0[j] += pw[i][j];
@@ -730,6 +872,21 @@ MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2
             }
         }
     }
+}
+
+template <int NP>
+MCV_HD void epnp_solve_small(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
+                             double (&Rout)[3][3], double (&tout)[3], EpnpWs& ws) {
+    EpnpCtrl C;
+    double al[NP][4];
+    {
+        double mtm[kMtmSums];
+        epnp_small_mtm<NP>(pw, us, cam, C, al, mtm);
+        for (int a = 0; a < 12; ++a)
+            for (int b = a; b < 12; ++b) ws[a][b] = ws[b][a] = mtm[mtm_index(a, b)];
+    }
+    epnp_null_and_l(C.cws, ws);
+    epnp_small_pose<NP>(pw, us, cam, al, EpnpWsRef{ws}, Rout, tout);
 }
 
 template <int NP>

@@ -534,8 +534,7 @@ MCV_HD bool pnp_kind_epnp(int kind) { return kind != 2 && kind != 5; }
 // image points go through undistortPoints with a CV_32F result (the normalised coordinates are
 // rounded to float), epnp::init_points maps them back to pixels (x * fu + uc in double), world
 // points are the float coordinates.
-MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose, EpnpWs& ws) {
-    double pw[5][3], us[5][2];
+MCV_HD void pnp_epnp5_points(const PnpCamera& c, const PnpPoint* p5, double (&pw)[5][3], double (&us)[5][2]) {
     for (int i = 0; i < 5; ++i) {
         const PnpPoint p = p5[i];
         double x, y;
@@ -544,6 +543,10 @@ MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose, Epn
         us[i][1] = (double)(float)y * c.fy + c.cy;
         pw[i][0] = p.X; pw[i][1] = p.Y; pw[i][2] = p.Z;
     }
+}
+MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose, EpnpWs& ws) {
+    double pw[5][3], us[5][2];
+    pnp_epnp5_points(c, p5, pw, us);
     const EpnpCam ec{c.fx, c.fy, c.cx, c.cy};
     double R[3][3], t[3];
     epnp_solve_small<5>(pw, us, ec, R, t, ws);
@@ -559,19 +562,19 @@ MCV_HD void pnp_epnp5(const PnpCamera& c, const PnpPoint* p5, PnpPose& pose) {
 
 // One EPnP hypothesis: 5 distinct indices (Philox stream) -> pnp_epnp5. EPnP always yields a
 // model (possibly non-finite, which then counts no inliers), as solvePnP(EPNP) returns true.
+MCV_HD bool pnp_sample5(int N, const Sampler& smp, uint64_t hyp, int (&idx)[5]) {
+    SubsetSrc<5> src(smp, hyp);
+    for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {   // search and solve apart (h_hypothesis)
+        const int got = src.next(N, idx);
+        if (got < 0) return false;
+        if (got > 0) return true;
+    }
+    return false;
+}
 MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
                                PnpPose& pose, int* idx_out, EpnpWs& ws) {
-    SubsetSrc<5> src(smp, hyp);
     int idx[5];
-    bool found = false;   // search and solve apart (h_hypothesis): one solve pass per wave
-    for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        const int got = src.next(N, idx);
-        if (got < 0) break;
-        if (got == 0) continue;
-        found = true;
-        break;
-    }
-    if (!found) return kStatusNoSample;
+    if (!pnp_sample5(N, smp, hyp, idx)) return kStatusNoSample;
     PnpPoint p5[5];
     for (int i = 0; i < 5; ++i) p5[i] = pts[idx[i]];
     if (idx_out) for (int i = 0; i < 5; ++i) idx_out[i] = idx[i];
@@ -582,6 +585,112 @@ MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, c
                                PnpPose& pose, int* idx_out) {
     EpnpWs ws;
     return pnp_hypothesis_epnp(pts, N, c, smp, hyp, pose, idx_out, ws);
+}
+
+// The split device generate: pnp_hypothesis_epnp as three kernels over a launch's hypotheses, which
+// pass their state through structure-of-arrays scratch (value e of hypothesis i at base[e * s + i]).
+// Kernel 1: sample, control points, alphas, M^T M. Kernel 2: the SVD's Jacobi sweeps, the only part
+// that needs a per-lane working matrix in LDS (jacobi12_sweeps_split: half of it in LDS, half in
+// registers, four waves per CU). Kernel 3: the SVD's tail (norms, sort, null-row completion) on the
+// matrix in global scratch, L_6x10, the betas, Gauss-Newton and the three poses. Every value crosses
+// the kernels as the same double and every operation keeps its order, so the composition computes
+// pnp_hypothesis_epnp's bits.
+static const int kEpnpCtx = 57;   // pw (15), us (10), al (20), cws (12)
+struct EpnpSplit {
+    double* mtm;   // kMtmSums x s
+    double* ctx;   // kEpnpCtx x s
+    double* A;     // 144 x s: the working matrix after the sweeps (EpnpWsSoA)
+    double* W;     // 12 x s: its squared row norms after the sweeps
+    int64_t s;
+};
+static const int kEpnpSplitDoubles = kMtmSums + kEpnpCtx + 144 + 12;
+static const int kEpnpLoStride = 74;   // doubles per lane of kernel 2's LDS (6 x 12 + pad, 16-byte rows)
+
+// Kernel 1: sample, points, control points, alphas and M^T M. Returns 1 or kStatusNoSample.
+MCV_HD int pnp_epnp_split_mtm(const PnpPoint* pts, int N, const PnpCamera& c, const Sampler& smp, uint64_t hyp,
+                              const EpnpSplit& X, int64_t i) {
+    int idx[5];
+    if (!pnp_sample5(N, smp, hyp, idx)) return kStatusNoSample;
+    PnpPoint p5[5];
+    for (int k = 0; k < 5; ++k) p5[k] = pts[idx[k]];
+    double pw[5][3], us[5][2], al[5][4], mtm[kMtmSums];
+    pnp_epnp5_points(c, p5, pw, us);
+    EpnpCtrl C;
+    epnp_small_mtm<5>(pw, us, EpnpCam{c.fx, c.fy, c.cx, c.cy}, C, al, mtm);
+    double* q = X.ctx + i;
+    int e = 0;
+    for (int k = 0; k < 5; ++k)
+        for (int j = 0; j < 3; ++j) q[(e++) * X.s] = pw[k][j];
+    for (int k = 0; k < 5; ++k)
+        for (int j = 0; j < 2; ++j) q[(e++) * X.s] = us[k][j];
+    for (int k = 0; k < 5; ++k)
+        for (int j = 0; j < 4; ++j) q[(e++) * X.s] = al[k][j];
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 3; ++j) q[(e++) * X.s] = C.cws[k][j];
+    for (int k = 0; k < kMtmSums; ++k) X.mtm[k * X.s + i] = mtm[k];
+    return 1;
+}
+
+// Kernel 2: M^T M into the split working matrix (lo: the lane's LDS slice), jacobi_svd_core's initial
+// squared norms and its sweeps; the matrix and the norms out.
+MCV_HD void pnp_epnp_split_sweeps(const EpnpSplit& X, int64_t i, double* lo) {
+    double hi[12][6], W[12];
+    MCV_SMALL_UNROLL
+    for (int a = 0; a < 12; ++a)
+        MCV_SMALL_UNROLL
+        for (int b = 0; b < 12; ++b) {
+            const double v = X.mtm[mtm_index(a < b ? a : b, a < b ? b : a) * X.s + i];
+            if (b < 6) lo[6 * a + b] = v;
+            else hi[a][b - 6] = v;
+        }
+    MCV_SMALL_UNROLL
+    for (int a = 0; a < 12; ++a) {
+        double sd = 0;
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 6; ++k) sd += lo[6 * a + k] * lo[6 * a + k];
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 6; ++k) sd += hi[a][k] * hi[a][k];
+        W[a] = sd;
+    }
+    jacobi12_sweeps_split(lo, hi, W);
+    const EpnpWsSoA o{X.A + i, X.s};
+    MCV_SMALL_UNROLL
+    for (int a = 0; a < 12; ++a) {
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 6; ++k) o(a, k) = lo[6 * a + k];
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 6; ++k) o(a, 6 + k) = hi[a][k];
+        X.W[a * X.s + i] = W[a];
+    }
+}
+
+// Kernel 3: the SVD's tail and L_6x10 on the matrix in scratch, then the betas, Gauss-Newton and the
+// pose pick.
+MCV_HD void pnp_epnp_split_pose(const PnpCamera& c, const EpnpSplit& X, int64_t i, PnpPose& pose) {
+    const EpnpWsSoA A{X.A + i, X.s};
+    {
+        double W[12], cws[4][3];
+        for (int a = 0; a < 12; ++a) W[a] = X.W[a * X.s + i];
+        jacobi12_tail(A, W);
+        for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < 3; ++j) cws[k][j] = X.ctx[(45 + 3 * k + j) * X.s + i];
+        epnp_l_rows(cws, A);
+    }
+    double pw[5][3], us[5][2], al[5][4];
+    const double* q = X.ctx + i;
+    int e = 0;
+    for (int k = 0; k < 5; ++k)
+        for (int j = 0; j < 3; ++j) pw[k][j] = q[(e++) * X.s];
+    for (int k = 0; k < 5; ++k)
+        for (int j = 0; j < 2; ++j) us[k][j] = q[(e++) * X.s];
+    for (int k = 0; k < 5; ++k)
+        for (int j = 0; j < 4; ++j) al[k][j] = q[(e++) * X.s];
+    double R[3][3], t[3];
+    epnp_small_pose<5>(pw, us, EpnpCam{c.fx, c.fy, c.cx, c.cy}, al, A, R, t);
+    for (int r = 0; r < 3; ++r) {
+        for (int j = 0; j < 3; ++j) pose.R[3 * r + j] = R[r][j];
+        pose.t[r] = t[r];
+    }
 }
 
 }  // namespace mcv

@@ -136,8 +136,10 @@ struct Ap3pOut {
 };
 void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_pts, hipStream_t s);
 // fast (MCV_FLAG_FAST_MINIMAL): the AP3P kernel's real-root-finder quartic instead of the reference's Ferrari
+// d_epnpScratch: kEpnpSplitDoubles x hypCount doubles (EPnP's split generate; unused by AP3P)
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
-                         bool epnp, void* d_models, int* d_counts, hipStream_t s, bool fast = false);
+                         bool epnp, void* d_models, int* d_counts, double* d_epnpScratch, hipStream_t s,
+                         bool fast = false);
 // d_ext: 3 doubles of device scratch filled by launch_pnp_extent (the certified sweep's bound).
 void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s);
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,

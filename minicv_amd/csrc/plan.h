@@ -75,6 +75,7 @@ struct Plan {
     DevBuf<double> epw;       // PnP: EPnP solve points (world, double)
     DevBuf<double> eus;       // PnP: EPnP solve points (pixels of the undistorted observations)
     DevBuf<int> eidx;         // PnP: inlier indices of the EPnP solve
+    DevBuf<double> escratch;  // PnP: the split EPnP generate's per-hypothesis state (kEpnpSplitDoubles each)
     LastChunk last;           // the last evaluated chunk (finalize takes the winner's model from its buffers)
     DevBuf<int> subsets;      // MCV_FLAG_CV_SAMPLER: OpenCV's getSubset stream, subsetM ints per hypothesis
     int64_t subsetRows = 0;   // hypotheses [0, subsetRows) covered by `subsets`

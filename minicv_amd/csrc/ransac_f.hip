@@ -379,12 +379,11 @@ static void launch_f_verify_pk_kp(const float4* p, int N, const FModelD* m, int*
     constexpr int target = 65536;
     const int step = 64 * P;
     int chunks = (target + waves - 1) / waves;
-    // and at least enough chunks (a power of two <= 8, one per XCD group) that an XCD's slice of the
-    // points stays within ~1 MB of its 4 MB L2 (2^20 hypotheses x 500k points: 8 chunks cut the fetches
-    // 4.0 GB -> 0.61 GB per launch, 224.1 -> 222.2 ms; the partial counts add 0.25 GB of writes)
-    int l2Chunks = 1;
-    while (l2Chunks < 8 && (int64_t)N * 16 > (int64_t)l2Chunks << 20) l2Chunks *= 2;
-    chunks = std::max(chunks, l2Chunks);
+    // No L2-sized chunking: 2^20 hypotheses x 500k points in 8 per-XCD chunks of 1 MB cut the fetches
+    // 4.0 -> 0.61 GB per launch but took eight count atomics per model (32 MiB of writes against the
+    // 4 MiB of one store each) for 222.2 vs 224.1 ms; a block-shared form (four chunks per block,
+    // counts added in LDS behind a barrier: 8 MiB) measured 279 ms. The sweep is VALU-bound, so the
+    // whole point set streams from the 256 MB MALL and each model's count is one store.
     const int maxChunks = std::max(1, N / 8192);
     chunks = std::max(1, std::min(chunks, maxChunks));
     int chunk = (N + chunks - 1) / chunks;

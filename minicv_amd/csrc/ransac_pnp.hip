@@ -39,11 +39,7 @@ __global__ __launch_bounds__(256) void mcv_pnp_pack(const double* __restrict__ i
     out[i] = p;
 }
 
-// EPnP's 12 x 12 SVD working matrix lives in LDS, one padded slice per lane (a private array with
-// the SVD's data-dependent row pairs went to scratch: 2.4 KB per lane at one wave per SIMD).
-static constexpr int kEpnpWsStride = 145;   // doubles per lane (12 x 12 + 1: bank spread)
-
-template <bool EPNP>
+// AP3P: one hypothesis per lane, one kernel.
 __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
                                                        Sampler smp, int64_t hypBegin, int hypCount,
                                                        PnpPose* __restrict__ models, int* __restrict__ counts,
@@ -51,20 +47,39 @@ __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restric
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hypCount) return;
     PnpPose p;
-    int st;
-    if constexpr (EPNP) {
-        __shared__ double ws[64 * kEpnpWsStride];
-        EpnpWs& A = *reinterpret_cast<EpnpWs*>(ws + (size_t)threadIdx.x * kEpnpWsStride);
-        st = pnp_hypothesis_epnp(pts, N, cam, smp, (uint64_t)(hypBegin + i), p, nullptr, A);
-    } else {
-        st = pnp_hypothesis(pts, N, cam, smp, (uint64_t)(hypBegin + i), p, nullptr, fast);
-    }
+    const int st = pnp_hypothesis(pts, N, cam, smp, (uint64_t)(hypBegin + i), p, nullptr, fast);
     if (st == 1) {
         models[i] = p;
         counts[i] = 0;
     } else {
         counts[i] = st;
     }
+}
+
+// EPnP: pnp_hypothesis_epnp split in three kernels (hyp_pnp.h, EpnpSplit). The first and the last
+// hold no LDS; the sweeps kernel between them keeps half of each lane's 12 x 12 in LDS (37 KB per
+// wave, four waves per CU) and half in registers.
+__global__ __launch_bounds__(256) void mcv_epnp_split_mtm(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
+                                                          Sampler smp, int64_t hypBegin, int hypCount, EpnpSplit X,
+                                                          int* __restrict__ counts) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= hypCount) return;
+    counts[i] = pnp_epnp_split_mtm(pts, N, cam, smp, (uint64_t)(hypBegin + i), X, i) == 1 ? 0 : kStatusNoSample;
+}
+__global__ __launch_bounds__(64) void mcv_epnp_split_sweeps(EpnpSplit X, const int* __restrict__ counts,
+                                                             int hypCount) {
+    __shared__ double lds[64 * kEpnpLoStride];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= hypCount || counts[i] < 0) return;
+    pnp_epnp_split_sweeps(X, i, lds + (size_t)threadIdx.x * kEpnpLoStride);
+}
+__global__ __launch_bounds__(256) void mcv_epnp_split_pose(PnpCamera cam, EpnpSplit X, PnpPose* __restrict__ models,
+                                                           const int* __restrict__ counts, int hypCount) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= hypCount || counts[i] < 0) return;
+    PnpPose p;
+    pnp_epnp_split_pose(cam, X, i, p);
+    models[i] = p;
 }
 
 template <int K, bool FUSED>
@@ -703,13 +718,22 @@ void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_
 }
 
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
-                         bool epnp, void* d_models, int* d_counts, hipStream_t s, bool fast) {
-    if (epnp)
-        hipLaunchKernelGGL(mcv_pnp_generate<true>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
-                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast);
-    else
-        hipLaunchKernelGGL(mcv_pnp_generate<false>, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts,
-                           N, to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast);
+                         bool epnp, void* d_models, int* d_counts, double* d_epnpScratch, hipStream_t s, bool fast) {
+    if (!epnp) {
+        hipLaunchKernelGGL(mcv_pnp_generate, dim3((hypCount + 63) / 64), dim3(64), 0, s, (const PnpPoint*)d_pts, N,
+                           to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast);
+        return;
+    }
+    const int64_t S = hypCount;
+    const EpnpSplit X{d_epnpScratch, d_epnpScratch + kMtmSums * S, d_epnpScratch + (kMtmSums + kEpnpCtx) * S,
+                      d_epnpScratch + (kMtmSums + kEpnpCtx + 144) * S, S};
+    const PnpCamera cam = to_cam(cam8);
+    hipLaunchKernelGGL(mcv_epnp_split_mtm, dim3((hypCount + 255) / 256), dim3(256), 0, s, (const PnpPoint*)d_pts, N,
+                       cam, smp, hypBegin, hypCount, X, d_counts);
+    hipLaunchKernelGGL(mcv_epnp_split_sweeps, dim3((hypCount + 63) / 64), dim3(64), 0, s, X,
+                       (const int*)d_counts, hypCount);
+    hipLaunchKernelGGL(mcv_epnp_split_pose, dim3((hypCount + 255) / 256), dim3(256), 0, s, cam, X,
+                       (PnpPose*)d_models, (const int*)d_counts, hypCount);
 }
 
 // Grid of a pose-wave x point-chunk sweep: waves x chunks >= ~8 waves per SIMD, chunks >= 2048
