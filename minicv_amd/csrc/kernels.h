@@ -140,10 +140,12 @@ void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
                          bool epnp, void* d_models, int* d_counts, double* d_epnpScratch, hipStream_t s,
                          bool fast = false);
-// d_ext: 3 doubles of device scratch filled by launch_pnp_extent (the certified sweep's bound).
-void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s);
+// d_ext: 3 doubles of device scratch filled by launch_pnp_extent (the certified sweep's bound);
+// d_pairs: kPnpPairFloatsPerPoint x N floats it fills with the sweep's pair layout.
+static const int kPnpPairFloatsPerPoint = 6;
+void launch_pnp_extent(const void* d_pts, int N, double* d_ext, float* d_pairs, hipStream_t s);
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
-                       float thr2, bool fused, const double* d_ext, hipStream_t s);
+                       float thr2, bool fused, const double* d_ext, const float* d_pairs, hipStream_t s);
 void launch_pnp_one(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hyp, bool epnp,
                     PnpOneOut* d_out, hipStream_t s, bool fast = false);
 void launch_pnp_solve5(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s);

@@ -200,20 +200,30 @@ __global__ __launch_bounds__(256) void mcv_hamming_partial(const uint32_t* __res
     }
 }
 
+// Eight lanes per query (chunks c = j mod 8 on lane j, then a 3-step butterfly): the fold is
+// load-latency-bound, so a query's chunks are read in parallel and 8x more CUs take part.
 __global__ __launch_bounds__(256) void mcv_hamming_merge(const uint2* __restrict__ part, int nq, int nchunks,
                                                          int* __restrict__ idx, int* __restrict__ dist,
                                                          int* __restrict__ idx2, int* __restrict__ dist2) {
-    const int qi = blockIdx.x * 256 + threadIdx.x;
-    if (qi >= nq) return;
+    const int qi = blockIdx.x * 32 + (threadIdx.x >> 3);
+    const int j = threadIdx.x & 7;
     uint32_t m1 = 0xFFFFFFFFu, m2 = 0xFFFFFFFFu;
-    // unrolled so that several partials are in flight per lane (the merge is load-latency-bound)
-#pragma unroll 8
-    for (int c = 0; c < nchunks; ++c) {
-        const uint2 p = part[(size_t)c * nq + qi];
-        m2 = min(m2, max(m1, p.x));
-        m1 = min(m1, p.x);
-        m2 = min(m2, p.y);
+    if (qi < nq) {
+#pragma unroll 4
+        for (int c = j; c < nchunks; c += 8) {
+            const uint2 p = part[(size_t)c * nq + qi];
+            m2 = min(m2, max(m1, p.x));
+            m1 = min(m1, p.x);
+            m2 = min(m2, p.y);
+        }
     }
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {   // keys are distinct (index field): min / max merge exactly
+        const uint32_t o1 = __shfl_xor(m1, off, 64), o2 = __shfl_xor(m2, off, 64);
+        m2 = min(max(m1, o1), min(m2, o2));
+        m1 = min(m1, o1);
+    }
+    if (qi >= nq || j != 0) return;
     idx[qi] = m1 == 0xFFFFFFFFu ? -1 : (int)(m1 & kIdxMask);
     dist[qi] = m1 == 0xFFFFFFFFu ? INT_MAX : (int)(m1 >> kIdxBits);
     if (idx2) idx2[qi] = m2 == 0xFFFFFFFFu ? -1 : (int)(m2 & kIdxMask);
@@ -250,12 +260,22 @@ static constexpr int kHamChunkRows = 4096;   // j' < 4096 < 8192: the key's inde
 // Block = WPB waves x QT query tiles of 32 (VGPR-resident B fragments); the block's train tiles (32
 // rows x Kp bytes, expanded from the packed rows) are staged in LDS (double buffer, 16-byte row pad:
 // conflict-free ds_read_b128) and each A fragment read from LDS feeds QT MFMAs. Grid = (query blocks)
-// x (train chunks of <= 4096 rows); the chunk's top-2 per query goes to part[chunk][query]
-// (mcv_hamming_merge folds the chunks).
+// x (train chunks of <= 4096 rows); the chunk's top-2 per query goes to part[chunk][query], and the
+// block that completes a query block's last chunk (an arrival counter per query block) folds its
+// chunks into the outputs as mcv_hamming_merge does, without a second launch. The XCDs' L2s are not
+// coherent, and an agent-scope fence writes back or invalidates a whole L2 (per block: 30 -> 93 us),
+// so every cross-block value is a device-scope atomic instead: the partials are stored and read with
+// agent-scope atomic stores / loads (sc1: performed at the device-coherent level, never stale in an
+// L2), each block waits for its stores to complete (s_waitcnt vmcnt(0), a compiler barrier too) before
+// its agent-scope arrival add, and the last block's loads are issued after that add returns.
 template <int W, int QT, int WPB, int SUB>
 __global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
                                                              const uint32_t* __restrict__ t, int nt, int ntTiles,
-                                                             int tilesPerChunk, uint2* __restrict__ part, bool xcdMap) {
+                                                             int tilesPerChunk, uint2* __restrict__ part, bool xcdMap,
+                                                             unsigned* __restrict__ arrivals, int* __restrict__ oIdx,
+                                                             int* __restrict__ oDist, int* __restrict__ oIdx2,
+                                                             int* __restrict__ oDist2) {
+    static_assert(QT * 32 * WPB == 64 * WPB, "the fold takes one query per thread");
     constexpr int KS = W;                  // k steps of 32 bytes (Kp = 32 W)
     constexpr int RB = 32 * KS;            // bytes per expanded row
     constexpr int RBP = RB + 16;           // LDS row stride
@@ -378,8 +398,38 @@ __global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const uint32_t* __r
             return k >= (1u << 29) ? 0xFFFFFFFFu : ((k >> 13) << kIdxBits) | (base + (k & (kHamChunkRows - 1)));
         };
         const int qi = q0 + 32 * qt + col;
-        if (h == 0 && qi < nq) part[(size_t)by * nq + qi] = make_uint2(glob(m1[qt]), glob(m2[qt]));
+        if (h == 0 && qi < nq) {
+            const uint64_t v = (uint64_t)glob(m1[qt]) | ((uint64_t)glob(m2[qt]) << 32);
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(part) + (size_t)by * nq + qi, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
+    __shared__ int lastBlock;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        lastBlock = __hip_atomic_fetch_add(arrivals + bx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    gridDim.y - 1u;
+    __syncthreads();
+    if (!lastBlock) return;
+    const int qm = bx * (QT * 32 * WPB) + threadIdx.x;
+    if (qm < nq) {
+        uint32_t a1 = 0xFFFFFFFFu, a2 = 0xFFFFFFFFu;
+#pragma unroll 8
+        for (int c = 0; c < (int)gridDim.y; ++c) {
+            const uint64_t pv = __hip_atomic_load(reinterpret_cast<const uint64_t*>(part) + (size_t)c * nq + qm,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint2 pc = make_uint2((uint32_t)pv, (uint32_t)(pv >> 32));
+            a2 = min(a2, max(a1, pc.x));
+            a1 = min(a1, pc.x);
+            a2 = min(a2, pc.y);
+        }
+        oIdx[qm] = a1 == 0xFFFFFFFFu ? -1 : (int)(a1 & kIdxMask);
+        oDist[qm] = a1 == 0xFFFFFFFFu ? INT_MAX : (int)(a1 >> kIdxBits);
+        if (oIdx2) oIdx2[qm] = a2 == 0xFFFFFFFFu ? -1 : (int)(a2 & kIdxMask);
+        if (oDist2) oDist2[qm] = a2 == 0xFFFFFFFFu ? INT_MAX : (int)(a2 >> kIdxBits);
+    }
+    if (threadIdx.x == 0) arrivals[bx] = 0u;   // re-armed for the next launch (ordered by the kernel boundary)
 }
 
 // Re-pack [n][bytes] rows into zero-padded [n][W] 32-bit words (XOR of the zero pads is 0).
@@ -400,6 +450,8 @@ __global__ void mcv_hamming_repack(const uint8_t* __restrict__ src, int n, int b
 struct HammingWork {
     DevBuf<uint32_t> qpack, tpack;
     DevBuf<uint2> part;
+    DevBuf<unsigned> arrivals;   // per query block of the GEMM form (zero between launches)
+    size_t arrivalsZeroed = 0;
     StreamFence fence;   // calls on different streams take turns on these buffers
 };
 
@@ -444,14 +496,17 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
         const bool xcdMap = (8 % nchunks) == 0 || nchunks % 8 == 0;
         wk.part.ensure((size_t)nchunks * nq);
+        if (wk.arrivalsZeroed < (size_t)qblocks) {
+            wk.arrivals.ensure((size_t)qblocks);
+            MCV_HIP(hipMemsetAsync(wk.arrivals.p, 0, wk.arrivals.n * sizeof(unsigned), s));
+            wk.arrivalsZeroed = wk.arrivals.n;
+        }
         {
             ProfScope ps("hamming", s);
             hipLaunchKernelGGL((W == 8 ? mcv_hamming_mfma<8, QT, WPB, SUB> : mcv_hamming_mfma<16, QT, WPB, SUB>),
                                dim3(qblocks, nchunks), dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, tilesPerChunk,
-                               wk.part.p, xcdMap);
+                               wk.part.p, xcdMap, wk.arrivals.p, d_idx, d_dist, d_idx2, d_dist2);
         }
-        hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nchunks, d_idx,
-                           d_dist, d_idx2, d_dist2);
         MCV_HIP(hipGetLastError());
         wk.fence.leave(s);
         return nq;
@@ -473,7 +528,7 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         hipLaunchKernelGGL((W == 8 ? mcv_hamming_partial<8, Q, NB> : mcv_hamming_partial<16, Q, NB>), grid, dim3(256),
                            0, s, q, nq, t, nt, chunkLen, wk.part.p);
     }
-    hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 255) / 256), dim3(256), 0, s, wk.part.p, nq, nparts, d_idx,
+    hipLaunchKernelGGL(mcv_hamming_merge, dim3((nq + 31) / 32), dim3(256), 0, s, wk.part.p, nq, nparts, d_idx,
                        d_dist, d_idx2, d_dist2);
     MCV_HIP(hipGetLastError());
     wk.fence.leave(s);

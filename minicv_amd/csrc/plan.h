@@ -64,7 +64,7 @@ struct Plan {
     DevBuf<float> bbox;       // max |x|, max |y| of the source points (fused fast-path bound)
     DevBuf<double> bb4;       // F / E: max |x1|, |y1|, |x2|, |y2| (packed-fp32 Sampson prefilter bound)
     DevBuf<double> h64;       // homography: each hypothesis' fp64 model (finalize takes the winner's)
-    DevBuf<float> pairs;      // homography: paired layout of the packed sweep (8 floats per 2)
+    DevBuf<float> pairs;      // paired point layout of the packed sweeps (homography 8, PnP 12 floats per 2)
     DevBuf<uint8_t> one;      // single-hypothesis output record
     DevBuf<double> ptsd;      // essential: double4 normalised correspondences
     DevBuf<double> raw;       // essential: uploaded V2d pairs (a then b)

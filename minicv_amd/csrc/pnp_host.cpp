@@ -142,9 +142,10 @@ void p_evaluate_chunk(Plan& P, const void* d_pts, int N, const RansacConfig& cfg
     }
     mark_chunk(P, hypBegin, hypCount, smp, d_pts, N, epnp ? 1 : (fast_ap3p(cfg) ? 2 : 0), s);
     P.bb4.ensure(4);
-    launch_pnp_extent(d_pts, N, P.bb4.p, s);
+    P.pairs.ensure((size_t)(N + 1) * kPnpPairFloatsPerPoint);
+    launch_pnp_extent(d_pts, N, P.bb4.p, P.pairs.p, s);
     ProfScope ps("pnp_verify", s);
-    launch_pnp_verify(d_pts, N, P.pnpCam, P.models.p, d_counts, hypCount, thr2, fused_pnp(cfg), P.bb4.p, s);
+    launch_pnp_verify(d_pts, N, P.pnpCam, P.models.p, d_counts, hypCount, thr2, fused_pnp(cfg), P.bb4.p, P.pairs.p, s);
 }
 
 static PnpOneOut pnp_fetch_one(Plan& P, hipStream_t s) {
@@ -869,9 +870,10 @@ extern "C" MCV_API int mcvTestPnpSweep(const float* pts, int N, const double* ca
         MCV_HIP(hipMemcpyAsync(P.models.p, m.data(), m.size() * sizeof(PnpPose), hipMemcpyHostToDevice, s));
         MCV_HIP(hipMemsetAsync(P.counts.p, 0, (size_t)nPoses * sizeof(int), s));
         P.bb4.ensure(4);
-        launch_pnp_extent(P.ptsd.p, N, P.bb4.p, s);
+        P.pairs.ensure((size_t)(N + 1) * kPnpPairFloatsPerPoint);
+        launch_pnp_extent(P.ptsd.p, N, P.bb4.p, P.pairs.p, s);
         launch_pnp_verify(P.ptsd.p, N, P.pnpCam, P.models.p, P.counts.p, nPoses, thr2, fused != 0,
-                          mode == 0 ? P.bb4.p : nullptr, s);
+                          mode == 0 ? P.bb4.p : nullptr, P.pairs.p, s);
         MCV_HIP(hipGetLastError());
         MCV_HIP(hipMemcpyAsync(counts, P.counts.p, (size_t)nPoses * sizeof(int), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));

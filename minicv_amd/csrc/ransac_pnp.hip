@@ -134,11 +134,16 @@ __global__ __launch_bounds__(256) void mcv_pnp_verify(const PnpPoint* __restrict
 
 // Point extents for the prefilter's bound: ext = {max |X|, max |Y|, max |Z|} as the ordered bit
 // patterns of non-negative doubles (atomicMax; zeroed by the caller), inf for a non-finite coordinate.
+// Also writes the sweep's pair layout: points 2j, 2j + 1 as kPnpPairFloats floats {X0 X1 Y0 Y1 | Z0 Z1
+// U0 U1 | V0 V1 - -} at pairs + kPnpPairFloats j (three 16-byte loads give a lane its packed operands).
+static constexpr int kPnpPairFloats = 2 * kPnpPairFloatsPerPoint;
 __global__ __launch_bounds__(256) void mcv_pnp_extent(const PnpPoint* __restrict__ pts, int N,
-                                                      unsigned long long* __restrict__ ext) {
+                                                      unsigned long long* __restrict__ ext, float* __restrict__ pairs) {
     double m0 = 0, m1 = 0, m2 = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < N; i += gridDim.x * 256) {
         const PnpPoint q = pts[i];
+        float* o = pairs + (size_t)(i >> 1) * kPnpPairFloats + (i & 1);
+        o[0] = q.X; o[2] = q.Y; o[4] = q.Z; o[6] = q.u; o[8] = q.v;
         const double x = q.X, y = q.Y, z = q.Z;
         m0 = x - x == 0 ? fmax(m0, fabs(x)) : __builtin_inf();
         m1 = y - y == 0 ? fmax(m1, fabs(y)) : __builtin_inf();
@@ -204,7 +209,7 @@ template <int K, int WPE, bool LANE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void mcv_pnp_verify_pk(const PnpPoint* __restrict__ pts, int N, int chunk,
                                                          PnpCamera cam, PnpPkCam pc, const PnpPose* __restrict__ models,
                                                          int* __restrict__ counts, int hypCount, float thr2, bool fused,
-                                                         const double* __restrict__ ext) {
+                                                         const double* __restrict__ ext, const float* __restrict__ pairs) {
     static_assert(K <= 8, "pose mask in 8 bits");
     constexpr int kCap = LANE ? kPnpLaneEvents : kPnpEvents;
     __shared__ uint32_t events[4][kCap];
@@ -250,14 +255,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int k = 0; k < K; ++k) cnt[k] = 0;
     int nev = 0;
-    for (int base = p0; base < p1; base += 128) {
+    // one trip: 128 points (two per lane) against the K poses; vm0 / vm1 = the lanes whose points exist
+    auto trip = [&](int base, pkf2 X, pkf2 Y, pkf2 Z, pkf2 U, pkf2 V, uint64_t vm0, uint64_t vm1) {
         const int i0 = base + 2 * lane, i1 = i0 + 1;
-        const bool v0 = i0 < p1, v1 = i1 < p1;
-        const PnpPoint a = pts[v0 ? i0 : p0];
-        const PnpPoint b = pts[v1 ? i1 : p0];
-        const uint64_t vm0 = __builtin_amdgcn_ballot_w64(v0), vm1 = __builtin_amdgcn_ballot_w64(v1);
-        const pkf2 X = pkf2{a.X, b.X}, Y = pkf2{a.Y, b.Y}, Z = pkf2{a.Z, b.Z};
-        const pkf2 U = pkf2{a.u, b.u}, V = pkf2{a.v, b.v};
         uint32_t und = 0;
         asm volatile("" : "+s"(cv.k2tp1), "+s"(cv.tp2p1), "+s"(cv.p2fx), "+s"(cv.fyA4));
 #pragma unroll
@@ -306,6 +306,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 ++nev;
             }
         }
+    };
+    // full trips: every point exists (chunks are multiples of 128 points); operands straight from the pair
+    // layout, no bounds or address selects
+    const int nFull = p0 + (p1 - p0) / 128 * 128;
+    const float4* pr4 = reinterpret_cast<const float4*>(pairs) + (size_t)(p0 / 2 + lane) * (kPnpPairFloats / 4);
+    for (int base = p0; base < nFull; base += 128, pr4 += 64 * (kPnpPairFloats / 4)) {
+        const float4 a = pr4[0], b = pr4[1], c = pr4[2];
+        trip(base, pkf2{a.x, a.y}, pkf2{a.z, a.w}, pkf2{b.x, b.y}, pkf2{b.z, b.w}, pkf2{c.x, c.y}, ~0ull, ~0ull);
+    }
+    if (nFull < p1) {   // the chunk's partial trip
+        const int base = nFull;
+        const int i0 = base + 2 * lane, i1 = i0 + 1;
+        const bool v0 = i0 < p1, v1 = i1 < p1;
+        const PnpPoint a = pts[v0 ? i0 : p0];
+        const PnpPoint b = pts[v1 ? i1 : p0];
+        trip(base, pkf2{a.X, b.X}, pkf2{a.Y, b.Y}, pkf2{a.Z, b.Z}, pkf2{a.u, b.u}, pkf2{a.v, b.v},
+             __builtin_amdgcn_ballot_w64(v0), __builtin_amdgcn_ballot_w64(v1));
     }
     if constexpr (LANE) {
         // exact recount, 64 logged lanes per pass; an overflowing log recounts every (point, pose) of
@@ -770,37 +787,39 @@ static void launch_pnp_verify_k(const void* d_pts, int N, const double* cam8, co
 template <int K>
 static void launch_pnp_verify_pk_k(const void* d_pts, int N, const double* cam8, const PnpPkCam& pc,
                                    const void* d_models, int* d_counts, int hypCount, float thr2, bool fused,
-                                   const double* d_ext, hipStream_t s) {
+                                   const double* d_ext, const float* d_pairs, hipStream_t s) {
     dim3 grid;
     int chunk;
     pnp_verify_grid(N, hypCount, K, 128, grid, chunk);
     // the per-lane log of undecided (point, pose) lanes needs (point - p0) << 3 in 32 bits; a larger
     // chunk takes the trip log (a whole fp64 trip per undecided (trip, pose))
     if (chunk < (1 << 28))
-        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3, true>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N,
-                           chunk, to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
+        hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 5, true>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N,
+                           chunk, to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext,
+                           d_pairs);
     else
         hipLaunchKernelGGL((mcv_pnp_verify_pk<K, 3, false>), grid, dim3(256), 0, s, (const PnpPoint*)d_pts, N, chunk,
-                           to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext);
+                           to_cam(cam8), pc, (const PnpPose*)d_models, d_counts, hypCount, thr2, fused, d_ext,
+                           d_pairs);
 }
 
-void launch_pnp_extent(const void* d_pts, int N, double* d_ext, hipStream_t s) {
+void launch_pnp_extent(const void* d_pts, int N, double* d_ext, float* d_pairs, hipStream_t s) {
     (void)hipMemsetAsync(d_ext, 0, 3 * sizeof(double), s);   // errors surface at the caller's hipGetLastError
     if (N <= 0) return;
     int blocks = (N + 255) / 256;
     if (blocks > 256) blocks = 256;
     hipLaunchKernelGGL(mcv_pnp_extent, dim3(blocks), dim3(256), 0, s, (const PnpPoint*)d_pts, N,
-                       (unsigned long long*)d_ext);
+                       (unsigned long long*)d_ext, d_pairs);
 }
 
 // The certified packed-fp32 sweep (kVerifyPnpPosesPerWave poses per wave); the all-fp64 sweep when the
 // camera / threshold leaves the bound's domain. d_ext = launch_pnp_extent's output.
 void launch_pnp_verify(const void* d_pts, int N, const double* cam8, const void* d_models, int* d_counts, int hypCount,
-                       float thr2, bool fused, const double* d_ext, hipStream_t s) {
+                       float thr2, bool fused, const double* d_ext, const float* d_pairs, hipStream_t s) {
     const PnpPkCam pc = pnp_pk_cam_host(cam8, thr2);
-    if (pc.ok && d_ext)
+    if (pc.ok && d_ext && d_pairs)
         launch_pnp_verify_pk_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, pc, d_models, d_counts, hypCount, thr2, fused,
-                                                       d_ext, s);
+                                                       d_ext, d_pairs, s);
     else
         launch_pnp_verify_k<kVerifyPnpPosesPerWave>(d_pts, N, cam8, d_models, d_counts, hypCount, thr2, fused, s);
 }
