@@ -294,13 +294,13 @@ def bench_matcher(args):
             if form == 16:   # f16-split GEMM form: three f16 MFMA products per (query, train, dim)
                 roof = {"bound": "mfma-f16", "achieved": 3.0 * tf, "peak": F16_MFMA_PEAK_TF, "unit": "TFLOP/s",
                         "frac": 3.0 * tf / F16_MFMA_PEAK_TF,
-                        "kernel": "mcv_l2_mfma16q",
+                        "kernel": "mcv_l2_gemm",
                         "model": "fp32 operands split into f16 hi + lo; hi.hi + hi.lo + lo.hi on "
                                  "v_mfma_f32_32x32x16_f16 = 3 x 2 Nq Nt D MFMA flops per launch; "
                                  f"algorithmic rate {tf:.1f} TFLOP/s (2 Nq Nt D)"}
             else:
                 roof = {"bound": "mfma", "achieved": tf, "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                        "frac": tf / FP32_MFMA_PEAK_TF, "kernel": "mcv_l2_mfma"}
+                        "frac": tf / FP32_MFMA_PEAK_TF, "kernel": "mcv_l2_gemm"}
             roof.update({"traffic": load_traffic(roof["kernel"], f"{nq}x{nt}"), "avg_launch_ms": avg_ms,
                          "timed_launches": launches, "timed_every": MATCHER_PROF_STRIDE})
             line = {"metric": "BF L2 knn-2 TFLOP/s, SIFT-128 50k x 50k fp32 GEMM on MFMA (BASELINE config[4])",

@@ -384,6 +384,12 @@ struct EpnpWsSoA {
     int64_t s;
     MCV_HD double& operator()(int r, int c) const { return p[(int64_t)(12 * r + c) * s]; }
 };
+// L_6x10 and rho alone (rows 0..5, columns 0..10) at p[11 r + c]: the betas kernel's per-lane LDS copy,
+// which Gauss-Newton re-reads every iteration.
+struct EpnpLRef {
+    double* p;
+    MCV_HD double& operator()(int r, int c) const { return p[11 * r + c]; }
+};
 
 // jacobi_svd_core's tail for the 12 x 12 without V (EPnP's cvSVD of M^T M) on a view: the row norms,
 // the descending selection sort (row swaps) and the cv::RNG completion of null rows, in the generic
@@ -408,37 +414,45 @@ MCV_HD void jacobi12_tail(const WS& A, double (&W)[12]) {
             for (int k = 0; k < 12; ++k) { const double t = A(i, k); A(i, k) = A(j, k); A(j, k) = t; }
         }
     }
+    // row i in registers while it is completed / normalised (the view may be memory the compiler cannot
+    // prove distinct from row j's)
     CvRng rng{0x12345678u};
     for (int i = 0; i < 12; ++i) {
         double sd = W[i];
+        double ri[12];
+        MCV_SMALL_UNROLL
+        for (int k = 0; k < 12; ++k) ri[k] = A(i, k);
         for (int ii = 0; ii < 100 && sd <= minval; ++ii) {
             const double val0 = 1. / 12;
             MCV_SMALL_UNROLL
-            for (int k = 0; k < 12; ++k) A(i, k) = (rng.next() & 256) != 0 ? val0 : -val0;
+            for (int k = 0; k < 12; ++k) ri[k] = (rng.next() & 256) != 0 ? val0 : -val0;
             for (int it = 0; it < 2; ++it)
                 for (int j = 0; j < i; ++j) {
+                    double rj[12];
+                    MCV_SMALL_UNROLL
+                    for (int k = 0; k < 12; ++k) rj[k] = A(j, k);
                     sd = 0;
                     MCV_SMALL_UNROLL
-                    for (int k = 0; k < 12; ++k) sd += A(i, k) * A(j, k);
+                    for (int k = 0; k < 12; ++k) sd += ri[k] * rj[k];
                     double asum = 0;
                     MCV_SMALL_UNROLL
                     for (int k = 0; k < 12; ++k) {
-                        const double t = A(i, k) - sd * A(j, k);
-                        A(i, k) = t;
+                        const double t = ri[k] - sd * rj[k];
+                        ri[k] = t;
                         asum += __builtin_fabs(t);
                     }
                     asum = asum > eps * 100 ? 1 / asum : 0;
                     MCV_SMALL_UNROLL
-                    for (int k = 0; k < 12; ++k) A(i, k) *= asum;
+                    for (int k = 0; k < 12; ++k) ri[k] *= asum;
                 }
             sd = 0;
             MCV_SMALL_UNROLL
-            for (int k = 0; k < 12; ++k) sd += A(i, k) * A(i, k);
+            for (int k = 0; k < 12; ++k) sd += ri[k] * ri[k];
             sd = __builtin_sqrt(sd);
         }
         const double s = sd > minval ? 1 / sd : 0.;
         MCV_SMALL_UNROLL
-        for (int k = 0; k < 12; ++k) A(i, k) *= s;
+        for (int k = 0; k < 12; ++k) A(i, k) = ri[k] * s;
     }
 }
 
@@ -832,10 +846,9 @@ MCV_HD void epnp_small_mtm(const double (&pw)[NP][3], const double (&us)[NP][2],
 }
 
 template <int NP, class WS>
-MCV_HD void epnp_small_pose(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
-                            const double (&al)[NP][4], const WS& ws, double (&Rout)[3][3], double (&tout)[3]) {
-    double betas[4][4];
-    epnp_betas_from_l(betas, ws);   // v, L and rho in ws
+MCV_HD void epnp_small_pick(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
+                            const double (&al)[NP][4], const WS& ws, const double (&betas)[4][4],
+                            double (&Rout)[3][3], double (&tout)[3]) {
     double pw0[3] = {0, 0, 0};
     for (int i = 0; i < NP; ++i)
         for (int j = 0; j < 3; ++j) pw0[j] += pw[i][j];
@@ -872,6 +885,15 @@ MCV_HD void epnp_small_pose(const double (&pw)[NP][3], const double (&us)[NP][2]
             }
         }
     }
+}
+
+// The betas of the three approximations (v, L and rho in ws), then the three poses and the pick.
+template <int NP, class WS>
+MCV_HD void epnp_small_pose(const double (&pw)[NP][3], const double (&us)[NP][2], const EpnpCam& cam,
+                            const double (&al)[NP][4], const WS& ws, double (&Rout)[3][3], double (&tout)[3]) {
+    double betas[4][4];
+    epnp_betas_from_l(betas, ws);
+    epnp_small_pick<NP>(pw, us, cam, al, ws, betas, Rout, tout);
 }
 
 template <int NP>

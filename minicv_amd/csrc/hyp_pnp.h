@@ -592,9 +592,12 @@ MCV_HD int pnp_hypothesis_epnp(const PnpPoint* pts, int N, const PnpCamera& c, c
 // Kernel 1: sample, control points, alphas, M^T M. Kernel 2: the SVD's Jacobi sweeps, the only part
 // that needs a per-lane working matrix in LDS (jacobi12_sweeps_split: half of it in LDS, half in
 // registers, four waves per CU). Kernel 3: the SVD's tail (norms, sort, null-row completion) on the
-// matrix in global scratch, L_6x10, the betas, Gauss-Newton and the three poses. Every value crosses
-// the kernels as the same double and every operation keeps its order, so the composition computes
-// pnp_hypothesis_epnp's bits.
+// matrix in global scratch and L_6x10. Kernel 4: the betas of the three approximations with their
+// Gauss-Newton steps (L_6x10 and rho copied to a per-lane LDS slice: Gauss-Newton re-reads them every
+// iteration). Kernel 5: the three poses and compute_pose's pick. Every value crosses the kernels as the
+// same double and every operation keeps its order, so the composition computes pnp_hypothesis_epnp's
+// bits. Split by register footprint: one kernel held 422 registers (one wave per SIMD) and 3.97 ms per
+// 2^20 hypotheses for kernels 3-5, which take 0.80 + 1.64 + 0.58 ms.
 static const int kEpnpCtx = 57;   // pw (15), us (10), al (20), cws (12)
 struct EpnpSplit {
     double* mtm;   // kMtmSums x s
@@ -664,18 +667,35 @@ MCV_HD void pnp_epnp_split_sweeps(const EpnpSplit& X, int64_t i, double* lo) {
     }
 }
 
-// Kernel 3: the SVD's tail and L_6x10 on the matrix in scratch, then the betas, Gauss-Newton and the
-// pose pick.
+// Kernel 3: the SVD's tail and L_6x10 on the matrix in scratch. Kernel 4: the betas of the three
+// approximations (Gauss-Newton included) into the M^T M slots, which kernel 2 has consumed.
+MCV_HD void pnp_epnp_split_tail(const EpnpSplit& X, int64_t i) {
+    const EpnpWsSoA A{X.A + i, X.s};
+    double W[12], cws[4][3];
+    for (int a = 0; a < 12; ++a) W[a] = X.W[a * X.s + i];
+    jacobi12_tail(A, W);
+    for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 3; ++j) cws[k][j] = X.ctx[(45 + 3 * k + j) * X.s + i];
+    epnp_l_rows(cws, A);
+}
+MCV_HD void pnp_epnp_split_betas(const EpnpSplit& X, int64_t i, double* lds66) {
+    const EpnpWsSoA A{X.A + i, X.s};
+    const EpnpLRef L{lds66};
+    for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 11; ++c) L(r, c) = A(r, c);
+    double betas[4][4];
+    epnp_betas_from_l(betas, L);
+    for (int n = 1; n < 4; ++n)
+        for (int k = 0; k < 4; ++k) X.mtm[(4 * (n - 1) + k) * X.s + i] = betas[n][k];
+}
+
+// Kernel 5: the three poses from the betas and the null-space vectors, and compute_pose's pick.
 MCV_HD void pnp_epnp_split_pose(const PnpCamera& c, const EpnpSplit& X, int64_t i, PnpPose& pose) {
     const EpnpWsSoA A{X.A + i, X.s};
-    {
-        double W[12], cws[4][3];
-        for (int a = 0; a < 12; ++a) W[a] = X.W[a * X.s + i];
-        jacobi12_tail(A, W);
-        for (int k = 0; k < 4; ++k)
-            for (int j = 0; j < 3; ++j) cws[k][j] = X.ctx[(45 + 3 * k + j) * X.s + i];
-        epnp_l_rows(cws, A);
-    }
+    double betas[4][4];
+    for (int k = 0; k < 4; ++k) betas[0][k] = 0;
+    for (int n = 1; n < 4; ++n)
+        for (int k = 0; k < 4; ++k) betas[n][k] = X.mtm[(4 * (n - 1) + k) * X.s + i];
     double pw[5][3], us[5][2], al[5][4];
     const double* q = X.ctx + i;
     int e = 0;
@@ -686,7 +706,7 @@ MCV_HD void pnp_epnp_split_pose(const PnpCamera& c, const EpnpSplit& X, int64_t 
     for (int k = 0; k < 5; ++k)
         for (int j = 0; j < 4; ++j) al[k][j] = q[(e++) * X.s];
     double R[3][3], t[3];
-    epnp_small_pose<5>(pw, us, EpnpCam{c.fx, c.fy, c.cx, c.cy}, al, A, R, t);
+    epnp_small_pick<5>(pw, us, EpnpCam{c.fx, c.fy, c.cx, c.cy}, al, A, betas, R, t);
     for (int r = 0; r < 3; ++r) {
         for (int j = 0; j < 3; ++j) pose.R[3 * r + j] = R[r][j];
         pose.t[r] = t[r];

@@ -56,9 +56,9 @@ __global__ __launch_bounds__(64) void mcv_pnp_generate(const PnpPoint* __restric
     }
 }
 
-// EPnP: pnp_hypothesis_epnp split in three kernels (hyp_pnp.h, EpnpSplit). The first and the last
-// hold no LDS; the sweeps kernel between them keeps half of each lane's 12 x 12 in LDS (37 KB per
-// wave, four waves per CU) and half in registers.
+// EPnP: pnp_hypothesis_epnp split in five kernels (hyp_pnp.h, EpnpSplit). The sweeps kernel keeps half
+// of each lane's 12 x 12 in LDS (37 KB per wave, four waves per CU) and half in registers; the betas
+// kernel keeps L_6x10 / rho in a per-lane LDS slice; the others hold no LDS.
 __global__ __launch_bounds__(256) void mcv_epnp_split_mtm(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
                                                           Sampler smp, int64_t hypBegin, int hypCount, EpnpSplit X,
                                                           int* __restrict__ counts) {
@@ -72,6 +72,17 @@ __global__ __launch_bounds__(64) void mcv_epnp_split_sweeps(EpnpSplit X, const i
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= hypCount || counts[i] < 0) return;
     pnp_epnp_split_sweeps(X, i, lds + (size_t)threadIdx.x * kEpnpLoStride);
+}
+__global__ __launch_bounds__(256) void mcv_epnp_split_tail(EpnpSplit X, const int* __restrict__ counts, int hypCount) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= hypCount || counts[i] < 0) return;
+    pnp_epnp_split_tail(X, i);
+}
+__global__ __launch_bounds__(64) void mcv_epnp_split_betas(EpnpSplit X, const int* __restrict__ counts, int hypCount) {
+    __shared__ double lds[64 * 67];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= hypCount || counts[i] < 0) return;
+    pnp_epnp_split_betas(X, i, lds + threadIdx.x * 67);
 }
 __global__ __launch_bounds__(256) void mcv_epnp_split_pose(PnpCamera cam, EpnpSplit X, PnpPose* __restrict__ models,
                                                            const int* __restrict__ counts, int hypCount) {
@@ -749,6 +760,10 @@ void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler s
                        cam, smp, hypBegin, hypCount, X, d_counts);
     hipLaunchKernelGGL(mcv_epnp_split_sweeps, dim3((hypCount + 63) / 64), dim3(64), 0, s, X,
                        (const int*)d_counts, hypCount);
+    hipLaunchKernelGGL(mcv_epnp_split_tail, dim3((hypCount + 255) / 256), dim3(256), 0, s, X, (const int*)d_counts,
+                       hypCount);
+    hipLaunchKernelGGL(mcv_epnp_split_betas, dim3((hypCount + 63) / 64), dim3(64), 0, s, X, (const int*)d_counts,
+                       hypCount);
     hipLaunchKernelGGL(mcv_epnp_split_pose, dim3((hypCount + 255) / 256), dim3(256), 0, s, cam, X,
                        (PnpPose*)d_models, (const int*)d_counts, hypCount);
 }

@@ -22,7 +22,7 @@ PROF = ROOT / "profiles"
 WORKLOADS = ["homography", "fundamental", "essential", "pnp", "hamming", "l2", "scaled"]
 # dominant kernel per BASELINE workload (substring of the demangled rocprofv3 kernel name)
 KERNELS = {"homography": "mcv_h_verify_cert", "fundamental": "mcv_f_verify", "hamming": "mcv_hamming_mfma",
-           "l2": "mcv_l2_mfma16q", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify",
+           "l2": "mcv_l2_gemm", "essential": "mcv_e_verify", "pnp": "mcv_pnp_verify",
            "scaled": "mcv_scaled_costs"}
 EXTRA_BENCH = ["homography_fused", "homography_fast", "pnp_ap3p", "essential_fast"]   # second bench lines (bench_<name>.log)
 
