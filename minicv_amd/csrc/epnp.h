@@ -47,6 +47,48 @@ MCV_HD double cv_hypot(double a, double b) {
     return 0;
 }
 
+// JacobiSVDImpl_'s rotation: with p the doubled dot product and a, b the two rows' squared norms,
+//   beta = a - b, gamma = hypot(p, beta) (cv_hypot), and for beta < 0: s = sqrt((gamma - beta) / 2 /
+//   gamma), c = p / (gamma s 2); else c = sqrt((gamma + beta) / (gamma 2)), s = p / (gamma c 2).
+// Device: when max(|p|, |beta|) is in [2^-63, 2^60] and min(|p|, |beta|) and |p| are 0 or >= 2^-900,
+// every quotient takes gfx950's refined-reciprocal form and every sqrt the unscaled expansion
+// (arguments in [0.5, 2]), both bit-identical to IEEE there (mcvTestDivF64 modes 0-5); a lane outside
+// that domain takes the IEEE operations (a branch no lane takes on EPnP's systems, so the wave skips
+// it). The dependent chain of a rotating pair shrinks from ~45 to ~30 fp64 operations. Host: IEEE.
+MCV_HD void svd_rotation(double p, double a, double b, double& c, double& s) {
+    const double beta = a - b;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double ap = __builtin_fabs(p), ab = __builtin_fabs(beta);
+    const bool pg = ap > ab;
+    const double hi = pg ? ap : ab, lo = pg ? ab : ap;
+    if (__builtin_expect(hi <= 0x1p60 && hi >= 0x1p-63 && (lo == 0.0 || lo >= 0x1p-900) && ap >= 0x1p-900, 1)) {
+        const double r1 = div_f64_refined(lo, hi, rcp_f64_refined(hi));
+        const double gamma = hi * sqrt_f64_1to2(1 + r1 * r1);   // cv_hypot(p, beta): either branch
+        if (beta < 0) {
+            const double delta = (gamma - beta) * 0.5;
+            s = sqrt_f64_1to2(div_f64_refined(delta, gamma, rcp_f64_refined(gamma)));
+            const double d2 = gamma * s * 2;
+            c = div_f64_refined(p, d2, rcp_f64_refined(d2));
+        } else {
+            const double g2 = gamma * 2;
+            c = sqrt_f64_1to2(div_f64_refined(gamma + beta, g2, rcp_f64_refined(g2)));
+            const double d2 = gamma * c * 2;
+            s = div_f64_refined(p, d2, rcp_f64_refined(d2));
+        }
+        return;
+    }
+#endif
+    const double gamma = cv_hypot(p, beta);
+    if (beta < 0) {
+        const double delta = (gamma - beta) * 0.5;
+        s = __builtin_sqrt(delta / gamma);
+        c = p / (gamma * s * 2);
+    } else {
+        c = __builtin_sqrt((gamma + beta) / (gamma * 2));
+        s = p / (gamma * c * 2);
+    }
+}
+
 // JacobiSVDImpl_<double>: A holds the N rows of length M of the TRANSPOSED input (At). On return
 // A's rows are the left singular vectors (normalised), Wo the singular values (descending), and
 // Vt (if non-null) the right singular vectors as rows. The A result does not depend on Vt.
@@ -91,16 +133,8 @@ MCV_HD void jacobi_svd_core(double (&A)[N1][M], double (&Wo)[N], double (*Vt)[N]
                     for (int k = 0; k < M; ++k) p += A[i][k] * A[j][k];
                     if (__builtin_fabs(p) <= eps * __builtin_sqrt(a * b)) continue;
                     p *= 2;
-                    const double beta = a - b, gamma = cv_hypot(p, beta);
                     double c, s;
-                    if (beta < 0) {
-                        const double delta = (gamma - beta) * 0.5;
-                        s = __builtin_sqrt(delta / gamma);
-                        c = p / (gamma * s * 2);
-                    } else {
-                        c = __builtin_sqrt((gamma + beta) / (gamma * 2));
-                        s = p / (gamma * c * 2);
-                    }
+                    svd_rotation(p, a, b, c, s);
                     a = b = 0;
                     MCV_SMALL_UNROLL
                     for (int k = 0; k < M; ++k) {
@@ -522,16 +556,8 @@ MCV_HD void j12_pairs(double* lo, double (&hi)[12][6], double (&W)[12], int i, d
         for (int k = 0; k < 12; ++k) p += ri[k] * rj[k];
         if (!(__builtin_fabs(p) <= eps * __builtin_sqrt(a * b))) {
             p *= 2;
-            const double beta = a - b, gamma = cv_hypot(p, beta);
             double c, s;
-            if (beta < 0) {
-                const double delta = (gamma - beta) * 0.5;
-                s = __builtin_sqrt(delta / gamma);
-                c = p / (gamma * s * 2);
-            } else {
-                c = __builtin_sqrt((gamma + beta) / (gamma * 2));
-                s = p / (gamma * c * 2);
-            }
+            svd_rotation(p, a, b, c, s);
             a = b = 0;
             MCV_SMALL_UNROLL
             for (int k = 0; k < 12; ++k) {

@@ -271,28 +271,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int i0 = base + 2 * lane, i1 = i0 + 1;
         uint32_t und = 0;
         asm volatile("" : "+s"(cv.k2tp1), "+s"(cv.tp2p1), "+s"(cv.p2fx), "+s"(cv.fyA4));
+        // every pose's projection, bound and masks first, in one basic block (the K dependent chains
+        // interleave), then the counts and the log
+        uint64_t in0[K], in1[K], out0[K], out1[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             asm volatile("" : "+s"(pp[k].r01), "+s"(pp[k].r23), "+s"(pp[k].r45), "+s"(pp[k].r67), "+s"(pp[k].r8c2));
             const PnpPkProj<pkf2> o = pnp_pk_project<pkf2>(cv, pp[k], X, Y, Z, U, V);
-            uint64_t in0 = 0, in1 = 0, out0 = 0, out1 = 0, u = vm0 | vm1;
-            if (u != 0) {   // wave-uniform: the per-lane bound for this (pose, trip)
-                pkf2 lo, hi;
-                pnp_pk_bound<pkf2>(cv, pp[k], o, lo, hi);
-                const uint64_t d0 = __builtin_amdgcn_ballot_w64(fabsf(o.Zc.x) >= pp[k].zmin);
-                const uint64_t d1 = __builtin_amdgcn_ballot_w64(fabsf(o.Zc.y) >= pp[k].zmin);
-                in0 |= __builtin_amdgcn_ballot_w64(o.S.x < lo.x) & d0;
-                in1 |= __builtin_amdgcn_ballot_w64(o.S.y < lo.y) & d1;
-                out0 |= __builtin_amdgcn_ballot_w64(o.S.x > hi.x) & d0;
-                out1 |= __builtin_amdgcn_ballot_w64(o.S.y > hi.y) & d1;
-                u = (vm0 & ~(in0 | out0)) | (vm1 & ~(in1 | out1));
-            }
-            const uint32_t c = (uint32_t)__popcll(in0 & vm0) + (uint32_t)__popcll(in1 & vm1);
+            pkf2 lo, hi;
+            pnp_pk_bound<pkf2>(cv, pp[k], o, lo, hi);
+            const uint64_t d0 = __builtin_amdgcn_ballot_w64(fabsf(o.Zc.x) >= pp[k].zmin);
+            const uint64_t d1 = __builtin_amdgcn_ballot_w64(fabsf(o.Zc.y) >= pp[k].zmin);
+            in0[k] = __builtin_amdgcn_ballot_w64(o.S.x < lo.x) & d0;
+            in1[k] = __builtin_amdgcn_ballot_w64(o.S.y < lo.y) & d1;
+            out0[k] = __builtin_amdgcn_ballot_w64(o.S.x > hi.x) & d0;
+            out1[k] = __builtin_amdgcn_ballot_w64(o.S.y > hi.y) & d1;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t u = (vm0 & ~(in0[k] | out0[k])) | (vm1 & ~(in1[k] | out1[k]));
+            const uint32_t c = (uint32_t)__popcll(in0[k] & vm0) + (uint32_t)__popcll(in1[k] & vm1);
             if constexpr (LANE) {
                 // the decided lanes count now; the undecided ones go to the log, one entry per lane
                 cnt[k] += c;
                 if (u != 0 && ((validMask >> k) & 1u)) {   // wave-uniform, rare
-                    const uint64_t ud0 = vm0 & ~(in0 | out0), ud1 = vm1 & ~(in1 | out1);
+                    const uint64_t ud0 = vm0 & ~(in0[k] | out0[k]), ud1 = vm1 & ~(in1[k] | out1[k]);
                     const int n0 = __popcll(ud0), n1 = __popcll(ud1);
                     if (nev + n0 + n1 <= kCap) {
                         const uint64_t lt = (1ull << lane) - 1ull;

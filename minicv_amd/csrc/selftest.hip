@@ -62,6 +62,7 @@ __device__ __forceinline__ double random_f64(uint64_t bits, uint64_t ebits, int 
 //   mode 0: |n| in [2^-900, 2^699]      mode 1: n = 1 (the reciprocal)
 //   mode 2: n = d * k, k a small integer (exact quotients)   mode 3: d at the domain ends
 //   mode 4: sqrt_f64_1to2(x) against sqrt(x), x in [1, 2] (the pair records (x, 0))
+//   mode 5: the same for x in [0.5, 1] (the cosines / sines of JacobiSVDImpl_'s rotation)
 __global__ __launch_bounds__(256) void mcv_div_check(uint64_t seed, uint64_t count, int mode,
                                                      unsigned long long* mism, double* first) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
@@ -69,8 +70,10 @@ __global__ __launch_bounds__(256) void mcv_div_check(uint64_t seed, uint64_t cou
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += stride) {
         const uint64_t a = splitmix64(seed ^ (i * 4 + 0)), b = splitmix64(seed ^ (i * 4 + 1));
         const uint64_t c = splitmix64(seed ^ (i * 4 + 2)), g = splitmix64(seed ^ (i * 4 + 3));
-        if (mode == 4) {
-            const double x = (g & 0xFFFF) == 0 ? 2.0 : random_f64(a & 0x000FFFFFFFFFFFFFull, b, 0, 0);
+        if (mode == 4 || mode == 5) {
+            const double x = (g & 0xFFFF) == 0 ? (mode == 4 ? 2.0 : 1.0)
+                                               : random_f64(a & 0x000FFFFFFFFFFFFFull, b, mode == 4 ? 0 : -1,
+                                                            mode == 4 ? 0 : -1);
             const double r = sqrt_f64_1to2(x), ref = __builtin_sqrt(x);
             if (__double_as_longlong(r) != __double_as_longlong(ref)) {
                 ++local;

@@ -177,9 +177,11 @@ def test_unscaled_f64_division_matches_ieee(native, gpu, mode):
     assert n == 0, first[:2 * min(n, 16)].reshape(-1, 2).tolist()
 
 
-def test_unscaled_sqrt_matches_ieee(native, gpu):
-    """sqrt_f64_1to2 (the Jacobi rotation's sqrt of 1 + r^2, r <= 1, without the denormal scaling and
-    class select) equals the IEEE sqrt over 2^26 sampled x in [1, 2] (x = 2 included)."""
+@pytest.mark.parametrize("mode", [4, 5])
+def test_unscaled_sqrt_matches_ieee(native, gpu, mode):
+    """sqrt_f64_1to2 (the Jacobi rotations' sqrt without the denormal scaling and class select) equals
+    the IEEE sqrt over 2^26 sampled x per mode: [1, 2] (the hypots' 1 + r^2, x = 2 included) and
+    [0.5, 1] (JacobiSVDImpl_'s cosine / sine arguments, x = 1 included)."""
     first = np.zeros(32, np.float64)
-    n = native.lib().mcvTestDivF64(4, 0x5EED + 4, 1 << 26, first.ctypes.data)
+    n = native.lib().mcvTestDivF64(mode, 0x5EED + mode, 1 << 26, first.ctypes.data)
     assert n == 0, first[:2 * min(n, 16)].reshape(-1, 2)[:, 0].tolist()
