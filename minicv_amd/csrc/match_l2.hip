@@ -70,6 +70,20 @@ __device__ __forceinline__ bool l2_f16_domain(L2Max dom) { return dom.p && l2_ma
 
 struct L2Part { float b1, b2, b3; int i1, i2, i3; };
 
+// A GEMM segment's partial top-3 for query q into its slot, and empty partials (+inf, index -1: they
+// change no merge) into the nEmpty slots after it that no segment of this (query block, chunk) item
+// writes (mcv_l2_gemm's partition).
+__device__ __forceinline__ void l2_part_store(L2Part* __restrict__ part, int nqPad, int slot, int nEmpty, int q,
+                                              const L2Part& p) {
+    part[(size_t)slot * nqPad + q] = p;
+    for (int e = 1; e <= nEmpty; ++e) {
+        L2Part z;
+        z.b1 = z.b2 = z.b3 = INFINITY;
+        z.i1 = z.i2 = z.i3 = -1;
+        part[(size_t)(slot + e) * nqPad + q] = z;
+    }
+}
+
 __device__ __forceinline__ bool lex_less(float a, int ia, float b, int ib) {
     return (a < b) | ((a == b) & ((unsigned)ia < (unsigned)ib));   // idx -1 sorts last
 }
@@ -276,9 +290,9 @@ __device__ __forceinline__ void l2_lstore_raw(float* __restrict__ lds, float* __
 // copies of mcv_l2_prep. lds: 2 TR (DP + 4) floats, lnorm: 2 TR floats.
 template <int DP, int TR, bool RAW>
 __device__ __forceinline__ void l2_gemm32_body(const float* __restrict__ qsrc, const float* __restrict__ tsrc, int nq,
-                                               int nt, int dim, const float* __restrict__ tnorm, int ntTiles,
-                                               int tilesPerChunk, int nqPad, L2Part* __restrict__ part, int bx,
-                                               int by, float* __restrict__ lds, float* __restrict__ lnorm) {
+                                               int nt, int dim, const float* __restrict__ tnorm, int tBegin,
+                                               int tEnd, int nqPad, L2Part* __restrict__ part, int bx, int slot,
+                                               int nEmpty, float* __restrict__ lds, float* __restrict__ lnorm) {
     constexpr int KS = DP / 2;          // MFMA k-steps (2 dims each)
     constexpr int ROWF = DP + 4;        // padded LDS row, floats
     constexpr int PER = RAW ? TR * DP / 256 : TR * DP / 1024;   // staging registers per thread per tile
@@ -302,8 +316,6 @@ __device__ __forceinline__ void l2_gemm32_body(const float* __restrict__ qsrc, c
         }
     }
 
-    const int tBegin = by * tilesPerChunk;
-    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
     float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
     int i1 = -1, i2 = -1;
 
@@ -387,7 +399,7 @@ __device__ __forceinline__ void l2_gemm32_body(const float* __restrict__ qsrc, c
         top2_push(b1, i1, b2, i2, ob2, oi2);
         L2Part p;
         p.b1 = b1; p.b2 = b2; p.b3 = c3; p.i1 = i1; p.i2 = i2; p.i3 = -1;
-        part[(size_t)by * nqPad + q0 + col] = p;
+        l2_part_store(part, nqPad, slot, nEmpty, q0 + col, p);
     }
 }
 
@@ -398,8 +410,9 @@ __global__ __launch_bounds__(256, 2) void mcv_l2_mfma(const float* __restrict__ 
                                                      int tilesPerChunk, int nqPad, L2Part* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) float lds[2 * TR * (DP + 4)];
     __shared__ __attribute__((aligned(16))) float lnorm[2 * TR];
-    l2_gemm32_body<DP, TR, false>(qp, tp, 0, 0, 0, tnorm, ntTiles, tilesPerChunk, nqPad, part, blockIdx.x, blockIdx.y,
-                                  lds, lnorm);
+    const int tBegin = blockIdx.y * tilesPerChunk;
+    l2_gemm32_body<DP, TR, false>(qp, tp, 0, 0, 0, tnorm, tBegin, min(tBegin + tilesPerChunk, ntTiles), nqPad, part,
+                                  blockIdx.x, blockIdx.y, 0, lds, lnorm);
 }
 
 // ---- f16-split GEMM form ---------------------------------------------------------------------
@@ -629,8 +642,8 @@ __device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const fl
 template <int DP, int WPB, int QT>
 __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, const _Float16* __restrict__ ql,
                                                const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
-                                               const float* __restrict__ tnorm, int ntTiles, int tilesPerChunk,
-                                               int nqPad, L2Part* __restrict__ part, int bx, int by,
+                                               const float* __restrict__ tnorm, int tBegin, int tEnd,
+                                               int nqPad, L2Part* __restrict__ part, int bx, int slot, int nEmpty,
                                                _Float16* __restrict__ lhb, _Float16* __restrict__ llb,
                                                float* __restrict__ lnb) {
     constexpr int TR = 32;
@@ -656,8 +669,6 @@ __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, 
             bl[q][kb] = rl[2 * kb];
         }
     }
-    const int tBegin = by * tilesPerChunk;
-    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
     float b1[QT], b2[QT], b3[QT];
     int i1[QT], i2[QT];
 #pragma unroll
@@ -719,7 +730,7 @@ __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, 
             top2_push(x1, j1, x2, j2, ob2, oi2);
             L2Part p;
             p.b1 = x1; p.b2 = x2; p.b3 = c3; p.i1 = j1; p.i2 = j2; p.i3 = -1;
-            part[(size_t)by * nqPad + q0 + 32 * q + col] = p;
+            l2_part_store(part, nqPad, slot, nEmpty, q0 + 32 * q + col, p);
         }
     }
 }
@@ -731,13 +742,22 @@ __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, 
 // waves per SIMD). XCD-aware (query block, train chunk) order when the chunk count divides 8: blocks
 // are dealt round-robin over the 8 XCDs, so chunk = linear block id mod C puts one chunk's train rows
 // on each XCD's L2.
+// Partition (round 5, stream-K style): the train set is split into C chunks (one per XCD group of
+// blocks) and the grid is C x BX resident blocks; block b serves chunk x = b % C (blocks are dealt
+// round-robin over the 8 XCDs, so with C = 8 each XCD's L2 holds one chunk) and, within it, the
+// contiguous range [j W / BX, (j + 1) W / BX), j = b / C, of the chunk's W = qblocks x tiles
+// (query block, tile) steps, query block by query block. Every block gets the same amount of work
+// (to a tile), so no round of resident blocks is left partly empty — the (query block, chunk) grid
+// this replaces ran 6 rounds for 5.6 rounds of work at cfg5. A (query block, chunk) item split over
+// k blocks writes k partials: slot = x G + (j - the block holding the item's first tile), G = the most
+// blocks an item spans, and the item's last segment writes empty partials into the slots up to G.
 struct L2GemmArgs {
     const _Float16 *qh, *ql, *th, *tl;
     const float *qraw, *traw, *tnorm;
-    int nq, nt, dim, ntTiles, tilesPerChunk, nqPad;
+    int nq, nt, dim, ntTiles, nqPad;
     L2Part* part;
     L2Max dom;
-    bool xcdMap;
+    int qblocks, chunks, tilesPerChunk, bx, segs;   // C, the chunk length, BX, G
 };
 template <int DP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void mcv_l2_gemm(L2GemmArgs a) {
@@ -745,16 +765,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     constexpr int HALVES = 2 * 2 * TR * ROWH, FLOATS = 2 * TR * ROWF;
     constexpr int BYTES = (HALVES * 2 > FLOATS * 4 ? HALVES * 2 : FLOATS * 4) + 2 * TR * 4;
     __shared__ __attribute__((aligned(16))) char smem[BYTES];
-    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
-    const int bx = a.xcdMap ? lin / gridDim.y : blockIdx.x, by = a.xcdMap ? lin % gridDim.y : blockIdx.y;
     float* lnorm = reinterpret_cast<float*>(smem + BYTES - 2 * TR * 4);
-    if (l2_f16_domain(a.dom)) {
+    const bool f16 = l2_f16_domain(a.dom);
+    const int x = (int)blockIdx.x % a.chunks, j = (int)blockIdx.x / a.chunks;
+    const int c0 = x * a.tilesPerChunk;
+    const int len = min(a.tilesPerChunk, a.ntTiles - c0);   // this chunk's tiles
+    if (len <= 0) return;
+    const int64_t W = (int64_t)a.qblocks * len;
+    const int64_t end = (int64_t)(j + 1) * W / a.bx;
+    // the segments of this block's range, each handed to body(q, tBegin, tEnd, slot, nEmpty)
+    auto segments = [&](auto&& body) {
+        for (int64_t pos = (int64_t)j * W / a.bx; pos < end;) {
+            const int q = (int)(pos / len);
+            const int64_t itemStart = (int64_t)q * len, itemEnd = itemStart + len;
+            const int64_t segEnd = end < itemEnd ? end : itemEnd;
+            const int tBegin = c0 + (int)(pos - itemStart), tEnd = tBegin + (int)(segEnd - pos);
+            // the block of this chunk group holding the item's first tile: the largest j0 with j0 W / BX <= itemStart
+            const int j0 = (int)(((itemStart + 1) * a.bx - 1) / W);
+            const int k = j - j0;
+            body(q, tBegin, tEnd, x * a.segs + k, segEnd == itemEnd ? a.segs - 1 - k : 0);
+            pos = segEnd;
+            __syncthreads();   // the next segment's staging reuses the LDS buffers
+        }
+    };
+    if (f16) {
         _Float16* lh = reinterpret_cast<_Float16*>(smem);
-        l2_gemm16_body<DP, 4, 1>(a.qh, a.ql, a.th, a.tl, a.tnorm, a.ntTiles, a.tilesPerChunk, a.nqPad, a.part, bx, by,
-                                 lh, lh + 2 * TR * ROWH, lnorm);
+        segments([&](int q, int tBegin, int tEnd, int slot, int nEmpty) {
+            l2_gemm16_body<DP, 4, 1>(a.qh, a.ql, a.th, a.tl, a.tnorm, tBegin, tEnd, a.nqPad, a.part, q, slot, nEmpty,
+                                     lh, lh + 2 * TR * ROWH, lnorm);
+        });
     } else {
-        l2_gemm32_body<DP, TR, true>(a.qraw, a.traw, a.nq, a.nt, a.dim, a.tnorm, a.ntTiles, a.tilesPerChunk, a.nqPad,
-                                     a.part, bx, by, reinterpret_cast<float*>(smem), lnorm);
+        segments([&](int q, int tBegin, int tEnd, int slot, int nEmpty) {
+            l2_gemm32_body<DP, TR, true>(a.qraw, a.traw, a.nq, a.nt, a.dim, a.tnorm, tBegin, tEnd, a.nqPad, a.part, q,
+                                         slot, nEmpty, reinterpret_cast<float*>(smem), lnorm);
+        });
     }
 }
 
@@ -1401,39 +1445,47 @@ int launch_match_l2(const float* d_q, int nq, const float* d_t, int nt, int dim,
     }
     const int qblocks = nqPad / 128;
     int nchunks = (2048 + qblocks - 1) / qblocks;
-    // f16-capable launch: 3 blocks per CU (the f16 form's budget), so a grid runs in "rounds" of
-    // 3 x CUs blocks and a round that is barely begun costs most of a block's time: the chunk count C
-    // minimises ceil(qblocks C / (3 CUs)) (1 / C + 0.01) (the 0.01: a block's fixed cost against a
-    // whole-train sweep) over C = 4 .. 24. Screened at cfg5's rank shares (scripts/gpu_r04_q.sh,
-    // 50k / N queries): C = 15 took N = 1 / 2 / 4 / 8 to 1.98 / 1.12 / 0.58 / 0.35 ms against
-    // 2.14 / 1.21 / 0.74 / 0.40 with 8 and 2.01 / 1.16 / 0.65 / 0.44 with 16 (N = 8: 800 blocks, one
-    // past a round).
     if (f16) {
+        // mcv_l2_gemm's partition: one train chunk per XCD, 3 resident blocks per CU (the f16 form's
+        // register budget) split evenly over the chunks, each block an equal range of its chunk's
+        // (query block, tile) steps (at least 16 tiles, so small calls keep few partials per query)
         static const int cus = [] {
             int d = 0, n = 0;
             (void)hipGetDevice(&d);
             return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
         }();
-        const int slots = 3 * cus;
-        double best = 1e30;
-        for (int c = 4; c <= 24; ++c) {
-            const double cost = (double)((qblocks * c + slots - 1) / slots) * (1.0 / c + 0.01);
-            if (cost < best - 1e-12) best = cost, nchunks = c;
+        // (round 5, the same box alternating at cfg5: 1.905-1.909 ms per step against 1.996 ms for the
+        // (query block, chunk) grid of 11 chunks chosen by round 4's round-count model)
+        int C = std::min(8, ntTiles);
+        const int tpc = (ntTiles + C - 1) / C;
+        C = (ntTiles + tpc - 1) / tpc;
+        int bx = std::max(1, 3 * cus / C);
+        bx = (int)std::max<int64_t>(1, std::min<int64_t>(bx, (int64_t)qblocks * tpc / 16));
+        int segs = 1;   // the most blocks one (query block, chunk) item spans
+        for (int x = 0; x < C; ++x) {
+            const int len = std::min(tpc, ntTiles - x * tpc);
+            const int64_t W = (int64_t)qblocks * len;
+            for (int q = 0; q < qblocks; ++q) {
+                const int64_t s0 = (int64_t)q * len, s1 = s0 + len - 1;
+                const int64_t j0 = ((s0 + 1) * bx - 1) / W, j1 = ((s1 + 1) * bx - 1) / W;
+                segs = std::max<int>(segs, (int)(j1 - j0 + 1));
+            }
         }
-    }
-    if (nchunks > ntTiles) nchunks = ntTiles;
-    if (nchunks < 1) nchunks = 1;
-    const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
-    nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
-    wk.part.ensure((size_t)nchunks * nqPad);
-    {
+        nchunks = C * segs;
+        wk.part.ensure((size_t)nchunks * nqPad);
         ProfScope ps("l2_mfma", s);
-        if (f16) {
-            const L2GemmArgs ga{wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, d_q, d_t, wk.tn.p, nq, nt, dim, ntTiles,
-                                tilesPerChunk, nqPad, wk.part.p, dom, (8 % nchunks) == 0};
-            hipLaunchKernelGGL((DP == 32 ? mcv_l2_gemm<32> : DP == 64 ? mcv_l2_gemm<64> : mcv_l2_gemm<128>),
-                               dim3(qblocks, nchunks), dim3(256), 0, s, ga);
-        } else {
+        const L2GemmArgs ga{wk.qh.p, wk.ql.p, wk.th.p, wk.tl.p, d_q, d_t, wk.tn.p, nq, nt, dim, ntTiles, nqPad,
+                            wk.part.p, dom, qblocks, C, tpc, bx, segs};
+        hipLaunchKernelGGL((DP == 32 ? mcv_l2_gemm<32> : DP == 64 ? mcv_l2_gemm<64> : mcv_l2_gemm<128>),
+                           dim3(C * bx), dim3(256), 0, s, ga);
+    } else {
+        if (nchunks > ntTiles) nchunks = ntTiles;
+        if (nchunks < 1) nchunks = 1;
+        const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
+        nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
+        wk.part.ensure((size_t)nchunks * nqPad);
+        ProfScope ps("l2_mfma", s);
+        {
             hipLaunchKernelGGL((mcv_l2_mfma<256, TR>), dim3(qblocks, nchunks), dim3(256), 0, s, wk.qp.p, wk.tp.p,
                                wk.tn.p, ntTiles, tilesPerChunk, nqPad, wk.part.p);
         }
