@@ -259,23 +259,29 @@ static constexpr int kHamChunkRows = 4096;   // j' < 4096 < 8192: the key's inde
 
 // Block = WPB waves x QT query tiles of 32 (VGPR-resident B fragments); the block's train tiles (32
 // rows x Kp bytes, expanded from the packed rows) are staged in LDS (double buffer, 16-byte row pad:
-// conflict-free ds_read_b128) and each A fragment read from LDS feeds QT MFMAs. Grid = (query blocks)
-// x (train chunks of <= 4096 rows); the chunk's top-2 per query goes to part[chunk][query], and the
-// block that completes a query block's last chunk (an arrival counter per query block) folds its
-// chunks into the outputs as mcv_hamming_merge does, without a second launch. The XCDs' L2s are not
-// coherent, and an agent-scope fence writes back or invalidates a whole L2 (per block: 30 -> 93 us),
-// so every cross-block value is a device-scope atomic instead: the partials are stored and read with
-// agent-scope atomic stores / loads (sc1: performed at the device-coherent level, never stale in an
-// L2), each block waits for its stores to complete (s_waitcnt vmcnt(0), a compiler barrier too) before
-// its agent-scope arrival add, and the last block's loads are issued after that add returns.
+// conflict-free ds_read_b128) and each A fragment read from LDS feeds QT MFMAs.
+// Partition (round 5, stream-K style): the (query block, train tile) steps in query-block-major order
+// are cut into gridDim.x equal contiguous ranges (at most 128 tiles, the key's 4096-row index field),
+// one per block, so every block does the same work to a tile (the (query block, chunk) grid it
+// replaces left its second round of resident blocks three quarters full at cfg2). A range's part of
+// one query block is a segment; segment k of a query block (k = the block - the block holding the
+// query block's first tile) writes its top-2 per query to part[k][query], and the block that
+// completes a query block's last segment (an arrival counter per query block against its segment
+// count) folds them into the outputs as mcv_hamming_merge does, without a second launch. The XCDs'
+// L2s are not coherent, and an agent-scope fence writes back or invalidates a whole L2 (per block:
+// 30 -> 93 us), so every cross-block value is a device-scope atomic instead: the partials are stored
+// and read with agent-scope atomic stores / loads (sc1: performed at the device-coherent level, never
+// stale in an L2), each block waits for its stores to complete (s_waitcnt vmcnt(0), a compiler barrier
+// too) before its agent-scope arrival add, and the last block's loads are issued after that add returns.
 template <int W, int QT, int WPB, int SUB>
-__global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
+__global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
                                                              const uint32_t* __restrict__ t, int nt, int ntTiles,
-                                                             int tilesPerChunk, uint2* __restrict__ part, bool xcdMap,
+                                                             int qblocks, uint2* __restrict__ part,
                                                              unsigned* __restrict__ arrivals, int* __restrict__ oIdx,
                                                              int* __restrict__ oDist, int* __restrict__ oIdx2,
                                                              int* __restrict__ oDist2) {
     static_assert(QT * 32 * WPB == 64 * WPB, "the fold takes one query per thread");
+    static_assert(SUB == 1, "segments are counted in 32-row tiles");
     constexpr int KS = W;                  // k steps of 32 bytes (Kp = 32 W)
     constexpr int RB = 32 * KS;            // bytes per expanded row
     constexpr int RBP = RB + 16;           // LDS row stride
@@ -283,78 +289,82 @@ __global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const uint32_t* __r
     constexpr int TRW = 32 * SUB;          // train rows per staged tile (SUB MFMA row tiles)
     constexpr int PER = (TRW * W + NT - 1) / NT;   // packed words of a tile per thread
     __shared__ __attribute__((aligned(16))) int8_t lt[2][TRW * RBP];
-    const unsigned lin = blockIdx.x + blockIdx.y * gridDim.x;
-    const unsigned bx = xcdMap ? lin / gridDim.y : blockIdx.x, by = xcdMap ? lin % gridDim.y : blockIdx.y;
+    __shared__ int lastBlock;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
-    const int q0 = (bx * WPB + wave) * QT * 32;
-    i32x4 bq[QT][KS];
+    const int B = (int)gridDim.x, blk = (int)blockIdx.x;
+    const int64_t Wt = (int64_t)qblocks * ntTiles;
+    const int64_t end = (int64_t)(blk + 1) * Wt / B;
+    for (int64_t pos = (int64_t)blk * Wt / B; pos < end;) {
+        const int bx = (int)(pos / ntTiles);
+        const int64_t itemStart = (int64_t)bx * ntTiles, itemEnd = itemStart + ntTiles;
+        const int64_t segEnd = end < itemEnd ? end : itemEnd;
+        const int tBegin = (int)(pos - itemStart), tEnd = tBegin + (int)(segEnd - pos);
+        // the blocks holding the query block's first and last tiles (the largest j with j Wt / B <= tile)
+        const int j0 = (int)(((itemStart + 1) * B - 1) / Wt), j1 = (int)((itemEnd * B - 1) / Wt);
+        const int slot = blk - j0, nseg = j1 - j0 + 1;
+        const int q0 = (bx * WPB + wave) * QT * 32;
+        i32x4 bq[QT][KS];
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        const int qi = min(q0 + 32 * qt + col, nq - 1);
-        const uint32_t* qr = q + (size_t)qi * W + (KS / 2) * h;
+        for (int qt = 0; qt < QT; ++qt) {
+            const int qi = min(q0 + 32 * qt + col, nq - 1);
+            const uint32_t* qr = q + (size_t)qi * W + (KS / 2) * h;
 #pragma unroll
-        for (int s2 = 0; s2 < KS / 2; ++s2) {
-            const uint32_t wd = ~qr[s2];
-            bq[qt][2 * s2] = i32x4{ham_expand_dword<true>(wd, 0), ham_expand_dword<true>(wd, 1),
-                                   ham_expand_dword<true>(wd, 2), ham_expand_dword<true>(wd, 3)};
-            bq[qt][2 * s2 + 1] = i32x4{ham_expand_dword<true>(wd, 4), ham_expand_dword<true>(wd, 5),
-                                       ham_expand_dword<true>(wd, 6), ham_expand_dword<true>(wd, 7)};
-        }
-    }
-    const int tBegin = by * tilesPerChunk;
-    const int tEnd = min(tBegin + tilesPerChunk, ntTiles);
-    uint32_t m1[QT], m2[QT], n1[QT], n2[QT];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = n1[qt] = n2[qt] = 0xFFFFFFFFu;
-    auto gload = [&](int tl, uint32_t (&st)[PER]) {
-#pragma unroll
-        for (int p = 0; p < PER; ++p) {
-            const int id = threadIdx.x + NT * p;
-            if (id < TRW * W) {
-                const int row = min(tl * TRW + id / W, nt - 1);
-                st[p] = t[(size_t)row * W + id % W];
+            for (int s2 = 0; s2 < KS / 2; ++s2) {
+                const uint32_t wd = ~qr[s2];
+                bq[qt][2 * s2] = i32x4{ham_expand_dword<true>(wd, 0), ham_expand_dword<true>(wd, 1),
+                                       ham_expand_dword<true>(wd, 2), ham_expand_dword<true>(wd, 3)};
+                bq[qt][2 * s2 + 1] = i32x4{ham_expand_dword<true>(wd, 4), ham_expand_dword<true>(wd, 5),
+                                           ham_expand_dword<true>(wd, 6), ham_expand_dword<true>(wd, 7)};
             }
         }
-    };
-    auto lstore = [&](int buf, const uint32_t (&st)[PER]) {
+        uint32_t m1[QT], m2[QT], n1[QT], n2[QT];
 #pragma unroll
-        for (int p = 0; p < PER; ++p) {
-            const int id = threadIdx.x + NT * p;
-            if (id < TRW * W) {
-                const uint32_t v = st[p];
-                int8_t* dst = &lt[buf][(id / W) * RBP + 32 * (id % W)];
-                *reinterpret_cast<i32x4*>(dst) = i32x4{ham_expand_dword<false>(v, 0), ham_expand_dword<false>(v, 1),
-                                                      ham_expand_dword<false>(v, 2), ham_expand_dword<false>(v, 3)};
-                *reinterpret_cast<i32x4*>(dst + 16) = i32x4{ham_expand_dword<false>(v, 4), ham_expand_dword<false>(v, 5),
-                                                           ham_expand_dword<false>(v, 6), ham_expand_dword<false>(v, 7)};
+        for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = n1[qt] = n2[qt] = 0xFFFFFFFFu;
+        auto gload = [&](int tl, uint32_t (&st)[PER]) {
+#pragma unroll
+            for (int p = 0; p < PER; ++p) {
+                const int id = threadIdx.x + NT * p;
+                if (id < TRW * W) {
+                    const int row = min(tl * TRW + id / W, nt - 1);
+                    st[p] = t[(size_t)row * W + id % W];
+                }
             }
-        }
-    };
-    // accumulator start values: 4096 Kp + j' (rows past nt: 2^30, which ends above every real key)
-    i32x16 c0;
+        };
+        auto lstore = [&](int buf, const uint32_t (&st)[PER]) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) c0[i] = 4096 * RB + (i & 3) + 8 * (i >> 2) + 4 * h;
-    uint32_t st[PER];
-    if (tBegin < tEnd) {
+            for (int p = 0; p < PER; ++p) {
+                const int id = threadIdx.x + NT * p;
+                if (id < TRW * W) {
+                    const uint32_t v = st[p];
+                    int8_t* dst = &lt[buf][(id / W) * RBP + 32 * (id % W)];
+                    *reinterpret_cast<i32x4*>(dst) = i32x4{ham_expand_dword<false>(v, 0), ham_expand_dword<false>(v, 1),
+                                                          ham_expand_dword<false>(v, 2), ham_expand_dword<false>(v, 3)};
+                    *reinterpret_cast<i32x4*>(dst + 16) = i32x4{ham_expand_dword<false>(v, 4), ham_expand_dword<false>(v, 5),
+                                                               ham_expand_dword<false>(v, 6), ham_expand_dword<false>(v, 7)};
+                }
+            }
+        };
+        // accumulator start values: 4096 Kp + j' (rows past nt: 2^30, which ends above every real key)
+        i32x16 c0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c0[i] = 4096 * RB + (i & 3) + 8 * (i >> 2) + 4 * h;
+        uint32_t st[PER];
         gload(tBegin, st);
         lstore(0, st);
         gload(min(tBegin + 1, tEnd - 1), st);
-    }
-    __syncthreads();
-    for (int tl = tBegin; tl < tEnd; ++tl) {
-        const int buf = (tl - tBegin) & 1;
-#pragma unroll
-        for (int sb = 0; sb < SUB; ++sb) {
+        __syncthreads();
+        for (int tl = tBegin; tl < tEnd; ++tl) {
+            const int buf = (tl - tBegin) & 1;
             i32x16 cs = c0;
-            if (__builtin_expect(tl * TRW + 32 * (sb + 1) > nt, 0)) {   // rows past nt (block-uniform)
+            if (__builtin_expect(tl * TRW + 32 > nt, 0)) {   // rows past nt (block-uniform)
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
-                    if (tl * TRW + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * h >= nt) cs[i] = 1 << 30;
+                    if (tl * TRW + (i & 3) + 8 * (i >> 2) + 4 * h >= nt) cs[i] = 1 << 30;
                 asm volatile("" : "+v"(cs));   // a branch once per launch, not 32 selects per tile
             }
             i32x16 acc[QT];
-            const int8_t* ar = &lt[buf][(32 * sb + col) * RBP + 16 * KS * h];
+            const int8_t* ar = &lt[buf][col * RBP + 16 * KS * h];
             {
                 const i32x4 a = *reinterpret_cast<const i32x4*>(ar);
 #pragma unroll
@@ -366,10 +376,8 @@ __global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const uint32_t* __r
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][s], acc[qt], 0, 0, 0);
             }
-            if (sb == SUB - 1) {
-                lstore(buf ^ 1, st);
-                gload(min(tl + 2, tEnd - 1), st);
-            }
+            lstore(buf ^ 1, st);
+            gload(min(tl + 2, tEnd - 1), st);
             // two independent top-2 chains per query tile (rows i < 8 and i >= 8), merged at the end:
             // the med3 / min updates of one chain depend on each other, two chains overlap
 #pragma unroll
@@ -381,55 +389,56 @@ __global__ __launch_bounds__(64 * WPB) void mcv_hamming_mfma(const uint32_t* __r
                 }
 #pragma unroll
             for (int i = 0; i < 16; ++i) c0[i] += 32;
+            __syncthreads();
         }
-        __syncthreads();
-    }
-    // lanes l and l + 32 hold the same query (other rows): merge, then the popcount form's keys
-    const uint32_t base = (uint32_t)tBegin * TRW;
+        // lanes l and l + 32 hold the same query (other rows): merge, then the popcount form's keys
+        const uint32_t base = (uint32_t)tBegin * TRW;
 #pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        top2_push(m1[qt], m2[qt], n1[qt]);   // chunk-local keys: the index field keeps them distinct
-        top2_push(m1[qt], m2[qt], n2[qt]);
-        const uint32_t o1 = __shfl_xor(m1[qt], 32, 64), o2 = __shfl_xor(m2[qt], 32, 64);
-        top2_push(m1[qt], m2[qt], o1);
-        top2_push(m1[qt], m2[qt], o2);
-        auto glob = [&](uint32_t k) {
-            // a masked row ends at 2^30 - 4096 (Kp - 2 ham) >= 2^30 - 2^22; a real key is below 2^23
-            return k >= (1u << 29) ? 0xFFFFFFFFu : ((k >> 13) << kIdxBits) | (base + (k & (kHamChunkRows - 1)));
-        };
-        const int qi = q0 + 32 * qt + col;
-        if (h == 0 && qi < nq) {
-            const uint64_t v = (uint64_t)glob(m1[qt]) | ((uint64_t)glob(m2[qt]) << 32);
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(part) + (size_t)by * nq + qi, v, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        for (int qt = 0; qt < QT; ++qt) {
+            top2_push(m1[qt], m2[qt], n1[qt]);   // segment-local keys: the index field keeps them distinct
+            top2_push(m1[qt], m2[qt], n2[qt]);
+            const uint32_t o1 = __shfl_xor(m1[qt], 32, 64), o2 = __shfl_xor(m2[qt], 32, 64);
+            top2_push(m1[qt], m2[qt], o1);
+            top2_push(m1[qt], m2[qt], o2);
+            auto glob = [&](uint32_t k) {
+                // a masked row ends at 2^30 - 4096 (Kp - 2 ham) >= 2^30 - 2^22; a real key is below 2^23
+                return k >= (1u << 29) ? 0xFFFFFFFFu : ((k >> 13) << kIdxBits) | (base + (k & (kHamChunkRows - 1)));
+            };
+            const int qi = q0 + 32 * qt + col;
+            if (h == 0 && qi < nq) {
+                const uint64_t v = (uint64_t)glob(m1[qt]) | ((uint64_t)glob(m2[qt]) << 32);
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(part) + (size_t)slot * nq + qi, v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
-    }
-    __shared__ int lastBlock;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        lastBlock = __hip_atomic_fetch_add(arrivals + bx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                    gridDim.y - 1u;
-    __syncthreads();
-    if (!lastBlock) return;
-    const int qm = bx * (QT * 32 * WPB) + threadIdx.x;
-    if (qm < nq) {
-        uint32_t a1 = 0xFFFFFFFFu, a2 = 0xFFFFFFFFu;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            lastBlock = __hip_atomic_fetch_add(arrivals + bx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        (unsigned)(nseg - 1);
+        __syncthreads();
+        if (lastBlock) {
+            const int qm = bx * (QT * 32 * WPB) + threadIdx.x;
+            if (qm < nq) {
+                uint32_t a1 = 0xFFFFFFFFu, a2 = 0xFFFFFFFFu;
 #pragma unroll 8
-        for (int c = 0; c < (int)gridDim.y; ++c) {
-            const uint64_t pv = __hip_atomic_load(reinterpret_cast<const uint64_t*>(part) + (size_t)c * nq + qm,
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint2 pc = make_uint2((uint32_t)pv, (uint32_t)(pv >> 32));
-            a2 = min(a2, max(a1, pc.x));
-            a1 = min(a1, pc.x);
-            a2 = min(a2, pc.y);
+                for (int c = 0; c < nseg; ++c) {
+                    const uint64_t pv = __hip_atomic_load(reinterpret_cast<const uint64_t*>(part) + (size_t)c * nq + qm,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint2 pc = make_uint2((uint32_t)pv, (uint32_t)(pv >> 32));
+                    a2 = min(a2, max(a1, pc.x));
+                    a1 = min(a1, pc.x);
+                    a2 = min(a2, pc.y);
+                }
+                oIdx[qm] = a1 == 0xFFFFFFFFu ? -1 : (int)(a1 & kIdxMask);
+                oDist[qm] = a1 == 0xFFFFFFFFu ? INT_MAX : (int)(a1 >> kIdxBits);
+                if (oIdx2) oIdx2[qm] = a2 == 0xFFFFFFFFu ? -1 : (int)(a2 & kIdxMask);
+                if (oDist2) oDist2[qm] = a2 == 0xFFFFFFFFu ? INT_MAX : (int)(a2 >> kIdxBits);
+            }
+            if (threadIdx.x == 0) arrivals[bx] = 0u;   // re-armed for the next launch (ordered by the kernel boundary)
         }
-        oIdx[qm] = a1 == 0xFFFFFFFFu ? -1 : (int)(a1 & kIdxMask);
-        oDist[qm] = a1 == 0xFFFFFFFFu ? INT_MAX : (int)(a1 >> kIdxBits);
-        if (oIdx2) oIdx2[qm] = a2 == 0xFFFFFFFFu ? -1 : (int)(a2 & kIdxMask);
-        if (oDist2) oDist2[qm] = a2 == 0xFFFFFFFFu ? INT_MAX : (int)(a2 >> kIdxBits);
+        pos = segEnd;
     }
-    if (threadIdx.x == 0) arrivals[bx] = 0u;   // re-armed for the next launch (ordered by the kernel boundary)
 }
 
 // Re-pack [n][bytes] rows into zero-padded [n][W] 32-bit words (XOR of the zero pads is 0).
@@ -483,19 +492,33 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     }
     // form 1: the XOR / popcount sweep (mcvMatchHammingDeviceForm); 0: the int8 GEMM (default)
     if (form == kHammingFormGemm && nt > 0) {
-        // 4 waves per block, 2 query tiles per wave, one 32-row MFMA tile per staged train tile, ~8192
-        // waves in the grid (cfg2 screens: 1 query tile, 2-tile staging 33.6 vs 32.1 us; 2048 / 4096 /
-        // 8192 / 16384 waves 43.2 / 33.3 / 32.1 / 34.8 us)
-        constexpr int WPB = 4, QT = 2, SUB = 1, target = 8192;
+        // 4 waves per block, 2 query tiles per wave, one 32-row MFMA tile per staged train tile (cfg2
+        // screens, round 4: 1 query tile, 2-tile staging 33.6 vs 32.1 us), one block per resident slot
+        // (3 per CU at 256-bit descriptors, 2 at 512-bit: the register budget). Round 5, the same box
+        // alternating at cfg2: the stream-K ranges 32.4 us per step against 35.0 us for round 4's
+        // (query block, chunk) grid of ~8192 waves; two blocks per slot 39.2 us.
+        constexpr int WPB = 4, QT = 2, SUB = 1;
         const int qblocks = (nq + 32 * QT * WPB - 1) / (32 * QT * WPB);
         const int ntTiles = (nt + 32 * SUB - 1) / (32 * SUB);
-        int nchunks = std::max(1, std::min(ntTiles, (target / WPB + qblocks - 1) / qblocks));
-        if (nchunks > 8) nchunks = nchunks / 8 * 8;   // whole XCD rounds
-        nchunks = std::max(nchunks, (ntTiles * 32 * SUB + kHamChunkRows - 1) / kHamChunkRows);   // key index field
-        const int tilesPerChunk = (ntTiles + nchunks - 1) / nchunks;
-        nchunks = (ntTiles + tilesPerChunk - 1) / tilesPerChunk;
-        const bool xcdMap = (8 % nchunks) == 0 || nchunks % 8 == 0;
-        wk.part.ensure((size_t)nchunks * nq);
+        static const int cus = [] {
+            int d = 0, n = 0;
+            (void)hipGetDevice(&d);
+            return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
+        }();
+        const int perCu = W == 8 ? 3 : 2;   // the kernel's __launch_bounds__
+        const int64_t Wt = (int64_t)qblocks * ntTiles;
+        // equal ranges of the (query block, tile) steps over the resident blocks, at most 128 tiles each
+        // (the key's index field) and at least 4 (the per-range query expansion and fold)
+        int64_t B = std::min<int64_t>((int64_t)perCu * cus, (Wt + 3) / 4);
+        B = std::max<int64_t>(B, (Wt + kHamChunkRows / 32 - 1) / (kHamChunkRows / 32));
+        B = std::max<int64_t>(1, std::min(B, Wt));
+        if (B > INT_MAX) fail("cvMatchHamming: %lld ranges", (long long)B);
+        int maxSeg = 1;
+        for (int64_t x = 0; x < qblocks; ++x) {
+            const int64_t j0 = ((x * ntTiles + 1) * B - 1) / Wt, j1 = ((x + 1) * ntTiles * B - 1) / Wt;
+            maxSeg = std::max(maxSeg, (int)(j1 - j0 + 1));
+        }
+        wk.part.ensure((size_t)maxSeg * nq);
         if (wk.arrivalsZeroed < (size_t)qblocks) {
             wk.arrivals.ensure((size_t)qblocks);
             MCV_HIP(hipMemsetAsync(wk.arrivals.p, 0, wk.arrivals.n * sizeof(unsigned), s));
@@ -504,8 +527,8 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         {
             ProfScope ps("hamming", s);
             hipLaunchKernelGGL((W == 8 ? mcv_hamming_mfma<8, QT, WPB, SUB> : mcv_hamming_mfma<16, QT, WPB, SUB>),
-                               dim3(qblocks, nchunks), dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, tilesPerChunk,
-                               wk.part.p, xcdMap, wk.arrivals.p, d_idx, d_dist, d_idx2, d_dist2);
+                               dim3((unsigned)B), dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, qblocks, wk.part.p,
+                               wk.arrivals.p, d_idx, d_dist, d_idx2, d_dist2);
         }
         MCV_HIP(hipGetLastError());
         wk.fence.leave(s);

@@ -45,14 +45,18 @@ def l2_shares():
         idx2 = torch.empty_like(idx)
         d1 = torch.empty(cnt, dtype=torch.float32, device=dev)
         d2 = torch.empty_like(d1)
+        # as bench.py's step loop: calls back to back on the stream, one synchronize per timed run (a
+        # synchronize per call would add the host round trip to a 0.3 ms share)
+        for _ in range(3):
+            D.match_l2(qs, td, idx, d1, idx2, d2)
         ts = []
-        for k in range(13):
+        for k in range(5):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            D.match_l2(qs, td, idx, d1, idx2, d2)
+            for _ in range(10):
+                D.match_l2(qs, td, idx, d1, idx2, d2)
             torch.cuda.synchronize()
-            if k >= 3:
-                ts.append(time.perf_counter() - t0)
+            ts.append((time.perf_counter() - t0) / 10)
         res[n] = float(np.median(ts)) * 1e3
     return res
 

@@ -293,3 +293,26 @@ def test_hamming_extreme_distances(gpu, oracle, hamming_form, nbytes):
     check_hamming_form(oracle, hamming_form, q, t)
     idx, dist, idx2, dist2 = check_hamming_form(oracle, hamming_form, q[:40], t2)
     assert (dist == 8 * nbytes).all() and (idx == 0).all() and (idx2 == 1).all()
+
+
+def test_hamming_gemm_long_ranges(gpu, oracle):
+    """A call large enough that the GEMM form's stream-K ranges reach their 128-tile cap (the key's
+    4096-row index field) and the grid exceeds the resident slots: 8000 x 120000 (32 query blocks x
+    3750 tiles -> 938 ranges of <= 128 tiles). Every query against the popcount form (an independent
+    kernel) and a sample of 400 queries against the oracle."""
+    import torch
+    from minicv_amd import device as D
+    q, t, _ = S.hamming_problem(8000, 120_000, seed=11)
+    dev = torch.device("cuda:0")
+    tq, tt = torch.from_numpy(q).to(dev), torch.from_numpy(t).to(dev)
+    outs = {}
+    for form in ("gemm", "popcount"):
+        o = [torch.empty(q.shape[0], dtype=torch.int32, device=dev) for _ in range(4)]
+        D.match_hamming(tq, tt, *o, form=form)
+        torch.cuda.synchronize()
+        outs[form] = [x.cpu().numpy() for x in o]
+    for g, p in zip(outs["gemm"], outs["popcount"]):
+        np.testing.assert_array_equal(g, p)
+    sel = np.random.default_rng(0).choice(q.shape[0], 400, replace=False)
+    for g, r in zip(outs["gemm"], oracle.match_hamming(q[sel], t)):
+        np.testing.assert_array_equal(g[sel], r)
