@@ -562,40 +562,6 @@ __global__ __launch_bounds__(256) void mcv_l2_prep16(L2PrepF16 q, L2PrepF16 t, i
     }
 }
 
-template <int DP, int TR, int NT>
-__device__ __forceinline__ void l2_gload16(const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
-                                           const float* __restrict__ tnorm, int tile,
-                                           f16x8 (&sh)[(TR * DP / 8 + NT - 1) / NT], f16x8 (&sl)[(TR * DP / 8 + NT - 1) / NT],
-                                           float& nstg) {
-    constexpr int CH = TR * DP / 8, PER = (CH + NT - 1) / NT;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int c = threadIdx.x + NT * j;
-        if (CH % NT == 0 || c < CH) {
-            sh[j] = reinterpret_cast<const f16x8*>(th + (size_t)tile * TR * DP)[c];
-            sl[j] = reinterpret_cast<const f16x8*>(tl + (size_t)tile * TR * DP)[c];
-        }
-    }
-    if (threadIdx.x < TR) nstg = tnorm[tile * TR + threadIdx.x];
-}
-
-template <int DP, int TR, int NT>
-__device__ __forceinline__ void l2_lstore16(_Float16* __restrict__ lh, _Float16* __restrict__ ll, float* __restrict__ lnorm,
-                                            const f16x8 (&sh)[(TR * DP / 8 + NT - 1) / NT],
-                                            const f16x8 (&sl)[(TR * DP / 8 + NT - 1) / NT], float nstg) {
-    constexpr int CH = TR * DP / 8, PER = (CH + NT - 1) / NT, ROWH = DP + 8;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int c = threadIdx.x + NT * j;
-        if (CH % NT == 0 || c < CH) {
-            const int row = c / (DP / 8), c8 = c % (DP / 8);
-            *reinterpret_cast<f16x8*>(&lh[row * ROWH + 8 * c8]) = sh[j];
-            *reinterpret_cast<f16x8*>(&ll[row * ROWH + 8 * c8]) = sl[j];
-        }
-    }
-    if (threadIdx.x < TR) lnorm[threadIdx.x] = nstg;
-}
-
 // A tile's scores (s = |t|^2 - 2 q.t from the two accumulator chains) -> the lane's running top-2 /
 // third place (train rows in ascending index order across calls with increasing ranges). One
 // wave-level test first: the tile's 16 scores per lane reduced by a min (v_min3), and the insertions
@@ -633,30 +599,66 @@ __device__ __forceinline__ void l2_epilogue16(const floatx16 (&am)[NC], const fl
 // 16-dim k block: A = the tile's hi / lo rows from LDS (one ds_read_b128 each: lane l holds row l & 31,
 // dims 16 kb + 8 (l >> 5) + j), B = the wave's queries hi / lo (VGPR-resident, the same dims), three
 // accumulator chains (hi.hi, then hi.lo and lo.hi into one) on v_mfma_f32_32x32x16_f16. One
-// accumulator set per query set, the next tile staged one tile ahead through one register set: 150
-// VGPRs for QT = 1, so three waves per SIMD (WAVES, amdgpu_waves_per_eu) overlap one wave's epilogue
-// with the others' MFMAs. WPB = 4, QT = 1: blocks of 128 queries, 3 blocks per CU. Screened in round
+// accumulator set per query set. WPB = 4, QT = 1: blocks of 128 queries, 3 blocks per CU (three waves
+// per SIMD, amdgpu_waves_per_eu, overlap one wave's epilogue with the others' MFMAs). Screened in round
 // 4 (cfg5): the round-3 form with two accumulator sets in turn 2.07 ms; QT = 2 at two waves per SIMD
 // (252 VGPRs) 2.17 ms, at one wave per SIMD 2.98 ms; s_setprio 1 around the MFMA cluster 1.95 ms;
-// 8-wave blocks 2.36 ms; four waves per SIMD (23 spilled VGPRs) 2.55 ms; this form 1.88 ms.
+// 8-wave blocks 2.36 ms; four waves per SIMD (23 spilled VGPRs) 2.55 ms; the round-4 form 1.88 ms.
+// Staging (round 5): the next tile arrives by LDS-DMA (global_load_lds_dwordx4: no staging registers,
+// no ds_write pass), issued at the top of the current tile and retired by the tile's closing barrier.
+// The DMA writes each wave-instruction's 64 x 16 B contiguously, so the tile image is unpadded
+// [32 rows][DP halves] with its 16-byte chunks XOR-swizzled per row (chunk c of row r at c ^ key(r),
+// key(r) = (r / (256 B / row bytes)) mod chunks per row; the swizzle goes on the DMA's per-lane source
+// address): the fragment reads of 16 consecutive rows then hit 16 distinct 4-bank groups, as the
+// padded rows of the register-staged form did.
+template <int DP>
+__device__ __forceinline__ int l2_swz_key(int r) {
+    constexpr int RB = DP * 2, CPR = DP / 8;   // row bytes, 16-byte chunks per row
+    return (r / (256 / RB)) & (CPR - 1);
+}
+
+template <int DP, int TR, int WPB>
+__device__ __forceinline__ void l2_glds16(const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
+                                          const float* __restrict__ tnorm, int tile, _Float16* lh, _Float16* ll,
+                                          float* ln) {
+    typedef __attribute__((address_space(3))) void* lptr;
+    typedef __attribute__((address_space(1))) void* gptr;
+    constexpr int RB = DP * 2, PIECES = TR * RB / 1024;   // 1 KiB wave-instructions per image
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int arr = 0; arr < 2; ++arr) {
+#pragma unroll
+        for (int i = 0; i < (PIECES + WPB - 1) / WPB; ++i) {
+            const int piece = wave + WPB * i;
+            if (PIECES % WPB == 0 || piece < PIECES) {
+                const int o = piece * 1024 + 16 * lane;   // byte offset in the image
+                const int r = o / RB, c = ((o % RB) >> 4) ^ l2_swz_key<DP>(r);
+                const _Float16* src = (arr ? tl : th) + ((size_t)tile * TR + r) * DP + 8 * c;
+                __builtin_amdgcn_global_load_lds((gptr)src, (lptr)((arr ? ll : lh) + piece * 512), 16, 0, 0);
+            }
+        }
+    }
+    if (wave == WPB - 1 && lane < TR)
+        __builtin_amdgcn_global_load_lds((gptr)(tnorm + (size_t)tile * TR + lane), (lptr)ln, 4, 0, 0);
+}
+
 template <int DP, int WPB, int QT>
 __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, const _Float16* __restrict__ ql,
                                                const _Float16* __restrict__ th, const _Float16* __restrict__ tl,
                                                const float* __restrict__ tnorm, int tBegin, int tEnd,
                                                int nqPad, L2Part* __restrict__ part, int bx, int slot, int nEmpty,
-                                               _Float16* __restrict__ lhb, _Float16* __restrict__ llb,
-                                               float* __restrict__ lnb) {
+                                               _Float16* __restrict__ img, float* __restrict__ lnb) {
     constexpr int TR = 32;
     constexpr int KB = DP / 16;
-    constexpr int ROWH = DP + 8;
-    constexpr int NT = 64 * WPB;
-    constexpr int PER = (TR * DP / 8 + NT - 1) / NT;
-    // LDS double buffers: lh / ll [2][TR * ROWH] halves, lnorm [2][TR]
-    auto lh = [&](int buf) { return lhb + buf * TR * ROWH; };
-    auto ll = [&](int buf) { return llb + buf * TR * ROWH; };
+    constexpr int RB = DP * 2;
+    // LDS: two buffers of [hi image | lo image] (TR x DP halves each), norms [2][TR]
+    auto lh = [&](int buf) { return img + buf * 2 * TR * DP; };
+    auto ll = [&](int buf) { return img + buf * 2 * TR * DP + TR * DP; };
     auto lnorm = [&](int buf) { return lnb + buf * TR; };
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
+    const int key = l2_swz_key<DP>(col);
     const int q0 = (bx * WPB + wave) * 32 * QT;
     f16x8 bh[QT][KB], bl[QT][KB];
 #pragma unroll
@@ -673,26 +675,25 @@ __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, 
     int i1[QT], i2[QT];
 #pragma unroll
     for (int q = 0; q < QT; ++q) b1[q] = b2[q] = b3[q] = INFINITY, i1[q] = i2[q] = -1;
-    f16x8 sh[PER], sl[PER];
-    float ns = 0.f;
-    if (tBegin < tEnd) {
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, tBegin, sh, sl, ns);
-        l2_lstore16<DP, TR, NT>(lh(0), ll(0), lnorm(0), sh, sl, ns);
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(tBegin + 1, tEnd - 1), sh, sl, ns);
-    }
+    if (tBegin < tEnd) l2_glds16<DP, TR, WPB>(th, tl, tnorm, tBegin, lh(0), ll(0), lnorm(0));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the first tile and the query fragments
     __syncthreads();
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // the query fragments' loads, once (vmcnt(0))
     for (int t = tBegin; t < tEnd; ++t) {
         const int buf = (t - tBegin) & 1;
+        // the next tile into the idle buffer (its last readers passed the previous tile's barrier)
+        if (t + 1 < tEnd) l2_glds16<DP, TR, WPB>(th, tl, tnorm, t + 1, lh(buf ^ 1), ll(buf ^ 1), lnorm(buf ^ 1));
         floatx16 m[QT], sm[QT];
 #pragma unroll
         for (int q = 0; q < QT; ++q)
 #pragma unroll
             for (int r = 0; r < 16; ++r) m[q][r] = sm[q][r] = 0.f;
+        const char* rowh = reinterpret_cast<const char*>(lh(buf)) + col * RB;
+        const char* rowl = reinterpret_cast<const char*>(ll(buf)) + col * RB;
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(lh(buf) + col * ROWH + 16 * kb + 8 * h);
-            const f16x8 al = *reinterpret_cast<const f16x8*>(ll(buf) + col * ROWH + 16 * kb + 8 * h);
+            const int p = ((2 * kb + h) ^ key) << 4;
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(rowh + p);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(rowl + p);
 #pragma unroll
             for (int q = 0; q < QT; ++q) m[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[q][kb], m[q], 0, 0, 0);
 #pragma unroll
@@ -700,9 +701,6 @@ __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, 
 #pragma unroll
             for (int q = 0; q < QT; ++q) sm[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[q][kb], sm[q], 0, 0, 0);
         }
-        // the next tile (staged a tile ago) into the idle LDS buffer, the one after into the staging set
-        l2_lstore16<DP, TR, NT>(lh(buf ^ 1), ll(buf ^ 1), lnorm(buf ^ 1), sh, sl, ns);
-        l2_gload16<DP, TR, NT>(th, tl, tnorm, min(t + 2, tEnd - 1), sh, sl, ns);
         float4 nv[1][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) nv[0][j] = *reinterpret_cast<const float4*>(lnorm(buf) + 8 * j + 4 * h);
@@ -711,6 +709,7 @@ __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, 
             const floatx16 am[1] = {m[q]}, as[1] = {sm[q]};
             l2_epilogue16<1>(am, as, nv, t * TR, b1[q], i1[q], b2[q], i2[q], b3[q]);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of the next tile landed
         __syncthreads();
     }
 #pragma unroll
@@ -792,7 +791,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         _Float16* lh = reinterpret_cast<_Float16*>(smem);
         segments([&](int q, int tBegin, int tEnd, int slot, int nEmpty) {
             l2_gemm16_body<DP, 4, 1>(a.qh, a.ql, a.th, a.tl, a.tnorm, tBegin, tEnd, a.nqPad, a.part, q, slot, nEmpty,
-                                     lh, lh + 2 * TR * ROWH, lnorm);
+                                     lh, lnorm);
         });
     } else {
         segments([&](int q, int tBegin, int tEnd, int slot, int nEmpty) {
