@@ -398,8 +398,10 @@ void launch_f_verify(const float* d_pts4, int N, const void* d_models, int* d_co
     const float4* p = (const float4*)d_pts4;
     const FModelD* m = (const FModelD*)d_models;
     const SampsonCut c = sampson_cut(thr2);
-    if (d_bb && kind <= 1) {   // Sampson: certified packed-fp32 prefilter, 4 model pairs per wave
-        launch_f_verify_pk_kp<4, 1>(p, N, m, d_counts, hypCount, thr2, kind, sampson_pk_cut_host(c), d_bb, s);
+    if (d_bb && kind <= 1) {   // Sampson: certified packed-fp32 prefilter, 3 model pairs per wave (four waves
+        // per SIMD at 121 VGPRs; round 5, same box: 218.2 ms per launch against 225.5 for 4 pairs at three
+        // waves per SIMD, 219.0-219.7 for 3 pairs x 2 points a trip, 233.5 for 2 pairs x 2 points)
+        launch_f_verify_pk_kp<3, 1>(p, N, m, d_counts, hypCount, thr2, kind, sampson_pk_cut_host(c), d_bb, s);
         return;
     }
     launch_f_verify_kp<kVerifyFHypPerWave, kVerifyFPtsPerLane>(p, N, m, d_counts, hypCount, thr2, kind, c.lo, c.hi, s);
