@@ -164,7 +164,10 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
     const int wave = __builtin_amdgcn_readfirstlane((int)((bx * 256u + threadIdx.x) >> 6));
     const int lane = threadIdx.x & 63;
     const int h0 = wave * K;
-    if (h0 >= hypCount) return;
+    // the block's 4 K counts leave through LDS in one contiguous store (a wave's own K counts were a
+    // partial-sector write each: 8.2 MiB written per launch at K = 6, 4 MiB of counts): no early return
+    // before that barrier, a wave past the end just sweeps nothing
+    __shared__ int blockCounts[4 * K];
     const double B[4] = {bb[0], bb[1], bb[2], bb[3]};
     bool valid[K];
 #pragma unroll
@@ -173,8 +176,8 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
 #pragma unroll
     for (int kp = 0; kp < KP; ++kp) {
         double Fa[9], Fb[9];
-        const FModelD ma = models[valid[2 * kp] ? h0 + 2 * kp : h0];
-        const FModelD mb = models[valid[2 * kp + 1] ? h0 + 2 * kp + 1 : h0];
+        const FModelD ma = models[valid[2 * kp] ? h0 + 2 * kp : 0];   // slot 0 exists (hypCount >= 1)
+        const FModelD mb = models[valid[2 * kp + 1] ? h0 + 2 * kp + 1 : 0];
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
             Fa[j] = valid[2 * kp] ? ma.f[j] : f_dummy_model(j);
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
     for (int k = 0; k < K; ++k) cnt[k] = 0;
     const int step = 64 * P;
     const int p0 = (int)by * chunk;
-    const int p1 = min(N, p0 + chunk);
+    const int p1 = h0 < hypCount ? min(N, p0 + chunk) : p0;
     const int nFull = p0 + (p1 - p0) / step * step;
     for (int base = p0; base < nFull; base += step) {
         float4 q[P];
@@ -219,15 +222,22 @@ __global__ __launch_bounds__(256) void mcv_f_verify_pk(const float4* __restrict_
         auto x64 = [&](double& x1, double& y1, double& x2, double& y2) { x1 = q.x; y1 = q.y; x2 = q.z; y2 = q.w; };
         spk_sweep_point<KP>(pr, q, v, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
     }
-    // lane k writes model k's count: one store / one atomic instruction per wave over K contiguous slots
+    // lane k stages model k's count (-1: not a valid model, nothing written), then the block's 4 K
+    // contiguous slots go out as one store (or one atomic each when the points are chunked)
     int mine = 0;
     bool mv = false;
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (lane == k) mine = (int)cnt[k], mv = valid[k];
-    if (lane < K && mv) {
-        if (gridDim.y == 1) counts[h0 + lane] = mine;
-        else if (mine) atomicAdd(counts + h0 + lane, mine);
+    if (lane < K) blockCounts[(threadIdx.x >> 6) * K + lane] = mv ? mine : -1;
+    __syncthreads();
+    if (threadIdx.x < 4 * K) {
+        const int v = blockCounts[threadIdx.x];
+        const int slot = (wave - (int)(threadIdx.x >> 6)) * K + (int)threadIdx.x;   // the block's first model + t
+        if (v >= 0) {
+            if (gridDim.y == 1) counts[slot] = v;
+            else if (v) atomicAdd(counts + slot, v);
+        }
     }
 }
 
