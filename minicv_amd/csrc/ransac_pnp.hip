@@ -636,7 +636,10 @@ __global__ __launch_bounds__(256) void mcv_epnp_prep_f64(const double* __restric
     for (int k = 0; k < 3; ++k) pw[3 * (size_t)i + k] = world[3 * (size_t)i + k];
 }
 
-static constexpr int kEpnpTile = 32;
+// 128 points a tile (round 5; 32 before): a quarter of the barrier rounds per 1024-point block, the
+// same per-accumulator point order (the sums are unchanged)
+static constexpr int kEpnpTile = 128;
+static constexpr int kEpnpTermCols = 39;   // the widest non-MtM pass (kSqpSums); MtM stages 24 doubles a point
 
 // One (point, accumulator) term of a pass — the body of the corresponding epnp.cpp loop; the MtM
 // pass adds two products per point (r1 and r2 rows), the others one (t[1] unused).
@@ -688,7 +691,8 @@ template <int MODE>
 __global__ __launch_bounds__(256) void mcv_epnp_pass(const double* __restrict__ pw, const double* __restrict__ us,
                                                      int n, EpnpPassArgs A, int nacc, int nblk,
                                                      double* __restrict__ part) {
-    __shared__ double term[kEpnpTile * 78];
+    static_assert(kSqpSums <= kEpnpTermCols && 24 <= kEpnpTermCols && 27 <= kEpnpTermCols, "term tile width");
+    __shared__ double term[kEpnpTile * kEpnpTermCols];
     int ma = 0, mb = 0;   // MtM: the accumulator's (row, column) of the upper triangle
     if (MODE == kEpnpPassMtm) {
         int r = threadIdx.x;
@@ -719,6 +723,36 @@ __global__ __launch_bounds__(256) void mcv_epnp_pass(const double* __restrict__ 
                     s += rows[j * 24 + ma] * rows[j * 24 + mb];
                     s += rows[j * 24 + 12 + ma] * rows[j * 24 + 12 + mb];
                 }
+        } else if (MODE == kEpnpPassPc || MODE == kEpnpPassAbt) {
+            // a point's three camera-frame positions (and, for A B^T, its centred world point) once
+            // per point instead of once per accumulator; the accumulators' terms are the same
+            // operations on the same values (Pc: pc[j]; Abt: (pc[j] - pc0[N][j]) * (p[k] - pw0[k]))
+            constexpr int W = MODE == kEpnpPassPc ? 9 : 12;
+            double* rows = term;   // [kEpnpTile][W]
+            for (int j = threadIdx.x; j < tn; j += 256) {
+                const double* p = pw + 3 * (size_t)(t0 + j);
+                double al[4];
+                epnp_alphas(A.C, p, al);
+#pragma unroll
+                for (int N = 0; N < 3; ++N) {
+                    double pc[3];
+                    epnp_pc(al, A.ccs[N], pc);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) rows[j * W + 3 * N + c] = MODE == kEpnpPassPc ? pc[c] : pc[c] - A.pc0[N][c];
+                }
+                if (MODE == kEpnpPassAbt)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) rows[j * W + 9 + k] = p[k] - A.pw0[k];
+            }
+            __syncthreads();
+            if (acc < nacc) {
+                if (MODE == kEpnpPassPc) {
+                    for (int j = 0; j < tn; ++j) s += rows[j * W + acc];
+                } else {
+                    const int a = 3 * (acc / 9) + (acc % 9) / 3, b = 9 + acc % 3;
+                    for (int j = 0; j < tn; ++j) s += rows[j * W + a] * rows[j * W + b];
+                }
+            }
         } else {
             for (int w = threadIdx.x; w < tn * nacc; w += 256) {
                 const int j = w / nacc, a = w - j * nacc;
