@@ -1011,7 +1011,8 @@ static void launch_h_verify_cert_k(const void* d_pairs, int N, const void* d_mod
 
 // Certified sweep of the op-by-op error + the exact recount of the slots it marks kStatusRedo.
 // <6, 1>: screened against <4, 2>, <4, 1>, <5, 1>, <3, 2>, <8, 2> and t = 2^-12 / 2^-11 / 2^-10
-// (28.8 ms vs 29.6-33 ms at cfg3; scripts/gpu_r02_cert.sh).
+// (28.8 ms vs 29.6-33 ms at cfg3; scripts/gpu_r02_cert.sh); re-screened in round 5 (same box: 29.9-30.0 ms
+// against 30.7-30.9 / 30.4-30.5 / 31.0-31.1 ms for <4, 1> / <5, 1> / <4, 2>; scripts/gpu_r05_am.sh).
 void launch_h_verify_certified(const float* d_pts4, const void* d_pairs, int N, const void* d_models, int* d_counts,
                                int hypCount, float thr2, const double* d_bb, hipStream_t s) {
     launch_h_verify_cert_k<6, 1>(d_pairs, N, d_models, d_counts, hypCount, thr2, d_bb, s);
