@@ -363,6 +363,9 @@ __global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(con
                     if (tl * TRW + (i & 3) + 8 * (i >> 2) + 4 * h >= nt) cs[i] = 1 << 30;
                 asm volatile("" : "+v"(cs));   // a branch once per launch, not 32 selects per tile
             }
+            // priority 0 for the MFMAs, 1 for the staging and top-2 updates (as mcv_l2_gemm's epilogue;
+            // round 5, same box: 31.9 vs 32.1 us per step)
+            __builtin_amdgcn_s_setprio(0);
             i32x16 acc[QT];
             const int8_t* ar = &lt[buf][col * RBP + 16 * KS * h];
             {
@@ -376,6 +379,7 @@ __global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(con
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][s], acc[qt], 0, 0, 0);
             }
+            __builtin_amdgcn_s_setprio(1);
             lstore(buf ^ 1, st);
             gload(min(tl + 2, tEnd - 1), st);
             // two independent top-2 chains per query tile (rows i < 8 and i >= 8), merged at the end:

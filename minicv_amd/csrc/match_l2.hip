@@ -689,6 +689,11 @@ __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, 
             for (int r = 0; r < 16; ++r) m[q][r] = sm[q][r] = 0.f;
         const char* rowh = reinterpret_cast<const char*>(lh(buf)) + col * RB;
         const char* rowl = reinterpret_cast<const char*>(ll(buf)) + col * RB;
+        // wave priority 0 for the MFMA block, 1 for the epilogue below: a wave that has its scores
+        // gets through its VALU work ahead of the waves issuing MFMAs, and back to the matrix pipe
+        // sooner (round 5, same box: GEMM 1.716 vs 1.739-1.747 ms, on another 1.736-1.744 vs 1.769-1.781 ms;
+        // priority 1 around the MFMAs instead 1.754-1.762)
+        __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
             const int p = ((2 * kb + h) ^ key) << 4;
@@ -701,6 +706,7 @@ __device__ __forceinline__ void l2_gemm16_body(const _Float16* __restrict__ qh, 
 #pragma unroll
             for (int q = 0; q < QT; ++q) sm[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[q][kb], sm[q], 0, 0, 0);
         }
+        __builtin_amdgcn_s_setprio(1);
         float4 nv[1][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) nv[0][j] = *reinterpret_cast<const float4*>(lnorm(buf) + 8 * j + 4 * h);
