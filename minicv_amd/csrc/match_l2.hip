@@ -903,13 +903,23 @@ __global__ __launch_bounds__(64) void mcv_l2_refine(const L2Part* __restrict__ p
     if (q >= nq) return;
     float b1 = INFINITY, b2 = INFINITY, c1 = INFINITY, c2 = INFINITY, c3 = INFINITY;
     int i1 = -1, i2 = -1;
-    for (int c = 0; c < nchunks; ++c) {
-        const L2Part p = part[(size_t)c * nqPad + q];
-        top2_push(b1, i1, b2, i2, p.b1, p.i1);
-        top2_push(b1, i1, b2, i2, p.b2, p.i2);
-        third_fold(c1, c2, c3, p.b1);
-        third_fold(c1, c2, c3, p.b2);
-        third_fold(c1, c2, c3, p.b3);
+    // eight partials in flight before the first fold (one load per iteration waited for its own
+    // round trip: 16 dependent loads a query at cfg5); the loads past the end re-read the last slot
+    // and fold as +inf (no change), so the fold order and the result are those of the plain loop
+    for (int c0 = 0; c0 < nchunks; c0 += 8) {
+        L2Part pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pp[u] = part[(size_t)min(c0 + u, nchunks - 1) * nqPad + q];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool in = c0 + u < nchunks;
+            const float s1 = in ? pp[u].b1 : INFINITY, s2 = in ? pp[u].b2 : INFINITY, s3 = in ? pp[u].b3 : INFINITY;
+            top2_push(b1, i1, b2, i2, s1, pp[u].i1);
+            top2_push(b1, i1, b2, i2, s2, pp[u].i2);
+            third_fold(c1, c2, c3, s1);
+            third_fold(c1, c2, c3, s2);
+            third_fold(c1, c2, c3, s3);
+        }
     }
     const float* qr = qraw + (size_t)q * dim;
     double e1 = INFINITY, e2 = INFINITY;
