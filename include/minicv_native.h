@@ -256,6 +256,19 @@ MCV_API int cvMatchHamming(const uint8_t* q, const int nq, const uint8_t* t, con
 MCV_API int cvMatchL2(const float* q, const int nq, const float* t, const int nt, const int dim,
                       int* idx, float* dist, int* idx2, float* dist2);
 
+/* Multi-GPU forms of the two matchers (query blocks Nq / D per GPU, train set
+ * replicated), for a host that calls one synchronous export from one process like the reference's
+ * P/Invoke layer (OpenCV.fs:339-382). The queries are split into deviceCount contiguous blocks (the
+ * first nq % deviceCount one query longer), block k runs on visible device (current + k) mod count,
+ * the train set is uploaded once and peer-copied over xGMI to the other devices, and every block's
+ * outputs land in the caller's arrays at its offset. Results are identical to deviceCount = 1.
+ * deviceCount in [1, 16]; the other arguments and the return are cvMatchHamming's / cvMatchL2's. */
+MCV_API int cvMatchHammingMulti(const uint8_t* q, const int nq, const uint8_t* t, const int nt,
+                                const int bytesPerDesc, const int deviceCount, int* idx, int* dist, int* idx2,
+                                int* dist2);
+MCV_API int cvMatchL2Multi(const float* q, const int nq, const float* t, const int nt, const int dim,
+                           const int deviceCount, int* idx, float* dist, int* idx2, float* dist2);
+
 /* Diagnostics of the exact L2 re-rank: queries the calling thread's last L2 match sent to the exact
  * full scan (near-ties the GEMM form cannot separate); synchronises that match's stream. */
 MCV_API int mcvL2LastExactScans(void);

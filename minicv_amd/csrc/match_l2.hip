@@ -905,7 +905,9 @@ __global__ __launch_bounds__(64) void mcv_l2_refine(const L2Part* __restrict__ p
     int i1 = -1, i2 = -1;
     // eight partials in flight before the first fold (one load per iteration waited for its own
     // round trip: 16 dependent loads a query at cfg5); the loads past the end re-read the last slot
-    // and fold as +inf (no change), so the fold order and the result are those of the plain loop
+    // and fold as the empty entry (+inf, -1): an empty entry never displaces anything (lex_less sorts
+    // index -1 last), so the fold order and the result are those of the plain loop. The index must be
+    // -1 too: (+inf, a real index) would win against an empty second place and duplicate i1.
     for (int c0 = 0; c0 < nchunks; c0 += 8) {
         L2Part pp[8];
 #pragma unroll
@@ -914,8 +916,8 @@ __global__ __launch_bounds__(64) void mcv_l2_refine(const L2Part* __restrict__ p
         for (int u = 0; u < 8; ++u) {
             const bool in = c0 + u < nchunks;
             const float s1 = in ? pp[u].b1 : INFINITY, s2 = in ? pp[u].b2 : INFINITY, s3 = in ? pp[u].b3 : INFINITY;
-            top2_push(b1, i1, b2, i2, s1, pp[u].i1);
-            top2_push(b1, i1, b2, i2, s2, pp[u].i2);
+            top2_push(b1, i1, b2, i2, s1, in ? pp[u].i1 : -1);
+            top2_push(b1, i1, b2, i2, s2, in ? pp[u].i2 : -1);
             third_fold(c1, c2, c3, s1);
             third_fold(c1, c2, c3, s2);
             third_fold(c1, c2, c3, s3);

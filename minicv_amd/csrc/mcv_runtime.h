@@ -62,6 +62,14 @@ struct DevBuf {
         MCV_HIP(hipMalloc((void**)&p, (count ? count : 1) * sizeof(T)));
         n = count;
     }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
@@ -92,22 +100,28 @@ struct StreamFence {
     hipEvent_t ev = nullptr;
     hipStream_t last = nullptr;
     bool used = false;
-    // A call on another stream than the previous one waits for the previous stream's work, recorded
-    // then (everything enqueued on it so far, the previous call included); calls that stay on one
-    // stream need no event (an event record costs the stream a marker packet, ~3 us per call). The
-    // previous call's stream must still exist; if the record fails the device is
-    // synchronised instead.
+    // The null stream and the per-thread default stream live as long as the process; a caller's own
+    // stream may be destroyed right after the call.
+    static bool persistent(hipStream_t s) { return s == nullptr || s == hipStreamPerThread; }
+    // A call on another stream than the previous one waits for the previous call's completion event.
+    // A call on a caller-created stream records that event when it leaves (one reused event), so a
+    // stream the caller destroys after the call is never touched again. A call on the null / per-thread
+    // stream defers the record to the next call that switches streams (an event record costs the stream
+    // a marker packet, ~3 us per call, which back-to-back calls on the default stream would otherwise
+    // pay on every call): those streams cannot be destroyed, so the deferred record is always valid.
     void enter(hipStream_t s) {
         if (!used || last == s) return;
-        if (!ev) MCV_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        if (hipEventRecord(ev, last) != hipSuccess) {
-            (void)hipGetLastError();
-            MCV_HIP(hipDeviceSynchronize());
-            return;
+        if (persistent(last)) {
+            if (!ev) MCV_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            MCV_HIP(hipEventRecord(ev, last));
         }
         MCV_HIP(hipStreamWaitEvent(s, ev, 0));
     }
     void leave(hipStream_t s) {
+        if (!persistent(s)) {
+            if (!ev) MCV_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            MCV_HIP(hipEventRecord(ev, s));
+        }
         last = s;
         used = true;
     }

@@ -114,6 +114,8 @@ SIGNATURES = {
     "cvMatchAndFindModel": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "cvMatchHamming": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
     "cvMatchL2": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P]),
+    "cvMatchHammingMulti": (_I, [_P, _I, _P, _I, _I, _I, _P, _P, _P, _P]),
+    "cvMatchL2Multi": (_I, [_P, _I, _P, _I, _I, _I, _P, _P, _P, _P]),
     "cvFindScaledPose": (_I, [_D, _P, _P, _P, _I, _P, _P, _P, _P]),
     "cvFindScaledPoseCosts": (_I, [_P, _P, _P, _I, _P, _P, _P, _P]),
     "mcvGetLastError": (C.c_char_p, []),

@@ -79,21 +79,27 @@ def findFundamentalMat(a, b, params: RansacParams | None = None):
     return cnt, np.array(F.M[:], dtype=np.float64).reshape(3, 3), ms[:n] != 0
 
 
-def matchHamming(q, t):
-    """BFMatcher(NORM_HAMMING).knnMatch(k=2). q, t: uint8 [n][bytes]. -> (idx, dist, idx2, dist2)."""
+def matchHamming(q, t, deviceCount: int = 1):
+    """BFMatcher(NORM_HAMMING).knnMatch(k=2). q, t: uint8 [n][bytes]. -> (idx, dist, idx2, dist2).
+    deviceCount > 1: cvMatchHammingMulti (query blocks over the visible GPUs, same answer)."""
     q = np.ascontiguousarray(q, dtype=np.uint8)
     t = np.ascontiguousarray(t, dtype=np.uint8)
     if q.ndim != 2 or t.ndim != 2 or q.shape[1] != t.shape[1]:
         raise ValueError("descriptor arrays must be [n][bytes] with equal widths")
     nq, nt, nb = q.shape[0], t.shape[0], q.shape[1]
     out = [np.empty(max(nq, 1), dtype=np.int32) for _ in range(4)]
-    r = N.lib().cvMatchHamming(q.ctypes.data, nq, t.ctypes.data, nt, nb, *[o.ctypes.data for o in out])
+    if deviceCount == 1:
+        r = N.lib().cvMatchHamming(q.ctypes.data, nq, t.ctypes.data, nt, nb, *[o.ctypes.data for o in out])
+    else:
+        r = N.lib().cvMatchHammingMulti(q.ctypes.data, nq, t.ctypes.data, nt, nb, int(deviceCount),
+                                        *[o.ctypes.data for o in out])
     N.check(r == nq, "cvMatchHamming")
     return tuple(o[:nq] for o in out)
 
 
-def matchL2(q, t):
-    """BFMatcher(NORM_L2).knnMatch(k=2). q, t: float32 [n][dim]. -> (idx, dist, idx2, dist2)."""
+def matchL2(q, t, deviceCount: int = 1):
+    """BFMatcher(NORM_L2).knnMatch(k=2). q, t: float32 [n][dim]. -> (idx, dist, idx2, dist2).
+    deviceCount > 1: cvMatchL2Multi (query blocks over the visible GPUs, same answer)."""
     q = np.ascontiguousarray(q, dtype=np.float32)
     t = np.ascontiguousarray(t, dtype=np.float32)
     if q.ndim != 2 or t.ndim != 2 or q.shape[1] != t.shape[1]:
@@ -101,8 +107,12 @@ def matchL2(q, t):
     nq, nt, dim = q.shape[0], t.shape[0], q.shape[1]
     idx, idx2 = np.empty(max(nq, 1), np.int32), np.empty(max(nq, 1), np.int32)
     d, d2 = np.empty(max(nq, 1), np.float32), np.empty(max(nq, 1), np.float32)
-    r = N.lib().cvMatchL2(q.ctypes.data, nq, t.ctypes.data, nt, dim, idx.ctypes.data, d.ctypes.data,
-                          idx2.ctypes.data, d2.ctypes.data)
+    if deviceCount == 1:
+        r = N.lib().cvMatchL2(q.ctypes.data, nq, t.ctypes.data, nt, dim, idx.ctypes.data, d.ctypes.data,
+                              idx2.ctypes.data, d2.ctypes.data)
+    else:
+        r = N.lib().cvMatchL2Multi(q.ctypes.data, nq, t.ctypes.data, nt, dim, int(deviceCount), idx.ctypes.data,
+                                   d.ctypes.data, idx2.ctypes.data, d2.ctypes.data)
     N.check(r == nq, "cvMatchL2")
     return idx[:nq], d[:nq], idx2[:nq], d2[:nq]
 

@@ -72,9 +72,9 @@ def check_l2(oracle, q, t):
     ri, rd, ri2, rd2 = oracle.match_l2(q, t)
     np.testing.assert_array_equal(idx, ri)
     np.testing.assert_array_equal(d, rd.astype(np.float32))
-    if len(t) > 1:
-        np.testing.assert_array_equal(idx2, ri2)
-        np.testing.assert_array_equal(d2, rd2.astype(np.float32))
+    # every shape, nt = 1 included (the second place must stay -1 / +inf there)
+    np.testing.assert_array_equal(idx2, ri2)
+    np.testing.assert_array_equal(d2, rd2.astype(np.float32))
     return 1.0
 
 
@@ -185,12 +185,13 @@ def test_l2_medium_vs_oracle(gpu, oracle):
 
 @pytest.mark.slow
 def test_l2_full_size_cfg5(gpu, oracle):
-    """BASELINE config[4] at full size (50k x 50k SIFT-128 fp32): 1000 sampled queries exactly equal
-    to the oracle (indices and distances bit for bit), planted-neighbour recall, determinism."""
+    """BASELINE config[4] at full size (50k x 50k SIFT-128 fp32): 4000 sampled queries plus the first
+    and last 64 exactly equal to the oracle (indices and distances bit for bit), planted-neighbour
+    recall, determinism. The multi-GPU rank slices: test_gpu_matcher_shards.py."""
     q, t, planted = S.l2_problem(50_000, 50_000, dim=128, seed=5)
     idx, d, idx2, d2 = opencv.matchL2(q, t)
     rng = np.random.default_rng(0)
-    pick = np.sort(rng.choice(50_000, size=1000, replace=False))
+    pick = np.unique(np.r_[0:64, 50_000 - 64:50_000, rng.choice(50_000, size=4000, replace=False)])
     ri, rd, ri2, rd2 = oracle.match_l2(q[pick], t)
     np.testing.assert_array_equal(idx[pick], ri)
     np.testing.assert_array_equal(idx2[pick], ri2)
