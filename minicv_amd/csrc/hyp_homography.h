@@ -192,17 +192,10 @@ MCV_HD bool h_solve4_elim(const float* sx, const float* sy, const float* dx, con
     return ok;
 }
 
-// Minimal 4-point homography src -> dst = HomographyEstimatorCallback::runKernel on the sample:
-// centroid + mean-|dev| normalisation, LtL[j][k] += Lx[j] Lx[k] + Ly[j] Ly[k] (k >= j, points in
-// order, from +0), cv::eigen (eig9_jacobi, jacobi_eig.h) -> H0 = the eigenvector of the smallest
-// eigenvalue, H = invHnorm H0 Hnorm2 (3x3 gemm order), scaled by 1/H22 (convertTo). Returns false
-// when the scales vanish (runKernel returns 0) or the result is not finite (a non-finite model
-// counts no inlier in OpenCV: the same RANSAC outcome as no model).
-template <class WS>
-MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const float* dy, double* H, WS& ws,
-                     bool fast = false) {
-    if (fast) return h_solve4_elim(sx, sy, dx, dy, H);
-    // Normalisation (runKernel): centroids and mean absolute deviations, in double.
+// runKernel's normalisation: centroids and mean absolute deviations in double -> nm = {cmx, cmy, smx,
+// smy, cMx, cMy, sMx, sMy} (the scales already inverted, 4 / sum). False when a scale vanishes
+// (runKernel returns 0).
+MCV_HD bool h_norm4(const float* sx, const float* sy, const float* dx, const float* dy, double (&nm)[8]) {
     double cMx = 0, cMy = 0, cmx = 0, cmy = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
@@ -222,9 +215,18 @@ MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const fl
     }
     if (fabs(smx) < kDblEpsilon || fabs(smy) < kDblEpsilon || fabs(sMx) < kDblEpsilon || fabs(sMy) < kDblEpsilon)
         return false;
-    smx = 4 / smx; smy = 4 / smy; sMx = 4 / sMx; sMy = 4 / sMy;
+    nm[0] = cmx; nm[1] = cmy; nm[2] = 4 / smx; nm[3] = 4 / smy;
+    nm[4] = cMx; nm[5] = cMy; nm[6] = 4 / sMx; nm[7] = 4 / sMy;
+    return true;
+}
 
-    // LtL: diagonal -> W slots, strict upper triangle -> packed A slots of the eigen workspace.
+// runKernel's LtL[j][k] += Lx[j] Lx[k] + Ly[j] Ly[k] (k >= j, points in order, from +0): diagonal ->
+// ws[kEigW..], strict upper triangle -> ws[kEigA..] (the eigen workspace's layout, both slice kinds).
+// False when an entry is not finite.
+template <class WS>
+MCV_HD bool h_ltl4(const float* sx, const float* sy, const float* dx, const float* dy, const double (&nm)[8], WS& ws) {
+    const double cmx = nm[0], cmy = nm[1], smx = nm[2], smy = nm[3], cMx = nm[4], cMy = nm[5], sMx = nm[6],
+                 sMy = nm[7];
     double dg[9], up[36];
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
@@ -268,14 +270,15 @@ MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const fl
         fin = fin && isfinite(dg[e]);
         ws[kEigW + e] = dg[e];
     }
-    if (!fin) return false;
-    double w[9];
-    const int r = eig9_jacobi(ws, w, 8);
-    double H0[9];
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-    for (int j = 0; j < 9; ++j) H0[j] = ws[kEigV + 9 * r + j];
+    return fin;
+}
+
+// H0 (the eigenvector) -> H = invHnorm H0 Hnorm2 (3x3 gemm order), scaled by 1/H22 (convertTo). False
+// when the result is not finite (a non-finite model counts no inlier in OpenCV: the same RANSAC outcome
+// as no model).
+MCV_HD bool h_from_eig(const double (&H0)[9], const double (&nm)[8], double* H) {
+    const double cmx = nm[0], cmy = nm[1], smx = nm[2], smy = nm[3], cMx = nm[4], cMy = nm[5], sMx = nm[6],
+                 sMy = nm[7];
     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
     double T[9];
@@ -293,20 +296,34 @@ MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const fl
     return ok;
 }
 
-// One hypothesis: returns 1 (model written), kStatusNoModel, or kStatusNoSample.
-// pts4: N packed {x, y, x', y'}. idx_out (optional) receives the accepted sample.
+// Minimal 4-point homography src -> dst = HomographyEstimatorCallback::runKernel on the sample:
+// centroid + mean-|dev| normalisation (h_norm4), the LtL (h_ltl4), cv::eigen (eig9_jacobi,
+// jacobi_eig.h) -> H0 = the eigenvector of the smallest eigenvalue, H = invHnorm H0 Hnorm2 / H22
+// (h_from_eig). Returns false when the scales vanish, the LtL or the result is not finite.
 template <class WS>
-MCV_HD int h_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t hyp, double* H, HModelF* mf,
-                        int* idx_out, WS& ws, bool fast = false) {
+MCV_HD bool h_solve4(const float* sx, const float* sy, const float* dx, const float* dy, double* H, WS& ws,
+                     bool fast = false) {
+    if (fast) return h_solve4_elim(sx, sy, dx, dy, H);
+    double nm[8];
+    if (!h_norm4(sx, sy, dx, dy, nm)) return false;
+    if (!h_ltl4(sx, sy, dx, dy, nm, ws)) return false;
+    double w[9];
+    const int r = eig9_jacobi(ws, w, 8);
+    double H0[9];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int j = 0; j < 9; ++j) H0[j] = ws[kEigV + 9 * r + j];
+    return h_from_eig(H0, nm, H);
+}
+
+// The sample search: OpenCV's getSubset attempts with the subset check (none for a tabled sampler),
+// the accepted sample's points and indices. False = the sampler is exhausted (OpenCV's `break`).
+MCV_HD bool h_sample(const float* pts4, int N, const Sampler& smp, uint64_t hyp, float* sx, float* sy, float* dx,
+                     float* dy, int* idx) {
     SubsetSrc<4> src(smp, hyp);
-    float sx[4], sy[4], dx[4], dy[4];
-    int idx[4];
-    // The sample search and the solve are kept apart: with the solve inside the attempt loop, lanes of
-    // one wave that accept their sample at different attempts would each run the eigen-solve in a
-    // separate pass of the loop (one pass per distinct attempt count).
-    bool found = false;
     for (int attempt = 0; attempt < kMaxAttempts; ++attempt) {
-        const int got = src.next(N, idx);
+        const int got = src.next(N, *reinterpret_cast<int(*)[4]>(idx));
         if (got < 0) break;
         if (got == 0) continue;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -317,18 +334,35 @@ MCV_HD int h_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t h
             sx[i] = p[0]; sy[i] = p[1]; dx[i] = p[2]; dy[i] = p[3];
         }
         if (!src.tabled() && !h_check_subset(sx, sy, dx, dy)) continue;
-        found = true;
-        break;
+        return true;
     }
-    if (!found) return kStatusNoSample;
-    if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
-    if (!h_solve4(sx, sy, dx, dy, H, ws, fast)) return kStatusNoModel;
+    return false;
+}
+
+// The fp32 sweep model of H (rows 0..1 and h20, h21 as float); false when one is not finite.
+MCV_HD bool h_model_f(const double* H, HModelF* mf) {
     bool ok = true;
     for (int i = 0; i < 8; ++i) {
         mf->h[i] = (float)H[i];
         ok = ok && isfinite(mf->h[i]);
     }
-    return ok ? 1 : kStatusNoModel;
+    return ok;
+}
+
+// One hypothesis: returns 1 (model written), kStatusNoModel, or kStatusNoSample.
+// pts4: N packed {x, y, x', y'}. idx_out (optional) receives the accepted sample.
+template <class WS>
+MCV_HD int h_hypothesis(const float* pts4, int N, const Sampler& smp, uint64_t hyp, double* H, HModelF* mf,
+                        int* idx_out, WS& ws, bool fast = false) {
+    float sx[4], sy[4], dx[4], dy[4];
+    int idx[4];
+    // The sample search and the solve are kept apart: with the solve inside the attempt loop, lanes of
+    // one wave that accept their sample at different attempts would each run the eigen-solve in a
+    // separate pass of the loop (one pass per distinct attempt count).
+    if (!h_sample(pts4, N, smp, hyp, sx, sy, dx, dy, idx)) return kStatusNoSample;
+    if (idx_out) for (int i = 0; i < 4; ++i) idx_out[i] = idx[i];
+    if (!h_solve4(sx, sy, dx, dy, H, ws, fast)) return kStatusNoModel;
+    return h_model_f(H, mf) ? 1 : kStatusNoModel;
 }
 
 // HomographyEstimatorCallback::computeError for one correspondence, two bit-level definitions

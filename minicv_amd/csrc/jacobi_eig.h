@@ -33,6 +33,28 @@ namespace mcv {
 // [0, 36) strict upper triangle, [36, 45) W, [45, 126) V, 126 = a junk slot (the rotation's
 // branch-free form sends the two skipped indices there).
 static constexpr int kEigA = 0, kEigW = 36, kEigV = 45, kEigJunk = 126, kEigWs = 127;
+// The split solve (eig9_jacobi<WS, true> + eig9_replay): pass 1 keeps only the upper triangle, W and
+// the junk slot (46 doubles, odd lane stride 47: 376 B per lane instead of 1016) and logs each
+// rotation; pass 2 replays the log on V alone (81 doubles, odd stride). Same operations on the same
+// values in the same order as the one-pass solve, so the same bits.
+static constexpr int kEigAwJunk = 45, kEigAwWs = 47, kEigVWs = 81;
+// One logged rotation: c (JacobiImpl_'s c = t / hypot(p, t) lies in [1/sqrt(2), 1], so its bits 62..53
+// are always 0b0111111111 and bit 63 is 0: bits 63..53 carry (k << 4) | l instead) and s.
+struct alignas(16) EigRot {
+    double c, s;
+};
+MCV_HD bool eig_rot_c_ok(double c) { return c >= 0.5 && c <= 1.0; }
+MCV_HD double eig_rot_pack(double c, int k, int l) {
+    const uint64_t b = (__builtin_bit_cast(uint64_t, c) & ((1ull << 53) - 1)) | ((uint64_t)((k << 4) | l) << 53);
+    return __builtin_bit_cast(double, b);
+}
+MCV_HD double eig_rot_c(double e, int& k, int& l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, e);
+    const int kl = (int)(b >> 53);
+    k = kl >> 4;
+    l = kl & 15;
+    return __builtin_bit_cast(double, (b & ((1ull << 53) - 1)) | (0x1FFull << 53));
+}
 // Lanes per hypothesis-kernel block: the 1016-byte working set per lane makes LDS the occupancy
 // limit (160 KB per CU). 40 lanes = 4 blocks of 40.6 KB per CU, one wave on every SIMD (cfg3 screen,
 // 2^20 hypotheses: 64 -> 39 lanes took the H generate 13.9 -> 11.4 ms; 39 vs 40 lanes 9.63 vs 9.34 ms
@@ -70,13 +92,13 @@ struct EigWsLane {
 struct EigPairLut {
     uint32_t w[36][12];
 };
-constexpr EigPairLut eig_make_pair_lut() {
+constexpr EigPairLut eig_make_pair_lut(int junk) {
     EigPairLut t{};
     for (int k = 0; k < 9; ++k)
         for (int l = k + 1; l < 9; ++l) {
             const int row = ((k * (15 - k)) >> 1) - 1 + l;
             for (int i = 0; i < 9; ++i) {
-                int e0 = kEigJunk, e1 = kEigJunk;
+                int e0 = junk, e1 = junk;
                 if (i != k && i != l) {
                     e0 = i < k ? ((i * (15 - i)) >> 1) - 1 + k : ((k * (15 - k)) >> 1) - 1 + i;
                     e1 = i < l ? ((i * (15 - i)) >> 1) - 1 + l : ((l * (15 - l)) >> 1) - 1 + i;
@@ -87,7 +109,8 @@ constexpr EigPairLut eig_make_pair_lut() {
     return t;
 }
 #if defined(__HIP__)
-static __constant__ EigPairLut kEigPairLut = eig_make_pair_lut();
+static __constant__ EigPairLut kEigPairLut = eig_make_pair_lut(kEigJunk);
+static __constant__ EigPairLut kEigPairLutAW = eig_make_pair_lut(kEigAwJunk);
 #endif
 
 // 4-bit fields: indR[i] at field i (i = 0..7), indC[i] at field i - 1 (i = 1..8).
@@ -151,14 +174,25 @@ MCV_HD void eig_pick(double& v, int& kl, double v2, int kl2) {
 // the function returns the workspace row of V (the original row index) that the sort moved to
 // position `pos` — V row `pos` of OpenCV's result is ws[kEigV + 9 * ret + j]. Returns the rotation
 // count through *iters when non-null (diagnostics).
-template <class WS>
-MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
+//
+// LOG = true (pass 1 of the split solve): the workspace is the 47-double AW slice, V is neither
+// initialised nor rotated, and rotation t goes to log[t * logStride] (EigRot, c packed with k, l).
+// *iters = the rotation count, or -1 when it would exceed logCap or a c falls outside [0.5, 1] (not
+// for finite input; the caller then runs the one-pass solve). The return value is as above; the
+// eigenvector is row `ret` of the V that eig9_replay rebuilds from the log.
+template <class WS, bool LOG = false>
+MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr, EigRot* log = nullptr,
+                       int logStride = 0, int logCap = 0) {
     constexpr int n = 9;
+    constexpr int junk = LOG ? kEigAwJunk : kEigJunk;
+    if constexpr (!LOG) {
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-    for (int i = 0; i < n * n; ++i) ws[kEigV + i] = (i / n == i % n) ? 1.0 : 0.0;
-    ws[kEigJunk] = 0.0;   // stays +0: the skipped pair rotates (0, 0) into (+0, +0)
+        for (int i = 0; i < n * n; ++i) ws[kEigV + i] = (i / n == i % n) ? 1.0 : 0.0;
+    }
+    ws[junk] = 0.0;   // stays +0: the skipped pair rotates (0, 0) into (+0, +0)
+    bool logOk = true;
     uint32_t indR = 0, indC = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
@@ -234,9 +268,10 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
 #if defined(__HIP_DEVICE_COMPILE__)
         if constexpr (std::is_same<WS, EigWsLane>::value) {
             // the pair table's row for this pivot (3 vector loads from L1) -> byte offsets
-            const uint4* lr = reinterpret_cast<const uint4*>(kEigPairLut.w[ekl]);
+            const EigPairLut& lut = LOG ? kEigPairLutAW : kEigPairLut;
+            const uint4* lr = reinterpret_cast<const uint4*>(lut.w[ekl]);
             const uint4 q0 = lr[0], q1 = lr[1];
-            const uint32_t q8 = kEigPairLut.w[ekl][8];
+            const uint32_t q8 = lut.w[ekl][8];
             const uint32_t qw[n] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q8};
             char* const b = reinterpret_cast<char*>(ws.p);
 #pragma unroll
@@ -258,23 +293,35 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
                 const int mk = -(int)(i < k), ml = -(int)(i < l), ms = -(int)(i == k || i == l);
                 const int x0 = ((eig_row_base(i) + k) & mk) | ((rk + i) & ~mk);
                 const int x1 = ((eig_row_base(i) + l) & ml) | ((rl + i) & ~ml);
-                e0[i] = (kEigJunk & ms) | (x0 & ~ms);
-                e1[i] = (kEigJunk & ms) | (x1 & ~ms);
+                e0[i] = (junk & ms) | (x0 & ~ms);
+                e1[i] = (junk & ms) | (x1 & ~ms);
                 a0[i] = ws[e0[i]];
                 b0[i] = ws[e1[i]];
             }
         }
         const int vk = kEigV + (k << 3) + k, vl = kEigV + (l << 3) + l;   // + 9 k, + 9 l
+        if constexpr (!LOG) {
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-        for (int i = 0; i < n; ++i) {
-            va[i] = ws[vk + i];
-            vb[i] = ws[vl + i];
+            for (int i = 0; i < n; ++i) {
+                va[i] = ws[vk + i];
+                vb[i] = ws[vl + i];
+            }
         }
         const double y = (wl - wk) * 0.5;
         double c, s, t;
         eig_rotation(p, y, c, s, t);
+        if constexpr (LOG) {
+            if (it >= logCap || !eig_rot_c_ok(c)) {
+                logOk = false;
+                break;
+            }
+            EigRot e;
+            e.c = eig_rot_pack(c, k, l);
+            e.s = s;
+            log[(int64_t)it * logStride] = e;
+        }
         ws[ekl] = 0;
         ws[kEigW + k] = wk - t;
         ws[kEigW + l] = wl + t;
@@ -298,12 +345,14 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
             ws[e1[i]] = nl[i];
         }
         // rotate eigenvectors
+        if constexpr (!LOG) {
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-        for (int i = 0; i < n; ++i) {
-            ws[vk + i] = va[i] * c - vb[i] * s;
-            ws[vl + i] = va[i] * s + vb[i] * c;
+            for (int i = 0; i < n; ++i) {
+                ws[vk + i] = va[i] * c - vb[i] * s;
+                ws[vl + i] = va[i] * s + vb[i] * c;
+            }
         }
         // refresh indR / indC of rows and columns k and l (first maximum by magnitude). OpenCV takes
         // the first in-range element unconditionally; here the index starts there (k + 1 for a row,
@@ -328,7 +377,7 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
         if (l < n - 1) indR = eig_set_nib(indR, l, mRl);
         indC = eig_set_nib(indC, l - 1, mCl);   // l >= 1
     }
-    if (iters) *iters = it;
+    if (iters) *iters = logOk ? it : -1;
     // descending selection sort, rows of V swapped along (tracked as a permutation)
     int perm[n];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -365,6 +414,60 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr) {
     for (int i = 0; i < n; ++i)
         if (i == pos) r = perm[i];
     return r;
+}
+
+// Pass 2 of the split solve: V (the 81-double slice v, row-major) rebuilt from pass 1's rotation log,
+// rotation by rotation exactly as eig9_jacobi rotates it (rows k and l, the same products and sums).
+// The columns of V rotate independently, so C columns from c0 can run on one lane (C = 9: the whole
+// matrix; C = 3: three lanes per hypothesis). The log entries stream through a ring of D loads in
+// flight (one load ahead waited out the HBM latency every rotation: 2.1 ms per 2^20 hypotheses).
+// The caller initialises V to the identity.
+// TR: V stored transposed (element (i, c) at 9 c + i: a lane's columns are contiguous).
+template <int C, int D, bool TR = false, class WS>
+MCV_HD void eig9_replay_cols(WS& v, int c0, const EigRot* log, int64_t logStride, int nrot) {
+    EigRot q[D];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int u = 0; u < D; ++u) q[u] = u < nrot ? log[(int64_t)u * logStride] : EigRot{0.0, 0.0};
+    for (int t0 = 0; t0 < nrot; t0 += D) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+        for (int u = 0; u < D; ++u) {
+            const EigRot e = q[u];
+            const int tn = t0 + u + D;
+            if (tn < nrot) q[u] = log[(int64_t)tn * logStride];
+            if (t0 + u < nrot) {
+                int k, l;
+                const double c = eig_rot_c(e.c, k, l), s = e.s;
+                // element (row, c0 + i): row-major 9 row + c0 + i, transposed 9 (c0 + i) + row
+                const int vk = TR ? 9 * c0 + k : (k << 3) + k + c0, vl = TR ? 9 * c0 + l : (l << 3) + l + c0;
+                constexpr int st = TR ? 9 : 1;
+                double va[C], vb[C];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+                for (int i = 0; i < C; ++i) {
+                    va[i] = v[vk + st * i];
+                    vb[i] = v[vl + st * i];
+                }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+                for (int i = 0; i < C; ++i) {
+                    v[vk + st * i] = va[i] * c - vb[i] * s;
+                    v[vl + st * i] = va[i] * s + vb[i] * c;
+                }
+            }
+        }
+    }
+}
+
+template <class WS>
+MCV_HD void eig9_replay(WS& v, const EigRot* log, int64_t logStride, int nrot) {
+    for (int i = 0; i < 81; ++i) v[i] = (i / 9 == i % 9) ? 1.0 : 0.0;
+    eig9_replay_cols<9, 4>(v, 0, log, logStride, nrot);
 }
 
 }  // namespace mcv

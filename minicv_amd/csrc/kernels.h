@@ -24,8 +24,11 @@ struct HOneOut {
 void launch_h_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast);
 void launch_h_mask_one(const float* d_pts4, int N, const HOneOut* d_one, float thr2, bool fused, uint8_t* d_mask,
                        int* d_count, hipStream_t s);
+// d_scratch (h_gen_scratch_bytes(hypCount) bytes): the split eigen generate's rotation log, samples
+// and overflow list (ransac_h.hip); nullptr runs the one-pass solve.
 void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_models,
-                       double* d_h64, int* d_counts, hipStream_t s, bool fast);
+                       double* d_h64, int* d_counts, hipStream_t s, bool fast, void* d_scratch = nullptr);
+size_t h_gen_scratch_bytes(int hypCount);
 void launch_h_verify(const float* d_pts4, int N, const void* d_models, int* d_counts, int hypCount, float thr2,
                      bool fused, const float* d_bbox, hipStream_t s);
 void launch_bbox(const float* d_pts4, int N, float* d_bbox, hipStream_t s);

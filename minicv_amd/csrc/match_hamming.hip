@@ -409,6 +409,18 @@ __global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(con
                 return k >= (1u << 29) ? 0xFFFFFFFFu : ((k >> 13) << kIdxBits) | (base + (k & (kHamChunkRows - 1)));
             };
             const int qi = q0 + 32 * qt + col;
+            // Memory ordering of the fold (why no release / acquire fence is needed). The hand-off is the
+            // write-through form MI355X_MICROARCH.md's correctness table lists in place of the agent-scope
+            // release / acquire pair: (1) EVERY store of the handed-off partials is an agent-scope atomic
+            // store, which gfx950 issues with sc1 — performed at the device-coherent level, past this CU's
+            // L1 and any XCD's L2, never left dirty in a non-coherent cache; (2) each storing wave drains
+            // them (s_waitcnt vmcnt(0) below) and the block's barrier follows before thread 0's arrival
+            // add, so the add is issued only after every partial of the block has been performed; (3) the
+            // arrival counter is itself an agent-scope atomic, and the last arriver reads the partials only
+            // after its add has returned (the __syncthreads after it), with agent-scope atomic loads (sc1:
+            // served from the coherent level, never from a stale L1 / L2 line). A counter value of nseg - 1
+            // therefore implies every segment's partials are visible to those loads. The agent-scope fence
+            // this replaces writes back / invalidates a whole XCD L2 per block (30 -> 93 us per launch).
             if (h == 0 && qi < nq) {
                 const uint64_t v = (uint64_t)glob(m1[qt]) | ((uint64_t)glob(m2[qt]) << 32);
                 __hip_atomic_store(reinterpret_cast<uint64_t*>(part) + (size_t)slot * nq + qi, v, __ATOMIC_RELAXED,

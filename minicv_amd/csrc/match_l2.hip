@@ -72,7 +72,10 @@ struct L2Part { float b1, b2, b3; int i1, i2, i3; };
 
 // A GEMM segment's partial top-3 for query q into its slot, and empty partials (+inf, index -1: they
 // change no merge) into the nEmpty slots after it that no segment of this (query block, chunk) item
-// writes (mcv_l2_gemm's partition).
+// writes (mcv_l2_gemm's partition). Memory ordering: unlike the Hamming GEMM's in-kernel fold, the L2
+// partials are folded by mcv_l2_refine, the next launch on the same stream; the kernel boundary writes
+// back the producing kernel's L2 lines and the consumer starts with invalidated caches, so plain stores
+// and loads suffice here (a stream-K fold inside mcv_l2_gemm measured slower: DESIGN.md §7).
 __device__ __forceinline__ void l2_part_store(L2Part* __restrict__ part, int nqPad, int slot, int nEmpty, int q,
                                               const L2Part& p) {
     part[(size_t)slot * nqPad + q] = p;

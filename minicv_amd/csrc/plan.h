@@ -64,6 +64,7 @@ struct Plan {
     DevBuf<float> bbox;       // max |x|, max |y| of the source points (fused fast-path bound)
     DevBuf<double> bb4;       // F / E: max |x1|, |y1|, |x2|, |y2| (packed-fp32 Sampson prefilter bound)
     DevBuf<double> h64;       // homography: each hypothesis' fp64 model (finalize takes the winner's)
+    DevBuf<uint8_t> hgen;     // homography: the split eigen generate's scratch (rotation log of one piece)
     DevBuf<float> pairs;      // paired point layout of the packed sweeps (homography 8, PnP 12 floats per 2)
     DevBuf<uint8_t> one;      // single-hypothesis output record
     DevBuf<double> ptsd;      // essential: double4 normalised correspondences

@@ -14,6 +14,7 @@
 //
 // Built with -ffp-contract=off (see hyp_homography.h): the fp32 error rounds exactly like the
 // host oracle, which is what makes the inlier masks bit-exact.
+#include <algorithm>
 #include <cstdlib>
 #include <cmath>
 #include "mcv_common.h"
@@ -55,6 +56,145 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
         for (int j = 0; j < 8; ++j) mf.h[j] = 0.f;
         models[i] = mf;
         counts[i] = st;
+    }
+}
+
+// The default generate as two passes over the split eigen-solve (round 6; jacobi_eig.h):
+//   mcv_h_gen_aw  lane per hypothesis: sample, subset check, runKernel's normalisation and LtL, then
+//                 JacobiImpl_ on the upper triangle and W only (a 47-double LDS slice per lane, 376 B
+//                 against the one-pass solve's 1016 B: 2.5x the lanes per CU) with every rotation's
+//                 (c, s, k, l) logged to HBM (16 B; SoA by hypothesis, so a wave's log writes and reads
+//                 are contiguous); the sort of W names the eigenvector's row r;
+//   mcv_h_gen_v   lane per hypothesis: V rebuilt from the log (an 81-double slice), row r -> H0, the
+//                 de-normalisation and the fp32 model (the normalisation recomputed from the stored
+//                 sample's four points);
+//   mcv_h_gen_ovf the one-pass solve for the lanes whose rotation count exceeded the log's capacity
+//                 (kEigLogCap; a cfg3 LtL takes 110-157 rotations) — normally none.
+// Every value is computed by the same operations in the same order as the one-pass solve, so the
+// models are the same bits (tests: the whole-range cfg3 counts, the eigen stress test).
+static constexpr int kEigLogCap = 192;
+// 54 x 376 B = 19.8 KB: 8 blocks (two waves per SIMD) per CU. Screen: 40 / 64 / 32-lane blocks (10 / 6 /
+// 13 per CU) 6.6 / 5.7 / 6.7 ms against 5.2 ms of generate per 2^20.
+static constexpr int kHGenAwLanes = 54;
+// pass 2: one column of V per lane (9 lanes per hypothesis, 7 hypotheses per 63-lane block), 4 log
+// loads in flight. Round-6 screen at cfg3 (generate ms per 2^20 hypotheses, pass 1 ~3.7 of it): one
+// lane per hypothesis with one load ahead 5.78, with 8 ahead 5.78; 3 lanes x 3 columns 5.16-5.17 (V
+// transposed 5.06); 9 lanes 4.76-4.81 (8 loads ahead, V transposed, 14 hypotheses per block: the same).
+// Every 9-lane form moves the same 288 LDS bytes per rotation and hypothesis: LDS-bandwidth-bound.
+static constexpr int kHGenVG = 9, kHGenVQ = 7, kHGenVD = 4;
+static constexpr int kHGenOvfBlocks = 64;
+// meta: >= 0 -> rotation count | r << 16 (pass 2 builds the model); kMetaDone: pass 1 wrote the
+// status; kMetaOverflow: mcv_h_gen_ovf solves it
+static constexpr int kMetaDone = -1, kMetaOverflow = -2;
+
+__device__ __forceinline__ void h_store_none(HModelF* models, int* counts, int i, int st) {
+    HModelF mf;
+    for (int j = 0; j < 8; ++j) mf.h[j] = 0.f;   // the zero model (w = 1) keeps the sweep's slot defined
+    models[i] = mf;
+    counts[i] = st;
+}
+
+template <int L>
+__global__ __launch_bounds__(L) void mcv_h_gen_aw(const float* __restrict__ pts4, int N, Sampler smp,
+                                                  int64_t hypBegin, int count, HModelF* __restrict__ models,
+                                                  int* __restrict__ counts, int4* __restrict__ sidx,
+                                                  int* __restrict__ meta, EigRot* __restrict__ log, int logStride,
+                                                  int* __restrict__ ovf, int ovfBase) {
+    const int j = blockIdx.x * L + threadIdx.x;   // lane within the piece
+    if (j >= count) return;
+    const int i = ovfBase + j;                    // hypothesis within the chunk
+    __shared__ double lds[kEigAwWs * L];
+    EigWsLane ws{lds + threadIdx.x * kEigAwWs};
+    float sx[4], sy[4], dx[4], dy[4];
+    int idx[4];
+    double nm[8];
+    int st = 0;
+    if (!h_sample(pts4, N, smp, (uint64_t)(hypBegin + i), sx, sy, dx, dy, idx)) st = kStatusNoSample;
+    else if (!h_norm4(sx, sy, dx, dy, nm) || !h_ltl4(sx, sy, dx, dy, nm, ws)) st = kStatusNoModel;
+    if (st != 0) {
+        h_store_none(models, counts, i, st);
+        meta[j] = kMetaDone;
+        return;
+    }
+    double w[9];
+    int nrot = 0;
+    const int r = eig9_jacobi<EigWsLane, true>(ws, w, 8, &nrot, log + j, logStride, kEigLogCap);
+    sidx[j] = make_int4(idx[0], idx[1], idx[2], idx[3]);
+    if (nrot < 0) {
+        meta[j] = kMetaOverflow;
+        ovf[1 + atomicAdd(ovf, 1)] = i;
+        return;
+    }
+    meta[j] = nrot | (r << 16);
+}
+
+// Pass 2: G lanes per hypothesis (9 / G columns of V each; G = 1 or 3), Q hypotheses per block.
+template <int G, int Q, int D, bool TR = false>
+__global__ __launch_bounds__(G * Q) void mcv_h_gen_v(const float* __restrict__ pts4, int count, int base,
+                                                     const int4* __restrict__ sidx, const int* __restrict__ meta,
+                                                     const EigRot* __restrict__ log, int logStride,
+                                                     HModelF* __restrict__ models, double* __restrict__ h64,
+                                                     int* __restrict__ counts) {
+    constexpr int C = 9 / G;
+    const int h = threadIdx.x / G, g = threadIdx.x - h * G;   // hypothesis of the block, column group
+    const int j = blockIdx.x * Q + h;
+    __shared__ double lds[kEigVWs * Q];
+    EigWsLane v{lds + h * kEigVWs};
+    const int m = j < count ? meta[j] : kMetaDone;
+    if (m >= 0) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[TR ? 9 * (g * C + c) + i : 9 * i + g * C + c] = (i == g * C + c) ? 1.0 : 0.0;
+        eig9_replay_cols<C, D, TR>(v, g * C, log + j, logStride, m & 0xffff);
+    }
+    if constexpr (G > 1) __syncthreads();   // the row's other columns come from the group's other lanes
+    if (m < 0 || g != 0) return;
+    const int i = base + j;
+    const int r = m >> 16;
+    double H0[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) H0[k] = v[TR ? 9 * k + r : 9 * r + k];
+    const int4 id = sidx[j];
+    const int ix[4] = {id.x, id.y, id.z, id.w};
+    float sx[4], sy[4], dx[4], dy[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 q = reinterpret_cast<const float4*>(pts4)[ix[k]];
+        sx[k] = q.x; sy[k] = q.y; dx[k] = q.z; dy[k] = q.w;
+    }
+    double nm[8], H[9];
+    HModelF mf;
+    (void)h_norm4(sx, sy, dx, dy, nm);   // pass 1 accepted this sample: the same values again
+    if (h_from_eig(H0, nm, H) && h_model_f(H, &mf)) {
+        models[i] = mf;
+        for (int k = 0; k < 9; ++k) h64[9 * (int64_t)i + k] = H[k];
+        counts[i] = 0;
+    } else {
+        h_store_none(models, counts, i, kStatusNoModel);
+    }
+}
+
+template <int L>
+__global__ __launch_bounds__(L) void mcv_h_gen_ovf(const float* __restrict__ pts4, int N, Sampler smp,
+                                                   int64_t hypBegin, const int* __restrict__ ovf,
+                                                   HModelF* __restrict__ models, double* __restrict__ h64,
+                                                   int* __restrict__ counts) {
+    __shared__ double lds[kEigWs * L];
+    EigWsLane ws{lds + threadIdx.x * kEigWs};
+    const int n = ovf[0];
+    for (int j = blockIdx.x * L + threadIdx.x; j < n; j += gridDim.x * L) {
+        const int i = ovf[1 + j];
+        double H[9];
+        HModelF mf;
+        const int st = h_hypothesis(pts4, N, smp, (uint64_t)(hypBegin + i), H, &mf, nullptr, ws);
+        if (st == 1) {
+            models[i] = mf;
+            for (int k = 0; k < 9; ++k) h64[9 * (int64_t)i + k] = H[k];
+            counts[i] = 0;
+        } else {
+            h_store_none(models, counts, i, st);
+        }
     }
 }
 
@@ -938,15 +1078,62 @@ struct OpLMErr {   // 1: |r|^2 only
 // ------------------------------------------------------------------------------------------
 // Launchers (host side, called from ransac_host.cpp)
 // ------------------------------------------------------------------------------------------
+template <int L>
+static int h_gen_piece_for() {
+    int d = 0, cus = 0, blocks = 0;
+    (void)hipGetDevice(&d);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mcv_h_gen_aw<L>, L, 0) != hipSuccess || blocks <= 0)
+        blocks = 8;
+    return 2 * cus * blocks * L;
+}
+// Rows of the split generate's scratch per piece: two rounds of mcv_h_gen_aw's resident lanes, so every
+// piece but the last fills the chip evenly (a piece of 2.4 rounds would idle 20 % of its third round).
+int h_gen_piece_lanes() {
+    static const int lanes = h_gen_piece_for<kHGenAwLanes>();
+    return lanes;
+}
+
+size_t h_gen_scratch_bytes(int hypCount) {
+    const size_t piece = (size_t)std::min(hypCount, h_gen_piece_lanes());
+    return piece * kEigLogCap * sizeof(EigRot) + piece * (sizeof(int4) + sizeof(int)) +
+           ((size_t)hypCount + 1) * sizeof(int);
+}
+
 void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin, int hypCount, void* d_models,
-                       double* d_h64, int* d_counts, hipStream_t s, bool fast) {
-    if (fast)
+                       double* d_h64, int* d_counts, hipStream_t s, bool fast, void* d_scratch) {
+    if (fast) {
         hipLaunchKernelGGL(mcv_h_generate<true>, dim3((hypCount + 255) / 256), dim3(256), 0, s, d_pts4, N, smp, hypBegin,
                            hypCount, (HModelF*)d_models, d_h64, d_counts);
-    else   // kEigLanes per block: LDS-bound occupancy, one wave per SIMD (jacobi_eig.h)
+        return;
+    }
+    if (!d_scratch) {   // the one-pass solve: kEigLanes per block, one wave per SIMD (jacobi_eig.h)
         hipLaunchKernelGGL((mcv_h_generate<false, kEigLanes>), dim3((hypCount + kEigLanes - 1) / kEigLanes),
                            dim3(kEigLanes), 0, s, d_pts4, N, smp, hypBegin, hypCount, (HModelF*)d_models, d_h64,
                            d_counts);
+        return;
+    }
+    const int piece = std::min(hypCount, h_gen_piece_lanes());
+    char* b = (char*)d_scratch;
+    EigRot* log = (EigRot*)b;
+    b += (size_t)piece * kEigLogCap * sizeof(EigRot);
+    int4* sidx = (int4*)b;
+    b += (size_t)piece * sizeof(int4);
+    int* meta = (int*)b;
+    b += (size_t)piece * sizeof(int);
+    int* ovf = (int*)b;
+    (void)hipMemsetAsync(ovf, 0, sizeof(int), s);   // errors surface at the caller's hipGetLastError
+    for (int base = 0; base < hypCount; base += piece) {
+        const int cnt = std::min(piece, hypCount - base);
+        hipLaunchKernelGGL(mcv_h_gen_aw<kHGenAwLanes>, dim3((cnt + kHGenAwLanes - 1) / kHGenAwLanes),
+                           dim3(kHGenAwLanes), 0, s, d_pts4, N, smp, hypBegin, cnt, (HModelF*)d_models, d_counts, sidx,
+                           meta, log, piece, ovf, base);
+        hipLaunchKernelGGL((mcv_h_gen_v<kHGenVG, kHGenVQ, kHGenVD>), dim3((cnt + kHGenVQ - 1) / kHGenVQ),
+                           dim3(kHGenVG * kHGenVQ), 0, s, d_pts4, cnt, base, sidx, meta, log, piece, (HModelF*)d_models,
+                           d_h64, d_counts);
+    }
+    hipLaunchKernelGGL(mcv_h_gen_ovf<kEigLanes>, dim3(kHGenOvfBlocks), dim3(kEigLanes), 0, s, d_pts4, N, smp, hypBegin,
+                       ovf, (HModelF*)d_models, d_h64, d_counts);
 }
 
 void launch_h_one(const float* d_pts4, int N, Sampler smp, int64_t hyp, HOneOut* d_out, hipStream_t s, bool fast) {
@@ -1104,3 +1291,4 @@ void h_reduce_lm(const float* d_pts4, int N, const uint8_t* d_mask, const double
 }
 
 }  // namespace mcv
+

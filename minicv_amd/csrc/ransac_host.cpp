@@ -355,8 +355,9 @@ void evaluate_chunk(Plan& P, const void* d_ptsv, int N, const RansacConfig& cfg,
         const Sampler smp = P.sampler(cfg);
         {
             ProfScope pg("h_generate", s);
+            if (!fast_minimal(cfg)) P.hgen.ensure(h_gen_scratch_bytes(hypCount));
             launch_h_generate(d_pts, N, smp, hypBegin, hypCount, P.models.p, P.h64.p, d_counts, s,
-                              fast_minimal(cfg));
+                              fast_minimal(cfg), fast_minimal(cfg) ? nullptr : P.hgen.p);
         }
         // the winner's models can come straight from this chunk's buffers (h_finalize)
         mark_chunk(P, hypBegin, hypCount, smp, d_pts, N, fast_minimal(cfg) ? 21 : 20, s);
