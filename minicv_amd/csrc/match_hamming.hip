@@ -243,8 +243,10 @@ __global__ __launch_bounds__(256) void mcv_hamming_merge(const uint2* __restrict
 //
 // The +-64 bytes are never stored: word w of a descriptor expands to the 32 bytes [32 w, 32 w + 32),
 // dword d of them holding bits d, d + 8, d + 16, d + 24 (one shift and one v_and_or_b32 per dword).
-// Queries are expanded once into their VGPR-resident B fragments; the block's train tiles are loaded
-// packed (32 B per 256-bit row) and expanded into the LDS tile. Lane l (row / column l & 31, half
+// Queries are expanded once into their VGPR-resident B fragments; the train tiles are loaded packed
+// (16 B of a 256-bit row per lane) and each A fragment is expanded in registers right before its MFMAs
+// (round 6: no LDS tile, no per-tile barrier; the round-5 LDS staging shared the expansion between a
+// block's four waves and measured the same 31-32 us at cfg2). Lane l (row / column l & 31, half
 // h = l >> 5) takes bytes [16 KS h + 16 s, + 16) of its row at k step s (word KS h / 2 + s / 2,
 // dwords 4 (s & 1) .. + 3); both operands use the same map.
 template <bool NEG>
@@ -257,9 +259,9 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 static constexpr int kHamChunkRows = 4096;   // j' < 4096 < 8192: the key's index field
 
-// Block = WPB waves x QT query tiles of 32 (VGPR-resident B fragments); the block's train tiles (32
-// rows x Kp bytes, expanded from the packed rows) are staged in LDS (double buffer, 16-byte row pad:
-// conflict-free ds_read_b128) and each A fragment read from LDS feeds QT MFMAs.
+// Block = WPB waves x QT query tiles of 32 (VGPR-resident B fragments); the waves of a block walk the
+// same train tiles (their 1 KB loads hit L1 after the first) and each expanded A fragment feeds QT
+// MFMAs.
 // Partition (round 5, stream-K style): the (query block, train tile) steps in query-block-major order
 // are cut into gridDim.x equal contiguous ranges (at most 128 tiles, the key's 4096-row index field),
 // one per block, so every block does the same work to a tile (the (query block, chunk) grid it
@@ -274,21 +276,16 @@ static constexpr int kHamChunkRows = 4096;   // j' < 4096 < 8192: the key's inde
 // stale in an L2), each block waits for its stores to complete (s_waitcnt vmcnt(0), a compiler barrier
 // too) before its agent-scope arrival add, and the last block's loads are issued after that add returns.
 template <int W, int QT, int WPB, int SUB>
-__global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
+__global__ __launch_bounds__(64 * WPB, W == 8 && QT <= 2 ? 3 : 2) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
                                                              const uint32_t* __restrict__ t, int nt, int ntTiles,
                                                              int qblocks, uint2* __restrict__ part,
                                                              unsigned* __restrict__ arrivals, int* __restrict__ oIdx,
                                                              int* __restrict__ oDist, int* __restrict__ oIdx2,
                                                              int* __restrict__ oDist2) {
-    static_assert(QT * 32 * WPB == 64 * WPB, "the fold takes one query per thread");
+    static_assert(QT % 2 == 0 || QT == 1, "the fold takes QT / 2 queries per thread");
     static_assert(SUB == 1, "segments are counted in 32-row tiles");
     constexpr int KS = W;                  // k steps of 32 bytes (Kp = 32 W)
-    constexpr int RB = 32 * KS;            // bytes per expanded row
-    constexpr int RBP = RB + 16;           // LDS row stride
-    constexpr int NT = 64 * WPB;
-    constexpr int TRW = 32 * SUB;          // train rows per staged tile (SUB MFMA row tiles)
-    constexpr int PER = (TRW * W + NT - 1) / NT;   // packed words of a tile per thread
-    __shared__ __attribute__((aligned(16))) int8_t lt[2][TRW * RBP];
+    constexpr int RB = 32 * KS;            // bytes per expanded row (Kp)
     __shared__ int lastBlock;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
@@ -305,13 +302,21 @@ __global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(con
         const int slot = blk - j0, nseg = j1 - j0 + 1;
         const int q0 = (bx * WPB + wave) * QT * 32;
         i32x4 bq[QT][KS];
+        uint4 qw[QT][W / 8];   // the lane's half query row: 16-byte loads, all issued before the expansion
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
             const int qi = min(q0 + 32 * qt + col, nq - 1);
-            const uint32_t* qr = q + (size_t)qi * W + (KS / 2) * h;
+            const uint4* qr = reinterpret_cast<const uint4*>(q + (size_t)qi * W + (KS / 2) * h);
+#pragma unroll
+            for (int v = 0; v < W / 8; ++v) qw[qt][v] = qr[v];
+        }
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
 #pragma unroll
             for (int s2 = 0; s2 < KS / 2; ++s2) {
-                const uint32_t wd = ~qr[s2];
+                const uint4 u4 = qw[qt][s2 >> 2];
+                const int wi = s2 & 3;
+                const uint32_t wd = ~(wi == 0 ? u4.x : wi == 1 ? u4.y : wi == 2 ? u4.z : u4.w);
                 bq[qt][2 * s2] = i32x4{ham_expand_dword<true>(wd, 0), ham_expand_dword<true>(wd, 1),
                                        ham_expand_dword<true>(wd, 2), ham_expand_dword<true>(wd, 3)};
                 bq[qt][2 * s2 + 1] = i32x4{ham_expand_dword<true>(wd, 4), ham_expand_dword<true>(wd, 5),
@@ -321,67 +326,47 @@ __global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(con
         uint32_t m1[QT], m2[QT], n1[QT], n2[QT];
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = n1[qt] = n2[qt] = 0xFFFFFFFFu;
-        auto gload = [&](int tl, uint32_t (&st)[PER]) {
+        // the lane's half of its train row (words [W h / 2, W h / 2 + W / 2): 16 B at W = 8) straight
+        // from global memory, the next tile's in flight under this tile's MFMAs (the block's four waves
+        // read the same 1 KB tile: L1 hits after the first)
+        constexpr int NV = W / 8;   // uint4 per lane per tile
+        auto tload = [&](int tl, uint4 (&dst)[NV]) {
+            const int row = min(tl * 32 + col, nt - 1);
+            const uint4* src = reinterpret_cast<const uint4*>(t + (size_t)row * W + (W / 2) * h);
 #pragma unroll
-            for (int p = 0; p < PER; ++p) {
-                const int id = threadIdx.x + NT * p;
-                if (id < TRW * W) {
-                    const int row = min(tl * TRW + id / W, nt - 1);
-                    st[p] = t[(size_t)row * W + id % W];
-                }
-            }
-        };
-        auto lstore = [&](int buf, const uint32_t (&st)[PER]) {
-#pragma unroll
-            for (int p = 0; p < PER; ++p) {
-                const int id = threadIdx.x + NT * p;
-                if (id < TRW * W) {
-                    const uint32_t v = st[p];
-                    int8_t* dst = &lt[buf][(id / W) * RBP + 32 * (id % W)];
-                    *reinterpret_cast<i32x4*>(dst) = i32x4{ham_expand_dword<false>(v, 0), ham_expand_dword<false>(v, 1),
-                                                          ham_expand_dword<false>(v, 2), ham_expand_dword<false>(v, 3)};
-                    *reinterpret_cast<i32x4*>(dst + 16) = i32x4{ham_expand_dword<false>(v, 4), ham_expand_dword<false>(v, 5),
-                                                               ham_expand_dword<false>(v, 6), ham_expand_dword<false>(v, 7)};
-                }
-            }
+            for (int v = 0; v < NV; ++v) dst[v] = src[v];
         };
         // accumulator start values: 4096 Kp + j' (rows past nt: 2^30, which ends above every real key)
         i32x16 c0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) c0[i] = 4096 * RB + (i & 3) + 8 * (i >> 2) + 4 * h;
-        uint32_t st[PER];
-        gload(tBegin, st);
-        lstore(0, st);
-        gload(min(tBegin + 1, tEnd - 1), st);
-        __syncthreads();
+        uint4 tw[NV], nx[NV];
+        tload(tBegin, tw);
         for (int tl = tBegin; tl < tEnd; ++tl) {
-            const int buf = (tl - tBegin) & 1;
+            tload(min(tl + 1, tEnd - 1), nx);
             i32x16 cs = c0;
-            if (__builtin_expect(tl * TRW + 32 > nt, 0)) {   // rows past nt (block-uniform)
+            if (__builtin_expect(tl * 32 + 32 > nt, 0)) {   // rows past nt (wave-uniform)
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
-                    if (tl * TRW + (i & 3) + 8 * (i >> 2) + 4 * h >= nt) cs[i] = 1 << 30;
+                    if (tl * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= nt) cs[i] = 1 << 30;
                 asm volatile("" : "+v"(cs));   // a branch once per launch, not 32 selects per tile
             }
-            // priority 0 for the MFMAs, 1 for the staging and top-2 updates (as mcv_l2_gemm's epilogue;
-            // round 5, same box: 31.9 vs 32.1 us per step)
+            // priority 0 for the MFMAs, 1 for the expansion and top-2 updates (as mcv_l2_gemm's epilogue)
             __builtin_amdgcn_s_setprio(0);
             i32x16 acc[QT];
-            const int8_t* ar = &lt[buf][col * RBP + 16 * KS * h];
-            {
-                const i32x4 a = *reinterpret_cast<const i32x4*>(ar);
 #pragma unroll
-                for (int qt = 0; qt < QT; ++qt) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][0], cs, 0, 0, 0);
-            }
+            for (int s = 0; s < KS; ++s) {
+                const uint4 u4 = tw[s >> 3];
+                const int wi = (s >> 1) & 3;
+                const uint32_t w = wi == 0 ? u4.x : wi == 1 ? u4.y : wi == 2 ? u4.z : u4.w;
+                const int d0 = 4 * (s & 1);
+                const i32x4 a = i32x4{ham_expand_dword<false>(w, d0), ham_expand_dword<false>(w, d0 + 1),
+                                      ham_expand_dword<false>(w, d0 + 2), ham_expand_dword<false>(w, d0 + 3)};
 #pragma unroll
-            for (int s = 1; s < KS; ++s) {
-                const i32x4 a = *reinterpret_cast<const i32x4*>(ar + 16 * s);
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][s], acc[qt], 0, 0, 0);
+                for (int qt = 0; qt < QT; ++qt)
+                    acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][s], s == 0 ? cs : acc[qt], 0, 0, 0);
             }
             __builtin_amdgcn_s_setprio(1);
-            lstore(buf ^ 1, st);
-            gload(min(tl + 2, tEnd - 1), st);
             // two independent top-2 chains per query tile (rows i < 8 and i >= 8), merged at the end:
             // the med3 / min updates of one chain depend on each other, two chains overlap
 #pragma unroll
@@ -393,10 +378,11 @@ __global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(con
                 }
 #pragma unroll
             for (int i = 0; i < 16; ++i) c0[i] += 32;
-            __syncthreads();
+#pragma unroll
+            for (int v = 0; v < NV; ++v) tw[v] = nx[v];
         }
         // lanes l and l + 32 hold the same query (other rows): merge, then the popcount form's keys
-        const uint32_t base = (uint32_t)tBegin * TRW;
+        const uint32_t base = (uint32_t)tBegin * 32;
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
             top2_push(m1[qt], m2[qt], n1[qt]);   // segment-local keys: the index field keeps them distinct
@@ -434,23 +420,36 @@ __global__ __launch_bounds__(64 * WPB, W == 8 ? 3 : 2) void mcv_hamming_mfma(con
                         (unsigned)(nseg - 1);
         __syncthreads();
         if (lastBlock) {
-            const int qm = bx * (QT * 32 * WPB) + threadIdx.x;
-            if (qm < nq) {
+          for (int qx = 0; qx < (QT + 1) / 2; ++qx) {
+            const int qm = bx * (QT * 32 * WPB) + threadIdx.x + 64 * WPB * qx;
+            if (qm < nq && (QT > 1 || threadIdx.x < 32 * WPB)) {
                 uint32_t a1 = 0xFFFFFFFFu, a2 = 0xFFFFFFFFu;
-#pragma unroll 8
-                for (int c = 0; c < nseg; ++c) {
-                    const uint64_t pv = __hip_atomic_load(reinterpret_cast<const uint64_t*>(part) + (size_t)c * nq + qm,
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint2 pc = make_uint2((uint32_t)pv, (uint32_t)(pv >> 32));
-                    a2 = min(a2, max(a1, pc.x));
-                    a1 = min(a1, pc.x);
-                    a2 = min(a2, pc.y);
+                // every partial of a batch of FB in flight before the first fold: the sc1 loads come from
+                // the coherent level (~1-2 us each), and a query block spans ~19 segments at cfg2 (~77
+                // for a 2500-query shard); eight per batch made the fold a chain of 3-10 round trips
+                constexpr int FB = 24;
+                for (int c0 = 0; c0 < nseg; c0 += FB) {
+                    uint64_t pv[FB];
+#pragma unroll
+                    for (int u = 0; u < FB; ++u)
+                        pv[u] = c0 + u < nseg ? __hip_atomic_load(reinterpret_cast<const uint64_t*>(part) +
+                                                                      (size_t)(c0 + u) * nq + qm,
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                              : ~0ull;
+#pragma unroll
+                    for (int u = 0; u < FB; ++u) {
+                        const uint2 pc = make_uint2((uint32_t)pv[u], (uint32_t)(pv[u] >> 32));
+                        a2 = min(a2, max(a1, pc.x));
+                        a1 = min(a1, pc.x);
+                        a2 = min(a2, pc.y);
+                    }
                 }
                 oIdx[qm] = a1 == 0xFFFFFFFFu ? -1 : (int)(a1 & kIdxMask);
                 oDist[qm] = a1 == 0xFFFFFFFFu ? INT_MAX : (int)(a1 >> kIdxBits);
                 if (oIdx2) oIdx2[qm] = a2 == 0xFFFFFFFFu ? -1 : (int)(a2 & kIdxMask);
                 if (oDist2) oDist2[qm] = a2 == 0xFFFFFFFFu ? INT_MAX : (int)(a2 >> kIdxBits);
             }
+          }
             if (threadIdx.x == 0) arrivals[bx] = 0u;   // re-armed for the next launch (ordered by the kernel boundary)
         }
         pos = segEnd;
@@ -480,6 +479,45 @@ struct HammingWork {
     StreamFence fence;   // calls on different streams take turns on these buffers
 };
 
+// The GEMM form's launch: WPB waves per block, QT query tiles per wave; stream-K ranges over the resident
+// blocks (occupancy of this instantiation).
+template <int WPB, int QT>
+static void launch_ham_gemm(HammingWork& wk, int W, const uint32_t* q, int nq, const uint32_t* t, int nt, int* d_idx,
+                            int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s) {
+    constexpr int SUB = 1;
+    const int qblocks = (nq + 32 * QT * WPB - 1) / (32 * QT * WPB);
+    const int ntTiles = (nt + 32 * SUB - 1) / (32 * SUB);
+    static const int cus = [] {
+        int d = 0, n = 0;
+        (void)hipGetDevice(&d);
+        return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
+    }();
+    auto kern = W == 8 ? mcv_hamming_mfma<8, QT, WPB, SUB> : mcv_hamming_mfma<16, QT, WPB, SUB>;
+    int perCu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, kern, 64 * WPB, 0) != hipSuccess || perCu <= 0) perCu = 1;
+    const int64_t Wt = (int64_t)qblocks * ntTiles;
+    // equal ranges of the (query block, tile) steps over the resident blocks, at most 128 tiles each
+    // (the key's index field) and at least 4 (the per-range query expansion and fold)
+    int64_t B = std::min<int64_t>((int64_t)perCu * cus, (Wt + 3) / 4);
+    B = std::max<int64_t>(B, (Wt + kHamChunkRows / 32 - 1) / (kHamChunkRows / 32));
+    B = std::max<int64_t>(1, std::min(B, Wt));
+    if (B > INT_MAX) fail("cvMatchHamming: %lld ranges", (long long)B);
+    int maxSeg = 1;
+    for (int64_t x = 0; x < qblocks; ++x) {
+        const int64_t j0 = ((x * ntTiles + 1) * B - 1) / Wt, j1 = ((x + 1) * ntTiles * B - 1) / Wt;
+        maxSeg = std::max(maxSeg, (int)(j1 - j0 + 1));
+    }
+    wk.part.ensure((size_t)maxSeg * nq);
+    if (wk.arrivalsZeroed < (size_t)qblocks) {
+        wk.arrivals.ensure((size_t)qblocks);
+        MCV_HIP(hipMemsetAsync(wk.arrivals.p, 0, wk.arrivals.n * sizeof(unsigned), s));
+        wk.arrivalsZeroed = wk.arrivals.n;
+    }
+    ProfScope ps("hamming", s);
+    hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, qblocks, wk.part.p,
+                       wk.arrivals.p, d_idx, d_dist, d_idx2, d_dist2);
+}
+
 int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc, int* d_idx,
                          int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s, int form) {
     if (bytesPerDesc < 1 || bytesPerDesc > 64) fail("cvMatchHamming: bytesPerDesc %d outside [1, 64]", bytesPerDesc);
@@ -494,7 +532,8 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     const int W = bytesPerDesc <= 32 ? 8 : 16;
     const uint32_t* q = (const uint32_t*)d_q;
     const uint32_t* t = (const uint32_t*)d_t;
-    const bool aligned = (((uintptr_t)d_q | (uintptr_t)d_t) & 3) == 0;
+    // the GEMM form reads each lane's half train row as 16-byte vectors
+    const bool aligned = (((uintptr_t)d_q | (uintptr_t)d_t) & 15) == 0;
     if (bytesPerDesc != 4 * W || !aligned) {
         wk.qpack.ensure((size_t)nq * W);
         wk.tpack.ensure((size_t)(nt > 0 ? nt : 1) * W);
@@ -508,44 +547,12 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
     }
     // form 1: the XOR / popcount sweep (mcvMatchHammingDeviceForm); 0: the int8 GEMM (default)
     if (form == kHammingFormGemm && nt > 0) {
-        // 4 waves per block, 2 query tiles per wave, one 32-row MFMA tile per staged train tile (cfg2
-        // screens, round 4: 1 query tile, 2-tile staging 33.6 vs 32.1 us), one block per resident slot
-        // (3 per CU at 256-bit descriptors, 2 at 512-bit: the register budget). Round 5, the same box
-        // alternating at cfg2: the stream-K ranges 32.4 us per step against 35.0 us for round 4's
-        // (query block, chunk) grid of ~8192 waves; two blocks per slot 39.2 us.
-        constexpr int WPB = 4, QT = 2, SUB = 1;
-        const int qblocks = (nq + 32 * QT * WPB - 1) / (32 * QT * WPB);
-        const int ntTiles = (nt + 32 * SUB - 1) / (32 * SUB);
-        static const int cus = [] {
-            int d = 0, n = 0;
-            (void)hipGetDevice(&d);
-            return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
-        }();
-        const int perCu = W == 8 ? 3 : 2;   // the kernel's __launch_bounds__
-        const int64_t Wt = (int64_t)qblocks * ntTiles;
-        // equal ranges of the (query block, tile) steps over the resident blocks, at most 128 tiles each
-        // (the key's index field) and at least 4 (the per-range query expansion and fold)
-        int64_t B = std::min<int64_t>((int64_t)perCu * cus, (Wt + 3) / 4);
-        B = std::max<int64_t>(B, (Wt + kHamChunkRows / 32 - 1) / (kHamChunkRows / 32));
-        B = std::max<int64_t>(1, std::min(B, Wt));
-        if (B > INT_MAX) fail("cvMatchHamming: %lld ranges", (long long)B);
-        int maxSeg = 1;
-        for (int64_t x = 0; x < qblocks; ++x) {
-            const int64_t j0 = ((x * ntTiles + 1) * B - 1) / Wt, j1 = ((x + 1) * ntTiles * B - 1) / Wt;
-            maxSeg = std::max(maxSeg, (int)(j1 - j0 + 1));
-        }
-        wk.part.ensure((size_t)maxSeg * nq);
-        if (wk.arrivalsZeroed < (size_t)qblocks) {
-            wk.arrivals.ensure((size_t)qblocks);
-            MCV_HIP(hipMemsetAsync(wk.arrivals.p, 0, wk.arrivals.n * sizeof(unsigned), s));
-            wk.arrivalsZeroed = wk.arrivals.n;
-        }
-        {
-            ProfScope ps("hamming", s);
-            hipLaunchKernelGGL((W == 8 ? mcv_hamming_mfma<8, QT, WPB, SUB> : mcv_hamming_mfma<16, QT, WPB, SUB>),
-                               dim3((unsigned)B), dim3(64 * WPB), 0, s, q, nq, t, nt, ntTiles, qblocks, wk.part.p,
-                               wk.arrivals.p, d_idx, d_dist, d_idx2, d_dist2);
-        }
+        // 4 waves per block, 2 query tiles per wave (cfg2 screens: round 4, 1 query tile 33.6 vs 32.1 us;
+        // round 6 without the LDS staging, 10k x 10k / 1250 x 10k / 10k x 40k: 2 waves per block 29.7 /
+        // 18.7 / 87.6 us, 8 waves 28.3 / 15.7 / 91.7, against 28.1-31.4 / 14.9-15.3 / 87.3-99.4 for 4;
+        // 4 query tiles per wave spill at 256 VGPRs), one block per resident slot (3 per CU at 256-bit
+        // descriptors, 2 at 512-bit).
+        launch_ham_gemm<4, 2>(wk, W, q, nq, t, nt, d_idx, d_dist, d_idx2, d_dist2, s);
         MCV_HIP(hipGetLastError());
         wk.fence.leave(s);
         return nq;
@@ -575,3 +582,4 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
 }
 
 }  // namespace mcv
+

@@ -191,7 +191,10 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
     const int lane = threadIdx.x & 63;
     const int total = __builtin_amdgcn_readfirstlane(*nDense);
     const int m0 = wave * K;
-    if (m0 >= total) return;
+    __shared__ int blockCounts[4 * K];
+    // a block's waves leave together (the count staging's barrier): a wave past the list stages nothing
+    if ((int)((bx * 256u) >> 6) * K >= total) return;   // the whole block is past the list
+    const bool live = m0 < total;
     const double B[4] = {bb[0], bb[1], bb[2], bb[3]};
     bool valid[K];
 #pragma unroll
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
     for (int k = 0; k < K; ++k) cnt[k] = 0;
     const int step = 64 * P;
     const int p0 = (int)by * chunk;
-    const int p1 = min(N, p0 + chunk);
+    const int p1 = live ? min(N, p0 + chunk) : p0;   // a wave past the list sweeps nothing
     const int nFull = p0 + (p1 - p0) / step * step;
     for (int base = p0; base < nFull; base += step) {
         float4 q[P];
@@ -252,16 +255,23 @@ __global__ __launch_bounds__(256) void mcv_e_verify_pk(const float4* __restrict_
         };
         spk_sweep_point<KP>(pr, q, v, cut.L32, cut.H32, kind, thr2, f64, x64, cnt);
     }
-    // lane k writes model k's count (one store / one atomic instruction per wave)
+    // lane k stages model k's count (-1: no model), then the block's 4 K dense models go out from one
+    // instruction (F's round-5 staging): their slots lie in one or two appending waves' hypothesis
+    // ranges, so the block writes a few cache lines instead of one partial line per wave
     int mine = 0;
     bool mv = false;
 #pragma unroll
     for (int k = 0; k < K; ++k)
         if (lane == k) mine = (int)cnt[k], mv = valid[k];
-    if (lane < K && mv) {
-        const int slot = denseSlot[m0 + lane];
-        if (gridDim.y == 1) counts[slot] = mine;
-        else if (mine) atomicAdd(counts + slot, mine);
+    if (lane < K) blockCounts[(threadIdx.x >> 6) * K + lane] = mv ? mine : -1;
+    __syncthreads();
+    if (threadIdx.x < 4 * K) {
+        const int v = blockCounts[threadIdx.x];
+        if (v >= 0) {
+            const int slot = denseSlot[(wave - (int)(threadIdx.x >> 6)) * K + (int)threadIdx.x];
+            if (gridDim.y == 1) counts[slot] = v;
+            else if (v) atomicAdd(counts + slot, v);
+        }
     }
 }
 
@@ -378,9 +388,14 @@ static void launch_e_verify_pk_kp(const float4* p32, const double4* p, int N, co
     // 12.16 ms, 16384-point chunks 12.25, 32768 12.04, 50000 11.92). At 2^20 hypotheses one chunk writes
     // 62 instead of 284 MB of partial counts per launch but streams the whole 4.8 MB point set through
     // each XCD's 4 MB L2 (24.8 GB of fetches per launch against 0.7 GB; the same 223 ms a step): kept at two.
+    // Round 6: one chunk once the model waves alone fill >= 32 rounds of the chip (2^20 hypotheses:
+    // ~470k waves) — the counts are then plain stores of the block-staged slots: WRITE_SIZE per launch
+    // 97.6 -> 41.2 MiB (two chunks' atomics before), the same verify time (one box, alternating: 301.1 /
+    // 301.7 ms against 300.3 / 300.5 with two chunks, scripts/exp/e_chunks.py's workload); smaller
+    // calls keep the chunks for their last round's tail.
     constexpr int minChunk = 50000;
     const int step = 64 * P;
-    int chunks = std::max(1, N / minChunk);
+    int chunks = (int64_t)blocks * 4 >= 32 * 1024 ? 1 : std::max(1, N / minChunk);
     int chunk = (N + chunks - 1) / chunks;
     chunk = (chunk + step - 1) / step * step;
     chunks = std::max(1, (N + chunk - 1) / chunk);
@@ -434,3 +449,4 @@ void launch_e_cheirality(const double* d_pts4, int N, const uint8_t* d_mask, con
 
 
 }  // namespace mcv
+
