@@ -139,7 +139,9 @@ struct Ap3pOut {
 };
 void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_pts, hipStream_t s);
 // fast (MCV_FLAG_FAST_MINIMAL): the AP3P kernel's real-root-finder quartic instead of the reference's Ferrari
-// d_epnpScratch: kEpnpSplitDoubles x hypCount doubles (EPnP's split generate; unused by AP3P)
+// d_epnpScratch: kEpnpSplitDoubles x min(hypCount, kEpnpPiece) doubles (EPnP's split generate runs over
+// sub-ranges of kEpnpPiece hypotheses; unused by AP3P)
+static const int kEpnpPiece = 1 << 18;
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
                          bool epnp, void* d_models, int* d_counts, double* d_epnpScratch, hipStream_t s,
                          bool fast = false);

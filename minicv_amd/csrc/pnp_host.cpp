@@ -125,7 +125,7 @@ bool pnp_cfg_epnp(const RansacConfig& cfg) { return pnp_kind_epnp(pnp_kind(cfg.p
 // complex-pow branch runs glibc's clog / exp / cos / atan2 as restated in glibc_math.h).
 static void pnp_generate_exact(Plan& P, const void* d_pts, int N, const Sampler& smp, int64_t hypBegin, int hypCount,
                                bool epnp, bool fast, void* d_models, int* d_counts, hipStream_t s) {
-    if (epnp) P.escratch.ensure((size_t)hypCount * kEpnpSplitDoubles);
+    if (epnp) P.escratch.ensure((size_t)std::min(hypCount, kEpnpPiece) * kEpnpSplitDoubles);
     launch_pnp_generate(d_pts, N, P.pnpCam, smp, hypBegin, hypCount, epnp, d_models, d_counts,
                         epnp ? P.escratch.p : nullptr, s, fast);
     MCV_HIP(hipGetLastError());

@@ -789,20 +789,24 @@ void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler s
                            to_cam(cam8), smp, hypBegin, hypCount, (PnpPose*)d_models, d_counts, fast);
         return;
     }
-    const int64_t S = hypCount;
+    // sub-ranges of at most kEpnpPiece hypotheses reuse one scratch of kEpnpPiece x kEpnpSplitDoubles
+    // doubles (610 MB; a whole 2^20 chunk's took 2.4 GB per plan and device)
+    const PnpCamera cam = to_cam(cam8);
+    const int piece = std::min(hypCount, kEpnpPiece);
+    const int64_t S = piece;
     const EpnpSplit X{d_epnpScratch, d_epnpScratch + kMtmSums * S, d_epnpScratch + (kMtmSums + kEpnpCtx) * S,
                       d_epnpScratch + (kMtmSums + kEpnpCtx + 144) * S, S};
-    const PnpCamera cam = to_cam(cam8);
-    hipLaunchKernelGGL(mcv_epnp_split_mtm, dim3((hypCount + 255) / 256), dim3(256), 0, s, (const PnpPoint*)d_pts, N,
-                       cam, smp, hypBegin, hypCount, X, d_counts);
-    hipLaunchKernelGGL(mcv_epnp_split_sweeps, dim3((hypCount + 63) / 64), dim3(64), 0, s, X,
-                       (const int*)d_counts, hypCount);
-    hipLaunchKernelGGL(mcv_epnp_split_tail, dim3((hypCount + 255) / 256), dim3(256), 0, s, X, (const int*)d_counts,
-                       hypCount);
-    hipLaunchKernelGGL(mcv_epnp_split_betas, dim3((hypCount + 63) / 64), dim3(64), 0, s, X, (const int*)d_counts,
-                       hypCount);
-    hipLaunchKernelGGL(mcv_epnp_split_pose, dim3((hypCount + 255) / 256), dim3(256), 0, s, cam, X,
-                       (PnpPose*)d_models, (const int*)d_counts, hypCount);
+    for (int off = 0; off < hypCount; off += piece) {
+        const int n = std::min(piece, hypCount - off);
+        int* cnt = d_counts + off;
+        PnpPose* mdl = (PnpPose*)d_models + off;
+        hipLaunchKernelGGL(mcv_epnp_split_mtm, dim3((n + 255) / 256), dim3(256), 0, s, (const PnpPoint*)d_pts, N, cam,
+                           smp, hypBegin + off, n, X, cnt);
+        hipLaunchKernelGGL(mcv_epnp_split_sweeps, dim3((n + 63) / 64), dim3(64), 0, s, X, (const int*)cnt, n);
+        hipLaunchKernelGGL(mcv_epnp_split_tail, dim3((n + 255) / 256), dim3(256), 0, s, X, (const int*)cnt, n);
+        hipLaunchKernelGGL(mcv_epnp_split_betas, dim3((n + 63) / 64), dim3(64), 0, s, X, (const int*)cnt, n);
+        hipLaunchKernelGGL(mcv_epnp_split_pose, dim3((n + 255) / 256), dim3(256), 0, s, cam, X, mdl, (const int*)cnt, n);
+    }
 }
 
 // Grid of a pose-wave x point-chunk sweep: waves x chunks >= ~8 waves per SIMD, chunks >= 2048
