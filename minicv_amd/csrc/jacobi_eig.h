@@ -33,11 +33,12 @@ namespace mcv {
 // [0, 36) strict upper triangle, [36, 45) W, [45, 126) V, 126 = a junk slot (the rotation's
 // branch-free form sends the two skipped indices there).
 static constexpr int kEigA = 0, kEigW = 36, kEigV = 45, kEigJunk = 126, kEigWs = 127;
-// The split solve (eig9_jacobi<WS, true> + eig9_replay): pass 1 keeps only the upper triangle, W and
-// the junk slot (46 doubles, odd lane stride 47: 376 B per lane instead of 1016) and logs each
+// The split solve (eig9_jacobi<WS, true> + eig9_replay): pass 1 keeps only the upper triangle and W
+// (45 doubles, an odd lane stride: 360 B per lane instead of 1016; it runs the 7-pair lane-slice form,
+// which needs no junk slot) and logs each
 // rotation; pass 2 replays the log on V alone (81 doubles, odd stride). Same operations on the same
 // values in the same order as the one-pass solve, so the same bits.
-static constexpr int kEigAwJunk = 45, kEigAwWs = 47, kEigVWs = 81;
+static constexpr int kEigAwWs = 45, kEigVWs = 81;
 // One logged rotation: c (JacobiImpl_'s c = t / hypot(p, t) lies in [1/sqrt(2), 1], so its bits 62..53
 // are always 0b0111111111 and bit 63 is 0: bits 63..53 carry (k << 4) | l instead) and s.
 struct alignas(16) EigRot {
@@ -85,32 +86,34 @@ struct EigWsLane {
     MCV_HD double& operator[](int e) { return p[e]; }
 };
 
-// Byte offsets of the rotated pairs per pivot: row tri(k, l) holds, for i = 0..8, the elements
-// (A(i|k), A(i|l)) of the packed upper triangle as 8 e (the junk slot for i = k, l) in the low / high
-// 16 bits of word i. The GPU lane-slice solver reads one 48-byte row per rotation (constant memory,
-// L1-resident: 1.7 KB) instead of selecting the 18 elements with ~100 integer ops.
+// Byte offsets of the rotated pairs per pivot: row tri(k, l) holds in word j (j < 7) the elements
+// (A(i|k), A(i|l)) of the packed upper triangle as 8 e in the low / high 16 bits, for i = i_j, the j-th
+// index outside {k, l} in increasing order (i_j = j + (j >= k) + (j >= l - 1)). The GPU lane-slice
+// solver reads one 32-byte row per rotation (constant memory, L1-resident) instead of selecting the
+// elements with ~100 integer ops, and rotates and rescans these 7 pairs only (round 6; before, 9 pairs
+// with the two at i = k, l sent to a junk slot, whose (0, 0) rotated to (+0, +0) and never won a
+// rescan: the same result with 12 more fp64 operations, 4 more LDS accesses and two more rescan steps
+// per rotation). The host / generic path keeps the 9-pair branch-free form.
 struct EigPairLut {
-    uint32_t w[36][12];
+    uint32_t w[36][8];
 };
-constexpr EigPairLut eig_make_pair_lut(int junk) {
+constexpr EigPairLut eig_make_pair_lut7() {
     EigPairLut t{};
     for (int k = 0; k < 9; ++k)
         for (int l = k + 1; l < 9; ++l) {
             const int row = ((k * (15 - k)) >> 1) - 1 + l;
+            int j = 0;
             for (int i = 0; i < 9; ++i) {
-                int e0 = junk, e1 = junk;
-                if (i != k && i != l) {
-                    e0 = i < k ? ((i * (15 - i)) >> 1) - 1 + k : ((k * (15 - k)) >> 1) - 1 + i;
-                    e1 = i < l ? ((i * (15 - i)) >> 1) - 1 + l : ((l * (15 - l)) >> 1) - 1 + i;
-                }
-                t.w[row][i] = (uint32_t)(8 * e0) | ((uint32_t)(8 * e1) << 16);
+                if (i == k || i == l) continue;
+                const int e0 = i < k ? ((i * (15 - i)) >> 1) - 1 + k : ((k * (15 - k)) >> 1) - 1 + i;
+                const int e1 = i < l ? ((i * (15 - i)) >> 1) - 1 + l : ((l * (15 - l)) >> 1) - 1 + i;
+                t.w[row][j++] = (uint32_t)(8 * e0) | ((uint32_t)(8 * e1) << 16);
             }
         }
     return t;
 }
 #if defined(__HIP__)
-static __constant__ EigPairLut kEigPairLut = eig_make_pair_lut(kEigJunk);
-static __constant__ EigPairLut kEigPairLutAW = eig_make_pair_lut(kEigAwJunk);
+static __constant__ EigPairLut kEigPairLut7 = eig_make_pair_lut7();
 #endif
 
 // 4-bit fields: indR[i] at field i (i = 0..7), indC[i] at field i - 1 (i = 1..8).
@@ -175,7 +178,7 @@ MCV_HD void eig_pick(double& v, int& kl, double v2, int kl2) {
 // position `pos` — V row `pos` of OpenCV's result is ws[kEigV + 9 * ret + j]. Returns the rotation
 // count through *iters when non-null (diagnostics).
 //
-// LOG = true (pass 1 of the split solve): the workspace is the 47-double AW slice, V is neither
+// LOG = true (pass 1 of the split solve): the workspace is the 45-double AW slice, V is neither
 // initialised nor rotated, and rotation t goes to log[t * logStride] (EigRot, c packed with k, l).
 // *iters = the rotation count, or -1 when it would exceed logCap or a c falls outside [0.5, 1] (not
 // for finite input; the caller then runs the one-pass solve). The return value is as above; the
@@ -184,14 +187,15 @@ template <class WS, bool LOG = false>
 MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr, EigRot* log = nullptr,
                        int logStride = 0, int logCap = 0) {
     constexpr int n = 9;
-    constexpr int junk = LOG ? kEigAwJunk : kEigJunk;
+    constexpr int junk = kEigJunk;   // the generic 9-pair form's skipped pairs (not with LOG: lane slices only)
+    static_assert(!LOG || std::is_same<WS, EigWsLane>::value, "the logged solve runs on lane slices");
     if constexpr (!LOG) {
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
         for (int i = 0; i < n * n; ++i) ws[kEigV + i] = (i / n == i % n) ? 1.0 : 0.0;
     }
-    ws[junk] = 0.0;   // stays +0: the skipped pair rotates (0, 0) into (+0, +0)
+    if constexpr (!LOG) ws[junk] = 0.0;   // stays +0: the skipped pair rotates (0, 0) into (+0, +0)
     bool logOk = true;
     uint32_t indR = 0, indC = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -262,27 +266,90 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr, Ei
         // other i the pair (A(k|i), A(l|i)) of the upper triangle (i = k, l read and write the junk
         // slot), and V rows k and l
         const double wk = ws[kEigW + k], wl = ws[kEigW + l];
+#if defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (std::is_same<WS, EigWsLane>::value) {
+            // the 7 pairs of the indices outside {k, l} (kEigPairLut7: 2 vector loads from L1)
+            constexpr int P7 = n - 2;
+            const uint4* lr = reinterpret_cast<const uint4*>(kEigPairLut7.w[ekl]);
+            const uint4 q0 = lr[0], q1 = lr[1];
+            const uint32_t qw[P7] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z};
+            char* const b = reinterpret_cast<char*>(ws.p);
+            int o0[P7], o1[P7];
+            double x0[P7], x1[P7], wa[n], wb[n];
+#pragma unroll
+            for (int j = 0; j < P7; ++j) {
+                o0[j] = (int)(qw[j] & 0xffffu);
+                o1[j] = (int)(qw[j] >> 16);
+                x0[j] = *reinterpret_cast<const double*>(b + o0[j]);
+                x1[j] = *reinterpret_cast<const double*>(b + o1[j]);
+            }
+            const int vk = kEigV + (k << 3) + k, vl = kEigV + (l << 3) + l;   // + 9 k, + 9 l
+            if constexpr (!LOG) {
+#pragma unroll
+                for (int i = 0; i < n; ++i) {
+                    wa[i] = ws[vk + i];
+                    wb[i] = ws[vl + i];
+                }
+            }
+            const double y = (wl - wk) * 0.5;
+            double c, s, t;
+            eig_rotation(p, y, c, s, t);
+            if constexpr (LOG) {
+                if (it >= logCap || !eig_rot_c_ok(c)) {
+                    logOk = false;
+                    break;
+                }
+                EigRot e;
+                e.c = eig_rot_pack(c, k, l);
+                e.s = s;
+                log[(int64_t)it * logStride] = e;
+            }
+            ws[ekl] = 0;
+            ws[kEigW + k] = wk - t;
+            ws[kEigW + l] = wl + t;
+            double nk[P7], nl[P7];
+#pragma unroll
+            for (int j = 0; j < P7; ++j) {
+                nk[j] = x0[j] * c - x1[j] * s;
+                nl[j] = x0[j] * s + x1[j] * c;
+                *reinterpret_cast<double*>(b + o0[j]) = nk[j];
+                *reinterpret_cast<double*>(b + o1[j]) = nl[j];
+            }
+            if constexpr (!LOG) {
+#pragma unroll
+                for (int i = 0; i < n; ++i) {
+                    ws[vk + i] = wa[i] * c - wb[i] * s;
+                    ws[vl + i] = wa[i] * s + wb[i] * c;
+                }
+            }
+            // the rescans over the 7 pairs in index order: i_j > k <=> j >= k, i_j > l <=> j >= l - 1;
+            // a tracker keeps the pair position j of its first maximum (-1: none beat the running 0, the
+            // start index: k + 1 for a row, 0 for a column), mapped back to i_j at the end
+            int jRk = -1, jCk = -1, jRl = -1, jCl = -1;
+            double vRk = 0, vCk = 0, vRl = 0, vCl = 0;
+#pragma unroll
+            for (int j = 0; j < P7; ++j) {
+                const double ak = __builtin_fabs(nk[j]), al = __builtin_fabs(nl[j]);
+                const bool tRk = j >= k && __builtin_fabs(vRk) < ak, tCk = j < k && __builtin_fabs(vCk) < ak;
+                const bool tRl = j >= l - 1 && __builtin_fabs(vRl) < al, tCl = j < l - 1 && __builtin_fabs(vCl) < al;
+                vRk = tRk ? nk[j] : vRk; jRk = tRk ? j : jRk;
+                vCk = tCk ? nk[j] : vCk; jCk = tCk ? j : jCk;
+                vRl = tRl ? nl[j] : vRl; jRl = tRl ? j : jRl;
+                vCl = tCl ? nl[j] : vCl; jCl = tCl ? j : jCl;
+            }
+            auto orig = [&](int j) { return j + (j >= k ? 1 : 0) + (j >= l - 1 ? 1 : 0); };
+            const int mRk = jRk < 0 ? k + 1 : orig(jRk), mCk = jCk < 0 ? 0 : orig(jCk);
+            const int mRl = jRl < 0 ? l + 1 : orig(jRl), mCl = jCl < 0 ? 0 : orig(jCl);
+            if (k < n - 1) indR = eig_set_nib(indR, k, mRk);
+            if (k > 0) indC = eig_set_nib(indC, k - 1, mCk);
+            if (l < n - 1) indR = eig_set_nib(indR, l, mRl);
+            indC = eig_set_nib(indC, l - 1, mCl);   // l >= 1
+            continue;
+        }
+#endif
         const int rk = eig_row_base(k), rl = eig_row_base(l);
         int e0[n], e1[n];
         double a0[n], b0[n], va[n], vb[n];
-#if defined(__HIP_DEVICE_COMPILE__)
-        if constexpr (std::is_same<WS, EigWsLane>::value) {
-            // the pair table's row for this pivot (3 vector loads from L1) -> byte offsets
-            const EigPairLut& lut = LOG ? kEigPairLutAW : kEigPairLut;
-            const uint4* lr = reinterpret_cast<const uint4*>(lut.w[ekl]);
-            const uint4 q0 = lr[0], q1 = lr[1];
-            const uint32_t q8 = lut.w[ekl][8];
-            const uint32_t qw[n] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q8};
-            char* const b = reinterpret_cast<char*>(ws.p);
-#pragma unroll
-            for (int i = 0; i < n; ++i) {
-                e0[i] = (int)(qw[i] & 0xffffu);
-                e1[i] = (int)(qw[i] >> 16);
-                a0[i] = *reinterpret_cast<const double*>(b + e0[i]);
-                b0[i] = *reinterpret_cast<const double*>(b + e1[i]);
-            }
-        } else
-#endif
         {
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
@@ -334,13 +401,6 @@ MCV_HD int eig9_jacobi(WS& ws, double (&w)[9], int pos, int* iters = nullptr, Ei
         for (int i = 0; i < n; ++i) {
             nk[i] = a0[i] * c - b0[i] * s;
             nl[i] = a0[i] * s + b0[i] * c;
-#if defined(__HIP_DEVICE_COMPILE__)
-            if constexpr (std::is_same<WS, EigWsLane>::value) {   // e0 / e1 are byte offsets here
-                *reinterpret_cast<double*>(reinterpret_cast<char*>(ws.p) + e0[i]) = nk[i];
-                *reinterpret_cast<double*>(reinterpret_cast<char*>(ws.p) + e1[i]) = nl[i];
-                continue;
-            }
-#endif
             ws[e0[i]] = nk[i];
             ws[e1[i]] = nl[i];
         }

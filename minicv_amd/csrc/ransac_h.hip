@@ -61,8 +61,8 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
 
 // The default generate as two passes over the split eigen-solve (round 6; jacobi_eig.h):
 //   mcv_h_gen_aw  lane per hypothesis: sample, subset check, runKernel's normalisation and LtL, then
-//                 JacobiImpl_ on the upper triangle and W only (a 47-double LDS slice per lane, 376 B
-//                 against the one-pass solve's 1016 B: 2.5x the lanes per CU) with every rotation's
+//                 JacobiImpl_ on the upper triangle and W only (a 45-double LDS slice per lane, 360 B
+//                 against the one-pass solve's 1016 B: 2.8x the lanes per CU) with every rotation's
 //                 (c, s, k, l) logged to HBM (16 B; SoA by hypothesis, so a wave's log writes and reads
 //                 are contiguous); the sort of W names the eigenvector's row r;
 //   mcv_h_gen_v   lane per hypothesis: V rebuilt from the log (an 81-double slice), row r -> H0, the
@@ -73,9 +73,9 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
 // Every value is computed by the same operations in the same order as the one-pass solve, so the
 // models are the same bits (tests: the whole-range cfg3 counts, the eigen stress test).
 static constexpr int kEigLogCap = 192;
-// 54 x 376 B = 19.8 KB: 8 blocks (two waves per SIMD) per CU. Screen: 40 / 64 / 32-lane blocks (10 / 6 /
-// 13 per CU) 6.6 / 5.7 / 6.7 ms against 5.2 ms of generate per 2^20.
-static constexpr int kHGenAwLanes = 54;
+// 56 x 360 B = 19.7 KB: 8 blocks (two waves per SIMD) per CU. Screen (with 376-byte slices): 40 / 64 /
+// 32-lane blocks (10 / 6 / 13 per CU) 6.6 / 5.7 / 6.7 ms against 5.2 ms of generate per 2^20 at 54.
+static constexpr int kHGenAwLanes = 56;
 // pass 2: one column of V per lane (9 lanes per hypothesis, 7 hypotheses per 63-lane block), 4 log
 // loads in flight. Round-6 screen at cfg3 (generate ms per 2^20 hypotheses, pass 1 ~3.7 of it): one
 // lane per hypothesis with one load ahead 5.78, with 8 ahead 5.78; 3 lanes x 3 columns 5.16-5.17 (V
