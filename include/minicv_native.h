@@ -511,6 +511,10 @@ MCV_API int mcvHostGlibcMath(int fn, const double* a, const double* b, int n, do
 MCV_API uint64_t mcvHostFingerprint(const void* buf, size_t bytes);
 /* The device kernel's fingerprint of a device buffer into d_out[0] (synchronous). Returns 1, 0 on error. */
 MCV_API int mcvTestFingerprint(const void* d_buf, size_t bytes, uint64_t* d_out);
+/* Round 6: the homography generate's split eigen-solve logs at most `cap` rotations per hypothesis
+ * (default and maximum 192; a cfg3 LtL takes 110-157); a hypothesis needing more is solved again by
+ * the one-pass kernel. Lowering the cap sends lanes down that path (tests). Returns the previous cap. */
+MCV_API int mcvTestEigLogCap(int cap);
 MCV_API void mcvHostPhilox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                            uint32_t* out4);
 /* Host twin of CameraPose.findScaled: the same candidates and costs as cvFindScaledPoseCosts,

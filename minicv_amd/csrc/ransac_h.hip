@@ -21,6 +21,7 @@
 #include "hyp_homography.h"
 #include "reduce.h"
 #include "kernels.h"
+#include "minicv_native.h"
 
 namespace mcv {
 
@@ -73,6 +74,8 @@ __global__ __launch_bounds__(FAST ? 256 : L) void mcv_h_generate(const float* __
 // Every value is computed by the same operations in the same order as the one-pass solve, so the
 // models are the same bits (tests: the whole-range cfg3 counts, the eigen stress test).
 static constexpr int kEigLogCap = 192;
+// the log rows pass 1 may use (mcvTestEigLogCap lowers it so the tests drive the overflow path)
+static int g_eig_log_cap = kEigLogCap;
 // 56 x 360 B = 19.7 KB: 8 blocks (two waves per SIMD) per CU. Screen (with 376-byte slices): 40 / 64 /
 // 32-lane blocks (10 / 6 / 13 per CU) 6.6 / 5.7 / 6.7 ms against 5.2 ms of generate per 2^20 at 54.
 static constexpr int kHGenAwLanes = 56;
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(L) void mcv_h_gen_aw(const float* __restrict__ pts4
                                                   int64_t hypBegin, int count, HModelF* __restrict__ models,
                                                   int* __restrict__ counts, int4* __restrict__ sidx,
                                                   int* __restrict__ meta, EigRot* __restrict__ log, int logStride,
-                                                  int* __restrict__ ovf, int ovfBase) {
+                                                  int* __restrict__ ovf, int ovfBase, int logCap) {
     const int j = blockIdx.x * L + threadIdx.x;   // lane within the piece
     if (j >= count) return;
     const int i = ovfBase + j;                    // hypothesis within the chunk
@@ -118,7 +121,7 @@ __global__ __launch_bounds__(L) void mcv_h_gen_aw(const float* __restrict__ pts4
     }
     double w[9];
     int nrot = 0;
-    const int r = eig9_jacobi<EigWsLane, true>(ws, w, 8, &nrot, log + j, logStride, kEigLogCap);
+    const int r = eig9_jacobi<EigWsLane, true>(ws, w, 8, &nrot, log + j, logStride, logCap);
     sidx[j] = make_int4(idx[0], idx[1], idx[2], idx[3]);
     if (nrot < 0) {
         meta[j] = kMetaOverflow;
@@ -1127,7 +1130,7 @@ void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin
         const int cnt = std::min(piece, hypCount - base);
         hipLaunchKernelGGL(mcv_h_gen_aw<kHGenAwLanes>, dim3((cnt + kHGenAwLanes - 1) / kHGenAwLanes),
                            dim3(kHGenAwLanes), 0, s, d_pts4, N, smp, hypBegin, cnt, (HModelF*)d_models, d_counts, sidx,
-                           meta, log, piece, ovf, base);
+                           meta, log, piece, ovf, base, g_eig_log_cap);
         hipLaunchKernelGGL((mcv_h_gen_v<kHGenVG, kHGenVQ, kHGenVD>), dim3((cnt + kHGenVQ - 1) / kHGenVQ),
                            dim3(kHGenVG * kHGenVQ), 0, s, d_pts4, cnt, base, sidx, meta, log, piece, (HModelF*)d_models,
                            d_h64, d_counts);
@@ -1292,3 +1295,11 @@ void h_reduce_lm(const float* d_pts4, int N, const uint8_t* d_mask, const double
 
 }  // namespace mcv
 
+
+// Test hook: the split generate's usable log rows in [0, 192] (lanes needing more go to the one-pass
+// overflow kernel); returns the previous value. Not thread-safe: tests only.
+extern "C" MCV_API int mcvTestEigLogCap(int cap) {
+    const int prev = mcv::g_eig_log_cap;
+    mcv::g_eig_log_cap = cap < 0 ? 0 : cap > mcv::kEigLogCap ? mcv::kEigLogCap : cap;
+    return prev;
+}

@@ -150,6 +150,7 @@ SIGNATURES = {
     "mcvHostFingerprint": (_U64, [_P, C.c_size_t]),
     "mcvHostGlibcMath": (_I, [_I, _P, _P, _I, _P]),
     "mcvTestFingerprint": (_I, [_P, C.c_size_t, _P]),
+    "mcvTestEigLogCap": (_I, [_I]),
     "mcvHostEssential": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostEssentialFast": (_I, [_P, _I, _U64, _I64, _P, _P]),
     "mcvHostFivePoint": (_I, [_P, _P]),

@@ -277,3 +277,21 @@ def test_finalize_fetch_and_resolve_paths(torch_dev, oracle, model):
             np.testing.assert_array_equal(M.ravel(), F)
         assert st == 1 and fc == ref_count == int(mask.sum().item())
     plan.close()
+
+
+@pytest.mark.parametrize("cap", [0, 100, 138, 150])
+def test_split_generate_overflow_path(torch_dev, oracle, cap):
+    """Round 6: the split eigen generate logs at most 192 rotations per hypothesis and hands a lane that
+    needs more to the one-pass kernel (mcv_h_gen_ovf). Random cfg3-like LtLs take 110-157 rotations,
+    so the overflow path is driven by lowering the log's usable rows: at 0 every hypothesis, at 100 /
+    138 / 150 about all / half / a few percent of them are solved by the fallback — the counts stay
+    the oracle's (and the one-pass kernel's) bit for bit."""
+    src, dst, _ = S.homography_problem(3000, 31, outlier_frac=0.5)
+    thr = 5e-3
+    prev = N.lib().mcvTestEigLogCap(cap)
+    try:
+        got, key = device_counts(torch_dev, src, dst, 31, 777, 6000, thr, unfused=True)
+    finally:
+        N.lib().mcvTestEigLogCap(prev)
+    ref = oracle.h_counts(oracle.pack4(src, dst), 31, 777, 6000, float(np.float32(thr * thr)), fused=False)
+    np.testing.assert_array_equal(got, ref)

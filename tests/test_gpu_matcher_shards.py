@@ -236,3 +236,14 @@ def test_l2_two_train_rows_one_nan(gpu, oracle, nan_row):
     np.testing.assert_array_equal(d, rd.astype(np.float32))
     np.testing.assert_array_equal(d2, rd2.astype(np.float32))
     assert (idx == 1 - nan_row).all()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("devices", [2, 8])
+def test_l2_multi_device_full_cfg5(gpu, cfg5, devices):
+    """cvMatchL2Multi over BASELINE cfg5 at full size (50k x 50k): every output of every query equal to
+    the single-device call (which test_l2_rank_slices_cfg5 / test_l2_full_size_cfg5 tie to the oracle)."""
+    q, t, full = cfg5
+    got = opencv.matchL2(q, t, deviceCount=devices)
+    for g, f in zip(got, full):
+        np.testing.assert_array_equal(g, f)
