@@ -130,4 +130,31 @@ struct StreamFence {
     }
 };
 
+// Waves of `kernel` (blocks of `threads`) the current device holds at once: its occupancy x the CUs.
+template <class K>
+inline int64_t resident_waves(K kernel, int threads) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || per <= 0) per = 1;
+    return (int64_t)per * cus * (threads / 64);
+}
+
+// Point chunks of a (model waves) x (point chunks) sweep: with c chunks the launch takes
+// ceil(waves c / resident) rounds of waves 1 / c as long, so the idle tail of the last round is what
+// the count changes. Returns the smallest c in [1, hi] within 1 % of the fewest one-chunk-wave
+// durations (more chunks cost per-wave model setup and count atomics).
+inline int tail_chunks(int64_t waves, int64_t resident, int hi) {
+    if (waves <= 0 || resident <= 0 || hi <= 1) return 1;
+    double best = 1e300;
+    for (int c = 1; c <= hi; ++c) {
+        const double cost = (double)((waves * c + resident - 1) / resident) / c;
+        if (cost < best) best = cost;
+    }
+    for (int c = 1; c <= hi; ++c)
+        if ((double)((waves * c + resident - 1) / resident) / c <= best * 1.01) return c;
+    return 1;
+}
+
 }  // namespace mcv

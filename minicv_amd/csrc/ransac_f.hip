@@ -18,6 +18,7 @@
 #include "sampson_pk.h"
 #include "reduce.h"
 #include "kernels.h"
+#include "mcv_runtime.h"
 #include <cstdlib>
 #include <algorithm>
 #include <cmath>
@@ -384,18 +385,21 @@ static void launch_f_verify_pk_kp(const float4* p, int N, const FModelD* m, int*
                                   int kind, const SampsonPkCut& cut, const double* d_bb, hipStream_t s) {
     const int waves = (hypCount + 2 * KP - 1) / (2 * KP);
     const int blocks = (waves + 3) / 4;
-    // point chunks: about 64 waves per SIMD in total (the last round is a small share), chunks
-    // of at least 8192 points (the per-wave model setup stays small against the sweep)
-    constexpr int target = 65536;
+    // point chunks of at least 8192 points (the per-wave model setup stays small against the sweep), as
+    // many as even out the last round of resident waves (tail_chunks). Round 6, same box, alternating:
+    // 2^17 / 2^18 / 2^19 hypotheses (the 8- / 4- / 2-rank shares) 28.5 / 56.0 / 110.8 ms a step against
+    // 28.7-28.8 / 56.4-56.5 / 112.9 with the fixed ~64-waves-per-SIMD target (2^17: 3 chunks, 16.0005
+    // rounds of 4 waves per SIMD); 2^20 keeps one chunk. PnP's verify measured slower with more chunks
+    // (its per-wave pose setup): not used there.
+    static const int64_t resident = resident_waves(mcv_f_verify_pk<KP, P>, 256);
     const int step = 64 * P;
-    int chunks = (target + waves - 1) / waves;
     // No L2-sized chunking: 2^20 hypotheses x 500k points in 8 per-XCD chunks of 1 MB cut the fetches
     // 4.0 -> 0.61 GB per launch but took eight count atomics per model (32 MiB of writes against the
     // 4 MiB of one store each) for 222.2 vs 224.1 ms; a block-shared form (four chunks per block,
     // counts added in LDS behind a barrier: 8 MiB) measured 279 ms. The sweep is VALU-bound, so the
     // whole point set streams from the 256 MB MALL and each model's count is one store.
     const int maxChunks = std::max(1, N / 8192);
-    chunks = std::max(1, std::min(chunks, maxChunks));
+    int chunks = tail_chunks(waves, resident, maxChunks);
     int chunk = (N + chunks - 1) / chunks;
     chunk = (chunk + step - 1) / step * step;
     chunks = std::max(1, (N + chunk - 1) / chunk);
