@@ -157,8 +157,11 @@ void launch_pnp_solve5(const void* d_pts, const double* cam8, PnpOneOut* d_out, 
 void launch_mask_compact(const uint8_t* d_mask, int N, int* d_idx, int* d_count, hipStream_t s);
 // EPnP over n points: d_pts (+ optional index list d_idx) fp32 PnpPoints, or d_img / d_world fp64.
 // normalized: d_us = undistortPoints' normalised coordinates (SQPnP) instead of x f + c (EPnP).
+// d_n (optional, fp32 points only): the point count on the device (a compaction's output); n is then
+// an upper bound that sizes the grid.
 void launch_epnp_prep(const void* d_pts, const int* d_idx, const double* d_img, const double* d_world, int n,
-                      const double* cam8, double* d_pw, double* d_us, hipStream_t s, bool normalized = false);
+                      const double* cam8, double* d_pw, double* d_us, hipStream_t s, bool normalized = false,
+                      const int* d_n = nullptr);
 // SQPnP passes (sqpnp.h): the 39 computeOmega sums; the positive-depth count of the pose R[0] / t[0].
 enum { kEpnpPassSumPw = 0, kEpnpPassPw0 = 1, kEpnpPassMtm = 2, kEpnpPassPc = 3, kEpnpPassAbt = 4, kEpnpPassReproj = 5,
        kEpnpPassSqp = 6, kEpnpPassSqpDepth = 7 };
@@ -172,11 +175,17 @@ struct EpnpPassArgs {
     double R[3][3][3];       // Reproj
     double t[3][3];
 };
+// d_n (optional): the point count on the device, n an upper bound; the partials keep the stride of the
+// device count's blocks (part[acc * nblk + blk], nblk = ceil(*d_n / kEpnpBlock)). d_prev (optional, Pw0 /
+// Abt): the previous pass's partials, from which the pass takes its centroid / pc0 on the device.
 void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, const EpnpPassArgs& a, int nacc,
-                      double* d_part, hipStream_t s);
+                      double* d_part, hipStream_t s, const int* d_n = nullptr, const double* d_prev = nullptr);
 void launch_pnp_solve4(const void* d_pts, const double* cam8, PnpOneOut* d_out, hipStream_t s, bool fast = false);
 void launch_pnp_mask(const void* d_pts, int N, const double* cam8, const double* R9, const double* t3, float thr2,
                      bool fused, uint8_t* d_mask, int* d_count, hipStream_t s);
+// The same mask for a pose already on the device (a chunk's model slot): no host round trip first.
+void launch_pnp_mask_dev(const void* d_pts, int N, const double* cam8, const void* d_pose, float thr2, bool fused,
+                         uint8_t* d_mask, int* d_count, hipStream_t s);
 void launch_pnp_ap3p(const Ap3pIn& in, Ap3pOut* d_out, hipStream_t s);
 void pnp_reduce_lm(const void* d_pts, int N, const uint8_t* d_mask, const double* cam8, const double* R9,
                    const double* t3, const double* dR27, bool wantJ, double* d_part, double* d_out, hipStream_t s);

@@ -270,40 +270,63 @@ void pnp_vvs(Plan& P, const void* d_pts, int N, double* rvec, double* t, int max
 
 // EPnP (epnp.h, OpenCV compute_pose) over n points already on the device as double world points
 // d_pw[3n] and pixel observations d_us[2n]: the O(n) loops run as blocked fixed-order passes
-// (mcv_epnp_pass), the 3x3 / 12x12 / 6xK algebra between them here on the host.
+// (mcv_epnp_pass), the 3x3 / 12x12 / 6xK algebra between them here on the host. The passes whose inputs
+// are only means of the previous pass's sums (Pw0 after SumPw, Abt after Pc) take them on the device
+// (round 6), so the solve costs four host round trips: {SumPw, Pw0}, MtM, {Pc, Abt}, Reproj.
+// first (optional): {SumPw, Pw0} already ran and came back with the caller's synchronisation.
+struct EpnpFirst {
+    double sum[3], p6[6], p0[3];
+};
+
+// Host sums of a pass's block partials, in block order from 0 (as the device's derived means).
+static void epnp_sums(const std::vector<double>& part, size_t off, int nacc, int nblk, double* out) {
+    for (int a = 0; a < nacc; ++a) {
+        double t = 0;
+        for (int b = 0; b < nblk; ++b) t += part[off + (size_t)a * nblk + b];
+        out[a] = t;
+    }
+}
+
 static void epnp_device(Plan& P, const double* d_pw, const double* d_us, int n, double* R9, double* t3,
-                        hipStream_t s) {
+                        hipStream_t s, const EpnpFirst* first = nullptr) {
     if (n < 4) fail("EPnP needs at least 4 points (n=%d)", n);
     EpnpPassArgs A;
     std::memset(&A, 0, sizeof(A));
     A.cam = EpnpCam{P.pnpCam[0], P.pnpCam[1], P.pnpCam[2], P.pnpCam[3]};
     const int nblk = (n + kEpnpBlock - 1) / kEpnpBlock;
-    std::vector<double> part;
-    auto pass = [&](int mode, int nacc, double* out) {
-        P.part.ensure((size_t)nacc * nblk);
-        launch_epnp_pass(mode, d_pw, d_us, n, A, nacc, P.part.p, s);
+    P.part.ensure((size_t)kMtmSums * nblk);   // two passes at once: [0, 9 nblk) and [9 nblk, 36 nblk)
+    std::vector<double> part((size_t)kMtmSums * nblk);
+    auto launch = [&](int mode, int nacc, size_t off, const double* prev) {
+        launch_epnp_pass(mode, d_pw, d_us, n, A, nacc, P.part.p + off, s, nullptr, prev);
         MCV_HIP(hipGetLastError());
-        part.resize((size_t)nacc * nblk);
-        MCV_HIP(hipMemcpyAsync(part.data(), P.part.p, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-        MCV_HIP(hipStreamSynchronize(s));
-        for (int a = 0; a < nacc; ++a) {
-            double t = 0;
-            for (int b = 0; b < nblk; ++b) t += part[(size_t)a * nblk + b];
-            out[a] = t;
-        }
     };
-    double sum[3], p6[6], mtm[kMtmSums], pcs[9], abt[27], rep3[3];
-    pass(kEpnpPassSumPw, 3, sum);
+    auto fetch = [&](size_t count, double* extra = nullptr, const double* d_extra = nullptr, size_t nextra = 0) {
+        MCV_HIP(hipMemcpyAsync(part.data(), P.part.p, count * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (extra) MCV_HIP(hipMemcpyAsync(extra, d_extra, nextra * sizeof(double), hipMemcpyDeviceToHost, s));
+        MCV_HIP(hipStreamSynchronize(s));
+    };
+    const size_t off1 = (size_t)9 * nblk;
+    double sum[3], p6[6], p0[3], mtm[kMtmSums], pcs[9], abt[27], rep3[3];
+    if (first) {
+        std::memcpy(sum, first->sum, sizeof(sum));
+        std::memcpy(p6, first->p6, sizeof(p6));
+        std::memcpy(p0, first->p0, sizeof(p0));
+    } else {
+        launch(kEpnpPassSumPw, 3, 0, nullptr);
+        launch(kEpnpPassPw0, 6, off1, P.part.p);   // centroid from SumPw's partials on the device
+        fetch(off1 + (size_t)6 * nblk, p0, d_pw, 3);
+        epnp_sums(part, 0, 3, nblk, sum);
+        epnp_sums(part, off1, 6, nblk, p6);
+    }
     for (int j = 0; j < 3; ++j) A.c0[j] = sum[j] / n;
-    pass(kEpnpPassPw0, 6, p6);
     const double P3[3][3] = {{p6[0], p6[1], p6[2]}, {p6[1], p6[3], p6[4]}, {p6[2], p6[4], p6[5]}};
     epnp_control(sum, P3, n, A.C);
-    pass(kEpnpPassMtm, kMtmSums, mtm);
+    launch(kEpnpPassMtm, kMtmSums, 0, nullptr);
+    fetch((size_t)kMtmSums * nblk);
+    epnp_sums(part, 0, kMtmSums, nblk, mtm);
     EpnpBetas B;
     epnp_betas(mtm, A.C, B);
-    double p0[3], al0[4];
-    MCV_HIP(hipMemcpyAsync(p0, d_pw, sizeof(p0), hipMemcpyDeviceToHost, s));
-    MCV_HIP(hipStreamSynchronize(s));
+    double al0[4];
     epnp_alphas(A.C, p0, al0);
     for (int N = 0; N < 3; ++N) {
         epnp_ccs(B, B.betas[N + 1], A.ccs[N]);
@@ -313,18 +336,23 @@ static void epnp_device(Plan& P, const double* d_pw, const double* d_us, int n, 
             for (int j = 0; j < 4; ++j)
                 for (int k = 0; k < 3; ++k) A.ccs[N][j][k] = -A.ccs[N][j][k];
     }
-    pass(kEpnpPassPc, 9, pcs);
+    for (int j = 0; j < 3; ++j) A.pw0[j] = sum[j] / n;
+    launch(kEpnpPassPc, 9, 0, nullptr);
+    launch(kEpnpPassAbt, 27, off1, P.part.p);   // pc0 from Pc's partials on the device
+    fetch(off1 + (size_t)27 * nblk);
+    epnp_sums(part, 0, 9, nblk, pcs);
+    epnp_sums(part, off1, 27, nblk, abt);
     for (int N = 0; N < 3; ++N)
         for (int j = 0; j < 3; ++j) A.pc0[N][j] = pcs[3 * N + j] / n;
-    for (int j = 0; j < 3; ++j) A.pw0[j] = sum[j] / n;
-    pass(kEpnpPassAbt, 27, abt);
     for (int N = 0; N < 3; ++N) {
         double ab[3][3];
         for (int j = 0; j < 3; ++j)
             for (int k = 0; k < 3; ++k) ab[j][k] = abt[9 * N + 3 * j + k];
         epnp_rt(ab, A.pc0[N], A.pw0, A.R[N], A.t[N]);
     }
-    pass(kEpnpPassReproj, 3, rep3);
+    launch(kEpnpPassReproj, 3, 0, nullptr);
+    fetch((size_t)3 * nblk);
+    epnp_sums(part, 0, 3, nblk, rep3);
     const double rep[4] = {0, rep3[0] / n, rep3[1] / n, rep3[2] / n};
     const int N = epnp_pick(rep) - 1;
     for (int i = 0; i < 3; ++i) {
@@ -376,19 +404,38 @@ static int sqpnp_device(Plan& P, const double* d_pw, const double* d_us, int n, 
 
 // solvePnPRansac's final EPnP: the inliers (compressElems order) of the float points as doubles,
 // image points through undistortPoints with a double result.
+// Round 6: the compaction, the prep and the first two passes run on the device count, and the count,
+// their sums and the first point return with one synchronisation (four before).
 static void epnp_inliers(Plan& P, const void* d_pts, int N, const uint8_t* d_mask, double* R9, double* t3,
                          hipStream_t s) {
     P.eidx.ensure((size_t)std::max(N, 1));
     launch_mask_compact(d_mask, N, P.eidx.p, P.count.p, s);
     MCV_HIP(hipGetLastError());
+    P.epw.ensure((size_t)3 * std::max(N, 1));
+    P.eus.ensure((size_t)2 * std::max(N, 1));
+    launch_epnp_prep(d_pts, P.eidx.p, nullptr, nullptr, N, P.pnpCam, P.epw.p, P.eus.p, s, false, P.count.p);
+    EpnpPassArgs A;
+    std::memset(&A, 0, sizeof(A));
+    const int nblkMax = (N + kEpnpBlock - 1) / kEpnpBlock;
+    P.part.ensure((size_t)9 * nblkMax);
+    double* d_sum = P.part.p;
+    double* d_p6 = P.part.p + (size_t)3 * nblkMax;
+    launch_epnp_pass(kEpnpPassSumPw, P.epw.p, P.eus.p, N, A, 3, d_sum, s, P.count.p);
+    launch_epnp_pass(kEpnpPassPw0, P.epw.p, P.eus.p, N, A, 6, d_p6, s, P.count.p, d_sum);
+    MCV_HIP(hipGetLastError());
+    std::vector<double> part((size_t)9 * nblkMax);
+    EpnpFirst F;
     MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipMemcpyAsync(part.data(), P.part.p, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    MCV_HIP(hipMemcpyAsync(F.p0, P.epw.p, sizeof(F.p0), hipMemcpyDeviceToHost, s));
     MCV_HIP(hipStreamSynchronize(s));
     const int n = P.h_i.p[0];
-    P.epw.ensure((size_t)3 * std::max(n, 1));
-    P.eus.ensure((size_t)2 * std::max(n, 1));
-    launch_epnp_prep(d_pts, P.eidx.p, nullptr, nullptr, n, P.pnpCam, P.epw.p, P.eus.p, s);
-    MCV_HIP(hipGetLastError());
-    epnp_device(P, P.epw.p, P.eus.p, n, R9, t3, s);
+    if (n < 4) fail("EPnP needs at least 4 points (n=%d)", n);
+    // the device count's block stride; Pw0's region starts at 3 nblkMax
+    const int nblk = (n + kEpnpBlock - 1) / kEpnpBlock;
+    epnp_sums(part, 0, 3, nblk, F.sum);
+    epnp_sums(part, (size_t)3 * nblkMax, 6, nblk, F.p6);
+    epnp_device(P, P.epw.p, P.eus.p, n, R9, t3, s, &F);
 }
 
 // Device API finalize: winner -> mask -> the inlier solve of the kind (solvePnPRansac's tail):
@@ -399,12 +446,19 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
     PnpOneOut one;
     const bool epnp = pnp_cfg_epnp(cfg);
     const Sampler smp = P.sampler(cfg);
+    int count = 0;
     if (P.last.covers(hyp, smp, d_pts, N, epnp ? 1 : (fast_ap3p(cfg) ? 2 : 0))) {
         // the winner's pose straight from the last chunk's model buffer (the same code produced it)
-        // instead of a single-lane re-solve
+        // instead of a single-lane re-solve; its mask and count from that slot too, so the pose, the
+        // count and the freshness check return with one synchronisation
         const PnpPose* d_m = (const PnpPose*)P.models.p + (hyp - P.last.begin);
         MCV_HIP(hipMemcpyAsync(P.h_one.p, d_m, sizeof(PnpPose), hipMemcpyDeviceToHost, s));
         queue_chunk_check(P, d_pts, N, s);
+        MCV_HIP(hipMemsetAsync(P.count.p, 0, sizeof(int), s));
+        launch_pnp_mask_dev(d_pts, N, P.pnpCam, d_m, (float)(cfg.threshold * cfg.threshold), fused_pnp(cfg), d_mask,
+                            P.count.p, s);
+        MCV_HIP(hipGetLastError());
+        MCV_HIP(hipMemcpyAsync(P.h_i.p, P.count.p, sizeof(int), hipMemcpyDeviceToHost, s));
         MCV_HIP(hipStreamSynchronize(s));
         if (!chunk_fresh(P)) {   // the points changed since the chunk was evaluated: re-solve
             P.last.clear();
@@ -415,13 +469,14 @@ int p_finalize(Plan& P, const void* d_pts, int N, const RansacConfig& cfg, int64
         std::memcpy(one.R, pose.R, sizeof(one.R));
         std::memcpy(one.t, pose.t, sizeof(one.t));
         one.status = 1;
+        count = P.h_i.p[0];
     } else {
         launch_pnp_one(d_pts, N, P.pnpCam, smp, hyp, epnp, (PnpOneOut*)P.one.p, s, fast_ap3p(cfg));
         MCV_HIP(hipGetLastError());
         one = pnp_fetch_one(P, s);
+        if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
+        count = pnp_mask_count(P, d_pts, N, cfg, one.R, one.t, d_mask, s);
     }
-    if (one.status != 1) fail("winning hypothesis %lld has no model (status %d)", (long long)hyp, one.status);
-    const int count = pnp_mask_count(P, d_pts, N, cfg, one.R, one.t, d_mask, s);
     double r[3], t[3] = {one.t[0], one.t[1], one.t[2]};
     rodrigues_inv(one.R, r);
     if (!(cfg.flags & MCV_FLAG_NO_REFINE) && count > 0) {

@@ -459,11 +459,13 @@ __global__ void mcv_pnp_solve4(const PnpPoint* __restrict__ pts, PnpCamera cam, 
     out->idx[4] = -1;
 }
 
+// mp (optional): the pose read from the device instead of the by-value m.
 __global__ __launch_bounds__(256) void mcv_pnp_mask(const PnpPoint* __restrict__ pts, int N, PnpCamera cam,
-                                                    PnpPose m, float thr2, bool fused, uint8_t* __restrict__ mask,
-                                                    int* __restrict__ count) {
+                                                    PnpPose m, const PnpPose* __restrict__ mp, float thr2, bool fused,
+                                                    uint8_t* __restrict__ mask, int* __restrict__ count) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     bool in = false;
+    if (mp) m = *mp;
     if (i < N) {
         const PnpPoint q = pts[i];
         in = pnp_error(cam, m.R, m.t, q.X, q.Y, q.Z, q.u, q.v, fused) <= thr2;
@@ -611,8 +613,9 @@ __global__ __launch_bounds__(1024) void mcv_mask_compact(const uint8_t* __restri
 // Points of the solve in double: pw = world, us = undistortPoints (double result) * f + c.
 __global__ __launch_bounds__(256) void mcv_epnp_prep_f32(const PnpPoint* __restrict__ pts, const int* __restrict__ idx,
                                                          int n, PnpCamera c, double* __restrict__ pw,
-                                                         double* __restrict__ us) {
+                                                         double* __restrict__ us, const int* __restrict__ nDev) {
     const int i = blockIdx.x * 256 + threadIdx.x;
+    if (nDev) n = *nDev;
     if (i >= n) return;
     const PnpPoint p = pts[idx ? idx[i] : i];
     double x, y;
@@ -690,7 +693,28 @@ __device__ __forceinline__ void epnp_pass_term(const double* __restrict__ pw, co
 template <int MODE>
 __global__ __launch_bounds__(256) void mcv_epnp_pass(const double* __restrict__ pw, const double* __restrict__ us,
                                                      int n, EpnpPassArgs A, int nacc, int nblk,
-                                                     double* __restrict__ part) {
+                                                     double* __restrict__ part, const int* __restrict__ nDev,
+                                                     const double* __restrict__ prev) {
+    if (nDev) {   // the grid covers the upper bound: blocks past the device count's write nothing
+        n = *nDev;
+        nblk = (n + kEpnpBlock - 1) / kEpnpBlock;
+        if ((int)blockIdx.x >= nblk) return;
+    }
+    // prev (optional): the previous pass's partials (same n), whose means this pass needs, summed over
+    // the blocks in order from 0 and divided by n exactly as the host does: Pw0's centroid from SumPw,
+    // Abt's pc0 from Pc. Saves the host round trip between the two passes.
+    if (prev && MODE == kEpnpPassPw0)
+        for (int j = 0; j < 3; ++j) {
+            double t = 0;
+            for (int b = 0; b < nblk; ++b) t += prev[(size_t)j * nblk + b];
+            A.c0[j] = t / n;
+        }
+    if (prev && MODE == kEpnpPassAbt)
+        for (int a = 0; a < 9; ++a) {
+            double t = 0;
+            for (int b = 0; b < nblk; ++b) t += prev[(size_t)a * nblk + b];
+            A.pc0[a / 3][a % 3] = t / n;
+        }
     static_assert(kSqpSums <= kEpnpTermCols && 24 <= kEpnpTermCols && 27 <= kEpnpTermCols, "term tile width");
     __shared__ double term[kEpnpTile * kEpnpTermCols];
     int ma = 0, mb = 0;   // MtM: the accumulator's (row, column) of the upper triangle
@@ -894,30 +918,33 @@ void launch_mask_compact(const uint8_t* d_mask, int N, int* d_idx, int* d_count,
     hipLaunchKernelGGL(mcv_mask_compact, dim3(1), dim3(1024), 0, s, d_mask, N, d_idx, d_count);
 }
 
+// d_n applies to the fp32 points (the inlier solve); the fp64 form always takes n.
 void launch_epnp_prep(const void* d_pts, const int* d_idx, const double* d_img, const double* d_world, int n,
-                      const double* cam8, double* d_pw, double* d_us, hipStream_t s, bool normalized) {
+                      const double* cam8, double* d_pw, double* d_us, hipStream_t s, bool normalized, const int* d_n) {
     if (n <= 0) return;
     if (d_pts)
         hipLaunchKernelGGL(mcv_epnp_prep_f32, dim3((n + 255) / 256), dim3(256), 0, s, (const PnpPoint*)d_pts, d_idx, n,
-                           to_cam(cam8), d_pw, d_us);
+                           to_cam(cam8), d_pw, d_us, d_n);
     else
         hipLaunchKernelGGL(mcv_epnp_prep_f64, dim3((n + 255) / 256), dim3(256), 0, s, d_img, d_world, n, to_cam(cam8),
                            d_pw, d_us, normalized);
 }
 
 void launch_epnp_pass(int mode, const double* d_pw, const double* d_us, int n, const EpnpPassArgs& a, int nacc,
-                      double* d_part, hipStream_t s) {
+                      double* d_part, hipStream_t s, const int* d_n, const double* d_prev) {
+    if (d_prev && mode != kEpnpPassPw0 && mode != kEpnpPassAbt) d_prev = nullptr;   // only these take means
     const int nblk = (n + kEpnpBlock - 1) / kEpnpBlock;
+    if (nblk <= 0) return;
     const dim3 grid(nblk), block(256);   // nacc <= 78 accumulators, one lane each
     switch (mode) {
-        case kEpnpPassSumPw: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSumPw>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
-        case kEpnpPassPw0: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassPw0>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
-        case kEpnpPassMtm: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassMtm>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
-        case kEpnpPassPc: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassPc>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
-        case kEpnpPassAbt: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassAbt>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
-        case kEpnpPassSqp: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSqp>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
-        case kEpnpPassSqpDepth: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSqpDepth>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part); break;
-        default: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassReproj>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part);
+        case kEpnpPassSumPw: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSumPw>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part, d_n, d_prev); break;
+        case kEpnpPassPw0: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassPw0>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part, d_n, d_prev); break;
+        case kEpnpPassMtm: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassMtm>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part, d_n, d_prev); break;
+        case kEpnpPassPc: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassPc>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part, d_n, d_prev); break;
+        case kEpnpPassAbt: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassAbt>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part, d_n, d_prev); break;
+        case kEpnpPassSqp: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSqp>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part, d_n, d_prev); break;
+        case kEpnpPassSqpDepth: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassSqpDepth>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part, d_n, d_prev); break;
+        default: hipLaunchKernelGGL(mcv_epnp_pass<kEpnpPassReproj>, grid, block, 0, s, d_pw, d_us, n, a, nacc, nblk, d_part, d_n, d_prev);
     }
 }
 
@@ -931,7 +958,14 @@ void launch_pnp_mask(const void* d_pts, int N, const double* cam8, const double*
     for (int k = 0; k < 9; ++k) m.R[k] = R9[k];
     for (int k = 0; k < 3; ++k) m.t[k] = t3[k];
     hipLaunchKernelGGL(mcv_pnp_mask, dim3((N + 255) / 256), dim3(256), 0, s, (const PnpPoint*)d_pts, N, to_cam(cam8),
-                       m, thr2, fused, d_mask, d_count);
+                       m, (const PnpPose*)nullptr, thr2, fused, d_mask, d_count);
+}
+
+void launch_pnp_mask_dev(const void* d_pts, int N, const double* cam8, const void* d_pose, float thr2, bool fused,
+                         uint8_t* d_mask, int* d_count, hipStream_t s) {
+    PnpPose m{};
+    hipLaunchKernelGGL(mcv_pnp_mask, dim3((N + 255) / 256), dim3(256), 0, s, (const PnpPoint*)d_pts, N, to_cam(cam8),
+                       m, (const PnpPose*)d_pose, thr2, fused, d_mask, d_count);
 }
 
 void launch_pnp_ap3p(const Ap3pIn& in, Ap3pOut* d_out, hipStream_t s) {
