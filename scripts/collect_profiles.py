@@ -62,6 +62,7 @@ def main():
             shutil.copy(ks, PROF / rnd / f"kernel_stats_{w}.csv")
     traffic = {}
     mean = lambda xs: sum(xs) / len(xs)
+    median = lambda xs: sorted(xs)[len(xs) // 2] if len(xs) % 2 else sum(sorted(xs)[len(xs) // 2 - 1:len(xs) // 2 + 1]) / 2
     for w, kernel in KERNELS.items():
         j = last_json(PROF / f"{rnd}_bench_{w}.json") if (PROF / f"{rnd}_bench_{w}.json").exists() else None
         if not j:
@@ -96,8 +97,11 @@ def main():
             f = pmc_sums(fetch, kernel).get("FETCH_SIZE")
             wr = pmc_sums(write, kernel).get("WRITE_SIZE")
             if f and wr:
-                t.update({"FETCH_SIZE_KB": mean(f), "WRITE_SIZE_KB": mean(wr), "dispatches": len(f),
-                          "hbm_bytes_per_launch": (2 * mean(f) + mean(wr)) * 1024.0})
+                # the median dispatch: a dispatch's counts also take the write-backs of lines the kernels
+                # before it left dirty (round 6: one E dispatch of five wrote 168 MiB against 41.1-41.2)
+                t.update({"FETCH_SIZE_KB": median(f), "WRITE_SIZE_KB": median(wr), "dispatches": len(f),
+                          "WRITE_SIZE_KB_range": [min(wr), max(wr)], "statistic": "median over the dispatches",
+                          "hbm_bytes_per_launch": (2 * median(f) + median(wr)) * 1024.0})
                 print("traffic", kernel, t["hbm_bytes_per_launch"])
         # MFMA SQ pass (matchers): MFMA instructions, MFMA busy share of the SIMD cycles
         mf_src = OUT / f"pmc_mfma_{w}" / "run_counter_collection.csv"
