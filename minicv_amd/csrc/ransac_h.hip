@@ -1081,24 +1081,15 @@ struct OpLMErr {   // 1: |r|^2 only
 // ------------------------------------------------------------------------------------------
 // Launchers (host side, called from ransac_host.cpp)
 // ------------------------------------------------------------------------------------------
-template <int L>
-static int h_gen_piece_for() {
-    int d = 0, cus = 0, blocks = 0;
-    (void)hipGetDevice(&d);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, mcv_h_gen_aw<L>, L, 0) != hipSuccess || blocks <= 0)
-        blocks = 8;
-    return 2 * cus * blocks * L;
-}
-// Rows of the split generate's scratch per piece: two rounds of mcv_h_gen_aw's resident lanes, so every
-// piece but the last fills the chip evenly (a piece of 2.4 rounds would idle 20 % of its third round).
-int h_gen_piece_lanes() {
-    static const int lanes = h_gen_piece_for<kHGenAwLanes>();
-    return lanes;
-}
+// Rows of the split generate's scratch per piece: the whole call up to 2^20 hypotheses (3.2 GB of
+// rotation log at 192 entries of 16 B). Round 6, same box: one piece 4.40 ms per 2^20 against 4.85 ms
+// for pieces of two rounds of mcv_h_gen_aw's resident lanes (5 pieces: each launch drains its slowest
+// waves, whose rotation counts vary per lane), 4.69 / 4.67 for pieces of four rounds / two halves.
+static constexpr int kHGenMaxPiece = 1 << 20;
+static int h_gen_piece(int hypCount) { return std::min(hypCount, kHGenMaxPiece); }
 
 size_t h_gen_scratch_bytes(int hypCount) {
-    const size_t piece = (size_t)std::min(hypCount, h_gen_piece_lanes());
+    const size_t piece = (size_t)h_gen_piece(hypCount);
     return piece * kEigLogCap * sizeof(EigRot) + piece * (sizeof(int4) + sizeof(int)) +
            ((size_t)hypCount + 1) * sizeof(int);
 }
@@ -1116,7 +1107,7 @@ void launch_h_generate(const float* d_pts4, int N, Sampler smp, int64_t hypBegin
                            d_counts);
         return;
     }
-    const int piece = std::min(hypCount, h_gen_piece_lanes());
+    const int piece = h_gen_piece(hypCount);
     char* b = (char*)d_scratch;
     EigRot* log = (EigRot*)b;
     b += (size_t)piece * kEigLogCap * sizeof(EigRot);
