@@ -140,8 +140,10 @@ struct Ap3pOut {
 void launch_pnp_pack(const double* d_img, const double* d_world, int N, void* d_pts, hipStream_t s);
 // fast (MCV_FLAG_FAST_MINIMAL): the AP3P kernel's real-root-finder quartic instead of the reference's Ferrari
 // d_epnpScratch: kEpnpSplitDoubles x min(hypCount, kEpnpPiece) doubles (EPnP's split generate runs over
-// sub-ranges of kEpnpPiece hypotheses; unused by AP3P)
-static const int kEpnpPiece = 1 << 18;
+// sub-ranges of kEpnpPiece hypotheses; unused by AP3P). Round 6: 2^20 (2.4 GB at 2^20 hypotheses): one
+// piece per chunk, 27.3-27.5 ms a PnP step against 27.9-28.2 ms with 2^18 pieces (610 MB; each of the
+// five kernels per piece drains its slowest waves) and 27.7-27.9 with 2^19, same box alternating.
+static const int kEpnpPiece = 1 << 20;
 void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler smp, int64_t hypBegin, int hypCount,
                          bool epnp, void* d_models, int* d_counts, double* d_epnpScratch, hipStream_t s,
                          bool fast = false);

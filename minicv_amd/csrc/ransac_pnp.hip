@@ -814,7 +814,8 @@ void launch_pnp_generate(const void* d_pts, int N, const double* cam8, Sampler s
         return;
     }
     // sub-ranges of at most kEpnpPiece hypotheses reuse one scratch of kEpnpPiece x kEpnpSplitDoubles
-    // doubles (610 MB; a whole 2^20 chunk's took 2.4 GB per plan and device)
+    // doubles (2.4 GB at the 2^20 piece: one piece per chunk measured 2.3 % faster than 2^18 pieces of
+    // 610 MB, kernels.h; the footprint is documented in INTEGRATION.md §5)
     const PnpCamera cam = to_cam(cam8);
     const int piece = std::min(hypCount, kEpnpPiece);
     const int64_t S = piece;
