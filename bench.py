@@ -56,6 +56,7 @@ FP32_MFMA_PEAK_TF = 157.3
 F16_MFMA_PEAK_TF = 2516.6      # dense f16 MFMA: 32x32x16 = 16384 MAC per 32 cycles per SIMD, 1024 SIMDs, 2.4 GHz
 INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 I8_MFMA_PEAK_TOPS = 2 * F16_MFMA_PEAK_TF   # MI355X_MICROARCH.md: i8 32x32x32 at the cycles of bf16 32x32x16
+FP4_MFMA_PEAK_TOPS = 4 * F16_MFMA_PEAK_TF  # MI355X_MICROARCH.md: fp4 32x32x64 at the cycles of bf16 32x32x16
 # Algorithmic work per unit: homography computeError = 25 flops per (hypothesis,
 # correspondence) (3 dot products, 1 reciprocal, 2 sub, 2 mul, 1 add, 1 compare); Sampson error =
 # 34 fp64 flops per (model, correspondence) (F x1 12, F^T x2 8, x2^T F x1 4, denominator 7, c^2,
@@ -140,7 +141,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hamming-form", default="gemm", choices=["gemm", "popcount"],
-                    help="Hamming kernel: int8 GEMM on the matrix cores (default) or the XOR / popcount sweep")
+                    help="Hamming kernel: fp4 GEMM on the matrix cores (default) or the XOR / popcount sweep")
     ap.add_argument("--pnp-kind", default="EPNP", choices=["Iterative", "EPNP", "P3P", "DLS", "UPNP", "AP3P"],
                     help="pnp workload: the reference's solverKind (EPNP = its own testPnp, Program.fs:27-32)")
     ap.add_argument("--no-secondary", action="store_true",
@@ -256,19 +257,20 @@ def bench_matcher(args):
             pairs = cnt * nt
             ach = pairs / (avg_ms * 1e-3)
             gemm = args.hamming_form == "gemm"
-            kp = 256   # 32-byte descriptors: 256 +-1 bytes per expanded row
-            mfma_roof = {"bound": "mfma-i8", "achieved": 2.0 * kp * ach / 1e12, "peak": I8_MFMA_PEAK_TOPS,
-                         "unit": "Tops/s", "frac": 2.0 * kp * ach / 1e12 / I8_MFMA_PEAK_TOPS,
+            kp = 256   # 32-byte descriptors: 256 fp4 elements per expanded row
+            mfma_roof = {"bound": "mfma-fp4", "achieved": 2.0 * kp * ach / 1e12, "peak": FP4_MFMA_PEAK_TOPS,
+                         "unit": "Tops/s", "frac": 2.0 * kp * ach / 1e12 / FP4_MFMA_PEAK_TOPS,
                          "traffic": load_traffic("mcv_hamming_mfma", f"{nq}x{nt}"), "kernel": "mcv_hamming_mfma",
                          "avg_launch_ms": avg_ms, "timed_launches": launches,
                          "timed_every": MATCHER_PROF_STRIDE,
-                         "model": "Hamming as a +-1 int8 GEMM: [nt x 256] x [256 x nq] on v_mfma_i32_32x32x32_i8 "
-                                  "(2 x 256 int8 ops per pair; sum a b = 256 - 2 ham), exact in int32; the "
-                                  f"popcount view: {HAM_OPS_PER_PAIR * ach / 1e12:.1f} of {INT32_PEAK_TOPS:.1f} "
+                         "model": "Hamming as an fp4 GEMM: [nt x 256] x [256 x nq] on v_mfma_f32_32x32x64_f8f6f4 "
+                                  "(2 x 256 fp4 ops per pair; products t (1 - 2 q), sum = ham - popcount(q)), exact "
+                                  f"in f32; against the i8 form's peak: {2.0 * kp * ach / 1e12 / I8_MFMA_PEAK_TOPS:.3f}; "
+                                  f"the popcount view: {HAM_OPS_PER_PAIR * ach / 1e12:.1f} of {INT32_PEAK_TOPS:.1f} "
                                   "int32 Tops/s at 24 ops per pair"}
             line = {"metric": "BF Hamming knn-2 queries/sec, 10k x 10k 256-bit (BASELINE config[1])",
                     "value": nq * args.steps / el, "unit": "queries/s",
-                    "hamming_form": "int8 GEMM on the matrix cores (default)" if gemm else
+                    "hamming_form": "fp4 GEMM on the matrix cores (default)" if gemm else
                                     "XOR / popcount sweep (--hamming-form popcount)",
                     "roofline": mfma_roof if gemm else {"bound": "int-valu", "achieved": HAM_OPS_PER_PAIR * ach / 1e12,
                                  "peak": INT32_PEAK_TOPS, "unit": "Tops/s",
@@ -285,7 +287,7 @@ def bench_matcher(args):
                                            "unit": "pairs/s", "frac": ach / issue_peak(HAMMING_CYC_PER_WAVE_PAIR),
                                            "model": f"{HAMMING_CYC_PER_WAVE_PAIR} SIMD cycles per 64 (query, "
                                                     "train) pairs at 2.4 GHz"}},
-                    "dtype": "i8" if gemm else "u32", "scaling": "strong"}
+                    "dtype": "fp4" if gemm else "u32", "scaling": "strong"}
         else:
             exact_scans = NL.lib().mcvL2LastExactScans()
             form = NL.lib().mcvL2LastGemmForm()

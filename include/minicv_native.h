@@ -390,7 +390,7 @@ MCV_API int  mcvReplayChunkModels(mcvReplayState* st, const int* counts, int64_t
 /* Device-level matchers: d_q/d_t device arrays, outputs device arrays. Asynchronous on stream. */
 MCV_API int mcvMatchHammingDevice(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc,
                                   int* d_idx, int* d_dist, int* d_idx2, int* d_dist2, void* stream);
-/* The same with the kernel form chosen explicitly: 0 = int8 GEMM on the matrix cores (the default of
+/* The same with the kernel form chosen explicitly: 0 = fp4 GEMM on the matrix cores (the default of
  * every other Hamming entry point), 1 = the XOR / popcount sweep. Identical results. */
 MCV_API int mcvMatchHammingDeviceForm(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int bytesPerDesc,
                                       int* d_idx, int* d_dist, int* d_idx2, int* d_dist2, int form, void* stream);

@@ -230,34 +230,52 @@ __global__ __launch_bounds__(256) void mcv_hamming_merge(const uint2* __restrict
     if (dist2) dist2[qi] = m2 == 0xFFFFFFFFu ? INT_MAX : (int)(m2 >> kIdxBits);
 }
 
-// ---- The GEMM form (default, round 4): Hamming distance as an int8 dot product on the matrix cores.
-// Every bit b of a descriptor becomes the byte 64 (1 - 2 b) (train) or -64 (1 - 2 b) (query), so the
-// int32 sum over the Kp = 32 W bit positions of train x query is -4096 (Kp - 2 ham) (the zero pad bits
-// are equal in both: they add nothing to ham), and with the accumulator started at C = 4096 Kp + j'
-// (j' = the train row's index inside its chunk, < 4096) the MFMA chain ends exactly at the key
-//   acc = 8192 ham + j',
-// ordered as (distance, lowest index): the top-2 update is one v_med3_u32 and one v_min_u32 per score
-// and no key arithmetic. The all-pairs keys are a dense [nt x Kp] x [Kp x nq] int8 GEMM on
-// v_mfma_i32_32x32x32_i8 (2x the bf16 rate, exact in int32). At the end the chunk-local keys become the
-// popcount form's ham << 22 | trainIdx (the same rule, bit for bit).
-//
-// The +-64 bytes are never stored: word w of a descriptor expands to the 32 bytes [32 w, 32 w + 32),
-// dword d of them holding bits d, d + 8, d + 16, d + 24 (one shift and one v_and_or_b32 per dword).
-// Queries are expanded once into their VGPR-resident B fragments; the train tiles are loaded packed
-// (16 B of a 256-bit row per lane) and each A fragment is expanded in registers right before its MFMAs
+// ---- The GEMM form (default since round 4; fp4 operands since round 6): Hamming distance as a dot
+// product on the matrix cores, v_mfma_f32_32x32x64_f8f6f4 with both operands in fp4 (e2m1) — K = 64
+// per instruction at the cycles of the i8 form's K = 32, so half the matrix time of round 4-5's
+// v_mfma_i32_32x32x32_i8, and a cheaper operand expansion.
+// Encoding. Dword d (0..3) of a 32-bit descriptor word w holds bit 4k + d of w in its nibble k, so one
+// word is one lane's 32 K elements (4 dwords) and the lane halves h = 0 / 1 (K [0, 32) / [32, 64)) take
+// words s of their half rows at k step s — the same map for both operands, so element k of a train
+// row meets element k of a query row. A train bit t becomes the nibble 0.5 t / 1.0 t / 2.0 t / 2.0 t for
+// d = 0 / 1 / 2 / 3 (w & 0x1.., w & 0x2.., w & 0x4.., (w >> 1) & 0x4..: no shift for d < 3), a query
+// bit q the nibble +-2 / +-1 / +-0.5 / +-0.5 with the sign bit = q, so every product is exactly
+// t (1 - 2 q) and the sum over a row pair is pt - 2 dot = ham - pq (pq = the query's popcount; the
+// zero pad bits have t = 0 and add nothing).
+// Key. The accumulator starts at C = Kp + (4064 + r) / 4096 (r = the row inside the 32-row tile; Kp =
+// 32 W bits), so a row's f32 result is H + f with H = Kp + ham - pq in [0, 2 Kp] and f = (4064 + r) /
+// 4096 in [0, 1): every value is a multiple of 2^-12 below 2^11, exact in f32 at every step of the
+// chain, and positive, so its bit pattern orders as the float does and the top-2 update stays one
+// v_med3_u32 and one v_min_u32 per score. Rows of earlier tiles must rank below a later tile's at
+// equal distance (the lowest index wins): instead of raising C by 32 rows per tile, the kept top-2 keys
+// move down by 32 / 4096 at the top of each tile (4 v_add_f32 per query tile instead of 16 integer adds
+// to C, and C stays loop-invariant). A key kept from tile k of an n-tile segment has moved n - 1 - k
+// times (<= 127, so f >= 0), and the epilogue recovers j' = 32 k + r = 4096 f - 4064 + 32 (n - 1), then
+// the popcount form's key (ham << 22 | trainIdx) with ham = H - Kp + pq (bit for bit the same rule).
+// Rows past nt get 2^20 after the chain (a branch once per launch), kept keys start at 2^30 (moving
+// them down leaves them there); both are >= 2^19 and fold to "no match".
+// Queries are expanded once per segment into VGPR-resident B fragments; each train tile is loaded packed
+// (16 B of a 256-bit row per lane) one tile ahead and expanded in registers right before its MFMAs
 // (round 6: no LDS tile, no per-tile barrier; the round-5 LDS staging shared the expansion between a
-// block's four waves and measured the same 31-32 us at cfg2). Lane l (row / column l & 31, half
-// h = l >> 5) takes bytes [16 KS h + 16 s, + 16) of its row at k step s (word KS h / 2 + s / 2,
-// dwords 4 (s & 1) .. + 3); both operands use the same map.
-template <bool NEG>
-__device__ __forceinline__ int32_t ham_expand_dword(uint32_t v, int d) {   // v: the word, already ~ for NEG
-    const uint32_t x = d < 7 ? v << (7 - d) : v;
-    return (int32_t)((x & 0x80808080u) | 0x40404040u);
+// block's four waves and measured the same).
+__device__ __forceinline__ int32_t ham_train_f4(uint32_t w, int d) {
+    return (int32_t)(d == 0 ? w & 0x11111111u : d == 1 ? w & 0x22222222u : d == 2 ? w & 0x44444444u
+                                                                                   : (w >> 1) & 0x44444444u);
+}
+__device__ __forceinline__ int32_t ham_query_f4(uint32_t w, int d) {
+    return (int32_t)(d == 0 ? 0x44444444u | ((w << 3) & 0x88888888u)
+                     : d == 1 ? 0x22222222u | ((w << 2) & 0x88888888u)
+                     : d == 2 ? 0x11111111u | ((w << 1) & 0x88888888u)
+                              : 0x11111111u | (w & 0x88888888u));
 }
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x16 __attribute__((ext_vector_type(16)));
-static constexpr int kHamChunkRows = 4096;   // j' < 4096 < 8192: the key's index field
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+static constexpr int kHamChunkRows = 4096;   // j' < 4096: the key's 12 fraction bits
+static constexpr int kHamJ0 = kHamChunkRows - 32;   // a new row's fraction field (4064 + r)
+static constexpr uint32_t kHamKeptStart = 0x4E800000u;   // 2^30 as f32
+static constexpr uint32_t kHamMaskedRow = 0x49800000u;   // 2^20 as f32
 
 // Block = WPB waves x QT query tiles of 32 (VGPR-resident B fragments); the waves of a block walk the
 // same train tiles (their 1 KB loads hit L1 after the first) and each expanded A fragment feeds QT
@@ -275,17 +293,17 @@ static constexpr int kHamChunkRows = 4096;   // j' < 4096 < 8192: the key's inde
 // and read with agent-scope atomic stores / loads (sc1: performed at the device-coherent level, never
 // stale in an L2), each block waits for its stores to complete (s_waitcnt vmcnt(0), a compiler barrier
 // too) before its agent-scope arrival add, and the last block's loads are issued after that add returns.
-template <int W, int QT, int WPB, int SUB>
-__global__ __launch_bounds__(64 * WPB, W == 8 && QT <= 2 ? 3 : 2) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
+template <int W, int QT, int WPB>
+__global__ __launch_bounds__(64 * WPB, 2) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
                                                              const uint32_t* __restrict__ t, int nt, int ntTiles,
                                                              int qblocks, uint2* __restrict__ part,
                                                              unsigned* __restrict__ arrivals, int* __restrict__ oIdx,
                                                              int* __restrict__ oDist, int* __restrict__ oIdx2,
                                                              int* __restrict__ oDist2) {
     static_assert(QT % 2 == 0 || QT == 1, "the fold takes QT / 2 queries per thread");
-    static_assert(SUB == 1, "segments are counted in 32-row tiles");
-    constexpr int KS = W;                  // k steps of 32 bytes (Kp = 32 W)
-    constexpr int RB = 32 * KS;            // bytes per expanded row (Kp)
+    constexpr int KS = W / 2;              // k steps: one word per lane half each (K = 64 bits)
+    constexpr int Kp = 32 * W;             // bits per row
+    constexpr int NV = W / 8;              // uint4 per lane per half row
     __shared__ int lastBlock;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, col = lane & 31;
@@ -302,69 +320,84 @@ __global__ __launch_bounds__(64 * WPB, W == 8 && QT <= 2 ? 3 : 2) void mcv_hammi
         const int slot = blk - j0, nseg = j1 - j0 + 1;
         const int q0 = (bx * WPB + wave) * QT * 32;
         i32x4 bq[QT][KS];
-        uint4 qw[QT][W / 8];   // the lane's half query row: 16-byte loads, all issued before the expansion
+        int pq[QT];   // the query's popcount (both halves)
+        {
+            uint4 qw[QT][NV];   // the lane's half query row: 16-byte loads, all issued before the expansion
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const int qi = min(q0 + 32 * qt + col, nq - 1);
-            const uint4* qr = reinterpret_cast<const uint4*>(q + (size_t)qi * W + (KS / 2) * h);
+            for (int qt = 0; qt < QT; ++qt) {
+                const int qi = min(q0 + 32 * qt + col, nq - 1);
+                const uint4* qr = reinterpret_cast<const uint4*>(q + (size_t)qi * W + (W / 2) * h);
 #pragma unroll
-            for (int v = 0; v < W / 8; ++v) qw[qt][v] = qr[v];
-        }
+                for (int v = 0; v < NV; ++v) qw[qt][v] = qr[v];
+            }
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
+            for (int qt = 0; qt < QT; ++qt) {
+                int c = 0;
 #pragma unroll
-            for (int s2 = 0; s2 < KS / 2; ++s2) {
-                const uint4 u4 = qw[qt][s2 >> 2];
-                const int wi = s2 & 3;
-                const uint32_t wd = ~(wi == 0 ? u4.x : wi == 1 ? u4.y : wi == 2 ? u4.z : u4.w);
-                bq[qt][2 * s2] = i32x4{ham_expand_dword<true>(wd, 0), ham_expand_dword<true>(wd, 1),
-                                       ham_expand_dword<true>(wd, 2), ham_expand_dword<true>(wd, 3)};
-                bq[qt][2 * s2 + 1] = i32x4{ham_expand_dword<true>(wd, 4), ham_expand_dword<true>(wd, 5),
-                                           ham_expand_dword<true>(wd, 6), ham_expand_dword<true>(wd, 7)};
+                for (int s = 0; s < KS; ++s) {
+                    const uint4 u4 = qw[qt][s >> 2];
+                    const int wi = s & 3;
+                    const uint32_t wd = wi == 0 ? u4.x : wi == 1 ? u4.y : wi == 2 ? u4.z : u4.w;
+                    bq[qt][s] = i32x4{ham_query_f4(wd, 0), ham_query_f4(wd, 1), ham_query_f4(wd, 2),
+                                      ham_query_f4(wd, 3)};
+                    c += __popc(wd);
+                }
+                pq[qt] = c + __shfl_xor(c, 32, 64);
             }
         }
         uint32_t m1[QT], m2[QT], n1[QT], n2[QT];
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = n1[qt] = n2[qt] = 0xFFFFFFFFu;
+        for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = n1[qt] = n2[qt] = kHamKeptStart;
         // the lane's half of its train row (words [W h / 2, W h / 2 + W / 2): 16 B at W = 8) straight
         // from global memory, the next tile's in flight under this tile's MFMAs (the block's four waves
         // read the same 1 KB tile: L1 hits after the first)
-        constexpr int NV = W / 8;   // uint4 per lane per tile
         auto tload = [&](int tl, uint4 (&dst)[NV]) {
             const int row = min(tl * 32 + col, nt - 1);
             const uint4* src = reinterpret_cast<const uint4*>(t + (size_t)row * W + (W / 2) * h);
 #pragma unroll
             for (int v = 0; v < NV; ++v) dst[v] = src[v];
         };
-        // accumulator start values: 4096 Kp + j' (rows past nt: 2^30, which ends above every real key)
-        i32x16 c0;
+        // accumulator start values Kp + (4064 + r) / 4096, rebuilt per segment from one opaque VGPR (the
+        // compiler otherwise keeps all 16 across the segment loop and spills them)
+        f32x16 c0;
+        int rbase = kHamJ0 + 4 * h;
+        asm volatile("" : "+v"(rbase));
 #pragma unroll
-        for (int i = 0; i < 16; ++i) c0[i] = 4096 * RB + (i & 3) + 8 * (i >> 2) + 4 * h;
+        for (int i = 0; i < 16; ++i) c0[i] = (float)Kp + (float)(rbase + (i & 3) + 8 * (i >> 2)) * (1.0f / 4096.0f);
         uint4 tw[NV], nx[NV];
         tload(tBegin, tw);
         for (int tl = tBegin; tl < tEnd; ++tl) {
             tload(min(tl + 1, tEnd - 1), nx);
-            i32x16 cs = c0;
-            if (__builtin_expect(tl * 32 + 32 > nt, 0)) {   // rows past nt (wave-uniform)
+            // the kept keys move 32 rows down (the first tile: start values only, which stay at 2^30)
+            auto down = [](uint32_t& k) { k = __float_as_uint(__uint_as_float(k) - 32.0f / 4096.0f); };
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    if (tl * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= nt) cs[i] = 1 << 30;
-                asm volatile("" : "+v"(cs));   // a branch once per launch, not 32 selects per tile
-            }
+            for (int qt = 0; qt < QT; ++qt) { down(m1[qt]); down(m2[qt]); down(n1[qt]); down(n2[qt]); }
             // priority 0 for the MFMAs, 1 for the expansion and top-2 updates (as mcv_l2_gemm's epilogue)
             __builtin_amdgcn_s_setprio(0);
-            i32x16 acc[QT];
+            f32x16 acc[QT];
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
-                const uint4 u4 = tw[s >> 3];
-                const int wi = (s >> 1) & 3;
+                const uint4 u4 = tw[s >> 2];
+                const int wi = s & 3;
                 const uint32_t w = wi == 0 ? u4.x : wi == 1 ? u4.y : wi == 2 ? u4.z : u4.w;
-                const int d0 = 4 * (s & 1);
-                const i32x4 a = i32x4{ham_expand_dword<false>(w, d0), ham_expand_dword<false>(w, d0 + 1),
-                                      ham_expand_dword<false>(w, d0 + 2), ham_expand_dword<false>(w, d0 + 3)};
+                const i32x8 a = i32x8{ham_train_f4(w, 0), ham_train_f4(w, 1), ham_train_f4(w, 2), ham_train_f4(w, 3),
+                                      0, 0, 0, 0};
 #pragma unroll
-                for (int qt = 0; qt < QT; ++qt)
-                    acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][s], s == 0 ? cs : acc[qt], 0, 0, 0);
+                for (int qt = 0; qt < QT; ++qt) {
+                    const i32x8 b = i32x8{bq[qt][s][0], bq[qt][s][1], bq[qt][s][2], bq[qt][s][3], 0, 0, 0, 0};
+                    // cbsz = blgp = 4: both operands fp4 (4 VGPRs each); zero scales select the unscaled form
+                    acc[qt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, s == 0 ? c0 : acc[qt], 4, 4, 0, 0,
+                                                                              0, 0);
+                }
+            }
+            if (__builtin_expect(tl * 32 + 32 > nt, 0)) {   // rows past nt (wave-uniform; once per launch)
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if (tl * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= nt) acc[qt][i] = __uint_as_float(kHamMaskedRow);
+                    asm volatile("" : "+v"(acc[qt]));
+                }
             }
             __builtin_amdgcn_s_setprio(1);
             // two independent top-2 chains per query tile (rows i < 8 and i >= 8), merged at the end:
@@ -373,11 +406,9 @@ __global__ __launch_bounds__(64 * WPB, W == 8 && QT <= 2 ? 3 : 2) void mcv_hammi
             for (int i = 0; i < 8; ++i)
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) {
-                    top2_push(m1[qt], m2[qt], (uint32_t)acc[qt][i]);
-                    top2_push(n1[qt], n2[qt], (uint32_t)acc[qt][i + 8]);
+                    top2_push(m1[qt], m2[qt], __float_as_uint(acc[qt][i]));
+                    top2_push(n1[qt], n2[qt], __float_as_uint(acc[qt][i + 8]));
                 }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) c0[i] += 32;
 #pragma unroll
             for (int v = 0; v < NV; ++v) tw[v] = nx[v];
         }
@@ -391,8 +422,12 @@ __global__ __launch_bounds__(64 * WPB, W == 8 && QT <= 2 ? 3 : 2) void mcv_hammi
             top2_push(m1[qt], m2[qt], o1);
             top2_push(m1[qt], m2[qt], o2);
             auto glob = [&](uint32_t k) {
-                // a masked row ends at 2^30 - 4096 (Kp - 2 ham) >= 2^30 - 2^22; a real key is below 2^23
-                return k >= (1u << 29) ? 0xFFFFFFFFu : ((k >> 13) << kIdxBits) | (base + (k & (kHamChunkRows - 1)));
+                // masked rows and start values are >= 2^19; a real key H + f is below 2 Kp + 1 <= 1025
+                const float kf = __uint_as_float(k);
+                if (kf >= 524288.0f) return 0xFFFFFFFFu;
+                const int H = (int)kf;
+                const int jp = (int)((kf - (float)H) * 4096.0f) - (kHamJ0 - 32 * (tEnd - tBegin - 1));
+                return ((uint32_t)(H - Kp + pq[qt]) << kIdxBits) | (base + (uint32_t)jp);
             };
             const int qi = q0 + 32 * qt + col;
             // Memory ordering of the fold (why no release / acquire fence is needed). The hand-off is the
@@ -484,21 +519,24 @@ struct HammingWork {
 template <int WPB, int QT>
 static void launch_ham_gemm(HammingWork& wk, int W, const uint32_t* q, int nq, const uint32_t* t, int nt, int* d_idx,
                             int* d_dist, int* d_idx2, int* d_dist2, hipStream_t s) {
-    constexpr int SUB = 1;
     const int qblocks = (nq + 32 * QT * WPB - 1) / (32 * QT * WPB);
-    const int ntTiles = (nt + 32 * SUB - 1) / (32 * SUB);
+    const int ntTiles = (nt + 31) / 32;
     static const int cus = [] {
         int d = 0, n = 0;
         (void)hipGetDevice(&d);
         return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
     }();
-    auto kern = W == 8 ? mcv_hamming_mfma<8, QT, WPB, SUB> : mcv_hamming_mfma<16, QT, WPB, SUB>;
+    auto kern = W == 8 ? mcv_hamming_mfma<8, QT, WPB> : mcv_hamming_mfma<16, QT, WPB>;
     int perCu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, kern, 64 * WPB, 0) != hipSuccess || perCu <= 0) perCu = 1;
     const int64_t Wt = (int64_t)qblocks * ntTiles;
-    // equal ranges of the (query block, tile) steps over the resident blocks, at most 128 tiles each
-    // (the key's index field) and at least 4 (the per-range query expansion and fold)
-    int64_t B = std::min<int64_t>((int64_t)perCu * cus, (Wt + 3) / 4);
+    // equal ranges of the (query block, tile) steps: ~24 tiles each between one and two blocks per CU
+    // (round 6 grid sweep, fp4 form, B = 128..768: 1250 / 2500 / 5000 / 10000 queries x 10k best at
+    // 128-256 / 192-256 / 256 / 512 blocks — fewer, longer ranges amortise the per-range query expansion
+    // and keep a query block's segments within one batch of the fold's loads), within the resident
+    // blocks, and at most 128 tiles per range (the key's index field)
+    int64_t B = std::min<int64_t>(std::max<int64_t>((Wt + 23) / 24, cus), 2 * (int64_t)cus);
+    B = std::min<int64_t>(B, (int64_t)perCu * cus);
     B = std::max<int64_t>(B, (Wt + kHamChunkRows / 32 - 1) / (kHamChunkRows / 32));
     B = std::max<int64_t>(1, std::min(B, Wt));
     if (B > INT_MAX) fail("cvMatchHamming: %lld ranges", (long long)B);
@@ -545,7 +583,7 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         q = wk.qpack.p;
         t = wk.tpack.p;
     }
-    // form 1: the XOR / popcount sweep (mcvMatchHammingDeviceForm); 0: the int8 GEMM (default)
+    // form 1: the XOR / popcount sweep (mcvMatchHammingDeviceForm); 0: the fp4 GEMM (default)
     if (form == kHammingFormGemm && nt > 0) {
         // 4 waves per block, 2 query tiles per wave (cfg2 screens: round 4, 1 query tile 33.6 vs 32.1 us;
         // round 6 without the LDS staging, 10k x 10k / 1250 x 10k / 10k x 40k: 2 waves per block 29.7 /

@@ -78,7 +78,7 @@ HAMMING_FORMS = {"gemm": 0, "popcount": 1}
 
 
 def match_hamming(q, t, idx, dist, idx2=None, dist2=None, stream=None, form="gemm") -> None:
-    """form: "gemm" (int8 GEMM on the matrix cores, the default) or "popcount" (XOR / popcount sweep)."""
+    """form: "gemm" (fp4 GEMM on the matrix cores, the default) or "popcount" (XOR / popcount sweep)."""
     r = N.lib().mcvMatchHammingDeviceForm(q.data_ptr(), q.shape[0], t.data_ptr(), t.shape[0], q.shape[1],
                                           idx.data_ptr(), dist.data_ptr(),
                                           idx2.data_ptr() if idx2 is not None else None,

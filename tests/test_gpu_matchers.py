@@ -253,7 +253,7 @@ def test_matchers_back_to_back_on_two_streams(gpu, oracle):
 
 @pytest.fixture(params=["gemm", "popcount"])
 def hamming_form(request):
-    """Both Hamming kernel forms: the int8 GEMM on the matrix cores (the default of every entry point)
+    """Both Hamming kernel forms: the fp4 GEMM on the matrix cores (the default of every entry point)
     and the XOR / popcount sweep, chosen through mcvMatchHammingDeviceForm."""
     return request.param
 
