@@ -590,7 +590,15 @@ int launch_match_hamming(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
         // 18.7 / 87.6 us, 8 waves 28.3 / 15.7 / 91.7, against 28.1-31.4 / 14.9-15.3 / 87.3-99.4 for 4;
         // 4 query tiles per wave spill at 256 VGPRs), one block per resident slot (3 per CU at 256-bit
         // descriptors, 2 at 512-bit).
-        launch_ham_gemm<4, 2>(wk, W, q, nq, t, nt, d_idx, d_dist, d_idx2, d_dist2, s);
+        // small problems (the multi-GPU shares): one query tile per wave, twice the query blocks, so the
+        // ranges stay ~24 tiles over more blocks (round 6, same box alternating: 1250 / 5000 x 10k
+        // 11.2-11.4 -> 10.0-10.1 / 14.4-14.6 -> 13.4 us; cfg2 17.7 -> 18.2-18.5 and 10k x 40k 46.0 -> 64.1
+        // us the other way)
+        const int64_t steps2 = (int64_t)((nq + 255) / 256) * ((nt + 31) / 32);
+        if (steps2 <= 8192)
+            launch_ham_gemm<4, 1>(wk, W, q, nq, t, nt, d_idx, d_dist, d_idx2, d_dist2, s);
+        else
+            launch_ham_gemm<4, 2>(wk, W, q, nq, t, nt, d_idx, d_dist, d_idx2, d_dist2, s);
         MCV_HIP(hipGetLastError());
         wk.fence.leave(s);
         return nq;
