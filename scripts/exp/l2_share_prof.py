@@ -1,31 +1,23 @@
-"""One rank's L2 share (50k / N queries x 50k train x 128) called back to back, for a rocprofv3
-kernel trace of what the N-GPU step is made of. Usage: l2_share_prof.py N"""
+"""The 8-rank L2 share (6250 of cfg5's 50k queries x 50k train, 128-d) called 30 times back to back, for
+rocprofv3 --kernel-trace --stats (per-kernel times of the share)."""
 import sys
-import time
-from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
+import torch
 
+sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[2]))
+from minicv_amd import device as D, synthetic as S
 
-def main():
-    import torch
-    from minicv_amd import device as D, synthetic as S
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    dev = torch.device("cuda:0")
-    q, t, _ = S.l2_problem(50_000, 50_000, dim=128, seed=5)
-    cnt = (50_000 + n - 1) // n
-    qs, td = torch.from_numpy(q[:cnt]).to(dev), torch.from_numpy(t).to(dev)
-    idx, idx2 = (torch.empty(cnt, dtype=torch.int32, device=dev) for _ in range(2))
-    d1, d2 = (torch.empty(cnt, dtype=torch.float32, device=dev) for _ in range(2))
-    for _ in range(3):
-        D.match_l2(qs, td, idx, d1, idx2, d2)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(20):
-        D.match_l2(qs, td, idx, d1, idx2, d2)
-    torch.cuda.synchronize()
-    print(f"N={n} share {(time.perf_counter() - t0) / 20 * 1e3:.3f} ms per call", flush=True)
-
-
-if __name__ == "__main__":
-    main()
+dev = torch.device("cuda:0")
+cnt = int(sys.argv[1]) if len(sys.argv) > 1 else 6250
+q, t, _ = S.l2_problem(50_000, 50_000, dim=128, seed=5)
+qd, td = torch.from_numpy(q[:cnt]).to(dev), torch.from_numpy(t).to(dev)
+idx = torch.empty(cnt, dtype=torch.int32, device=dev)
+idx2 = torch.empty_like(idx)
+d1 = torch.empty(cnt, dtype=torch.float32, device=dev)
+d2 = torch.empty_like(d1)
+for _ in range(30):
+    D.match_l2(qd, td, idx, d1, idx2, d2)
+torch.cuda.synchronize()
+print("ok", cnt)
+from minicv_amd import native as NL
+print("queued exact scans", NL.lib().mcvL2LastExactScans())
