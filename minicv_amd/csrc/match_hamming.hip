@@ -293,6 +293,43 @@ static constexpr uint32_t kHamMaskedRow = 0x49800000u;   // 2^20 as f32
 // and read with agent-scope atomic stores / loads (sc1: performed at the device-coherent level, never
 // stale in an L2), each block waits for its stores to complete (s_waitcnt vmcnt(0), a compiler barrier
 // too) before its agent-scope arrival add, and the last block's loads are issued after that add returns.
+// The tile's top-2 tree runs on the keys as floats (positive, finite, no denormals: their order is the
+// bit patterns' order, and min / med3 return one of their operands bit for bit), through operations the
+// compiler emits itself: these read MFMA results directly, and the hazard recognizer pads an MFMA ->
+// VALU read only for instructions it generated (a v_min3_u32 / v_med3_u32 inline-asm form of this tree
+// gave wrong keys for 512-bit descriptors, whose 8-long MFMA chains end right before it).
+__device__ __forceinline__ float fmin3k(float a, float b, float c) { return fminf(fminf(a, b), c); }
+__device__ __forceinline__ float fmed3k(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
+// Two top-2 pairs (x1 <= x2), (y1 <= y2) merged into x: the minimum, and the second smallest of the four,
+// min(max(x1, y1), min(x2, y2)) = med3(x1, y1, min(x2, y2)) (min(x2, y2) >= min(x1, y1)).
+__device__ __forceinline__ void top2_merge(float& x1, float& x2, float y1, float y2) {
+    const float s2 = fmed3k(x1, y1, fminf(x2, y2));
+    x1 = fminf(x1, y1);
+    x2 = s2;
+}
+// The top-2 of a lane's 16 scores of a tile as a tree (round 6): five triples (min3 / med3: the smallest
+// two of three in two instructions), the sixteenth pushed into the fifth, four pairwise merges, then one
+// merge into the kept pair — ~86 issue cycles against 96 for 16 sequential med3 / min pushes, and a
+// dependency depth of 5 merges instead of 8 pushes per chain. Keys are distinct (the row fraction)
+// except masked rows, which fold to "no match" whatever their order.
+__device__ __forceinline__ void top2_tile16(uint32_t& m1, uint32_t& m2, const f32x16& k) {
+    float a1[5], a2[5];
+#pragma unroll
+    for (int g = 0; g < 5; ++g) {
+        a1[g] = fmin3k(k[3 * g], k[3 * g + 1], k[3 * g + 2]);
+        a2[g] = fmed3k(k[3 * g], k[3 * g + 1], k[3 * g + 2]);
+    }
+    top2_merge(a1[0], a2[0], a1[1], a2[1]);
+    top2_merge(a1[2], a2[2], a1[3], a2[3]);
+    a2[4] = fmed3k(a1[4], k[15], a2[4]);
+    a1[4] = fminf(a1[4], k[15]);
+    top2_merge(a1[0], a2[0], a1[2], a2[2]);
+    top2_merge(a1[0], a2[0], a1[4], a2[4]);
+    float x1 = __uint_as_float(m1), x2 = __uint_as_float(m2);
+    top2_merge(x1, x2, a1[0], a2[0]);
+    m1 = __float_as_uint(x1);
+    m2 = __float_as_uint(x2);
+}
 template <int W, int QT, int WPB>
 __global__ __launch_bounds__(64 * WPB, 2) void mcv_hamming_mfma(const uint32_t* __restrict__ q, int nq,
                                                              const uint32_t* __restrict__ t, int nt, int ntTiles,
@@ -345,9 +382,9 @@ __global__ __launch_bounds__(64 * WPB, 2) void mcv_hamming_mfma(const uint32_t* 
                 pq[qt] = c + __shfl_xor(c, 32, 64);
             }
         }
-        uint32_t m1[QT], m2[QT], n1[QT], n2[QT];
+        uint32_t m1[QT], m2[QT];
 #pragma unroll
-        for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = n1[qt] = n2[qt] = kHamKeptStart;
+        for (int qt = 0; qt < QT; ++qt) m1[qt] = m2[qt] = kHamKeptStart;
         // the lane's half of its train row (words [W h / 2, W h / 2 + W / 2): 16 B at W = 8) straight
         // from global memory, the next tile's in flight under this tile's MFMAs (the block's four waves
         // read the same 1 KB tile: L1 hits after the first)
@@ -371,7 +408,7 @@ __global__ __launch_bounds__(64 * WPB, 2) void mcv_hamming_mfma(const uint32_t* 
             // the kept keys move 32 rows down (the first tile: start values only, which stay at 2^30)
             auto down = [](uint32_t& k) { k = __float_as_uint(__uint_as_float(k) - 32.0f / 4096.0f); };
 #pragma unroll
-            for (int qt = 0; qt < QT; ++qt) { down(m1[qt]); down(m2[qt]); down(n1[qt]); down(n2[qt]); }
+            for (int qt = 0; qt < QT; ++qt) { down(m1[qt]); down(m2[qt]); }
             // priority 0 for the MFMAs, 1 for the expansion and top-2 updates (as mcv_l2_gemm's epilogue)
             __builtin_amdgcn_s_setprio(0);
             f32x16 acc[QT];
@@ -400,15 +437,10 @@ __global__ __launch_bounds__(64 * WPB, 2) void mcv_hamming_mfma(const uint32_t* 
                 }
             }
             __builtin_amdgcn_s_setprio(1);
-            // two independent top-2 chains per query tile (rows i < 8 and i >= 8), merged at the end:
-            // the med3 / min updates of one chain depend on each other, two chains overlap
+            // the tile's 16 scores per lane and query tile merged as a tree (round 6: two sequential
+            // chains of 8 pushes before — cfg2 18.0 -> 17.5 us, 10k x 40k 47.2 -> 44.1 us, same box)
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int qt = 0; qt < QT; ++qt) {
-                    top2_push(m1[qt], m2[qt], __float_as_uint(acc[qt][i]));
-                    top2_push(n1[qt], n2[qt], __float_as_uint(acc[qt][i + 8]));
-                }
+            for (int qt = 0; qt < QT; ++qt) top2_tile16(m1[qt], m2[qt], acc[qt]);
 #pragma unroll
             for (int v = 0; v < NV; ++v) tw[v] = nx[v];
         }
@@ -416,8 +448,6 @@ __global__ __launch_bounds__(64 * WPB, 2) void mcv_hamming_mfma(const uint32_t* 
         const uint32_t base = (uint32_t)tBegin * 32;
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt) {
-            top2_push(m1[qt], m2[qt], n1[qt]);   // segment-local keys: the index field keeps them distinct
-            top2_push(m1[qt], m2[qt], n2[qt]);
             const uint32_t o1 = __shfl_xor(m1[qt], 32, 64), o2 = __shfl_xor(m2[qt], 32, 64);
             top2_push(m1[qt], m2[qt], o1);
             top2_push(m1[qt], m2[qt], o2);
