@@ -245,10 +245,10 @@ __global__ __launch_bounds__(256) void mcv_hamming_merge(const uint2* __restrict
 // Key. The accumulator starts at C = Kp + (4064 + r) / 4096 (r = the row inside the 32-row tile; Kp =
 // 32 W bits), so a row's f32 result is H + f with H = Kp + ham - pq in [0, 2 Kp] and f = (4064 + r) /
 // 4096 in [0, 1): every value is a multiple of 2^-12 below 2^11, exact in f32 at every step of the
-// chain, and positive, so its bit pattern orders as the float does and the top-2 update stays one
-// v_med3_u32 and one v_min_u32 per score. Rows of earlier tiles must rank below a later tile's at
+// chain, and positive, so the float and its bit pattern order alike: the tile's scores fold into the
+// kept top-2 by min3 / med3 (top2_tile16) and the fold across segments stays on the bit patterns. Rows of earlier tiles must rank below a later tile's at
 // equal distance (the lowest index wins): instead of raising C by 32 rows per tile, the kept top-2 keys
-// move down by 32 / 4096 at the top of each tile (4 v_add_f32 per query tile instead of 16 integer adds
+// move down by 32 / 4096 at the top of each tile (2 v_add_f32 per query tile instead of 16 integer adds
 // to C, and C stays loop-invariant). A key kept from tile k of an n-tile segment has moved n - 1 - k
 // times (<= 127, so f >= 0), and the epilogue recovers j' = 32 k + r = 4096 f - 4064 + 32 (n - 1), then
 // the popcount form's key (ham << 22 | trainIdx) with ham = H - Kp + pq (bit for bit the same rule).
